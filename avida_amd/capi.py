@@ -1,0 +1,220 @@
+"""ctypes mirror of include/avida_gpu.h (structures + the product library loader).
+
+The product library is ``avida_amd/libavida_gpu.so`` (built in-tree by
+``__graft_entry__.build()`` / ``avida_amd/build.py``).  There is no fallback:
+if the library or a GPU is missing, calls raise.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+MAX_REACTIONS = 16
+MAX_GENOME = 2048
+STACK_SIZE = 10
+MAX_LABEL = 10
+
+MODE_WORLD, MODE_TEST, MODE_FROZEN = 0, 1, 2
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libavida_gpu.so")
+
+
+class AvgpuCfg(C.Structure):
+    _fields_ = [
+        ("world_x", C.c_int32), ("world_y", C.c_int32), ("world_geometry", C.c_int32),
+        ("ave_time_slice", C.c_int32), ("slicing_method", C.c_int32),
+        ("base_merit_method", C.c_int32), ("base_const_merit", C.c_int32),
+        ("default_bonus", C.c_double),
+        ("copy_mut_prob", C.c_double), ("copy_ins_prob", C.c_double), ("copy_del_prob", C.c_double),
+        ("divide_mut_prob", C.c_double), ("divide_ins_prob", C.c_double),
+        ("divide_del_prob", C.c_double),
+        ("offspring_size_range", C.c_double), ("min_copied_lines", C.c_double),
+        ("min_exe_lines", C.c_double),
+        ("require_allocate", C.c_int32), ("death_method", C.c_int32), ("age_limit", C.c_int32),
+        ("alloc_method", C.c_int32), ("divide_method", C.c_int32),
+        ("max_label_exe_size", C.c_int32), ("birth_method", C.c_int32),
+        ("prefer_empty", C.c_int32), ("allow_parent", C.c_int32),
+        ("test_cpu_time_mod", C.c_int32), ("min_genome_size", C.c_int32),
+        ("max_genome_size", C.c_int32), ("inherit_merit", C.c_int32),
+        ("merit_default_bonus", C.c_double), ("required_bonus", C.c_double),
+        ("seed", C.c_uint64),
+    ]
+
+
+class AvgpuReaction(C.Structure):
+    _fields_ = [
+        ("task", C.c_int32), ("type", C.c_int32), ("value", C.c_double),
+        ("max_number", C.c_double), ("min_count", C.c_int32), ("max_count", C.c_int32),
+        ("has_requisite", C.c_int32), ("pad", C.c_int32),
+    ]
+
+
+class AvgpuCpuState(C.Structure):
+    _fields_ = [
+        ("reg", C.c_int32 * 3), ("head", C.c_int32 * 4),
+        ("stack", (C.c_int32 * STACK_SIZE) * 2), ("stack_ptr", C.c_int32 * 2),
+        ("cur_stack", C.c_int32), ("read_label_len", C.c_int32),
+        ("read_label", C.c_int8 * MAX_LABEL), ("pad0", C.c_int16),
+        ("mal_active", C.c_int32), ("mem_size", C.c_int32),
+        ("cpu_cycles_used", C.c_int32), ("time_used", C.c_int32),
+        ("gestation_start", C.c_int32), ("gestation_time", C.c_int32),
+        ("num_divides", C.c_int32), ("generation", C.c_int32), ("alive", C.c_int32),
+        ("genome_length", C.c_int32), ("copied_size", C.c_int32),
+        ("child_copied_size", C.c_int32), ("executed_size", C.c_int32),
+        ("max_executed", C.c_int32), ("birth_length", C.c_int32), ("input_ptr", C.c_int32),
+        ("input_buf", C.c_int32 * 3), ("input_total", C.c_int32),
+        ("output_buf", C.c_int32), ("output_total", C.c_int32), ("inputs", C.c_int32 * 3),
+        ("cur_task_count", C.c_int32 * MAX_REACTIONS),
+        ("last_task_count", C.c_int32 * MAX_REACTIONS),
+        ("cur_reaction_count", C.c_int32 * MAX_REACTIONS),
+        ("rng_counter", C.c_uint32), ("rng_key_lo", C.c_uint32), ("rng_key_hi", C.c_uint32),
+        ("errors", C.c_int32),
+        ("cur_bonus", C.c_double), ("merit", C.c_double), ("fitness", C.c_double),
+    ]
+
+
+class AvgpuTestResult(C.Structure):
+    _fields_ = [
+        ("divided", C.c_int32), ("copy_true", C.c_int32), ("copied_size", C.c_int32),
+        ("executed_size", C.c_int32), ("gestation_time", C.c_int32),
+        ("offspring_len", C.c_int32), ("genome_length", C.c_int32), ("time_used", C.c_int32),
+        ("merit", C.c_double), ("fitness", C.c_double),
+        ("task_count", C.c_int32 * MAX_REACTIONS),
+    ]
+
+
+class AvgpuUpdateStats(C.Structure):
+    _fields_ = [
+        ("update", C.c_int64), ("num_organisms", C.c_int64), ("insts_executed", C.c_int64),
+        ("births", C.c_int64), ("births_dropped", C.c_int64), ("deaths", C.c_int64),
+        ("divides", C.c_int64), ("task_orgs", C.c_int64 * MAX_REACTIONS),
+        ("sum_merit", C.c_double), ("sum_fitness", C.c_double), ("sum_gestation", C.c_double),
+        ("sum_genome_length", C.c_double), ("max_fitness", C.c_double),
+        ("ave_generation", C.c_double),
+    ]
+
+
+# C-ABI symbols declared in include/avida_gpu.h (checked by tests/test_capi.py)
+EXPORTED = [
+    "avgpu_last_error", "avgpu_cfg_defaults", "avgpu_create", "avgpu_destroy", "avgpu_sync",
+    "avgpu_load_instset", "avgpu_load_env", "avgpu_set_org", "avgpu_set_orgs", "avgpu_kill",
+    "avgpu_step", "avgpu_run_update", "avgpu_run_updates", "avgpu_get_states",
+    "avgpu_test_genomes", "avgpu_get_stats", "avgpu_stats_vector", "avgpu_set_global_totals",
+    "avgpu_halo_pack", "avgpu_halo_unpack", "avgpu_halo_record_bytes",
+    "avgpu_last_step_insts", "avgpu_last_kernel_ms",
+]
+
+
+def cfg_from_avida(cfg, seed=None) -> AvgpuCfg:
+    """Fill an AvgpuCfg from a files.AvidaConfig."""
+    g = cfg.get
+    c = AvgpuCfg()
+    c.world_x, c.world_y = g("WORLD_X"), g("WORLD_Y")
+    c.world_geometry = g("WORLD_GEOMETRY")
+    c.ave_time_slice = g("AVE_TIME_SLICE")
+    c.slicing_method = g("SLICING_METHOD")
+    c.base_merit_method = g("BASE_MERIT_METHOD")
+    c.base_const_merit = g("BASE_CONST_MERIT")
+    c.default_bonus = g("DEFAULT_BONUS")
+    c.copy_mut_prob = g("COPY_MUT_PROB")
+    c.copy_ins_prob = g("COPY_INS_PROB")
+    c.copy_del_prob = g("COPY_DEL_PROB")
+    c.divide_mut_prob = g("DIVIDE_MUT_PROB")
+    c.divide_ins_prob = g("DIVIDE_INS_PROB")
+    c.divide_del_prob = g("DIVIDE_DEL_PROB")
+    c.offspring_size_range = g("OFFSPRING_SIZE_RANGE")
+    c.min_copied_lines = g("MIN_COPIED_LINES")
+    c.min_exe_lines = g("MIN_EXE_LINES")
+    c.require_allocate = g("REQUIRE_ALLOCATE")
+    c.death_method = g("DEATH_METHOD")
+    c.age_limit = g("AGE_LIMIT")
+    c.alloc_method = g("ALLOC_METHOD")
+    c.divide_method = g("DIVIDE_METHOD")
+    c.max_label_exe_size = g("MAX_LABEL_EXE_SIZE")
+    c.birth_method = g("BIRTH_METHOD")
+    c.prefer_empty = g("PREFER_EMPTY")
+    c.allow_parent = g("ALLOW_PARENT")
+    c.test_cpu_time_mod = g("TEST_CPU_TIME_MOD")
+    c.min_genome_size = g("MIN_GENOME_SIZE")
+    c.max_genome_size = g("MAX_GENOME_SIZE")
+    c.inherit_merit = g("INHERIT_MERIT")
+    c.merit_default_bonus = g("MERIT_DEFAULT_BONUS")
+    c.required_bonus = g("REQUIRED_BONUS")
+    s = g("RANDOM_SEED") if seed is None else seed
+    c.seed = int(s) & 0xFFFFFFFFFFFFFFFF if int(s) >= 0 else 0x1234ABCD
+    return c
+
+
+def reactions_array(reactions):
+    arr = (AvgpuReaction * max(1, len(reactions)))()
+    for i, r in enumerate(reactions):
+        arr[i].task, arr[i].type, arr[i].value = r.task, r.proc_type, r.value
+        arr[i].max_number, arr[i].min_count = r.max_number, r.min_count
+        arr[i].max_count, arr[i].has_requisite = r.max_count, r.has_requisite
+    return arr
+
+
+def bind_common(lib, prefix):
+    """Declare argtypes for the functions shared by the product and the oracle."""
+    p = prefix
+    V, I64, I32 = C.c_void_p, C.c_int64, C.c_int32
+    sig = {
+        "load_instset": (C.c_int, [V, C.c_int, C.POINTER(C.c_uint8), C.POINTER(C.c_int32)]),
+        "load_env": (C.c_int, [V, C.c_int, C.POINTER(AvgpuReaction)]),
+        "set_orgs": (C.c_int, [V, I64, I64, C.POINTER(C.c_uint8), C.POINTER(C.c_int32),
+                               C.POINTER(C.c_double), C.POINTER(C.c_int32), C.c_int]),
+        "kill": (C.c_int, [V, I64]),
+        "step": (C.c_int, [V, I64, I64, C.POINTER(C.c_int32), I32, C.c_int]),
+        "get_states": (C.c_int, [V, I64, I64, C.POINTER(AvgpuCpuState), C.POINTER(C.c_uint8),
+                                 C.POINTER(C.c_uint8), C.c_int]),
+        "test_genomes": (C.c_int, [V, C.c_int, C.POINTER(C.c_uint8), C.POINTER(C.c_int32),
+                                   C.POINTER(AvgpuTestResult), C.c_char_p, C.c_int,
+                                   C.POINTER(C.c_uint8)]),
+        "run_update": (C.c_int, [V, C.POINTER(AvgpuUpdateStats)]),
+        "run_updates": (C.c_int, [V, C.c_int, C.POINTER(AvgpuUpdateStats)]),
+        "last_step_insts": (C.c_int, [V, C.POINTER(C.c_int64)]),
+        "set_global_totals": (C.c_int, [V, C.c_double, I64]),
+        "destroy": (C.c_int, [V]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, p + name, None)
+        if fn is not None:
+            fn.restype, fn.argtypes = res, args
+    getattr(lib, p + "last_error").restype = C.c_char_p
+    return lib
+
+
+_lib = None
+
+
+def load_product():
+    """Load the in-tree HIP library; raise if it is missing (no fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"{LIB_PATH} missing: run __graft_entry__.build() first")
+    lib = C.CDLL(LIB_PATH)
+    bind_common(lib, "avgpu_")
+    lib.avgpu_create.restype = C.c_void_p
+    lib.avgpu_create.argtypes = [C.POINTER(AvgpuCfg), C.c_int, C.c_int64]
+    lib.avgpu_cfg_defaults.argtypes = [C.POINTER(AvgpuCfg)]
+    lib.avgpu_sync.argtypes = [C.c_void_p]
+    lib.avgpu_get_stats.argtypes = [C.c_void_p, C.POINTER(AvgpuUpdateStats)]
+    lib.avgpu_stats_vector.argtypes = [C.c_void_p, C.POINTER(C.c_void_p)]
+    lib.avgpu_halo_pack.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_int64,
+                                    C.POINTER(C.c_int64)]
+    lib.avgpu_halo_unpack.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_int64]
+    lib.avgpu_halo_record_bytes.restype = C.c_int64
+    lib.avgpu_last_kernel_ms.argtypes = [C.c_void_p, C.POINTER(C.c_double),
+                                         C.POINTER(C.c_int64)]
+    _lib = lib
+    return lib
+
+
+def check(lib, rc, prefix="avgpu_"):
+    if rc < 0:
+        msg = getattr(lib, prefix + "last_error")()
+        raise RuntimeError(f"{prefix}call failed ({rc}): {msg.decode() if msg else ''}")
+    return rc

@@ -1,0 +1,324 @@
+/*
+ * avida_gpu.h -- C-ABI of the MI355X batched Avida virtual-CPU interpreter.
+ *
+ * This is the drop-in boundary for ONE hot path of fortunalab/avida: the
+ * per-organism heads-CPU execution loop (cHardwareCPU::SingleProcess) as driven
+ * by cPopulation::ProcessStep, with its fused neighbours (Divide_DoMutations,
+ * the IO-driven logic-9 task check, merit-weighted time slicing, birth
+ * placement).  Every entry point below names the reference interface it
+ * replaces (paths relative to avida-core/source/ of the reference).
+ *
+ * Conventions
+ *   - plain C types only; no torch / HIP types cross this boundary;
+ *   - every call returns >= 0 on success, a negative AVGPU_E* code on error,
+ *     with a human readable message from avgpu_last_error();
+ *   - one host thread per handle; work is enqueued on the handle's own HIP
+ *     stream and avgpu_sync() waits for it;
+ *   - genomes cross the boundary as instruction-set op codes (the byte values
+ *     cInstSet assigns, i.e. INST line order), exactly like
+ *     Avida::InstructionSequence (include/public/avida/core/InstructionSequence.h).
+ */
+#ifndef AVIDA_GPU_H
+#define AVIDA_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- constants (include/public/avida/core/Definitions.h:28-29,
+ *      cpu/nHardware.h:32-34, cpu/cCodeLabel.cc MAX_LENGTH) ---------------- */
+#define AVGPU_MIN_GENOME 8
+#define AVGPU_MAX_GENOME 2048
+#define AVGPU_STACK_SIZE 10
+#define AVGPU_MAX_LABEL 10
+#define AVGPU_MAX_INST 64
+#define AVGPU_MAX_REACTIONS 16
+#define AVGPU_NUM_LOGIC_TASKS 9
+
+/* error codes */
+#define AVGPU_OK 0
+#define AVGPU_EINVAL -1
+#define AVGPU_EHIP -2
+#define AVGPU_ESTATE -3
+#define AVGPU_ENOMEM -4
+#define AVGPU_EUNSUPPORTED -5
+
+/* Canonical instruction handlers of the heads_default / classic instruction
+ * sets: the 26 tInstLibEntry rows of cpu/cHardwareCPU.cc:85-375 that
+ * support/config/instset-heads.cfg and tests/.../instset-classic.cfg name.
+ * The value is the handler id, NOT the op code: the op code is the INST line
+ * position, mapped to a handler by avgpu_load_instset (cInstSet::Load,
+ * cpu/cInstSet.cc:152-312). */
+enum avgpu_handler {
+  AVGPU_H_NOP_A = 0,   /* cpu/cHardwareBase.cc:1179 (Inst_Nop), nop-mod 0 */
+  AVGPU_H_NOP_B = 1,   /* nop-mod 1 */
+  AVGPU_H_NOP_C = 2,   /* nop-mod 2 */
+  AVGPU_H_IF_N_EQU = 3,  /* cpu/cHardwareCPU.cc:2190 */
+  AVGPU_H_IF_LESS = 4,   /* :2235 */
+  AVGPU_H_POP = 5,       /* :2698 */
+  AVGPU_H_PUSH = 6,      /* :2705 */
+  AVGPU_H_SWAP_STK = 7,  /* :2739 */
+  AVGPU_H_SWAP = 8,      /* :2742 */
+  AVGPU_H_SHIFT_R = 9,   /* :2806 */
+  AVGPU_H_SHIFT_L = 10,  /* :2813 */
+  AVGPU_H_INC = 11,      /* :2864 */
+  AVGPU_H_DEC = 12,      /* :2871 */
+  AVGPU_H_ADD = 13,      /* :2959 */
+  AVGPU_H_SUB = 14,      /* :2968 */
+  AVGPU_H_NAND = 15,     /* :3018 */
+  AVGPU_H_IO = 16,       /* :4188 (Inst_TaskIO) */
+  AVGPU_H_H_ALLOC = 17,  /* :3294 (Inst_MaxAlloc) */
+  AVGPU_H_H_DIVIDE = 18, /* :6961 -> :6942 */
+  AVGPU_H_H_COPY = 19,   /* :7130 */
+  AVGPU_H_H_SEARCH = 20, /* :7245 */
+  AVGPU_H_MOV_HEAD = 21, /* :6809 */
+  AVGPU_H_JMP_HEAD = 22, /* :6859 */
+  AVGPU_H_GET_HEAD = 23, /* :6907 */
+  AVGPU_H_IF_LABEL = 24, /* :6914 */
+  AVGPU_H_SET_FLOW = 25, /* :7270 */
+  AVGPU_H_COUNT = 26
+};
+
+/* logic-9 task ids (main/cTaskLib.cc:511-575) */
+enum avgpu_task {
+  AVGPU_T_NOT = 0, AVGPU_T_NAND, AVGPU_T_AND, AVGPU_T_ORN, AVGPU_T_OR,
+  AVGPU_T_ANDN, AVGPU_T_NOR, AVGPU_T_XOR, AVGPU_T_EQU
+};
+
+/* reaction process types (main/nReaction.h PROCTYPE_*) */
+enum avgpu_proctype { AVGPU_PROC_ADD = 0, AVGPU_PROC_MULT = 1, AVGPU_PROC_POW = 2 };
+
+/* Execution modes of avgpu_step.
+ *  WORLD : cPopulation::ActivateOffspring semantics -- a successful divide runs
+ *          Divide_DoMutations on the child and appends it to the birth queue;
+ *  TEST  : cTestCPU::ProcessGestation semantics (cpu/cTestCPU.cc:144-188) --
+ *          the organism stops at its first successful divide
+ *          (cTestCPUInterface::Divide -> cPhenotype::TestDivideReset);
+ *  FROZEN: divide resets the parent (DIVIDE_METHOD 1) and the offspring is
+ *          discarded; used for frozen-population trace parity (BASELINE cfg 2). */
+enum avgpu_mode { AVGPU_MODE_WORLD = 0, AVGPU_MODE_TEST = 1, AVGPU_MODE_FROZEN = 2 };
+
+/* Scheduler (SLICING_METHOD, main/cPopulation.cc:7326-7358) */
+enum avgpu_slicing { AVGPU_SLICE_CONSTANT = 0, AVGPU_SLICE_PROBABILISTIC = 1,
+                     AVGPU_SLICE_INTEGRATED = 2 };
+
+/* The avida.cfg subset on this path (main/cAvidaConfig.h; defaults are the
+ * values of support/config/avida.cfg).  avgpu_cfg_defaults() fills them. */
+typedef struct avgpu_cfg {
+  int32_t world_x, world_y;        /* WORLD_X, WORLD_Y */
+  int32_t world_geometry;          /* 1 grid, 2 torus */
+  int32_t ave_time_slice;          /* AVE_TIME_SLICE */
+  int32_t slicing_method;          /* SLICING_METHOD */
+  int32_t base_merit_method;       /* BASE_MERIT_METHOD (0..5) */
+  int32_t base_const_merit;        /* BASE_CONST_MERIT */
+  double default_bonus;            /* DEFAULT_BONUS */
+  double copy_mut_prob;            /* COPY_MUT_PROB */
+  double copy_ins_prob;            /* COPY_INS_PROB */
+  double copy_del_prob;            /* COPY_DEL_PROB */
+  double divide_mut_prob;          /* DIVIDE_MUT_PROB */
+  double divide_ins_prob;          /* DIVIDE_INS_PROB */
+  double divide_del_prob;          /* DIVIDE_DEL_PROB */
+  double offspring_size_range;     /* OFFSPRING_SIZE_RANGE */
+  double min_copied_lines;         /* MIN_COPIED_LINES */
+  double min_exe_lines;            /* MIN_EXE_LINES */
+  int32_t require_allocate;        /* REQUIRE_ALLOCATE */
+  int32_t death_method;            /* DEATH_METHOD 0/1/2 */
+  int32_t age_limit;               /* AGE_LIMIT */
+  int32_t alloc_method;            /* ALLOC_METHOD (0 default inst, 2 random) */
+  int32_t divide_method;           /* DIVIDE_METHOD (1 split) */
+  int32_t max_label_exe_size;      /* MAX_LABEL_EXE_SIZE */
+  int32_t birth_method;            /* BIRTH_METHOD (0 random nbhd, 3 empty only) */
+  int32_t prefer_empty;            /* PREFER_EMPTY */
+  int32_t allow_parent;            /* ALLOW_PARENT */
+  int32_t test_cpu_time_mod;       /* TEST_CPU_TIME_MOD */
+  int32_t min_genome_size;         /* MIN_GENOME_SIZE (0 = none) */
+  int32_t max_genome_size;         /* MAX_GENOME_SIZE (0 = none) */
+  int32_t inherit_merit;           /* INHERIT_MERIT */
+  double merit_default_bonus;      /* MERIT_DEFAULT_BONUS */
+  double required_bonus;           /* REQUIRED_BONUS */
+  uint64_t seed;                   /* RANDOM_SEED (counter-RNG key) */
+} avgpu_cfg;
+
+/* One REACTION line of environment.cfg (main/cEnvironment.cc:1185-1211),
+ * infinite-resource process on a logic-9 task. */
+typedef struct avgpu_reaction {
+  int32_t task;          /* avgpu_task */
+  int32_t type;          /* avgpu_proctype */
+  double value;          /* process:value */
+  double max_number;     /* process:max (consumed amount, default 1.0) */
+  int32_t min_count;     /* requisite:min_count (default 0) */
+  int32_t max_count;     /* requisite:max_count (INT32_MAX when absent) */
+  int32_t has_requisite; /* 0: TestRequisites returns !on_divide */
+  int32_t pad;
+} avgpu_reaction;
+
+/* Architectural + phenotype state of one organism: the tuple a
+ * cHardwareStatusPrinter trace shows (cpu/cHardwareCPU.cc:1111-1169) plus the
+ * phenotype counters the hot path mutates.  Used by avgpu_get_states /
+ * avgpu_set_states and by the oracle, so traces compare field by field. */
+typedef struct avgpu_cpu_state {
+  int32_t reg[3];                      /* AX BX CX */
+  int32_t head[4];                     /* IP READ WRITE FLOW */
+  int32_t stack[2][AVGPU_STACK_SIZE];  /* [0] thread stack, [1] global stack (raw ring) */
+  int32_t stack_ptr[2];
+  int32_t cur_stack;
+  int32_t read_label_len;
+  int8_t read_label[AVGPU_MAX_LABEL];  /* nop-mods */
+  int16_t pad0;
+  int32_t mal_active;
+  int32_t mem_size;
+  int32_t cpu_cycles_used;             /* cPhenotype::cpu_cycles_used */
+  int32_t time_used;                   /* cPhenotype::time_used */
+  int32_t gestation_start;
+  int32_t gestation_time;
+  int32_t num_divides;
+  int32_t generation;
+  int32_t alive;
+  int32_t genome_length;               /* cPhenotype::genome_length */
+  int32_t copied_size;                 /* cPhenotype::copied_size (inherited) */
+  int32_t child_copied_size;           /* cPhenotype::child_copied_size (SetLinesCopied) */
+  int32_t executed_size;               /* cPhenotype::executed_size (SetLinesExecuted) */
+  int32_t max_executed;                /* cOrganism::m_max_executed */
+  int32_t birth_length;                /* length of the genome the organism was born with */
+  int32_t input_ptr;                   /* cOrganism::m_input_pointer */
+  int32_t input_buf[3];                /* tBuffer<int> ring, most recent first */
+  int32_t input_total;
+  int32_t output_buf;                  /* capacity-1 output buffer */
+  int32_t output_total;
+  int32_t inputs[3];                   /* cell inputs (cPopulationCell::m_inputs) */
+  int32_t cur_task_count[AVGPU_MAX_REACTIONS];
+  int32_t last_task_count[AVGPU_MAX_REACTIONS];
+  int32_t cur_reaction_count[AVGPU_MAX_REACTIONS];
+  uint32_t rng_counter;                /* draws consumed from this organism's stream */
+  uint32_t rng_key_lo, rng_key_hi;
+  int32_t errors;                      /* cPhenotype::cur_num_errors (faults) */
+  double cur_bonus;
+  double merit;
+  double fitness;
+} avgpu_cpu_state;
+
+/* Result of one test-CPU gestation (cpu/cTestCPU.cc:144-326 +
+ * main/cPlasticPhenotype.cc) */
+typedef struct avgpu_test_result {
+  int32_t divided;        /* 1 if a divide happened within TEST_CPU_TIME_MOD*len */
+  int32_t copy_true;      /* offspring == genome */
+  int32_t copied_size;
+  int32_t executed_size;
+  int32_t gestation_time;
+  int32_t offspring_len;
+  int32_t genome_length;
+  int32_t time_used;
+  double merit;
+  double fitness;
+  int32_t task_count[AVGPU_MAX_REACTIONS];  /* last_task_count after divide */
+} avgpu_test_result;
+
+/* Per-update statistics (the reduction inputs of cStats / count.dat:
+ * main/cStats.cc:1081-1100). */
+typedef struct avgpu_update_stats {
+  int64_t update;
+  int64_t num_organisms;
+  int64_t insts_executed;      /* organism-instructions this update */
+  int64_t births;              /* offspring placed this update */
+  int64_t births_dropped;      /* birth-queue overflow or placement failure */
+  int64_t deaths;              /* old-age deaths this update */
+  int64_t divides;             /* successful divides this update */
+  int64_t task_orgs[AVGPU_MAX_REACTIONS]; /* organisms whose last gestation did task t */
+  double sum_merit;
+  double sum_fitness;
+  double sum_gestation;
+  double sum_genome_length;
+  double max_fitness;
+  double ave_generation;
+} avgpu_update_stats;
+
+typedef struct avgpu_world avgpu_world;   /* opaque handle */
+
+/* ---- lifecycle ---------------------------------------------------------- */
+const char* avgpu_last_error(void);
+void avgpu_cfg_defaults(avgpu_cfg* cfg);
+/* cWorld::setup + cPopulation::SetupCellGrid (main/cWorld.cc:95-200,
+ * main/cPopulation.cc:323-404): allocates SoA state for num_cells organisms
+ * (world_x*world_y when num_cells <= 0) on HIP device `device`. */
+avgpu_world* avgpu_create(const avgpu_cfg* cfg, int device, int64_t num_cells);
+int avgpu_destroy(avgpu_world* w);
+int avgpu_sync(avgpu_world* w);
+
+/* cInstSet::Load (cpu/cInstSet.cc:152-312): op code i runs handler
+ * handler_id[i] and is drawn by GetRandomInst with weight redundancy[i]
+ * (cpu/cInstSet.cc:83-88). The handler mapping must be injective. */
+int avgpu_load_instset(avgpu_world* w, int n, const uint8_t* handler_id,
+                       const int32_t* redundancy);
+/* cEnvironment::Load REACTION lines (main/cEnvironment.cc:1185-1211). */
+int avgpu_load_env(avgpu_world* w, int nreact, const avgpu_reaction* reactions);
+
+/* ---- population --------------------------------------------------------- */
+/* cPopulation::Inject / ActivateOrganism (main/cPopulation.cc:1320-1340) +
+ * cPhenotype::SetupInject (main/cPhenotype.cc:599-640): put `genome` in
+ * `cell`. inputs==NULL draws cell inputs from the cell's RNG stream
+ * (cEnvironment::SetupInputs random, main/cEnvironment.cc:1252-1296);
+ * deterministic_inputs!=0 uses the test-CPU constants instead. */
+int avgpu_set_org(avgpu_world* w, int64_t cell, const uint8_t* genome, int len,
+                  double merit, const int32_t* inputs);
+/* bulk form: genomes packed back to back, lens[i] each. */
+int avgpu_set_orgs(avgpu_world* w, int64_t first_cell, int64_t count,
+                   const uint8_t* genomes, const int32_t* lens, const double* merits,
+                   const int32_t* inputs /* count*3 or NULL */, int deterministic_inputs);
+/* cPopulation::KillOrganism (main/cPopulation.cc:2219-2290) */
+int avgpu_kill(avgpu_world* w, int64_t cell);
+
+/* ---- the hot path ------------------------------------------------------- */
+/* Batched cHardwareCPU::SingleProcess (cpu/cHardwareCPU.cc:908-1058): every
+ * live organism in [first_cell, first_cell+count) executes budget[i]
+ * instructions (budget==NULL: budget_uniform each) in the given avgpu_mode.
+ * Asynchronous on the handle's stream. */
+int avgpu_step(avgpu_world* w, int64_t first_cell, int64_t count,
+               const int32_t* budget, int32_t budget_uniform, int mode);
+/* One whole update of Avida2Driver::Run (targets/avida/Avida2Driver.cc:91-163):
+ * merit-weighted allotment of AVE_TIME_SLICE*N instructions (cScheduler),
+ * interpretation, birth placement (cPopulation::PositionOffspring,
+ * main/cPopulation.cc:5185-5414), statistics. out may be NULL (no host sync). */
+int avgpu_run_update(avgpu_world* w, avgpu_update_stats* out);
+int avgpu_run_updates(avgpu_world* w, int n_updates, avgpu_update_stats* last);
+
+/* ---- inspection (cHardwareBase inspection API, cpu/cHardwareBase.h:145-200) */
+int avgpu_get_states(avgpu_world* w, int64_t first_cell, int64_t count,
+                     avgpu_cpu_state* states, uint8_t* mem_ops, uint8_t* mem_flags,
+                     int mem_cap);
+/* Batched cTestCPU::TestGenome (cpu/cTestCPU.cc:190-326), one gestation
+ * each, deterministic inputs, mutations off. executed_flags (n*flags_cap)
+ * receives '+'/'-' for the parent part at the divide (or the whole memory
+ * at timeout), offspring (n*AVGPU_MAX_GENOME) the offspring op codes. */
+int avgpu_test_genomes(avgpu_world* w, int n, const uint8_t* genomes, const int32_t* lens,
+                       avgpu_test_result* results, char* executed_flags, int flags_cap,
+                       uint8_t* offspring);
+
+/* ---- statistics / multi-GPU plumbing ------------------------------------ */
+int avgpu_get_stats(avgpu_world* w, avgpu_update_stats* out);
+/* device pointer of the 32-double reduction vector of the last update
+ * (N, sum merit, executed, births, ...) for an external all-reduce
+ * (RCCL, cMultiProcessWorld.cc:375-405); avgpu_set_global_merit feeds the
+ * reduced totals back before the next allotment. */
+int avgpu_stats_vector(avgpu_world* w, void** dev_ptr);
+int avgpu_set_global_totals(avgpu_world* w, double total_merit, int64_t total_orgs);
+/* Halo births (cMultiProcessWorld.cc:142-190 migrant protocol): births that
+ * target cells outside this tile are packed into dev buffer records; see
+ * INTEGRATION.md for the record layout. */
+int avgpu_halo_pack(avgpu_world* w, int side, void* dev_buf, int64_t cap_records,
+                    int64_t* n_records);
+int avgpu_halo_unpack(avgpu_world* w, int side, const void* dev_buf, int64_t n_records);
+int64_t avgpu_halo_record_bytes(void);
+
+/* counters of the last avgpu_step: instructions executed (sum over lanes) */
+int avgpu_last_step_insts(avgpu_world* w, int64_t* insts);
+/* kernel timing of the dominant interpreter kernel in the last call
+ * (HIP events on the handle's stream), milliseconds summed over launches */
+int avgpu_last_kernel_ms(avgpu_world* w, double* ms, int64_t* launches);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* AVIDA_GPU_H */

@@ -1,0 +1,1171 @@
+// oracle/oracle.cc -- TEST INFRASTRUCTURE ONLY.
+//
+// CPU restatement of the fortunalab/avida hot path (heads-CPU execution,
+// test CPU, divide/mutation, logic-9 tasks, batch world update, and the
+// reference-style serial world loop used as the CPU baseline).  It is the
+// parity checker for the HIP path in avida_amd/csrc and is never linked into,
+// called by, or shipped with the product.  Only tests/, __graft_entry__.smoke()
+// and bench.py's cpu_baseline leg may load liboracle.so.
+//
+// The reference itself cannot be built here (libs/apto is an empty submodule;
+// see DESIGN.md "Oracle"), so this file restates its algorithms line by line.
+// Citations are avida-core/source/<path>:<line> of /root/reference.
+// Pinning: tests/test_oracle_golden.py checks it against the reference's own
+// RNG-free golden vectors (tests/_analyze_detail_all/expected/data/
+// detail-recalc.dat, 1794 genomes; the default-heads ancestor 389/97/100).
+//
+// RNG: Apto::RNG::AvidaRNG is absent, so (like the product) the oracle uses the
+// project's counter-based stream spec (DESIGN.md "RNG spec"); RNG-dependent
+// trajectories are therefore compared statistically to the reference, and
+// bit-exactly only between this oracle and the GPU path.
+//
+// Build: oracle/Makefile (g++ -O2 -ffp-contract=off).
+
+#include "../include/avida_gpu.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <cstdio>
+#include <cstdlib>
+#include <string>
+#include <vector>
+
+namespace {
+
+// ---------------------------------------------------------------------------
+// RNG spec: 32-bit counter-based draws keyed by a 64-bit stream id.
+static inline uint32_t lowbias32(uint32_t x) {
+  x ^= x >> 16; x *= 0x7feb352dU; x ^= x >> 15; x *= 0x846ca68bU; x ^= x >> 16;
+  return x;
+}
+struct Stream {
+  uint32_t lo = 0, hi = 0, ctr = 0;
+  uint32_t next() {
+    uint32_t a = lowbias32(ctr * 0x9E3779B9U + hi);
+    uint32_t b = lowbias32(a ^ lo);
+    ++ctr;
+    return b;
+  }
+  // cRandom::GetUInt(n) restated on a 32-bit draw
+  uint32_t uint_below(uint32_t n) { return (uint32_t)(((uint64_t)next() * n) >> 32); }
+  // cRandom::P(p): threshold precomputed as floor(p * 2^32)
+  bool p(uint64_t thresh) { return (uint64_t)next() < thresh; }
+};
+static inline uint64_t prob_thresh(double p) {
+  if (!(p > 0.0)) return 0;
+  if (p >= 1.0) return 1ULL << 32;
+  return (uint64_t)(p * 4294967296.0);
+}
+static inline void derive_key(uint32_t a_lo, uint32_t a_hi, uint32_t x, uint32_t y,
+                              uint32_t* lo, uint32_t* hi) {
+  *lo = lowbias32(lowbias32(x ^ a_lo) + y);
+  *hi = lowbias32(lowbias32(y ^ a_hi) + x + 0x632BE5ABU);
+}
+
+// ---------------------------------------------------------------------------
+// heads_default handler ids (include/avida_gpu.h enum avgpu_handler)
+enum { H_NOP_A = 0, H_NOP_B, H_NOP_C, H_IF_N_EQU, H_IF_LESS, H_POP, H_PUSH, H_SWAP_STK,
+       H_SWAP, H_SHIFT_R, H_SHIFT_L, H_INC, H_DEC, H_ADD, H_SUB, H_NAND, H_IO, H_H_ALLOC,
+       H_H_DIVIDE, H_H_COPY, H_H_SEARCH, H_MOV_HEAD, H_JMP_HEAD, H_GET_HEAD, H_IF_LABEL,
+       H_SET_FLOW };
+
+const int INST_ERROR = 255;  // cInstSet::GetInstError (cpu/cHeadCPU.h:167-170)
+const int REG_AX = 0, REG_BX = 1, REG_CX = 2;
+const int HEAD_IP = 0, HEAD_READ = 1, HEAD_WRITE = 2, HEAD_FLOW = 3;  // cpu/nHardware.h:32
+const int NUM_NOPS = 3;      // cpu/cHardwareCPU.h:64
+
+// cCPUMemory flag masks (cpu/cCPUMemory.h:31-37)
+const uint8_t F_COPIED = 0x01, F_MUTATED = 0x02, F_EXECUTED = 0x04, F_COPYMUT = 0x10;
+
+struct InstSet {
+  int n = 0;
+  int handler[256];
+  int nopmod[256];   // -1 if not a nop (cInstSet::IsNop / GetNopMod, cpu/cInstSet.h:127-131)
+  int64_t cum[256];  // cOrderedWeightedIndex cumulative weights (tools/cOrderedWeightedIndex.cc:43-50)
+  int64_t total = 0;
+  bool is_nop(int op) const { return op >= 0 && op < n && nopmod[op] >= 0; }
+  // cInstSet::GetRandomInst (cpu/cInstSet.cc:83-88) on the project RNG
+  int random_inst(Stream& s) const {
+    uint32_t r = s.uint_below((uint32_t)total);
+    for (int i = 0; i < n; i++) if (cum[i] > (int64_t)r) return i;
+    return n - 1;
+  }
+};
+
+struct Reaction {
+  avgpu_reaction r;
+  double mult;  // pow: 2^(max_number*value) ; mult: max_number*value
+  double add;
+};
+
+// cCodeLabel (cpu/cCodeLabel.h:76-100): nop sequence, AddNop ignores overflow.
+struct Label {
+  int8_t nops[AVGPU_MAX_LABEL];
+  int size = 0;
+  void clear() { size = 0; }
+  void add(int n) { if (size < AVGPU_MAX_LABEL) nops[size++] = (int8_t)n; }
+  void rotate(int rot, int base) {
+    for (int i = 0; i < size; i++) { nops[i] += rot; if (nops[i] >= base) nops[i] -= base; }
+  }
+  bool eq(const Label& o) const {
+    if (size != o.size) return false;
+    for (int i = 0; i < size; i++) if (nops[i] != o.nops[i]) return false;
+    return true;
+  }
+};
+
+// cCPUStack (cpu/cCPUStack.h:60-90)
+struct CPUStack {
+  int s[AVGPU_STACK_SIZE];
+  int sp = 0;
+  void clear() { for (int i = 0; i < AVGPU_STACK_SIZE; i++) s[i] = 0; sp = 0; }
+  void push(int v) { sp = (sp == 0) ? AVGPU_STACK_SIZE - 1 : sp - 1; s[sp] = v; }
+  int pop() { int v = s[sp]; s[sp] = 0; sp++; if (sp == AVGPU_STACK_SIZE) sp = 0; return v; }
+};
+
+// tBuffer<int> (tools/tBuffer.h:32-84)
+struct Buffer {
+  int data[3] = {0, 0, 0};
+  int cap = 1, offset = 0, total = 0;
+  void clear() { offset = 0; total = 0; }
+  void add(int v) { data[offset] = v; total++; offset++; offset %= cap; }
+  int operator[](int i) const { int idx = offset - i - 1; if (idx < 0) idx += cap; return data[idx]; }
+  int num_stored() const { return total <= cap ? total : cap; }
+};
+
+struct Org {
+  bool alive = false;
+  // hardware (cpu/cHardwareCPU.h:61-129)
+  std::vector<uint8_t> mem, flg;
+  int reg[3];
+  int head[4];
+  CPUStack stk[2];       // [0] thread-local stack, [1] m_global_stack
+  int cur_stack = 0;
+  Label read_label, next_label;
+  bool mal_active = false;
+  bool advance_ip = true;
+  // organism (main/cOrganism.h)
+  std::vector<uint8_t> genome;  // m_initial_genome (birth genome)
+  Buffer input_buf, output_buf;
+  int input_ptr = 0;
+  int max_executed = 0;
+  int inputs[3];
+  // phenotype (main/cPhenotype.h)
+  int cpu_cycles_used = 0, time_used = 0, gestation_start = 0, gestation_time = 0;
+  int num_divides = 0, generation = 0;
+  int genome_length = 0, copied_size = 0, child_copied_size = 0, executed_size = 0;
+  int errors = 0;
+  double cur_bonus = 1.0, merit = 0.0, fitness = 0.0;
+  int cur_task[AVGPU_MAX_REACTIONS], last_task[AVGPU_MAX_REACTIONS];
+  int cur_react[AVGPU_MAX_REACTIONS];
+  bool to_die = false;
+  // batch-world bookkeeping
+  Stream rng;
+  double credit = 0.0;
+  int spec_count = 0;
+  // test-CPU outputs
+  std::vector<uint8_t> offspring;
+  std::string exec_flags_at_divide;
+};
+
+struct Birth {
+  int64_t parent;
+  uint32_t seq;
+  std::vector<uint8_t> genome;
+  double merit;
+  int generation;
+  int child_copied, executed, gestation_time;
+  double fitness;
+  Stream rng;     // the child's stream
+  int64_t target = -1;
+  bool placed = false;
+};
+
+struct World {
+  avgpu_cfg cfg;
+  int64_t ncells = 0;
+  InstSet is;
+  std::vector<Reaction> react;
+  int num_tasks_in_env = 0;
+  std::vector<Org> orgs;
+  uint64_t th_copy_mut = 0, th_copy_ins = 0, th_copy_del = 0;
+  uint64_t th_div_mut = 0, th_div_ins = 0, th_div_del = 0;
+  // batch world
+  std::vector<Birth> births;
+  int64_t update = 0;
+  avgpu_update_stats stats;
+  int64_t step_insts = 0;
+  // multi-GPU style overrides (unused by the oracle tests unless set)
+  bool have_global = false;
+  double global_merit = 0.0;
+  int64_t global_orgs = 0;
+  Stream global_rng;   // serial world scheduler stream
+};
+
+thread_local std::string g_err;
+static int g_trace = getenv("ORACLE_TRACE") ? 1 : 0;
+int fail(int code, const std::string& msg) { g_err = msg; return code; }
+
+// cHeadCPU::Adjust / fullAdjust (cpu/cHeadCPU.h:63, cpu/cHeadCPU.cc:27-50)
+static inline int adjust(int pos, int size) {
+  if (pos >= 0 && pos < size) return pos;
+  if (size == 0 || pos < 0) return 0;
+  if (pos < 2 * size) return pos - size;
+  return pos % size;
+}
+static inline int wrap_add(int a, int b) { return (int)((uint32_t)a + (uint32_t)b); }
+
+struct Exec {
+  World& w;
+  Org& o;
+  int mode;
+  bool stop = false;   // TEST mode: gestation finished
+
+  int size() const { return (int)o.mem.size(); }
+  // cHeadCPU::GetNextInst (cpu/cHeadCPU.h:167-170)
+  int next_inst(int pos) const { return (pos + 1 == size()) ? INST_ERROR : o.mem[pos + 1]; }
+  void advance_ip() { o.head[HEAD_IP] = adjust(o.head[HEAD_IP] + 1, size()); }
+
+  // FindModifiedRegister / FindModifiedHead (cpu/cHardwareCPU.cc:1622-1672)
+  int find_modified(int def) {
+    int nx = next_inst(o.head[HEAD_IP]);
+    if (w.is.is_nop(nx)) {
+      advance_ip();
+      def = w.is.nopmod[o.mem[o.head[HEAD_IP]]];
+      o.flg[o.head[HEAD_IP]] |= F_EXECUTED;
+    }
+    return def;
+  }
+  static int next_reg(int r) { return (r + 1) % 3; }  // FindNextRegister :1676-1679
+
+  // cHardwareCPU::ReadLabel (cpu/cHardwareCPU.cc:1484-1502)
+  void read_label() {
+    int count = 0;
+    o.next_label.clear();
+    while (w.is.is_nop(next_inst(o.head[HEAD_IP])) && count < AVGPU_MAX_LABEL) {
+      count++;
+      advance_ip();
+      o.next_label.add(w.is.nopmod[o.mem[o.head[HEAD_IP]]]);
+      if (o.next_label.size <= w.cfg.max_label_exe_size) o.flg[o.head[HEAD_IP]] |= F_EXECUTED;
+    }
+  }
+
+  // FindLabel_Forward (cpu/cHardwareCPU.cc:1219-1295)
+  int find_label_forward(const Label& lab, int pos) {
+    const int gsize = size();
+    int search_start = pos;
+    int label_size = lab.size;
+    bool found = false;
+    pos += label_size;
+    while (pos < gsize) {
+      if (w.is.is_nop(o.mem[pos])) {
+        int start_pos = pos, end_pos = pos + 1;
+        while (start_pos > search_start && w.is.is_nop(o.mem[start_pos - 1])) start_pos--;
+        while (end_pos < gsize && w.is.is_nop(o.mem[end_pos])) end_pos++;
+        int test_size = end_pos - start_pos;
+        int max_offset = test_size - label_size + 1;
+        int offset;
+        for (offset = start_pos; offset < start_pos + max_offset; offset++) {
+          int m;
+          for (m = 0; m < label_size; m++)
+            if (lab.nops[m] != w.is.nopmod[o.mem[offset + m]]) break;
+          if (m == label_size) { found = true; break; }
+        }
+        if (found) { pos = label_size + offset; break; }
+        pos = end_pos;
+      }
+      pos += label_size;
+    }
+    if (!found) pos = -1;
+    return pos;
+  }
+
+  // FindLabel(0) (cpu/cHardwareCPU.cc:1177-1212): returns the position of the
+  // search head (IP copy when label empty / not found)
+  int find_label_from_start() {
+    int ip = o.head[HEAD_IP];
+    if (o.next_label.size == 0) return ip;
+    int found = find_label_forward(o.next_label, 0);
+    if (found >= 0) return adjust(found - 1, size());  // search_head.Set(found_pos - 1)
+    return ip;
+  }
+
+  // cHardwareCPU::Allocate_Main (cpu/cHardwareCPU.cc:1707-1763)
+  bool allocate_main(int allocated_size) {
+    if (w.cfg.require_allocate && o.mal_active) { o.errors++; return false; }
+    if (allocated_size < 1) { o.errors++; return false; }
+    const int old_size = size();
+    const int new_size = old_size + allocated_size;
+    if (new_size > AVGPU_MAX_GENOME || new_size < AVGPU_MIN_GENOME) { o.errors++; return false; }
+    const int max_alloc = (int)(old_size * w.cfg.offspring_size_range);
+    if (allocated_size > max_alloc) { o.errors++; return false; }
+    const int max_old = (int)(allocated_size * w.cfg.offspring_size_range);
+    if (old_size > max_old) { o.errors++; return false; }
+    o.mem.resize(new_size, 0);   // ALLOC_METHOD 0: new sites are op 0 (Allocate_Default :1698-1705)
+    o.flg.resize(new_size, 0);
+    if (w.cfg.alloc_method == 2) {  // ALLOC_METHOD_RANDOM (Allocate_Random :1688-1696)
+      for (int i = old_size; i < new_size; i++) o.mem[i] = (uint8_t)w.is.random_inst(o.rng);
+    }
+    o.mal_active = true;
+    return true;
+  }
+
+  // CalcSizeMerit (main/cPhenotype.cc:1760-1816)
+  int calc_size_merit() const {
+    switch (w.cfg.base_merit_method) {
+      case 1: return o.copied_size;
+      case 2: return o.executed_size;
+      case 3: return o.genome_length;
+      case 4: { int s = o.genome_length; if (s > o.copied_size) s = o.copied_size;
+                if (s > o.executed_size) s = o.executed_size; return s; }
+      case 5: { int s = o.genome_length; if (s > o.copied_size) s = o.copied_size;
+                if (s > o.executed_size) s = o.executed_size; return (int)std::sqrt((double)s); }
+      default: return w.cfg.base_const_merit;
+    }
+  }
+
+  // cHardwareCPU::Reset -> internalReset + cLocalThread::Reset (cpu/cHardwareCPU.cc:813-900)
+  void hw_reset() {
+    for (int i = 0; i < 3; i++) o.reg[i] = 0;
+    for (int i = 0; i < 4; i++) o.head[i] = 0;
+    o.stk[0].clear(); o.stk[1].clear();
+    o.cur_stack = 0;
+    o.read_label.clear(); o.next_label.clear();
+    o.mal_active = false;
+  }
+
+  // cPhenotype::DivideReset / TestDivideReset (main/cPhenotype.cc:824-1000, :1064-1180)
+  void divide_reset() {
+    double base = (double)calc_size_merit();
+    if (w.cfg.merit_default_bonus != 0.0) o.cur_bonus = w.cfg.merit_default_bonus;
+    o.merit = base * o.cur_bonus;
+    if (w.cfg.inherit_merit == 0) o.merit = base;
+    o.genome_length = (int)o.genome.size();
+    o.gestation_time = o.time_used - o.gestation_start;
+    o.gestation_start = o.time_used;
+    o.fitness = base * o.cur_bonus / o.gestation_time;   // CalcFitness :1827 (FITNESS_METHOD 0)
+    for (int i = 0; i < AVGPU_MAX_REACTIONS; i++) {
+      o.last_task[i] = o.cur_task[i];
+      o.cur_task[i] = 0;
+      o.cur_react[i] = 0;
+    }
+    o.cur_bonus = w.cfg.default_bonus;
+    o.cpu_cycles_used = 0;
+    o.errors = 0;
+    o.num_divides++;
+    if (mode == AVGPU_MODE_TEST) o.generation++;  // TestDivideReset :1160; world: GENERATION_INC_METHOD 1
+    else o.generation++;
+  }
+
+  // Divide_DoMutations (cpu/cHardwareBase.cc:296-569), the default-config subset:
+  // divide slip (always draws), divide mut, ins, del (always draw); per-site
+  // rates and parent mutations are zero in every config on this path.
+  void divide_mutations(std::vector<uint8_t>& child) {
+    Stream& r = o.rng;
+    int max_g = w.cfg.max_genome_size; if (!max_g || max_g > AVGPU_MAX_GENOME) max_g = AVGPU_MAX_GENOME;
+    int min_g = w.cfg.min_genome_size; if (!min_g || min_g < AVGPU_MIN_GENOME) min_g = AVGPU_MIN_GENOME;
+    if (w.th_div_mut && r.p(w.th_div_mut)) {
+      uint32_t line = r.uint_below((uint32_t)child.size());
+      child[line] = (uint8_t)w.is.random_inst(r);
+    }
+    if (w.th_div_ins && r.p(w.th_div_ins) && (int)child.size() < max_g) {
+      uint32_t line = r.uint_below((uint32_t)child.size() + 1);
+      child.insert(child.begin() + line, (uint8_t)w.is.random_inst(r));
+    }
+    if (w.th_div_del && r.p(w.th_div_del) && (int)child.size() > min_g) {
+      uint32_t line = r.uint_below((uint32_t)child.size());
+      child.erase(child.begin() + line);
+    }
+  }
+
+  // Divide_CheckViable (cpu/cHardwareBase.cc:140-289 + main/cOrganism.cc:788-919)
+  bool check_viable(int parent_size, int child_size, int* exe_out, int* copied_out) {
+    const int genome_size = (int)o.genome.size();
+    const double range = w.cfg.offspring_size_range;
+    const int min_size = std::max(AVGPU_MIN_GENOME, (int)(genome_size / range));
+    const int max_size = std::min(AVGPU_MAX_GENOME, (int)(genome_size * range));
+    if (child_size < min_size || child_size > max_size) { o.errors++; return false; }
+    if (parent_size < min_size || parent_size > max_size) { o.errors++; return false; }
+    const int ming = w.cfg.min_genome_size, maxg = w.cfg.max_genome_size;
+    if ((ming && child_size < ming) || (maxg && child_size > maxg)) { o.errors++; return false; }
+    if ((ming && parent_size < ming) || (maxg && parent_size > maxg)) { o.errors++; return false; }
+    int executed = 0;
+    for (int i = 0; i < parent_size; i++) if (o.flg[i] & F_EXECUTED) executed++;
+    const int min_exe = (int)(parent_size * w.cfg.min_exe_lines);
+    if (executed < min_exe) { o.errors++; return false; }
+    int copied = 0;
+    for (int i = parent_size; i < parent_size + child_size; i++) if (o.flg[i] & F_COPIED) copied++;
+    const int min_copied = (int)(child_size * w.cfg.min_copied_lines);
+    if (copied < min_copied) { o.errors++; return false; }
+    // cOrganism::Divide_CheckViable
+    if (o.cur_bonus < w.cfg.required_bonus) return false;
+    double base = (double)calc_size_merit();
+    double bonus = o.cur_bonus;
+    if (w.cfg.merit_default_bonus != 0.0) bonus = w.cfg.merit_default_bonus;
+    double off_merit = base * bonus;
+    if (w.cfg.inherit_merit == 0) off_merit = base;
+    if (off_merit == 0) return false;
+    *exe_out = executed; *copied_out = copied;
+    return true;
+  }
+
+  // Inst_HeadDivideMut -> Divide_Main (cpu/cHardwareCPU.cc:6942-6959, :1775-1843)
+  bool h_divide(int64_t cell) {
+    const int sz0 = size();
+    for (int i = 0; i < 4; i++) o.head[i] = adjust(o.head[i], sz0);  // AdjustHeads
+    const int div_point = o.head[HEAD_READ];
+    int child_end = o.head[HEAD_WRITE];
+    if (child_end == 0) child_end = sz0;
+    const int extra = sz0 - child_end;
+    const int child_size = sz0 - div_point - extra;
+    int exe = 0, cop = 0;
+    if (!check_viable(div_point, child_size, &exe, &cop)) {
+      for (int i = 0; i < 4; i++) o.head[i] = adjust(o.head[i], size());
+      return false;
+    }
+    o.executed_size = exe;       // SetLinesExecuted
+    o.child_copied_size = cop;   // SetLinesCopied
+    std::vector<uint8_t> child(o.mem.begin() + div_point, o.mem.begin() + div_point + child_size);
+    if (mode == AVGPU_MODE_TEST) {
+      o.exec_flags_at_divide.assign(div_point, '-');
+      for (int i = 0; i < div_point; i++) if (o.flg[i] & F_EXECUTED) o.exec_flags_at_divide[i] = '+';
+    }
+    o.mem.resize(div_point);
+    o.flg.resize(div_point);
+    if (mode == AVGPU_MODE_WORLD) divide_mutations(child);
+    o.mal_active = false;
+    o.advance_ip = false;   // DIVIDE_METHOD_SPLIT
+    // ActivateDivide: the on-divide DoOutput runs no reaction for logic-9
+    // environments (every requisite has divide_only 0; TestRequisites :1408).
+    divide_reset();
+    if (mode == AVGPU_MODE_WORLD) {
+      Birth b;
+      b.parent = cell;
+      b.seq = (uint32_t)o.num_divides;
+      b.genome = child;
+      b.merit = o.merit;
+      b.generation = o.generation;
+      b.child_copied = o.child_copied_size;
+      b.executed = o.executed_size;
+      b.gestation_time = o.gestation_time;
+      b.fitness = o.fitness;
+      derive_key(o.rng.lo, o.rng.hi, (uint32_t)o.num_divides, 0x1B873593U, &b.rng.lo, &b.rng.hi);
+      b.rng.ctr = 0;
+      w.births.push_back(std::move(b));
+    } else if (mode == AVGPU_MODE_TEST) {
+      o.offspring = child;
+      stop = true;
+    }
+    // parent alive: Reset + ClearFlags (:1836-1839)
+    hw_reset();
+    std::fill(o.flg.begin(), o.flg.end(), 0);
+    return true;
+  }
+
+  // cTaskLib::SetupTests logic id (main/cTaskLib.cc:369-448)
+  static int logic_id(const Buffer& in, int out_val) {
+    const int num_inputs = in.num_stored();
+    int ti[3];
+    for (int i = 0; i < 3; i++) ti[i] = (num_inputs > i) ? in[i] : 0;
+    int to = out_val;
+    int lo[8];
+    for (int i = 0; i < 8; i++) lo[i] = -1;
+    for (int tp = 0; tp < 32; tp++) {
+      int lp = 0;
+      for (int i = 0; i < 3; i++) lp += (ti[i] & 1) << i;
+      if (lo[lp] != -1 && lo[lp] != (to & 1)) return -1;
+      lo[lp] = to & 1;
+      to >>= 1;
+      for (int i = 0; i < 3; i++) ti[i] >>= 1;
+    }
+    if (num_inputs < 1) lo[1] = lo[0];
+    if (num_inputs < 2) { lo[2] = lo[0]; lo[3] = lo[1]; }
+    if (num_inputs < 3) { lo[4] = lo[0]; lo[5] = lo[1]; lo[6] = lo[2]; lo[7] = lo[3]; }
+    int id = 0;
+    for (int i = 0; i < 8; i++) id += lo[i] << i;
+    return id;
+  }
+  // Task_Not ... Task_Equ (main/cTaskLib.cc:511-575)
+  static bool task_done(int task, int id) {
+    switch (task) {
+      case 0: return id == 15 || id == 51 || id == 85;
+      case 1: return id == 63 || id == 95 || id == 119;
+      case 2: return id == 136 || id == 160 || id == 192;
+      case 3: return id == 175 || id == 187 || id == 207 || id == 221 || id == 243 || id == 245;
+      case 4: return id == 238 || id == 250 || id == 252;
+      case 5: return id == 10 || id == 12 || id == 34 || id == 48 || id == 68 || id == 80;
+      case 6: return id == 3 || id == 5 || id == 17;
+      case 7: return id == 60 || id == 90 || id == 102;
+      case 8: return id == 153 || id == 165 || id == 195;
+    }
+    return false;
+  }
+
+  // cOrganism::DoOutput -> cPhenotype::TestOutput -> cEnvironment::TestOutput
+  // (main/cOrganism.cc:385-521, main/cPhenotype.cc:1493-1700,
+  //  main/cEnvironment.cc:1314-1406, :1408-1503, :1610-1760)
+  void do_output(int value) {
+    o.output_buf.add(value);
+    const int id = logic_id(o.input_buf, o.output_buf[0]);
+    bool done[AVGPU_MAX_REACTIONS] = {false};
+    double mult = 1.0, add = 0.0;
+    bool any = false;
+    for (size_t i = 0; i < w.react.size(); i++) {
+      const avgpu_reaction& r = w.react[i].r;
+      const int task_cnt = o.cur_task[r.task];    // eff_task_count
+      if (r.has_requisite) {
+        if (task_cnt < r.min_count) continue;
+        if (task_cnt >= r.max_count) continue;
+      }
+      if (id < 0 || !task_done(r.task, id)) continue;
+      done[r.task] = true;
+      any = true;
+      if (r.type == AVGPU_PROC_POW) mult *= w.react[i].mult;
+      else if (r.type == AVGPU_PROC_MULT) mult *= w.react[i].mult;
+      else add += w.react[i].add;
+      o.cur_react[i]++;
+    }
+    if (!any) return;
+    for (int t = 0; t < AVGPU_MAX_REACTIONS; t++) if (done[t]) o.cur_task[t]++;
+    o.cur_bonus *= mult;
+    o.cur_bonus += add;
+  }
+
+  // cOrganism::GetNextInput (main/cOrganism.h:249 -> main/cPopulationCell.h:214-218,
+  // cpu/cTestCPU.h:132-136)
+  int next_input() {
+    if (o.input_ptr >= 3) o.input_ptr = 0;
+    return o.inputs[o.input_ptr++];
+  }
+
+  // Inst_HeadCopy (cpu/cHardwareCPU.cc:7130-7167)
+  void h_copy() {
+    const int sz = size();
+    int& rh = o.head[HEAD_READ];
+    int& wh = o.head[HEAD_WRITE];
+    rh = adjust(rh, sz);
+    wh = adjust(wh, sz);
+    int read_inst = o.mem[rh];
+    // ReadInst (:1459-1466)
+    if (w.is.is_nop(read_inst)) o.read_label.add(read_inst); else o.read_label.clear();
+    // the test CPU runs with cleared mutation rates (cpu/cTestCPU.cc:270,
+    // main/cMutationRates.cc:78-120)
+    const bool muts = mode != AVGPU_MODE_TEST;
+    if (muts && w.th_copy_mut && o.rng.p(w.th_copy_mut)) {
+      read_inst = w.is.random_inst(o.rng);
+      o.flg[wh] |= F_MUTATED | F_COPYMUT;
+    }
+    o.mem[wh] = (uint8_t)read_inst;
+    o.flg[wh] |= F_COPIED;
+    if (muts && w.th_copy_ins && o.rng.p(w.th_copy_ins) && size() < AVGPU_MAX_GENOME) {
+      int ins = w.is.random_inst(o.rng);
+      o.mem.insert(o.mem.begin() + wh, (uint8_t)ins);
+      o.flg.insert(o.flg.begin() + wh, 0);
+    }
+    if (muts && w.th_copy_del && o.rng.p(w.th_copy_del) && size() > 1) {
+      o.mem.erase(o.mem.begin() + wh);
+      o.flg.erase(o.flg.begin() + wh);
+    }
+    rh = adjust(rh + 1, size());
+    wh = adjust(wh + 1, size());
+  }
+
+  // One SingleProcess cycle (cpu/cHardwareCPU.cc:908-1058), single thread,
+  // no costs / promoters / speculation.  Returns true if the instruction ran.
+  void single_process(int64_t cell) {
+    o.cpu_cycles_used++;
+    o.time_used++;
+    o.advance_ip = true;
+    o.head[HEAD_IP] = adjust(o.head[HEAD_IP], size());
+    const int op = o.mem[o.head[HEAD_IP]];
+    if (g_trace) {
+      fprintf(stderr, "%d IP:%d op:%d AX:%d BX:%d CX:%d R:%d W:%d F:%d RL:", o.cpu_cycles_used,
+              o.head[HEAD_IP], op, o.reg[0], o.reg[1], o.reg[2], o.head[1], o.head[2], o.head[3]);
+      for (int i = 0; i < o.read_label.size; i++) fputc('A' + o.read_label.nops[i], stderr);
+      fprintf(stderr, " mem:%d\n", (int)o.mem.size());
+    }
+    o.flg[o.head[HEAD_IP]] |= F_EXECUTED;
+    switch (w.is.handler[op]) {
+      case H_NOP_A: case H_NOP_B: case H_NOP_C: break;
+      case H_IF_N_EQU: { int a = find_modified(REG_BX), b = next_reg(a);
+        if (o.reg[a] == o.reg[b]) advance_ip(); break; }
+      case H_IF_LESS: { int a = find_modified(REG_BX), b = next_reg(a);
+        if (o.reg[a] >= o.reg[b]) advance_ip(); break; }
+      case H_POP: { int r = find_modified(REG_BX); o.reg[r] = o.stk[o.cur_stack].pop(); break; }
+      case H_PUSH: { int r = find_modified(REG_BX); o.stk[o.cur_stack].push(o.reg[r]); break; }
+      case H_SWAP_STK: o.cur_stack = o.cur_stack ? 0 : 1; break;
+      case H_SWAP: { int a = find_modified(REG_BX), b = next_reg(a);
+        std::swap(o.reg[a], o.reg[b]); break; }
+      case H_SHIFT_R: { int r = find_modified(REG_BX); o.reg[r] >>= 1; break; }
+      case H_SHIFT_L: { int r = find_modified(REG_BX); o.reg[r] = (int)((uint32_t)o.reg[r] << 1); break; }
+      case H_INC: { int r = find_modified(REG_BX); o.reg[r] = wrap_add(o.reg[r], 1); break; }
+      case H_DEC: { int r = find_modified(REG_BX); o.reg[r] = wrap_add(o.reg[r], -1); break; }
+      case H_ADD: { int r = find_modified(REG_BX); o.reg[r] = wrap_add(o.reg[REG_BX], o.reg[REG_CX]); break; }
+      case H_SUB: { int r = find_modified(REG_BX);
+        o.reg[r] = (int)((uint32_t)o.reg[REG_BX] - (uint32_t)o.reg[REG_CX]); break; }
+      case H_NAND: { int r = find_modified(REG_BX); o.reg[r] = ~(o.reg[REG_BX] & o.reg[REG_CX]); break; }
+      case H_IO: { int r = find_modified(REG_BX);
+        do_output(o.reg[r]);
+        int in = next_input();
+        o.reg[r] = in;
+        o.input_buf.add(in);
+        break; }
+      case H_H_ALLOC: {  // Inst_MaxAlloc (:3294-3303)
+        const int cur = size();
+        const int alloc = std::min((int)(w.cfg.offspring_size_range * cur), AVGPU_MAX_GENOME - cur);
+        if (allocate_main(alloc)) o.reg[REG_AX] = cur;
+        break; }
+      case H_H_DIVIDE: h_divide(cell); break;
+      case H_H_COPY: h_copy(); break;
+      case H_H_SEARCH: {  // :7245-7256
+        read_label();
+        o.next_label.rotate(1, NUM_NOPS);
+        int found = find_label_from_start();
+        o.reg[REG_BX] = found - o.head[HEAD_IP];
+        o.reg[REG_CX] = o.next_label.size;
+        o.head[HEAD_FLOW] = found;                               // Set(found_pos): copy, no adjust
+        o.head[HEAD_FLOW] = adjust(o.head[HEAD_FLOW] + 1, size()); // Advance
+        break; }
+      case H_MOV_HEAD: { int h = find_modified(HEAD_IP);
+        o.head[h] = o.head[HEAD_FLOW];
+        if (h == HEAD_IP) o.advance_ip = false;
+        break; }
+      case H_JMP_HEAD: { int h = find_modified(HEAD_IP);
+        o.head[h] = adjust(wrap_add(o.head[h], o.reg[REG_CX]), size()); break; }
+      case H_GET_HEAD: { int h = find_modified(HEAD_IP); o.reg[REG_CX] = o.head[h]; break; }
+      case H_IF_LABEL: {
+        read_label();
+        o.next_label.rotate(1, NUM_NOPS);
+        if (!o.next_label.eq(o.read_label)) advance_ip();
+        break; }
+      case H_SET_FLOW: { int r = find_modified(REG_CX);
+        o.head[HEAD_FLOW] = adjust(o.reg[r], size()); break; }
+      default: break;
+    }
+    if (stop) return;
+    if (o.advance_ip) advance_ip();
+    // death (:1045-1049)
+    if ((o.max_executed > 0 && o.time_used >= o.max_executed) || o.to_die) o.alive = false;
+  }
+};
+
+// cPhenotype::SetupInject + cOrganism::initialize (main/cPhenotype.cc:599-640,
+// main/cOrganism.cc:216-236)
+void setup_inject(World& w, Org& o, const uint8_t* genome, int len, double merit) {
+  o = Org();
+  o.alive = true;
+  o.genome.assign(genome, genome + len);
+  o.mem = o.genome;
+  o.flg.assign(len, 0);
+  for (int i = 0; i < 3; i++) o.reg[i] = 0;
+  for (int i = 0; i < 4; i++) o.head[i] = 0;
+  o.stk[0].clear(); o.stk[1].clear();
+  o.input_buf.cap = 3; o.output_buf.cap = 1;
+  o.genome_length = len; o.copied_size = len; o.executed_size = len; o.child_copied_size = 0;
+  o.merit = merit > 0 ? merit : (double)len;
+  o.cur_bonus = w.cfg.default_bonus;
+  for (int i = 0; i < AVGPU_MAX_REACTIONS; i++) { o.cur_task[i] = o.last_task[i] = o.cur_react[i] = 0; }
+  o.max_executed = 0;
+  if (w.cfg.death_method > 0) {
+    o.max_executed = w.cfg.age_limit;
+    if (w.cfg.death_method == 2) o.max_executed *= len;
+    if (o.max_executed < 1) o.max_executed = 1;
+  }
+}
+
+void dump_state(const World& w, const Org& o, avgpu_cpu_state* s, uint8_t* ops, uint8_t* flags, int cap) {
+  memset(s, 0, sizeof(*s));
+  for (int i = 0; i < 3; i++) s->reg[i] = o.reg[i];
+  for (int i = 0; i < 4; i++) s->head[i] = o.head[i];
+  for (int k = 0; k < 2; k++) {
+    for (int i = 0; i < AVGPU_STACK_SIZE; i++) s->stack[k][i] = o.stk[k].s[i];
+    s->stack_ptr[k] = o.stk[k].sp;
+  }
+  s->cur_stack = o.cur_stack;
+  s->read_label_len = o.read_label.size;
+  for (int i = 0; i < o.read_label.size; i++) s->read_label[i] = o.read_label.nops[i];
+  s->mal_active = o.mal_active;
+  s->mem_size = (int)o.mem.size();
+  s->cpu_cycles_used = o.cpu_cycles_used;
+  s->time_used = o.time_used;
+  s->gestation_start = o.gestation_start;
+  s->gestation_time = o.gestation_time;
+  s->num_divides = o.num_divides;
+  s->generation = o.generation;
+  s->alive = o.alive;
+  s->genome_length = o.genome_length;
+  s->copied_size = o.copied_size;
+  s->child_copied_size = o.child_copied_size;
+  s->executed_size = o.executed_size;
+  s->max_executed = o.max_executed;
+  s->birth_length = (int)o.genome.size();
+  s->input_ptr = o.input_ptr;
+  for (int i = 0; i < 3; i++) s->input_buf[i] = (i < o.input_buf.num_stored()) ? o.input_buf[i] : 0;
+  s->input_total = o.input_buf.total;
+  s->output_buf = o.output_buf.total ? o.output_buf[0] : 0;
+  s->output_total = o.output_buf.total;
+  for (int i = 0; i < 3; i++) s->inputs[i] = o.inputs[i];
+  for (int i = 0; i < AVGPU_MAX_REACTIONS; i++) {
+    s->cur_task_count[i] = o.cur_task[i];
+    s->last_task_count[i] = o.last_task[i];
+    s->cur_reaction_count[i] = o.cur_react[i];
+  }
+  s->rng_counter = o.rng.ctr;
+  s->rng_key_lo = o.rng.lo;
+  s->rng_key_hi = o.rng.hi;
+  s->errors = o.errors;
+  s->cur_bonus = o.cur_bonus;
+  s->merit = o.merit;
+  s->fitness = o.fitness;
+  (void)w;
+  if (ops && flags) {
+    for (int i = 0; i < cap; i++) {
+      ops[i] = i < (int)o.mem.size() ? o.mem[i] : 0;
+      // exported flags: bit0 copied, bit2 executed (the execution-relevant bits)
+      flags[i] = i < (int)o.flg.size() ? (o.flg[i] & (F_COPIED | F_EXECUTED)) : 0;
+    }
+  }
+}
+
+// Deterministic total merit: fixed 256-cell blocks, pairwise tree, then block
+// partials in order (the same order the device reduction uses).
+double tree_merit_sum(const World& w, int64_t* n_alive) {
+  int64_t nb = (w.ncells + 255) / 256;
+  double total = 0.0;
+  int64_t cnt = 0;
+  for (int64_t b = 0; b < nb; b++) {
+    double s[256];
+    for (int i = 0; i < 256; i++) {
+      int64_t c = b * 256 + i;
+      s[i] = (c < w.ncells && w.orgs[c].alive) ? w.orgs[c].merit : 0.0;
+      if (c < w.ncells && w.orgs[c].alive) cnt++;
+    }
+    for (int stride = 128; stride >= 1; stride >>= 1)
+      for (int i = 0; i < stride; i++) s[i] = s[i] + s[i + stride];
+    total = total + s[0];
+  }
+  *n_alive = cnt;
+  return total;
+}
+
+// torus / grid neighbourhood (tools/cTopology.h:40-55 build_torus/build_grid),
+// fixed order: NW N NE W E SW S SE
+int neighbours(const World& w, int64_t cell, int64_t* out) {
+  const int X = w.cfg.world_x, Y = w.cfg.world_y;
+  const int x = (int)(cell % X), y = (int)(cell / X);
+  int n = 0;
+  for (int dy = -1; dy <= 1; dy++)
+    for (int dx = -1; dx <= 1; dx++) {
+      if (dx == 0 && dy == 0) continue;
+      int nx = x + dx, ny = y + dy;
+      if (w.cfg.world_geometry == 1) {
+        if (nx < 0 || nx >= X || ny < 0 || ny >= Y) continue;
+      } else {
+        nx = (nx + X) % X; ny = (ny + Y) % Y;
+      }
+      out[n++] = (int64_t)ny * X + nx;
+    }
+  return n;
+}
+
+// cPopulation::ActivateOrganism for a child (main/cPopulation.cc:1320-1340)
+// + cPhenotype::SetupOffspring (main/cPhenotype.cc:349-420)
+void activate_child(World& w, Birth& b, int64_t cell) {
+  Org& o = w.orgs[cell];
+  setup_inject(w, o, b.genome.data(), (int)b.genome.size(), b.merit);
+  o.merit = b.merit;
+  o.copied_size = b.child_copied;
+  o.executed_size = b.executed;
+  o.gestation_time = b.gestation_time;
+  o.fitness = b.fitness;
+  o.generation = b.generation;
+  o.rng = b.rng;
+  // cEnvironment::SetupInputs random (main/cEnvironment.cc:1268-1271)
+  o.inputs[0] = (15 << 24) + (int)o.rng.uint_below(1u << 24);
+  o.inputs[1] = (51 << 24) + (int)o.rng.uint_below(1u << 24);
+  o.inputs[2] = (85 << 24) + (int)o.rng.uint_below(1u << 24);
+}
+
+}  // namespace
+
+// ===========================================================================
+extern "C" {
+
+const char* orc_last_error(void) { return g_err.c_str(); }
+
+void* orc_create(const avgpu_cfg* cfg, int64_t ncells) {
+  World* w = new World();
+  w->cfg = *cfg;
+  w->ncells = ncells > 0 ? ncells : (int64_t)cfg->world_x * cfg->world_y;
+  w->orgs.resize(w->ncells);
+  w->th_copy_mut = prob_thresh(cfg->copy_mut_prob);
+  w->th_copy_ins = prob_thresh(cfg->copy_ins_prob);
+  w->th_copy_del = prob_thresh(cfg->copy_del_prob);
+  w->th_div_mut = prob_thresh(cfg->divide_mut_prob);
+  w->th_div_ins = prob_thresh(cfg->divide_ins_prob);
+  w->th_div_del = prob_thresh(cfg->divide_del_prob);
+  memset(&w->stats, 0, sizeof(w->stats));
+  derive_key((uint32_t)cfg->seed, (uint32_t)(cfg->seed >> 32), 0x5CEDu, 0xC0FFEEu,
+             &w->global_rng.lo, &w->global_rng.hi);
+  return w;
+}
+
+void orc_destroy(void* h) { delete (World*)h; }
+
+int orc_load_instset(void* h, int n, const uint8_t* handler_id, const int32_t* redundancy) {
+  World& w = *(World*)h;
+  if (n <= 0 || n > AVGPU_MAX_INST) return fail(AVGPU_EINVAL, "bad instset size");
+  w.is.n = n;
+  int64_t cum = 0;
+  for (int i = 0; i < n; i++) {
+    w.is.handler[i] = handler_id[i];
+    w.is.nopmod[i] = handler_id[i] <= 2 ? handler_id[i] : -1;
+    cum += redundancy[i];
+    w.is.cum[i] = cum;
+  }
+  w.is.total = cum;
+  return 0;
+}
+
+int orc_load_env(void* h, int n, const avgpu_reaction* r) {
+  World& w = *(World*)h;
+  w.react.clear();
+  for (int i = 0; i < n; i++) {
+    Reaction x;
+    x.r = r[i];
+    double bonus = r[i].max_number * r[i].value;
+    x.mult = (r[i].type == AVGPU_PROC_POW) ? std::pow(2.0, bonus) : bonus;
+    x.add = bonus;
+    w.react.push_back(x);
+  }
+  return 0;
+}
+
+int orc_set_orgs(void* h, int64_t first, int64_t count, const uint8_t* genomes, const int32_t* lens,
+                 const double* merits, const int32_t* inputs, int deterministic) {
+  World& w = *(World*)h;
+  size_t off = 0;
+  for (int64_t i = 0; i < count; i++) {
+    int64_t c = first + i;
+    Org& o = w.orgs[c];
+    setup_inject(w, o, genomes + off, lens[i], merits ? merits[i] : 0.0);
+    off += lens[i];
+    derive_key((uint32_t)w.cfg.seed, (uint32_t)(w.cfg.seed >> 32), (uint32_t)c, 0xA5A5A5A5U,
+               &o.rng.lo, &o.rng.hi);
+    o.rng.ctr = 0;
+    if (inputs) { for (int k = 0; k < 3; k++) o.inputs[k] = inputs[i * 3 + k]; }
+    else if (deterministic) {  // cEnvironment::SetupInputs(random=false) :1286-1289
+      o.inputs[0] = 0x0f13149f; o.inputs[1] = 0x3308e53e; o.inputs[2] = 0x556241eb;
+    } else {
+      o.inputs[0] = (15 << 24) + (int)o.rng.uint_below(1u << 24);
+      o.inputs[1] = (51 << 24) + (int)o.rng.uint_below(1u << 24);
+      o.inputs[2] = (85 << 24) + (int)o.rng.uint_below(1u << 24);
+    }
+  }
+  return 0;
+}
+
+int orc_kill(void* h, int64_t cell) { ((World*)h)->orgs[cell].alive = false; return 0; }
+
+// Batched SingleProcess for a range (FROZEN / TEST / WORLD semantics).
+int orc_step(void* h, int64_t first, int64_t count, const int32_t* budget, int32_t uniform, int mode) {
+  World& w = *(World*)h;
+  int64_t insts = 0;
+  for (int64_t i = 0; i < count; i++) {
+    int64_t c = first + i;
+    Org& o = w.orgs[c];
+    int b = budget ? budget[i] : uniform;
+    Exec ex{w, o, mode};
+    for (int k = 0; k < b && o.alive && !ex.stop; k++) { ex.single_process(c); insts++; }
+  }
+  w.step_insts = insts;
+  return 0;
+}
+
+int orc_last_step_insts(void* h, int64_t* out) { *out = ((World*)h)->step_insts; return 0; }
+
+int orc_get_states(void* h, int64_t first, int64_t count, avgpu_cpu_state* st, uint8_t* ops,
+                   uint8_t* flags, int cap) {
+  World& w = *(World*)h;
+  for (int64_t i = 0; i < count; i++)
+    dump_state(w, w.orgs[first + i], &st[i], ops ? ops + i * cap : nullptr,
+               flags ? flags + i * cap : nullptr, cap);
+  return 0;
+}
+
+// cTestCPU::TestGenome_Body for one gestation (cpu/cTestCPU.cc:144-188, :233-326)
+int orc_test_genomes(void* h, int n, const uint8_t* genomes, const int32_t* lens,
+                     avgpu_test_result* res, char* exec_flags, int flags_cap, uint8_t* offspring) {
+  World& w = *(World*)h;
+  size_t off = 0;
+  for (int i = 0; i < n; i++) {
+    Org o;
+    const int len = lens[i];
+    setup_inject(w, o, genomes + off, len, 0.0);
+    off += len;
+    o.inputs[0] = 0x0f13149f; o.inputs[1] = 0x3308e53e; o.inputs[2] = 0x556241eb;
+    Exec ex{w, o, AVGPU_MODE_TEST};
+    const int time_allocated = w.cfg.test_cpu_time_mod * len;
+    int t = 0;
+    while (t < time_allocated && o.num_divides == 0 && o.alive) { t++; ex.single_process(-1); }
+    avgpu_test_result& r = res[i];
+    memset(&r, 0, sizeof(r));
+    r.divided = o.num_divides > 0;
+    r.copied_size = o.copied_size;
+    r.executed_size = o.executed_size;
+    r.gestation_time = o.gestation_time;
+    r.genome_length = o.genome_length;
+    r.time_used = o.time_used;
+    r.merit = o.merit;
+    r.fitness = o.fitness;
+    for (int k = 0; k < AVGPU_MAX_REACTIONS; k++) r.task_count[k] = o.last_task[k];
+    r.offspring_len = (int)o.offspring.size();
+    r.copy_true = r.divided && o.offspring == o.genome;
+    if (exec_flags) {
+      std::string f = o.exec_flags_at_divide;
+      if (!r.divided) {
+        f.assign(o.mem.size(), '-');
+        for (size_t k = 0; k < o.mem.size(); k++) if (o.flg[k] & F_EXECUTED) f[k] = '+';
+      }
+      char* dst = exec_flags + (size_t)i * flags_cap;
+      memset(dst, 0, flags_cap);
+      memcpy(dst, f.data(), std::min((int)f.size(), flags_cap - 1));
+    }
+    if (offspring) {
+      uint8_t* dst = offspring + (size_t)i * AVGPU_MAX_GENOME;
+      memset(dst, 0, AVGPU_MAX_GENOME);
+      memcpy(dst, o.offspring.data(), o.offspring.size());
+    }
+  }
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
+// Batch-synchronous world update: the exact semantics the device implements
+// (DESIGN.md "Update semantics"): allot -> interpret -> place births -> stats.
+static int run_update_impl(World& w) {
+  avgpu_update_stats& st = w.stats;
+  memset(&st, 0, sizeof(st));
+  st.update = w.update;
+  int64_t n_alive = 0;
+  double sum_merit = tree_merit_sum(w, &n_alive);
+  if (w.have_global) { sum_merit = w.global_merit; n_alive = w.global_orgs; }
+  const int64_t ud = (int64_t)w.cfg.ave_time_slice * n_alive;
+  // 1. allotment (cScheduler restated; DESIGN.md "Scheduler")
+  std::vector<int32_t> budget(w.ncells, 0);
+  for (int64_t c = 0; c < w.ncells; c++) {
+    Org& o = w.orgs[c];
+    if (!o.alive) continue;
+    if (w.cfg.slicing_method == AVGPU_SLICE_CONSTANT || !(sum_merit > 0.0)) {
+      budget[c] = w.cfg.ave_time_slice;
+      continue;
+    }
+    double lam = ((double)ud * o.merit) / sum_merit;
+    if (lam > 1.0e8) lam = 1.0e8;
+    if (w.cfg.slicing_method == AVGPU_SLICE_INTEGRATED) {
+      o.credit = o.credit + lam;
+      double fl = std::floor(o.credit);
+      budget[c] = (int32_t)fl;
+      o.credit = o.credit - fl;
+    } else {
+      double fl = std::floor(lam);
+      double frac = lam - fl;
+      uint64_t th = (uint64_t)(frac * 4294967296.0);
+      budget[c] = (int32_t)fl + (o.rng.p(th) ? 1 : 0);
+    }
+  }
+  // 2. interpretation
+  w.births.clear();
+  int64_t insts = 0, deaths = 0, divides = 0;
+  for (int64_t c = 0; c < w.ncells; c++) {
+    Org& o = w.orgs[c];
+    if (!o.alive) continue;
+    Exec ex{w, o, AVGPU_MODE_WORLD};
+    int d0 = o.num_divides;
+    for (int k = 0; k < budget[c] && o.alive; k++) { ex.single_process(c); insts++; }
+    divides += o.num_divides - d0;
+    if (!o.alive) deaths++;
+  }
+  // 3. placement rounds (PositionOffspring restated, main/cPopulation.cc:5353-5413)
+  const int64_t nbirth = (int64_t)w.births.size();
+  std::vector<uint8_t> occ(w.ncells);
+  for (int64_t c = 0; c < w.ncells; c++) occ[c] = w.orgs[c].alive ? 1 : 0;
+  std::vector<uint64_t> claim(w.ncells, 0);
+  std::vector<int64_t> owner(w.ncells, -1);
+  std::vector<uint64_t> prio(nbirth, 0);
+  std::vector<int8_t> state(nbirth, 0);   // 0 pending, 1 placed, -1 failed
+  for (int round = 0; round < 4; round++) {
+    for (int64_t i = 0; i < nbirth; i++) {
+      Birth& b = w.births[i];
+      if (state[i] != 0) continue;
+      int64_t nb[8];
+      const int nn = neighbours(w, b.parent, nb);
+      int64_t cand[9];
+      int nc = 0;
+      if (w.cfg.prefer_empty)
+        for (int k = 0; k < nn; k++) if (!occ[nb[k]]) cand[nc++] = nb[k];
+      if (nc == 0 && w.cfg.birth_method != 3) {
+        for (int k = 0; k < nn; k++) cand[nc++] = nb[k];
+        if (w.cfg.allow_parent) cand[nc++] = b.parent;
+      }
+      if (nc == 0) { state[i] = -1; continue; }
+      b.target = cand[b.rng.uint_below((uint32_t)nc)];
+      prio[i] = ((uint64_t)b.rng.next() << 32) | ((uint64_t)(b.parent & 0xFFFFFF) << 8) | (b.seq & 0xFF);
+      if (prio[i] > claim[b.target]) claim[b.target] = prio[i];
+    }
+    for (int64_t i = 0; i < nbirth; i++) {
+      if (state[i] != 0) continue;
+      Birth& b = w.births[i];
+      if (claim[b.target] == prio[i]) { state[i] = 1; occ[b.target] = 1; owner[b.target] = i; }
+    }
+    for (int64_t i = 0; i < nbirth; i++) if (w.births[i].target >= 0) claim[w.births[i].target] = 0;
+  }
+  // 4. activation (the last round's winner owns the cell)
+  int64_t placed = 0, dropped = 0;
+  for (int64_t i = 0; i < nbirth; i++) {
+    Birth& b = w.births[i];
+    if (state[i] == 1 && owner[b.target] == i) { activate_child(w, b, b.target); placed++; }
+    else dropped++;
+  }
+  // 5. statistics (main/cStats.cc:1081-1100 inputs)
+  st.insts_executed = insts;
+  st.births = placed;
+  st.births_dropped = dropped;
+  st.deaths = deaths;
+  st.divides = divides;
+  double gen = 0.0;
+  for (int64_t c = 0; c < w.ncells; c++) {
+    const Org& o = w.orgs[c];
+    if (!o.alive) continue;
+    st.num_organisms++;
+    st.sum_merit += o.merit;
+    st.sum_fitness += o.fitness;
+    st.sum_gestation += o.gestation_time;
+    st.sum_genome_length += (double)o.genome.size();
+    if (o.fitness > st.max_fitness) st.max_fitness = o.fitness;
+    gen += o.generation;
+    for (int t = 0; t < AVGPU_MAX_REACTIONS; t++) if (o.last_task[t] > 0) st.task_orgs[t]++;
+  }
+  st.ave_generation = st.num_organisms ? gen / st.num_organisms : 0.0;
+  w.update++;
+  return 0;
+}
+
+int orc_run_update(void* h, avgpu_update_stats* out) {
+  World& w = *(World*)h;
+  int rc = run_update_impl(w);
+  if (out) *out = w.stats;
+  return rc;
+}
+
+int orc_run_updates(void* h, int n, avgpu_update_stats* out) {
+  World& w = *(World*)h;
+  for (int i = 0; i < n; i++) run_update_impl(w);
+  if (out) *out = w.stats;
+  return 0;
+}
+
+int orc_set_global_totals(void* h, double merit, int64_t orgs) {
+  World& w = *(World*)h;
+  w.have_global = true; w.global_merit = merit; w.global_orgs = orgs;
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
+// Reference-style serial world (the CPU baseline): Avida2Driver::Run's update
+// loop (targets/avida/Avida2Driver.cc:91-163) with cPopulation::ScheduleOrganism
+// (probabilistic pick proportional to merit; a cWeightedIndex-style sum tree,
+// tools/cWeightedIndex.cc:49-115) and ProcessStepSpeculative
+// (main/cPopulation.cc:5740-5788), births placed immediately
+// (ActivateOffspring main/cPopulation.cc:621-952).
+struct SerialSched {
+  int64_t n = 0, size = 1;
+  std::vector<double> tree;
+  void init(int64_t cells) {
+    n = cells; size = 1; while (size < n) size <<= 1;
+    tree.assign(2 * size, 0.0);
+  }
+  void set(int64_t i, double v) {
+    int64_t p = size + i; tree[p] = v;
+    for (p >>= 1; p >= 1; p >>= 1) tree[p] = tree[2 * p] + tree[2 * p + 1];
+  }
+  int64_t find(double x) const {
+    int64_t p = 1;
+    while (p < size) {
+      if (x < tree[2 * p]) p = 2 * p; else { x -= tree[2 * p]; p = 2 * p + 1; }
+    }
+    return p - size;
+  }
+};
+
+static void serial_place(World& w, SerialSched& sch, Birth& b) {
+  int64_t nb[8];
+  const int nn = neighbours(w, b.parent, nb);
+  int64_t cand[9];
+  int nc = 0;
+  if (w.cfg.prefer_empty) for (int k = 0; k < nn; k++) if (!w.orgs[nb[k]].alive) cand[nc++] = nb[k];
+  if (nc == 0 && w.cfg.birth_method != 3) {
+    for (int k = 0; k < nn; k++) cand[nc++] = nb[k];
+    if (w.cfg.allow_parent) cand[nc++] = b.parent;
+  }
+  if (nc == 0) return;
+  int64_t t = cand[w.global_rng.uint_below((uint32_t)nc)];
+  activate_child(w, b, t);
+  w.orgs[t].spec_count = 0;
+  sch.set(t, w.orgs[t].merit);
+}
+
+int orc_run_serial_updates(void* h, int n_updates, avgpu_update_stats* out) {
+  World& w = *(World*)h;
+  SerialSched sch;
+  sch.init(w.ncells);
+  for (int64_t c = 0; c < w.ncells; c++) sch.set(c, w.orgs[c].alive ? w.orgs[c].merit : 0.0);
+  int64_t insts = 0;
+  for (int u = 0; u < n_updates; u++) {
+    int64_t n_alive = 0;
+    for (int64_t c = 0; c < w.ncells; c++) n_alive += w.orgs[c].alive;
+    const int64_t ud = (int64_t)w.cfg.ave_time_slice * n_alive;   // cWorld::CalculateUpdateSize
+    int64_t births = 0;
+    for (int64_t i = 0; i < ud; i++) {
+      const double tot = sch.tree[1];
+      if (!(tot > 0.0)) break;
+      double x = (double)w.global_rng.next() * (1.0 / 4294967296.0) * tot;
+      int64_t c = sch.find(x);
+      Org& o = w.orgs[c];
+      if (!o.alive) continue;
+      insts++;
+      if (o.spec_count > 0) { o.spec_count--; continue; }
+      Exec ex{w, o, AVGPU_MODE_WORLD};
+      w.births.clear();
+      ex.single_process(c);
+      // speculative run-ahead: up to 32 more, stopping before STALL insts
+      // (IO, h-divide: cpu/cHardwareCPU.cc:961-968)
+      int spec = 0;
+      while (spec < 32 && o.alive && w.births.empty()) {
+        int hid = w.is.handler[o.mem[adjust(o.head[HEAD_IP], (int)o.mem.size())]];
+        if (hid == H_IO || hid == H_H_DIVIDE) break;
+        ex.single_process(c);
+        spec++;
+      }
+      o.spec_count = spec;
+      if (!o.alive) { sch.set(c, 0.0); }
+      for (auto& b : w.births) {
+        sch.set(c, o.alive ? o.merit : 0.0);   // AdjustSchedule(parent) :933
+        serial_place(w, sch, b);
+        births++;
+      }
+      w.births.clear();
+    }
+    w.update++;
+    (void)births;
+  }
+  w.stats.insts_executed = insts;
+  w.stats.num_organisms = 0;
+  for (int64_t c = 0; c < w.ncells; c++) w.stats.num_organisms += w.orgs[c].alive;
+  if (out) *out = w.stats;
+  return 0;
+}
+
+}  // extern "C"

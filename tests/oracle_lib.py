@@ -1,0 +1,159 @@
+"""Test-infrastructure loader for the CPU oracle (oracle/liboracle.so).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg use this.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+from avida_amd import capi, files
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_DIR = os.path.join(ROOT, "oracle")
+ORACLE_SO = os.path.join(ORACLE_DIR, "liboracle.so")
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+
+_lib = None
+
+
+def load_oracle():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(ORACLE_SO):
+        subprocess.run(["make", "-s", "-C", ORACLE_DIR], check=True)
+    lib = C.CDLL(ORACLE_SO)
+    capi.bind_common(lib, "orc_")
+    lib.orc_create.restype = C.c_void_p
+    lib.orc_create.argtypes = [C.POINTER(capi.AvgpuCfg), C.c_int64]
+    lib.orc_destroy.restype = None
+    lib.orc_run_serial_updates.argtypes = [C.c_void_p, C.c_int, C.POINTER(capi.AvgpuUpdateStats)]
+    _lib = lib
+    return lib
+
+
+class Backend:
+    """Uniform wrapper over the oracle (prefix orc_) and the product (avgpu_)."""
+
+    def __init__(self, kind, cfg: capi.AvgpuCfg, instset: files.InstSet, reactions, ncells=0,
+                 device=0):
+        self.kind = kind
+        if kind == "oracle":
+            self.lib, self.p = load_oracle(), "orc_"
+            self.h = self.lib.orc_create(C.byref(cfg), ncells)
+        else:
+            self.lib, self.p = capi.load_product(), "avgpu_"
+            self.h = self.lib.avgpu_create(C.byref(cfg), device, ncells)
+            if not self.h:
+                raise RuntimeError(self.lib.avgpu_last_error().decode())
+        self.cfg = cfg
+        self.instset = instset
+        hid = (C.c_uint8 * len(instset.names))(*instset.handlers)
+        red = (C.c_int32 * len(instset.names))(*instset.redundancy)
+        self._call("load_instset", self.h, len(instset.names), hid, red)
+        arr = capi.reactions_array(reactions)
+        self._call("load_env", self.h, len(reactions), arr)
+
+    def _call(self, name, *args):
+        rc = getattr(self.lib, self.p + name)(*args)
+        if rc is not None and rc < 0:
+            msg = getattr(self.lib, self.p + "last_error")()
+            raise RuntimeError(f"{self.p}{name}: {msg.decode() if msg else rc}")
+        return rc
+
+    def close(self):
+        if self.h:
+            getattr(self.lib, self.p + "destroy")(self.h)
+            self.h = None
+
+    def set_orgs(self, first, genomes, merits=None, inputs=None, deterministic=True):
+        n = len(genomes)
+        blob = b"".join(genomes)
+        buf = (C.c_uint8 * max(1, len(blob))).from_buffer_copy(blob or b"\0")
+        lens = (C.c_int32 * n)(*[len(g) for g in genomes])
+        m = (C.c_double * n)(*(merits or [0.0] * n))
+        inp = None
+        if inputs is not None:
+            flat = [v for t in inputs for v in t]
+            inp = (C.c_int32 * len(flat))(*flat)
+        self._call("set_orgs", self.h, first, n, buf, lens, m, inp, 1 if deterministic else 0)
+
+    def step(self, first, count, budget=None, uniform=0, mode=capi.MODE_FROZEN):
+        b = None
+        if budget is not None:
+            b = (C.c_int32 * count)(*budget)
+        self._call("step", self.h, first, count, b, uniform, mode)
+        if self.kind != "oracle":
+            self.lib.avgpu_sync(self.h)
+
+    def states(self, first, count, cap=capi.MAX_GENOME):
+        st = (capi.AvgpuCpuState * count)()
+        ops = (C.c_uint8 * (count * cap))()
+        fl = (C.c_uint8 * (count * cap))()
+        self._call("get_states", self.h, first, count, st, ops, fl, cap)
+        return st, bytes(ops), bytes(fl)
+
+    def test_genomes(self, genomes, flags_cap=2049):
+        n = len(genomes)
+        blob = b"".join(genomes)
+        buf = (C.c_uint8 * len(blob)).from_buffer_copy(blob)
+        lens = (C.c_int32 * n)(*[len(g) for g in genomes])
+        res = (capi.AvgpuTestResult * n)()
+        flags = C.create_string_buffer(n * flags_cap)
+        off = (C.c_uint8 * (n * capi.MAX_GENOME))()
+        self._call("test_genomes", self.h, n, buf, lens, res, flags, flags_cap, off)
+        out = []
+        raw = flags.raw
+        offb = bytes(off)
+        for i in range(n):
+            r = res[i]
+            f = raw[i * flags_cap:(i + 1) * flags_cap].split(b"\0", 1)[0].decode()
+            child = offb[i * capi.MAX_GENOME:i * capi.MAX_GENOME + r.offspring_len]
+            out.append((r, f, child))
+        return out
+
+    def run_update(self):
+        st = capi.AvgpuUpdateStats()
+        self._call("run_update", self.h, C.byref(st))
+        return st
+
+
+def recalculate(backend: Backend, genomes, generations=3):
+    """cTestCPU::TestGenome viability recursion (cpu/cTestCPU.cc:233-326) over a batch.
+
+    Returns per genome (result_at_depth0, exec_flags, viable)."""
+    first = backend.test_genomes(genomes)
+    viable = [False] * len(genomes)
+    # chains: genome index -> list of ancestors' genomes for case 3
+    pending = []
+    for i, (r, f, child) in enumerate(first):
+        if not r.divided:
+            continue
+        if r.copy_true:
+            viable[i] = True
+        else:
+            pending.append((i, [genomes[i]], child))
+    depth = 1
+    while pending and depth < generations:
+        nxt = []
+        res = backend.test_genomes([c for (_, _, c) in pending])
+        for (i, anc, child), (r, f, grandchild) in zip(pending, res):
+            if not r.divided:
+                continue
+            if r.copy_true:
+                viable[i] = True
+                continue
+            anc2 = anc + [child]
+            if any(grandchild == a for a in anc2):
+                viable[i] = True
+                continue
+            nxt.append((i, anc2, grandchild))
+        # case 3 at depth>0 checks the offspring of depth d against ancestors < d
+        pending = nxt
+        depth += 1
+    return [(r, f, viable[i]) for i, (r, f, _) in enumerate(first)]
+
+
+AVGPU_FLAGS_CAP = 2049

@@ -1,0 +1,89 @@
+"""Pin the CPU oracle to the reference's own RNG-free golden vectors.
+
+* tests/golden/detail-recalc.dat: avida-core/tests/_analyze_detail_all/expected/
+  data/detail-recalc.dat -- analyze-mode RECALCULATE (cTestCPU, deterministic
+  inputs, cleared mutation rates) of 1794 genotypes with the classic legacy
+  instruction set and the logic-9 environment.  Every column the hot path
+  determines is compared exactly: viable, copy_length, exe_length, merit,
+  gest_time, fitness (to the file's printed precision), executed_flags and the
+  nine task counts.
+* the default-heads ancestor: gestation 389, 97 executed, 100 copied, merit 97,
+  fitness 0.249357 (tests/heads_default_100u/expected/data/detail-100.spop:22).
+"""
+import os
+
+import pytest
+
+from avida_amd import capi, files
+import oracle_lib as ol
+
+
+def _backend(golden, instset_file):
+    iset = files.read_instset(os.path.join(golden, instset_file))
+    env = files.read_environment(os.path.join(golden, "environment-logic9.cfg"))
+    cfg = capi.cfg_from_avida(files.read_avida_cfg(None))
+    return ol.Backend("oracle", cfg, iset, env, ncells=1), iset
+
+
+def _fmt(x):
+    # cDataFile prints doubles with the default ostream precision (6 significant)
+    return "%g" % x
+
+
+def test_detail_recalc_all_rows(golden):
+    b, iset = _backend(golden, "instset-classic.cfg")
+    fmt, rows = files.parse_detail_dat(os.path.join(golden, "detail-recalc.dat"))
+    assert len(rows) == 1794
+    genomes = [iset.parse_sequence(r[8]) for r in rows]
+    res = ol.recalculate(b, genomes)
+    bad = []
+    for row, (r, flags, viable) in zip(rows, res):
+        got = [int(viable), r.copied_size, r.executed_size, _fmt(r.merit), r.gestation_time,
+               _fmt(r.fitness) if r.gestation_time else "0", flags,
+               [int(x) for x in list(r.task_count)[:9]]]
+        exp = [int(row[10]), int(row[11]), int(row[12]), _fmt(float(row[13])), int(row[15]),
+               row[17] if row[17] != "0" else "0", row[19], [int(x) for x in row[20:29]]]
+        if got != exp:
+            bad.append((row[0], exp, got))
+    assert not bad, f"{len(bad)} mismatches, first: {bad[:3]}"
+
+
+def test_ancestor_heads_default(golden):
+    b, iset = _backend(golden, "instset-heads.cfg")
+    anc = files.read_org(os.path.join(golden, "default-heads.org"), iset)
+    assert len(anc) == 100
+    (r, flags, child), = b.test_genomes([anc])
+    assert r.divided and r.copy_true
+    assert r.gestation_time == 389
+    assert r.executed_size == 97
+    assert r.copied_size == 100
+    assert r.merit == 97.0
+    assert _fmt(r.fitness) == "0.249357"
+    # Appendix B: executed everywhere except sites 3, 95, 99
+    assert [i for i, c in enumerate(flags) if c == "-"] == [3, 95, 99]
+    # detail-100.spop:22 records the same phenotype for the world-run ancestor
+    line = [l for l in open(os.path.join(golden, "detail-100.spop")) if l.startswith("1 div:ext")][0]
+    toks = line.split()
+    assert toks[6:10] == ["100", "97", "389", "0.249357"]
+
+
+def test_ancestor_trace_prefix(golden):
+    """Appendix B cycle-level KAT: h-alloc, h-search, mov-head, 85 nops, h-search."""
+    b, iset = _backend(golden, "instset-heads.cfg")
+    anc = files.read_org(os.path.join(golden, "default-heads.org"), iset)
+    b.set_orgs(0, [anc])
+    b.step(0, 1, uniform=1, mode=capi.MODE_FROZEN)
+    st, _, _ = b.states(0, 1)
+    assert st[0].mem_size == 300 and st[0].reg[0] == 100       # h-alloc
+    b.step(0, 1, uniform=1, mode=capi.MODE_FROZEN)
+    st, _, _ = b.states(0, 1)
+    assert (st[0].reg[1], st[0].reg[2], st[0].head[3], st[0].head[0]) == (96, 2, 100, 4)
+    b.step(0, 1, uniform=1, mode=capi.MODE_FROZEN)
+    st, _, _ = b.states(0, 1)
+    assert st[0].head[2] == 100 and st[0].head[0] == 6          # mov-head nop-C -> WRITE
+    b.step(0, 1, uniform=86, mode=capi.MODE_FROZEN)
+    st, _, _ = b.states(0, 1)
+    assert (st[0].reg[1], st[0].reg[2], st[0].head[3]) == (0, 0, 92)  # empty-label h-search
+    b.step(0, 1, uniform=300, mode=capi.MODE_FROZEN)
+    st, _, _ = b.states(0, 1)
+    assert st[0].num_divides == 1 and st[0].gestation_time == 389

@@ -91,7 +91,8 @@ class AvgpuUpdateStats(C.Structure):
         ("divides", C.c_int64), ("task_orgs", C.c_int64 * MAX_REACTIONS),
         ("sum_merit", C.c_double), ("sum_fitness", C.c_double), ("sum_gestation", C.c_double),
         ("sum_genome_length", C.c_double), ("max_fitness", C.c_double),
-        ("ave_generation", C.c_double),
+        ("ave_generation", C.c_double), ("sum_mem_size", C.c_double),
+        ("cum_insts_executed", C.c_int64), ("cum_births", C.c_int64), ("slices", C.c_int64),
     ]
 
 
@@ -99,7 +100,8 @@ class AvgpuUpdateStats(C.Structure):
 EXPORTED = [
     "avgpu_last_error", "avgpu_cfg_defaults", "avgpu_create", "avgpu_destroy", "avgpu_sync",
     "avgpu_load_instset", "avgpu_load_env", "avgpu_set_org", "avgpu_set_orgs", "avgpu_kill",
-    "avgpu_step", "avgpu_run_update", "avgpu_run_updates", "avgpu_get_states",
+    "avgpu_step", "avgpu_run_update", "avgpu_run_updates", "avgpu_update_totals",
+    "avgpu_update_run", "avgpu_set_stream", "avgpu_get_states",
     "avgpu_test_genomes", "avgpu_get_stats", "avgpu_stats_vector", "avgpu_set_global_totals",
     "avgpu_halo_pack", "avgpu_halo_unpack", "avgpu_halo_record_bytes",
     "avgpu_last_step_insts", "avgpu_last_kernel_ms",
@@ -209,6 +211,9 @@ def load_product():
     lib.avgpu_halo_record_bytes.restype = C.c_int64
     lib.avgpu_last_kernel_ms.argtypes = [C.c_void_p, C.POINTER(C.c_double),
                                          C.POINTER(C.c_int64)]
+    lib.avgpu_update_totals.argtypes = [C.c_void_p, C.c_void_p]
+    lib.avgpu_update_run.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(AvgpuUpdateStats)]
+    lib.avgpu_set_stream.argtypes = [C.c_void_p, C.c_void_p]
     _lib = lib
     return lib
 

@@ -1,0 +1,684 @@
+// capi.hip -- host side of the C-ABI declared in include/avida_gpu.h.
+//
+// The world object owns every device allocation (SoA organism state, tapes,
+// birth queue, scratch) on one HIP device and one HIP stream.  Each entry
+// point names the reference interface it replaces in the header.  There is no
+// CPU execution path in this library: every state transition of the hot path
+// runs in the kernels of interp.hip / world.hip.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "device.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define HIPCHK(x)                                                                   \
+  do {                                                                              \
+    hipError_t _e = (x);                                                            \
+    if (_e != hipSuccess) return fail(AVGPU_EHIP, std::string(#x ": ") + hipGetErrorString(_e)); \
+  } while (0)
+
+}  // namespace
+
+struct avgpu_world {
+  avgpu_cfg cfg;
+  int device = 0;
+  hipStream_t stream = nullptr;      // current stream (own or external)
+  hipStream_t own_stream = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  // event ring around interpreter phases (avgpu_last_kernel_ms)
+  static const int RING = 512;
+  hipEvent_t ring0[RING] = {}, ring1[RING] = {};
+  int ring_head = 0, ring_count = 0;
+  double acc_ms = 0.0;
+  int64_t acc_phases = 0;
+  DevWorld W;
+  std::vector<void*> allocs;
+  // instruction set translation
+  int n_ops = 0;
+  uint8_t op2code[256];
+  int16_t code2op[64];
+  bool instset_loaded = false;
+  bool env_loaded = false;
+  // device scratch
+  double* d_totals = nullptr;   // [8 + partials]
+  double* d_stats = nullptr;    // [32 + partials]
+  bool use_global = false;
+  int64_t update = 0;
+  float last_kernel_ms = 0.f;
+  int64_t last_launches = 0;
+  bool has_test_buffers = false;
+
+  template <typename T>
+  int alloc(T** p, size_t count) {
+    void* q = nullptr;
+    size_t bytes = std::max<size_t>(count * sizeof(T), 16);
+    hipError_t e = hipMalloc(&q, bytes);
+    if (e != hipSuccess) return fail(AVGPU_ENOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
+    hipMemsetAsync(q, 0, bytes, stream);
+    allocs.push_back(q);
+    *p = reinterpret_cast<T*>(q);
+    return 0;
+  }
+};
+
+namespace {
+
+int setup_world(avgpu_world* w, int64_t n, bool test_buffers) {
+  DevWorld& W = w->W;
+  memset(&W, 0, sizeof(W));
+  W.n = n;
+  const avgpu_cfg& c = w->cfg;
+  int rc = 0;
+#define A(ptr, cnt) if ((rc = w->alloc(&W.ptr, (size_t)(cnt))) < 0) return rc
+  A(reg, 3 * n); A(head, 4 * n); A(ctl, n); A(rlabel, n); A(mem_size, n); A(cycles, n);
+  A(time_used, n); A(gest_start, n); A(max_exec, n); A(birth_len, n); A(rng, 3 * n);
+  A(budget, n); A(tape, (size_t)n * TAPE_SLOT);
+  A(stack, 2 * AVGPU_STACK_SIZE * n); A(inbuf, 3 * n); A(in_total, n); A(in_ptr, n);
+  A(outbuf, n); A(out_total, n); A(inputs, 3 * n);
+  A(cur_task, AVGPU_MAX_REACTIONS * n); A(last_task, AVGPU_MAX_REACTIONS * n);
+  A(cur_react, AVGPU_MAX_REACTIONS * n);
+  A(cur_bonus, n); A(merit, n); A(fitness, n); A(credit, n); A(gest_time, n); A(num_div, n);
+  A(generation, n); A(copied, n); A(child_copied, n); A(executed, n); A(errors, n);
+  A(class_list, NUM_CLASSES * n); A(class_count, NUM_CLASSES); A(counters, 16);
+  W.bcap = test_buffers ? 16 : std::max<int64_t>(4096, n / 2);
+  A(b_count, 1); A(b_parent, W.bcap); A(b_seq, W.bcap); A(b_len, W.bcap); A(b_merit, W.bcap);
+  A(b_fitness, W.bcap); A(b_gen, W.bcap); A(b_ccopied, W.bcap); A(b_exec, W.bcap);
+  A(b_gest, W.bcap); A(b_rng, 3 * W.bcap); A(b_target, W.bcap); A(b_state, W.bcap);
+  A(b_prio, W.bcap); A(b_genome, (size_t)W.bcap * TAPE_SLOT);
+  A(occ, n); A(claim, n); A(owner, n);
+  if (test_buffers) {
+    A(t_flags, (size_t)n * TAPE_SLOT); A(t_flags_len, n); A(t_child, (size_t)n * TAPE_SLOT);
+    A(t_child_len, n);
+  }
+  A(rand_cum, 64); A(rand_code, 64); A(task_lut, 256);
+  const int64_t nb = (n + 255) / 256;
+  if ((rc = w->alloc(&w->d_totals, (size_t)(8 + 2 * nb)))) return rc;
+  if ((rc = w->alloc(&w->d_stats, (size_t)(40 + 24 * nb)))) return rc;
+#undef A
+  w->has_test_buffers = test_buffers;
+  // config scalars
+  W.world_x = c.world_x; W.world_y = c.world_y; W.geometry = c.world_geometry;
+  W.ave_time_slice = c.ave_time_slice; W.slicing = c.slicing_method;
+  W.base_merit_method = c.base_merit_method; W.base_const_merit = c.base_const_merit;
+  W.default_bonus = c.default_bonus; W.size_range = c.offspring_size_range;
+  W.min_copied_lines = c.min_copied_lines; W.min_exe_lines = c.min_exe_lines;
+  W.merit_default_bonus = c.merit_default_bonus; W.required_bonus = c.required_bonus;
+  W.inherit_merit = c.inherit_merit; W.require_allocate = c.require_allocate;
+  W.alloc_method = c.alloc_method; W.max_label_exe = c.max_label_exe_size;
+  W.cfg_min_genome = c.min_genome_size; W.cfg_max_genome = c.max_genome_size;
+  W.max_genome = (!c.max_genome_size || c.max_genome_size > AVGPU_MAX_GENOME) ? AVGPU_MAX_GENOME : c.max_genome_size;
+  W.min_genome = (!c.min_genome_size || c.min_genome_size < AVGPU_MIN_GENOME) ? AVGPU_MIN_GENOME : c.min_genome_size;
+  W.death_method = c.death_method; W.age_limit = c.age_limit;
+  W.prefer_empty = c.prefer_empty; W.allow_parent = c.allow_parent; W.birth_method = c.birth_method;
+  auto th = [](double p) -> uint64_t {
+    if (!(p > 0.0)) return 0;
+    if (p >= 1.0) return 1ull << 32;
+    return (uint64_t)(p * 4294967296.0);
+  };
+  W.th_copy_mut = th(c.copy_mut_prob);
+  W.th_div_mut = th(c.divide_mut_prob);
+  W.th_div_ins = th(c.divide_ins_prob);
+  W.th_div_del = th(c.divide_del_prob);
+  W.seed_lo = (uint32_t)c.seed;
+  W.seed_hi = (uint32_t)(c.seed >> 32);
+  W.row0 = 0;
+  W.global_rows = c.world_y;
+  // logic id -> task bitmask (main/cTaskLib.cc:511-575)
+  static const int sets[9][6] = {
+      {15, 51, 85, -1, -1, -1}, {63, 95, 119, -1, -1, -1}, {136, 160, 192, -1, -1, -1},
+      {175, 187, 207, 221, 243, 245}, {238, 250, 252, -1, -1, -1}, {10, 12, 34, 48, 68, 80},
+      {3, 5, 17, -1, -1, -1}, {60, 90, 102, -1, -1, -1}, {153, 165, 195, -1, -1, -1}};
+  uint16_t lut[256] = {0};
+  for (int t = 0; t < 9; t++)
+    for (int k = 0; k < 6; k++)
+      if (sets[t][k] >= 0) lut[sets[t][k]] |= (uint16_t)(1u << t);
+  HIPCHK(hipMemcpyAsync(W.task_lut, lut, sizeof(lut), hipMemcpyHostToDevice, w->stream));
+  HIPCHK(hipStreamSynchronize(w->stream));
+  return 0;
+}
+
+avgpu_world* create_world(const avgpu_cfg* cfg, int device, int64_t n, bool test_buffers) {
+  if (!cfg) { fail(AVGPU_EINVAL, "cfg is NULL"); return nullptr; }
+  if (cfg->copy_ins_prob > 0.0 || cfg->copy_del_prob > 0.0) {
+    fail(AVGPU_EUNSUPPORTED, "COPY_INS_PROB / COPY_DEL_PROB are not on the GPU path yet");
+    return nullptr;
+  }
+  if (cfg->divide_method != 1) {
+    fail(AVGPU_EUNSUPPORTED, "only DIVIDE_METHOD 1 (split) is on the GPU path");
+    return nullptr;
+  }
+  if (hipSetDevice(device) != hipSuccess) { fail(AVGPU_EHIP, "hipSetDevice failed"); return nullptr; }
+  avgpu_world* w = new avgpu_world();
+  w->cfg = *cfg;
+  w->device = device;
+  if (n <= 0) n = (int64_t)cfg->world_x * cfg->world_y;
+  if (n <= 0 || n > (1ll << 30)) { delete w; fail(AVGPU_EINVAL, "bad cell count"); return nullptr; }
+  if (hipStreamCreateWithFlags(&w->own_stream, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreate(&w->ev0) != hipSuccess || hipEventCreate(&w->ev1) != hipSuccess) {
+    delete w; fail(AVGPU_EHIP, "stream/event creation failed"); return nullptr;
+  }
+  w->stream = w->own_stream;
+  for (int i = 0; i < avgpu_world::RING; i++) {
+    if (hipEventCreate(&w->ring0[i]) != hipSuccess || hipEventCreate(&w->ring1[i]) != hipSuccess) {
+      fail(AVGPU_EHIP, "event creation failed"); return nullptr;
+    }
+  }
+  for (int i = 0; i < 64; i++) w->code2op[i] = -1;
+  if (setup_world(w, n, test_buffers) < 0) {
+    std::string e = g_err;
+    avgpu_destroy(w);
+    g_err = e;
+    return nullptr;
+  }
+  return w;
+}
+
+int copy_tables(avgpu_world* dst, const avgpu_world* src) {
+  DevWorld& D = dst->W;
+  const DevWorld& S = src->W;
+  D.n_ops = S.n_ops; D.rand_total = S.rand_total; D.fill_code = S.fill_code;
+  D.n_react = S.n_react;
+  memcpy(D.react_task, S.react_task, sizeof(D.react_task));
+  memcpy(D.react_type, S.react_type, sizeof(D.react_type));
+  memcpy(D.react_min, S.react_min, sizeof(D.react_min));
+  memcpy(D.react_max, S.react_max, sizeof(D.react_max));
+  memcpy(D.react_hasreq, S.react_hasreq, sizeof(D.react_hasreq));
+  memcpy(D.react_mult, S.react_mult, sizeof(D.react_mult));
+  memcpy(D.react_add, S.react_add, sizeof(D.react_add));
+  HIPCHK(hipMemcpy(D.rand_cum, S.rand_cum, 64 * sizeof(int32_t), hipMemcpyDeviceToDevice));
+  HIPCHK(hipMemcpy(D.rand_code, S.rand_code, 64, hipMemcpyDeviceToDevice));
+  dst->n_ops = src->n_ops;
+  memcpy(dst->op2code, src->op2code, sizeof(dst->op2code));
+  memcpy(dst->code2op, src->code2op, sizeof(dst->code2op));
+  dst->instset_loaded = src->instset_loaded;
+  dst->env_loaded = src->env_loaded;
+  return 0;
+}
+
+int ready(avgpu_world* w) {
+  if (!w) return fail(AVGPU_EINVAL, "NULL world");
+  if (!w->instset_loaded) return fail(AVGPU_ESTATE, "avgpu_load_instset not called");
+  if (!w->env_loaded) return fail(AVGPU_ESTATE, "avgpu_load_env not called");
+  return 0;
+}
+
+int translate_genomes(avgpu_world* w, const uint8_t* genomes, const int32_t* lens, int64_t count,
+                      std::vector<uint8_t>& codes, std::vector<int32_t>& offsets) {
+  codes.clear();
+  offsets.resize(count);
+  size_t off = 0;
+  for (int64_t i = 0; i < count; i++) {
+    const int len = lens[i];
+    if (len < 1 || len > AVGPU_MAX_GENOME) return fail(AVGPU_EINVAL, "genome length out of range");
+    offsets[i] = (int32_t)codes.size();
+    for (int k = 0; k < len; k++) {
+      const uint8_t op = genomes[off + k];
+      if (op >= w->n_ops) return fail(AVGPU_EINVAL, "genome op outside instruction set");
+      codes.push_back(w->op2code[op]);
+    }
+    off += len;
+    while (codes.size() & 3) codes.push_back(0);
+  }
+  if (codes.empty()) codes.push_back(0);
+  return 0;
+}
+
+int set_orgs_impl(avgpu_world* w, int64_t first, int64_t count, const uint8_t* genomes,
+                  const int32_t* lens, const double* merits, const int32_t* inputs, int det) {
+  if (first < 0 || count < 0 || first + count > w->W.n) return fail(AVGPU_EINVAL, "cell range");
+  if (count == 0) return 0;
+  std::vector<uint8_t> codes;
+  std::vector<int32_t> offsets;
+  int rc = translate_genomes(w, genomes, lens, count, codes, offsets);
+  if (rc < 0) return rc;
+  uint8_t* d_codes = nullptr;
+  int32_t *d_off = nullptr, *d_len = nullptr, *d_in = nullptr;
+  double* d_m = nullptr;
+  HIPCHK(hipMalloc(&d_codes, codes.size()));
+  HIPCHK(hipMalloc(&d_off, count * sizeof(int32_t)));
+  HIPCHK(hipMalloc(&d_len, count * sizeof(int32_t)));
+  HIPCHK(hipMemcpyAsync(d_codes, codes.data(), codes.size(), hipMemcpyHostToDevice, w->stream));
+  HIPCHK(hipMemcpyAsync(d_off, offsets.data(), count * sizeof(int32_t), hipMemcpyHostToDevice, w->stream));
+  HIPCHK(hipMemcpyAsync(d_len, lens, count * sizeof(int32_t), hipMemcpyHostToDevice, w->stream));
+  if (merits) {
+    HIPCHK(hipMalloc(&d_m, count * sizeof(double)));
+    HIPCHK(hipMemcpyAsync(d_m, merits, count * sizeof(double), hipMemcpyHostToDevice, w->stream));
+  }
+  if (inputs) {
+    HIPCHK(hipMalloc(&d_in, 3 * count * sizeof(int32_t)));
+    HIPCHK(hipMemcpyAsync(d_in, inputs, 3 * count * sizeof(int32_t), hipMemcpyHostToDevice, w->stream));
+  }
+  launch_set_orgs(w->W, w->stream, first, count, d_codes, d_off, d_len, d_m, d_in, det);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(w->stream));
+  hipFree(d_codes); hipFree(d_off); hipFree(d_len);
+  if (d_m) hipFree(d_m);
+  if (d_in) hipFree(d_in);
+  return 0;
+}
+
+int drain_ring(avgpu_world* w, int keep) {
+  while (w->ring_count > keep) {
+    const int i = (w->ring_head - w->ring_count + avgpu_world::RING) % avgpu_world::RING;
+    HIPCHK(hipEventSynchronize(w->ring1[i]));
+    float f = 0.f;
+    HIPCHK(hipEventElapsedTime(&f, w->ring0[i], w->ring1[i]));
+    w->acc_ms += f;
+    w->acc_phases++;
+    w->ring_count--;
+  }
+  return 0;
+}
+
+int interpret(avgpu_world* w, int mode, int64_t max_lanes) {
+  int launches = 0;
+  int rc = drain_ring(w, avgpu_world::RING - 1);
+  if (rc < 0) return rc;
+  const int i = w->ring_head;
+  HIPCHK(hipEventRecord(w->ring0[i], w->stream));
+  launch_interpret_classes(w->W, mode, w->stream, max_lanes, nullptr, &launches);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipEventRecord(w->ring1[i], w->stream));
+  w->ring_head = (i + 1) % avgpu_world::RING;
+  w->ring_count++;
+  w->last_launches = launches;
+  return 0;
+}
+
+int update_run(avgpu_world* w, const double* dev_totals, avgpu_update_stats* out);
+
+}  // namespace
+
+// ===========================================================================
+extern "C" {
+
+const char* avgpu_last_error(void) { return g_err.c_str(); }
+
+void avgpu_cfg_defaults(avgpu_cfg* c) {
+  memset(c, 0, sizeof(*c));
+  c->world_x = 60; c->world_y = 60; c->world_geometry = 2;
+  c->ave_time_slice = 30; c->slicing_method = 1; c->base_merit_method = 4;
+  c->base_const_merit = 100; c->default_bonus = 1.0;
+  c->copy_mut_prob = 0.0075; c->divide_ins_prob = 0.05; c->divide_del_prob = 0.05;
+  c->offspring_size_range = 2.0; c->min_copied_lines = 0.5; c->min_exe_lines = 0.5;
+  c->require_allocate = 1; c->death_method = 2; c->age_limit = 20; c->alloc_method = 0;
+  c->divide_method = 1; c->max_label_exe_size = 1; c->birth_method = 0; c->prefer_empty = 1;
+  c->allow_parent = 1; c->test_cpu_time_mod = 20; c->inherit_merit = 1;
+  c->seed = 101;
+}
+
+avgpu_world* avgpu_create(const avgpu_cfg* cfg, int device, int64_t num_cells) {
+  return create_world(cfg, device, num_cells, false);
+}
+
+int avgpu_destroy(avgpu_world* w) {
+  if (!w) return 0;
+  if (w->stream) hipStreamSynchronize(w->stream);
+  if (w->own_stream) hipStreamSynchronize(w->own_stream);
+  for (void* p : w->allocs) hipFree(p);
+  if (w->ev0) hipEventDestroy(w->ev0);
+  if (w->ev1) hipEventDestroy(w->ev1);
+  for (int i = 0; i < avgpu_world::RING; i++) {
+    if (w->ring0[i]) hipEventDestroy(w->ring0[i]);
+    if (w->ring1[i]) hipEventDestroy(w->ring1[i]);
+  }
+  if (w->own_stream) hipStreamDestroy(w->own_stream);
+  delete w;
+  return 0;
+}
+
+int avgpu_set_stream(avgpu_world* w, void* hip_stream) {
+  if (!w) return fail(AVGPU_EINVAL, "NULL world");
+  HIPCHK(hipStreamSynchronize(w->stream));
+  w->stream = hip_stream ? reinterpret_cast<hipStream_t>(hip_stream) : w->own_stream;
+  return 0;
+}
+
+int avgpu_sync(avgpu_world* w) {
+  if (!w) return fail(AVGPU_EINVAL, "NULL world");
+  HIPCHK(hipStreamSynchronize(w->stream));
+  return 0;
+}
+
+int avgpu_load_instset(avgpu_world* w, int n, const uint8_t* handler_id, const int32_t* redundancy) {
+  if (!w || n <= 0 || n > AVGPU_MAX_INST) return fail(AVGPU_EINVAL, "instruction set size");
+  int32_t cum[64] = {0};
+  uint8_t code[64] = {0};
+  bool used[64] = {false};
+  int32_t total = 0;
+  for (int i = 0; i < 64; i++) w->code2op[i] = -1;
+  for (int i = 0; i < n; i++) {
+    const int h = handler_id[i];
+    if (h < 0 || h >= AVGPU_H_COUNT) return fail(AVGPU_EINVAL, "unknown handler id");
+    if (used[h]) return fail(AVGPU_EUNSUPPORTED, "handler mapped twice (non-injective instset)");
+    if (h < 3 && h != i) return fail(AVGPU_EUNSUPPORTED, "nops must be ops 0..2 in A,B,C order");
+    used[h] = true;
+    total += redundancy ? redundancy[i] : 1;
+    cum[i] = total;
+    code[i] = (uint8_t)h;
+    w->op2code[i] = (uint8_t)h;
+    w->code2op[h] = (int16_t)i;
+  }
+  if (total <= 0) return fail(AVGPU_EINVAL, "zero total redundancy");
+  w->n_ops = n;
+  w->W.n_ops = n;
+  w->W.rand_total = total;
+  w->W.fill_code = code[0];
+  HIPCHK(hipMemcpyAsync(w->W.rand_cum, cum, sizeof(cum), hipMemcpyHostToDevice, w->stream));
+  HIPCHK(hipMemcpyAsync(w->W.rand_code, code, sizeof(code), hipMemcpyHostToDevice, w->stream));
+  HIPCHK(hipStreamSynchronize(w->stream));
+  w->instset_loaded = true;
+  return 0;
+}
+
+int avgpu_load_env(avgpu_world* w, int nreact, const avgpu_reaction* r) {
+  if (!w || nreact < 0 || nreact > AVGPU_MAX_REACTIONS) return fail(AVGPU_EINVAL, "reaction count");
+  DevWorld& W = w->W;
+  W.n_react = nreact;
+  for (int i = 0; i < nreact; i++) {
+    if (r[i].task < 0 || r[i].task >= AVGPU_NUM_LOGIC_TASKS) return fail(AVGPU_EINVAL, "task id");
+    W.react_task[i] = r[i].task;
+    W.react_type[i] = r[i].type;
+    W.react_min[i] = r[i].min_count;
+    W.react_max[i] = r[i].max_count;
+    W.react_hasreq[i] = r[i].has_requisite;
+    const double bonus = r[i].max_number * r[i].value;  // DoProcesses: consumed * value
+    W.react_mult[i] = (r[i].type == AVGPU_PROC_POW) ? std::pow(2.0, bonus) : bonus;
+    W.react_add[i] = bonus;
+  }
+  w->env_loaded = true;
+  return 0;
+}
+
+int avgpu_set_org(avgpu_world* w, int64_t cell, const uint8_t* genome, int len, double merit,
+                  const int32_t* inputs) {
+  int rc = ready(w);
+  if (rc < 0) return rc;
+  const int32_t l = len;
+  return set_orgs_impl(w, cell, 1, genome, &l, merit > 0 ? &merit : nullptr, inputs, 0);
+}
+
+int avgpu_set_orgs(avgpu_world* w, int64_t first, int64_t count, const uint8_t* genomes,
+                   const int32_t* lens, const double* merits, const int32_t* inputs, int det) {
+  int rc = ready(w);
+  if (rc < 0) return rc;
+  return set_orgs_impl(w, first, count, genomes, lens, merits, inputs, det);
+}
+
+int avgpu_kill(avgpu_world* w, int64_t cell) {
+  if (!w || cell < 0 || cell >= w->W.n) return fail(AVGPU_EINVAL, "cell");
+  uint32_t ctl = 0;
+  HIPCHK(hipStreamSynchronize(w->stream));
+  HIPCHK(hipMemcpy(&ctl, w->W.ctl + cell, 4, hipMemcpyDeviceToHost));
+  ctl &= ~CTL_ALIVE;
+  HIPCHK(hipMemcpy(w->W.ctl + cell, &ctl, 4, hipMemcpyHostToDevice));
+  return 0;
+}
+
+int avgpu_step(avgpu_world* w, int64_t first, int64_t count, const int32_t* budget,
+               int32_t budget_uniform, int mode) {
+  int rc = ready(w);
+  if (rc < 0) return rc;
+  if (first < 0 || count < 0 || first + count > w->W.n) return fail(AVGPU_EINVAL, "cell range");
+  if (mode < 0 || mode > 2) return fail(AVGPU_EINVAL, "mode");
+  if (mode == AVGPU_MODE_TEST && !w->has_test_buffers)
+    return fail(AVGPU_ESTATE, "TEST mode needs a test world (avgpu_test_genomes)");
+  if (count == 0) return 0;
+  int32_t* d_b = nullptr;
+  if (budget) {
+    HIPCHK(hipMalloc(&d_b, count * sizeof(int32_t)));
+    HIPCHK(hipMemcpyAsync(d_b, budget, count * sizeof(int32_t), hipMemcpyHostToDevice, w->stream));
+  }
+  HIPCHK(hipMemsetAsync(w->W.counters, 0, CNT_PER_UPDATE * sizeof(unsigned long long), w->stream));
+  HIPCHK(hipMemsetAsync(w->W.b_count, 0, sizeof(int32_t), w->stream));
+  launch_classify_uniform(w->W, w->stream, first, count, d_b, budget_uniform);
+  HIPCHK(hipGetLastError());
+  rc = interpret(w, mode, count);
+  if (d_b) { hipStreamSynchronize(w->stream); hipFree(d_b); }
+  return rc;
+}
+
+int avgpu_update_totals(avgpu_world* w, double* dev_totals) {
+  int rc = ready(w);
+  if (rc < 0) return rc;
+  if (!dev_totals) return fail(AVGPU_EINVAL, "dev_totals is NULL");
+  launch_merit_total(w->W, w->stream, dev_totals, w->d_totals + 8);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+int avgpu_update_run(avgpu_world* w, const double* dev_totals, avgpu_update_stats* out) {
+  int rc = ready(w);
+  if (rc < 0) return rc;
+  if (!dev_totals) return fail(AVGPU_EINVAL, "dev_totals is NULL");
+  launch_world_pre(w->W, w->stream, dev_totals);
+  HIPCHK(hipGetLastError());
+  rc = interpret(w, AVGPU_MODE_WORLD, w->W.n);
+  if (rc < 0) return rc;
+  launch_world_post(w->W, w->stream, w->d_stats);
+  HIPCHK(hipGetLastError());
+  w->update++;
+  if (out) return avgpu_get_stats(w, out);
+  return 0;
+}
+
+int avgpu_run_update(avgpu_world* w, avgpu_update_stats* out) {
+  int rc = ready(w);
+  if (rc < 0) return rc;
+  if (!w->use_global) {
+    launch_merit_total(w->W, w->stream, w->d_totals, w->d_totals + 8);
+    HIPCHK(hipGetLastError());
+  }
+  w->use_global = false;
+  return avgpu_update_run(w, w->d_totals, out);
+}
+
+int avgpu_run_updates(avgpu_world* w, int n, avgpu_update_stats* last) {
+  for (int i = 0; i < n; i++) {
+    int rc = avgpu_run_update(w, nullptr);
+    if (rc < 0) return rc;
+  }
+  if (last) return avgpu_get_stats(w, last);
+  return 0;
+}
+
+int avgpu_get_stats(avgpu_world* w, avgpu_update_stats* out) {
+  if (!w || !out) return fail(AVGPU_EINVAL, "args");
+  double v[40];
+  HIPCHK(hipMemcpyAsync(v, w->d_stats, sizeof(v), hipMemcpyDeviceToHost, w->stream));
+  HIPCHK(hipStreamSynchronize(w->stream));
+  memset(out, 0, sizeof(*out));
+  out->update = w->update - 1;
+  out->num_organisms = (int64_t)v[0];
+  out->sum_merit = v[1];
+  out->sum_fitness = v[2];
+  out->sum_gestation = v[3];
+  out->sum_genome_length = v[4];
+  out->max_fitness = v[5];
+  out->ave_generation = v[0] > 0 ? v[6] / v[0] : 0.0;
+  for (int t = 0; t < AVGPU_NUM_LOGIC_TASKS; t++) out->task_orgs[t] = (int64_t)v[8 + t];
+  out->insts_executed = (int64_t)v[24];
+  out->deaths = (int64_t)v[25];
+  out->divides = (int64_t)v[26];
+  out->births = (int64_t)v[27];
+  out->births_dropped = (int64_t)v[28];
+  out->sum_mem_size = v[7];
+  out->cum_insts_executed = (int64_t)v[30];
+  out->cum_births = (int64_t)v[31];
+  out->slices = (int64_t)v[32];
+  return 0;
+}
+
+int avgpu_get_states(avgpu_world* w, int64_t first, int64_t count, avgpu_cpu_state* states,
+                     uint8_t* mem_ops, uint8_t* mem_flags, int mem_cap) {
+  if (!w || first < 0 || count < 0 || first + count > w->W.n) return fail(AVGPU_EINVAL, "cell range");
+  if (count == 0) return 0;
+  avgpu_cpu_state* d_s = nullptr;
+  uint8_t* d_c = nullptr;
+  const bool want_mem = mem_ops && mem_flags && mem_cap > 0;
+  HIPCHK(hipMalloc(&d_s, count * sizeof(avgpu_cpu_state)));
+  if (want_mem) {
+    HIPCHK(hipMalloc(&d_c, (size_t)count * mem_cap));
+    HIPCHK(hipMemsetAsync(d_c, 0, (size_t)count * mem_cap, w->stream));
+  }
+  launch_get_states(w->W, w->stream, first, count, d_s, d_c, mem_cap);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(states, d_s, count * sizeof(avgpu_cpu_state), hipMemcpyDeviceToHost, w->stream));
+  std::vector<uint8_t> codes;
+  if (want_mem) {
+    codes.resize((size_t)count * mem_cap);
+    HIPCHK(hipMemcpyAsync(codes.data(), d_c, codes.size(), hipMemcpyDeviceToHost, w->stream));
+  }
+  HIPCHK(hipStreamSynchronize(w->stream));
+  hipFree(d_s);
+  if (d_c) hipFree(d_c);
+  if (want_mem) {
+    for (int64_t i = 0; i < count; i++) {
+      const int m = std::min(states[i].mem_size, mem_cap);
+      for (int k = 0; k < mem_cap; k++) {
+        const size_t o = (size_t)i * mem_cap + k;
+        if (k < m) {
+          const uint8_t b = codes[o];
+          const int op = w->code2op[b & CODE_MASK];
+          mem_ops[o] = (uint8_t)(op < 0 ? 255 : op);
+          mem_flags[o] = (uint8_t)(((b & TF_COPIED) ? 0x01 : 0) | ((b & TF_EXEC) ? 0x04 : 0));
+        } else {
+          mem_ops[o] = 0;
+          mem_flags[o] = 0;
+        }
+      }
+    }
+  }
+  return 0;
+}
+
+int avgpu_test_genomes(avgpu_world* w, int n, const uint8_t* genomes, const int32_t* lens,
+                       avgpu_test_result* results, char* executed_flags, int flags_cap,
+                       uint8_t* offspring) {
+  int rc = ready(w);
+  if (rc < 0) return rc;
+  if (n <= 0) return 0;
+  avgpu_cfg tc = w->cfg;
+  tc.copy_mut_prob = 0; tc.divide_mut_prob = 0; tc.divide_ins_prob = 0; tc.divide_del_prob = 0;
+  avgpu_world* t = create_world(&tc, w->device, n, true);
+  if (!t) return AVGPU_ENOMEM;
+  if ((rc = copy_tables(t, w)) < 0) { avgpu_destroy(t); return rc; }
+  if ((rc = set_orgs_impl(t, 0, n, genomes, lens, nullptr, nullptr, 1)) < 0) { avgpu_destroy(t); return rc; }
+  std::vector<int32_t> budget(n);
+  for (int i = 0; i < n; i++) budget[i] = w->cfg.test_cpu_time_mod * lens[i];
+  if ((rc = avgpu_step(t, 0, n, budget.data(), 0, AVGPU_MODE_TEST)) < 0) { avgpu_destroy(t); return rc; }
+  std::vector<avgpu_cpu_state> st(n);
+  std::vector<uint8_t> ops((size_t)n * AVGPU_MAX_GENOME), fl((size_t)n * AVGPU_MAX_GENOME);
+  if ((rc = avgpu_get_states(t, 0, n, st.data(), ops.data(), fl.data(), AVGPU_MAX_GENOME)) < 0) {
+    avgpu_destroy(t); return rc;
+  }
+  std::vector<uint8_t> tflags((size_t)n * TAPE_SLOT), tchild((size_t)n * TAPE_SLOT);
+  std::vector<int32_t> tflen(n), tclen(n);
+  hipMemcpy(tflags.data(), t->W.t_flags, tflags.size(), hipMemcpyDeviceToHost);
+  hipMemcpy(tchild.data(), t->W.t_child, tchild.size(), hipMemcpyDeviceToHost);
+  hipMemcpy(tflen.data(), t->W.t_flags_len, n * 4, hipMemcpyDeviceToHost);
+  hipMemcpy(tclen.data(), t->W.t_child_len, n * 4, hipMemcpyDeviceToHost);
+  size_t off = 0;
+  for (int i = 0; i < n; i++) {
+    avgpu_test_result& r = results[i];
+    const avgpu_cpu_state& s = st[i];
+    memset(&r, 0, sizeof(r));
+    r.divided = s.num_divides > 0;
+    r.copied_size = s.copied_size;
+    r.executed_size = s.executed_size;
+    r.gestation_time = s.gestation_time;
+    r.genome_length = s.genome_length;
+    r.time_used = s.time_used;
+    r.merit = s.merit;
+    r.fitness = s.fitness;
+    for (int k = 0; k < AVGPU_MAX_REACTIONS; k++) r.task_count[k] = s.last_task_count[k];
+    r.offspring_len = r.divided ? tclen[i] : 0;
+    bool same = r.divided && tclen[i] == lens[i];
+    for (int k = 0; same && k < lens[i]; k++)
+      same = (w->code2op[tchild[(size_t)i * TAPE_SLOT + k]] == genomes[off + k]);
+    r.copy_true = same;
+    if (executed_flags && flags_cap > 0) {
+      char* dst = executed_flags + (size_t)i * flags_cap;
+      memset(dst, 0, flags_cap);
+      if (r.divided) {
+        const int m = std::min(tflen[i], flags_cap - 1);
+        memcpy(dst, tflags.data() + (size_t)i * TAPE_SLOT, m);
+      } else {
+        const int m = std::min(s.mem_size, flags_cap - 1);
+        for (int k = 0; k < m; k++) dst[k] = (fl[(size_t)i * AVGPU_MAX_GENOME + k] & 0x04) ? '+' : '-';
+      }
+    }
+    if (offspring) {
+      uint8_t* d = offspring + (size_t)i * AVGPU_MAX_GENOME;
+      memset(d, 0, AVGPU_MAX_GENOME);
+      for (int k = 0; k < r.offspring_len; k++)
+        d[k] = (uint8_t)w->code2op[tchild[(size_t)i * TAPE_SLOT + k]];
+    }
+    off += lens[i];
+  }
+  avgpu_destroy(t);
+  return 0;
+}
+
+int avgpu_stats_vector(avgpu_world* w, void** dev_ptr) {
+  if (!w || !dev_ptr) return fail(AVGPU_EINVAL, "args");
+  *dev_ptr = w->d_stats;
+  return 0;
+}
+
+int avgpu_set_global_totals(avgpu_world* w, double total_merit, int64_t total_orgs) {
+  if (!w) return fail(AVGPU_EINVAL, "NULL world");
+  double v[2] = {total_merit, (double)total_orgs};
+  HIPCHK(hipMemcpyAsync(w->d_totals, v, sizeof(v), hipMemcpyHostToDevice, w->stream));
+  HIPCHK(hipStreamSynchronize(w->stream));
+  w->use_global = true;
+  return 0;
+}
+
+int avgpu_halo_pack(avgpu_world* w, int side, void* dev_buf, int64_t cap, int64_t* n) {
+  (void)w; (void)side; (void)dev_buf; (void)cap; (void)n;
+  return fail(AVGPU_EUNSUPPORTED, "halo exchange not built yet");
+}
+
+int avgpu_halo_unpack(avgpu_world* w, int side, const void* dev_buf, int64_t n) {
+  (void)w; (void)side; (void)dev_buf; (void)n;
+  return fail(AVGPU_EUNSUPPORTED, "halo exchange not built yet");
+}
+
+int64_t avgpu_halo_record_bytes(void) { return 0; }
+
+int avgpu_last_step_insts(avgpu_world* w, int64_t* insts) {
+  if (!w || !insts) return fail(AVGPU_EINVAL, "args");
+  unsigned long long v = 0;
+  HIPCHK(hipMemcpyAsync(&v, w->W.counters + CNT_INSTS, 8, hipMemcpyDeviceToHost, w->stream));
+  HIPCHK(hipStreamSynchronize(w->stream));
+  *insts = (int64_t)v;
+  return 0;
+}
+
+int avgpu_last_kernel_ms(avgpu_world* w, double* ms, int64_t* launches) {
+  if (!w) return fail(AVGPU_EINVAL, "NULL world");
+  int rc = drain_ring(w, 0);
+  if (rc < 0) return rc;
+  if (ms) *ms = w->acc_ms;
+  if (launches) *launches = w->acc_phases;
+  w->acc_ms = 0.0;
+  w->acc_phases = 0;
+  return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,220 @@
+// device.h -- HBM layout of the organism SoA and device helpers shared by the
+// HIP kernels of the batched heads-CPU interpreter (gfx950 / MI355X).
+//
+// Layout (DESIGN.md "Data layout in HBM"): one organism per cell, structure of
+// arrays, every array indexed [field_row * N + cell] so that a wavefront of 64
+// consecutive list entries touches 64 consecutive words when the list is in
+// cell order.  The memory tape of cell c lives in tape[c * TAPE_SLOT ...] as one
+// byte per site: bits 0-5 = canonical handler id (include/avida_gpu.h), bit 6 =
+// copied flag, bit 7 = executed flag (cpu/cCPUMemory.h:31-37; the mutated /
+// copy-mut flags are statistics only and are not kept on device).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/avida_gpu.h"
+
+#define TAPE_SLOT 2048
+#define CODE_MASK 0x3F
+#define TF_COPIED 0x40
+#define TF_EXEC 0x80
+#define CODE_ERROR 0x3F  /* cInstSet::GetInstError: never a nop */
+
+// ctl word bits
+#define CTL_SP0(c) ((c) & 0xF)
+#define CTL_SP1(c) (((c) >> 4) & 0xF)
+#define CTL_CURSTK 0x100u
+#define CTL_MAL 0x200u
+#define CTL_ALIVE 0x400u
+
+#define NUM_CLASSES 4
+
+struct DevWorld {
+  int64_t n;  // cells
+  // --- hot state (registers in the interpreter) ---
+  int32_t* reg;       // [3][n]
+  int32_t* head;      // [4][n]
+  uint32_t* ctl;      // [n]  sp0 | sp1<<4 | cur_stack | mal_active | alive
+  uint32_t* rlabel;   // [n]  read_label: len (4b) | nop i at bits 4+2i
+  int32_t* mem_size;  // [n]
+  int32_t* cycles;    // [n]  cpu_cycles_used
+  int32_t* time_used; // [n]
+  int32_t* gest_start;// [n]
+  int32_t* max_exec;  // [n]
+  int32_t* birth_len; // [n]  genome length at birth (cPhenotype::genome_length)
+  uint32_t* rng;      // [3][n] key_lo, key_hi, ctr
+  int32_t* budget;    // [n]  instructions left in this update
+  uint8_t* tape;      // [n][TAPE_SLOT]
+  // --- cold state (touched in place by IO / stack / divide) ---
+  int32_t* stack;     // [2*10][n]
+  int32_t* inbuf;     // [3][n] most recent first
+  int32_t* in_total;  // [n]
+  int32_t* in_ptr;    // [n]
+  int32_t* outbuf;    // [n]
+  int32_t* out_total; // [n]
+  int32_t* inputs;    // [3][n] cell inputs
+  int32_t* cur_task;  // [16][n]
+  int32_t* last_task; // [16][n]
+  int32_t* cur_react; // [16][n]
+  double* cur_bonus;  // [n]
+  double* merit;      // [n]
+  double* fitness;    // [n]
+  double* credit;     // [n]
+  int32_t* gest_time; // [n]
+  int32_t* num_div;   // [n]
+  int32_t* generation;// [n]
+  int32_t* copied;    // [n]
+  int32_t* child_copied; // [n]
+  int32_t* executed;  // [n]
+  int32_t* errors;    // [n]
+  // --- per-update work lists / queues ---
+  int32_t* class_list;   // [NUM_CLASSES][n]
+  int32_t* class_count;  // [NUM_CLASSES]
+  unsigned long long* counters; // [16] insts, deaths, divides, births, dropped, ...
+  // birth queue
+  int64_t bcap;
+  int32_t* b_count;   // [1]
+  int32_t* b_parent;  // [bcap]
+  uint32_t* b_seq;    // [bcap]
+  int32_t* b_len;     // [bcap]
+  double* b_merit;    // [bcap]
+  double* b_fitness;  // [bcap]
+  int32_t* b_gen;     // [bcap]
+  int32_t* b_ccopied; // [bcap]
+  int32_t* b_exec;    // [bcap]
+  int32_t* b_gest;    // [bcap]
+  uint32_t* b_rng;    // [3][bcap]
+  int32_t* b_target;  // [bcap]
+  int8_t* b_state;    // [bcap]  0 pending 1 placed -1 failed
+  unsigned long long* b_prio; // [bcap]
+  uint8_t* b_genome;  // [bcap][TAPE_SLOT]
+  // placement scratch
+  uint8_t* occ;       // [n]
+  unsigned long long* claim; // [n]
+  int32_t* owner;     // [n]
+  // test-CPU outputs
+  uint8_t* t_flags;   // [n][TAPE_SLOT] executed flags snapshot ('+'/'-')
+  int32_t* t_flags_len; // [n]
+  uint8_t* t_child;   // [n][TAPE_SLOT]
+  int32_t* t_child_len; // [n]
+  // tables
+  int32_t* rand_cum;  // [64] cumulative integer weights
+  uint8_t* rand_code; // [64] canonical code of op i
+  uint16_t* task_lut; // [256] logic id -> task bitmask
+  int n_ops;
+  int32_t rand_total;
+  int n_react;
+  int32_t react_task[AVGPU_MAX_REACTIONS];
+  int32_t react_type[AVGPU_MAX_REACTIONS];
+  int32_t react_min[AVGPU_MAX_REACTIONS];
+  int32_t react_max[AVGPU_MAX_REACTIONS];
+  int32_t react_hasreq[AVGPU_MAX_REACTIONS];
+  double react_mult[AVGPU_MAX_REACTIONS];
+  double react_add[AVGPU_MAX_REACTIONS];
+  uint8_t fill_code;   // code of op 0 (new sites on allocate)
+  // config scalars
+  int32_t world_x, world_y, geometry;
+  int32_t ave_time_slice, slicing;
+  int32_t base_merit_method, base_const_merit;
+  double default_bonus, size_range, min_copied_lines, min_exe_lines;
+  double merit_default_bonus, required_bonus;
+  int32_t inherit_merit, require_allocate, alloc_method, max_label_exe;
+  int32_t min_genome, max_genome;  // resolved MIN/MAX (>= 8, <= 2048)
+  int32_t cfg_min_genome, cfg_max_genome;  // raw MIN_GENOME_SIZE / MAX_GENOME_SIZE
+  int32_t death_method, age_limit;
+  int32_t prefer_empty, allow_parent, birth_method;
+  uint64_t th_copy_mut, th_div_mut, th_div_ins, th_div_del;
+  uint32_t seed_lo, seed_hi;
+  // tile geometry for multi-GPU strips (rows [row0,row0+rows) of a
+  // world_x x global_rows torus); single GPU: row0=0, rows=world_y
+  int32_t row0, global_rows;
+};
+
+// counters[] slots
+#define CNT_INSTS 0
+#define CNT_DEATHS 1
+#define CNT_DIVIDES 2
+#define CNT_BIRTHS 3
+#define CNT_DROPPED 4
+#define CNT_SPILLS 5
+#define CNT_SLICES 6
+#define CNT_PER_UPDATE 8      /* slots [0, 8) are reset every update */
+#define CNT_CUM_INSTS 8
+#define CNT_CUM_BIRTHS 9
+
+// ---------------------------------------------------------------------------
+// RNG spec: identical arithmetic to the oracle's Stream.
+__device__ __forceinline__ uint32_t lowbias32(uint32_t x) {
+  x ^= x >> 16; x *= 0x7feb352dU; x ^= x >> 15; x *= 0x846ca68bU; x ^= x >> 16;
+  return x;
+}
+__device__ __forceinline__ uint32_t rng_next(uint32_t lo, uint32_t hi, uint32_t& ctr) {
+  uint32_t a = lowbias32(ctr * 0x9E3779B9U + hi);
+  uint32_t b = lowbias32(a ^ lo);
+  ++ctr;
+  return b;
+}
+__device__ __forceinline__ uint32_t rng_below(uint32_t lo, uint32_t hi, uint32_t& ctr, uint32_t n) {
+  return (uint32_t)(((uint64_t)rng_next(lo, hi, ctr) * n) >> 32);
+}
+__device__ __forceinline__ bool rng_p(uint32_t lo, uint32_t hi, uint32_t& ctr, uint64_t th) {
+  return (uint64_t)rng_next(lo, hi, ctr) < th;
+}
+__device__ __forceinline__ void derive_key(uint32_t a_lo, uint32_t a_hi, uint32_t x, uint32_t y,
+                                           uint32_t& lo, uint32_t& hi) {
+  lo = lowbias32(lowbias32(x ^ a_lo) + y);
+  hi = lowbias32(lowbias32(y ^ a_hi) + x + 0x632BE5ABU);
+}
+
+// cHeadCPU::Adjust (cpu/cHeadCPU.cc:27-50)
+__device__ __forceinline__ int head_adjust(int pos, int size) {
+  if ((unsigned)pos < (unsigned)size) return pos;
+  if (pos < 0) return 0;
+  if (pos < 2 * size) return pos - size;
+  return pos % size;
+}
+
+// cInstSet::GetRandomInst (cpu/cInstSet.cc:83-88) -> canonical code
+__device__ __forceinline__ uint8_t random_code(const DevWorld& W, uint32_t lo, uint32_t hi,
+                                               uint32_t& ctr) {
+  uint32_t r = rng_below(lo, hi, ctr, (uint32_t)W.rand_total);
+  int i = 0;
+  while (i < W.n_ops - 1 && W.rand_cum[i] <= (int32_t)r) i++;
+  return W.rand_code[i];
+}
+
+// CalcSizeMerit (main/cPhenotype.cc:1760-1816)
+__device__ __forceinline__ int calc_size_merit(const DevWorld& W, int glen, int copied, int exe) {
+  int s;
+  switch (W.base_merit_method) {
+    case 1: return copied;
+    case 2: return exe;
+    case 3: return glen;
+    case 4: s = glen; if (s > copied) s = copied; if (s > exe) s = exe; return s;
+    case 5: s = glen; if (s > copied) s = copied; if (s > exe) s = exe;
+            return (int)sqrt((double)s);
+    default: return W.base_const_merit;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// host-side launchers (defined next to their kernels)
+struct LaunchInfo {
+  hipStream_t stream;
+  hipEvent_t ev0, ev1;
+  bool timed;
+};
+
+void launch_interpret_classes(const DevWorld& W, int mode, hipStream_t s, int64_t max_lanes,
+                              float* kernel_ms, int* launches);
+void launch_world_pre(const DevWorld& W, hipStream_t s, const double* d_totals);
+void launch_world_post(const DevWorld& W, hipStream_t s, double* d_stats);
+void launch_classify_uniform(const DevWorld& W, hipStream_t s, int64_t first, int64_t count,
+                             const int32_t* d_budget, int32_t uniform);
+void launch_set_orgs(const DevWorld& W, hipStream_t s, int64_t first, int64_t count,
+                     const uint8_t* d_codes, const int32_t* d_offsets, const int32_t* d_lens,
+                     const double* d_merits, const int32_t* d_inputs, int deterministic);
+void launch_get_states(const DevWorld& W, hipStream_t s, int64_t first, int64_t count,
+                       avgpu_cpu_state* d_states, uint8_t* d_codes, int cap);
+void launch_merit_total(const DevWorld& W, hipStream_t s, double* d_totals, double* d_scratch);

@@ -1,0 +1,509 @@
+// world.hip -- the per-update kernels around k_interpret:
+//   k_set_orgs       cPopulation::Inject / ActivateOrganism + cPhenotype::SetupInject
+//   k_get_states     cHardwareBase inspection API (trace tuple gather)
+//   k_classify_*     budget + LDS size-class lists for k_interpret
+//   k_merit_*        deterministic total merit (scheduler input)
+//   k_allot          merit-weighted time slicing (cScheduler restated)
+//   k_place_*        cPopulation::PositionOffspring in conflict-resolving rounds
+//   k_activate       cPopulation::ActivateOrganism + cPhenotype::SetupOffspring
+//   k_stats          cStats reduction inputs
+// Paths are relative to avida-core/source/ of the reference.
+#include "device.h"
+
+#pragma clang fp contract(off)
+
+namespace {
+
+__device__ __forceinline__ int class_of(int need) {
+  return need <= 384 ? 0 : (need <= 768 ? 1 : (need <= 1536 ? 2 : 3));
+}
+
+// Append `cell` to its size-class list (wave-aggregated atomics per class).
+__device__ __forceinline__ void enqueue_class(const DevWorld& W, int cell, bool want, int cls) {
+  for (int k = 0; k < NUM_CLASSES; k++) {
+    const bool mine = want && cls == k;
+    const unsigned long long mask = __ballot(mine);
+    if (!mask) continue;
+    const int lane = threadIdx.x & 63;
+    const int leader = __ffsll((long long)mask) - 1;
+    int base = 0;
+    if (lane == leader) base = atomicAdd(&W.class_count[k], __popcll(mask));
+    base = __shfl(base, leader);
+    if (mine) {
+      const int rank = __popcll(mask & ((1ull << lane) - 1ull));
+      W.class_list[(int64_t)k * W.n + base + rank] = cell;
+    }
+  }
+}
+
+__device__ __forceinline__ int need_of(const DevWorld& W, int cell) {
+  const int m = W.mem_size[cell];
+  if (W.ctl[cell] & CTL_MAL) return m;
+  const int grown = m + min((int)(W.size_range * m), AVGPU_MAX_GENOME - m);
+  return grown > m ? grown : m;
+}
+
+// ---------------------------------------------------------------------------
+__global__ void k_set_orgs(DevWorld W, int64_t first, int64_t count, const uint8_t* codes,
+                           const int32_t* offsets, const int32_t* lens, const double* merits,
+                           const int32_t* inputs, int deterministic) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= count) return;
+  const int64_t N = W.n;
+  const int64_t c = first + i;
+  const int len = lens[i];
+  const uint8_t* g = codes + offsets[i];
+  uint8_t* t = W.tape + c * TAPE_SLOT;
+  for (int k = 0; k < len; k++) t[k] = g[k] & CODE_MASK;
+  for (int k = 0; k < 3; k++) W.reg[k * N + c] = 0;
+  for (int k = 0; k < 4; k++) W.head[k * N + c] = 0;
+  for (int k = 0; k < 2 * AVGPU_STACK_SIZE; k++) W.stack[k * N + c] = 0;
+  W.ctl[c] = CTL_ALIVE;
+  W.rlabel[c] = 0;
+  W.mem_size[c] = len;
+  W.cycles[c] = 0; W.time_used[c] = 0; W.gest_start[c] = 0;
+  int mx = 0;
+  if (W.death_method > 0) {                 // cOrganism::initialize (main/cOrganism.cc:216-236)
+    mx = W.age_limit;
+    if (W.death_method == 2) mx *= len;
+    if (mx < 1) mx = 1;
+  }
+  W.max_exec[c] = mx;
+  W.birth_len[c] = len;
+  // stream key (DESIGN.md RNG spec)
+  uint32_t lo, hi, ctr = 0;
+  derive_key(W.seed_lo, W.seed_hi, (uint32_t)c, 0xA5A5A5A5U, lo, hi);
+  int in0, in1, in2;
+  if (inputs) { in0 = inputs[3 * i]; in1 = inputs[3 * i + 1]; in2 = inputs[3 * i + 2]; }
+  else if (deterministic) { in0 = 0x0f13149f; in1 = 0x3308e53e; in2 = 0x556241eb; }
+  else {                                      // cEnvironment::SetupInputs random
+    in0 = (15 << 24) + (int)rng_below(lo, hi, ctr, 1u << 24);
+    in1 = (51 << 24) + (int)rng_below(lo, hi, ctr, 1u << 24);
+    in2 = (85 << 24) + (int)rng_below(lo, hi, ctr, 1u << 24);
+  }
+  W.rng[c] = lo; W.rng[N + c] = hi; W.rng[2 * N + c] = ctr;
+  W.inputs[c] = in0; W.inputs[N + c] = in1; W.inputs[2 * N + c] = in2;
+  W.budget[c] = 0;
+  for (int k = 0; k < 3; k++) W.inbuf[k * N + c] = 0;
+  W.in_total[c] = 0; W.in_ptr[c] = 0; W.outbuf[c] = 0; W.out_total[c] = 0;
+  for (int k = 0; k < AVGPU_MAX_REACTIONS; k++) {
+    W.cur_task[k * N + c] = 0; W.last_task[k * N + c] = 0; W.cur_react[k * N + c] = 0;
+  }
+  // cPhenotype::SetupInject (main/cPhenotype.cc:599-640)
+  W.cur_bonus[c] = W.default_bonus;
+  W.merit[c] = (merits && merits[i] > 0.0) ? merits[i] : (double)len;
+  W.fitness[c] = 0.0;
+  W.credit[c] = 0.0;
+  W.gest_time[c] = 0; W.num_div[c] = 0; W.generation[c] = 0;
+  W.copied[c] = len; W.child_copied[c] = 0; W.executed[c] = len; W.errors[c] = 0;
+}
+
+__global__ void k_get_states(DevWorld W, int64_t first, int64_t count, avgpu_cpu_state* out,
+                             uint8_t* codes, int cap) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= count) return;
+  const int64_t N = W.n;
+  const int64_t c = first + i;
+  avgpu_cpu_state s;
+  memset(&s, 0, sizeof(s));
+  for (int k = 0; k < 3; k++) s.reg[k] = W.reg[k * N + c];
+  for (int k = 0; k < 4; k++) s.head[k] = W.head[k * N + c];
+  for (int k = 0; k < 2; k++)
+    for (int j = 0; j < AVGPU_STACK_SIZE; j++) s.stack[k][j] = W.stack[(k * AVGPU_STACK_SIZE + j) * N + c];
+  const uint32_t ctl = W.ctl[c];
+  s.stack_ptr[0] = CTL_SP0(ctl); s.stack_ptr[1] = CTL_SP1(ctl);
+  s.cur_stack = (ctl & CTL_CURSTK) ? 1 : 0;
+  s.mal_active = (ctl & CTL_MAL) ? 1 : 0;
+  s.alive = (ctl & CTL_ALIVE) ? 1 : 0;
+  const uint32_t rl = W.rlabel[c];
+  s.read_label_len = rl & 15;
+  for (int k = 0; k < (int)(rl & 15); k++) s.read_label[k] = (int8_t)((rl >> (4 + 2 * k)) & 3);
+  s.mem_size = W.mem_size[c];
+  s.cpu_cycles_used = W.cycles[c];
+  s.time_used = W.time_used[c];
+  s.gestation_start = W.gest_start[c];
+  s.gestation_time = W.gest_time[c];
+  s.num_divides = W.num_div[c];
+  s.generation = W.generation[c];
+  s.genome_length = W.birth_len[c];
+  s.copied_size = W.copied[c];
+  s.child_copied_size = W.child_copied[c];
+  s.executed_size = W.executed[c];
+  s.max_executed = W.max_exec[c];
+  s.birth_length = W.birth_len[c];
+  s.input_ptr = W.in_ptr[c];
+  const int tot = W.in_total[c];
+  for (int k = 0; k < 3; k++) s.input_buf[k] = (k < tot) ? W.inbuf[k * N + c] : 0;
+  s.input_total = tot;
+  s.output_total = W.out_total[c];
+  s.output_buf = s.output_total ? W.outbuf[c] : 0;
+  for (int k = 0; k < 3; k++) s.inputs[k] = W.inputs[k * N + c];
+  for (int k = 0; k < AVGPU_MAX_REACTIONS; k++) {
+    s.cur_task_count[k] = W.cur_task[k * N + c];
+    s.last_task_count[k] = W.last_task[k * N + c];
+    s.cur_reaction_count[k] = W.cur_react[k * N + c];
+  }
+  s.rng_key_lo = W.rng[c]; s.rng_key_hi = W.rng[N + c]; s.rng_counter = W.rng[2 * N + c];
+  s.errors = W.errors[c];
+  s.cur_bonus = W.cur_bonus[c];
+  s.merit = W.merit[c];
+  s.fitness = W.fitness[c];
+  out[i] = s;
+  if (codes) {
+    const uint8_t* t = W.tape + c * TAPE_SLOT;
+    uint8_t* d = codes + i * cap;
+    const int m = s.mem_size < cap ? s.mem_size : cap;
+    for (int k = 0; k < m; k++) d[k] = t[k];
+  }
+}
+
+// budget = uniform or per-cell array, all live cells of [first, first+count)
+__global__ void k_classify_uniform(DevWorld W, int64_t first, int64_t count, const int32_t* budget,
+                                   int32_t uniform) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool in = i < count;
+  const int cell = in ? (int)(first + i) : 0;
+  int b = 0;
+  bool want = false;
+  int cls = 0;
+  if (in) {
+    b = budget ? budget[i] : uniform;
+    W.budget[cell] = b;
+    want = (W.ctl[cell] & CTL_ALIVE) && b > 0;
+    if (want) cls = class_of(need_of(W, cell));
+  }
+  enqueue_class(W, cell, want, cls);
+}
+
+// ---- deterministic total merit: 256-cell blocks, fixed pairwise tree ----
+__global__ __launch_bounds__(256) void k_merit_partial(DevWorld W, double* partial, int32_t* alive_partial) {
+  __shared__ double s[256];
+  __shared__ int a[256];
+  const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const bool live = c < W.n && (W.ctl[c] & CTL_ALIVE);
+  s[threadIdx.x] = live ? W.merit[c] : 0.0;
+  a[threadIdx.x] = live ? 1 : 0;
+  __syncthreads();
+  for (int stride = 128; stride >= 1; stride >>= 1) {
+    if ((int)threadIdx.x < stride) {
+      s[threadIdx.x] = __dadd_rn(s[threadIdx.x], s[threadIdx.x + stride]);
+      a[threadIdx.x] += a[threadIdx.x + stride];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) { partial[blockIdx.x] = s[0]; alive_partial[blockIdx.x] = a[0]; }
+}
+
+// totals[0] = sum merit (block partials added in order), totals[1] = alive count
+__global__ __launch_bounds__(256) void k_merit_final(const double* partial, const int32_t* alive_partial,
+                                                     int64_t nb, double* totals, int use_global) {
+  __shared__ double s[256];
+  __shared__ long long cnt[256];
+  // counts: any order (integers)
+  long long c = 0;
+  for (int64_t b = threadIdx.x; b < nb; b += 256) c += alive_partial[b];
+  cnt[threadIdx.x] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    long long tc = 0;
+    for (int i = 0; i < 256; i++) tc += cnt[i];
+    if (!use_global) {
+      double t = 0.0;
+      for (int64_t b = 0; b < nb; b++) t = __dadd_rn(t, partial[b]);
+      totals[0] = t;
+      totals[1] = (double)tc;
+    }
+    totals[2] = (double)tc;  // local organisms
+  }
+  (void)s;
+}
+
+// cScheduler restated (DESIGN.md "Scheduler"): lambda = UD * merit / total
+__global__ void k_allot(DevWorld W, const double* totals) {
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool in = c < W.n;
+  bool want = false;
+  int cls = 0;
+  if (in) {
+    int b = 0;
+    if (W.ctl[c] & CTL_ALIVE) {
+      const double sum = totals[0];
+      const int64_t ud = (int64_t)W.ave_time_slice * (int64_t)totals[1];
+      if (W.slicing == AVGPU_SLICE_CONSTANT || !(sum > 0.0)) {
+        b = W.ave_time_slice;
+      } else {
+        double lam = __ddiv_rn(__dmul_rn((double)ud, W.merit[c]), sum);
+        if (lam > 1.0e8) lam = 1.0e8;
+        if (W.slicing == AVGPU_SLICE_INTEGRATED) {
+          double cr = __dadd_rn(W.credit[c], lam);
+          const double fl = floor(cr);
+          b = (int)fl;
+          W.credit[c] = __dsub_rn(cr, fl);
+        } else {
+          const double fl = floor(lam);
+          const double frac = __dsub_rn(lam, fl);
+          const uint64_t th = (uint64_t)__dmul_rn(frac, 4294967296.0);
+          uint32_t ctr = W.rng[2 * W.n + c];
+          const bool extra = rng_p(W.rng[c], W.rng[W.n + c], ctr, th);
+          W.rng[2 * W.n + c] = ctr;
+          b = (int)fl + (extra ? 1 : 0);
+        }
+      }
+      want = b > 0;
+      if (want) cls = class_of(need_of(W, (int)c));
+    }
+    W.budget[c] = b;
+  }
+  const unsigned long long m = __ballot(want);
+  if ((threadIdx.x & 63) == 0 && m) atomicAdd(&W.counters[CNT_SLICES], (unsigned long long)__popcll(m));
+  enqueue_class(W, (int)c, want, cls);
+}
+
+// ---- birth placement (cPopulation::PositionOffspring restated) ----
+// neighbour k of cell in fixed order NW N NE W E SW S SE (tools/cTopology.h)
+__device__ __forceinline__ int neighbours(const DevWorld& W, int cell, int* out) {
+  const int X = W.world_x, Y = W.world_y;
+  const int x = cell % X, y = cell / X;
+  int n = 0;
+  for (int dy = -1; dy <= 1; dy++)
+    for (int dx = -1; dx <= 1; dx++) {
+      if (dx == 0 && dy == 0) continue;
+      int nx = x + dx, ny = y + dy;
+      if (W.geometry == 1) {
+        if (nx < 0 || nx >= X || ny < 0 || ny >= Y) continue;
+      } else {
+        nx = (nx + X) % X; ny = (ny + Y) % Y;
+      }
+      out[n++] = ny * X + nx;
+    }
+  return n;
+}
+
+__global__ void k_occ_init(DevWorld W) {
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c < W.n) { W.occ[c] = (W.ctl[c] & CTL_ALIVE) ? 1 : 0; W.owner[c] = -1; }
+}
+
+__global__ void k_place_pick(DevWorld W) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int nb = min(*W.b_count, (int)W.bcap);
+  if (i >= nb || W.b_state[i] != 0) return;
+  const int parent = W.b_parent[i];
+  int nbr[8];
+  const int nn = neighbours(W, parent, nbr);
+  int cand[9];
+  int nc = 0;
+  if (W.prefer_empty)
+    for (int k = 0; k < nn; k++) if (!W.occ[nbr[k]]) cand[nc++] = nbr[k];
+  if (nc == 0 && W.birth_method != 3) {
+    for (int k = 0; k < nn; k++) cand[nc++] = nbr[k];
+    if (W.allow_parent) cand[nc++] = parent;
+  }
+  if (nc == 0) { W.b_state[i] = -1; return; }
+  const uint32_t lo = W.b_rng[i], hi = W.b_rng[W.bcap + i];
+  uint32_t ctr = W.b_rng[2 * W.bcap + i];
+  const int t = cand[rng_below(lo, hi, ctr, (uint32_t)nc)];
+  const unsigned long long prio = ((unsigned long long)rng_next(lo, hi, ctr) << 32) |
+                                  ((unsigned long long)(parent & 0xFFFFFF) << 8) |
+                                  (unsigned long long)(W.b_seq[i] & 0xFF);
+  W.b_rng[2 * W.bcap + i] = ctr;
+  W.b_target[i] = t;
+  W.b_prio[i] = prio;
+  atomicMax(&W.claim[t], prio);
+}
+
+__global__ void k_place_resolve(DevWorld W) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int nb = min(*W.b_count, (int)W.bcap);
+  if (i >= nb || W.b_state[i] != 0) return;
+  const int t = W.b_target[i];
+  if (W.claim[t] == W.b_prio[i]) {
+    W.b_state[i] = 1;
+    W.occ[t] = 1;
+    W.owner[t] = (int)i;
+  }
+}
+
+__global__ void k_place_clear(DevWorld W) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int nb = min(*W.b_count, (int)W.bcap);
+  if (i >= nb) return;
+  const int t = W.b_target[i];
+  if (t >= 0) W.claim[t] = 0ull;
+}
+
+// ActivateOrganism (main/cPopulation.cc:1320-1340) + SetupOffspring (main/cPhenotype.cc:349-420)
+// One wave per birth: the genome copy is coalesced across the wave.
+__global__ __launch_bounds__(64) void k_activate(DevWorld W) {
+  const int nb = min(*W.b_count, (int)W.bcap);
+  for (int64_t i = blockIdx.x; i < nb; i += gridDim.x) {
+  const int lane = threadIdx.x;
+  const int tgt = W.b_target[i];
+  const bool won = W.b_state[i] == 1 && tgt >= 0 && W.owner[tgt] == (int)i;
+  if (!won) {
+    if (lane == 0) atomicAdd(&W.counters[CNT_DROPPED], 1ull);
+    continue;
+  }
+  const int64_t N = W.n;
+  const int64_t c = W.b_target[i];
+  const int len = W.b_len[i];
+  const uint32_t* src = reinterpret_cast<const uint32_t*>(W.b_genome + i * TAPE_SLOT);
+  uint32_t* dst = reinterpret_cast<uint32_t*>(W.tape + c * TAPE_SLOT);
+  for (int w = lane; w < (len + 3) / 4; w += 64) dst[w] = src[w];
+  if (lane < 2 * AVGPU_STACK_SIZE) W.stack[lane * N + c] = 0;
+  if (lane < AVGPU_MAX_REACTIONS) {
+    W.cur_task[lane * N + c] = 0; W.last_task[lane * N + c] = 0; W.cur_react[lane * N + c] = 0;
+  }
+  if (lane < 3) { W.reg[lane * N + c] = 0; W.inbuf[lane * N + c] = 0; }
+  if (lane < 4) W.head[lane * N + c] = 0;
+  if (lane == 0) {
+    W.ctl[c] = CTL_ALIVE;
+    W.rlabel[c] = 0;
+    W.mem_size[c] = len;
+    W.cycles[c] = 0; W.time_used[c] = 0; W.gest_start[c] = 0;
+    int mx = 0;
+    if (W.death_method > 0) { mx = W.age_limit; if (W.death_method == 2) mx *= len; if (mx < 1) mx = 1; }
+    W.max_exec[c] = mx;
+    W.birth_len[c] = len;
+    const uint32_t lo = W.b_rng[i], hi = W.b_rng[W.bcap + i];
+    uint32_t ctr = W.b_rng[2 * W.bcap + i];
+    // cEnvironment::SetupInputs random (main/cEnvironment.cc:1268-1271)
+    W.inputs[c] = (15 << 24) + (int)rng_below(lo, hi, ctr, 1u << 24);
+    W.inputs[N + c] = (51 << 24) + (int)rng_below(lo, hi, ctr, 1u << 24);
+    W.inputs[2 * N + c] = (85 << 24) + (int)rng_below(lo, hi, ctr, 1u << 24);
+    W.rng[c] = lo; W.rng[N + c] = hi; W.rng[2 * N + c] = ctr;
+    W.budget[c] = 0;
+    W.in_total[c] = 0; W.in_ptr[c] = 0; W.outbuf[c] = 0; W.out_total[c] = 0;
+    W.cur_bonus[c] = W.default_bonus;
+    W.merit[c] = W.b_merit[i];
+    W.fitness[c] = W.b_fitness[i];
+    W.credit[c] = 0.0;
+    W.gest_time[c] = W.b_gest[i];
+    W.num_div[c] = 0;
+    W.generation[c] = W.b_gen[i];
+    W.copied[c] = W.b_ccopied[i];
+    W.child_copied[c] = 0;
+    W.executed[c] = W.b_exec[i];
+    W.errors[c] = 0;
+    atomicAdd(&W.counters[CNT_BIRTHS], 1ull);
+  }
+  }
+}
+
+// ---- statistics: per-block partials, then one block ----
+// partial slots: 0 orgs 1 merit 2 fitness 3 gestation 4 genome length 5 max fitness
+// 6 generation 7 memory size 8..16 task organisms
+#define NPART 24
+#define NSTAT 40
+__global__ __launch_bounds__(256) void k_stats_partial(DevWorld W, double* part) {
+  __shared__ double s[NPART][256];
+  const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  double v[NPART];
+  for (int k = 0; k < NPART; k++) v[k] = 0.0;
+  if (c < W.n && (W.ctl[c] & CTL_ALIVE)) {
+    v[0] = 1.0;
+    v[1] = W.merit[c];
+    v[2] = W.fitness[c];
+    v[3] = (double)W.gest_time[c];
+    v[4] = (double)W.birth_len[c];
+    v[5] = W.fitness[c];   // max
+    v[6] = (double)W.generation[c];
+    v[7] = (double)W.mem_size[c];
+    for (int t = 0; t < AVGPU_NUM_LOGIC_TASKS; t++) v[8 + t] = W.last_task[t * W.n + c] > 0 ? 1.0 : 0.0;
+  }
+  for (int k = 0; k < NPART; k++) s[k][threadIdx.x] = v[k];
+  __syncthreads();
+  for (int stride = 128; stride >= 1; stride >>= 1) {
+    if ((int)threadIdx.x < stride)
+      for (int k = 0; k < NPART; k++) {
+        const double o = s[k][threadIdx.x + stride];
+        s[k][threadIdx.x] = (k == 5) ? fmax(s[k][threadIdx.x], o) : s[k][threadIdx.x] + o;
+      }
+    __syncthreads();
+  }
+  if (threadIdx.x < NPART) part[blockIdx.x * NPART + threadIdx.x] = s[threadIdx.x][0];
+}
+
+// out: [0..23] partial sums, 24 insts 25 deaths 26 divides 27 births 28 dropped
+// 29 spills 30 cumulative insts 31 cumulative births 32 slices
+__global__ __launch_bounds__(64) void k_stats_final(DevWorld W, const double* part, int64_t nb,
+                                                    double* out) {
+  const int k = threadIdx.x;
+  if (k < NPART) {
+    double acc = 0.0;
+    for (int64_t b = 0; b < nb; b++) {
+      const double o = part[b * NPART + k];
+      acc = (k == 5) ? fmax(acc, o) : acc + o;
+    }
+    out[k] = acc;
+  }
+  if (k == 0) {
+    W.counters[CNT_CUM_INSTS] += W.counters[CNT_INSTS];
+    W.counters[CNT_CUM_BIRTHS] += W.counters[CNT_BIRTHS];
+    out[24] = (double)W.counters[CNT_INSTS];
+    out[25] = (double)W.counters[CNT_DEATHS];
+    out[26] = (double)W.counters[CNT_DIVIDES];
+    out[27] = (double)W.counters[CNT_BIRTHS];
+    out[28] = (double)W.counters[CNT_DROPPED];
+    out[29] = (double)W.counters[CNT_SPILLS];
+    out[30] = (double)W.counters[CNT_CUM_INSTS];
+    out[31] = (double)W.counters[CNT_CUM_BIRTHS];
+    out[32] = (double)W.counters[CNT_SLICES];
+  }
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+static inline unsigned nblk(int64_t n, int b) { return (unsigned)((n + b - 1) / b); }
+
+void launch_set_orgs(const DevWorld& W, hipStream_t s, int64_t first, int64_t count,
+                     const uint8_t* codes, const int32_t* offsets, const int32_t* lens,
+                     const double* merits, const int32_t* inputs, int deterministic) {
+  hipLaunchKernelGGL(k_set_orgs, dim3(nblk(count, 64)), dim3(64), 0, s, W, first, count, codes,
+                     offsets, lens, merits, inputs, deterministic);
+}
+
+void launch_get_states(const DevWorld& W, hipStream_t s, int64_t first, int64_t count,
+                       avgpu_cpu_state* states, uint8_t* codes, int cap) {
+  hipLaunchKernelGGL(k_get_states, dim3(nblk(count, 64)), dim3(64), 0, s, W, first, count, states,
+                     codes, cap);
+}
+
+void launch_classify_uniform(const DevWorld& W, hipStream_t s, int64_t first, int64_t count,
+                             const int32_t* budget, int32_t uniform) {
+  hipMemsetAsync(W.class_count, 0, sizeof(int32_t) * NUM_CLASSES, s);
+  hipLaunchKernelGGL(k_classify_uniform, dim3(nblk(count, 256)), dim3(256), 0, s, W, first, count,
+                     budget, uniform);
+}
+
+// totals: [0] sum merit, [1] organisms (deterministic order; DESIGN.md "Scheduler").
+// scratch: (n+255)/256 doubles + as many int32 partials
+void launch_merit_total(const DevWorld& W, hipStream_t s, double* totals, double* scratch) {
+  const int64_t nb = (W.n + 255) / 256;
+  int32_t* alive_partial = reinterpret_cast<int32_t*>(scratch + nb);
+  hipLaunchKernelGGL(k_merit_partial, dim3((unsigned)nb), dim3(256), 0, s, W, scratch, alive_partial);
+  hipLaunchKernelGGL(k_merit_final, dim3(1), dim3(256), 0, s, scratch, alive_partial, nb, totals, 0);
+}
+
+void launch_world_pre(const DevWorld& W, hipStream_t s, const double* totals) {
+  hipMemsetAsync(W.counters, 0, sizeof(unsigned long long) * CNT_PER_UPDATE, s);
+  hipMemsetAsync(W.b_count, 0, sizeof(int32_t), s);
+  hipMemsetAsync(W.class_count, 0, sizeof(int32_t) * NUM_CLASSES, s);
+  hipLaunchKernelGGL(k_allot, dim3(nblk(W.n, 256)), dim3(256), 0, s, W, totals);
+}
+
+void launch_world_post(const DevWorld& W, hipStream_t s, double* stats) {
+  const unsigned bb = nblk(W.bcap, 256);
+  hipLaunchKernelGGL(k_occ_init, dim3(nblk(W.n, 256)), dim3(256), 0, s, W);
+  for (int round = 0; round < 4; round++) {
+    hipLaunchKernelGGL(k_place_pick, dim3(bb), dim3(256), 0, s, W);
+    hipLaunchKernelGGL(k_place_resolve, dim3(bb), dim3(256), 0, s, W);
+    hipLaunchKernelGGL(k_place_clear, dim3(bb), dim3(256), 0, s, W);
+  }
+  hipLaunchKernelGGL(k_activate, dim3(4096), dim3(64), 0, s, W);
+  const int64_t nb = (W.n + 255) / 256;
+  double* part = stats + NSTAT;
+  hipLaunchKernelGGL(k_stats_partial, dim3((unsigned)nb), dim3(256), 0, s, W, part);
+  hipLaunchKernelGGL(k_stats_final, dim3(1), dim3(64), 0, s, W, part, nb, stats);
+}

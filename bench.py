@@ -1,0 +1,238 @@
+"""Throughput benchmark of the batched heads-CPU interpreter (one JSON line).
+
+Workload (BASELINE.json configs[2], metric "organism-instructions/sec +
+updates/sec, 1M-org logic-9 world"): a 1024x1024 torus per GPU, logic-9
+environment, default avida.cfg mutation rates (copy 0.0075, divide ins/del
+0.05), births on.  Every cell starts occupied by an evolved logic-9 genotype
+from the reference's own fixture (tests/heads_midrun_30u/config/
+detail-50000.pop, classic legacy instset; inputs synthetic per cell), so the
+timed updates measure a mature population rather than an ancestor ramp-up.
+
+A "step" is one whole Avida update (Avida2Driver::Run loop body): merit-
+weighted allotment of AVE_TIME_SLICE*N instructions, interpretation, birth
+placement, statistics.  value = organism-instructions executed by all ranks /
+max-over-ranks wall time of the K timed updates.
+
+Multi-GPU (torch.distributed.run, one rank per GPU, RCCL): each rank owns one
+1024x1024 tile (weak scaling); the scheduler's {sum merit, organisms} are
+all-reduced every update so that each tile's share of AVE_TIME_SLICE*N_global
+follows its merit share (cMultiProcessWorld.cc:375-405).
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "organism-instructions/sec + updates/sec, 1M-org logic-9 world, 1/8 GPUs"
+STATE_BYTES_PER_SLICE = 140   # hot state read + write per organism time slice
+HBM_PEAK_GBS = 8000.0         # MI355X_MICROARCH.md chip table (spec)
+
+
+def _pool(golden):
+    from avida_amd import files
+    iset = files.read_instset(os.path.join(golden, "instset-classic.cfg"))
+    pool = []
+    for g in files.read_pop(os.path.join(golden, "detail-50000.pop")):
+        pool.extend([iset.parse_sequence(g.sequence)] * g.num_cpus)
+    return iset, pool
+
+
+def _genomes_for(n, pool, salt):
+    import numpy as np
+    idx = (np.arange(n, dtype=np.uint64) * np.uint64(2654435761) + np.uint64(salt)) % np.uint64(len(pool))
+    return [pool[int(i)] for i in idx]
+
+
+def build_world(lib, capi, files, golden, side, seed, device, rank):
+    iset, pool = _pool(golden)
+    env = files.read_environment(os.path.join(golden, "environment-logic9.cfg"))
+    cfg = capi.cfg_from_avida(files.read_avida_cfg(None, {"WORLD_X": side, "WORLD_Y": side}),
+                              seed=seed + 1000003 * rank)
+    n = side * side
+    h = lib.avgpu_create(C.byref(cfg), device, n)
+    if not h:
+        raise RuntimeError(lib.avgpu_last_error().decode())
+    hid = (C.c_uint8 * len(iset.names))(*iset.handlers)
+    red = (C.c_int32 * len(iset.names))(*iset.redundancy)
+    capi.check(lib, lib.avgpu_load_instset(h, len(iset.names), hid, red))
+    arr = capi.reactions_array(env)
+    capi.check(lib, lib.avgpu_load_env(h, len(env), arr))
+    genomes = _genomes_for(n, pool, rank * 7919)
+    blob = b"".join(genomes)
+    buf = (C.c_uint8 * len(blob)).from_buffer_copy(blob)
+    lens = (C.c_int32 * n)(*[len(g) for g in genomes])
+    capi.check(lib, lib.avgpu_set_orgs(h, 0, n, buf, lens, None, None, 0))
+    return h, cfg, n
+
+
+def cpu_baseline(golden, seconds):
+    """Reference-style serial world (tests/oracle_lib.py, CPU restatement) on one
+    host core: a 60x60 world filled from the same genotype pool, updates until
+    `seconds` elapse."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from avida_amd import capi, files
+    import oracle_lib as ol
+    iset, pool = _pool(golden)
+    env = files.read_environment(os.path.join(golden, "environment-logic9.cfg"))
+    cfg = capi.cfg_from_avida(files.read_avida_cfg(None), seed=101)
+    n = cfg.world_x * cfg.world_y
+    b = ol.Backend("oracle", cfg, iset, env, ncells=n)
+    b.set_orgs(0, _genomes_for(n, pool, 0), deterministic=False)
+    st = capi.AvgpuUpdateStats()
+    insts, updates = 0, 0
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        b.lib.orc_run_serial_updates(b.h, 10, C.byref(st))
+        insts += st.insts_executed
+        updates += 10
+    dt = time.perf_counter() - t0
+    return {"value": insts / dt, "unit": "organism-instructions/s", "cores": 1, "kind": "port",
+            "sample": f"oracle serial world (reference-style scheduler + speculative steps), "
+                      f"60x60 evolved logic-9 population, {updates} updates, {insts} insts, "
+                      f"{dt:.1f} s on 1 host core",
+            "updates_per_sec": updates / dt}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--side", type=int, default=1024)
+    ap.add_argument("--seed", type=int, default=101)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl")
+
+    from avida_amd import capi, files
+    lib = capi.load_product()
+    golden = os.path.join(ROOT, "tests", "golden")
+    h, cfg, n = build_world(lib, capi, files, golden, args.side, args.seed, local, rank)
+    stream = torch.cuda.current_stream()
+    capi.check(lib, lib.avgpu_set_stream(h, C.c_void_p(stream.cuda_stream)))
+    totals = torch.zeros(8, dtype=torch.float64, device="cuda")
+
+    def update():
+        if world > 1:
+            capi.check(lib, lib.avgpu_update_totals(h, C.c_void_p(totals.data_ptr())))
+            dist.all_reduce(totals[:2])
+            capi.check(lib, lib.avgpu_update_run(h, C.c_void_p(totals.data_ptr()), None))
+        else:
+            capi.check(lib, lib.avgpu_run_update(h, None))
+
+    for _ in range(args.warmup):
+        update()
+    torch.cuda.synchronize()
+    s0 = capi.AvgpuUpdateStats()
+    capi.check(lib, lib.avgpu_get_stats(h, C.byref(s0)))
+    kms, phases = C.c_double(), C.c_int64()
+    capi.check(lib, lib.avgpu_last_kernel_ms(h, C.byref(kms), C.byref(phases)))  # reset
+
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        update()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    t1 = time.perf_counter()
+
+    s1 = capi.AvgpuUpdateStats()
+    capi.check(lib, lib.avgpu_get_stats(h, C.byref(s1)))
+    capi.check(lib, lib.avgpu_last_kernel_ms(h, C.byref(kms), C.byref(phases)))
+    insts = s1.cum_insts_executed - s0.cum_insts_executed
+    births = s1.cum_births - s0.cum_births
+    dt = t1 - t0
+    vec = torch.tensor([dt, float(insts), float(births), float(s1.num_organisms),
+                        kms.value, float(phases.value), float(s1.slices), s1.sum_mem_size],
+                       dtype=torch.float64, device="cuda")
+    if dist:
+        mx = vec.clone()
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        dist.all_reduce(vec)
+        dt_max = mx[0].item()
+        kernel_ms_avg = mx[4].item() / max(1.0, mx[5].item())
+    else:
+        dt_max = vec[0].item()
+        kernel_ms_avg = vec[4].item() / max(1.0, vec[5].item())
+    tot_insts, tot_births, tot_orgs = vec[1].item(), vec[2].item(), vec[3].item()
+    if rank != 0:
+        if dist:
+            dist.destroy_process_group()
+        return
+    value = tot_insts / dt_max
+    # roofline of the dominant kernel (k_interpret, all size classes of one
+    # update = one "launch" phase): algorithmic bytes = per slice the hot state
+    # (STATE_BYTES_PER_SLICE) + memory tape read and written once (2 B/site).
+    slices = s1.slices
+    mean_mem = s1.sum_mem_size / max(1, s1.num_organisms)
+    bytes_per_phase = slices * (STATE_BYTES_PER_SLICE + 2.0 * mean_mem)
+    achieved = bytes_per_phase / (kernel_ms_avg * 1e-3) / 1e9 if kernel_ms_avg > 0 else 0.0
+    out = {
+        "metric": METRIC,
+        "value": value,
+        "unit": "organism-instructions/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": dt_max * 1e3 / args.steps,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "int32",
+        "data": "synthetic",
+        "config": {
+            "workload": f"configs[2]: {args.side}x{args.side} torus per GPU, logic-9, default "
+                        "avida.cfg mutation rates, births on, seeded with the detail-50000.pop "
+                        "evolved genotypes (classic instset)",
+            "world": f"{args.side}x{args.side}x{world}",
+            "organisms": int(tot_orgs),
+            "updates_per_sec": args.steps / dt_max,
+            "births_per_update": tot_births / args.steps,
+            "insts_per_update": tot_insts / args.steps,
+            "parallelism": f"tiles{world}",
+        },
+        "roofline": {
+            "bound": "hbm",
+            "achieved": achieved,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS,
+            "traffic": None,
+            "kernel": "k_interpret (all LDS size classes of one update)",
+            "kernel_ms": kernel_ms_avg,
+            "bytes_per_launch": bytes_per_phase,
+            "mean_mem_sites": mean_mem,
+            "slices_per_launch": slices,
+        },
+        "cpu_baseline": None,
+    }
+    if world == 1 and not args.no_cpu:
+        out["cpu_baseline"] = cpu_baseline(golden, args.cpu_seconds)
+    lib.avgpu_destroy(h)
+    print(json.dumps(out), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

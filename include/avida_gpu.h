@@ -233,6 +233,10 @@ typedef struct avgpu_update_stats {
   double sum_genome_length;
   double max_fitness;
   double ave_generation;
+  double sum_mem_size;         /* sum of memory-tape sizes after the update */
+  int64_t cum_insts_executed;  /* since avgpu_create */
+  int64_t cum_births;
+  int64_t slices;              /* organism time slices interpreted this update */
 } avgpu_update_stats;
 
 typedef struct avgpu_world avgpu_world;   /* opaque handle */
@@ -283,6 +287,18 @@ int avgpu_step(avgpu_world* w, int64_t first_cell, int64_t count,
  * main/cPopulation.cc:5185-5414), statistics. out may be NULL (no host sync). */
 int avgpu_run_update(avgpu_world* w, avgpu_update_stats* out);
 int avgpu_run_updates(avgpu_world* w, int n_updates, avgpu_update_stats* last);
+/* The same update split around an external all-reduce (multi-GPU tiles,
+ * cMultiProcessWorld::CalculateUpdateSize main/cMultiProcessWorld.cc:375-405):
+ * avgpu_update_totals writes the tile's {sum merit, organisms} into the
+ * 2-double device buffer dev_totals; after the caller sums it over ranks
+ * (RCCL all-reduce, stream-ordered), avgpu_update_run allots
+ * AVE_TIME_SLICE * N_global instructions in proportion to merit / global merit. */
+int avgpu_update_totals(avgpu_world* w, double* dev_totals);
+int avgpu_update_run(avgpu_world* w, const double* dev_totals, avgpu_update_stats* out);
+/* Run the handle's work on an external HIP stream (e.g. the framework's
+ * current stream, so that collectives order against it). NULL restores the
+ * handle's own stream. */
+int avgpu_set_stream(avgpu_world* w, void* hip_stream);
 
 /* ---- inspection (cHardwareBase inspection API, cpu/cHardwareBase.h:145-200) */
 int avgpu_get_states(avgpu_world* w, int64_t first_cell, int64_t count,
@@ -314,8 +330,9 @@ int64_t avgpu_halo_record_bytes(void);
 
 /* counters of the last avgpu_step: instructions executed (sum over lanes) */
 int avgpu_last_step_insts(avgpu_world* w, int64_t* insts);
-/* kernel timing of the dominant interpreter kernel in the last call
- * (HIP events on the handle's stream), milliseconds summed over launches */
+/* Interpreter-kernel time (HIP events recorded on the handle's stream around
+ * every k_interpret launch sequence) accumulated since the previous call:
+ * total milliseconds and number of interpret phases; resets the accumulator. */
 int avgpu_last_kernel_ms(avgpu_world* w, double* ms, int64_t* launches);
 
 #ifdef __cplusplus

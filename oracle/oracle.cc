@@ -195,6 +195,7 @@ struct World {
   // batch world
   std::vector<Birth> births;
   int64_t update = 0;
+  int64_t cum_insts = 0, cum_births = 0;
   avgpu_update_stats stats;
   int64_t step_insts = 0;
   // multi-GPU style overrides (unused by the oracle tests unless set)
@@ -380,25 +381,27 @@ struct Exec {
     }
   }
 
-  // Divide_CheckViable (cpu/cHardwareBase.cc:140-289 + main/cOrganism.cc:788-919)
+  // Divide_CheckViable (cpu/cHardwareBase.cc:140-289 + main/cOrganism.cc:788-919);
+  // ORG_FAULT is gated by ctx.OrgFaultReporting(), off by default
+  // (main/cAvidaContext.h:45), so these failures do not count errors.
   bool check_viable(int parent_size, int child_size, int* exe_out, int* copied_out) {
     const int genome_size = (int)o.genome.size();
     const double range = w.cfg.offspring_size_range;
     const int min_size = std::max(AVGPU_MIN_GENOME, (int)(genome_size / range));
     const int max_size = std::min(AVGPU_MAX_GENOME, (int)(genome_size * range));
-    if (child_size < min_size || child_size > max_size) { o.errors++; return false; }
-    if (parent_size < min_size || parent_size > max_size) { o.errors++; return false; }
+    if (child_size < min_size || child_size > max_size) { return false; }
+    if (parent_size < min_size || parent_size > max_size) { return false; }
     const int ming = w.cfg.min_genome_size, maxg = w.cfg.max_genome_size;
-    if ((ming && child_size < ming) || (maxg && child_size > maxg)) { o.errors++; return false; }
-    if ((ming && parent_size < ming) || (maxg && parent_size > maxg)) { o.errors++; return false; }
+    if ((ming && child_size < ming) || (maxg && child_size > maxg)) { return false; }
+    if ((ming && parent_size < ming) || (maxg && parent_size > maxg)) { return false; }
     int executed = 0;
     for (int i = 0; i < parent_size; i++) if (o.flg[i] & F_EXECUTED) executed++;
     const int min_exe = (int)(parent_size * w.cfg.min_exe_lines);
-    if (executed < min_exe) { o.errors++; return false; }
+    if (executed < min_exe) { return false; }
     int copied = 0;
     for (int i = parent_size; i < parent_size + child_size; i++) if (o.flg[i] & F_COPIED) copied++;
     const int min_copied = (int)(child_size * w.cfg.min_copied_lines);
-    if (copied < min_copied) { o.errors++; return false; }
+    if (copied < min_copied) { return false; }
     // cOrganism::Divide_CheckViable
     if (o.cur_bonus < w.cfg.required_bonus) return false;
     double base = (double)calc_size_merit();
@@ -484,7 +487,7 @@ struct Exec {
     if (num_inputs < 2) { lo[2] = lo[0]; lo[3] = lo[1]; }
     if (num_inputs < 3) { lo[4] = lo[0]; lo[5] = lo[1]; lo[6] = lo[2]; lo[7] = lo[3]; }
     int id = 0;
-    for (int i = 0; i < 8; i++) id += lo[i] << i;
+    for (int i = 0; i < 8; i++) id += lo[i] * (1 << i);  // -1 entries contribute -2^i
     return id;
   }
   // Task_Not ... Task_Equ (main/cTaskLib.cc:511-575)
@@ -976,6 +979,8 @@ static int run_update_impl(World& w) {
       budget[c] = (int32_t)fl + (o.rng.p(th) ? 1 : 0);
     }
   }
+  int64_t slices = 0;
+  for (int64_t c = 0; c < w.ncells; c++) slices += budget[c] > 0;
   // 2. interpretation
   w.births.clear();
   int64_t insts = 0, deaths = 0, divides = 0;
@@ -1049,6 +1054,12 @@ static int run_update_impl(World& w) {
     for (int t = 0; t < AVGPU_MAX_REACTIONS; t++) if (o.last_task[t] > 0) st.task_orgs[t]++;
   }
   st.ave_generation = st.num_organisms ? gen / st.num_organisms : 0.0;
+  for (int64_t c = 0; c < w.ncells; c++) if (w.orgs[c].alive) st.sum_mem_size += (double)w.orgs[c].mem.size();
+  w.cum_insts += insts;
+  w.cum_births += placed;
+  st.cum_insts_executed = w.cum_insts;
+  st.cum_births = w.cum_births;
+  st.slices = slices;
   w.update++;
   return 0;
 }

@@ -1,0 +1,114 @@
+"""GPU parity: the HIP interpreter (through the C-ABI) against the CPU oracle
+and the reference's golden vectors.  Integer/byte state must match bit for bit;
+doubles (merit, bonus, fitness) must match exactly too, because both sides
+perform the same IEEE operations without contraction."""
+import os
+
+import pytest
+
+from avida_amd import capi, files
+import oracle_lib as ol
+import parity_util as pu
+
+pytestmark = pytest.mark.gpu
+CAP = capi.MAX_GENOME
+
+
+def _pair(golden, n, instset="instset-heads.cfg", overrides=None, seed=7):
+    iset, env, cfg = pu.load_env(golden, instset, overrides, seed)
+    return (ol.Backend("oracle", cfg, iset, env, ncells=n),
+            ol.Backend("gpu", cfg, iset, env, ncells=n), iset)
+
+
+def _run_compare(orc, gpu, n, chunks, mode=capi.MODE_FROZEN):
+    for budget in chunks:
+        orc.step(0, n, uniform=budget, mode=mode)
+        gpu.step(0, n, uniform=budget, mode=mode)
+        a, oa, fa = orc.states(0, n, CAP)
+        b, ob, fb = gpu.states(0, n, CAP)
+        bad = pu.diff_states(a, b, oa, ob, fa, fb, CAP)
+        assert not bad, f"{len(bad)} mismatches after budget {budget}: {bad[:5]}"
+
+
+def test_test_cpu_detail_recalc_on_gpu(golden):
+    """All 1794 golden genomes recalculated by the GPU test-CPU path."""
+    iset, env, cfg = pu.load_env(golden, "instset-classic.cfg")
+    gpu = ol.Backend("gpu", cfg, iset, env, ncells=16)
+    fmt, rows = files.parse_detail_dat(os.path.join(golden, "detail-recalc.dat"))
+    genomes = [iset.parse_sequence(r[8]) for r in rows]
+    res = ol.recalculate(gpu, genomes)
+    bad = []
+    for row, (r, flags, viable) in zip(rows, res):
+        got = [int(viable), r.copied_size, r.executed_size, "%g" % r.merit, r.gestation_time,
+               flags, [int(x) for x in list(r.task_count)[:9]]]
+        exp = [int(row[10]), int(row[11]), int(row[12]), "%g" % float(row[13]), int(row[15]),
+               row[19], [int(x) for x in row[20:29]]]
+        if got != exp:
+            bad.append((row[0], exp, got))
+    assert not bad, f"{len(bad)} mismatches: {bad[:3]}"
+
+
+@pytest.mark.parametrize("death", [0, 2])
+def test_frozen_population_config2(golden, death):
+    """BASELINE config 2: frozen 3600-organism population, mutations off,
+    10^4 instructions per organism; per-lane state compared after every chunk."""
+    iset_c = files.read_instset(os.path.join(golden, "instset-classic.cfg"))
+    genomes = pu.pop_genomes(golden, iset_c)
+    anc = files.read_org(os.path.join(golden, "default-heads.org"),
+                         files.read_instset(os.path.join(golden, "instset-heads.cfg")))
+    # the ancestor re-expressed in classic op codes
+    heads = files.read_instset(os.path.join(golden, "instset-heads.cfg"))
+    anc_c = bytes(iset_c.op_of_name(heads.names[o]) for o in anc)
+    genomes = genomes[:3599] + [anc_c]
+    n = len(genomes)
+    assert n == 3600
+    ov = {"COPY_MUT_PROB": 0.0, "DIVIDE_INS_PROB": 0.0, "DIVIDE_DEL_PROB": 0.0,
+          "DEATH_METHOD": death}
+    orc, gpu, iset = _pair(golden, n, "instset-classic.cfg", ov)
+    orc.set_orgs(0, genomes, deterministic=False)
+    gpu.set_orgs(0, genomes, deterministic=False)
+    _run_compare(orc, gpu, n, [1, 29, 970, 3000, 6000])
+
+
+def test_random_genomes_fuzz(golden):
+    """Random genomes 8..2048 sites (all LDS size classes, spills, faults)."""
+    orc, gpu, iset = _pair(golden, 512, overrides={"DEATH_METHOD": 0})
+    g = pu.random_genomes(iset, 384, 8, 300, seed=11) + pu.random_genomes(iset, 128, 300, 2048, seed=12)
+    orc.set_orgs(0, g, deterministic=False)
+    gpu.set_orgs(0, g, deterministic=False)
+    _run_compare(orc, gpu, len(g), [1, 7, 500, 1500])
+
+
+def test_ancestor_mutants_fuzz(golden):
+    """Point mutants of the ancestor with copy mutations ON (FROZEN mode draws
+    copy mutations from the per-organism counter stream on both sides)."""
+    orc, gpu, iset = _pair(golden, 1024, overrides={"DEATH_METHOD": 0, "COPY_MUT_PROB": 0.02})
+    anc = files.read_org(os.path.join(golden, "default-heads.org"), iset)
+    g = pu.mutants_of(anc, iset, 1024, rate=0.03, seed=5)
+    orc.set_orgs(0, g, deterministic=False)
+    gpu.set_orgs(0, g, deterministic=False)
+    _run_compare(orc, gpu, len(g), [250, 750, 2000])
+
+
+def test_world_updates_bit_exact(golden):
+    """Full batch-synchronous updates (allot, interpret with copy/divide
+    mutations, birth placement, activation) from one injected ancestor on a
+    60x60 torus: GPU world == oracle world, every cell, every field."""
+    iset, env, cfg = pu.load_env(golden, seed=101)
+    n = cfg.world_x * cfg.world_y
+    orc = ol.Backend("oracle", cfg, iset, env, ncells=n)
+    gpu = ol.Backend("gpu", cfg, iset, env, ncells=n)
+    anc = files.read_org(os.path.join(golden, "default-heads.org"), iset)
+    center = (cfg.world_y // 2) * cfg.world_x + cfg.world_x // 2
+    for b in (orc, gpu):
+        b.set_orgs(center, [anc], deterministic=False)
+    for upd in range(150):
+        so = orc.run_update()
+        sg = gpu.run_update()
+        for f in ("num_organisms", "insts_executed", "births", "deaths", "divides"):
+            assert getattr(so, f) == getattr(sg, f), (upd, f, getattr(so, f), getattr(sg, f))
+    a, oa, fa = orc.states(0, n, CAP)
+    b, ob, fb = gpu.states(0, n, CAP)
+    bad = pu.diff_states(a, b, oa, ob, fa, fb, CAP)
+    assert not bad, f"{len(bad)} mismatches: {bad[:5]}"
+    assert so.num_organisms > 100

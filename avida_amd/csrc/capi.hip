@@ -93,7 +93,7 @@ int setup_world(avgpu_world* w, int64_t n, bool test_buffers) {
   A(cur_react, AVGPU_MAX_REACTIONS * n);
   A(cur_bonus, n); A(merit, n); A(fitness, n); A(credit, n); A(gest_time, n); A(num_div, n);
   A(generation, n); A(copied, n); A(child_copied, n); A(executed, n); A(errors, n);
-  A(class_list, NUM_CLASSES * n); A(class_count, NUM_CLASSES); A(counters, 16);
+  A(class_list, NUM_CLASSES * n); A(class_count, NUM_CLASSES); A(counters, CNT_WORDS);
   W.bcap = test_buffers ? 16 : std::max<int64_t>(4096, n / 2);
   A(b_count, 1); A(b_parent, W.bcap); A(b_seq, W.bcap); A(b_len, W.bcap); A(b_merit, W.bcap);
   A(b_fitness, W.bcap); A(b_gen, W.bcap); A(b_ccopied, W.bcap); A(b_exec, W.bcap);
@@ -284,13 +284,13 @@ int drain_ring(avgpu_world* w, int keep) {
   return 0;
 }
 
-int interpret(avgpu_world* w, int mode, int64_t max_lanes) {
+int interpret(avgpu_world* w, int mode, int64_t first, int64_t count) {
   int launches = 0;
   int rc = drain_ring(w, avgpu_world::RING - 1);
   if (rc < 0) return rc;
   const int i = w->ring_head;
   HIPCHK(hipEventRecord(w->ring0[i], w->stream));
-  launch_interpret_classes(w->W, mode, w->stream, max_lanes, nullptr, &launches);
+  launch_interpret_classes(w->W, mode, w->stream, first, count, &launches);
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(w->ring1[i], w->stream));
   w->ring_head = (i + 1) % avgpu_world::RING;
@@ -443,11 +443,11 @@ int avgpu_step(avgpu_world* w, int64_t first, int64_t count, const int32_t* budg
     HIPCHK(hipMalloc(&d_b, count * sizeof(int32_t)));
     HIPCHK(hipMemcpyAsync(d_b, budget, count * sizeof(int32_t), hipMemcpyHostToDevice, w->stream));
   }
-  HIPCHK(hipMemsetAsync(w->W.counters, 0, CNT_PER_UPDATE * sizeof(unsigned long long), w->stream));
+  HIPCHK(hipMemsetAsync(w->W.counters, 0, NSHARD * CNT_STRIDE * sizeof(unsigned long long), w->stream));
   HIPCHK(hipMemsetAsync(w->W.b_count, 0, sizeof(int32_t), w->stream));
   launch_classify_uniform(w->W, w->stream, first, count, d_b, budget_uniform);
   HIPCHK(hipGetLastError());
-  rc = interpret(w, mode, count);
+  rc = interpret(w, mode, first, count);
   if (d_b) { hipStreamSynchronize(w->stream); hipFree(d_b); }
   return rc;
 }
@@ -467,7 +467,7 @@ int avgpu_update_run(avgpu_world* w, const double* dev_totals, avgpu_update_stat
   if (!dev_totals) return fail(AVGPU_EINVAL, "dev_totals is NULL");
   launch_world_pre(w->W, w->stream, dev_totals);
   HIPCHK(hipGetLastError());
-  rc = interpret(w, AVGPU_MODE_WORLD, w->W.n);
+  rc = interpret(w, AVGPU_MODE_WORLD, 0, w->W.n);
   if (rc < 0) return rc;
   launch_world_post(w->W, w->stream, w->d_stats);
   HIPCHK(hipGetLastError());
@@ -663,10 +663,12 @@ int64_t avgpu_halo_record_bytes(void) { return 0; }
 
 int avgpu_last_step_insts(avgpu_world* w, int64_t* insts) {
   if (!w || !insts) return fail(AVGPU_EINVAL, "args");
-  unsigned long long v = 0;
-  HIPCHK(hipMemcpyAsync(&v, w->W.counters + CNT_INSTS, 8, hipMemcpyDeviceToHost, w->stream));
+  std::vector<unsigned long long> v(NSHARD * CNT_STRIDE);
+  HIPCHK(hipMemcpyAsync(v.data(), w->W.counters, v.size() * 8, hipMemcpyDeviceToHost, w->stream));
   HIPCHK(hipStreamSynchronize(w->stream));
-  *insts = (int64_t)v;
+  unsigned long long s = 0;
+  for (int sh = 0; sh < NSHARD; sh++) s += v[sh * CNT_STRIDE + CNT_INSTS];
+  *insts = (int64_t)s;
   return 0;
 }
 

@@ -139,9 +139,14 @@ struct DevWorld {
 #define CNT_DROPPED 4
 #define CNT_SPILLS 5
 #define CNT_SLICES 6
-#define CNT_PER_UPDATE 8      /* slots [0, 8) are reset every update */
-#define CNT_CUM_INSTS 8
-#define CNT_CUM_BIRTHS 9
+// Counters are sharded over NSHARD cache lines (16 x u64 = 128 B each) so that
+// the per-wave adds of a 16K-wave launch do not serialise on one L2 address;
+// counters[NSHARD*16 + k] hold the cumulative totals.
+#define NSHARD 64
+#define CNT_STRIDE 16
+#define CNT_WORDS (NSHARD * CNT_STRIDE + CNT_STRIDE)
+#define CNT_CUM_INSTS (NSHARD * CNT_STRIDE + 0)
+#define CNT_CUM_BIRTHS (NSHARD * CNT_STRIDE + 1)
 
 // ---------------------------------------------------------------------------
 // RNG spec: identical arithmetic to the oracle's Stream.
@@ -198,6 +203,23 @@ __device__ __forceinline__ int calc_size_merit(const DevWorld& W, int glen, int 
   }
 }
 
+__device__ __forceinline__ void count_add(const DevWorld& W, int slot, unsigned long long v) {
+  atomicAdd(&W.counters[(blockIdx.x & (NSHARD - 1)) * CNT_STRIDE + slot], v);
+}
+
+// LDS size classes of k_interpret (bytes of tape per lane)
+#define CLASS0_SIZE 384
+__device__ __forceinline__ int class_of(int need) {
+  return need <= CLASS0_SIZE ? 0 : (need <= 768 ? 1 : (need <= 1536 ? 2 : 3));
+}
+// tape capacity an organism may need this slice: its memory, or the size
+// h-alloc would grow it to when it has not allocated yet
+__device__ __forceinline__ int need_of(int m, uint32_t ctl, double size_range) {
+  if (ctl & CTL_MAL) return m;
+  const int grown = m + min((int)(size_range * m), AVGPU_MAX_GENOME - m);
+  return grown > m ? grown : m;
+}
+
 // ---------------------------------------------------------------------------
 // host-side launchers (defined next to their kernels)
 struct LaunchInfo {
@@ -206,8 +228,9 @@ struct LaunchInfo {
   bool timed;
 };
 
-void launch_interpret_classes(const DevWorld& W, int mode, hipStream_t s, int64_t max_lanes,
-                              float* kernel_ms, int* launches);
+// class 0 runs densely over cells [first, first+count); classes 1..3 over their lists
+void launch_interpret_classes(const DevWorld& W, int mode, hipStream_t s, int64_t first,
+                              int64_t count, int* launches);
 void launch_world_pre(const DevWorld& W, hipStream_t s, const double* d_totals);
 void launch_world_post(const DevWorld& W, hipStream_t s, double* d_stats);
 void launch_classify_uniform(const DevWorld& W, hipStream_t s, int64_t first, int64_t count,

@@ -20,26 +20,45 @@
 namespace {
 
 template <int S>
-__global__ __launch_bounds__(64) void k_interpret(DevWorld W, int cls, int mode) {
+__global__ __launch_bounds__(64) void k_interpret(DevWorld W, int cls, int mode, int64_t first,
+                                                  int64_t count) {
   constexpr int STRIDE = S + 4;
   __shared__ uint32_t lds32[64 * STRIDE / 4];
   uint8_t* lds = reinterpret_cast<uint8_t*>(lds32);
 
   const int lane = threadIdx.x;
-  const int count = W.class_count[cls];
-  const int base = blockIdx.x * 64;
-  if (base >= count) return;
   const int64_t N = W.n;
-  const int idx = base + lane;
-  const bool active = idx < count;
-  const int cell = active ? W.class_list[(int64_t)cls * N + idx] : -1;
-  int M = active ? W.mem_size[cell] : 0;
+  int cell = -1;
+  int M = 0;
+  if (cls == 0) {
+    // dense sweep in cell order: coalesced hot-state loads, no list
+    const int64_t c = first + (int64_t)blockIdx.x * 64 + lane;
+    if (c < first + count) {
+      const uint32_t c0 = W.ctl[c];
+      const int m0 = W.mem_size[c];
+      if ((c0 & CTL_ALIVE) && W.budget[c] > 0 && class_of(need_of(m0, c0, W.size_range)) == 0) {
+        cell = (int)c;
+        M = m0;
+      }
+    }
+  } else {
+    const int lcount = W.class_count[cls];
+    const int base = blockIdx.x * 64;
+    if (base >= lcount) return;
+    const int idx = base + lane;
+    if (idx < lcount) {
+      cell = W.class_list[(int64_t)cls * N + idx];
+      M = W.mem_size[cell];
+    }
+  }
+  const bool active = cell >= 0;
+  if (!__any(active)) return;
 
-  // ---- stage the 64 tapes into LDS (each tape copied by the whole wave) ----
+  // ---- stage the tapes into LDS (each tape copied by the whole wave) ----
   for (int j = 0; j < 64; j++) {
     const int c = __shfl(cell, j);
     const int m = __shfl(M, j);
-    if (c < 0) break;
+    if (c < 0) continue;
     const uint32_t* src = reinterpret_cast<const uint32_t*>(W.tape + (int64_t)c * TAPE_SLOT);
     uint32_t* dst = lds32 + j * (STRIDE / 4);
     const int words = (m + 3) >> 2;
@@ -346,7 +365,7 @@ __global__ __launch_bounds__(64) void k_interpret(DevWorld W, int cls, int mode)
             W.b_state[slot] = 0;
             W.b_target[slot] = -1;
           } else {
-            atomicAdd(&W.counters[CNT_DROPPED], 1ull);
+            count_add(W, CNT_DROPPED, 1ull);
           }
         }
         divides++;
@@ -477,14 +496,14 @@ __global__ __launch_bounds__(64) void k_interpret(DevWorld W, int cls, int mode)
     if (spill) {
       const int slot = atomicAdd(&W.class_count[cls + 1], 1);
       W.class_list[(int64_t)(cls + 1) * N + slot] = cell;
-      atomicAdd(&W.counters[CNT_SPILLS], 1ull);
+      count_add(W, CNT_SPILLS, 1ull);
     }
   }
   __syncthreads();
   for (int j = 0; j < 64; j++) {
     const int c = __shfl(cell, j);
     const int m = __shfl(M, j);
-    if (c < 0) break;
+    if (c < 0) continue;
     uint32_t* dst = reinterpret_cast<uint32_t*>(W.tape + (int64_t)c * TAPE_SLOT);
     const uint32_t* src = lds32 + j * (STRIDE / 4);
     const int words = (m + 3) >> 2;
@@ -500,29 +519,21 @@ __global__ __launch_bounds__(64) void k_interpret(DevWorld W, int cls, int mode)
     dv += __shfl_down(dv, off);
   }
   if (lane == 0) {
-    atomicAdd(&W.counters[CNT_INSTS], e);
-    if (dead) atomicAdd(&W.counters[CNT_DEATHS], (unsigned long long)dead);
-    if (dv) atomicAdd(&W.counters[CNT_DIVIDES], (unsigned long long)dv);
+    count_add(W, CNT_INSTS, e);
+    if (dead) count_add(W, CNT_DEATHS, (unsigned long long)dead);
+    if (dv) count_add(W, CNT_DIVIDES, (unsigned long long)dv);
   }
 }
 
 }  // namespace
 
-static const int kClassSize[NUM_CLASSES] = {384, 768, 1536, 2048};
-
-void launch_interpret_classes(const DevWorld& W, int mode, hipStream_t s, int64_t max_lanes,
-                              float* kernel_ms, int* launches) {
-  const unsigned blocks = (unsigned)((max_lanes + 63) / 64);
+void launch_interpret_classes(const DevWorld& W, int mode, hipStream_t s, int64_t first,
+                              int64_t count, int* launches) {
+  const unsigned blocks = (unsigned)((count + 63) / 64);
   if (blocks == 0) return;
-  for (int cls = 0; cls < NUM_CLASSES; cls++) {
-    switch (cls) {
-      case 0: hipLaunchKernelGGL(k_interpret<384>, dim3(blocks), dim3(64), 0, s, W, cls, mode); break;
-      case 1: hipLaunchKernelGGL(k_interpret<768>, dim3(blocks), dim3(64), 0, s, W, cls, mode); break;
-      case 2: hipLaunchKernelGGL(k_interpret<1536>, dim3(blocks), dim3(64), 0, s, W, cls, mode); break;
-      default: hipLaunchKernelGGL(k_interpret<2048>, dim3(blocks), dim3(64), 0, s, W, cls, mode); break;
-    }
-    if (launches) (*launches)++;
-  }
-  (void)kernel_ms;
-  (void)kClassSize;
+  hipLaunchKernelGGL(k_interpret<CLASS0_SIZE>, dim3(blocks), dim3(64), 0, s, W, 0, mode, first, count);
+  hipLaunchKernelGGL(k_interpret<768>, dim3(blocks), dim3(64), 0, s, W, 1, mode, first, count);
+  hipLaunchKernelGGL(k_interpret<1536>, dim3(blocks), dim3(64), 0, s, W, 2, mode, first, count);
+  hipLaunchKernelGGL(k_interpret<2048>, dim3(blocks), dim3(64), 0, s, W, 3, mode, first, count);
+  if (launches) *launches += 4;
 }

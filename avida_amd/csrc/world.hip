@@ -14,13 +14,10 @@
 
 namespace {
 
-__device__ __forceinline__ int class_of(int need) {
-  return need <= 384 ? 0 : (need <= 768 ? 1 : (need <= 1536 ? 2 : 3));
-}
-
 // Append `cell` to its size-class list (wave-aggregated atomics per class).
+// Class 0 is not listed: k_interpret<CLASS0_SIZE> sweeps the cells densely.
 __device__ __forceinline__ void enqueue_class(const DevWorld& W, int cell, bool want, int cls) {
-  for (int k = 0; k < NUM_CLASSES; k++) {
+  for (int k = 1; k < NUM_CLASSES; k++) {
     const bool mine = want && cls == k;
     const unsigned long long mask = __ballot(mine);
     if (!mask) continue;
@@ -36,11 +33,8 @@ __device__ __forceinline__ void enqueue_class(const DevWorld& W, int cell, bool 
   }
 }
 
-__device__ __forceinline__ int need_of(const DevWorld& W, int cell) {
-  const int m = W.mem_size[cell];
-  if (W.ctl[cell] & CTL_MAL) return m;
-  const int grown = m + min((int)(W.size_range * m), AVGPU_MAX_GENOME - m);
-  return grown > m ? grown : m;
+__device__ __forceinline__ int need_of_cell(const DevWorld& W, int cell) {
+  return ::need_of(W.mem_size[cell], W.ctl[cell], W.size_range);
 }
 
 // ---------------------------------------------------------------------------
@@ -170,7 +164,7 @@ __global__ void k_classify_uniform(DevWorld W, int64_t first, int64_t count, con
     b = budget ? budget[i] : uniform;
     W.budget[cell] = b;
     want = (W.ctl[cell] & CTL_ALIVE) && b > 0;
-    if (want) cls = class_of(need_of(W, cell));
+    if (want) cls = class_of(need_of_cell(W, cell));
   }
   enqueue_class(W, cell, want, cls);
 }
@@ -194,28 +188,35 @@ __global__ __launch_bounds__(256) void k_merit_partial(DevWorld W, double* parti
   if (threadIdx.x == 0) { partial[blockIdx.x] = s[0]; alive_partial[blockIdx.x] = a[0]; }
 }
 
-// totals[0] = sum merit (block partials added in order), totals[1] = alive count
+// totals[0] = sum merit, totals[1] = alive count.  Lane t sums partials
+// t, t+256, ... in order, then the fixed pairwise tree (oracle: tree_merit_sum).
 __global__ __launch_bounds__(256) void k_merit_final(const double* partial, const int32_t* alive_partial,
                                                      int64_t nb, double* totals, int use_global) {
   __shared__ double s[256];
   __shared__ long long cnt[256];
-  // counts: any order (integers)
   long long c = 0;
-  for (int64_t b = threadIdx.x; b < nb; b += 256) c += alive_partial[b];
-  cnt[threadIdx.x] = c;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    long long tc = 0;
-    for (int i = 0; i < 256; i++) tc += cnt[i];
-    if (!use_global) {
-      double t = 0.0;
-      for (int64_t b = 0; b < nb; b++) t = __dadd_rn(t, partial[b]);
-      totals[0] = t;
-      totals[1] = (double)tc;
-    }
-    totals[2] = (double)tc;  // local organisms
+  double acc = 0.0;
+  for (int64_t b = threadIdx.x; b < nb; b += 256) {
+    c += alive_partial[b];
+    acc = __dadd_rn(acc, partial[b]);
   }
-  (void)s;
+  cnt[threadIdx.x] = c;
+  s[threadIdx.x] = acc;
+  __syncthreads();
+  for (int stride = 128; stride >= 1; stride >>= 1) {
+    if ((int)threadIdx.x < stride) {
+      s[threadIdx.x] = __dadd_rn(s[threadIdx.x], s[threadIdx.x + stride]);
+      cnt[threadIdx.x] += cnt[threadIdx.x + stride];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    if (!use_global) {
+      totals[0] = s[0];
+      totals[1] = (double)cnt[0];
+    }
+    totals[2] = (double)cnt[0];  // local organisms
+  }
 }
 
 // cScheduler restated (DESIGN.md "Scheduler"): lambda = UD * merit / total
@@ -250,12 +251,12 @@ __global__ void k_allot(DevWorld W, const double* totals) {
         }
       }
       want = b > 0;
-      if (want) cls = class_of(need_of(W, (int)c));
+      if (want) cls = class_of(need_of_cell(W, (int)c));
     }
     W.budget[c] = b;
   }
   const unsigned long long m = __ballot(want);
-  if ((threadIdx.x & 63) == 0 && m) atomicAdd(&W.counters[CNT_SLICES], (unsigned long long)__popcll(m));
+  if ((threadIdx.x & 63) == 0 && m) count_add(W, CNT_SLICES, (unsigned long long)__popcll(m));
   enqueue_class(W, (int)c, want, cls);
 }
 
@@ -336,57 +337,78 @@ __global__ void k_place_clear(DevWorld W) {
 // One wave per birth: the genome copy is coalesced across the wave.
 __global__ __launch_bounds__(64) void k_activate(DevWorld W) {
   const int nb = min(*W.b_count, (int)W.bcap);
-  for (int64_t i = blockIdx.x; i < nb; i += gridDim.x) {
   const int lane = threadIdx.x;
-  const int tgt = W.b_target[i];
-  const bool won = W.b_state[i] == 1 && tgt >= 0 && W.owner[tgt] == (int)i;
-  if (!won) {
-    if (lane == 0) atomicAdd(&W.counters[CNT_DROPPED], 1ull);
-    continue;
-  }
   const int64_t N = W.n;
-  const int64_t c = W.b_target[i];
-  const int len = W.b_len[i];
-  const uint32_t* src = reinterpret_cast<const uint32_t*>(W.b_genome + i * TAPE_SLOT);
-  uint32_t* dst = reinterpret_cast<uint32_t*>(W.tape + c * TAPE_SLOT);
-  for (int w = lane; w < (len + 3) / 4; w += 64) dst[w] = src[w];
-  if (lane < 2 * AVGPU_STACK_SIZE) W.stack[lane * N + c] = 0;
-  if (lane < AVGPU_MAX_REACTIONS) {
-    W.cur_task[lane * N + c] = 0; W.last_task[lane * N + c] = 0; W.cur_react[lane * N + c] = 0;
+  unsigned long long born = 0, lost = 0;
+  for (int64_t i = blockIdx.x; i < nb; i += gridDim.x) {
+    const int tgt = W.b_target[i];
+    const bool won = W.b_state[i] == 1 && tgt >= 0 && W.owner[tgt] == (int)i;
+    if (!won) { lost++; continue; }
+    born++;
+    const int64_t c = tgt;
+    const int len = W.b_len[i];
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(W.b_genome + i * TAPE_SLOT);
+    uint32_t* dst = reinterpret_cast<uint32_t*>(W.tape + c * TAPE_SLOT);
+    for (int w = lane; w < (len + 3) / 4; w += 64) dst[w] = src[w];
+    // one store per lane: the organism's fields are scattered over SoA rows
+    if (lane < 2 * AVGPU_STACK_SIZE) W.stack[lane * N + c] = 0;
+    if (lane < AVGPU_MAX_REACTIONS) {
+      W.cur_task[lane * N + c] = 0; W.last_task[lane * N + c] = 0; W.cur_react[lane * N + c] = 0;
+    }
+    switch (lane) {
+      case 20: W.reg[c] = 0; break;
+      case 21: W.reg[N + c] = 0; break;
+      case 22: W.reg[2 * N + c] = 0; break;
+      case 23: W.inbuf[c] = 0; break;
+      case 24: W.inbuf[N + c] = 0; break;
+      case 25: W.inbuf[2 * N + c] = 0; break;
+      case 26: W.head[c] = 0; break;
+      case 27: W.head[N + c] = 0; break;
+      case 28: W.head[2 * N + c] = 0; break;
+      case 29: W.head[3 * N + c] = 0; break;
+      case 30: W.ctl[c] = CTL_ALIVE; break;
+      case 31: W.rlabel[c] = 0; break;
+      case 32: W.mem_size[c] = len; break;
+      case 33: W.cycles[c] = 0; break;
+      case 34: W.time_used[c] = 0; break;
+      case 35: W.gest_start[c] = 0; break;
+      case 36: {
+        int mx = 0;
+        if (W.death_method > 0) { mx = W.age_limit; if (W.death_method == 2) mx *= len; if (mx < 1) mx = 1; }
+        W.max_exec[c] = mx;
+        break; }
+      case 37: W.birth_len[c] = len; break;
+      case 38: W.budget[c] = 0; break;
+      case 39: W.in_total[c] = 0; break;
+      case 40: W.in_ptr[c] = 0; break;
+      case 41: W.outbuf[c] = 0; break;
+      case 42: W.out_total[c] = 0; break;
+      case 43: W.cur_bonus[c] = W.default_bonus; break;
+      case 44: W.merit[c] = W.b_merit[i]; break;
+      case 45: W.fitness[c] = W.b_fitness[i]; break;
+      case 46: W.credit[c] = 0.0; break;
+      case 47: W.gest_time[c] = W.b_gest[i]; break;
+      case 48: W.num_div[c] = 0; break;
+      case 49: W.generation[c] = W.b_gen[i]; break;
+      case 50: W.copied[c] = W.b_ccopied[i]; break;
+      case 51: W.child_copied[c] = 0; break;
+      case 52: W.executed[c] = W.b_exec[i]; break;
+      case 53: W.errors[c] = 0; break;
+      case 54: {
+        const uint32_t lo = W.b_rng[i], hi = W.b_rng[W.bcap + i];
+        uint32_t ctr = W.b_rng[2 * W.bcap + i];
+        // cEnvironment::SetupInputs random (main/cEnvironment.cc:1268-1271)
+        W.inputs[c] = (15 << 24) + (int)rng_below(lo, hi, ctr, 1u << 24);
+        W.inputs[N + c] = (51 << 24) + (int)rng_below(lo, hi, ctr, 1u << 24);
+        W.inputs[2 * N + c] = (85 << 24) + (int)rng_below(lo, hi, ctr, 1u << 24);
+        W.rng[c] = lo; W.rng[N + c] = hi; W.rng[2 * N + c] = ctr;
+        break; }
+      default: break;
+    }
   }
-  if (lane < 3) { W.reg[lane * N + c] = 0; W.inbuf[lane * N + c] = 0; }
-  if (lane < 4) W.head[lane * N + c] = 0;
   if (lane == 0) {
-    W.ctl[c] = CTL_ALIVE;
-    W.rlabel[c] = 0;
-    W.mem_size[c] = len;
-    W.cycles[c] = 0; W.time_used[c] = 0; W.gest_start[c] = 0;
-    int mx = 0;
-    if (W.death_method > 0) { mx = W.age_limit; if (W.death_method == 2) mx *= len; if (mx < 1) mx = 1; }
-    W.max_exec[c] = mx;
-    W.birth_len[c] = len;
-    const uint32_t lo = W.b_rng[i], hi = W.b_rng[W.bcap + i];
-    uint32_t ctr = W.b_rng[2 * W.bcap + i];
-    // cEnvironment::SetupInputs random (main/cEnvironment.cc:1268-1271)
-    W.inputs[c] = (15 << 24) + (int)rng_below(lo, hi, ctr, 1u << 24);
-    W.inputs[N + c] = (51 << 24) + (int)rng_below(lo, hi, ctr, 1u << 24);
-    W.inputs[2 * N + c] = (85 << 24) + (int)rng_below(lo, hi, ctr, 1u << 24);
-    W.rng[c] = lo; W.rng[N + c] = hi; W.rng[2 * N + c] = ctr;
-    W.budget[c] = 0;
-    W.in_total[c] = 0; W.in_ptr[c] = 0; W.outbuf[c] = 0; W.out_total[c] = 0;
-    W.cur_bonus[c] = W.default_bonus;
-    W.merit[c] = W.b_merit[i];
-    W.fitness[c] = W.b_fitness[i];
-    W.credit[c] = 0.0;
-    W.gest_time[c] = W.b_gest[i];
-    W.num_div[c] = 0;
-    W.generation[c] = W.b_gen[i];
-    W.copied[c] = W.b_ccopied[i];
-    W.child_copied[c] = 0;
-    W.executed[c] = W.b_exec[i];
-    W.errors[c] = 0;
-    atomicAdd(&W.counters[CNT_BIRTHS], 1ull);
-  }
+    if (born) count_add(W, CNT_BIRTHS, born);
+    if (lost) count_add(W, CNT_DROPPED, lost);
   }
 }
 
@@ -426,29 +448,40 @@ __global__ __launch_bounds__(256) void k_stats_partial(DevWorld W, double* part)
 
 // out: [0..23] partial sums, 24 insts 25 deaths 26 divides 27 births 28 dropped
 // 29 spills 30 cumulative insts 31 cumulative births 32 slices
-__global__ __launch_bounds__(64) void k_stats_final(DevWorld W, const double* part, int64_t nb,
-                                                    double* out) {
-  const int k = threadIdx.x;
-  if (k < NPART) {
+__global__ __launch_bounds__(256) void k_stats_final(DevWorld W, const double* part, int64_t nb,
+                                                     double* out) {
+  __shared__ double s[256];
+  const int tid = threadIdx.x;
+  for (int k = 0; k < NPART; k++) {
     double acc = 0.0;
-    for (int64_t b = 0; b < nb; b++) {
+    for (int64_t b = tid; b < nb; b += 256) {
       const double o = part[b * NPART + k];
       acc = (k == 5) ? fmax(acc, o) : acc + o;
     }
-    out[k] = acc;
+    s[tid] = acc;
+    __syncthreads();
+    for (int stride = 128; stride >= 1; stride >>= 1) {
+      if (tid < stride) s[tid] = (k == 5) ? fmax(s[tid], s[tid + stride]) : s[tid] + s[tid + stride];
+      __syncthreads();
+    }
+    if (tid == 0) out[k] = s[0];
+    __syncthreads();
   }
-  if (k == 0) {
-    W.counters[CNT_CUM_INSTS] += W.counters[CNT_INSTS];
-    W.counters[CNT_CUM_BIRTHS] += W.counters[CNT_BIRTHS];
-    out[24] = (double)W.counters[CNT_INSTS];
-    out[25] = (double)W.counters[CNT_DEATHS];
-    out[26] = (double)W.counters[CNT_DIVIDES];
-    out[27] = (double)W.counters[CNT_BIRTHS];
-    out[28] = (double)W.counters[CNT_DROPPED];
-    out[29] = (double)W.counters[CNT_SPILLS];
+  if (tid == 0) {
+    unsigned long long c[CNT_STRIDE] = {0};
+    for (int sh = 0; sh < NSHARD; sh++)
+      for (int k = 0; k < CNT_STRIDE; k++) c[k] += W.counters[sh * CNT_STRIDE + k];
+    W.counters[CNT_CUM_INSTS] += c[CNT_INSTS];
+    W.counters[CNT_CUM_BIRTHS] += c[CNT_BIRTHS];
+    out[24] = (double)c[CNT_INSTS];
+    out[25] = (double)c[CNT_DEATHS];
+    out[26] = (double)c[CNT_DIVIDES];
+    out[27] = (double)c[CNT_BIRTHS];
+    out[28] = (double)c[CNT_DROPPED];
+    out[29] = (double)c[CNT_SPILLS];
     out[30] = (double)W.counters[CNT_CUM_INSTS];
     out[31] = (double)W.counters[CNT_CUM_BIRTHS];
-    out[32] = (double)W.counters[CNT_SLICES];
+    out[32] = (double)c[CNT_SLICES];
   }
 }
 
@@ -487,7 +520,7 @@ void launch_merit_total(const DevWorld& W, hipStream_t s, double* totals, double
 }
 
 void launch_world_pre(const DevWorld& W, hipStream_t s, const double* totals) {
-  hipMemsetAsync(W.counters, 0, sizeof(unsigned long long) * CNT_PER_UPDATE, s);
+  hipMemsetAsync(W.counters, 0, sizeof(unsigned long long) * NSHARD * CNT_STRIDE, s);
   hipMemsetAsync(W.b_count, 0, sizeof(int32_t), s);
   hipMemsetAsync(W.class_count, 0, sizeof(int32_t) * NUM_CLASSES, s);
   hipLaunchKernelGGL(k_allot, dim3(nblk(W.n, 256)), dim3(256), 0, s, W, totals);
@@ -501,9 +534,9 @@ void launch_world_post(const DevWorld& W, hipStream_t s, double* stats) {
     hipLaunchKernelGGL(k_place_resolve, dim3(bb), dim3(256), 0, s, W);
     hipLaunchKernelGGL(k_place_clear, dim3(bb), dim3(256), 0, s, W);
   }
-  hipLaunchKernelGGL(k_activate, dim3(4096), dim3(64), 0, s, W);
+  hipLaunchKernelGGL(k_activate, dim3((unsigned)std::min<int64_t>(W.bcap, 32768)), dim3(64), 0, s, W);
   const int64_t nb = (W.n + 255) / 256;
   double* part = stats + NSTAT;
   hipLaunchKernelGGL(k_stats_partial, dim3((unsigned)nb), dim3(256), 0, s, W, part);
-  hipLaunchKernelGGL(k_stats_final, dim3(1), dim3(64), 0, s, W, part, nb, stats);
+  hipLaunchKernelGGL(k_stats_final, dim3(1), dim3(256), 0, s, W, part, nb, stats);
 }

@@ -40,7 +40,8 @@ def _pool(golden):
     iset = files.read_instset(os.path.join(golden, "instset-classic.cfg"))
     pool = []
     for g in files.read_pop(os.path.join(golden, "detail-50000.pop")):
-        pool.extend([iset.parse_sequence(g.sequence)] * g.num_cpus)
+        # cPopulation::LoadPopulation keeps the recorded merit (main/cPopulation.cc:6723-7000)
+        pool.extend([(iset.parse_sequence(g.sequence), g.merit)] * g.num_cpus)
     return iset, pool
 
 
@@ -64,11 +65,12 @@ def build_world(lib, capi, files, golden, side, seed, device, rank):
     capi.check(lib, lib.avgpu_load_instset(h, len(iset.names), hid, red))
     arr = capi.reactions_array(env)
     capi.check(lib, lib.avgpu_load_env(h, len(env), arr))
-    genomes = _genomes_for(n, pool, rank * 7919)
-    blob = b"".join(genomes)
+    picks = _genomes_for(n, pool, rank * 7919)
+    blob = b"".join(g for g, _ in picks)
     buf = (C.c_uint8 * len(blob)).from_buffer_copy(blob)
-    lens = (C.c_int32 * n)(*[len(g) for g in genomes])
-    capi.check(lib, lib.avgpu_set_orgs(h, 0, n, buf, lens, None, None, 0))
+    lens = (C.c_int32 * n)(*[len(g) for g, _ in picks])
+    merits = (C.c_double * n)(*[m for _, m in picks])
+    capi.check(lib, lib.avgpu_set_orgs(h, 0, n, buf, lens, merits, None, 0))
     return h, cfg, n
 
 
@@ -84,7 +86,8 @@ def cpu_baseline(golden, seconds):
     cfg = capi.cfg_from_avida(files.read_avida_cfg(None), seed=101)
     n = cfg.world_x * cfg.world_y
     b = ol.Backend("oracle", cfg, iset, env, ncells=n)
-    b.set_orgs(0, _genomes_for(n, pool, 0), deterministic=False)
+    picks = _genomes_for(n, pool, 0)
+    b.set_orgs(0, [g for g, _ in picks], merits=[m for _, m in picks], deterministic=False)
     st = capi.AvgpuUpdateStats()
     insts, updates = 0, 0
     t0 = time.perf_counter()

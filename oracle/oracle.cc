@@ -734,9 +734,11 @@ void dump_state(const World& w, const Org& o, avgpu_cpu_state* s, uint8_t* ops, 
 
 // Deterministic total merit: fixed 256-cell blocks, pairwise tree, then block
 // partials in order (the same order the device reduction uses).
+// Level 2: 256 lanes, lane t sums partials t, t+256, t+512, ... in order, then
+// the same pairwise tree over the 256 lane sums (DESIGN.md "Scheduler").
 double tree_merit_sum(const World& w, int64_t* n_alive) {
   int64_t nb = (w.ncells + 255) / 256;
-  double total = 0.0;
+  std::vector<double> part(nb);
   int64_t cnt = 0;
   for (int64_t b = 0; b < nb; b++) {
     double s[256];
@@ -747,10 +749,18 @@ double tree_merit_sum(const World& w, int64_t* n_alive) {
     }
     for (int stride = 128; stride >= 1; stride >>= 1)
       for (int i = 0; i < stride; i++) s[i] = s[i] + s[i + stride];
-    total = total + s[0];
+    part[b] = s[0];
   }
+  double lane[256];
+  for (int t = 0; t < 256; t++) {
+    double acc = 0.0;
+    for (int64_t b = t; b < nb; b += 256) acc = acc + part[b];
+    lane[t] = acc;
+  }
+  for (int stride = 128; stride >= 1; stride >>= 1)
+    for (int i = 0; i < stride; i++) lane[i] = lane[i] + lane[i + stride];
   *n_alive = cnt;
-  return total;
+  return lane[0];
 }
 
 // torus / grid neighbourhood (tools/cTopology.h:40-55 build_torus/build_grid),

@@ -25,6 +25,8 @@ def diff_states(a, b, ops_a, ops_b, fl_a, fl_b, cap):
     """Return a list of (index, field, a, b) mismatches; memory compared up to mem_size."""
     bad = []
     for i in range(len(a)):
+        if a[i].birth_length == 0 and b[i].birth_length == 0:
+            continue   # never-occupied cell: no organism, nothing to compare
         ta, tb = state_tuple(a[i]), state_tuple(b[i])
         for k in STATE_FIELDS:
             if ta[k] != tb[k]:

@@ -93,6 +93,7 @@ class AvgpuUpdateStats(C.Structure):
         ("sum_genome_length", C.c_double), ("max_fitness", C.c_double),
         ("ave_generation", C.c_double), ("sum_mem_size", C.c_double),
         ("cum_insts_executed", C.c_int64), ("cum_births", C.c_int64), ("slices", C.c_int64),
+        ("lane_steps", C.c_int64),
     ]
 
 

@@ -520,6 +520,7 @@ int avgpu_get_stats(avgpu_world* w, avgpu_update_stats* out) {
   out->cum_insts_executed = (int64_t)v[30];
   out->cum_births = (int64_t)v[31];
   out->slices = (int64_t)v[32];
+  out->lane_steps = (int64_t)v[33];
   return 0;
 }
 

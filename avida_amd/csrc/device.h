@@ -139,6 +139,7 @@ struct DevWorld {
 #define CNT_DROPPED 4
 #define CNT_SPILLS 5
 #define CNT_SLICES 6
+#define CNT_LANESTEPS 7   /* 64 x the longest lane of each wave: lane efficiency = insts / this */
 // Counters are sharded over NSHARD cache lines (16 x u64 = 128 B each) so that
 // the per-wave adds of a 16K-wave launch do not serialise on one L2 address;
 // counters[NSHARD*16 + k] hold the cumulative totals.

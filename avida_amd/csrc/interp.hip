@@ -4,11 +4,16 @@
 // cHardwareCPU::SingleProcess (targets/avida/Avida2Driver.cc:111-116,
 // main/cPopulation.cc:5698-5788, cpu/cHardwareCPU.cc:908-1058).
 //
-// One organism per wavefront lane; 64-thread workgroups (one wave each).  The
-// lane's memory tape is staged into LDS (S + 4 bytes per lane, the 4-byte pad
-// rotates lanes across banks), all architectural hot state lives in VGPRs, and
-// the cold state (stacks, IO buffers, task counters, bonus) is accessed in
-// place in HBM only by the instructions that use it.  Divide appends the
+// One organism per wavefront lane; 64-thread workgroups (one wave each).
+// On-chip state for the whole time slice:
+//   VGPRs : registers, heads, label, counters, RNG stream, IO buffers, cell
+//           inputs, merit bonus, task counts, fault count;
+//   LDS   : the memory tape (S + 4 bytes per lane; the 4-byte pad rotates
+//           lanes across banks), both 10-deep stacks ([row][lane], conflict
+//           free), and the block-shared tables (logic-id -> task mask,
+//           mutation weights).
+// HBM is touched only to stage state in/out, by h-divide (offspring, phenotype
+// reset) and by fire-and-forget reaction-count atomics.  Divide appends the
 // mutated offspring to a birth queue; IO runs the logic-9 task check fused.
 // Lanes whose next h-alloc would outgrow their LDS slot stop before it
 // ("spill") and are appended, with their remaining budget, to the next size
@@ -19,19 +24,44 @@
 
 namespace {
 
+// popcount of `bitmask`-selected flag bits over tape sites [from, to)
+__device__ __forceinline__ int count_flag(const uint8_t* T, int from, int to, uint32_t bit) {
+  const uint32_t* T32 = reinterpret_cast<const uint32_t*>(T);
+  const uint32_t m4 = bit * 0x01010101u;
+  int n = 0;
+  int i = from;
+  for (; i < to && (i & 3); i++) n += (T[i] & bit) ? 1 : 0;
+  const int wend = to >> 2;
+  int w = i >> 2;
+  for (; w + 4 <= wend; w += 4) {
+    const uint32_t a = T32[w], b = T32[w + 1], c = T32[w + 2], d = T32[w + 3];
+    n += __popc(a & m4) + __popc(b & m4) + __popc(c & m4) + __popc(d & m4);
+  }
+  for (; w < wend; w++) n += __popc(T32[w] & m4);
+  for (i = max(i, wend << 2); i < to; i++) n += (T[i] & bit) ? 1 : 0;
+  return n;
+}
+
 template <int S>
 __global__ __launch_bounds__(64) void k_interpret(DevWorld W, int cls, int mode, int64_t first,
                                                   int64_t count) {
   constexpr int STRIDE = S + 4;
-  __shared__ uint32_t lds32[64 * STRIDE / 4];
+  constexpr int TAPE_WORDS = 64 * STRIDE / 4;
+  constexpr int STK_WORDS = 2 * AVGPU_STACK_SIZE * 64;
+  // one __shared__ object: tapes | stacks | task LUT (256 x u16) | rand_cum (64 x i32) | rand_code (64 B)
+  __shared__ uint32_t lds32[TAPE_WORDS + STK_WORDS + 128 + 64 + 16];
   uint8_t* lds = reinterpret_cast<uint8_t*>(lds32);
+  int32_t* stk = reinterpret_cast<int32_t*>(lds32 + TAPE_WORDS);
+  const uint16_t* lut = reinterpret_cast<const uint16_t*>(lds32 + TAPE_WORDS + STK_WORDS);
+  const int32_t* rcum = reinterpret_cast<const int32_t*>(lds32 + TAPE_WORDS + STK_WORDS + 128);
+  const uint8_t* rcode = reinterpret_cast<const uint8_t*>(lds32 + TAPE_WORDS + STK_WORDS + 192);
 
   const int lane = threadIdx.x;
   const int64_t N = W.n;
   int cell = -1;
   int M = 0;
   if (cls == 0) {
-    // dense sweep in cell order: coalesced hot-state loads, no list
+    // dense sweep in cell order: coalesced state loads, no list
     const int64_t c = first + (int64_t)blockIdx.x * 64 + lane;
     if (c < first + count) {
       const uint32_t c0 = W.ctl[c];
@@ -54,24 +84,52 @@ __global__ __launch_bounds__(64) void k_interpret(DevWorld W, int cls, int mode,
   const bool active = cell >= 0;
   if (!__any(active)) return;
 
-  // ---- stage the tapes into LDS (each tape copied by the whole wave) ----
+  // ---- block-shared tables ----
+  {
+    uint32_t* l32 = lds32 + TAPE_WORDS + STK_WORDS;
+    const uint32_t* g_lut = reinterpret_cast<const uint32_t*>(W.task_lut);
+    l32[lane] = g_lut[lane];
+    l32[64 + lane] = g_lut[64 + lane];
+    l32[128 + lane] = (uint32_t)W.rand_cum[lane];
+    if (lane < 16) l32[192 + lane] = reinterpret_cast<const uint32_t*>(W.rand_code)[lane];
+  }
+  // ---- stage tapes and stacks into LDS by LDS-DMA (global_load_lds_dword:
+  // per-lane source, lane-linear destination); all copies are in flight
+  // together and retired by the single wait below ----
+  typedef __attribute__((address_space(3))) void* lds_ptr_t;
   for (int j = 0; j < 64; j++) {
     const int c = __shfl(cell, j);
     const int m = __shfl(M, j);
     if (c < 0) continue;
     const uint32_t* src = reinterpret_cast<const uint32_t*>(W.tape + (int64_t)c * TAPE_SLOT);
-    uint32_t* dst = lds32 + j * (STRIDE / 4);
     const int words = (m + 3) >> 2;
-    for (int w = lane; w < words; w += 64) dst[w] = src[w];
+    for (int k = 0; k * 64 < words; k++) {
+      if (k * 64 + lane < words)
+        __builtin_amdgcn_global_load_lds((void*)(src + k * 64 + lane),
+                                         (lds_ptr_t)(lds32 + j * (STRIDE / 4) + k * 64), 4, 0, 0);
+    }
   }
-  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 2 * AVGPU_STACK_SIZE; k++) {
+    if (active)
+      __builtin_amdgcn_global_load_lds((void*)(W.stack + (int64_t)k * N + cell),
+                                       (lds_ptr_t)(stk + k * 64), 4, 0, 0);
+    else
+      stk[k * 64 + lane] = 0;
+  }
 
   uint8_t* T = lds + lane * STRIDE;
 
   // ---- hot state into registers ----
   int r0 = 0, r1 = 0, r2 = 0, ip = 0, rh = 0, wh = 0, fh = 0;
   uint32_t ctl = 0, rl = 0, klo = 0, khi = 0, kct = 0;
-  int cyc = 0, tu = 0, gs = 0, mx = 0, blen = 0, budget = 0;
+  int cyc = 0, tu = 0, gs = 0, mx = 0, blen = 0, budget = 0, errs = 0;
+  int in0 = 0, in1 = 0, in2 = 0, intot = 0, inptr = 0, inp0 = 0, inp1 = 0, inp2 = 0;
+  int outv = 0, outtot = 0;
+  double bonus = 0.0;
+  int tc[AVGPU_NUM_LOGIC_TASKS];
+#pragma unroll
+  for (int q = 0; q < AVGPU_NUM_LOGIC_TASKS; q++) tc[q] = 0;
   if (active) {
     r0 = W.reg[cell]; r1 = W.reg[N + cell]; r2 = W.reg[2 * N + cell];
     ip = W.head[cell]; rh = W.head[N + cell]; wh = W.head[2 * N + cell]; fh = W.head[3 * N + cell];
@@ -80,10 +138,29 @@ __global__ __launch_bounds__(64) void k_interpret(DevWorld W, int cls, int mode,
     mx = W.max_exec[cell]; blen = W.birth_len[cell];
     klo = W.rng[cell]; khi = W.rng[N + cell]; kct = W.rng[2 * N + cell];
     budget = W.budget[cell];
+    errs = W.errors[cell];
+    in0 = W.inbuf[cell]; in1 = W.inbuf[N + cell]; in2 = W.inbuf[2 * N + cell];
+    intot = W.in_total[cell]; inptr = W.in_ptr[cell];
+    inp0 = W.inputs[cell]; inp1 = W.inputs[N + cell]; inp2 = W.inputs[2 * N + cell];
+    outv = W.outbuf[cell]; outtot = W.out_total[cell];
+    bonus = W.cur_bonus[cell];
+#pragma unroll
+    for (int q = 0; q < AVGPU_NUM_LOGIC_TASKS; q++) tc[q] = W.cur_task[(int64_t)q * N + cell];
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
   bool alive = active && (ctl & CTL_ALIVE);
   bool stop = false, spill = false;
   int executed = 0, divides = 0;
+
+  // cInstSet::GetRandomInst (cpu/cInstSet.cc:83-88) from the LDS tables
+  auto rand_code = [&]() -> uint8_t {
+    const uint32_t r = rng_below(klo, khi, kct, (uint32_t)W.rand_total);
+    int i = 0;
+    while (i < W.n_ops - 1 && rcum[i] <= (int32_t)r) i++;
+    return rcode[i];
+  };
 
 #define GETREG(i) ((i) == 0 ? r0 : ((i) == 1 ? r1 : r2))
 #define SETREG(i, v) do { const int _v = (v); if ((i) == 0) r0 = _v; else if ((i) == 1) r1 = _v; else r2 = _v; } while (0)
@@ -93,7 +170,12 @@ __global__ __launch_bounds__(64) void k_interpret(DevWorld W, int cls, int mode,
   while (alive && budget > 0) {
     // ---- SingleProcess (cpu/cHardwareCPU.cc:908-1058) ----
     const int ipa = head_adjust(ip, M);                       // ip.Adjust() :952
-    const int op = T[ipa] & CODE_MASK;                        // fetch :959
+    // fetch window: sites ipa .. ipa+4 in two independent word reads
+    const uint32_t* T32 = reinterpret_cast<const uint32_t*>(T);
+    const uint64_t fwin = ((uint64_t)T32[(ipa >> 2) + 1] << 32) | (uint64_t)T32[ipa >> 2];
+    const uint32_t fsh = (uint32_t)(ipa & 3) * 8u;
+    const int cur_byte = (int)((fwin >> fsh) & 0xFFu);
+    const int op = cur_byte & CODE_MASK;                      // fetch :959
     if (op == AVGPU_H_H_ALLOC) {
       // would this allocation outgrow the LDS slot?  (spill check; the
       // instruction is then executed by the next size class)
@@ -109,11 +191,11 @@ __global__ __launch_bounds__(64) void k_interpret(DevWorld W, int cls, int mode,
     cyc++;                                                    // IncCPUCyclesUsed :929
     tu++;                                                     // IncTimeUsed :930
     ip = ipa;
-    T[ip] |= TF_EXEC;                                         // SetFlagExecuted :996
+    T[ip] = (uint8_t)(cur_byte | TF_EXEC);                    // SetFlagExecuted :996
     executed++;
     budget--;
     bool adv = true;                                          // m_advance_ip
-    const int nxt = (ip + 1 < M) ? (T[ip + 1] & CODE_MASK) : CODE_ERROR;  // GetNextInst
+    const int nxt = (ip + 1 < M) ? (int)((fwin >> (fsh + 8u)) & CODE_MASK) : CODE_ERROR;  // GetNextInst
     // FindModifiedRegister / FindModifiedHead (:1622-1672)
 #define FMOD(def) ((nxt < 3) ? (ip = ip + 1, T[ip] |= TF_EXEC, nxt) : (def))
 
@@ -132,7 +214,7 @@ __global__ __launch_bounds__(64) void k_interpret(DevWorld W, int cls, int mode,
         const int r = FMOD(1);
         const int k = (ctl & CTL_CURSTK) ? 1 : 0;
         int sp = k ? CTL_SP1(ctl) : CTL_SP0(ctl);
-        int32_t* slot = W.stack + ((int64_t)(k * AVGPU_STACK_SIZE + sp)) * N + cell;
+        int32_t* slot = stk + (k * AVGPU_STACK_SIZE + sp) * 64 + lane;
         const int v = *slot;
         *slot = 0;
         sp = (sp + 1 == AVGPU_STACK_SIZE) ? 0 : sp + 1;
@@ -144,7 +226,7 @@ __global__ __launch_bounds__(64) void k_interpret(DevWorld W, int cls, int mode,
         const int k = (ctl & CTL_CURSTK) ? 1 : 0;
         int sp = k ? CTL_SP1(ctl) : CTL_SP0(ctl);
         sp = (sp == 0) ? AVGPU_STACK_SIZE - 1 : sp - 1;
-        W.stack[((int64_t)(k * AVGPU_STACK_SIZE + sp)) * N + cell] = GETREG(r);
+        stk[(k * AVGPU_STACK_SIZE + sp) * 64 + lane] = GETREG(r);
         ctl = k ? ((ctl & ~0xF0u) | ((uint32_t)sp << 4)) : ((ctl & ~0xFu) | (uint32_t)sp);
         break; }
       case AVGPU_H_SWAP_STK:                                  // :2739
@@ -166,14 +248,12 @@ __global__ __launch_bounds__(64) void k_interpret(DevWorld W, int cls, int mode,
         const int r = FMOD(1);
         const int out = GETREG(r);
         // cOrganism::DoOutput -> cTaskLib::SetupTests (main/cTaskLib.cc:369-448)
-        W.outbuf[cell] = out;
-        W.out_total[cell] += 1;
-        const int i0 = W.inbuf[cell], i1 = W.inbuf[N + cell], i2 = W.inbuf[2 * N + cell];
-        const int tot = W.in_total[cell];
-        const int num = tot < 3 ? tot : 3;
-        const uint32_t a = num > 0 ? (uint32_t)i0 : 0u;
-        const uint32_t b = num > 1 ? (uint32_t)i1 : 0u;
-        const uint32_t c = num > 2 ? (uint32_t)i2 : 0u;
+        outv = out;
+        outtot++;
+        const int num = intot < 3 ? intot : 3;
+        const uint32_t a = num > 0 ? (uint32_t)in0 : 0u;
+        const uint32_t b = num > 1 ? (uint32_t)in1 : 0u;
+        const uint32_t c = num > 2 ? (uint32_t)in2 : 0u;
         const uint32_t o = (uint32_t)out;
         int lo[8];
         bool bad = false;
@@ -190,38 +270,36 @@ __global__ __launch_bounds__(64) void k_interpret(DevWorld W, int cls, int mode,
         int id = 0;
 #pragma unroll
         for (int p = 0; p < 8; p++) id += lo[p] * (1 << p);
-        const uint32_t tmask = (!bad && id >= 0 && id < 256) ? W.task_lut[id] : 0u;
+        const uint32_t tmask = (!bad && id >= 0 && id < 256) ? lut[id] : 0u;
         if (tmask) {
           // cEnvironment::TestOutput / TestRequisites / DoProcesses
           // (main/cEnvironment.cc:1314-1406, :1408-1503, :1610-1760)
           uint32_t done = 0;
           double mult = 1.0, addb = 0.0;
           for (int i = 0; i < W.n_react; i++) {
-            const int t = W.react_task[i];
+            const int t = W.react_task[i];                    // uniform
             if (!((tmask >> t) & 1u)) continue;
-            const int cnt = W.cur_task[(int64_t)t * N + cell];
+            int cnt = 0;
+#pragma unroll
+            for (int q = 0; q < AVGPU_NUM_LOGIC_TASKS; q++) cnt = (q == t) ? tc[q] : cnt;
             if (W.react_hasreq[i] && (cnt < W.react_min[i] || cnt >= W.react_max[i])) continue;
             done |= 1u << t;
             if (W.react_type[i] == AVGPU_PROC_ADD) addb = __dadd_rn(addb, W.react_add[i]);
             else mult = __dmul_rn(mult, W.react_mult[i]);
-            W.cur_react[(int64_t)i * N + cell] += 1;
+            atomicAdd(&W.cur_react[(int64_t)i * N + cell], 1);  // no return: no wait
           }
           if (done) {
-            for (int t = 0; t < AVGPU_NUM_LOGIC_TASKS; t++)
-              if ((done >> t) & 1u) W.cur_task[(int64_t)t * N + cell] += 1;
-            const double bon = W.cur_bonus[cell];
-            W.cur_bonus[cell] = __dadd_rn(__dmul_rn(bon, mult), addb);  // cPhenotype.cc:1645-1646
+#pragma unroll
+            for (int q = 0; q < AVGPU_NUM_LOGIC_TASKS; q++) tc[q] += (done >> q) & 1u;
+            bonus = __dadd_rn(__dmul_rn(bonus, mult), addb);   // cPhenotype.cc:1645-1646
           }
         }
         // GetNextInput (main/cOrganism.h:249 -> cPopulationCell.h:214-218) + DoInput
-        int p = W.in_ptr[cell];
-        if (p >= 3) p = 0;
-        const int in = W.inputs[(int64_t)p * N + cell];
-        W.in_ptr[cell] = p + 1;
-        W.inbuf[2 * N + cell] = i1;
-        W.inbuf[N + cell] = i0;
-        W.inbuf[cell] = in;
-        W.in_total[cell] = tot + 1;
+        const int p = inptr >= 3 ? 0 : inptr;
+        const int in = p == 0 ? inp0 : (p == 1 ? inp1 : inp2);
+        inptr = p + 1;
+        in2 = in1; in1 = in0; in0 = in;
+        intot++;
         SETREG(r, in);
         break; }
       case AVGPU_H_H_ALLOC: {                                 // :3294 Inst_MaxAlloc -> Allocate_Main :1707
@@ -232,9 +310,9 @@ __global__ __launch_bounds__(64) void k_interpret(DevWorld W, int cls, int mode,
         const bool ok = !(W.require_allocate && (ctl & CTL_MAL)) && alloc >= 1 &&
                         nsz <= AVGPU_MAX_GENOME && nsz >= AVGPU_MIN_GENOME &&
                         alloc <= (int)(cur * W.size_range) && cur <= (int)(alloc * W.size_range);
-        if (!ok) { W.errors[cell] += 1; break; }
+        if (!ok) { errs++; break; }                           // cOrganism::Fault
         if (W.alloc_method == 2) {
-          for (int i = cur; i < nsz; i++) T[i] = random_code(W, klo, khi, kct);
+          for (int i = cur; i < nsz; i++) T[i] = rand_code();
         } else {
           const uint32_t f = W.fill_code;
           int i = cur;
@@ -259,23 +337,22 @@ __global__ __launch_bounds__(64) void k_interpret(DevWorld W, int cls, int mode,
         if (ok && W.cfg_min_genome && (child < W.cfg_min_genome || div < W.cfg_min_genome)) ok = false;
         if (ok && W.cfg_max_genome && (child > W.cfg_max_genome || div > W.cfg_max_genome)) ok = false;
         int exe = 0, cop = 0;
-        if (ok) {
-          for (int i = 0; i < div; i++) exe += (T[i] >> 7);
+        if (ok) {                                             // calcExecutedSize (cpu/cHardwareBase.cc:130-138)
+          exe = count_flag(T, 0, div, TF_EXEC);
           ok = exe >= (int)(div * W.min_exe_lines);
         }
-        if (ok) {
-          for (int i = div; i < div + child; i++) cop += (T[i] >> 6) & 1;
+        if (ok) {                                             // calcCopiedSize (cpu/cHardwareCPU.cc:1765-1772)
+          cop = count_flag(T, div, div + child, TF_COPIED);
           ok = cop >= (int)(child * W.min_copied_lines);
         }
-        double bonus = 0.0;
+        double bon = bonus;
         int old_exe = 0, copied = 0;
         if (ok) {  // cOrganism::Divide_CheckViable (main/cOrganism.cc:788-919)
-          bonus = W.cur_bonus[cell];
-          if (bonus < W.required_bonus) ok = false;
+          if (bon < W.required_bonus) ok = false;
           old_exe = W.executed[cell];
           copied = W.copied[cell];
           const double base0 = (double)calc_size_merit(W, blen, copied, old_exe);
-          double b0 = bonus;
+          double b0 = bon;
           if (W.merit_default_bonus != 0.0) b0 = W.merit_default_bonus;
           double off_merit = __dmul_rn(base0, b0);
           if (W.inherit_merit == 0) off_merit = base0;
@@ -285,7 +362,7 @@ __global__ __launch_bounds__(64) void k_interpret(DevWorld W, int cls, int mode,
         W.executed[cell] = exe;                               // SetLinesExecuted
         W.child_copied[cell] = cop;                           // SetLinesCopied
         // ---- offspring ----
-        int nd = W.num_div[cell] + 1;
+        const int nd = W.num_div[cell] + 1;
         if (mode == AVGPU_MODE_TEST) {
           uint8_t* fl = W.t_flags + (int64_t)cell * TAPE_SLOT;
           for (int i = 0; i < div; i++) fl[i] = (T[i] & TF_EXEC) ? '+' : '-';
@@ -297,11 +374,11 @@ __global__ __launch_bounds__(64) void k_interpret(DevWorld W, int cls, int mode,
         }
         // DivideReset / TestDivideReset (main/cPhenotype.cc:824-1000, :1064-1180)
         const double base = (double)calc_size_merit(W, blen, copied, exe);
-        if (W.merit_default_bonus != 0.0) bonus = W.merit_default_bonus;
-        double merit = __dmul_rn(base, bonus);
+        if (W.merit_default_bonus != 0.0) bon = W.merit_default_bonus;
+        double merit = __dmul_rn(base, bon);
         if (W.inherit_merit == 0) merit = base;
         const int gt = tu - gs;
-        const double fit = __ddiv_rn(__dmul_rn(base, bonus), (double)gt);
+        const double fit = __ddiv_rn(__dmul_rn(base, bon), (double)gt);
         W.merit[cell] = merit;
         W.gest_time[cell] = gt;
         W.fitness[cell] = fit;
@@ -309,12 +386,13 @@ __global__ __launch_bounds__(64) void k_interpret(DevWorld W, int cls, int mode,
         W.num_div[cell] = nd;
         const int gen = W.generation[cell] + 1;
         W.generation[cell] = gen;
-        W.errors[cell] = 0;
-        W.cur_bonus[cell] = W.default_bonus;
+        errs = 0;
+        bonus = W.default_bonus;
         cyc = 0;
-        for (int t = 0; t < AVGPU_NUM_LOGIC_TASKS; t++) {
-          W.last_task[(int64_t)t * N + cell] = W.cur_task[(int64_t)t * N + cell];
-          W.cur_task[(int64_t)t * N + cell] = 0;
+#pragma unroll
+        for (int q = 0; q < AVGPU_NUM_LOGIC_TASKS; q++) {
+          W.last_task[(int64_t)q * N + cell] = tc[q];
+          tc[q] = 0;
         }
         for (int i = 0; i < W.n_react; i++) W.cur_react[(int64_t)i * N + cell] = 0;
         if (mode == AVGPU_MODE_WORLD) {
@@ -324,11 +402,11 @@ __global__ __launch_bounds__(64) void k_interpret(DevWorld W, int cls, int mode,
           uint8_t mcode = 0, icode = 0;
           if (W.th_div_mut && rng_p(klo, khi, kct, W.th_div_mut)) {
             mline = (int)rng_below(klo, khi, kct, (uint32_t)len);
-            mcode = random_code(W, klo, khi, kct);
+            mcode = rand_code();
           }
           if (W.th_div_ins && rng_p(klo, khi, kct, W.th_div_ins) && len < W.max_genome) {
             iline = (int)rng_below(klo, khi, kct, (uint32_t)len + 1);
-            icode = random_code(W, klo, khi, kct);
+            icode = rand_code();
             len++;
           }
           if (W.th_div_del && rng_p(klo, khi, kct, W.th_div_del) && len > W.min_genome) {
@@ -337,16 +415,22 @@ __global__ __launch_bounds__(64) void k_interpret(DevWorld W, int cls, int mode,
           }
           const int slot = atomicAdd(W.b_count, 1);
           if (slot < W.bcap) {
-            uint8_t* g = W.b_genome + (int64_t)slot * TAPE_SLOT;
-            for (int j = 0; j < len; j++) {
-              int k2 = (dline >= 0 && j >= dline) ? j + 1 : j;       // index before the deletion
-              int v;
-              if (iline >= 0 && k2 == iline) v = icode;
-              else {
-                const int k1 = (iline >= 0 && k2 > iline) ? k2 - 1 : k2;  // before the insertion
-                v = (k1 == mline) ? mcode : (T[div + k1] & CODE_MASK);
+            uint32_t* g32 = reinterpret_cast<uint32_t*>(W.b_genome + (int64_t)slot * TAPE_SLOT);
+            for (int j0 = 0; j0 < len; j0 += 4) {
+              uint32_t word = 0;
+#pragma unroll
+              for (int b = 0; b < 4; b++) {
+                const int j = j0 + b;
+                const int k2 = (dline >= 0 && j >= dline) ? j + 1 : j;       // index before the deletion
+                int v;
+                if (iline >= 0 && k2 == iline) v = icode;
+                else {
+                  const int k1 = (iline >= 0 && k2 > iline) ? k2 - 1 : k2;  // before the insertion
+                  v = (k1 == mline) ? mcode : (T[div + k1] & CODE_MASK);
+                }
+                word |= (j < len ? (uint32_t)v : 0u) << (8 * b);
               }
-              g[j] = (uint8_t)v;
+              g32[j0 >> 2] = word;
             }
             W.b_parent[slot] = cell;
             W.b_seq[slot] = (uint32_t)nd;
@@ -373,10 +457,14 @@ __global__ __launch_bounds__(64) void k_interpret(DevWorld W, int cls, int mode,
         M = div;
         r0 = r1 = r2 = 0;
         ip = rh = wh = fh = 0;
-        for (int k = 0; k < 2 * AVGPU_STACK_SIZE; k++) W.stack[(int64_t)k * N + cell] = 0;
+#pragma unroll
+        for (int k = 0; k < 2 * AVGPU_STACK_SIZE; k++) stk[k * 64 + lane] = 0;
         ctl = CTL_ALIVE;
         rl = 0;
-        for (int i = 0; i < div; i++) T[i] &= CODE_MASK;
+        {
+          uint32_t* W32 = reinterpret_cast<uint32_t*>(T);
+          for (int w = 0; w < ((div + 3) >> 2); w++) W32[w] &= 0x3F3F3F3Fu;  // ClearFlags (beyond div: unused)
+        }
         adv = false;
         break; }
       case AVGPU_H_H_COPY: {                                  // :7130 Inst_HeadCopy
@@ -391,25 +479,34 @@ __global__ __launch_bounds__(64) void k_interpret(DevWorld W, int cls, int mode,
           rl = 0;
         }
         if (mode != AVGPU_MODE_TEST && W.th_copy_mut && rng_p(klo, khi, kct, W.th_copy_mut))
-          v = random_code(W, klo, khi, kct);
+          v = rand_code();
         T[wh] = (uint8_t)((T[wh] & TF_EXEC) | TF_COPIED | v);
         rh = head_adjust(rh + 1, M);
         wh = head_adjust(wh + 1, M);
         break; }
       case AVGPU_H_H_SEARCH:                                  // :7245 Inst_HeadSearch
       case AVGPU_H_IF_LABEL: {                                // :6914 Inst_IfLabel
-        // ReadLabel (:1484-1502)
+        // ReadLabel (:1484-1502): the up to 10 sites after IP come from one
+        // 16-byte window (4 independent word reads)
         uint32_t lab = 0;
         int len = 0;
-        while (len < AVGPU_MAX_LABEL) {
-          const int p = ip + 1;
-          if (p >= M) break;
-          const int cc = T[p] & CODE_MASK;
-          if (cc >= 3) break;
-          ip = p;
-          lab |= (uint32_t)cc << (2 * len);
-          len++;
-          if (len <= W.max_label_exe) T[ip] |= TF_EXEC;
+        {
+          const int base = ip + 1;
+          const int w0 = base >> 2;
+          const uint64_t lo64 = ((uint64_t)T32[w0 + 1] << 32) | (uint64_t)T32[w0];
+          const uint64_t hi64 = ((uint64_t)T32[w0 + 3] << 32) | (uint64_t)T32[w0 + 2];
+          const int b0 = base & 3;
+          while (len < AVGPU_MAX_LABEL) {
+            const int p = base + len;
+            if (p >= M) break;
+            const int k = b0 + len;
+            const int cc = (int)(((k < 8) ? (lo64 >> (8 * k)) : (hi64 >> (8 * (k - 8)))) & CODE_MASK);
+            if (cc >= 3) break;
+            lab |= (uint32_t)cc << (2 * len);
+            len++;
+            if (len <= W.max_label_exe) T[p] |= TF_EXEC;
+          }
+          ip += len;
         }
         // Rotate(1, NUM_NOPS)
         uint32_t rot = 0;
@@ -423,29 +520,33 @@ __global__ __launch_bounds__(64) void k_interpret(DevWorld W, int cls, int mode,
           if (packed != rl) ip = head_adjust(ip + 1, M);
           break;
         }
-        // FindLabel(0) -> FindLabel_Forward(label, memory, 0) (:1177-1295)
+        // FindLabel(0) -> FindLabel_Forward(label, memory, 0) (:1177-1295).
+        // The reference probes every label_size sites and, inside a probed nop
+        // run, tests every offset; every maximal nop run that can hold the
+        // label is probed except a run that ends exactly at label_size.  Its
+        // answer is therefore the smallest offset o whose label_size sites
+        // spell the label (all nops) and that is not that unprobed run
+        // (o > 0, or site label_size is a nop).  A rolling 2-bit window over
+        // 16-site word batches finds it (DESIGN.md "h-search").
         int found = ip;
         if (len > 0) {
-          int pos = len;
+          uint32_t lab_rev = 0;
+          for (int i = 0; i < len; i++) lab_rev |= ((rot >> (2 * i)) & 3u) << (2 * (len - 1 - i));
+          const uint32_t msk = (len == 16) ? 0xFFFFFFFFu : ((1u << (2 * len)) - 1u);
+          const bool run0_ok = len < M && (T[len] & CODE_MASK) < 3;
+          uint32_t wnd = 0xFFFFFFFFu;
           int fpos = -1;
-          while (pos < M) {
-            if ((T[pos] & CODE_MASK) < 3) {
-              int sp0 = pos, ep = pos + 1;
-              while (sp0 > 0 && (T[sp0 - 1] & CODE_MASK) < 3) sp0--;
-              while (ep < M && (T[ep] & CODE_MASK) < 3) ep++;
-              const int max_off = (ep - sp0) - len + 1;
-              int off = sp0;
-              bool hit = false;
-              for (; off < sp0 + max_off; off++) {
-                int mm = 0;
-                for (; mm < len; mm++)
-                  if ((int)((rot >> (2 * mm)) & 3u) != (T[off + mm] & CODE_MASK)) break;
-                if (mm == len) { hit = true; break; }
-              }
-              if (hit) { fpos = len + off; break; }
-              pos = ep;
+          for (int w = 0; (w << 2) < M && fpos < 0; w += 4) {
+            const uint32_t q0 = T32[w], q1 = T32[w + 1], q2 = T32[w + 2], q3 = T32[w + 3];
+#pragma unroll
+            for (int b = 0; b < 16; b++) {
+              const uint32_t q = (b < 4) ? q0 : (b < 8) ? q1 : (b < 12) ? q2 : q3;
+              const int j = (w << 2) + b;
+              uint32_t cc = (q >> (8 * (b & 3))) & CODE_MASK;
+              cc = cc < 3u ? cc : 3u;
+              wnd = (wnd << 2) | cc;
+              if (fpos < 0 && j < M && (wnd & msk) == lab_rev && (j != len - 1 || run0_ok)) fpos = j + 1;
             }
-            pos += len;
           }
           if (fpos >= 0) found = head_adjust(fpos - 1, M);
         }
@@ -484,6 +585,7 @@ __global__ __launch_bounds__(64) void k_interpret(DevWorld W, int cls, int mode,
 #undef SETHEAD
 
   // ---- write back ----
+  __syncthreads();
   if (active) {
     W.reg[cell] = r0; W.reg[N + cell] = r1; W.reg[2 * N + cell] = r2;
     W.head[cell] = ip; W.head[N + cell] = rh; W.head[2 * N + cell] = wh; W.head[3 * N + cell] = fh;
@@ -493,13 +595,21 @@ __global__ __launch_bounds__(64) void k_interpret(DevWorld W, int cls, int mode,
     W.cycles[cell] = cyc; W.time_used[cell] = tu; W.gest_start[cell] = gs;
     W.rng[2 * N + cell] = kct;
     W.budget[cell] = spill ? budget : 0;
+    W.errors[cell] = errs;
+    W.inbuf[cell] = in0; W.inbuf[N + cell] = in1; W.inbuf[2 * N + cell] = in2;
+    W.in_total[cell] = intot; W.in_ptr[cell] = inptr;
+    W.outbuf[cell] = outv; W.out_total[cell] = outtot;
+    W.cur_bonus[cell] = bonus;
+#pragma unroll
+    for (int q = 0; q < AVGPU_NUM_LOGIC_TASKS; q++) W.cur_task[(int64_t)q * N + cell] = tc[q];
+#pragma unroll
+    for (int k = 0; k < 2 * AVGPU_STACK_SIZE; k++) W.stack[(int64_t)k * N + cell] = stk[k * 64 + lane];
     if (spill) {
       const int slot = atomicAdd(&W.class_count[cls + 1], 1);
       W.class_list[(int64_t)(cls + 1) * N + slot] = cell;
       count_add(W, CNT_SPILLS, 1ull);
     }
   }
-  __syncthreads();
   for (int j = 0; j < 64; j++) {
     const int c = __shfl(cell, j);
     const int m = __shfl(M, j);
@@ -513,12 +623,15 @@ __global__ __launch_bounds__(64) void k_interpret(DevWorld W, int cls, int mode,
   unsigned long long e = (unsigned long long)executed;
   int dead = (active && !alive) ? 1 : 0;
   int dv = divides;
+  int mxe = executed;
   for (int off = 32; off > 0; off >>= 1) {
     e += __shfl_down(e, off);
     dead += __shfl_down(dead, off);
     dv += __shfl_down(dv, off);
+    mxe = max(mxe, __shfl_down(mxe, off));
   }
   if (lane == 0) {
+    count_add(W, CNT_LANESTEPS, 64ull * (unsigned long long)mxe);   // issued lane-steps
     count_add(W, CNT_INSTS, e);
     if (dead) count_add(W, CNT_DEATHS, (unsigned long long)dead);
     if (dv) count_add(W, CNT_DIVIDES, (unsigned long long)dv);

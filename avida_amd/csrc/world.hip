@@ -482,6 +482,7 @@ __global__ __launch_bounds__(256) void k_stats_final(DevWorld W, const double* p
     out[30] = (double)W.counters[CNT_CUM_INSTS];
     out[31] = (double)W.counters[CNT_CUM_BIRTHS];
     out[32] = (double)c[CNT_SLICES];
+    out[33] = (double)c[CNT_LANESTEPS];
   }
 }
 

@@ -226,6 +226,7 @@ def main():
             "bytes_per_launch": bytes_per_phase,
             "mean_mem_sites": mean_mem,
             "slices_per_launch": slices,
+            "lane_efficiency": s1.insts_executed / max(1, s1.lane_steps),
         },
         "cpu_baseline": None,
     }

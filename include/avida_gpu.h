@@ -237,6 +237,7 @@ typedef struct avgpu_update_stats {
   int64_t cum_insts_executed;  /* since avgpu_create */
   int64_t cum_births;
   int64_t slices;              /* organism time slices interpreted this update */
+  int64_t lane_steps;          /* 64 x longest lane per wave (SIMD lane-issue slots used) */
 } avgpu_update_stats;
 
 typedef struct avgpu_world avgpu_world;   /* opaque handle */

@@ -207,6 +207,7 @@ struct World {
 
 thread_local std::string g_err;
 static int g_trace = getenv("ORACLE_TRACE") ? 1 : 0;
+static int64_t g_op_hist[64];   // executed instructions per handler (instruction-mix statistics)
 int fail(int code, const std::string& msg) { g_err = msg; return code; }
 
 // cHeadCPU::Adjust / fullAdjust (cpu/cHeadCPU.h:63, cpu/cHeadCPU.cc:27-50)
@@ -590,6 +591,7 @@ struct Exec {
       fprintf(stderr, " mem:%d\n", (int)o.mem.size());
     }
     o.flg[o.head[HEAD_IP]] |= F_EXECUTED;
+    g_op_hist[w.is.handler[op]]++;
     switch (w.is.handler[op]) {
       case H_NOP_A: case H_NOP_B: case H_NOP_C: break;
       case H_IF_N_EQU: { int a = find_modified(REG_BX), b = next_reg(a);
@@ -881,6 +883,12 @@ int orc_set_orgs(void* h, int64_t first, int64_t count, const uint8_t* genomes, 
 }
 
 int orc_kill(void* h, int64_t cell) { ((World*)h)->orgs[cell].alive = false; return 0; }
+
+// instruction-mix histogram over everything executed since the last call
+int orc_op_hist(int64_t* out, int n) {
+  for (int i = 0; i < n && i < 64; i++) { out[i] = g_op_hist[i]; g_op_hist[i] = 0; }
+  return 0;
+}
 
 // Batched SingleProcess for a range (FROZEN / TEST / WORLD semantics).
 int orc_step(void* h, int64_t first, int64_t count, const int32_t* budget, int32_t uniform, int mode) {

@@ -14,30 +14,34 @@ ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 SOURCES = ["interp.hip", "world.hip", "capi.hip"]
 OUT = os.path.join(HERE, "libavida_gpu.so")
+# diagnostic variant with per-phase s_memtime clocks (tools/phase_clocks.py only)
+OUT_CLK = os.path.join(HERE, "libavida_gpu_clk.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["-O3", "--offload-arch=gfx950", "-std=c++17", "-fPIC", "-shared",
          "-ffp-contract=off", "-Wno-unused-result", "-Wno-unused-value"]
 
 
-def needs_build() -> bool:
-    if not os.path.exists(OUT):
+def needs_build(out: str = OUT) -> bool:
+    if not os.path.exists(out):
         return True
-    t = os.path.getmtime(OUT)
+    t = os.path.getmtime(out)
     deps = [os.path.join(CSRC, f) for f in os.listdir(CSRC)]
     deps.append(os.path.join(ROOT, "include", "avida_gpu.h"))
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
-    if not force and not needs_build():
-        return OUT
-    cmd = [HIPCC, *FLAGS, "-o", OUT + ".tmp", *[os.path.join(CSRC, s) for s in SOURCES]]
+def build(force: bool = False, verbose: bool = False, clocks: bool = False) -> str:
+    out = OUT_CLK if clocks else OUT
+    if not force and not needs_build(out):
+        return out
+    extra = ["-DAVGPU_PHASE_CLOCKS"] if clocks else []
+    cmd = [HIPCC, *FLAGS, *extra, "-o", out + ".tmp", *[os.path.join(CSRC, s) for s in SOURCES]]
     if verbose:
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)
-    os.replace(OUT + ".tmp", OUT)
-    return OUT
+    os.replace(out + ".tmp", out)
+    return out
 
 
 if __name__ == "__main__":
-    build(force="--force" in sys.argv, verbose=True)
+    build(force="--force" in sys.argv, verbose=True, clocks="--clocks" in sys.argv)

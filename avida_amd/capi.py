@@ -15,6 +15,11 @@ STACK_SIZE = 10
 MAX_LABEL = 10
 
 MODE_WORLD, MODE_TEST, MODE_FROZEN = 0, 1, 2
+# enum avgpu_counter
+(CNT_INSTS, CNT_DEATHS, CNT_DIVIDES, CNT_BIRTHS, CNT_DROPPED, CNT_SPILLS, CNT_SLICES,
+ CNT_LANESTEPS, CNT_C0_SLICES, CNT_C0_SITES, CNT_CLK_STAGE, CNT_CLK_LOOP, CNT_CLK_WB,
+ CNT_ITERS, CNT_IT_FAST, CNT_IT_COPY, CNT_IT_SLOW, CNT_WAVES) = range(18)
+NUM_COUNTERS = 32
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libavida_gpu.so")
@@ -105,7 +110,7 @@ EXPORTED = [
     "avgpu_update_run", "avgpu_set_stream", "avgpu_get_states",
     "avgpu_test_genomes", "avgpu_get_stats", "avgpu_stats_vector", "avgpu_set_global_totals",
     "avgpu_halo_pack", "avgpu_halo_unpack", "avgpu_halo_record_bytes",
-    "avgpu_last_step_insts", "avgpu_last_kernel_ms",
+    "avgpu_last_step_insts", "avgpu_last_kernel_ms", "avgpu_kernel_times", "avgpu_counters",
 ]
 
 
@@ -191,14 +196,16 @@ def bind_common(lib, prefix):
 _lib = None
 
 
-def load_product():
-    """Load the in-tree HIP library; raise if it is missing (no fallback)."""
+def load_product(path=None):
+    """Load the in-tree HIP library; raise if it is missing (no fallback).
+    `path` selects a diagnostic build (tools/phase_clocks.py); it is not cached."""
     global _lib
-    if _lib is not None:
+    if path is None and _lib is not None:
         return _lib
-    if not os.path.exists(LIB_PATH):
-        raise RuntimeError(f"{LIB_PATH} missing: run __graft_entry__.build() first")
-    lib = C.CDLL(LIB_PATH)
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        raise RuntimeError(f"{p} missing: run __graft_entry__.build() first")
+    lib = C.CDLL(p)
     bind_common(lib, "avgpu_")
     lib.avgpu_create.restype = C.c_void_p
     lib.avgpu_create.argtypes = [C.POINTER(AvgpuCfg), C.c_int, C.c_int64]
@@ -212,10 +219,13 @@ def load_product():
     lib.avgpu_halo_record_bytes.restype = C.c_int64
     lib.avgpu_last_kernel_ms.argtypes = [C.c_void_p, C.POINTER(C.c_double),
                                          C.POINTER(C.c_int64)]
+    lib.avgpu_kernel_times.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_int64)]
+    lib.avgpu_counters.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_int64), C.c_int]
     lib.avgpu_update_totals.argtypes = [C.c_void_p, C.c_void_p]
     lib.avgpu_update_run.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(AvgpuUpdateStats)]
     lib.avgpu_set_stream.argtypes = [C.c_void_p, C.c_void_p]
-    _lib = lib
+    if path is None:
+        _lib = lib
     return lib
 
 

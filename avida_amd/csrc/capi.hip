@@ -39,11 +39,13 @@ struct avgpu_world {
   hipStream_t stream = nullptr;      // current stream (own or external)
   hipStream_t own_stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
-  // event ring around interpreter phases (avgpu_last_kernel_ms)
+  // event ring around interpreter phases (avgpu_last_kernel_ms,
+  // avgpu_kernel_times): ev[i][0] before class 0, ev[i][k+1] after class k
   static const int RING = 512;
-  hipEvent_t ring0[RING] = {}, ring1[RING] = {};
+  hipEvent_t ring[RING][NUM_CLASSES + 1] = {};
   int ring_head = 0, ring_count = 0;
   double acc_ms = 0.0;
+  double acc_class_ms[NUM_CLASSES] = {};
   int64_t acc_phases = 0;
   DevWorld W;
   std::vector<void*> allocs;
@@ -173,9 +175,10 @@ avgpu_world* create_world(const avgpu_cfg* cfg, int device, int64_t n, bool test
   }
   w->stream = w->own_stream;
   for (int i = 0; i < avgpu_world::RING; i++) {
-    if (hipEventCreate(&w->ring0[i]) != hipSuccess || hipEventCreate(&w->ring1[i]) != hipSuccess) {
-      fail(AVGPU_EHIP, "event creation failed"); return nullptr;
-    }
+    for (int k = 0; k <= NUM_CLASSES; k++)
+      if (hipEventCreate(&w->ring[i][k]) != hipSuccess) {
+        fail(AVGPU_EHIP, "event creation failed"); return nullptr;
+      }
   }
   for (int i = 0; i < 64; i++) w->code2op[i] = -1;
   if (setup_world(w, n, test_buffers) < 0) {
@@ -274,10 +277,13 @@ int set_orgs_impl(avgpu_world* w, int64_t first, int64_t count, const uint8_t* g
 int drain_ring(avgpu_world* w, int keep) {
   while (w->ring_count > keep) {
     const int i = (w->ring_head - w->ring_count + avgpu_world::RING) % avgpu_world::RING;
-    HIPCHK(hipEventSynchronize(w->ring1[i]));
-    float f = 0.f;
-    HIPCHK(hipEventElapsedTime(&f, w->ring0[i], w->ring1[i]));
-    w->acc_ms += f;
+    HIPCHK(hipEventSynchronize(w->ring[i][NUM_CLASSES]));
+    for (int k = 0; k < NUM_CLASSES; k++) {
+      float f = 0.f;
+      HIPCHK(hipEventElapsedTime(&f, w->ring[i][k], w->ring[i][k + 1]));
+      w->acc_class_ms[k] += f;
+      w->acc_ms += f;
+    }
     w->acc_phases++;
     w->ring_count--;
   }
@@ -289,10 +295,9 @@ int interpret(avgpu_world* w, int mode, int64_t first, int64_t count) {
   int rc = drain_ring(w, avgpu_world::RING - 1);
   if (rc < 0) return rc;
   const int i = w->ring_head;
-  HIPCHK(hipEventRecord(w->ring0[i], w->stream));
-  launch_interpret_classes(w->W, mode, w->stream, first, count, &launches);
+  HIPCHK(hipEventRecord(w->ring[i][0], w->stream));
+  launch_interpret_classes(w->W, mode, w->stream, first, count, &launches, &w->ring[i][1]);
   HIPCHK(hipGetLastError());
-  HIPCHK(hipEventRecord(w->ring1[i], w->stream));
   w->ring_head = (i + 1) % avgpu_world::RING;
   w->ring_count++;
   w->last_launches = launches;
@@ -333,8 +338,8 @@ int avgpu_destroy(avgpu_world* w) {
   if (w->ev0) hipEventDestroy(w->ev0);
   if (w->ev1) hipEventDestroy(w->ev1);
   for (int i = 0; i < avgpu_world::RING; i++) {
-    if (w->ring0[i]) hipEventDestroy(w->ring0[i]);
-    if (w->ring1[i]) hipEventDestroy(w->ring1[i]);
+    for (int k = 0; k <= NUM_CLASSES; k++)
+      if (w->ring[i][k]) hipEventDestroy(w->ring[i][k]);
   }
   if (w->own_stream) hipStreamDestroy(w->own_stream);
   delete w;
@@ -681,6 +686,36 @@ int avgpu_last_kernel_ms(avgpu_world* w, double* ms, int64_t* launches) {
   if (launches) *launches = w->acc_phases;
   w->acc_ms = 0.0;
   w->acc_phases = 0;
+  for (int k = 0; k < NUM_CLASSES; k++) w->acc_class_ms[k] = 0.0;
+  return 0;
+}
+
+int avgpu_kernel_times(avgpu_world* w, double* class_ms, int64_t* phases) {
+  if (!w) return fail(AVGPU_EINVAL, "NULL world");
+  int rc = drain_ring(w, 0);
+  if (rc < 0) return rc;
+  if (class_ms)
+    for (int k = 0; k < NUM_CLASSES; k++) class_ms[k] = w->acc_class_ms[k];
+  if (phases) *phases = w->acc_phases;
+  w->acc_ms = 0.0;
+  w->acc_phases = 0;
+  for (int k = 0; k < NUM_CLASSES; k++) w->acc_class_ms[k] = 0.0;
+  return 0;
+}
+
+int avgpu_counters(avgpu_world* w, int cumulative, int64_t* out, int n) {
+  if (!w || !out || n < 0) return fail(AVGPU_EINVAL, "args");
+  if (n > AVGPU_NUM_COUNTERS) n = AVGPU_NUM_COUNTERS;
+  std::vector<unsigned long long> v(CNT_WORDS);
+  HIPCHK(hipMemcpyAsync(v.data(), w->W.counters, v.size() * 8, hipMemcpyDeviceToHost, w->stream));
+  HIPCHK(hipStreamSynchronize(w->stream));
+  for (int k = 0; k < n; k++) {
+    unsigned long long s = 0;
+    if (cumulative) s = v[CNT_CUM_BASE + k];
+    else
+      for (int sh = 0; sh < NSHARD; sh++) s += v[sh * CNT_STRIDE + k];
+    out[k] = (int64_t)s;
+  }
   return 0;
 }
 

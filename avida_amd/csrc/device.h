@@ -140,14 +140,27 @@ struct DevWorld {
 #define CNT_SPILLS 5
 #define CNT_SLICES 6
 #define CNT_LANESTEPS 7   /* 64 x the longest lane of each wave: lane efficiency = insts / this */
-// Counters are sharded over NSHARD cache lines (16 x u64 = 128 B each) so that
-// the per-wave adds of a 16K-wave launch do not serialise on one L2 address;
-// counters[NSHARD*16 + k] hold the cumulative totals.
+#define CNT_C0_SLICES 8   /* slices run by the class-0 interpreter launch */
+#define CNT_C0_SITES 9    /* tape sites it staged in + wrote back (sum of M at entry and exit) */
+// slots 10..17: AVGPU_PHASE_CLOCKS diagnostic builds only (s_memtime per wave)
+#define CNT_CLK_STAGE 10
+#define CNT_CLK_LOOP 11
+#define CNT_CLK_WB 12
+#define CNT_ITERS 13      /* loop iterations of the wave */
+#define CNT_IT_FAST 14    /* iterations in which some lane took the branch-free block */
+#define CNT_IT_COPY 15    /* ... the h-copy block */
+#define CNT_IT_SLOW 16    /* ... the switch */
+#define CNT_WAVES 17
+// Counters are sharded over NSHARD lines (CNT_STRIDE x u64 each) so that the
+// per-wave adds of a 16K-wave launch do not serialise on one L2 address; they
+// are cleared every update, and counters[CNT_CUM_BASE + k] accumulates slot k
+// over all updates (k_stats_final).
 #define NSHARD 64
-#define CNT_STRIDE 16
+#define CNT_STRIDE 32
+#define CNT_CUM_BASE (NSHARD * CNT_STRIDE)
 #define CNT_WORDS (NSHARD * CNT_STRIDE + CNT_STRIDE)
-#define CNT_CUM_INSTS (NSHARD * CNT_STRIDE + 0)
-#define CNT_CUM_BIRTHS (NSHARD * CNT_STRIDE + 1)
+#define CNT_CUM_INSTS (CNT_CUM_BASE + CNT_INSTS)
+#define CNT_CUM_BIRTHS (CNT_CUM_BASE + CNT_BIRTHS)
 
 // ---------------------------------------------------------------------------
 // RNG spec: identical arithmetic to the oracle's Stream.
@@ -230,8 +243,9 @@ struct LaunchInfo {
 };
 
 // class 0 runs densely over cells [first, first+count); classes 1..3 over their lists
+// after_class[k] (optional): event recorded after the class-k launch
 void launch_interpret_classes(const DevWorld& W, int mode, hipStream_t s, int64_t first,
-                              int64_t count, int* launches);
+                              int64_t count, int* launches, hipEvent_t* after_class = nullptr);
 void launch_world_pre(const DevWorld& W, hipStream_t s, const double* d_totals);
 void launch_world_post(const DevWorld& W, hipStream_t s, double* d_stats);
 void launch_classify_uniform(const DevWorld& W, hipStream_t s, int64_t first, int64_t count,

@@ -24,6 +24,35 @@
 
 namespace {
 
+// Decode tables over canonical handler ids (include/avida_gpu.h).
+// Ops that call FindModifiedRegister/FindModifiedHead (cpu/cHardwareCPU.cc:1622-1672):
+#define OPB(x) (1u << (x))
+constexpr uint32_t MOD_OPS =
+    OPB(AVGPU_H_IF_N_EQU) | OPB(AVGPU_H_IF_LESS) | OPB(AVGPU_H_POP) | OPB(AVGPU_H_PUSH) |
+    OPB(AVGPU_H_SWAP) | OPB(AVGPU_H_SHIFT_R) | OPB(AVGPU_H_SHIFT_L) | OPB(AVGPU_H_INC) |
+    OPB(AVGPU_H_DEC) | OPB(AVGPU_H_ADD) | OPB(AVGPU_H_SUB) | OPB(AVGPU_H_NAND) | OPB(AVGPU_H_IO) |
+    OPB(AVGPU_H_MOV_HEAD) | OPB(AVGPU_H_JMP_HEAD) | OPB(AVGPU_H_GET_HEAD) | OPB(AVGPU_H_SET_FLOW);
+// their default register/head (2 bits per op): BX for register ops and IO,
+// HEAD_IP for the head ops, CX for set-flow
+constexpr uint64_t DEF_OPS =
+    (1ull << (2 * AVGPU_H_IF_N_EQU)) | (1ull << (2 * AVGPU_H_IF_LESS)) | (1ull << (2 * AVGPU_H_POP)) |
+    (1ull << (2 * AVGPU_H_PUSH)) | (1ull << (2 * AVGPU_H_SWAP)) | (1ull << (2 * AVGPU_H_SHIFT_R)) |
+    (1ull << (2 * AVGPU_H_SHIFT_L)) | (1ull << (2 * AVGPU_H_INC)) | (1ull << (2 * AVGPU_H_DEC)) |
+    (1ull << (2 * AVGPU_H_ADD)) | (1ull << (2 * AVGPU_H_SUB)) | (1ull << (2 * AVGPU_H_NAND)) |
+    (1ull << (2 * AVGPU_H_IO)) | (2ull << (2 * AVGPU_H_SET_FLOW));
+// ops executed by the branch-free block
+constexpr uint32_t FAST_OPS =
+    OPB(AVGPU_H_NOP_A) | OPB(AVGPU_H_NOP_B) | OPB(AVGPU_H_NOP_C) | OPB(AVGPU_H_IF_N_EQU) |
+    OPB(AVGPU_H_IF_LESS) | OPB(AVGPU_H_SWAP_STK) | OPB(AVGPU_H_SWAP) | OPB(AVGPU_H_SHIFT_R) |
+    OPB(AVGPU_H_SHIFT_L) | OPB(AVGPU_H_INC) | OPB(AVGPU_H_DEC) | OPB(AVGPU_H_ADD) |
+    OPB(AVGPU_H_SUB) | OPB(AVGPU_H_NAND) | OPB(AVGPU_H_MOV_HEAD) | OPB(AVGPU_H_JMP_HEAD) |
+    OPB(AVGPU_H_GET_HEAD) | OPB(AVGPU_H_SET_FLOW);
+// fast ops that write reg[r]
+constexpr uint32_t WR_OPS =
+    OPB(AVGPU_H_SWAP) | OPB(AVGPU_H_SHIFT_R) | OPB(AVGPU_H_SHIFT_L) | OPB(AVGPU_H_INC) |
+    OPB(AVGPU_H_DEC) | OPB(AVGPU_H_ADD) | OPB(AVGPU_H_SUB) | OPB(AVGPU_H_NAND);
+#undef OPB
+
 // popcount of `bitmask`-selected flag bits over tape sites [from, to)
 __device__ __forceinline__ int count_flag(const uint8_t* T, int from, int to, uint32_t bit) {
   const uint32_t* T32 = reinterpret_cast<const uint32_t*>(T);
@@ -83,6 +112,11 @@ __global__ __launch_bounds__(64) void k_interpret(DevWorld W, int cls, int mode,
   }
   const bool active = cell >= 0;
   if (!__any(active)) return;
+#ifdef AVGPU_PHASE_CLOCKS
+  const uint64_t clk0 = __builtin_amdgcn_s_memtime();
+  int it_fast = 0, it_copy = 0, it_slow = 0;
+#endif
+  const int m_in = M;
 
   // ---- block-shared tables ----
   {
@@ -105,15 +139,23 @@ __global__ __launch_bounds__(64) void k_interpret(DevWorld W, int cls, int mode,
     const int words = (m + 3) >> 2;
     for (int k = 0; k * 64 < words; k++) {
       if (k * 64 + lane < words)
+#ifdef AVGPU_NO_LDS_DMA
+        lds32[j * (STRIDE / 4) + k * 64 + lane] = src[k * 64 + lane];
+#else
         __builtin_amdgcn_global_load_lds((void*)(src + k * 64 + lane),
                                          (lds_ptr_t)(lds32 + j * (STRIDE / 4) + k * 64), 4, 0, 0);
+#endif
     }
   }
 #pragma unroll
   for (int k = 0; k < 2 * AVGPU_STACK_SIZE; k++) {
     if (active)
+#ifdef AVGPU_NO_LDS_DMA
+      stk[k * 64 + lane] = W.stack[(int64_t)k * N + cell];
+#else
       __builtin_amdgcn_global_load_lds((void*)(W.stack + (int64_t)k * N + cell),
                                        (lds_ptr_t)(stk + k * 64), 4, 0, 0);
+#endif
     else
       stk[k * 64 + lane] = 0;
   }
@@ -147,8 +189,11 @@ __global__ __launch_bounds__(64) void k_interpret(DevWorld W, int cls, int mode,
 #pragma unroll
     for (int q = 0; q < AVGPU_NUM_LOGIC_TASKS; q++) tc[q] = W.cur_task[(int64_t)q * N + cell];
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0), visible to the compiler's waitcnt tracking
   __syncthreads();
+#ifdef AVGPU_PHASE_CLOCKS
+  const uint64_t clk1 = __builtin_amdgcn_s_memtime();
+#endif
 
   bool alive = active && (ctl & CTL_ALIVE);
   bool stop = false, spill = false;
@@ -195,23 +240,71 @@ __global__ __launch_bounds__(64) void k_interpret(DevWorld W, int cls, int mode,
     executed++;
     budget--;
     bool adv = true;                                          // m_advance_ip
-    const int nxt = (ip + 1 < M) ? (int)((fwin >> (fsh + 8u)) & CODE_MASK) : CODE_ERROR;  // GetNextInst
-    // FindModifiedRegister / FindModifiedHead (:1622-1672)
-#define FMOD(def) ((nxt < 3) ? (ip = ip + 1, T[ip] |= TF_EXEC, nxt) : (def))
+    const int nbyte = (int)((fwin >> (fsh + 8u)) & 0xFFu);
+    const int nxt = (ip + 1 < M) ? (nbyte & CODE_MASK) : CODE_ERROR;  // GetNextInst
+    // ---- FindModifiedRegister / FindModifiedHead (:1622-1672), applied once
+    // for every op that takes a nop modifier: r = nop-mod or the op's default ----
+    const uint32_t obit = 1u << op;
+    const bool mod = ((MOD_OPS & obit) != 0u) && nxt < 3;
+    const int r = mod ? nxt : (int)((DEF_OPS >> (2 * op)) & 3ull);
+    if (mod) { ip = ip + 1; T[ip] = (uint8_t)(nbyte | TF_EXEC); }
+#ifdef AVGPU_PHASE_CLOCKS
+    it_fast += __ballot((FAST_OPS & obit) != 0u) != 0ull;
+    it_copy += __ballot(op == AVGPU_H_H_COPY) != 0ull;
+    it_slow += __ballot(!(FAST_OPS & obit) && op != AVGPU_H_H_COPY) != 0ull;
+#endif
 
-    switch (op) {
-      case AVGPU_H_NOP_A: case AVGPU_H_NOP_B: case AVGPU_H_NOP_C:
-        break;
-      case AVGPU_H_IF_N_EQU: {                                // :2190
-        const int a = FMOD(1); const int b = (a + 1) % 3;
-        if (GETREG(a) == GETREG(b)) ip = head_adjust(ip + 1, M);
-        break; }
-      case AVGPU_H_IF_LESS: {                                 // :2235
-        const int a = FMOD(1); const int b = (a + 1) % 3;
-        if (GETREG(a) >= GETREG(b)) ip = head_adjust(ip + 1, M);
-        break; }
+    if (FAST_OPS & obit) {
+      // ---- branch-free ops: register ALU, swap, conditionals, head moves ----
+      const int rn = (r == 2) ? 0 : r + 1;                    // FindNextRegister :1676
+      const int ra = (r == 0) ? r0 : ((r == 1) ? r1 : r2);
+      const int rb = (rn == 0) ? r0 : ((rn == 1) ? r1 : r2);
+      int res = ~(r1 & r2);                                                  // nand :3018
+      res = (op == AVGPU_H_ADD) ? (int)((uint32_t)r1 + (uint32_t)r2) : res;  // add :2959
+      res = (op == AVGPU_H_SUB) ? (int)((uint32_t)r1 - (uint32_t)r2) : res;  // sub :2968
+      res = (op == AVGPU_H_INC) ? (int)((uint32_t)ra + 1u) : res;            // inc :2864
+      res = (op == AVGPU_H_DEC) ? (int)((uint32_t)ra - 1u) : res;            // dec :2871
+      res = (op == AVGPU_H_SHIFT_R) ? (ra >> 1) : res;                       // shift-r :2806
+      res = (op == AVGPU_H_SHIFT_L) ? (int)((uint32_t)ra << 1) : res;        // shift-l :2813
+      res = (op == AVGPU_H_SWAP) ? rb : res;                                 // swap :2742
+      const bool wr = (WR_OPS & obit) != 0u;
+      const bool sw = op == AVGPU_H_SWAP;
+      // head ops: head id = nop-mod or IP (mov-head :6809, jmp-head :6859, get-head :6907)
+      const int hv = (r == 0) ? ip : ((r == 1) ? rh : wh);
+      const bool hw = op == AVGPU_H_MOV_HEAD || op == AVGPU_H_JMP_HEAD;
+      int hnew = fh;                                                         // mov-head: Set(FLOW), no adjust
+      if (op == AVGPU_H_JMP_HEAD) hnew = head_adjust((int)((uint32_t)hv + (uint32_t)r2), M);
+      r0 = (wr && r == 0) ? res : ((sw && rn == 0) ? ra : r0);
+      r1 = (wr && r == 1) ? res : ((sw && rn == 1) ? ra : r1);
+      r2 = (wr && r == 2) ? res : ((sw && rn == 2) ? ra : r2);
+      r2 = (op == AVGPU_H_GET_HEAD) ? hv : r2;
+      rh = (hw && r == 1) ? hnew : rh;
+      wh = (hw && r == 2) ? hnew : wh;
+      if (op == AVGPU_H_SET_FLOW) fh = head_adjust(ra, M);                   // set-flow :7270
+      if (hw && r == 0) ip = hnew;
+      adv = !(op == AVGPU_H_MOV_HEAD && r == 0);
+      // if-n-equ :2190 / if-less :2235 skip the next instruction
+      const bool skip = (op == AVGPU_H_IF_N_EQU && ra == rb) || (op == AVGPU_H_IF_LESS && ra >= rb);
+      if (skip) ip = head_adjust(ip + 1, M);
+      ctl ^= (op == AVGPU_H_SWAP_STK) ? CTL_CURSTK : 0u;                     // swap-stk :2739
+    } else if (op == AVGPU_H_H_COPY) {                        // :7130 Inst_HeadCopy
+      rh = head_adjust(rh, M);
+      wh = head_adjust(wh, M);
+      int v = T[rh] & CODE_MASK;
+      // ReadInst (:1459-1466)
+      if (v < 3) {
+        const int len = rl & 15;
+        if (len < AVGPU_MAX_LABEL) rl = (rl & ~15u) | (uint32_t)(len + 1) | ((uint32_t)v << (4 + 2 * len));
+      } else {
+        rl = 0;
+      }
+      if (mode != AVGPU_MODE_TEST && W.th_copy_mut && rng_p(klo, khi, kct, W.th_copy_mut))
+        v = rand_code();
+      T[wh] = (uint8_t)((T[wh] & TF_EXEC) | TF_COPIED | v);
+      rh = head_adjust(rh + 1, M);
+      wh = head_adjust(wh + 1, M);
+    } else switch (op) {
       case AVGPU_H_POP: {                                     // :2698, cCPUStack::Pop
-        const int r = FMOD(1);
         const int k = (ctl & CTL_CURSTK) ? 1 : 0;
         int sp = k ? CTL_SP1(ctl) : CTL_SP0(ctl);
         int32_t* slot = stk + (k * AVGPU_STACK_SIZE + sp) * 64 + lane;
@@ -222,30 +315,13 @@ __global__ __launch_bounds__(64) void k_interpret(DevWorld W, int cls, int mode,
         SETREG(r, v);
         break; }
       case AVGPU_H_PUSH: {                                    // :2705, cCPUStack::Push
-        const int r = FMOD(1);
         const int k = (ctl & CTL_CURSTK) ? 1 : 0;
         int sp = k ? CTL_SP1(ctl) : CTL_SP0(ctl);
         sp = (sp == 0) ? AVGPU_STACK_SIZE - 1 : sp - 1;
         stk[(k * AVGPU_STACK_SIZE + sp) * 64 + lane] = GETREG(r);
         ctl = k ? ((ctl & ~0xF0u) | ((uint32_t)sp << 4)) : ((ctl & ~0xFu) | (uint32_t)sp);
         break; }
-      case AVGPU_H_SWAP_STK:                                  // :2739
-        ctl ^= CTL_CURSTK;
-        break;
-      case AVGPU_H_SWAP: {                                    // :2742
-        const int a = FMOD(1); const int b = (a + 1) % 3;
-        const int va = GETREG(a), vb = GETREG(b);
-        SETREG(a, vb); SETREG(b, va);
-        break; }
-      case AVGPU_H_SHIFT_R: { const int r = FMOD(1); SETREG(r, GETREG(r) >> 1); break; }
-      case AVGPU_H_SHIFT_L: { const int r = FMOD(1); SETREG(r, (int)((uint32_t)GETREG(r) << 1)); break; }
-      case AVGPU_H_INC: { const int r = FMOD(1); SETREG(r, (int)((uint32_t)GETREG(r) + 1u)); break; }
-      case AVGPU_H_DEC: { const int r = FMOD(1); SETREG(r, (int)((uint32_t)GETREG(r) - 1u)); break; }
-      case AVGPU_H_ADD: { const int r = FMOD(1); SETREG(r, (int)((uint32_t)r1 + (uint32_t)r2)); break; }
-      case AVGPU_H_SUB: { const int r = FMOD(1); SETREG(r, (int)((uint32_t)r1 - (uint32_t)r2)); break; }
-      case AVGPU_H_NAND: { const int r = FMOD(1); SETREG(r, ~(r1 & r2)); break; }
       case AVGPU_H_IO: {                                      // :4188 Inst_TaskIO
-        const int r = FMOD(1);
         const int out = GETREG(r);
         // cOrganism::DoOutput -> cTaskLib::SetupTests (main/cTaskLib.cc:369-448)
         outv = out;
@@ -467,23 +543,6 @@ __global__ __launch_bounds__(64) void k_interpret(DevWorld W, int cls, int mode,
         }
         adv = false;
         break; }
-      case AVGPU_H_H_COPY: {                                  // :7130 Inst_HeadCopy
-        rh = head_adjust(rh, M);
-        wh = head_adjust(wh, M);
-        int v = T[rh] & CODE_MASK;
-        // ReadInst (:1459-1466)
-        if (v < 3) {
-          const int len = rl & 15;
-          if (len < AVGPU_MAX_LABEL) rl = (rl & ~15u) | (uint32_t)(len + 1) | ((uint32_t)v << (4 + 2 * len));
-        } else {
-          rl = 0;
-        }
-        if (mode != AVGPU_MODE_TEST && W.th_copy_mut && rng_p(klo, khi, kct, W.th_copy_mut))
-          v = rand_code();
-        T[wh] = (uint8_t)((T[wh] & TF_EXEC) | TF_COPIED | v);
-        rh = head_adjust(rh + 1, M);
-        wh = head_adjust(wh + 1, M);
-        break; }
       case AVGPU_H_H_SEARCH:                                  // :7245 Inst_HeadSearch
       case AVGPU_H_IF_LABEL: {                                // :6914 Inst_IfLabel
         // ReadLabel (:1484-1502): the up to 10 sites after IP come from one
@@ -554,27 +613,9 @@ __global__ __launch_bounds__(64) void k_interpret(DevWorld W, int cls, int mode,
         r2 = len;
         fh = head_adjust(found + 1, M);
         break; }
-      case AVGPU_H_MOV_HEAD: {                                // :6809
-        const int h = FMOD(0);
-        SETHEAD(h, fh);
-        if (h == 0) adv = false;
-        break; }
-      case AVGPU_H_JMP_HEAD: {                                // :6859
-        const int h = FMOD(0);
-        SETHEAD(h, head_adjust((int)((uint32_t)GETHEAD(h) + (uint32_t)r2), M));
-        break; }
-      case AVGPU_H_GET_HEAD: {                                // :6907
-        const int h = FMOD(0);
-        r2 = GETHEAD(h);
-        break; }
-      case AVGPU_H_SET_FLOW: {                                // :7270
-        const int r = FMOD(2);
-        fh = head_adjust(GETREG(r), M);
-        break; }
       default:
         break;
     }
-#undef FMOD
     if (stop) break;
     if (adv) ip = head_adjust(ip + 1, M);                     // ip.Advance() :1013
     if (mx > 0 && tu >= mx) alive = false;                    // death :1045-1049
@@ -585,6 +626,9 @@ __global__ __launch_bounds__(64) void k_interpret(DevWorld W, int cls, int mode,
 #undef SETHEAD
 
   // ---- write back ----
+#ifdef AVGPU_PHASE_CLOCKS
+  const uint64_t clk2 = __builtin_amdgcn_s_memtime();
+#endif
   __syncthreads();
   if (active) {
     W.reg[cell] = r0; W.reg[N + cell] = r1; W.reg[2 * N + cell] = r2;
@@ -624,29 +668,64 @@ __global__ __launch_bounds__(64) void k_interpret(DevWorld W, int cls, int mode,
   int dead = (active && !alive) ? 1 : 0;
   int dv = divides;
   int mxe = executed;
+  int sl = active ? 1 : 0;
+  int sites = active ? m_in + M : 0;
   for (int off = 32; off > 0; off >>= 1) {
     e += __shfl_down(e, off);
     dead += __shfl_down(dead, off);
     dv += __shfl_down(dv, off);
     mxe = max(mxe, __shfl_down(mxe, off));
+    sl += __shfl_down(sl, off);
+    sites += __shfl_down(sites, off);
   }
   if (lane == 0) {
     count_add(W, CNT_LANESTEPS, 64ull * (unsigned long long)mxe);   // issued lane-steps
     count_add(W, CNT_INSTS, e);
     if (dead) count_add(W, CNT_DEATHS, (unsigned long long)dead);
     if (dv) count_add(W, CNT_DIVIDES, (unsigned long long)dv);
+    if (cls == 0) {
+      count_add(W, CNT_C0_SLICES, (unsigned long long)sl);
+      count_add(W, CNT_C0_SITES, (unsigned long long)sites);
+    }
   }
+#ifdef AVGPU_PHASE_CLOCKS
+  {
+    const uint64_t clk3 = __builtin_amdgcn_s_memtime();
+    for (int off = 32; off > 0; off >>= 1) {
+      it_fast = max(it_fast, __shfl_down(it_fast, off));
+      it_copy = max(it_copy, __shfl_down(it_copy, off));
+      it_slow = max(it_slow, __shfl_down(it_slow, off));
+    }
+    if (lane == 0 && cls == 0) {
+      count_add(W, CNT_CLK_STAGE, clk1 - clk0);
+      count_add(W, CNT_CLK_LOOP, clk2 - clk1);
+      count_add(W, CNT_CLK_WB, clk3 - clk2);
+      count_add(W, CNT_ITERS, (unsigned long long)mxe);
+      count_add(W, CNT_IT_FAST, (unsigned long long)it_fast);
+      count_add(W, CNT_IT_COPY, (unsigned long long)it_copy);
+      count_add(W, CNT_IT_SLOW, (unsigned long long)it_slow);
+      count_add(W, CNT_WAVES, 1ull);
+    }
+  }
+#endif
 }
 
 }  // namespace
 
 void launch_interpret_classes(const DevWorld& W, int mode, hipStream_t s, int64_t first,
-                              int64_t count, int* launches) {
+                              int64_t count, int* launches, hipEvent_t* after_class) {
   const unsigned blocks = (unsigned)((count + 63) / 64);
-  if (blocks == 0) return;
-  hipLaunchKernelGGL(k_interpret<CLASS0_SIZE>, dim3(blocks), dim3(64), 0, s, W, 0, mode, first, count);
-  hipLaunchKernelGGL(k_interpret<768>, dim3(blocks), dim3(64), 0, s, W, 1, mode, first, count);
-  hipLaunchKernelGGL(k_interpret<1536>, dim3(blocks), dim3(64), 0, s, W, 2, mode, first, count);
-  hipLaunchKernelGGL(k_interpret<2048>, dim3(blocks), dim3(64), 0, s, W, 3, mode, first, count);
-  if (launches) *launches += 4;
+  if (blocks > 0) {
+    hipLaunchKernelGGL(k_interpret<CLASS0_SIZE>, dim3(blocks), dim3(64), 0, s, W, 0, mode, first, count);
+    if (after_class) hipEventRecord(after_class[0], s);
+    hipLaunchKernelGGL(k_interpret<768>, dim3(blocks), dim3(64), 0, s, W, 1, mode, first, count);
+    if (after_class) hipEventRecord(after_class[1], s);
+    hipLaunchKernelGGL(k_interpret<1536>, dim3(blocks), dim3(64), 0, s, W, 2, mode, first, count);
+    if (after_class) hipEventRecord(after_class[2], s);
+    hipLaunchKernelGGL(k_interpret<2048>, dim3(blocks), dim3(64), 0, s, W, 3, mode, first, count);
+    if (launches) *launches += 4;
+  } else if (after_class) {
+    for (int k = 0; k < 3; k++) hipEventRecord(after_class[k], s);
+  }
+  if (after_class) hipEventRecord(after_class[3], s);
 }

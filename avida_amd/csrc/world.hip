@@ -417,10 +417,21 @@ __global__ __launch_bounds__(64) void k_activate(DevWorld W) {
 // 6 generation 7 memory size 8..16 task organisms
 #define NPART 24
 #define NSTAT 40
+__device__ __forceinline__ double wave_sum(double v) {
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+  return v;
+}
+__device__ __forceinline__ double wave_max(double v) {
+  for (int off = 32; off > 0; off >>= 1) v = fmax(v, __shfl_xor(v, off));
+  return v;
+}
+// part layout [NPART][nb] so that k_stats_final reads it coalesced
 __global__ __launch_bounds__(256) void k_stats_partial(DevWorld W, double* part) {
-  __shared__ double s[NPART][256];
+  __shared__ double s[4][NPART];
   const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
   double v[NPART];
+#pragma unroll
   for (int k = 0; k < NPART; k++) v[k] = 0.0;
   if (c < W.n && (W.ctl[c] & CTL_ALIVE)) {
     v[0] = 1.0;
@@ -431,58 +442,63 @@ __global__ __launch_bounds__(256) void k_stats_partial(DevWorld W, double* part)
     v[5] = W.fitness[c];   // max
     v[6] = (double)W.generation[c];
     v[7] = (double)W.mem_size[c];
+#pragma unroll
     for (int t = 0; t < AVGPU_NUM_LOGIC_TASKS; t++) v[8 + t] = W.last_task[t * W.n + c] > 0 ? 1.0 : 0.0;
   }
-  for (int k = 0; k < NPART; k++) s[k][threadIdx.x] = v[k];
-  __syncthreads();
-  for (int stride = 128; stride >= 1; stride >>= 1) {
-    if ((int)threadIdx.x < stride)
-      for (int k = 0; k < NPART; k++) {
-        const double o = s[k][threadIdx.x + stride];
-        s[k][threadIdx.x] = (k == 5) ? fmax(s[k][threadIdx.x], o) : s[k][threadIdx.x] + o;
-      }
-    __syncthreads();
+#pragma unroll
+  for (int k = 0; k < NPART; k++) {
+    const double r = (k == 5) ? wave_max(v[k]) : wave_sum(v[k]);
+    if (lane == 0) s[wv][k] = r;
   }
-  if (threadIdx.x < NPART) part[blockIdx.x * NPART + threadIdx.x] = s[threadIdx.x][0];
+  __syncthreads();
+  if (threadIdx.x < NPART) {
+    const int k = threadIdx.x;
+    double r = s[0][k];
+    for (int q = 1; q < 4; q++) r = (k == 5) ? fmax(r, s[q][k]) : r + s[q][k];
+    part[(int64_t)k * gridDim.x + blockIdx.x] = r;
+  }
 }
 
 // out: [0..23] partial sums, 24 insts 25 deaths 26 divides 27 births 28 dropped
-// 29 spills 30 cumulative insts 31 cumulative births 32 slices
+// 29 spills 30 cumulative insts 31 cumulative births 32 slices 33 lane steps
 __global__ __launch_bounds__(256) void k_stats_final(DevWorld W, const double* part, int64_t nb,
                                                      double* out) {
-  __shared__ double s[256];
-  const int tid = threadIdx.x;
-  for (int k = 0; k < NPART; k++) {
+  __shared__ unsigned long long cs[8][CNT_STRIDE];
+  const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
+  for (int k = wv; k < NPART; k += 4) {
     double acc = 0.0;
-    for (int64_t b = tid; b < nb; b += 256) {
-      const double o = part[b * NPART + k];
+    for (int64_t b = lane; b < nb; b += 64) {
+      const double o = part[(int64_t)k * nb + b];
       acc = (k == 5) ? fmax(acc, o) : acc + o;
     }
-    s[tid] = acc;
-    __syncthreads();
-    for (int stride = 128; stride >= 1; stride >>= 1) {
-      if (tid < stride) s[tid] = (k == 5) ? fmax(s[tid], s[tid + stride]) : s[tid] + s[tid + stride];
-      __syncthreads();
-    }
-    if (tid == 0) out[k] = s[0];
-    __syncthreads();
+    acc = (k == 5) ? wave_max(acc) : wave_sum(acc);
+    if (lane == 0) out[k] = acc;
   }
+  {
+    const int slot = tid & (CNT_STRIDE - 1), g = tid / CNT_STRIDE;   // 8 groups of shards
+    unsigned long long a = 0;
+    for (int sh = g; sh < NSHARD; sh += 8) a += W.counters[sh * CNT_STRIDE + slot];
+    cs[g][slot] = a;
+  }
+  __syncthreads();
+  if (tid < CNT_STRIDE) {
+    unsigned long long t = 0;
+    for (int g = 0; g < 8; g++) t += cs[g][tid];
+    cs[0][tid] = t;
+    W.counters[CNT_CUM_BASE + tid] += t;
+  }
+  __syncthreads();
   if (tid == 0) {
-    unsigned long long c[CNT_STRIDE] = {0};
-    for (int sh = 0; sh < NSHARD; sh++)
-      for (int k = 0; k < CNT_STRIDE; k++) c[k] += W.counters[sh * CNT_STRIDE + k];
-    W.counters[CNT_CUM_INSTS] += c[CNT_INSTS];
-    W.counters[CNT_CUM_BIRTHS] += c[CNT_BIRTHS];
-    out[24] = (double)c[CNT_INSTS];
-    out[25] = (double)c[CNT_DEATHS];
-    out[26] = (double)c[CNT_DIVIDES];
-    out[27] = (double)c[CNT_BIRTHS];
-    out[28] = (double)c[CNT_DROPPED];
-    out[29] = (double)c[CNT_SPILLS];
+    out[24] = (double)cs[0][CNT_INSTS];
+    out[25] = (double)cs[0][CNT_DEATHS];
+    out[26] = (double)cs[0][CNT_DIVIDES];
+    out[27] = (double)cs[0][CNT_BIRTHS];
+    out[28] = (double)cs[0][CNT_DROPPED];
+    out[29] = (double)cs[0][CNT_SPILLS];
     out[30] = (double)W.counters[CNT_CUM_INSTS];
     out[31] = (double)W.counters[CNT_CUM_BIRTHS];
-    out[32] = (double)c[CNT_SLICES];
-    out[33] = (double)c[CNT_LANESTEPS];
+    out[32] = (double)cs[0][CNT_SLICES];
+    out[33] = (double)cs[0][CNT_LANESTEPS];
   }
 }
 

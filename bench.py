@@ -31,8 +31,13 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "organism-instructions/sec + updates/sec, 1M-org logic-9 world, 1/8 GPUs"
-STATE_BYTES_PER_SLICE = 140   # hot state read + write per organism time slice
+# SURVEY.md 8(d) algorithmic bytes: per organism time slice the packed
+# architectural + phenotype state (224 B) is read and written, and the memory
+# tape at 1.25 B/site (op byte + 2 flag bits) is read and written.
+STATE_BYTES = 224.0
+SITE_BYTES = 1.25
 HBM_PEAK_GBS = 8000.0         # MI355X_MICROARCH.md chip table (spec)
+PMC_FILE = os.path.join(ROOT, "profiles", "pmc_k_interpret384.json")
 
 
 def _pool(golden):
@@ -145,8 +150,10 @@ def main():
     torch.cuda.synchronize()
     s0 = capi.AvgpuUpdateStats()
     capi.check(lib, lib.avgpu_get_stats(h, C.byref(s0)))
-    kms, phases = C.c_double(), C.c_int64()
-    capi.check(lib, lib.avgpu_last_kernel_ms(h, C.byref(kms), C.byref(phases)))  # reset
+    cms, phases = (C.c_double * 4)(), C.c_int64()
+    capi.check(lib, lib.avgpu_kernel_times(h, cms, C.byref(phases)))  # reset
+    cnt0 = (C.c_int64 * capi.NUM_COUNTERS)()
+    capi.check(lib, lib.avgpu_counters(h, 1, cnt0, capi.NUM_COUNTERS))
 
     if dist:
         dist.barrier()
@@ -161,35 +168,45 @@ def main():
 
     s1 = capi.AvgpuUpdateStats()
     capi.check(lib, lib.avgpu_get_stats(h, C.byref(s1)))
-    capi.check(lib, lib.avgpu_last_kernel_ms(h, C.byref(kms), C.byref(phases)))
+    capi.check(lib, lib.avgpu_kernel_times(h, cms, C.byref(phases)))
+    cnt1 = (C.c_int64 * capi.NUM_COUNTERS)()
+    capi.check(lib, lib.avgpu_counters(h, 1, cnt1, capi.NUM_COUNTERS))
     insts = s1.cum_insts_executed - s0.cum_insts_executed
     births = s1.cum_births - s0.cum_births
     dt = t1 - t0
-    vec = torch.tensor([dt, float(insts), float(births), float(s1.num_organisms),
-                        kms.value, float(phases.value), float(s1.slices), s1.sum_mem_size],
+    vec = torch.tensor([dt, float(insts), float(births), float(s1.num_organisms)],
                        dtype=torch.float64, device="cuda")
     if dist:
         mx = vec.clone()
         dist.all_reduce(mx, op=dist.ReduceOp.MAX)
         dist.all_reduce(vec)
         dt_max = mx[0].item()
-        kernel_ms_avg = mx[4].item() / max(1.0, mx[5].item())
     else:
         dt_max = vec[0].item()
-        kernel_ms_avg = vec[4].item() / max(1.0, vec[5].item())
     tot_insts, tot_births, tot_orgs = vec[1].item(), vec[2].item(), vec[3].item()
+    d = [cnt1[k] - cnt0[k] for k in range(capi.NUM_COUNTERS)]
+    nph = max(1, phases.value)
     if rank != 0:
         if dist:
             dist.destroy_process_group()
         return
     value = tot_insts / dt_max
-    # roofline of the dominant kernel (k_interpret, all size classes of one
-    # update = one "launch" phase): algorithmic bytes = per slice the hot state
-    # (STATE_BYTES_PER_SLICE) + memory tape read and written once (2 B/site).
-    slices = s1.slices
-    mean_mem = s1.sum_mem_size / max(1, s1.num_organisms)
-    bytes_per_phase = slices * (STATE_BYTES_PER_SLICE + 2.0 * mean_mem)
-    achieved = bytes_per_phase / (kernel_ms_avg * 1e-3) / 1e9 if kernel_ms_avg > 0 else 0.0
+    # roofline of the dominant kernel k_interpret<384> (LDS size class 0, one
+    # launch per update), this rank: algorithmic bytes per launch =
+    # slices * 2 * 224 B + tape sites staged in and written back * 1.25 B,
+    # over its HIP-event-timed average duration on the world's stream.
+    c0_ms = cms[0] / nph
+    c0_slices = d[capi.CNT_C0_SLICES] / nph
+    c0_sites = d[capi.CNT_C0_SITES] / nph
+    bytes_per_launch = 2.0 * STATE_BYTES * c0_slices + SITE_BYTES * c0_sites
+    achieved = bytes_per_launch / (c0_ms * 1e-3) / 1e9 if c0_ms > 0 else 0.0
+    traffic, traffic_src = None, None
+    if os.path.exists(PMC_FILE):
+        with open(PMC_FILE) as f:
+            pmc = json.load(f)
+        if pmc.get("world") == f"{args.side}x{args.side}":
+            traffic = pmc["hbm_bytes_per_launch"]
+            traffic_src = pmc["source"]
     out = {
         "metric": METRIC,
         "value": value,
@@ -220,13 +237,17 @@ def main():
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS,
-            "traffic": None,
-            "kernel": "k_interpret (all LDS size classes of one update)",
-            "kernel_ms": kernel_ms_avg,
-            "bytes_per_launch": bytes_per_phase,
-            "mean_mem_sites": mean_mem,
-            "slices_per_launch": slices,
-            "lane_efficiency": s1.insts_executed / max(1, s1.lane_steps),
+            "traffic": traffic,
+            "traffic_source": traffic_src,
+            "kernel": "k_interpret<384> (LDS size class 0)",
+            "kernel_ms": c0_ms,
+            "bytes_per_launch": bytes_per_launch,
+            "slices_per_launch": c0_slices,
+            "mean_sites_per_slice": c0_sites / max(1.0, 2.0 * c0_slices),
+            "all_classes_ms": sum(cms) / nph,
+            "class_ms": [x / nph for x in cms],
+            "lane_efficiency": d[capi.CNT_INSTS] / max(1, d[capi.CNT_LANESTEPS]),
+            "insts_per_kernel_second": d[capi.CNT_INSTS] / max(1e-9, sum(cms) * 1e-3),
         },
         "cpu_baseline": None,
     }

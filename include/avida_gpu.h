@@ -335,6 +335,29 @@ int avgpu_last_step_insts(avgpu_world* w, int64_t* insts);
  * every k_interpret launch sequence) accumulated since the previous call:
  * total milliseconds and number of interpret phases; resets the accumulator. */
 int avgpu_last_kernel_ms(avgpu_world* w, double* ms, int64_t* launches);
+/* The same accumulators split by interpreter size class (k_interpret<384>,
+ * <768>, <1536>, <2048>): class_ms[4] milliseconds and the number of interpret
+ * phases since the previous call; resets them (and avgpu_last_kernel_ms's). */
+int avgpu_kernel_times(avgpu_world* w, double* class_ms, int64_t* phases);
+
+/* Device event counters (no reference equivalent: measurement only).
+ * cumulative = 0: the last update (or avgpu_step); 1: summed over every
+ * avgpu_run_update/update_run since creation.  Slots: */
+enum avgpu_counter {
+  AVGPU_CNT_INSTS = 0,      /* instructions executed (count.dat "insts executed") */
+  AVGPU_CNT_DEATHS = 1,
+  AVGPU_CNT_DIVIDES = 2,
+  AVGPU_CNT_BIRTHS = 3,
+  AVGPU_CNT_DROPPED = 4,    /* offspring not placed */
+  AVGPU_CNT_SPILLS = 5,     /* slices handed to a larger LDS size class */
+  AVGPU_CNT_SLICES = 6,     /* organisms with a non-zero allotment */
+  AVGPU_CNT_LANESTEPS = 7,  /* 64 x longest lane per wave (lane efficiency = INSTS / this) */
+  AVGPU_CNT_C0_SLICES = 8,  /* slices run by the class-0 (<=384 sites) launch */
+  AVGPU_CNT_C0_SITES = 9,   /* tape sites that launch staged in plus wrote back */
+  /* 10..17: per-phase clocks of diagnostic (AVGPU_PHASE_CLOCKS) builds */
+  AVGPU_NUM_COUNTERS = 32
+};
+int avgpu_counters(avgpu_world* w, int cumulative, int64_t* out, int n);
 
 #ifdef __cplusplus
 }

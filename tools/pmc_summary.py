@@ -1,0 +1,47 @@
+"""Average rocprofv3 --pmc counters per dispatch for kernels matching a regex.
+
+usage: python tools/pmc_summary.py 'gpurun_out/pmc_TAG_*/**/*counter_collection.csv' [regex]
+       [--json OUT --world 1024x1024 --source TEXT]
+
+With --json, also writes the HBM traffic per launch of the matched kernel
+(MI355X_MICROARCH.md "HBM": FETCH_SIZE on gfx950 reports half of the bytes of
+a coalesced read, so traffic = 2 * FETCH_SIZE + WRITE_SIZE; both in KiB)."""
+import argparse
+import csv
+import glob
+import json
+import re
+from collections import defaultdict
+
+
+def summarize(pattern, regex="k_interpret<384>|k_interpretILi384"):
+    vals = defaultdict(list)
+    for f in sorted(glob.glob(pattern, recursive=True)):
+        with open(f) as fh:
+            for row in csv.DictReader(fh):
+                if not re.search(regex, row.get("Kernel_Name", "")):
+                    continue
+                vals[row["Counter_Name"]].append(float(row["Counter_Value"]))
+    return {k: sum(v) / len(v) for k, v in vals.items()}, {k: len(v) for k, v in vals.items()}
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("pattern")
+    ap.add_argument("regex", nargs="?", default="k_interpret<384>|k_interpretILi384")
+    ap.add_argument("--json")
+    ap.add_argument("--world", default="1024x1024")
+    ap.add_argument("--source", default="")
+    a = ap.parse_args()
+    avg, n = summarize(a.pattern, a.regex)
+    for k in sorted(avg):
+        print("%-28s %18.1f  (n=%d)" % (k, avg[k], n[k]))
+    if a.json:
+        fetch = avg.get("FETCH_SIZE", 0.0) * 1024.0
+        write = avg.get("WRITE_SIZE", 0.0) * 1024.0
+        out = {"kernel": a.regex, "world": a.world, "source": a.source,
+               "fetch_size_bytes": fetch, "write_size_bytes": write,
+               "hbm_bytes_per_launch": 2.0 * fetch + write,
+               "counters_per_dispatch": avg}
+        with open(a.json, "w") as f:
+            json.dump(out, f, indent=1)

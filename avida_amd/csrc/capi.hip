@@ -48,6 +48,9 @@ struct avgpu_world {
   double acc_class_ms[NUM_CLASSES] = {};
   int64_t acc_phases = 0;
   DevWorld W;
+  DevWorld* d_W = nullptr;      // device copy of W read by k_interpret
+  DevWorld pushed;              // what d_W holds
+  bool pushed_valid = false;
   std::vector<void*> allocs;
   // instruction set translation
   int n_ops = 0;
@@ -96,17 +99,22 @@ int setup_world(avgpu_world* w, int64_t n, bool test_buffers) {
   A(cur_bonus, n); A(merit, n); A(fitness, n); A(credit, n); A(gest_time, n); A(num_div, n);
   A(generation, n); A(copied, n); A(child_copied, n); A(executed, n); A(errors, n);
   A(class_list, NUM_CLASSES * n); A(class_count, NUM_CLASSES); A(counters, CNT_WORDS);
-  W.bcap = test_buffers ? 16 : std::max<int64_t>(4096, n / 2);
-  A(b_count, 1); A(b_parent, W.bcap); A(b_seq, W.bcap); A(b_len, W.bcap); A(b_merit, W.bcap);
-  A(b_fitness, W.bcap); A(b_gen, W.bcap); A(b_ccopied, W.bcap); A(b_exec, W.bcap);
-  A(b_gest, W.bcap); A(b_rng, 3 * W.bcap); A(b_target, W.bcap); A(b_state, W.bcap);
-  A(b_prio, W.bcap); A(b_genome, (size_t)W.bcap * TAPE_SLOT);
+  // birth records: one primary record per cell + overflow for further
+  // offspring of one slice (device.h); test worlds never enqueue births
+  W.rcap = n + (test_buffers ? 16 : std::max<int64_t>(4096, n / 4));
+  const int64_t R = W.rcap;
+  A(b_count, 2); A(b_list, n); A(b_parent, R); A(b_seq, R); A(b_len, R); A(b_merit, R);
+  A(b_fitness, R); A(b_gen, R); A(b_ccopied, R); A(b_exec, R);
+  A(b_gest, R); A(b_rng, 3 * R); A(b_target, R); A(b_state, R);
+  A(b_prio, R); A(b_genome, (size_t)R * TAPE_SLOT);
   A(occ, n); A(claim, n); A(owner, n);
   if (test_buffers) {
     A(t_flags, (size_t)n * TAPE_SLOT); A(t_flags_len, n); A(t_child, (size_t)n * TAPE_SLOT);
     A(t_child_len, n);
   }
-  A(rand_cum, 64); A(rand_code, 64); A(task_lut, 256);
+  A(rand_cum, 64); A(rand_code, 64); A(task_lut, 256); A(rand_lut, 256);
+  A(react_tab, AVGPU_MAX_REACTIONS * RT_STRIDE);
+  if ((rc = w->alloc(&w->d_W, 1))) return rc;
   const int64_t nb = (n + 255) / 256;
   if ((rc = w->alloc(&w->d_totals, (size_t)(8 + 2 * nb)))) return rc;
   if ((rc = w->alloc(&w->d_stats, (size_t)(40 + 24 * nb)))) return rc;
@@ -195,13 +203,9 @@ int copy_tables(avgpu_world* dst, const avgpu_world* src) {
   const DevWorld& S = src->W;
   D.n_ops = S.n_ops; D.rand_total = S.rand_total; D.fill_code = S.fill_code;
   D.n_react = S.n_react;
-  memcpy(D.react_task, S.react_task, sizeof(D.react_task));
-  memcpy(D.react_type, S.react_type, sizeof(D.react_type));
-  memcpy(D.react_min, S.react_min, sizeof(D.react_min));
-  memcpy(D.react_max, S.react_max, sizeof(D.react_max));
-  memcpy(D.react_hasreq, S.react_hasreq, sizeof(D.react_hasreq));
-  memcpy(D.react_mult, S.react_mult, sizeof(D.react_mult));
-  memcpy(D.react_add, S.react_add, sizeof(D.react_add));
+  HIPCHK(hipMemcpy(D.react_tab, S.react_tab, AVGPU_MAX_REACTIONS * RT_STRIDE * sizeof(int32_t),
+                   hipMemcpyDeviceToDevice));
+  HIPCHK(hipMemcpy(D.rand_lut, S.rand_lut, 256, hipMemcpyDeviceToDevice));
   HIPCHK(hipMemcpy(D.rand_cum, S.rand_cum, 64 * sizeof(int32_t), hipMemcpyDeviceToDevice));
   HIPCHK(hipMemcpy(D.rand_code, S.rand_code, 64, hipMemcpyDeviceToDevice));
   dst->n_ops = src->n_ops;
@@ -290,13 +294,27 @@ int drain_ring(avgpu_world* w, int keep) {
   return 0;
 }
 
+// refresh the device copy of the world descriptor when the host copy changed
+int push_world(avgpu_world* w) {
+  if (w->pushed_valid && memcmp(&w->pushed, &w->W, sizeof(DevWorld)) == 0) return 0;
+  HIPCHK(hipMemcpyAsync(w->d_W, &w->W, sizeof(DevWorld), hipMemcpyHostToDevice, w->stream));
+  HIPCHK(hipStreamSynchronize(w->stream));
+  memcpy(&w->pushed, &w->W, sizeof(DevWorld));
+  w->pushed_valid = true;
+  return 0;
+}
+
 int interpret(avgpu_world* w, int mode, int64_t first, int64_t count) {
   int launches = 0;
+  {
+    const int prc = push_world(w);
+    if (prc < 0) return prc;
+  }
   int rc = drain_ring(w, avgpu_world::RING - 1);
   if (rc < 0) return rc;
   const int i = w->ring_head;
   HIPCHK(hipEventRecord(w->ring[i][0], w->stream));
-  launch_interpret_classes(w->W, mode, w->stream, first, count, &launches, &w->ring[i][1]);
+  launch_interpret_classes(w->W, w->d_W, mode, w->stream, first, count, &launches, &w->ring[i][1]);
   HIPCHK(hipGetLastError());
   w->ring_head = (i + 1) % avgpu_world::RING;
   w->ring_count++;
@@ -385,6 +403,15 @@ int avgpu_load_instset(avgpu_world* w, int n, const uint8_t* handler_id, const i
   w->W.fill_code = code[0];
   HIPCHK(hipMemcpyAsync(w->W.rand_cum, cum, sizeof(cum), hipMemcpyHostToDevice, w->stream));
   HIPCHK(hipMemcpyAsync(w->W.rand_code, code, sizeof(code), hipMemcpyHostToDevice, w->stream));
+  // GetRandomInst as one table lookup when the weights fit (cpu/cInstSet.cc:83-88)
+  uint8_t rlut[256];
+  memset(rlut, 0, sizeof(rlut));
+  if (total <= 256)
+    for (int v = 0, i = 0; v < total; v++) {
+      while (i < n - 1 && cum[i] <= v) i++;
+      rlut[v] = code[i];
+    }
+  HIPCHK(hipMemcpyAsync(w->W.rand_lut, rlut, sizeof(rlut), hipMemcpyHostToDevice, w->stream));
   HIPCHK(hipStreamSynchronize(w->stream));
   w->instset_loaded = true;
   return 0;
@@ -393,18 +420,25 @@ int avgpu_load_instset(avgpu_world* w, int n, const uint8_t* handler_id, const i
 int avgpu_load_env(avgpu_world* w, int nreact, const avgpu_reaction* r) {
   if (!w || nreact < 0 || nreact > AVGPU_MAX_REACTIONS) return fail(AVGPU_EINVAL, "reaction count");
   DevWorld& W = w->W;
-  W.n_react = nreact;
+  int32_t tab[AVGPU_MAX_REACTIONS * RT_STRIDE];
+  memset(tab, 0, sizeof(tab));
   for (int i = 0; i < nreact; i++) {
     if (r[i].task < 0 || r[i].task >= AVGPU_NUM_LOGIC_TASKS) return fail(AVGPU_EINVAL, "task id");
-    W.react_task[i] = r[i].task;
-    W.react_type[i] = r[i].type;
-    W.react_min[i] = r[i].min_count;
-    W.react_max[i] = r[i].max_count;
-    W.react_hasreq[i] = r[i].has_requisite;
+    int32_t* t = tab + i * RT_STRIDE;
+    t[RT_TASK] = r[i].task;
+    t[RT_TYPE] = r[i].type;
+    t[RT_MIN] = r[i].min_count;
+    t[RT_MAX] = r[i].max_count;
+    t[RT_HASREQ] = r[i].has_requisite;
+    t[RT_USED] = 1;
     const double bonus = r[i].max_number * r[i].value;  // DoProcesses: consumed * value
-    W.react_mult[i] = (r[i].type == AVGPU_PROC_POW) ? std::pow(2.0, bonus) : bonus;
-    W.react_add[i] = bonus;
+    const double mult = (r[i].type == AVGPU_PROC_POW) ? std::pow(2.0, bonus) : bonus;
+    memcpy(t + RT_MULT, &mult, 8);
+    memcpy(t + RT_ADD, &bonus, 8);
   }
+  W.n_react = nreact;
+  HIPCHK(hipMemcpyAsync(W.react_tab, tab, sizeof(tab), hipMemcpyHostToDevice, w->stream));
+  HIPCHK(hipStreamSynchronize(w->stream));
   w->env_loaded = true;
   return 0;
 }
@@ -443,13 +477,19 @@ int avgpu_step(avgpu_world* w, int64_t first, int64_t count, const int32_t* budg
   if (mode == AVGPU_MODE_TEST && !w->has_test_buffers)
     return fail(AVGPU_ESTATE, "TEST mode needs a test world (avgpu_test_genomes)");
   if (count == 0) return 0;
+  // budgets are below 2^30 (bit 30 tags spilled slices on device, device.h)
+  if (!budget && (budget_uniform < 0 || budget_uniform >= BUDGET_PRIM))
+    return fail(AVGPU_EINVAL, "budget out of range [0, 2^30)");
+  if (budget)
+    for (int64_t i = 0; i < count; i++)
+      if (budget[i] < 0 || budget[i] >= BUDGET_PRIM) return fail(AVGPU_EINVAL, "budget out of range [0, 2^30)");
   int32_t* d_b = nullptr;
   if (budget) {
     HIPCHK(hipMalloc(&d_b, count * sizeof(int32_t)));
     HIPCHK(hipMemcpyAsync(d_b, budget, count * sizeof(int32_t), hipMemcpyHostToDevice, w->stream));
   }
   HIPCHK(hipMemsetAsync(w->W.counters, 0, NSHARD * CNT_STRIDE * sizeof(unsigned long long), w->stream));
-  HIPCHK(hipMemsetAsync(w->W.b_count, 0, sizeof(int32_t), w->stream));
+  HIPCHK(hipMemsetAsync(w->W.b_count, 0, 2 * sizeof(int32_t), w->stream));
   launch_classify_uniform(w->W, w->stream, first, count, d_b, budget_uniform);
   HIPCHK(hipGetLastError());
   rc = interpret(w, mode, first, count);

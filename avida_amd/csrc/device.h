@@ -29,6 +29,11 @@
 #define CTL_ALIVE 0x400u
 
 #define NUM_CLASSES 4
+#define RT_STRIDE 12
+enum { RT_TASK = 0, RT_TYPE = 1, RT_MIN = 2, RT_MAX = 3, RT_HASREQ = 4, RT_USED = 5, RT_MULT = 6, RT_ADD = 8 };
+// budget bit carried by a slice handed to the next size class: its primary
+// birth record is already in use (budgets are < 2^30: avgpu_step checks)
+#define BUDGET_PRIM 0x40000000
 
 struct DevWorld {
   int64_t n;  // cells
@@ -72,23 +77,28 @@ struct DevWorld {
   int32_t* class_list;   // [NUM_CLASSES][n]
   int32_t* class_count;  // [NUM_CLASSES]
   unsigned long long* counters; // [16] insts, deaths, divides, births, dropped, ...
-  // birth queue
-  int64_t bcap;
-  int32_t* b_count;   // [1]
-  int32_t* b_parent;  // [bcap]
-  uint32_t* b_seq;    // [bcap]
-  int32_t* b_len;     // [bcap]
-  double* b_merit;    // [bcap]
-  double* b_fitness;  // [bcap]
-  int32_t* b_gen;     // [bcap]
-  int32_t* b_ccopied; // [bcap]
-  int32_t* b_exec;    // [bcap]
-  int32_t* b_gest;    // [bcap]
-  uint32_t* b_rng;    // [3][bcap]
-  int32_t* b_target;  // [bcap]
-  int8_t* b_state;    // [bcap]  0 pending 1 placed -1 failed
-  unsigned long long* b_prio; // [bcap]
-  uint8_t* b_genome;  // [bcap][TAPE_SLOT]
+  // birth records.  Record r < n holds the first offspring that cell r's
+  // parent produced in its slice (no atomics in the interpreter loop); records
+  // n .. n+ocap-1 hold further offspring of one slice, reserved atomically.
+  // Queue entry i < b_count[0] is record b_list[i]; entry b_count[0] + j is
+  // record n + j (rec_of below).
+  int64_t rcap;       // n + ocap
+  int32_t* b_count;   // [2] primary records listed, overflow records used
+  int32_t* b_list;    // [n] primary record ids, appended per wave after the loop
+  int32_t* b_parent;  // [rcap]
+  uint32_t* b_seq;    // [rcap]
+  int32_t* b_len;     // [rcap]
+  double* b_merit;    // [rcap]
+  double* b_fitness;  // [rcap]
+  int32_t* b_gen;     // [rcap]
+  int32_t* b_ccopied; // [rcap]
+  int32_t* b_exec;    // [rcap]
+  int32_t* b_gest;    // [rcap]
+  uint32_t* b_rng;    // [3][rcap]
+  int32_t* b_target;  // [rcap]
+  int8_t* b_state;    // [rcap]  0 pending 1 placed -1 failed
+  unsigned long long* b_prio; // [rcap]
+  uint8_t* b_genome;  // [rcap][TAPE_SLOT]
   // placement scratch
   uint8_t* occ;       // [n]
   unsigned long long* claim; // [n]
@@ -104,14 +114,11 @@ struct DevWorld {
   uint16_t* task_lut; // [256] logic id -> task bitmask
   int n_ops;
   int32_t rand_total;
+  uint8_t* rand_lut;  // [256] draw -> canonical code when rand_total <= 256
   int n_react;
-  int32_t react_task[AVGPU_MAX_REACTIONS];
-  int32_t react_type[AVGPU_MAX_REACTIONS];
-  int32_t react_min[AVGPU_MAX_REACTIONS];
-  int32_t react_max[AVGPU_MAX_REACTIONS];
-  int32_t react_hasreq[AVGPU_MAX_REACTIONS];
-  double react_mult[AVGPU_MAX_REACTIONS];
-  double react_add[AVGPU_MAX_REACTIONS];
+  // reactions, RT_STRIDE words each: task, process type, requisite min / max
+  // count, has-requisite, in-use, bonus multiplier (f64), bonus addend (f64)
+  int32_t* react_tab; // [AVGPU_MAX_REACTIONS][RT_STRIDE]
   uint8_t fill_code;   // code of op 0 (new sites on allocate)
   // config scalars
   int32_t world_x, world_y, geometry;
@@ -161,6 +168,32 @@ struct DevWorld {
 #define CNT_WORDS (NSHARD * CNT_STRIDE + CNT_STRIDE)
 #define CNT_CUM_INSTS (CNT_CUM_BASE + CNT_INSTS)
 #define CNT_CUM_BIRTHS (CNT_CUM_BASE + CNT_BIRTHS)
+
+__device__ __forceinline__ int queue_len(const DevWorld& W) {
+  const int64_t n = (int64_t)W.b_count[0] + (int64_t)min(W.b_count[1], (int)(W.rcap - W.n));
+  return (int)n;
+}
+__device__ __forceinline__ int64_t rec_of(const DevWorld& W, int64_t i) {
+  const int p = W.b_count[0];
+  return i < p ? (int64_t)W.b_list[i] : W.n + (i - p);
+}
+
+// Stores issued from inside the interpreter loop for write-only data (birth
+// records, test-CPU snapshots) that no later instruction of the kernel reads.
+// As inline asm they are outside the compiler's s_waitcnt bookkeeping, so no
+// loop iteration waits on vmcnt for them: with compiler-visible stores there,
+// every following iteration drained all of the wave's outstanding memory
+// operations (~3000 cycles under load) before its first LDS read.  expcnt(0)
+// lets the data VGPRs be reused immediately.
+__device__ __forceinline__ void st_async_u32(void* p, uint32_t v) {
+  asm volatile("global_store_dword %0, %1, off\n\ts_waitcnt expcnt(0)" ::"v"(p), "v"(v) : "memory");
+}
+__device__ __forceinline__ void st_async_u64(void* p, uint64_t v) {
+  asm volatile("global_store_dwordx2 %0, %1, off\n\ts_waitcnt expcnt(0)" ::"v"(p), "v"(v) : "memory");
+}
+__device__ __forceinline__ void st_async_u8(void* p, uint32_t v) {
+  asm volatile("global_store_byte %0, %1, off\n\ts_waitcnt expcnt(0)" ::"v"(p), "v"(v) : "memory");
+}
 
 // ---------------------------------------------------------------------------
 // RNG spec: identical arithmetic to the oracle's Stream.
@@ -222,9 +255,14 @@ __device__ __forceinline__ void count_add(const DevWorld& W, int slot, unsigned 
 }
 
 // LDS size classes of k_interpret (bytes of tape per lane)
-#define CLASS0_SIZE 384
+// (a block of class S uses 64 x (S + 16) B of LDS for tapes; class 0 is sized
+// so that 5 blocks fit a CU's 160 KiB with the stacks and tables)
+#define CLASS0_SIZE 368
+#define CLASS1_SIZE 768
+#define CLASS2_SIZE 1536
+#define CLASS3_SIZE 2048
 __device__ __forceinline__ int class_of(int need) {
-  return need <= CLASS0_SIZE ? 0 : (need <= 768 ? 1 : (need <= 1536 ? 2 : 3));
+  return need <= CLASS0_SIZE ? 0 : (need <= CLASS1_SIZE ? 1 : (need <= CLASS2_SIZE ? 2 : 3));
 }
 // tape capacity an organism may need this slice: its memory, or the size
 // h-alloc would grow it to when it has not allocated yet
@@ -244,8 +282,10 @@ struct LaunchInfo {
 
 // class 0 runs densely over cells [first, first+count); classes 1..3 over their lists
 // after_class[k] (optional): event recorded after the class-k launch
-void launch_interpret_classes(const DevWorld& W, int mode, hipStream_t s, int64_t first,
-                              int64_t count, int* launches, hipEvent_t* after_class = nullptr);
+// dW: device copy of W (avgpu_world::push_world)
+void launch_interpret_classes(const DevWorld& W, const DevWorld* dW, int mode, hipStream_t s,
+                              int64_t first, int64_t count, int* launches,
+                              hipEvent_t* after_class = nullptr);
 void launch_world_pre(const DevWorld& W, hipStream_t s, const double* d_totals);
 void launch_world_post(const DevWorld& W, hipStream_t s, double* d_stats);
 void launch_classify_uniform(const DevWorld& W, hipStream_t s, int64_t first, int64_t count,

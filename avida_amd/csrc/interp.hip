@@ -53,37 +53,44 @@ constexpr uint32_t WR_OPS =
     OPB(AVGPU_H_DEC) | OPB(AVGPU_H_ADD) | OPB(AVGPU_H_SUB) | OPB(AVGPU_H_NAND);
 #undef OPB
 
-// popcount of `bitmask`-selected flag bits over tape sites [from, to)
-__device__ __forceinline__ int count_flag(const uint8_t* T, int from, int to, uint32_t bit) {
-  const uint32_t* T32 = reinterpret_cast<const uint32_t*>(T);
-  const uint32_t m4 = bit * 0x01010101u;
-  int n = 0;
-  int i = from;
-  for (; i < to && (i & 3); i++) n += (T[i] & bit) ? 1 : 0;
-  const int wend = to >> 2;
-  int w = i >> 2;
-  for (; w + 4 <= wend; w += 4) {
-    const uint32_t a = T32[w], b = T32[w + 1], c = T32[w + 2], d = T32[w + 3];
-    n += __popc(a & m4) + __popc(b & m4) + __popc(c & m4) + __popc(d & m4);
-  }
-  for (; w < wend; w++) n += __popc(T32[w] & m4);
-  for (i = max(i, wend << 2); i < to; i++) n += (T[i] & bit) ? 1 : 0;
-  return n;
+// bytes of the tape word starting at site w4 that lie in [from, to)
+__device__ __forceinline__ uint32_t byte_mask(int w4, int from, int to) {
+  uint32_t m = 0;
+#pragma unroll
+  for (int q = 0; q < 4; q++) m |= (w4 + q >= from && w4 + q < to) ? (0xFFu << (8 * q)) : 0u;
+  return m;
+}
+__device__ __forceinline__ int wave_sum_i32(int v) {
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+  return v;
 }
 
 template <int S>
-__global__ __launch_bounds__(64) void k_interpret(DevWorld W, int cls, int mode, int64_t first,
-                                                  int64_t count) {
-  constexpr int STRIDE = S + 4;
+// The world descriptor is read through a device pointer rather than passed by
+// value: as a by-value kernel argument its ~70 pointers and scalars were all
+// held in SGPRs and spilled into VGPR lanes (hundreds of v_readlane in the
+// loop); through the pointer each field is a scalar load at its use.
+__global__ __launch_bounds__(64) void k_interpret(const DevWorld* __restrict__ Wp, int cls, int mode,
+                                                  int64_t first, int64_t count) {
+  const DevWorld& W = *Wp;
+  // per-lane tape stride: a whole number of 16-byte quads (16-B LDS-DMA) with
+  // room for the fetch / label windows that read up to 16 bytes past a site
+  constexpr int STRIDE = S + 16;
+  constexpr int QUADS = STRIDE / 16;
   constexpr int TAPE_WORDS = 64 * STRIDE / 4;
   constexpr int STK_WORDS = 2 * AVGPU_STACK_SIZE * 64;
-  // one __shared__ object: tapes | stacks | task LUT (256 x u16) | rand_cum (64 x i32) | rand_code (64 B)
-  __shared__ uint32_t lds32[TAPE_WORDS + STK_WORDS + 128 + 64 + 16];
+  // one __shared__ object: tapes | stacks | task LUT (256 x u16) | rand_cum (64 x i32) |
+  // rand_code (64 B) | rand_lut (256 B) | reactions (16 x RT_STRIDE words)
+  constexpr int TAB_WORDS = 128 + 64 + 16 + 64 + AVGPU_MAX_REACTIONS * RT_STRIDE;
+  __shared__ __attribute__((aligned(16))) uint32_t lds32[TAPE_WORDS + STK_WORDS + TAB_WORDS];
   uint8_t* lds = reinterpret_cast<uint8_t*>(lds32);
   int32_t* stk = reinterpret_cast<int32_t*>(lds32 + TAPE_WORDS);
-  const uint16_t* lut = reinterpret_cast<const uint16_t*>(lds32 + TAPE_WORDS + STK_WORDS);
-  const int32_t* rcum = reinterpret_cast<const int32_t*>(lds32 + TAPE_WORDS + STK_WORDS + 128);
-  const uint8_t* rcode = reinterpret_cast<const uint8_t*>(lds32 + TAPE_WORDS + STK_WORDS + 192);
+  uint32_t* tab = lds32 + TAPE_WORDS + STK_WORDS;
+  const uint16_t* lut = reinterpret_cast<const uint16_t*>(tab);
+  const int32_t* rcum = reinterpret_cast<const int32_t*>(tab + 128);
+  const uint8_t* rcode = reinterpret_cast<const uint8_t*>(tab + 192);
+  const uint8_t* rlut = reinterpret_cast<const uint8_t*>(tab + 208);
+  const int32_t* rtab = reinterpret_cast<const int32_t*>(tab + 272);
 
   const int lane = threadIdx.x;
   const int64_t N = W.n;
@@ -120,32 +127,29 @@ __global__ __launch_bounds__(64) void k_interpret(DevWorld W, int cls, int mode,
 
   // ---- block-shared tables ----
   {
-    uint32_t* l32 = lds32 + TAPE_WORDS + STK_WORDS;
+    uint32_t* l32 = tab;
     const uint32_t* g_lut = reinterpret_cast<const uint32_t*>(W.task_lut);
     l32[lane] = g_lut[lane];
     l32[64 + lane] = g_lut[64 + lane];
     l32[128 + lane] = (uint32_t)W.rand_cum[lane];
     if (lane < 16) l32[192 + lane] = reinterpret_cast<const uint32_t*>(W.rand_code)[lane];
+    l32[208 + lane] = reinterpret_cast<const uint32_t*>(W.rand_lut)[lane];
+    for (int k = lane; k < AVGPU_MAX_REACTIONS * RT_STRIDE; k += 64) l32[272 + k] = (uint32_t)W.react_tab[k];
   }
-  // ---- stage tapes and stacks into LDS by LDS-DMA (global_load_lds_dword:
-  // per-lane source, lane-linear destination); all copies are in flight
-  // together and retired by the single wait below ----
+  // ---- stage tapes and stacks into LDS by LDS-DMA.  The 64 tapes form one
+  // lane-linear image of 64 x QUADS quads (quad i = organism i / QUADS, part
+  // i % QUADS), so each global_load_lds_dwordx4 moves 1 KiB with per-lane
+  // sources; all copies are in flight together and retired by one wait ----
   typedef __attribute__((address_space(3))) void* lds_ptr_t;
-  for (int j = 0; j < 64; j++) {
+#pragma unroll 1
+  for (int it = 0; it < QUADS; it++) {
+    const int i = it * 64 + lane;
+    const int j = i / QUADS, q = i - j * QUADS;
     const int c = __shfl(cell, j);
     const int m = __shfl(M, j);
-    if (c < 0) continue;
-    const uint32_t* src = reinterpret_cast<const uint32_t*>(W.tape + (int64_t)c * TAPE_SLOT);
-    const int words = (m + 3) >> 2;
-    for (int k = 0; k * 64 < words; k++) {
-      if (k * 64 + lane < words)
-#ifdef AVGPU_NO_LDS_DMA
-        lds32[j * (STRIDE / 4) + k * 64 + lane] = src[k * 64 + lane];
-#else
-        __builtin_amdgcn_global_load_lds((void*)(src + k * 64 + lane),
-                                         (lds_ptr_t)(lds32 + j * (STRIDE / 4) + k * 64), 4, 0, 0);
-#endif
-    }
+    if (c >= 0 && q * 16 < m)
+      __builtin_amdgcn_global_load_lds((void*)(W.tape + (int64_t)c * TAPE_SLOT + q * 16),
+                                       (lds_ptr_t)(lds32 + it * 256), 16, 0, 0);
   }
 #pragma unroll
   for (int k = 0; k < 2 * AVGPU_STACK_SIZE; k++) {
@@ -172,6 +176,18 @@ __global__ __launch_bounds__(64) void k_interpret(DevWorld W, int cls, int mode,
   int tc[AVGPU_NUM_LOGIC_TASKS];
 #pragma unroll
   for (int q = 0; q < AVGPU_NUM_LOGIC_TASKS; q++) tc[q] = 0;
+  // divide bookkeeping kept on chip so that no global load or store is
+  // compiler-visible inside the loop (written back after it if a divide happened)
+  int dexe = 0, dcop = 0, dnd = 0, dgen = 0, dccop = 0, dgt = 0;
+  double dmerit = 0.0, dfit = 0.0;
+  int lt[AVGPU_NUM_LOGIC_TASKS];
+  int rc[AVGPU_MAX_REACTIONS];   // reaction counts since slice start / last reset
+#pragma unroll
+  for (int q = 0; q < AVGPU_NUM_LOGIC_TASKS; q++) lt[q] = 0;
+#pragma unroll
+  for (int q = 0; q < AVGPU_MAX_REACTIONS; q++) rc[q] = 0;
+  bool didv = false, prim = false, prim0 = false;
+  int ndrop = 0;
   if (active) {
     r0 = W.reg[cell]; r1 = W.reg[N + cell]; r2 = W.reg[2 * N + cell];
     ip = W.head[cell]; rh = W.head[N + cell]; wh = W.head[2 * N + cell]; fh = W.head[3 * N + cell];
@@ -180,6 +196,8 @@ __global__ __launch_bounds__(64) void k_interpret(DevWorld W, int cls, int mode,
     mx = W.max_exec[cell]; blen = W.birth_len[cell];
     klo = W.rng[cell]; khi = W.rng[N + cell]; kct = W.rng[2 * N + cell];
     budget = W.budget[cell];
+    prim = (budget & BUDGET_PRIM) != 0;   // a spilled slice already used its primary record
+    budget &= ~BUDGET_PRIM;
     errs = W.errors[cell];
     in0 = W.inbuf[cell]; in1 = W.inbuf[N + cell]; in2 = W.inbuf[2 * N + cell];
     intot = W.in_total[cell]; inptr = W.in_ptr[cell];
@@ -188,7 +206,9 @@ __global__ __launch_bounds__(64) void k_interpret(DevWorld W, int cls, int mode,
     bonus = W.cur_bonus[cell];
 #pragma unroll
     for (int q = 0; q < AVGPU_NUM_LOGIC_TASKS; q++) tc[q] = W.cur_task[(int64_t)q * N + cell];
+    dexe = W.executed[cell]; dcop = W.copied[cell]; dnd = W.num_div[cell]; dgen = W.generation[cell];
   }
+  prim0 = prim;
   __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0), visible to the compiler's waitcnt tracking
   __syncthreads();
 #ifdef AVGPU_PHASE_CLOCKS
@@ -202,6 +222,7 @@ __global__ __launch_bounds__(64) void k_interpret(DevWorld W, int cls, int mode,
   // cInstSet::GetRandomInst (cpu/cInstSet.cc:83-88) from the LDS tables
   auto rand_code = [&]() -> uint8_t {
     const uint32_t r = rng_below(klo, khi, kct, (uint32_t)W.rand_total);
+    if (W.rand_total <= 256) return rlut[r];
     int i = 0;
     while (i < W.n_ops - 1 && rcum[i] <= (int32_t)r) i++;
     return rcode[i];
@@ -212,34 +233,49 @@ __global__ __launch_bounds__(64) void k_interpret(DevWorld W, int cls, int mode,
 #define GETHEAD(i) ((i) == 0 ? ip : ((i) == 1 ? rh : ((i) == 2 ? wh : fh)))
 #define SETHEAD(i, v) do { const int _v = (v); if ((i) == 0) ip = _v; else if ((i) == 1) rh = _v; else if ((i) == 2) wh = _v; else fh = _v; } while (0)
 
-  while (alive && budget > 0) {
-    // ---- SingleProcess (cpu/cHardwareCPU.cc:908-1058) ----
-    const int ipa = head_adjust(ip, M);                       // ip.Adjust() :952
-    // fetch window: sites ipa .. ipa+4 in two independent word reads
-    const uint32_t* T32 = reinterpret_cast<const uint32_t*>(T);
-    const uint64_t fwin = ((uint64_t)T32[(ipa >> 2) + 1] << 32) | (uint64_t)T32[ipa >> 2];
-    const uint32_t fsh = (uint32_t)(ipa & 3) * 8u;
-    const int cur_byte = (int)((fwin >> fsh) & 0xFFu);
-    const int op = cur_byte & CODE_MASK;                      // fetch :959
-    if (op == AVGPU_H_H_ALLOC) {
-      // would this allocation outgrow the LDS slot?  (spill check; the
-      // instruction is then executed by the next size class)
-      const int cur = M;
-      int alloc = (int)(W.size_range * cur);
-      if (alloc > AVGPU_MAX_GENOME - cur) alloc = AVGPU_MAX_GENOME - cur;
-      const int nsz = cur + alloc;
-      const bool ok = !(W.require_allocate && (ctl & CTL_MAL)) && alloc >= 1 &&
-                      nsz <= AVGPU_MAX_GENOME && nsz >= AVGPU_MIN_GENOME &&
-                      alloc <= (int)(cur * W.size_range) && cur <= (int)(alloc * W.size_range);
-      if (ok && nsz > S) { spill = true; ip = ipa; break; }
-    }
+  // Requests for the O(memory) parts of heavy instructions -- the divide's
+  // flag counts, offspring copy and flag clearing, h-alloc's fill, h-search's
+  // label scan.  A lane decodes such an instruction and posts a request; the
+  // whole wave then serves the requests one lane at a time, 64 sites per
+  // instruction (DESIGN.md "Cooperative heavy ops").  Run per lane, every
+  // iteration of the wave paid for the longest such loop of any of its lanes.
+  const int RQ_NONE = 0, RQ_DIVIDE = 1, RQ_FILL = 2, RQ_SEARCH = 3;
+  const uint32_t fill4 = (uint32_t)W.fill_code * 0x01010101u;
+  while (true) {
+    const bool run = alive && budget > 0 && !stop && !spill;
+    if (!__any(run)) break;                                   // wave-uniform loop
+    int rq = RQ_NONE, qa = 0, qb = 0;
+    bool adv = true;                                          // m_advance_ip
+    bool stepped = false;
+    if (run) {
+      // ---- SingleProcess (cpu/cHardwareCPU.cc:908-1058) ----
+      const int ipa = head_adjust(ip, M);                     // ip.Adjust() :952
+      // fetch window: sites ipa .. ipa+4 in two independent word reads
+      const uint32_t* T32 = reinterpret_cast<const uint32_t*>(T);
+      const uint64_t fwin = ((uint64_t)T32[(ipa >> 2) + 1] << 32) | (uint64_t)T32[ipa >> 2];
+      const uint32_t fsh = (uint32_t)(ipa & 3) * 8u;
+      const int cur_byte = (int)((fwin >> fsh) & 0xFFu);
+      const int op = cur_byte & CODE_MASK;                    // fetch :959
+      if (op == AVGPU_H_H_ALLOC) {
+        // would this allocation outgrow the LDS slot?  (spill check; the
+        // instruction is then executed by the next size class)
+        const int cur = M;
+        int alloc = (int)(W.size_range * cur);
+        if (alloc > AVGPU_MAX_GENOME - cur) alloc = AVGPU_MAX_GENOME - cur;
+        const int nsz = cur + alloc;
+        const bool ok = !(W.require_allocate && (ctl & CTL_MAL)) && alloc >= 1 &&
+                        nsz <= AVGPU_MAX_GENOME && nsz >= AVGPU_MIN_GENOME &&
+                        alloc <= (int)(cur * W.size_range) && cur <= (int)(alloc * W.size_range);
+        if (ok && nsz > S) { spill = true; ip = ipa; }
+      }
+    if (!spill) {
+    stepped = true;
     cyc++;                                                    // IncCPUCyclesUsed :929
     tu++;                                                     // IncTimeUsed :930
     ip = ipa;
     T[ip] = (uint8_t)(cur_byte | TF_EXEC);                    // SetFlagExecuted :996
     executed++;
     budget--;
-    bool adv = true;                                          // m_advance_ip
     const int nbyte = (int)((fwin >> (fsh + 8u)) & 0xFFu);
     const int nxt = (ip + 1 < M) ? (nbyte & CODE_MASK) : CODE_ERROR;  // GetNextInst
     // ---- FindModifiedRegister / FindModifiedHead (:1622-1672), applied once
@@ -253,7 +289,6 @@ __global__ __launch_bounds__(64) void k_interpret(DevWorld W, int cls, int mode,
     it_copy += __ballot(op == AVGPU_H_H_COPY) != 0ull;
     it_slow += __ballot(!(FAST_OPS & obit) && op != AVGPU_H_H_COPY) != 0ull;
 #endif
-
     if (FAST_OPS & obit) {
       // ---- branch-free ops: register ALU, swap, conditionals, head moves ----
       const int rn = (r == 2) ? 0 : r + 1;                    // FindNextRegister :1676
@@ -352,17 +387,23 @@ __global__ __launch_bounds__(64) void k_interpret(DevWorld W, int cls, int mode,
           // (main/cEnvironment.cc:1314-1406, :1408-1503, :1610-1760)
           uint32_t done = 0;
           double mult = 1.0, addb = 0.0;
-          for (int i = 0; i < W.n_react; i++) {
-            const int t = W.react_task[i];                    // uniform
-            if (!((tmask >> t) & 1u)) continue;
+#pragma unroll
+          for (int i = 0; i < AVGPU_MAX_REACTIONS; i++) {
+            const int32_t* rt = rtab + i * RT_STRIDE;         // uniform LDS reads
+            const int t = rt[RT_TASK];
             int cnt = 0;
 #pragma unroll
             for (int q = 0; q < AVGPU_NUM_LOGIC_TASKS; q++) cnt = (q == t) ? tc[q] : cnt;
-            if (W.react_hasreq[i] && (cnt < W.react_min[i] || cnt >= W.react_max[i])) continue;
-            done |= 1u << t;
-            if (W.react_type[i] == AVGPU_PROC_ADD) addb = __dadd_rn(addb, W.react_add[i]);
-            else mult = __dmul_rn(mult, W.react_mult[i]);
-            atomicAdd(&W.cur_react[(int64_t)i * N + cell], 1);  // no return: no wait
+            const bool fire = rt[RT_USED] && ((tmask >> t) & 1u) &&
+                              !(rt[RT_HASREQ] && (cnt < rt[RT_MIN] || cnt >= rt[RT_MAX]));
+            if (fire) {
+              done |= 1u << t;
+              if (rt[RT_TYPE] == AVGPU_PROC_ADD)
+                addb = __dadd_rn(addb, *reinterpret_cast<const double*>(rt + RT_ADD));
+              else
+                mult = __dmul_rn(mult, *reinterpret_cast<const double*>(rt + RT_MULT));
+              rc[i]++;
+            }
           }
           if (done) {
 #pragma unroll
@@ -390,12 +431,7 @@ __global__ __launch_bounds__(64) void k_interpret(DevWorld W, int cls, int mode,
         if (W.alloc_method == 2) {
           for (int i = cur; i < nsz; i++) T[i] = rand_code();
         } else {
-          const uint32_t f = W.fill_code;
-          int i = cur;
-          for (; i < nsz && (i & 3); i++) T[i] = (uint8_t)f;
-          const uint32_t f4 = f * 0x01010101u;
-          for (; i + 4 <= nsz; i += 4) *reinterpret_cast<uint32_t*>(T + i) = f4;
-          for (; i < nsz; i++) T[i] = (uint8_t)f;
+          rq = RQ_FILL; qa = cur; qb = nsz;                   // new sites = op 0 (wave fill below)
         }
         M = nsz;
         ctl |= CTL_MAL;
@@ -406,142 +442,14 @@ __global__ __launch_bounds__(64) void k_interpret(DevWorld W, int cls, int mode,
         const int div = rh;
         const int child_end = (wh == 0) ? M : wh;
         const int child = child_end - div;
-        // Divide_CheckViable (cpu/cHardwareBase.cc:140-289)
+        // Divide_CheckViable (cpu/cHardwareBase.cc:140-289): sizes here, the
+        // executed / copied line counts in the wave phase below
         const int min_size = max(AVGPU_MIN_GENOME, (int)(blen / W.size_range));
         const int max_size = min(AVGPU_MAX_GENOME, (int)(blen * W.size_range));
         bool ok = child >= min_size && child <= max_size && div >= min_size && div <= max_size;
         if (ok && W.cfg_min_genome && (child < W.cfg_min_genome || div < W.cfg_min_genome)) ok = false;
         if (ok && W.cfg_max_genome && (child > W.cfg_max_genome || div > W.cfg_max_genome)) ok = false;
-        int exe = 0, cop = 0;
-        if (ok) {                                             // calcExecutedSize (cpu/cHardwareBase.cc:130-138)
-          exe = count_flag(T, 0, div, TF_EXEC);
-          ok = exe >= (int)(div * W.min_exe_lines);
-        }
-        if (ok) {                                             // calcCopiedSize (cpu/cHardwareCPU.cc:1765-1772)
-          cop = count_flag(T, div, div + child, TF_COPIED);
-          ok = cop >= (int)(child * W.min_copied_lines);
-        }
-        double bon = bonus;
-        int old_exe = 0, copied = 0;
-        if (ok) {  // cOrganism::Divide_CheckViable (main/cOrganism.cc:788-919)
-          if (bon < W.required_bonus) ok = false;
-          old_exe = W.executed[cell];
-          copied = W.copied[cell];
-          const double base0 = (double)calc_size_merit(W, blen, copied, old_exe);
-          double b0 = bon;
-          if (W.merit_default_bonus != 0.0) b0 = W.merit_default_bonus;
-          double off_merit = __dmul_rn(base0, b0);
-          if (W.inherit_merit == 0) off_merit = base0;
-          if (off_merit == 0.0) ok = false;
-        }
-        if (!ok) break;                                       // AdjustHeads again: no-op
-        W.executed[cell] = exe;                               // SetLinesExecuted
-        W.child_copied[cell] = cop;                           // SetLinesCopied
-        // ---- offspring ----
-        const int nd = W.num_div[cell] + 1;
-        if (mode == AVGPU_MODE_TEST) {
-          uint8_t* fl = W.t_flags + (int64_t)cell * TAPE_SLOT;
-          for (int i = 0; i < div; i++) fl[i] = (T[i] & TF_EXEC) ? '+' : '-';
-          W.t_flags_len[cell] = div;
-          uint8_t* ch = W.t_child + (int64_t)cell * TAPE_SLOT;
-          for (int i = 0; i < child; i++) ch[i] = T[div + i] & CODE_MASK;
-          W.t_child_len[cell] = child;
-          stop = true;
-        }
-        // DivideReset / TestDivideReset (main/cPhenotype.cc:824-1000, :1064-1180)
-        const double base = (double)calc_size_merit(W, blen, copied, exe);
-        if (W.merit_default_bonus != 0.0) bon = W.merit_default_bonus;
-        double merit = __dmul_rn(base, bon);
-        if (W.inherit_merit == 0) merit = base;
-        const int gt = tu - gs;
-        const double fit = __ddiv_rn(__dmul_rn(base, bon), (double)gt);
-        W.merit[cell] = merit;
-        W.gest_time[cell] = gt;
-        W.fitness[cell] = fit;
-        gs = tu;
-        W.num_div[cell] = nd;
-        const int gen = W.generation[cell] + 1;
-        W.generation[cell] = gen;
-        errs = 0;
-        bonus = W.default_bonus;
-        cyc = 0;
-#pragma unroll
-        for (int q = 0; q < AVGPU_NUM_LOGIC_TASKS; q++) {
-          W.last_task[(int64_t)q * N + cell] = tc[q];
-          tc[q] = 0;
-        }
-        for (int i = 0; i < W.n_react; i++) W.cur_react[(int64_t)i * N + cell] = 0;
-        if (mode == AVGPU_MODE_WORLD) {
-          // Divide_DoMutations (cpu/cHardwareBase.cc:296-569), default subset
-          int len = child;
-          int mline = -1, iline = -1, dline = -1;
-          uint8_t mcode = 0, icode = 0;
-          if (W.th_div_mut && rng_p(klo, khi, kct, W.th_div_mut)) {
-            mline = (int)rng_below(klo, khi, kct, (uint32_t)len);
-            mcode = rand_code();
-          }
-          if (W.th_div_ins && rng_p(klo, khi, kct, W.th_div_ins) && len < W.max_genome) {
-            iline = (int)rng_below(klo, khi, kct, (uint32_t)len + 1);
-            icode = rand_code();
-            len++;
-          }
-          if (W.th_div_del && rng_p(klo, khi, kct, W.th_div_del) && len > W.min_genome) {
-            dline = (int)rng_below(klo, khi, kct, (uint32_t)len);
-            len--;
-          }
-          const int slot = atomicAdd(W.b_count, 1);
-          if (slot < W.bcap) {
-            uint32_t* g32 = reinterpret_cast<uint32_t*>(W.b_genome + (int64_t)slot * TAPE_SLOT);
-            for (int j0 = 0; j0 < len; j0 += 4) {
-              uint32_t word = 0;
-#pragma unroll
-              for (int b = 0; b < 4; b++) {
-                const int j = j0 + b;
-                const int k2 = (dline >= 0 && j >= dline) ? j + 1 : j;       // index before the deletion
-                int v;
-                if (iline >= 0 && k2 == iline) v = icode;
-                else {
-                  const int k1 = (iline >= 0 && k2 > iline) ? k2 - 1 : k2;  // before the insertion
-                  v = (k1 == mline) ? mcode : (T[div + k1] & CODE_MASK);
-                }
-                word |= (j < len ? (uint32_t)v : 0u) << (8 * b);
-              }
-              g32[j0 >> 2] = word;
-            }
-            W.b_parent[slot] = cell;
-            W.b_seq[slot] = (uint32_t)nd;
-            W.b_len[slot] = len;
-            W.b_merit[slot] = merit;
-            W.b_fitness[slot] = fit;
-            W.b_gen[slot] = gen;
-            W.b_ccopied[slot] = cop;
-            W.b_exec[slot] = exe;
-            W.b_gest[slot] = gt;
-            uint32_t clo, chi;
-            derive_key(klo, khi, (uint32_t)nd, 0x1B873593U, clo, chi);
-            W.b_rng[slot] = clo;
-            W.b_rng[W.bcap + slot] = chi;
-            W.b_rng[2 * W.bcap + slot] = 0;
-            W.b_state[slot] = 0;
-            W.b_target[slot] = -1;
-          } else {
-            count_add(W, CNT_DROPPED, 1ull);
-          }
-        }
-        divides++;
-        // parent: Resize(div), Reset (:813-900), ClearFlags (:1839); no IP advance
-        M = div;
-        r0 = r1 = r2 = 0;
-        ip = rh = wh = fh = 0;
-#pragma unroll
-        for (int k = 0; k < 2 * AVGPU_STACK_SIZE; k++) stk[k * 64 + lane] = 0;
-        ctl = CTL_ALIVE;
-        rl = 0;
-        {
-          uint32_t* W32 = reinterpret_cast<uint32_t*>(T);
-          for (int w = 0; w < ((div + 3) >> 2); w++) W32[w] &= 0x3F3F3F3Fu;  // ClearFlags (beyond div: unused)
-        }
-        adv = false;
+        if (ok) { rq = RQ_DIVIDE; qa = div; qb = child; }
         break; }
       case AVGPU_H_H_SEARCH:                                  // :7245 Inst_HeadSearch
       case AVGPU_H_IF_LABEL: {                                // :6914 Inst_IfLabel
@@ -579,46 +487,235 @@ __global__ __launch_bounds__(64) void k_interpret(DevWorld W, int cls, int mode,
           if (packed != rl) ip = head_adjust(ip + 1, M);
           break;
         }
-        // FindLabel(0) -> FindLabel_Forward(label, memory, 0) (:1177-1295).
-        // The reference probes every label_size sites and, inside a probed nop
-        // run, tests every offset; every maximal nop run that can hold the
-        // label is probed except a run that ends exactly at label_size.  Its
-        // answer is therefore the smallest offset o whose label_size sites
-        // spell the label (all nops) and that is not that unprobed run
-        // (o > 0, or site label_size is a nop).  A rolling 2-bit window over
-        // 16-site word batches finds it (DESIGN.md "h-search").
-        int found = ip;
-        if (len > 0) {
-          uint32_t lab_rev = 0;
-          for (int i = 0; i < len; i++) lab_rev |= ((rot >> (2 * i)) & 3u) << (2 * (len - 1 - i));
-          const uint32_t msk = (len == 16) ? 0xFFFFFFFFu : ((1u << (2 * len)) - 1u);
-          const bool run0_ok = len < M && (T[len] & CODE_MASK) < 3;
-          uint32_t wnd = 0xFFFFFFFFu;
-          int fpos = -1;
-          for (int w = 0; (w << 2) < M && fpos < 0; w += 4) {
-            const uint32_t q0 = T32[w], q1 = T32[w + 1], q2 = T32[w + 2], q3 = T32[w + 3];
-#pragma unroll
-            for (int b = 0; b < 16; b++) {
-              const uint32_t q = (b < 4) ? q0 : (b < 8) ? q1 : (b < 12) ? q2 : q3;
-              const int j = (w << 2) + b;
-              uint32_t cc = (q >> (8 * (b & 3))) & CODE_MASK;
-              cc = cc < 3u ? cc : 3u;
-              wnd = (wnd << 2) | cc;
-              if (fpos < 0 && j < M && (wnd & msk) == lab_rev && (j != len - 1 || run0_ok)) fpos = j + 1;
-            }
-          }
-          if (fpos >= 0) found = head_adjust(fpos - 1, M);
-        }
-        r1 = found - ip;
-        r2 = len;
-        fh = head_adjust(found + 1, M);
+        if (len > 0) { rq = RQ_SEARCH; qa = len; qb = (int)rot; break; }   // label scan below
+        r1 = 0;                                               // empty label: found = IP
+        r2 = 0;
+        fh = head_adjust(ip + 1, M);
         break; }
       default:
         break;
     }
-    if (stop) break;
-    if (adv) ip = head_adjust(ip + 1, M);                     // ip.Advance() :1013
-    if (mx > 0 && tu >= mx) alive = false;                    // death :1045-1049
+    }  // !spill
+    }  // run
+
+    // ---- wave phase: serve the posted requests, one lane at a time ----
+    unsigned long long pend = __ballot(rq != RQ_NONE);
+    while (pend) {
+      const int L = __ffsll((long long)pend) - 1;            // wave-uniform
+      pend &= pend - 1ull;
+      const int kind = __shfl(rq, L);
+      const int a = __shfl(qa, L), b = __shfl(qb, L);
+      uint32_t* TL32 = lds32 + L * (STRIDE / 4);
+      const uint8_t* TL = lds + L * STRIDE;
+      if (kind == RQ_FILL) {
+        // Allocate_Main: new sites [a, b) get op 0 (ALLOC_METHOD 0/1)
+        for (int w = (a >> 2) + lane; (w << 2) < b; w += 64) {
+          const uint32_t keep = byte_mask(w << 2, a, b);
+          TL32[w] = (TL32[w] & ~keep) | (fill4 & keep);
+        }
+      } else if (kind == RQ_SEARCH) {
+        // FindLabel(0) -> FindLabel_Forward(label, memory, 0) (:1177-1295).
+        // The reference probes every label_size sites and, inside a probed
+        // nop run, tests every offset; every maximal nop run that can hold the
+        // label is probed except a run that ends exactly at label_size.  Its
+        // answer is therefore the smallest offset o whose label_size sites
+        // spell the label (all nops) and that is not that unprobed run
+        // (o > 0, or site label_size is a nop).  Lane t tests the window that
+        // ends at site base + t.
+        const int len = a;
+        const uint32_t rot = (uint32_t)b;
+        const int ML = __shfl(M, L);
+        const bool run0_ok = len < ML && (TL[len] & CODE_MASK) < 3;
+        int fpos = -1;
+        for (int base = 0; base < ML && fpos < 0; base += 64) {
+          const int j = base + lane;
+          bool m = j < ML && j >= len - 1 && (j != len - 1 || run0_ok);
+          if (m) {
+            const int st = j - len + 1;
+            const int w0 = st >> 2;
+            const uint64_t lo64 = ((uint64_t)TL32[w0 + 1] << 32) | (uint64_t)TL32[w0];
+            const uint64_t hi64 = ((uint64_t)TL32[w0 + 3] << 32) | (uint64_t)TL32[w0 + 2];
+            const int b0 = st & 3;
+            for (int i = 0; i < len; i++) {
+              const int k = b0 + i;
+              const uint32_t cc = (uint32_t)(((k < 8) ? (lo64 >> (8 * k)) : (hi64 >> (8 * (k - 8)))) & CODE_MASK);
+              m = m && cc == ((rot >> (2 * i)) & 3u);
+            }
+          }
+          const unsigned long long bm = __ballot(m);
+          if (bm) fpos = base + __ffsll((long long)bm);        // first site after the label
+        }
+        if (lane == L) {
+          const int found = fpos >= 0 ? head_adjust(fpos - 1, M) : ip;
+          r1 = found - ip;
+          r2 = len;
+          fh = head_adjust(found + 1, M);
+        }
+      } else {
+        // ---- Divide_Main (:1775-1843) for lane L ----
+        const int div = a, child = b;
+        // calcExecutedSize (cpu/cHardwareBase.cc:130-138), calcCopiedSize (cpu/cHardwareCPU.cc:1765-1772)
+        int ne = 0, nc = 0;
+        for (int w = lane; (w << 2) < div + child; w += 64) {
+          const uint32_t v = TL32[w];
+          ne += __popc(v & (TF_EXEC * 0x01010101u) & byte_mask(w << 2, 0, div));
+          nc += __popc(v & (TF_COPIED * 0x01010101u) & byte_mask(w << 2, div, div + child));
+        }
+        const int exe = wave_sum_i32(ne), cop = wave_sum_i32(nc);
+        int okw = 0, rec = -1, len = 0, ml = -1, il = -1, dl = -1, mc = 0, ic = 0;
+        if (lane == L) {
+          bool ok = exe >= (int)(div * W.min_exe_lines) && cop >= (int)(child * W.min_copied_lines);
+          double bon = bonus;
+          if (ok) {  // cOrganism::Divide_CheckViable (main/cOrganism.cc:788-919)
+            if (bon < W.required_bonus) ok = false;
+            const double base0 = (double)calc_size_merit(W, blen, dcop, dexe);
+            double b0 = bon;
+            if (W.merit_default_bonus != 0.0) b0 = W.merit_default_bonus;
+            double off_merit = __dmul_rn(base0, b0);
+            if (W.inherit_merit == 0) off_merit = base0;
+            if (off_merit == 0.0) ok = false;
+          }
+          if (ok) {
+            okw = 1;
+            dexe = exe;                                       // SetLinesExecuted
+            dccop = cop;                                      // SetLinesCopied
+            const int nd = dnd + 1;
+            // DivideReset / TestDivideReset (main/cPhenotype.cc:824-1000, :1064-1180)
+            const double base = (double)calc_size_merit(W, blen, dcop, exe);
+            if (W.merit_default_bonus != 0.0) bon = W.merit_default_bonus;
+            double merit = __dmul_rn(base, bon);
+            if (W.inherit_merit == 0) merit = base;
+            const int gt = tu - gs;
+            const double fit = __ddiv_rn(__dmul_rn(base, bon), (double)gt);
+            dmerit = merit;
+            dgt = gt;
+            dfit = fit;
+            gs = tu;
+            dnd = nd;
+            const int gen = dgen + 1;
+            dgen = gen;
+            didv = true;
+            errs = 0;
+            bonus = W.default_bonus;
+            cyc = 0;
+#pragma unroll
+            for (int q = 0; q < AVGPU_NUM_LOGIC_TASKS; q++) {
+              lt[q] = tc[q];
+              tc[q] = 0;
+            }
+#pragma unroll
+            for (int i = 0; i < AVGPU_MAX_REACTIONS; i++) rc[i] = 0;
+            len = child;
+            if (mode == AVGPU_MODE_TEST) {
+              st_async_u32(W.t_flags_len + cell, (uint32_t)div);
+              st_async_u32(W.t_child_len + cell, (uint32_t)child);
+              stop = true;
+            } else if (mode == AVGPU_MODE_WORLD) {
+              // Divide_DoMutations (cpu/cHardwareBase.cc:296-569), default subset
+              if (W.th_div_mut && rng_p(klo, khi, kct, W.th_div_mut)) {
+                ml = (int)rng_below(klo, khi, kct, (uint32_t)len);
+                mc = rand_code();
+              }
+              if (W.th_div_ins && rng_p(klo, khi, kct, W.th_div_ins) && len < W.max_genome) {
+                il = (int)rng_below(klo, khi, kct, (uint32_t)len + 1);
+                ic = rand_code();
+                len++;
+              }
+              if (W.th_div_del && rng_p(klo, khi, kct, W.th_div_del) && len > W.min_genome) {
+                dl = (int)rng_below(klo, khi, kct, (uint32_t)len);
+                len--;
+              }
+              // record: the cell's primary record for the slice's first
+              // offspring, an overflow record (atomic) for any further one
+              rec = cell;
+              if (prim) {
+                rec = (int)min((int64_t)W.n + atomicAdd(W.b_count + 1, 1), W.rcap);
+                if (rec >= W.rcap) { rec = -1; ndrop++; }
+              }
+              prim = true;
+              if (rec >= 0) {
+                uint32_t clo, chi;
+                derive_key(klo, khi, (uint32_t)nd, 0x1B873593U, clo, chi);
+                st_async_u32(W.b_parent + rec, (uint32_t)cell);
+                st_async_u32(W.b_seq + rec, (uint32_t)nd);
+                st_async_u32(W.b_len + rec, (uint32_t)len);
+                st_async_u64(W.b_merit + rec, (uint64_t)__double_as_longlong(merit));
+                st_async_u64(W.b_fitness + rec, (uint64_t)__double_as_longlong(fit));
+                st_async_u32(W.b_gen + rec, (uint32_t)gen);
+                st_async_u32(W.b_ccopied + rec, (uint32_t)cop);
+                st_async_u32(W.b_exec + rec, (uint32_t)exe);
+                st_async_u32(W.b_gest + rec, (uint32_t)gt);
+                st_async_u32(W.b_rng + rec, clo);
+                st_async_u32(W.b_rng + W.rcap + rec, chi);
+                st_async_u32(W.b_rng + 2 * W.rcap + rec, 0u);
+                st_async_u8(W.b_state + rec, 0u);
+                st_async_u32(W.b_target + rec, 0xFFFFFFFFu);
+              }
+            }
+            divides++;
+            // parent: Resize(div), Reset (:813-900), ClearFlags (:1839); no IP advance
+            M = div;
+            r0 = r1 = r2 = 0;
+            ip = rh = wh = fh = 0;
+            ctl = CTL_ALIVE;
+            rl = 0;
+            adv = false;
+          }
+        }
+        okw = __shfl(okw, L);
+        if (okw) {
+          rec = __shfl(rec, L); len = __shfl(len, L);
+          ml = __shfl(ml, L); il = __shfl(il, L); dl = __shfl(dl, L);
+          mc = __shfl(mc, L); ic = __shfl(ic, L);
+          const int cell_l = __shfl(cell, L);
+          if (mode == AVGPU_MODE_TEST) {
+            // test-CPU snapshots: executed flags of the parent part, the offspring
+            uint8_t* fl = W.t_flags + (int64_t)cell_l * TAPE_SLOT;
+            uint8_t* ch = W.t_child + (int64_t)cell_l * TAPE_SLOT;
+            for (int w = lane; (w << 2) < div; w += 64) {
+              uint32_t wd = 0;
+#pragma unroll
+              for (int q = 0; q < 4; q++)
+                wd |= (uint32_t)((TL[4 * w + q] & TF_EXEC) ? '+' : '-') << (8 * q);
+              st_async_u32(fl + 4 * w, wd);
+            }
+            for (int w = lane; (w << 2) < child; w += 64) {
+              uint32_t wd = 0;
+#pragma unroll
+              for (int q = 0; q < 4; q++) wd |= (uint32_t)(TL[div + 4 * w + q] & CODE_MASK) << (8 * q);
+              st_async_u32(ch + 4 * w, wd);
+            }
+          } else if (mode == AVGPU_MODE_WORLD && rec >= 0) {
+            // offspring genome with the divide mutations, 4 sites per lane
+            uint8_t* g = W.b_genome + (int64_t)rec * TAPE_SLOT;
+            for (int w = lane; (w << 2) < len; w += 64) {
+              uint32_t word = 0;
+#pragma unroll
+              for (int q = 0; q < 4; q++) {
+                const int j = 4 * w + q;
+                const int k2 = (dl >= 0 && j >= dl) ? j + 1 : j;        // index before the deletion
+                int v;
+                if (il >= 0 && k2 == il) v = ic;
+                else {
+                  const int k1 = (il >= 0 && k2 > il) ? k2 - 1 : k2;   // before the insertion
+                  v = (k1 == ml) ? mc : (TL[div + k1] & CODE_MASK);
+                }
+                word |= (j < len ? (uint32_t)v : 0u) << (8 * q);
+              }
+              st_async_u32(g + 4 * w, word);
+            }
+          }
+          // parent ClearFlags over its remaining sites, empty stacks
+          for (int w = lane; (w << 2) < div; w += 64) TL32[w] &= 0x3F3F3F3Fu;
+          if (lane < 2 * AVGPU_STACK_SIZE) stk[lane * 64 + L] = 0;
+        }
+      }
+    }
+
+    if (stepped && !stop) {
+      if (adv) ip = head_adjust(ip + 1, M);                   // ip.Advance() :1013
+      if (mx > 0 && tu >= mx) alive = false;                  // death :1045-1049
+    }
   }
 #undef GETREG
 #undef SETREG
@@ -638,7 +735,7 @@ __global__ __launch_bounds__(64) void k_interpret(DevWorld W, int cls, int mode,
     W.mem_size[cell] = M;
     W.cycles[cell] = cyc; W.time_used[cell] = tu; W.gest_start[cell] = gs;
     W.rng[2 * N + cell] = kct;
-    W.budget[cell] = spill ? budget : 0;
+    W.budget[cell] = spill ? (budget | (prim ? BUDGET_PRIM : 0)) : 0;
     W.errors[cell] = errs;
     W.inbuf[cell] = in0; W.inbuf[N + cell] = in1; W.inbuf[2 * N + cell] = in2;
     W.in_total[cell] = intot; W.in_ptr[cell] = inptr;
@@ -646,6 +743,23 @@ __global__ __launch_bounds__(64) void k_interpret(DevWorld W, int cls, int mode,
     W.cur_bonus[cell] = bonus;
 #pragma unroll
     for (int q = 0; q < AVGPU_NUM_LOGIC_TASKS; q++) W.cur_task[(int64_t)q * N + cell] = tc[q];
+    if (didv) {
+      W.executed[cell] = dexe; W.child_copied[cell] = dccop;
+      W.merit[cell] = dmerit; W.fitness[cell] = dfit; W.gest_time[cell] = dgt;
+      W.num_div[cell] = dnd; W.generation[cell] = dgen;
+#pragma unroll
+      for (int q = 0; q < AVGPU_NUM_LOGIC_TASKS; q++) W.last_task[(int64_t)q * N + cell] = lt[q];
+    }
+    // cur_reaction_count: reset at a divide, counted since (or added to the
+    // stored counts when no divide happened in this slice)
+#pragma unroll
+    for (int i = 0; i < AVGPU_MAX_REACTIONS; i++) {
+      int32_t* p = W.cur_react + (int64_t)i * N + cell;
+      if (i < W.n_react) {
+        if (didv) *p = rc[i];
+        else if (rc[i]) *p += rc[i];
+      }
+    }
 #pragma unroll
     for (int k = 0; k < 2 * AVGPU_STACK_SIZE; k++) W.stack[(int64_t)k * N + cell] = stk[k * 64 + lane];
     if (spill) {
@@ -654,14 +768,28 @@ __global__ __launch_bounds__(64) void k_interpret(DevWorld W, int cls, int mode,
       count_add(W, CNT_SPILLS, 1ull);
     }
   }
-  for (int j = 0; j < 64; j++) {
+  // tapes back to HBM: the same lane-linear quad image, 16 B per lane
+#pragma unroll 2
+  for (int it = 0; it < QUADS; it++) {
+    const int i = it * 64 + lane;
+    const int j = i / QUADS, q = i - j * QUADS;
     const int c = __shfl(cell, j);
     const int m = __shfl(M, j);
-    if (c < 0) continue;
-    uint32_t* dst = reinterpret_cast<uint32_t*>(W.tape + (int64_t)c * TAPE_SLOT);
-    const uint32_t* src = lds32 + j * (STRIDE / 4);
-    const int words = (m + 3) >> 2;
-    for (int w = lane; w < words; w += 64) dst[w] = src[w];
+    if (c >= 0 && q * 16 < m) {
+      const uint4 v = reinterpret_cast<const uint4*>(lds32)[i];
+      *reinterpret_cast<uint4*>(W.tape + (int64_t)c * TAPE_SLOT + q * 16) = v;
+    }
+  }
+  // ---- primary birth records -> birth queue (wavefront ballot + prefix) ----
+  {
+    const bool fresh = prim && !prim0;
+    const unsigned long long bm = __ballot(fresh);
+    if (bm) {
+      int base = 0;
+      if (lane == 0) base = atomicAdd(W.b_count, (int)__popcll(bm));
+      base = __shfl(base, 0);
+      if (fresh) W.b_list[base + (int)__popcll(bm & ((1ull << lane) - 1ull))] = cell;
+    }
   }
   // counters: one atomic per wave
   unsigned long long e = (unsigned long long)executed;
@@ -671,6 +799,7 @@ __global__ __launch_bounds__(64) void k_interpret(DevWorld W, int cls, int mode,
   int sl = active ? 1 : 0;
   int sites = active ? m_in + M : 0;
   for (int off = 32; off > 0; off >>= 1) {
+    ndrop += __shfl_down(ndrop, off);
     e += __shfl_down(e, off);
     dead += __shfl_down(dead, off);
     dv += __shfl_down(dv, off);
@@ -683,6 +812,7 @@ __global__ __launch_bounds__(64) void k_interpret(DevWorld W, int cls, int mode,
     count_add(W, CNT_INSTS, e);
     if (dead) count_add(W, CNT_DEATHS, (unsigned long long)dead);
     if (dv) count_add(W, CNT_DIVIDES, (unsigned long long)dv);
+    if (ndrop) count_add(W, CNT_DROPPED, (unsigned long long)ndrop);
     if (cls == 0) {
       count_add(W, CNT_C0_SLICES, (unsigned long long)sl);
       count_add(W, CNT_C0_SITES, (unsigned long long)sites);
@@ -712,17 +842,17 @@ __global__ __launch_bounds__(64) void k_interpret(DevWorld W, int cls, int mode,
 
 }  // namespace
 
-void launch_interpret_classes(const DevWorld& W, int mode, hipStream_t s, int64_t first,
-                              int64_t count, int* launches, hipEvent_t* after_class) {
+void launch_interpret_classes(const DevWorld& W, const DevWorld* dW, int mode, hipStream_t s,
+                              int64_t first, int64_t count, int* launches, hipEvent_t* after_class) {
   const unsigned blocks = (unsigned)((count + 63) / 64);
   if (blocks > 0) {
-    hipLaunchKernelGGL(k_interpret<CLASS0_SIZE>, dim3(blocks), dim3(64), 0, s, W, 0, mode, first, count);
+    hipLaunchKernelGGL(k_interpret<CLASS0_SIZE>, dim3(blocks), dim3(64), 0, s, dW, 0, mode, first, count);
     if (after_class) hipEventRecord(after_class[0], s);
-    hipLaunchKernelGGL(k_interpret<768>, dim3(blocks), dim3(64), 0, s, W, 1, mode, first, count);
+    hipLaunchKernelGGL(k_interpret<CLASS1_SIZE>, dim3(blocks), dim3(64), 0, s, dW, 1, mode, first, count);
     if (after_class) hipEventRecord(after_class[1], s);
-    hipLaunchKernelGGL(k_interpret<1536>, dim3(blocks), dim3(64), 0, s, W, 2, mode, first, count);
+    hipLaunchKernelGGL(k_interpret<CLASS2_SIZE>, dim3(blocks), dim3(64), 0, s, dW, 2, mode, first, count);
     if (after_class) hipEventRecord(after_class[2], s);
-    hipLaunchKernelGGL(k_interpret<2048>, dim3(blocks), dim3(64), 0, s, W, 3, mode, first, count);
+    hipLaunchKernelGGL(k_interpret<CLASS3_SIZE>, dim3(blocks), dim3(64), 0, s, dW, 3, mode, first, count);
     if (launches) *launches += 4;
   } else if (after_class) {
     for (int k = 0; k < 3; k++) hipEventRecord(after_class[k], s);

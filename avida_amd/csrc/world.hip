@@ -287,9 +287,10 @@ __global__ void k_occ_init(DevWorld W) {
 
 __global__ void k_place_pick(DevWorld W) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int nb = min(*W.b_count, (int)W.bcap);
-  if (i >= nb || W.b_state[i] != 0) return;
-  const int parent = W.b_parent[i];
+  if (i >= queue_len(W)) return;
+  const int64_t r = rec_of(W, i);
+  if (W.b_state[r] != 0) return;
+  const int parent = W.b_parent[r];
   int nbr[8];
   const int nn = neighbours(W, parent, nbr);
   int cand[9];
@@ -300,47 +301,48 @@ __global__ void k_place_pick(DevWorld W) {
     for (int k = 0; k < nn; k++) cand[nc++] = nbr[k];
     if (W.allow_parent) cand[nc++] = parent;
   }
-  if (nc == 0) { W.b_state[i] = -1; return; }
-  const uint32_t lo = W.b_rng[i], hi = W.b_rng[W.bcap + i];
-  uint32_t ctr = W.b_rng[2 * W.bcap + i];
+  if (nc == 0) { W.b_state[r] = -1; return; }
+  const uint32_t lo = W.b_rng[r], hi = W.b_rng[W.rcap + r];
+  uint32_t ctr = W.b_rng[2 * W.rcap + r];
   const int t = cand[rng_below(lo, hi, ctr, (uint32_t)nc)];
   const unsigned long long prio = ((unsigned long long)rng_next(lo, hi, ctr) << 32) |
                                   ((unsigned long long)(parent & 0xFFFFFF) << 8) |
-                                  (unsigned long long)(W.b_seq[i] & 0xFF);
-  W.b_rng[2 * W.bcap + i] = ctr;
-  W.b_target[i] = t;
-  W.b_prio[i] = prio;
+                                  (unsigned long long)(W.b_seq[r] & 0xFF);
+  W.b_rng[2 * W.rcap + r] = ctr;
+  W.b_target[r] = t;
+  W.b_prio[r] = prio;
   atomicMax(&W.claim[t], prio);
 }
 
 __global__ void k_place_resolve(DevWorld W) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int nb = min(*W.b_count, (int)W.bcap);
-  if (i >= nb || W.b_state[i] != 0) return;
-  const int t = W.b_target[i];
-  if (W.claim[t] == W.b_prio[i]) {
-    W.b_state[i] = 1;
+  if (i >= queue_len(W)) return;
+  const int64_t r = rec_of(W, i);
+  if (W.b_state[r] != 0) return;
+  const int t = W.b_target[r];
+  if (W.claim[t] == W.b_prio[r]) {
+    W.b_state[r] = 1;
     W.occ[t] = 1;
-    W.owner[t] = (int)i;
+    W.owner[t] = (int)r;
   }
 }
 
 __global__ void k_place_clear(DevWorld W) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int nb = min(*W.b_count, (int)W.bcap);
-  if (i >= nb) return;
-  const int t = W.b_target[i];
+  if (i >= queue_len(W)) return;
+  const int t = W.b_target[rec_of(W, i)];
   if (t >= 0) W.claim[t] = 0ull;
 }
 
 // ActivateOrganism (main/cPopulation.cc:1320-1340) + SetupOffspring (main/cPhenotype.cc:349-420)
 // One wave per birth: the genome copy is coalesced across the wave.
 __global__ __launch_bounds__(64) void k_activate(DevWorld W) {
-  const int nb = min(*W.b_count, (int)W.bcap);
+  const int nb = queue_len(W);
   const int lane = threadIdx.x;
   const int64_t N = W.n;
   unsigned long long born = 0, lost = 0;
-  for (int64_t i = blockIdx.x; i < nb; i += gridDim.x) {
+  for (int64_t q = blockIdx.x; q < nb; q += gridDim.x) {
+    const int64_t i = rec_of(W, q);
     const int tgt = W.b_target[i];
     const bool won = W.b_state[i] == 1 && tgt >= 0 && W.owner[tgt] == (int)i;
     if (!won) { lost++; continue; }
@@ -395,8 +397,8 @@ __global__ __launch_bounds__(64) void k_activate(DevWorld W) {
       case 52: W.executed[c] = W.b_exec[i]; break;
       case 53: W.errors[c] = 0; break;
       case 54: {
-        const uint32_t lo = W.b_rng[i], hi = W.b_rng[W.bcap + i];
-        uint32_t ctr = W.b_rng[2 * W.bcap + i];
+        const uint32_t lo = W.b_rng[i], hi = W.b_rng[W.rcap + i];
+        uint32_t ctr = W.b_rng[2 * W.rcap + i];
         // cEnvironment::SetupInputs random (main/cEnvironment.cc:1268-1271)
         W.inputs[c] = (15 << 24) + (int)rng_below(lo, hi, ctr, 1u << 24);
         W.inputs[N + c] = (51 << 24) + (int)rng_below(lo, hi, ctr, 1u << 24);
@@ -538,20 +540,20 @@ void launch_merit_total(const DevWorld& W, hipStream_t s, double* totals, double
 
 void launch_world_pre(const DevWorld& W, hipStream_t s, const double* totals) {
   hipMemsetAsync(W.counters, 0, sizeof(unsigned long long) * NSHARD * CNT_STRIDE, s);
-  hipMemsetAsync(W.b_count, 0, sizeof(int32_t), s);
+  hipMemsetAsync(W.b_count, 0, 2 * sizeof(int32_t), s);
   hipMemsetAsync(W.class_count, 0, sizeof(int32_t) * NUM_CLASSES, s);
   hipLaunchKernelGGL(k_allot, dim3(nblk(W.n, 256)), dim3(256), 0, s, W, totals);
 }
 
 void launch_world_post(const DevWorld& W, hipStream_t s, double* stats) {
-  const unsigned bb = nblk(W.bcap, 256);
+  const unsigned bb = nblk(W.rcap, 256);
   hipLaunchKernelGGL(k_occ_init, dim3(nblk(W.n, 256)), dim3(256), 0, s, W);
   for (int round = 0; round < 4; round++) {
     hipLaunchKernelGGL(k_place_pick, dim3(bb), dim3(256), 0, s, W);
     hipLaunchKernelGGL(k_place_resolve, dim3(bb), dim3(256), 0, s, W);
     hipLaunchKernelGGL(k_place_clear, dim3(bb), dim3(256), 0, s, W);
   }
-  hipLaunchKernelGGL(k_activate, dim3((unsigned)std::min<int64_t>(W.bcap, 32768)), dim3(64), 0, s, W);
+  hipLaunchKernelGGL(k_activate, dim3((unsigned)std::min<int64_t>(W.rcap, 32768)), dim3(64), 0, s, W);
   const int64_t nb = (W.n + 255) / 256;
   double* part = stats + NSTAT;
   hipLaunchKernelGGL(k_stats_partial, dim3((unsigned)nb), dim3(256), 0, s, W, part);

@@ -18,7 +18,8 @@ MODE_WORLD, MODE_TEST, MODE_FROZEN = 0, 1, 2
 # enum avgpu_counter
 (CNT_INSTS, CNT_DEATHS, CNT_DIVIDES, CNT_BIRTHS, CNT_DROPPED, CNT_SPILLS, CNT_SLICES,
  CNT_LANESTEPS, CNT_C0_SLICES, CNT_C0_SITES, CNT_CLK_STAGE, CNT_CLK_LOOP, CNT_CLK_WB,
- CNT_ITERS, CNT_IT_FAST, CNT_IT_COPY, CNT_IT_SLOW, CNT_WAVES) = range(18)
+ CNT_ITERS, CNT_IT_FAST, CNT_IT_COPY, CNT_IT_SLOW, CNT_WAVES, CNT_HALO_SENT,
+ CNT_HALO_LOST) = range(20)
 NUM_COUNTERS = 32
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -109,7 +110,8 @@ EXPORTED = [
     "avgpu_step", "avgpu_run_update", "avgpu_run_updates", "avgpu_update_totals",
     "avgpu_update_run", "avgpu_set_stream", "avgpu_get_states",
     "avgpu_test_genomes", "avgpu_get_stats", "avgpu_stats_vector", "avgpu_set_global_totals",
-    "avgpu_halo_pack", "avgpu_halo_unpack", "avgpu_halo_record_bytes",
+    "avgpu_set_tile", "avgpu_tile_buffer_bytes", "avgpu_set_tile_buffers", "avgpu_tile_partials",
+    "avgpu_tile_begin", "avgpu_tile_place", "avgpu_tile_finish",
     "avgpu_last_step_insts", "avgpu_last_kernel_ms", "avgpu_kernel_times", "avgpu_counters",
 ]
 
@@ -184,6 +186,15 @@ def bind_common(lib, prefix):
         "last_step_insts": (C.c_int, [V, C.POINTER(C.c_int64)]),
         "set_global_totals": (C.c_int, [V, C.c_double, I64]),
         "destroy": (C.c_int, [V]),
+        # strip tiles (include/avida_gpu.h "strip tiles")
+        "set_tile": (C.c_int, [V, I64, I64]),
+        "tile_buffer_bytes": (C.c_int, [V, C.POINTER(I64), C.POINTER(I64), C.POINTER(I64)]),
+        "set_tile_buffers": (C.c_int, [V] + [V] * 8),
+        "tile_partials": (C.c_int, [V, V]),
+        "tile_begin": (C.c_int, [V, V, C.c_int]),
+        "tile_place": (C.c_int, [V, C.c_int, C.c_int]),
+        "tile_finish": (C.c_int, [V, C.POINTER(AvgpuUpdateStats)]),
+        "get_stats": (C.c_int, [V, C.POINTER(AvgpuUpdateStats)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, p + name, None)
@@ -213,10 +224,6 @@ def load_product(path=None):
     lib.avgpu_sync.argtypes = [C.c_void_p]
     lib.avgpu_get_stats.argtypes = [C.c_void_p, C.POINTER(AvgpuUpdateStats)]
     lib.avgpu_stats_vector.argtypes = [C.c_void_p, C.POINTER(C.c_void_p)]
-    lib.avgpu_halo_pack.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_int64,
-                                    C.POINTER(C.c_int64)]
-    lib.avgpu_halo_unpack.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_int64]
-    lib.avgpu_halo_record_bytes.restype = C.c_int64
     lib.avgpu_last_kernel_ms.argtypes = [C.c_void_p, C.POINTER(C.c_double),
                                          C.POINTER(C.c_int64)]
     lib.avgpu_kernel_times.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_int64)]

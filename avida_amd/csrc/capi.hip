@@ -66,6 +66,9 @@ struct avgpu_world {
   float last_kernel_ms = 0.f;
   int64_t last_launches = 0;
   bool has_test_buffers = false;
+  // strip tiles
+  int ntiles_last = 0;
+  bool tile_buffers = false;
 
   template <typename T>
   int alloc(T** p, size_t count) {
@@ -107,7 +110,8 @@ int setup_world(avgpu_world* w, int64_t n, bool test_buffers) {
   A(b_fitness, R); A(b_gen, R); A(b_ccopied, R); A(b_exec, R);
   A(b_gest, R); A(b_rng, 3 * R); A(b_target, R); A(b_state, R);
   A(b_prio, R); A(b_genome, (size_t)R * TAPE_SLOT);
-  A(occ, n); A(claim, n); A(owner, n);
+  // placement scratch with two ghost rows (strip tiles)
+  A(occ, n + 2 * c.world_x); A(claim, n + 2 * c.world_x); A(owner, n + 2 * c.world_x);
   if (test_buffers) {
     A(t_flags, (size_t)n * TAPE_SLOT); A(t_flags_len, n); A(t_child, (size_t)n * TAPE_SLOT);
     A(t_child_len, n);
@@ -147,6 +151,9 @@ int setup_world(avgpu_world* w, int64_t n, bool test_buffers) {
   W.seed_hi = (uint32_t)(c.seed >> 32);
   W.row0 = 0;
   W.global_rows = c.world_y;
+  W.rows = c.world_y;
+  W.tiled = 0;
+  W.cell0 = 0;
   // logic id -> task bitmask (main/cTaskLib.cc:511-575)
   static const int sets[9][6] = {
       {15, 51, 85, -1, -1, -1}, {63, 95, 119, -1, -1, -1}, {136, 160, 192, -1, -1, -1},
@@ -695,17 +702,103 @@ int avgpu_set_global_totals(avgpu_world* w, double total_merit, int64_t total_or
   return 0;
 }
 
-int avgpu_halo_pack(avgpu_world* w, int side, void* dev_buf, int64_t cap, int64_t* n) {
-  (void)w; (void)side; (void)dev_buf; (void)cap; (void)n;
-  return fail(AVGPU_EUNSUPPORTED, "halo exchange not built yet");
+// ---- strip tiles (DESIGN.md "Multi-GPU") ----
+int avgpu_set_tile(avgpu_world* w, int64_t row0, int64_t arena_bytes) {
+  if (!w) return fail(AVGPU_EINVAL, "NULL world");
+  DevWorld& W = w->W;
+  const int64_t X = W.world_x;
+  if (X <= 0 || W.n % X) return fail(AVGPU_EINVAL, "tile cells must be whole rows of WORLD_X");
+  const int64_t rows = W.n / X;
+  if (rows < 2) return fail(AVGPU_EINVAL, "a tile needs at least 2 rows");
+  if (W.n % 256) return fail(AVGPU_EINVAL, "tile cells must be a multiple of 256 (merit blocks)");
+  if (row0 < 0 || row0 + rows > W.global_rows)
+    return fail(AVGPU_EINVAL, "tile rows outside WORLD_Y (the global row count)");
+  if (arena_bytes <= 0) arena_bytes = std::max<int64_t>(256 * 1024, X * 256);
+  arena_bytes = (arena_bytes + 15) / 16 * 16;
+  W.row0 = (int32_t)row0;
+  W.rows = (int32_t)rows;
+  W.tiled = rows < W.global_rows ? 1 : 0;
+  W.cell0 = row0 * X;
+  W.r_arena = arena_bytes;
+  w->tile_buffers = false;
+  return 0;
 }
 
-int avgpu_halo_unpack(avgpu_world* w, int side, const void* dev_buf, int64_t n) {
-  (void)w; (void)side; (void)dev_buf; (void)n;
-  return fail(AVGPU_EUNSUPPORTED, "halo exchange not built yet");
+int avgpu_tile_buffer_bytes(avgpu_world* w, int64_t* partial_bytes, int64_t* halo_b, int64_t* record_b) {
+  if (!w) return fail(AVGPU_EINVAL, "NULL world");
+  if (partial_bytes) *partial_bytes = 2 * ((w->W.n + 255) / 256) * (int64_t)sizeof(double);
+  if (halo_b) *halo_b = halo_bytes(w->W.world_x);
+  if (record_b) *record_b = record_bytes(w->W.world_x, w->W.r_arena);
+  return 0;
 }
 
-int64_t avgpu_halo_record_bytes(void) { return 0; }
+int avgpu_set_tile_buffers(avgpu_world* w, void* halo_send_up, void* halo_send_down, void* halo_recv_up,
+                           void* halo_recv_down, void* rec_send_up, void* rec_send_down,
+                           void* rec_recv_up, void* rec_recv_down) {
+  if (!w) return fail(AVGPU_EINVAL, "NULL world");
+  if (!w->W.tiled) return fail(AVGPU_ESTATE, "avgpu_set_tile did not make this world a strip tile");
+  void* p[8] = {halo_send_up, halo_send_down, halo_recv_up, halo_recv_down,
+                rec_send_up, rec_send_down, rec_recv_up, rec_recv_down};
+  for (int i = 0; i < 8; i++)
+    if (!p[i]) return fail(AVGPU_EINVAL, "NULL tile buffer");
+  DevWorld& W = w->W;
+  W.h_send[0] = (uint8_t*)p[0]; W.h_send[1] = (uint8_t*)p[1];
+  W.h_recv[0] = (uint8_t*)p[2]; W.h_recv[1] = (uint8_t*)p[3];
+  W.r_send[0] = (uint8_t*)p[4]; W.r_send[1] = (uint8_t*)p[5];
+  W.r_recv[0] = (uint8_t*)p[6]; W.r_recv[1] = (uint8_t*)p[7];
+  w->tile_buffers = true;
+  return 0;
+}
+
+static int tile_ready(avgpu_world* w) {
+  int rc = ready(w);
+  if (rc < 0) return rc;
+  if (!w->W.tiled || !w->tile_buffers) return fail(AVGPU_ESTATE, "not a strip tile with registered buffers");
+  return 0;
+}
+
+int avgpu_tile_partials(avgpu_world* w, double* dev_out) {
+  int rc = ready(w);
+  if (rc < 0) return rc;
+  if (!dev_out) return fail(AVGPU_EINVAL, "dev_out is NULL");
+  launch_tile_partials(w->W, w->stream, dev_out);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+int avgpu_tile_begin(avgpu_world* w, const double* dev_gathered, int ntiles) {
+  int rc = tile_ready(w);
+  if (rc < 0) return rc;
+  if (!dev_gathered || ntiles < 1) return fail(AVGPU_EINVAL, "gathered partials");
+  launch_tile_totals(w->W, w->stream, dev_gathered, ntiles, w->d_totals);
+  launch_world_pre(w->W, w->stream, w->d_totals);
+  HIPCHK(hipGetLastError());
+  rc = interpret(w, AVGPU_MODE_WORLD, 0, w->W.n);
+  if (rc < 0) return rc;
+  launch_tile_after_interpret(w->W, w->stream);
+  HIPCHK(hipGetLastError());
+  w->ntiles_last = ntiles;
+  return 0;
+}
+
+int avgpu_tile_place(avgpu_world* w, int round, int phase) {
+  int rc = tile_ready(w);
+  if (rc < 0) return rc;
+  if (round < 0 || round > 3 || phase < 0 || phase > 3) return fail(AVGPU_EINVAL, "round / phase");
+  launch_tile_place(w->W, w->stream, round, phase);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+int avgpu_tile_finish(avgpu_world* w, avgpu_update_stats* out) {
+  int rc = tile_ready(w);
+  if (rc < 0) return rc;
+  launch_tile_finish(w->W, w->stream, w->d_stats);
+  HIPCHK(hipGetLastError());
+  w->update++;
+  if (out) return avgpu_get_stats(w, out);
+  return 0;
+}
 
 int avgpu_last_step_insts(avgpu_world* w, int64_t* insts) {
   if (!w || !insts) return fail(AVGPU_EINVAL, "args");

@@ -96,13 +96,13 @@ struct DevWorld {
   int32_t* b_gest;    // [rcap]
   uint32_t* b_rng;    // [3][rcap]
   int32_t* b_target;  // [rcap]
-  int8_t* b_state;    // [rcap]  0 pending 1 placed -1 failed
+  int8_t* b_state;    // [rcap]  0 pending, 1+k placed in round k, -1 failed
   unsigned long long* b_prio; // [rcap]
   uint8_t* b_genome;  // [rcap][TAPE_SLOT]
-  // placement scratch
-  uint8_t* occ;       // [n]
-  unsigned long long* claim; // [n]
-  int32_t* owner;     // [n]
+  // placement scratch, n cells + 2 ghost rows (strip tiles, below)
+  uint8_t* occ;       // [n + 2X]
+  unsigned long long* claim; // [n + 2X]
+  int32_t* owner;     // [n + 2X]  record id, -1 none, REMOTE_OWNER(k) won by a halo birth in round k
   // test-CPU outputs
   uint8_t* t_flags;   // [n][TAPE_SLOT] executed flags snapshot ('+'/'-')
   int32_t* t_flags_len; // [n]
@@ -133,10 +133,37 @@ struct DevWorld {
   int32_t prefer_empty, allow_parent, birth_method;
   uint64_t th_copy_mut, th_div_mut, th_div_ins, th_div_del;
   uint32_t seed_lo, seed_hi;
-  // tile geometry for multi-GPU strips (rows [row0,row0+rows) of a
-  // world_x x global_rows torus); single GPU: row0=0, rows=world_y
-  int32_t row0, global_rows;
+  // Strip tiles (multi-GPU, DESIGN.md "Multi-GPU"): this world holds rows
+  // [row0, row0+rows) of a world_x x global_rows torus / grid.  When tiled,
+  // occ / claim / owner carry two ghost rows after the n cells: [n, n+X) is
+  // global row row0-1 (the tile above), [n+X, n+2X) global row row0+rows (the
+  // tile below).  Single world: tiled = 0, row0 = 0, rows = global_rows = world_y.
+  int32_t row0, global_rows, rows, tiled;
+  int64_t cell0;          // row0 * world_x: global id of local cell 0 (RNG keys, priorities)
+  // halo buffers per direction d (0: tile above, 1: tile below), registered by
+  // the host: HALO_BYTES(X) = X u64 claims then X u8 occupancy flags
+  uint8_t* h_send[2];
+  uint8_t* h_recv[2];
+  // birth-record buffers per direction: HaloHdr, X HaloRec, arena of r_arena bytes
+  uint8_t* r_send[2];
+  uint8_t* r_recv[2];
+  int64_t r_arena;
 };
+
+#define REMOTE_OWNER(k) (-2 - (k))
+__host__ __device__ inline int64_t halo_bytes(int x) { return ((int64_t)x * 9 + 15) / 16 * 16; }
+struct HaloHdr { int32_t count, arena_used, overflow, pad; };
+// one offspring placed across a tile edge (the migrant record of
+// cMultiProcessWorld.cc:142-190, restated for strip tiles)
+struct HaloRec {
+  int32_t col, round, len, gen, ccopied, exec, gest;
+  uint32_t rng_lo, rng_hi, rng_ctr;
+  int32_t off, pad;
+  double merit, fitness;
+};
+__host__ __device__ inline int64_t record_bytes(int x, int64_t arena) {
+  return (int64_t)sizeof(HaloHdr) + (int64_t)x * (int64_t)sizeof(HaloRec) + arena;
+}
 
 // counters[] slots
 #define CNT_INSTS 0
@@ -158,6 +185,8 @@ struct DevWorld {
 #define CNT_IT_COPY 15    /* ... the h-copy block */
 #define CNT_IT_SLOW 16    /* ... the switch */
 #define CNT_WAVES 17
+#define CNT_HALO_SENT 18  /* offspring shipped to a neighbouring tile */
+#define CNT_HALO_LOST 19  /* offspring lost to a full halo arena (counted in DROPPED too) */
 // Counters are sharded over NSHARD lines (CNT_STRIDE x u64 each) so that the
 // per-wave adds of a 16K-wave launch do not serialise on one L2 address; they
 // are cleared every update, and counters[CNT_CUM_BASE + k] accumulates slot k
@@ -296,3 +325,10 @@ void launch_set_orgs(const DevWorld& W, hipStream_t s, int64_t first, int64_t co
 void launch_get_states(const DevWorld& W, hipStream_t s, int64_t first, int64_t count,
                        avgpu_cpu_state* d_states, uint8_t* d_codes, int cap);
 void launch_merit_total(const DevWorld& W, hipStream_t s, double* d_totals, double* d_scratch);
+// strip tiles
+void launch_tile_partials(const DevWorld& W, hipStream_t s, double* d_out);
+void launch_tile_totals(const DevWorld& W, hipStream_t s, const double* d_gathered, int ntiles,
+                        double* d_totals);
+void launch_tile_after_interpret(const DevWorld& W, hipStream_t s);
+void launch_tile_place(const DevWorld& W, hipStream_t s, int round, int phase);
+void launch_tile_finish(const DevWorld& W, hipStream_t s, double* d_stats);

@@ -66,7 +66,7 @@ __global__ void k_set_orgs(DevWorld W, int64_t first, int64_t count, const uint8
   W.birth_len[c] = len;
   // stream key (DESIGN.md RNG spec)
   uint32_t lo, hi, ctr = 0;
-  derive_key(W.seed_lo, W.seed_hi, (uint32_t)c, 0xA5A5A5A5U, lo, hi);
+  derive_key(W.seed_lo, W.seed_hi, (uint32_t)(W.cell0 + c), 0xA5A5A5A5U, lo, hi);
   int in0, in1, in2;
   if (inputs) { in0 = inputs[3 * i]; in1 = inputs[3 * i + 1]; in2 = inputs[3 * i + 2]; }
   else if (deterministic) { in0 = 0x0f13149f; in1 = 0x3308e53e; in2 = 0x556241eb; }
@@ -170,7 +170,11 @@ __global__ void k_classify_uniform(DevWorld W, int64_t first, int64_t count, con
 }
 
 // ---- deterministic total merit: 256-cell blocks, fixed pairwise tree ----
-__global__ __launch_bounds__(256) void k_merit_partial(DevWorld W, double* partial, int32_t* alive_partial) {
+// (strip tiles hold whole 256-cell blocks, so the block partials of a tiled
+// world are the single world's partials; alive_d: alive counts as doubles
+// after the merits, the layout tiles exchange)
+__global__ __launch_bounds__(256) void k_merit_partial(DevWorld W, double* partial, int32_t* alive_partial,
+                                                       double* alive_d) {
   __shared__ double s[256];
   __shared__ int a[256];
   const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -185,20 +189,34 @@ __global__ __launch_bounds__(256) void k_merit_partial(DevWorld W, double* parti
     }
     __syncthreads();
   }
-  if (threadIdx.x == 0) { partial[blockIdx.x] = s[0]; alive_partial[blockIdx.x] = a[0]; }
+  if (threadIdx.x == 0) {
+    partial[blockIdx.x] = s[0];
+    if (alive_partial) alive_partial[blockIdx.x] = a[0];
+    if (alive_d) alive_d[blockIdx.x] = (double)a[0];
+  }
 }
 
 // totals[0] = sum merit, totals[1] = alive count.  Lane t sums partials
 // t, t+256, ... in order, then the fixed pairwise tree (oracle: tree_merit_sum).
+// Tiled: the partials of tile k are gathered[k*2*nb ..], alive counts after them.
+template <bool TILES>
 __global__ __launch_bounds__(256) void k_merit_final(const double* partial, const int32_t* alive_partial,
-                                                     int64_t nb, double* totals, int use_global) {
+                                                     const double* gathered, int64_t nb, int ntiles,
+                                                     double* totals, int use_global) {
   __shared__ double s[256];
   __shared__ long long cnt[256];
   long long c = 0;
   double acc = 0.0;
-  for (int64_t b = threadIdx.x; b < nb; b += 256) {
-    c += alive_partial[b];
-    acc = __dadd_rn(acc, partial[b]);
+  const int64_t total = TILES ? nb * ntiles : nb;
+  for (int64_t b = threadIdx.x; b < total; b += 256) {
+    if (TILES) {
+      const int64_t k = b / nb, j = b - k * nb;
+      acc = __dadd_rn(acc, gathered[k * 2 * nb + j]);
+      c += (long long)gathered[k * 2 * nb + nb + j];
+    } else {
+      c += alive_partial[b];
+      acc = __dadd_rn(acc, partial[b]);
+    }
   }
   cnt[threadIdx.x] = c;
   s[threadIdx.x] = acc;
@@ -210,12 +228,9 @@ __global__ __launch_bounds__(256) void k_merit_final(const double* partial, cons
     }
     __syncthreads();
   }
-  if (threadIdx.x == 0) {
-    if (!use_global) {
-      totals[0] = s[0];
-      totals[1] = (double)cnt[0];
-    }
-    totals[2] = (double)cnt[0];  // local organisms
+  if (threadIdx.x == 0 && !use_global) {
+    totals[0] = s[0];
+    totals[1] = (double)cnt[0];
   }
 }
 
@@ -261,9 +276,11 @@ __global__ void k_allot(DevWorld W, const double* totals) {
 }
 
 // ---- birth placement (cPopulation::PositionOffspring restated) ----
-// neighbour k of cell in fixed order NW N NE W E SW S SE (tools/cTopology.h)
+// neighbour k of cell in fixed order NW N NE W E SW S SE (tools/cTopology.h).
+// Tiled worlds map the rows above / below the strip to the ghost rows
+// [n, n+X) / [n+X, n+2X) of occ / claim / owner.
 __device__ __forceinline__ int neighbours(const DevWorld& W, int cell, int* out) {
-  const int X = W.world_x, Y = W.world_y;
+  const int X = W.world_x, R = W.rows;
   const int x = cell % X, y = cell / X;
   int n = 0;
   for (int dy = -1; dy <= 1; dy++)
@@ -271,18 +288,29 @@ __device__ __forceinline__ int neighbours(const DevWorld& W, int cell, int* out)
       if (dx == 0 && dy == 0) continue;
       int nx = x + dx, ny = y + dy;
       if (W.geometry == 1) {
-        if (nx < 0 || nx >= X || ny < 0 || ny >= Y) continue;
+        if (nx < 0 || nx >= X) continue;
       } else {
-        nx = (nx + X) % X; ny = (ny + Y) % Y;
+        nx = (nx + X) % X;
       }
-      out[n++] = ny * X + nx;
+      if (ny >= 0 && ny < R) {
+        out[n++] = ny * X + nx;
+      } else if (!W.tiled) {
+        if (W.geometry == 1) continue;
+        ny = (ny + R) % R;
+        out[n++] = ny * X + nx;
+      } else {
+        const int gy = W.row0 + ny;
+        if (W.geometry == 1 && (gy < 0 || gy >= W.global_rows)) continue;
+        out[n++] = (int)W.n + (ny < 0 ? 0 : X) + nx;
+      }
     }
   return n;
 }
 
 __global__ void k_occ_init(DevWorld W) {
   const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (c < W.n) { W.occ[c] = (W.ctl[c] & CTL_ALIVE) ? 1 : 0; W.owner[c] = -1; }
+  const int64_t ext = W.n + (W.tiled ? 2 * (int64_t)W.world_x : 0);
+  if (c < ext) { W.occ[c] = (c < W.n && (W.ctl[c] & CTL_ALIVE)) ? 1 : 0; W.owner[c] = -1; }
 }
 
 __global__ void k_place_pick(DevWorld W) {
@@ -305,8 +333,9 @@ __global__ void k_place_pick(DevWorld W) {
   const uint32_t lo = W.b_rng[r], hi = W.b_rng[W.rcap + r];
   uint32_t ctr = W.b_rng[2 * W.rcap + r];
   const int t = cand[rng_below(lo, hi, ctr, (uint32_t)nc)];
+  // priority: draw, then the parent's GLOBAL cell id, so that tiles agree
   const unsigned long long prio = ((unsigned long long)rng_next(lo, hi, ctr) << 32) |
-                                  ((unsigned long long)(parent & 0xFFFFFF) << 8) |
+                                  ((unsigned long long)((W.cell0 + parent) & 0xFFFFFF) << 8) |
                                   (unsigned long long)(W.b_seq[r] & 0xFF);
   W.b_rng[2 * W.rcap + r] = ctr;
   W.b_target[r] = t;
@@ -314,14 +343,16 @@ __global__ void k_place_pick(DevWorld W) {
   atomicMax(&W.claim[t], prio);
 }
 
-__global__ void k_place_resolve(DevWorld W) {
+// which: 0 every target, 1 targets inside the tile, 2 ghost-row targets
+__global__ void k_place_resolve(DevWorld W, int round, int which) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= queue_len(W)) return;
   const int64_t r = rec_of(W, i);
   if (W.b_state[r] != 0) return;
   const int t = W.b_target[r];
+  if ((which == 1 && t >= W.n) || (which == 2 && t < W.n)) return;
   if (W.claim[t] == W.b_prio[r]) {
-    W.b_state[r] = 1;
+    W.b_state[r] = (int8_t)(1 + round);
     W.occ[t] = 1;
     W.owner[t] = (int)r;
   }
@@ -334,79 +365,235 @@ __global__ void k_place_clear(DevWorld W) {
   if (t >= 0) W.claim[t] = 0ull;
 }
 
-// ActivateOrganism (main/cPopulation.cc:1320-1340) + SetupOffspring (main/cPhenotype.cc:349-420)
-// One wave per birth: the genome copy is coalesced across the wave.
+// ---- strip-tile halo (DESIGN.md "Multi-GPU") ----
+// Edge rows: top = local row 0, bottom = local row rows-1; ghost rows after n.
+__device__ __forceinline__ int64_t edge_cell(const DevWorld& W, int d, int x) {
+  return d == 0 ? (int64_t)x : (int64_t)(W.rows - 1) * W.world_x + x;
+}
+__device__ __forceinline__ int64_t ghost_cell(const DevWorld& W, int d, int x) {
+  return W.n + (int64_t)d * W.world_x + x;
+}
+__device__ __forceinline__ unsigned long long* halo_claims(uint8_t* b) {
+  return reinterpret_cast<unsigned long long*>(b);
+}
+__device__ __forceinline__ uint8_t* halo_occ(uint8_t* b, int X) { return b + (int64_t)X * 8; }
+
+// what: 0 edge-row occupancy; 1 ghost-row claims; 2 merged edge-row claims + occupancy
+__global__ void k_halo_export(DevWorld W, int what) {
+  const int X = W.world_x;
+  const int g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= 2 * X) return;
+  const int d = g / X, x = g - d * X;
+  uint8_t* b = W.h_send[d];
+  if (what == 1) {
+    halo_claims(b)[x] = W.claim[ghost_cell(W, d, x)];
+  } else {
+    const int64_t c = edge_cell(W, d, x);
+    halo_occ(b, X)[x] = W.occ[c];
+    halo_claims(b)[x] = what == 2 ? W.claim[c] : 0ull;
+  }
+}
+
+// what 0: ghost occupancy from the neighbours' edge rows (before round 0);
+// what 1: merge the neighbours' claims on my edge rows and mark the cells a
+//         halo birth won (unique maximum priority) this round;
+// what 2: ghost rows take the neighbours' merged claims and occupancy.
+__global__ void k_halo_import(DevWorld W, int what, int round) {
+  const int X = W.world_x;
+  const int g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= 2 * X) return;
+  const int d = g / X, x = g - d * X;
+  uint8_t* b = W.h_recv[d];
+  if (what == 0) {
+    W.occ[ghost_cell(W, d, x)] = halo_occ(b, X)[x];
+  } else if (what == 1) {
+    const int64_t c = edge_cell(W, d, x);
+    const unsigned long long rc = halo_claims(b)[x];
+    unsigned long long m = W.claim[c];
+    if (rc > m) m = rc;
+    W.claim[c] = m;
+    if (rc != 0ull && m == rc) { W.owner[c] = REMOTE_OWNER(round); W.occ[c] = 1; }
+  } else {
+    const int64_t c = ghost_cell(W, d, x);
+    W.claim[c] = halo_claims(b)[x];
+    W.occ[c] = halo_occ(b, X)[x];
+  }
+}
+
+// claims on the edge rows and ghost rows are cleared wholesale (remote
+// records claim there without being in this tile's queue)
+__global__ void k_halo_clear(DevWorld W) {
+  const int X = W.world_x;
+  const int g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= 2 * X) return;
+  const int d = g / X, x = g - d * X;
+  W.claim[edge_cell(W, d, x)] = 0ull;
+  W.claim[ghost_cell(W, d, x)] = 0ull;
+}
+
+// ActivateOrganism (main/cPopulation.cc:1320-1340) + SetupOffspring
+// (main/cPhenotype.cc:349-420) of one offspring into cell c by one wave: lane
+// k < 20 clears stack slot k, the rest of the organism's fields are scattered
+// over SoA rows, so each lane stores one of them.
+struct Child {
+  int len, gen, ccopied, exec, gest;
+  double merit, fitness;
+  uint32_t lo, hi, ctr;
+};
+__device__ __forceinline__ void setup_child(const DevWorld& W, int64_t c, const Child& b,
+                                            const uint32_t* src, int lane) {
+  const int64_t N = W.n;
+  const int len = b.len;
+  uint32_t* dst = reinterpret_cast<uint32_t*>(W.tape + c * TAPE_SLOT);
+  for (int w = lane; w < (len + 3) / 4; w += 64) dst[w] = src[w];
+  if (lane < 2 * AVGPU_STACK_SIZE) W.stack[lane * N + c] = 0;
+  if (lane < AVGPU_MAX_REACTIONS) {
+    W.cur_task[lane * N + c] = 0; W.last_task[lane * N + c] = 0; W.cur_react[lane * N + c] = 0;
+  }
+  switch (lane) {
+    case 20: W.reg[c] = 0; break;
+    case 21: W.reg[N + c] = 0; break;
+    case 22: W.reg[2 * N + c] = 0; break;
+    case 23: W.inbuf[c] = 0; break;
+    case 24: W.inbuf[N + c] = 0; break;
+    case 25: W.inbuf[2 * N + c] = 0; break;
+    case 26: W.head[c] = 0; break;
+    case 27: W.head[N + c] = 0; break;
+    case 28: W.head[2 * N + c] = 0; break;
+    case 29: W.head[3 * N + c] = 0; break;
+    case 30: W.ctl[c] = CTL_ALIVE; break;
+    case 31: W.rlabel[c] = 0; break;
+    case 32: W.mem_size[c] = len; break;
+    case 33: W.cycles[c] = 0; break;
+    case 34: W.time_used[c] = 0; break;
+    case 35: W.gest_start[c] = 0; break;
+    case 36: {
+      int mx = 0;
+      if (W.death_method > 0) { mx = W.age_limit; if (W.death_method == 2) mx *= len; if (mx < 1) mx = 1; }
+      W.max_exec[c] = mx;
+      break; }
+    case 37: W.birth_len[c] = len; break;
+    case 38: W.budget[c] = 0; break;
+    case 39: W.in_total[c] = 0; break;
+    case 40: W.in_ptr[c] = 0; break;
+    case 41: W.outbuf[c] = 0; break;
+    case 42: W.out_total[c] = 0; break;
+    case 43: W.cur_bonus[c] = W.default_bonus; break;
+    case 44: W.merit[c] = b.merit; break;
+    case 45: W.fitness[c] = b.fitness; break;
+    case 46: W.credit[c] = 0.0; break;
+    case 47: W.gest_time[c] = b.gest; break;
+    case 48: W.num_div[c] = 0; break;
+    case 49: W.generation[c] = b.gen; break;
+    case 50: W.copied[c] = b.ccopied; break;
+    case 51: W.child_copied[c] = 0; break;
+    case 52: W.executed[c] = b.exec; break;
+    case 53: W.errors[c] = 0; break;
+    case 54: {
+      uint32_t ctr = b.ctr;
+      // cEnvironment::SetupInputs random (main/cEnvironment.cc:1268-1271)
+      W.inputs[c] = (15 << 24) + (int)rng_below(b.lo, b.hi, ctr, 1u << 24);
+      W.inputs[N + c] = (51 << 24) + (int)rng_below(b.lo, b.hi, ctr, 1u << 24);
+      W.inputs[2 * N + c] = (85 << 24) + (int)rng_below(b.lo, b.hi, ctr, 1u << 24);
+      W.rng[c] = b.lo; W.rng[N + c] = b.hi; W.rng[2 * N + c] = ctr;
+      break; }
+    default: break;
+  }
+}
+
+// One wave per queued birth: the winners of cells inside the tile are
+// activated; winners of ghost-row cells were shipped by k_halo_pack.
 __global__ __launch_bounds__(64) void k_activate(DevWorld W) {
   const int nb = queue_len(W);
   const int lane = threadIdx.x;
-  const int64_t N = W.n;
   unsigned long long born = 0, lost = 0;
   for (int64_t q = blockIdx.x; q < nb; q += gridDim.x) {
     const int64_t i = rec_of(W, q);
     const int tgt = W.b_target[i];
-    const bool won = W.b_state[i] == 1 && tgt >= 0 && W.owner[tgt] == (int)i;
+    const bool won = W.b_state[i] > 0 && tgt >= 0 && W.owner[tgt] == (int)i;
+    if (won && tgt >= W.n) continue;          // sent to the neighbouring tile
     if (!won) { lost++; continue; }
     born++;
-    const int64_t c = tgt;
+    Child b;
+    b.len = W.b_len[i]; b.gen = W.b_gen[i]; b.ccopied = W.b_ccopied[i]; b.exec = W.b_exec[i];
+    b.gest = W.b_gest[i]; b.merit = W.b_merit[i]; b.fitness = W.b_fitness[i];
+    b.lo = W.b_rng[i]; b.hi = W.b_rng[W.rcap + i]; b.ctr = W.b_rng[2 * W.rcap + i];
+    setup_child(W, tgt, b, reinterpret_cast<const uint32_t*>(W.b_genome + i * TAPE_SLOT), lane);
+  }
+  if (lane == 0) {
+    if (born) count_add(W, CNT_BIRTHS, born);
+    if (lost) count_add(W, CNT_DROPPED, lost);
+  }
+}
+
+// Winners of ghost-row cells -> record buffer of that direction (one wave per
+// queued birth; one record per ghost cell at most: its last winner here).
+__global__ __launch_bounds__(64) void k_halo_pack(DevWorld W) {
+  const int nb = queue_len(W);
+  const int lane = threadIdx.x;
+  const int X = W.world_x;
+  unsigned long long sent = 0, lost = 0;
+  for (int64_t q = blockIdx.x; q < nb; q += gridDim.x) {
+    const int64_t i = rec_of(W, q);
+    const int tgt = W.b_target[i];
+    if (W.b_state[i] <= 0 || tgt < W.n || W.owner[tgt] != (int)i) continue;
+    const int d = (tgt - (int)W.n) / X, col = (tgt - (int)W.n) - d * X;
     const int len = W.b_len[i];
-    const uint32_t* src = reinterpret_cast<const uint32_t*>(W.b_genome + i * TAPE_SLOT);
-    uint32_t* dst = reinterpret_cast<uint32_t*>(W.tape + c * TAPE_SLOT);
-    for (int w = lane; w < (len + 3) / 4; w += 64) dst[w] = src[w];
-    // one store per lane: the organism's fields are scattered over SoA rows
-    if (lane < 2 * AVGPU_STACK_SIZE) W.stack[lane * N + c] = 0;
-    if (lane < AVGPU_MAX_REACTIONS) {
-      W.cur_task[lane * N + c] = 0; W.last_task[lane * N + c] = 0; W.cur_react[lane * N + c] = 0;
+    HaloHdr* hdr = reinterpret_cast<HaloHdr*>(W.r_send[d]);
+    HaloRec* recs = reinterpret_cast<HaloRec*>(W.r_send[d] + sizeof(HaloHdr));
+    uint8_t* arena = W.r_send[d] + sizeof(HaloHdr) + (int64_t)X * sizeof(HaloRec);
+    int slot = 0, off = 0;
+    if (lane == 0) {
+      slot = atomicAdd(&hdr->count, 1);
+      off = atomicAdd(&hdr->arena_used, (len + 3) & ~3);
     }
-    switch (lane) {
-      case 20: W.reg[c] = 0; break;
-      case 21: W.reg[N + c] = 0; break;
-      case 22: W.reg[2 * N + c] = 0; break;
-      case 23: W.inbuf[c] = 0; break;
-      case 24: W.inbuf[N + c] = 0; break;
-      case 25: W.inbuf[2 * N + c] = 0; break;
-      case 26: W.head[c] = 0; break;
-      case 27: W.head[N + c] = 0; break;
-      case 28: W.head[2 * N + c] = 0; break;
-      case 29: W.head[3 * N + c] = 0; break;
-      case 30: W.ctl[c] = CTL_ALIVE; break;
-      case 31: W.rlabel[c] = 0; break;
-      case 32: W.mem_size[c] = len; break;
-      case 33: W.cycles[c] = 0; break;
-      case 34: W.time_used[c] = 0; break;
-      case 35: W.gest_start[c] = 0; break;
-      case 36: {
-        int mx = 0;
-        if (W.death_method > 0) { mx = W.age_limit; if (W.death_method == 2) mx *= len; if (mx < 1) mx = 1; }
-        W.max_exec[c] = mx;
-        break; }
-      case 37: W.birth_len[c] = len; break;
-      case 38: W.budget[c] = 0; break;
-      case 39: W.in_total[c] = 0; break;
-      case 40: W.in_ptr[c] = 0; break;
-      case 41: W.outbuf[c] = 0; break;
-      case 42: W.out_total[c] = 0; break;
-      case 43: W.cur_bonus[c] = W.default_bonus; break;
-      case 44: W.merit[c] = W.b_merit[i]; break;
-      case 45: W.fitness[c] = W.b_fitness[i]; break;
-      case 46: W.credit[c] = 0.0; break;
-      case 47: W.gest_time[c] = W.b_gest[i]; break;
-      case 48: W.num_div[c] = 0; break;
-      case 49: W.generation[c] = W.b_gen[i]; break;
-      case 50: W.copied[c] = W.b_ccopied[i]; break;
-      case 51: W.child_copied[c] = 0; break;
-      case 52: W.executed[c] = W.b_exec[i]; break;
-      case 53: W.errors[c] = 0; break;
-      case 54: {
-        const uint32_t lo = W.b_rng[i], hi = W.b_rng[W.rcap + i];
-        uint32_t ctr = W.b_rng[2 * W.rcap + i];
-        // cEnvironment::SetupInputs random (main/cEnvironment.cc:1268-1271)
-        W.inputs[c] = (15 << 24) + (int)rng_below(lo, hi, ctr, 1u << 24);
-        W.inputs[N + c] = (51 << 24) + (int)rng_below(lo, hi, ctr, 1u << 24);
-        W.inputs[2 * N + c] = (85 << 24) + (int)rng_below(lo, hi, ctr, 1u << 24);
-        W.rng[c] = lo; W.rng[N + c] = hi; W.rng[2 * N + c] = ctr;
-        break; }
-      default: break;
+    slot = __shfl(slot, 0);
+    off = __shfl(off, 0);
+    const bool fits = (int64_t)off + len <= W.r_arena;
+    if (lane == 0) {
+      HaloRec r;
+      r.col = col; r.round = W.b_state[i] - 1; r.len = fits ? len : -1;
+      r.gen = W.b_gen[i]; r.ccopied = W.b_ccopied[i]; r.exec = W.b_exec[i]; r.gest = W.b_gest[i];
+      r.rng_lo = W.b_rng[i]; r.rng_hi = W.b_rng[W.rcap + i]; r.rng_ctr = W.b_rng[2 * W.rcap + i];
+      r.off = off; r.pad = 0; r.merit = W.b_merit[i]; r.fitness = W.b_fitness[i];
+      recs[slot] = r;
+      if (!fits) atomicAdd(&hdr->overflow, 1);
     }
+    if (fits) {
+      const uint32_t* src = reinterpret_cast<const uint32_t*>(W.b_genome + i * TAPE_SLOT);
+      uint32_t* dst = reinterpret_cast<uint32_t*>(arena + off);
+      for (int w = lane; w < (len + 3) / 4; w += 64) dst[w] = src[w];
+      sent++;
+    } else {
+      lost++;
+    }
+  }
+  if (lane == 0) {
+    if (sent) count_add(W, CNT_HALO_SENT, sent);
+    if (lost) { count_add(W, CNT_HALO_LOST, lost); count_add(W, CNT_DROPPED, lost); }
+  }
+}
+
+// Records received from direction d: the offspring owns its target cell when
+// it was that cell's last winner (owner == REMOTE_OWNER(its round)).
+__global__ __launch_bounds__(64) void k_activate_remote(DevWorld W, int d) {
+  const int lane = threadIdx.x;
+  const int X = W.world_x;
+  const HaloHdr* hdr = reinterpret_cast<const HaloHdr*>(W.r_recv[d]);
+  const HaloRec* recs = reinterpret_cast<const HaloRec*>(W.r_recv[d] + sizeof(HaloHdr));
+  const uint8_t* arena = W.r_recv[d] + sizeof(HaloHdr) + (int64_t)X * sizeof(HaloRec);
+  const int nrec = min(hdr->count, X);
+  unsigned long long born = 0, lost = 0;
+  for (int q = blockIdx.x; q < nrec; q += gridDim.x) {
+    const HaloRec r = recs[q];
+    if (r.len < 0) continue;                  // lost at the sender (counted there)
+    const int64_t c = edge_cell(W, d, r.col);
+    if (W.owner[c] != REMOTE_OWNER(r.round)) { lost++; continue; }
+    born++;
+    Child b;
+    b.len = r.len; b.gen = r.gen; b.ccopied = r.ccopied; b.exec = r.exec; b.gest = r.gest;
+    b.merit = r.merit; b.fitness = r.fitness; b.lo = r.rng_lo; b.hi = r.rng_hi; b.ctr = r.rng_ctr;
+    setup_child(W, c, b, reinterpret_cast<const uint32_t*>(arena + r.off), lane);
   }
   if (lane == 0) {
     if (born) count_add(W, CNT_BIRTHS, born);
@@ -534,8 +721,10 @@ void launch_classify_uniform(const DevWorld& W, hipStream_t s, int64_t first, in
 void launch_merit_total(const DevWorld& W, hipStream_t s, double* totals, double* scratch) {
   const int64_t nb = (W.n + 255) / 256;
   int32_t* alive_partial = reinterpret_cast<int32_t*>(scratch + nb);
-  hipLaunchKernelGGL(k_merit_partial, dim3((unsigned)nb), dim3(256), 0, s, W, scratch, alive_partial);
-  hipLaunchKernelGGL(k_merit_final, dim3(1), dim3(256), 0, s, scratch, alive_partial, nb, totals, 0);
+  hipLaunchKernelGGL(k_merit_partial, dim3((unsigned)nb), dim3(256), 0, s, W, scratch, alive_partial,
+                     (double*)nullptr);
+  hipLaunchKernelGGL(k_merit_final<false>, dim3(1), dim3(256), 0, s, scratch, alive_partial,
+                     (const double*)nullptr, nb, 1, totals, 0);
 }
 
 void launch_world_pre(const DevWorld& W, hipStream_t s, const double* totals) {
@@ -545,17 +734,77 @@ void launch_world_pre(const DevWorld& W, hipStream_t s, const double* totals) {
   hipLaunchKernelGGL(k_allot, dim3(nblk(W.n, 256)), dim3(256), 0, s, W, totals);
 }
 
+static void launch_stats(const DevWorld& W, hipStream_t s, double* stats) {
+  const int64_t nb = (W.n + 255) / 256;
+  double* part = stats + NSTAT;
+  hipLaunchKernelGGL(k_stats_partial, dim3((unsigned)nb), dim3(256), 0, s, W, part);
+  hipLaunchKernelGGL(k_stats_final, dim3(1), dim3(256), 0, s, W, part, nb, stats);
+}
+
+static unsigned activate_grid(const DevWorld& W) { return (unsigned)std::min<int64_t>(W.rcap, 32768); }
+
 void launch_world_post(const DevWorld& W, hipStream_t s, double* stats) {
   const unsigned bb = nblk(W.rcap, 256);
   hipLaunchKernelGGL(k_occ_init, dim3(nblk(W.n, 256)), dim3(256), 0, s, W);
   for (int round = 0; round < 4; round++) {
     hipLaunchKernelGGL(k_place_pick, dim3(bb), dim3(256), 0, s, W);
-    hipLaunchKernelGGL(k_place_resolve, dim3(bb), dim3(256), 0, s, W);
+    hipLaunchKernelGGL(k_place_resolve, dim3(bb), dim3(256), 0, s, W, round, 0);
     hipLaunchKernelGGL(k_place_clear, dim3(bb), dim3(256), 0, s, W);
   }
-  hipLaunchKernelGGL(k_activate, dim3((unsigned)std::min<int64_t>(W.rcap, 32768)), dim3(64), 0, s, W);
+  hipLaunchKernelGGL(k_activate, dim3(activate_grid(W)), dim3(64), 0, s, W);
+  launch_stats(W, s, stats);
+}
+
+// ---- strip tiles: the same update split around the halo exchanges ----
+void launch_tile_partials(const DevWorld& W, hipStream_t s, double* out) {
   const int64_t nb = (W.n + 255) / 256;
-  double* part = stats + NSTAT;
-  hipLaunchKernelGGL(k_stats_partial, dim3((unsigned)nb), dim3(256), 0, s, W, part);
-  hipLaunchKernelGGL(k_stats_final, dim3(1), dim3(256), 0, s, W, part, nb, stats);
+  hipLaunchKernelGGL(k_merit_partial, dim3((unsigned)nb), dim3(256), 0, s, W, out, (int32_t*)nullptr,
+                     out + nb);
+}
+
+void launch_tile_totals(const DevWorld& W, hipStream_t s, const double* gathered, int ntiles,
+                        double* totals) {
+  const int64_t nb = (W.n + 255) / 256;
+  hipLaunchKernelGGL(k_merit_final<true>, dim3(1), dim3(256), 0, s, (const double*)nullptr,
+                     (const int32_t*)nullptr, gathered, nb, ntiles, totals, 0);
+}
+
+// after interpretation: occupancy (cells + ghost rows) and the edge-row export
+void launch_tile_after_interpret(const DevWorld& W, hipStream_t s) {
+  hipLaunchKernelGGL(k_occ_init, dim3(nblk(W.n + 2 * (int64_t)W.world_x, 256)), dim3(256), 0, s, W);
+  hipLaunchKernelGGL(k_halo_export, dim3(nblk(2 * (int64_t)W.world_x, 256)), dim3(256), 0, s, W, 0);
+}
+
+// phase 0: (round 0: ghost occupancy in) pick, ghost claims out
+// phase 1: neighbours' claims merged in, resolve inside the tile, edge rows out
+// phase 2: ghost rows in, resolve ghost targets, clear claims
+// phase 3: pack the ghost-row winners into the record buffers
+void launch_tile_place(const DevWorld& W, hipStream_t s, int round, int phase) {
+  const unsigned bb = nblk(W.rcap, 256);
+  const unsigned hb = nblk(2 * (int64_t)W.world_x, 256);
+  if (phase == 0) {
+    if (round == 0) hipLaunchKernelGGL(k_halo_import, dim3(hb), dim3(256), 0, s, W, 0, round);
+    hipLaunchKernelGGL(k_place_pick, dim3(bb), dim3(256), 0, s, W);
+    hipLaunchKernelGGL(k_halo_export, dim3(hb), dim3(256), 0, s, W, 1);
+  } else if (phase == 1) {
+    hipLaunchKernelGGL(k_halo_import, dim3(hb), dim3(256), 0, s, W, 1, round);
+    hipLaunchKernelGGL(k_place_resolve, dim3(bb), dim3(256), 0, s, W, round, 1);
+    hipLaunchKernelGGL(k_halo_export, dim3(hb), dim3(256), 0, s, W, 2);
+  } else if (phase == 2) {
+    hipLaunchKernelGGL(k_halo_import, dim3(hb), dim3(256), 0, s, W, 2, round);
+    hipLaunchKernelGGL(k_place_resolve, dim3(bb), dim3(256), 0, s, W, round, 2);
+    hipLaunchKernelGGL(k_place_clear, dim3(bb), dim3(256), 0, s, W);
+    hipLaunchKernelGGL(k_halo_clear, dim3(hb), dim3(256), 0, s, W);
+  } else {
+    for (int d = 0; d < 2; d++) hipMemsetAsync(W.r_send[d], 0, sizeof(HaloHdr), s);
+    hipLaunchKernelGGL(k_halo_pack, dim3(activate_grid(W)), dim3(64), 0, s, W);
+  }
+}
+
+void launch_tile_finish(const DevWorld& W, hipStream_t s, double* stats) {
+  hipLaunchKernelGGL(k_activate, dim3(activate_grid(W)), dim3(64), 0, s, W);
+  for (int d = 0; d < 2; d++)
+    hipLaunchKernelGGL(k_activate_remote, dim3((unsigned)std::max(1, std::min(W.world_x, 4096))), dim3(64),
+                       0, s, W, d);
+  launch_stats(W, s, stats);
 }

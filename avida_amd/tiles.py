@@ -1,0 +1,146 @@
+"""Host driver of strip-tiled worlds: one global Avida world split into row
+strips, one strip per GPU (or several strips in one process for tests).
+
+This is the host half of the multi-GPU row of the hot path.  It
+replaces cMultiProcessWorld (main/cMultiProcessWorld.cc:142-190 migrant
+exchange, :375-405 update-size all-reduce) -- the reference's only
+multi-process world -- with strips of ONE torus, so that an update of the
+tiled world equals the same update of the untiled world cell for cell
+(DESIGN.md "Multi-GPU").  The per-update schedule is the one documented in
+include/avida_gpu.h ("strip tiles"):
+
+    tile_partials -> all_gather -> tile_begin -> exchange(halo)
+    4 x [tile_place(r,0) -> exchange(halo) -> tile_place(r,1) -> exchange(halo) -> tile_place(r,2)]
+    tile_place(3,3) -> exchange(records) -> tile_finish
+
+`lib` may be the product (prefix "avgpu_", device buffers, RCCL/NCCL or an
+in-process loopback) or the CPU oracle (prefix "orc_", host buffers, gloo);
+the driver itself holds no arithmetic of the path.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import torch
+
+
+def _check(lib, prefix, rc, what):
+    if rc is not None and rc < 0:
+        msg = getattr(lib, prefix + "last_error")()
+        raise RuntimeError(f"{prefix}{what} failed ({rc}): {msg.decode() if msg else ''}")
+    return rc
+
+
+class Tile:
+    """Buffers of one strip: merit partials, gathered partials, 2x2 halo and
+    2x2 birth-record buffers (index 0 = the tile above, 1 = the tile below)."""
+
+    def __init__(self, lib, prefix, handle, row0, ntiles, device, arena_bytes=0):
+        self.lib, self.p, self.h = lib, prefix, handle
+        self.row0 = row0
+        self.ntiles = ntiles
+        _check(lib, prefix, getattr(lib, prefix + "set_tile")(handle, row0, arena_bytes), "set_tile")
+        pb, hb, rb = C.c_int64(), C.c_int64(), C.c_int64()
+        _check(lib, prefix, getattr(lib, prefix + "tile_buffer_bytes")(
+            handle, C.byref(pb), C.byref(hb), C.byref(rb)), "tile_buffer_bytes")
+        self.n_part = pb.value // 8
+        u8 = dict(dtype=torch.uint8, device=device)
+        self.part = torch.zeros(self.n_part, dtype=torch.float64, device=device)
+        self.gathered = torch.zeros(self.n_part * ntiles, dtype=torch.float64, device=device)
+        self.halo_send = [torch.zeros(hb.value, **u8) for _ in range(2)]
+        self.halo_recv = [torch.zeros(hb.value, **u8) for _ in range(2)]
+        self.rec_send = [torch.zeros(rb.value, **u8) for _ in range(2)]
+        self.rec_recv = [torch.zeros(rb.value, **u8) for _ in range(2)]
+        ptrs = [C.c_void_p(t.data_ptr()) for t in
+                self.halo_send + self.halo_recv + self.rec_send + self.rec_recv]
+        _check(lib, prefix, getattr(lib, prefix + "set_tile_buffers")(handle, *ptrs),
+               "set_tile_buffers")
+
+    def call(self, name, *args):
+        return _check(self.lib, self.p, getattr(self.lib, self.p + name)(self.h, *args), name)
+
+
+class LoopbackTransport:
+    """All strips in this process (tests on one GPU, or the CPU oracle):
+    exchanges are tensor copies in tile order on the current stream."""
+
+    def all_gather(self, tiles):
+        full = torch.cat([t.part for t in tiles])
+        for t in tiles:
+            t.gathered.copy_(full)
+
+    def exchange(self, tiles, kind):
+        T = len(tiles)
+        for i, t in enumerate(tiles):
+            up, down = tiles[(i - 1) % T], tiles[(i + 1) % T]
+            if kind == "halo":
+                t.halo_recv[0].copy_(up.halo_send[1])
+                t.halo_recv[1].copy_(down.halo_send[0])
+            else:
+                t.rec_recv[0].copy_(up.rec_send[1])
+                t.rec_recv[1].copy_(down.rec_send[0])
+
+
+class DistTransport:
+    """One strip per rank over torch.distributed (backend "nccl" = RCCL over
+    xGMI on MI355X, or "gloo" for the CPU oracle).  Strip k belongs to rank k;
+    the tile above rank r is rank r-1 (mod T), the tile below rank r+1."""
+
+    def __init__(self, dist, group=None):
+        self.dist = dist
+        self.group = group
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+
+    def all_gather(self, tiles):
+        (t,) = tiles
+        if hasattr(self.dist, "all_gather_into_tensor") and t.part.is_cuda:
+            self.dist.all_gather_into_tensor(t.gathered, t.part, group=self.group)
+        else:
+            chunks = list(t.gathered.split(t.n_part))
+            self.dist.all_gather(chunks, t.part, group=self.group)
+
+    def exchange(self, tiles, kind):
+        (t,) = tiles
+        send, recv = (t.halo_send, t.halo_recv) if kind == "halo" else (t.rec_send, t.rec_recv)
+        up = (self.rank - 1) % self.world
+        down = (self.rank + 1) % self.world
+        d = self.dist
+        # sends [to above, to below], receives [from below, from above]: with
+        # two strips both peers are the same rank, and point-to-point messages
+        # between a pair match in issue order, so this order pairs each send
+        # with the receive of the same edge.
+        ops = [d.P2POp(d.isend, send[0], up, self.group), d.P2POp(d.isend, send[1], down, self.group),
+               d.P2POp(d.irecv, recv[1], down, self.group), d.P2POp(d.irecv, recv[0], up, self.group)]
+        for w in d.batch_isend_irecv(ops):
+            w.wait()
+
+
+class StripWorld:
+    """Runs updates of the strips this process holds (`tiles`, in global row
+    order) with `transport` doing the collective steps."""
+
+    def __init__(self, tiles, transport):
+        self.tiles = tiles
+        self.tr = transport
+
+    def update(self):
+        tiles = self.tiles
+        for t in tiles:
+            t.call("tile_partials", C.c_void_p(t.part.data_ptr()))
+        self.tr.all_gather(tiles)
+        for t in tiles:
+            t.call("tile_begin", C.c_void_p(t.gathered.data_ptr()), t.ntiles)
+        self.tr.exchange(tiles, "halo")
+        for rnd in range(4):
+            for phase in (0, 1):
+                for t in tiles:
+                    t.call("tile_place", rnd, phase)
+                self.tr.exchange(tiles, "halo")
+            for t in tiles:
+                t.call("tile_place", rnd, 2)
+        for t in tiles:
+            t.call("tile_place", 3, 3)
+        self.tr.exchange(tiles, "records")
+        for t in tiles:
+            t.call("tile_finish", None)

@@ -13,10 +13,12 @@ weighted allotment of AVE_TIME_SLICE*N instructions, interpretation, birth
 placement, statistics.  value = organism-instructions executed by all ranks /
 max-over-ranks wall time of the K timed updates.
 
-Multi-GPU (torch.distributed.run, one rank per GPU, RCCL): each rank owns one
-1024x1024 tile (weak scaling); the scheduler's {sum merit, organisms} are
-all-reduced every update so that each tile's share of AVE_TIME_SLICE*N_global
-follows its merit share (cMultiProcessWorld.cc:375-405).
+Multi-GPU (torch.distributed.run, one rank per GPU, RCCL over xGMI): the
+world is ONE 1024 x (1024*N) torus cut into N row strips of 1024x1024 (weak
+scaling).  Every update all-gathers the 256-cell merit partials (the
+scheduler's global total, cMultiProcessWorld.cc:375-405) and exchanges
+occupancy / placement claims / offspring across strip edges
+(avida_amd/tiles.py), so the N-GPU run is cell for cell the untiled world.
 """
 from __future__ import annotations
 
@@ -37,7 +39,7 @@ METRIC = "organism-instructions/sec + updates/sec, 1M-org logic-9 world, 1/8 GPU
 STATE_BYTES = 224.0
 SITE_BYTES = 1.25
 HBM_PEAK_GBS = 8000.0         # MI355X_MICROARCH.md chip table (spec)
-PMC_FILE = os.path.join(ROOT, "profiles", "pmc_k_interpret384.json")
+PMC_FILE = os.path.join(ROOT, "profiles", "pmc_k_interpret368.json")
 
 
 def _pool(golden):
@@ -50,17 +52,21 @@ def _pool(golden):
     return iset, pool
 
 
-def _genomes_for(n, pool, salt):
+def _genomes_for(n, pool, first=0):
+    """genotype of global cells first .. first+n-1 (a fixed hash of the cell id)"""
     import numpy as np
-    idx = (np.arange(n, dtype=np.uint64) * np.uint64(2654435761) + np.uint64(salt)) % np.uint64(len(pool))
+    idx = ((np.arange(n, dtype=np.uint64) + np.uint64(first)) * np.uint64(2654435761)) % np.uint64(len(pool))
     return [pool[int(i)] for i in idx]
 
 
-def build_world(lib, capi, files, golden, side, seed, device, rank):
+def build_world(lib, capi, files, golden, side, seed, device, rank, world, on_tile=None):
+    """One 1024x1024 strip per rank of a side x (side*world) torus (world = 1:
+    the untiled side x side world).  on_tile(h) places the strip before the
+    organisms are injected (their RNG streams are keyed by global cell id)."""
     iset, pool = _pool(golden)
     env = files.read_environment(os.path.join(golden, "environment-logic9.cfg"))
-    cfg = capi.cfg_from_avida(files.read_avida_cfg(None, {"WORLD_X": side, "WORLD_Y": side}),
-                              seed=seed + 1000003 * rank)
+    cfg = capi.cfg_from_avida(files.read_avida_cfg(None, {"WORLD_X": side, "WORLD_Y": side * world}),
+                              seed=seed)
     n = side * side
     h = lib.avgpu_create(C.byref(cfg), device, n)
     if not h:
@@ -70,13 +76,14 @@ def build_world(lib, capi, files, golden, side, seed, device, rank):
     capi.check(lib, lib.avgpu_load_instset(h, len(iset.names), hid, red))
     arr = capi.reactions_array(env)
     capi.check(lib, lib.avgpu_load_env(h, len(env), arr))
-    picks = _genomes_for(n, pool, rank * 7919)
+    tile = on_tile(h) if on_tile else None
+    picks = _genomes_for(n, pool, rank * n)
     blob = b"".join(g for g, _ in picks)
     buf = (C.c_uint8 * len(blob)).from_buffer_copy(blob)
     lens = (C.c_int32 * n)(*[len(g) for g, _ in picks])
     merits = (C.c_double * n)(*[m for _, m in picks])
     capi.check(lib, lib.avgpu_set_orgs(h, 0, n, buf, lens, merits, None, 0))
-    return h, cfg, n
+    return h, cfg, n, tile
 
 
 def cpu_baseline(golden, seconds):
@@ -91,7 +98,7 @@ def cpu_baseline(golden, seconds):
     cfg = capi.cfg_from_avida(files.read_avida_cfg(None), seed=101)
     n = cfg.world_x * cfg.world_y
     b = ol.Backend("oracle", cfg, iset, env, ncells=n)
-    picks = _genomes_for(n, pool, 0)
+    picks = _genomes_for(n, pool)
     b.set_orgs(0, [g for g, _ in picks], merits=[m for _, m in picks], deterministic=False)
     st = capi.AvgpuUpdateStats()
     insts, updates = 0, 0
@@ -129,19 +136,24 @@ def main():
         import torch.distributed as dist
         dist.init_process_group("nccl")
 
-    from avida_amd import capi, files
+    from avida_amd import capi, files, tiles
     lib = capi.load_product()
     golden = os.path.join(ROOT, "tests", "golden")
-    h, cfg, n = build_world(lib, capi, files, golden, args.side, args.seed, local, rank)
     stream = torch.cuda.current_stream()
-    capi.check(lib, lib.avgpu_set_stream(h, C.c_void_p(stream.cuda_stream)))
-    totals = torch.zeros(8, dtype=torch.float64, device="cuda")
+
+    def on_tile(h):
+        capi.check(lib, lib.avgpu_set_stream(h, C.c_void_p(stream.cuda_stream)))
+        if world == 1:
+            return None
+        return tiles.Tile(lib, "avgpu_", h, rank * args.side, world, "cuda")
+
+    h, cfg, n, tile = build_world(lib, capi, files, golden, args.side, args.seed, local, rank, world,
+                                  on_tile)
+    strips = tiles.StripWorld([tile], tiles.DistTransport(dist)) if tile else None
 
     def update():
-        if world > 1:
-            capi.check(lib, lib.avgpu_update_totals(h, C.c_void_p(totals.data_ptr())))
-            dist.all_reduce(totals[:2])
-            capi.check(lib, lib.avgpu_update_run(h, C.c_void_p(totals.data_ptr()), None))
+        if strips:
+            strips.update()      # halo-birth exchange + gathered scheduler totals over RCCL
         else:
             capi.check(lib, lib.avgpu_run_update(h, None))
 
@@ -191,7 +203,7 @@ def main():
             dist.destroy_process_group()
         return
     value = tot_insts / dt_max
-    # roofline of the dominant kernel k_interpret<384> (LDS size class 0, one
+    # roofline of the dominant kernel k_interpret<368> (LDS size class 0, one
     # launch per update), this rank: algorithmic bytes per launch =
     # slices * 2 * 224 B + tape sites staged in and written back * 1.25 B,
     # over its HIP-event-timed average duration on the world's stream.
@@ -229,7 +241,7 @@ def main():
             "updates_per_sec": args.steps / dt_max,
             "births_per_update": tot_births / args.steps,
             "insts_per_update": tot_insts / args.steps,
-            "parallelism": f"tiles{world}",
+            "parallelism": f"strips{world}",
         },
         "roofline": {
             "bound": "hbm",
@@ -239,7 +251,7 @@ def main():
             "frac": achieved / HBM_PEAK_GBS,
             "traffic": traffic,
             "traffic_source": traffic_src,
-            "kernel": "k_interpret<384> (LDS size class 0)",
+            "kernel": "k_interpret<368> (LDS size class 0)",
             "kernel_ms": c0_ms,
             "bytes_per_launch": bytes_per_launch,
             "slices_per_launch": c0_slices,

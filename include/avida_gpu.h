@@ -321,13 +321,50 @@ int avgpu_get_stats(avgpu_world* w, avgpu_update_stats* out);
  * reduced totals back before the next allotment. */
 int avgpu_stats_vector(avgpu_world* w, void** dev_ptr);
 int avgpu_set_global_totals(avgpu_world* w, double total_merit, int64_t total_orgs);
-/* Halo births (cMultiProcessWorld.cc:142-190 migrant protocol): births that
- * target cells outside this tile are packed into dev buffer records; see
- * INTEGRATION.md for the record layout. */
-int avgpu_halo_pack(avgpu_world* w, int side, void* dev_buf, int64_t cap_records,
-                    int64_t* n_records);
-int avgpu_halo_unpack(avgpu_world* w, int side, const void* dev_buf, int64_t n_records);
-int64_t avgpu_halo_record_bytes(void);
+/* ---- strip tiles: one global world over several GPUs --------------------
+ * Replaces the reference's only multi-process world, cMultiProcessWorld
+ * (main/cMultiProcessWorld.cc:142-190 migrant exchange, :375-405 update-size
+ * all-reduce), with row strips of ONE torus / grid.  The world is created with
+ * cfg.world_y = the GLOBAL row count and num_cells = rows*world_x of this tile;
+ * avgpu_set_tile(row0) places it.  An update of a tiled world is identical,
+ * cell for cell, to the same update of the untiled world (DESIGN.md
+ * "Multi-GPU"), given this host schedule with exchange(halo) meaning: send
+ * halo_send_up to the tile above (rank-1 mod T) and halo_send_down to the
+ * tile below, receive into halo_recv_up from the tile above and into
+ * halo_recv_down from the tile below (same for records):
+ *
+ *   avgpu_tile_partials(w, part)         all_gather(part) in tile order
+ *   avgpu_tile_begin(w, gathered, T)     exchange(halo)
+ *   for round 0..3:
+ *     avgpu_tile_place(w, round, 0)      exchange(halo)
+ *     avgpu_tile_place(w, round, 1)      exchange(halo)
+ *     avgpu_tile_place(w, round, 2)
+ *   avgpu_tile_place(w, 3, 3)            exchange(records)
+ *   avgpu_tile_finish(w, stats)
+ *
+ * Every call is stream-ordered on the handle's stream (no host sync).
+ * Requirements: rows >= 2, tile cells a multiple of 256 and of world_x.
+ * arena_bytes (<= 0: default max(256 KiB, 256 B x world_x)) bounds the
+ * offspring genome bytes shipped per direction per update; an offspring that
+ * does not fit is dropped (AVGPU_CNT_HALO_LOST). */
+int avgpu_set_tile(avgpu_world* w, int64_t row0, int64_t arena_bytes);
+/* byte sizes of the partials vector (avgpu_tile_partials output, per tile),
+ * of one halo buffer and of one record buffer */
+int avgpu_tile_buffer_bytes(avgpu_world* w, int64_t* partial_bytes, int64_t* halo_bytes,
+                            int64_t* record_bytes);
+/* device buffers the host exchanges (8 distinct allocations) */
+int avgpu_set_tile_buffers(avgpu_world* w, void* halo_send_up, void* halo_send_down,
+                           void* halo_recv_up, void* halo_recv_down, void* rec_send_up,
+                           void* rec_send_down, void* rec_recv_up, void* rec_recv_down);
+/* per-256-cell merit partials, then alive counts (doubles), for the all-gather */
+int avgpu_tile_partials(avgpu_world* w, double* dev_out);
+/* global totals from the gathered partials (T x partials, tile order), then
+ * allotment + interpretation of this tile, occupancy of its edge rows out */
+int avgpu_tile_begin(avgpu_world* w, const double* dev_gathered, int ntiles);
+/* placement round 0..3, phase 0..2; phase 3 packs the halo birth records */
+int avgpu_tile_place(avgpu_world* w, int round, int phase);
+/* activation of this tile's winners and of the received records, statistics */
+int avgpu_tile_finish(avgpu_world* w, avgpu_update_stats* out);
 
 /* counters of the last avgpu_step: instructions executed (sum over lanes) */
 int avgpu_last_step_insts(avgpu_world* w, int64_t* insts);
@@ -355,6 +392,8 @@ enum avgpu_counter {
   AVGPU_CNT_C0_SLICES = 8,  /* slices run by the class-0 (<=384 sites) launch */
   AVGPU_CNT_C0_SITES = 9,   /* tape sites that launch staged in plus wrote back */
   /* 10..17: per-phase clocks of diagnostic (AVGPU_PHASE_CLOCKS) builds */
+  AVGPU_CNT_HALO_SENT = 18, /* offspring shipped to a neighbouring tile */
+  AVGPU_CNT_HALO_LOST = 19, /* offspring dropped because the halo arena was full */
   AVGPU_NUM_COUNTERS = 32
 };
 int avgpu_counters(avgpu_world* w, int cumulative, int64_t* out, int n);

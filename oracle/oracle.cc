@@ -203,6 +203,22 @@ struct World {
   double global_merit = 0.0;
   int64_t global_orgs = 0;
   Stream global_rng;   // serial world scheduler stream
+  // strip tiles (avgpu_set_tile): rows [row0, row0+rows) of a world_x x
+  // global_rows world; occ / claim / owner carry two ghost rows after n
+  int64_t row0 = 0, rows = 0, global_rows = 0, cell0 = 0;
+  bool tiled = false;
+  int64_t r_arena = 0;
+  uint8_t* h_send[2] = {nullptr, nullptr};
+  uint8_t* h_recv[2] = {nullptr, nullptr};
+  uint8_t* r_send[2] = {nullptr, nullptr};
+  uint8_t* r_recv[2] = {nullptr, nullptr};
+  // per-update placement state of the tiled path
+  std::vector<uint8_t> occ;
+  std::vector<uint64_t> claim;
+  std::vector<int64_t> owner;     // birth index, -1 none, -2-k won by a halo birth in round k
+  std::vector<uint64_t> prio;
+  std::vector<int8_t> bstate;     // 0 pending, 1+k placed in round k, -1 failed
+  int64_t t_insts = 0, t_deaths = 0, t_divides = 0, t_slices = 0, t_born = 0, t_dropped = 0;
 };
 
 thread_local std::string g_err;
@@ -766,21 +782,35 @@ double tree_merit_sum(const World& w, int64_t* n_alive) {
 }
 
 // torus / grid neighbourhood (tools/cTopology.h:40-55 build_torus/build_grid),
-// fixed order: NW N NE W E SW S SE
+// fixed order: NW N NE W E SW S SE.  A strip tile maps the rows above / below
+// it to the ghost rows [n, n+X) / [n+X, n+2X).
 int neighbours(const World& w, int64_t cell, int64_t* out) {
-  const int X = w.cfg.world_x, Y = w.cfg.world_y;
-  const int x = (int)(cell % X), y = (int)(cell / X);
+  const int X = w.cfg.world_x;
+  const int64_t R = w.rows;
+  const int x = (int)(cell % X);
+  const int64_t y = cell / X;
   int n = 0;
   for (int dy = -1; dy <= 1; dy++)
     for (int dx = -1; dx <= 1; dx++) {
       if (dx == 0 && dy == 0) continue;
-      int nx = x + dx, ny = y + dy;
+      int nx = x + dx;
+      int64_t ny = y + dy;
       if (w.cfg.world_geometry == 1) {
-        if (nx < 0 || nx >= X || ny < 0 || ny >= Y) continue;
+        if (nx < 0 || nx >= X) continue;
       } else {
-        nx = (nx + X) % X; ny = (ny + Y) % Y;
+        nx = (nx + X) % X;
       }
-      out[n++] = (int64_t)ny * X + nx;
+      if (ny >= 0 && ny < R) {
+        out[n++] = ny * X + nx;
+      } else if (!w.tiled) {
+        if (w.cfg.world_geometry == 1) continue;
+        ny = (ny + R) % R;
+        out[n++] = ny * X + nx;
+      } else {
+        const int64_t gy = w.row0 + ny;
+        if (w.cfg.world_geometry == 1 && (gy < 0 || gy >= w.global_rows)) continue;
+        out[n++] = w.ncells + (ny < 0 ? 0 : X) + nx;
+      }
     }
   return n;
 }
@@ -815,6 +845,8 @@ void* orc_create(const avgpu_cfg* cfg, int64_t ncells) {
   w->cfg = *cfg;
   w->ncells = ncells > 0 ? ncells : (int64_t)cfg->world_x * cfg->world_y;
   w->orgs.resize(w->ncells);
+  w->rows = cfg->world_y;
+  w->global_rows = cfg->world_y;
   w->th_copy_mut = prob_thresh(cfg->copy_mut_prob);
   w->th_copy_ins = prob_thresh(cfg->copy_ins_prob);
   w->th_copy_del = prob_thresh(cfg->copy_del_prob);
@@ -867,7 +899,7 @@ int orc_set_orgs(void* h, int64_t first, int64_t count, const uint8_t* genomes, 
     Org& o = w.orgs[c];
     setup_inject(w, o, genomes + off, lens[i], merits ? merits[i] : 0.0);
     off += lens[i];
-    derive_key((uint32_t)w.cfg.seed, (uint32_t)(w.cfg.seed >> 32), (uint32_t)c, 0xA5A5A5A5U,
+    derive_key((uint32_t)w.cfg.seed, (uint32_t)(w.cfg.seed >> 32), (uint32_t)(w.cell0 + c), 0xA5A5A5A5U,
                &o.rng.lo, &o.rng.hi);
     o.rng.ctr = 0;
     if (inputs) { for (int k = 0; k < 3; k++) o.inputs[k] = inputs[i * 3 + k]; }
@@ -966,15 +998,9 @@ int orc_test_genomes(void* h, int n, const uint8_t* genomes, const int32_t* lens
 // ---------------------------------------------------------------------------
 // Batch-synchronous world update: the exact semantics the device implements
 // (DESIGN.md "Update semantics"): allot -> interpret -> place births -> stats.
-static int run_update_impl(World& w) {
-  avgpu_update_stats& st = w.stats;
-  memset(&st, 0, sizeof(st));
-  st.update = w.update;
-  int64_t n_alive = 0;
-  double sum_merit = tree_merit_sum(w, &n_alive);
-  if (w.have_global) { sum_merit = w.global_merit; n_alive = w.global_orgs; }
+// 1. allotment (cScheduler restated; DESIGN.md "Scheduler") + 2. interpretation
+static void allot_interpret(World& w, double sum_merit, int64_t n_alive) {
   const int64_t ud = (int64_t)w.cfg.ave_time_slice * n_alive;
-  // 1. allotment (cScheduler restated; DESIGN.md "Scheduler")
   std::vector<int32_t> budget(w.ncells, 0);
   for (int64_t c = 0; c < w.ncells; c++) {
     Org& o = w.orgs[c];
@@ -997,9 +1023,8 @@ static int run_update_impl(World& w) {
       budget[c] = (int32_t)fl + (o.rng.p(th) ? 1 : 0);
     }
   }
-  int64_t slices = 0;
-  for (int64_t c = 0; c < w.ncells; c++) slices += budget[c] > 0;
-  // 2. interpretation
+  w.t_slices = 0;
+  for (int64_t c = 0; c < w.ncells; c++) w.t_slices += budget[c] > 0;
   w.births.clear();
   int64_t insts = 0, deaths = 0, divides = 0;
   for (int64_t c = 0; c < w.ncells; c++) {
@@ -1011,53 +1036,19 @@ static int run_update_impl(World& w) {
     divides += o.num_divides - d0;
     if (!o.alive) deaths++;
   }
-  // 3. placement rounds (PositionOffspring restated, main/cPopulation.cc:5353-5413)
-  const int64_t nbirth = (int64_t)w.births.size();
-  std::vector<uint8_t> occ(w.ncells);
-  for (int64_t c = 0; c < w.ncells; c++) occ[c] = w.orgs[c].alive ? 1 : 0;
-  std::vector<uint64_t> claim(w.ncells, 0);
-  std::vector<int64_t> owner(w.ncells, -1);
-  std::vector<uint64_t> prio(nbirth, 0);
-  std::vector<int8_t> state(nbirth, 0);   // 0 pending, 1 placed, -1 failed
-  for (int round = 0; round < 4; round++) {
-    for (int64_t i = 0; i < nbirth; i++) {
-      Birth& b = w.births[i];
-      if (state[i] != 0) continue;
-      int64_t nb[8];
-      const int nn = neighbours(w, b.parent, nb);
-      int64_t cand[9];
-      int nc = 0;
-      if (w.cfg.prefer_empty)
-        for (int k = 0; k < nn; k++) if (!occ[nb[k]]) cand[nc++] = nb[k];
-      if (nc == 0 && w.cfg.birth_method != 3) {
-        for (int k = 0; k < nn; k++) cand[nc++] = nb[k];
-        if (w.cfg.allow_parent) cand[nc++] = b.parent;
-      }
-      if (nc == 0) { state[i] = -1; continue; }
-      b.target = cand[b.rng.uint_below((uint32_t)nc)];
-      prio[i] = ((uint64_t)b.rng.next() << 32) | ((uint64_t)(b.parent & 0xFFFFFF) << 8) | (b.seq & 0xFF);
-      if (prio[i] > claim[b.target]) claim[b.target] = prio[i];
-    }
-    for (int64_t i = 0; i < nbirth; i++) {
-      if (state[i] != 0) continue;
-      Birth& b = w.births[i];
-      if (claim[b.target] == prio[i]) { state[i] = 1; occ[b.target] = 1; owner[b.target] = i; }
-    }
-    for (int64_t i = 0; i < nbirth; i++) if (w.births[i].target >= 0) claim[w.births[i].target] = 0;
-  }
-  // 4. activation (the last round's winner owns the cell)
-  int64_t placed = 0, dropped = 0;
-  for (int64_t i = 0; i < nbirth; i++) {
-    Birth& b = w.births[i];
-    if (state[i] == 1 && owner[b.target] == i) { activate_child(w, b, b.target); placed++; }
-    else dropped++;
-  }
-  // 5. statistics (main/cStats.cc:1081-1100 inputs)
-  st.insts_executed = insts;
+  w.t_insts = insts; w.t_deaths = deaths; w.t_divides = divides;
+}
+
+// 5. statistics (main/cStats.cc:1081-1100 inputs)
+static void finish_stats(World& w, int64_t placed, int64_t dropped) {
+  avgpu_update_stats& st = w.stats;
+  memset(&st, 0, sizeof(st));
+  st.update = w.update;
+  st.insts_executed = w.t_insts;
   st.births = placed;
   st.births_dropped = dropped;
-  st.deaths = deaths;
-  st.divides = divides;
+  st.deaths = w.t_deaths;
+  st.divides = w.t_divides;
   double gen = 0.0;
   for (int64_t c = 0; c < w.ncells; c++) {
     const Org& o = w.orgs[c];
@@ -1073,12 +1064,69 @@ static int run_update_impl(World& w) {
   }
   st.ave_generation = st.num_organisms ? gen / st.num_organisms : 0.0;
   for (int64_t c = 0; c < w.ncells; c++) if (w.orgs[c].alive) st.sum_mem_size += (double)w.orgs[c].mem.size();
-  w.cum_insts += insts;
+  w.cum_insts += w.t_insts;
   w.cum_births += placed;
   st.cum_insts_executed = w.cum_insts;
   st.cum_births = w.cum_births;
-  st.slices = slices;
+  st.slices = w.t_slices;
   w.update++;
+}
+
+// placement pick for birth i (PositionOffspring restated, main/cPopulation.cc:5353-5413)
+static void place_pick(World& w, int64_t i, const std::vector<uint8_t>& occ, std::vector<uint64_t>& claim,
+                       std::vector<uint64_t>& prio, std::vector<int8_t>& state) {
+  Birth& b = w.births[i];
+  int64_t nb[8];
+  const int nn = neighbours(w, b.parent, nb);
+  int64_t cand[9];
+  int nc = 0;
+  if (w.cfg.prefer_empty)
+    for (int k = 0; k < nn; k++) if (!occ[nb[k]]) cand[nc++] = nb[k];
+  if (nc == 0 && w.cfg.birth_method != 3) {
+    for (int k = 0; k < nn; k++) cand[nc++] = nb[k];
+    if (w.cfg.allow_parent) cand[nc++] = b.parent;
+  }
+  if (nc == 0) { state[i] = -1; return; }
+  b.target = cand[b.rng.uint_below((uint32_t)nc)];
+  prio[i] = ((uint64_t)b.rng.next() << 32) | ((uint64_t)((w.cell0 + b.parent) & 0xFFFFFF) << 8) |
+            (b.seq & 0xFF);
+  if (prio[i] > claim[b.target]) claim[b.target] = prio[i];
+}
+
+// ---------------------------------------------------------------------------
+// Batch-synchronous world update: the exact semantics the device implements
+// (DESIGN.md "Update semantics"): allot -> interpret -> place births -> stats.
+static int run_update_impl(World& w) {
+  int64_t n_alive = 0;
+  double sum_merit = tree_merit_sum(w, &n_alive);
+  if (w.have_global) { sum_merit = w.global_merit; n_alive = w.global_orgs; }
+  allot_interpret(w, sum_merit, n_alive);
+  // 3. placement rounds
+  const int64_t nbirth = (int64_t)w.births.size();
+  std::vector<uint8_t> occ(w.ncells);
+  for (int64_t c = 0; c < w.ncells; c++) occ[c] = w.orgs[c].alive ? 1 : 0;
+  std::vector<uint64_t> claim(w.ncells, 0);
+  std::vector<int64_t> owner(w.ncells, -1);
+  std::vector<uint64_t> prio(nbirth, 0);
+  std::vector<int8_t> state(nbirth, 0);   // 0 pending, 1 placed, -1 failed
+  for (int round = 0; round < 4; round++) {
+    for (int64_t i = 0; i < nbirth; i++)
+      if (state[i] == 0) place_pick(w, i, occ, claim, prio, state);
+    for (int64_t i = 0; i < nbirth; i++) {
+      if (state[i] != 0) continue;
+      Birth& b = w.births[i];
+      if (claim[b.target] == prio[i]) { state[i] = 1; occ[b.target] = 1; owner[b.target] = i; }
+    }
+    for (int64_t i = 0; i < nbirth; i++) if (w.births[i].target >= 0) claim[w.births[i].target] = 0;
+  }
+  // 4. activation (the last round's winner owns the cell)
+  int64_t placed = 0, dropped = 0;
+  for (int64_t i = 0; i < nbirth; i++) {
+    Birth& b = w.births[i];
+    if (state[i] == 1 && owner[b.target] == i) { activate_child(w, b, b.target); placed++; }
+    else dropped++;
+  }
+  finish_stats(w, placed, dropped);
   return 0;
 }
 
@@ -1101,6 +1149,234 @@ int orc_set_global_totals(void* h, double merit, int64_t orgs) {
   w.have_global = true; w.global_merit = merit; w.global_orgs = orgs;
   return 0;
 }
+
+// ---------------------------------------------------------------------------
+// Strip tiles (include/avida_gpu.h "strip tiles"; DESIGN.md "Multi-GPU"): the
+// same update as run_update_impl, split around the halo exchanges the host
+// performs.  Buffer layouts are the device's: halo = X u64 claims then X u8
+// occupancy flags; records = HaloHdr, X HaloRec, genome arena.
+namespace {
+struct HaloHdr { int32_t count, arena_used, overflow, pad; };
+struct HaloRec {
+  int32_t col, round, len, gen, ccopied, exec, gest;
+  uint32_t rng_lo, rng_hi, rng_ctr;
+  int32_t off, pad;
+  double merit, fitness;
+};
+static_assert(sizeof(HaloRec) == 64, "HaloRec layout");
+int64_t halo_bytes_of(int x) { return ((int64_t)x * 9 + 15) / 16 * 16; }
+uint64_t* hclaims(uint8_t* b) { return reinterpret_cast<uint64_t*>(b); }
+uint8_t* hocc(uint8_t* b, int x) { return b + (int64_t)x * 8; }
+int64_t edge_cell(const World& w, int d, int x) { return d == 0 ? x : (w.rows - 1) * w.cfg.world_x + x; }
+int64_t ghost_cell(const World& w, int d, int x) { return w.ncells + (int64_t)d * w.cfg.world_x + x; }
+bool tile_ok(World& w) { return w.tiled && w.h_send[0] && w.r_recv[1]; }
+}  // namespace
+
+int orc_set_tile(void* h, int64_t row0, int64_t arena) {
+  World& w = *(World*)h;
+  const int64_t X = w.cfg.world_x;
+  if (X <= 0 || w.ncells % X) return fail(AVGPU_EINVAL, "tile cells must be whole rows of WORLD_X");
+  const int64_t rows = w.ncells / X;
+  if (rows < 2) return fail(AVGPU_EINVAL, "a tile needs at least 2 rows");
+  if (w.ncells % 256) return fail(AVGPU_EINVAL, "tile cells must be a multiple of 256 (merit blocks)");
+  if (row0 < 0 || row0 + rows > w.global_rows) return fail(AVGPU_EINVAL, "tile rows outside WORLD_Y");
+  if (arena <= 0) arena = std::max<int64_t>(256 * 1024, X * 256);
+  w.row0 = row0; w.rows = rows; w.tiled = rows < w.global_rows; w.cell0 = row0 * X;
+  w.r_arena = (arena + 15) / 16 * 16;
+  return 0;
+}
+
+int orc_tile_buffer_bytes(void* h, int64_t* part, int64_t* halo, int64_t* rec) {
+  World& w = *(World*)h;
+  const int X = w.cfg.world_x;
+  if (part) *part = 2 * ((w.ncells + 255) / 256) * 8;
+  if (halo) *halo = halo_bytes_of(X);
+  if (rec) *rec = (int64_t)sizeof(HaloHdr) + (int64_t)X * (int64_t)sizeof(HaloRec) + w.r_arena;
+  return 0;
+}
+
+int orc_set_tile_buffers(void* h, void* hs0, void* hs1, void* hr0, void* hr1, void* rs0, void* rs1,
+                         void* rr0, void* rr1) {
+  World& w = *(World*)h;
+  if (!w.tiled) return fail(AVGPU_ESTATE, "not a strip tile");
+  w.h_send[0] = (uint8_t*)hs0; w.h_send[1] = (uint8_t*)hs1;
+  w.h_recv[0] = (uint8_t*)hr0; w.h_recv[1] = (uint8_t*)hr1;
+  w.r_send[0] = (uint8_t*)rs0; w.r_send[1] = (uint8_t*)rs1;
+  w.r_recv[0] = (uint8_t*)rr0; w.r_recv[1] = (uint8_t*)rr1;
+  return 0;
+}
+
+// the 256-cell block partials of tree_merit_sum (level 1), then alive counts
+int orc_tile_partials(void* h, double* out) {
+  World& w = *(World*)h;
+  const int64_t nb = (w.ncells + 255) / 256;
+  for (int64_t b = 0; b < nb; b++) {
+    double s[256];
+    int64_t cnt = 0;
+    for (int i = 0; i < 256; i++) {
+      const int64_t c = b * 256 + i;
+      const bool live = c < w.ncells && w.orgs[c].alive;
+      s[i] = live ? w.orgs[c].merit : 0.0;
+      cnt += live;
+    }
+    for (int stride = 128; stride >= 1; stride >>= 1)
+      for (int i = 0; i < stride; i++) s[i] = s[i] + s[i + stride];
+    out[b] = s[0];
+    out[nb + b] = (double)cnt;
+  }
+  return 0;
+}
+
+int orc_tile_begin(void* h, const double* gathered, int ntiles) {
+  World& w = *(World*)h;
+  if (!tile_ok(w)) return fail(AVGPU_ESTATE, "not a strip tile with buffers");
+  // tree_merit_sum level 2 over the gathered partials (tile order = block order)
+  const int64_t nb = (w.ncells + 255) / 256, total = nb * ntiles;
+  double lane[256];
+  int64_t cnt = 0;
+  for (int t = 0; t < 256; t++) {
+    double acc = 0.0;
+    for (int64_t g = t; g < total; g += 256) {
+      const int64_t k = g / nb, j = g % nb;
+      acc = acc + gathered[k * 2 * nb + j];
+      cnt += (int64_t)gathered[k * 2 * nb + nb + j];
+    }
+    lane[t] = acc;
+  }
+  for (int stride = 128; stride >= 1; stride >>= 1)
+    for (int i = 0; i < stride; i++) lane[i] = lane[i] + lane[i + stride];
+  allot_interpret(w, lane[0], cnt);
+  const int X = w.cfg.world_x;
+  const int64_t ext = w.ncells + 2 * X, nbirth = (int64_t)w.births.size();
+  w.occ.assign(ext, 0);
+  for (int64_t c = 0; c < w.ncells; c++) w.occ[c] = w.orgs[c].alive ? 1 : 0;
+  w.claim.assign(ext, 0);
+  w.owner.assign(ext, -1);
+  w.prio.assign(nbirth, 0);
+  w.bstate.assign(nbirth, 0);
+  for (int d = 0; d < 2; d++)
+    for (int x = 0; x < X; x++) {
+      hocc(w.h_send[d], X)[x] = w.occ[edge_cell(w, d, x)];
+      hclaims(w.h_send[d])[x] = 0;
+    }
+  return 0;
+}
+
+int orc_tile_place(void* h, int round, int phase) {
+  World& w = *(World*)h;
+  if (!tile_ok(w)) return fail(AVGPU_ESTATE, "not a strip tile with buffers");
+  const int X = w.cfg.world_x;
+  const int64_t nbirth = (int64_t)w.births.size();
+  if (phase == 0) {
+    if (round == 0)
+      for (int d = 0; d < 2; d++)
+        for (int x = 0; x < X; x++) w.occ[ghost_cell(w, d, x)] = hocc(w.h_recv[d], X)[x];
+    for (int64_t i = 0; i < nbirth; i++)
+      if (w.bstate[i] == 0) place_pick(w, i, w.occ, w.claim, w.prio, w.bstate);
+    for (int d = 0; d < 2; d++)
+      for (int x = 0; x < X; x++) hclaims(w.h_send[d])[x] = w.claim[ghost_cell(w, d, x)];
+  } else if (phase == 1) {
+    for (int d = 0; d < 2; d++)
+      for (int x = 0; x < X; x++) {
+        const int64_t c = edge_cell(w, d, x);
+        const uint64_t rc = hclaims(w.h_recv[d])[x];
+        if (rc > w.claim[c]) w.claim[c] = rc;
+        if (rc != 0 && w.claim[c] == rc) { w.owner[c] = -2 - round; w.occ[c] = 1; }
+      }
+    for (int64_t i = 0; i < nbirth; i++) {
+      if (w.bstate[i] != 0 || w.births[i].target >= w.ncells) continue;
+      const int64_t t = w.births[i].target;
+      if (w.claim[t] == w.prio[i]) { w.bstate[i] = (int8_t)(1 + round); w.occ[t] = 1; w.owner[t] = i; }
+    }
+    for (int d = 0; d < 2; d++)
+      for (int x = 0; x < X; x++) {
+        const int64_t c = edge_cell(w, d, x);
+        hclaims(w.h_send[d])[x] = w.claim[c];
+        hocc(w.h_send[d], X)[x] = w.occ[c];
+      }
+  } else if (phase == 2) {
+    for (int d = 0; d < 2; d++)
+      for (int x = 0; x < X; x++) {
+        const int64_t c = ghost_cell(w, d, x);
+        w.claim[c] = hclaims(w.h_recv[d])[x];
+        w.occ[c] = hocc(w.h_recv[d], X)[x];
+      }
+    for (int64_t i = 0; i < nbirth; i++) {
+      if (w.bstate[i] != 0 || w.births[i].target < w.ncells) continue;
+      const int64_t t = w.births[i].target;
+      if (w.claim[t] == w.prio[i]) { w.bstate[i] = (int8_t)(1 + round); w.owner[t] = i; }
+    }
+    for (int64_t i = 0; i < nbirth; i++) if (w.births[i].target >= 0) w.claim[w.births[i].target] = 0;
+    for (int d = 0; d < 2; d++)
+      for (int x = 0; x < X; x++) { w.claim[edge_cell(w, d, x)] = 0; w.claim[ghost_cell(w, d, x)] = 0; }
+  } else {
+    // pack the last winner of every ghost cell (births in queue order)
+    w.t_born = 0; w.t_dropped = 0;
+    for (int d = 0; d < 2; d++) memset(w.r_send[d], 0, sizeof(HaloHdr));
+    for (int64_t i = 0; i < nbirth; i++) {
+      const Birth& b = w.births[i];
+      if (w.bstate[i] <= 0 || b.target < w.ncells || w.owner[b.target] != i) continue;
+      const int d = (int)((b.target - w.ncells) / X), col = (int)((b.target - w.ncells) % X);
+      HaloHdr* hdr = reinterpret_cast<HaloHdr*>(w.r_send[d]);
+      HaloRec* recs = reinterpret_cast<HaloRec*>(w.r_send[d] + sizeof(HaloHdr));
+      uint8_t* arena = w.r_send[d] + sizeof(HaloHdr) + (int64_t)X * sizeof(HaloRec);
+      const int len = (int)b.genome.size();
+      const int slot = hdr->count++;
+      const int off = hdr->arena_used;
+      hdr->arena_used += (len + 3) & ~3;
+      const bool fits = (int64_t)off + len <= w.r_arena;
+      HaloRec r;
+      r.col = col; r.round = w.bstate[i] - 1; r.len = fits ? len : -1;
+      r.gen = b.generation; r.ccopied = b.child_copied; r.exec = b.executed; r.gest = b.gestation_time;
+      r.rng_lo = b.rng.lo; r.rng_hi = b.rng.hi; r.rng_ctr = b.rng.ctr;
+      r.off = off; r.pad = 0; r.merit = b.merit; r.fitness = b.fitness;
+      recs[slot] = r;
+      if (fits) memcpy(arena + off, b.genome.data(), len);
+      else { hdr->overflow++; w.t_dropped++; }
+    }
+  }
+  return 0;
+}
+
+int orc_tile_finish(void* h, avgpu_update_stats* out) {
+  World& w = *(World*)h;
+  if (!tile_ok(w)) return fail(AVGPU_ESTATE, "not a strip tile with buffers");
+  const int X = w.cfg.world_x;
+  const int64_t nbirth = (int64_t)w.births.size();
+  int64_t placed = 0, dropped = w.t_dropped;
+  for (int64_t i = 0; i < nbirth; i++) {
+    Birth& b = w.births[i];
+    const bool won = w.bstate[i] > 0 && b.target >= 0 && w.owner[b.target] == i;
+    if (won && b.target >= w.ncells) continue;   // shipped to the neighbour
+    if (won) { activate_child(w, b, b.target); placed++; }
+    else dropped++;
+  }
+  for (int d = 0; d < 2; d++) {
+    const HaloHdr* hdr = reinterpret_cast<const HaloHdr*>(w.r_recv[d]);
+    const HaloRec* recs = reinterpret_cast<const HaloRec*>(w.r_recv[d] + sizeof(HaloHdr));
+    const uint8_t* arena = w.r_recv[d] + sizeof(HaloHdr) + (int64_t)X * sizeof(HaloRec);
+    const int nrec = std::min(hdr->count, X);
+    for (int q = 0; q < nrec; q++) {
+      const HaloRec& r = recs[q];
+      if (r.len < 0) continue;
+      const int64_t c = edge_cell(w, d, r.col);
+      if (w.owner[c] != -2 - r.round) { dropped++; continue; }
+      Birth b;
+      b.parent = -1; b.seq = 0;
+      b.genome.assign(arena + r.off, arena + r.off + r.len);
+      b.merit = r.merit; b.generation = r.gen; b.child_copied = r.ccopied; b.executed = r.exec;
+      b.gestation_time = r.gest; b.fitness = r.fitness;
+      b.rng.lo = r.rng_lo; b.rng.hi = r.rng_hi; b.rng.ctr = r.rng_ctr;
+      activate_child(w, b, c);
+      placed++;
+    }
+  }
+  finish_stats(w, placed, dropped);
+  if (out) *out = w.stats;
+  return 0;
+}
+
+int orc_get_stats(void* h, avgpu_update_stats* out) { *out = ((World*)h)->stats; return 0; }
 
 // ---------------------------------------------------------------------------
 // Reference-style serial world (the CPU baseline): Avida2Driver::Run's update

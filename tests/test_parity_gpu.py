@@ -112,3 +112,35 @@ def test_world_updates_bit_exact(golden):
     bad = pu.diff_states(a, b, oa, ob, fa, fb, CAP)
     assert not bad, f"{len(bad)} mismatches: {bad[:5]}"
     assert so.num_organisms > 100
+
+
+@pytest.mark.parametrize("T,geometry", [(2, 2), (4, 2), (2, 1)])
+def test_gpu_strip_tiles_equal_single_world(golden, T, geometry):
+    """Multi-GPU row on one GPU: T strips of one 64x64 world run
+    through the halo protocol (avida_amd/tiles.py, in-process loopback
+    transport) equal the untiled oracle world, every cell, every field."""
+    import torch
+    from avida_amd import tiles
+    import tile_util as tu
+    X, Y, U = 64, 64, 40
+    ref, rstats = tu.single("oracle", golden, X, Y, U, geometry=geometry)
+    pairs = [tu.make_tile("gpu", golden, X, Y, T, k, geometry=geometry, device="cuda")
+             for k in range(T)]
+    world = tiles.StripWorld([t for _, t in pairs], tiles.LoopbackTransport())
+    sent = 0
+    for u in range(U):
+        world.update()
+        torch.cuda.synchronize()
+        sent += sum(tu.records_sent(t) for _, t in pairs)
+        tot = [tu.tile_stats(b) for b, _ in pairs]
+        for f in ("num_organisms", "insts_executed", "births", "deaths", "divides", "births_dropped"):
+            assert sum(getattr(s, f) for s in tot) == getattr(rstats[u], f), (u, f)
+    a, oa, fa = ref.states(0, X * Y, CAP)
+    per = X * Y // T
+    for k, (b, _) in enumerate(pairs):
+        s, o, f = b.states(0, per, CAP)
+        lo = k * per
+        bad = pu.diff_states(a[lo:lo + per], s, oa[lo * CAP:(lo + per) * CAP], o,
+                             fa[lo * CAP:(lo + per) * CAP], f, CAP)
+        assert not bad, f"tile {k}: {len(bad)} mismatches, first {bad[:3]}"
+    assert sent > 0

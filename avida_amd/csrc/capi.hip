@@ -374,7 +374,9 @@ int avgpu_destroy(avgpu_world* w) {
 int avgpu_set_stream(avgpu_world* w, void* hip_stream) {
   if (!w) return fail(AVGPU_EINVAL, "NULL world");
   HIPCHK(hipStreamSynchronize(w->stream));
-  w->stream = hip_stream ? reinterpret_cast<hipStream_t>(hip_stream) : w->own_stream;
+  // NULL is the HIP null stream -- the stream PyTorch's default current
+  // stream reports as 0 -- not the handle's own stream
+  w->stream = reinterpret_cast<hipStream_t>(hip_stream);
   return 0;
 }
 

@@ -187,6 +187,11 @@ __host__ __device__ inline int64_t record_bytes(int x, int64_t arena) {
 #define CNT_WAVES 17
 #define CNT_HALO_SENT 18  /* offspring shipped to a neighbouring tile */
 #define CNT_HALO_LOST 19  /* offspring lost to a full halo arena (counted in DROPPED too) */
+// 20..25: AVGPU_PHASE_CLOCKS loop cycles by block (decode, fast, copy, switch,
+// wave phase, advance); 26..30: iterations with a lane in pop/push, IO,
+// h-alloc, h-divide, h-search/if-label
+#define CNT_CB0 20
+#define CNT_CASE0 26
 // Counters are sharded over NSHARD lines (CNT_STRIDE x u64 each) so that the
 // per-wave adds of a 16K-wave launch do not serialise on one L2 address; they
 // are cleared every update, and counters[CNT_CUM_BASE + k] accumulates slot k

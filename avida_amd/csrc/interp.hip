@@ -65,13 +65,17 @@ __device__ __forceinline__ int wave_sum_i32(int v) {
   return v;
 }
 
-template <int S>
 // The world descriptor is read through a device pointer rather than passed by
 // value: as a by-value kernel argument its ~70 pointers and scalars were all
 // held in SGPRs and spilled into VGPR lanes (hundreds of v_readlane in the
 // loop); through the pointer each field is a scalar load at its use.
-__global__ __launch_bounds__(64) void k_interpret(const DevWorld* __restrict__ Wp, int cls, int mode,
-                                                  int64_t first, int64_t count) {
+//
+// One 64-organism chunk: class 0 = cells first + 64*chunk + lane (dense
+// sweep), classes 1..3 = entries 64*chunk + lane of the class list.
+template <int S>
+__device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp, int cls, int mode,
+                                                int64_t first, int64_t count, int64_t chunk,
+                                                uint32_t* __restrict__ lds32) {
   const DevWorld& W = *Wp;
   // per-lane tape stride: a whole number of 16-byte quads (16-B LDS-DMA) with
   // room for the fetch / label windows that read up to 16 bytes past a site
@@ -81,8 +85,6 @@ __global__ __launch_bounds__(64) void k_interpret(const DevWorld* __restrict__ W
   constexpr int STK_WORDS = 2 * AVGPU_STACK_SIZE * 64;
   // one __shared__ object: tapes | stacks | task LUT (256 x u16) | rand_cum (64 x i32) |
   // rand_code (64 B) | rand_lut (256 B) | reactions (16 x RT_STRIDE words)
-  constexpr int TAB_WORDS = 128 + 64 + 16 + 64 + AVGPU_MAX_REACTIONS * RT_STRIDE;
-  __shared__ __attribute__((aligned(16))) uint32_t lds32[TAPE_WORDS + STK_WORDS + TAB_WORDS];
   uint8_t* lds = reinterpret_cast<uint8_t*>(lds32);
   int32_t* stk = reinterpret_cast<int32_t*>(lds32 + TAPE_WORDS);
   uint32_t* tab = lds32 + TAPE_WORDS + STK_WORDS;
@@ -98,7 +100,7 @@ __global__ __launch_bounds__(64) void k_interpret(const DevWorld* __restrict__ W
   int M = 0;
   if (cls == 0) {
     // dense sweep in cell order: coalesced state loads, no list
-    const int64_t c = first + (int64_t)blockIdx.x * 64 + lane;
+    const int64_t c = first + chunk * 64 + lane;
     if (c < first + count) {
       const uint32_t c0 = W.ctl[c];
       const int m0 = W.mem_size[c];
@@ -109,9 +111,9 @@ __global__ __launch_bounds__(64) void k_interpret(const DevWorld* __restrict__ W
     }
   } else {
     const int lcount = W.class_count[cls];
-    const int base = blockIdx.x * 64;
+    const int64_t base = chunk * 64;
     if (base >= lcount) return;
-    const int idx = base + lane;
+    const int idx = (int)base + lane;
     if (idx < lcount) {
       cell = W.class_list[(int64_t)cls * N + idx];
       M = W.mem_size[cell];
@@ -122,6 +124,14 @@ __global__ __launch_bounds__(64) void k_interpret(const DevWorld* __restrict__ W
 #ifdef AVGPU_PHASE_CLOCKS
   const uint64_t clk0 = __builtin_amdgcn_s_memtime();
   int it_fast = 0, it_copy = 0, it_slow = 0;
+  // loop cycles by block: decode, fast, copy, switch, wave phase, advance
+  uint64_t cb[6] = {0, 0, 0, 0, 0, 0};
+  uint64_t clast = 0;
+  // iterations in which some lane ran: pop/push, IO, h-alloc, h-divide, h-search/if-label
+  int it_case[5] = {0, 0, 0, 0, 0};
+#define CK(k) do { const uint64_t _n = __builtin_amdgcn_s_memtime(); cb[k] += _n - clast; clast = _n; } while (0)
+#else
+#define CK(k) do { } while (0)
 #endif
   const int m_in = M;
 
@@ -244,6 +254,10 @@ __global__ __launch_bounds__(64) void k_interpret(const DevWorld* __restrict__ W
   while (true) {
     const bool run = alive && budget > 0 && !stop && !spill;
     if (!__any(run)) break;                                   // wave-uniform loop
+#ifdef AVGPU_PHASE_CLOCKS
+    if (clast == 0) clast = __builtin_amdgcn_s_memtime();
+    CK(5);
+#endif
     int rq = RQ_NONE, qa = 0, qb = 0;
     bool adv = true;                                          // m_advance_ip
     bool stepped = false;
@@ -288,7 +302,13 @@ __global__ __launch_bounds__(64) void k_interpret(const DevWorld* __restrict__ W
     it_fast += __ballot((FAST_OPS & obit) != 0u) != 0ull;
     it_copy += __ballot(op == AVGPU_H_H_COPY) != 0ull;
     it_slow += __ballot(!(FAST_OPS & obit) && op != AVGPU_H_H_COPY) != 0ull;
+    it_case[0] += __ballot(op == AVGPU_H_POP || op == AVGPU_H_PUSH) != 0ull;
+    it_case[1] += __ballot(op == AVGPU_H_IO) != 0ull;
+    it_case[2] += __ballot(op == AVGPU_H_H_ALLOC) != 0ull;
+    it_case[3] += __ballot(op == AVGPU_H_H_DIVIDE) != 0ull;
+    it_case[4] += __ballot(op == AVGPU_H_H_SEARCH || op == AVGPU_H_IF_LABEL) != 0ull;
 #endif
+    CK(0);
     if (FAST_OPS & obit) {
       // ---- branch-free ops: register ALU, swap, conditionals, head moves ----
       const int rn = (r == 2) ? 0 : r + 1;                    // FindNextRegister :1676
@@ -322,7 +342,9 @@ __global__ __launch_bounds__(64) void k_interpret(const DevWorld* __restrict__ W
       const bool skip = (op == AVGPU_H_IF_N_EQU && ra == rb) || (op == AVGPU_H_IF_LESS && ra >= rb);
       if (skip) ip = head_adjust(ip + 1, M);
       ctl ^= (op == AVGPU_H_SWAP_STK) ? CTL_CURSTK : 0u;                     // swap-stk :2739
-    } else if (op == AVGPU_H_H_COPY) {                        // :7130 Inst_HeadCopy
+    }
+    CK(1);
+    if (op == AVGPU_H_H_COPY) {                               // :7130 Inst_HeadCopy
       rh = head_adjust(rh, M);
       wh = head_adjust(wh, M);
       int v = T[rh] & CODE_MASK;
@@ -338,7 +360,9 @@ __global__ __launch_bounds__(64) void k_interpret(const DevWorld* __restrict__ W
       T[wh] = (uint8_t)((T[wh] & TF_EXEC) | TF_COPIED | v);
       rh = head_adjust(rh + 1, M);
       wh = head_adjust(wh + 1, M);
-    } else switch (op) {
+    }
+    CK(2);
+    if (!(FAST_OPS & obit) && op != AVGPU_H_H_COPY) switch (op) {
       case AVGPU_H_POP: {                                     // :2698, cCPUStack::Pop
         const int k = (ctl & CTL_CURSTK) ? 1 : 0;
         int sp = k ? CTL_SP1(ctl) : CTL_SP0(ctl);
@@ -497,6 +521,7 @@ __global__ __launch_bounds__(64) void k_interpret(const DevWorld* __restrict__ W
     }
     }  // !spill
     }  // run
+    CK(3);
 
     // ---- wave phase: serve the posted requests, one lane at a time ----
     unsigned long long pend = __ballot(rq != RQ_NONE);
@@ -712,11 +737,13 @@ __global__ __launch_bounds__(64) void k_interpret(const DevWorld* __restrict__ W
       }
     }
 
+    CK(4);
     if (stepped && !stop) {
       if (adv) ip = head_adjust(ip + 1, M);                   // ip.Advance() :1013
       if (mx > 0 && tu >= mx) alive = false;                  // death :1045-1049
     }
   }
+#undef CK
 #undef GETREG
 #undef SETREG
 #undef GETHEAD
@@ -835,9 +862,28 @@ __global__ __launch_bounds__(64) void k_interpret(const DevWorld* __restrict__ W
       count_add(W, CNT_IT_COPY, (unsigned long long)it_copy);
       count_add(W, CNT_IT_SLOW, (unsigned long long)it_slow);
       count_add(W, CNT_WAVES, 1ull);
+      for (int k = 0; k < 6; k++) count_add(W, CNT_CB0 + k, cb[k]);
+      for (int k = 0; k < 5; k++) count_add(W, CNT_CASE0 + k, (unsigned long long)it_case[k]);
     }
   }
 #endif
+}
+
+template <int S>
+__global__ __launch_bounds__(64) void k_interpret(const DevWorld* __restrict__ Wp, int cls, int mode,
+                                                  int64_t first, int64_t count) {
+  constexpr int TAB_WORDS = 128 + 64 + 16 + 64 + AVGPU_MAX_REACTIONS * RT_STRIDE;
+  __shared__ __attribute__((aligned(16))) uint32_t lds32[64 * (S + 16) / 4 + 2 * AVGPU_STACK_SIZE * 64 + TAB_WORDS];
+  if (cls == 0) {
+    interpret_chunk<S>(Wp, 0, mode, first, count, blockIdx.x, lds32);
+    return;
+  }
+  // list classes: grid-stride over the list (its length is known on device only)
+  const int lcount = Wp->class_count[cls];
+  for (int64_t chunk = blockIdx.x; chunk * 64 < lcount; chunk += gridDim.x) {
+    interpret_chunk<S>(Wp, cls, mode, first, count, chunk, lds32);
+    __syncthreads();
+  }
 }
 
 }  // namespace
@@ -845,14 +891,16 @@ __global__ __launch_bounds__(64) void k_interpret(const DevWorld* __restrict__ W
 void launch_interpret_classes(const DevWorld& W, const DevWorld* dW, int mode, hipStream_t s,
                               int64_t first, int64_t count, int* launches, hipEvent_t* after_class) {
   const unsigned blocks = (unsigned)((count + 63) / 64);
+  // list classes: a capped grid strides over the list
+  const unsigned lblocks = std::min(blocks, 2048u);
   if (blocks > 0) {
     hipLaunchKernelGGL(k_interpret<CLASS0_SIZE>, dim3(blocks), dim3(64), 0, s, dW, 0, mode, first, count);
     if (after_class) hipEventRecord(after_class[0], s);
-    hipLaunchKernelGGL(k_interpret<CLASS1_SIZE>, dim3(blocks), dim3(64), 0, s, dW, 1, mode, first, count);
+    hipLaunchKernelGGL(k_interpret<CLASS1_SIZE>, dim3(lblocks), dim3(64), 0, s, dW, 1, mode, first, count);
     if (after_class) hipEventRecord(after_class[1], s);
-    hipLaunchKernelGGL(k_interpret<CLASS2_SIZE>, dim3(blocks), dim3(64), 0, s, dW, 2, mode, first, count);
+    hipLaunchKernelGGL(k_interpret<CLASS2_SIZE>, dim3(lblocks), dim3(64), 0, s, dW, 2, mode, first, count);
     if (after_class) hipEventRecord(after_class[2], s);
-    hipLaunchKernelGGL(k_interpret<CLASS3_SIZE>, dim3(blocks), dim3(64), 0, s, dW, 3, mode, first, count);
+    hipLaunchKernelGGL(k_interpret<CLASS3_SIZE>, dim3(lblocks), dim3(64), 0, s, dW, 3, mode, first, count);
     if (launches) *launches += 4;
   } else if (after_class) {
     for (int k = 0; k < 3; k++) hipEventRecord(after_class[k], s);

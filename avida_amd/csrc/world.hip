@@ -313,9 +313,7 @@ __global__ void k_occ_init(DevWorld W) {
   if (c < ext) { W.occ[c] = (c < W.n && (W.ctl[c] & CTL_ALIVE)) ? 1 : 0; W.owner[c] = -1; }
 }
 
-__global__ void k_place_pick(DevWorld W) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= queue_len(W)) return;
+__device__ __forceinline__ void place_pick_one(const DevWorld& W, int64_t i) {
   const int64_t r = rec_of(W, i);
   if (W.b_state[r] != 0) return;
   const int parent = W.b_parent[r];
@@ -344,9 +342,7 @@ __global__ void k_place_pick(DevWorld W) {
 }
 
 // which: 0 every target, 1 targets inside the tile, 2 ghost-row targets
-__global__ void k_place_resolve(DevWorld W, int round, int which) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= queue_len(W)) return;
+__device__ __forceinline__ void place_resolve_one(const DevWorld& W, int64_t i, int round, int which) {
   const int64_t r = rec_of(W, i);
   if (W.b_state[r] != 0) return;
   const int t = W.b_target[r];
@@ -358,11 +354,19 @@ __global__ void k_place_resolve(DevWorld W, int round, int which) {
   }
 }
 
+// grid-stride over the birth queue (its length is only known on the device)
+#define QUEUE_LOOP(i) \
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, _qn = queue_len(W); i < _qn; \
+       i += (int64_t)gridDim.x * blockDim.x)
+__global__ void k_place_pick(DevWorld W) { QUEUE_LOOP(i) place_pick_one(W, i); }
+__global__ void k_place_resolve(DevWorld W, int round, int which) {
+  QUEUE_LOOP(i) place_resolve_one(W, i, round, which);
+}
 __global__ void k_place_clear(DevWorld W) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= queue_len(W)) return;
-  const int t = W.b_target[rec_of(W, i)];
-  if (t >= 0) W.claim[t] = 0ull;
+  QUEUE_LOOP(i) {
+    const int t = W.b_target[rec_of(W, i)];
+    if (t >= 0) W.claim[t] = 0ull;
+  }
 }
 
 // ---- strip-tile halo (DESIGN.md "Multi-GPU") ----
@@ -649,19 +653,31 @@ __global__ __launch_bounds__(256) void k_stats_partial(DevWorld W, double* part)
 }
 
 // out: [0..23] partial sums, 24 insts 25 deaths 26 divides 27 births 28 dropped
-// 29 spills 30 cumulative insts 31 cumulative births 32 slices 33 lane steps
+// 29 spills 30 cumulative insts 31 cumulative births 32 slices 33 lane steps.
+// Block k < NPART reduces partial row k (256 lanes, fixed order: lane t sums
+// entries t, t+256, ..., then a pairwise tree); block NPART sums the counter
+// shards.
 __global__ __launch_bounds__(256) void k_stats_final(DevWorld W, const double* part, int64_t nb,
                                                      double* out) {
+  __shared__ double sd[256];
   __shared__ unsigned long long cs[8][CNT_STRIDE];
-  const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
-  for (int k = wv; k < NPART; k += 4) {
+  const int tid = threadIdx.x;
+  const int k = blockIdx.x;
+  if (k < NPART) {
+    const bool mx = k == 5;
     double acc = 0.0;
-    for (int64_t b = lane; b < nb; b += 64) {
+    for (int64_t b = tid; b < nb; b += 256) {
       const double o = part[(int64_t)k * nb + b];
-      acc = (k == 5) ? fmax(acc, o) : acc + o;
+      acc = mx ? fmax(acc, o) : acc + o;
     }
-    acc = (k == 5) ? wave_max(acc) : wave_sum(acc);
-    if (lane == 0) out[k] = acc;
+    sd[tid] = acc;
+    __syncthreads();
+    for (int stride = 128; stride >= 1; stride >>= 1) {
+      if (tid < stride) sd[tid] = mx ? fmax(sd[tid], sd[tid + stride]) : sd[tid] + sd[tid + stride];
+      __syncthreads();
+    }
+    if (tid == 0) out[k] = sd[0];
+    return;
   }
   {
     const int slot = tid & (CNT_STRIDE - 1), g = tid / CNT_STRIDE;   // 8 groups of shards
@@ -738,13 +754,15 @@ static void launch_stats(const DevWorld& W, hipStream_t s, double* stats) {
   const int64_t nb = (W.n + 255) / 256;
   double* part = stats + NSTAT;
   hipLaunchKernelGGL(k_stats_partial, dim3((unsigned)nb), dim3(256), 0, s, W, part);
-  hipLaunchKernelGGL(k_stats_final, dim3(1), dim3(256), 0, s, W, part, nb, stats);
+  hipLaunchKernelGGL(k_stats_final, dim3(NPART + 1), dim3(256), 0, s, W, part, nb, stats);
 }
 
 static unsigned activate_grid(const DevWorld& W) { return (unsigned)std::min<int64_t>(W.rcap, 32768); }
+// placement kernels stride over the queue; 8 blocks of 256 per CU cover it
+static unsigned place_grid(const DevWorld& W) { return (unsigned)std::min<int64_t>(nblk(W.rcap, 256), 2048); }
 
 void launch_world_post(const DevWorld& W, hipStream_t s, double* stats) {
-  const unsigned bb = nblk(W.rcap, 256);
+  const unsigned bb = place_grid(W);
   hipLaunchKernelGGL(k_occ_init, dim3(nblk(W.n, 256)), dim3(256), 0, s, W);
   for (int round = 0; round < 4; round++) {
     hipLaunchKernelGGL(k_place_pick, dim3(bb), dim3(256), 0, s, W);
@@ -780,7 +798,7 @@ void launch_tile_after_interpret(const DevWorld& W, hipStream_t s) {
 // phase 2: ghost rows in, resolve ghost targets, clear claims
 // phase 3: pack the ghost-row winners into the record buffers
 void launch_tile_place(const DevWorld& W, hipStream_t s, int round, int phase) {
-  const unsigned bb = nblk(W.rcap, 256);
+  const unsigned bb = place_grid(W);
   const unsigned hb = nblk(2 * (int64_t)W.world_x, 256);
   if (phase == 0) {
     if (round == 0) hipLaunchKernelGGL(k_halo_import, dim3(hb), dim3(256), 0, s, W, 0, round);

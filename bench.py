@@ -121,6 +121,9 @@ def main():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--side", type=int, default=1024)
+    ap.add_argument("--burn-in", type=int, default=150,
+                    help="untimed updates that age the seeded population before the warmup "
+                         "(its organisms start in lock step; ~10 gestations spread them out)")
     ap.add_argument("--seed", type=int, default=101)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
@@ -157,7 +160,7 @@ def main():
         else:
             capi.check(lib, lib.avgpu_run_update(h, None))
 
-    for _ in range(args.warmup):
+    for _ in range(args.burn_in + args.warmup):
         update()
     torch.cuda.synchronize()
     s0 = capi.AvgpuUpdateStats()
@@ -237,6 +240,7 @@ def main():
                         "avida.cfg mutation rates, births on, seeded with the detail-50000.pop "
                         "evolved genotypes (classic instset)",
             "world": f"{args.side}x{args.side}x{world}",
+            "burn_in_updates": args.burn_in,
             "organisms": int(tot_orgs),
             "updates_per_sec": args.steps / dt_max,
             "births_per_update": tot_births / args.steps,

@@ -297,8 +297,9 @@ int avgpu_run_updates(avgpu_world* w, int n_updates, avgpu_update_stats* last);
 int avgpu_update_totals(avgpu_world* w, double* dev_totals);
 int avgpu_update_run(avgpu_world* w, const double* dev_totals, avgpu_update_stats* out);
 /* Run the handle's work on an external HIP stream (e.g. the framework's
- * current stream, so that collectives order against it). NULL restores the
- * handle's own stream. */
+ * current stream, so that collectives order against it).  NULL is the HIP
+ * null stream (what PyTorch's default stream reports as 0); a new handle
+ * starts on a private non-blocking stream of its own. */
 int avgpu_set_stream(avgpu_world* w, void* hip_stream);
 
 /* ---- inspection (cHardwareBase inspection API, cpu/cHardwareBase.h:145-200) */

@@ -23,8 +23,9 @@ def main():
     updates = int(sys.argv[2]) if len(sys.argv) > 2 else 10
     lib = capi.load_product(build.OUT_CLK)
     golden = os.path.join(ROOT, "tests", "golden")
-    h, cfg, n = bench.build_world(lib, capi, files, golden, side, 101, 0, 0)
-    for _ in range(3):
+    h, cfg, n, _ = bench.build_world(lib, capi, files, golden, side, 101, 0, 0, 1)
+    burn = int(sys.argv[3]) if len(sys.argv) > 3 else 200
+    for _ in range(burn):
         capi.check(lib, lib.avgpu_run_update(h, None))
     tot = [0] * capi.NUM_COUNTERS
     buf = (C.c_int64 * capi.NUM_COUNTERS)()
@@ -49,6 +50,10 @@ def main():
         "c0_sites_per_slice": tot[capi.CNT_C0_SITES] / max(1, tot[capi.CNT_C0_SLICES]),
         "lane_efficiency": tot[capi.CNT_INSTS] / max(1, tot[capi.CNT_LANESTEPS]),
         "spills_per_update": tot[capi.CNT_SPILLS] / updates,
+        "loop_cycles_per_iter_by_block": {k: tot[20 + i] / it for i, k in enumerate(
+            ["decode", "fast", "copy", "switch", "wave_phase", "advance"])},
+        "frac_iters_with": {k: tot[26 + i] / it for i, k in enumerate(
+            ["pop_push", "io", "h_alloc", "h_divide", "search_label"])},
     }
     lib.avgpu_destroy(h)
     print(json.dumps(out, indent=1))

@@ -10,6 +10,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -117,7 +118,7 @@ int setup_world(avgpu_world* w, int64_t n, bool test_buffers) {
     A(t_child_len, n);
   }
   A(rand_cum, 64); A(rand_code, 64); A(task_lut, 256); A(rand_lut, 256);
-  A(react_tab, AVGPU_MAX_REACTIONS * RT_STRIDE);
+  A(react_tab, AVGPU_MAX_REACTIONS * RT_STRIDE); A(task_tab, 32);
   if ((rc = w->alloc(&w->d_W, 1))) return rc;
   const int64_t nb = (n + 255) / 256;
   if ((rc = w->alloc(&w->d_totals, (size_t)(8 + 2 * nb)))) return rc;
@@ -149,6 +150,9 @@ int setup_world(avgpu_world* w, int64_t n, bool test_buffers) {
   W.th_div_del = th(c.divide_del_prob);
   W.seed_lo = (uint32_t)c.seed;
   W.seed_hi = (uint32_t)(c.seed >> 32);
+  // interpreter slow-op batching (interp.hip); AVGPU_SLOW_BATCH overrides (tuning)
+  W.slow_batch = 8;
+  if (const char* e = getenv("AVGPU_SLOW_BATCH")) W.slow_batch = std::max(1, std::min(64, atoi(e)));
   W.row0 = 0;
   W.global_rows = c.world_y;
   W.rows = c.world_y;
@@ -210,6 +214,8 @@ int copy_tables(avgpu_world* dst, const avgpu_world* src) {
   const DevWorld& S = src->W;
   D.n_ops = S.n_ops; D.rand_total = S.rand_total; D.fill_code = S.fill_code;
   D.n_react = S.n_react;
+  D.env_simple = S.env_simple; D.env_react_mask = S.env_react_mask; D.env_once_mask = S.env_once_mask;
+  HIPCHK(hipMemcpy(D.task_tab, S.task_tab, 32 * sizeof(double), hipMemcpyDeviceToDevice));
   HIPCHK(hipMemcpy(D.react_tab, S.react_tab, AVGPU_MAX_REACTIONS * RT_STRIDE * sizeof(int32_t),
                    hipMemcpyDeviceToDevice));
   HIPCHK(hipMemcpy(D.rand_lut, S.rand_lut, 256, hipMemcpyDeviceToDevice));
@@ -446,6 +452,29 @@ int avgpu_load_env(avgpu_world* w, int nreact, const avgpu_reaction* r) {
     memcpy(t + RT_ADD, &bonus, 8);
   }
   W.n_react = nreact;
+  // simple-environment fast path of the IO task check (interp.hip)
+  double ttab[32];
+  for (int t = 0; t < 16; t++) { ttab[t] = 1.0; ttab[16 + t] = 0.0; }
+  bool simple = true;
+  uint32_t rmask = 0, omask = 0;
+  for (int i = 0; i < nreact; i++) {
+    const int32_t* t = tab + i * RT_STRIDE;
+    if (t[RT_TASK] != i) simple = false;
+    if (t[RT_HASREQ]) {
+      if (t[RT_MIN] > 0) simple = false;
+      else if (t[RT_MAX] == 1) omask |= 1u << i;
+      else if (t[RT_MAX] != INT32_MAX) simple = false;
+    }
+    rmask |= 1u << i;
+    double m, a;
+    memcpy(&m, t + RT_MULT, 8);
+    memcpy(&a, t + RT_ADD, 8);
+    if (t[RT_TYPE] == AVGPU_PROC_ADD) ttab[16 + i] = a; else ttab[i] = m;
+  }
+  W.env_simple = simple ? 1 : 0;
+  W.env_react_mask = rmask;
+  W.env_once_mask = omask;
+  HIPCHK(hipMemcpyAsync(W.task_tab, ttab, sizeof(ttab), hipMemcpyHostToDevice, w->stream));
   HIPCHK(hipMemcpyAsync(W.react_tab, tab, sizeof(tab), hipMemcpyHostToDevice, w->stream));
   HIPCHK(hipStreamSynchronize(w->stream));
   w->env_loaded = true;

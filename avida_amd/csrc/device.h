@@ -115,10 +115,17 @@ struct DevWorld {
   int n_ops;
   int32_t rand_total;
   uint8_t* rand_lut;  // [256] draw -> canonical code when rand_total <= 256
+  int32_t slow_batch;   // parked lanes that trigger the interpreter's slow phase (1..64)
   int n_react;
   // reactions, RT_STRIDE words each: task, process type, requisite min / max
   // count, has-requisite, in-use, bonus multiplier (f64), bonus addend (f64)
   int32_t* react_tab; // [AVGPU_MAX_REACTIONS][RT_STRIDE]
+  // simple environment (reaction i rewards task i; requisites absent, or
+  // min_count <= 0 with max_count 1 or unlimited): the IO check is bit logic
+  int32_t env_simple;
+  uint32_t env_react_mask;   // tasks with a reaction
+  uint32_t env_once_mask;    // tasks whose reaction has max_count 1
+  double* task_tab;          // [32]: bonus factor of task t's reaction, then its addend
   uint8_t fill_code;   // code of op 0 (new sites on allocate)
   // config scalars
   int32_t world_x, world_y, geometry;
@@ -188,7 +195,7 @@ __host__ __device__ inline int64_t record_bytes(int x, int64_t arena) {
 #define CNT_HALO_SENT 18  /* offspring shipped to a neighbouring tile */
 #define CNT_HALO_LOST 19  /* offspring lost to a full halo arena (counted in DROPPED too) */
 // 20..25: AVGPU_PHASE_CLOCKS loop cycles by block (decode, fast, copy, switch,
-// wave phase, advance); 26..30: iterations with a lane in pop/push, IO,
+// wave phase, advance); 26..31: slow-switch cycles in pop, push, IO,
 // h-alloc, h-divide, h-search/if-label
 #define CNT_CB0 20
 #define CNT_CASE0 26

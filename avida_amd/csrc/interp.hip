@@ -84,7 +84,8 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
   constexpr int TAPE_WORDS = 64 * STRIDE / 4;
   constexpr int STK_WORDS = 2 * AVGPU_STACK_SIZE * 64;
   // one __shared__ object: tapes | stacks | task LUT (256 x u16) | rand_cum (64 x i32) |
-  // rand_code (64 B) | rand_lut (256 B) | reactions (16 x RT_STRIDE words)
+  // rand_code (64 B) | rand_lut (256 B) | reactions (16 x RT_STRIDE words) |
+  // task bonus factors (16 doubles) | task bonus addends (16 doubles)
   uint8_t* lds = reinterpret_cast<uint8_t*>(lds32);
   int32_t* stk = reinterpret_cast<int32_t*>(lds32 + TAPE_WORDS);
   uint32_t* tab = lds32 + TAPE_WORDS + STK_WORDS;
@@ -93,6 +94,9 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
   const uint8_t* rcode = reinterpret_cast<const uint8_t*>(tab + 192);
   const uint8_t* rlut = reinterpret_cast<const uint8_t*>(tab + 208);
   const int32_t* rtab = reinterpret_cast<const int32_t*>(tab + 272);
+  // per-task bonus factor / addend of the simple-environment path (16 + 16 doubles)
+  const double* tmul = reinterpret_cast<const double*>(tab + 272 + AVGPU_MAX_REACTIONS * RT_STRIDE);
+  const double* tadd = tmul + 16;
 
   const int lane = threadIdx.x;
   const int64_t N = W.n;
@@ -127,11 +131,13 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
   // loop cycles by block: decode, fast, copy, switch, wave phase, advance
   uint64_t cb[6] = {0, 0, 0, 0, 0, 0};
   uint64_t clast = 0;
-  // iterations in which some lane ran: pop/push, IO, h-alloc, h-divide, h-search/if-label
-  int it_case[5] = {0, 0, 0, 0, 0};
+  // slow-switch cycles by case: pop, push, IO, h-alloc, h-divide, h-search/if-label
+  uint64_t cc[6] = {0, 0, 0, 0, 0, 0};
 #define CK(k) do { const uint64_t _n = __builtin_amdgcn_s_memtime(); cb[k] += _n - clast; clast = _n; } while (0)
+#define CKC(k) do { const uint64_t _n = __builtin_amdgcn_s_memtime(); cc[k] += _n - clast; clast = _n; } while (0)
 #else
 #define CK(k) do { } while (0)
+#define CKC(k) do { } while (0)
 #endif
   const int m_in = M;
 
@@ -145,6 +151,7 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
     if (lane < 16) l32[192 + lane] = reinterpret_cast<const uint32_t*>(W.rand_code)[lane];
     l32[208 + lane] = reinterpret_cast<const uint32_t*>(W.rand_lut)[lane];
     for (int k = lane; k < AVGPU_MAX_REACTIONS * RT_STRIDE; k += 64) l32[272 + k] = (uint32_t)W.react_tab[k];
+    l32[272 + AVGPU_MAX_REACTIONS * RT_STRIDE + lane] = reinterpret_cast<const uint32_t*>(W.task_tab)[lane];
   }
   // ---- stage tapes and stacks into LDS by LDS-DMA.  The 64 tapes form one
   // lane-linear image of 64 x QUADS quads (quad i = organism i / QUADS, part
@@ -192,6 +199,7 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
   double dmerit = 0.0, dfit = 0.0;
   int lt[AVGPU_NUM_LOGIC_TASKS];
   int rc[AVGPU_MAX_REACTIONS];   // reaction counts since slice start / last reset
+  uint32_t nzm = 0;              // tasks with a non-zero count this gestation
 #pragma unroll
   for (int q = 0; q < AVGPU_NUM_LOGIC_TASKS; q++) lt[q] = 0;
 #pragma unroll
@@ -215,7 +223,10 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
     outv = W.outbuf[cell]; outtot = W.out_total[cell];
     bonus = W.cur_bonus[cell];
 #pragma unroll
-    for (int q = 0; q < AVGPU_NUM_LOGIC_TASKS; q++) tc[q] = W.cur_task[(int64_t)q * N + cell];
+    for (int q = 0; q < AVGPU_NUM_LOGIC_TASKS; q++) {
+      tc[q] = W.cur_task[(int64_t)q * N + cell];
+      nzm |= (tc[q] > 0 ? 1u : 0u) << q;
+    }
     dexe = W.executed[cell]; dcop = W.copied[cell]; dnd = W.num_div[cell]; dgen = W.generation[cell];
   }
   prim0 = prim;
@@ -251,21 +262,28 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
   // iteration of the wave paid for the longest such loop of any of its lanes.
   const int RQ_NONE = 0, RQ_DIVIDE = 1, RQ_FILL = 2, RQ_SEARCH = 3;
   const uint32_t fill4 = (uint32_t)W.fill_code * 0x01010101u;
+  // Slow ops (stack, IO, h-alloc, h-divide, h-search, if-label) are batched:
+  // a lane that decodes one parks (the decode is committed: counters,
+  // executed flags, modifier) and keeps its op; the wave runs the divergent
+  // slow switch only once W.slow_batch lanes are parked, or when no unparked
+  // lane can step any more.  Each organism still executes its own
+  // instructions in order -- only the interleaving across lanes changes.
+  int pop = -1, pr = 0;                                       // parked op, its register
+  const uint32_t* T32 = reinterpret_cast<const uint32_t*>(T);
+  const int slow_batch = W.slow_batch;
   while (true) {
-    const bool run = alive && budget > 0 && !stop && !spill;
-    if (!__any(run)) break;                                   // wave-uniform loop
+    const bool run = alive && budget > 0 && !stop && !spill && pop < 0;
+    if (!__any(run || pop >= 0)) break;                       // wave-uniform loop
 #ifdef AVGPU_PHASE_CLOCKS
     if (clast == 0) clast = __builtin_amdgcn_s_memtime();
     CK(5);
 #endif
-    int rq = RQ_NONE, qa = 0, qb = 0;
     bool adv = true;                                          // m_advance_ip
     bool stepped = false;
     if (run) {
       // ---- SingleProcess (cpu/cHardwareCPU.cc:908-1058) ----
       const int ipa = head_adjust(ip, M);                     // ip.Adjust() :952
       // fetch window: sites ipa .. ipa+4 in two independent word reads
-      const uint32_t* T32 = reinterpret_cast<const uint32_t*>(T);
       const uint64_t fwin = ((uint64_t)T32[(ipa >> 2) + 1] << 32) | (uint64_t)T32[ipa >> 2];
       const uint32_t fsh = (uint32_t)(ipa & 3) * 8u;
       const int cur_byte = (int)((fwin >> fsh) & 0xFFu);
@@ -301,12 +319,6 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
 #ifdef AVGPU_PHASE_CLOCKS
     it_fast += __ballot((FAST_OPS & obit) != 0u) != 0ull;
     it_copy += __ballot(op == AVGPU_H_H_COPY) != 0ull;
-    it_slow += __ballot(!(FAST_OPS & obit) && op != AVGPU_H_H_COPY) != 0ull;
-    it_case[0] += __ballot(op == AVGPU_H_POP || op == AVGPU_H_PUSH) != 0ull;
-    it_case[1] += __ballot(op == AVGPU_H_IO) != 0ull;
-    it_case[2] += __ballot(op == AVGPU_H_H_ALLOC) != 0ull;
-    it_case[3] += __ballot(op == AVGPU_H_H_DIVIDE) != 0ull;
-    it_case[4] += __ballot(op == AVGPU_H_H_SEARCH || op == AVGPU_H_IF_LABEL) != 0ull;
 #endif
     CK(0);
     if (FAST_OPS & obit) {
@@ -362,7 +374,28 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
       wh = head_adjust(wh + 1, M);
     }
     CK(2);
-    if (!(FAST_OPS & obit) && op != AVGPU_H_H_COPY) switch (op) {
+    if (!(FAST_OPS & obit) && op != AVGPU_H_H_COPY) { pop = op; pr = r; stepped = false; }   // park
+    }  // !spill
+    }  // run
+    if (stepped && !stop) {
+      if (adv) ip = head_adjust(ip + 1, M);                   // ip.Advance() :1013
+      if (mx > 0 && tu >= mx) alive = false;                  // death :1045-1049
+    }
+    // ---- slow phase ----
+    const int npark = __popcll(__ballot(pop >= 0));
+    if (npark == 0) continue;
+    if (npark < slow_batch && __any(alive && budget > 0 && !stop && !spill && pop < 0)) continue;
+#ifdef AVGPU_PHASE_CLOCKS
+    it_slow++;
+#endif
+    {
+    int rq = RQ_NONE, qa = 0, qb = 0;
+    bool adv = true;
+    const bool sstep = pop >= 0;
+    if (sstep) {
+      const int op = pop, r = pr;
+      CK(3);
+      switch (op) {
       case AVGPU_H_POP: {                                     // :2698, cCPUStack::Pop
         const int k = (ctl & CTL_CURSTK) ? 1 : 0;
         int sp = k ? CTL_SP1(ctl) : CTL_SP0(ctl);
@@ -372,6 +405,7 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
         sp = (sp + 1 == AVGPU_STACK_SIZE) ? 0 : sp + 1;
         ctl = k ? ((ctl & ~0xF0u) | ((uint32_t)sp << 4)) : ((ctl & ~0xFu) | (uint32_t)sp);
         SETREG(r, v);
+        CKC(0);
         break; }
       case AVGPU_H_PUSH: {                                    // :2705, cCPUStack::Push
         const int k = (ctl & CTL_CURSTK) ? 1 : 0;
@@ -379,6 +413,7 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
         sp = (sp == 0) ? AVGPU_STACK_SIZE - 1 : sp - 1;
         stk[(k * AVGPU_STACK_SIZE + sp) * 64 + lane] = GETREG(r);
         ctl = k ? ((ctl & ~0xF0u) | ((uint32_t)sp << 4)) : ((ctl & ~0xFu) | (uint32_t)sp);
+        CKC(1);
         break; }
       case AVGPU_H_IO: {                                      // :4188 Inst_TaskIO
         const int out = GETREG(r);
@@ -406,13 +441,34 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
 #pragma unroll
         for (int p = 0; p < 8; p++) id += lo[p] * (1 << p);
         const uint32_t tmask = (!bad && id >= 0 && id < 256) ? lut[id] : 0u;
-        if (tmask) {
-          // cEnvironment::TestOutput / TestRequisites / DoProcesses
-          // (main/cEnvironment.cc:1314-1406, :1408-1503, :1610-1760)
+        // cEnvironment::TestOutput / TestRequisites / DoProcesses
+        // (main/cEnvironment.cc:1314-1406, :1408-1503, :1610-1760)
+        if (tmask && W.env_simple) {
+          // reaction i rewards task i, requisites at most "max_count=1"
+          // (capi.hip avgpu_load_env): the firing set is a bit operation and
+          // the bonus factors multiply in reaction order (ascending bits)
+          const uint32_t done = tmask & W.env_react_mask & ~(W.env_once_mask & nzm);
+          if (done) {
+            double mult = 1.0, addb = 0.0;
+            for (uint32_t d = done; d; d &= d - 1u) {
+              const int t = __ffs(d) - 1;
+              mult = __dmul_rn(mult, tmul[t]);
+              addb = __dadd_rn(addb, tadd[t]);
+            }
+#pragma unroll
+            for (int q = 0; q < AVGPU_NUM_LOGIC_TASKS; q++) {
+              tc[q] += (done >> q) & 1u;
+              rc[q] += (done >> q) & 1u;
+            }
+            nzm |= done;
+            bonus = __dadd_rn(__dmul_rn(bonus, mult), addb);   // cPhenotype.cc:1645-1646
+          }
+        } else if (tmask) {
           uint32_t done = 0;
           double mult = 1.0, addb = 0.0;
 #pragma unroll
           for (int i = 0; i < AVGPU_MAX_REACTIONS; i++) {
+            if (i >= W.n_react) break;
             const int32_t* rt = rtab + i * RT_STRIDE;         // uniform LDS reads
             const int t = rt[RT_TASK];
             int cnt = 0;
@@ -432,6 +488,7 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
           if (done) {
 #pragma unroll
             for (int q = 0; q < AVGPU_NUM_LOGIC_TASKS; q++) tc[q] += (done >> q) & 1u;
+            nzm |= done;
             bonus = __dadd_rn(__dmul_rn(bonus, mult), addb);   // cPhenotype.cc:1645-1646
           }
         }
@@ -442,6 +499,7 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
         in2 = in1; in1 = in0; in0 = in;
         intot++;
         SETREG(r, in);
+        CKC(2);
         break; }
       case AVGPU_H_H_ALLOC: {                                 // :3294 Inst_MaxAlloc -> Allocate_Main :1707
         const int cur = M;
@@ -460,6 +518,7 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
         M = nsz;
         ctl |= CTL_MAL;
         r0 = cur;
+        CKC(3);
         break; }
       case AVGPU_H_H_DIVIDE: {                                // :6961 -> :6942 -> Divide_Main :1775
         ip = head_adjust(ip, M); rh = head_adjust(rh, M); wh = head_adjust(wh, M); fh = head_adjust(fh, M);
@@ -474,38 +533,38 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
         if (ok && W.cfg_min_genome && (child < W.cfg_min_genome || div < W.cfg_min_genome)) ok = false;
         if (ok && W.cfg_max_genome && (child > W.cfg_max_genome || div > W.cfg_max_genome)) ok = false;
         if (ok) { rq = RQ_DIVIDE; qa = div; qb = child; }
+        CKC(4);
         break; }
       case AVGPU_H_H_SEARCH:                                  // :7245 Inst_HeadSearch
       case AVGPU_H_IF_LABEL: {                                // :6914 Inst_IfLabel
-        // ReadLabel (:1484-1502): the up to 10 sites after IP come from one
-        // 16-byte window (4 independent word reads)
-        uint32_t lab = 0;
-        int len = 0;
-        {
-          const int base = ip + 1;
-          const int w0 = base >> 2;
-          const uint64_t lo64 = ((uint64_t)T32[w0 + 1] << 32) | (uint64_t)T32[w0];
-          const uint64_t hi64 = ((uint64_t)T32[w0 + 3] << 32) | (uint64_t)T32[w0 + 2];
-          const int b0 = base & 3;
-          while (len < AVGPU_MAX_LABEL) {
-            const int p = base + len;
-            if (p >= M) break;
-            const int k = b0 + len;
-            const int cc = (int)(((k < 8) ? (lo64 >> (8 * k)) : (hi64 >> (8 * (k - 8)))) & CODE_MASK);
-            if (cc >= 3) break;
-            lab |= (uint32_t)cc << (2 * len);
-            len++;
-            if (len <= W.max_label_exe) T[p] |= TF_EXEC;
-          }
-          ip += len;
-        }
-        // Rotate(1, NUM_NOPS)
-        uint32_t rot = 0;
-        for (int i = 0; i < len; i++) {
-          uint32_t nv = ((lab >> (2 * i)) & 3u) + 1u;
-          if (nv >= 3u) nv -= 3u;
-          rot |= nv << (2 * i);
-        }
+        // ReadLabel (:1484-1502), branch free: the up to 10 sites after IP
+        // come from one 16-byte window; a byte is a nop iff its code < 3,
+        // i.e. (code + 0x7D) has bit 7 clear (codes are <= 0x3F, no carries)
+        const int base = ip + 1;
+        const int w0 = base >> 2;
+        const uint32_t bsh = (uint32_t)(base & 3) * 8u;
+        uint64_t lo64 = ((uint64_t)T32[w0 + 1] << 32) | (uint64_t)T32[w0];
+        uint64_t hi64 = ((uint64_t)T32[w0 + 3] << 32) | (uint64_t)T32[w0 + 2];
+        if (bsh) { lo64 = (lo64 >> bsh) | (hi64 << (64u - bsh)); hi64 >>= bsh; }
+        const uint64_t K3F = 0x3F3F3F3F3F3F3F3Full, K7D = 0x7D7D7D7D7D7D7D7Dull, K80 = 0x8080808080808080ull;
+        const uint64_t cl = lo64 & K3F, ch = hi64 & K3F;
+        const uint64_t nl = (cl + K7D) & K80, nh = (ch + K7D) & K80;
+        int len = nl ? (int)(__ffsll((long long)nl) - 8) >> 3 : 8 + (nh ? (int)(__ffsll((long long)nh) - 8) >> 3 : 8);
+        len = min(len, min(AVGPU_MAX_LABEL, M - base));
+        len = max(len, 0);
+        // 2-bit nop codes of bytes 0..7 packed (SWAR), bytes 8, 9 after them
+        uint64_t v = cl & 0x0303030303030303ull;
+        v = (v | (v >> 6)) & 0x000F000F000F000Full;
+        v = (v | (v >> 12)) & 0x000000FF000000FFull;
+        v = (v | (v >> 24)) & 0xFFFFull;
+        uint32_t lab = (uint32_t)v | ((uint32_t)(ch & 3u) << 16) | ((uint32_t)((ch >> 8) & 3u) << 18);
+        const uint32_t lmask = (1u << (2 * len)) - 1u;
+        lab &= lmask;
+        for (int k = 0; k < min(len, W.max_label_exe); k++) T[base + k] |= TF_EXEC;
+        ip += len;
+        // Rotate(1, NUM_NOPS): per 2-bit digit 0->1, 1->2, 2->0
+        const uint32_t dl = lab & 0x55555u, dh = (lab >> 1) & 0x55555u;
+        const uint32_t rot = ((~dl & ~dh & 0x55555u) | (dl << 1)) & lmask;
         if (op == AVGPU_H_IF_LABEL) {
           const uint32_t packed = (uint32_t)len | (rot << 4);
           if (packed != rl) ip = head_adjust(ip + 1, M);
@@ -515,12 +574,12 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
         r1 = 0;                                               // empty label: found = IP
         r2 = 0;
         fh = head_adjust(ip + 1, M);
+        CKC(5);
         break; }
       default:
         break;
     }
-    }  // !spill
-    }  // run
+    }
     CK(3);
 
     // ---- wave phase: serve the posted requests, one lane at a time ----
@@ -628,6 +687,7 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
               lt[q] = tc[q];
               tc[q] = 0;
             }
+            nzm = 0;
 #pragma unroll
             for (int i = 0; i < AVGPU_MAX_REACTIONS; i++) rc[i] = 0;
             len = child;
@@ -737,13 +797,16 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
       }
     }
 
-    CK(4);
-    if (stepped && !stop) {
+    if (sstep && !stop) {
       if (adv) ip = head_adjust(ip + 1, M);                   // ip.Advance() :1013
       if (mx > 0 && tu >= mx) alive = false;                  // death :1045-1049
     }
+    pop = -1;
+    CK(4);
+    }
   }
 #undef CK
+#undef CKC
 #undef GETREG
 #undef SETREG
 #undef GETHEAD
@@ -863,7 +926,7 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
       count_add(W, CNT_IT_SLOW, (unsigned long long)it_slow);
       count_add(W, CNT_WAVES, 1ull);
       for (int k = 0; k < 6; k++) count_add(W, CNT_CB0 + k, cb[k]);
-      for (int k = 0; k < 5; k++) count_add(W, CNT_CASE0 + k, (unsigned long long)it_case[k]);
+      for (int k = 0; k < 6; k++) count_add(W, CNT_CASE0 + k, cc[k]);
     }
   }
 #endif
@@ -872,7 +935,7 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
 template <int S>
 __global__ __launch_bounds__(64) void k_interpret(const DevWorld* __restrict__ Wp, int cls, int mode,
                                                   int64_t first, int64_t count) {
-  constexpr int TAB_WORDS = 128 + 64 + 16 + 64 + AVGPU_MAX_REACTIONS * RT_STRIDE;
+  constexpr int TAB_WORDS = 128 + 64 + 16 + 64 + AVGPU_MAX_REACTIONS * RT_STRIDE + 64;
   __shared__ __attribute__((aligned(16))) uint32_t lds32[64 * (S + 16) / 4 + 2 * AVGPU_STACK_SIZE * 64 + TAB_WORDS];
   if (cls == 0) {
     interpret_chunk<S>(Wp, 0, mode, first, count, blockIdx.x, lds32);

@@ -52,8 +52,8 @@ def main():
         "spills_per_update": tot[capi.CNT_SPILLS] / updates,
         "loop_cycles_per_iter_by_block": {k: tot[20 + i] / it for i, k in enumerate(
             ["decode", "fast", "copy", "switch", "wave_phase", "advance"])},
-        "frac_iters_with": {k: tot[26 + i] / it for i, k in enumerate(
-            ["pop_push", "io", "h_alloc", "h_divide", "search_label"])},
+        "slow_phase_cycles_per_iter_by_case": {k: tot[26 + i] / it for i, k in enumerate(
+            ["pop", "push", "io", "h_alloc", "h_divide", "search_label"])},
     }
     lib.avgpu_destroy(h)
     print(json.dumps(out, indent=1))

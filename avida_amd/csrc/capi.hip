@@ -102,7 +102,7 @@ int setup_world(avgpu_world* w, int64_t n, bool test_buffers) {
   A(cur_react, AVGPU_MAX_REACTIONS * n);
   A(cur_bonus, n); A(merit, n); A(fitness, n); A(credit, n); A(gest_time, n); A(num_div, n);
   A(generation, n); A(copied, n); A(child_copied, n); A(executed, n); A(errors, n);
-  A(class_list, NUM_CLASSES * n); A(class_count, NUM_CLASSES); A(counters, CNT_WORDS);
+  A(class_list, NUM_CLASSES * n); A(order, n); A(class_count, NUM_CLASSES); A(counters, CNT_WORDS);
   // birth records: one primary record per cell + overflow for further
   // offspring of one slice (device.h); test worlds never enqueue births
   W.rcap = n + (test_buffers ? 16 : std::max<int64_t>(4096, n / 4));
@@ -317,7 +317,7 @@ int push_world(avgpu_world* w) {
   return 0;
 }
 
-int interpret(avgpu_world* w, int mode, int64_t first, int64_t count) {
+int interpret(avgpu_world* w, int mode, int64_t first, int64_t count, bool sorted = false) {
   int launches = 0;
   {
     const int prc = push_world(w);
@@ -327,7 +327,7 @@ int interpret(avgpu_world* w, int mode, int64_t first, int64_t count) {
   if (rc < 0) return rc;
   const int i = w->ring_head;
   HIPCHK(hipEventRecord(w->ring[i][0], w->stream));
-  launch_interpret_classes(w->W, w->d_W, mode, w->stream, first, count, &launches, &w->ring[i][1]);
+  launch_interpret_classes(w->W, w->d_W, mode, w->stream, first, count, &launches, &w->ring[i][1], sorted);
   HIPCHK(hipGetLastError());
   w->ring_head = (i + 1) % avgpu_world::RING;
   w->ring_count++;
@@ -550,7 +550,7 @@ int avgpu_update_run(avgpu_world* w, const double* dev_totals, avgpu_update_stat
   if (!dev_totals) return fail(AVGPU_EINVAL, "dev_totals is NULL");
   launch_world_pre(w->W, w->stream, dev_totals);
   HIPCHK(hipGetLastError());
-  rc = interpret(w, AVGPU_MODE_WORLD, 0, w->W.n);
+  rc = interpret(w, AVGPU_MODE_WORLD, 0, w->W.n, true);
   if (rc < 0) return rc;
   launch_world_post(w->W, w->stream, w->d_stats);
   HIPCHK(hipGetLastError());
@@ -804,7 +804,7 @@ int avgpu_tile_begin(avgpu_world* w, const double* dev_gathered, int ntiles) {
   launch_tile_totals(w->W, w->stream, dev_gathered, ntiles, w->d_totals);
   launch_world_pre(w->W, w->stream, w->d_totals);
   HIPCHK(hipGetLastError());
-  rc = interpret(w, AVGPU_MODE_WORLD, 0, w->W.n);
+  rc = interpret(w, AVGPU_MODE_WORLD, 0, w->W.n, true);
   if (rc < 0) return rc;
   launch_tile_after_interpret(w->W, w->stream);
   HIPCHK(hipGetLastError());

@@ -75,6 +75,7 @@ struct DevWorld {
   int32_t* errors;    // [n]
   // --- per-update work lists / queues ---
   int32_t* class_list;   // [NUM_CLASSES][n]
+  int32_t* order;        // [n] class-0 order of a world update: cells of each SORT_WIN window by budget
   int32_t* class_count;  // [NUM_CLASSES]
   unsigned long long* counters; // [16] insts, deaths, divides, births, dropped, ...
   // birth records.  Record r < n holds the first offspring that cell r's
@@ -326,7 +327,10 @@ struct LaunchInfo {
 // dW: device copy of W (avgpu_world::push_world)
 void launch_interpret_classes(const DevWorld& W, const DevWorld* dW, int mode, hipStream_t s,
                               int64_t first, int64_t count, int* launches,
-                              hipEvent_t* after_class = nullptr);
+                              hipEvent_t* after_class = nullptr, bool sorted = false);
+// class-0 windows: k_allot's budgets sorted (descending) inside windows of
+// SORT_WIN cells, so that a wave's 64 organisms get similar time slices
+#define SORT_WIN 2048
 void launch_world_pre(const DevWorld& W, hipStream_t s, const double* d_totals);
 void launch_world_post(const DevWorld& W, hipStream_t s, double* d_stats);
 void launch_classify_uniform(const DevWorld& W, hipStream_t s, int64_t first, int64_t count,

@@ -75,7 +75,7 @@ __device__ __forceinline__ int wave_sum_i32(int v) {
 template <int S>
 __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp, int cls, int mode,
                                                 int64_t first, int64_t count, int64_t chunk,
-                                                uint32_t* __restrict__ lds32) {
+                                                uint32_t* __restrict__ lds32, bool sorted) {
   const DevWorld& W = *Wp;
   // per-lane tape stride: a whole number of 16-byte quads (16-B LDS-DMA) with
   // room for the fetch / label windows that read up to 16 bytes past a site
@@ -103,8 +103,10 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
   int cell = -1;
   int M = 0;
   if (cls == 0) {
-    // dense sweep in cell order: coalesced state loads, no list
-    const int64_t c = first + chunk * 64 + lane;
+    // dense sweep: in cell order, or (world updates) through the
+    // budget-sorted windows of k_window_sort
+    const int64_t c = sorted ? (chunk * 64 + lane < count ? (int64_t)W.order[chunk * 64 + lane] : first + count)
+                             : first + chunk * 64 + lane;
     if (c < first + count) {
       const uint32_t c0 = W.ctl[c];
       const int m0 = W.mem_size[c];
@@ -934,17 +936,21 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
 
 template <int S>
 __global__ __launch_bounds__(64) void k_interpret(const DevWorld* __restrict__ Wp, int cls, int mode,
-                                                  int64_t first, int64_t count) {
+                                                  int64_t first, int64_t count, int sorted) {
   constexpr int TAB_WORDS = 128 + 64 + 16 + 64 + AVGPU_MAX_REACTIONS * RT_STRIDE + 64;
   __shared__ __attribute__((aligned(16))) uint32_t lds32[64 * (S + 16) / 4 + 2 * AVGPU_STACK_SIZE * 64 + TAB_WORDS];
   if (cls == 0) {
-    interpret_chunk<S>(Wp, 0, mode, first, count, blockIdx.x, lds32);
+    // sorted windows: the 32 chunks of a window run on one XCD (blocks are
+    // dealt to the 8 XCDs round robin), so its state lines meet in one L2
+    int64_t chunk = blockIdx.x;
+    if (sorted && (gridDim.x & 7) == 0) chunk = (int64_t)(blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
+    interpret_chunk<S>(Wp, 0, mode, first, count, chunk, lds32, sorted);
     return;
   }
   // list classes: grid-stride over the list (its length is known on device only)
   const int lcount = Wp->class_count[cls];
   for (int64_t chunk = blockIdx.x; chunk * 64 < lcount; chunk += gridDim.x) {
-    interpret_chunk<S>(Wp, cls, mode, first, count, chunk, lds32);
+    interpret_chunk<S>(Wp, cls, mode, first, count, chunk, lds32, false);
     __syncthreads();
   }
 }
@@ -952,18 +958,20 @@ __global__ __launch_bounds__(64) void k_interpret(const DevWorld* __restrict__ W
 }  // namespace
 
 void launch_interpret_classes(const DevWorld& W, const DevWorld* dW, int mode, hipStream_t s,
-                              int64_t first, int64_t count, int* launches, hipEvent_t* after_class) {
+                              int64_t first, int64_t count, int* launches, hipEvent_t* after_class,
+                              bool sorted) {
+  const int srt = (sorted && first == 0 && count == W.n) ? 1 : 0;
   const unsigned blocks = (unsigned)((count + 63) / 64);
   // list classes: a capped grid strides over the list
   const unsigned lblocks = std::min(blocks, 2048u);
   if (blocks > 0) {
-    hipLaunchKernelGGL(k_interpret<CLASS0_SIZE>, dim3(blocks), dim3(64), 0, s, dW, 0, mode, first, count);
+    hipLaunchKernelGGL(k_interpret<CLASS0_SIZE>, dim3(blocks), dim3(64), 0, s, dW, 0, mode, first, count, srt);
     if (after_class) hipEventRecord(after_class[0], s);
-    hipLaunchKernelGGL(k_interpret<CLASS1_SIZE>, dim3(lblocks), dim3(64), 0, s, dW, 1, mode, first, count);
+    hipLaunchKernelGGL(k_interpret<CLASS1_SIZE>, dim3(lblocks), dim3(64), 0, s, dW, 1, mode, first, count, 0);
     if (after_class) hipEventRecord(after_class[1], s);
-    hipLaunchKernelGGL(k_interpret<CLASS2_SIZE>, dim3(lblocks), dim3(64), 0, s, dW, 2, mode, first, count);
+    hipLaunchKernelGGL(k_interpret<CLASS2_SIZE>, dim3(lblocks), dim3(64), 0, s, dW, 2, mode, first, count, 0);
     if (after_class) hipEventRecord(after_class[2], s);
-    hipLaunchKernelGGL(k_interpret<CLASS3_SIZE>, dim3(lblocks), dim3(64), 0, s, dW, 3, mode, first, count);
+    hipLaunchKernelGGL(k_interpret<CLASS3_SIZE>, dim3(lblocks), dim3(64), 0, s, dW, 3, mode, first, count, 0);
     if (launches) *launches += 4;
   } else if (after_class) {
     for (int k = 0; k < 3; k++) hipEventRecord(after_class[k], s);

@@ -275,6 +275,47 @@ __global__ void k_allot(DevWorld W, const double* totals) {
   enqueue_class(W, (int)c, want, cls);
 }
 
+// ---- budget-sorted class-0 windows ----
+// A wave runs until its longest slice ends, so the class-0 interpreter takes
+// its 64 organisms from a window of SORT_WIN cells sorted by budget
+// (descending; ties in cell order).  Execution order does not change any
+// organism's result (per-organism RNG streams, placement by priority), only
+// how many lanes idle.  One 1024-thread block sorts one window in LDS
+// (bitonic network over keys budget << 11 | (2047 - index)).
+__global__ __launch_bounds__(1024) void k_window_sort(DevWorld W) {
+  __shared__ uint32_t key[SORT_WIN];
+  const int64_t base = (int64_t)blockIdx.x * SORT_WIN;
+  for (int i = threadIdx.x; i < SORT_WIN; i += 1024) {
+    const int64_t c = base + i;
+    uint32_t b = 0;
+    if (c < W.n) {
+      const uint32_t ctl = W.ctl[c];
+      const int bud = W.budget[c];
+      if ((ctl & CTL_ALIVE) && bud > 0 && class_of(need_of(W.mem_size[c], ctl, W.size_range)) == 0)
+        b = (uint32_t)min(bud, 0xFFFFF);
+    }
+    key[i] = (b << 11) | (uint32_t)(SORT_WIN - 1 - i);
+  }
+  __syncthreads();
+  for (int k = 2; k <= SORT_WIN; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = threadIdx.x; i < SORT_WIN; i += 1024) {
+        const int l = i ^ j;
+        if (l > i) {
+          const uint32_t a = key[i], b = key[l];
+          const bool desc = (i & k) == 0;          // descending runs first
+          if (desc ? (a < b) : (a > b)) { key[i] = b; key[l] = a; }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  for (int i = threadIdx.x; i < SORT_WIN; i += 1024) {
+    const int64_t c = base + (SORT_WIN - 1 - (int64_t)(key[i] & (SORT_WIN - 1)));
+    if (base + i < W.n) W.order[base + i] = (int32_t)c;
+  }
+}
+
 // ---- birth placement (cPopulation::PositionOffspring restated) ----
 // neighbour k of cell in fixed order NW N NE W E SW S SE (tools/cTopology.h).
 // Tiled worlds map the rows above / below the strip to the ghost rows
@@ -748,6 +789,7 @@ void launch_world_pre(const DevWorld& W, hipStream_t s, const double* totals) {
   hipMemsetAsync(W.b_count, 0, 2 * sizeof(int32_t), s);
   hipMemsetAsync(W.class_count, 0, sizeof(int32_t) * NUM_CLASSES, s);
   hipLaunchKernelGGL(k_allot, dim3(nblk(W.n, 256)), dim3(256), 0, s, W, totals);
+  hipLaunchKernelGGL(k_window_sort, dim3(nblk(W.n, SORT_WIN)), dim3(1024), 0, s, W);
 }
 
 static void launch_stats(const DevWorld& W, hipStream_t s, double* stats) {

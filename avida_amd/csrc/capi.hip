@@ -39,6 +39,8 @@ struct avgpu_world {
   int device = 0;
   hipStream_t stream = nullptr;      // current stream (own or external)
   hipStream_t own_stream = nullptr;
+  hipStream_t aux_stream[3] = {};   // classes 1..3 beside class 0 (world updates)
+  hipEvent_t ev_fork = nullptr, ev_join[3] = {};
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   // event ring around interpreter phases (avgpu_last_kernel_ms,
   // avgpu_kernel_times): ev[i][0] before class 0, ev[i][k+1] after class k
@@ -102,7 +104,7 @@ int setup_world(avgpu_world* w, int64_t n, bool test_buffers) {
   A(cur_react, AVGPU_MAX_REACTIONS * n);
   A(cur_bonus, n); A(merit, n); A(fitness, n); A(credit, n); A(gest_time, n); A(num_div, n);
   A(generation, n); A(copied, n); A(child_copied, n); A(executed, n); A(errors, n);
-  A(class_list, NUM_CLASSES * n); A(order, n); A(class_count, NUM_CLASSES); A(counters, CNT_WORDS);
+  A(class_list, NUM_LISTS * n); A(order, n); A(class_count, 8); A(counters, CNT_WORDS);
   // birth records: one primary record per cell + overflow for further
   // offspring of one slice (device.h); test worlds never enqueue births
   W.rcap = n + (test_buffers ? 16 : std::max<int64_t>(4096, n / 4));
@@ -151,7 +153,7 @@ int setup_world(avgpu_world* w, int64_t n, bool test_buffers) {
   W.seed_lo = (uint32_t)c.seed;
   W.seed_hi = (uint32_t)(c.seed >> 32);
   // interpreter slow-op batching (interp.hip); AVGPU_SLOW_BATCH overrides (tuning)
-  W.slow_batch = 8;
+  W.slow_batch = 12;
   if (const char* e = getenv("AVGPU_SLOW_BATCH")) W.slow_batch = std::max(1, std::min(64, atoi(e)));
   W.row0 = 0;
   W.global_rows = c.world_y;
@@ -189,6 +191,13 @@ avgpu_world* create_world(const avgpu_cfg* cfg, int device, int64_t n, bool test
   if (n <= 0) n = (int64_t)cfg->world_x * cfg->world_y;
   if (n <= 0 || n > (1ll << 30)) { delete w; fail(AVGPU_EINVAL, "bad cell count"); return nullptr; }
   if (hipStreamCreateWithFlags(&w->own_stream, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&w->aux_stream[0], hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&w->aux_stream[1], hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&w->aux_stream[2], hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&w->ev_fork, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&w->ev_join[0], hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&w->ev_join[1], hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&w->ev_join[2], hipEventDisableTiming) != hipSuccess ||
       hipEventCreate(&w->ev0) != hipSuccess || hipEventCreate(&w->ev1) != hipSuccess) {
     delete w; fail(AVGPU_EHIP, "stream/event creation failed"); return nullptr;
   }
@@ -327,7 +336,8 @@ int interpret(avgpu_world* w, int mode, int64_t first, int64_t count, bool sorte
   if (rc < 0) return rc;
   const int i = w->ring_head;
   HIPCHK(hipEventRecord(w->ring[i][0], w->stream));
-  launch_interpret_classes(w->W, w->d_W, mode, w->stream, first, count, &launches, &w->ring[i][1], sorted);
+  launch_interpret_classes(w->W, w->d_W, mode, w->stream, first, count, &launches, &w->ring[i][1], sorted,
+                           sorted ? w->aux_stream : nullptr, w->ev_fork, w->ev_join);
   HIPCHK(hipGetLastError());
   w->ring_head = (i + 1) % avgpu_world::RING;
   w->ring_count++;
@@ -373,6 +383,11 @@ int avgpu_destroy(avgpu_world* w) {
       if (w->ring[i][k]) hipEventDestroy(w->ring[i][k]);
   }
   if (w->own_stream) hipStreamDestroy(w->own_stream);
+  for (int k = 0; k < 3; k++) {
+    if (w->aux_stream[k]) { hipStreamSynchronize(w->aux_stream[k]); hipStreamDestroy(w->aux_stream[k]); }
+    if (w->ev_join[k]) hipEventDestroy(w->ev_join[k]);
+  }
+  if (w->ev_fork) hipEventDestroy(w->ev_fork);
   delete w;
   return 0;
 }

@@ -29,6 +29,7 @@
 #define CTL_ALIVE 0x400u
 
 #define NUM_CLASSES 4
+#define NUM_LISTS 7
 #define RT_STRIDE 12
 enum { RT_TASK = 0, RT_TYPE = 1, RT_MIN = 2, RT_MAX = 3, RT_HASREQ = 4, RT_USED = 5, RT_MULT = 6, RT_ADD = 8 };
 // budget bit carried by a slice handed to the next size class: its primary
@@ -74,9 +75,11 @@ struct DevWorld {
   int32_t* executed;  // [n]
   int32_t* errors;    // [n]
   // --- per-update work lists / queues ---
-  int32_t* class_list;   // [NUM_CLASSES][n]
+  // size-class lists: row k = 1..3 the organisms k_allot put in class k,
+  // row 3 + k the organisms that spilled into class k during the update
+  int32_t* class_list;   // [NUM_LISTS][n]
   int32_t* order;        // [n] class-0 order of a world update: cells of each SORT_WIN window by budget
-  int32_t* class_count;  // [NUM_CLASSES]
+  int32_t* class_count;  // [8] entries of each list row
   unsigned long long* counters; // [16] insts, deaths, divides, births, dropped, ...
   // birth records.  Record r < n holds the first offspring that cell r's
   // parent produced in its slice (no atomics in the interpreter loop); records
@@ -325,9 +328,13 @@ struct LaunchInfo {
 // class 0 runs densely over cells [first, first+count); classes 1..3 over their lists
 // after_class[k] (optional): event recorded after the class-k launch
 // dW: device copy of W (avgpu_world::push_world)
+// aux (optional): three streams on which the classes 1..3 of k_allot's
+// lists run concurrently with class 0 (ev_fork / ev_join[3] order them)
 void launch_interpret_classes(const DevWorld& W, const DevWorld* dW, int mode, hipStream_t s,
                               int64_t first, int64_t count, int* launches,
-                              hipEvent_t* after_class = nullptr, bool sorted = false);
+                              hipEvent_t* after_class = nullptr, bool sorted = false,
+                              hipStream_t* aux = nullptr, hipEvent_t ev_fork = nullptr,
+                              hipEvent_t* ev_join = nullptr);
 // class-0 windows: k_allot's budgets sorted (descending) inside windows of
 // SORT_WIN cells, so that a wave's 64 organisms get similar time slices
 #define SORT_WIN 2048

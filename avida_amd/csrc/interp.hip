@@ -75,7 +75,7 @@ __device__ __forceinline__ int wave_sum_i32(int v) {
 template <int S>
 __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp, int cls, int mode,
                                                 int64_t first, int64_t count, int64_t chunk,
-                                                uint32_t* __restrict__ lds32, bool sorted) {
+                                                uint32_t* __restrict__ lds32, bool sorted, int row) {
   const DevWorld& W = *Wp;
   // per-lane tape stride: a whole number of 16-byte quads (16-B LDS-DMA) with
   // room for the fetch / label windows that read up to 16 bytes past a site
@@ -116,12 +116,12 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
       }
     }
   } else {
-    const int lcount = W.class_count[cls];
+    const int lcount = W.class_count[row];
     const int64_t base = chunk * 64;
     if (base >= lcount) return;
     const int idx = (int)base + lane;
     if (idx < lcount) {
-      cell = W.class_list[(int64_t)cls * N + idx];
+      cell = W.class_list[(int64_t)row * N + idx];
       M = W.mem_size[cell];
     }
   }
@@ -855,8 +855,8 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
 #pragma unroll
     for (int k = 0; k < 2 * AVGPU_STACK_SIZE; k++) W.stack[(int64_t)k * N + cell] = stk[k * 64 + lane];
     if (spill) {
-      const int slot = atomicAdd(&W.class_count[cls + 1], 1);
-      W.class_list[(int64_t)(cls + 1) * N + slot] = cell;
+      const int slot = atomicAdd(&W.class_count[3 + cls + 1], 1);     // spill row of class cls+1
+      W.class_list[(int64_t)(3 + cls + 1) * N + slot] = cell;
       count_add(W, CNT_SPILLS, 1ull);
     }
   }
@@ -935,7 +935,7 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
 }
 
 template <int S>
-__global__ __launch_bounds__(64) void k_interpret(const DevWorld* __restrict__ Wp, int cls, int mode,
+__global__ __launch_bounds__(64) void k_interpret(const DevWorld* __restrict__ Wp, int cls, int row, int mode,
                                                   int64_t first, int64_t count, int sorted) {
   constexpr int TAB_WORDS = 128 + 64 + 16 + 64 + AVGPU_MAX_REACTIONS * RT_STRIDE + 64;
   __shared__ __attribute__((aligned(16))) uint32_t lds32[64 * (S + 16) / 4 + 2 * AVGPU_STACK_SIZE * 64 + TAB_WORDS];
@@ -944,13 +944,13 @@ __global__ __launch_bounds__(64) void k_interpret(const DevWorld* __restrict__ W
     // dealt to the 8 XCDs round robin), so its state lines meet in one L2
     int64_t chunk = blockIdx.x;
     if (sorted && (gridDim.x & 7) == 0) chunk = (int64_t)(blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
-    interpret_chunk<S>(Wp, 0, mode, first, count, chunk, lds32, sorted);
+    interpret_chunk<S>(Wp, 0, mode, first, count, chunk, lds32, sorted, 0);
     return;
   }
   // list classes: grid-stride over the list (its length is known on device only)
-  const int lcount = Wp->class_count[cls];
+  const int lcount = Wp->class_count[row];
   for (int64_t chunk = blockIdx.x; chunk * 64 < lcount; chunk += gridDim.x) {
-    interpret_chunk<S>(Wp, cls, mode, first, count, chunk, lds32, false);
+    interpret_chunk<S>(Wp, cls, mode, first, count, chunk, lds32, false, row);
     __syncthreads();
   }
 }
@@ -959,22 +959,44 @@ __global__ __launch_bounds__(64) void k_interpret(const DevWorld* __restrict__ W
 
 void launch_interpret_classes(const DevWorld& W, const DevWorld* dW, int mode, hipStream_t s,
                               int64_t first, int64_t count, int* launches, hipEvent_t* after_class,
-                              bool sorted) {
+                              bool sorted, hipStream_t* aux, hipEvent_t ev_fork, hipEvent_t* ev_join) {
   const int srt = (sorted && first == 0 && count == W.n) ? 1 : 0;
   const unsigned blocks = (unsigned)((count + 63) / 64);
   // list classes: a capped grid strides over the list
-  const unsigned lblocks = std::min(blocks, 2048u);
-  if (blocks > 0) {
-    hipLaunchKernelGGL(k_interpret<CLASS0_SIZE>, dim3(blocks), dim3(64), 0, s, dW, 0, mode, first, count, srt);
-    if (after_class) hipEventRecord(after_class[0], s);
-    hipLaunchKernelGGL(k_interpret<CLASS1_SIZE>, dim3(lblocks), dim3(64), 0, s, dW, 1, mode, first, count, 0);
-    if (after_class) hipEventRecord(after_class[1], s);
-    hipLaunchKernelGGL(k_interpret<CLASS2_SIZE>, dim3(lblocks), dim3(64), 0, s, dW, 2, mode, first, count, 0);
-    if (after_class) hipEventRecord(after_class[2], s);
-    hipLaunchKernelGGL(k_interpret<CLASS3_SIZE>, dim3(lblocks), dim3(64), 0, s, dW, 3, mode, first, count, 0);
-    if (launches) *launches += 4;
-  } else if (after_class) {
-    for (int k = 0; k < 3; k++) hipEventRecord(after_class[k], s);
+  const unsigned lb = std::min(blocks, 2048u);
+  if (blocks == 0) {
+    if (after_class)
+      for (int k = 0; k < 4; k++) hipEventRecord(after_class[k], s);
+    return;
   }
+  // Organisms k_allot put in classes 1..3 (list rows 1..3) do not depend on
+  // class 0; with an aux stream they run beside it and fill the CUs its tail
+  // leaves idle.  Spills (rows 4..6) run after both, in class order.
+  auto list = [&](int k, hipStream_t st) {
+    if (k == 1) hipLaunchKernelGGL(k_interpret<CLASS1_SIZE>, dim3(lb), dim3(64), 0, st, dW, 1, 1, mode, first, count, 0);
+    if (k == 2) hipLaunchKernelGGL(k_interpret<CLASS2_SIZE>, dim3(lb), dim3(64), 0, st, dW, 2, 2, mode, first, count, 0);
+    if (k == 3) hipLaunchKernelGGL(k_interpret<CLASS3_SIZE>, dim3(lb), dim3(64), 0, st, dW, 3, 3, mode, first, count, 0);
+  };
+  if (aux) {
+    // one aux stream per list: each is latency-bound on its longest slice
+    hipEventRecord(ev_fork, s);
+    for (int k = 0; k < 3; k++) {
+      hipStreamWaitEvent(aux[k], ev_fork, 0);
+      list(k + 1, aux[k]);
+      hipEventRecord(ev_join[k], aux[k]);
+    }
+  }
+  hipLaunchKernelGGL(k_interpret<CLASS0_SIZE>, dim3(blocks), dim3(64), 0, s, dW, 0, 0, mode, first, count, srt);
+  if (after_class) hipEventRecord(after_class[0], s);
+  if (aux)
+    for (int k = 0; k < 3; k++) hipStreamWaitEvent(s, ev_join[k], 0);
+  else
+    for (int k = 1; k <= 3; k++) list(k, s);
+  hipLaunchKernelGGL(k_interpret<CLASS1_SIZE>, dim3(lb), dim3(64), 0, s, dW, 1, 4, mode, first, count, 0);
+  if (after_class) hipEventRecord(after_class[1], s);
+  hipLaunchKernelGGL(k_interpret<CLASS2_SIZE>, dim3(lb), dim3(64), 0, s, dW, 2, 5, mode, first, count, 0);
+  if (after_class) hipEventRecord(after_class[2], s);
+  hipLaunchKernelGGL(k_interpret<CLASS3_SIZE>, dim3(lb), dim3(64), 0, s, dW, 3, 6, mode, first, count, 0);
   if (after_class) hipEventRecord(after_class[3], s);
+  if (launches) *launches += 7;
 }

@@ -14,21 +14,37 @@
 
 namespace {
 
-// Append `cell` to its size-class list (wave-aggregated atomics per class).
-// Class 0 is not listed: k_interpret<CLASS0_SIZE> sweeps the cells densely.
+// Append `cell` to its size-class list (rows 1..3).  Class 0 is not listed:
+// k_interpret<CLASS0_SIZE> sweeps the cells densely.  Block-aggregated: one
+// global atomic per class and block (a per-wave atomic on three addresses
+// serialised ~16K waves in L2), lanes then write at block base + wave offset
+// + rank.  blockDim.x must be 256.
 __device__ __forceinline__ void enqueue_class(const DevWorld& W, int cell, bool want, int cls) {
+  __shared__ int s_cnt[NUM_CLASSES], s_base[NUM_CLASSES];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if (threadIdx.x < NUM_CLASSES) s_cnt[threadIdx.x] = 0;
+  __syncthreads();
+  int woff[NUM_CLASSES];
+  unsigned long long masks[NUM_CLASSES];
+#pragma unroll
   for (int k = 1; k < NUM_CLASSES; k++) {
-    const bool mine = want && cls == k;
-    const unsigned long long mask = __ballot(mine);
-    if (!mask) continue;
-    const int lane = threadIdx.x & 63;
-    const int leader = __ffsll((long long)mask) - 1;
-    int base = 0;
-    if (lane == leader) base = atomicAdd(&W.class_count[k], __popcll(mask));
-    base = __shfl(base, leader);
-    if (mine) {
-      const int rank = __popcll(mask & ((1ull << lane) - 1ull));
-      W.class_list[(int64_t)k * W.n + base + rank] = cell;
+    masks[k] = __ballot(want && cls == k);
+    woff[k] = 0;
+    // waves take their offsets in wave order (deterministic list order)
+    for (int w = 0; w < 4; w++) {
+      if (w == wv && lane == 0 && masks[k]) s_cnt[k] += __popcll(masks[k]);
+      __syncthreads();
+      if (w == wv) woff[k] = s_cnt[k] - __popcll(masks[k]);
+    }
+  }
+  if (threadIdx.x > 0 && threadIdx.x < NUM_CLASSES)
+    s_base[threadIdx.x] = s_cnt[threadIdx.x] ? atomicAdd(&W.class_count[threadIdx.x], s_cnt[threadIdx.x]) : 0;
+  __syncthreads();
+#pragma unroll
+  for (int k = 1; k < NUM_CLASSES; k++) {
+    if (want && cls == k) {
+      const int rank = __popcll(masks[k] & ((1ull << lane) - 1ull));
+      W.class_list[(int64_t)k * W.n + s_base[k] + woff[k] + rank] = cell;
     }
   }
 }
@@ -768,7 +784,7 @@ void launch_get_states(const DevWorld& W, hipStream_t s, int64_t first, int64_t 
 
 void launch_classify_uniform(const DevWorld& W, hipStream_t s, int64_t first, int64_t count,
                              const int32_t* budget, int32_t uniform) {
-  hipMemsetAsync(W.class_count, 0, sizeof(int32_t) * NUM_CLASSES, s);
+  hipMemsetAsync(W.class_count, 0, sizeof(int32_t) * 8, s);
   hipLaunchKernelGGL(k_classify_uniform, dim3(nblk(count, 256)), dim3(256), 0, s, W, first, count,
                      budget, uniform);
 }
@@ -787,7 +803,7 @@ void launch_merit_total(const DevWorld& W, hipStream_t s, double* totals, double
 void launch_world_pre(const DevWorld& W, hipStream_t s, const double* totals) {
   hipMemsetAsync(W.counters, 0, sizeof(unsigned long long) * NSHARD * CNT_STRIDE, s);
   hipMemsetAsync(W.b_count, 0, 2 * sizeof(int32_t), s);
-  hipMemsetAsync(W.class_count, 0, sizeof(int32_t) * NUM_CLASSES, s);
+  hipMemsetAsync(W.class_count, 0, sizeof(int32_t) * 8, s);
   hipLaunchKernelGGL(k_allot, dim3(nblk(W.n, 256)), dim3(256), 0, s, W, totals);
   hipLaunchKernelGGL(k_window_sort, dim3(nblk(W.n, SORT_WIN)), dim3(1024), 0, s, W);
 }

@@ -27,6 +27,11 @@
 #define CTL_CURSTK 0x100u
 #define CTL_MAL 0x200u
 #define CTL_ALIVE 0x400u
+// "fresh" offspring (k_activate): registers, heads, stacks, label, IO
+// buffers, counters, task / reaction counts and bonus hold their birth values
+// (zero, default bonus) implicitly -- the SoA rows are stale until the
+// organism's first slice writes them back.  Every reader honours the bit.
+#define CTL_FRESH 0x800u
 
 #define NUM_CLASSES 4
 #define NUM_LISTS 7

@@ -127,6 +127,7 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
   }
   const bool active = cell >= 0;
   if (!__any(active)) return;
+  const bool fresh = active && (W.ctl[cell] & CTL_FRESH);
 #ifdef AVGPU_PHASE_CLOCKS
   const uint64_t clk0 = __builtin_amdgcn_s_memtime();
   int it_fast = 0, it_copy = 0, it_slow = 0;
@@ -172,7 +173,7 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
   }
 #pragma unroll
   for (int k = 0; k < 2 * AVGPU_STACK_SIZE; k++) {
-    if (active)
+    if (active && !fresh)
 #ifdef AVGPU_NO_LDS_DMA
       stk[k * 64 + lane] = W.stack[(int64_t)k * N + cell];
 #else
@@ -197,31 +198,33 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
   for (int q = 0; q < AVGPU_NUM_LOGIC_TASKS; q++) tc[q] = 0;
   // divide bookkeeping kept on chip so that no global load or store is
   // compiler-visible inside the loop (written back after it if a divide happened)
-  int dexe = 0, dcop = 0, dnd = 0, dgen = 0, dccop = 0, dgt = 0;
-  double dmerit = 0.0, dfit = 0.0;
-  int lt[AVGPU_NUM_LOGIC_TASKS];
+  int dexe = 0, dcop = 0, dnd = 0, dgen = 0;
   int rc[AVGPU_MAX_REACTIONS];   // reaction counts since slice start / last reset
   uint32_t nzm = 0;              // tasks with a non-zero count this gestation
-#pragma unroll
-  for (int q = 0; q < AVGPU_NUM_LOGIC_TASKS; q++) lt[q] = 0;
 #pragma unroll
   for (int q = 0; q < AVGPU_MAX_REACTIONS; q++) rc[q] = 0;
   bool didv = false, prim = false, prim0 = false;
   int ndrop = 0;
   if (active) {
-    r0 = W.reg[cell]; r1 = W.reg[N + cell]; r2 = W.reg[2 * N + cell];
-    ip = W.head[cell]; rh = W.head[N + cell]; wh = W.head[2 * N + cell]; fh = W.head[3 * N + cell];
-    ctl = W.ctl[cell]; rl = W.rlabel[cell];
-    cyc = W.cycles[cell]; tu = W.time_used[cell]; gs = W.gest_start[cell];
+    // written at birth (setup_child) or by the previous slice
+    ctl = W.ctl[cell];
     mx = W.max_exec[cell]; blen = W.birth_len[cell];
     klo = W.rng[cell]; khi = W.rng[N + cell]; kct = W.rng[2 * N + cell];
     budget = W.budget[cell];
     prim = (budget & BUDGET_PRIM) != 0;   // a spilled slice already used its primary record
     budget &= ~BUDGET_PRIM;
+    inp0 = W.inputs[cell]; inp1 = W.inputs[N + cell]; inp2 = W.inputs[2 * N + cell];
+    dexe = W.executed[cell]; dcop = W.copied[cell]; dgen = W.generation[cell];
+    bonus = W.default_bonus;
+  }
+  if (active && !fresh) {
+    r0 = W.reg[cell]; r1 = W.reg[N + cell]; r2 = W.reg[2 * N + cell];
+    ip = W.head[cell]; rh = W.head[N + cell]; wh = W.head[2 * N + cell]; fh = W.head[3 * N + cell];
+    rl = W.rlabel[cell];
+    cyc = W.cycles[cell]; tu = W.time_used[cell]; gs = W.gest_start[cell];
     errs = W.errors[cell];
     in0 = W.inbuf[cell]; in1 = W.inbuf[N + cell]; in2 = W.inbuf[2 * N + cell];
     intot = W.in_total[cell]; inptr = W.in_ptr[cell];
-    inp0 = W.inputs[cell]; inp1 = W.inputs[N + cell]; inp2 = W.inputs[2 * N + cell];
     outv = W.outbuf[cell]; outtot = W.out_total[cell];
     bonus = W.cur_bonus[cell];
 #pragma unroll
@@ -229,7 +232,7 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
       tc[q] = W.cur_task[(int64_t)q * N + cell];
       nzm |= (tc[q] > 0 ? 1u : 0u) << q;
     }
-    dexe = W.executed[cell]; dcop = W.copied[cell]; dnd = W.num_div[cell]; dgen = W.generation[cell];
+    dnd = W.num_div[cell];
   }
   prim0 = prim;
   __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0), visible to the compiler's waitcnt tracking
@@ -664,7 +667,6 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
           if (ok) {
             okw = 1;
             dexe = exe;                                       // SetLinesExecuted
-            dccop = cop;                                      // SetLinesCopied
             const int nd = dnd + 1;
             // DivideReset / TestDivideReset (main/cPhenotype.cc:824-1000, :1064-1180)
             const double base = (double)calc_size_merit(W, blen, dcop, exe);
@@ -673,9 +675,13 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
             if (W.inherit_merit == 0) merit = base;
             const int gt = tu - gs;
             const double fit = __ddiv_rn(__dmul_rn(base, bon), (double)gt);
-            dmerit = merit;
-            dgt = gt;
-            dfit = fit;
+            // write-only phenotype fields go out now (fire and forget) rather
+            // than being held in registers to the end of the slice
+            st_async_u64(W.merit + cell, (uint64_t)__double_as_longlong(merit));
+            st_async_u64(W.fitness + cell, (uint64_t)__double_as_longlong(fit));
+            st_async_u32(W.gest_time + cell, (uint32_t)gt);
+            st_async_u32(W.child_copied + cell, (uint32_t)cop);   // SetLinesCopied
+            st_async_u32(W.executed + cell, (uint32_t)exe);
             gs = tu;
             dnd = nd;
             const int gen = dgen + 1;
@@ -686,7 +692,7 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
             cyc = 0;
 #pragma unroll
             for (int q = 0; q < AVGPU_NUM_LOGIC_TASKS; q++) {
-              lt[q] = tc[q];
+              st_async_u32(W.last_task + (int64_t)q * N + cell, (uint32_t)tc[q]);
               tc[q] = 0;
             }
             nzm = 0;
@@ -823,7 +829,7 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
     W.reg[cell] = r0; W.reg[N + cell] = r1; W.reg[2 * N + cell] = r2;
     W.head[cell] = ip; W.head[N + cell] = rh; W.head[2 * N + cell] = wh; W.head[3 * N + cell] = fh;
     if (!alive) ctl &= ~CTL_ALIVE;
-    W.ctl[cell] = ctl; W.rlabel[cell] = rl;
+    W.ctl[cell] = ctl & ~CTL_FRESH; W.rlabel[cell] = rl;
     W.mem_size[cell] = M;
     W.cycles[cell] = cyc; W.time_used[cell] = tu; W.gest_start[cell] = gs;
     W.rng[2 * N + cell] = kct;
@@ -835,12 +841,20 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
     W.cur_bonus[cell] = bonus;
 #pragma unroll
     for (int q = 0; q < AVGPU_NUM_LOGIC_TASKS; q++) W.cur_task[(int64_t)q * N + cell] = tc[q];
-    if (didv) {
-      W.executed[cell] = dexe; W.child_copied[cell] = dccop;
-      W.merit[cell] = dmerit; W.fitness[cell] = dfit; W.gest_time[cell] = dgt;
-      W.num_div[cell] = dnd; W.generation[cell] = dgen;
+    // merit, fitness, gestation time, copied / executed sizes and last-task
+    // counts were stored at the divide (st_async)
+    if (didv || fresh) { W.num_div[cell] = dnd; W.generation[cell] = dgen; }
+    if (fresh) {
 #pragma unroll
-      for (int q = 0; q < AVGPU_NUM_LOGIC_TASKS; q++) W.last_task[(int64_t)q * N + cell] = lt[q];
+      for (int q = AVGPU_NUM_LOGIC_TASKS; q < AVGPU_MAX_REACTIONS; q++) {
+        W.cur_task[(int64_t)q * N + cell] = 0;
+        W.last_task[(int64_t)q * N + cell] = 0;
+      }
+      if (!didv) {
+        W.child_copied[cell] = 0;
+#pragma unroll
+        for (int q = 0; q < AVGPU_NUM_LOGIC_TASKS; q++) W.last_task[(int64_t)q * N + cell] = 0;
+      }
     }
     // cur_reaction_count: reset at a divide, counted since (or added to the
     // stored counts when no divide happened in this slice)
@@ -848,8 +862,10 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
     for (int i = 0; i < AVGPU_MAX_REACTIONS; i++) {
       int32_t* p = W.cur_react + (int64_t)i * N + cell;
       if (i < W.n_react) {
-        if (didv) *p = rc[i];
+        if (didv || fresh) *p = rc[i];
         else if (rc[i]) *p += rc[i];
+      } else if (fresh) {
+        *p = 0;
       }
     }
 #pragma unroll
@@ -934,8 +950,10 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
 #endif
 }
 
+// class 0 must keep 2 waves per SIMD (its LDS admits 5 blocks per CU): the
+// second bound caps it at 256 registers (VGPR + AGPR)
 template <int S>
-__global__ __launch_bounds__(64) void k_interpret(const DevWorld* __restrict__ Wp, int cls, int row, int mode,
+__global__ __launch_bounds__(64, (S == CLASS0_SIZE) ? 2 : 1) void k_interpret(const DevWorld* __restrict__ Wp, int cls, int row, int mode,
                                                   int64_t first, int64_t count, int sorted) {
   constexpr int TAB_WORDS = 128 + 64 + 16 + 64 + AVGPU_MAX_REACTIONS * RT_STRIDE + 64;
   __shared__ __attribute__((aligned(16))) uint32_t lds32[64 * (S + 16) / 4 + 2 * AVGPU_STACK_SIZE * 64 + TAB_WORDS];

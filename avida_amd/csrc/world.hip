@@ -116,46 +116,49 @@ __global__ void k_get_states(DevWorld W, int64_t first, int64_t count, avgpu_cpu
   const int64_t c = first + i;
   avgpu_cpu_state s;
   memset(&s, 0, sizeof(s));
+  const bool fresh = (W.ctl[c] & CTL_FRESH) != 0;   // birth values implied (setup_child)
+  if (!fresh) {
   for (int k = 0; k < 3; k++) s.reg[k] = W.reg[k * N + c];
   for (int k = 0; k < 4; k++) s.head[k] = W.head[k * N + c];
   for (int k = 0; k < 2; k++)
     for (int j = 0; j < AVGPU_STACK_SIZE; j++) s.stack[k][j] = W.stack[(k * AVGPU_STACK_SIZE + j) * N + c];
+  }
   const uint32_t ctl = W.ctl[c];
   s.stack_ptr[0] = CTL_SP0(ctl); s.stack_ptr[1] = CTL_SP1(ctl);
   s.cur_stack = (ctl & CTL_CURSTK) ? 1 : 0;
   s.mal_active = (ctl & CTL_MAL) ? 1 : 0;
   s.alive = (ctl & CTL_ALIVE) ? 1 : 0;
-  const uint32_t rl = W.rlabel[c];
+  const uint32_t rl = fresh ? 0u : W.rlabel[c];
   s.read_label_len = rl & 15;
   for (int k = 0; k < (int)(rl & 15); k++) s.read_label[k] = (int8_t)((rl >> (4 + 2 * k)) & 3);
   s.mem_size = W.mem_size[c];
-  s.cpu_cycles_used = W.cycles[c];
-  s.time_used = W.time_used[c];
-  s.gestation_start = W.gest_start[c];
+  s.cpu_cycles_used = fresh ? 0 : W.cycles[c];
+  s.time_used = fresh ? 0 : W.time_used[c];
+  s.gestation_start = fresh ? 0 : W.gest_start[c];
   s.gestation_time = W.gest_time[c];
-  s.num_divides = W.num_div[c];
+  s.num_divides = fresh ? 0 : W.num_div[c];
   s.generation = W.generation[c];
   s.genome_length = W.birth_len[c];
   s.copied_size = W.copied[c];
-  s.child_copied_size = W.child_copied[c];
+  s.child_copied_size = fresh ? 0 : W.child_copied[c];
   s.executed_size = W.executed[c];
   s.max_executed = W.max_exec[c];
   s.birth_length = W.birth_len[c];
-  s.input_ptr = W.in_ptr[c];
-  const int tot = W.in_total[c];
+  s.input_ptr = fresh ? 0 : W.in_ptr[c];
+  const int tot = fresh ? 0 : W.in_total[c];
   for (int k = 0; k < 3; k++) s.input_buf[k] = (k < tot) ? W.inbuf[k * N + c] : 0;
   s.input_total = tot;
-  s.output_total = W.out_total[c];
+  s.output_total = fresh ? 0 : W.out_total[c];
   s.output_buf = s.output_total ? W.outbuf[c] : 0;
   for (int k = 0; k < 3; k++) s.inputs[k] = W.inputs[k * N + c];
-  for (int k = 0; k < AVGPU_MAX_REACTIONS; k++) {
+  for (int k = 0; k < AVGPU_MAX_REACTIONS && !fresh; k++) {
     s.cur_task_count[k] = W.cur_task[k * N + c];
     s.last_task_count[k] = W.last_task[k * N + c];
     s.cur_reaction_count[k] = W.cur_react[k * N + c];
   }
   s.rng_key_lo = W.rng[c]; s.rng_key_hi = W.rng[N + c]; s.rng_counter = W.rng[2 * N + c];
-  s.errors = W.errors[c];
-  s.cur_bonus = W.cur_bonus[c];
+  s.errors = fresh ? 0 : W.errors[c];
+  s.cur_bonus = fresh ? W.default_bonus : W.cur_bonus[c];
   s.merit = W.merit[c];
   s.fitness = W.fitness[c];
   out[i] = s;
@@ -493,9 +496,12 @@ __global__ void k_halo_clear(DevWorld W) {
 }
 
 // ActivateOrganism (main/cPopulation.cc:1320-1340) + SetupOffspring
-// (main/cPhenotype.cc:349-420) of one offspring into cell c by one wave: lane
-// k < 20 clears stack slot k, the rest of the organism's fields are scattered
-// over SoA rows, so each lane stores one of them.
+// (main/cPhenotype.cc:349-420) of one offspring into cell c by one wave.  The
+// organism is marked CTL_FRESH: its zero / default fields (registers, heads,
+// stacks, IO buffers, counters, task and reaction counts, bonus) are implied
+// by the bit instead of stored -- they sit in ~90 SoA rows, one scattered
+// store each -- and its first slice writes them back.  What is stored here,
+// one field per lane: the genome, its length and the phenotype it inherits.
 struct Child {
   int len, gen, ccopied, exec, gest;
   double merit, fitness;
@@ -507,50 +513,23 @@ __device__ __forceinline__ void setup_child(const DevWorld& W, int64_t c, const 
   const int len = b.len;
   uint32_t* dst = reinterpret_cast<uint32_t*>(W.tape + c * TAPE_SLOT);
   for (int w = lane; w < (len + 3) / 4; w += 64) dst[w] = src[w];
-  if (lane < 2 * AVGPU_STACK_SIZE) W.stack[lane * N + c] = 0;
-  if (lane < AVGPU_MAX_REACTIONS) {
-    W.cur_task[lane * N + c] = 0; W.last_task[lane * N + c] = 0; W.cur_react[lane * N + c] = 0;
-  }
   switch (lane) {
-    case 20: W.reg[c] = 0; break;
-    case 21: W.reg[N + c] = 0; break;
-    case 22: W.reg[2 * N + c] = 0; break;
-    case 23: W.inbuf[c] = 0; break;
-    case 24: W.inbuf[N + c] = 0; break;
-    case 25: W.inbuf[2 * N + c] = 0; break;
-    case 26: W.head[c] = 0; break;
-    case 27: W.head[N + c] = 0; break;
-    case 28: W.head[2 * N + c] = 0; break;
-    case 29: W.head[3 * N + c] = 0; break;
-    case 30: W.ctl[c] = CTL_ALIVE; break;
-    case 31: W.rlabel[c] = 0; break;
-    case 32: W.mem_size[c] = len; break;
-    case 33: W.cycles[c] = 0; break;
-    case 34: W.time_used[c] = 0; break;
-    case 35: W.gest_start[c] = 0; break;
-    case 36: {
+    case 0: W.ctl[c] = CTL_ALIVE | CTL_FRESH; break;
+    case 1: W.mem_size[c] = len; break;
+    case 2: {
       int mx = 0;
       if (W.death_method > 0) { mx = W.age_limit; if (W.death_method == 2) mx *= len; if (mx < 1) mx = 1; }
       W.max_exec[c] = mx;
       break; }
-    case 37: W.birth_len[c] = len; break;
-    case 38: W.budget[c] = 0; break;
-    case 39: W.in_total[c] = 0; break;
-    case 40: W.in_ptr[c] = 0; break;
-    case 41: W.outbuf[c] = 0; break;
-    case 42: W.out_total[c] = 0; break;
-    case 43: W.cur_bonus[c] = W.default_bonus; break;
-    case 44: W.merit[c] = b.merit; break;
-    case 45: W.fitness[c] = b.fitness; break;
-    case 46: W.credit[c] = 0.0; break;
-    case 47: W.gest_time[c] = b.gest; break;
-    case 48: W.num_div[c] = 0; break;
-    case 49: W.generation[c] = b.gen; break;
-    case 50: W.copied[c] = b.ccopied; break;
-    case 51: W.child_copied[c] = 0; break;
-    case 52: W.executed[c] = b.exec; break;
-    case 53: W.errors[c] = 0; break;
-    case 54: {
+    case 3: W.birth_len[c] = len; break;
+    case 4: W.merit[c] = b.merit; break;
+    case 5: W.fitness[c] = b.fitness; break;
+    case 6: W.credit[c] = 0.0; break;
+    case 7: W.gest_time[c] = b.gest; break;
+    case 8: W.generation[c] = b.gen; break;
+    case 9: W.copied[c] = b.ccopied; break;
+    case 10: W.executed[c] = b.exec; break;
+    case 11: {
       uint32_t ctr = b.ctr;
       // cEnvironment::SetupInputs random (main/cEnvironment.cc:1268-1271)
       W.inputs[c] = (15 << 24) + (int)rng_below(b.lo, b.hi, ctr, 1u << 24);
@@ -692,8 +671,9 @@ __global__ __launch_bounds__(256) void k_stats_partial(DevWorld W, double* part)
     v[5] = W.fitness[c];   // max
     v[6] = (double)W.generation[c];
     v[7] = (double)W.mem_size[c];
+    if (!(W.ctl[c] & CTL_FRESH))   // a fresh offspring has no last-gestation tasks yet
 #pragma unroll
-    for (int t = 0; t < AVGPU_NUM_LOGIC_TASKS; t++) v[8 + t] = W.last_task[t * W.n + c] > 0 ? 1.0 : 0.0;
+      for (int t = 0; t < AVGPU_NUM_LOGIC_TASKS; t++) v[8 + t] = W.last_task[t * W.n + c] > 0 ? 1.0 : 0.0;
   }
 #pragma unroll
   for (int k = 0; k < NPART; k++) {

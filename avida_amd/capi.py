@@ -213,7 +213,7 @@ def load_product(path=None):
     global _lib
     if path is None and _lib is not None:
         return _lib
-    p = path or LIB_PATH
+    p = path or os.environ.get("AVGPU_DIAG_LIB") or LIB_PATH   # diagnostic builds (tools/)
     if not os.path.exists(p):
         raise RuntimeError(f"{p} missing: run __graft_entry__.build() first")
     lib = C.CDLL(p)

@@ -245,12 +245,20 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
   bool stop = false, spill = false;
   int executed = 0, divides = 0;
 
+  // world scalars the loop uses, read once: through the descriptor pointer
+  // each use was an s_load + lgkmcnt wait inside the loop
+  const double k_size_range = W.size_range;
+  const int k_require_allocate = W.require_allocate, k_alloc_method = W.alloc_method;
+  const uint64_t k_th_copy_mut = W.th_copy_mut;
+  const int k_rand_total = W.rand_total, k_n_ops = W.n_ops, k_n_react = W.n_react;
+  const int k_env_simple = W.env_simple, k_max_label_exe = W.max_label_exe;
+  const uint32_t k_env_react_mask = W.env_react_mask, k_env_once_mask = W.env_once_mask;
   // cInstSet::GetRandomInst (cpu/cInstSet.cc:83-88) from the LDS tables
   auto rand_code = [&]() -> uint8_t {
-    const uint32_t r = rng_below(klo, khi, kct, (uint32_t)W.rand_total);
-    if (W.rand_total <= 256) return rlut[r];
+    const uint32_t r = rng_below(klo, khi, kct, (uint32_t)k_rand_total);
+    if (k_rand_total <= 256) return rlut[r];
     int i = 0;
-    while (i < W.n_ops - 1 && rcum[i] <= (int32_t)r) i++;
+    while (i < k_n_ops - 1 && rcum[i] <= (int32_t)r) i++;
     return rcode[i];
   };
 
@@ -297,12 +305,12 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
         // would this allocation outgrow the LDS slot?  (spill check; the
         // instruction is then executed by the next size class)
         const int cur = M;
-        int alloc = (int)(W.size_range * cur);
+        int alloc = (int)(k_size_range * cur);
         if (alloc > AVGPU_MAX_GENOME - cur) alloc = AVGPU_MAX_GENOME - cur;
         const int nsz = cur + alloc;
-        const bool ok = !(W.require_allocate && (ctl & CTL_MAL)) && alloc >= 1 &&
+        const bool ok = !(k_require_allocate && (ctl & CTL_MAL)) && alloc >= 1 &&
                         nsz <= AVGPU_MAX_GENOME && nsz >= AVGPU_MIN_GENOME &&
-                        alloc <= (int)(cur * W.size_range) && cur <= (int)(alloc * W.size_range);
+                        alloc <= (int)(cur * k_size_range) && cur <= (int)(alloc * k_size_range);
         if (ok && nsz > S) { spill = true; ip = ipa; }
       }
     if (!spill) {
@@ -372,7 +380,7 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
       } else {
         rl = 0;
       }
-      if (mode != AVGPU_MODE_TEST && W.th_copy_mut && rng_p(klo, khi, kct, W.th_copy_mut))
+      if (mode != AVGPU_MODE_TEST && k_th_copy_mut && rng_p(klo, khi, kct, k_th_copy_mut))
         v = rand_code();
       T[wh] = (uint8_t)((T[wh] & TF_EXEC) | TF_COPIED | v);
       rh = head_adjust(rh + 1, M);
@@ -430,29 +438,49 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
         const uint32_t b = num > 1 ? (uint32_t)in1 : 0u;
         const uint32_t c = num > 2 ? (uint32_t)in2 : 0u;
         const uint32_t o = (uint32_t)out;
-        int lo[8];
-        bool bad = false;
+        // logic id (cTaskLib::SetupTests): per input combination p the
+        // output bits at the positions where the inputs spell p must agree
+        // ("ones" / "zeros" seen).  With three inputs and every combination
+        // present -- always, for SetupInputs' 0x0F/0x33/0x55 top bytes -- the
+        // id is the "ones" mask; otherwise the general rule below.
+        uint32_t ones = 0u, zeros = 0u;
 #pragma unroll
         for (int p = 0; p < 8; p++) {
           const uint32_t m = ((p & 1) ? a : ~a) & ((p & 2) ? b : ~b) & ((p & 4) ? c : ~c);
-          const uint32_t v = o & m;
-          lo[p] = (m == 0u) ? -1 : (v == m ? 1 : 0);
-          bad |= (m != 0u) && (v != m) && (v != 0u);
+          ones |= min(o & m, 1u) << p;
+          zeros |= min(~o & m, 1u) << p;
         }
-        if (num < 1) lo[1] = lo[0];
-        if (num < 2) { lo[2] = lo[0]; lo[3] = lo[1]; }
-        if (num < 3) { lo[4] = lo[0]; lo[5] = lo[1]; lo[6] = lo[2]; lo[7] = lo[3]; }
-        int id = 0;
+        uint32_t tmask = 0u;
+        if (num == 3 && (ones | zeros) == 0xFFu) {
+          tmask = (ones & zeros) ? 0u : lut[ones];
+        } else {
+          int lo[8];
+          bool bad = false;
 #pragma unroll
-        for (int p = 0; p < 8; p++) id += lo[p] * (1 << p);
-        const uint32_t tmask = (!bad && id >= 0 && id < 256) ? lut[id] : 0u;
+          for (int p = 0; p < 8; p++) {
+            const uint32_t m = ((p & 1) ? a : ~a) & ((p & 2) ? b : ~b) & ((p & 4) ? c : ~c);
+            const uint32_t v = o & m;
+            lo[p] = (m == 0u) ? -1 : (v == m ? 1 : 0);
+            bad |= (m != 0u) && (v != m) && (v != 0u);
+          }
+          if (num < 1) lo[1] = lo[0];
+          if (num < 2) { lo[2] = lo[0]; lo[3] = lo[1]; }
+          if (num < 3) { lo[4] = lo[0]; lo[5] = lo[1]; lo[6] = lo[2]; lo[7] = lo[3]; }
+          int id = 0;
+#pragma unroll
+          for (int p = 0; p < 8; p++) id += lo[p] * (1 << p);
+          tmask = (!bad && id >= 0 && id < 256) ? lut[id] : 0u;
+        }
+#ifdef AVGPU_ABL_IO
+        tmask = 0u;   // DIAGNOSTIC ablation build only (tools/ablate.sh)
+#endif
         // cEnvironment::TestOutput / TestRequisites / DoProcesses
         // (main/cEnvironment.cc:1314-1406, :1408-1503, :1610-1760)
-        if (tmask && W.env_simple) {
+        if (tmask && k_env_simple) {
           // reaction i rewards task i, requisites at most "max_count=1"
           // (capi.hip avgpu_load_env): the firing set is a bit operation and
           // the bonus factors multiply in reaction order (ascending bits)
-          const uint32_t done = tmask & W.env_react_mask & ~(W.env_once_mask & nzm);
+          const uint32_t done = tmask & k_env_react_mask & ~(k_env_once_mask & nzm);
           if (done) {
             double mult = 1.0, addb = 0.0;
             for (uint32_t d = done; d; d &= d - 1u) {
@@ -473,7 +501,7 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
           double mult = 1.0, addb = 0.0;
 #pragma unroll
           for (int i = 0; i < AVGPU_MAX_REACTIONS; i++) {
-            if (i >= W.n_react) break;
+            if (i >= k_n_react) break;
             const int32_t* rt = rtab + i * RT_STRIDE;         // uniform LDS reads
             const int t = rt[RT_TASK];
             int cnt = 0;
@@ -508,14 +536,14 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
         break; }
       case AVGPU_H_H_ALLOC: {                                 // :3294 Inst_MaxAlloc -> Allocate_Main :1707
         const int cur = M;
-        int alloc = (int)(W.size_range * cur);
+        int alloc = (int)(k_size_range * cur);
         if (alloc > AVGPU_MAX_GENOME - cur) alloc = AVGPU_MAX_GENOME - cur;
         const int nsz = cur + alloc;
-        const bool ok = !(W.require_allocate && (ctl & CTL_MAL)) && alloc >= 1 &&
+        const bool ok = !(k_require_allocate && (ctl & CTL_MAL)) && alloc >= 1 &&
                         nsz <= AVGPU_MAX_GENOME && nsz >= AVGPU_MIN_GENOME &&
-                        alloc <= (int)(cur * W.size_range) && cur <= (int)(alloc * W.size_range);
+                        alloc <= (int)(cur * k_size_range) && cur <= (int)(alloc * k_size_range);
         if (!ok) { errs++; break; }                           // cOrganism::Fault
-        if (W.alloc_method == 2) {
+        if (k_alloc_method == 2) {
           for (int i = cur; i < nsz; i++) T[i] = rand_code();
         } else {
           rq = RQ_FILL; qa = cur; qb = nsz;                   // new sites = op 0 (wave fill below)
@@ -532,8 +560,8 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
         const int child = child_end - div;
         // Divide_CheckViable (cpu/cHardwareBase.cc:140-289): sizes here, the
         // executed / copied line counts in the wave phase below
-        const int min_size = max(AVGPU_MIN_GENOME, (int)(blen / W.size_range));
-        const int max_size = min(AVGPU_MAX_GENOME, (int)(blen * W.size_range));
+        const int min_size = max(AVGPU_MIN_GENOME, (int)(blen / k_size_range));
+        const int max_size = min(AVGPU_MAX_GENOME, (int)(blen * k_size_range));
         bool ok = child >= min_size && child <= max_size && div >= min_size && div <= max_size;
         if (ok && W.cfg_min_genome && (child < W.cfg_min_genome || div < W.cfg_min_genome)) ok = false;
         if (ok && W.cfg_max_genome && (child > W.cfg_max_genome || div > W.cfg_max_genome)) ok = false;
@@ -556,6 +584,9 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
         const uint64_t nl = (cl + K7D) & K80, nh = (ch + K7D) & K80;
         int len = nl ? (int)(__ffsll((long long)nl) - 8) >> 3 : 8 + (nh ? (int)(__ffsll((long long)nh) - 8) >> 3 : 8);
         len = min(len, min(AVGPU_MAX_LABEL, M - base));
+#ifdef AVGPU_ABL_LABEL
+        len = 0;                     // DIAGNOSTIC ablation build only
+#endif
         len = max(len, 0);
         // 2-bit nop codes of bytes 0..7 packed (SWAR), bytes 8, 9 after them
         uint64_t v = cl & 0x0303030303030303ull;
@@ -565,7 +596,7 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
         uint32_t lab = (uint32_t)v | ((uint32_t)(ch & 3u) << 16) | ((uint32_t)((ch >> 8) & 3u) << 18);
         const uint32_t lmask = (1u << (2 * len)) - 1u;
         lab &= lmask;
-        for (int k = 0; k < min(len, W.max_label_exe); k++) T[base + k] |= TF_EXEC;
+        for (int k = 0; k < min(len, k_max_label_exe); k++) T[base + k] |= TF_EXEC;
         ip += len;
         // Rotate(1, NUM_NOPS): per 2-bit digit 0->1, 1->2, 2->0
         const uint32_t dl = lab & 0x55555u, dh = (lab >> 1) & 0x55555u;
@@ -575,7 +606,9 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
           if (packed != rl) ip = head_adjust(ip + 1, M);
           break;
         }
+#ifndef AVGPU_ABL_SEARCHRQ
         if (len > 0) { rq = RQ_SEARCH; qa = len; qb = (int)rot; break; }   // label scan below
+#endif
         r1 = 0;                                               // empty label: found = IP
         r2 = 0;
         fh = head_adjust(ip + 1, M);

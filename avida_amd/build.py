@@ -12,7 +12,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
-SOURCES = ["interp.hip", "world.hip", "capi.hip"]
+SOURCES = ["interp.hip", "world.hip", "resources.hip", "capi.hip"]
 OUT = os.path.join(HERE, "libavida_gpu.so")
 # diagnostic variant with per-phase s_memtime clocks (tools/phase_clocks.py only)
 OUT_CLK = os.path.join(HERE, "libavida_gpu_clk.so")

@@ -52,8 +52,27 @@ class AvgpuReaction(C.Structure):
     _fields_ = [
         ("task", C.c_int32), ("type", C.c_int32), ("value", C.c_double),
         ("max_number", C.c_double), ("min_count", C.c_int32), ("max_count", C.c_int32),
-        ("has_requisite", C.c_int32), ("pad", C.c_int32),
+        ("has_requisite", C.c_int32), ("resource", C.c_int32),
+        ("min_number", C.c_double), ("max_fraction", C.c_double),
+        ("depletable", C.c_int32), ("pad", C.c_int32),
     ]
+
+
+class AvgpuResource(C.Structure):
+    _fields_ = [
+        ("geometry", C.c_int32), ("pad", C.c_int32),
+        ("initial", C.c_double), ("inflow", C.c_double), ("outflow", C.c_double),
+        ("inflow_x1", C.c_int32), ("inflow_x2", C.c_int32), ("inflow_y1", C.c_int32),
+        ("inflow_y2", C.c_int32), ("outflow_x1", C.c_int32), ("outflow_x2", C.c_int32),
+        ("outflow_y1", C.c_int32), ("outflow_y2", C.c_int32),
+        ("xdiffuse", C.c_double), ("ydiffuse", C.c_double), ("xgravity", C.c_double),
+        ("ygravity", C.c_double),
+    ]
+
+
+class AvgpuCellResource(C.Structure):
+    _fields_ = [("resource", C.c_int32), ("cell", C.c_int32), ("initial", C.c_double),
+                ("inflow", C.c_double), ("outflow", C.c_double)]
 
 
 class AvgpuCpuState(C.Structure):
@@ -106,7 +125,7 @@ class AvgpuUpdateStats(C.Structure):
 # C-ABI symbols declared in include/avida_gpu.h (checked by tests/test_capi.py)
 EXPORTED = [
     "avgpu_last_error", "avgpu_cfg_defaults", "avgpu_create", "avgpu_destroy", "avgpu_sync",
-    "avgpu_load_instset", "avgpu_load_env", "avgpu_set_org", "avgpu_set_orgs", "avgpu_kill",
+    "avgpu_load_instset", "avgpu_load_env", "avgpu_load_resources", "avgpu_get_resources", "avgpu_set_org", "avgpu_set_orgs", "avgpu_kill",
     "avgpu_step", "avgpu_run_update", "avgpu_run_updates", "avgpu_update_totals",
     "avgpu_update_run", "avgpu_set_stream", "avgpu_get_states",
     "avgpu_test_genomes", "avgpu_get_stats", "avgpu_stats_vector", "avgpu_set_global_totals",
@@ -162,7 +181,25 @@ def reactions_array(reactions):
         arr[i].task, arr[i].type, arr[i].value = r.task, r.proc_type, r.value
         arr[i].max_number, arr[i].min_count = r.max_number, r.min_count
         arr[i].max_count, arr[i].has_requisite = r.max_count, r.has_requisite
+        arr[i].resource = getattr(r, "resource", 0)   # 1 + index, 0 = infinite
+        arr[i].min_number = getattr(r, "min_number", 0.0)
+        arr[i].max_fraction = getattr(r, "max_fraction", 1.0)
+        arr[i].depletable = getattr(r, "depletable", 1)
     return arr
+
+
+def resources_arrays(resources, cells):
+    """files.Resource / files.CellResource lists -> ctypes arrays"""
+    ra = (AvgpuResource * max(1, len(resources)))()
+    for i, r in enumerate(resources):
+        for f, _ in AvgpuResource._fields_:
+            if f != "pad":
+                setattr(ra[i], f, getattr(r, f))
+    ca = (AvgpuCellResource * max(1, len(cells)))()
+    for i, c in enumerate(cells):
+        ca[i].resource, ca[i].cell = c.resource, c.cell
+        ca[i].initial, ca[i].inflow, ca[i].outflow = c.initial, c.inflow, c.outflow
+    return ra, ca
 
 
 def bind_common(lib, prefix):
@@ -195,6 +232,9 @@ def bind_common(lib, prefix):
         "tile_place": (C.c_int, [V, C.c_int, C.c_int]),
         "tile_finish": (C.c_int, [V, C.POINTER(AvgpuUpdateStats)]),
         "get_stats": (C.c_int, [V, C.POINTER(AvgpuUpdateStats)]),
+        "load_resources": (C.c_int, [V, C.c_int, C.POINTER(AvgpuResource), C.c_int,
+                                     C.POINTER(AvgpuCellResource)]),
+        "get_resources": (C.c_int, [V, C.POINTER(C.c_double), C.POINTER(C.c_double)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, p + name, None)

@@ -60,6 +60,7 @@ struct avgpu_world {
   uint8_t op2code[256];
   int16_t code2op[64];
   bool instset_loaded = false;
+  int res_geom[AVGPU_MAX_RESOURCES] = {};
   bool env_loaded = false;
   // device scratch
   double* d_totals = nullptr;   // [8 + partials]
@@ -121,6 +122,8 @@ int setup_world(avgpu_world* w, int64_t n, bool test_buffers) {
   }
   A(rand_cum, 64); A(rand_code, 64); A(task_lut, 256); A(rand_lut, 256);
   A(react_tab, AVGPU_MAX_REACTIONS * RT_STRIDE); A(task_tab, 32);
+  A(react_res, AVGPU_MAX_REACTIONS * RR_STRIDE); A(res_param, AVGPU_MAX_RESOURCES);
+  A(res_global, AVGPU_MAX_RESOURCES); A(res_cons, AVGPU_MAX_RESOURCES);
   if ((rc = w->alloc(&w->d_W, 1))) return rc;
   const int64_t nb = (n + 255) / 256;
   if ((rc = w->alloc(&w->d_totals, (size_t)(8 + 2 * nb)))) return rc;
@@ -486,6 +489,32 @@ int avgpu_load_env(avgpu_world* w, int nreact, const avgpu_reaction* r) {
     memcpy(&a, t + RT_ADD, 8);
     if (t[RT_TYPE] == AVGPU_PROC_ADD) ttab[16 + i] = a; else ttab[i] = m;
   }
+  // resource-bound processes (cEnvironment::DoProcesses): the general path
+  double rr[AVGPU_MAX_REACTIONS * RR_STRIDE];
+  memset(rr, 0, sizeof(rr));
+  int uses = 0;
+  uint32_t res_seen = 0;
+  for (int i = 0; i < nreact; i++) {
+    const int res = r[i].resource;       // 1 + index, 0 = infinite
+    if (res == 0) continue;
+    if (res < 0 || res > W.n_res) return fail(AVGPU_EINVAL, "reaction names an unknown resource");
+    if (res_seen & (1u << (res - 1)))
+      return fail(AVGPU_EUNSUPPORTED, "a resource consumed by two reactions is not on the GPU path");
+    res_seen |= 1u << (res - 1);
+    double* q = rr + i * RR_STRIDE;
+    q[RR_RES] = (double)res;
+    q[RR_SPATIAL] = w->res_geom[res - 1] != AVGPU_RES_GLOBAL ? 1.0 : 0.0;
+    q[RR_DEPL] = r[i].depletable ? 1.0 : 0.0;
+    q[RR_TYPE] = (double)r[i].type;
+    q[RR_FRAC] = r[i].max_fraction > 1.0 ? 1.0 : r[i].max_fraction;
+    q[RR_MIN] = r[i].min_number;
+    q[RR_MAX] = r[i].max_number;
+    q[RR_VALUE] = r[i].value;
+    uses++;
+  }
+  if (uses) simple = false;
+  W.env_resources = uses ? 1 : 0;
+  HIPCHK(hipMemcpyAsync(W.react_res, rr, sizeof(rr), hipMemcpyHostToDevice, w->stream));
   W.env_simple = simple ? 1 : 0;
   W.env_react_mask = rmask;
   W.env_once_mask = omask;
@@ -564,6 +593,7 @@ int avgpu_update_run(avgpu_world* w, const double* dev_totals, avgpu_update_stat
   if (rc < 0) return rc;
   if (!dev_totals) return fail(AVGPU_EINVAL, "dev_totals is NULL");
   launch_world_pre(w->W, w->stream, dev_totals);
+  w->W.res_first = 0;
   HIPCHK(hipGetLastError());
   rc = interpret(w, AVGPU_MODE_WORLD, 0, w->W.n, true);
   if (rc < 0) return rc;
@@ -748,6 +778,119 @@ int avgpu_set_global_totals(avgpu_world* w, double total_merit, int64_t total_or
   return 0;
 }
 
+// ---- resources (resources.hip; DESIGN.md "Resources") ----
+int avgpu_load_resources(avgpu_world* w, int nres, const avgpu_resource* res, int ncell,
+                         const avgpu_cell_resource* cells) {
+  if (!w || nres < 0 || nres > AVGPU_MAX_RESOURCES || ncell < 0 || (ncell && !cells) || (nres && !res))
+    return fail(AVGPU_EINVAL, "resource arguments");
+  DevWorld& W = w->W;
+  if (W.tiled) return fail(AVGPU_EUNSUPPORTED, "resources on strip tiles are not on the GPU path yet");
+  int nsp = 0;
+  ResParam P[AVGPU_MAX_RESOURCES];
+  double glob[AVGPU_MAX_RESOURCES];
+  memset(P, 0, sizeof(P));
+  memset(glob, 0, sizeof(glob));
+  for (int r = 0; r < nres; r++) {
+    const avgpu_resource& q = res[r];
+    if (q.geometry < 0 || q.geometry > 2) return fail(AVGPU_EINVAL, "resource geometry");
+    if (q.initial < 0 || q.inflow < 0 || q.outflow < 0 || q.outflow > 1)
+      return fail(AVGPU_EINVAL, "resource initial / inflow / outflow out of range");
+    ResParam& p = P[r];
+    p.geometry = q.geometry;
+    p.slot = q.geometry == AVGPU_RES_GLOBAL ? -1 : nsp++;
+    p.in_x1 = q.inflow_x1; p.in_x2 = q.inflow_x2; p.in_y1 = q.inflow_y1; p.in_y2 = q.inflow_y2;
+    p.out_x1 = q.outflow_x1; p.out_x2 = q.outflow_x2; p.out_y1 = q.outflow_y1; p.out_y2 = q.outflow_y2;
+    const double decay = 1.0 - q.outflow;                        // cPopulation.cc:440
+    // Source: amount / cells of the inflow rectangle (cSpatialResCount.cc:341-353)
+    const double boxcells = (double)(p.in_y2 - p.in_y1 + 1) * (double)(p.in_x2 - p.in_x1 + 1) * 1.0;
+    p.in_share = q.inflow / boxcells;
+    p.sink_frac = 1.0 - decay;
+    p.has_sink = (p.out_x1 != AVGPU_RES_NONE && p.out_y1 != AVGPU_RES_NONE &&
+                  p.out_x2 != AVGPU_RES_NONE && p.out_y2 != AVGPU_RES_NONE) ? 1 : 0;
+    p.xdiffuse = q.xdiffuse; p.ydiffuse = q.ydiffuse; p.xgravity = q.xgravity; p.ygravity = q.ygravity;
+    p.flows = (q.xdiffuse != 0.0 || q.ydiffuse != 0.0 || q.xgravity != 0.0 || q.ygravity != 0.0) ? 1 : 0;
+    // precalc tables (cResourceCount.cc:336-345), the reference's own loop
+    const double step_decay = std::pow(decay, 1.0 / 10000.0), step_inflow = q.inflow * (1.0 / 10000.0);
+    double dp = 1.0, ip = 0.0;
+    for (int i = 1; i <= 100; i++) {
+      dp = dp * step_decay;
+      ip = ip * step_decay + step_inflow;
+      if (i == 99) { p.decay99 = dp; p.inflow99 = ip; }
+    }
+    p.decay100 = dp; p.inflow100 = ip;
+    glob[r] = q.geometry == AVGPU_RES_GLOBAL ? q.initial : 0.0;
+    w->res_geom[r] = q.geometry;
+    W.res_spatial_host[r] = q.geometry != AVGPU_RES_GLOBAL;
+    W.res_flows_host[r] = (int8_t)p.flows;
+  }
+  for (int i = 0; i < ncell; i++)
+    if (cells[i].resource < 0 || cells[i].resource >= nres || res[cells[i].resource].geometry == AVGPU_RES_GLOBAL)
+      return fail(AVGPU_EINVAL, "CELL entry names a resource that is not spatial");
+  const int64_t n = W.n;
+  if (nsp) {
+    if (!W.res_amount) {
+      HIPCHK(hipMalloc(&W.res_amount, (size_t)AVGPU_MAX_RESOURCES * n * sizeof(double)));
+      w->allocs.push_back(W.res_amount);
+      HIPCHK(hipMalloc(&W.res_delta, (size_t)n * sizeof(double)));
+      w->allocs.push_back(W.res_delta);
+    }
+    // initial: initial / cells everywhere, then + the CELL initial (Setup, SetCellList)
+    std::vector<double> amt((size_t)nsp * n);
+    for (int r = 0; r < nres; r++) {
+      if (P[r].slot < 0) continue;
+      const double per = res[r].initial / (double)n;
+      for (int64_t c = 0; c < n; c++) amt[(size_t)P[r].slot * n + c] = 0.0 + per;
+    }
+    for (int i = 0; i < ncell; i++) {
+      const int r = cells[i].resource;
+      const int64_t c = cells[i].cell;
+      if (c >= 0 && c < n) {
+        double& a = amt[(size_t)P[r].slot * n + c];
+        a = a + (0.0 + cells[i].initial);
+      }
+    }
+    HIPCHK(hipMemcpyAsync(W.res_amount, amt.data(), amt.size() * sizeof(double), hipMemcpyHostToDevice, w->stream));
+  }
+  if (ncell) {
+    if (W.res_cells) hipFree(W.res_cells);
+    HIPCHK(hipMalloc(&W.res_cells, ncell * sizeof(avgpu_cell_resource)));
+    HIPCHK(hipMemcpyAsync(W.res_cells, cells, ncell * sizeof(avgpu_cell_resource), hipMemcpyHostToDevice, w->stream));
+  }
+  W.n_res = nres;
+  W.n_cellres = ncell;
+  W.res_first = 1;
+  HIPCHK(hipMemcpyAsync(W.res_param, P, sizeof(P), hipMemcpyHostToDevice, w->stream));
+  HIPCHK(hipMemcpyAsync(W.res_global, glob, sizeof(glob), hipMemcpyHostToDevice, w->stream));
+  HIPCHK(hipMemsetAsync(W.res_cons, 0, AVGPU_MAX_RESOURCES * sizeof(unsigned long long), w->stream));
+  HIPCHK(hipStreamSynchronize(w->stream));
+  return 0;
+}
+
+int avgpu_get_resources(avgpu_world* w, double* levels, double* spatial) {
+  if (!w || !levels) return fail(AVGPU_EINVAL, "args");
+  DevWorld& W = w->W;
+  HIPCHK(hipStreamSynchronize(w->stream));
+  double glob[AVGPU_MAX_RESOURCES];
+  ResParam P[AVGPU_MAX_RESOURCES];
+  HIPCHK(hipMemcpy(glob, W.res_global, sizeof(glob), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(P, W.res_param, sizeof(P), hipMemcpyDeviceToHost));
+  std::vector<double> row(W.n);
+  for (int r = 0; r < W.n_res; r++) {
+    if (P[r].slot < 0) {
+      levels[r] = glob[r];
+      if (spatial) memset(spatial + (size_t)r * W.n, 0, W.n * sizeof(double));
+      continue;
+    }
+    HIPCHK(hipMemcpy(row.data(), W.res_amount + (size_t)P[r].slot * W.n, W.n * sizeof(double),
+                     hipMemcpyDeviceToHost));
+    double sum = 0.0;                                   // cStats::PrintResourceData order
+    for (int64_t c = 0; c < W.n; c++) sum += row[c];
+    levels[r] = sum;
+    if (spatial) memcpy(spatial + (size_t)r * W.n, row.data(), W.n * sizeof(double));
+  }
+  return 0;
+}
+
 // ---- strip tiles (DESIGN.md "Multi-GPU") ----
 int avgpu_set_tile(avgpu_world* w, int64_t row0, int64_t arena_bytes) {
   if (!w) return fail(AVGPU_EINVAL, "NULL world");
@@ -815,9 +958,11 @@ int avgpu_tile_partials(avgpu_world* w, double* dev_out) {
 int avgpu_tile_begin(avgpu_world* w, const double* dev_gathered, int ntiles) {
   int rc = tile_ready(w);
   if (rc < 0) return rc;
+  if (w->W.n_res) return fail(AVGPU_EUNSUPPORTED, "resources on strip tiles are not on the GPU path yet");
   if (!dev_gathered || ntiles < 1) return fail(AVGPU_EINVAL, "gathered partials");
   launch_tile_totals(w->W, w->stream, dev_gathered, ntiles, w->d_totals);
   launch_world_pre(w->W, w->stream, w->d_totals);
+  w->W.res_first = 0;
   HIPCHK(hipGetLastError());
   rc = interpret(w, AVGPU_MODE_WORLD, 0, w->W.n, true);
   if (rc < 0) return rc;

@@ -34,6 +34,21 @@
 #define CTL_FRESH 0x800u
 
 #define NUM_CLASSES 4
+// react_res row: resource slot+1 (0 infinite), spatial?, depletable, type, frac, min, max, value
+#define RR_STRIDE 8
+enum { RR_RES = 0, RR_SPATIAL = 1, RR_DEPL = 2, RR_TYPE = 3, RR_FRAC = 4, RR_MIN = 5, RR_MAX = 6, RR_VALUE = 7 };
+#define RES_FIX 4294967296.0   /* global consumption accumulates in units of 2^-32 */
+
+struct ResParam {
+  int32_t geometry, slot;       // slot: row of res_amount (spatial) or -1
+  int32_t in_x1, in_x2, in_y1, in_y2, out_x1, out_x2, out_y1, out_y2;
+  double in_share;              // inflow / cells of the inflow box (cSpatialResCount::Source)
+  double sink_frac;             // 1 - decay, decay = 1 - outflow (cPopulation.cc:440, Sink)
+  double xdiffuse, ydiffuse, xgravity, ygravity;
+  double decay100, inflow100;   // decay_precalc / inflow_precalc at PRECALC_DISTANCE (global)
+  double decay99, inflow99;     // ... at 99 steps (the last block of update 0's 9999 steps)
+  int32_t flows, has_sink;      // FlowAll does anything; the outflow box is set
+};
 #define NUM_LISTS 7
 #define RT_STRIDE 12
 enum { RT_TASK = 0, RT_TYPE = 1, RT_MIN = 2, RT_MAX = 3, RT_HASREQ = 4, RT_USED = 5, RT_MULT = 6, RT_ADD = 8 };
@@ -135,6 +150,18 @@ struct DevWorld {
   uint32_t env_react_mask;   // tasks with a reaction
   uint32_t env_once_mask;    // tasks whose reaction has max_count 1
   double* task_tab;          // [32]: bonus factor of task t's reaction, then its addend
+  // ---- resources (resources.hip; DESIGN.md "Resources") ----
+  int32_t n_res, n_cellres, env_resources;   // env_resources: some reaction consumes a resource
+  struct ResParam* res_param;   // [AVGPU_MAX_RESOURCES]
+  double* res_amount;           // [n_spatial][n] spatial amounts (row = ResParam::slot)
+  double* res_delta;            // [n] rate scratch of the spatial step
+  double* res_global;           // [AVGPU_MAX_RESOURCES] global levels, fixed during an update
+  unsigned long long* res_cons; // [AVGPU_MAX_RESOURCES] global consumption of the update, 2^-32 units
+  avgpu_cell_resource* res_cells; // [n_cellres] CELL entries (cell ids are global)
+  double* react_res;            // [AVGPU_MAX_REACTIONS][RR_STRIDE] resource-bound process settings
+  int8_t res_spatial_host[AVGPU_MAX_RESOURCES];   // host-side launch flags
+  int8_t res_flows_host[AVGPU_MAX_RESOURCES];
+  int8_t res_first;             // host: the next update is the first since the load
   uint8_t fill_code;   // code of op 0 (new sites on allocate)
   // config scalars
   int32_t world_x, world_y, geometry;
@@ -286,6 +313,18 @@ __device__ __forceinline__ uint8_t random_code(const DevWorld& W, uint32_t lo, u
   return W.rand_code[i];
 }
 
+// 2^x from IEEE adds / multiplies only (Horner on the Taylor series of
+// e^(f ln2), f in [0,1), then an exact scale by 2^n): the same bits on the
+// device and in the oracle (oracle/oracle.cc det_exp2); within 1 ulp of
+// pow(2, x) (cEnvironment::DoProcesses PROCTYPE_POW, main/cEnvironment.cc:1752)
+__device__ __forceinline__ double det_exp2(double x) {
+  const double n = floor(x);
+  const double t = __dmul_rn(__dsub_rn(x, n), 0.6931471805599453094);
+  double y = 1.0;
+  for (int k = 22; k >= 1; k--) y = __dadd_rn(1.0, __dmul_rn(y, __ddiv_rn(t, (double)k)));
+  return ldexp(y, (int)n);
+}
+
 // CalcSizeMerit (main/cPhenotype.cc:1760-1816)
 __device__ __forceinline__ int calc_size_merit(const DevWorld& W, int glen, int copied, int exe) {
   int s;
@@ -344,6 +383,8 @@ void launch_interpret_classes(const DevWorld& W, const DevWorld* dW, int mode, h
 // SORT_WIN cells, so that a wave's 64 organisms get similar time slices
 #define SORT_WIN 2048
 void launch_world_pre(const DevWorld& W, hipStream_t s, const double* d_totals);
+void launch_resources_begin(const DevWorld& W, hipStream_t s);
+void launch_resources_end(const DevWorld& W, hipStream_t s);
 void launch_world_post(const DevWorld& W, hipStream_t s, double* d_stats);
 void launch_classify_uniform(const DevWorld& W, hipStream_t s, int64_t first, int64_t count,
                              const int32_t* d_budget, int32_t uniform);

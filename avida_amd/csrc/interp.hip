@@ -252,6 +252,7 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
   const uint64_t k_th_copy_mut = W.th_copy_mut;
   const int k_rand_total = W.rand_total, k_n_ops = W.n_ops, k_n_react = W.n_react;
   const int k_env_simple = W.env_simple, k_max_label_exe = W.max_label_exe;
+  const int k_env_resources = W.env_resources;
   const uint32_t k_env_react_mask = W.env_react_mask, k_env_once_mask = W.env_once_mask;
   // cInstSet::GetRandomInst (cpu/cInstSet.cc:83-88) from the LDS tables
   auto rand_code = [&]() -> uint8_t {
@@ -510,12 +511,38 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
             const bool fire = rt[RT_USED] && ((tmask >> t) & 1u) &&
                               !(rt[RT_HASREQ] && (cnt < rt[RT_MIN] || cnt >= rt[RT_MAX]));
             if (fire) {
-              done |= 1u << t;
-              if (rt[RT_TYPE] == AVGPU_PROC_ADD)
-                addb = __dadd_rn(addb, *reinterpret_cast<const double*>(rt + RT_ADD));
-              else
-                mult = __dmul_rn(mult, *reinterpret_cast<const double*>(rt + RT_MULT));
-              rc[i]++;
+              done |= 1u << t;                                // MarkTask precedes the processes
+              const double* rr = W.react_res + i * RR_STRIDE; // uniform (scalar) loads
+              if (!k_env_resources || rr[RR_RES] == 0.0) {    // infinite resource
+                if (rt[RT_TYPE] == AVGPU_PROC_ADD)
+                  addb = __dadd_rn(addb, *reinterpret_cast<const double*>(rt + RT_ADD));
+                else
+                  mult = __dmul_rn(mult, *reinterpret_cast<const double*>(rt + RT_MULT));
+                rc[i]++;
+              } else {
+                // cEnvironment::DoProcesses finite resource (main/cEnvironment.cc:1660-1724):
+                // the organism's own cell (spatial) or the update's global level
+                const int slot = (int)rr[RR_RES] - 1;
+                const bool spatial = rr[RR_SPATIAL] != 0.0;
+                double* cellp = W.res_amount + (int64_t)slot * N + cell;
+                const double level = spatial ? *cellp : W.res_global[slot];
+                double consumed = (level == 0.0) ? 0.0 : __dmul_rn(level, rr[RR_FRAC]);
+                if (consumed > rr[RR_MAX]) consumed = rr[RR_MAX];
+                if (consumed < rr[RR_MIN]) consumed = 0.0;
+                if (consumed != 0.0) {
+                  consumed = fmin(consumed, level);
+                  if (rr[RR_DEPL] != 0.0) {
+                    if (spatial) *cellp = __dsub_rn(level, consumed);   // ModifyCell: applied at once
+                    else atomicAdd(W.res_cons + slot, (unsigned long long)__dmul_rn(consumed, RES_FIX));
+                  }
+                  const double bon = __dmul_rn(consumed, rr[RR_VALUE]);
+                  const int ty = (int)rr[RR_TYPE];
+                  if (ty == AVGPU_PROC_ADD) addb = __dadd_rn(addb, bon);
+                  else if (ty == AVGPU_PROC_MULT) mult = __dmul_rn(mult, bon);
+                  else mult = __dmul_rn(mult, det_exp2(bon));
+                  rc[i]++;
+                }
+              }
             }
           }
           if (done) {

@@ -781,6 +781,7 @@ void launch_merit_total(const DevWorld& W, hipStream_t s, double* totals, double
 }
 
 void launch_world_pre(const DevWorld& W, hipStream_t s, const double* totals) {
+  launch_resources_begin(W, s);   // ProcessPreUpdate + the update's first DoUpdates
   hipMemsetAsync(W.counters, 0, sizeof(unsigned long long) * NSHARD * CNT_STRIDE, s);
   hipMemsetAsync(W.b_count, 0, 2 * sizeof(int32_t), s);
   hipMemsetAsync(W.class_count, 0, sizeof(int32_t) * 8, s);
@@ -800,6 +801,7 @@ static unsigned activate_grid(const DevWorld& W) { return (unsigned)std::min<int
 static unsigned place_grid(const DevWorld& W) { return (unsigned)std::min<int64_t>(nblk(W.rcap, 256), 2048); }
 
 void launch_world_post(const DevWorld& W, hipStream_t s, double* stats) {
+  launch_resources_end(W, s);
   const unsigned bb = place_grid(W);
   hipLaunchKernelGGL(k_occ_init, dim3(nblk(W.n, 256)), dim3(256), 0, s, W);
   for (int round = 0; round < 4; round++) {

@@ -116,26 +116,150 @@ def read_instset(path: str) -> InstSet:
 class Reaction:
     name: str
     task: int
-    proc_type: int = 2
+    proc_type: int = 0           # cReactionProcess default PROCTYPE_ADD (main/cReactionProcess.h:73-88)
     value: float = 1.0
     max_number: float = 1.0
     min_count: int = 0
     max_count: int = INT32_MAX
     has_requisite: int = 0
+    resource: int = 0            # 1 + resource index, 0 = infinite
+    min_number: float = 0.0
+    max_fraction: float = 1.0
+    depletable: int = 1
+
+
+RES_NONE = -99                   # cResource::NONE
+
+
+@dataclass
+class Resource:
+    """RESOURCE name:... (main/cEnvironment.cc:474-661; defaults main/cResource.cc:44-64)"""
+    name: str
+    geometry: int = 0            # 0 global, 1 grid, 2 torus
+    initial: float = 0.0
+    inflow: float = 0.0
+    outflow: float = 0.0
+    inflow_x1: int = RES_NONE
+    inflow_x2: int = RES_NONE
+    inflow_y1: int = RES_NONE
+    inflow_y2: int = RES_NONE
+    outflow_x1: int = RES_NONE
+    outflow_x2: int = RES_NONE
+    outflow_y1: int = RES_NONE
+    outflow_y2: int = RES_NONE
+    xdiffuse: float = 1.0
+    ydiffuse: float = 1.0
+    xgravity: float = 0.0
+    ygravity: float = 0.0
+
+
+@dataclass
+class CellResource:
+    resource: int
+    cell: int
+    initial: float = 0.0
+    inflow: float = 0.0
+    outflow: float = 0.0
+
+
+class Environment(list):
+    """The REACTION list (what avgpu_load_env takes) plus .resources / .cells."""
+    def __init__(self):
+        super().__init__()
+        self.resources = []
+        self.cells = []
+
+
+def _cell_list(spec):
+    """cStringUtil::ReturnArray: comma separated ids and a..b ranges"""
+    out = []
+    for part in spec.split(","):
+        if ".." in part:
+            a, b = part.split("..")
+            out.extend(range(int(a), int(b) + 1))
+        elif part:
+            out.append(int(part))
+    return out
+
+
+def _parse_resource(tok, env, geometry_names={"global": 0, "grid": 1, "torus": 2}):
+    name, _, rest = tok.partition(":")
+    res = next((r for r in env.resources if r.name == name), None)
+    if res is None:
+        res = Resource(name)
+        env.resources.append(res)
+    keys = {"inflowx": "inflow_x1", "inflowx1": "inflow_x1", "inflowx2": "inflow_x2",
+            "inflowy": "inflow_y1", "inflowy1": "inflow_y1", "inflowy2": "inflow_y2",
+            "outflowx": "outflow_x1", "outflowx1": "outflow_x1", "outflowx2": "outflow_x2",
+            "outflowy": "outflow_y1", "outflowy1": "outflow_y1", "outflowy2": "outflow_y2"}
+    for kv in rest.split(":"):
+        if not kv:
+            continue
+        k, _, v = kv.partition("=")
+        k = k.lower()
+        if k in ("inflow", "outflow", "initial", "xdiffuse", "ydiffuse", "xgravity", "ygravity"):
+            setattr(res, k, float(v))
+        elif k == "geometry":
+            if v.lower() not in geometry_names:
+                raise ValueError(f"resource geometry {v!r} not supported on this path")
+            res.geometry = geometry_names[v.lower()]
+        elif k in keys:
+            setattr(res, keys[k], int(v))
+        else:
+            raise ValueError(f"resource setting {k!r} not supported on this path")
+    # one-point boxes (main/cEnvironment.cc:636-657)
+    if res.inflow_x1 >= 0 and res.inflow_x2 == RES_NONE:
+        res.inflow_x2 = res.inflow_x1
+    if res.inflow_y1 >= 0 and res.inflow_y2 == RES_NONE:
+        res.inflow_y2 = res.inflow_y1
+    if res.outflow_x1 > 0 and res.outflow_x2 == RES_NONE:
+        res.outflow_x2 = res.outflow_x1
+    if res.outflow_y1 > 0 and res.outflow_y2 == RES_NONE:
+        res.outflow_y2 = res.outflow_y1
+
+
+def _parse_cell(tok, env):
+    """CELL name:cells[:initial=..:inflow=..:outflow=..] (main/cEnvironment.cc:663-755)"""
+    parts = tok.split(":")
+    name, cells = parts[0], _cell_list(parts[1])
+    idx = next((i for i, r in enumerate(env.resources) if r.name == name), None)
+    if idx is None:
+        env.resources.append(Resource(name, geometry=1, xdiffuse=0.0, ydiffuse=0.0))
+        idx = len(env.resources) - 1
+    vals = {"initial": 0.0, "inflow": 0.0, "outflow": 0.0}
+    for kv in parts[2:]:
+        k, _, v = kv.partition("=")
+        if k not in vals:
+            raise ValueError(f"CELL setting {k!r} unknown")
+        vals[k] = float(v)
+    for c in cells:
+        old = next((x for x in env.cells if x.resource == idx and x.cell == c), None)
+        if old:
+            old.initial, old.inflow, old.outflow = vals["initial"], vals["inflow"], vals["outflow"]
+        else:
+            env.cells.append(CellResource(idx, c, **vals))
 
 
 def read_environment(path: str):
-    """REACTION name task process:... requisite:... (main/cEnvironment.cc:1185-1211).
-
-    RESOURCE/CELL/GRID lines belong to the resource subsystem (next row of
-    SURVEY §8f) and are rejected loudly rather than ignored."""
-    out = []
+    """REACTION name task process:... requisite:... (main/cEnvironment.cc:1185-1211),
+    RESOURCE and CELL lines (:474-755).  Returns an Environment (a list of
+    Reaction with .resources and .cells)."""
+    out = Environment()
     with open(path) as f:
-        for raw in f:
+        text = re.sub(r"\\[ \t]*\r?\n[ \t]*", "", f.read())   # "\" joins the next line
+    for raw in text.splitlines():
             line = _strip(raw)
             if not line:
                 continue
             toks = line.split()
+            if toks[0] == "RESOURCE":
+                for tok in toks[1:]:
+                    _parse_resource(tok, out)
+                continue
+            if toks[0] == "CELL":
+                for tok in toks[1:]:
+                    _parse_cell(tok, out)
+                continue
             if toks[0] != "REACTION":
                 raise ValueError(f"environment keyword {toks[0]} not supported on this path")
             name, task = toks[1], toks[2].split(":")[0]
@@ -152,8 +276,20 @@ def read_environment(path: str):
                         r.value = float(kv["value"])
                     if "max" in kv:
                         r.max_number = float(kv["max"])
+                    if "min" in kv:
+                        r.min_number = float(kv["min"])
+                    if "frac" in kv:
+                        r.max_fraction = min(1.0, float(kv["frac"]))
+                    if "depletable" in kv:
+                        r.depletable = int(kv["depletable"])
                     if "resource" in kv and kv["resource"] not in ("none", ""):
-                        raise ValueError("resource-bound processes are not on this path yet")
+                        names = [x.name for x in out.resources]
+                        if kv["resource"] not in names:
+                            raise ValueError(f"unknown resource {kv['resource']!r}")
+                        r.resource = 1 + names.index(kv["resource"])
+                    for k in kv:
+                        if k not in ("type", "value", "max", "min", "frac", "depletable", "resource"):
+                            raise ValueError(f"process setting {k!r} not supported on this path")
                 elif kind == "requisite":
                     r.has_requisite = 1
                     if "max_count" in kv:

@@ -142,8 +142,8 @@ typedef struct avgpu_cfg {
   uint64_t seed;                   /* RANDOM_SEED (counter-RNG key) */
 } avgpu_cfg;
 
-/* One REACTION line of environment.cfg (main/cEnvironment.cc:1185-1211),
- * infinite-resource process on a logic-9 task. */
+/* One REACTION line of environment.cfg (main/cEnvironment.cc:1185-1211,
+ * process settings :147-300) on a logic-9 task. */
 typedef struct avgpu_reaction {
   int32_t task;          /* avgpu_task */
   int32_t type;          /* avgpu_proctype */
@@ -152,8 +152,31 @@ typedef struct avgpu_reaction {
   int32_t min_count;     /* requisite:min_count (default 0) */
   int32_t max_count;     /* requisite:max_count (INT32_MAX when absent) */
   int32_t has_requisite; /* 0: TestRequisites returns !on_divide */
+  int32_t resource;      /* process:resource: 1 + index into avgpu_load_resources, 0 = infinite */
+  double min_number;     /* process:min (default 0.0) */
+  double max_fraction;   /* process:frac (default 1.0, capped at 1) */
+  int32_t depletable;    /* process:depletable (default 1) */
   int32_t pad;
 } avgpu_reaction;
+
+/* One RESOURCE of environment.cfg (main/cEnvironment.cc:474-661; dynamics
+ * main/cResourceCount.cc:207-358, :757-880, main/cSpatialResCount.cc:101-437). */
+enum avgpu_res_geometry { AVGPU_RES_GLOBAL = 0, AVGPU_RES_GRID = 1, AVGPU_RES_TORUS = 2 };
+#define AVGPU_RES_NONE (-99)   /* cResource::NONE */
+#define AVGPU_MAX_RESOURCES 16
+typedef struct avgpu_resource {
+  int32_t geometry;      /* avgpu_res_geometry */
+  int32_t pad;
+  double initial, inflow, outflow;
+  int32_t inflow_x1, inflow_x2, inflow_y1, inflow_y2;     /* AVGPU_RES_NONE when absent */
+  int32_t outflow_x1, outflow_x2, outflow_y1, outflow_y2;
+  double xdiffuse, ydiffuse, xgravity, ygravity;
+} avgpu_resource;
+/* One cell of a CELL line (main/cEnvironment.cc:663-755). */
+typedef struct avgpu_cell_resource {
+  int32_t resource, cell;
+  double initial, inflow, outflow;
+} avgpu_cell_resource;
 
 /* Architectural + phenotype state of one organism: the tuple a
  * cHardwareStatusPrinter trace shows (cpu/cHardwareCPU.cc:1111-1169) plus the
@@ -259,6 +282,23 @@ int avgpu_load_instset(avgpu_world* w, int n, const uint8_t* handler_id,
                        const int32_t* redundancy);
 /* cEnvironment::Load REACTION lines (main/cEnvironment.cc:1185-1211). */
 int avgpu_load_env(avgpu_world* w, int nreact, const avgpu_reaction* reactions);
+/* RESOURCE / CELL lines: cPopulation's resource setup (main/cPopulation.cc:
+ * 407-480 -> cResourceCount::Setup).  Call before avgpu_load_env when its
+ * reactions name resources.  Update semantics (DESIGN.md "Resources"): at the
+ * start of every update the spatial resources take one step of inflow /
+ * outflow / diffusion (cSpatialResCount::Source, Sink, CellInflow,
+ * CellOutflow, FlowAll, StateAll) and the global ones one update of decay +
+ * inflow (DoNonSpatialUpdates over 1/UPDATE_STEP steps).  The first update
+ * after this call is the reference's update 0: no spatial step, and 9999
+ * global steps (its update_time sums to just under 1.0).  Organisms consume
+ * from their own cell immediately and from global resources at the level the
+ * update started with (the update's consumption is subtracted at its end). */
+int avgpu_load_resources(avgpu_world* w, int nres, const avgpu_resource* res, int ncell,
+                         const avgpu_cell_resource* cells);
+/* current levels: global[nres] (spatial resources: sum over cells, like
+ * cStats::PrintResourceData main/cStats.cc:1551-1579); spatial (optional)
+ * [nres][cells], zero rows for global resources */
+int avgpu_get_resources(avgpu_world* w, double* levels, double* spatial);
 
 /* ---- population --------------------------------------------------------- */
 /* cPopulation::Inject / ActivateOrganism (main/cPopulation.cc:1320-1340) +

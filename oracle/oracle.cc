@@ -219,6 +219,14 @@ struct World {
   std::vector<uint64_t> prio;
   std::vector<int8_t> bstate;     // 0 pending, 1+k placed in round k, -1 failed
   int64_t t_insts = 0, t_deaths = 0, t_divides = 0, t_slices = 0, t_born = 0, t_dropped = 0;
+  // resources (avgpu_load_resources): literal restatement of cResourceCount /
+  // cSpatialResCount, stepped once per update
+  std::vector<avgpu_resource> res;
+  std::vector<avgpu_cell_resource> res_cells;
+  std::vector<std::vector<double>> res_amount, res_delta;   // spatial grids (empty for global)
+  std::vector<double> res_global, res_decay100, res_inflow100, res_decay99, res_inflow99;
+  bool res_first = false;   // the first update after the load: no spatial step, 9999 global steps
+  std::vector<uint64_t> res_cons;
 };
 
 thread_local std::string g_err;
@@ -235,11 +243,23 @@ static inline int adjust(int pos, int size) {
 }
 static inline int wrap_add(int a, int b) { return (int)((uint32_t)a + (uint32_t)b); }
 
+// 2^x from IEEE adds / multiplies only (the device's det_exp2, device.h):
+// cEnvironment::DoProcesses PROCTYPE_POW (main/cEnvironment.cc:1752) uses
+// pow(2, bonus); this restatement is within 1 ulp of it and identical on both sides.
+static double det_exp2(double x) {
+  const double n = std::floor(x);
+  const double t = (x - n) * 0.6931471805599453094;
+  double y = 1.0;
+  for (int k = 22; k >= 1; k--) y = 1.0 + y * (t / (double)k);
+  return std::ldexp(y, (int)n);
+}
+
 struct Exec {
   World& w;
   Org& o;
   int mode;
   bool stop = false;   // TEST mode: gestation finished
+  int64_t cur_cell = -1;  // the organism's cell (spatial resources)
 
   int size() const { return (int)o.mem.size(); }
   // cHeadCPU::GetNextInst (cpu/cHeadCPU.h:167-170)
@@ -540,11 +560,35 @@ struct Exec {
         if (task_cnt >= r.max_count) continue;
       }
       if (id < 0 || !task_done(r.task, id)) continue;
-      done[r.task] = true;
+      done[r.task] = true;                          // MarkTask precedes DoProcesses
       any = true;
-      if (r.type == AVGPU_PROC_POW) mult *= w.react[i].mult;
-      else if (r.type == AVGPU_PROC_MULT) mult *= w.react[i].mult;
-      else add += w.react[i].add;
+      if (r.resource == 0 || mode == AVGPU_MODE_TEST) {   // infinite (the test CPU: no resource grid)
+        if (r.type == AVGPU_PROC_POW) mult *= w.react[i].mult;
+        else if (r.type == AVGPU_PROC_MULT) mult *= w.react[i].mult;
+        else add += w.react[i].add;
+        o.cur_react[i]++;
+        continue;
+      }
+      // cEnvironment::DoProcesses, finite resource (main/cEnvironment.cc:1660-1724)
+      const int res = r.resource - 1;
+      const bool spatial = w.res[res].geometry != AVGPU_RES_GLOBAL;
+      const double level = spatial ? w.res_amount[res][cur_cell] : w.res_global[res];
+      double consumed;
+      if (level == 0) consumed = 0;
+      else consumed = level * std::min(r.max_fraction, 1.0);
+      if (consumed > r.max_number) consumed = r.max_number;
+      consumed = consumed * 1.0 * 1.0;              // task quality, plasticity modifier
+      if (consumed < r.min_number) consumed = 0.0;
+      if (consumed == 0.0) continue;
+      consumed = std::min(consumed, level);
+      if (r.depletable) {
+        if (spatial) w.res_amount[res][cur_cell] = level + (-consumed);   // ModifyCell: Rate + State
+        else w.res_cons[res] += (uint64_t)(consumed * 4294967296.0);
+      }
+      const double bonus = consumed * r.value;
+      if (r.type == AVGPU_PROC_ADD) add += bonus;
+      else if (r.type == AVGPU_PROC_MULT) mult *= bonus;
+      else mult *= det_exp2(bonus);
       o.cur_react[i]++;
     }
     if (!any) return;
@@ -595,6 +639,7 @@ struct Exec {
   // One SingleProcess cycle (cpu/cHardwareCPU.cc:908-1058), single thread,
   // no costs / promoters / speculation.  Returns true if the instruction ran.
   void single_process(int64_t cell) {
+    cur_cell = cell;
     o.cpu_cycles_used++;
     o.time_used++;
     o.advance_ip = true;
@@ -876,6 +921,65 @@ int orc_load_instset(void* h, int n, const uint8_t* handler_id, const int32_t* r
   return 0;
 }
 
+int orc_load_resources(void* h, int nres, const avgpu_resource* res, int ncell,
+                       const avgpu_cell_resource* cells) {
+  World& w = *(World*)h;
+  if (nres < 0 || nres > AVGPU_MAX_RESOURCES) return fail(AVGPU_EINVAL, "resource count");
+  if (w.tiled) return fail(AVGPU_EUNSUPPORTED, "resources on strip tiles");
+  const int64_t n = w.ncells;
+  w.res.assign(res, res + nres);
+  w.res_cells.assign(cells, cells + ncell);
+  w.res_amount.assign(nres, {});
+  w.res_delta.assign(nres, {});
+  w.res_global.assign(nres, 0.0);
+  w.res_decay100.assign(nres, 1.0);
+  w.res_inflow100.assign(nres, 0.0);
+  w.res_decay99.assign(nres, 1.0);
+  w.res_inflow99.assign(nres, 0.0);
+  w.res_cons.assign(nres, 0);
+  w.res_first = true;
+  for (int r = 0; r < nres; r++) {
+    const avgpu_resource& q = res[r];
+    // decay_precalc / inflow_precalc (main/cResourceCount.cc:336-345)
+    const double decay = 1.0 - q.outflow;
+    const double step_decay = std::pow(decay, 1.0 / 10000.0), step_inflow = q.inflow * (1.0 / 10000.0);
+    double dp = 1.0, ip = 0.0;
+    for (int i = 1; i <= 100; i++) {
+      dp = dp * step_decay;
+      ip = ip * step_decay + step_inflow;
+      if (i == 99) { w.res_decay99[r] = dp; w.res_inflow99[r] = ip; }
+    }
+    w.res_decay100[r] = dp;
+    w.res_inflow100[r] = ip;
+    if (q.geometry == AVGPU_RES_GLOBAL) { w.res_global[r] = q.initial; continue; }
+    // Setup: RateAll(initial / size) + StateAll (cResourceCount.cc:323-328)
+    w.res_amount[r].assign(n, 0.0 + q.initial / (double)n);
+    w.res_delta[r].assign(n, 0.0);
+  }
+  for (int i = 0; i < ncell; i++) {   // SetCellList: Rate + State (cSpatialResCount.cc:216-231)
+    const auto& c = cells[i];
+    if (c.cell >= 0 && c.cell < n) w.res_amount[c.resource][c.cell] += (0.0 + c.initial);
+  }
+  return 0;
+}
+
+int orc_get_resources(void* h, double* levels, double* spatial) {
+  World& w = *(World*)h;
+  const int64_t n = w.ncells;
+  for (size_t r = 0; r < w.res.size(); r++) {
+    if (w.res[r].geometry == AVGPU_RES_GLOBAL) {
+      levels[r] = w.res_global[r];
+      if (spatial) std::fill(spatial + r * n, spatial + (r + 1) * n, 0.0);
+      continue;
+    }
+    double sum = 0.0;
+    for (int64_t c = 0; c < n; c++) sum += w.res_amount[r][c];
+    levels[r] = sum;
+    if (spatial) std::copy(w.res_amount[r].begin(), w.res_amount[r].end(), spatial + r * n);
+  }
+  return 0;
+}
+
 int orc_load_env(void* h, int n, const avgpu_reaction* r) {
   World& w = *(World*)h;
   w.react.clear();
@@ -998,6 +1102,122 @@ int orc_test_genomes(void* h, int n, const uint8_t* genomes, const int32_t* lens
 // ---------------------------------------------------------------------------
 // Batch-synchronous world update: the exact semantics the device implements
 // (DESIGN.md "Update semantics"): allot -> interpret -> place births -> stats.
+static int amod(int x, int y) { x %= y; return x < 0 ? x + y : x; }   // AvidaTools::Mod
+
+// FlowMatter (main/cResourceCount.cc:40-110)
+static void flow_matter(double a1, double a2, double& d1, double& d2, const avgpu_resource& r,
+                        int xdist, int ydist, double dist) {
+  double diff, flowamt, xgravity, xdiffuse, ygravity, ydiffuse;
+  diff = (a1 - a2);
+  if (xdist != 0) {
+    if (((xdist > 0) && (r.xgravity > 0.0)) || ((xdist < 0) && (r.xgravity < 0.0)))
+      xgravity = a1 * std::fabs(r.xgravity) / 3.0;
+    else
+      xgravity = -a2 * std::fabs(r.xgravity) / 3.0;
+    xdiffuse = r.xdiffuse * diff / 16.0;
+  } else {
+    xdiffuse = 0.0;
+    xgravity = 0.0;
+  }
+  if (ydist != 0) {
+    if (((ydist > 0) && (r.ygravity > 0.0)) || ((ydist < 0) && (r.ygravity < 0.0)))
+      ygravity = a1 * std::fabs(r.ygravity) / 3.0;
+    else
+      ygravity = -a2 * std::fabs(r.ygravity) / 3.0;
+    ydiffuse = r.ydiffuse * diff / 16.0;
+  } else {
+    ydiffuse = 0.0;
+    ygravity = 0.0;
+  }
+  flowamt = ((xdiffuse + ydiffuse + xgravity + ygravity) /
+             (std::fabs(xdist * 1.0) + std::fabs(ydist * 1.0))) / dist;
+  d1 -= flowamt;
+  d2 += flowamt;
+}
+
+// one update of resources at its start (cPopulation::ProcessPreUpdate + the
+// first DoUpdates: DoSpatialUpdates main/cResourceCount.cc:830-846 with
+// Source / Sink / CellInflow / CellOutflow / FlowAll / StateAll of
+// main/cSpatialResCount.cc, and DoNonSpatialUpdates :814-827).
+// Update 0 has no spatial step (m_spatial_update == m_last_updated == 0,
+// :797) and 9999 global steps: the update_time the steps of update 0 add up
+// to falls just short of 1.0, so (int)(update_time / UPDATE_STEP) is 9999
+// (:780) and the remainder carries, making every later update 10000 steps.
+// Pinned by tests/golden/spatial_res_100u (test_resources.py).
+static void res_begin(World& w) {
+  const int X = w.cfg.world_x, Y = w.cfg.world_y;
+  const int64_t n = w.ncells;
+  const bool first = w.res_first;
+  w.res_first = false;
+  for (size_t r = 0; r < w.res.size(); r++) {
+    const avgpu_resource& q = w.res[r];
+    if (q.geometry == AVGPU_RES_GLOBAL) {
+      double R = w.res_global[r];
+      int steps = first ? 9999 : 10000;
+      while (steps > 100) { R *= w.res_decay100[r]; R += w.res_inflow100[r]; steps -= 100; }
+      if (steps == 100) { R *= w.res_decay100[r]; R += w.res_inflow100[r]; }
+      else { R *= w.res_decay99[r]; R += w.res_inflow99[r]; }
+      w.res_global[r] = R;
+      continue;
+    }
+    if (first) continue;
+    std::vector<double>& amt = w.res_amount[r];
+    std::vector<double>& d = w.res_delta[r];
+    // Source
+    double amount = q.inflow;
+    const double totalcells = (q.inflow_y2 - q.inflow_y1 + 1) * (q.inflow_x2 - q.inflow_x1 + 1) * 1.0;
+    amount /= totalcells;
+    for (int i = q.inflow_y1; i <= q.inflow_y2; i++)
+      for (int j = q.inflow_x1; j <= q.inflow_x2; j++) d[amod(i, Y) * X + amod(j, X)] += amount;
+    // Sink
+    const double decay = 1.0 - q.outflow;
+    if (!(q.outflow_x1 == AVGPU_RES_NONE || q.outflow_y1 == AVGPU_RES_NONE ||
+          q.outflow_x2 == AVGPU_RES_NONE || q.outflow_y2 == AVGPU_RES_NONE))
+      for (int i = q.outflow_y1; i <= q.outflow_y2; i++)
+        for (int j = q.outflow_x1; j <= q.outflow_x2; j++) {
+          const int64_t e = amod(i, Y) * X + amod(j, X);
+          d[e] += -std::max(amt[e] * (1.0 - decay), 0.0);
+        }
+    // CellInflow / CellOutflow
+    bool any_cells = false;
+    for (const auto& c : w.res_cells) if (c.resource == (int)r) any_cells = true;
+    if (any_cells) {
+      for (const auto& c : w.res_cells)
+        if (c.resource == (int)r && c.cell >= 0 && c.cell < n) d[c.cell] += c.inflow;
+      for (const auto& c : w.res_cells)
+        if (c.resource == (int)r && c.cell >= 0 && c.cell < n) d[c.cell] += -std::max(amt[c.cell] * c.outflow, 0.0);
+    }
+    // FlowAll: pointers 3..6 of every cell, in cell order
+    if (q.xdiffuse != 0.0 || q.ydiffuse != 0.0 || q.xgravity != 0.0 || q.ygravity != 0.0) {
+      const double SQRT2 = std::sqrt(2.0);
+      const int dxk[7] = {0, 0, 0, 1, 1, 0, -1}, dyk[7] = {0, 0, 0, 0, 1, 1, 1};
+      for (int64_t i = 0; i < n; i++) {
+        const int x = (int)(i % X), y = (int)(i / X);
+        for (int k = 3; k <= 6; k++) {
+          if (q.geometry == AVGPU_RES_GRID) {
+            if ((k == 3 || k == 4) && x == X - 1) continue;
+            if (k == 6 && x == 0) continue;
+            if (k != 3 && y == Y - 1) continue;
+          }
+          const int64_t ii = (int64_t)amod(y + dyk[k], Y) * X + amod(x + dxk[k], X);
+          flow_matter(amt[i], amt[ii], d[i], d[ii], q, dxk[k], dyk[k], (k == 4 || k == 6) ? SQRT2 : 1.0);
+        }
+      }
+    }
+    // StateAll
+    for (int64_t i = 0; i < n; i++) { amt[i] += d[i]; d[i] = 0.0; }
+  }
+}
+
+// the update's consumption of global resources (fixed point, DESIGN.md "Resources")
+static void res_end(World& w) {
+  for (size_t r = 0; r < w.res.size(); r++) {
+    if (w.res[r].geometry != AVGPU_RES_GLOBAL) continue;
+    w.res_global[r] = std::max(w.res_global[r] - (double)w.res_cons[r] / 4294967296.0, 0.0);
+    w.res_cons[r] = 0;
+  }
+}
+
 // 1. allotment (cScheduler restated; DESIGN.md "Scheduler") + 2. interpretation
 static void allot_interpret(World& w, double sum_merit, int64_t n_alive) {
   const int64_t ud = (int64_t)w.cfg.ave_time_slice * n_alive;
@@ -1100,7 +1320,9 @@ static int run_update_impl(World& w) {
   int64_t n_alive = 0;
   double sum_merit = tree_merit_sum(w, &n_alive);
   if (w.have_global) { sum_merit = w.global_merit; n_alive = w.global_orgs; }
+  res_begin(w);
   allot_interpret(w, sum_merit, n_alive);
+  res_end(w);
   // 3. placement rounds
   const int64_t nbirth = (int64_t)w.births.size();
   std::vector<uint8_t> occ(w.ncells);

@@ -53,6 +53,9 @@ class Backend:
         hid = (C.c_uint8 * len(instset.names))(*instset.handlers)
         red = (C.c_int32 * len(instset.names))(*instset.redundancy)
         self._call("load_instset", self.h, len(instset.names), hid, red)
+        self.nres = 0
+        if getattr(reactions, "resources", None):   # resources first: reactions name them
+            self.load_resources(reactions)
         arr = capi.reactions_array(reactions)
         self._call("load_env", self.h, len(reactions), arr)
 
@@ -113,6 +116,21 @@ class Backend:
             child = offb[i * capi.MAX_GENOME:i * capi.MAX_GENOME + r.offspring_len]
             out.append((r, f, child))
         return out
+
+    def load_resources(self, env):
+        self.nres = len(env.resources)
+        ra, ca = capi.resources_arrays(env.resources, env.cells)
+        self._call("load_resources", self.h, len(env.resources), ra, len(env.cells), ca)
+
+    def resources(self, spatial=False):
+        """(levels, per-cell grids or None): avgpu_get_resources"""
+        nres = self.nres
+        n = self.cfg.world_x * self.cfg.world_y
+        lv = (C.c_double * max(1, nres))()
+        sp = (C.c_double * max(1, nres * n))() if spatial else None
+        self._call("get_resources", self.h, lv, sp)
+        grids = [list(sp[r * n:(r + 1) * n]) for r in range(nres)] if spatial else None
+        return list(lv[:nres]), grids
 
     def run_update(self):
         st = capi.AvgpuUpdateStats()

@@ -144,3 +144,54 @@ def test_gpu_strip_tiles_equal_single_world(golden, T, geometry):
                              fa[lo * CAP:(lo + per) * CAP], f, CAP)
         assert not bad, f"tile {k}: {len(bad)} mismatches, first {bad[:3]}"
     assert sent > 0
+
+
+def _resource_env(golden, variant):
+    """spatial_res_100u's environment (variant "flow": diffusion and gravity on,
+    a torus ResA and a grid ResB, so FlowAll runs) or resources_9r's nine
+    consumed global pools"""
+    import copy
+    if variant == "9r":
+        d = os.path.join(golden, "resources_9r")
+        return files.read_environment(os.path.join(d, "environment.9resource")), \
+            files.read_org(os.path.join(d, "9task.org"),
+                           files.read_instset(os.path.join(d, "instset-heads.cfg")))
+    env = files.read_environment(os.path.join(golden, "spatial_res_100u", "environment.cfg"))
+    if variant == "flow":
+        env = copy.deepcopy(env)
+        a, b = env.resources[0], env.resources[1]
+        a.geometry, a.xdiffuse, a.ydiffuse, a.xgravity, a.ygravity = 2, 1.0, 0.5, 0.2, -0.1
+        a.inflow_x1, a.inflow_x2, a.inflow_y1, a.inflow_y2 = 40, 50, 45, 52    # box wraps the torus
+        b.xdiffuse, b.ydiffuse, b.xgravity, b.ygravity = 0.3, 1.0, -0.4, 0.25
+    iset = files.read_instset(os.path.join(golden, "resources_9r", "instset-heads.cfg"))
+    return env, iset.parse_sequence("rucavcqgfcqapqeccthzscpcccpqcxaqnccxxbcgdutycasvab")
+
+
+@pytest.mark.parametrize("variant", ["spatial", "flow", "9r"])
+def test_world_updates_resources_bit_exact(golden, variant):
+    """Updates with environment resources (the environment around the
+    path): spatial grids, CELL lists, diffusion/gravity flows and consumed
+    global pools; GPU world == oracle world, every cell, every field, and every
+    resource level and per-cell amount bit for bit."""
+    env, anc = _resource_env(golden, variant)
+    iset = files.read_instset(os.path.join(golden, "resources_9r", "instset-heads.cfg"))
+    cfg = capi.cfg_from_avida(files.read_avida_cfg(None, {"WORLD_X": 48, "WORLD_Y": 40}), seed=23)
+    n = cfg.world_x * cfg.world_y
+    orc = ol.Backend("oracle", cfg, iset, env, ncells=n)
+    gpu = ol.Backend("gpu", cfg, iset, env, ncells=n)
+    for b in (orc, gpu):
+        b.set_orgs(0, [anc] * 200, [100.0] * 200, deterministic=False)
+    for upd in range(60):
+        so = orc.run_update()
+        sg = gpu.run_update()
+        for f in ("num_organisms", "insts_executed", "births", "deaths", "divides"):
+            assert getattr(so, f) == getattr(sg, f), (upd, f, getattr(so, f), getattr(sg, f))
+        lo, go = orc.resources(spatial=True)
+        lg, gg = gpu.resources(spatial=True)
+        assert lo == lg, (upd, lo, lg)
+        assert go == gg, upd
+    a, oa, fa = orc.states(0, n, CAP)
+    b, ob, fb = gpu.states(0, n, CAP)
+    bad = pu.diff_states(a, b, oa, ob, fa, fb, CAP)
+    assert not bad, f"{len(bad)} mismatches: {bad[:5]}"
+    assert so.num_organisms > 200

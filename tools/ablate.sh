@@ -7,7 +7,7 @@ cd "$(dirname "$0")/.."
 if [ "$1" != run ]; then
   for X in IO LABEL SEARCHRQ; do
     /opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 -std=c++17 -fPIC -shared -ffp-contract=off -Wno-unused-result -Wno-unused-value \
-      -DAVGPU_ABL_$X -o avida_amd/libavida_gpu_abl_$X.so avida_amd/csrc/interp.hip avida_amd/csrc/world.hip avida_amd/csrc/capi.hip &
+      -DAVGPU_ABL_$X -o avida_amd/libavida_gpu_abl_$X.so avida_amd/csrc/interp.hip avida_amd/csrc/world.hip avida_amd/csrc/resources.hip avida_amd/csrc/capi.hip &
   done
   wait
   exit 0

@@ -130,7 +130,8 @@ EXPORTED = [
     "avgpu_update_run", "avgpu_set_stream", "avgpu_get_states",
     "avgpu_test_genomes", "avgpu_get_stats", "avgpu_stats_vector", "avgpu_set_global_totals",
     "avgpu_set_tile", "avgpu_tile_buffer_bytes", "avgpu_set_tile_buffers", "avgpu_tile_partials",
-    "avgpu_tile_begin", "avgpu_tile_place", "avgpu_tile_finish",
+    "avgpu_tile_begin", "avgpu_tile_place", "avgpu_tile_finish", "avgpu_tile_res_bytes",
+    "avgpu_set_tile_res_buffers", "avgpu_tile_res_cons", "avgpu_tile_res_settle",
     "avgpu_last_step_insts", "avgpu_last_kernel_ms", "avgpu_kernel_times", "avgpu_counters",
 ]
 
@@ -231,6 +232,10 @@ def bind_common(lib, prefix):
         "tile_begin": (C.c_int, [V, V, C.c_int]),
         "tile_place": (C.c_int, [V, C.c_int, C.c_int]),
         "tile_finish": (C.c_int, [V, C.POINTER(AvgpuUpdateStats)]),
+        "tile_res_bytes": (C.c_int, [V, C.POINTER(I64)]),
+        "set_tile_res_buffers": (C.c_int, [V] * 5),
+        "tile_res_cons": (C.c_int, [V, V]),
+        "tile_res_settle": (C.c_int, [V, V]),
         "get_stats": (C.c_int, [V, C.POINTER(AvgpuUpdateStats)]),
         "load_resources": (C.c_int, [V, C.c_int, C.POINTER(AvgpuResource), C.c_int,
                                      C.POINTER(AvgpuCellResource)]),

@@ -61,6 +61,8 @@ struct avgpu_world {
   int16_t code2op[64];
   bool instset_loaded = false;
   int res_geom[AVGPU_MAX_RESOURCES] = {};
+  std::vector<avgpu_resource> res_spec;       // avgpu_load_resources input (re-seeded by set_tile)
+  std::vector<avgpu_cell_resource> cell_spec;
   bool env_loaded = false;
   // device scratch
   double* d_totals = nullptr;   // [8 + partials]
@@ -779,17 +781,50 @@ int avgpu_set_global_totals(avgpu_world* w, double total_merit, int64_t total_or
 }
 
 // ---- resources (resources.hip; DESIGN.md "Resources") ----
+// initial amounts of this world's cells (cResourceCount::Setup: RateAll(
+// initial / size) + StateAll, main/cResourceCount.cc:323-328; SetCellList:
+// Rate + State, main/cSpatialResCount.cc:216-231; a strip tile seeds its rows)
+static int res_seed(avgpu_world* w) {
+  DevWorld& W = w->W;
+  HIPCHK(hipStreamSynchronize(w->stream));   // res_param may still be in flight
+  const int64_t n = W.n, nglobal = (int64_t)W.world_x * W.world_y;
+  const int nres = (int)w->res_spec.size();
+  ResParam P[AVGPU_MAX_RESOURCES];
+  HIPCHK(hipMemcpy(P, W.res_param, sizeof(P), hipMemcpyDeviceToHost));
+  double glob[AVGPU_MAX_RESOURCES];
+  memset(glob, 0, sizeof(glob));
+  if (W.n_spatial) {
+    std::vector<double> amt((size_t)W.n_spatial * n);
+    for (int r = 0; r < nres; r++) {
+      if (P[r].slot < 0) continue;
+      const double per = w->res_spec[r].initial / (double)nglobal;
+      for (int64_t c = 0; c < n; c++) amt[(size_t)P[r].slot * n + c] = 0.0 + per;
+    }
+    for (const avgpu_cell_resource& e : w->cell_spec) {
+      const int64_t l = e.cell - W.cell0;
+      if (e.cell >= 0 && e.cell < nglobal && l >= 0 && l < n) {
+        double& a = amt[(size_t)P[e.resource].slot * n + l];
+        a = a + (0.0 + e.initial);
+      }
+    }
+    HIPCHK(hipMemcpyAsync(W.res_amount, amt.data(), amt.size() * sizeof(double), hipMemcpyHostToDevice, w->stream));
+  }
+  for (int r = 0; r < nres; r++) glob[r] = P[r].slot < 0 ? w->res_spec[r].initial : 0.0;
+  HIPCHK(hipMemcpyAsync(W.res_global, glob, sizeof(glob), hipMemcpyHostToDevice, w->stream));
+  HIPCHK(hipMemsetAsync(W.res_cons, 0, AVGPU_MAX_RESOURCES * sizeof(unsigned long long), w->stream));
+  HIPCHK(hipStreamSynchronize(w->stream));
+  W.res_first = 1;
+  return 0;
+}
+
 int avgpu_load_resources(avgpu_world* w, int nres, const avgpu_resource* res, int ncell,
                          const avgpu_cell_resource* cells) {
   if (!w || nres < 0 || nres > AVGPU_MAX_RESOURCES || ncell < 0 || (ncell && !cells) || (nres && !res))
     return fail(AVGPU_EINVAL, "resource arguments");
   DevWorld& W = w->W;
-  if (W.tiled) return fail(AVGPU_EUNSUPPORTED, "resources on strip tiles are not on the GPU path yet");
   int nsp = 0;
   ResParam P[AVGPU_MAX_RESOURCES];
-  double glob[AVGPU_MAX_RESOURCES];
   memset(P, 0, sizeof(P));
-  memset(glob, 0, sizeof(glob));
   for (int r = 0; r < nres; r++) {
     const avgpu_resource& q = res[r];
     if (q.geometry < 0 || q.geometry > 2) return fail(AVGPU_EINVAL, "resource geometry");
@@ -818,7 +853,6 @@ int avgpu_load_resources(avgpu_world* w, int nres, const avgpu_resource* res, in
       if (i == 99) { p.decay99 = dp; p.inflow99 = ip; }
     }
     p.decay100 = dp; p.inflow100 = ip;
-    glob[r] = q.geometry == AVGPU_RES_GLOBAL ? q.initial : 0.0;
     w->res_geom[r] = q.geometry;
     W.res_spatial_host[r] = q.geometry != AVGPU_RES_GLOBAL;
     W.res_flows_host[r] = (int8_t)p.flows;
@@ -827,29 +861,11 @@ int avgpu_load_resources(avgpu_world* w, int nres, const avgpu_resource* res, in
     if (cells[i].resource < 0 || cells[i].resource >= nres || res[cells[i].resource].geometry == AVGPU_RES_GLOBAL)
       return fail(AVGPU_EINVAL, "CELL entry names a resource that is not spatial");
   const int64_t n = W.n;
-  if (nsp) {
-    if (!W.res_amount) {
-      HIPCHK(hipMalloc(&W.res_amount, (size_t)AVGPU_MAX_RESOURCES * n * sizeof(double)));
-      w->allocs.push_back(W.res_amount);
-      HIPCHK(hipMalloc(&W.res_delta, (size_t)n * sizeof(double)));
-      w->allocs.push_back(W.res_delta);
-    }
-    // initial: initial / cells everywhere, then + the CELL initial (Setup, SetCellList)
-    std::vector<double> amt((size_t)nsp * n);
-    for (int r = 0; r < nres; r++) {
-      if (P[r].slot < 0) continue;
-      const double per = res[r].initial / (double)n;
-      for (int64_t c = 0; c < n; c++) amt[(size_t)P[r].slot * n + c] = 0.0 + per;
-    }
-    for (int i = 0; i < ncell; i++) {
-      const int r = cells[i].resource;
-      const int64_t c = cells[i].cell;
-      if (c >= 0 && c < n) {
-        double& a = amt[(size_t)P[r].slot * n + c];
-        a = a + (0.0 + cells[i].initial);
-      }
-    }
-    HIPCHK(hipMemcpyAsync(W.res_amount, amt.data(), amt.size() * sizeof(double), hipMemcpyHostToDevice, w->stream));
+  if (nsp && !W.res_amount) {
+    HIPCHK(hipMalloc(&W.res_amount, (size_t)AVGPU_MAX_RESOURCES * n * sizeof(double)));
+    w->allocs.push_back(W.res_amount);
+    HIPCHK(hipMalloc(&W.res_delta, (size_t)n * sizeof(double)));
+    w->allocs.push_back(W.res_delta);
   }
   if (ncell) {
     if (W.res_cells) hipFree(W.res_cells);
@@ -858,12 +874,11 @@ int avgpu_load_resources(avgpu_world* w, int nres, const avgpu_resource* res, in
   }
   W.n_res = nres;
   W.n_cellres = ncell;
-  W.res_first = 1;
+  W.n_spatial = nsp;
+  w->res_spec.assign(res, res + nres);
+  w->cell_spec.assign(cells, cells + ncell);
   HIPCHK(hipMemcpyAsync(W.res_param, P, sizeof(P), hipMemcpyHostToDevice, w->stream));
-  HIPCHK(hipMemcpyAsync(W.res_global, glob, sizeof(glob), hipMemcpyHostToDevice, w->stream));
-  HIPCHK(hipMemsetAsync(W.res_cons, 0, AVGPU_MAX_RESOURCES * sizeof(unsigned long long), w->stream));
-  HIPCHK(hipStreamSynchronize(w->stream));
-  return 0;
+  return res_seed(w);
 }
 
 int avgpu_get_resources(avgpu_world* w, double* levels, double* spatial) {
@@ -910,6 +925,46 @@ int avgpu_set_tile(avgpu_world* w, int64_t row0, int64_t arena_bytes) {
   W.cell0 = row0 * X;
   W.r_arena = arena_bytes;
   w->tile_buffers = false;
+  W.rs_send[0] = W.rs_send[1] = W.rs_recv[0] = W.rs_recv[1] = nullptr;
+  if (W.n_res) return res_seed(w);   // this strip's share of the initial amounts
+  return 0;
+}
+
+int avgpu_tile_res_bytes(avgpu_world* w, int64_t* bytes) {
+  if (!w) return fail(AVGPU_EINVAL, "NULL world");
+  if (bytes) *bytes = (int64_t)w->W.n_spatial * w->W.world_x * (int64_t)sizeof(double);
+  return 0;
+}
+
+int avgpu_set_tile_res_buffers(avgpu_world* w, void* send_up, void* send_down, void* recv_up,
+                               void* recv_down) {
+  if (!w) return fail(AVGPU_EINVAL, "NULL world");
+  if (!w->W.tiled) return fail(AVGPU_ESTATE, "avgpu_set_tile did not make this world a strip tile");
+  if (w->W.n_spatial && (!send_up || !send_down || !recv_up || !recv_down))
+    return fail(AVGPU_EINVAL, "NULL tile resource buffer");
+  DevWorld& W = w->W;
+  W.rs_send[0] = (double*)send_up; W.rs_send[1] = (double*)send_down;
+  W.rs_recv[0] = (double*)recv_up; W.rs_recv[1] = (double*)recv_down;
+  return 0;
+}
+
+int avgpu_tile_res_cons(avgpu_world* w, uint64_t* dev_out) {
+  int rc = ready(w);
+  if (rc < 0) return rc;
+  if (!dev_out) return fail(AVGPU_EINVAL, "dev_out is NULL");
+  HIPCHK(hipMemcpyAsync(dev_out, w->W.res_cons, AVGPU_MAX_RESOURCES * sizeof(unsigned long long),
+                        hipMemcpyDeviceToDevice, w->stream));
+  int g = 0;
+  for (int r = 0; r < w->W.n_res; r++) g += w->res_geom[r] == AVGPU_RES_GLOBAL;
+  return g;
+}
+
+int avgpu_tile_res_settle(avgpu_world* w, const uint64_t* dev_sum) {
+  int rc = ready(w);
+  if (rc < 0) return rc;
+  if (!dev_sum) return fail(AVGPU_EINVAL, "dev_sum is NULL");
+  launch_resources_settle(w->W, w->stream, (const unsigned long long*)dev_sum);
+  HIPCHK(hipGetLastError());
   return 0;
 }
 
@@ -951,6 +1006,7 @@ int avgpu_tile_partials(avgpu_world* w, double* dev_out) {
   if (rc < 0) return rc;
   if (!dev_out) return fail(AVGPU_EINVAL, "dev_out is NULL");
   launch_tile_partials(w->W, w->stream, dev_out);
+  if (w->W.tiled) launch_resources_pack(w->W, w->stream);
   HIPCHK(hipGetLastError());
   return 0;
 }
@@ -958,7 +1014,8 @@ int avgpu_tile_partials(avgpu_world* w, double* dev_out) {
 int avgpu_tile_begin(avgpu_world* w, const double* dev_gathered, int ntiles) {
   int rc = tile_ready(w);
   if (rc < 0) return rc;
-  if (w->W.n_res) return fail(AVGPU_EUNSUPPORTED, "resources on strip tiles are not on the GPU path yet");
+  if (w->W.n_spatial && !w->W.rs_recv[0])
+    return fail(AVGPU_ESTATE, "spatial resources need avgpu_set_tile_res_buffers");
   if (!dev_gathered || ntiles < 1) return fail(AVGPU_EINVAL, "gathered partials");
   launch_tile_totals(w->W, w->stream, dev_gathered, ntiles, w->d_totals);
   launch_world_pre(w->W, w->stream, w->d_totals);

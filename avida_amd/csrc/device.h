@@ -162,6 +162,9 @@ struct DevWorld {
   int8_t res_spatial_host[AVGPU_MAX_RESOURCES];   // host-side launch flags
   int8_t res_flows_host[AVGPU_MAX_RESOURCES];
   int8_t res_first;             // host: the next update is the first since the load
+  int32_t n_spatial;            // spatial resources (rows of res_amount)
+  double* rs_send[2];           // strip tiles: [n_spatial][X] first / last row out
+  double* rs_recv[2];           //   and the rows above / below in
   uint8_t fill_code;   // code of op 0 (new sites on allocate)
   // config scalars
   int32_t world_x, world_y, geometry;
@@ -385,6 +388,8 @@ void launch_interpret_classes(const DevWorld& W, const DevWorld* dW, int mode, h
 void launch_world_pre(const DevWorld& W, hipStream_t s, const double* d_totals);
 void launch_resources_begin(const DevWorld& W, hipStream_t s);
 void launch_resources_end(const DevWorld& W, hipStream_t s);
+void launch_resources_pack(const DevWorld& W, hipStream_t s);
+void launch_resources_settle(const DevWorld& W, hipStream_t s, const unsigned long long* sum);
 void launch_world_post(const DevWorld& W, hipStream_t s, double* d_stats);
 void launch_classify_uniform(const DevWorld& W, hipStream_t s, int64_t first, int64_t count,
                              const int32_t* d_budget, int32_t uniform);

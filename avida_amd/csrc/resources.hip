@@ -26,12 +26,14 @@ __device__ __forceinline__ int cover(int v, int a, int b, int L) {
   return i0 > b ? 0 : 1 + (b - i0) / L;
 }
 
+// coordinates are global (a strip tile holds rows [row0, row0 + rows) of the
+// WORLD_X x world_y grid; boxes and CELL ids refer to the global grid)
 __global__ void k_res_spatial_rates(DevWorld W, int r) {
   const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= W.n) return;
   const ResParam P = W.res_param[r];
   const int X = W.world_x, Y = W.world_y;
-  const int x = (int)(c % X), y = (int)(c / X);
+  const int x = (int)(c % X), y = W.row0 + (int)(c / X);
   double d = 0.0;
   const int nin = cover(y, P.in_y1, P.in_y2, Y) * cover(x, P.in_x1, P.in_x2, X);
   for (int k = 0; k < nin; k++) d = __dadd_rn(d, P.in_share);
@@ -48,15 +50,19 @@ __global__ void k_res_cell_rates(DevWorld W, int r) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   const ResParam P = W.res_param[r];
   const double* amt = W.res_amount + (int64_t)P.slot * W.n;
+  const int64_t nglobal = (int64_t)W.world_x * W.world_y;
   for (int i = 0; i < W.n_cellres; i++) {
     const avgpu_cell_resource e = W.res_cells[i];
-    if (e.resource == r && e.cell >= 0 && e.cell < W.n) W.res_delta[e.cell] = __dadd_rn(W.res_delta[e.cell], e.inflow);
+    const int64_t l = e.cell - W.cell0;
+    if (e.resource == r && e.cell >= 0 && e.cell < nglobal && l >= 0 && l < W.n)
+      W.res_delta[l] = __dadd_rn(W.res_delta[l], e.inflow);
   }
   for (int i = 0; i < W.n_cellres; i++) {
     const avgpu_cell_resource e = W.res_cells[i];
-    if (e.resource == r && e.cell >= 0 && e.cell < W.n) {
-      const double dec = fmax(__dmul_rn(amt[e.cell], e.outflow), 0.0);
-      W.res_delta[e.cell] = __dadd_rn(W.res_delta[e.cell], -dec);
+    const int64_t l = e.cell - W.cell0;
+    if (e.resource == r && e.cell >= 0 && e.cell < nglobal && l >= 0 && l < W.n) {
+      const double dec = fmax(__dmul_rn(amt[l], e.outflow), 0.0);
+      W.res_delta[l] = __dadd_rn(W.res_delta[l], -dec);
     }
   }
 }
@@ -99,16 +105,27 @@ __device__ __forceinline__ bool res_ptr(int geometry, int X, int Y, int x, int y
   return true;
 }
 
+// amount of global cell (gx, gy): this world's rows, else the edge row the
+// tile above (gy = row0 - 1) or below sent
+__device__ __forceinline__ double res_at(const DevWorld& W, const double* amt, int slot, int gx, int gy) {
+  const int ly = gy - W.row0;
+  if (ly >= 0 && ly < W.rows) return amt[(int64_t)ly * W.world_x + gx];
+  const int up = amod(W.row0 - 1, W.world_y);
+  return (gy == up ? W.rs_recv[0] : W.rs_recv[1])[(int64_t)slot * W.world_x + gx];
+}
+
 // FlowAll: cell c's delta gets -flow for its own pointers 3..6 and +flow from
 // every cell whose pointer 3..6 is c, added in increasing (computing cell, k)
-// order like the reference's loop over i
+// order (global cell ids) like the reference's loop over i
 __global__ void k_res_flow(DevWorld W, int r) {
   const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= W.n) return;
   const ResParam P = W.res_param[r];
   const int X = W.world_x, Y = W.world_y;
   const double* amt = W.res_amount + (int64_t)P.slot * W.n;
-  const int x = (int)(c % X), y = (int)(c / X);
+  const int x = (int)(c % X), y = W.row0 + (int)(c / X);
+  const int64_t gc = (int64_t)y * X + x;
+  const double a_c = amt[c];
   const double SQRT2 = 1.4142135623730951;   // sqrt(2.0)
   int64_t key[8];
   double val[8];
@@ -117,8 +134,8 @@ __global__ void k_res_flow(DevWorld W, int r) {
     int nx, ny;
     if (!res_ptr(P.geometry, X, Y, x, y, k, nx, ny)) continue;
     const int xd = (k == 3 || k == 4) ? 1 : (k == 5 ? 0 : -1), yd = (k == 3) ? 0 : 1;
-    key[m] = c * 8 + k;
-    val[m] = -flow_amt(P, amt[c], amt[(int64_t)ny * X + nx], xd, yd, (k == 4 || k == 6) ? SQRT2 : 1.0);
+    key[m] = gc * 8 + k;
+    val[m] = -flow_amt(P, a_c, res_at(W, amt, P.slot, nx, ny), xd, yd, (k == 4 || k == 6) ? SQRT2 : 1.0);
     m++;
   }
   for (int k = 3; k <= 6; k++) {                       // cells whose pointer k is c
@@ -126,9 +143,8 @@ __global__ void k_res_flow(DevWorld W, int r) {
     const int jx = amod(x - dx, X), jy = amod(y - dy, Y);
     int nx, ny;
     if (!res_ptr(P.geometry, X, Y, jx, jy, k, nx, ny) || nx != x || ny != y) continue;
-    const int64_t j = (int64_t)jy * X + jx;
-    key[m] = j * 8 + k;
-    val[m] = flow_amt(P, amt[j], amt[c], dx, dy, (k == 4 || k == 6) ? SQRT2 : 1.0);
+    key[m] = ((int64_t)jy * X + jx) * 8 + k;
+    val[m] = flow_amt(P, res_at(W, amt, P.slot, jx, jy), a_c, dx, dy, (k == 4 || k == 6) ? SQRT2 : 1.0);
     m++;
   }
   for (int a = 1; a < m; a++)                          // insertion sort by (cell, k)
@@ -174,6 +190,26 @@ __global__ void k_res_global_end(DevWorld W) {
   W.res_cons[r] = 0ull;
 }
 
+// strip tiles: first and last row of every spatial resource for the neighbours
+__global__ void k_res_pack(DevWorld W) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int X = W.world_x;
+  if (i >= (int64_t)W.n_spatial * X) return;
+  const int slot = (int)(i / X), x = (int)(i % X);
+  const double* amt = W.res_amount + (int64_t)slot * W.n;
+  W.rs_send[0][i] = amt[x];
+  W.rs_send[1][i] = amt[(int64_t)(W.rows - 1) * X + x];
+}
+
+// strip tiles: every tile subtracts the consumption summed over all tiles
+__global__ void k_res_settle(DevWorld W, const unsigned long long* sum) {
+  const int r = threadIdx.x;
+  if (r >= W.n_res || W.res_param[r].slot >= 0) return;
+  const double used = (double)sum[r] / RES_FIX;
+  W.res_global[r] = fmax(__dsub_rn(W.res_global[r], used), 0.0);
+  W.res_cons[r] = 0ull;
+}
+
 }  // namespace
 
 static inline unsigned rblk(int64_t n) { return (unsigned)((n + 255) / 256); }
@@ -195,4 +231,13 @@ void launch_resources_begin(const DevWorld& W, hipStream_t s) {
 void launch_resources_end(const DevWorld& W, hipStream_t s) {
   if (W.n_res == 0) return;
   hipLaunchKernelGGL(k_res_global_end, dim3(1), dim3(64), 0, s, W);
+}
+
+void launch_resources_pack(const DevWorld& W, hipStream_t s) {
+  if (W.n_spatial == 0 || !W.rs_send[0]) return;
+  hipLaunchKernelGGL(k_res_pack, dim3(rblk((int64_t)W.n_spatial * W.world_x)), dim3(256), 0, s, W);
+}
+
+void launch_resources_settle(const DevWorld& W, hipStream_t s, const unsigned long long* sum) {
+  hipLaunchKernelGGL(k_res_settle, dim3(1), dim3(64), 0, s, W, sum);
 }

@@ -12,6 +12,8 @@ include/avida_gpu.h ("strip tiles"):
     tile_partials -> all_gather -> tile_begin -> exchange(halo)
     4 x [tile_place(r,0) -> exchange(halo) -> tile_place(r,1) -> exchange(halo) -> tile_place(r,2)]
     tile_place(3,3) -> exchange(records) -> tile_finish
+    with resources: exchange(resources) after the all_gather (edge rows of
+    the spatial grids), all_reduce(consumption) + tile_res_settle at the end
 
 `lib` may be the product (prefix "avgpu_", device buffers, RCCL/NCCL or an
 in-process loopback) or the CPU oracle (prefix "orc_", host buffers, gloo);
@@ -55,9 +57,29 @@ class Tile:
                 self.halo_send + self.halo_recv + self.rec_send + self.rec_recv]
         _check(lib, prefix, getattr(lib, prefix + "set_tile_buffers")(handle, *ptrs),
                "set_tile_buffers")
+        self.resources_changed(device)
+
+    def resources_changed(self, device):
+        """(Re)size the resource edge-row buffers after avgpu_load_resources."""
+        lib, prefix, handle = self.lib, self.p, self.h
+        sb = C.c_int64()
+        _check(lib, prefix, getattr(lib, prefix + "tile_res_bytes")(handle, C.byref(sb)), "tile_res_bytes")
+        f64 = dict(dtype=torch.float64, device=device)
+        self.res_send = [torch.zeros(max(1, sb.value // 8), **f64) for _ in range(2)]
+        self.res_recv = [torch.zeros(max(1, sb.value // 8), **f64) for _ in range(2)]
+        self.has_res_rows = sb.value > 0
+        ptrs = [C.c_void_p(t.data_ptr()) for t in self.res_send + self.res_recv]
+        _check(lib, prefix, getattr(lib, prefix + "set_tile_res_buffers")(handle, *ptrs),
+               "set_tile_res_buffers")
+        self.cons = torch.zeros(16, dtype=torch.int64, device=device)   # AVGPU_MAX_RESOURCES
 
     def call(self, name, *args):
         return _check(self.lib, self.p, getattr(self.lib, self.p + name)(self.h, *args), name)
+
+
+def _buffers(kind):
+    return {"halo": ("halo_send", "halo_recv"), "records": ("rec_send", "rec_recv"),
+            "resources": ("res_send", "res_recv")}[kind]
 
 
 class LoopbackTransport:
@@ -73,12 +95,14 @@ class LoopbackTransport:
         T = len(tiles)
         for i, t in enumerate(tiles):
             up, down = tiles[(i - 1) % T], tiles[(i + 1) % T]
-            if kind == "halo":
-                t.halo_recv[0].copy_(up.halo_send[1])
-                t.halo_recv[1].copy_(down.halo_send[0])
-            else:
-                t.rec_recv[0].copy_(up.rec_send[1])
-                t.rec_recv[1].copy_(down.rec_send[0])
+            send, recv = _buffers(kind)
+            getattr(t, recv)[0].copy_(getattr(up, send)[1])
+            getattr(t, recv)[1].copy_(getattr(down, send)[0])
+
+    def all_reduce_sum(self, tiles):
+        total = sum(t.cons for t in tiles)
+        for t in tiles:
+            t.cons.copy_(total)
 
 
 class DistTransport:
@@ -100,9 +124,13 @@ class DistTransport:
             chunks = list(t.gathered.split(t.n_part))
             self.dist.all_gather(chunks, t.part, group=self.group)
 
+    def all_reduce_sum(self, tiles):
+        (t,) = tiles
+        self.dist.all_reduce(t.cons, group=self.group)   # int64 sum == the uint64 sum mod 2^64
+
     def exchange(self, tiles, kind):
         (t,) = tiles
-        send, recv = (t.halo_send, t.halo_recv) if kind == "halo" else (t.rec_send, t.rec_recv)
+        send, recv = (getattr(t, n) for n in _buffers(kind))
         up = (self.rank - 1) % self.world
         down = (self.rank + 1) % self.world
         d = self.dist
@@ -129,6 +157,8 @@ class StripWorld:
         for t in tiles:
             t.call("tile_partials", C.c_void_p(t.part.data_ptr()))
         self.tr.all_gather(tiles)
+        if tiles[0].has_res_rows:
+            self.tr.exchange(tiles, "resources")
         for t in tiles:
             t.call("tile_begin", C.c_void_p(t.gathered.data_ptr()), t.ntiles)
         self.tr.exchange(tiles, "halo")
@@ -144,3 +174,8 @@ class StripWorld:
         self.tr.exchange(tiles, "records")
         for t in tiles:
             t.call("tile_finish", None)
+        pools = [t.call("tile_res_cons", C.c_void_p(t.cons.data_ptr())) for t in tiles]
+        if pools[0] > 0:
+            self.tr.all_reduce_sum(tiles)
+            for t in tiles:
+                t.call("tile_res_settle", C.c_void_p(t.cons.data_ptr()))

@@ -375,6 +375,7 @@ int avgpu_set_global_totals(avgpu_world* w, double total_merit, int64_t total_or
  * halo_recv_down from the tile below (same for records):
  *
  *   avgpu_tile_partials(w, part)         all_gather(part) in tile order
+ *                                        [exchange(resource rows): spatial resources]
  *   avgpu_tile_begin(w, gathered, T)     exchange(halo)
  *   for round 0..3:
  *     avgpu_tile_place(w, round, 0)      exchange(halo)
@@ -382,7 +383,11 @@ int avgpu_set_global_totals(avgpu_world* w, double total_merit, int64_t total_or
  *     avgpu_tile_place(w, round, 2)
  *   avgpu_tile_place(w, 3, 3)            exchange(records)
  *   avgpu_tile_finish(w, stats)
+ *   [avgpu_tile_res_cons(w, cons)        all_reduce(cons, sum): global pools,
+ *    avgpu_tile_res_settle(w, cons)      when avgpu_tile_res_cons returned > 0]
  *
+ * Resources on tiles: call avgpu_set_tile before (or after: it re-seeds them)
+ * avgpu_load_resources; CELL ids and inflow/outflow boxes stay global.
  * Every call is stream-ordered on the handle's stream (no host sync).
  * Requirements: rows >= 2, tile cells a multiple of 256 and of world_x.
  * arena_bytes (<= 0: default max(256 KiB, 256 B x world_x)) bounds the
@@ -406,6 +411,20 @@ int avgpu_tile_begin(avgpu_world* w, const double* dev_gathered, int ntiles);
 int avgpu_tile_place(avgpu_world* w, int round, int phase);
 /* activation of this tile's winners and of the received records, statistics */
 int avgpu_tile_finish(avgpu_world* w, avgpu_update_stats* out);
+/* spatial resources on strips: bytes of one resource-row buffer (n_spatial x
+ * world_x doubles, 0 without spatial resources) and the 4 device buffers
+ * exchanged like the halo (avgpu_tile_partials fills the send rows: first and
+ * last row of every spatial resource; the flow step of avgpu_tile_begin reads
+ * the rows above and below from the receive buffers) */
+int avgpu_tile_res_bytes(avgpu_world* w, int64_t* bytes);
+int avgpu_set_tile_res_buffers(avgpu_world* w, void* send_up, void* send_down, void* recv_up,
+                               void* recv_down);
+/* global pools on strips: this tile's consumption of the update
+ * (AVGPU_MAX_RESOURCES uint64, 2^-32 units, device memory); returns the number
+ * of global resources (0: skip the all-reduce and the settle) */
+int avgpu_tile_res_cons(avgpu_world* w, uint64_t* dev_out);
+/* subtract the summed consumption of all tiles (same on every tile) */
+int avgpu_tile_res_settle(avgpu_world* w, const uint64_t* dev_sum);
 
 /* counters of the last avgpu_step: instructions executed (sum over lanes) */
 int avgpu_last_step_insts(avgpu_world* w, int64_t* insts);

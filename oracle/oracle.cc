@@ -227,6 +227,11 @@ struct World {
   std::vector<double> res_global, res_decay100, res_inflow100, res_decay99, res_inflow99;
   bool res_first = false;   // the first update after the load: no spatial step, 9999 global steps
   std::vector<uint64_t> res_cons;
+  // strip tiles: edge rows of the spatial amounts, [slot][X] (0 = above, 1 = below)
+  std::vector<int> res_slot;   // resource -> spatial slot or -1
+  int n_spatial = 0;
+  double* rs_send[2] = {nullptr, nullptr};
+  double* rs_recv[2] = {nullptr, nullptr};
 };
 
 thread_local std::string g_err;
@@ -921,25 +926,45 @@ int orc_load_instset(void* h, int n, const uint8_t* handler_id, const int32_t* r
   return 0;
 }
 
+// initial amounts (cResourceCount::Setup: RateAll(initial / size) + StateAll,
+// main/cResourceCount.cc:323-328; SetCellList: Rate + State,
+// main/cSpatialResCount.cc:216-231) of this world's cells (a strip tile holds
+// rows [row0, row0 + rows) of the global grid)
+static void res_init(World& w) {
+  const int64_t n = w.ncells, nglobal = (int64_t)w.cfg.world_x * w.global_rows;
+  const int nres = (int)w.res.size();
+  w.res_amount.assign(nres, {});
+  w.res_delta.assign(nres, {});
+  w.res_global.assign(nres, 0.0);
+  w.res_cons.assign(nres, 0);
+  w.res_first = true;
+  for (int r = 0; r < nres; r++) {
+    const avgpu_resource& q = w.res[r];
+    if (q.geometry == AVGPU_RES_GLOBAL) { w.res_global[r] = q.initial; continue; }
+    w.res_amount[r].assign(n, 0.0 + q.initial / (double)nglobal);
+    w.res_delta[r].assign(n, 0.0);
+  }
+  for (const auto& c : w.res_cells) {
+    const int64_t l = c.cell - w.cell0;
+    if (c.cell >= 0 && c.cell < nglobal && l >= 0 && l < n) w.res_amount[c.resource][l] += (0.0 + c.initial);
+  }
+}
+
 int orc_load_resources(void* h, int nres, const avgpu_resource* res, int ncell,
                        const avgpu_cell_resource* cells) {
   World& w = *(World*)h;
   if (nres < 0 || nres > AVGPU_MAX_RESOURCES) return fail(AVGPU_EINVAL, "resource count");
-  if (w.tiled) return fail(AVGPU_EUNSUPPORTED, "resources on strip tiles");
-  const int64_t n = w.ncells;
   w.res.assign(res, res + nres);
   w.res_cells.assign(cells, cells + ncell);
-  w.res_amount.assign(nres, {});
-  w.res_delta.assign(nres, {});
-  w.res_global.assign(nres, 0.0);
   w.res_decay100.assign(nres, 1.0);
   w.res_inflow100.assign(nres, 0.0);
   w.res_decay99.assign(nres, 1.0);
   w.res_inflow99.assign(nres, 0.0);
-  w.res_cons.assign(nres, 0);
-  w.res_first = true;
+  w.res_slot.assign(nres, -1);
+  w.n_spatial = 0;
   for (int r = 0; r < nres; r++) {
     const avgpu_resource& q = res[r];
+    if (q.geometry != AVGPU_RES_GLOBAL) w.res_slot[r] = w.n_spatial++;
     // decay_precalc / inflow_precalc (main/cResourceCount.cc:336-345)
     const double decay = 1.0 - q.outflow;
     const double step_decay = std::pow(decay, 1.0 / 10000.0), step_inflow = q.inflow * (1.0 / 10000.0);
@@ -951,15 +976,8 @@ int orc_load_resources(void* h, int nres, const avgpu_resource* res, int ncell,
     }
     w.res_decay100[r] = dp;
     w.res_inflow100[r] = ip;
-    if (q.geometry == AVGPU_RES_GLOBAL) { w.res_global[r] = q.initial; continue; }
-    // Setup: RateAll(initial / size) + StateAll (cResourceCount.cc:323-328)
-    w.res_amount[r].assign(n, 0.0 + q.initial / (double)n);
-    w.res_delta[r].assign(n, 0.0);
   }
-  for (int i = 0; i < ncell; i++) {   // SetCellList: Rate + State (cSpatialResCount.cc:216-231)
-    const auto& c = cells[i];
-    if (c.cell >= 0 && c.cell < n) w.res_amount[c.resource][c.cell] += (0.0 + c.initial);
-  }
+  res_init(w);
   return 0;
 }
 
@@ -1145,10 +1163,16 @@ static void flow_matter(double a1, double a2, double& d1, double& d2, const avgp
 // (:780) and the remainder carries, making every later update 10000 steps.
 // Pinned by tests/golden/spatial_res_100u (test_resources.py).
 static void res_begin(World& w) {
-  const int X = w.cfg.world_x, Y = w.cfg.world_y;
+  const int X = w.cfg.world_x, Yg = (int)w.global_rows;
   const int64_t n = w.ncells;
   const bool first = w.res_first;
   w.res_first = false;
+  // this world's rows of the global grid; a strip tile reads the rows above
+  // and below from the edge rows its neighbours sent (rs_recv)
+  auto local = [&](int64_t g) -> int64_t {
+    const int64_t l = g - w.cell0;
+    return (l >= 0 && l < n) ? l : -1;
+  };
   for (size_t r = 0; r < w.res.size(); r++) {
     const avgpu_resource& q = w.res[r];
     if (q.geometry == AVGPU_RES_GLOBAL) {
@@ -1163,46 +1187,70 @@ static void res_begin(World& w) {
     if (first) continue;
     std::vector<double>& amt = w.res_amount[r];
     std::vector<double>& d = w.res_delta[r];
+    const int slot = w.res_slot[r];
+    auto amount = [&](int gy, int x) -> double {
+      const int ly = gy - (int)w.row0;
+      if (ly >= 0 && ly < w.rows) return amt[(int64_t)ly * X + x];
+      if (gy == amod((int)w.row0 - 1, Yg)) return w.rs_recv[0][(int64_t)slot * X + x];
+      return w.rs_recv[1][(int64_t)slot * X + x];
+    };
     // Source
-    double amount = q.inflow;
+    double amount_in = q.inflow;
     const double totalcells = (q.inflow_y2 - q.inflow_y1 + 1) * (q.inflow_x2 - q.inflow_x1 + 1) * 1.0;
-    amount /= totalcells;
+    amount_in /= totalcells;
     for (int i = q.inflow_y1; i <= q.inflow_y2; i++)
-      for (int j = q.inflow_x1; j <= q.inflow_x2; j++) d[amod(i, Y) * X + amod(j, X)] += amount;
+      for (int j = q.inflow_x1; j <= q.inflow_x2; j++) {
+        const int64_t l = local((int64_t)amod(i, Yg) * X + amod(j, X));
+        if (l >= 0) d[l] += amount_in;
+      }
     // Sink
     const double decay = 1.0 - q.outflow;
     if (!(q.outflow_x1 == AVGPU_RES_NONE || q.outflow_y1 == AVGPU_RES_NONE ||
           q.outflow_x2 == AVGPU_RES_NONE || q.outflow_y2 == AVGPU_RES_NONE))
       for (int i = q.outflow_y1; i <= q.outflow_y2; i++)
         for (int j = q.outflow_x1; j <= q.outflow_x2; j++) {
-          const int64_t e = amod(i, Y) * X + amod(j, X);
-          d[e] += -std::max(amt[e] * (1.0 - decay), 0.0);
+          const int64_t l = local((int64_t)amod(i, Yg) * X + amod(j, X));
+          if (l >= 0) d[l] += -std::max(amt[l] * (1.0 - decay), 0.0);
         }
-    // CellInflow / CellOutflow
+    // CellInflow / CellOutflow (cell ids are global)
     bool any_cells = false;
     for (const auto& c : w.res_cells) if (c.resource == (int)r) any_cells = true;
     if (any_cells) {
-      for (const auto& c : w.res_cells)
-        if (c.resource == (int)r && c.cell >= 0 && c.cell < n) d[c.cell] += c.inflow;
-      for (const auto& c : w.res_cells)
-        if (c.resource == (int)r && c.cell >= 0 && c.cell < n) d[c.cell] += -std::max(amt[c.cell] * c.outflow, 0.0);
+      for (const auto& c : w.res_cells) {
+        const int64_t l = local(c.cell);
+        if (c.resource == (int)r && l >= 0) d[l] += c.inflow;
+      }
+      for (const auto& c : w.res_cells) {
+        const int64_t l = local(c.cell);
+        if (c.resource == (int)r && l >= 0) d[l] += -std::max(amt[l] * c.outflow, 0.0);
+      }
     }
-    // FlowAll: pointers 3..6 of every cell, in cell order
+    // FlowAll: pointers 3..6 of every cell in global cell order; the cells
+    // that reach this world's rows are its own and those of the row above
     if (q.xdiffuse != 0.0 || q.ydiffuse != 0.0 || q.xgravity != 0.0 || q.ygravity != 0.0) {
       const double SQRT2 = std::sqrt(2.0);
       const int dxk[7] = {0, 0, 0, 1, 1, 0, -1}, dyk[7] = {0, 0, 0, 0, 1, 1, 1};
-      for (int64_t i = 0; i < n; i++) {
-        const int x = (int)(i % X), y = (int)(i / X);
-        for (int k = 3; k <= 6; k++) {
-          if (q.geometry == AVGPU_RES_GRID) {
-            if ((k == 3 || k == 4) && x == X - 1) continue;
-            if (k == 6 && x == 0) continue;
-            if (k != 3 && y == Y - 1) continue;
+      std::vector<int> rows_g;
+      for (int ly = 0; ly < w.rows; ly++) rows_g.push_back((int)w.row0 + ly);
+      if (w.tiled && (w.row0 > 0 || q.geometry != AVGPU_RES_GRID)) rows_g.push_back(amod((int)w.row0 - 1, Yg));
+      std::sort(rows_g.begin(), rows_g.end());
+      for (int gy : rows_g)
+        for (int x = 0; x < X; x++) {
+          const int64_t li = local((int64_t)gy * X + x);
+          for (int k = 3; k <= 6; k++) {
+            if (q.geometry == AVGPU_RES_GRID) {
+              if ((k == 3 || k == 4) && x == X - 1) continue;
+              if (k == 6 && x == 0) continue;
+              if (k != 3 && gy == Yg - 1) continue;
+            }
+            const int ny = amod(gy + dyk[k], Yg), nx = amod(x + dxk[k], X);
+            const int64_t lii = local((int64_t)ny * X + nx);
+            if (li < 0 && lii < 0) continue;
+            double sink1 = 0.0, sink2 = 0.0;
+            flow_matter(amount(gy, x), amount(ny, nx), li >= 0 ? d[li] : sink1, lii >= 0 ? d[lii] : sink2,
+                        q, dxk[k], dyk[k], (k == 4 || k == 6) ? SQRT2 : 1.0);
           }
-          const int64_t ii = (int64_t)amod(y + dyk[k], Y) * X + amod(x + dxk[k], X);
-          flow_matter(amt[i], amt[ii], d[i], d[ii], q, dxk[k], dyk[k], (k == 4 || k == 6) ? SQRT2 : 1.0);
         }
-      }
     }
     // StateAll
     for (int64_t i = 0; i < n; i++) { amt[i] += d[i]; d[i] = 0.0; }
@@ -1405,6 +1453,41 @@ int orc_set_tile(void* h, int64_t row0, int64_t arena) {
   if (arena <= 0) arena = std::max<int64_t>(256 * 1024, X * 256);
   w.row0 = row0; w.rows = rows; w.tiled = rows < w.global_rows; w.cell0 = row0 * X;
   w.r_arena = (arena + 15) / 16 * 16;
+  if (!w.res.empty()) res_init(w);   // this strip's share of the initial amounts
+  return 0;
+}
+
+int orc_tile_res_bytes(void* h, int64_t* bytes) {
+  World& w = *(World*)h;
+  if (bytes) *bytes = (int64_t)w.n_spatial * w.cfg.world_x * 8;
+  return 0;
+}
+
+int orc_set_tile_res_buffers(void* h, void* send_up, void* send_down, void* recv_up, void* recv_down) {
+  World& w = *(World*)h;
+  if (!w.tiled) return fail(AVGPU_ESTATE, "not a strip tile");
+  w.rs_send[0] = (double*)send_up; w.rs_send[1] = (double*)send_down;
+  w.rs_recv[0] = (double*)recv_up; w.rs_recv[1] = (double*)recv_down;
+  return 0;
+}
+
+// the update's consumption of the global pools by this strip (2^-32 units)
+int orc_tile_res_cons(void* h, uint64_t* out) {
+  World& w = *(World*)h;
+  int g = 0;
+  for (int r = 0; r < AVGPU_MAX_RESOURCES; r++) out[r] = 0;
+  for (size_t r = 0; r < w.res.size(); r++) {
+    out[r] = w.res_cons[r];
+    g += w.res[r].geometry == AVGPU_RES_GLOBAL;
+  }
+  return g;
+}
+
+// subtract every strip's consumption (summed over the strips): res_end
+int orc_tile_res_settle(void* h, const uint64_t* sum) {
+  World& w = *(World*)h;
+  for (size_t r = 0; r < w.res.size(); r++) w.res_cons[r] = sum[r];
+  res_end(w);
   return 0;
 }
 
@@ -1446,6 +1529,17 @@ int orc_tile_partials(void* h, double* out) {
     out[b] = s[0];
     out[nb + b] = (double)cnt;
   }
+  // edge rows of the spatial amounts for the neighbours' flow step
+  const int X = w.cfg.world_x;
+  if (w.tiled && w.rs_send[0])
+    for (size_t r = 0; r < w.res.size(); r++) {
+      const int slot = w.res_slot[r];
+      if (slot < 0) continue;
+      for (int x = 0; x < X; x++) {
+        w.rs_send[0][(int64_t)slot * X + x] = w.res_amount[r][x];
+        w.rs_send[1][(int64_t)slot * X + x] = w.res_amount[r][(w.rows - 1) * X + x];
+      }
+    }
   return 0;
 }
 
@@ -1467,6 +1561,8 @@ int orc_tile_begin(void* h, const double* gathered, int ntiles) {
   }
   for (int stride = 128; stride >= 1; stride >>= 1)
     for (int i = 0; i < stride; i++) lane[i] = lane[i] + lane[i + stride];
+  if (w.n_spatial && !w.rs_recv[0]) return fail(AVGPU_ESTATE, "spatial resources need the tile resource buffers");
+  res_begin(w);
   allot_interpret(w, lane[0], cnt);
   const int X = w.cfg.world_x;
   const int64_t ext = w.ncells + 2 * X, nbirth = (int64_t)w.births.size();

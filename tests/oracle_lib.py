@@ -49,6 +49,7 @@ class Backend:
             if not self.h:
                 raise RuntimeError(self.lib.avgpu_last_error().decode())
         self.cfg = cfg
+        self.ncells = ncells or cfg.world_x * cfg.world_y
         self.instset = instset
         hid = (C.c_uint8 * len(instset.names))(*instset.handlers)
         red = (C.c_int32 * len(instset.names))(*instset.redundancy)
@@ -125,7 +126,7 @@ class Backend:
     def resources(self, spatial=False):
         """(levels, per-cell grids or None): avgpu_get_resources"""
         nres = self.nres
-        n = self.cfg.world_x * self.cfg.world_y
+        n = self.ncells
         lv = (C.c_double * max(1, nres))()
         sp = (C.c_double * max(1, nres * n))() if spatial else None
         self._call("get_resources", self.h, lv, sp)

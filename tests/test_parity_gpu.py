@@ -195,3 +195,38 @@ def test_world_updates_resources_bit_exact(golden, variant):
     bad = pu.diff_states(a, b, oa, ob, fa, fb, CAP)
     assert not bad, f"{len(bad)} mismatches: {bad[:5]}"
     assert so.num_organisms > 200
+
+
+@pytest.mark.parametrize("T,geometry", [(2, 2), (4, 1)])
+def test_gpu_strip_tiles_with_resources(golden, T, geometry):
+    """Config 5's path on one GPU: T strips with spatial resources (flows,
+    inflow box and CELL list across strip edges, edge rows exchanged) and a
+    consumed global pool (consumption all-reduced) == the untiled oracle world:
+    organisms, per-cell amounts and pool levels bit for bit, every update."""
+    import torch
+    from avida_amd import tiles
+    import tile_util as tu
+    from test_tiles import resource_grids_match
+    X, Y, U = 64, 64, 30
+    env = tu.resource_env(golden)
+    per_update = []
+    ref, rstats = tu.single("oracle", golden, X, Y, U, geometry=geometry, env=env,
+                            on_update=lambda u, b: per_update.append(b.resources(spatial=True)))
+    pairs = [tu.make_tile("gpu", golden, X, Y, T, k, geometry=geometry, device="cuda", env=env)
+             for k in range(T)]
+    world = tiles.StripWorld([t for _, t in pairs], tiles.LoopbackTransport())
+    for u in range(U):
+        world.update()
+        torch.cuda.synchronize()
+        tot = [tu.tile_stats(b) for b, _ in pairs]
+        for f in ("num_organisms", "insts_executed", "births", "deaths", "divides"):
+            assert sum(getattr(s, f) for s in tot) == getattr(rstats[u], f), (u, f)
+        resource_grids_match(per_update[u], [b for b, _ in pairs], T, X, Y)
+    a, oa, fa = ref.states(0, X * Y, CAP)
+    per = X * Y // T
+    for k, (b, _) in enumerate(pairs):
+        s, o, f = b.states(0, per, CAP)
+        lo = k * per
+        bad = pu.diff_states(a[lo:lo + per], s, oa[lo * CAP:(lo + per) * CAP], o,
+                             fa[lo * CAP:(lo + per) * CAP], f, CAP)
+        assert not bad, f"tile {k}: {len(bad)} mismatches, first {bad[:3]}"

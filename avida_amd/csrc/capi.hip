@@ -495,7 +495,7 @@ int avgpu_load_env(avgpu_world* w, int nreact, const avgpu_reaction* r) {
   double rr[AVGPU_MAX_REACTIONS * RR_STRIDE];
   memset(rr, 0, sizeof(rr));
   int uses = 0;
-  uint32_t res_seen = 0;
+  uint32_t res_seen = 0, res_mask = 0;
   for (int i = 0; i < nreact; i++) {
     const int res = r[i].resource;       // 1 + index, 0 = infinite
     if (res == 0) continue;
@@ -513,9 +513,10 @@ int avgpu_load_env(avgpu_world* w, int nreact, const avgpu_reaction* r) {
     q[RR_MAX] = r[i].max_number;
     q[RR_VALUE] = r[i].value;
     uses++;
+    res_mask |= 1u << i;
   }
-  if (uses) simple = false;
   W.env_resources = uses ? 1 : 0;
+  W.env_res_mask = simple ? res_mask : 0u;   // the simple path indexes reactions by task
   HIPCHK(hipMemcpyAsync(W.react_res, rr, sizeof(rr), hipMemcpyHostToDevice, w->stream));
   W.env_simple = simple ? 1 : 0;
   W.env_react_mask = rmask;
@@ -581,6 +582,14 @@ int avgpu_step(avgpu_world* w, int64_t first, int64_t count, const int32_t* budg
   return rc;
 }
 
+// after launch_world_pre: the spatial step wrote res_amount_alt; later
+// launches read the new amounts
+static void after_resources_begin(avgpu_world* w) {
+  DevWorld& W = w->W;
+  if (res_stepped(W)) std::swap(W.res_amount, W.res_amount_alt);
+  W.res_first = 0;
+}
+
 int avgpu_update_totals(avgpu_world* w, double* dev_totals) {
   int rc = ready(w);
   if (rc < 0) return rc;
@@ -595,7 +604,7 @@ int avgpu_update_run(avgpu_world* w, const double* dev_totals, avgpu_update_stat
   if (rc < 0) return rc;
   if (!dev_totals) return fail(AVGPU_EINVAL, "dev_totals is NULL");
   launch_world_pre(w->W, w->stream, dev_totals);
-  w->W.res_first = 0;
+  after_resources_begin(w);
   HIPCHK(hipGetLastError());
   rc = interpret(w, AVGPU_MODE_WORLD, 0, w->W.n, true);
   if (rc < 0) return rc;
@@ -856,14 +865,21 @@ int avgpu_load_resources(avgpu_world* w, int nres, const avgpu_resource* res, in
     w->res_geom[r] = q.geometry;
     W.res_spatial_host[r] = q.geometry != AVGPU_RES_GLOBAL;
     W.res_flows_host[r] = (int8_t)p.flows;
+    W.res_cells_host[r] = 0;
   }
-  for (int i = 0; i < ncell; i++)
+  for (int i = 0; i < ncell; i++) {
     if (cells[i].resource < 0 || cells[i].resource >= nres || res[cells[i].resource].geometry == AVGPU_RES_GLOBAL)
       return fail(AVGPU_EINVAL, "CELL entry names a resource that is not spatial");
+    W.res_cells_host[cells[i].resource] = 1;
+  }
   const int64_t n = W.n;
+  if ((int64_t)W.world_x * W.world_y >= (int64_t)1 << 31)
+    return fail(AVGPU_EUNSUPPORTED, "resources need fewer than 2^31 cells in the world");
   if (nsp && !W.res_amount) {
     HIPCHK(hipMalloc(&W.res_amount, (size_t)AVGPU_MAX_RESOURCES * n * sizeof(double)));
     w->allocs.push_back(W.res_amount);
+    HIPCHK(hipMalloc(&W.res_amount_alt, (size_t)AVGPU_MAX_RESOURCES * n * sizeof(double)));
+    w->allocs.push_back(W.res_amount_alt);
     HIPCHK(hipMalloc(&W.res_delta, (size_t)n * sizeof(double)));
     w->allocs.push_back(W.res_delta);
   }
@@ -1019,7 +1035,7 @@ int avgpu_tile_begin(avgpu_world* w, const double* dev_gathered, int ntiles) {
   if (!dev_gathered || ntiles < 1) return fail(AVGPU_EINVAL, "gathered partials");
   launch_tile_totals(w->W, w->stream, dev_gathered, ntiles, w->d_totals);
   launch_world_pre(w->W, w->stream, w->d_totals);
-  w->W.res_first = 0;
+  after_resources_begin(w);
   HIPCHK(hipGetLastError());
   rc = interpret(w, AVGPU_MODE_WORLD, 0, w->W.n, true);
   if (rc < 0) return rc;

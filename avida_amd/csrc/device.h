@@ -149,6 +149,7 @@ struct DevWorld {
   int32_t env_simple;
   uint32_t env_react_mask;   // tasks with a reaction
   uint32_t env_once_mask;    // tasks whose reaction has max_count 1
+  uint32_t env_res_mask;     // reactions drawing on a finite resource
   double* task_tab;          // [32]: bonus factor of task t's reaction, then its addend
   // ---- resources (resources.hip; DESIGN.md "Resources") ----
   int32_t n_res, n_cellres, env_resources;   // env_resources: some reaction consumes a resource
@@ -161,6 +162,8 @@ struct DevWorld {
   double* react_res;            // [AVGPU_MAX_REACTIONS][RR_STRIDE] resource-bound process settings
   int8_t res_spatial_host[AVGPU_MAX_RESOURCES];   // host-side launch flags
   int8_t res_flows_host[AVGPU_MAX_RESOURCES];
+  int8_t res_cells_host[AVGPU_MAX_RESOURCES];     // resource has CELL entries
+  double* res_amount_alt;       // [n_spatial][n] the other buffer of the spatial step
   int8_t res_first;             // host: the next update is the first since the load
   int32_t n_spatial;            // spatial resources (rows of res_amount)
   double* rs_send[2];           // strip tiles: [n_spatial][X] first / last row out
@@ -389,6 +392,7 @@ void launch_world_pre(const DevWorld& W, hipStream_t s, const double* d_totals);
 void launch_resources_begin(const DevWorld& W, hipStream_t s);
 void launch_resources_end(const DevWorld& W, hipStream_t s);
 void launch_resources_pack(const DevWorld& W, hipStream_t s);
+bool res_stepped(const DevWorld& W);   // launch_resources_begin wrote res_amount_alt
 void launch_resources_settle(const DevWorld& W, hipStream_t s, const unsigned long long* sum);
 void launch_world_post(const DevWorld& W, hipStream_t s, double* d_stats);
 void launch_classify_uniform(const DevWorld& W, hipStream_t s, int64_t first, int64_t count,

@@ -72,6 +72,33 @@ __device__ __forceinline__ int wave_sum_i32(int v) {
 //
 // One 64-organism chunk: class 0 = cells first + 64*chunk + lane (dense
 // sweep), classes 1..3 = entries 64*chunk + lane of the class list.
+// cEnvironment::DoProcesses, finite resource (main/cEnvironment.cc:1660-1724):
+// the organism's own cell (spatial; ModifyCell applies at once) or the
+// update's global level (consumption summed in 2^-32 units, subtracted at the
+// update's end).  Returns whether the process paid (rc counts it).
+__device__ __forceinline__ bool consume_resource(const DevWorld& W, const double* rr, int64_t N, int64_t cell,
+                                                 double& mult, double& addb) {
+  const int slot = (int)rr[RR_RES] - 1;
+  const bool spatial = rr[RR_SPATIAL] != 0.0;
+  double* cellp = W.res_amount + (int64_t)W.res_param[slot].slot * N + cell;
+  const double level = spatial ? *cellp : W.res_global[slot];
+  double consumed = (level == 0.0) ? 0.0 : __dmul_rn(level, rr[RR_FRAC]);
+  if (consumed > rr[RR_MAX]) consumed = rr[RR_MAX];
+  if (consumed < rr[RR_MIN]) consumed = 0.0;
+  if (consumed == 0.0) return false;
+  consumed = fmin(consumed, level);
+  if (rr[RR_DEPL] != 0.0) {
+    if (spatial) *cellp = __dsub_rn(level, consumed);
+    else atomicAdd(W.res_cons + slot, (unsigned long long)__dmul_rn(consumed, RES_FIX));
+  }
+  const double bon = __dmul_rn(consumed, rr[RR_VALUE]);
+  const int ty = (int)rr[RR_TYPE];
+  if (ty == AVGPU_PROC_ADD) addb = __dadd_rn(addb, bon);
+  else if (ty == AVGPU_PROC_MULT) mult = __dmul_rn(mult, bon);
+  else mult = __dmul_rn(mult, det_exp2(bon));
+  return true;
+}
+
 template <int S>
 __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp, int cls, int mode,
                                                 int64_t first, int64_t count, int64_t chunk,
@@ -253,6 +280,7 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
   const int k_rand_total = W.rand_total, k_n_ops = W.n_ops, k_n_react = W.n_react;
   const int k_env_simple = W.env_simple, k_max_label_exe = W.max_label_exe;
   const int k_env_resources = W.env_resources;
+  const uint32_t k_env_res_mask = W.env_res_mask;
   const uint32_t k_env_react_mask = W.env_react_mask, k_env_once_mask = W.env_once_mask;
   // cInstSet::GetRandomInst (cpu/cInstSet.cc:83-88) from the LDS tables
   auto rand_code = [&]() -> uint8_t {
@@ -484,15 +512,20 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
           const uint32_t done = tmask & k_env_react_mask & ~(k_env_once_mask & nzm);
           if (done) {
             double mult = 1.0, addb = 0.0;
+            uint32_t paid = done;
             for (uint32_t d = done; d; d &= d - 1u) {
               const int t = __ffs(d) - 1;
-              mult = __dmul_rn(mult, tmul[t]);
-              addb = __dadd_rn(addb, tadd[t]);
+              if ((k_env_res_mask >> t) & 1u) {                 // finite resource (general path below)
+                if (!consume_resource(W, W.react_res + t * RR_STRIDE, N, cell, mult, addb)) paid &= ~(1u << t);
+              } else {
+                mult = __dmul_rn(mult, tmul[t]);
+                addb = __dadd_rn(addb, tadd[t]);
+              }
             }
 #pragma unroll
             for (int q = 0; q < AVGPU_NUM_LOGIC_TASKS; q++) {
               tc[q] += (done >> q) & 1u;
-              rc[q] += (done >> q) & 1u;
+              rc[q] += (paid >> q) & 1u;
             }
             nzm |= done;
             bonus = __dadd_rn(__dmul_rn(bonus, mult), addb);   // cPhenotype.cc:1645-1646
@@ -519,29 +552,8 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
                 else
                   mult = __dmul_rn(mult, *reinterpret_cast<const double*>(rt + RT_MULT));
                 rc[i]++;
-              } else {
-                // cEnvironment::DoProcesses finite resource (main/cEnvironment.cc:1660-1724):
-                // the organism's own cell (spatial) or the update's global level
-                const int slot = (int)rr[RR_RES] - 1;
-                const bool spatial = rr[RR_SPATIAL] != 0.0;
-                double* cellp = W.res_amount + (int64_t)slot * N + cell;
-                const double level = spatial ? *cellp : W.res_global[slot];
-                double consumed = (level == 0.0) ? 0.0 : __dmul_rn(level, rr[RR_FRAC]);
-                if (consumed > rr[RR_MAX]) consumed = rr[RR_MAX];
-                if (consumed < rr[RR_MIN]) consumed = 0.0;
-                if (consumed != 0.0) {
-                  consumed = fmin(consumed, level);
-                  if (rr[RR_DEPL] != 0.0) {
-                    if (spatial) *cellp = __dsub_rn(level, consumed);   // ModifyCell: applied at once
-                    else atomicAdd(W.res_cons + slot, (unsigned long long)__dmul_rn(consumed, RES_FIX));
-                  }
-                  const double bon = __dmul_rn(consumed, rr[RR_VALUE]);
-                  const int ty = (int)rr[RR_TYPE];
-                  if (ty == AVGPU_PROC_ADD) addb = __dadd_rn(addb, bon);
-                  else if (ty == AVGPU_PROC_MULT) mult = __dmul_rn(mult, bon);
-                  else mult = __dmul_rn(mult, det_exp2(bon));
-                  rc[i]++;
-                }
+              } else if (consume_resource(W, rr, N, cell, mult, addb)) {
+                rc[i]++;
               }
             }
           }

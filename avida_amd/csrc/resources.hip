@@ -1,19 +1,28 @@
 // resources.hip -- environment resources around the interpreter (config 5):
-//   k_res_spatial_rates  cSpatialResCount::Source + Sink      (main/cSpatialResCount.cc:341-394)
-//   k_res_cell_rates     CellInflow + CellOutflow              (:356-404), list order, one thread
-//   k_res_flow           FlowAll / FlowMatter                  (:323-338, main/cResourceCount.cc:40-110)
-//   k_res_state          StateAll                              (:307-314)
+//   k_res_step<true>     one cSpatialResCount step of a resource, fused:
+//                        Source + Sink (main/cSpatialResCount.cc:341-394),
+//                        FlowAll / FlowMatter (:323-338, main/cResourceCount.cc:40-110),
+//                        StateAll (:307-314), double-buffered
+//   k_res_spatial_rates  Source + Sink into res_delta  } resources with CELL
+//   k_res_cell_rates     CellInflow + CellOutflow      } entries: then
+//                        (:356-404), list order        } k_res_step<false>
 //   k_res_global_begin   DoNonSpatialUpdates over one update   (main/cResourceCount.cc:757-827)
 //   k_res_global_end     the update's consumption of global resources
+//   k_res_pack / k_res_settle   strip tiles: edge rows out; summed consumption in
 // Every per-cell sum is formed in the reference's order (the sequential loops
 // of cSpatialResCount add into a cell's delta in increasing index of the cell
 // doing the computing), so the device agrees bit for bit with the oracle's
-// literal restatement of those loops (oracle/oracle.cc res_spatial_step).
+// literal restatement of those loops (oracle/oracle.cc res_begin).
 #include "device.h"
 
 #pragma clang fp contract(off)
 
 namespace {
+
+// x + d for |d| <= 1 wrapped into [0, L): amod without the division
+__device__ __forceinline__ int wrap1(int x, int L) {
+  return x >= L ? x - L : (x < 0 ? x + L : x);
+}
 
 __device__ __forceinline__ int amod(int x, int y) {   // AvidaTools::Mod
   x %= y;
@@ -67,28 +76,31 @@ __global__ void k_res_cell_rates(DevWorld W, int r) {
   }
 }
 
-// FlowMatter (main/cResourceCount.cc:40-110) from elem1 = a1 to elem2 = a2
+// FlowMatter (main/cResourceCount.cc:40-110) from elem1 = a1 to elem2 = a2.
+// Exact rewrites: x / 16 == x * 0.0625 and x / 2 == x * 0.5 (power-of-two
+// divisors: the same real value, so the same rounding), and with zero gravity
+// the reference's (-a2 * 0) / 3 is the signed zero (-a2 * 0) itself.
+__device__ __forceinline__ double gravity_term(double a1, double a2, int dist, double g) {
+  if (g == 0.0) return __dmul_rn(-a2, 0.0);
+  if ((dist > 0 && g > 0.0) || (dist < 0 && g < 0.0)) return __ddiv_rn(__dmul_rn(a1, fabs(g)), 3.0);
+  return __ddiv_rn(__dmul_rn(-a2, fabs(g)), 3.0);
+}
+
 __device__ __forceinline__ double flow_amt(const ResParam& P, double a1, double a2, int xdist, int ydist,
-                                           double dist) {
+                                           bool diagonal) {
   const double diff = __dsub_rn(a1, a2);
   double xg = 0.0, xd = 0.0, yg = 0.0, yd = 0.0;
   if (xdist != 0) {
-    if ((xdist > 0 && P.xgravity > 0.0) || (xdist < 0 && P.xgravity < 0.0))
-      xg = __ddiv_rn(__dmul_rn(a1, fabs(P.xgravity)), 3.0);
-    else
-      xg = __ddiv_rn(__dmul_rn(-a2, fabs(P.xgravity)), 3.0);
-    xd = __ddiv_rn(__dmul_rn(P.xdiffuse, diff), 16.0);
+    xg = gravity_term(a1, a2, xdist, P.xgravity);
+    xd = __dmul_rn(__dmul_rn(P.xdiffuse, diff), 0.0625);
   }
   if (ydist != 0) {
-    if ((ydist > 0 && P.ygravity > 0.0) || (ydist < 0 && P.ygravity < 0.0))
-      yg = __ddiv_rn(__dmul_rn(a1, fabs(P.ygravity)), 3.0);
-    else
-      yg = __ddiv_rn(__dmul_rn(-a2, fabs(P.ygravity)), 3.0);
-    yd = __ddiv_rn(__dmul_rn(P.ydiffuse, diff), 16.0);
+    yg = gravity_term(a1, a2, ydist, P.ygravity);
+    yd = __dmul_rn(__dmul_rn(P.ydiffuse, diff), 0.0625);
   }
   const double num = __dadd_rn(__dadd_rn(__dadd_rn(xd, yd), xg), yg);
-  const double den = __dadd_rn(fabs((double)xdist), fabs((double)ydist));
-  return __ddiv_rn(__ddiv_rn(num, den), dist);
+  const double q = diagonal ? __dmul_rn(num, 0.5) : num;        // / (|xdist| + |ydist|)
+  return diagonal ? __ddiv_rn(q, 1.4142135623730951) : q;       // / dist (sqrt(2.0) or 1)
 }
 
 // pointer k = 3..6 of cell (x, y): E, SE, S, SW (cSpatialResCount::SetPointers)
@@ -100,8 +112,8 @@ __device__ __forceinline__ bool res_ptr(int geometry, int X, int Y, int x, int y
     if (k == 6 && x == 0) return false;
     if (k != 3 && y == Y - 1) return false;
   }
-  nx = amod(x + dx, X);
-  ny = amod(y + dy, Y);
+  nx = wrap1(x + dx, X);
+  ny = wrap1(y + dy, Y);
   return true;
 }
 
@@ -110,58 +122,80 @@ __device__ __forceinline__ bool res_ptr(int geometry, int X, int Y, int x, int y
 __device__ __forceinline__ double res_at(const DevWorld& W, const double* amt, int slot, int gx, int gy) {
   const int ly = gy - W.row0;
   if (ly >= 0 && ly < W.rows) return amt[(int64_t)ly * W.world_x + gx];
-  const int up = amod(W.row0 - 1, W.world_y);
+  const int up = wrap1(W.row0 - 1, W.world_y);
   return (gy == up ? W.rs_recv[0] : W.rs_recv[1])[(int64_t)slot * W.world_x + gx];
 }
 
-// FlowAll: cell c's delta gets -flow for its own pointers 3..6 and +flow from
+template <int I, int J>
+__device__ __forceinline__ void cswap(int64_t (&key)[8], double (&val)[8]) {
+  if (key[J] < key[I]) {
+    const int64_t tk = key[I]; key[I] = key[J]; key[J] = tk;
+    const double tv = val[I]; val[I] = val[J]; val[J] = tv;
+  }
+}
+
+// One DoSpatialUpdates step of resource r for cell c, double-buffered
+// (res_amount -> res_amount_alt): the cell's rate is Source + Sink (FUSED; or
+// res_delta after k_res_spatial_rates + k_res_cell_rates when r has CELL
+// entries), then FlowAll -- -flow for its own pointers 3..6 and +flow from
 // every cell whose pointer 3..6 is c, added in increasing (computing cell, k)
-// order (global cell ids) like the reference's loop over i
-__global__ void k_res_flow(DevWorld W, int r) {
-  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+// order of global cell ids like the reference's loop over i (an 8-entry
+// sorting network keeps the order in registers) -- then StateAll.
+template <bool FUSED>
+__global__ void k_res_step(DevWorld W, int r) {
+  const int c = (int)(blockIdx.x * blockDim.x + threadIdx.x);   // n < 2^31 (avgpu_load_resources)
   if (c >= W.n) return;
   const ResParam P = W.res_param[r];
   const int X = W.world_x, Y = W.world_y;
   const double* amt = W.res_amount + (int64_t)P.slot * W.n;
-  const int x = (int)(c % X), y = W.row0 + (int)(c / X);
-  const int64_t gc = (int64_t)y * X + x;
+  const int ly = (int)((unsigned)c / (unsigned)X), x = c - ly * X, y = W.row0 + ly;
   const double a_c = amt[c];
-  const double SQRT2 = 1.4142135623730951;   // sqrt(2.0)
-  int64_t key[8];
-  double val[8];
-  int m = 0;
-  for (int k = 3; k <= 6; k++) {                       // own pointers
-    int nx, ny;
-    if (!res_ptr(P.geometry, X, Y, x, y, k, nx, ny)) continue;
-    const int xd = (k == 3 || k == 4) ? 1 : (k == 5 ? 0 : -1), yd = (k == 3) ? 0 : 1;
-    key[m] = gc * 8 + k;
-    val[m] = -flow_amt(P, a_c, res_at(W, amt, P.slot, nx, ny), xd, yd, (k == 4 || k == 6) ? SQRT2 : 1.0);
-    m++;
-  }
-  for (int k = 3; k <= 6; k++) {                       // cells whose pointer k is c
-    const int dx = (k == 3 || k == 4) ? 1 : (k == 5 ? 0 : -1), dy = (k == 3) ? 0 : 1;
-    const int jx = amod(x - dx, X), jy = amod(y - dy, Y);
-    int nx, ny;
-    if (!res_ptr(P.geometry, X, Y, jx, jy, k, nx, ny) || nx != x || ny != y) continue;
-    key[m] = ((int64_t)jy * X + jx) * 8 + k;
-    val[m] = flow_amt(P, res_at(W, amt, P.slot, jx, jy), a_c, dx, dy, (k == 4 || k == 6) ? SQRT2 : 1.0);
-    m++;
-  }
-  for (int a = 1; a < m; a++)                          // insertion sort by (cell, k)
-    for (int b = a; b > 0 && key[b - 1] > key[b]; b--) {
-      const int64_t tk = key[b]; key[b] = key[b - 1]; key[b - 1] = tk;
-      const double tv = val[b]; val[b] = val[b - 1]; val[b - 1] = tv;
+  double d;
+  if (FUSED) {
+    d = 0.0;
+    const int nin = cover(y, P.in_y1, P.in_y2, Y) * cover(x, P.in_x1, P.in_x2, X);
+    for (int k = 0; k < nin; k++) d = __dadd_rn(d, P.in_share);
+    if (P.has_sink) {
+      const int nout = cover(y, P.out_y1, P.out_y2, Y) * cover(x, P.out_x1, P.out_x2, X);
+      const double dec = fmax(__dmul_rn(a_c, P.sink_frac), 0.0);
+      for (int k = 0; k < nout; k++) d = __dadd_rn(d, -dec);
     }
-  double d = W.res_delta[c];
-  for (int a = 0; a < m; a++) d = __dadd_rn(d, val[a]);
-  W.res_delta[c] = d;
-}
-
-__global__ void k_res_state(DevWorld W, int r) {
-  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= W.n) return;
-  double* a = W.res_amount + (int64_t)W.res_param[r].slot * W.n + c;
-  *a = __dadd_rn(*a, W.res_delta[c]);
+  } else {
+    d = W.res_delta[c];
+  }
+  if (P.flows) {
+    const int64_t gc = (int64_t)y * X + x;
+    int64_t key[8];
+    double val[8];
+#pragma unroll
+    for (int k = 3; k <= 6; k++) {                     // own pointers: slots 0..3
+      const int dx = (k == 3 || k == 4) ? 1 : (k == 5 ? 0 : -1), dy = (k == 3) ? 0 : 1;
+      int nx, ny;
+      const bool ok = res_ptr(P.geometry, X, Y, x, y, k, nx, ny);
+      key[k - 3] = ok ? gc * 8 + k : INT64_MAX;
+      val[k - 3] = ok ? -flow_amt(P, a_c, res_at(W, amt, P.slot, nx, ny), dx, dy, k == 4 || k == 6) : 0.0;
+    }
+#pragma unroll
+    for (int k = 3; k <= 6; k++) {                     // cells whose pointer k is c: slots 4..7
+      const int dx = (k == 3 || k == 4) ? 1 : (k == 5 ? 0 : -1), dy = (k == 3) ? 0 : 1;
+      const int jx = wrap1(x - dx, X), jy = wrap1(y - dy, Y);
+      int nx, ny;
+      const bool ok = res_ptr(P.geometry, X, Y, jx, jy, k, nx, ny) && nx == x && ny == y;
+      key[k + 1] = ok ? ((int64_t)jy * X + jx) * 8 + k : INT64_MAX;
+      val[k + 1] = ok ? flow_amt(P, res_at(W, amt, P.slot, jx, jy), a_c, dx, dy, k == 4 || k == 6) : 0.0;
+    }
+    // Batcher odd-even merge sort of 8 (19 compare-exchanges)
+    cswap<0, 1>(key, val); cswap<2, 3>(key, val); cswap<4, 5>(key, val); cswap<6, 7>(key, val);
+    cswap<0, 2>(key, val); cswap<1, 3>(key, val); cswap<4, 6>(key, val); cswap<5, 7>(key, val);
+    cswap<1, 2>(key, val); cswap<5, 6>(key, val);
+    cswap<0, 4>(key, val); cswap<1, 5>(key, val); cswap<2, 6>(key, val); cswap<3, 7>(key, val);
+    cswap<2, 4>(key, val); cswap<3, 5>(key, val);
+    cswap<1, 2>(key, val); cswap<3, 4>(key, val); cswap<5, 6>(key, val);
+#pragma unroll
+    for (int a = 0; a < 8; a++)
+      if (key[a] != INT64_MAX) d = __dadd_rn(d, val[a]);
+  }
+  W.res_amount_alt[(int64_t)P.slot * W.n + c] = __dadd_rn(a_c, d);
 }
 
 // one update of DoNonSpatialUpdates (main/cResourceCount.cc:814-827): 10000
@@ -217,16 +251,22 @@ static inline unsigned rblk(int64_t n) { return (unsigned)((n + 255) / 256); }
 void launch_resources_begin(const DevWorld& W, hipStream_t s) {
   if (W.n_res == 0) return;
   // spatial resources: one step of the reference's DoSpatialUpdates, in
-  // resource order (each resource owns its own grid); none in update 0
+  // resource order (each resource owns its own grid); none in update 0.  The
+  // caller swaps res_amount / res_amount_alt afterwards (res_stepped).
   for (int r = 0; r < W.n_res && !W.res_first; r++) {
     if (!W.res_spatial_host[r]) continue;
-    hipLaunchKernelGGL(k_res_spatial_rates, dim3(rblk(W.n)), dim3(256), 0, s, W, r);
-    if (W.n_cellres) hipLaunchKernelGGL(k_res_cell_rates, dim3(1), dim3(64), 0, s, W, r);
-    if (W.res_flows_host[r]) hipLaunchKernelGGL(k_res_flow, dim3(rblk(W.n)), dim3(256), 0, s, W, r);
-    hipLaunchKernelGGL(k_res_state, dim3(rblk(W.n)), dim3(256), 0, s, W, r);
+    if (W.res_cells_host[r]) {
+      hipLaunchKernelGGL(k_res_spatial_rates, dim3(rblk(W.n)), dim3(256), 0, s, W, r);
+      hipLaunchKernelGGL(k_res_cell_rates, dim3(1), dim3(64), 0, s, W, r);
+      hipLaunchKernelGGL(k_res_step<false>, dim3(rblk(W.n)), dim3(256), 0, s, W, r);
+    } else {
+      hipLaunchKernelGGL(k_res_step<true>, dim3(rblk(W.n)), dim3(256), 0, s, W, r);
+    }
   }
   hipLaunchKernelGGL(k_res_global_begin, dim3(1), dim3(64), 0, s, W, (int)W.res_first);
 }
+
+bool res_stepped(const DevWorld& W) { return W.n_spatial > 0 && !W.res_first; }
 
 void launch_resources_end(const DevWorld& W, hipStream_t s) {
   if (W.n_res == 0) return;

@@ -244,9 +244,14 @@ def read_environment(path: str):
     """REACTION name task process:... requisite:... (main/cEnvironment.cc:1185-1211),
     RESOURCE and CELL lines (:474-755).  Returns an Environment (a list of
     Reaction with .resources and .cells)."""
-    out = Environment()
     with open(path) as f:
-        text = re.sub(r"\\[ \t]*\r?\n[ \t]*", "", f.read())   # "\" joins the next line
+        return parse_environment(f.read())
+
+
+def parse_environment(text: str):
+    """read_environment on the text of an environment file"""
+    out = Environment()
+    text = re.sub(r"\\[ \t]*\r?\n[ \t]*", "", text)   # "\" joins the next line
     for raw in text.splitlines():
             line = _strip(raw)
             if not line:

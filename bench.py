@@ -59,12 +59,38 @@ def _genomes_for(n, pool, first=0):
     return [pool[int(i)] for i in idx]
 
 
-def build_world(lib, capi, files, golden, side, seed, device, rank, world, on_tile=None):
+LOGIC9 = [("NOT", "not", 1.0), ("NAND", "nand", 1.0), ("AND", "and", 2.0), ("ORN", "orn", 2.0),
+          ("OR", "or", 4.0), ("ANDN", "andn", 4.0), ("NOR", "nor", 8.0), ("XOR", "xor", 8.0),
+          ("EQU", "equ", 16.0)]
+
+
+def resource_env_text(X, Y, inflow_per_cell=1.0, outflow=0.01):
+    """configs[4]: resource-limited logic-9 -- one spatial torus resource per
+    reaction, inflow and outflow over the whole world, diffusion on; the
+    reactions follow the reference's resources_9r environment (frac=0.0025,
+    max=25, additive bonus consumed * value, values 1 1 2 2 4 4 8 8 16)"""
+    box = f"inflowx1=0:inflowx2={X - 1}:inflowy1=0:inflowy2={Y - 1}:" \
+          f"outflowx1=0:outflowx2={X - 1}:outflowy1=0:outflowy2={Y - 1}"
+    lines = [f"RESOURCE res{name}:geometry=torus:initial={X * Y * inflow_per_cell}:"
+             f"inflow={X * Y * inflow_per_cell}:outflow={outflow}:{box}:xdiffuse=1:ydiffuse=1"
+             for name, _, _ in LOGIC9]
+    lines += [f"REACTION {name} {task} process:resource=res{name}:value={v}:frac=0.0025:max=25"
+              for name, task, v in LOGIC9]
+    return "\n".join(lines) + "\n"
+
+
+def environment(files, golden, kind, X, Y):
+    if kind == "resources":
+        return files.parse_environment(resource_env_text(X, Y))
+    return files.read_environment(os.path.join(golden, "environment-logic9.cfg"))
+
+
+def build_world(lib, capi, files, golden, side, seed, device, rank, world, on_tile=None, env_kind="logic9"):
     """One 1024x1024 strip per rank of a side x (side*world) torus (world = 1:
     the untiled side x side world).  on_tile(h) places the strip before the
     organisms are injected (their RNG streams are keyed by global cell id)."""
     iset, pool = _pool(golden)
-    env = files.read_environment(os.path.join(golden, "environment-logic9.cfg"))
+    env = environment(files, golden, env_kind, side, side * world)
     cfg = capi.cfg_from_avida(files.read_avida_cfg(None, {"WORLD_X": side, "WORLD_Y": side * world}),
                               seed=seed)
     n = side * side
@@ -74,6 +100,9 @@ def build_world(lib, capi, files, golden, side, seed, device, rank, world, on_ti
     hid = (C.c_uint8 * len(iset.names))(*iset.handlers)
     red = (C.c_int32 * len(iset.names))(*iset.redundancy)
     capi.check(lib, lib.avgpu_load_instset(h, len(iset.names), hid, red))
+    if env.resources:
+        ra, ca = capi.resources_arrays(env.resources, env.cells)
+        capi.check(lib, lib.avgpu_load_resources(h, len(env.resources), ra, len(env.cells), ca))
     arr = capi.reactions_array(env)
     capi.check(lib, lib.avgpu_load_env(h, len(env), arr))
     tile = on_tile(h) if on_tile else None
@@ -86,7 +115,7 @@ def build_world(lib, capi, files, golden, side, seed, device, rank, world, on_ti
     return h, cfg, n, tile
 
 
-def cpu_baseline(golden, seconds):
+def cpu_baseline(golden, seconds, env_kind="logic9"):
     """Reference-style serial world (tests/oracle_lib.py, CPU restatement) on one
     host core: a 60x60 world filled from the same genotype pool, updates until
     `seconds` elapse."""
@@ -94,7 +123,7 @@ def cpu_baseline(golden, seconds):
     from avida_amd import capi, files
     import oracle_lib as ol
     iset, pool = _pool(golden)
-    env = files.read_environment(os.path.join(golden, "environment-logic9.cfg"))
+    env = environment(files, golden, env_kind, 60, 60)
     cfg = capi.cfg_from_avida(files.read_avida_cfg(None), seed=101)
     n = cfg.world_x * cfg.world_y
     b = ol.Backend("oracle", cfg, iset, env, ncells=n)
@@ -110,7 +139,7 @@ def cpu_baseline(golden, seconds):
     dt = time.perf_counter() - t0
     return {"value": insts / dt, "unit": "organism-instructions/s", "cores": 1, "kind": "port",
             "sample": f"oracle serial world (reference-style scheduler + speculative steps), "
-                      f"60x60 evolved logic-9 population, {updates} updates, {insts} insts, "
+                      f"60x60 evolved logic-9 population ({env_kind} environment), {updates} updates, {insts} insts, "
                       f"{dt:.1f} s on 1 host core",
             "updates_per_sec": updates / dt}
 
@@ -127,6 +156,9 @@ def main():
     ap.add_argument("--seed", type=int, default=101)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--env", choices=["logic9", "resources"], default="logic9",
+                    help="logic9: configs[2] (the metric's workload); resources: configs[4], "
+                         "one diffusing spatial resource per logic-9 reaction")
     args = ap.parse_args()
 
     import torch
@@ -151,7 +183,7 @@ def main():
         return tiles.Tile(lib, "avgpu_", h, rank * args.side, world, "cuda")
 
     h, cfg, n, tile = build_world(lib, capi, files, golden, args.side, args.seed, local, rank, world,
-                                  on_tile)
+                                  on_tile, args.env)
     strips = tiles.StripWorld([tile], tiles.DistTransport(dist)) if tile else None
 
     def update():
@@ -236,9 +268,13 @@ def main():
         "dtype": "int32",
         "data": "synthetic",
         "config": {
-            "workload": f"configs[2]: {args.side}x{args.side} torus per GPU, logic-9, default "
-                        "avida.cfg mutation rates, births on, seeded with the detail-50000.pop "
-                        "evolved genotypes (classic instset)",
+            "workload": (f"configs[2]: {args.side}x{args.side} torus per GPU, logic-9, default "
+                         "avida.cfg mutation rates, births on, seeded with the detail-50000.pop "
+                         "evolved genotypes (classic instset)") if args.env == "logic9" else
+                        (f"configs[4]: {args.side}x{args.side} torus per GPU, resource-limited logic-9 "
+                         "(9 spatial torus resources, inflow/outflow everywhere, diffusion 1), default "
+                         "mutation rates, births on, seeded with the detail-50000.pop genotypes"),
+            "environment": args.env,
             "world": f"{args.side}x{args.side}x{world}",
             "burn_in_updates": args.burn_in,
             "organisms": int(tot_orgs),
@@ -268,7 +304,7 @@ def main():
         "cpu_baseline": None,
     }
     if world == 1 and not args.no_cpu:
-        out["cpu_baseline"] = cpu_baseline(golden, args.cpu_seconds)
+        out["cpu_baseline"] = cpu_baseline(golden, args.cpu_seconds, args.env)
     lib.avgpu_destroy(h)
     print(json.dumps(out), flush=True)
     if dist:

@@ -1751,6 +1751,7 @@ int orc_run_serial_updates(void* h, int n_updates, avgpu_update_stats* out) {
     for (int64_t c = 0; c < w.ncells; c++) n_alive += w.orgs[c].alive;
     const int64_t ud = (int64_t)w.cfg.ave_time_slice * n_alive;   // cWorld::CalculateUpdateSize
     int64_t births = 0;
+    res_begin(w);   // ProcessPreUpdate + the update's first DoUpdates
     for (int64_t i = 0; i < ud; i++) {
       const double tot = sch.tree[1];
       if (!(tot > 0.0)) break;
@@ -1781,6 +1782,7 @@ int orc_run_serial_updates(void* h, int n_updates, avgpu_update_stats* out) {
       }
       w.births.clear();
     }
+    res_end(w);
     w.update++;
     (void)births;
   }

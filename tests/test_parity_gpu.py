@@ -151,23 +151,40 @@ def _resource_env(golden, variant):
     a torus ResA and a grid ResB, so FlowAll runs) or resources_9r's nine
     consumed global pools"""
     import copy
+    if variant == "bench":
+        import bench
+        return files.parse_environment(bench.resource_env_text(48, 40)), \
+            files.read_instset(os.path.join(golden, "resources_9r", "instset-heads.cfg")).parse_sequence(
+                "rucavcqgfcqapqeccthzscpcccpqcxaqnccxxbcgdutycasvab")
     if variant == "9r":
         d = os.path.join(golden, "resources_9r")
         return files.read_environment(os.path.join(d, "environment.9resource")), \
             files.read_org(os.path.join(d, "9task.org"),
                            files.read_instset(os.path.join(d, "instset-heads.cfg")))
     env = files.read_environment(os.path.join(golden, "spatial_res_100u", "environment.cfg"))
-    if variant == "flow":
+    if variant in ("flow", "diffuse"):
         env = copy.deepcopy(env)
         a, b = env.resources[0], env.resources[1]
         a.geometry, a.xdiffuse, a.ydiffuse, a.xgravity, a.ygravity = 2, 1.0, 0.5, 0.2, -0.1
         a.inflow_x1, a.inflow_x2, a.inflow_y1, a.inflow_y2 = 40, 50, 45, 52    # box wraps the torus
         b.xdiffuse, b.ydiffuse, b.xgravity, b.ygravity = 0.3, 1.0, -0.4, 0.25
+        if variant == "diffuse":     # zero gravity (one axis of ResB only)
+            a.xgravity = a.ygravity = 0.0
+            b.xgravity = 0.0
+            # the global pool first (resource index != spatial slot), drawn on by AND
+            order = [2, 0, 1]
+            env.resources[:] = [env.resources[i] for i in order]
+            for r in env:
+                if r.resource:
+                    r.resource = 1 + order.index(r.resource - 1)
+            for c in env.cells:
+                c.resource = order.index(c.resource)
+            env[2].resource, env[2].max_fraction, env[2].max_number = 1, 0.01, 5.0
     iset = files.read_instset(os.path.join(golden, "resources_9r", "instset-heads.cfg"))
     return env, iset.parse_sequence("rucavcqgfcqapqeccthzscpcccpqcxaqnccxxbcgdutycasvab")
 
 
-@pytest.mark.parametrize("variant", ["spatial", "flow", "9r"])
+@pytest.mark.parametrize("variant", ["spatial", "flow", "diffuse", "9r", "bench"])
 def test_world_updates_resources_bit_exact(golden, variant):
     """Updates with environment resources (the environment around the
     path): spatial grids, CELL lists, diffusion/gravity flows and consumed

@@ -853,6 +853,8 @@ int avgpu_load_resources(avgpu_world* w, int nres, const avgpu_resource* res, in
                   p.out_x2 != AVGPU_RES_NONE && p.out_y2 != AVGPU_RES_NONE) ? 1 : 0;
     p.xdiffuse = q.xdiffuse; p.ydiffuse = q.ydiffuse; p.xgravity = q.xgravity; p.ygravity = q.ygravity;
     p.flows = (q.xdiffuse != 0.0 || q.ydiffuse != 0.0 || q.xgravity != 0.0 || q.ygravity != 0.0) ? 1 : 0;
+    p.in_all = (p.in_x2 - p.in_x1 + 1 == W.world_x && p.in_y2 - p.in_y1 + 1 == W.world_y) ? 1 : 0;
+    p.out_all = (p.out_x2 - p.out_x1 + 1 == W.world_x && p.out_y2 - p.out_y1 + 1 == W.world_y) ? 1 : 0;
     // precalc tables (cResourceCount.cc:336-345), the reference's own loop
     const double step_decay = std::pow(decay, 1.0 / 10000.0), step_inflow = q.inflow * (1.0 / 10000.0);
     double dp = 1.0, ip = 0.0;

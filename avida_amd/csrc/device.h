@@ -48,6 +48,7 @@ struct ResParam {
   double decay100, inflow100;   // decay_precalc / inflow_precalc at PRECALC_DISTANCE (global)
   double decay99, inflow99;     // ... at 99 steps (the last block of update 0's 9999 steps)
   int32_t flows, has_sink;      // FlowAll does anything; the outflow box is set
+  int32_t in_all, out_all;      // the inflow / outflow box covers every cell exactly once
 };
 #define NUM_LISTS 7
 #define RT_STRIDE 12

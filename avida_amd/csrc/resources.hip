@@ -153,17 +153,30 @@ __global__ void k_res_step(DevWorld W, int r) {
   double d;
   if (FUSED) {
     d = 0.0;
-    const int nin = cover(y, P.in_y1, P.in_y2, Y) * cover(x, P.in_x1, P.in_x2, X);
+    const int nin = P.in_all ? 1 : cover(y, P.in_y1, P.in_y2, Y) * cover(x, P.in_x1, P.in_x2, X);
     for (int k = 0; k < nin; k++) d = __dadd_rn(d, P.in_share);
     if (P.has_sink) {
-      const int nout = cover(y, P.out_y1, P.out_y2, Y) * cover(x, P.out_x1, P.out_x2, X);
+      const int nout = P.out_all ? 1 : cover(y, P.out_y1, P.out_y2, Y) * cover(x, P.out_x1, P.out_x2, X);
       const double dec = fmax(__dmul_rn(a_c, P.sink_frac), 0.0);
       for (int k = 0; k < nout; k++) d = __dadd_rn(d, -dec);
     }
   } else {
     d = W.res_delta[c];
   }
-  if (P.flows) {
+  if (P.flows && x >= 1 && x <= X - 2 && y >= 1 && y <= Y - 2) {
+    // interior cell (either geometry): all eight flows exist and the order of
+    // their computing cells is fixed -- NW, N, NE (row above), W, then c
+    const double a_nw = res_at(W, amt, P.slot, x - 1, y - 1), a_n = res_at(W, amt, P.slot, x, y - 1);
+    const double a_ne = res_at(W, amt, P.slot, x + 1, y - 1), a_w = amt[c - 1];
+    d = __dadd_rn(d, flow_amt(P, a_nw, a_c, 1, 1, true));
+    d = __dadd_rn(d, flow_amt(P, a_n, a_c, 0, 1, false));
+    d = __dadd_rn(d, flow_amt(P, a_ne, a_c, -1, 1, true));
+    d = __dadd_rn(d, flow_amt(P, a_w, a_c, 1, 0, false));
+    d = __dadd_rn(d, -flow_amt(P, a_c, amt[c + 1], 1, 0, false));
+    d = __dadd_rn(d, -flow_amt(P, a_c, res_at(W, amt, P.slot, x + 1, y + 1), 1, 1, true));
+    d = __dadd_rn(d, -flow_amt(P, a_c, res_at(W, amt, P.slot, x, y + 1), 0, 1, false));
+    d = __dadd_rn(d, -flow_amt(P, a_c, res_at(W, amt, P.slot, x - 1, y + 1), -1, 1, true));
+  } else if (P.flows) {
     const int64_t gc = (int64_t)y * X + x;
     int64_t key[8];
     double val[8];

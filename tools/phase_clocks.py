@@ -23,7 +23,8 @@ def main():
     updates = int(sys.argv[2]) if len(sys.argv) > 2 else 10
     lib = capi.load_product(build.OUT_CLK)
     golden = os.path.join(ROOT, "tests", "golden")
-    h, cfg, n, _ = bench.build_world(lib, capi, files, golden, side, 101, 0, 0, 1)
+    env_kind = sys.argv[4] if len(sys.argv) > 4 else "logic9"
+    h, cfg, n, _ = bench.build_world(lib, capi, files, golden, side, 101, 0, 0, 1, env_kind=env_kind)
     burn = int(sys.argv[3]) if len(sys.argv) > 3 else 200
     for _ in range(burn):
         capi.check(lib, lib.avgpu_run_update(h, None))
@@ -37,7 +38,7 @@ def main():
     waves = max(1, tot[capi.CNT_WAVES])
     it = max(1, tot[capi.CNT_ITERS])
     out = {
-        "side": side, "updates": updates, "waves_per_update": waves / updates,
+        "side": side, "env": env_kind, "updates": updates, "waves_per_update": waves / updates,
         "stage_cycles_per_wave": tot[capi.CNT_CLK_STAGE] / waves,
         "loop_cycles_per_wave": tot[capi.CNT_CLK_LOOP] / waves,
         "wb_cycles_per_wave": tot[capi.CNT_CLK_WB] / waves,

@@ -119,6 +119,7 @@ struct DevWorld {
   int32_t* b_ccopied; // [rcap]
   int32_t* b_exec;    // [rcap]
   int32_t* b_gest;    // [rcap]
+  int32_t* b_ltask;   // [9][rcap] the parent's last task counts (cPhenotype::SetupOffspring :447)
   uint32_t* b_rng;    // [3][rcap]
   int32_t* b_target;  // [rcap]
   int8_t* b_state;    // [rcap]  0 pending, 1+k placed in round k, -1 failed
@@ -210,6 +211,7 @@ struct HaloRec {
   uint32_t rng_lo, rng_hi, rng_ctr;
   int32_t off, pad;
   double merit, fitness;
+  int32_t last_task[AVGPU_NUM_LOGIC_TASKS], pad2[3];   // the parent's (SetupOffspring)
 };
 __host__ __device__ inline int64_t record_bytes(int x, int64_t arena) {
   return (int64_t)sizeof(HaloHdr) + (int64_t)x * (int64_t)sizeof(HaloRec) + arena;

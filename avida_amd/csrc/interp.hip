@@ -763,10 +763,8 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
             bonus = W.default_bonus;
             cyc = 0;
 #pragma unroll
-            for (int q = 0; q < AVGPU_NUM_LOGIC_TASKS; q++) {
+            for (int q = 0; q < AVGPU_NUM_LOGIC_TASKS; q++)
               st_async_u32(W.last_task + (int64_t)q * N + cell, (uint32_t)tc[q]);
-              tc[q] = 0;
-            }
             nzm = 0;
 #pragma unroll
             for (int i = 0; i < AVGPU_MAX_REACTIONS; i++) rc[i] = 0;
@@ -815,8 +813,13 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
                 st_async_u32(W.b_rng + 2 * W.rcap + rec, 0u);
                 st_async_u8(W.b_state + rec, 0u);
                 st_async_u32(W.b_target + rec, 0xFFFFFFFFu);
+#pragma unroll
+                for (int q = 0; q < AVGPU_NUM_LOGIC_TASKS; q++)   // SetupOffspring copies them (:447)
+                  st_async_u32(W.b_ltask + (int64_t)q * W.rcap + rec, (uint32_t)tc[q]);
               }
             }
+#pragma unroll
+            for (int q = 0; q < AVGPU_NUM_LOGIC_TASKS; q++) tc[q] = 0;
             divides++;
             // parent: Resize(div), Reset (:813-900), ClearFlags (:1839); no IP advance
             M = div;
@@ -922,11 +925,7 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
         W.cur_task[(int64_t)q * N + cell] = 0;
         W.last_task[(int64_t)q * N + cell] = 0;
       }
-      if (!didv) {
-        W.child_copied[cell] = 0;
-#pragma unroll
-        for (int q = 0; q < AVGPU_NUM_LOGIC_TASKS; q++) W.last_task[(int64_t)q * N + cell] = 0;
-      }
+      if (!didv) W.child_copied[cell] = 0;   // last_task: the parent's, set at activation
     }
     // cur_reaction_count: reset at a divide, counted since (or added to the
     // stored counts when no divide happened in this slice)

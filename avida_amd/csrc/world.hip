@@ -153,9 +153,10 @@ __global__ void k_get_states(DevWorld W, int64_t first, int64_t count, avgpu_cpu
   for (int k = 0; k < 3; k++) s.inputs[k] = W.inputs[k * N + c];
   for (int k = 0; k < AVGPU_MAX_REACTIONS && !fresh; k++) {
     s.cur_task_count[k] = W.cur_task[k * N + c];
-    s.last_task_count[k] = W.last_task[k * N + c];
     s.cur_reaction_count[k] = W.cur_react[k * N + c];
   }
+  for (int k = 0; k < AVGPU_MAX_REACTIONS; k++)   // a fresh offspring's were set at activation
+    s.last_task_count[k] = (fresh && k >= AVGPU_NUM_LOGIC_TASKS) ? 0 : W.last_task[k * N + c];
   s.rng_key_lo = W.rng[c]; s.rng_key_hi = W.rng[N + c]; s.rng_counter = W.rng[2 * N + c];
   s.errors = fresh ? 0 : W.errors[c];
   s.cur_bonus = fresh ? W.default_bonus : W.cur_bonus[c];
@@ -506,6 +507,8 @@ struct Child {
   int len, gen, ccopied, exec, gest;
   double merit, fitness;
   uint32_t lo, hi, ctr;
+  const int32_t* ltask;   // the parent's last task counts, ltask[q * lstride]
+  int64_t lstride;
 };
 __device__ __forceinline__ void setup_child(const DevWorld& W, int64_t c, const Child& b,
                                             const uint32_t* src, int lane) {
@@ -537,7 +540,10 @@ __device__ __forceinline__ void setup_child(const DevWorld& W, int64_t c, const 
       W.inputs[2 * N + c] = (85 << 24) + (int)rng_below(b.lo, b.hi, ctr, 1u << 24);
       W.rng[c] = b.lo; W.rng[N + c] = b.hi; W.rng[2 * N + c] = ctr;
       break; }
-    default: break;
+    default:                                   // last_task_count = the parent's (:447)
+      if (lane >= 12 && lane < 12 + AVGPU_NUM_LOGIC_TASKS)
+        W.last_task[(int64_t)(lane - 12) * N + c] = b.ltask[(int64_t)(lane - 12) * b.lstride];
+      break;
   }
 }
 
@@ -558,6 +564,7 @@ __global__ __launch_bounds__(64) void k_activate(DevWorld W) {
     b.len = W.b_len[i]; b.gen = W.b_gen[i]; b.ccopied = W.b_ccopied[i]; b.exec = W.b_exec[i];
     b.gest = W.b_gest[i]; b.merit = W.b_merit[i]; b.fitness = W.b_fitness[i];
     b.lo = W.b_rng[i]; b.hi = W.b_rng[W.rcap + i]; b.ctr = W.b_rng[2 * W.rcap + i];
+    b.ltask = W.b_ltask + i; b.lstride = W.rcap;
     setup_child(W, tgt, b, reinterpret_cast<const uint32_t*>(W.b_genome + i * TAPE_SLOT), lane);
   }
   if (lane == 0) {
@@ -596,6 +603,9 @@ __global__ __launch_bounds__(64) void k_halo_pack(DevWorld W) {
       r.gen = W.b_gen[i]; r.ccopied = W.b_ccopied[i]; r.exec = W.b_exec[i]; r.gest = W.b_gest[i];
       r.rng_lo = W.b_rng[i]; r.rng_hi = W.b_rng[W.rcap + i]; r.rng_ctr = W.b_rng[2 * W.rcap + i];
       r.off = off; r.pad = 0; r.merit = W.b_merit[i]; r.fitness = W.b_fitness[i];
+#pragma unroll
+      for (int t = 0; t < AVGPU_NUM_LOGIC_TASKS; t++) r.last_task[t] = W.b_ltask[(int64_t)t * W.rcap + i];
+      r.pad2[0] = r.pad2[1] = r.pad2[2] = 0;
       recs[slot] = r;
       if (!fits) atomicAdd(&hdr->overflow, 1);
     }
@@ -633,6 +643,7 @@ __global__ __launch_bounds__(64) void k_activate_remote(DevWorld W, int d) {
     Child b;
     b.len = r.len; b.gen = r.gen; b.ccopied = r.ccopied; b.exec = r.exec; b.gest = r.gest;
     b.merit = r.merit; b.fitness = r.fitness; b.lo = r.rng_lo; b.hi = r.rng_hi; b.ctr = r.rng_ctr;
+    b.ltask = recs[q].last_task; b.lstride = 1;
     setup_child(W, c, b, reinterpret_cast<const uint32_t*>(arena + r.off), lane);
   }
   if (lane == 0) {
@@ -671,9 +682,8 @@ __global__ __launch_bounds__(256) void k_stats_partial(DevWorld W, double* part)
     v[5] = W.fitness[c];   // max
     v[6] = (double)W.generation[c];
     v[7] = (double)W.mem_size[c];
-    if (!(W.ctl[c] & CTL_FRESH))   // a fresh offspring has no last-gestation tasks yet
 #pragma unroll
-      for (int t = 0; t < AVGPU_NUM_LOGIC_TASKS; t++) v[8 + t] = W.last_task[t * W.n + c] > 0 ? 1.0 : 0.0;
+    for (int t = 0; t < AVGPU_NUM_LOGIC_TASKS; t++) v[8 + t] = W.last_task[t * W.n + c] > 0 ? 1.0 : 0.0;
   }
 #pragma unroll
   for (int k = 0; k < NPART; k++) {

@@ -178,6 +178,7 @@ struct Birth {
   int generation;
   int child_copied, executed, gestation_time;
   double fitness;
+  int last_task[AVGPU_NUM_LOGIC_TASKS];   // SetupOffspring copies the parent's (main/cPhenotype.cc:447)
   Stream rng;     // the child's stream
   int64_t target = -1;
   bool placed = false;
@@ -496,6 +497,7 @@ struct Exec {
       b.executed = o.executed_size;
       b.gestation_time = o.gestation_time;
       b.fitness = o.fitness;
+      for (int t = 0; t < AVGPU_NUM_LOGIC_TASKS; t++) b.last_task[t] = o.last_task[t];
       derive_key(o.rng.lo, o.rng.hi, (uint32_t)o.num_divides, 0x1B873593U, &b.rng.lo, &b.rng.hi);
       b.rng.ctr = 0;
       w.births.push_back(std::move(b));
@@ -876,6 +878,7 @@ void activate_child(World& w, Birth& b, int64_t cell) {
   o.gestation_time = b.gestation_time;
   o.fitness = b.fitness;
   o.generation = b.generation;
+  for (int t = 0; t < AVGPU_NUM_LOGIC_TASKS; t++) o.last_task[t] = b.last_task[t];
   o.rng = b.rng;
   // cEnvironment::SetupInputs random (main/cEnvironment.cc:1268-1271)
   o.inputs[0] = (15 << 24) + (int)o.rng.uint_below(1u << 24);
@@ -1432,8 +1435,9 @@ struct HaloRec {
   uint32_t rng_lo, rng_hi, rng_ctr;
   int32_t off, pad;
   double merit, fitness;
+  int32_t last_task[AVGPU_NUM_LOGIC_TASKS], pad2[3];
 };
-static_assert(sizeof(HaloRec) == 64, "HaloRec layout");
+static_assert(sizeof(HaloRec) == 112, "HaloRec layout");
 int64_t halo_bytes_of(int x) { return ((int64_t)x * 9 + 15) / 16 * 16; }
 uint64_t* hclaims(uint8_t* b) { return reinterpret_cast<uint64_t*>(b); }
 uint8_t* hocc(uint8_t* b, int x) { return b + (int64_t)x * 8; }
@@ -1648,6 +1652,8 @@ int orc_tile_place(void* h, int round, int phase) {
       r.gen = b.generation; r.ccopied = b.child_copied; r.exec = b.executed; r.gest = b.gestation_time;
       r.rng_lo = b.rng.lo; r.rng_hi = b.rng.hi; r.rng_ctr = b.rng.ctr;
       r.off = off; r.pad = 0; r.merit = b.merit; r.fitness = b.fitness;
+      for (int t = 0; t < AVGPU_NUM_LOGIC_TASKS; t++) r.last_task[t] = b.last_task[t];
+      r.pad2[0] = r.pad2[1] = r.pad2[2] = 0;
       recs[slot] = r;
       if (fits) memcpy(arena + off, b.genome.data(), len);
       else { hdr->overflow++; w.t_dropped++; }
@@ -1684,6 +1690,7 @@ int orc_tile_finish(void* h, avgpu_update_stats* out) {
       b.genome.assign(arena + r.off, arena + r.off + r.len);
       b.merit = r.merit; b.generation = r.gen; b.child_copied = r.ccopied; b.executed = r.exec;
       b.gestation_time = r.gest; b.fitness = r.fitness;
+      for (int t = 0; t < AVGPU_NUM_LOGIC_TASKS; t++) b.last_task[t] = r.last_task[t];
       b.rng.lo = r.rng_lo; b.rng.hi = r.rng_hi; b.rng.ctr = r.rng_ctr;
       activate_child(w, b, c);
       placed++;

@@ -96,6 +96,7 @@ class AvgpuCpuState(C.Structure):
         ("rng_counter", C.c_uint32), ("rng_key_lo", C.c_uint32), ("rng_key_hi", C.c_uint32),
         ("errors", C.c_int32),
         ("cur_bonus", C.c_double), ("merit", C.c_double), ("fitness", C.c_double),
+        ("credit", C.c_double),
     ]
 
 
@@ -125,7 +126,8 @@ class AvgpuUpdateStats(C.Structure):
 # C-ABI symbols declared in include/avida_gpu.h (checked by tests/test_capi.py)
 EXPORTED = [
     "avgpu_last_error", "avgpu_cfg_defaults", "avgpu_create", "avgpu_destroy", "avgpu_sync",
-    "avgpu_load_instset", "avgpu_load_env", "avgpu_load_resources", "avgpu_get_resources", "avgpu_set_org", "avgpu_set_orgs", "avgpu_kill",
+    "avgpu_load_instset", "avgpu_load_env", "avgpu_load_resources", "avgpu_get_resources",
+    "avgpu_set_resources", "avgpu_set_org", "avgpu_set_orgs", "avgpu_kill", "avgpu_set_states", "avgpu_set_clock",
     "avgpu_step", "avgpu_run_update", "avgpu_run_updates", "avgpu_update_totals",
     "avgpu_update_run", "avgpu_set_stream", "avgpu_get_states",
     "avgpu_test_genomes", "avgpu_get_stats", "avgpu_stats_vector", "avgpu_set_global_totals",
@@ -240,6 +242,10 @@ def bind_common(lib, prefix):
         "load_resources": (C.c_int, [V, C.c_int, C.POINTER(AvgpuResource), C.c_int,
                                      C.POINTER(AvgpuCellResource)]),
         "get_resources": (C.c_int, [V, C.POINTER(C.c_double), C.POINTER(C.c_double)]),
+        "set_resources": (C.c_int, [V, C.POINTER(C.c_double), C.POINTER(C.c_double)]),
+        "set_states": (C.c_int, [V, I64, I64, C.POINTER(AvgpuCpuState), C.POINTER(C.c_uint8),
+                                 C.POINTER(C.c_uint8), C.c_int]),
+        "set_clock": (C.c_int, [V, C.POINTER(AvgpuUpdateStats)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, p + name, None)

@@ -1,0 +1,75 @@
+"""Checkpoint / resume of a world through the C-ABI.
+
+The reference saves populations as genotype lists (`SavePopulation`,
+main/cPopulation.cc:6294-6600) and restarts organisms from their genomes.
+Here a checkpoint holds the whole architectural + phenotype state of every
+cell (`avgpu_get_states`: registers, heads, stacks, labels, counters, RNG
+stream position, tape with copied / executed flags), the update clock and
+cumulative counters (`avgpu_get_stats`), and the resource levels and grids
+(`avgpu_get_resources`), so a restored world continues bit for bit -- on the
+same backend or the other one (product "avgpu_" or CPU oracle "orc_").
+
+File: one `numpy.savez_compressed` archive (no pickles): `states` (raw
+avgpu_cpu_state records), `tape` (one byte per site: op | copied << 6 |
+executed << 7, `cap` bytes per cell), `stats` (raw avgpu_update_stats),
+`levels` / `grids` (resources).
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import capi
+
+
+def _call(lib, prefix, name, *args):
+    rc = getattr(lib, prefix + name)(*args)
+    if rc is not None and rc < 0:
+        msg = getattr(lib, prefix + "last_error")()
+        raise RuntimeError(f"{prefix}{name}: {msg.decode() if msg else rc}")
+    return rc
+
+
+def save(lib, prefix, handle, ncells, nres, path):
+    """Write the world behind `handle` (ncells cells, nres resources) to `path`."""
+    st = (capi.AvgpuCpuState * ncells)()
+    _call(lib, prefix, "get_states", handle, 0, ncells, st, None, None, 0)
+    cap = max([1] + [st[i].mem_size for i in range(ncells)])
+    ops = (C.c_uint8 * (ncells * cap))()
+    fl = (C.c_uint8 * (ncells * cap))()
+    _call(lib, prefix, "get_states", handle, 0, ncells, st, ops, fl, cap)
+    o = np.frombuffer(ops, dtype=np.uint8)
+    f = np.frombuffer(fl, dtype=np.uint8)
+    tape = (o & 0x3F) | ((f & 0x01) << 6) | (((f >> 2) & 0x01) << 7)
+    stats = capi.AvgpuUpdateStats()
+    _call(lib, prefix, "get_stats", handle, C.byref(stats))
+    levels = np.zeros(max(1, nres))
+    grids = np.zeros(max(1, nres * ncells))
+    if nres:
+        _call(lib, prefix, "get_resources", handle, levels.ctypes.data_as(C.POINTER(C.c_double)),
+              grids.ctypes.data_as(C.POINTER(C.c_double)))
+    np.savez_compressed(path, states=np.frombuffer(st, dtype=np.uint8), tape=tape.astype(np.uint8),
+                        cap=np.int64(cap), stats=np.frombuffer(stats, dtype=np.uint8),
+                        levels=levels[:nres], grids=grids[:nres * ncells], ncells=np.int64(ncells))
+
+
+def load(lib, prefix, handle, path):
+    """Restore a checkpoint into a world created with the same configuration,
+    instruction set and environment (resources loaded)."""
+    z = np.load(path, allow_pickle=False)
+    ncells, cap = int(z["ncells"]), int(z["cap"])
+    st = (capi.AvgpuCpuState * ncells).from_buffer_copy(z["states"].tobytes())
+    tape = z["tape"]
+    ops = np.ascontiguousarray(tape & 0x3F)
+    fl = np.ascontiguousarray(((tape >> 6) & 0x01) | (((tape >> 7) & 0x01) << 2))
+    _call(lib, prefix, "set_states", handle, 0, ncells, st, ops.ctypes.data_as(C.POINTER(C.c_uint8)),
+          fl.ctypes.data_as(C.POINTER(C.c_uint8)), cap)
+    stats = capi.AvgpuUpdateStats.from_buffer_copy(z["stats"].tobytes())
+    _call(lib, prefix, "set_clock", handle, C.byref(stats))
+    levels = np.ascontiguousarray(z["levels"], dtype=np.float64)
+    if len(levels):
+        grids = np.ascontiguousarray(z["grids"], dtype=np.float64)
+        _call(lib, prefix, "set_resources", handle, levels.ctypes.data_as(C.POINTER(C.c_double)),
+              grids.ctypes.data_as(C.POINTER(C.c_double)))
+    return stats

@@ -706,6 +706,53 @@ int avgpu_get_states(avgpu_world* w, int64_t first, int64_t count, avgpu_cpu_sta
   return 0;
 }
 
+int avgpu_set_states(avgpu_world* w, int64_t first, int64_t count, const avgpu_cpu_state* states,
+                     const uint8_t* mem_ops, const uint8_t* mem_flags, int mem_cap) {
+  int rc = ready(w);
+  if (rc < 0) return rc;
+  if (first < 0 || count < 0 || first + count > w->W.n) return fail(AVGPU_EINVAL, "cell range");
+  if (!states || !mem_ops || !mem_flags || mem_cap <= 0) return fail(AVGPU_EINVAL, "states / memory");
+  if (count == 0) return 0;
+  std::vector<uint8_t> codes((size_t)count * mem_cap, 0);
+  for (int64_t i = 0; i < count; i++) {
+    const avgpu_cpu_state& st = states[i];
+    if (st.mem_size < 0 || st.mem_size > AVGPU_MAX_GENOME || st.mem_size > mem_cap)
+      return fail(AVGPU_EINVAL, "memory size outside the tape / mem_cap");
+    for (int k = 0; k < st.mem_size; k++) {
+      const size_t o = (size_t)i * mem_cap + k;
+      if (mem_ops[o] >= w->n_ops) return fail(AVGPU_EINVAL, "op code outside the instruction set");
+      codes[o] = (uint8_t)(w->op2code[mem_ops[o]] | ((mem_flags[o] & 0x01) ? TF_COPIED : 0) |
+                           ((mem_flags[o] & 0x04) ? TF_EXEC : 0));
+    }
+  }
+  avgpu_cpu_state* d_s = nullptr;
+  uint8_t* d_c = nullptr;
+  HIPCHK(hipMalloc(&d_s, count * sizeof(avgpu_cpu_state)));
+  HIPCHK(hipMalloc(&d_c, codes.size()));
+  HIPCHK(hipMemcpyAsync(d_s, states, count * sizeof(avgpu_cpu_state), hipMemcpyHostToDevice, w->stream));
+  HIPCHK(hipMemcpyAsync(d_c, codes.data(), codes.size(), hipMemcpyHostToDevice, w->stream));
+  launch_set_states(w->W, w->stream, first, count, d_s, d_c, mem_cap);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(w->stream));
+  hipFree(d_s);
+  hipFree(d_c);
+  return 0;
+}
+
+int avgpu_set_clock(avgpu_world* w, const avgpu_update_stats* last) {
+  if (!w || !last) return fail(AVGPU_EINVAL, "args");
+  double v[2] = {(double)last->cum_insts_executed, (double)last->cum_births};
+  HIPCHK(hipMemcpyAsync(w->d_stats + 30, v, sizeof(v), hipMemcpyHostToDevice, w->stream));
+  // the running sums k_stats_final adds each update to
+  const unsigned long long ci = (unsigned long long)last->cum_insts_executed;
+  const unsigned long long cb = (unsigned long long)last->cum_births;
+  HIPCHK(hipMemcpyAsync(w->W.counters + CNT_CUM_INSTS, &ci, sizeof(ci), hipMemcpyHostToDevice, w->stream));
+  HIPCHK(hipMemcpyAsync(w->W.counters + CNT_CUM_BIRTHS, &cb, sizeof(cb), hipMemcpyHostToDevice, w->stream));
+  HIPCHK(hipStreamSynchronize(w->stream));
+  w->update = last->update + 1;
+  return 0;
+}
+
 int avgpu_test_genomes(avgpu_world* w, int n, const uint8_t* genomes, const int32_t* lens,
                        avgpu_test_result* results, char* executed_flags, int flags_cap,
                        uint8_t* offspring) {
@@ -897,6 +944,26 @@ int avgpu_load_resources(avgpu_world* w, int nres, const avgpu_resource* res, in
   w->cell_spec.assign(cells, cells + ncell);
   HIPCHK(hipMemcpyAsync(W.res_param, P, sizeof(P), hipMemcpyHostToDevice, w->stream));
   return res_seed(w);
+}
+
+int avgpu_set_resources(avgpu_world* w, const double* levels, const double* spatial) {
+  if (!w || !levels) return fail(AVGPU_EINVAL, "args");
+  DevWorld& W = w->W;
+  HIPCHK(hipStreamSynchronize(w->stream));
+  double glob[AVGPU_MAX_RESOURCES];
+  ResParam P[AVGPU_MAX_RESOURCES];
+  HIPCHK(hipMemcpy(glob, W.res_global, sizeof(glob), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(P, W.res_param, sizeof(P), hipMemcpyDeviceToHost));
+  for (int r = 0; r < W.n_res; r++) {
+    if (P[r].slot < 0) { glob[r] = levels[r]; continue; }
+    if (!spatial) return fail(AVGPU_EINVAL, "spatial resources need their grids");
+    HIPCHK(hipMemcpy(W.res_amount + (size_t)P[r].slot * W.n, spatial + (size_t)r * W.n, W.n * sizeof(double),
+                     hipMemcpyHostToDevice));
+  }
+  HIPCHK(hipMemcpy(W.res_global, glob, sizeof(glob), hipMemcpyHostToDevice));
+  HIPCHK(hipMemset(W.res_cons, 0, AVGPU_MAX_RESOURCES * sizeof(unsigned long long)));
+  W.res_first = 0;
+  return 0;
 }
 
 int avgpu_get_resources(avgpu_world* w, double* levels, double* spatial) {

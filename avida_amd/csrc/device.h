@@ -405,6 +405,8 @@ void launch_set_orgs(const DevWorld& W, hipStream_t s, int64_t first, int64_t co
                      const double* d_merits, const int32_t* d_inputs, int deterministic);
 void launch_get_states(const DevWorld& W, hipStream_t s, int64_t first, int64_t count,
                        avgpu_cpu_state* d_states, uint8_t* d_codes, int cap);
+void launch_set_states(const DevWorld& W, hipStream_t s, int64_t first, int64_t count, const avgpu_cpu_state* in,
+                       const uint8_t* codes, int cap);
 void launch_merit_total(const DevWorld& W, hipStream_t s, double* d_totals, double* d_scratch);
 // strip tiles
 void launch_tile_partials(const DevWorld& W, hipStream_t s, double* d_out);

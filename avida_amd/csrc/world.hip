@@ -162,6 +162,7 @@ __global__ void k_get_states(DevWorld W, int64_t first, int64_t count, avgpu_cpu
   s.cur_bonus = fresh ? W.default_bonus : W.cur_bonus[c];
   s.merit = W.merit[c];
   s.fitness = W.fitness[c];
+  s.credit = W.credit[c];
   out[i] = s;
   if (codes) {
     const uint8_t* t = W.tape + c * TAPE_SLOT;
@@ -169,6 +170,51 @@ __global__ void k_get_states(DevWorld W, int64_t first, int64_t count, avgpu_cpu
     const int m = s.mem_size < cap ? s.mem_size : cap;
     for (int k = 0; k < m; k++) d[k] = t[k];
   }
+}
+
+// checkpoint restore: the inverse of k_get_states; `codes` holds device codes
+// with the TF_* flag bits, cap bytes per cell
+__global__ void k_set_states(DevWorld W, int64_t first, int64_t count, const avgpu_cpu_state* in,
+                             const uint8_t* codes, int cap) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= count) return;
+  const int64_t N = W.n;
+  const int64_t c = first + i;
+  const avgpu_cpu_state s = in[i];
+  for (int k = 0; k < 3; k++) W.reg[k * N + c] = s.reg[k];
+  for (int k = 0; k < 4; k++) W.head[k * N + c] = s.head[k];
+  for (int k = 0; k < 2; k++)
+    for (int j = 0; j < AVGPU_STACK_SIZE; j++) W.stack[(k * AVGPU_STACK_SIZE + j) * N + c] = s.stack[k][j];
+  W.ctl[c] = (uint32_t)(s.stack_ptr[0] & 0xF) | ((uint32_t)(s.stack_ptr[1] & 0xF) << 4) |
+             (s.cur_stack ? CTL_CURSTK : 0u) | (s.mal_active ? CTL_MAL : 0u) | (s.alive ? CTL_ALIVE : 0u);
+  uint32_t rl = (uint32_t)(s.read_label_len & 15);
+  for (int k = 0; k < (s.read_label_len & 15) && k < AVGPU_MAX_LABEL; k++)
+    rl |= (uint32_t)(s.read_label[k] & 3) << (4 + 2 * k);
+  W.rlabel[c] = rl;
+  W.mem_size[c] = s.mem_size;
+  W.cycles[c] = s.cpu_cycles_used; W.time_used[c] = s.time_used; W.gest_start[c] = s.gestation_start;
+  W.gest_time[c] = s.gestation_time; W.num_div[c] = s.num_divides; W.generation[c] = s.generation;
+  W.birth_len[c] = s.birth_length;
+  W.copied[c] = s.copied_size; W.child_copied[c] = s.child_copied_size; W.executed[c] = s.executed_size;
+  W.max_exec[c] = s.max_executed;
+  W.in_ptr[c] = s.input_ptr;
+  for (int k = 0; k < 3; k++) W.inbuf[k * N + c] = s.input_buf[k];
+  W.in_total[c] = s.input_total;
+  W.outbuf[c] = s.output_buf; W.out_total[c] = s.output_total;
+  for (int k = 0; k < 3; k++) W.inputs[k * N + c] = s.inputs[k];
+  for (int k = 0; k < AVGPU_MAX_REACTIONS; k++) {
+    W.cur_task[k * N + c] = s.cur_task_count[k];
+    W.last_task[k * N + c] = s.last_task_count[k];
+    W.cur_react[k * N + c] = s.cur_reaction_count[k];
+  }
+  W.rng[c] = s.rng_key_lo; W.rng[N + c] = s.rng_key_hi; W.rng[2 * N + c] = s.rng_counter;
+  W.errors[c] = s.errors;
+  W.cur_bonus[c] = s.cur_bonus; W.merit[c] = s.merit; W.fitness[c] = s.fitness; W.credit[c] = s.credit;
+  W.budget[c] = 0;
+  uint8_t* t = W.tape + c * TAPE_SLOT;
+  const uint8_t* src = codes + i * cap;
+  const int m = s.mem_size < cap ? s.mem_size : cap;
+  for (int k = 0; k < m; k++) t[k] = src[k];
 }
 
 // budget = uniform or per-cell array, all live cells of [first, first+count)
@@ -769,6 +815,12 @@ void launch_set_orgs(const DevWorld& W, hipStream_t s, int64_t first, int64_t co
 void launch_get_states(const DevWorld& W, hipStream_t s, int64_t first, int64_t count,
                        avgpu_cpu_state* states, uint8_t* codes, int cap) {
   hipLaunchKernelGGL(k_get_states, dim3(nblk(count, 64)), dim3(64), 0, s, W, first, count, states,
+                     codes, cap);
+}
+
+void launch_set_states(const DevWorld& W, hipStream_t s, int64_t first, int64_t count, const avgpu_cpu_state* in,
+                       const uint8_t* codes, int cap) {
+  hipLaunchKernelGGL(k_set_states, dim3((unsigned)((count + 127) / 128)), dim3(128), 0, s, W, first, count, in,
                      codes, cap);
 }
 

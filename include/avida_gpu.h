@@ -221,6 +221,7 @@ typedef struct avgpu_cpu_state {
   double cur_bonus;
   double merit;
   double fitness;
+  double credit;                       /* INTEGRATED slicing carry (cScheduler restated) */
 } avgpu_cpu_state;
 
 /* Result of one test-CPU gestation (cpu/cTestCPU.cc:144-326 +
@@ -295,6 +296,10 @@ int avgpu_load_env(avgpu_world* w, int nreact, const avgpu_reaction* reactions);
  * update started with (the update's consumption is subtracted at its end). */
 int avgpu_load_resources(avgpu_world* w, int nres, const avgpu_resource* res, int ncell,
                          const avgpu_cell_resource* cells);
+/* checkpoint / resume: overwrite the levels (global[nres]; spatial[nres][cells]
+ * rows of spatial resources) as read by avgpu_get_resources; the next update
+ * then steps them like any later update (no update-0 rule) */
+int avgpu_set_resources(avgpu_world* w, const double* levels, const double* spatial);
 /* current levels: global[nres] (spatial resources: sum over cells, like
  * cStats::PrintResourceData main/cStats.cc:1551-1579); spatial (optional)
  * [nres][cells], zero rows for global resources */
@@ -346,6 +351,16 @@ int avgpu_set_stream(avgpu_world* w, void* hip_stream);
 int avgpu_get_states(avgpu_world* w, int64_t first_cell, int64_t count,
                      avgpu_cpu_state* states, uint8_t* mem_ops, uint8_t* mem_flags,
                      int mem_cap);
+/* checkpoint / resume: the inverse of avgpu_get_states -- cells first ..
+ * first+count-1 take states[i] and their tapes from mem_ops / mem_flags
+ * (instruction-set op codes; flags bit0 copied, bit2 executed), mem_cap bytes
+ * per cell.  A world restored from avgpu_get_states + avgpu_get_stats +
+ * avgpu_get_resources continues bit for bit (avida_amd/checkpoint.py). */
+int avgpu_set_states(avgpu_world* w, int64_t first, int64_t count, const avgpu_cpu_state* states,
+                     const uint8_t* mem_ops, const uint8_t* mem_flags, int mem_cap);
+/* checkpoint / resume: the update counter and cumulative counters of
+ * avgpu_get_stats (`last` = the stats of the checkpointed world's last update) */
+int avgpu_set_clock(avgpu_world* w, const avgpu_update_stats* last);
 /* Batched cTestCPU::TestGenome (cpu/cTestCPU.cc:190-326), one gestation
  * each, deterministic inputs, mutations off. executed_flags (n*flags_cap)
  * receives '+'/'-' for the parent part at the divide (or the whole memory

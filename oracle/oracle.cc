@@ -792,6 +792,7 @@ void dump_state(const World& w, const Org& o, avgpu_cpu_state* s, uint8_t* ops, 
   s->cur_bonus = o.cur_bonus;
   s->merit = o.merit;
   s->fitness = o.fitness;
+  s->credit = o.credit;
   (void)w;
   if (ops && flags) {
     for (int i = 0; i < cap; i++) {
@@ -984,6 +985,19 @@ int orc_load_resources(void* h, int nres, const avgpu_resource* res, int ncell,
   return 0;
 }
 
+int orc_set_resources(void* h, const double* levels, const double* spatial) {
+  World& w = *(World*)h;
+  const int64_t n = w.ncells;
+  for (size_t r = 0; r < w.res.size(); r++) {
+    if (w.res[r].geometry == AVGPU_RES_GLOBAL) { w.res_global[r] = levels[r]; continue; }
+    if (!spatial) return fail(AVGPU_EINVAL, "spatial resources need their grids");
+    std::copy(spatial + r * n, spatial + (r + 1) * n, w.res_amount[r].begin());
+  }
+  std::fill(w.res_cons.begin(), w.res_cons.end(), 0);
+  w.res_first = false;
+  return 0;
+}
+
 int orc_get_resources(void* h, double* levels, double* spatial) {
   World& w = *(World*)h;
   const int64_t n = w.ncells;
@@ -1070,6 +1084,67 @@ int orc_get_states(void* h, int64_t first, int64_t count, avgpu_cpu_state* st, u
   for (int64_t i = 0; i < count; i++)
     dump_state(w, w.orgs[first + i], &st[i], ops ? ops + i * cap : nullptr,
                flags ? flags + i * cap : nullptr, cap);
+  return 0;
+}
+
+// checkpoint restore: the inverse of dump_state (ops are instruction-set op
+// codes; flags bit0 copied, bit2 executed)
+int orc_set_states(void* h, int64_t first, int64_t count, const avgpu_cpu_state* st, const uint8_t* ops,
+                   const uint8_t* flags, int cap) {
+  World& w = *(World*)h;
+  if (first < 0 || count < 0 || first + count > w.ncells) return fail(AVGPU_EINVAL, "cell range");
+  for (int64_t i = 0; i < count; i++) {
+    const avgpu_cpu_state& s = st[i];
+    if (s.mem_size < 0 || s.mem_size > cap) return fail(AVGPU_EINVAL, "memory size outside mem_cap");
+    Org& o = w.orgs[first + i];
+    o = Org();
+    o.alive = s.alive != 0;
+    o.mem.assign(ops + i * cap, ops + i * cap + s.mem_size);
+    o.flg.assign(flags + i * cap, flags + i * cap + s.mem_size);
+    for (auto& f : o.flg) f &= (F_COPIED | F_EXECUTED);
+    for (int k = 0; k < 3; k++) o.reg[k] = s.reg[k];
+    for (int k = 0; k < 4; k++) o.head[k] = s.head[k];
+    for (int k = 0; k < 2; k++) {
+      for (int j = 0; j < AVGPU_STACK_SIZE; j++) o.stk[k].s[j] = s.stack[k][j];
+      o.stk[k].sp = s.stack_ptr[k];
+    }
+    o.cur_stack = s.cur_stack;
+    o.read_label.size = s.read_label_len;
+    for (int k = 0; k < s.read_label_len && k < AVGPU_MAX_LABEL; k++) o.read_label.nops[k] = s.read_label[k];
+    o.mal_active = s.mal_active != 0;
+    // the birth genome: only its length is state (birth_length); its sites are
+    // the memory's leading sites at the checkpoint
+    o.genome.assign(o.mem.begin(), o.mem.begin() + std::min<int>(s.birth_length, (int)o.mem.size()));
+    o.genome.resize(s.birth_length, 0);
+    o.cpu_cycles_used = s.cpu_cycles_used; o.time_used = s.time_used;
+    o.gestation_start = s.gestation_start; o.gestation_time = s.gestation_time;
+    o.num_divides = s.num_divides; o.generation = s.generation;
+    o.genome_length = s.genome_length; o.copied_size = s.copied_size;
+    o.child_copied_size = s.child_copied_size; o.executed_size = s.executed_size;
+    o.max_executed = s.max_executed;
+    o.input_ptr = s.input_ptr;
+    o.input_buf.cap = 3; o.input_buf.offset = 0; o.input_buf.total = s.input_total;
+    for (int k = 0; k < 3; k++) o.input_buf.data[2 - k] = s.input_buf[k];   // [i] = data[cap-1-i]
+    o.output_buf.cap = 1; o.output_buf.offset = 0; o.output_buf.total = s.output_total;
+    o.output_buf.data[0] = s.output_buf;
+    for (int k = 0; k < 3; k++) o.inputs[k] = s.inputs[k];
+    for (int k = 0; k < AVGPU_MAX_REACTIONS; k++) {
+      o.cur_task[k] = s.cur_task_count[k];
+      o.last_task[k] = s.last_task_count[k];
+      o.cur_react[k] = s.cur_reaction_count[k];
+    }
+    o.rng.lo = s.rng_key_lo; o.rng.hi = s.rng_key_hi; o.rng.ctr = s.rng_counter;
+    o.errors = s.errors;
+    o.cur_bonus = s.cur_bonus; o.merit = s.merit; o.fitness = s.fitness; o.credit = s.credit;
+  }
+  return 0;
+}
+
+int orc_set_clock(void* h, const avgpu_update_stats* last) {
+  World& w = *(World*)h;
+  w.update = last->update + 1;
+  w.cum_insts = last->cum_insts_executed;
+  w.cum_births = last->cum_births;
   return 0;
 }
 

@@ -133,6 +133,14 @@ class Backend:
         grids = [list(sp[r * n:(r + 1) * n]) for r in range(nres)] if spatial else None
         return list(lv[:nres]), grids
 
+    def checkpoint(self, path):
+        from avida_amd import checkpoint
+        checkpoint.save(self.lib, self.p, self.h, self.ncells, self.nres, path)
+
+    def restore(self, path):
+        from avida_amd import checkpoint
+        return checkpoint.load(self.lib, self.p, self.h, path)
+
     def run_update(self):
         st = capi.AvgpuUpdateStats()
         self._call("run_update", self.h, C.byref(st))

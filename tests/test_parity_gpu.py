@@ -247,3 +247,12 @@ def test_gpu_strip_tiles_with_resources(golden, T, geometry):
         bad = pu.diff_states(a[lo:lo + per], s, oa[lo * CAP:(lo + per) * CAP], o,
                              fa[lo * CAP:(lo + per) * CAP], f, CAP)
         assert not bad, f"tile {k}: {len(bad)} mismatches, first {bad[:3]}"
+
+
+@pytest.mark.parametrize("kinds", [("gpu", "gpu"), ("gpu", "oracle"), ("oracle", "gpu")])
+@pytest.mark.parametrize("env_kind", ["logic9", "resources"])
+def test_checkpoint_resume_across_backends(golden, tmp_path, kinds, env_kind):
+    """A checkpoint written by one backend and restored into the other (or the
+    same) continues bit for bit like the world that never stopped."""
+    from test_checkpoint import resume_case
+    resume_case(kinds[0], kinds[1], golden, env_kind, tmp_path)

@@ -256,3 +256,24 @@ def test_checkpoint_resume_across_backends(golden, tmp_path, kinds, env_kind):
     same) continues bit for bit like the world that never stopped."""
     from test_checkpoint import resume_case
     resume_case(kinds[0], kinds[1], golden, env_kind, tmp_path)
+
+
+def test_driver_gpu_equals_oracle(golden, tmp_path):
+    """avida_amd/driver.py on the GPU (ProductWorld) and on the oracle over the
+    spatial_res_100u config: the data files agree (count, tasks, resource
+    exactly; averages to print precision -- their sums reduce in another order)."""
+    from avida_amd import driver
+    cfgdir = os.path.join(golden, "spatial_res_100u", "config")
+    g, o = tmp_path / "gpu", tmp_path / "oracle"
+    dg = driver.Driver(cfgdir, str(g))
+    assert dg.run() == 100
+    dg.world.close()
+    driver.Driver(cfgdir, str(o), make_world=lambda cfg, iset, env: ol.Backend("oracle", cfg, iset, env)).run()
+
+    def rows(p):
+        return [l.split() for l in open(p) if l.strip() and not l.startswith("#")]
+    for name in ("count.dat", "tasks.dat", "resource.dat"):
+        assert rows(g / name) == rows(o / name), name
+    for name in ("average.dat", "time.dat"):
+        for a, b in zip(rows(g / name), rows(o / name)):
+            assert [float(x) for x in a] == pytest.approx([float(x) for x in b], rel=1e-5), name

@@ -144,6 +144,27 @@ def cpu_baseline(golden, seconds, env_kind="logic9"):
             "updates_per_sec": updates / dt}
 
 
+def cpu_baseline_multi(golden, seconds, env_kind, procs):
+    """the reference's rate_runner measures P independent
+    processes, one per host core, and sums their OI/s.  Each worker is a
+    fresh `python bench.py --cpu-worker` child (started before this process
+    touches the GPU) running the single-core baseline for `seconds`."""
+    import subprocess
+    cmd = [sys.executable, os.path.abspath(__file__), "--cpu-worker", "--cpu-seconds", str(seconds),
+           "--env", env_kind]
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    ps = [subprocess.Popen(cmd, stdout=subprocess.PIPE, env=env) for _ in range(procs)]
+    outs = [json.loads(p.communicate()[0].decode().strip().splitlines()[-1]) for p in ps]
+    if any(p.returncode for p in ps):
+        raise RuntimeError("a CPU baseline worker failed")
+    single = outs[0]
+    return {"value": sum(o["value"] for o in outs), "unit": "organism-instructions/s", "cores": procs,
+            "kind": "port", "single_core_value": single["value"],
+            "sample": f"{procs} independent oracle serial worlds (one process per host core, like the "
+                      f"reference's heads_perf_1000u_rate rate_runner), each: {single['sample']}",
+            "updates_per_sec": sum(o["updates_per_sec"] for o in outs)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -159,7 +180,19 @@ def main():
     ap.add_argument("--env", choices=["logic9", "resources"], default="logic9",
                     help="logic9: configs[2] (the metric's workload); resources: configs[4], "
                          "one diffusing spatial resource per logic-9 reaction")
+    ap.add_argument("--cpu-procs", type=int, default=0,
+                    help="CPU baseline processes (0: min(16, host CPUs) -- 16 is a GPU box's share)")
+    ap.add_argument("--cpu-worker", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
+    golden = os.path.join(ROOT, "tests", "golden")
+    if args.cpu_worker:                       # one CPU baseline process (no GPU)
+        print(json.dumps(cpu_baseline(golden, args.cpu_seconds, args.env)), flush=True)
+        return
+    rank0 = int(os.environ.get("RANK", "0")) == 0 and int(os.environ.get("WORLD_SIZE", "1")) == 1
+    cpu = None
+    if rank0 and not args.no_cpu:             # before this process initialises the GPU
+        procs = args.cpu_procs or min(16, os.cpu_count() or 1)
+        cpu = cpu_baseline_multi(golden, args.cpu_seconds, args.env, procs)
 
     import torch
     rank = int(os.environ.get("RANK", "0"))
@@ -304,7 +337,7 @@ def main():
         "cpu_baseline": None,
     }
     if world == 1 and not args.no_cpu:
-        out["cpu_baseline"] = cpu_baseline(golden, args.cpu_seconds, args.env)
+        out["cpu_baseline"] = cpu
     lib.avgpu_destroy(h)
     print(json.dumps(out), flush=True)
     if dist:

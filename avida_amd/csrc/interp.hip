@@ -109,7 +109,10 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
   constexpr int STRIDE = S + 16;
   constexpr int QUADS = STRIDE / 16;
   constexpr int TAPE_WORDS = 64 * STRIDE / 4;
-  constexpr int STK_WORDS = 2 * AVGPU_STACK_SIZE * 64;
+  // class 0 keeps the two stacks in VGPRs (sv[]): without their 5 KiB of LDS a
+  // block needs 26 KiB and 6 blocks fit a CU instead of 5
+  constexpr bool VSTK = (S == CLASS0_SIZE);
+  constexpr int STK_WORDS = VSTK ? 0 : 2 * AVGPU_STACK_SIZE * 64;
   // one __shared__ object: tapes | stacks | task LUT (256 x u16) | rand_cum (64 x i32) |
   // rand_code (64 B) | rand_lut (256 B) | reactions (16 x RT_STRIDE words) |
   // task bonus factors (16 doubles) | task bonus addends (16 doubles)
@@ -198,17 +201,21 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
       __builtin_amdgcn_global_load_lds((void*)(W.tape + (int64_t)c * TAPE_SLOT + q * 16),
                                        (lds_ptr_t)(lds32 + it * 256), 16, 0, 0);
   }
+  int32_t sv[2 * AVGPU_STACK_SIZE];
 #pragma unroll
   for (int k = 0; k < 2 * AVGPU_STACK_SIZE; k++) {
-    if (active && !fresh)
+    if (VSTK) {
+      sv[k] = (active && !fresh) ? W.stack[(int64_t)k * N + cell] : 0;
+    } else if (active && !fresh) {
 #ifdef AVGPU_NO_LDS_DMA
       stk[k * 64 + lane] = W.stack[(int64_t)k * N + cell];
 #else
       __builtin_amdgcn_global_load_lds((void*)(W.stack + (int64_t)k * N + cell),
                                        (lds_ptr_t)(stk + k * 64), 4, 0, 0);
 #endif
-    else
+    } else {
       stk[k * 64 + lane] = 0;
+    }
   }
 
   uint8_t* T = lds + lane * STRIDE;
@@ -441,9 +448,19 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
       case AVGPU_H_POP: {                                     // :2698, cCPUStack::Pop
         const int k = (ctl & CTL_CURSTK) ? 1 : 0;
         int sp = k ? CTL_SP1(ctl) : CTL_SP0(ctl);
-        int32_t* slot = stk + (k * AVGPU_STACK_SIZE + sp) * 64 + lane;
-        const int v = *slot;
-        *slot = 0;
+        int v = 0;
+        if (VSTK) {
+          const int idx = k * AVGPU_STACK_SIZE + sp;
+#pragma unroll
+          for (int i = 0; i < 2 * AVGPU_STACK_SIZE; i++) {
+            v = (i == idx) ? sv[i] : v;
+            sv[i] = (i == idx) ? 0 : sv[i];
+          }
+        } else {
+          int32_t* slot = stk + (k * AVGPU_STACK_SIZE + sp) * 64 + lane;
+          v = *slot;
+          *slot = 0;
+        }
         sp = (sp + 1 == AVGPU_STACK_SIZE) ? 0 : sp + 1;
         ctl = k ? ((ctl & ~0xF0u) | ((uint32_t)sp << 4)) : ((ctl & ~0xFu) | (uint32_t)sp);
         SETREG(r, v);
@@ -453,7 +470,13 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
         const int k = (ctl & CTL_CURSTK) ? 1 : 0;
         int sp = k ? CTL_SP1(ctl) : CTL_SP0(ctl);
         sp = (sp == 0) ? AVGPU_STACK_SIZE - 1 : sp - 1;
-        stk[(k * AVGPU_STACK_SIZE + sp) * 64 + lane] = GETREG(r);
+        if (VSTK) {
+          const int idx = k * AVGPU_STACK_SIZE + sp, val = GETREG(r);
+#pragma unroll
+          for (int i = 0; i < 2 * AVGPU_STACK_SIZE; i++) sv[i] = (i == idx) ? val : sv[i];
+        } else {
+          stk[(k * AVGPU_STACK_SIZE + sp) * 64 + lane] = GETREG(r);
+        }
         ctl = k ? ((ctl & ~0xF0u) | ((uint32_t)sp << 4)) : ((ctl & ~0xFu) | (uint32_t)sp);
         CKC(1);
         break; }
@@ -875,7 +898,14 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
           }
           // parent ClearFlags over its remaining sites, empty stacks
           for (int w = lane; (w << 2) < div; w += 64) TL32[w] &= 0x3F3F3F3Fu;
-          if (lane < 2 * AVGPU_STACK_SIZE) stk[lane * 64 + L] = 0;
+          if (VSTK) {
+            if (lane == L) {
+#pragma unroll
+              for (int i = 0; i < 2 * AVGPU_STACK_SIZE; i++) sv[i] = 0;
+            }
+          } else if (lane < 2 * AVGPU_STACK_SIZE) {
+            stk[lane * 64 + L] = 0;
+          }
         }
       }
     }
@@ -940,7 +970,7 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
       }
     }
 #pragma unroll
-    for (int k = 0; k < 2 * AVGPU_STACK_SIZE; k++) W.stack[(int64_t)k * N + cell] = stk[k * 64 + lane];
+    for (int k = 0; k < 2 * AVGPU_STACK_SIZE; k++) W.stack[(int64_t)k * N + cell] = VSTK ? sv[k] : stk[k * 64 + lane];
     if (spill) {
       const int slot = atomicAdd(&W.class_count[3 + cls + 1], 1);     // spill row of class cls+1
       W.class_list[(int64_t)(3 + cls + 1) * N + slot] = cell;
@@ -1027,7 +1057,8 @@ template <int S>
 __global__ __launch_bounds__(64, (S == CLASS0_SIZE) ? 2 : 1) void k_interpret(const DevWorld* __restrict__ Wp, int cls, int row, int mode,
                                                   int64_t first, int64_t count, int sorted) {
   constexpr int TAB_WORDS = 128 + 64 + 16 + 64 + AVGPU_MAX_REACTIONS * RT_STRIDE + 64;
-  __shared__ __attribute__((aligned(16))) uint32_t lds32[64 * (S + 16) / 4 + 2 * AVGPU_STACK_SIZE * 64 + TAB_WORDS];
+  constexpr int STK = (S == CLASS0_SIZE) ? 0 : 2 * AVGPU_STACK_SIZE * 64;   // class 0: stacks in VGPRs
+  __shared__ __attribute__((aligned(16))) uint32_t lds32[64 * (S + 16) / 4 + STK + TAB_WORDS];
   if (cls == 0) {
     // sorted windows: the 32 chunks of a window run on one XCD (blocks are
     // dealt to the 8 XCDs round robin), so its state lines meet in one L2

@@ -355,7 +355,7 @@ __device__ __forceinline__ void count_add(const DevWorld& W, int slot, unsigned 
 // LDS size classes of k_interpret (bytes of tape per lane)
 // (a block of class S uses 64 x (S + 16) B of LDS for tapes; class 0 is sized
 // so that 5 blocks fit a CU's 160 KiB with the stacks and tables)
-#define CLASS0_SIZE 368
+#define CLASS0_SIZE 336
 #define CLASS1_SIZE 768
 #define CLASS2_SIZE 1536
 #define CLASS3_SIZE 2048

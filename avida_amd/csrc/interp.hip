@@ -119,13 +119,17 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
   uint8_t* lds = reinterpret_cast<uint8_t*>(lds32);
   int32_t* stk = reinterpret_cast<int32_t*>(lds32 + TAPE_WORDS);
   uint32_t* tab = lds32 + TAPE_WORDS + STK_WORDS;
-  const uint16_t* lut = reinterpret_cast<const uint16_t*>(tab);
-  const int32_t* rcum = reinterpret_cast<const int32_t*>(tab + 128);
-  const uint8_t* rcode = reinterpret_cast<const uint8_t*>(tab + 192);
-  const uint8_t* rlut = reinterpret_cast<const uint8_t*>(tab + 208);
-  const int32_t* rtab = reinterpret_cast<const int32_t*>(tab + 272);
+  // class 0 reads the small tables from global memory (L1 / scalar cache):
+  // with tapes only, its block needs 22 KiB of LDS and 7 blocks fit a CU
+  constexpr bool GTAB = (S == CLASS0_SIZE);
+  const uint16_t* lut = GTAB ? W.task_lut : reinterpret_cast<const uint16_t*>(tab);
+  const int32_t* rcum = GTAB ? W.rand_cum : reinterpret_cast<const int32_t*>(tab + 128);
+  const uint8_t* rcode = GTAB ? W.rand_code : reinterpret_cast<const uint8_t*>(tab + 192);
+  const uint8_t* rlut = GTAB ? W.rand_lut : reinterpret_cast<const uint8_t*>(tab + 208);
+  const int32_t* rtab = GTAB ? W.react_tab : reinterpret_cast<const int32_t*>(tab + 272);
   // per-task bonus factor / addend of the simple-environment path (16 + 16 doubles)
-  const double* tmul = reinterpret_cast<const double*>(tab + 272 + AVGPU_MAX_REACTIONS * RT_STRIDE);
+  const double* tmul = GTAB ? W.task_tab
+                            : reinterpret_cast<const double*>(tab + 272 + AVGPU_MAX_REACTIONS * RT_STRIDE);
   const double* tadd = tmul + 16;
 
   const int lane = threadIdx.x;
@@ -175,7 +179,7 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
   const int m_in = M;
 
   // ---- block-shared tables ----
-  {
+  if (!GTAB) {
     uint32_t* l32 = tab;
     const uint32_t* g_lut = reinterpret_cast<const uint32_t*>(W.task_lut);
     l32[lane] = g_lut[lane];
@@ -1057,8 +1061,10 @@ template <int S>
 __global__ __launch_bounds__(64, (S == CLASS0_SIZE) ? 2 : 1) void k_interpret(const DevWorld* __restrict__ Wp, int cls, int row, int mode,
                                                   int64_t first, int64_t count, int sorted) {
   constexpr int TAB_WORDS = 128 + 64 + 16 + 64 + AVGPU_MAX_REACTIONS * RT_STRIDE + 64;
-  constexpr int STK = (S == CLASS0_SIZE) ? 0 : 2 * AVGPU_STACK_SIZE * 64;   // class 0: stacks in VGPRs
-  __shared__ __attribute__((aligned(16))) uint32_t lds32[64 * (S + 16) / 4 + STK + TAB_WORDS];
+  // class 0: stacks in VGPRs, tables in global memory -- only the tapes in LDS
+  constexpr int STK = (S == CLASS0_SIZE) ? 0 : 2 * AVGPU_STACK_SIZE * 64;
+  constexpr int TAB = (S == CLASS0_SIZE) ? 0 : TAB_WORDS;
+  __shared__ __attribute__((aligned(16))) uint32_t lds32[64 * (S + 16) / 4 + STK + TAB];
   if (cls == 0) {
     // sorted windows: the 32 chunks of a window run on one XCD (blocks are
     // dealt to the 8 XCDs round robin), so its state lines meet in one L2

@@ -39,7 +39,7 @@ METRIC = "organism-instructions/sec + updates/sec, 1M-org logic-9 world, 1/8 GPU
 STATE_BYTES = 224.0
 SITE_BYTES = 1.25
 HBM_PEAK_GBS = 8000.0         # MI355X_MICROARCH.md chip table (spec)
-PMC_FILE = os.path.join(ROOT, "profiles", "pmc_k_interpret368.json")
+PMC_FILE = os.path.join(ROOT, "profiles", "pmc_k_interpret336.json")
 
 
 def _pool(golden):
@@ -271,7 +271,7 @@ def main():
             dist.destroy_process_group()
         return
     value = tot_insts / dt_max
-    # roofline of the dominant kernel k_interpret<368> (LDS size class 0, one
+    # roofline of the dominant kernel k_interpret<336> (LDS size class 0, one
     # launch per update), this rank: algorithmic bytes per launch =
     # slices * 2 * 224 B + tape sites staged in and written back * 1.25 B,
     # over its HIP-event-timed average duration on the world's stream.
@@ -324,7 +324,7 @@ def main():
             "frac": achieved / HBM_PEAK_GBS,
             "traffic": traffic,
             "traffic_source": traffic_src,
-            "kernel": "k_interpret<368> (LDS size class 0)",
+            "kernel": "k_interpret<336> (LDS size class 0)",
             "kernel_ms": c0_ms,
             "bytes_per_launch": bytes_per_launch,
             "slices_per_launch": c0_slices,

@@ -42,6 +42,38 @@ HBM_PEAK_GBS = 8000.0         # MI355X_MICROARCH.md chip table (spec)
 PMC_FILE = os.path.join(ROOT, "profiles", "pmc_k_interpret336.json")
 
 
+
+def issue_roofline(cnt, c0_ms, c0_insts):
+    """Instruction-issue roofline of k_interpret<336> (the second roofline the
+    north star asks for). PMC wave-instruction counts per class-0 dispatch
+    (profiles/pmc_k_interpret336.json, same world) over this run's live
+    HIP-event duration of that kernel. VALU peak: a wave64 VALU instruction
+    occupies its SIMD-32 for 2 cycles (MI355X_MICROARCH.md, wave scheduling),
+    4 SIMDs x 256 CUs x 2.4 GHz / 2 = 1.23e12 wave-instructions/s; SALU peak:
+    one scalar instruction per CU per cycle = 6.1e11/s. `oi_ceiling` is the
+    OI/s at which VALU issue alone would saturate with this build's VALU
+    instructions per organism instruction."""
+    if c0_ms <= 0 or c0_insts <= 0:
+        return None
+    sec = c0_ms * 1e-3
+    valu, salu = cnt["SQ_INSTS_VALU"], cnt["SQ_INSTS_SALU"]
+    valu_peak = 256 * 4 * 2.4e9 / 2.0
+    salu_peak = 256 * 2.4e9
+    wc = cnt["SQ_WAVE_CYCLES"]
+    return {
+        "bound": "valu-issue",
+        "achieved": valu / sec,
+        "peak": valu_peak,
+        "unit": "wave-instructions/s",
+        "frac": valu / sec / valu_peak,
+        "salu_frac": salu / sec / salu_peak,
+        "valu_per_oi": valu / c0_insts,
+        "oi_ceiling": valu_peak / (valu / c0_insts),
+        "wave_cycles_active": cnt["SQ_ACTIVE_INST_ANY"] / wc,
+        "wave_cycles_waitcnt": cnt["SQ_WAIT_ANY"] / wc,
+        "wave_cycles_issue_stall": cnt["SQ_WAIT_INST_ANY"] / wc,
+        "lds_bank_conflict_frac": cnt["SQ_LDS_BANK_CONFLICT"] / max(1.0, cnt["SQ_LDS_IDX_ACTIVE"]),
+    }
 def _pool(golden):
     from avida_amd import files
     iset = files.read_instset(os.path.join(golden, "instset-classic.cfg"))
@@ -280,13 +312,15 @@ def main():
     c0_sites = d[capi.CNT_C0_SITES] / nph
     bytes_per_launch = 2.0 * STATE_BYTES * c0_slices + SITE_BYTES * c0_sites
     achieved = bytes_per_launch / (c0_ms * 1e-3) / 1e9 if c0_ms > 0 else 0.0
-    traffic, traffic_src = None, None
+    traffic, traffic_src, issue = None, None, None
     if os.path.exists(PMC_FILE):
         with open(PMC_FILE) as f:
             pmc = json.load(f)
-        if pmc.get("world") == f"{args.side}x{args.side}":
+        if pmc.get("world") == f"{args.side}x{args.side}" and args.env == "logic9":
             traffic = pmc["hbm_bytes_per_launch"]
             traffic_src = pmc["source"]
+            issue = issue_roofline(pmc["counters_per_dispatch"], c0_ms,
+                                   d[capi.CNT_INSTS] / nph * c0_slices / max(1.0, d[capi.CNT_SLICES] / nph))
     out = {
         "metric": METRIC,
         "value": value,
@@ -333,6 +367,7 @@ def main():
             "class_ms": [x / nph for x in cms],
             "lane_efficiency": d[capi.CNT_INSTS] / max(1, d[capi.CNT_LANESTEPS]),
             "insts_per_kernel_second": d[capi.CNT_INSTS] / max(1e-9, sum(cms) * 1e-3),
+            "issue": issue,
         },
         "cpu_baseline": None,
     }

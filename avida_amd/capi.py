@@ -9,6 +9,8 @@ from __future__ import annotations
 import ctypes as C
 import os
 
+import numpy as np
+
 MAX_REACTIONS = 16
 MAX_GENOME = 2048
 STACK_SIZE = 10
@@ -123,13 +125,30 @@ class AvgpuUpdateStats(C.Structure):
     ]
 
 
+# avgpu_census (include/avida_gpu.h), read straight into numpy
+CENSUS_DTYPE = np.dtype([("genotype_key", "<u8"), ("merit", "<f8"), ("fitness", "<f8"),
+                         ("genome_length", "<i4"), ("gestation_time", "<i4"), ("copied_size", "<i4"),
+                         ("executed_size", "<i4"), ("generation", "<i4"), ("num_divides", "<i4")])
+assert CENSUS_DTYPE.itemsize == 48
+
+
+def get_census(lib, prefix, handle, first, count):
+    """Census rows (CENSUS_DTYPE) of cells first .. first+count-1 through
+    {prefix}get_census (avgpu_ = the product, orc_ = the oracle)."""
+    out = np.zeros(count, dtype=CENSUS_DTYPE)
+    rc = getattr(lib, prefix + "get_census")(handle, first, count, out.ctypes.data_as(C.c_void_p))
+    if rc < 0:
+        raise RuntimeError(f"{prefix}get_census: {getattr(lib, prefix + 'last_error')().decode()}")
+    return out
+
+
 # C-ABI symbols declared in include/avida_gpu.h (checked by tests/test_capi.py)
 EXPORTED = [
     "avgpu_last_error", "avgpu_cfg_defaults", "avgpu_create", "avgpu_destroy", "avgpu_sync",
     "avgpu_load_instset", "avgpu_load_env", "avgpu_load_resources", "avgpu_get_resources",
     "avgpu_set_resources", "avgpu_set_org", "avgpu_set_orgs", "avgpu_kill", "avgpu_set_states", "avgpu_set_clock",
     "avgpu_step", "avgpu_run_update", "avgpu_run_updates", "avgpu_update_totals",
-    "avgpu_update_run", "avgpu_set_stream", "avgpu_get_states",
+    "avgpu_update_run", "avgpu_set_stream", "avgpu_get_states", "avgpu_get_census", "avgpu_set_genotype_keys",
     "avgpu_test_genomes", "avgpu_get_stats", "avgpu_stats_vector", "avgpu_set_global_totals",
     "avgpu_set_tile", "avgpu_tile_buffer_bytes", "avgpu_set_tile_buffers", "avgpu_tile_partials",
     "avgpu_tile_begin", "avgpu_tile_place", "avgpu_tile_finish", "avgpu_tile_res_bytes",
@@ -246,6 +265,8 @@ def bind_common(lib, prefix):
         "set_states": (C.c_int, [V, I64, I64, C.POINTER(AvgpuCpuState), C.POINTER(C.c_uint8),
                                  C.POINTER(C.c_uint8), C.c_int]),
         "set_clock": (C.c_int, [V, C.POINTER(AvgpuUpdateStats)]),
+        "get_census": (C.c_int, [V, I64, I64, V]),
+        "set_genotype_keys": (C.c_int, [V, I64, I64, V]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, p + name, None)

@@ -12,7 +12,9 @@ same backend or the other one (product "avgpu_" or CPU oracle "orc_").
 File: one `numpy.savez_compressed` archive (no pickles): `states` (raw
 avgpu_cpu_state records), `tape` (one byte per site: op | copied << 6 |
 executed << 7, `cap` bytes per cell), `stats` (raw avgpu_update_stats),
-`levels` / `grids` (resources).
+`levels` / `grids` (resources), `gkeys` (the census genotype keys of the
+birth genomes, which the tape no longer holds once an organism copied into
+its own sites; avgpu_set_genotype_keys).
 """
 from __future__ import annotations
 
@@ -49,7 +51,8 @@ def save(lib, prefix, handle, ncells, nres, path):
     if nres:
         _call(lib, prefix, "get_resources", handle, levels.ctypes.data_as(C.POINTER(C.c_double)),
               grids.ctypes.data_as(C.POINTER(C.c_double)))
-    np.savez_compressed(path, states=np.frombuffer(st, dtype=np.uint8), tape=tape.astype(np.uint8),
+    gkeys = capi.get_census(lib, prefix, handle, 0, ncells)["genotype_key"]
+    np.savez_compressed(path, states=np.frombuffer(st, dtype=np.uint8), tape=tape.astype(np.uint8), gkeys=gkeys,
                         cap=np.int64(cap), stats=np.frombuffer(stats, dtype=np.uint8),
                         levels=levels[:nres], grids=grids[:nres * ncells], ncells=np.int64(ncells))
 
@@ -65,6 +68,9 @@ def load(lib, prefix, handle, path):
     fl = np.ascontiguousarray(((tape >> 6) & 0x01) | (((tape >> 7) & 0x01) << 2))
     _call(lib, prefix, "set_states", handle, 0, ncells, st, ops.ctypes.data_as(C.POINTER(C.c_uint8)),
           fl.ctypes.data_as(C.POINTER(C.c_uint8)), cap)
+    if "gkeys" in z.files:                     # genotype keys of the birth genomes
+        gk = np.ascontiguousarray(z["gkeys"], dtype=np.uint64)
+        _call(lib, prefix, "set_genotype_keys", handle, 0, ncells, gk.ctypes.data_as(C.c_void_p))
     stats = capi.AvgpuUpdateStats.from_buffer_copy(z["stats"].tobytes())
     _call(lib, prefix, "set_clock", handle, C.byref(stats))
     levels = np.ascontiguousarray(z["levels"], dtype=np.float64)

@@ -99,7 +99,7 @@ int setup_world(avgpu_world* w, int64_t n, bool test_buffers) {
   int rc = 0;
 #define A(ptr, cnt) if ((rc = w->alloc(&W.ptr, (size_t)(cnt))) < 0) return rc
   A(reg, 3 * n); A(head, 4 * n); A(ctl, n); A(rlabel, n); A(mem_size, n); A(cycles, n);
-  A(time_used, n); A(gest_start, n); A(max_exec, n); A(birth_len, n); A(rng, 3 * n);
+  A(time_used, n); A(gest_start, n); A(max_exec, n); A(birth_len, n); A(gkey, n); A(rng, 3 * n);
   A(budget, n); A(tape, (size_t)n * TAPE_SLOT);
   A(stack, 2 * AVGPU_STACK_SIZE * n); A(inbuf, 3 * n); A(in_total, n); A(in_ptr, n);
   A(outbuf, n); A(out_total, n); A(inputs, 3 * n);
@@ -660,6 +660,27 @@ int avgpu_get_stats(avgpu_world* w, avgpu_update_stats* out) {
   out->cum_births = (int64_t)v[31];
   out->slices = (int64_t)v[32];
   out->lane_steps = (int64_t)v[33];
+  return 0;
+}
+
+int avgpu_get_census(avgpu_world* w, int64_t first, int64_t count, avgpu_census* out) {
+  if (!w || !out || first < 0 || count < 0 || first + count > w->W.n) return fail(AVGPU_EINVAL, "cell range");
+  if (count == 0) return 0;
+  avgpu_census* d = nullptr;
+  HIPCHK(hipMalloc(&d, count * sizeof(avgpu_census)));
+  launch_get_census(w->W, w->stream, first, count, d);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(out, d, count * sizeof(avgpu_census), hipMemcpyDeviceToHost, w->stream));
+  HIPCHK(hipStreamSynchronize(w->stream));
+  hipFree(d);
+  return 0;
+}
+
+int avgpu_set_genotype_keys(avgpu_world* w, int64_t first, int64_t count, const uint64_t* keys) {
+  if (!w || !keys || first < 0 || count < 0 || first + count > w->W.n) return fail(AVGPU_EINVAL, "cell range");
+  if (count == 0) return 0;
+  HIPCHK(hipMemcpyAsync(w->W.gkey + first, keys, count * sizeof(uint64_t), hipMemcpyHostToDevice, w->stream));
+  HIPCHK(hipStreamSynchronize(w->stream));
   return 0;
 }
 

@@ -70,6 +70,7 @@ struct DevWorld {
   int32_t* gest_start;// [n]
   int32_t* max_exec;  // [n]
   int32_t* birth_len; // [n]  genome length at birth (cPhenotype::genome_length)
+  uint64_t* gkey;     // [n]  genome key of the birth genome (systematics census)
   uint32_t* rng;      // [3][n] key_lo, key_hi, ctr
   int32_t* budget;    // [n]  instructions left in this update
   uint8_t* tape;      // [n][TAPE_SLOT]
@@ -306,6 +307,37 @@ __device__ __forceinline__ void derive_key(uint32_t a_lo, uint32_t a_hi, uint32_
 }
 
 // cHeadCPU::Adjust (cpu/cHeadCPU.cc:27-50)
+// Genome key (restated in oracle/oracle.cc and
+// avida_amd/systematics.py): words w = 0 .. ceil(len/4)-1 of the birth genome
+// in canonical codes (4 sites little-endian, sites >= len zero) each mixed with
+// their index, summed mod 2^64, then mixed with the length.  The sum makes it
+// wave-parallel: each lane folds the words it copies, one wave_sum finishes.
+__device__ __forceinline__ uint64_t gk_mix(uint64_t z) {
+  z ^= z >> 30; z *= 0xBF58476D1CE4E5B9ull;
+  z ^= z >> 27; z *= 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+__device__ __forceinline__ uint64_t gk_word(uint32_t word, int w, int len) {
+  word &= 0x3F3F3F3Fu;
+  const int keep = len - 4 * w;                 // sites of this word inside the genome
+  if (keep < 4) word &= (1u << (8 * keep)) - 1u;
+  return gk_mix(((uint64_t)(w + 1) << 32) | word);
+}
+__device__ __forceinline__ uint64_t gk_final(uint64_t sum, int len) {
+  const uint64_t k = gk_mix(sum ^ ((uint64_t)len * 0x9E3779B97F4A7C15ull));
+  return k ? k : 1ull;
+}
+// serial form over a tape (one lane)
+__device__ __forceinline__ uint64_t gk_tape(const uint8_t* t, int len) {
+  uint64_t s = 0;
+  for (int w = 0; w < (len + 3) / 4; w++) {
+    uint32_t v = 0;
+    for (int j = 0; j < 4 && 4 * w + j < len; j++) v |= (uint32_t)t[4 * w + j] << (8 * j);
+    s += gk_word(v, w, len);
+  }
+  return gk_final(s, len);
+}
+
 __device__ __forceinline__ int head_adjust(int pos, int size) {
   if ((unsigned)pos < (unsigned)size) return pos;
   if (pos < 0) return 0;
@@ -407,6 +439,7 @@ void launch_get_states(const DevWorld& W, hipStream_t s, int64_t first, int64_t 
                        avgpu_cpu_state* d_states, uint8_t* d_codes, int cap);
 void launch_set_states(const DevWorld& W, hipStream_t s, int64_t first, int64_t count, const avgpu_cpu_state* in,
                        const uint8_t* codes, int cap);
+void launch_get_census(const DevWorld& W, hipStream_t s, int64_t first, int64_t count, avgpu_census* d_out);
 void launch_merit_total(const DevWorld& W, hipStream_t s, double* d_totals, double* d_scratch);
 // strip tiles
 void launch_tile_partials(const DevWorld& W, hipStream_t s, double* d_out);

@@ -80,6 +80,7 @@ __global__ void k_set_orgs(DevWorld W, int64_t first, int64_t count, const uint8
   }
   W.max_exec[c] = mx;
   W.birth_len[c] = len;
+  W.gkey[c] = gk_tape(t, len);
   // stream key (DESIGN.md RNG spec)
   uint32_t lo, hi, ctr = 0;
   derive_key(W.seed_lo, W.seed_hi, (uint32_t)(W.cell0 + c), 0xA5A5A5A5U, lo, hi);
@@ -215,6 +216,38 @@ __global__ void k_set_states(DevWorld W, int64_t first, int64_t count, const avg
   const uint8_t* src = codes + i * cap;
   const int m = s.mem_size < cap ? s.mem_size : cap;
   for (int k = 0; k < m; k++) t[k] = src[k];
+  // the birth genome is the tape prefix (as the oracle restores it)
+  uint64_t gs = 0;
+  const int bl = s.birth_length < m ? s.birth_length : m;
+  for (int w = 0; w < (bl + 3) / 4; w++) {
+    uint32_t v = 0;
+    for (int j = 0; j < 4 && 4 * w + j < bl; j++) v |= (uint32_t)(t[4 * w + j] & CODE_MASK) << (8 * j);
+    gs += gk_word(v, w, s.birth_length);
+  }
+  W.gkey[c] = gk_final(gs, s.birth_length);
+}
+
+// systematics census (include/avida_gpu.h avgpu_census): one row per cell,
+// written as one coalesced 48-B struct per lane
+__global__ void k_census(DevWorld W, int64_t first, int64_t count, avgpu_census* out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= count) return;
+  const int64_t c = first + i;
+  const uint32_t ctl = W.ctl[c];
+  avgpu_census r;
+  memset(&r, 0, sizeof(r));
+  if (ctl & CTL_ALIVE) {
+    r.genotype_key = W.gkey[c];
+    r.merit = W.merit[c];
+    r.fitness = W.fitness[c];
+    r.genome_length = W.birth_len[c];
+    r.gestation_time = W.gest_time[c];
+    r.copied_size = W.copied[c];
+    r.executed_size = W.executed[c];
+    r.generation = W.generation[c];
+    r.num_divides = (ctl & CTL_FRESH) ? 0 : W.num_div[c];
+  }
+  out[i] = r;
 }
 
 // budget = uniform or per-cell array, all live cells of [first, first+count)
@@ -561,7 +594,14 @@ __device__ __forceinline__ void setup_child(const DevWorld& W, int64_t c, const 
   const int64_t N = W.n;
   const int len = b.len;
   uint32_t* dst = reinterpret_cast<uint32_t*>(W.tape + c * TAPE_SLOT);
-  for (int w = lane; w < (len + 3) / 4; w += 64) dst[w] = src[w];
+  uint64_t gsum = 0;
+  for (int w = lane; w < (len + 3) / 4; w += 64) {
+    const uint32_t v = src[w];
+    dst[w] = v;
+    gsum += gk_word(v, w, len);
+  }
+  for (int off = 32; off > 0; off >>= 1) gsum += __shfl_xor(gsum, off);
+  if (lane == 0) W.gkey[c] = gk_final(gsum, len);
   switch (lane) {
     case 0: W.ctl[c] = CTL_ALIVE | CTL_FRESH; break;
     case 1: W.mem_size[c] = len; break;
@@ -818,6 +858,10 @@ void launch_get_states(const DevWorld& W, hipStream_t s, int64_t first, int64_t 
                      codes, cap);
 }
 
+void launch_get_census(const DevWorld& W, hipStream_t s, int64_t first, int64_t count, avgpu_census* d_out) {
+  if (count <= 0) return;
+  k_census<<<(unsigned)((count + 255) / 256), 256, 0, s>>>(W, first, count, d_out);
+}
 void launch_set_states(const DevWorld& W, hipStream_t s, int64_t first, int64_t count, const avgpu_cpu_state* in,
                        const uint8_t* codes, int cap) {
   hipLaunchKernelGGL(k_set_states, dim3((unsigned)((count + 127) / 128)), dim3(128), 0, s, W, first, count, in,

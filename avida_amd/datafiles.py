@@ -5,7 +5,9 @@ cStats::Print{Count,Average,Tasks,Time,Resource}Data write them
 the same header comments and column legends, one row per printed update,
 numbers in C++ ostream default format (6 significant digits, '%g').
 
-Columns the hot path does not track (genotype / species / lineage counts,
+dominant.dat (PrintDominantData, actions/PrintActions.cc:5405-5440) and
+count.dat's genotype columns come from the host genotype classification
+(avida_amd/systematics.py).  Columns the hot path does not track (species / lineage counts,
 breed-true, thread counts, repro rate, copied / executed size averages,
 neutral metric, lineage label) are written as 0 and listed in
 UNTRACKED; the tracked ones come from avgpu_update_stats.
@@ -30,12 +32,22 @@ AVERAGE_COLS = ["Update", "Merit", "Gestation Time", "Fitness", "Repro Rate?", "
                 "(deprecated) Genotype Depth", "Generation", "Neutral Metric", "Lineage Label",
                 "True Replication Rate (based on births/update, time-averaged)"]
 TIME_COLS = ["update", "avida time", "average generation", "num_executed?"]
-UNTRACKED = {"count.dat": [4, 5, 11, 12, 13, 16], "average.dat": [5, 7, 8, 11, 14, 15, 16]}
+DOMINANT_COLS = ["Update", "Average Merit of the Dominant Genotype",
+                 "Average Gestation Time of the Dominant Genotype",
+                 "Average Fitness of the Dominant Genotype", "Repro Rate?", "Size of Dominant Genotype",
+                 "Copied Size of Dominant Genotype", "Executed Size of Dominant Genotype",
+                 "Abundance of Dominant Genotype", "Number of Births", "Number of Dominant Breed True?",
+                 "Dominant Gene Depth", "Dominant Breed In", "Max Fitness?",
+                 "Genotype ID of Dominant Genotype", "Name of the Dominant Genotype"]
+# count.dat 4 / 5 come from the genotype classification (avida_amd/systematics.py)
+# when the driver runs one; dominant.dat 8 is 0 in the reference as well
+UNTRACKED = {"count.dat": [11, 12, 13, 16], "average.dat": [5, 7, 8, 11, 14, 15, 16],
+             "dominant.dat": [10, 11, 12, 13]}
 
 
 def fmt(x):
     """cDataFile / ostream default: 6 significant digits"""
-    if isinstance(x, int):
+    if isinstance(x, (int, str)):
         return str(x)
     return "%g" % x
 
@@ -72,6 +84,7 @@ class StatsRecorder:
         self.avida_time = 0.0
         self.last = None
         self.resource_names = list(resource_names)
+        self.arbiter = None       # systematics.GenotypeArbiter, set by the driver
 
     def _stamp(self):
         return time.strftime("%a %b %d %H:%M:%S %Y")
@@ -95,7 +108,17 @@ class StatsRecorder:
         s = self.last
         n = s.num_organisms
         f = self._file(name, ["Avida count data", self._stamp()], COUNT_COLS)
-        f.row([s.update, s.insts_executed, n, 0, 0, 0, 0, 0, s.births, s.deaths, 0, 0, 0, n, 0, 0])
+        a = self.arbiter
+        ng, nt = (a.num_genotypes(), a.num_threshold()) if a is not None else (0, 0)
+        f.row([s.update, s.insts_executed, n, ng, nt, 0, 0, 0, s.births, s.deaths, 0, 0, 0, n, 0, 0])
+
+    def print_dominant(self, name="dominant.dat"):
+        """cActionPrintDominantData (actions/PrintActions.cc:5405-5440): the
+        file is opened on the first call; with no organism no row is written"""
+        f = self._file(name, ["Avida Dominant Data", self._stamp()], DOMINANT_COLS)
+        row = self.arbiter.dominant_row(self.last.update) if self.arbiter is not None else None
+        if row is not None:
+            f.row(row)
 
     def print_average(self, name="average.dat"):
         s = self.last

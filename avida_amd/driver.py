@@ -23,7 +23,7 @@ import ctypes as C
 import os
 import sys
 
-from . import capi, checkpoint, datafiles, files
+from . import capi, checkpoint, datafiles, files, systematics
 
 
 class ProductWorld:
@@ -64,6 +64,9 @@ class ProductWorld:
         st = capi.AvgpuUpdateStats()
         self._call("run_update", self.h, C.byref(st))
         return st
+
+    def census(self, first=0, count=None):
+        return capi.get_census(self.lib, self.p, self.h, first, self.ncells - first if count is None else count)
 
     def resources(self, spatial=False):
         lv = (C.c_double * max(1, self.nres))()
@@ -120,6 +123,12 @@ class Driver:
         self.world = (make_world or ProductWorld)(self.cfg, self.iset, self.env)
         self.rec = datafiles.StatsRecorder(data_dir, [r.name for r in getattr(self.env, "resources", [])])
         self.data_dir = data_dir
+        # genotype classification runs every update when a data file needs it
+        # (the reference's systematics manager classifies every birth)
+        need = {"PrintCountData", "PrintDominantData"}
+        self.arbiter = systematics.GenotypeArbiter(int(acfg.get("THRESHOLD", 3))) \
+            if any(e[2] in need for e in self.events) else None
+        self.rec.arbiter = self.arbiter
         self.done = False
         self.update = -1
 
@@ -143,8 +152,14 @@ class Driver:
             end = int(args[2]) if len(args) > 2 else start + 1
             merit = float(args[3]) if len(args) > 3 else -1.0
             w.set_orgs(start, [g] * (end - start), [max(0.0, merit)] * (end - start), deterministic=False)
-        elif action == "PrintCountData":
+        if action in ("Inject", "InjectAll") or action.lower() == "injectsequence":
+            if self.arbiter is not None:      # injected units are classified at once
+                self.arbiter.update(w.census(), max(self.update, 0))
+            return
+        if action == "PrintCountData":
             self.rec.print_count(*args[:1])
+        elif action == "PrintDominantData":
+            self.rec.print_dominant(*args[:1])
         elif action == "PrintAverageData":
             self.rec.print_average(*args[:1])
         elif action == "PrintTasksData":
@@ -174,6 +189,8 @@ class Driver:
             if self.update > 0:
                 self.rec.begin_update()
             self.rec.end_update(self.world.run_update())
+            if self.arbiter is not None:
+                self.arbiter.update(self.world.census(), self.update)
             for trig, start, action, args in self.events:
                 if _fires(trig, start, self.update):
                     self._action(action, args)

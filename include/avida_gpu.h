@@ -347,10 +347,44 @@ int avgpu_update_run(avgpu_world* w, const double* dev_totals, avgpu_update_stat
  * starts on a private non-blocking stream of its own. */
 int avgpu_set_stream(avgpu_world* w, void* hip_stream);
 
+/* ---- systematics census ----
+ * One row per cell for the host-side genotype classification that replaces
+ * Systematics::GenotypeArbiter::ClassifyNewUnit (systematics/GenotypeArbiter.cc:
+ * 280-380): the reference files every newborn under the genotype whose
+ * InstructionSequence equals its birth genome (bucketed by hashGenome,
+ * :470-480).  Here the device keys each birth genome once, when the
+ * organism is activated (or set / restored), and the host groups cells by
+ * key.  genotype_key is the 64-bit "genome key" of the birth genome over
+ * canonical instruction codes (DESIGN.md section 10 gives the function;
+ * oracle/oracle.cc and avida_amd/systematics.py restate it); 0 = empty cell.
+ * The other fields are the phenotype values cStats / the Genotype data
+ * providers average (systematics/Genotype.cc:493-540). */
+typedef struct avgpu_census {
+  uint64_t genotype_key;
+  double merit;
+  double fitness;
+  int32_t genome_length;
+  int32_t gestation_time;
+  int32_t copied_size;
+  int32_t executed_size;
+  int32_t generation;
+  int32_t num_divides;
+} avgpu_census;
+
 /* ---- inspection (cHardwareBase inspection API, cpu/cHardwareBase.h:145-200) */
 int avgpu_get_states(avgpu_world* w, int64_t first_cell, int64_t count,
                      avgpu_cpu_state* states, uint8_t* mem_ops, uint8_t* mem_flags,
                      int mem_cap);
+/* Census rows of cells first .. first+count-1 into host memory (48 B per
+ * cell): the data PrintDominantData / PrintCountData's genotype columns and
+ * the dominant genotype's averages are computed from on the host. */
+int avgpu_get_census(avgpu_world* w, int64_t first_cell, int64_t count, avgpu_census* out);
+/* checkpoint / resume: genotype keys of cells first .. first+count-1 (as
+ * avgpu_get_census reported them).  avgpu_set_states keys an organism from
+ * its tape prefix, which differs from the birth genome once an organism has
+ * copied into its own sites; a checkpoint carries the keys and sets them
+ * after avgpu_set_states (avida_amd/checkpoint.py). */
+int avgpu_set_genotype_keys(avgpu_world* w, int64_t first_cell, int64_t count, const uint64_t* keys);
 /* checkpoint / resume: the inverse of avgpu_get_states -- cells first ..
  * first+count-1 take states[i] and their tapes from mem_ops / mem_flags
  * (instruction-set op codes; flags bit0 copied, bit2 executed), mem_cap bytes

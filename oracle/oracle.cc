@@ -148,6 +148,7 @@ struct Org {
   bool advance_ip = true;
   // organism (main/cOrganism.h)
   std::vector<uint8_t> genome;  // m_initial_genome (birth genome)
+  uint64_t gkey_restored = 0;    // genotype key carried by a checkpoint (orc_set_genotype_keys)
   Buffer input_buf, output_buf;
   int input_ptr = 0;
   int max_executed = 0;
@@ -1084,6 +1085,58 @@ int orc_get_states(void* h, int64_t first, int64_t count, avgpu_cpu_state* st, u
   for (int64_t i = 0; i < count; i++)
     dump_state(w, w.orgs[first + i], &st[i], ops ? ops + i * cap : nullptr,
                flags ? flags + i * cap : nullptr, cap);
+  return 0;
+}
+
+// Genome key of a birth genome (the device's
+// gk_* in avida_amd/csrc/device.h): canonical codes handler[op] in 4-site
+// little-endian words, each mixed with its index, summed mod 2^64, mixed with
+// the length.  Stands in for the genome equality that files a newborn under
+// its genotype (Systematics::GenotypeArbiter::ClassifyNewUnit,
+// systematics/GenotypeArbiter.cc:280-380; hashGenome :470-480).
+static uint64_t gk_mix(uint64_t z) {
+  z ^= z >> 30; z *= 0xBF58476D1CE4E5B9ull;
+  z ^= z >> 27; z *= 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+static uint64_t genome_key(const World& w, const std::vector<uint8_t>& g) {
+  const int len = (int)g.size();
+  uint64_t sum = 0;
+  for (int wd = 0; wd < (len + 3) / 4; wd++) {
+    uint32_t v = 0;
+    for (int j = 0; j < 4 && 4 * wd + j < len; j++)
+      v |= (uint32_t)(w.is.handler[g[4 * wd + j]] & 0x3F) << (8 * j);
+    sum += gk_mix(((uint64_t)(wd + 1) << 32) | v);
+  }
+  const uint64_t k = gk_mix(sum ^ ((uint64_t)len * 0x9E3779B97F4A7C15ull));
+  return k ? k : 1ull;
+}
+
+int orc_get_census(void* h, int64_t first, int64_t count, avgpu_census* out) {
+  World& w = *(World*)h;
+  if (first < 0 || count < 0 || first + count > w.ncells) return fail(AVGPU_EINVAL, "cell range");
+  for (int64_t i = 0; i < count; i++) {
+    const Org& o = w.orgs[first + i];
+    avgpu_census& r = out[i];
+    memset(&r, 0, sizeof(r));
+    if (!o.alive) continue;
+    r.genotype_key = o.gkey_restored ? o.gkey_restored : genome_key(w, o.genome);
+    r.merit = o.merit;
+    r.fitness = o.fitness;
+    r.genome_length = (int)o.genome.size();
+    r.gestation_time = o.gestation_time;
+    r.copied_size = o.copied_size;
+    r.executed_size = o.executed_size;
+    r.generation = o.generation;
+    r.num_divides = o.num_divides;
+  }
+  return 0;
+}
+
+int orc_set_genotype_keys(void* h, int64_t first, int64_t count, const uint64_t* keys) {
+  World& w = *(World*)h;
+  if (first < 0 || count < 0 || first + count > w.ncells) return fail(AVGPU_EINVAL, "cell range");
+  for (int64_t i = 0; i < count; i++) w.orgs[first + i].gkey_restored = keys[i];
   return 0;
 }
 

@@ -99,6 +99,12 @@ class Backend:
         self._call("get_states", self.h, first, count, st, ops, fl, cap)
         return st, bytes(ops), bytes(fl)
 
+    def census(self, first=0, count=None):
+        """avgpu_census rows (numpy, capi.CENSUS_DTYPE) of a cell range"""
+        if count is None:
+            count = self.ncells - first
+        return capi.get_census(self.lib, self.p, self.h, first, count)
+
     def test_genomes(self, genomes, flags_cap=2049):
         n = len(genomes)
         blob = b"".join(genomes)

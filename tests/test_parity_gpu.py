@@ -260,8 +260,8 @@ def test_checkpoint_resume_across_backends(golden, tmp_path, kinds, env_kind):
 
 def test_driver_gpu_equals_oracle(golden, tmp_path):
     """avida_amd/driver.py on the GPU (ProductWorld) and on the oracle over the
-    spatial_res_100u config: the data files agree (count, tasks, resource
-    exactly; averages to print precision -- their sums reduce in another order)."""
+    spatial_res_100u config: the data files agree (count with its genotype
+    columns, tasks, resource, dominant exactly: the census is equal; averages to print precision -- their sums reduce in another order)."""
     from avida_amd import driver
     cfgdir = os.path.join(golden, "spatial_res_100u", "config")
     g, o = tmp_path / "gpu", tmp_path / "oracle"
@@ -272,7 +272,7 @@ def test_driver_gpu_equals_oracle(golden, tmp_path):
 
     def rows(p):
         return [l.split() for l in open(p) if l.strip() and not l.startswith("#")]
-    for name in ("count.dat", "tasks.dat", "resource.dat"):
+    for name in ("count.dat", "tasks.dat", "resource.dat", "dominant.dat"):
         assert rows(g / name) == rows(o / name), name
     for name in ("average.dat", "time.dat"):
         for a, b in zip(rows(g / name), rows(o / name)):

@@ -39,7 +39,7 @@ struct avgpu_world {
   int device = 0;
   hipStream_t stream = nullptr;      // current stream (own or external)
   hipStream_t own_stream = nullptr;
-  hipStream_t aux_stream[3] = {};   // classes 1..3 beside class 0 (world updates)
+  hipStream_t aux_stream[3] = {};   // [0] class 1, [1] classes 2 + 3 beside class 0 (world updates); [2] unused
   hipEvent_t ev_fork = nullptr, ev_join[3] = {};
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   // event ring around interpreter phases (avgpu_last_kernel_ms,
@@ -198,7 +198,6 @@ avgpu_world* create_world(const avgpu_cfg* cfg, int device, int64_t n, bool test
   if (hipStreamCreateWithFlags(&w->own_stream, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&w->aux_stream[0], hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&w->aux_stream[1], hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&w->aux_stream[2], hipStreamNonBlocking) != hipSuccess ||
       hipEventCreateWithFlags(&w->ev_fork, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&w->ev_join[0], hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&w->ev_join[1], hipEventDisableTiming) != hipSuccess ||

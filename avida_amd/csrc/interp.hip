@@ -18,6 +18,8 @@
 // Lanes whose next h-alloc would outgrow their LDS slot stop before it
 // ("spill") and are appended, with their remaining budget, to the next size
 // class, which is launched afterwards on the same stream.
+#include <cstdlib>
+
 #include "device.h"
 
 #pragma clang fp contract(off)
@@ -102,7 +104,8 @@ __device__ __forceinline__ bool consume_resource(const DevWorld& W, const double
 template <int S>
 __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp, int cls, int mode,
                                                 int64_t first, int64_t count, int64_t chunk,
-                                                uint32_t* __restrict__ lds32, bool sorted, int row) {
+                                                uint32_t* __restrict__ lds32, bool sorted, int row,
+                                                int lpw) {
   const DevWorld& W = *Wp;
   // per-lane tape stride: a whole number of 16-byte quads (16-B LDS-DMA) with
   // room for the fetch / label windows that read up to 16 bytes past a site
@@ -150,11 +153,12 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
       }
     }
   } else {
+    // list rows: lpw entries per wave (lanes >= lpw idle)
     const int lcount = W.class_count[row];
-    const int64_t base = chunk * 64;
+    const int64_t base = chunk * lpw;
     if (base >= lcount) return;
     const int idx = (int)base + lane;
-    if (idx < lcount) {
+    if (lane < lpw && idx < lcount) {
       cell = W.class_list[(int64_t)row * N + idx];
       M = W.mem_size[cell];
     }
@@ -1059,7 +1063,7 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
 // second bound caps it at 256 registers (VGPR + AGPR)
 template <int S>
 __global__ __launch_bounds__(64, (S == CLASS0_SIZE) ? 2 : 1) void k_interpret(const DevWorld* __restrict__ Wp, int cls, int row, int mode,
-                                                  int64_t first, int64_t count, int sorted) {
+                                                  int64_t first, int64_t count, int sorted, int lpw) {
   constexpr int TAB_WORDS = 128 + 64 + 16 + 64 + AVGPU_MAX_REACTIONS * RT_STRIDE + 64;
   // class 0: stacks in VGPRs, tables in global memory -- only the tapes in LDS
   constexpr int STK = (S == CLASS0_SIZE) ? 0 : 2 * AVGPU_STACK_SIZE * 64;
@@ -1070,18 +1074,29 @@ __global__ __launch_bounds__(64, (S == CLASS0_SIZE) ? 2 : 1) void k_interpret(co
     // dealt to the 8 XCDs round robin), so its state lines meet in one L2
     int64_t chunk = blockIdx.x;
     if (sorted && (gridDim.x & 7) == 0) chunk = (int64_t)(blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
-    interpret_chunk<S>(Wp, 0, mode, first, count, chunk, lds32, sorted, 0);
+    interpret_chunk<S>(Wp, 0, mode, first, count, chunk, lds32, sorted, 0, 64);
     return;
   }
   // list classes: grid-stride over the list (its length is known on device only)
   const int lcount = Wp->class_count[row];
-  for (int64_t chunk = blockIdx.x; chunk * 64 < lcount; chunk += gridDim.x) {
-    interpret_chunk<S>(Wp, cls, mode, first, count, chunk, lds32, false, row);
+  for (int64_t chunk = blockIdx.x; chunk * lpw < lcount; chunk += gridDim.x) {
+    interpret_chunk<S>(Wp, cls, mode, first, count, chunk, lds32, false, row, lpw);
     __syncthreads();
   }
 }
 
 }  // namespace
+
+// lanes per wave of the spill rows (AVGPU_SPILL_LPW overrides for sweeps)
+static int spill_lpw() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("AVGPU_SPILL_LPW");
+    const int x = e ? atoi(e) : 0;
+    v = (x >= 1 && x <= 64) ? x : 1;
+  }
+  return v;
+}
 
 void launch_interpret_classes(const DevWorld& W, const DevWorld* dW, int mode, hipStream_t s,
                               int64_t first, int64_t count, int* launches, hipEvent_t* after_class,
@@ -1099,30 +1114,39 @@ void launch_interpret_classes(const DevWorld& W, const DevWorld* dW, int mode, h
   // class 0; with an aux stream they run beside it and fill the CUs its tail
   // leaves idle.  Spills (rows 4..6) run after both, in class order.
   auto list = [&](int k, hipStream_t st) {
-    if (k == 1) hipLaunchKernelGGL(k_interpret<CLASS1_SIZE>, dim3(lb), dim3(64), 0, st, dW, 1, 1, mode, first, count, 0);
-    if (k == 2) hipLaunchKernelGGL(k_interpret<CLASS2_SIZE>, dim3(lb), dim3(64), 0, st, dW, 2, 2, mode, first, count, 0);
-    if (k == 3) hipLaunchKernelGGL(k_interpret<CLASS3_SIZE>, dim3(lb), dim3(64), 0, st, dW, 3, 3, mode, first, count, 0);
+    if (k == 1) hipLaunchKernelGGL(k_interpret<CLASS1_SIZE>, dim3(lb), dim3(64), 0, st, dW, 1, 1, mode, first, count, 0, 64);
+    if (k == 2) hipLaunchKernelGGL(k_interpret<CLASS2_SIZE>, dim3(lb), dim3(64), 0, st, dW, 2, 2, mode, first, count, 0, 64);
+    if (k == 3) hipLaunchKernelGGL(k_interpret<CLASS3_SIZE>, dim3(lb), dim3(64), 0, st, dW, 3, 3, mode, first, count, 0, 64);
   };
-  if (aux) {
-    // one aux stream per list: each is latency-bound on its longest slice
-    hipEventRecord(ev_fork, s);
-    for (int k = 0; k < 3; k++) {
-      hipStreamWaitEvent(aux[k], ev_fork, 0);
-      list(k + 1, aux[k]);
-      hipEventRecord(ev_join[k], aux[k]);
-    }
-  }
-  hipLaunchKernelGGL(k_interpret<CLASS0_SIZE>, dim3(blocks), dim3(64), 0, s, dW, 0, 0, mode, first, count, srt);
+  // Class 0 is submitted first so that nothing queued for the aux lists can
+  // sit in front of it.  Two aux streams (class 1; classes 2 + 3, which are
+  // short): with the world's stream that is three HIP streams, so they keep
+  // distinct hardware queues (GPU_MAX_HW_QUEUES = 4); a third aux stream
+  // shared a queue with the world's stream and serialised class 3 in front
+  // of class 0.
+  if (aux) hipEventRecord(ev_fork, s);
+  hipLaunchKernelGGL(k_interpret<CLASS0_SIZE>, dim3(blocks), dim3(64), 0, s, dW, 0, 0, mode, first, count, srt, 64);
   if (after_class) hipEventRecord(after_class[0], s);
-  if (aux)
-    for (int k = 0; k < 3; k++) hipStreamWaitEvent(s, ev_join[k], 0);
-  else
+  if (aux) {
+    for (int k = 0; k < 2; k++) hipStreamWaitEvent(aux[k], ev_fork, 0);
+    list(1, aux[0]);
+    list(2, aux[1]);
+    list(3, aux[1]);
+    for (int k = 0; k < 2; k++) {
+      hipEventRecord(ev_join[k], aux[k]);
+      hipStreamWaitEvent(s, ev_join[k], 0);
+    }
+  } else
     for (int k = 1; k <= 3; k++) list(k, s);
-  hipLaunchKernelGGL(k_interpret<CLASS1_SIZE>, dim3(lb), dim3(64), 0, s, dW, 1, 4, mode, first, count, 0);
+  // Spill rows run after class 0, alone on the chip and latency-bound on their
+  // longest remaining slice; spread over waves (spill_lpw lanes each), a
+  // wave's iterations no longer pay for its other lanes' divergent paths.
+  const int slpw = spill_lpw();
+  hipLaunchKernelGGL(k_interpret<CLASS1_SIZE>, dim3(lb), dim3(64), 0, s, dW, 1, 4, mode, first, count, 0, slpw);
   if (after_class) hipEventRecord(after_class[1], s);
-  hipLaunchKernelGGL(k_interpret<CLASS2_SIZE>, dim3(lb), dim3(64), 0, s, dW, 2, 5, mode, first, count, 0);
+  hipLaunchKernelGGL(k_interpret<CLASS2_SIZE>, dim3(lb), dim3(64), 0, s, dW, 2, 5, mode, first, count, 0, slpw);
   if (after_class) hipEventRecord(after_class[2], s);
-  hipLaunchKernelGGL(k_interpret<CLASS3_SIZE>, dim3(lb), dim3(64), 0, s, dW, 3, 6, mode, first, count, 0);
+  hipLaunchKernelGGL(k_interpret<CLASS3_SIZE>, dim3(lb), dim3(64), 0, s, dW, 3, 6, mode, first, count, 0, slpw);
   if (after_class) hipEventRecord(after_class[3], s);
   if (launches) *launches += 7;
 }

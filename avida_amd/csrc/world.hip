@@ -589,18 +589,22 @@ struct Child {
   const int32_t* ltask;   // the parent's last task counts, ltask[q * lstride]
   int64_t lstride;
 };
+// Run by a group of G lanes (G = 64: a wave, 32: a half-wave); `lane` is the
+// lane's index inside its group.
+template <int G>
 __device__ __forceinline__ void setup_child(const DevWorld& W, int64_t c, const Child& b,
                                             const uint32_t* src, int lane) {
+  static_assert(G == 32 || G == 64, "group = wave or half-wave");
   const int64_t N = W.n;
   const int len = b.len;
   uint32_t* dst = reinterpret_cast<uint32_t*>(W.tape + c * TAPE_SLOT);
   uint64_t gsum = 0;
-  for (int w = lane; w < (len + 3) / 4; w += 64) {
+  for (int w = lane; w < (len + 3) / 4; w += G) {
     const uint32_t v = src[w];
     dst[w] = v;
     gsum += gk_word(v, w, len);
   }
-  for (int off = 32; off > 0; off >>= 1) gsum += __shfl_xor(gsum, off);
+  for (int off = G / 2; off > 0; off >>= 1) gsum += __shfl_xor(gsum, off);
   if (lane == 0) W.gkey[c] = gk_final(gsum, len);
   switch (lane) {
     case 0: W.ctl[c] = CTL_ALIVE | CTL_FRESH; break;
@@ -633,13 +637,15 @@ __device__ __forceinline__ void setup_child(const DevWorld& W, int64_t c, const 
   }
 }
 
-// One wave per queued birth: the winners of cells inside the tile are
-// activated; winners of ghost-row cells were shipped by k_halo_pack.
+// One half-wave per queued birth (a genome of <= 128 sites is one 32-lane
+// pass, and the 21 stored fields fit 32 lanes): the winners of cells inside
+// the tile are activated; winners of ghost-row cells were shipped by
+// k_halo_pack.
 __global__ __launch_bounds__(64) void k_activate(DevWorld W) {
   const int nb = queue_len(W);
-  const int lane = threadIdx.x;
+  const int lane = threadIdx.x & 31;
   unsigned long long born = 0, lost = 0;
-  for (int64_t q = blockIdx.x; q < nb; q += gridDim.x) {
+  for (int64_t q = 2 * (int64_t)blockIdx.x + (threadIdx.x >> 5); q < nb; q += 2 * (int64_t)gridDim.x) {
     const int64_t i = rec_of(W, q);
     const int tgt = W.b_target[i];
     const bool won = W.b_state[i] > 0 && tgt >= 0 && W.owner[tgt] == (int)i;
@@ -651,9 +657,11 @@ __global__ __launch_bounds__(64) void k_activate(DevWorld W) {
     b.gest = W.b_gest[i]; b.merit = W.b_merit[i]; b.fitness = W.b_fitness[i];
     b.lo = W.b_rng[i]; b.hi = W.b_rng[W.rcap + i]; b.ctr = W.b_rng[2 * W.rcap + i];
     b.ltask = W.b_ltask + i; b.lstride = W.rcap;
-    setup_child(W, tgt, b, reinterpret_cast<const uint32_t*>(W.b_genome + i * TAPE_SLOT), lane);
+    setup_child<32>(W, tgt, b, reinterpret_cast<const uint32_t*>(W.b_genome + i * TAPE_SLOT), lane);
   }
-  if (lane == 0) {
+  born += __shfl_xor(born, 32);                 // both halves' lane 0
+  lost += __shfl_xor(lost, 32);
+  if (threadIdx.x == 0) {
     if (born) count_add(W, CNT_BIRTHS, born);
     if (lost) count_add(W, CNT_DROPPED, lost);
   }
@@ -730,7 +738,7 @@ __global__ __launch_bounds__(64) void k_activate_remote(DevWorld W, int d) {
     b.len = r.len; b.gen = r.gen; b.ccopied = r.ccopied; b.exec = r.exec; b.gest = r.gest;
     b.merit = r.merit; b.fitness = r.fitness; b.lo = r.rng_lo; b.hi = r.rng_hi; b.ctr = r.rng_ctr;
     b.ltask = recs[q].last_task; b.lstride = 1;
-    setup_child(W, c, b, reinterpret_cast<const uint32_t*>(arena + r.off), lane);
+    setup_child<64>(W, c, b, reinterpret_cast<const uint32_t*>(arena + r.off), lane);
   }
   if (lane == 0) {
     if (born) count_add(W, CNT_BIRTHS, born);
@@ -886,11 +894,17 @@ void launch_merit_total(const DevWorld& W, hipStream_t s, double* totals, double
                      (const double*)nullptr, nb, 1, totals, 0);
 }
 
+// the update's counters, birth-queue and class-list lengths, zeroed by one
+// launch instead of three fill packets (~10 us each on the queue)
+__global__ __launch_bounds__(256) void k_reset_counts(DevWorld W) {
+  for (int i = threadIdx.x; i < NSHARD * CNT_STRIDE; i += 256) W.counters[i] = 0ull;
+  if (threadIdx.x < 2) W.b_count[threadIdx.x] = 0;
+  if (threadIdx.x < 8) W.class_count[threadIdx.x] = 0;
+}
+
 void launch_world_pre(const DevWorld& W, hipStream_t s, const double* totals) {
   launch_resources_begin(W, s);   // ProcessPreUpdate + the update's first DoUpdates
-  hipMemsetAsync(W.counters, 0, sizeof(unsigned long long) * NSHARD * CNT_STRIDE, s);
-  hipMemsetAsync(W.b_count, 0, 2 * sizeof(int32_t), s);
-  hipMemsetAsync(W.class_count, 0, sizeof(int32_t) * 8, s);
+  hipLaunchKernelGGL(k_reset_counts, dim3(1), dim3(256), 0, s, W);
   hipLaunchKernelGGL(k_allot, dim3(nblk(W.n, 256)), dim3(256), 0, s, W, totals);
   hipLaunchKernelGGL(k_window_sort, dim3(nblk(W.n, SORT_WIN)), dim3(1024), 0, s, W);
 }

@@ -307,8 +307,9 @@ int set_orgs_impl(avgpu_world* w, int64_t first, int64_t count, const uint8_t* g
 int drain_ring(avgpu_world* w, int keep) {
   while (w->ring_count > keep) {
     const int i = (w->ring_head - w->ring_count + avgpu_world::RING) % avgpu_world::RING;
-    HIPCHK(hipEventSynchronize(w->ring[i][NUM_CLASSES]));
-    for (int k = 0; k < NUM_CLASSES; k++) {
+    const int nk = class_timing_all() ? NUM_CLASSES : 1;   // class 0 only: 2 events
+    HIPCHK(hipEventSynchronize(w->ring[i][nk]));
+    for (int k = 0; k < nk; k++) {
       float f = 0.f;
       HIPCHK(hipEventElapsedTime(&f, w->ring[i][k], w->ring[i][k + 1]));
       w->acc_class_ms[k] += f;
@@ -602,7 +603,7 @@ int avgpu_update_run(avgpu_world* w, const double* dev_totals, avgpu_update_stat
   int rc = ready(w);
   if (rc < 0) return rc;
   if (!dev_totals) return fail(AVGPU_EINVAL, "dev_totals is NULL");
-  launch_world_pre(w->W, w->stream, dev_totals);
+  launch_world_pre(w->W, w->stream, dev_totals, w->ev_fork);
   after_resources_begin(w);
   HIPCHK(hipGetLastError());
   rc = interpret(w, AVGPU_MODE_WORLD, 0, w->W.n, true);
@@ -1123,7 +1124,7 @@ int avgpu_tile_begin(avgpu_world* w, const double* dev_gathered, int ntiles) {
     return fail(AVGPU_ESTATE, "spatial resources need avgpu_set_tile_res_buffers");
   if (!dev_gathered || ntiles < 1) return fail(AVGPU_EINVAL, "gathered partials");
   launch_tile_totals(w->W, w->stream, dev_gathered, ntiles, w->d_totals);
-  launch_world_pre(w->W, w->stream, w->d_totals);
+  launch_world_pre(w->W, w->stream, w->d_totals, w->ev_fork);
   after_resources_begin(w);
   HIPCHK(hipGetLastError());
   rc = interpret(w, AVGPU_MODE_WORLD, 0, w->W.n, true);

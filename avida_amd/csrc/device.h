@@ -423,7 +423,8 @@ void launch_interpret_classes(const DevWorld& W, const DevWorld* dW, int mode, h
 // class-0 windows: k_allot's budgets sorted (descending) inside windows of
 // SORT_WIN cells, so that a wave's 64 organisms get similar time slices
 #define SORT_WIN 2048
-void launch_world_pre(const DevWorld& W, hipStream_t s, const double* d_totals);
+bool class_timing_all();   // AVGPU_CLASS_TIMING (interp.hip)
+void launch_world_pre(const DevWorld& W, hipStream_t s, const double* d_totals, hipEvent_t lists_ready);
 void launch_resources_begin(const DevWorld& W, hipStream_t s);
 void launch_resources_end(const DevWorld& W, hipStream_t s);
 void launch_resources_pack(const DevWorld& W, hipStream_t s);

@@ -1098,13 +1098,31 @@ static int spill_lpw() {
   return v;
 }
 
+// timing events after every class (default) or after class 0 only
+// (AVGPU_CLASS_TIMING=0): each timed event record costs ~10 us of queue time
+bool class_timing_all() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("AVGPU_CLASS_TIMING");
+    v = (e && atoi(e) == 0) ? 0 : 1;
+  }
+  return v == 1;
+}
+
 void launch_interpret_classes(const DevWorld& W, const DevWorld* dW, int mode, hipStream_t s,
                               int64_t first, int64_t count, int* launches, hipEvent_t* after_class,
                               bool sorted, hipStream_t* aux, hipEvent_t ev_fork, hipEvent_t* ev_join) {
   const int srt = (sorted && first == 0 && count == W.n) ? 1 : 0;
+  const bool tall = class_timing_all();
   const unsigned blocks = (unsigned)((count + 63) / 64);
-  // list classes: a capped grid strides over the list
-  const unsigned lb = std::min(blocks, 2048u);
+  // list classes: a capped grid strides over the list (length known on the
+  // device only).  The caps follow the blocks a CU holds (LDS: 3 of class 1,
+  // 1 of classes 2 / 3) and the lists' usual lengths (class 1 ~1 %, classes
+  // 2 / 3 and the spill rows tens of organisms): a 2048-block grid of
+  // 132-KiB class-3 blocks costs 8 dispatch rounds even when its list is
+  // empty.
+  const unsigned lb = std::min(blocks, 768u);
+  const unsigned lb_small = std::min(blocks, 256u);
   if (blocks == 0) {
     if (after_class)
       for (int k = 0; k < 4; k++) hipEventRecord(after_class[k], s);
@@ -1115,38 +1133,39 @@ void launch_interpret_classes(const DevWorld& W, const DevWorld* dW, int mode, h
   // leaves idle.  Spills (rows 4..6) run after both, in class order.
   auto list = [&](int k, hipStream_t st) {
     if (k == 1) hipLaunchKernelGGL(k_interpret<CLASS1_SIZE>, dim3(lb), dim3(64), 0, st, dW, 1, 1, mode, first, count, 0, 64);
-    if (k == 2) hipLaunchKernelGGL(k_interpret<CLASS2_SIZE>, dim3(lb), dim3(64), 0, st, dW, 2, 2, mode, first, count, 0, 64);
-    if (k == 3) hipLaunchKernelGGL(k_interpret<CLASS3_SIZE>, dim3(lb), dim3(64), 0, st, dW, 3, 3, mode, first, count, 0, 64);
+    if (k == 2) hipLaunchKernelGGL(k_interpret<CLASS2_SIZE>, dim3(lb_small), dim3(64), 0, st, dW, 2, 2, mode, first, count, 0, 64);
+    if (k == 3) hipLaunchKernelGGL(k_interpret<CLASS3_SIZE>, dim3(lb_small), dim3(64), 0, st, dW, 3, 3, mode, first, count, 0, 64);
   };
-  // Class 0 is submitted first so that nothing queued for the aux lists can
-  // sit in front of it.  Two aux streams (class 1; classes 2 + 3, which are
-  // short): with the world's stream that is three HIP streams, so they keep
-  // distinct hardware queues (GPU_MAX_HW_QUEUES = 4); a third aux stream
-  // shared a queue with the world's stream and serialised class 3 in front
-  // of class 0.
-  if (aux) hipEventRecord(ev_fork, s);
-  hipLaunchKernelGGL(k_interpret<CLASS0_SIZE>, dim3(blocks), dim3(64), 0, s, dW, 0, 0, mode, first, count, srt, 64);
-  if (after_class) hipEventRecord(after_class[0], s);
+  // Two aux streams (class 1; classes 2 + 3, which are short): with the
+  // world's stream that is three HIP streams, so they keep distinct hardware
+  // queues (GPU_MAX_HW_QUEUES = 4); a third aux stream shared a queue with
+  // the world's stream and serialised class 3 in front of class 0.  The aux
+  // lists start after k_allot, beside k_window_sort, so that they take their
+  // CUs before class 0 and end well inside it (forked after the sort they only
+  // got CUs as class-0 waves retired and ended ~40-55 us after class 0).
   if (aux) {
+    // ev_fork: recorded by launch_world_pre right after k_allot built the lists
     for (int k = 0; k < 2; k++) hipStreamWaitEvent(aux[k], ev_fork, 0);
     list(1, aux[0]);
     list(2, aux[1]);
     list(3, aux[1]);
-    for (int k = 0; k < 2; k++) {
-      hipEventRecord(ev_join[k], aux[k]);
-      hipStreamWaitEvent(s, ev_join[k], 0);
-    }
+    for (int k = 0; k < 2; k++) hipEventRecord(ev_join[k], aux[k]);
+  }
+  hipLaunchKernelGGL(k_interpret<CLASS0_SIZE>, dim3(blocks), dim3(64), 0, s, dW, 0, 0, mode, first, count, srt, 64);
+  if (after_class) hipEventRecord(after_class[0], s);
+  if (aux) {
+    for (int k = 0; k < 2; k++) hipStreamWaitEvent(s, ev_join[k], 0);
   } else
     for (int k = 1; k <= 3; k++) list(k, s);
   // Spill rows run after class 0, alone on the chip and latency-bound on their
   // longest remaining slice; spread over waves (spill_lpw lanes each), a
   // wave's iterations no longer pay for its other lanes' divergent paths.
   const int slpw = spill_lpw();
-  hipLaunchKernelGGL(k_interpret<CLASS1_SIZE>, dim3(lb), dim3(64), 0, s, dW, 1, 4, mode, first, count, 0, slpw);
-  if (after_class) hipEventRecord(after_class[1], s);
-  hipLaunchKernelGGL(k_interpret<CLASS2_SIZE>, dim3(lb), dim3(64), 0, s, dW, 2, 5, mode, first, count, 0, slpw);
-  if (after_class) hipEventRecord(after_class[2], s);
-  hipLaunchKernelGGL(k_interpret<CLASS3_SIZE>, dim3(lb), dim3(64), 0, s, dW, 3, 6, mode, first, count, 0, slpw);
-  if (after_class) hipEventRecord(after_class[3], s);
+  hipLaunchKernelGGL(k_interpret<CLASS1_SIZE>, dim3(lb_small), dim3(64), 0, s, dW, 1, 4, mode, first, count, 0, slpw);
+  if (after_class && tall) hipEventRecord(after_class[1], s);
+  hipLaunchKernelGGL(k_interpret<CLASS2_SIZE>, dim3(std::min(lb_small, 64u)), dim3(64), 0, s, dW, 2, 5, mode, first, count, 0, slpw);
+  if (after_class && tall) hipEventRecord(after_class[2], s);
+  hipLaunchKernelGGL(k_interpret<CLASS3_SIZE>, dim3(std::min(lb_small, 64u)), dim3(64), 0, s, dW, 3, 6, mode, first, count, 0, slpw);
+  if (after_class && tall) hipEventRecord(after_class[3], s);
   if (launches) *launches += 7;
 }

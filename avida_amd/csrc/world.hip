@@ -902,10 +902,13 @@ __global__ __launch_bounds__(256) void k_reset_counts(DevWorld W) {
   if (threadIdx.x < 8) W.class_count[threadIdx.x] = 0;
 }
 
-void launch_world_pre(const DevWorld& W, hipStream_t s, const double* totals) {
+void launch_world_pre(const DevWorld& W, hipStream_t s, const double* totals, hipEvent_t lists_ready) {
   launch_resources_begin(W, s);   // ProcessPreUpdate + the update's first DoUpdates
   hipLaunchKernelGGL(k_reset_counts, dim3(1), dim3(256), 0, s, W);
   hipLaunchKernelGGL(k_allot, dim3(nblk(W.n, 256)), dim3(256), 0, s, W, totals);
+  // the class lists are complete: the aux streams of the list classes start
+  // here, beside the window sort (launch_interpret_classes)
+  hipEventRecord(lists_ready, s);
   hipLaunchKernelGGL(k_window_sort, dim3(nblk(W.n, SORT_WIN)), dim3(1024), 0, s, W);
 }
 

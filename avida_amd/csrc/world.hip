@@ -750,6 +750,7 @@ __global__ __launch_bounds__(64) void k_activate_remote(DevWorld W, int d) {
 // partial slots: 0 orgs 1 merit 2 fitness 3 gestation 4 genome length 5 max fitness
 // 6 generation 7 memory size 8..16 task organisms
 #define NPART 24
+#define NUSED (8 + AVGPU_NUM_LOGIC_TASKS)
 #define NSTAT 40
 __device__ __forceinline__ double wave_sum(double v) {
   for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
@@ -779,13 +780,15 @@ __global__ __launch_bounds__(256) void k_stats_partial(DevWorld W, double* part)
 #pragma unroll
     for (int t = 0; t < AVGPU_NUM_LOGIC_TASKS; t++) v[8 + t] = W.last_task[t * W.n + c] > 0 ? 1.0 : 0.0;
   }
+  // only the NUSED slots carry data (the rest of the NPART rows are never
+  // written and k_stats_final reports them as 0)
 #pragma unroll
-  for (int k = 0; k < NPART; k++) {
+  for (int k = 0; k < NUSED; k++) {
     const double r = (k == 5) ? wave_max(v[k]) : wave_sum(v[k]);
     if (lane == 0) s[wv][k] = r;
   }
   __syncthreads();
-  if (threadIdx.x < NPART) {
+  if (threadIdx.x < NUSED) {
     const int k = threadIdx.x;
     double r = s[0][k];
     for (int q = 1; q < 4; q++) r = (k == 5) ? fmax(r, s[q][k]) : r + s[q][k];
@@ -804,6 +807,10 @@ __global__ __launch_bounds__(256) void k_stats_final(DevWorld W, const double* p
   __shared__ unsigned long long cs[8][CNT_STRIDE];
   const int tid = threadIdx.x;
   const int k = blockIdx.x;
+  if (k >= NUSED && k < NPART) {
+    if (tid == 0) out[k] = 0.0;
+    return;
+  }
   if (k < NPART) {
     const bool mx = k == 5;
     double acc = 0.0;

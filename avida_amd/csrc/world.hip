@@ -20,31 +20,30 @@ namespace {
 // serialised ~16K waves in L2), lanes then write at block base + wave offset
 // + rank.  blockDim.x must be 256.
 __device__ __forceinline__ void enqueue_class(const DevWorld& W, int cell, bool want, int cls) {
-  __shared__ int s_cnt[NUM_CLASSES], s_base[NUM_CLASSES];
+  __shared__ int s_pc[NUM_CLASSES][4], s_base[NUM_CLASSES];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  if (threadIdx.x < NUM_CLASSES) s_cnt[threadIdx.x] = 0;
-  __syncthreads();
-  int woff[NUM_CLASSES];
   unsigned long long masks[NUM_CLASSES];
+  __syncthreads();                             // s_pc / s_base free (repeat calls)
 #pragma unroll
   for (int k = 1; k < NUM_CLASSES; k++) {
     masks[k] = __ballot(want && cls == k);
-    woff[k] = 0;
-    // waves take their offsets in wave order (deterministic list order)
-    for (int w = 0; w < 4; w++) {
-      if (w == wv && lane == 0 && masks[k]) s_cnt[k] += __popcll(masks[k]);
-      __syncthreads();
-      if (w == wv) woff[k] = s_cnt[k] - __popcll(masks[k]);
-    }
+    if (lane == 0) s_pc[k][wv] = __popcll(masks[k]);
   }
-  if (threadIdx.x > 0 && threadIdx.x < NUM_CLASSES)
-    s_base[threadIdx.x] = s_cnt[threadIdx.x] ? atomicAdd(&W.class_count[threadIdx.x], s_cnt[threadIdx.x]) : 0;
+  __syncthreads();
+  // waves take their offsets in wave order (deterministic list order)
+  if (threadIdx.x > 0 && threadIdx.x < NUM_CLASSES) {
+    const int k = threadIdx.x;
+    const int tot = s_pc[k][0] + s_pc[k][1] + s_pc[k][2] + s_pc[k][3];
+    s_base[k] = tot ? atomicAdd(&W.class_count[k], tot) : 0;
+  }
   __syncthreads();
 #pragma unroll
   for (int k = 1; k < NUM_CLASSES; k++) {
     if (want && cls == k) {
+      int woff = 0;
+      for (int w = 0; w < wv; w++) woff += s_pc[k][w];
       const int rank = __popcll(masks[k] & ((1ull << lane) - 1ull));
-      W.class_list[(int64_t)k * W.n + s_base[k] + woff[k] + rank] = cell;
+      W.class_list[(int64_t)k * W.n + s_base[k] + woff + rank] = cell;
     }
   }
 }

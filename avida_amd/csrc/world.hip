@@ -760,33 +760,51 @@ __device__ __forceinline__ double wave_max(double v) {
   return v;
 }
 // part layout [NPART][nb] so that k_stats_final reads it coalesced
+__device__ __forceinline__ int wave_sum_i(int v) {
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+  return v;
+}
+__device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v) {
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+  return v;
+}
+// Integer-valued slots (organisms, gestation, genome length, generation,
+// memory, task organisms) reduce as integers: their double sums are exact in
+// any order, so the partials are the same numbers at a third of the shuffle
+// work; the nine task flags go as one u64 of 7-bit lanes (<= 64 per wave).
 __global__ __launch_bounds__(256) void k_stats_partial(DevWorld W, double* part) {
   __shared__ double s[4][NPART];
   const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  double v[NPART];
-#pragma unroll
-  for (int k = 0; k < NPART; k++) v[k] = 0.0;
+  double merit = 0.0, fit = 0.0;
+  int iv[5] = {0, 0, 0, 0, 0};                 // slots 0 3 4 6 7
+  unsigned long long tasks = 0;
   if (c < W.n && (W.ctl[c] & CTL_ALIVE)) {
-    v[0] = 1.0;
-    v[1] = W.merit[c];
-    v[2] = W.fitness[c];
-    v[3] = (double)W.gest_time[c];
-    v[4] = (double)W.birth_len[c];
-    v[5] = W.fitness[c];   // max
-    v[6] = (double)W.generation[c];
-    v[7] = (double)W.mem_size[c];
+    merit = W.merit[c];
+    fit = W.fitness[c];
+    iv[0] = 1;
+    iv[1] = W.gest_time[c];
+    iv[2] = W.birth_len[c];
+    iv[3] = W.generation[c];
+    iv[4] = W.mem_size[c];
 #pragma unroll
-    for (int t = 0; t < AVGPU_NUM_LOGIC_TASKS; t++) v[8 + t] = W.last_task[t * W.n + c] > 0 ? 1.0 : 0.0;
+    for (int t = 0; t < AVGPU_NUM_LOGIC_TASKS; t++)
+      tasks |= (W.last_task[t * W.n + c] > 0 ? 1ull : 0ull) << (7 * t);
   }
-  // only the NUSED slots carry data (the rest of the NPART rows are never
-  // written and k_stats_final reports them as 0)
+  const double rm = wave_sum(merit), rf = wave_sum(fit), rx = wave_max(fit);
+  int ri[5];
 #pragma unroll
-  for (int k = 0; k < NUSED; k++) {
-    const double r = (k == 5) ? wave_max(v[k]) : wave_sum(v[k]);
-    if (lane == 0) s[wv][k] = r;
+  for (int k = 0; k < 5; k++) ri[k] = wave_sum_i(iv[k]);
+  const unsigned long long rt = wave_sum_u64(tasks);
+  if (lane == 0) {
+    s[wv][0] = (double)ri[0]; s[wv][1] = rm; s[wv][2] = rf; s[wv][3] = (double)ri[1];
+    s[wv][4] = (double)ri[2]; s[wv][5] = rx; s[wv][6] = (double)ri[3]; s[wv][7] = (double)ri[4];
+#pragma unroll
+    for (int t = 0; t < AVGPU_NUM_LOGIC_TASKS; t++) s[wv][8 + t] = (double)((rt >> (7 * t)) & 127ull);
   }
   __syncthreads();
+  // only the NUSED slots carry data (the rest of the NPART rows are never
+  // written and k_stats_final reports them as 0)
   if (threadIdx.x < NUSED) {
     const int k = threadIdx.x;
     double r = s[0][k];

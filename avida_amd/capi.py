@@ -154,11 +154,56 @@ EXPORTED = [
     "avgpu_tile_begin", "avgpu_tile_place", "avgpu_tile_finish", "avgpu_tile_res_bytes",
     "avgpu_set_tile_res_buffers", "avgpu_tile_res_cons", "avgpu_tile_res_settle",
     "avgpu_last_step_insts", "avgpu_last_kernel_ms", "avgpu_kernel_times", "avgpu_counters",
+    "avgpu_state_digests",
 ]
 
 
+# avida.cfg knobs that change the semantics of this path when non-zero and
+# that it does not implement (main/cAvidaConfig.h:309-361, 372): the per-site,
+# Poisson, translocation, lateral-transfer, parent, point, inject and meta
+# mutations, copy uniform / slip, death on divide.  cfg_from_avida refuses a
+# config that sets any of them rather than run it with different semantics.
+# (COPY_INS_PROB / COPY_DEL_PROB travel in avgpu_cfg; avgpu_create refuses them.)
+UNSUPPORTED_NONZERO = [
+    "COPY_UNIFORM_PROB", "COPY_SLIP_PROB",
+    "POINT_MUT_PROB", "POINT_INS_PROB", "POINT_DEL_PROB", "INST_POINT_MUT_PROB",
+    "DIV_MUT_PROB", "DIV_INS_PROB", "DIV_DEL_PROB", "DIV_UNIFORM_PROB", "DIV_SLIP_PROB",
+    "DIV_TRANS_PROB", "DIV_LGT_PROB",
+    "DIVIDE_SLIP_PROB", "DIVIDE_UNIFORM_PROB", "DIVIDE_TRANS_PROB", "DIVIDE_LGT_PROB",
+    "DIVIDE_POISSON_MUT_MEAN", "DIVIDE_POISSON_INS_MEAN", "DIVIDE_POISSON_DEL_MEAN",
+    "DIVIDE_POISSON_SLIP_MEAN", "DIVIDE_POISSON_TRANS_MEAN", "DIVIDE_POISSON_LGT_MEAN",
+    "INJECT_MUT_PROB", "INJECT_INS_PROB", "INJECT_DEL_PROB",
+    "PARENT_MUT_PROB", "PARENT_INS_PROB", "PARENT_DEL_PROB",
+    "META_COPY_MUT", "META_STD_DEV", "DEATH_PROB",
+]
+# Knobs accepted without effect, with the reason.  SPECULATIVE only decides
+# whether the reference's serial ProcessStep pre-executes up to 32 more
+# instructions of the picked organism (main/cPopulation.cc:5740-5788); the
+# batched update has no serial interleaving to speculate on.
+IGNORED = {"SPECULATIVE": "batched update: no serial schedule to speculate on"}
+
+
+def unsupported_knobs(cfg):
+    """Names of the UNSUPPORTED_NONZERO keys a files.AvidaConfig sets non-zero."""
+    bad = []
+    for k in UNSUPPORTED_NONZERO:
+        v = cfg.get(k, 0)
+        try:
+            nz = float(v) != 0.0
+        except (TypeError, ValueError):
+            nz = True
+        if nz:
+            bad.append(k)
+    return bad
+
+
 def cfg_from_avida(cfg, seed=None) -> AvgpuCfg:
-    """Fill an AvgpuCfg from a files.AvidaConfig."""
+    """Fill an AvgpuCfg from a files.AvidaConfig; raise ValueError for a knob
+    of UNSUPPORTED_NONZERO set non-zero."""
+    bad = unsupported_knobs(cfg)
+    if bad:
+        raise ValueError("avida.cfg sets mutation / death knobs this path does not implement: "
+                         + ", ".join(bad))
     g = cfg.get
     c = AvgpuCfg()
     c.world_x, c.world_y = g("WORLD_X"), g("WORLD_Y")
@@ -267,6 +312,7 @@ def bind_common(lib, prefix):
         "set_clock": (C.c_int, [V, C.POINTER(AvgpuUpdateStats)]),
         "get_census": (C.c_int, [V, I64, I64, V]),
         "set_genotype_keys": (C.c_int, [V, I64, I64, V]),
+        "state_digests": (C.c_int, [V, I64, I64, V]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, p + name, None)

@@ -34,6 +34,7 @@
 #define CTL_FRESH 0x800u
 
 #define NUM_CLASSES 4
+#define ACLASS_NONE 0xFF
 // react_res row: resource slot+1 (0 infinite), spatial?, depletable, type, frac, min, max, value
 #define RR_STRIDE 8
 enum { RR_RES = 0, RR_SPATIAL = 1, RR_DEPL = 2, RR_TYPE = 3, RR_FRAC = 4, RR_MIN = 5, RR_MAX = 6, RR_VALUE = 7 };
@@ -73,6 +74,13 @@ struct DevWorld {
   uint64_t* gkey;     // [n]  genome key of the birth genome (systematics census)
   uint32_t* rng;      // [3][n] key_lo, key_hi, ctr
   int32_t* budget;    // [n]  instructions left in this update
+  // [n] size class k_allot / k_classify_uniform gave the cell's slice this
+  // update (0..3, ACLASS_NONE: no slice).  Only those kernels write it: the
+  // class-0 launch and k_window_sort select their cells by this tag, never by
+  // the live mem_size / budget that list classes running beside them on the
+  // aux streams rewrite (a list-class slice that divides down to a class-0
+  // size must not be picked up by class 0 in the same update).
+  uint8_t* aclass;
   uint8_t* tape;      // [n][TAPE_SLOT]
   // --- cold state (touched in place by IO / stack / divide) ---
   int32_t* stack;     // [2*10][n]
@@ -440,6 +448,7 @@ void launch_get_states(const DevWorld& W, hipStream_t s, int64_t first, int64_t 
                        avgpu_cpu_state* d_states, uint8_t* d_codes, int cap);
 void launch_set_states(const DevWorld& W, hipStream_t s, int64_t first, int64_t count, const avgpu_cpu_state* in,
                        const uint8_t* codes, int cap);
+void launch_state_digest(const DevWorld& W, hipStream_t s, int64_t first, int64_t count, uint64_t* d_out);
 void launch_get_census(const DevWorld& W, hipStream_t s, int64_t first, int64_t count, avgpu_census* d_out);
 void launch_merit_total(const DevWorld& W, hipStream_t s, double* d_totals, double* d_scratch);
 // strip tiles

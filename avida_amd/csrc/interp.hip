@@ -144,13 +144,11 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
     // budget-sorted windows of k_window_sort
     const int64_t c = sorted ? (chunk * 64 + lane < count ? (int64_t)W.order[chunk * 64 + lane] : first + count)
                              : first + chunk * 64 + lane;
-    if (c < first + count) {
-      const uint32_t c0 = W.ctl[c];
-      const int m0 = W.mem_size[c];
-      if ((c0 & CTL_ALIVE) && W.budget[c] > 0 && class_of(need_of(m0, c0, W.size_range)) == 0) {
-        cell = (int)c;
-        M = m0;
-      }
+    // the cell's slice is class 0 by k_allot's tag (device.h aclass), not by
+    // its live size: list classes may be rewriting their cells concurrently
+    if (c < first + count && W.aclass[c] == 0) {
+      cell = (int)c;
+      M = W.mem_size[c];
     }
   } else {
     // list rows: lpw entries per wave (lanes >= lpw idle)
@@ -215,12 +213,8 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
     if (VSTK) {
       sv[k] = (active && !fresh) ? W.stack[(int64_t)k * N + cell] : 0;
     } else if (active && !fresh) {
-#ifdef AVGPU_NO_LDS_DMA
-      stk[k * 64 + lane] = W.stack[(int64_t)k * N + cell];
-#else
       __builtin_amdgcn_global_load_lds((void*)(W.stack + (int64_t)k * N + cell),
                                        (lds_ptr_t)(stk + k * 64), 4, 0, 0);
-#endif
     } else {
       stk[k * 64 + lane] = 0;
     }
@@ -531,9 +525,6 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
           for (int p = 0; p < 8; p++) id += lo[p] * (1 << p);
           tmask = (!bad && id >= 0 && id < 256) ? lut[id] : 0u;
         }
-#ifdef AVGPU_ABL_IO
-        tmask = 0u;   // DIAGNOSTIC ablation build only (tools/ablate.sh)
-#endif
         // cEnvironment::TestOutput / TestRequisites / DoProcesses
         // (main/cEnvironment.cc:1314-1406, :1408-1503, :1610-1760)
         if (tmask && k_env_simple) {
@@ -654,9 +645,6 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
         const uint64_t nl = (cl + K7D) & K80, nh = (ch + K7D) & K80;
         int len = nl ? (int)(__ffsll((long long)nl) - 8) >> 3 : 8 + (nh ? (int)(__ffsll((long long)nh) - 8) >> 3 : 8);
         len = min(len, min(AVGPU_MAX_LABEL, M - base));
-#ifdef AVGPU_ABL_LABEL
-        len = 0;                     // DIAGNOSTIC ablation build only
-#endif
         len = max(len, 0);
         // 2-bit nop codes of bytes 0..7 packed (SWAR), bytes 8, 9 after them
         uint64_t v = cl & 0x0303030303030303ull;
@@ -676,9 +664,7 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
           if (packed != rl) ip = head_adjust(ip + 1, M);
           break;
         }
-#ifndef AVGPU_ABL_SEARCHRQ
         if (len > 0) { rq = RQ_SEARCH; qa = len; qb = (int)rot; break; }   // label scan below
-#endif
         r1 = 0;                                               // empty label: found = IP
         r2 = 0;
         fh = head_adjust(ip + 1, M);
@@ -1123,6 +1109,12 @@ void launch_interpret_classes(const DevWorld& W, const DevWorld* dW, int mode, h
   // empty.
   const unsigned lb = std::min(blocks, 768u);
   const unsigned lb_small = std::min(blocks, 256u);
+  // classes 2 / 3 beside class 0: a handful of blocks.  Each of their blocks
+  // needs most of a CU's LDS (99 / 132 KiB), so a 256-block grid queued behind
+  // the running class-0 blocks for most of class 0's duration (rocprof: 0.52
+  // ms average k_interpret<2048> with lists of tens of organisms) and took
+  // CUs away from it as their blocks dispatched one by one.
+  const unsigned lb_c2 = std::min(blocks, 8u), lb_c3 = std::min(blocks, 4u);
   if (blocks == 0) {
     if (after_class)
       for (int k = 0; k < 4; k++) hipEventRecord(after_class[k], s);
@@ -1133,8 +1125,8 @@ void launch_interpret_classes(const DevWorld& W, const DevWorld* dW, int mode, h
   // leaves idle.  Spills (rows 4..6) run after both, in class order.
   auto list = [&](int k, hipStream_t st) {
     if (k == 1) hipLaunchKernelGGL(k_interpret<CLASS1_SIZE>, dim3(lb), dim3(64), 0, st, dW, 1, 1, mode, first, count, 0, 64);
-    if (k == 2) hipLaunchKernelGGL(k_interpret<CLASS2_SIZE>, dim3(lb_small), dim3(64), 0, st, dW, 2, 2, mode, first, count, 0, 64);
-    if (k == 3) hipLaunchKernelGGL(k_interpret<CLASS3_SIZE>, dim3(lb_small), dim3(64), 0, st, dW, 3, 3, mode, first, count, 0, 64);
+    if (k == 2) hipLaunchKernelGGL(k_interpret<CLASS2_SIZE>, dim3(lb_c2), dim3(64), 0, st, dW, 2, 2, mode, first, count, 0, 64);
+    if (k == 3) hipLaunchKernelGGL(k_interpret<CLASS3_SIZE>, dim3(lb_c3), dim3(64), 0, st, dW, 3, 3, mode, first, count, 0, 64);
   };
   // Two aux streams (class 1; classes 2 + 3, which are short): with the
   // world's stream that is three HIP streams, so they keep distinct hardware

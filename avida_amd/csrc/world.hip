@@ -108,13 +108,10 @@ __global__ void k_set_orgs(DevWorld W, int64_t first, int64_t count, const uint8
   W.copied[c] = len; W.child_copied[c] = 0; W.executed[c] = len; W.errors[c] = 0;
 }
 
-__global__ void k_get_states(DevWorld W, int64_t first, int64_t count, avgpu_cpu_state* out,
-                             uint8_t* codes, int cap) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= count) return;
+// the cHardwareBase inspection tuple of cell c (zero padding: the digest below
+// hashes its bytes)
+__device__ void build_state(const DevWorld& W, int64_t c, avgpu_cpu_state& s) {
   const int64_t N = W.n;
-  const int64_t c = first + i;
-  avgpu_cpu_state s;
   memset(&s, 0, sizeof(s));
   const bool fresh = (W.ctl[c] & CTL_FRESH) != 0;   // birth values implied (setup_child)
   if (!fresh) {
@@ -163,6 +160,15 @@ __global__ void k_get_states(DevWorld W, int64_t first, int64_t count, avgpu_cpu
   s.merit = W.merit[c];
   s.fitness = W.fitness[c];
   s.credit = W.credit[c];
+}
+
+__global__ void k_get_states(DevWorld W, int64_t first, int64_t count, avgpu_cpu_state* out,
+                             uint8_t* codes, int cap) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= count) return;
+  const int64_t c = first + i;
+  avgpu_cpu_state s;
+  build_state(W, c, s);
   out[i] = s;
   if (codes) {
     const uint8_t* t = W.tape + c * TAPE_SLOT;
@@ -170,6 +176,32 @@ __global__ void k_get_states(DevWorld W, int64_t first, int64_t count, avgpu_cpu
     const int m = s.mem_size < cap ? s.mem_size : cap;
     for (int k = 0; k < m; k++) d[k] = t[k];
   }
+}
+
+// Per-cell state digest (include/avida_gpu.h avgpu_state_digests): a chained
+// 64-bit mix over the 32-bit words of the inspection tuple, then over the
+// memory tape in canonical bytes (handler id | copied << 6 | executed << 7, 4
+// sites per word, sites >= mem_size zero).  oracle/oracle.cc restates it on its
+// own state, so GPU and oracle worlds of any size compare digest for digest.
+__global__ void k_state_digest(DevWorld W, int64_t first, int64_t count, uint64_t* out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= count) return;
+  const int64_t c = first + i;
+  avgpu_cpu_state s;
+  build_state(W, c, s);
+  if (s.birth_length == 0) { out[i] = 0; return; }   // never occupied
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(&s);
+  uint64_t h = 0x9E3779B97F4A7C15ull;
+  for (int k = 0; k < (int)(sizeof(s) / 4); k++) h = gk_mix(h ^ ((uint64_t)k << 32 | w[k]));
+  const uint32_t* t = reinterpret_cast<const uint32_t*>(W.tape + c * TAPE_SLOT);
+  const int m = min(max(s.mem_size, 0), TAPE_SLOT);
+  for (int k = 0; k < (m + 3) / 4; k++) {
+    uint32_t v = t[k];
+    const int keep = m - 4 * k;
+    if (keep < 4) v &= (1u << (8 * keep)) - 1u;
+    h = gk_mix(h ^ ((uint64_t)(0x10000 + k) << 32 | v));
+  }
+  out[i] = h;
 }
 
 // checkpoint restore: the inverse of k_get_states; `codes` holds device codes
@@ -263,6 +295,7 @@ __global__ void k_classify_uniform(DevWorld W, int64_t first, int64_t count, con
     W.budget[cell] = b;
     want = (W.ctl[cell] & CTL_ALIVE) && b > 0;
     if (want) cls = class_of(need_of_cell(W, cell));
+    W.aclass[cell] = want ? (uint8_t)cls : (uint8_t)ACLASS_NONE;
   }
   enqueue_class(W, cell, want, cls);
 }
@@ -367,6 +400,7 @@ __global__ void k_allot(DevWorld W, const double* totals) {
       if (want) cls = class_of(need_of_cell(W, (int)c));
     }
     W.budget[c] = b;
+    W.aclass[c] = want ? (uint8_t)cls : (uint8_t)ACLASS_NONE;
   }
   const unsigned long long m = __ballot(want);
   if ((threadIdx.x & 63) == 0 && m) count_add(W, CNT_SLICES, (unsigned long long)__popcll(m));
@@ -386,12 +420,9 @@ __global__ __launch_bounds__(1024) void k_window_sort(DevWorld W) {
   for (int i = threadIdx.x; i < SORT_WIN; i += 1024) {
     const int64_t c = base + i;
     uint32_t b = 0;
-    if (c < W.n) {
-      const uint32_t ctl = W.ctl[c];
-      const int bud = W.budget[c];
-      if ((ctl & CTL_ALIVE) && bud > 0 && class_of(need_of(W.mem_size[c], ctl, W.size_range)) == 0)
-        b = (uint32_t)min(bud, 0xFFFFF);
-    }
+    // class-0 cells by k_allot's tag: the list classes on the aux streams
+    // rewrite budget / mem_size of their own cells while this kernel runs
+    if (c < W.n && W.aclass[c] == 0) b = (uint32_t)min(W.budget[c], 0xFFFFF);
     key[i] = (b << 11) | (uint32_t)(SORT_WIN - 1 - i);
   }
   __syncthreads();
@@ -888,6 +919,11 @@ void launch_get_states(const DevWorld& W, hipStream_t s, int64_t first, int64_t 
                        avgpu_cpu_state* states, uint8_t* codes, int cap) {
   hipLaunchKernelGGL(k_get_states, dim3(nblk(count, 64)), dim3(64), 0, s, W, first, count, states,
                      codes, cap);
+}
+
+void launch_state_digest(const DevWorld& W, hipStream_t s, int64_t first, int64_t count, uint64_t* d_out) {
+  if (count <= 0) return;
+  k_state_digest<<<(unsigned)((count + 127) / 128), 128, 0, s>>>(W, first, count, d_out);
 }
 
 void launch_get_census(const DevWorld& W, hipStream_t s, int64_t first, int64_t count, avgpu_census* d_out) {

@@ -192,9 +192,46 @@ def cpu_baseline_multi(golden, seconds, env_kind, procs):
     single = outs[0]
     return {"value": sum(o["value"] for o in outs), "unit": "organism-instructions/s", "cores": procs,
             "kind": "port", "single_core_value": single["value"],
+            "host_cpus": os.cpu_count(),
+            "label": "restatement (reference unbuildable here: its libs/apto submodule is absent)",
             "sample": f"{procs} independent oracle serial worlds (one process per host core, like the "
-                      f"reference's heads_perf_1000u_rate rate_runner), each: {single['sample']}",
+                      f"reference's heads_perf_1000u_rate rate_runner; {procs} of the box's "
+                      f"{os.cpu_count()} host CPUs), each: {single['sample']}",
             "updates_per_sec": sum(o["updates_per_sec"] for o in outs)}
+
+
+def free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def relaunch_ranks(n, argv, script=None, env=None):
+    """`bench.py --gpus N` started without torch.distributed.run (no
+    WORLD_SIZE in the environment): this parent process -- which has not
+    touched the GPU -- starts the N ranks itself, one per GPU, exactly as the
+    driver's multi-GPU form does (python -m torch.distributed.run --nnodes=1
+    --nproc-per-node N --master-addr 127.0.0.1 ...), and exits with their
+    status.  Rank 0 prints the JSON line.  (cMultiProcessWorld,
+    main/cMultiProcessWorld.cc:375-405, is the reference's multi-process
+    world; here one process per GPU, RCCL over xGMI.)"""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", f"--master-port={free_port()}",
+           script or os.path.abspath(__file__)] + list(argv)
+    return subprocess.run(cmd, env=env).returncode
+
+
+def rank_env(gpus):
+    """(rank, world, local rank) of this process; under torch.distributed.run
+    WORLD_SIZE must equal --gpus, so that n_gpus in the JSON line is what ran."""
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if "WORLD_SIZE" in os.environ and world != gpus:
+        raise SystemExit(f"bench.py: WORLD_SIZE={world} but --gpus {gpus}")
+    return rank, world, local
 
 
 def main():
@@ -215,26 +252,29 @@ def main():
     ap.add_argument("--cpu-procs", type=int, default=0,
                     help="CPU baseline processes (0: min(16, host CPUs) -- 16 is a GPU box's share)")
     ap.add_argument("--cpu-worker", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--long-updates", type=int, default=200,
+                    help="after the K timed steps, a second untimed-by-contract run of this many "
+                         "updates reported as config.long_run (stability cross-check; 0 = off)")
     args = ap.parse_args()
     golden = os.path.join(ROOT, "tests", "golden")
     if args.cpu_worker:                       # one CPU baseline process (no GPU)
         print(json.dumps(cpu_baseline(golden, args.cpu_seconds, args.env)), flush=True)
         return
-    rank0 = int(os.environ.get("RANK", "0")) == 0 and int(os.environ.get("WORLD_SIZE", "1")) == 1
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(relaunch_ranks(args.gpus, sys.argv[1:]))
+    rank, world, local = rank_env(args.gpus)
     cpu = None
-    if rank0 and not args.no_cpu:             # before this process initialises the GPU
+    if rank == 0 and world == 1 and not args.no_cpu:   # before this process initialises the GPU
         procs = args.cpu_procs or min(16, os.cpu_count() or 1)
         cpu = cpu_baseline_multi(golden, args.cpu_seconds, args.env, procs)
 
     import torch
-    rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
     dist = None
     if world > 1:
         import torch.distributed as dist
         dist.init_process_group("nccl")
+        assert dist.get_world_size() == world == args.gpus
 
     from avida_amd import capi, files, tiles
     lib = capi.load_product()
@@ -298,6 +338,37 @@ def main():
     tot_insts, tot_births, tot_orgs = vec[1].item(), vec[2].item(), vec[3].item()
     d = [cnt1[k] - cnt0[k] for k in range(capi.NUM_COUNTERS)]
     nph = max(1, phases.value)
+    # births the update could not place (queue overflow, no target) and
+    # slices handed to a larger LDS class, summed over ranks
+    extra = torch.tensor([float(d[capi.CNT_DROPPED]), float(d[capi.CNT_SPILLS])],
+                         dtype=torch.float64, device="cuda")
+    if dist:
+        dist.all_reduce(extra)
+    long_run = None
+    if args.long_updates > 0:
+        # stability cross-check outside the contract's timed region: the same
+        # updates, many more of them, under the same barrier / max-over-ranks clock
+        ls0 = capi.AvgpuUpdateStats()
+        capi.check(lib, lib.avgpu_get_stats(h, C.byref(ls0)))
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize()
+        l0 = time.perf_counter()
+        for _ in range(args.long_updates):
+            update()
+        torch.cuda.synchronize()
+        if dist:
+            dist.barrier()
+        ldt = torch.tensor([time.perf_counter() - l0], dtype=torch.float64, device="cuda")
+        ls1 = capi.AvgpuUpdateStats()
+        capi.check(lib, lib.avgpu_get_stats(h, C.byref(ls1)))
+        lins = torch.tensor([float(ls1.cum_insts_executed - ls0.cum_insts_executed)],
+                            dtype=torch.float64, device="cuda")
+        if dist:
+            dist.all_reduce(ldt, op=dist.ReduceOp.MAX)
+            dist.all_reduce(lins)
+        long_run = {"updates": args.long_updates, "value": lins.item() / ldt.item(),
+                    "ms_per_step": ldt.item() * 1e3 / args.long_updates}
     if rank != 0:
         if dist:
             dist.destroy_process_group()
@@ -347,11 +418,18 @@ def main():
             "organisms": int(tot_orgs),
             "updates_per_sec": args.steps / dt_max,
             "births_per_update": tot_births / args.steps,
+            "births_dropped_per_update": extra[0].item() / args.steps,
+            "spills_per_update": extra[1].item() / args.steps,
             "insts_per_update": tot_insts / args.steps,
             "parallelism": f"strips{world}",
+            "ranks": world,
+            "long_run": long_run,
         },
         "roofline": {
             "bound": "hbm",
+            # the HBM roofline is the contract's form; the resource that binds
+            # k_interpret is instruction issue + exposed latency ("issue" below)
+            "binding": "instruction issue + latency (see issue)",
             "achieved": achieved,
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",

@@ -379,6 +379,13 @@ int avgpu_get_states(avgpu_world* w, int64_t first_cell, int64_t count,
  * cell): the data PrintDominantData / PrintCountData's genotype columns and
  * the dominant genotype's averages are computed from on the host. */
 int avgpu_get_census(avgpu_world* w, int64_t first_cell, int64_t count, avgpu_census* out);
+/* Verification (no reference equivalent): one 64-bit digest per cell of
+ * cells first .. first+count-1 into host memory -- a chained mix over the 32-bit
+ * words of the cell's state record, as avgpu_get_states returns it, and its
+ * memory tape in canonical bytes (handler id | copied << 6 | executed << 7).
+ * oracle/oracle.cc computes the same digest, so worlds of any size (configs[2]
+ * and [3]) compare cell for cell without copying 2 KiB tapes to the host. */
+int avgpu_state_digests(avgpu_world* w, int64_t first_cell, int64_t count, uint64_t* out);
 /* checkpoint / resume: genotype keys of cells first .. first+count-1 (as
  * avgpu_get_census reported them).  avgpu_set_states keys an organism from
  * its tape prefix, which differs from the birth genome once an organism has

@@ -1112,6 +1112,38 @@ static uint64_t genome_key(const World& w, const std::vector<uint8_t>& g) {
   return k ? k : 1ull;
 }
 
+// Per-cell state digest, restating the device's k_state_digest (avida_amd/
+// csrc/world.hip): chained mix over the words of the dump_state tuple, then the
+// tape in canonical bytes (handler | copied << 6 | executed << 7).  0 for a
+// cell that never held an organism.
+int orc_state_digests(void* h, int64_t first, int64_t count, uint64_t* out) {
+  World& w = *(World*)h;
+  if (first < 0 || count < 0 || first + count > w.ncells) return fail(AVGPU_EINVAL, "cell range");
+  for (int64_t i = 0; i < count; i++) {
+    const Org& o = w.orgs[first + i];
+    if (o.genome.empty()) { out[i] = 0; continue; }
+    avgpu_cpu_state s;
+    dump_state(w, o, &s, nullptr, nullptr, 0);
+    uint32_t wd[sizeof(s) / 4];
+    memcpy(wd, &s, sizeof(wd));
+    uint64_t hsh = 0x9E3779B97F4A7C15ull;
+    for (int k = 0; k < (int)(sizeof(s) / 4); k++) hsh = gk_mix(hsh ^ ((uint64_t)k << 32 | wd[k]));
+    const int m = (int)o.mem.size();
+    for (int k = 0; k < (m + 3) / 4; k++) {
+      uint32_t v = 0;
+      for (int j = 0; j < 4 && 4 * k + j < m; j++) {
+        const int q = 4 * k + j;
+        const uint32_t b = (uint32_t)(w.is.handler[o.mem[q]] & 0x3F) | ((o.flg[q] & F_COPIED) ? 0x40u : 0u) |
+                           ((o.flg[q] & F_EXECUTED) ? 0x80u : 0u);
+        v |= b << (8 * j);
+      }
+      hsh = gk_mix(hsh ^ ((uint64_t)(0x10000 + k) << 32 | v));
+    }
+    out[i] = hsh;
+  }
+  return 0;
+}
+
 int orc_get_census(void* h, int64_t first, int64_t count, avgpu_census* out) {
   World& w = *(World*)h;
   if (first < 0 || count < 0 || first + count > w.ncells) return fail(AVGPU_EINVAL, "cell range");

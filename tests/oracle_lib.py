@@ -84,6 +84,20 @@ class Backend:
             inp = (C.c_int32 * len(flat))(*flat)
         self._call("set_orgs", self.h, first, n, buf, lens, m, inp, 1 if deterministic else 0)
 
+    def set_orgs_np(self, first, blob, lens, merits=None, deterministic=False):
+        """set_orgs for large worlds: genomes packed in `blob` (bytes), lens /
+        merits numpy arrays"""
+        import numpy as np
+        lens = np.ascontiguousarray(lens, dtype=np.int32)
+        n = len(lens)
+        buf = (C.c_uint8 * max(1, len(blob))).from_buffer_copy(blob or b"\0")
+        m = None
+        if merits is not None:
+            merits = np.ascontiguousarray(merits, dtype=np.float64)
+            m = merits.ctypes.data_as(C.POINTER(C.c_double))
+        self._call("set_orgs", self.h, first, n, buf, lens.ctypes.data_as(C.POINTER(C.c_int32)), m, None,
+                   1 if deterministic else 0)
+
     def step(self, first, count, budget=None, uniform=0, mode=capi.MODE_FROZEN):
         b = None
         if budget is not None:
@@ -98,6 +112,16 @@ class Backend:
         fl = (C.c_uint8 * (count * cap))()
         self._call("get_states", self.h, first, count, st, ops, fl, cap)
         return st, bytes(ops), bytes(fl)
+
+    def digests(self, first=0, count=None):
+        """per-cell state digests (numpy uint64) of a cell range:
+        avgpu_state_digests / orc_state_digests"""
+        import numpy as np
+        if count is None:
+            count = self.ncells - first
+        out = np.zeros(count, dtype=np.uint64)
+        self._call("state_digests", self.h, first, count, out.ctypes.data_as(C.c_void_p))
+        return out
 
     def census(self, first=0, count=None):
         """avgpu_census rows (numpy, capi.CENSUS_DTYPE) of a cell range"""

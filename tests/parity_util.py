@@ -79,3 +79,75 @@ def mutants_of(seq, iset, n, rate=0.03, seed=2):
                 g[i] = rnd.randrange(len(iset.names))
         out.append(bytes(g))
     return out
+
+
+def diff_states_np(a, b, ops_a, ops_b, fl_a, fl_b, cap, first=0, limit=20):
+    """diff_states for large worlds: raw struct bytes and memory images are
+    compared with numpy, the field-by-field report only for mismatching cells
+    (at most `limit`).  Returns (number of mismatching cells, report)."""
+    import ctypes as C
+    import numpy as np
+    n = len(a)
+    sz = C.sizeof(capi.AvgpuCpuState)
+    ra = np.frombuffer(a, dtype=np.uint8).reshape(n, sz)
+    rb = np.frombuffer(b, dtype=np.uint8).reshape(n, sz)
+    bad = np.any(ra != rb, axis=1)
+    msz = np.frombuffer(a, dtype=np.uint8).reshape(n, sz)[:, capi.AvgpuCpuState.mem_size.offset:
+                                                            capi.AvgpuCpuState.mem_size.offset + 4]
+    m = np.ascontiguousarray(msz).view(np.int32).reshape(n)
+    keep = np.arange(cap)[None, :] < np.minimum(m, cap)[:, None]
+    oa = np.frombuffer(ops_a, dtype=np.uint8).reshape(n, cap)
+    ob = np.frombuffer(ops_b, dtype=np.uint8).reshape(n, cap)
+    fa = np.frombuffer(fl_a, dtype=np.uint8).reshape(n, cap)
+    fb = np.frombuffer(fl_b, dtype=np.uint8).reshape(n, cap)
+    bad |= np.any((oa != ob) & keep, axis=1) | np.any((fa != fb) & keep, axis=1)
+    idx = np.nonzero(bad)[0]
+    report = []
+    for i in idx[:limit]:
+        i = int(i)
+        ta, tb = state_tuple(a[i]), state_tuple(b[i])
+        diffs = [k for k in STATE_FIELDS if ta[k] != tb[k]]
+        report.append((first + i, diffs or ["memory"]))
+    return len(idx), report
+
+
+M64 = (1 << 64) - 1
+
+
+def _mix(z):
+    z ^= z >> 30
+    z = (z * 0xBF58476D1CE4E5B9) & M64
+    z ^= z >> 27
+    z = (z * 0x94D049BB133111EB) & M64
+    return z ^ (z >> 31)
+
+
+def digest_of(state, ops, flags, handlers):
+    """Python restatement of the per-cell state digest (avida_amd/csrc/world.hip
+    k_state_digest, oracle orc_state_digests) from one avgpu_get_states record
+    and its memory (op codes, flags bit0 copied / bit2 executed)."""
+    import ctypes as C
+    import struct
+    if state.birth_length == 0:
+        return 0
+    raw = bytes(C.string_at(C.addressof(state), C.sizeof(state)))
+    h = 0x9E3779B97F4A7C15
+    for k, (w,) in enumerate(struct.iter_unpack("<I", raw)):
+        h = _mix(h ^ ((k << 32) | w))
+    m = state.mem_size
+    for k in range((m + 3) // 4):
+        v = 0
+        for j in range(4):
+            q = 4 * k + j
+            if q < m:
+                b = (handlers[ops[q]] & 0x3F) | (0x40 if flags[q] & 1 else 0) | (0x80 if flags[q] & 4 else 0)
+                v |= b << (8 * j)
+        h = _mix(h ^ (((0x10000 + k) << 32) | v))
+    return h
+
+
+def compare_digests(da, db, first=0, limit=10):
+    """(number of differing cells, first `limit` differing global cell ids)"""
+    import numpy as np
+    idx = np.nonzero(da != db)[0]
+    return len(idx), [int(first + i) for i in idx[:limit]]

@@ -65,3 +65,21 @@ def test_create_without_gpu_fails_loudly():
     h = lib.avgpu_create(C.byref(c), 0, 16)
     assert not h
     assert lib.avgpu_last_error()
+
+
+def test_unsupported_mutation_knobs_are_refused(golden, tmp_path):
+    """A reference avida.cfg that sets a mutation knob this path does not
+    implement is refused, not run with different semantics (capi.UNSUPPORTED_NONZERO)."""
+    from avida_amd import files
+    for key in ["DIV_MUT_PROB", "PARENT_MUT_PROB", "DIVIDE_POISSON_MUT_MEAN", "COPY_SLIP_PROB",
+                "COPY_UNIFORM_PROB", "DIVIDE_TRANS_PROB"]:
+        with pytest.raises(ValueError, match=key):
+            capi.cfg_from_avida(files.read_avida_cfg(None, {key: 0.01}))
+    text = open(os.path.join(golden, "avida-default.cfg")).read().replace(
+        "DIV_INS_PROB 0.0", "DIV_INS_PROB 0.001")
+    p = tmp_path / "avida.cfg"
+    p.write_text(text)
+    with pytest.raises(ValueError, match="DIV_INS_PROB"):
+        capi.cfg_from_avida(files.read_avida_cfg(str(p)))
+    # the reference's default config itself is accepted
+    capi.cfg_from_avida(files.read_avida_cfg(os.path.join(golden, "avida-default.cfg")))

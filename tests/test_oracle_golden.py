@@ -87,3 +87,22 @@ def test_ancestor_trace_prefix(golden):
     b.step(0, 1, uniform=300, mode=capi.MODE_FROZEN)
     st, _, _ = b.states(0, 1)
     assert st[0].num_divides == 1 and st[0].gestation_time == 389
+
+
+def test_state_digest_restatement(golden):
+    """The oracle's per-cell state digest (the cross-check the full-size GPU
+    parity tests use) equals its Python restatement on a stepped world, and
+    is 0 only for never-occupied cells."""
+    import parity_util as pu
+    iset, env, cfg = pu.load_env(golden, overrides={"WORLD_X": 12, "WORLD_Y": 10}, seed=5)
+    b = ol.Backend("oracle", cfg, iset, env, ncells=120)
+    anc = files.read_org(os.path.join(golden, "default-heads.org"), iset)
+    b.set_orgs(0, pu.mutants_of(anc, iset, 100, rate=0.05, seed=3), deterministic=False)
+    for _ in range(12):
+        b.run_update()
+    d = b.digests()
+    st, ops, fl = b.states(0, 120, 2048)
+    for i in range(120):
+        exp = pu.digest_of(st[i], ops[i * 2048:(i + 1) * 2048], fl[i * 2048:(i + 1) * 2048], iset.handlers)
+        assert int(d[i]) == exp, i
+    assert (d[:100] != 0).all() and (d[100:] == 0).all() == (st[110].birth_length == 0)

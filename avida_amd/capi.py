@@ -21,8 +21,9 @@ MODE_WORLD, MODE_TEST, MODE_FROZEN = 0, 1, 2
 (CNT_INSTS, CNT_DEATHS, CNT_DIVIDES, CNT_BIRTHS, CNT_DROPPED, CNT_SPILLS, CNT_SLICES,
  CNT_LANESTEPS, CNT_C0_SLICES, CNT_C0_SITES, CNT_CLK_STAGE, CNT_CLK_LOOP, CNT_CLK_WB,
  CNT_ITERS, CNT_IT_FAST, CNT_IT_COPY, CNT_IT_SLOW, CNT_WAVES, CNT_HALO_SENT,
- CNT_HALO_LOST) = range(20)
-NUM_COUNTERS = 32
+ CNT_HALO_LOST, CNT_REC_EXHAUSTED, CNT_OVERSIZE) = range(22)
+RNG_COUNTER, RNG_RECORDED = 0, 1
+NUM_COUNTERS = 48
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libavida_gpu.so")
@@ -47,6 +48,8 @@ class AvgpuCfg(C.Structure):
         ("max_genome_size", C.c_int32), ("inherit_merit", C.c_int32),
         ("merit_default_bonus", C.c_double), ("required_bonus", C.c_double),
         ("seed", C.c_uint64),
+        ("divide_slip_prob", C.c_double), ("divide_uniform_prob", C.c_double),
+        ("slip_fill_mode", C.c_int32), ("pad_cfg", C.c_int32),
     ]
 
 
@@ -96,7 +99,7 @@ class AvgpuCpuState(C.Structure):
         ("last_task_count", C.c_int32 * MAX_REACTIONS),
         ("cur_reaction_count", C.c_int32 * MAX_REACTIONS),
         ("rng_counter", C.c_uint32), ("rng_key_lo", C.c_uint32), ("rng_key_hi", C.c_uint32),
-        ("errors", C.c_int32),
+        ("errors", C.c_int32), ("pad1", C.c_int32),
         ("cur_bonus", C.c_double), ("merit", C.c_double), ("fitness", C.c_double),
         ("credit", C.c_double),
     ]
@@ -154,7 +157,7 @@ EXPORTED = [
     "avgpu_tile_begin", "avgpu_tile_place", "avgpu_tile_finish", "avgpu_tile_res_bytes",
     "avgpu_set_tile_res_buffers", "avgpu_tile_res_cons", "avgpu_tile_res_settle",
     "avgpu_last_step_insts", "avgpu_last_kernel_ms", "avgpu_kernel_times", "avgpu_counters",
-    "avgpu_state_digests",
+    "avgpu_state_digests", "avgpu_set_rng_mode",
 ]
 
 
@@ -169,7 +172,7 @@ UNSUPPORTED_NONZERO = [
     "POINT_MUT_PROB", "POINT_INS_PROB", "POINT_DEL_PROB", "INST_POINT_MUT_PROB",
     "DIV_MUT_PROB", "DIV_INS_PROB", "DIV_DEL_PROB", "DIV_UNIFORM_PROB", "DIV_SLIP_PROB",
     "DIV_TRANS_PROB", "DIV_LGT_PROB",
-    "DIVIDE_SLIP_PROB", "DIVIDE_UNIFORM_PROB", "DIVIDE_TRANS_PROB", "DIVIDE_LGT_PROB",
+    "DIVIDE_TRANS_PROB", "DIVIDE_LGT_PROB",
     "DIVIDE_POISSON_MUT_MEAN", "DIVIDE_POISSON_INS_MEAN", "DIVIDE_POISSON_DEL_MEAN",
     "DIVIDE_POISSON_SLIP_MEAN", "DIVIDE_POISSON_TRANS_MEAN", "DIVIDE_POISSON_LGT_MEAN",
     "INJECT_MUT_PROB", "INJECT_INS_PROB", "INJECT_DEL_PROB",
@@ -239,6 +242,9 @@ def cfg_from_avida(cfg, seed=None) -> AvgpuCfg:
     c.required_bonus = g("REQUIRED_BONUS")
     s = g("RANDOM_SEED") if seed is None else seed
     c.seed = int(s) & 0xFFFFFFFFFFFFFFFF if int(s) >= 0 else 0x1234ABCD
+    c.divide_slip_prob = float(g("DIVIDE_SLIP_PROB", 0.0))
+    c.divide_uniform_prob = float(g("DIVIDE_UNIFORM_PROB", 0.0))
+    c.slip_fill_mode = int(float(g("SLIP_FILL_MODE", 0)))
     return c
 
 
@@ -313,6 +319,7 @@ def bind_common(lib, prefix):
         "get_census": (C.c_int, [V, I64, I64, V]),
         "set_genotype_keys": (C.c_int, [V, I64, I64, V]),
         "state_digests": (C.c_int, [V, I64, I64, V]),
+        "set_rng_mode": (C.c_int, [V, C.c_int, V, I64, V]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, p + name, None)

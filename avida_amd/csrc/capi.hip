@@ -72,6 +72,7 @@ struct avgpu_world {
   float last_kernel_ms = 0.f;
   int64_t last_launches = 0;
   bool has_test_buffers = false;
+  double* rec_buf = nullptr;    // RECORDED mode stream (avgpu_set_rng_mode)
   // strip tiles
   int ntiles_last = 0;
   bool tile_buffers = false;
@@ -147,15 +148,22 @@ int setup_world(avgpu_world* w, int64_t n, bool test_buffers) {
   W.min_genome = (!c.min_genome_size || c.min_genome_size < AVGPU_MIN_GENOME) ? AVGPU_MIN_GENOME : c.min_genome_size;
   W.death_method = c.death_method; W.age_limit = c.age_limit;
   W.prefer_empty = c.prefer_empty; W.allow_parent = c.allow_parent; W.birth_method = c.birth_method;
+  // P(p) = u < p: a 32-bit counter draw x hits iff x < ceil(p 2^32)
   auto th = [](double p) -> uint64_t {
     if (!(p > 0.0)) return 0;
     if (p >= 1.0) return 1ull << 32;
-    return (uint64_t)(p * 4294967296.0);
+    return (uint64_t)std::ceil(p * 4294967296.0);
   };
   W.th_copy_mut = th(c.copy_mut_prob);
   W.th_div_mut = th(c.divide_mut_prob);
   W.th_div_ins = th(c.divide_ins_prob);
   W.th_div_del = th(c.divide_del_prob);
+  W.th_div_slip = th(c.divide_slip_prob);
+  W.th_div_uni = th(c.divide_uniform_prob);
+  W.p_copy_mut = c.copy_mut_prob; W.p_div_mut = c.divide_mut_prob; W.p_div_ins = c.divide_ins_prob;
+  W.p_div_del = c.divide_del_prob; W.p_div_slip = c.divide_slip_prob; W.p_div_uni = c.divide_uniform_prob;
+  W.slip_fill_mode = c.slip_fill_mode;
+  W.rec = nullptr; W.rec_n = 0; W.rec_off = nullptr;
   W.seed_lo = (uint32_t)c.seed;
   W.seed_hi = (uint32_t)(c.seed >> 32);
   // interpreter slow-op batching (interp.hip); AVGPU_SLOW_BATCH overrides (tuning)
@@ -184,6 +192,10 @@ avgpu_world* create_world(const avgpu_cfg* cfg, int device, int64_t n, bool test
   if (!cfg) { fail(AVGPU_EINVAL, "cfg is NULL"); return nullptr; }
   if (cfg->copy_ins_prob > 0.0 || cfg->copy_del_prob > 0.0) {
     fail(AVGPU_EUNSUPPORTED, "COPY_INS_PROB / COPY_DEL_PROB are not on the GPU path yet");
+    return nullptr;
+  }
+  if (cfg->divide_slip_prob > 0.0 && cfg->slip_fill_mode != 0 && cfg->slip_fill_mode != 4) {
+    fail(AVGPU_EUNSUPPORTED, "SLIP_FILL_MODE 1-3 (nop-X, random, scrambled) are not on the GPU path");
     return nullptr;
   }
   if (cfg->divide_method != 1) {
@@ -382,6 +394,7 @@ int avgpu_destroy(avgpu_world* w) {
   if (w->stream) hipStreamSynchronize(w->stream);
   if (w->own_stream) hipStreamSynchronize(w->own_stream);
   for (void* p : w->allocs) hipFree(p);
+  if (w->rec_buf) hipFree(w->rec_buf);
   if (w->ev0) hipEventDestroy(w->ev0);
   if (w->ev1) hipEventDestroy(w->ev1);
   for (int i = 0; i < avgpu_world::RING; i++) {
@@ -604,7 +617,7 @@ int avgpu_update_run(avgpu_world* w, const double* dev_totals, avgpu_update_stat
   int rc = ready(w);
   if (rc < 0) return rc;
   if (!dev_totals) return fail(AVGPU_EINVAL, "dev_totals is NULL");
-  launch_world_pre(w->W, w->stream, dev_totals, w->ev_fork);
+  launch_world_pre(w->W, w->stream, dev_totals, w->ev_fork, (uint32_t)w->update);
   after_resources_begin(w);
   HIPCHK(hipGetLastError());
   rc = interpret(w, AVGPU_MODE_WORLD, 0, w->W.n, true);
@@ -687,6 +700,38 @@ int avgpu_state_digests(avgpu_world* w, int64_t first, int64_t count, uint64_t* 
   HIPCHK(hipMemcpyAsync(out, d, count * sizeof(uint64_t), hipMemcpyDeviceToHost, w->stream));
   HIPCHK(hipStreamSynchronize(w->stream));
   hipFree(d);
+  return 0;
+}
+
+int avgpu_set_rng_mode(avgpu_world* w, int mode, const double* stream, int64_t n, const int64_t* offsets) {
+  if (!w) return fail(AVGPU_EINVAL, "NULL world");
+  DevWorld& W = w->W;
+  HIPCHK(hipStreamSynchronize(w->stream));
+  if (mode == AVGPU_RNG_COUNTER) {
+    W.rec = nullptr;
+    W.rec_n = 0;
+    if (W.rec_off) HIPCHK(hipMemset(W.rec_off, 0xFF, W.n * sizeof(int64_t)));   // -1: counter streams
+    return 0;
+  }
+  if (mode != AVGPU_RNG_RECORDED || !stream || n <= 0) return fail(AVGPU_EINVAL, "rng mode / stream");
+  std::vector<int64_t> off(W.n, 0);
+  if (offsets)
+    for (int64_t c = 0; c < W.n; c++) {
+      if (offsets[c] < 0 || offsets[c] > n) return fail(AVGPU_EINVAL, "stream offset outside the stream");
+      off[c] = offsets[c];
+    }
+  if (w->rec_buf) { hipFree(w->rec_buf); w->rec_buf = nullptr; }
+  HIPCHK(hipMalloc(&w->rec_buf, n * sizeof(double)));
+  HIPCHK(hipMemcpy(w->rec_buf, stream, n * sizeof(double), hipMemcpyHostToDevice));
+  if (!W.rec_off) {
+    HIPCHK(hipMalloc(&W.rec_off, W.n * sizeof(int64_t)));
+    w->allocs.push_back(W.rec_off);
+  }
+  HIPCHK(hipMemcpy(W.rec_off, off.data(), W.n * sizeof(int64_t), hipMemcpyHostToDevice));
+  W.rec = w->rec_buf;
+  W.rec_n = n;
+  // every organism's position in its segment starts at 0
+  HIPCHK(hipMemset(W.rng + 2 * W.n, 0, W.n * sizeof(uint32_t)));
   return 0;
 }
 
@@ -1138,7 +1183,7 @@ int avgpu_tile_begin(avgpu_world* w, const double* dev_gathered, int ntiles) {
     return fail(AVGPU_ESTATE, "spatial resources need avgpu_set_tile_res_buffers");
   if (!dev_gathered || ntiles < 1) return fail(AVGPU_EINVAL, "gathered partials");
   launch_tile_totals(w->W, w->stream, dev_gathered, ntiles, w->d_totals);
-  launch_world_pre(w->W, w->stream, w->d_totals, w->ev_fork);
+  launch_world_pre(w->W, w->stream, w->d_totals, w->ev_fork, (uint32_t)w->update);
   after_resources_begin(w);
   HIPCHK(hipGetLastError());
   rc = interpret(w, AVGPU_MODE_WORLD, 0, w->W.n, true);

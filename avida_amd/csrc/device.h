@@ -191,7 +191,17 @@ struct DevWorld {
   int32_t cfg_min_genome, cfg_max_genome;  // raw MIN_GENOME_SIZE / MAX_GENOME_SIZE
   int32_t death_method, age_limit;
   int32_t prefer_empty, allow_parent, birth_method;
-  uint64_t th_copy_mut, th_div_mut, th_div_ins, th_div_del;
+  // P(p) = u < p: counter threshold ceil(p 2^32), and p itself
+  // for RECORDED draws
+  uint64_t th_copy_mut, th_div_mut, th_div_ins, th_div_del, th_div_slip, th_div_uni;
+  double p_copy_mut, p_div_mut, p_div_ins, p_div_del, p_div_slip, p_div_uni;
+  int32_t slip_fill_mode;
+  // RECORDED mode (avgpu_set_rng_mode): rec_n doubles; rec_off[c] = the start
+  // of cell c's organism's segment, -1 = a counter stream.  rec == nullptr:
+  // COUNTER mode everywhere (the REC-free interpreter instantiations run).
+  const double* rec;
+  int64_t rec_n;
+  int64_t* rec_off;
   uint32_t seed_lo, seed_hi;
   // Strip tiles (multi-GPU, DESIGN.md "Multi-GPU"): this world holds rows
   // [row0, row0+rows) of a world_x x global_rows torus / grid.  When tiled,
@@ -248,17 +258,19 @@ __host__ __device__ inline int64_t record_bytes(int x, int64_t arena) {
 #define CNT_WAVES 17
 #define CNT_HALO_SENT 18  /* offspring shipped to a neighbouring tile */
 #define CNT_HALO_LOST 19  /* offspring lost to a full halo arena (counted in DROPPED too) */
-// 20..25: AVGPU_PHASE_CLOCKS loop cycles by block (decode, fast, copy, switch,
-// wave phase, advance); 26..31: slow-switch cycles in pop, push, IO,
-// h-alloc, h-divide, h-search/if-label
-#define CNT_CB0 20
-#define CNT_CASE0 26
+#define CNT_REC_OVER 20   /* RECORDED draws past the end of the stream */
+#define CNT_OVERSIZE 21   /* offspring a slip grew past AVGPU_MAX_GENOME (counted in DROPPED too) */
+// 32..37: AVGPU_PHASE_CLOCKS loop cycles by block (decode, fast, copy, switch,
+// wave phase, advance); 38..43: slow-switch cycles in pop, push, IO, h-alloc,
+// h-divide, h-search/if-label
+#define CNT_CB0 32
+#define CNT_CASE0 38
 // Counters are sharded over NSHARD lines (CNT_STRIDE x u64 each) so that the
 // per-wave adds of a 16K-wave launch do not serialise on one L2 address; they
 // are cleared every update, and counters[CNT_CUM_BASE + k] accumulates slot k
 // over all updates (k_stats_final).
 #define NSHARD 64
-#define CNT_STRIDE 32
+#define CNT_STRIDE 64
 #define CNT_CUM_BASE (NSHARD * CNT_STRIDE)
 #define CNT_WORDS (NSHARD * CNT_STRIDE + CNT_STRIDE)
 #define CNT_CUM_INSTS (CNT_CUM_BASE + CNT_INSTS)
@@ -432,7 +444,12 @@ void launch_interpret_classes(const DevWorld& W, const DevWorld* dW, int mode, h
 // SORT_WIN cells, so that a wave's 64 organisms get similar time slices
 #define SORT_WIN 2048
 bool class_timing_all();   // AVGPU_CLASS_TIMING (interp.hip)
-void launch_world_pre(const DevWorld& W, hipStream_t s, const double* d_totals, hipEvent_t lists_ready);
+void launch_world_pre(const DevWorld& W, hipStream_t s, const double* d_totals, hipEvent_t lists_ready,
+                      uint32_t update);
+// allotment draw of organism (lo, hi) in update u (oracle allot_draw)
+__device__ __forceinline__ uint32_t allot_draw(uint32_t lo, uint32_t hi, uint32_t update) {
+  return lowbias32(lowbias32(update * 0x85EBCA6BU + hi) ^ lo ^ 0x27D4EB2FU);
+}
 void launch_resources_begin(const DevWorld& W, hipStream_t s);
 void launch_resources_end(const DevWorld& W, hipStream_t s);
 void launch_resources_pack(const DevWorld& W, hipStream_t s);

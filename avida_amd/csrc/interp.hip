@@ -101,7 +101,11 @@ __device__ __forceinline__ bool consume_resource(const DevWorld& W, const double
   return true;
 }
 
-template <int S>
+// divide-mutation edits (Divide_DoMutations, applied in order): kind | a << 3 | b << 15
+enum { E_SLIP = 1, E_POINT = 2, E_INS = 3, E_DEL = 4 };
+__device__ __forceinline__ int edit_word(int kind, int a, int b) { return kind | (a << 3) | (b << 15); }
+
+template <int S, bool REC>
 __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp, int cls, int mode,
                                                 int64_t first, int64_t count, int64_t chunk,
                                                 uint32_t* __restrict__ lds32, bool sorted, int row,
@@ -122,13 +126,16 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
   uint8_t* lds = reinterpret_cast<uint8_t*>(lds32);
   int32_t* stk = reinterpret_cast<int32_t*>(lds32 + TAPE_WORDS);
   uint32_t* tab = lds32 + TAPE_WORDS + STK_WORDS;
-  // class 0 reads the small tables from global memory (L1 / scalar cache):
-  // with tapes only, its block needs 22 KiB of LDS and 7 blocks fit a CU
+  // class 0 keeps only the two per-lane lookup tables in LDS after the tapes
+  // (task LUT 512 B + random-instruction LUT 256 B: 22.5 + 0.75 KiB per block,
+  // still 7 blocks per CU) -- a vector global load there made the IO path
+  // wait on vmcnt(0), i.e. for every store the wave still had in flight --
+  // and reads the rest from global memory through uniform (scalar) loads
   constexpr bool GTAB = (S == CLASS0_SIZE);
-  const uint16_t* lut = GTAB ? W.task_lut : reinterpret_cast<const uint16_t*>(tab);
+  const uint16_t* lut = reinterpret_cast<const uint16_t*>(tab);
   const int32_t* rcum = GTAB ? W.rand_cum : reinterpret_cast<const int32_t*>(tab + 128);
   const uint8_t* rcode = GTAB ? W.rand_code : reinterpret_cast<const uint8_t*>(tab + 192);
-  const uint8_t* rlut = GTAB ? W.rand_lut : reinterpret_cast<const uint8_t*>(tab + 208);
+  const uint8_t* rlut = reinterpret_cast<const uint8_t*>(tab + (GTAB ? 128 : 208));
   const int32_t* rtab = GTAB ? W.react_tab : reinterpret_cast<const int32_t*>(tab + 272);
   // per-task bonus factor / addend of the simple-environment path (16 + 16 doubles)
   const double* tmul = GTAB ? W.task_tab
@@ -181,7 +188,12 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
   const int m_in = M;
 
   // ---- block-shared tables ----
-  if (!GTAB) {
+  if (GTAB) {
+    const uint32_t* g_lut = reinterpret_cast<const uint32_t*>(W.task_lut);
+    tab[lane] = g_lut[lane];
+    tab[64 + lane] = g_lut[64 + lane];
+    tab[128 + lane] = reinterpret_cast<const uint32_t*>(W.rand_lut)[lane];
+  } else {
     uint32_t* l32 = tab;
     const uint32_t* g_lut = reinterpret_cast<const uint32_t*>(W.task_lut);
     l32[lane] = g_lut[lane];
@@ -240,7 +252,7 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
 #pragma unroll
   for (int q = 0; q < AVGPU_MAX_REACTIONS; q++) rc[q] = 0;
   bool didv = false, prim = false, prim0 = false;
-  int ndrop = 0;
+  int ndrop = 0, noversize = 0;
   if (active) {
     // written at birth (setup_child) or by the previous slice
     ctl = W.ctl[cell];
@@ -287,13 +299,37 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
   const int k_require_allocate = W.require_allocate, k_alloc_method = W.alloc_method;
   const uint64_t k_th_copy_mut = W.th_copy_mut;
   const int k_rand_total = W.rand_total, k_n_ops = W.n_ops, k_n_react = W.n_react;
+  // RECORDED streams (include/avida_gpu.h "random streams"): the organism's
+  // k-th draw is rbase[k]; REC = false compiles the counter path only
+  const double* rbase = nullptr;
+  int64_t rlim = 0;
+  bool rover = false;
+  if (REC && active) {
+    const int64_t off = W.rec_off[cell];
+    if (off >= 0) { rbase = W.rec + off; rlim = W.rec_n - off; }
+  }
+  // the reference's draws on a uniform u (Apto::RNG P / GetUInt)
+  auto rd = [&]() -> double {
+    const uint32_t k = kct++;
+    if ((int64_t)k < rlim) return rbase[k];
+    rover = true;
+    return 0.0;
+  };
+  auto draw_p = [&](uint64_t th, double p) -> bool {
+    if (REC && rbase) return rd() < p;
+    return rng_p(klo, khi, kct, th);
+  };
+  auto draw_below = [&](uint32_t n) -> uint32_t {
+    if (REC && rbase) { const uint32_t v = (uint32_t)(rd() * (double)n); return v < n ? v : n - 1u; }
+    return rng_below(klo, khi, kct, n);
+  };
   const int k_env_simple = W.env_simple, k_max_label_exe = W.max_label_exe;
   const int k_env_resources = W.env_resources;
   const uint32_t k_env_res_mask = W.env_res_mask;
   const uint32_t k_env_react_mask = W.env_react_mask, k_env_once_mask = W.env_once_mask;
   // cInstSet::GetRandomInst (cpu/cInstSet.cc:83-88) from the LDS tables
   auto rand_code = [&]() -> uint8_t {
-    const uint32_t r = rng_below(klo, khi, kct, (uint32_t)k_rand_total);
+    const uint32_t r = draw_below((uint32_t)k_rand_total);
     if (k_rand_total <= 256) return rlut[r];
     int i = 0;
     while (i < k_n_ops - 1 && rcum[i] <= (int32_t)r) i++;
@@ -418,7 +454,8 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
       } else {
         rl = 0;
       }
-      if (mode != AVGPU_MODE_TEST && k_th_copy_mut && rng_p(klo, khi, kct, k_th_copy_mut))
+      // TestCopyMut: no draw at rate 0 (main/cMutationRates.h:112)
+      if (mode != AVGPU_MODE_TEST && k_th_copy_mut && draw_p(k_th_copy_mut, W.p_copy_mut))
         v = rand_code();
       T[wh] = (uint8_t)((T[wh] & TF_EXEC) | TF_COPIED | v);
       rh = head_adjust(rh + 1, M);
@@ -535,6 +572,17 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
           if (done) {
             double mult = 1.0, addb = 0.0;
             uint32_t paid = done;
+            if (GTAB && !k_env_resources) {
+              // tasks in ascending order with wave-uniform indices: the factors
+              // are scalar loads (no vector-memory wait)
+#pragma unroll
+              for (int t = 0; t < AVGPU_NUM_LOGIC_TASKS; t++) {
+                if ((done >> t) & 1u) {
+                  mult = __dmul_rn(mult, W.task_tab[t]);
+                  addb = __dadd_rn(addb, W.task_tab[16 + t]);
+                }
+              }
+            } else {
             for (uint32_t d = done; d; d &= d - 1u) {
               const int t = __ffs(d) - 1;
               if ((k_env_res_mask >> t) & 1u) {                 // finite resource (general path below)
@@ -543,6 +591,7 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
                 mult = __dmul_rn(mult, tmul[t]);
                 addb = __dadd_rn(addb, tadd[t]);
               }
+            }
             }
 #pragma unroll
             for (int q = 0; q < AVGPU_NUM_LOGIC_TASKS; q++) {
@@ -740,7 +789,7 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
           nc += __popc(v & (TF_COPIED * 0x01010101u) & byte_mask(w << 2, div, div + child));
         }
         const int exe = wave_sum_i32(ne), cop = wave_sum_i32(nc);
-        int okw = 0, rec = -1, len = 0, ml = -1, il = -1, dl = -1, mc = 0, ic = 0;
+        int okw = 0, rec = -1, len = 0, e0 = 0, e1 = 0, e2 = 0, e3 = 0, e4 = 0;   // edits: slip mut ins del uniform
         if (lane == L) {
           bool ok = exe >= (int)(div * W.min_exe_lines) && cop >= (int)(child * W.min_copied_lines);
           double bon = bonus;
@@ -790,29 +839,56 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
               st_async_u32(W.t_flags_len + cell, (uint32_t)div);
               st_async_u32(W.t_child_len + cell, (uint32_t)child);
               stop = true;
-            } else if (mode == AVGPU_MODE_WORLD) {
-              // Divide_DoMutations (cpu/cHardwareBase.cc:296-569), default subset
-              if (W.th_div_mut && rng_p(klo, khi, kct, W.th_div_mut)) {
-                ml = (int)rng_below(klo, khi, kct, (uint32_t)len);
-                mc = rand_code();
+            } else {
+              // Divide_DoMutations (cpu/cHardwareBase.cc:296-569) in the
+              // reference's order of draws (oracle divide_mutations): slip,
+              // mut, ins, del always draw; uniform only at a non-zero rate.
+              // The offspring is this lane's child sites under up to 5 edits,
+              // one fixed slot per kind (e0 .. e4, 0 = none) in the order applied.
+              if (draw_p(W.th_div_slip, W.p_div_slip)) {          // doSlipMutation :621-694
+                const int from = (int)draw_below((uint32_t)len + 1u);
+                const int to = from == 0 ? (int)draw_below((uint32_t)len) : (int)draw_below((uint32_t)len + 1u);
+                e0 = edit_word(E_SLIP, from, to);
+                len += from - to;
               }
-              if (W.th_div_ins && rng_p(klo, khi, kct, W.th_div_ins) && len < W.max_genome) {
-                il = (int)rng_below(klo, khi, kct, (uint32_t)len + 1);
-                ic = rand_code();
+              if (draw_p(W.th_div_mut, W.p_div_mut)) {
+                const int line = (int)draw_below((uint32_t)len);
+                e1 = edit_word(E_POINT, line, rand_code());
+              }
+              if (draw_p(W.th_div_ins, W.p_div_ins) && len < W.max_genome) {
+                const int line = (int)draw_below((uint32_t)len + 1u);
+                e2 = edit_word(E_INS, line, rand_code());
                 len++;
               }
-              if (W.th_div_del && rng_p(klo, khi, kct, W.th_div_del) && len > W.min_genome) {
-                dl = (int)rng_below(klo, khi, kct, (uint32_t)len);
+              if (draw_p(W.th_div_del, W.p_div_del) && len > W.min_genome) {
+                e3 = edit_word(E_DEL, (int)draw_below((uint32_t)len), 0);
                 len--;
               }
-              // record: the cell's primary record for the slice's first
-              // offspring, an overflow record (atomic) for any further one
+              if (W.th_div_uni && draw_p(W.th_div_uni, W.p_div_uni)) {   // doUniformMutation :572-595
+                const int mut = (int)draw_below((uint32_t)(2 * k_n_ops + 1));
+                if (mut < k_n_ops) {
+                  e4 = edit_word(E_POINT, (int)draw_below((uint32_t)len), rcode[mut]);
+                } else if (mut == k_n_ops) {
+                  if (len != W.min_genome) { e4 = edit_word(E_DEL, (int)draw_below((uint32_t)len), 0); len--; }
+                } else if (len != W.max_genome) {
+                  e4 = edit_word(E_INS, (int)draw_below((uint32_t)len + 1u), rcode[mut - k_n_ops - 1]);
+                  len++;
+                }
+              }
+              // record (WORLD): the cell's primary record for the slice's
+              // first offspring, an overflow record (atomic) for any further
+              // one; an offspring a slip grew past the largest genome is dropped
+              if (mode == AVGPU_MODE_WORLD && len > AVGPU_MAX_GENOME) {
+                ndrop++;
+                noversize++;
+              } else if (mode == AVGPU_MODE_WORLD) {
               rec = cell;
               if (prim) {
                 rec = (int)min((int64_t)W.n + atomicAdd(W.b_count + 1, 1), W.rcap);
                 if (rec >= W.rcap) { rec = -1; ndrop++; }
               }
               prim = true;
+              }
               if (rec >= 0) {
                 uint32_t clo, chi;
                 derive_key(klo, khi, (uint32_t)nd, 0x1B873593U, clo, chi);
@@ -850,8 +926,7 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
         okw = __shfl(okw, L);
         if (okw) {
           rec = __shfl(rec, L); len = __shfl(len, L);
-          ml = __shfl(ml, L); il = __shfl(il, L); dl = __shfl(dl, L);
-          mc = __shfl(mc, L); ic = __shfl(ic, L);
+          e0 = __shfl(e0, L); e1 = __shfl(e1, L); e2 = __shfl(e2, L); e3 = __shfl(e3, L); e4 = __shfl(e4, L);
           const int cell_l = __shfl(cell, L);
           if (mode == AVGPU_MODE_TEST) {
             // test-CPU snapshots: executed flags of the parent part, the offspring
@@ -871,20 +946,34 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
               st_async_u32(ch + 4 * w, wd);
             }
           } else if (mode == AVGPU_MODE_WORLD && rec >= 0) {
-            // offspring genome with the divide mutations, 4 sites per lane
+            // offspring genome, 4 sites per lane: site j of the mutated child
+            // is traced back through the edits (last first) to a site of the
+            // unmutated child or to a value an edit wrote
             uint8_t* g = W.b_genome + (int64_t)rec * TAPE_SLOT;
+            const bool nopc = W.slip_fill_mode == 4;
             for (int w = lane; (w << 2) < len; w += 64) {
               uint32_t word = 0;
 #pragma unroll
               for (int q = 0; q < 4; q++) {
                 const int j = 4 * w + q;
-                const int k2 = (dl >= 0 && j >= dl) ? j + 1 : j;        // index before the deletion
-                int v;
-                if (il >= 0 && k2 == il) v = ic;
-                else {
-                  const int k1 = (il >= 0 && k2 > il) ? k2 - 1 : k2;   // before the insertion
-                  v = (k1 == ml) ? mc : (TL[div + k1] & CODE_MASK);
-                }
+                int src = j, val = -1;
+                // straight-line over e4 .. e0 (no indexed register array)
+                auto undo = [&](int ew) {
+                  if (ew == 0 || val >= 0) return;
+                  const int kind = ew & 7, a = (ew >> 3) & 0xFFF, b = (ew >> 15) & 0xFFF;
+                  if (kind == E_POINT) {
+                    if (src == a) val = b;
+                  } else if (kind == E_INS) {
+                    if (src == a) val = b; else if (src > a) src--;
+                  } else if (kind == E_DEL) {
+                    if (src >= a) src++;
+                  } else {                                    // slip from a to b
+                    if (nopc && a > b && src >= a && src < 2 * a - b) val = AVGPU_H_NOP_C;
+                    else if (src >= a) src = b + (src - a);
+                  }
+                };
+                undo(e4); undo(e3); undo(e2); undo(e1); undo(e0);
+                const int v = val >= 0 ? val : (TL[div + src] & CODE_MASK);
                 word |= (j < len ? (uint32_t)v : 0u) << (8 * q);
               }
               st_async_u32(g + 4 * w, word);
@@ -1001,8 +1090,11 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
   int mxe = executed;
   int sl = active ? 1 : 0;
   int sites = active ? m_in + M : 0;
+  int nover = noversize, nrover = rover ? 1 : 0;
   for (int off = 32; off > 0; off >>= 1) {
     ndrop += __shfl_down(ndrop, off);
+    nover += __shfl_down(nover, off);
+    if (REC) nrover += __shfl_down(nrover, off);
     e += __shfl_down(e, off);
     dead += __shfl_down(dead, off);
     dv += __shfl_down(dv, off);
@@ -1016,6 +1108,8 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
     if (dead) count_add(W, CNT_DEATHS, (unsigned long long)dead);
     if (dv) count_add(W, CNT_DIVIDES, (unsigned long long)dv);
     if (ndrop) count_add(W, CNT_DROPPED, (unsigned long long)ndrop);
+    if (nover) count_add(W, CNT_OVERSIZE, (unsigned long long)nover);
+    if (REC && nrover) count_add(W, CNT_REC_OVER, (unsigned long long)nrover);
     if (cls == 0) {
       count_add(W, CNT_C0_SLICES, (unsigned long long)sl);
       count_add(W, CNT_C0_SITES, (unsigned long long)sites);
@@ -1047,26 +1141,26 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
 
 // class 0 must keep 2 waves per SIMD (its LDS admits 5 blocks per CU): the
 // second bound caps it at 256 registers (VGPR + AGPR)
-template <int S>
+template <int S, bool REC>
 __global__ __launch_bounds__(64, (S == CLASS0_SIZE) ? 2 : 1) void k_interpret(const DevWorld* __restrict__ Wp, int cls, int row, int mode,
                                                   int64_t first, int64_t count, int sorted, int lpw) {
   constexpr int TAB_WORDS = 128 + 64 + 16 + 64 + AVGPU_MAX_REACTIONS * RT_STRIDE + 64;
   // class 0: stacks in VGPRs, tables in global memory -- only the tapes in LDS
   constexpr int STK = (S == CLASS0_SIZE) ? 0 : 2 * AVGPU_STACK_SIZE * 64;
-  constexpr int TAB = (S == CLASS0_SIZE) ? 0 : TAB_WORDS;
+  constexpr int TAB = (S == CLASS0_SIZE) ? 192 : TAB_WORDS;   // class 0: task LUT + random LUT
   __shared__ __attribute__((aligned(16))) uint32_t lds32[64 * (S + 16) / 4 + STK + TAB];
   if (cls == 0) {
     // sorted windows: the 32 chunks of a window run on one XCD (blocks are
     // dealt to the 8 XCDs round robin), so its state lines meet in one L2
     int64_t chunk = blockIdx.x;
     if (sorted && (gridDim.x & 7) == 0) chunk = (int64_t)(blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
-    interpret_chunk<S>(Wp, 0, mode, first, count, chunk, lds32, sorted, 0, 64);
+    interpret_chunk<S, REC>(Wp, 0, mode, first, count, chunk, lds32, sorted, 0, 64);
     return;
   }
   // list classes: grid-stride over the list (its length is known on device only)
   const int lcount = Wp->class_count[row];
   for (int64_t chunk = blockIdx.x; chunk * lpw < lcount; chunk += gridDim.x) {
-    interpret_chunk<S>(Wp, cls, mode, first, count, chunk, lds32, false, row, lpw);
+    interpret_chunk<S, REC>(Wp, cls, mode, first, count, chunk, lds32, false, row, lpw);
     __syncthreads();
   }
 }
@@ -1095,9 +1189,10 @@ bool class_timing_all() {
   return v == 1;
 }
 
-void launch_interpret_classes(const DevWorld& W, const DevWorld* dW, int mode, hipStream_t s,
-                              int64_t first, int64_t count, int* launches, hipEvent_t* after_class,
-                              bool sorted, hipStream_t* aux, hipEvent_t ev_fork, hipEvent_t* ev_join) {
+template <bool REC>
+static void launch_classes(const DevWorld& W, const DevWorld* dW, int mode, hipStream_t s,
+                           int64_t first, int64_t count, int* launches, hipEvent_t* after_class,
+                           bool sorted, hipStream_t* aux, hipEvent_t ev_fork, hipEvent_t* ev_join) {
   const int srt = (sorted && first == 0 && count == W.n) ? 1 : 0;
   const bool tall = class_timing_all();
   const unsigned blocks = (unsigned)((count + 63) / 64);
@@ -1124,9 +1219,9 @@ void launch_interpret_classes(const DevWorld& W, const DevWorld* dW, int mode, h
   // class 0; with an aux stream they run beside it and fill the CUs its tail
   // leaves idle.  Spills (rows 4..6) run after both, in class order.
   auto list = [&](int k, hipStream_t st) {
-    if (k == 1) hipLaunchKernelGGL(k_interpret<CLASS1_SIZE>, dim3(lb), dim3(64), 0, st, dW, 1, 1, mode, first, count, 0, 64);
-    if (k == 2) hipLaunchKernelGGL(k_interpret<CLASS2_SIZE>, dim3(lb_c2), dim3(64), 0, st, dW, 2, 2, mode, first, count, 0, 64);
-    if (k == 3) hipLaunchKernelGGL(k_interpret<CLASS3_SIZE>, dim3(lb_c3), dim3(64), 0, st, dW, 3, 3, mode, first, count, 0, 64);
+    if (k == 1) hipLaunchKernelGGL((k_interpret<CLASS1_SIZE, REC>), dim3(lb), dim3(64), 0, st, dW, 1, 1, mode, first, count, 0, 64);
+    if (k == 2) hipLaunchKernelGGL((k_interpret<CLASS2_SIZE, REC>), dim3(lb_c2), dim3(64), 0, st, dW, 2, 2, mode, first, count, 0, 64);
+    if (k == 3) hipLaunchKernelGGL((k_interpret<CLASS3_SIZE, REC>), dim3(lb_c3), dim3(64), 0, st, dW, 3, 3, mode, first, count, 0, 64);
   };
   // Two aux streams (class 1; classes 2 + 3, which are short): with the
   // world's stream that is three HIP streams, so they keep distinct hardware
@@ -1143,7 +1238,7 @@ void launch_interpret_classes(const DevWorld& W, const DevWorld* dW, int mode, h
     list(3, aux[1]);
     for (int k = 0; k < 2; k++) hipEventRecord(ev_join[k], aux[k]);
   }
-  hipLaunchKernelGGL(k_interpret<CLASS0_SIZE>, dim3(blocks), dim3(64), 0, s, dW, 0, 0, mode, first, count, srt, 64);
+  hipLaunchKernelGGL((k_interpret<CLASS0_SIZE, REC>), dim3(blocks), dim3(64), 0, s, dW, 0, 0, mode, first, count, srt, 64);
   if (after_class) hipEventRecord(after_class[0], s);
   if (aux) {
     for (int k = 0; k < 2; k++) hipStreamWaitEvent(s, ev_join[k], 0);
@@ -1153,11 +1248,21 @@ void launch_interpret_classes(const DevWorld& W, const DevWorld* dW, int mode, h
   // longest remaining slice; spread over waves (spill_lpw lanes each), a
   // wave's iterations no longer pay for its other lanes' divergent paths.
   const int slpw = spill_lpw();
-  hipLaunchKernelGGL(k_interpret<CLASS1_SIZE>, dim3(lb_small), dim3(64), 0, s, dW, 1, 4, mode, first, count, 0, slpw);
+  hipLaunchKernelGGL((k_interpret<CLASS1_SIZE, REC>), dim3(lb_small), dim3(64), 0, s, dW, 1, 4, mode, first, count, 0, slpw);
   if (after_class && tall) hipEventRecord(after_class[1], s);
-  hipLaunchKernelGGL(k_interpret<CLASS2_SIZE>, dim3(std::min(lb_small, 64u)), dim3(64), 0, s, dW, 2, 5, mode, first, count, 0, slpw);
+  hipLaunchKernelGGL((k_interpret<CLASS2_SIZE, REC>), dim3(std::min(lb_small, 64u)), dim3(64), 0, s, dW, 2, 5, mode, first, count, 0, slpw);
   if (after_class && tall) hipEventRecord(after_class[2], s);
-  hipLaunchKernelGGL(k_interpret<CLASS3_SIZE>, dim3(std::min(lb_small, 64u)), dim3(64), 0, s, dW, 3, 6, mode, first, count, 0, slpw);
+  hipLaunchKernelGGL((k_interpret<CLASS3_SIZE, REC>), dim3(std::min(lb_small, 64u)), dim3(64), 0, s, dW, 3, 6, mode, first, count, 0, slpw);
   if (after_class && tall) hipEventRecord(after_class[3], s);
   if (launches) *launches += 7;
+}
+
+// RECORDED streams launch the REC instantiations (device.h DevWorld::rec)
+void launch_interpret_classes(const DevWorld& W, const DevWorld* dW, int mode, hipStream_t s,
+                              int64_t first, int64_t count, int* launches, hipEvent_t* after_class,
+                              bool sorted, hipStream_t* aux, hipEvent_t ev_fork, hipEvent_t* ev_join) {
+  if (W.rec)
+    launch_classes<true>(W, dW, mode, s, first, count, launches, after_class, sorted, aux, ev_fork, ev_join);
+  else
+    launch_classes<false>(W, dW, mode, s, first, count, launches, after_class, sorted, aux, ev_fork, ev_join);
 }

@@ -92,6 +92,7 @@ __global__ void k_set_orgs(DevWorld W, int64_t first, int64_t count, const uint8
     in2 = (85 << 24) + (int)rng_below(lo, hi, ctr, 1u << 24);
   }
   W.rng[c] = lo; W.rng[N + c] = hi; W.rng[2 * N + c] = ctr;
+  if (W.rec_off) W.rec_off[c] = -1;   // a new organism draws from its counter stream
   W.inputs[c] = in0; W.inputs[N + c] = in1; W.inputs[2 * N + c] = in2;
   W.budget[c] = 0;
   for (int k = 0; k < 3; k++) W.inbuf[k * N + c] = 0;
@@ -190,7 +191,8 @@ __global__ void k_state_digest(DevWorld W, int64_t first, int64_t count, uint64_
   avgpu_cpu_state s;
   build_state(W, c, s);
   if (s.birth_length == 0) { out[i] = 0; return; }   // never occupied
-  const uint32_t* w = reinterpret_cast<const uint32_t*>(&s);
+  uint32_t w[sizeof(s) / 4];
+  memcpy(w, &s, sizeof(s));              // the record's bytes (no type-punned loads)
   uint64_t h = 0x9E3779B97F4A7C15ull;
   for (int k = 0; k < (int)(sizeof(s) / 4); k++) h = gk_mix(h ^ ((uint64_t)k << 32 | w[k]));
   const uint32_t* t = reinterpret_cast<const uint32_t*>(W.tape + c * TAPE_SLOT);
@@ -240,6 +242,7 @@ __global__ void k_set_states(DevWorld W, int64_t first, int64_t count, const avg
     W.cur_react[k * N + c] = s.cur_reaction_count[k];
   }
   W.rng[c] = s.rng_key_lo; W.rng[N + c] = s.rng_key_hi; W.rng[2 * N + c] = s.rng_counter;
+  if (W.rec_off) W.rec_off[c] = -1;   // restored organisms draw from counter streams
   W.errors[c] = s.errors;
   W.cur_bonus[c] = s.cur_bonus; W.merit[c] = s.merit; W.fitness[c] = s.fitness; W.credit[c] = s.credit;
   W.budget[c] = 0;
@@ -366,7 +369,7 @@ __global__ __launch_bounds__(256) void k_merit_final(const double* partial, cons
 }
 
 // cScheduler restated (DESIGN.md "Scheduler"): lambda = UD * merit / total
-__global__ void k_allot(DevWorld W, const double* totals) {
+__global__ void k_allot(DevWorld W, const double* totals, uint32_t update) {
   const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const bool in = c < W.n;
   bool want = false;
@@ -389,10 +392,11 @@ __global__ void k_allot(DevWorld W, const double* totals) {
         } else {
           const double fl = floor(lam);
           const double frac = __dsub_rn(lam, fl);
-          const uint64_t th = (uint64_t)__dmul_rn(frac, 4294967296.0);
-          uint32_t ctr = W.rng[2 * W.n + c];
-          const bool extra = rng_p(W.rng[c], W.rng[W.n + c], ctr, th);
-          W.rng[2 * W.n + c] = ctr;
+          // P(frac) on the stateless allotment draw (the organism's own
+          // stream carries only the reference's ctx.GetRandom() calls)
+          const double t = __dmul_rn(frac, 4294967296.0);
+          const uint64_t th = (uint64_t)ceil(t);
+          const bool extra = (uint64_t)allot_draw(W.rng[c], W.rng[W.n + c], update) < th;
           b = (int)fl + (extra ? 1 : 0);
         }
       }
@@ -659,6 +663,7 @@ __device__ __forceinline__ void setup_child(const DevWorld& W, int64_t c, const 
       W.inputs[N + c] = (51 << 24) + (int)rng_below(b.lo, b.hi, ctr, 1u << 24);
       W.inputs[2 * N + c] = (85 << 24) + (int)rng_below(b.lo, b.hi, ctr, 1u << 24);
       W.rng[c] = b.lo; W.rng[N + c] = b.hi; W.rng[2 * N + c] = ctr;
+      if (W.rec_off) W.rec_off[c] = -1;         // offspring: counter streams
       break; }
     default:                                   // last_task_count = the parent's (:447)
       if (lane >= 12 && lane < 12 + AVGPU_NUM_LOGIC_TASKS)
@@ -852,7 +857,8 @@ __global__ __launch_bounds__(256) void k_stats_partial(DevWorld W, double* part)
 __global__ __launch_bounds__(256) void k_stats_final(DevWorld W, const double* part, int64_t nb,
                                                      double* out) {
   __shared__ double sd[256];
-  __shared__ unsigned long long cs[8][CNT_STRIDE];
+  constexpr int NG = 256 / CNT_STRIDE;          // groups of shards the block sums in parallel
+  __shared__ unsigned long long cs[NG][CNT_STRIDE];
   const int tid = threadIdx.x;
   const int k = blockIdx.x;
   if (k >= NUSED && k < NPART) {
@@ -876,15 +882,15 @@ __global__ __launch_bounds__(256) void k_stats_final(DevWorld W, const double* p
     return;
   }
   {
-    const int slot = tid & (CNT_STRIDE - 1), g = tid / CNT_STRIDE;   // 8 groups of shards
+    const int slot = tid & (CNT_STRIDE - 1), g = tid / CNT_STRIDE;
     unsigned long long a = 0;
-    for (int sh = g; sh < NSHARD; sh += 8) a += W.counters[sh * CNT_STRIDE + slot];
+    for (int sh = g; sh < NSHARD; sh += NG) a += W.counters[sh * CNT_STRIDE + slot];
     cs[g][slot] = a;
   }
   __syncthreads();
   if (tid < CNT_STRIDE) {
     unsigned long long t = 0;
-    for (int g = 0; g < 8; g++) t += cs[g][tid];
+    for (int g = 0; g < NG; g++) t += cs[g][tid];
     cs[0][tid] = t;
     W.counters[CNT_CUM_BASE + tid] += t;
   }
@@ -962,10 +968,11 @@ __global__ __launch_bounds__(256) void k_reset_counts(DevWorld W) {
   if (threadIdx.x < 8) W.class_count[threadIdx.x] = 0;
 }
 
-void launch_world_pre(const DevWorld& W, hipStream_t s, const double* totals, hipEvent_t lists_ready) {
+void launch_world_pre(const DevWorld& W, hipStream_t s, const double* totals, hipEvent_t lists_ready,
+                      uint32_t update) {
   launch_resources_begin(W, s);   // ProcessPreUpdate + the update's first DoUpdates
   hipLaunchKernelGGL(k_reset_counts, dim3(1), dim3(256), 0, s, W);
-  hipLaunchKernelGGL(k_allot, dim3(nblk(W.n, 256)), dim3(256), 0, s, W, totals);
+  hipLaunchKernelGGL(k_allot, dim3(nblk(W.n, 256)), dim3(256), 0, s, W, totals, update);
   // the class lists are complete: the aux streams of the list classes start
   // here, beside the window sort (launch_interpret_classes)
   hipEventRecord(lists_ready, s);

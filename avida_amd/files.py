@@ -341,13 +341,14 @@ CFG_KEYS_INT = {
     "DIVIDE_METHOD": 1, "MAX_LABEL_EXE_SIZE": 1, "BIRTH_METHOD": 0, "PREFER_EMPTY": 1,
     "ALLOW_PARENT": 1, "TEST_CPU_TIME_MOD": 20, "MIN_GENOME_SIZE": 0,
     "MAX_GENOME_SIZE": 0, "INHERIT_MERIT": 1, "RANDOM_SEED": -1,
-    "INST_SET_LOAD_LEGACY": 0,
+    "INST_SET_LOAD_LEGACY": 0, "SLIP_FILL_MODE": 0,
 }
 CFG_KEYS_FLOAT = {
     "DEFAULT_BONUS": 1.0, "COPY_MUT_PROB": 0.0075, "COPY_INS_PROB": 0.0,
     "COPY_DEL_PROB": 0.0, "DIVIDE_MUT_PROB": 0.0, "DIVIDE_INS_PROB": 0.05,
     "DIVIDE_DEL_PROB": 0.05, "OFFSPRING_SIZE_RANGE": 2.0, "MIN_COPIED_LINES": 0.5,
     "MIN_EXE_LINES": 0.5, "MERIT_DEFAULT_BONUS": 0.0, "REQUIRED_BONUS": 0.0,
+    "DIVIDE_SLIP_PROB": 0.0, "DIVIDE_UNIFORM_PROB": 0.0,
 }
 
 

@@ -140,6 +140,10 @@ typedef struct avgpu_cfg {
   double merit_default_bonus;      /* MERIT_DEFAULT_BONUS */
   double required_bonus;           /* REQUIRED_BONUS */
   uint64_t seed;                   /* RANDOM_SEED (counter-RNG key) */
+  double divide_slip_prob;         /* DIVIDE_SLIP_PROB (TestDivideSlip always draws) */
+  double divide_uniform_prob;      /* DIVIDE_UNIFORM_PROB */
+  int32_t slip_fill_mode;          /* SLIP_FILL_MODE: 0 duplication, 4 nop-C (1-3 refused) */
+  int32_t pad_cfg;
 } avgpu_cfg;
 
 /* One REACTION line of environment.cfg (main/cEnvironment.cc:1185-1211,
@@ -218,6 +222,7 @@ typedef struct avgpu_cpu_state {
   uint32_t rng_counter;                /* draws consumed from this organism's stream */
   uint32_t rng_key_lo, rng_key_hi;
   int32_t errors;                      /* cPhenotype::cur_num_errors (faults) */
+  int32_t pad1;                        /* explicit: the record's bytes are digested (avgpu_state_digests) */
   double cur_bonus;
   double merit;
   double fitness;
@@ -371,6 +376,29 @@ typedef struct avgpu_census {
   int32_t num_divides;
 } avgpu_census;
 
+/* ---- random streams ------------------------------
+ * Apto::RNG::AvidaRNG (main/cWorld.h:72) is absent, so every draw of the path
+ * is a uniform u in [0,1) with the reference's interface on top (P(p) = u < p,
+ * GetUInt(n) = floor(u n)), consumed in the reference's call order per
+ * organism: copy mutation per h-copy (cpu/cHardwareCPU.cc:7144-7161), random
+ * fill of ALLOC_METHOD 2, the divide-mutation sequence of Divide_DoMutations
+ * (cpu/cHardwareBase.cc:296-569: TestDivideSlip, -Mut, -Ins, -Del always
+ * draw; -Uniform only when non-zero).
+ *   AVGPU_RNG_COUNTER (default): u from the organism's counter stream
+ *     (key, counter; offspring keys derived from the parent's);
+ *   AVGPU_RNG_RECORDED: organism c's k-th draw is stream[offsets[c] + k]
+ *     (offsets NULL: every cell starts at 0), the reference's recorded
+ *     ctx.GetRandom() doubles -- bit-exact traces with mutations on.  The call
+ *     sets every cell's stream position (rng_counter) to 0; organisms set or
+ *     born afterwards use counter streams; draws past the end of the array
+ *     return 0 and count in AVGPU_CNT_REC_EXHAUSTED.
+ * The allotment draw of SLICING_METHOD 1 is a stateless hash of the
+ * organism's key and the update (the reference's scheduler has its own
+ * generator, main/cPopulation.cc:7341-7346), in both modes. */
+enum avgpu_rng_mode { AVGPU_RNG_COUNTER = 0, AVGPU_RNG_RECORDED = 1 };
+int avgpu_set_rng_mode(avgpu_world* w, int mode, const double* stream, int64_t n,
+                       const int64_t* offsets);
+
 /* ---- inspection (cHardwareBase inspection API, cpu/cHardwareBase.h:145-200) */
 int avgpu_get_states(avgpu_world* w, int64_t first_cell, int64_t count,
                      avgpu_cpu_state* states, uint8_t* mem_ops, uint8_t* mem_flags,
@@ -510,7 +538,9 @@ enum avgpu_counter {
   /* 10..17: per-phase clocks of diagnostic (AVGPU_PHASE_CLOCKS) builds */
   AVGPU_CNT_HALO_SENT = 18, /* offspring shipped to a neighbouring tile */
   AVGPU_CNT_HALO_LOST = 19, /* offspring dropped because the halo arena was full */
-  AVGPU_NUM_COUNTERS = 32
+  AVGPU_CNT_REC_EXHAUSTED = 20, /* RECORDED draws past the end of the stream */
+  AVGPU_CNT_OVERSIZE = 21,  /* offspring longer than AVGPU_MAX_GENOME after a slip (dropped) */
+  AVGPU_NUM_COUNTERS = 48   /* 32..47: AVGPU_PHASE_CLOCKS diagnostic builds */
 };
 int avgpu_counters(avgpu_world* w, int cumulative, int64_t* out, int n);
 

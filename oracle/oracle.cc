@@ -35,28 +35,63 @@
 namespace {
 
 // ---------------------------------------------------------------------------
-// RNG spec: 32-bit counter-based draws keyed by a 64-bit stream id.
+// RNG spec.  Every draw is a uniform u in [0, 1) with the
+// reference's RNG interface on top of it (Apto::RNG: P(p) = u < p, GetUInt(n) =
+// GetInt(n) = floor(u n), GetDouble(x) = u x).  u comes from the organism's
+// COUNTER stream (32-bit draws x, u = x 2^-32, so P(p) = x < ceil(p 2^32) and
+// GetUInt(n) = (x n) >> 32 exactly) or, in RECORDED mode
+// (avgpu_set_rng_mode), from its segment of a host-supplied array of doubles.
 static inline uint32_t lowbias32(uint32_t x) {
   x ^= x >> 16; x *= 0x7feb352dU; x ^= x >> 15; x *= 0x846ca68bU; x ^= x >> 16;
   return x;
 }
+// a probability and its COUNTER-mode threshold ceil(p 2^32) (P(p) = u < p)
+struct Prob {
+  double p = 0.0;
+  uint64_t th = 0;
+};
+static inline Prob make_prob(double p) {
+  Prob r;
+  r.p = p;
+  if (!(p > 0.0)) r.th = 0;
+  else if (p >= 1.0) r.th = 1ULL << 32;
+  else r.th = (uint64_t)std::ceil(p * 4294967296.0);
+  return r;
+}
+static int64_t g_rec_over = 0;   // RECORDED draws past the end of a segment
 struct Stream {
   uint32_t lo = 0, hi = 0, ctr = 0;
+  const double* rec = nullptr;   // RECORDED: this organism's segment
+  int64_t rec_len = 0;
   uint32_t next() {
     uint32_t a = lowbias32(ctr * 0x9E3779B9U + hi);
     uint32_t b = lowbias32(a ^ lo);
     ++ctr;
     return b;
   }
-  // cRandom::GetUInt(n) restated on a 32-bit draw
-  uint32_t uint_below(uint32_t n) { return (uint32_t)(((uint64_t)next() * n) >> 32); }
-  // cRandom::P(p): threshold precomputed as floor(p * 2^32)
-  bool p(uint64_t thresh) { return (uint64_t)next() < thresh; }
+  double rd() {
+    const uint32_t k = ctr++;
+    if ((int64_t)k < rec_len) return rec[k];
+    g_rec_over++;
+    return 0.0;
+  }
+  // Apto::RNG::GetUInt(n) / GetInt(n): floor(u n)
+  uint32_t uint_below(uint32_t n) {
+    if (rec) { const uint32_t v = (uint32_t)(rd() * (double)n); return v < n ? v : n - 1; }
+    return (uint32_t)(((uint64_t)next() * n) >> 32);
+  }
+  // Apto::RNG::P(p): u < p
+  bool p(const Prob& q) {
+    if (rec) return rd() < q.p;
+    return (uint64_t)next() < q.th;
+  }
 };
-static inline uint64_t prob_thresh(double p) {
-  if (!(p > 0.0)) return 0;
-  if (p >= 1.0) return 1ULL << 32;
-  return (uint64_t)(p * 4294967296.0);
+// Allotment draw of organism (lo, hi) in update u: a stateless hash, so the
+// organism's own stream carries exactly the reference's ctx.GetRandom() calls
+// (the reference's scheduler draws from its own generator,
+// main/cPopulation.cc:7341-7346)
+static inline uint32_t allot_draw(uint32_t lo, uint32_t hi, uint32_t update) {
+  return lowbias32(lowbias32(update * 0x85EBCA6BU + hi) ^ lo ^ 0x27D4EB2FU);
 }
 static inline void derive_key(uint32_t a_lo, uint32_t a_hi, uint32_t x, uint32_t y,
                               uint32_t* lo, uint32_t* hi) {
@@ -192,8 +227,9 @@ struct World {
   std::vector<Reaction> react;
   int num_tasks_in_env = 0;
   std::vector<Org> orgs;
-  uint64_t th_copy_mut = 0, th_copy_ins = 0, th_copy_del = 0;
-  uint64_t th_div_mut = 0, th_div_ins = 0, th_div_del = 0;
+  Prob p_copy_mut, p_copy_ins, p_copy_del;
+  Prob p_div_mut, p_div_ins, p_div_del, p_div_slip, p_div_uni;
+  std::vector<double> rec;   // RECORDED mode: the host's stream (organisms point into it)
   // batch world
   std::vector<Birth> births;
   int64_t update = 0;
@@ -221,6 +257,7 @@ struct World {
   std::vector<uint64_t> prio;
   std::vector<int8_t> bstate;     // 0 pending, 1+k placed in round k, -1 failed
   int64_t t_insts = 0, t_deaths = 0, t_divides = 0, t_slices = 0, t_born = 0, t_dropped = 0;
+  int64_t t_oversize = 0;   // offspring longer than AVGPU_MAX_GENOME after a slip (dropped at the divide)
   // resources (avgpu_load_resources): literal restatement of cResourceCount /
   // cSpatialResCount, stepped once per update
   std::vector<avgpu_resource> res;
@@ -404,24 +441,55 @@ struct Exec {
     else o.generation++;
   }
 
-  // Divide_DoMutations (cpu/cHardwareBase.cc:296-569), the default-config subset:
-  // divide slip (always draws), divide mut, ins, del (always draw); per-site
-  // rates and parent mutations are zero in every config on this path.
+  // cHardwareBase::doSlipMutation (cpu/cHardwareBase.cc:621-694), SLIP_FILL_MODE
+  // 0 (duplication) and 4 (nop-C; the device refuses 1-3)
+  void slip_mutation(std::vector<uint8_t>& g, Stream& r) {
+    const std::vector<uint8_t> copy = g;
+    const int size = (int)copy.size();
+    const int from = (int)r.uint_below((uint32_t)size + 1);
+    const int to = (from == 0) ? (int)r.uint_below((uint32_t)size) : (int)r.uint_below((uint32_t)size + 1);
+    int ins = from - to;
+    g.resize(size + ins);
+    for (int i = 0; i < ins; i++) g[from + i] = w.cfg.slip_fill_mode == 4 ? (uint8_t)H_NOP_C : copy[to + i];
+    if (ins < 0) ins = 0;
+    for (int i = ins; i < size - to; i++) g[from + i] = copy[to + i];
+  }
+
+  // Divide_DoMutations (cpu/cHardwareBase.cc:296-569) in the reference's order
+  // of draws: TestDivideSlip always draws (main/cMutationRates.h:128), the
+  // translocation / LGT / Poisson / per-site / parent kinds are refused when
+  // non-zero (avida_amd/capi.py UNSUPPORTED_NONZERO) and draw nothing at zero,
+  // TestDivideMut / Ins / Del always draw (:121-123; the size limits are
+  // tested after the draw), TestDivideUniform draws only when non-zero (:124-127).
   void divide_mutations(std::vector<uint8_t>& child) {
     Stream& r = o.rng;
     int max_g = w.cfg.max_genome_size; if (!max_g || max_g > AVGPU_MAX_GENOME) max_g = AVGPU_MAX_GENOME;
     int min_g = w.cfg.min_genome_size; if (!min_g || min_g < AVGPU_MIN_GENOME) min_g = AVGPU_MIN_GENOME;
-    if (w.th_div_mut && r.p(w.th_div_mut)) {
+    if (r.p(w.p_div_slip)) slip_mutation(child, r);
+    if (r.p(w.p_div_mut)) {
       uint32_t line = r.uint_below((uint32_t)child.size());
       child[line] = (uint8_t)w.is.random_inst(r);
     }
-    if (w.th_div_ins && r.p(w.th_div_ins) && (int)child.size() < max_g) {
+    if (r.p(w.p_div_ins) && (int)child.size() < max_g) {
       uint32_t line = r.uint_below((uint32_t)child.size() + 1);
       child.insert(child.begin() + line, (uint8_t)w.is.random_inst(r));
     }
-    if (w.th_div_del && r.p(w.th_div_del) && (int)child.size() > min_g) {
+    if (r.p(w.p_div_del) && (int)child.size() > min_g) {
       uint32_t line = r.uint_below((uint32_t)child.size());
       child.erase(child.begin() + line);
+    }
+    if (w.p_div_uni.p != 0.0 && r.p(w.p_div_uni)) {
+      // doUniformMutation (cpu/cHardwareBase.cc:572-595): op codes, not weighted
+      const int n_ops = w.is.n;
+      const int mut = (int)r.uint_below((uint32_t)(2 * n_ops + 1));
+      if (mut < n_ops) {
+        child[r.uint_below((uint32_t)child.size())] = (uint8_t)mut;
+      } else if (mut == n_ops) {
+        if ((int)child.size() != min_g) child.erase(child.begin() + r.uint_below((uint32_t)child.size()));
+      } else if ((int)child.size() != max_g) {
+        const uint32_t site = r.uint_below((uint32_t)child.size() + 1);
+        child.insert(child.begin() + site, (uint8_t)(mut - n_ops - 1));
+      }
     }
   }
 
@@ -481,13 +549,18 @@ struct Exec {
     }
     o.mem.resize(div_point);
     o.flg.resize(div_point);
-    if (mode == AVGPU_MODE_WORLD) divide_mutations(child);
+    // the reference draws the divide mutations in every mode with a world
+    // (Divide_Main :1806); FROZEN discards the offspring afterwards, the test
+    // CPU runs without mutations and stops at its divide
+    if (mode != AVGPU_MODE_TEST) divide_mutations(child);
     o.mal_active = false;
     o.advance_ip = false;   // DIVIDE_METHOD_SPLIT
     // ActivateDivide: the on-divide DoOutput runs no reaction for logic-9
     // environments (every requisite has divide_only 0; TestRequisites :1408).
     divide_reset();
-    if (mode == AVGPU_MODE_WORLD) {
+    if (mode == AVGPU_MODE_WORLD && (int)child.size() > AVGPU_MAX_GENOME) {
+      w.t_oversize++;     // a slip outgrew the largest genome: the offspring is dropped
+    } else if (mode == AVGPU_MODE_WORLD) {
       Birth b;
       b.parent = cell;
       b.seq = (uint32_t)o.num_divides;
@@ -625,18 +698,19 @@ struct Exec {
     // the test CPU runs with cleared mutation rates (cpu/cTestCPU.cc:270,
     // main/cMutationRates.cc:78-120)
     const bool muts = mode != AVGPU_MODE_TEST;
-    if (muts && w.th_copy_mut && o.rng.p(w.th_copy_mut)) {
+    // TestCopy*: no draw when the rate is 0 (main/cMutationRates.h:111-120)
+    if (muts && w.p_copy_mut.th && o.rng.p(w.p_copy_mut)) {
       read_inst = w.is.random_inst(o.rng);
       o.flg[wh] |= F_MUTATED | F_COPYMUT;
     }
     o.mem[wh] = (uint8_t)read_inst;
     o.flg[wh] |= F_COPIED;
-    if (muts && w.th_copy_ins && o.rng.p(w.th_copy_ins) && size() < AVGPU_MAX_GENOME) {
+    if (muts && w.p_copy_ins.th && o.rng.p(w.p_copy_ins) && size() < AVGPU_MAX_GENOME) {
       int ins = w.is.random_inst(o.rng);
       o.mem.insert(o.mem.begin() + wh, (uint8_t)ins);
       o.flg.insert(o.flg.begin() + wh, 0);
     }
-    if (muts && w.th_copy_del && o.rng.p(w.th_copy_del) && size() > 1) {
+    if (muts && w.p_copy_del.th && o.rng.p(w.p_copy_del) && size() > 1) {
       o.mem.erase(o.mem.begin() + wh);
       o.flg.erase(o.flg.begin() + wh);
     }
@@ -902,12 +976,14 @@ void* orc_create(const avgpu_cfg* cfg, int64_t ncells) {
   w->orgs.resize(w->ncells);
   w->rows = cfg->world_y;
   w->global_rows = cfg->world_y;
-  w->th_copy_mut = prob_thresh(cfg->copy_mut_prob);
-  w->th_copy_ins = prob_thresh(cfg->copy_ins_prob);
-  w->th_copy_del = prob_thresh(cfg->copy_del_prob);
-  w->th_div_mut = prob_thresh(cfg->divide_mut_prob);
-  w->th_div_ins = prob_thresh(cfg->divide_ins_prob);
-  w->th_div_del = prob_thresh(cfg->divide_del_prob);
+  w->p_copy_mut = make_prob(cfg->copy_mut_prob);
+  w->p_copy_ins = make_prob(cfg->copy_ins_prob);
+  w->p_copy_del = make_prob(cfg->copy_del_prob);
+  w->p_div_mut = make_prob(cfg->divide_mut_prob);
+  w->p_div_ins = make_prob(cfg->divide_ins_prob);
+  w->p_div_del = make_prob(cfg->divide_del_prob);
+  w->p_div_slip = make_prob(cfg->divide_slip_prob);
+  w->p_div_uni = make_prob(cfg->divide_uniform_prob);
   memset(&w->stats, 0, sizeof(w->stats));
   derive_key((uint32_t)cfg->seed, (uint32_t)(cfg->seed >> 32), 0x5CEDu, 0xC0FFEEu,
              &w->global_rng.lo, &w->global_rng.hi);
@@ -915,6 +991,29 @@ void* orc_create(const avgpu_cfg* cfg, int64_t ncells) {
 }
 
 void orc_destroy(void* h) { delete (World*)h; }
+
+// avgpu_set_rng_mode restated (include/avida_gpu.h "random streams")
+int orc_set_rng_mode(void* h, int mode, const double* stream, int64_t n, const int64_t* offsets) {
+  World& w = *(World*)h;
+  if (mode == AVGPU_RNG_COUNTER) {
+    for (Org& o : w.orgs) { o.rng.rec = nullptr; o.rng.rec_len = 0; }
+    w.rec.clear();
+    return 0;
+  }
+  if (mode != AVGPU_RNG_RECORDED || !stream || n <= 0) return fail(AVGPU_EINVAL, "rng mode / stream");
+  w.rec.assign(stream, stream + n);
+  for (int64_t c = 0; c < w.ncells; c++) {
+    const int64_t off = offsets ? offsets[c] : 0;
+    if (off < 0 || off > n) return fail(AVGPU_EINVAL, "stream offset outside the stream");
+    Org& o = w.orgs[c];
+    o.rng.rec = w.rec.data() + off;
+    o.rng.rec_len = n - off;
+    o.rng.ctr = 0;
+  }
+  return 0;
+}
+
+int64_t orc_rec_exhausted(void) { return g_rec_over; }
 
 int orc_load_instset(void* h, int n, const uint8_t* handler_id, const int32_t* redundancy) {
   World& w = *(World*)h;
@@ -1219,6 +1318,7 @@ int orc_set_states(void* h, int64_t first, int64_t count, const avgpu_cpu_state*
       o.cur_react[k] = s.cur_reaction_count[k];
     }
     o.rng.lo = s.rng_key_lo; o.rng.hi = s.rng_key_hi; o.rng.ctr = s.rng_counter;
+    o.rng.rec = nullptr; o.rng.rec_len = 0;   // restored organisms draw from counter streams
     o.errors = s.errors;
     o.cur_bonus = s.cur_bonus; o.merit = s.merit; o.fitness = s.fitness; o.credit = s.credit;
   }
@@ -1450,8 +1550,8 @@ static void allot_interpret(World& w, double sum_merit, int64_t n_alive) {
     } else {
       double fl = std::floor(lam);
       double frac = lam - fl;
-      uint64_t th = (uint64_t)(frac * 4294967296.0);
-      budget[c] = (int32_t)fl + (o.rng.p(th) ? 1 : 0);
+      const uint64_t th = make_prob(frac).th;
+      budget[c] = (int32_t)fl + ((uint64_t)allot_draw(o.rng.lo, o.rng.hi, (uint32_t)w.update) < th ? 1 : 0);
     }
   }
   w.t_slices = 0;
@@ -1477,7 +1577,8 @@ static void finish_stats(World& w, int64_t placed, int64_t dropped) {
   st.update = w.update;
   st.insts_executed = w.t_insts;
   st.births = placed;
-  st.births_dropped = dropped;
+  st.births_dropped = dropped + w.t_oversize;
+  w.t_oversize = 0;
   st.deaths = w.t_deaths;
   st.divides = w.t_divides;
   double gen = 0.0;

@@ -30,6 +30,7 @@ def load_oracle():
     lib.orc_create.argtypes = [C.POINTER(capi.AvgpuCfg), C.c_int64]
     lib.orc_destroy.restype = None
     lib.orc_run_serial_updates.argtypes = [C.c_void_p, C.c_int, C.POINTER(capi.AvgpuUpdateStats)]
+    lib.orc_rec_exhausted.restype = C.c_int64
     _lib = lib
     return lib
 
@@ -122,6 +123,25 @@ class Backend:
         out = np.zeros(count, dtype=np.uint64)
         self._call("state_digests", self.h, first, count, out.ctypes.data_as(C.c_void_p))
         return out
+
+    def set_rng_mode(self, mode, stream=None, offsets=None):
+        """avgpu_set_rng_mode / orc_set_rng_mode: stream = numpy float64
+        array (RECORDED), offsets = numpy int64 per cell or None"""
+        import numpy as np
+        sp, n, op = None, 0, None
+        if stream is not None:
+            self._rec = np.ascontiguousarray(stream, dtype=np.float64)
+            sp, n = self._rec.ctypes.data_as(C.c_void_p), len(self._rec)
+        if offsets is not None:
+            self._off = np.ascontiguousarray(offsets, dtype=np.int64)
+            op = self._off.ctypes.data_as(C.c_void_p)
+        self._call("set_rng_mode", self.h, mode, sp, n, op)
+
+    def counters(self):
+        """avgpu_counters of the last update (product only)"""
+        out = (C.c_int64 * capi.NUM_COUNTERS)()
+        self._call("counters", self.h, 0, out, capi.NUM_COUNTERS)
+        return list(out)
 
     def census(self, first=0, count=None):
         """avgpu_census rows (numpy, capi.CENSUS_DTYPE) of a cell range"""

@@ -106,3 +106,28 @@ def test_state_digest_restatement(golden):
         exp = pu.digest_of(st[i], ops[i * 2048:(i + 1) * 2048], fl[i * 2048:(i + 1) * 2048], iset.handlers)
         assert int(d[i]) == exp, i
     assert (d[:100] != 0).all() and (d[100:] == 0).all() == (st[110].birth_length == 0)
+
+
+def test_print_status_format(golden):
+    """avida_amd.trace.status_text renders cHardwareCPU::PrintStatus
+    (cpu/cHardwareCPU.cc:1111-1169) for the ancestor before its first and
+    after 20 instructions (oracle state, SURVEY.md Appendix B prefix)."""
+    from avida_amd import trace
+    iset = files.read_instset(os.path.join(golden, "instset-heads.cfg"))
+    env = files.read_environment(os.path.join(golden, "environment-logic9.cfg"))
+    cfg = capi.cfg_from_avida(files.read_avida_cfg(None))
+    anc = files.read_org(os.path.join(golden, "default-heads.org"), iset)
+    b = ol.Backend("oracle", cfg, iset, env, ncells=1)
+    b.set_orgs(0, [anc], deterministic=True)
+    st, ops, _ = b.states(0, 1)
+    t0 = trace.status_text(st[0], ops, iset)
+    assert t0.splitlines()[0] == "1 IP:0 (h-alloc)"
+    assert t0.splitlines()[1] == "AX:0 [0x0]  BX:0 [0x0]  CX:0 [0x0]  "
+    assert t0.splitlines()[3] == "* Stack 0:" + " Ox00000000" * 10
+    assert t0.splitlines()[5].startswith("  Mem (100):  " + iset.to_sequence(anc[:5]))
+    b.step(0, 1, uniform=1)
+    st, ops, _ = b.states(0, 1)
+    t1 = trace.status_text(st[0], ops, iset).splitlines()
+    # h-alloc grew the memory to 300 and put its old size in AX
+    assert t1[0].startswith("2 IP:1 (") and t1[1].startswith("AX:100 [0x64]")
+    assert t1[5].startswith("  Mem (300):")

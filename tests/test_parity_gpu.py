@@ -277,3 +277,35 @@ def test_driver_gpu_equals_oracle(golden, tmp_path):
     for name in ("average.dat", "time.dat"):
         for a, b in zip(rows(g / name), rows(o / name)):
             assert [float(x) for x in a] == pytest.approx([float(x) for x in b], rel=1e-5), name
+
+
+def test_trace_every_instruction(golden):
+    """Per-instruction traces (avida_amd/trace.py, the reference tracer's
+    PrintStatus at cpu/cHardwareCPU.cc:956): 192 organisms -- ancestor mutants
+    and evolved detail-50000 genotypes -- single-stepped 600 times with copy
+    and divide mutations on; GPU state == oracle state before every one of the
+    600 instructions (no divergence can hide between chunk boundaries), and the
+    PrintStatus texts agree."""
+    from avida_amd import trace
+    iset, env, cfg = pu.load_env(golden, overrides={"COPY_MUT_PROB": 0.02, "DIVIDE_MUT_PROB": 0.05,
+                                                    "DEATH_METHOD": 0})
+    anc = files.read_org(os.path.join(golden, "default-heads.org"), iset)
+    iset_c = files.read_instset(os.path.join(golden, "instset-classic.cfg"))
+    pop = [bytes(iset.op_of_name(iset_c.names[o]) for o in g) for g in pu.pop_genomes(golden, iset_c)[::40][:96]]
+    g = pu.mutants_of(anc, iset, 96, rate=0.02, seed=4) + pop
+    n = len(g)
+    orc, gpu = (ol.Backend(k, cfg, iset, env, ncells=n) for k in ("oracle", "gpu"))
+    for b in (orc, gpu):
+        b.set_orgs(0, g, deterministic=False)
+    for step in range(600):
+        a, oa, fa = orc.states(0, n, 512)
+        s, os_, fs = gpu.states(0, n, 512)
+        nbad, rep = pu.diff_states_np(a, s, oa, os_, fa, fs, 512)
+        assert nbad == 0, f"before instruction {step + 1}: {nbad} organisms differ {rep[:3]}"
+        if step % 150 == 0:
+            for i in range(0, n, 17):
+                assert trace.status_text(a[i], oa[i * 512:(i + 1) * 512], iset) == \
+                    trace.status_text(s[i], os_[i * 512:(i + 1) * 512], iset)
+        orc.step(0, n, uniform=1, mode=capi.MODE_FROZEN)
+        gpu.step(0, n, uniform=1, mode=capi.MODE_FROZEN)
+    assert sum(a[i].num_divides for i in range(n)) > 0

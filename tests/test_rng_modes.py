@@ -1,0 +1,113 @@
+"""Random streams (include/avida_gpu.h "random streams").
+
+CPU: the oracle's RECORDED mode consumes the host's doubles with the
+reference's Apto::RNG interface -- P(p) = u < p, GetUInt(n) = floor(u n),
+GetRandomInst = the cOrderedWeightedIndex lookup of u * total weight -- in the
+reference's call order (Divide_DoMutations: TestDivideSlip, -Mut, -Ins, -Del
+always draw; cpu/cHardwareBase.cc:296-569, main/cMutationRates.h:119-128).
+GPU: the device equals the oracle bit for bit with mutations on, fed from a
+recorded stream (FROZEN traces of the configs[2] population) and with the
+divide slip / uniform mutations in a world."""
+import os
+
+import numpy as np
+import pytest
+
+from avida_amd import capi, files
+import oracle_lib as ol
+import parity_util as pu
+
+CAP = capi.MAX_GENOME
+
+
+def _ancestor(golden, overrides):
+    iset, env, cfg = pu.load_env(golden, overrides=overrides, seed=3)
+    anc = files.read_org(os.path.join(golden, "default-heads.org"), iset)
+    return iset, env, cfg, anc
+
+
+def test_recorded_draws_follow_reference_interface(golden):
+    """Every h-copy mutates (COPY_MUT_PROB 1: P(1) = u < 1 always), every
+    draw is u = 0.37: the ancestor's 100 copies each consume two doubles (the
+    test, then GetRandomInst = the op whose cumulative weight first exceeds
+    0.37 * total), the divide consumes slip, mut, ins, del tests (DIVIDE_MUT 0:
+    no hit at u < 0) -- so the offspring is 100 copies of that op and the
+    stream position after the first gestation is 2 * 100 + 4 (+ the line and
+    instruction draws of an insertion hit when 0.37 < DIVIDE_INS_PROB)."""
+    iset, env, cfg, anc = _ancestor(golden, {"COPY_MUT_PROB": 1.0, "DIVIDE_INS_PROB": 0.5,
+                                             "DIVIDE_DEL_PROB": 0.1, "DEATH_METHOD": 0})
+    b = ol.Backend("oracle", cfg, iset, env, ncells=1)
+    b.set_orgs(0, [anc], deterministic=True)
+    u = 0.37
+    b.set_rng_mode(capi.RNG_RECORDED, np.full(4096, u))
+    st0, _, _ = b.states(0, 1, CAP)
+    assert st0[0].rng_counter == 0
+    # run until the first divide (one gestation: 389 instructions without mutations)
+    for k in range(2000):
+        b.step(0, 1, uniform=1, mode=capi.MODE_FROZEN)
+        st, ops, _ = b.states(0, 1, CAP)
+        if st[0].num_divides:
+            break
+    assert st[0].num_divides == 1
+    # 100 h-copies x (P + GetRandomInst), then slip, mut, ins (hit: u < 0.5 ->
+    # GetUInt(101), GetRandomInst), del (u >= 0.1: no hit)
+    assert st[0].rng_counter == 2 * 100 + 1 + 1 + 1 + 2 + 1
+    assert b.lib.orc_rec_exhausted() == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("muts", ["copy", "all"])
+def test_recorded_stream_frozen_traces_gpu(golden, muts):
+    """BASELINE configs[2] traces with mutations on, fed from one recorded
+    stream: 3600 organisms of the detail-50000 population, each with its own
+    segment, FROZEN mode (divide-mutation draws happen, the offspring is
+    discarded); per-lane state equal after 1, 30, 1000, 4000 instructions."""
+    iset_c = files.read_instset(os.path.join(golden, "instset-classic.cfg"))
+    genomes = pu.pop_genomes(golden, iset_c)[:3600]
+    ov = {"COPY_MUT_PROB": 0.02, "DIVIDE_INS_PROB": 0.05, "DIVIDE_DEL_PROB": 0.05, "DEATH_METHOD": 0}
+    if muts == "all":
+        ov.update({"DIVIDE_MUT_PROB": 0.1, "DIVIDE_SLIP_PROB": 0.05, "DIVIDE_UNIFORM_PROB": 0.05})
+    iset, env, cfg = pu.load_env(golden, "instset-classic.cfg", ov)
+    n = len(genomes)
+    rng = np.random.default_rng(42)
+    per = 4500              # h-copy alone draws once per copy at a non-zero rate
+    stream = rng.random(n * per)
+    offsets = np.arange(n, dtype=np.int64) * per
+    pair = [ol.Backend(k, cfg, iset, env, ncells=n) for k in ("oracle", "gpu")]
+    for b in pair:
+        b.set_orgs(0, genomes, deterministic=False)
+        b.set_rng_mode(capi.RNG_RECORDED, stream, offsets)
+    for budget in [1, 29, 970, 3000]:
+        for b in pair:
+            b.step(0, n, uniform=budget, mode=capi.MODE_FROZEN)
+        a, oa, fa = pair[0].states(0, n, CAP)
+        g, og, fg = pair[1].states(0, n, CAP)
+        bad = pu.diff_states(a, g, oa, og, fa, fg, CAP)
+        assert not bad, f"after {budget}: {len(bad)} mismatches {bad[:4]}"
+    assert max(a[i].rng_counter for i in range(n)) > 10
+    assert max(a[i].rng_counter for i in range(n)) < per    # no segment ran into the next one
+    assert pair[1].counters()[capi.CNT_REC_EXHAUSTED] == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fill", [0, 4])
+def test_divide_slip_uniform_world_gpu(golden, fill):
+    """World updates with DIVIDE_SLIP_PROB (SLIP_FILL_MODE 0 duplication / 4
+    nop-C) and DIVIDE_UNIFORM_PROB on top of the default mutations: GPU world
+    == oracle world, every cell digest, 120 updates."""
+    ov = {"DIVIDE_SLIP_PROB": 0.1, "DIVIDE_UNIFORM_PROB": 0.1, "SLIP_FILL_MODE": fill,
+          "WORLD_X": 48, "WORLD_Y": 48}
+    iset, env, cfg, anc = _ancestor(golden, ov)
+    n = 48 * 48
+    pair = [ol.Backend(k, cfg, iset, env, ncells=n) for k in ("oracle", "gpu")]
+    g = pu.mutants_of(anc, iset, n // 4, rate=0.01, seed=9)
+    for b in pair:
+        b.set_orgs(0, g, deterministic=False)
+    for u in range(120):
+        so, sg = pair[0].run_update(), pair[1].run_update()
+        for f in ("num_organisms", "insts_executed", "births", "deaths", "divides", "births_dropped"):
+            assert getattr(so, f) == getattr(sg, f), (u, f)
+    nbad, cells = pu.compare_digests(pair[0].digests(), pair[1].digests())
+    assert nbad == 0, cells
+    lens = {pair[0].states(c, 1)[0][0].birth_length for c in range(0, n, 7)}
+    assert len(lens) > 5      # slips changed genome lengths

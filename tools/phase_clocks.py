@@ -51,9 +51,9 @@ def main():
         "c0_sites_per_slice": tot[capi.CNT_C0_SITES] / max(1, tot[capi.CNT_C0_SLICES]),
         "lane_efficiency": tot[capi.CNT_INSTS] / max(1, tot[capi.CNT_LANESTEPS]),
         "spills_per_update": tot[capi.CNT_SPILLS] / updates,
-        "loop_cycles_per_iter_by_block": {k: tot[20 + i] / it for i, k in enumerate(
+        "loop_cycles_per_iter_by_block": {k: tot[32 + i] / it for i, k in enumerate(
             ["decode", "fast", "copy", "switch", "wave_phase", "advance"])},
-        "slow_phase_cycles_per_iter_by_case": {k: tot[26 + i] / it for i, k in enumerate(
+        "slow_phase_cycles_per_iter_by_case": {k: tot[38 + i] / it for i, k in enumerate(
             ["pop", "push", "io", "h_alloc", "h_divide", "search_label"])},
     }
     lib.avgpu_destroy(h)

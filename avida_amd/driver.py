@@ -10,9 +10,11 @@ shows the state at the end of update u, and "u N Exit" ends after update N.
 
 Events on this path (main/cEventList.cc syntax "u <start>[:<interval>[:<end>]]"):
 Inject <org> [cell] [merit], InjectAll <org> [merit], InjectSequence <seq>
-[start] [end] [merit], Print{Count,Average,Tasks,Time,Resource}Data [file],
-SavePopulation [file] (a checkpoint, avida_amd/checkpoint.py),
-LoadCheckpoint <file>, Exit.  Anything else is an error.
+[start] [end] [merit], LoadPopulation <file> [update] [cellid_offset] (.pop /
+.spop, avida_amd/population.py), SavePopulation [name] (<name>-<update>.spop),
+Print{Count,Average,Tasks,Time,Resource,Dominant}Data [file], SaveCheckpoint
+[file] / LoadCheckpoint <file> (full hardware state, avida_amd/checkpoint.py),
+Exit.  Other Print* events write nothing; anything else is an error.
 
     python -m avida_amd.driver -c <config dir> -d <data dir> [-u MAX_UPDATES]
 """
@@ -23,7 +25,7 @@ import ctypes as C
 import os
 import sys
 
-from . import capi, checkpoint, datafiles, files, systematics
+from . import capi, checkpoint, datafiles, files, population, systematics
 
 
 class ProductWorld:
@@ -64,6 +66,26 @@ class ProductWorld:
         st = capi.AvgpuUpdateStats()
         self._call("run_update", self.h, C.byref(st))
         return st
+
+    def kill(self, cell):
+        self._call("kill", self.h, cell)
+
+    def states(self, first, count, cap=capi.MAX_GENOME):
+        st = (capi.AvgpuCpuState * count)()
+        ops = (C.c_uint8 * (count * cap))()
+        fl = (C.c_uint8 * (count * cap))()
+        self._call("get_states", self.h, first, count, st, ops, fl, cap)
+        return st, bytes(ops), bytes(fl)
+
+    def test_genomes(self, genomes, flags_cap=2049):
+        n = len(genomes)
+        blob = b"".join(genomes)
+        buf = (C.c_uint8 * len(blob)).from_buffer_copy(blob)
+        lens = (C.c_int32 * n)(*[len(g) for g in genomes])
+        res = (capi.AvgpuTestResult * n)()
+        flags = C.create_string_buffer(n * flags_cap)
+        self._call("test_genomes", self.h, n, buf, lens, res, flags, flags_cap, None)
+        return [(res[i], None, None) for i in range(n)]
 
     def census(self, first=0, count=None):
         return capi.get_census(self.lib, self.p, self.h, first, self.ncells - first if count is None else count)
@@ -125,7 +147,7 @@ class Driver:
         self.data_dir = data_dir
         # genotype classification runs every update when a data file needs it
         # (the reference's systematics manager classifies every birth)
-        need = {"PrintCountData", "PrintDominantData"}
+        need = {"PrintCountData", "PrintDominantData", "SavePopulation"}
         self.arbiter = systematics.GenotypeArbiter(int(acfg.get("THRESHOLD", 3))) \
             if any(e[2] in need for e in self.events) else None
         self.rec.arbiter = self.arbiter
@@ -168,8 +190,21 @@ class Driver:
             self.rec.print_time(*args[:1])
         elif action == "PrintResourceData":
             self.rec.print_resource(w.resources()[0], *args[:1])
-        elif action == "SavePopulation":
-            name = args[0] if args else f"detail-{self.update}.npz"
+        elif action == "SavePopulation":          # actions/SaveLoadActions.cc:168-176
+            name = args[0] if args else "detail"
+            population.save_population(w, self.iset, self.arbiter,
+                                       os.path.join(self.data_dir, f"{name}-{max(self.update, 0)}.spop"),
+                                       max(self.update, 0))
+        elif action == "LoadPopulation":          # actions/SaveLoadActions.cc:62-88
+            if len(args) > 1 and int(args[1]) >= 0:
+                self.update = int(args[1]) - 1     # SetCurrentUpdate: the next update is that one
+            offset = int(args[2]) if len(args) > 2 else 0
+            population.load_population(w, self.iset, os.path.join(self.config_dir, args[0]),
+                                       w.ncells, offset)
+            if self.arbiter is not None:
+                self.arbiter.update(w.census(), max(self.update, 0))
+        elif action == "SaveCheckpoint":
+            name = args[0] if args else f"checkpoint-{self.update}.npz"
             w.checkpoint(os.path.join(self.data_dir, name))
         elif action == "LoadCheckpoint":
             self.rec.end_update(w.restore(os.path.join(self.config_dir, args[0])))

@@ -402,10 +402,19 @@ class Genotype:
     gest_time: int
     fitness: float
     sequence: str
+    cells: list | None = None        # .spop "cells" (structured population)
+    gest_offset: list | None = None  # .spop "gest_offset" (CPU cycles into the gestation)
+    props: dict = field(default_factory=dict)
+
+
+def _int_list(v):
+    return [int(x) for x in v.split(",")] if v not in (None, "", "(none)") else None
 
 
 def read_pop(path: str):
-    """.pop genotype_data file (#format line names the columns)."""
+    """.pop / .spop genotype_data file (#format line names the columns;
+    cPopulation::LoadPopulation reads num_units, falling back to num_cpus,
+    main/cPopulation.cc:6747-6766)."""
     fmt = None
     out = []
     with open(path) as f:
@@ -417,11 +426,13 @@ def read_pop(path: str):
                 continue
             toks = raw.split()
             rec = dict(zip(fmt, toks))
+            num = rec.get("num_units", rec.get("num_cpus", 1))
             out.append(Genotype(
-                int(rec.get("id", 0)), int(rec.get("num_cpus", 1)),
+                int(rec.get("id", 0)), int(num),
                 int(rec.get("length", len(rec["sequence"]))),
                 float(rec.get("merit", 0)), int(float(rec.get("gest_time", 0))),
-                float(rec.get("fitness", 0)), rec["sequence"]))
+                float(rec.get("fitness", 0)), rec["sequence"],
+                _int_list(rec.get("cells")), _int_list(rec.get("gest_offset")), rec))
     return out
 
 

@@ -99,6 +99,9 @@ class Backend:
         self._call("set_orgs", self.h, first, n, buf, lens.ctypes.data_as(C.POINTER(C.c_int32)), m, None,
                    1 if deterministic else 0)
 
+    def kill(self, cell):
+        self._call("kill", self.h, cell)
+
     def step(self, first, count, budget=None, uniform=0, mode=capi.MODE_FROZEN):
         b = None
         if budget is not None:

@@ -114,7 +114,8 @@ int setup_world(avgpu_world* w, int64_t n, bool test_buffers) {
   // offspring of one slice (device.h); test worlds never enqueue births
   W.rcap = n + (test_buffers ? 16 : std::max<int64_t>(4096, n / 4));
   const int64_t R = W.rcap;
-  A(b_count, 2); A(b_list, n); A(b_parent, R); A(b_seq, R); A(b_len, R); A(b_merit, R);
+  A(b_count, 2); A(b_list, n); A(b_parent, R); A(b_seq, R); A(b_len, R); A(b_len0, R); A(b_edit, 5 * R);
+  A(b_merit, R);
   A(b_fitness, R); A(b_gen, R); A(b_ccopied, R); A(b_exec, R);
   A(b_gest, R); A(b_ltask, AVGPU_NUM_LOGIC_TASKS * R); A(b_rng, 3 * R); A(b_target, R); A(b_state, R);
   A(b_prio, R); A(b_genome, (size_t)R * TAPE_SLOT);

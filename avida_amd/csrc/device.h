@@ -121,7 +121,9 @@ struct DevWorld {
   int32_t* b_list;    // [n] primary record ids, appended per wave after the loop
   int32_t* b_parent;  // [rcap]
   uint32_t* b_seq;    // [rcap]
-  int32_t* b_len;     // [rcap]
+  int32_t* b_len;     // [rcap]  offspring length after the divide mutations
+  int32_t* b_len0;    // [rcap]  the child's length before them (b_genome holds that child)
+  int32_t* b_edit;    // [5][rcap] its divide-mutation edits (interp.hip edit_word; 0 = none)
   double* b_merit;    // [rcap]
   double* b_fitness;  // [rcap]
   int32_t* b_gen;     // [rcap]

@@ -101,6 +101,8 @@ __device__ __forceinline__ bool consume_resource(const DevWorld& W, const double
   return true;
 }
 
+__host__ __device__ constexpr int tape_stride(int S) { return S == CLASS0_SIZE ? S : S + 16; }
+
 // divide-mutation edits (Divide_DoMutations, applied in order): kind | a << 3 | b << 15
 enum { E_SLIP = 1, E_POINT = 2, E_INS = 3, E_DEL = 4 };
 __device__ __forceinline__ int edit_word(int kind, int a, int b) { return kind | (a << 3) | (b << 15); }
@@ -111,9 +113,13 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
                                                 uint32_t* __restrict__ lds32, bool sorted, int row,
                                                 int lpw) {
   const DevWorld& W = *Wp;
-  // per-lane tape stride: a whole number of 16-byte quads (16-B LDS-DMA) with
-  // room for the fetch / label windows that read up to 16 bytes past a site
-  constexpr int STRIDE = S + 16;
+  // per-lane tape stride: a whole number of 16-byte quads (16-B LDS-DMA).
+  // The fetch / label / search windows read up to 16 bytes past a site; what
+  // they read beyond the organism's memory is masked off.  Classes 1-3 keep a
+  // 16-byte pad; class 0 has none -- a window past lane L's slot reads lane
+  // L+1's tape (lane 63's: the lookup tables after the tapes) -- so that its
+  // block (tapes 21 KiB + tables 0.75 KiB) stays at 7 per CU.
+  constexpr int STRIDE = tape_stride(S);
   constexpr int QUADS = STRIDE / 16;
   constexpr int TAPE_WORDS = 64 * STRIDE / 4;
   // class 0 keeps the two stacks in VGPRs (sv[]): without their 5 KiB of LDS a
@@ -572,17 +578,7 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
           if (done) {
             double mult = 1.0, addb = 0.0;
             uint32_t paid = done;
-            if (GTAB && !k_env_resources) {
-              // tasks in ascending order with wave-uniform indices: the factors
-              // are scalar loads (no vector-memory wait)
-#pragma unroll
-              for (int t = 0; t < AVGPU_NUM_LOGIC_TASKS; t++) {
-                if ((done >> t) & 1u) {
-                  mult = __dmul_rn(mult, W.task_tab[t]);
-                  addb = __dadd_rn(addb, W.task_tab[16 + t]);
-                }
-              }
-            } else {
+            {
             for (uint32_t d = done; d; d &= d - 1u) {
               const int t = __ffs(d) - 1;
               if ((k_env_res_mask >> t) & 1u) {                 // finite resource (general path below)
@@ -895,6 +891,12 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
                 st_async_u32(W.b_parent + rec, (uint32_t)cell);
                 st_async_u32(W.b_seq + rec, (uint32_t)nd);
                 st_async_u32(W.b_len + rec, (uint32_t)len);
+                st_async_u32(W.b_len0 + rec, (uint32_t)child);   // k_apply_mutations edits the copy
+                st_async_u32(W.b_edit + rec, (uint32_t)e0);
+                st_async_u32(W.b_edit + W.rcap + rec, (uint32_t)e1);
+                st_async_u32(W.b_edit + 2 * W.rcap + rec, (uint32_t)e2);
+                st_async_u32(W.b_edit + 3 * W.rcap + rec, (uint32_t)e3);
+                st_async_u32(W.b_edit + 4 * W.rcap + rec, (uint32_t)e4);
                 st_async_u64(W.b_merit + rec, (uint64_t)__double_as_longlong(merit));
                 st_async_u64(W.b_fitness + rec, (uint64_t)__double_as_longlong(fit));
                 st_async_u32(W.b_gen + rec, (uint32_t)gen);
@@ -926,7 +928,6 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
         okw = __shfl(okw, L);
         if (okw) {
           rec = __shfl(rec, L); len = __shfl(len, L);
-          e0 = __shfl(e0, L); e1 = __shfl(e1, L); e2 = __shfl(e2, L); e3 = __shfl(e3, L); e4 = __shfl(e4, L);
           const int cell_l = __shfl(cell, L);
           if (mode == AVGPU_MODE_TEST) {
             // test-CPU snapshots: executed flags of the parent part, the offspring
@@ -946,37 +947,17 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
               st_async_u32(ch + 4 * w, wd);
             }
           } else if (mode == AVGPU_MODE_WORLD && rec >= 0) {
-            // offspring genome, 4 sites per lane: site j of the mutated child
-            // is traced back through the edits (last first) to a site of the
-            // unmutated child or to a value an edit wrote
+            // the unmutated child, 4 sites per lane; its divide mutations are
+            // applied by k_apply_mutations (world.hip) before placement, from
+            // the edits stored with the record -- keeping the per-site edit
+            // composition out of this kernel's registers
             uint8_t* g = W.b_genome + (int64_t)rec * TAPE_SLOT;
-            const bool nopc = W.slip_fill_mode == 4;
-            for (int w = lane; (w << 2) < len; w += 64) {
-              uint32_t word = 0;
-#pragma unroll
-              for (int q = 0; q < 4; q++) {
-                const int j = 4 * w + q;
-                int src = j, val = -1;
-                // straight-line over e4 .. e0 (no indexed register array)
-                auto undo = [&](int ew) {
-                  if (ew == 0 || val >= 0) return;
-                  const int kind = ew & 7, a = (ew >> 3) & 0xFFF, b = (ew >> 15) & 0xFFF;
-                  if (kind == E_POINT) {
-                    if (src == a) val = b;
-                  } else if (kind == E_INS) {
-                    if (src == a) val = b; else if (src > a) src--;
-                  } else if (kind == E_DEL) {
-                    if (src >= a) src++;
-                  } else {                                    // slip from a to b
-                    if (nopc && a > b && src >= a && src < 2 * a - b) val = AVGPU_H_NOP_C;
-                    else if (src >= a) src = b + (src - a);
-                  }
-                };
-                undo(e4); undo(e3); undo(e2); undo(e1); undo(e0);
-                const int v = val >= 0 ? val : (TL[div + src] & CODE_MASK);
-                word |= (j < len ? (uint32_t)v : 0u) << (8 * q);
-              }
-              st_async_u32(g + 4 * w, word);
+            const uint32_t dsh = (uint32_t)(div & 3) * 8u;
+            for (int w = lane; (w << 2) < child; w += 64) {
+              const int a = (div >> 2) + w;                 // aligned words around sites div+4w ..
+              const uint32_t lo = TL32[a], hi = TL32[a + 1];
+              const uint32_t v = dsh ? ((lo >> dsh) | (hi << (32u - dsh))) : lo;
+              st_async_u32(g + 4 * w, v & 0x3F3F3F3Fu & byte_mask(w << 2, 0, child));
             }
           }
           // parent ClearFlags over its remaining sites, empty stacks
@@ -1148,7 +1129,7 @@ __global__ __launch_bounds__(64, (S == CLASS0_SIZE) ? 2 : 1) void k_interpret(co
   // class 0: stacks in VGPRs, tables in global memory -- only the tapes in LDS
   constexpr int STK = (S == CLASS0_SIZE) ? 0 : 2 * AVGPU_STACK_SIZE * 64;
   constexpr int TAB = (S == CLASS0_SIZE) ? 192 : TAB_WORDS;   // class 0: task LUT + random LUT
-  __shared__ __attribute__((aligned(16))) uint32_t lds32[64 * (S + 16) / 4 + STK + TAB];
+  __shared__ __attribute__((aligned(16))) uint32_t lds32[64 * tape_stride(S) / 4 + STK + TAB];
   if (cls == 0) {
     // sorted windows: the 32 chunks of a window run on one XCD (blocks are
     // dealt to the 8 XCDs round robin), so its state lines meet in one L2

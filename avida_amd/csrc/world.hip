@@ -609,6 +609,66 @@ __global__ void k_halo_clear(DevWorld W) {
   W.claim[ghost_cell(W, d, x)] = 0ull;
 }
 
+// Divide_DoMutations' edits (cpu/cHardwareBase.cc:296-569), drawn in the
+// interpreter in the reference's order and stored with the birth record
+// (interp.hip): one wave per queued offspring that has any rewrites its
+// genome -- site j of the mutated child is traced back through the edits
+// (last first) to a site of the unmutated child or to a value an edit wrote.
+// Runs before placement, so halo records and activation see final genomes.
+__device__ __forceinline__ int mut_source(int j, const int* e, bool nopc, int& val) {
+  int src = j;
+  val = -1;
+#pragma unroll
+  for (int k = 4; k >= 0; k--) {
+    const int ew = e[k];
+    if (ew == 0 || val >= 0) continue;
+    const int kind = ew & 7, a = (ew >> 3) & 0xFFF, b = (ew >> 15) & 0xFFF;
+    if (kind == 2) {                         // point (E_POINT)
+      if (src == a) val = b;
+    } else if (kind == 3) {                  // insertion (E_INS)
+      if (src == a) val = b; else if (src > a) src--;
+    } else if (kind == 4) {                  // deletion (E_DEL)
+      if (src >= a) src++;
+    } else {                                 // slip from a to b (E_SLIP)
+      if (nopc && a > b && src >= a && src < 2 * a - b) val = AVGPU_H_NOP_C;
+      else if (src >= a) src = b + (src - a);
+    }
+  }
+  return src;
+}
+
+__global__ __launch_bounds__(64) void k_apply_mutations(DevWorld W) {
+  __shared__ uint8_t child[TAPE_SLOT + 16];
+  const int nb = queue_len(W);
+  const int lane = threadIdx.x;
+  const bool nopc = W.slip_fill_mode == 4;
+  for (int64_t q = blockIdx.x; q < nb; q += gridDim.x) {
+    const int64_t r = rec_of(W, q);
+    int e[5];
+#pragma unroll
+    for (int k = 0; k < 5; k++) e[k] = W.b_edit[(int64_t)k * W.rcap + r];
+    if ((e[0] | e[1] | e[2] | e[3] | e[4]) == 0) continue;   // wave-uniform
+    const int len0 = W.b_len0[r], len = W.b_len[r];
+    uint32_t* g32 = reinterpret_cast<uint32_t*>(W.b_genome + r * TAPE_SLOT);
+    uint32_t* c32 = reinterpret_cast<uint32_t*>(child);
+    for (int w = lane; (w << 2) < len0; w += 64) c32[w] = g32[w];
+    __syncthreads();
+    for (int w = lane; (w << 2) < len; w += 64) {
+      uint32_t word = 0;
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        const int j = 4 * w + k;
+        int val;
+        const int src = mut_source(j, e, nopc, val);
+        const uint32_t v = val >= 0 ? (uint32_t)val : (uint32_t)child[src];
+        word |= (j < len ? v : 0u) << (8 * k);
+      }
+      g32[w] = word;
+    }
+    __syncthreads();
+  }
+}
+
 // ActivateOrganism (main/cPopulation.cc:1320-1340) + SetupOffspring
 // (main/cPhenotype.cc:349-420) of one offspring into cell c by one wave.  The
 // organism is marked CTL_FRESH: its zero / default fields (registers, heads,
@@ -990,7 +1050,14 @@ static unsigned activate_grid(const DevWorld& W) { return (unsigned)std::min<int
 // placement kernels stride over the queue; 8 blocks of 256 per CU cover it
 static unsigned place_grid(const DevWorld& W) { return (unsigned)std::min<int64_t>(nblk(W.rcap, 256), 2048); }
 
+static unsigned activate_grid(const DevWorld& W);
+static void launch_apply_mutations(const DevWorld& W, hipStream_t s) {
+  if (W.th_div_mut | W.th_div_ins | W.th_div_del | W.th_div_slip | W.th_div_uni)
+    hipLaunchKernelGGL(k_apply_mutations, dim3(activate_grid(W)), dim3(64), 0, s, W);
+}
+
 void launch_world_post(const DevWorld& W, hipStream_t s, double* stats) {
+  launch_apply_mutations(W, s);
   launch_resources_end(W, s);
   const unsigned bb = place_grid(W);
   hipLaunchKernelGGL(k_occ_init, dim3(nblk(W.n, 256)), dim3(256), 0, s, W);
@@ -1019,6 +1086,7 @@ void launch_tile_totals(const DevWorld& W, hipStream_t s, const double* gathered
 
 // after interpretation: occupancy (cells + ghost rows) and the edge-row export
 void launch_tile_after_interpret(const DevWorld& W, hipStream_t s) {
+  launch_apply_mutations(W, s);
   hipLaunchKernelGGL(k_occ_init, dim3(nblk(W.n + 2 * (int64_t)W.world_x, 256)), dim3(256), 0, s, W);
   hipLaunchKernelGGL(k_halo_export, dim3(nblk(2 * (int64_t)W.world_x, 256)), dim3(256), 0, s, W, 0);
 }

@@ -41,7 +41,7 @@ DOMINANT_COLS = ["Update", "Average Merit of the Dominant Genotype",
                  "Genotype ID of Dominant Genotype", "Name of the Dominant Genotype"]
 # count.dat 4 / 5 come from the genotype classification (avida_amd/systematics.py)
 # when the driver runs one; dominant.dat 8 is 0 in the reference as well
-UNTRACKED = {"count.dat": [11, 12, 13, 16], "average.dat": [5, 7, 8, 11, 14, 15, 16],
+UNTRACKED = {"count.dat": [11, 12, 13, 16], "average.dat": [5, 6, 11, 14, 15, 16],
              "dominant.dat": [10, 11, 12, 13]}
 
 
@@ -85,6 +85,7 @@ class StatsRecorder:
         self.last = None
         self.resource_names = list(resource_names)
         self.arbiter = None       # systematics.GenotypeArbiter, set by the driver
+        self.injected = 0         # organisms injected / loaded in the current update
 
     def _stamp(self):
         return time.strftime("%a %b %d %H:%M:%S %Y")
@@ -102,6 +103,12 @@ class StatsRecorder:
             self.avida_time += 1.0 / (s.sum_merit / s.num_organisms)
 
     def end_update(self, stats):
+        """the reference counts injected and loaded organisms as births of the
+        update they arrive in (cPopulation::ActivateOrganism -> cStats
+        RecordBirth, main/cPopulation.cc:1320-1340)"""
+        if self.injected:
+            stats.births += self.injected
+            self.injected = 0
         self.last = stats
 
     def print_count(self, name="count.dat"):
@@ -125,7 +132,13 @@ class StatsRecorder:
         n = s.num_organisms
         avg = (lambda v: v / n) if n else (lambda v: 0.0)
         f = self._file(name, ["Avida Average Data", self._stamp()], AVERAGE_COLS)
-        f.row([s.update, avg(s.sum_merit), avg(s.sum_gestation), avg(s.sum_fitness), 0, 0, 0, 0, 0,
+        copied = executed = 0.0
+        c = self.arbiter.census if self.arbiter is not None else None
+        if c is not None and n:                     # cStats copied / executed size sums
+            live = c["genotype_key"] != 0
+            copied = float(c["copied_size"][live].astype("f8").sum()) / n
+            executed = float(c["executed_size"][live].astype("f8").sum()) / n
+        f.row([s.update, avg(s.sum_merit), avg(s.sum_gestation), avg(s.sum_fitness), 0, 0, copied, executed, 0,
                (s.births / n) if n else 0.0, 0, 0, s.ave_generation, 0, 0, 0])
 
     def print_tasks(self, name="tasks.dat"):

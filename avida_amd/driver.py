@@ -147,7 +147,7 @@ class Driver:
         self.data_dir = data_dir
         # genotype classification runs every update when a data file needs it
         # (the reference's systematics manager classifies every birth)
-        need = {"PrintCountData", "PrintDominantData", "SavePopulation"}
+        need = {"PrintCountData", "PrintDominantData", "SavePopulation", "PrintAverageData"}
         self.arbiter = systematics.GenotypeArbiter(int(acfg.get("THRESHOLD", 3))) \
             if any(e[2] in need for e in self.events) else None
         self.rec.arbiter = self.arbiter
@@ -163,17 +163,20 @@ class Driver:
             cell = int(args[1]) if len(args) > 1 else 0
             merit = float(args[2]) if len(args) > 2 else -1.0
             w.set_orgs(cell, [self._org(args[0])], [max(0.0, merit)], deterministic=False)
+            self.rec.injected += 1
         elif action == "InjectAll":
             g = self._org(args[0])
             merit = float(args[1]) if len(args) > 1 else -1.0
             n = self.cfg.world_x * self.cfg.world_y
             w.set_orgs(0, [g] * n, [max(0.0, merit)] * n, deterministic=False)
+            self.rec.injected += n
         elif action.lower() == "injectsequence":
             g = self.iset.parse_sequence(args[0])
             start = int(args[1]) if len(args) > 1 else 0
             end = int(args[2]) if len(args) > 2 else start + 1
             merit = float(args[3]) if len(args) > 3 else -1.0
             w.set_orgs(start, [g] * (end - start), [max(0.0, merit)] * (end - start), deterministic=False)
+            self.rec.injected += end - start
         if action in ("Inject", "InjectAll") or action.lower() == "injectsequence":
             if self.arbiter is not None:      # injected units are classified at once
                 self.arbiter.update(w.census(), max(self.update, 0))
@@ -199,8 +202,8 @@ class Driver:
             if len(args) > 1 and int(args[1]) >= 0:
                 self.update = int(args[1]) - 1     # SetCurrentUpdate: the next update is that one
             offset = int(args[2]) if len(args) > 2 else 0
-            population.load_population(w, self.iset, os.path.join(self.config_dir, args[0]),
-                                       w.ncells, offset)
+            self.rec.injected += population.load_population(
+                w, self.iset, os.path.join(self.config_dir, args[0]), w.ncells, offset)
             if self.arbiter is not None:
                 self.arbiter.update(w.census(), max(self.update, 0))
         elif action == "SaveCheckpoint":

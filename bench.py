@@ -162,13 +162,13 @@ def cpu_baseline(golden, seconds, env_kind="logic9"):
     picks = _genomes_for(n, pool)
     b.set_orgs(0, [g for g, _ in picks], merits=[m for _, m in picks], deterministic=False)
     st = capi.AvgpuUpdateStats()
-    insts, updates = 0, 0
+    updates = 0
     t0 = time.perf_counter()
     while time.perf_counter() - t0 < seconds:
         b.lib.orc_run_serial_updates(b.h, 10, C.byref(st))
-        insts += st.insts_executed
         updates += 10
     dt = time.perf_counter() - t0
+    insts = st.cum_insts_executed
     return {"value": insts / dt, "unit": "organism-instructions/s", "cores": 1, "kind": "port",
             "sample": f"oracle serial world (reference-style scheduler + speculative steps), "
                       f"60x60 evolved logic-9 population ({env_kind} environment), {updates} updates, {insts} insts, "

@@ -1991,7 +1991,8 @@ struct SerialSched {
   }
 };
 
-static void serial_place(World& w, SerialSched& sch, Birth& b) {
+// returns 1 if the offspring was placed (2 if it replaced a living organism)
+static int serial_place(World& w, SerialSched& sch, Birth& b) {
   int64_t nb[8];
   const int nn = neighbours(w, b.parent, nb);
   int64_t cand[9];
@@ -2001,11 +2002,13 @@ static void serial_place(World& w, SerialSched& sch, Birth& b) {
     for (int k = 0; k < nn; k++) cand[nc++] = nb[k];
     if (w.cfg.allow_parent) cand[nc++] = b.parent;
   }
-  if (nc == 0) return;
+  if (nc == 0) return 0;
   int64_t t = cand[w.global_rng.uint_below((uint32_t)nc)];
+  const int killed = w.orgs[t].alive ? 1 : 0;
   activate_child(w, b, t);
   w.orgs[t].spec_count = 0;
   sch.set(t, w.orgs[t].merit);
+  return 1 + killed;
 }
 
 int orc_run_serial_updates(void* h, int n_updates, avgpu_update_stats* out) {
@@ -2013,12 +2016,11 @@ int orc_run_serial_updates(void* h, int n_updates, avgpu_update_stats* out) {
   SerialSched sch;
   sch.init(w.ncells);
   for (int64_t c = 0; c < w.ncells; c++) sch.set(c, w.orgs[c].alive ? w.orgs[c].merit : 0.0);
-  int64_t insts = 0;
   for (int u = 0; u < n_updates; u++) {
     int64_t n_alive = 0;
     for (int64_t c = 0; c < w.ncells; c++) n_alive += w.orgs[c].alive;
     const int64_t ud = (int64_t)w.cfg.ave_time_slice * n_alive;   // cWorld::CalculateUpdateSize
-    int64_t births = 0;
+    int64_t insts = 0, births = 0, deaths = 0, divides = 0;
     res_begin(w);   // ProcessPreUpdate + the update's first DoUpdates
     for (int64_t i = 0; i < ud; i++) {
       const double tot = sch.tree[1];
@@ -2031,6 +2033,7 @@ int orc_run_serial_updates(void* h, int n_updates, avgpu_update_stats* out) {
       if (o.spec_count > 0) { o.spec_count--; continue; }
       Exec ex{w, o, AVGPU_MODE_WORLD};
       w.births.clear();
+      const int d0 = o.num_divides;
       ex.single_process(c);
       // speculative run-ahead: up to 32 more, stopping before STALL insts
       // (IO, h-divide: cpu/cHardwareCPU.cc:961-968)
@@ -2042,21 +2045,21 @@ int orc_run_serial_updates(void* h, int n_updates, avgpu_update_stats* out) {
         spec++;
       }
       o.spec_count = spec;
-      if (!o.alive) { sch.set(c, 0.0); }
+      divides += o.num_divides - d0;
+      if (!o.alive) { sch.set(c, 0.0); deaths++; }
       for (auto& b : w.births) {
         sch.set(c, o.alive ? o.merit : 0.0);   // AdjustSchedule(parent) :933
-        serial_place(w, sch, b);
-        births++;
+        const int r = serial_place(w, sch, b);
+        births += r > 0;
+        deaths += r == 2;                       // KillOrganism of the replaced occupant
       }
       w.births.clear();
     }
     res_end(w);
-    w.update++;
-    (void)births;
+    // cStats for the update (finish_stats advances the update counter)
+    w.t_insts = insts; w.t_deaths = deaths; w.t_divides = divides; w.t_slices = 0;
+    finish_stats(w, births, 0);
   }
-  w.stats.insts_executed = insts;
-  w.stats.num_organisms = 0;
-  for (int64_t c = 0; c < w.ncells; c++) w.stats.num_organisms += w.orgs[c].alive;
   if (out) *out = w.stats;
   return 0;
 }

@@ -1,0 +1,92 @@
+"""Statistical parity on the bench's own population (SURVEY.md north star:
+"task-discovery times and fitness trajectories within stated statistical
+tolerance of the reference over many seeds").
+
+The reference's heads_midrun_30u test (tests/golden/heads_midrun_30u: its
+config directory -- LoadPopulation detail-50000.pop, the evolved logic-9
+genotypes bench.py seeds from -- and its expected data files) is one run of the
+reference, printed every 5 updates.  Each configuration below runs the same
+config directory through the Avida2Driver restatement (avida_amd/driver.py:
+LoadPopulation, count / tasks / average data files) over many seeds and
+compares the reference's numbers -- the nine task-organism counts, average
+merit, gestation time and fitness -- with the seed distribution:
+
+* the oracle's serial world (the reference's own update semantics: a
+  merit-weighted pick per instruction, speculative run-ahead, births placed at
+  once): |reference - mean| <= 3 sd + 1 % at every printed update 5..30;
+* the GPU batch world (the product's update): at updates
+  10..30 within 8 % of the reference.  Update 5 is the documented exception:
+  the loaded population starts in lock step, ~45 % of it reaches its first
+  divide in the same update, and the batch model places those births at the
+  end of the update, where the reference places each one at once and kills a
+  neighbour that might have divided later in the update -- the batch world
+  shows ~40 % more completed gestations at update 5 (measured 2348 vs 1670
+  task organisms) and converges by update 10.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+import pytest
+
+from avida_amd import capi, driver
+import oracle_lib as ol
+
+U = [5, 10, 15, 20, 25, 30]
+COLS = [f"task{t}" for t in range(9)] + ["merit", "gestation", "fitness"]
+
+
+def _rows(path):
+    return {int(l.split()[0]): [float(x) for x in l.split()[1:]] for l in open(path)
+            if l.strip() and not l.startswith("#")}
+
+
+def _ref(golden):
+    d = os.path.join(golden, "heads_midrun_30u", "expected")
+    t, a = _rows(os.path.join(d, "tasks.dat")), _rows(os.path.join(d, "average.dat"))
+    return {u: t[u] + a[u][:3] for u in U}
+
+
+def _run(golden, tmp_path, make_world, seeds):
+    cfg = os.path.join(golden, "heads_midrun_30u", "config")
+    out = {u: [] for u in U}
+    for s in seeds:
+        d = str(tmp_path / f"s{s}")
+        drv = driver.Driver(cfg, d, make_world=make_world, seed=s)
+        assert drv.run() == 30                   # "u 30 Exit"
+        drv.world.close()
+        t, a = _rows(os.path.join(d, "tasks.dat")), _rows(os.path.join(d, "average.dat"))
+        for u in U:
+            out[u].append(t[u] + a[u][:3])
+    return {u: np.array(v) for u, v in out.items()}
+
+
+class _SerialOracle(ol.Backend):
+    """the oracle's reference-semantics serial world (orc_run_serial_updates)"""
+
+    def run_update(self):
+        st = capi.AvgpuUpdateStats()
+        self.lib.orc_run_serial_updates(self.h, 1, C.byref(st))
+        return st
+
+
+def test_serial_oracle_matches_reference_midrun(golden, tmp_path):
+    ref = _ref(golden)
+    res = _run(golden, tmp_path, lambda cfg, iset, env: _SerialOracle("oracle", cfg, iset, env),
+               range(1, 13))
+    for u in U:
+        m, sd = res[u].mean(0), res[u].std(0, ddof=1)
+        for k, name in enumerate(COLS):
+            tol = 3 * sd[k] + 0.01 * abs(ref[u][k])
+            assert abs(ref[u][k] - m[k]) <= tol, (u, name, ref[u][k], m[k], sd[k])
+
+
+@pytest.mark.gpu
+def test_gpu_batch_world_midrun(golden, tmp_path):
+    ref = _ref(golden)
+    res = _run(golden, tmp_path, lambda cfg, iset, env: driver.ProductWorld(cfg, iset, env), range(1, 33))
+    for u in U:
+        m = res[u].mean(0)
+        for k, name in enumerate(COLS):
+            rel = abs(ref[u][k] - m[k]) / max(abs(ref[u][k]), 1e-12)
+            assert rel <= (0.45 if u == 5 else 0.08), (u, name, ref[u][k], m[k], rel)

@@ -366,6 +366,10 @@ __device__ __forceinline__ int head_adjust(int pos, int size) {
   if (pos < 2 * size) return pos - size;
   return pos % size;
 }
+// head_adjust of a position known to lie in [0, size] (one past a valid site)
+__device__ __forceinline__ int head_wrap(int pos, int size) {
+  return (unsigned)pos < (unsigned)size ? pos : pos - size;
+}
 
 // cInstSet::GetRandomInst (cpu/cInstSet.cc:83-88) -> canonical code
 __device__ __forceinline__ uint8_t random_code(const DevWorld& W, uint32_t lo, uint32_t hi,

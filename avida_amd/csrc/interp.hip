@@ -183,10 +183,14 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
   // loop cycles by block: decode, fast, copy, switch, wave phase, advance
   uint64_t cb[6] = {0, 0, 0, 0, 0, 0};
   uint64_t clast = 0;
-  // slow-switch cycles by case: pop, push, IO, h-alloc, h-divide, h-search/if-label
-  uint64_t cc[6] = {0, 0, 0, 0, 0, 0};
+  // slow-switch cycles by case: pop, push, IO, h-alloc, h-divide, h-search,
+  // if-label, and the stretch from the copy block to the switch
+  uint64_t cc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #define CK(k) do { const uint64_t _n = __builtin_amdgcn_s_memtime(); cb[k] += _n - clast; clast = _n; } while (0)
 #define CKC(k) do { const uint64_t _n = __builtin_amdgcn_s_memtime(); cc[k] += _n - clast; clast = _n; } while (0)
+#elif defined(AVGPU_ISA_MARKS)
+#define CK(k) asm volatile("; @MARK CK" #k)
+#define CKC(k) asm volatile("; @MARK CKC" #k)
 #else
 #define CK(k) do { } while (0)
 #define CKC(k) do { } while (0)
@@ -378,6 +382,10 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
       const int ipa = head_adjust(ip, M);                     // ip.Adjust() :952
       // fetch window: sites ipa .. ipa+4 in two independent word reads
       const uint64_t fwin = ((uint64_t)T32[(ipa >> 2) + 1] << 32) | (uint64_t)T32[ipa >> 2];
+      // h-copy's two sites, read with the fetch (one LDS round trip per
+      // iteration instead of two); used only if the op is h-copy
+      const int rha = head_adjust(rh, M), wha = head_adjust(wh, M);
+      const int src_byte = T[rha], dst_byte = T[wha];
       const uint32_t fsh = (uint32_t)(ipa & 3) * 8u;
       const int cur_byte = (int)((fwin >> fsh) & 0xFFu);
       const int op = cur_byte & CODE_MASK;                    // fetch :959
@@ -445,14 +453,14 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
       adv = !(op == AVGPU_H_MOV_HEAD && r == 0);
       // if-n-equ :2190 / if-less :2235 skip the next instruction
       const bool skip = (op == AVGPU_H_IF_N_EQU && ra == rb) || (op == AVGPU_H_IF_LESS && ra >= rb);
-      if (skip) ip = head_adjust(ip + 1, M);
+      if (skip) ip = head_wrap(ip + 1, M);
       ctl ^= (op == AVGPU_H_SWAP_STK) ? CTL_CURSTK : 0u;                     // swap-stk :2739
     }
     CK(1);
     if (op == AVGPU_H_H_COPY) {                               // :7130 Inst_HeadCopy
-      rh = head_adjust(rh, M);
-      wh = head_adjust(wh, M);
-      int v = T[rh] & CODE_MASK;
+      rh = rha;
+      wh = wha;
+      int v = src_byte & CODE_MASK;
       // ReadInst (:1459-1466)
       if (v < 3) {
         const int len = rl & 15;
@@ -463,16 +471,18 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
       // TestCopyMut: no draw at rate 0 (main/cMutationRates.h:112)
       if (mode != AVGPU_MODE_TEST && k_th_copy_mut && draw_p(k_th_copy_mut, W.p_copy_mut))
         v = rand_code();
-      T[wh] = (uint8_t)((T[wh] & TF_EXEC) | TF_COPIED | v);
-      rh = head_adjust(rh + 1, M);
-      wh = head_adjust(wh + 1, M);
+      // the write head's executed flag: as read, or just set if it is the IP
+      const int wex = (wh == ip) ? TF_EXEC : (dst_byte & TF_EXEC);
+      T[wh] = (uint8_t)(wex | TF_COPIED | v);
+      rh = head_wrap(rh + 1, M);
+      wh = head_wrap(wh + 1, M);
     }
     CK(2);
     if (!(FAST_OPS & obit) && op != AVGPU_H_H_COPY) { pop = op; pr = r; stepped = false; }   // park
     }  // !spill
     }  // run
     if (stepped && !stop) {
-      if (adv) ip = head_adjust(ip + 1, M);                   // ip.Advance() :1013
+      if (adv) ip = head_wrap(ip + 1, M);                     // ip.Advance() :1013
       if (mx > 0 && tu >= mx) alive = false;                  // death :1045-1049
     }
     // ---- slow phase ----
@@ -488,7 +498,7 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
     const bool sstep = pop >= 0;
     if (sstep) {
       const int op = pop, r = pr;
-      CK(3);
+      CKC(7);
       switch (op) {
       case AVGPU_H_POP: {                                     // :2698, cCPUStack::Pop
         const int k = (ctl & CTL_CURSTK) ? 1 : 0;
@@ -707,9 +717,10 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
         if (op == AVGPU_H_IF_LABEL) {
           const uint32_t packed = (uint32_t)len | (rot << 4);
           if (packed != rl) ip = head_adjust(ip + 1, M);
+          CKC(6);
           break;
         }
-        if (len > 0) { rq = RQ_SEARCH; qa = len; qb = (int)rot; break; }   // label scan below
+        if (len > 0) { rq = RQ_SEARCH; qa = len; qb = (int)rot; CKC(5); break; }   // label scan below
         r1 = 0;                                               // empty label: found = IP
         r2 = 0;
         fh = head_adjust(ip + 1, M);
@@ -1114,7 +1125,7 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
       count_add(W, CNT_IT_SLOW, (unsigned long long)it_slow);
       count_add(W, CNT_WAVES, 1ull);
       for (int k = 0; k < 6; k++) count_add(W, CNT_CB0 + k, cb[k]);
-      for (int k = 0; k < 6; k++) count_add(W, CNT_CASE0 + k, cc[k]);
+      for (int k = 0; k < 8; k++) count_add(W, CNT_CASE0 + k, cc[k]);
     }
   }
 #endif

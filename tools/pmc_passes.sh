@@ -15,7 +15,7 @@ for C in "FETCH_SIZE" "WRITE_SIZE GRBM_COUNT GRBM_GUI_ACTIVE" \
          "SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_BRANCH SQ_ACTIVE_INST_VALU" \
          "SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE"; do
   timeout -s KILL 120 rocprofv3 --pmc $C --output-format csv -d gpurun_out/pmc_${TAG}_$P -o run -- \
-    python bench.py --steps 5 --warmup 2 --no-cpu > gpurun_out/pmc_${TAG}_$P.log 2>&1 || { echo "pass $P failed"; exit 1; }
+    python bench.py --steps 5 --warmup 2 --no-cpu --long-updates 0 > gpurun_out/pmc_${TAG}_$P.log 2>&1 || { echo "pass $P failed"; exit 1; }
   P=$((P + 1))
 done
 python tools/pmc_summary.py "gpurun_out/pmc_${TAG}_*/**/*counter_collection.csv" \

@@ -295,13 +295,13 @@ __device__ __forceinline__ int64_t rec_of(const DevWorld& W, int64_t i) {
 // operations (~3000 cycles under load) before its first LDS read.  expcnt(0)
 // lets the data VGPRs be reused immediately.
 __device__ __forceinline__ void st_async_u32(void* p, uint32_t v) {
-  asm volatile("global_store_dword %0, %1, off\n\ts_waitcnt expcnt(0)" ::"v"(p), "v"(v) : "memory");
+  asm volatile("global_store_dword %0, %1, off\n\ts_waitcnt expcnt(0)" ::"v"(p), "v"(v));
 }
 __device__ __forceinline__ void st_async_u64(void* p, uint64_t v) {
-  asm volatile("global_store_dwordx2 %0, %1, off\n\ts_waitcnt expcnt(0)" ::"v"(p), "v"(v) : "memory");
+  asm volatile("global_store_dwordx2 %0, %1, off\n\ts_waitcnt expcnt(0)" ::"v"(p), "v"(v));
 }
 __device__ __forceinline__ void st_async_u8(void* p, uint32_t v) {
-  asm volatile("global_store_byte %0, %1, off\n\ts_waitcnt expcnt(0)" ::"v"(p), "v"(v) : "memory");
+  asm volatile("global_store_byte %0, %1, off\n\ts_waitcnt expcnt(0)" ::"v"(p), "v"(v));
 }
 
 // ---------------------------------------------------------------------------
@@ -393,26 +393,32 @@ __device__ __forceinline__ double det_exp2(double x) {
 }
 
 // CalcSizeMerit (main/cPhenotype.cc:1760-1816)
-__device__ __forceinline__ int calc_size_merit(const DevWorld& W, int glen, int copied, int exe) {
+__device__ __forceinline__ int size_merit(int method, int base_const, int glen, int copied, int exe) {
   int s;
-  switch (W.base_merit_method) {
+  switch (method) {
     case 1: return copied;
     case 2: return exe;
     case 3: return glen;
     case 4: s = glen; if (s > copied) s = copied; if (s > exe) s = exe; return s;
     case 5: s = glen; if (s > copied) s = copied; if (s > exe) s = exe;
             return (int)sqrt((double)s);
-    default: return W.base_const_merit;
+    default: return base_const;
   }
 }
+__device__ __forceinline__ int calc_size_merit(const DevWorld& W, int glen, int copied, int exe) {
+  return size_merit(W.base_merit_method, W.base_const_merit, glen, copied, exe);
+}
+// a value the compiler must keep (in an SGPR, or spilled) rather than
+// re-load from its invariant source at each use
+#define OPQ(x) asm("" : "+s"(x))
 
 __device__ __forceinline__ void count_add(const DevWorld& W, int slot, unsigned long long v) {
   atomicAdd(&W.counters[(blockIdx.x & (NSHARD - 1)) * CNT_STRIDE + slot], v);
 }
 
 // LDS size classes of k_interpret (bytes of tape per lane)
-// (a block of class S uses 64 x (S + 16) B of LDS for tapes; class 0 is sized
-// so that 5 blocks fit a CU's 160 KiB with the stacks and tables)
+// (a block of class S uses 64 x tape_stride(S) B of LDS for tapes; class 0 is
+// sized so that 7 blocks fit a CU's 160 KiB with its two lookup tables)
 #define CLASS0_SIZE 336
 #define CLASS1_SIZE 768
 #define CLASS2_SIZE 1536

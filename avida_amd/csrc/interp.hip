@@ -798,15 +798,31 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
         const int exe = wave_sum_i32(ne), cop = wave_sum_i32(nc);
         int okw = 0, rec = -1, len = 0, e0 = 0, e1 = 0, e2 = 0, e3 = 0, e4 = 0;   // edits: slip mut ins del uniform
         if (lane == L) {
-          bool ok = exe >= (int)(div * W.min_exe_lines) && cop >= (int)(child * W.min_copied_lines);
+          // The world parameters and phenotype arrays this block uses, loaded
+          // together and made opaque (OPQ): the asm stores below are
+          // scheduling barriers, and the compiler re-issued each invariant
+          // scalar load just before its use -- one load-to-use wait per field.
+          double p_min_exe = W.min_exe_lines, p_min_cop = W.min_copied_lines, p_req = W.required_bonus;
+          double p_mdb = W.merit_default_bonus, p_defb = W.default_bonus;
+          int p_inherit = W.inherit_merit, p_bmm = W.base_merit_method, p_bcm = W.base_const_merit;
+          double* g_merit = W.merit;
+          double* g_fitness = W.fitness;
+          int32_t* g_gest = W.gest_time;
+          int32_t* g_ccop = W.child_copied;
+          int32_t* g_exec = W.executed;
+          int32_t* g_ltask = W.last_task;
+          OPQ(p_min_exe); OPQ(p_min_cop); OPQ(p_req); OPQ(p_mdb); OPQ(p_defb);
+          OPQ(p_inherit); OPQ(p_bmm); OPQ(p_bcm);
+          OPQ(g_merit); OPQ(g_fitness); OPQ(g_gest); OPQ(g_ccop); OPQ(g_exec); OPQ(g_ltask);
+          bool ok = exe >= (int)(div * p_min_exe) && cop >= (int)(child * p_min_cop);
           double bon = bonus;
           if (ok) {  // cOrganism::Divide_CheckViable (main/cOrganism.cc:788-919)
-            if (bon < W.required_bonus) ok = false;
-            const double base0 = (double)calc_size_merit(W, blen, dcop, dexe);
+            if (bon < p_req) ok = false;
+            const double base0 = (double)size_merit(p_bmm, p_bcm, blen, dcop, dexe);
             double b0 = bon;
-            if (W.merit_default_bonus != 0.0) b0 = W.merit_default_bonus;
+            if (p_mdb != 0.0) b0 = p_mdb;
             double off_merit = __dmul_rn(base0, b0);
-            if (W.inherit_merit == 0) off_merit = base0;
+            if (p_inherit == 0) off_merit = base0;
             if (off_merit == 0.0) ok = false;
           }
           if (ok) {
@@ -814,30 +830,30 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
             dexe = exe;                                       // SetLinesExecuted
             const int nd = dnd + 1;
             // DivideReset / TestDivideReset (main/cPhenotype.cc:824-1000, :1064-1180)
-            const double base = (double)calc_size_merit(W, blen, dcop, exe);
-            if (W.merit_default_bonus != 0.0) bon = W.merit_default_bonus;
+            const double base = (double)size_merit(p_bmm, p_bcm, blen, dcop, exe);
+            if (p_mdb != 0.0) bon = p_mdb;
             double merit = __dmul_rn(base, bon);
-            if (W.inherit_merit == 0) merit = base;
+            if (p_inherit == 0) merit = base;
             const int gt = tu - gs;
             const double fit = __ddiv_rn(__dmul_rn(base, bon), (double)gt);
             // write-only phenotype fields go out now (fire and forget) rather
             // than being held in registers to the end of the slice
-            st_async_u64(W.merit + cell, (uint64_t)__double_as_longlong(merit));
-            st_async_u64(W.fitness + cell, (uint64_t)__double_as_longlong(fit));
-            st_async_u32(W.gest_time + cell, (uint32_t)gt);
-            st_async_u32(W.child_copied + cell, (uint32_t)cop);   // SetLinesCopied
-            st_async_u32(W.executed + cell, (uint32_t)exe);
+            st_async_u64(g_merit + cell, (uint64_t)__double_as_longlong(merit));
+            st_async_u64(g_fitness + cell, (uint64_t)__double_as_longlong(fit));
+            st_async_u32(g_gest + cell, (uint32_t)gt);
+            st_async_u32(g_ccop + cell, (uint32_t)cop);       // SetLinesCopied
+            st_async_u32(g_exec + cell, (uint32_t)exe);
             gs = tu;
             dnd = nd;
             const int gen = dgen + 1;
             dgen = gen;
             didv = true;
             errs = 0;
-            bonus = W.default_bonus;
+            bonus = p_defb;
             cyc = 0;
 #pragma unroll
             for (int q = 0; q < AVGPU_NUM_LOGIC_TASKS; q++)
-              st_async_u32(W.last_task + (int64_t)q * N + cell, (uint32_t)tc[q]);
+              st_async_u32(g_ltask + (int64_t)q * N + cell, (uint32_t)tc[q]);
             nzm = 0;
 #pragma unroll
             for (int i = 0; i < AVGPU_MAX_REACTIONS; i++) rc[i] = 0;
@@ -852,32 +868,39 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
               // mut, ins, del always draw; uniform only at a non-zero rate.
               // The offspring is this lane's child sites under up to 5 edits,
               // one fixed slot per kind (e0 .. e4, 0 = none) in the order applied.
-              if (draw_p(W.th_div_slip, W.p_div_slip)) {          // doSlipMutation :621-694
+              uint64_t t_slip = W.th_div_slip, t_mut = W.th_div_mut, t_ins = W.th_div_ins;
+              uint64_t t_del = W.th_div_del, t_uni = W.th_div_uni;
+              double q_slip = W.p_div_slip, q_mut = W.p_div_mut, q_ins = W.p_div_ins;
+              double q_del = W.p_div_del, q_uni = W.p_div_uni;
+              int g_max = W.max_genome, g_min = W.min_genome;
+              OPQ(t_slip); OPQ(t_mut); OPQ(t_ins); OPQ(t_del); OPQ(t_uni);
+              OPQ(q_slip); OPQ(q_mut); OPQ(q_ins); OPQ(q_del); OPQ(q_uni); OPQ(g_max); OPQ(g_min);
+              if (draw_p(t_slip, q_slip)) {          // doSlipMutation :621-694
                 const int from = (int)draw_below((uint32_t)len + 1u);
                 const int to = from == 0 ? (int)draw_below((uint32_t)len) : (int)draw_below((uint32_t)len + 1u);
                 e0 = edit_word(E_SLIP, from, to);
                 len += from - to;
               }
-              if (draw_p(W.th_div_mut, W.p_div_mut)) {
+              if (draw_p(t_mut, q_mut)) {
                 const int line = (int)draw_below((uint32_t)len);
                 e1 = edit_word(E_POINT, line, rand_code());
               }
-              if (draw_p(W.th_div_ins, W.p_div_ins) && len < W.max_genome) {
+              if (draw_p(t_ins, q_ins) && len < g_max) {
                 const int line = (int)draw_below((uint32_t)len + 1u);
                 e2 = edit_word(E_INS, line, rand_code());
                 len++;
               }
-              if (draw_p(W.th_div_del, W.p_div_del) && len > W.min_genome) {
+              if (draw_p(t_del, q_del) && len > g_min) {
                 e3 = edit_word(E_DEL, (int)draw_below((uint32_t)len), 0);
                 len--;
               }
-              if (W.th_div_uni && draw_p(W.th_div_uni, W.p_div_uni)) {   // doUniformMutation :572-595
+              if (t_uni && draw_p(t_uni, q_uni)) {   // doUniformMutation :572-595
                 const int mut = (int)draw_below((uint32_t)(2 * k_n_ops + 1));
                 if (mut < k_n_ops) {
                   e4 = edit_word(E_POINT, (int)draw_below((uint32_t)len), rcode[mut]);
                 } else if (mut == k_n_ops) {
-                  if (len != W.min_genome) { e4 = edit_word(E_DEL, (int)draw_below((uint32_t)len), 0); len--; }
-                } else if (len != W.max_genome) {
+                  if (len != g_min) { e4 = edit_word(E_DEL, (int)draw_below((uint32_t)len), 0); len--; }
+                } else if (len != g_max) {
                   e4 = edit_word(E_INS, (int)draw_below((uint32_t)len + 1u), rcode[mut - k_n_ops - 1]);
                   len++;
                 }
@@ -899,29 +922,49 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
               if (rec >= 0) {
                 uint32_t clo, chi;
                 derive_key(klo, khi, (uint32_t)nd, 0x1B873593U, clo, chi);
-                st_async_u32(W.b_parent + rec, (uint32_t)cell);
-                st_async_u32(W.b_seq + rec, (uint32_t)nd);
-                st_async_u32(W.b_len + rec, (uint32_t)len);
-                st_async_u32(W.b_len0 + rec, (uint32_t)child);   // k_apply_mutations edits the copy
-                st_async_u32(W.b_edit + rec, (uint32_t)e0);
-                st_async_u32(W.b_edit + W.rcap + rec, (uint32_t)e1);
-                st_async_u32(W.b_edit + 2 * W.rcap + rec, (uint32_t)e2);
-                st_async_u32(W.b_edit + 3 * W.rcap + rec, (uint32_t)e3);
-                st_async_u32(W.b_edit + 4 * W.rcap + rec, (uint32_t)e4);
-                st_async_u64(W.b_merit + rec, (uint64_t)__double_as_longlong(merit));
-                st_async_u64(W.b_fitness + rec, (uint64_t)__double_as_longlong(fit));
-                st_async_u32(W.b_gen + rec, (uint32_t)gen);
-                st_async_u32(W.b_ccopied + rec, (uint32_t)cop);
-                st_async_u32(W.b_exec + rec, (uint32_t)exe);
-                st_async_u32(W.b_gest + rec, (uint32_t)gt);
-                st_async_u32(W.b_rng + rec, clo);
-                st_async_u32(W.b_rng + W.rcap + rec, chi);
-                st_async_u32(W.b_rng + 2 * W.rcap + rec, 0u);
-                st_async_u8(W.b_state + rec, 0u);
-                st_async_u32(W.b_target + rec, 0xFFFFFFFFu);
+                // the record arrays, loaded together (see OPQ above)
+                int32_t* b_parent = W.b_parent;
+                uint32_t* b_seq = W.b_seq;
+                int32_t* b_len = W.b_len;
+                int32_t* b_len0 = W.b_len0;
+                int32_t* b_edit = W.b_edit;
+                double* b_merit = W.b_merit;
+                double* b_fitness = W.b_fitness;
+                int32_t* b_gen = W.b_gen;
+                int32_t* b_ccopied = W.b_ccopied;
+                int32_t* b_exec = W.b_exec;
+                int32_t* b_gest = W.b_gest;
+                uint32_t* b_rng = W.b_rng;
+                int8_t* b_state = W.b_state;
+                int32_t* b_target = W.b_target;
+                int32_t* b_ltask = W.b_ltask;
+                int64_t rcap = W.rcap;
+                OPQ(b_parent); OPQ(b_seq); OPQ(b_len); OPQ(b_len0); OPQ(b_edit); OPQ(b_merit);
+                OPQ(b_fitness); OPQ(b_gen); OPQ(b_ccopied); OPQ(b_exec); OPQ(b_gest); OPQ(b_rng);
+                OPQ(b_state); OPQ(b_target); OPQ(b_ltask); OPQ(rcap);
+                st_async_u32(b_parent + rec, (uint32_t)cell);
+                st_async_u32(b_seq + rec, (uint32_t)nd);
+                st_async_u32(b_len + rec, (uint32_t)len);
+                st_async_u32(b_len0 + rec, (uint32_t)child);   // k_apply_mutations edits the copy
+                st_async_u32(b_edit + rec, (uint32_t)e0);
+                st_async_u32(b_edit + rcap + rec, (uint32_t)e1);
+                st_async_u32(b_edit + 2 * rcap + rec, (uint32_t)e2);
+                st_async_u32(b_edit + 3 * rcap + rec, (uint32_t)e3);
+                st_async_u32(b_edit + 4 * rcap + rec, (uint32_t)e4);
+                st_async_u64(b_merit + rec, (uint64_t)__double_as_longlong(merit));
+                st_async_u64(b_fitness + rec, (uint64_t)__double_as_longlong(fit));
+                st_async_u32(b_gen + rec, (uint32_t)gen);
+                st_async_u32(b_ccopied + rec, (uint32_t)cop);
+                st_async_u32(b_exec + rec, (uint32_t)exe);
+                st_async_u32(b_gest + rec, (uint32_t)gt);
+                st_async_u32(b_rng + rec, clo);
+                st_async_u32(b_rng + rcap + rec, chi);
+                st_async_u32(b_rng + 2 * rcap + rec, 0u);
+                st_async_u8(b_state + rec, 0u);
+                st_async_u32(b_target + rec, 0xFFFFFFFFu);
 #pragma unroll
                 for (int q = 0; q < AVGPU_NUM_LOGIC_TASKS; q++)   // SetupOffspring copies them (:447)
-                  st_async_u32(W.b_ltask + (int64_t)q * W.rcap + rec, (uint32_t)tc[q]);
+                  st_async_u32(b_ltask + (int64_t)q * rcap + rec, (uint32_t)tc[q]);
               }
             }
 #pragma unroll

@@ -300,6 +300,18 @@ __device__ __forceinline__ void st_async_u32(void* p, uint32_t v) {
 __device__ __forceinline__ void st_async_u64(void* p, uint64_t v) {
   asm volatile("global_store_dwordx2 %0, %1, off\n\ts_waitcnt expcnt(0)" ::"v"(p), "v"(v));
 }
+// global loads on rarely taken paths that wait for their own data, so that
+// the compiler's wait bookkeeping sees no load outstanding after them
+__device__ __forceinline__ uint32_t ld_sync_u32(const void* p) {
+  uint32_t v;
+  asm volatile("global_load_dword %0, %1, off\n\ts_waitcnt vmcnt(0)" : "=v"(v) : "v"(p) : "memory");
+  return v;
+}
+__device__ __forceinline__ uint32_t ld_sync_u8(const void* p) {
+  uint32_t v;
+  asm volatile("global_load_ubyte %0, %1, off\n\ts_waitcnt vmcnt(0)" : "=v"(v) : "v"(p) : "memory");
+  return v;
+}
 __device__ __forceinline__ void st_async_u8(void* p, uint32_t v) {
   asm volatile("global_store_byte %0, %1, off\n\ts_waitcnt expcnt(0)" ::"v"(p), "v"(v));
 }

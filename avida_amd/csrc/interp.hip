@@ -138,16 +138,27 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
   // wait on vmcnt(0), i.e. for every store the wave still had in flight --
   // and reads the rest from global memory through uniform (scalar) loads
   constexpr bool GTAB = (S == CLASS0_SIZE);
-  const uint16_t* lut = reinterpret_cast<const uint16_t*>(tab);
+  // the two lookup tables are always in LDS; said so explicitly, or an access
+  // through a generic pointer is a flat load, whose wait also drains every
+  // outstanding global store of the wave
+  typedef const __attribute__((address_space(3))) uint16_t lds_u16_t;
+  typedef const __attribute__((address_space(3))) uint8_t lds_u8_t;
+  lds_u16_t* lut = (lds_u16_t*)(tab);
   const int32_t* rcum = GTAB ? W.rand_cum : reinterpret_cast<const int32_t*>(tab + 128);
   const uint8_t* rcode = GTAB ? W.rand_code : reinterpret_cast<const uint8_t*>(tab + 192);
-  const uint8_t* rlut = reinterpret_cast<const uint8_t*>(tab + (GTAB ? 128 : 208));
+  lds_u8_t* rlut = (lds_u8_t*)(tab + (GTAB ? 128 : 208));
   const int32_t* rtab = GTAB ? W.react_tab : reinterpret_cast<const int32_t*>(tab + 272);
   // per-task bonus factor / addend of the simple-environment path (16 + 16 doubles)
   const double* tmul = GTAB ? W.task_tab
                             : reinterpret_cast<const double*>(tab + 272 + AVGPU_MAX_REACTIONS * RT_STRIDE);
   const double* tadd = tmul + 16;
 
+  // class 0 reads the cumulative random-instruction weights and codes from
+  // global memory (rare paths) by loads that wait for themselves: a
+  // compiler-visible load there left an outstanding-load wait at the join
+  // with the LDS path, i.e. every copy mutation drained the wave's stores
+  auto tab_i32 = [&](const int32_t* p) -> int32_t { return GTAB ? (int32_t)ld_sync_u32(p) : *p; };
+  auto tab_u8 = [&](const uint8_t* p) -> uint32_t { return GTAB ? ld_sync_u8(p) : (uint32_t)*p; };
   const int lane = threadIdx.x;
   const int64_t N = W.n;
   int cell = -1;
@@ -342,8 +353,8 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
     const uint32_t r = draw_below((uint32_t)k_rand_total);
     if (k_rand_total <= 256) return rlut[r];
     int i = 0;
-    while (i < k_n_ops - 1 && rcum[i] <= (int32_t)r) i++;
-    return rcode[i];
+    while (i < k_n_ops - 1 && tab_i32(rcum + i) <= (int32_t)r) i++;
+    return (uint8_t)tab_u8(rcode + i);
   };
 
 #define GETREG(i) ((i) == 0 ? r0 : ((i) == 1 ? r1 : r2))
@@ -897,11 +908,11 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
               if (t_uni && draw_p(t_uni, q_uni)) {   // doUniformMutation :572-595
                 const int mut = (int)draw_below((uint32_t)(2 * k_n_ops + 1));
                 if (mut < k_n_ops) {
-                  e4 = edit_word(E_POINT, (int)draw_below((uint32_t)len), rcode[mut]);
+                  e4 = edit_word(E_POINT, (int)draw_below((uint32_t)len), (int)tab_u8(rcode + mut));
                 } else if (mut == k_n_ops) {
                   if (len != g_min) { e4 = edit_word(E_DEL, (int)draw_below((uint32_t)len), 0); len--; }
                 } else if (len != g_max) {
-                  e4 = edit_word(E_INS, (int)draw_below((uint32_t)len + 1u), rcode[mut - k_n_ops - 1]);
+                  e4 = edit_word(E_INS, (int)draw_below((uint32_t)len + 1u), (int)tab_u8(rcode + mut - k_n_ops - 1));
                   len++;
                 }
               }

@@ -120,7 +120,7 @@ int setup_world(avgpu_world* w, int64_t n, bool test_buffers) {
   A(b_gest, R); A(b_ltask, AVGPU_NUM_LOGIC_TASKS * R); A(b_rng, 3 * R); A(b_target, R); A(b_state, R);
   A(b_prio, R); A(b_genome, (size_t)R * TAPE_SLOT);
   // placement scratch with two ghost rows (strip tiles)
-  A(occ, n + 2 * c.world_x); A(claim, n + 2 * c.world_x); A(owner, n + 2 * c.world_x);
+  A(occ, n + 2 * c.world_x); A(claim, n + 2 * c.world_x); A(claim2, n); A(owner, n + 2 * c.world_x);
   if (test_buffers) {
     A(t_flags, (size_t)n * TAPE_SLOT); A(t_flags_len, n); A(t_child, (size_t)n * TAPE_SLOT);
     A(t_child_len, n);
@@ -633,12 +633,21 @@ int avgpu_update_run(avgpu_world* w, const double* dev_totals, avgpu_update_stat
 int avgpu_run_update(avgpu_world* w, avgpu_update_stats* out) {
   int rc = ready(w);
   if (rc < 0) return rc;
-  if (!w->use_global) {
-    launch_merit_total(w->W, w->stream, w->d_totals, w->d_totals + 8);
-    HIPCHK(hipGetLastError());
+  if (w->use_global) {                 // totals handed in (avgpu_update_totals / tiles)
+    w->use_global = false;
+    return avgpu_update_run(w, w->d_totals, out);
   }
-  w->use_global = false;
-  return avgpu_update_run(w, w->d_totals, out);
+  // total merit, allotment, class lists and the class-0 order: two launches
+  launch_world_begin(w->W, w->stream, w->d_totals, w->d_totals + 8, w->ev_fork, (uint32_t)w->update);
+  after_resources_begin(w);
+  HIPCHK(hipGetLastError());
+  rc = interpret(w, AVGPU_MODE_WORLD, 0, w->W.n, true);
+  if (rc < 0) return rc;
+  launch_world_post(w->W, w->stream, w->d_stats);
+  HIPCHK(hipGetLastError());
+  w->update++;
+  if (out) return avgpu_get_stats(w, out);
+  return 0;
 }
 
 int avgpu_run_updates(avgpu_world* w, int n, avgpu_update_stats* last) {

@@ -139,6 +139,7 @@ struct DevWorld {
   // placement scratch, n cells + 2 ghost rows (strip tiles, below)
   uint8_t* occ;       // [n + 2X]
   unsigned long long* claim; // [n + 2X]
+  unsigned long long* claim2; // [n] odd placement rounds of a single world (launch_world_post)
   int32_t* owner;     // [n + 2X]  record id, -1 none, REMOTE_OWNER(k) won by a halo birth in round k
   // test-CPU outputs
   uint8_t* t_flags;   // [n][TAPE_SLOT] executed flags snapshot ('+'/'-')
@@ -467,7 +468,12 @@ void launch_interpret_classes(const DevWorld& W, const DevWorld* dW, int mode, h
 // class-0 windows: k_allot's budgets sorted (descending) inside windows of
 // SORT_WIN cells, so that a wave's 64 organisms get similar time slices
 #define SORT_WIN 2048
+// k_allot_sort's buckets: budgets 0 .. SORT_BUCKETS-3 (larger ones share the
+// last of them), then one bucket for the window's cells that are not class 0
+#define SORT_BUCKETS 258
 bool class_timing_all();   // AVGPU_CLASS_TIMING (interp.hip)
+void launch_world_begin(const DevWorld& W, hipStream_t s, double* d_totals, double* d_scratch,
+                        hipEvent_t lists_ready, uint32_t update);
 void launch_world_pre(const DevWorld& W, hipStream_t s, const double* d_totals, hipEvent_t lists_ready,
                       uint32_t update);
 // allotment draw of organism (lo, hi) in update u (oracle allot_draw)

@@ -1224,13 +1224,15 @@ static int spill_lpw() {
   return v;
 }
 
-// timing events after every class (default) or after class 0 only
-// (AVGPU_CLASS_TIMING=0): each timed event record costs ~10 us of queue time
+// timing events around class 0 only (default) or after every class
+// (AVGPU_CLASS_TIMING=1, diagnostics): each timed event record costs ~10 us
+// of queue time, and the three spill-row launches sit on the update's
+// critical path
 bool class_timing_all() {
   static int v = -1;
   if (v < 0) {
     const char* e = getenv("AVGPU_CLASS_TIMING");
-    v = (e && atoi(e) == 0) ? 0 : 1;
+    v = (e && atoi(e) == 1) ? 1 : 0;
   }
   return v == 1;
 }

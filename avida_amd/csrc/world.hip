@@ -18,9 +18,10 @@ namespace {
 // k_interpret<CLASS0_SIZE> sweeps the cells densely.  Block-aggregated: one
 // global atomic per class and block (a per-wave atomic on three addresses
 // serialised ~16K waves in L2), lanes then write at block base + wave offset
-// + rank.  blockDim.x must be 256.
+// + rank.  blockDim.x must be 64 * WAVES.
+template <int WAVES = 4>
 __device__ __forceinline__ void enqueue_class(const DevWorld& W, int cell, bool want, int cls) {
-  __shared__ int s_pc[NUM_CLASSES][4], s_base[NUM_CLASSES];
+  __shared__ int s_pc[NUM_CLASSES][WAVES], s_base[NUM_CLASSES];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   unsigned long long masks[NUM_CLASSES];
   __syncthreads();                             // s_pc / s_base free (repeat calls)
@@ -33,7 +34,8 @@ __device__ __forceinline__ void enqueue_class(const DevWorld& W, int cell, bool 
   // waves take their offsets in wave order (deterministic list order)
   if (threadIdx.x > 0 && threadIdx.x < NUM_CLASSES) {
     const int k = threadIdx.x;
-    const int tot = s_pc[k][0] + s_pc[k][1] + s_pc[k][2] + s_pc[k][3];
+    int tot = 0;
+    for (int w = 0; w < WAVES; w++) tot += s_pc[k][w];
     s_base[k] = tot ? atomicAdd(&W.class_count[k], tot) : 0;
   }
   __syncthreads();
@@ -307,10 +309,19 @@ __global__ void k_classify_uniform(DevWorld W, int64_t first, int64_t count, con
 // (strip tiles hold whole 256-cell blocks, so the block partials of a tiled
 // world are the single world's partials; alive_d: alive counts as doubles
 // after the merits, the layout tiles exchange)
+__device__ __forceinline__ void reset_counts_block(const DevWorld& W) {
+  for (int i = threadIdx.x; i < NSHARD * CNT_STRIDE; i += blockDim.x) W.counters[i] = 0ull;
+  if (threadIdx.x < 2) W.b_count[threadIdx.x] = 0;
+  if (threadIdx.x < 8) W.class_count[threadIdx.x] = 0;
+}
+
+// reset: block 0 also zeroes the update's counters, birth-queue and class-list
+// lengths (k_reset_counts' work; the previous update's statistics have read them)
 __global__ __launch_bounds__(256) void k_merit_partial(DevWorld W, double* partial, int32_t* alive_partial,
-                                                       double* alive_d) {
+                                                       double* alive_d, int reset) {
   __shared__ double s[256];
   __shared__ int a[256];
+  if (reset && blockIdx.x == 0) reset_counts_block(W);
   const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const bool live = c < W.n && (W.ctl[c] & CTL_ALIVE);
   s[threadIdx.x] = live ? W.merit[c] : 0.0;
@@ -368,17 +379,16 @@ __global__ __launch_bounds__(256) void k_merit_final(const double* partial, cons
   }
 }
 
-// cScheduler restated (DESIGN.md "Scheduler"): lambda = UD * merit / total
-__global__ void k_allot(DevWorld W, const double* totals, uint32_t update) {
-  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const bool in = c < W.n;
-  bool want = false;
-  int cls = 0;
-  if (in) {
+// cScheduler restated (DESIGN.md "Scheduler"): lambda = UD * merit / total.
+// Writes the cell's budget and class tag; returns the budget.
+__device__ __forceinline__ int allot_cell(const DevWorld& W, int64_t c, double sum, double alive, uint32_t update,
+                                          bool& want, int& cls) {
+  want = false;
+  cls = 0;
+  {
     int b = 0;
     if (W.ctl[c] & CTL_ALIVE) {
-      const double sum = totals[0];
-      const int64_t ud = (int64_t)W.ave_time_slice * (int64_t)totals[1];
+      const int64_t ud = (int64_t)W.ave_time_slice * (int64_t)alive;
       if (W.slicing == AVGPU_SLICE_CONSTANT || !(sum > 0.0)) {
         b = W.ave_time_slice;
       } else {
@@ -405,10 +415,109 @@ __global__ void k_allot(DevWorld W, const double* totals, uint32_t update) {
     }
     W.budget[c] = b;
     W.aclass[c] = want ? (uint8_t)cls : (uint8_t)ACLASS_NONE;
+    return b;
   }
+}
+
+__global__ void k_allot(DevWorld W, const double* totals, uint32_t update) {
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  bool want = false;
+  int cls = 0;
+  if (c < W.n) allot_cell(W, c, totals[0], totals[1], update, want, cls);
   const unsigned long long m = __ballot(want);
   if ((threadIdx.x & 63) == 0 && m) count_add(W, CNT_SLICES, (unsigned long long)__popcll(m));
   enqueue_class(W, (int)c, want, cls);
+}
+
+// A single world's update start in one launch (k_merit_final + k_allot +
+// k_window_sort): one SORT_WIN window per block of 1024 threads, two cells
+// per thread.  Each block first recomputes the total merit from the block
+// partials of k_merit_partial in k_merit_final's fixed order (lane t sums
+// partials t, t+256, ..., then the pairwise tree), so every block holds the
+// same bits; block 0 stores them.  The window's class-0 cells are then
+// ordered by budget (descending) with a counting sort: which cell runs in
+// which wave changes no organism's result (per-organism streams, placement by
+// priority), it only groups similar slices, so the order inside a budget is
+// free (LDS atomics).
+__global__ __launch_bounds__(1024) void k_allot_sort(DevWorld W, const double* partial,
+                                                     const int32_t* alive_partial, int64_t nb,
+                                                     double* totals, uint32_t update) {
+  __shared__ double s_sum[256];
+  __shared__ long long s_cnt[256];
+  __shared__ int hist[SORT_BUCKETS];
+  const int tid = threadIdx.x;
+  if (tid < 256) {
+    double acc = 0.0;
+    long long cnt = 0;
+    for (int64_t b0 = tid; b0 < nb; b0 += 256 * 8) {
+      double v[8];
+      int a[8];
+#pragma unroll
+      for (int k = 0; k < 8; k++) {
+        const int64_t b = b0 + 256 * k;
+        v[k] = b < nb ? partial[b] : 0.0;
+        a[k] = b < nb ? alive_partial[b] : 0;
+      }
+#pragma unroll
+      for (int k = 0; k < 8; k++)
+        if (b0 + 256 * k < nb) { acc = __dadd_rn(acc, v[k]); cnt += a[k]; }
+    }
+    s_sum[tid] = acc;
+    s_cnt[tid] = cnt;
+  }
+  for (int i = tid; i < SORT_BUCKETS; i += 1024) hist[i] = 0;
+  __syncthreads();
+  for (int stride = 128; stride >= 1; stride >>= 1) {
+    if (tid < stride) {
+      s_sum[tid] = __dadd_rn(s_sum[tid], s_sum[tid + stride]);
+      s_cnt[tid] += s_cnt[tid + stride];
+    }
+    __syncthreads();
+  }
+  const double sum = s_sum[0], alive = (double)s_cnt[0];
+  if (blockIdx.x == 0 && tid == 0) { totals[0] = sum; totals[1] = alive; }
+  const int64_t base = (int64_t)blockIdx.x * SORT_WIN;
+  int bucket[2];
+  for (int h = 0; h < 2; h++) {
+    const int64_t c = base + h * 1024 + tid;
+    bool want = false;
+    int cls = 0, b = 0;
+    if (c < W.n) b = allot_cell(W, c, sum, alive, update, want, cls);
+    const unsigned long long m = __ballot(want);
+    if ((tid & 63) == 0 && m) count_add(W, CNT_SLICES, (unsigned long long)__popcll(m));
+    enqueue_class<16>(W, (int)c, want, cls);
+    bucket[h] = c >= W.n ? -1 : ((want && cls == 0) ? SORT_BUCKETS - 2 - min(b, SORT_BUCKETS - 2) : SORT_BUCKETS - 1);
+    if (bucket[h] >= 0) atomicAdd(&hist[bucket[h]], 1);
+  }
+  __syncthreads();
+  if (tid < 64) {                              // exclusive scan of the buckets by one wave
+    constexpr int PER = (SORT_BUCKETS + 63) / 64;
+    int loc[PER], t = 0;
+#pragma unroll
+    for (int k = 0; k < PER; k++) {
+      const int i = tid * PER + k;
+      loc[k] = i < SORT_BUCKETS ? hist[i] : 0;
+      t += loc[k];
+    }
+    int incl = t;
+    for (int off = 1; off < 64; off <<= 1) {
+      const int o = __shfl_up(incl, off);
+      if (tid >= off) incl += o;
+    }
+    int run = incl - t;
+#pragma unroll
+    for (int k = 0; k < PER; k++) {
+      const int i = tid * PER + k;
+      if (i < SORT_BUCKETS) hist[i] = run;
+      run += loc[k];
+    }
+  }
+  __syncthreads();
+  for (int h = 0; h < 2; h++) {
+    if (bucket[h] < 0) continue;
+    const int pos = atomicAdd(&hist[bucket[h]], 1);
+    W.order[base + pos] = (int32_t)(base + h * 1024 + tid);
+  }
 }
 
 // ---- budget-sorted class-0 windows ----
@@ -481,14 +590,27 @@ __device__ __forceinline__ int neighbours(const DevWorld& W, int cell, int* out)
   return n;
 }
 
+__device__ __forceinline__ void occ_init_cell(const DevWorld& W, int64_t c) {
+  W.occ[c] = (c < W.n && (W.ctl[c] & CTL_ALIVE)) ? 1 : 0;
+  W.owner[c] = -1;
+}
+
 __global__ void k_occ_init(DevWorld W) {
   const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t ext = W.n + (W.tiled ? 2 * (int64_t)W.world_x : 0);
-  if (c < ext) { W.occ[c] = (c < W.n && (W.ctl[c] & CTL_ALIVE)) ? 1 : 0; W.owner[c] = -1; }
+  if (c < ext) occ_init_cell(W, c);
 }
 
-__device__ __forceinline__ void place_pick_one(const DevWorld& W, int64_t i) {
+// claim / prev: this round's claim array and (single world) the previous
+// round's, whose entry at the record's last target is zeroed first -- the
+// rounds alternate between two arrays, so no clearing pass sits between them
+__device__ __forceinline__ void place_pick_one(const DevWorld& W, int64_t i, unsigned long long* claim,
+                                               unsigned long long* prev) {
   const int64_t r = rec_of(W, i);
+  if (prev) {
+    const int t0 = W.b_target[r];
+    if (t0 >= 0) prev[t0] = 0ull;
+  }
   if (W.b_state[r] != 0) return;
   const int parent = W.b_parent[r];
   int nbr[8];
@@ -512,16 +634,17 @@ __device__ __forceinline__ void place_pick_one(const DevWorld& W, int64_t i) {
   W.b_rng[2 * W.rcap + r] = ctr;
   W.b_target[r] = t;
   W.b_prio[r] = prio;
-  atomicMax(&W.claim[t], prio);
+  atomicMax(&claim[t], prio);
 }
 
 // which: 0 every target, 1 targets inside the tile, 2 ghost-row targets
-__device__ __forceinline__ void place_resolve_one(const DevWorld& W, int64_t i, int round, int which) {
+__device__ __forceinline__ void place_resolve_one(const DevWorld& W, int64_t i, int round, int which,
+                                                  const unsigned long long* claim) {
   const int64_t r = rec_of(W, i);
   if (W.b_state[r] != 0) return;
   const int t = W.b_target[r];
   if ((which == 1 && t >= W.n) || (which == 2 && t < W.n)) return;
-  if (W.claim[t] == W.b_prio[r]) {
+  if (claim[t] == W.b_prio[r]) {
     W.b_state[r] = (int8_t)(1 + round);
     W.occ[t] = 1;
     W.owner[t] = (int)r;
@@ -532,9 +655,11 @@ __device__ __forceinline__ void place_resolve_one(const DevWorld& W, int64_t i, 
 #define QUEUE_LOOP(i) \
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, _qn = queue_len(W); i < _qn; \
        i += (int64_t)gridDim.x * blockDim.x)
-__global__ void k_place_pick(DevWorld W) { QUEUE_LOOP(i) place_pick_one(W, i); }
-__global__ void k_place_resolve(DevWorld W, int round, int which) {
-  QUEUE_LOOP(i) place_resolve_one(W, i, round, which);
+__global__ void k_place_pick(DevWorld W, unsigned long long* claim, unsigned long long* prev) {
+  QUEUE_LOOP(i) place_pick_one(W, i, claim, prev);
+}
+__global__ void k_place_resolve(DevWorld W, int round, int which, const unsigned long long* claim) {
+  QUEUE_LOOP(i) place_resolve_one(W, i, round, which, claim);
 }
 __global__ void k_place_clear(DevWorld W) {
   QUEUE_LOOP(i) {
@@ -637,12 +762,20 @@ __device__ __forceinline__ int mut_source(int j, const int* e, bool nopc, int& v
   return src;
 }
 
-__global__ __launch_bounds__(64) void k_apply_mutations(DevWorld W) {
+// blocks [0, mblocks) apply the divide mutations; any further blocks
+// initialise the placement occupancy of the n cells (k_occ_init's work), so
+// that a single world's update needs one launch for both
+__global__ __launch_bounds__(64) void k_apply_mutations(DevWorld W, int mblocks) {
   __shared__ uint8_t child[TAPE_SLOT + 16];
+  if ((int)blockIdx.x >= mblocks) {
+    const int64_t nthr = (int64_t)(gridDim.x - mblocks) * 64;
+    for (int64_t c = (int64_t)(blockIdx.x - mblocks) * 64 + threadIdx.x; c < W.n; c += nthr) occ_init_cell(W, c);
+    return;
+  }
   const int nb = queue_len(W);
   const int lane = threadIdx.x;
   const bool nopc = W.slip_fill_mode == 4;
-  for (int64_t q = blockIdx.x; q < nb; q += gridDim.x) {
+  for (int64_t q = blockIdx.x; q < nb; q += mblocks) {
     const int64_t r = rec_of(W, q);
     int e[5];
 #pragma unroll
@@ -736,13 +869,16 @@ __device__ __forceinline__ void setup_child(const DevWorld& W, int64_t c, const 
 // pass, and the 21 stored fields fit 32 lanes): the winners of cells inside
 // the tile are activated; winners of ghost-row cells were shipped by
 // k_halo_pack.
-__global__ __launch_bounds__(64) void k_activate(DevWorld W) {
+// last: (single world) the claim array of the last placement round, zeroed
+// at each record's target for the next update
+__global__ __launch_bounds__(64) void k_activate(DevWorld W, unsigned long long* last) {
   const int nb = queue_len(W);
   const int lane = threadIdx.x & 31;
   unsigned long long born = 0, lost = 0;
   for (int64_t q = 2 * (int64_t)blockIdx.x + (threadIdx.x >> 5); q < nb; q += 2 * (int64_t)gridDim.x) {
     const int64_t i = rec_of(W, q);
     const int tgt = W.b_target[i];
+    if (last && lane == 0 && tgt >= 0) last[tgt] = 0ull;
     const bool won = W.b_state[i] > 0 && tgt >= 0 && W.owner[tgt] == (int)i;
     if (won && tgt >= W.n) continue;          // sent to the neighbouring tile
     if (!won) { lost++; continue; }
@@ -1015,17 +1151,28 @@ void launch_merit_total(const DevWorld& W, hipStream_t s, double* totals, double
   const int64_t nb = (W.n + 255) / 256;
   int32_t* alive_partial = reinterpret_cast<int32_t*>(scratch + nb);
   hipLaunchKernelGGL(k_merit_partial, dim3((unsigned)nb), dim3(256), 0, s, W, scratch, alive_partial,
-                     (double*)nullptr);
+                     (double*)nullptr, 0);
   hipLaunchKernelGGL(k_merit_final<false>, dim3(1), dim3(256), 0, s, scratch, alive_partial,
                      (const double*)nullptr, nb, 1, totals, 0);
 }
 
 // the update's counters, birth-queue and class-list lengths, zeroed by one
 // launch instead of three fill packets (~10 us each on the queue)
-__global__ __launch_bounds__(256) void k_reset_counts(DevWorld W) {
-  for (int i = threadIdx.x; i < NSHARD * CNT_STRIDE; i += 256) W.counters[i] = 0ull;
-  if (threadIdx.x < 2) W.b_count[threadIdx.x] = 0;
-  if (threadIdx.x < 8) W.class_count[threadIdx.x] = 0;
+__global__ __launch_bounds__(256) void k_reset_counts(DevWorld W) { reset_counts_block(W); }
+
+// single world: total merit, allotment, class lists and class-0 order in
+// two launches (k_merit_partial also zeroes the update's counters)
+void launch_world_begin(const DevWorld& W, hipStream_t s, double* totals, double* scratch,
+                        hipEvent_t lists_ready, uint32_t update) {
+  const int64_t nb = (W.n + 255) / 256;
+  int32_t* alive_partial = reinterpret_cast<int32_t*>(scratch + nb);
+  launch_resources_begin(W, s);   // ProcessPreUpdate + the update's first DoUpdates
+  hipLaunchKernelGGL(k_merit_partial, dim3((unsigned)nb), dim3(256), 0, s, W, scratch, alive_partial,
+                     (double*)nullptr, 1);
+  hipLaunchKernelGGL(k_allot_sort, dim3(nblk(W.n, SORT_WIN)), dim3(1024), 0, s, W, (const double*)scratch,
+                     (const int32_t*)alive_partial, nb, totals, update);
+  // the class lists are complete: the aux streams of the list classes start here
+  hipEventRecord(lists_ready, s);
 }
 
 void launch_world_pre(const DevWorld& W, hipStream_t s, const double* totals, hipEvent_t lists_ready,
@@ -1051,22 +1198,34 @@ static unsigned activate_grid(const DevWorld& W) { return (unsigned)std::min<int
 static unsigned place_grid(const DevWorld& W) { return (unsigned)std::min<int64_t>(nblk(W.rcap, 256), 2048); }
 
 static unsigned activate_grid(const DevWorld& W);
+static bool has_divide_mutations(const DevWorld& W) {
+  return (W.th_div_mut | W.th_div_ins | W.th_div_del | W.th_div_slip | W.th_div_uni) != 0;
+}
 static void launch_apply_mutations(const DevWorld& W, hipStream_t s) {
-  if (W.th_div_mut | W.th_div_ins | W.th_div_del | W.th_div_slip | W.th_div_uni)
-    hipLaunchKernelGGL(k_apply_mutations, dim3(activate_grid(W)), dim3(64), 0, s, W);
+  if (has_divide_mutations(W))
+    hipLaunchKernelGGL(k_apply_mutations, dim3(activate_grid(W)), dim3(64), 0, s, W, (int)activate_grid(W));
 }
 
+// Placement rounds alternate between the claim arrays claim / claim2 (round k
+// claims into array k & 1 after zeroing its records' round k-1 claims; the
+// last round's are zeroed by k_activate): no clearing launch per round.
 void launch_world_post(const DevWorld& W, hipStream_t s, double* stats) {
-  launch_apply_mutations(W, s);
+  if (has_divide_mutations(W)) {
+    const unsigned mb = activate_grid(W);
+    hipLaunchKernelGGL(k_apply_mutations, dim3(mb + 2048), dim3(64), 0, s, W, (int)mb);
+  } else {
+    hipLaunchKernelGGL(k_occ_init, dim3(nblk(W.n, 256)), dim3(256), 0, s, W);
+  }
   launch_resources_end(W, s);
   const unsigned bb = place_grid(W);
-  hipLaunchKernelGGL(k_occ_init, dim3(nblk(W.n, 256)), dim3(256), 0, s, W);
+  unsigned long long* buf[2] = {W.claim, W.claim2};
   for (int round = 0; round < 4; round++) {
-    hipLaunchKernelGGL(k_place_pick, dim3(bb), dim3(256), 0, s, W);
-    hipLaunchKernelGGL(k_place_resolve, dim3(bb), dim3(256), 0, s, W, round, 0);
-    hipLaunchKernelGGL(k_place_clear, dim3(bb), dim3(256), 0, s, W);
+    hipLaunchKernelGGL(k_place_pick, dim3(bb), dim3(256), 0, s, W, buf[round & 1],
+                       round ? buf[(round - 1) & 1] : (unsigned long long*)nullptr);
+    hipLaunchKernelGGL(k_place_resolve, dim3(bb), dim3(256), 0, s, W, round, 0,
+                       (const unsigned long long*)buf[round & 1]);
   }
-  hipLaunchKernelGGL(k_activate, dim3(activate_grid(W)), dim3(64), 0, s, W);
+  hipLaunchKernelGGL(k_activate, dim3(activate_grid(W)), dim3(64), 0, s, W, buf[1]);
   launch_stats(W, s, stats);
 }
 
@@ -1074,7 +1233,7 @@ void launch_world_post(const DevWorld& W, hipStream_t s, double* stats) {
 void launch_tile_partials(const DevWorld& W, hipStream_t s, double* out) {
   const int64_t nb = (W.n + 255) / 256;
   hipLaunchKernelGGL(k_merit_partial, dim3((unsigned)nb), dim3(256), 0, s, W, out, (int32_t*)nullptr,
-                     out + nb);
+                     out + nb, 0);
 }
 
 void launch_tile_totals(const DevWorld& W, hipStream_t s, const double* gathered, int ntiles,
@@ -1100,15 +1259,15 @@ void launch_tile_place(const DevWorld& W, hipStream_t s, int round, int phase) {
   const unsigned hb = nblk(2 * (int64_t)W.world_x, 256);
   if (phase == 0) {
     if (round == 0) hipLaunchKernelGGL(k_halo_import, dim3(hb), dim3(256), 0, s, W, 0, round);
-    hipLaunchKernelGGL(k_place_pick, dim3(bb), dim3(256), 0, s, W);
+    hipLaunchKernelGGL(k_place_pick, dim3(bb), dim3(256), 0, s, W, W.claim, (unsigned long long*)nullptr);
     hipLaunchKernelGGL(k_halo_export, dim3(hb), dim3(256), 0, s, W, 1);
   } else if (phase == 1) {
     hipLaunchKernelGGL(k_halo_import, dim3(hb), dim3(256), 0, s, W, 1, round);
-    hipLaunchKernelGGL(k_place_resolve, dim3(bb), dim3(256), 0, s, W, round, 1);
+    hipLaunchKernelGGL(k_place_resolve, dim3(bb), dim3(256), 0, s, W, round, 1, (const unsigned long long*)W.claim);
     hipLaunchKernelGGL(k_halo_export, dim3(hb), dim3(256), 0, s, W, 2);
   } else if (phase == 2) {
     hipLaunchKernelGGL(k_halo_import, dim3(hb), dim3(256), 0, s, W, 2, round);
-    hipLaunchKernelGGL(k_place_resolve, dim3(bb), dim3(256), 0, s, W, round, 2);
+    hipLaunchKernelGGL(k_place_resolve, dim3(bb), dim3(256), 0, s, W, round, 2, (const unsigned long long*)W.claim);
     hipLaunchKernelGGL(k_place_clear, dim3(bb), dim3(256), 0, s, W);
     hipLaunchKernelGGL(k_halo_clear, dim3(hb), dim3(256), 0, s, W);
   } else {
@@ -1118,7 +1277,7 @@ void launch_tile_place(const DevWorld& W, hipStream_t s, int round, int phase) {
 }
 
 void launch_tile_finish(const DevWorld& W, hipStream_t s, double* stats) {
-  hipLaunchKernelGGL(k_activate, dim3(activate_grid(W)), dim3(64), 0, s, W);
+  hipLaunchKernelGGL(k_activate, dim3(activate_grid(W)), dim3(64), 0, s, W, (unsigned long long*)nullptr);
   for (int d = 0; d < 2; d++)
     hipLaunchKernelGGL(k_activate_remote, dim3((unsigned)std::max(1, std::min(W.world_x, 4096))), dim3(64),
                        0, s, W, d);

@@ -209,9 +209,15 @@ avgpu_world* create_world(const avgpu_cfg* cfg, int device, int64_t n, bool test
   w->device = device;
   if (n <= 0) n = (int64_t)cfg->world_x * cfg->world_y;
   if (n <= 0 || n > (1ll << 30)) { delete w; fail(AVGPU_EINVAL, "bad cell count"); return nullptr; }
+  // The list classes' aux streams get the higher priority: their blocks
+  // become ready together with class 0's (both wait for k_allot_sort) and must
+  // take their CUs first -- a class-3 block needs a whole CU's LDS, which a
+  // CU full of class-0 blocks frees only when all of them have retired.
+  int prio_lo = 0, prio_hi = 0;
+  if (hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi) != hipSuccess) prio_lo = prio_hi = 0;
   if (hipStreamCreateWithFlags(&w->own_stream, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&w->aux_stream[0], hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&w->aux_stream[1], hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithPriority(&w->aux_stream[0], hipStreamNonBlocking, prio_hi) != hipSuccess ||
+      hipStreamCreateWithPriority(&w->aux_stream[1], hipStreamNonBlocking, prio_hi) != hipSuccess ||
       hipEventCreateWithFlags(&w->ev_fork, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&w->ev_join[0], hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&w->ev_join[1], hipEventDisableTiming) != hipSuccess ||

@@ -429,22 +429,16 @@ __global__ void k_allot(DevWorld W, const double* totals, uint32_t update) {
   enqueue_class(W, (int)c, want, cls);
 }
 
-// A single world's update start in one launch (k_merit_final + k_allot +
-// k_window_sort): one SORT_WIN window per block of 1024 threads, two cells
-// per thread.  Each block first recomputes the total merit from the block
-// partials of k_merit_partial in k_merit_final's fixed order (lane t sums
-// partials t, t+256, ..., then the pairwise tree), so every block holds the
-// same bits; block 0 stores them.  The window's class-0 cells are then
-// ordered by budget (descending) with a counting sort: which cell runs in
-// which wave changes no organism's result (per-organism streams, placement by
-// priority), it only groups similar slices, so the order inside a budget is
-// free (LDS atomics).
-__global__ __launch_bounds__(1024) void k_allot_sort(DevWorld W, const double* partial,
-                                                     const int32_t* alive_partial, int64_t nb,
-                                                     double* totals, uint32_t update) {
+// A single world's allotment with its total merit (k_merit_final + k_allot
+// in one launch): blocks of 1024 threads, two cells per thread.  Each block
+// first recomputes the total merit from the block partials of k_merit_partial
+// in k_merit_final's fixed order (lane t sums partials t, t+256, ..., then the
+// pairwise tree), so every block holds the same bits; block 0 stores them.
+__global__ __launch_bounds__(1024) void k_allot_total(DevWorld W, const double* partial,
+                                                      const int32_t* alive_partial, int64_t nb,
+                                                      double* totals, uint32_t update) {
   __shared__ double s_sum[256];
   __shared__ long long s_cnt[256];
-  __shared__ int hist[SORT_BUCKETS];
   const int tid = threadIdx.x;
   if (tid < 256) {
     double acc = 0.0;
@@ -465,7 +459,6 @@ __global__ __launch_bounds__(1024) void k_allot_sort(DevWorld W, const double* p
     s_sum[tid] = acc;
     s_cnt[tid] = cnt;
   }
-  for (int i = tid; i < SORT_BUCKETS; i += 1024) hist[i] = 0;
   __syncthreads();
   for (int stride = 128; stride >= 1; stride >>= 1) {
     if (tid < stride) {
@@ -476,18 +469,39 @@ __global__ __launch_bounds__(1024) void k_allot_sort(DevWorld W, const double* p
   }
   const double sum = s_sum[0], alive = (double)s_cnt[0];
   if (blockIdx.x == 0 && tid == 0) { totals[0] = sum; totals[1] = alive; }
-  const int64_t base = (int64_t)blockIdx.x * SORT_WIN;
-  int bucket[2];
   for (int h = 0; h < 2; h++) {
-    const int64_t c = base + h * 1024 + tid;
+    const int64_t c = (int64_t)blockIdx.x * 2048 + h * 1024 + tid;
     bool want = false;
-    int cls = 0, b = 0;
-    if (c < W.n) b = allot_cell(W, c, sum, alive, update, want, cls);
+    int cls = 0;
+    if (c < W.n) allot_cell(W, c, sum, alive, update, want, cls);
     const unsigned long long m = __ballot(want);
     if ((tid & 63) == 0 && m) count_add(W, CNT_SLICES, (unsigned long long)__popcll(m));
     enqueue_class<16>(W, (int)c, want, cls);
-    bucket[h] = c >= W.n ? -1 : ((want && cls == 0) ? SORT_BUCKETS - 2 - min(b, SORT_BUCKETS - 2) : SORT_BUCKETS - 1);
-    if (bucket[h] >= 0) atomicAdd(&hist[bucket[h]], 1);
+  }
+}
+
+// The window's class-0 cells ordered by budget (descending) with a counting
+// sort (k_window_sort's job, one SORT_WIN window per block): which cell runs
+// in which wave changes no organism's result (per-organism streams, placement
+// by priority), it only groups similar slices, so the order inside a budget
+// is free (LDS atomics).
+__global__ __launch_bounds__(1024) void k_window_count(DevWorld W) {
+  __shared__ int hist[SORT_BUCKETS];
+  const int tid = threadIdx.x;
+  const int64_t base = (int64_t)blockIdx.x * SORT_WIN;
+  for (int i = tid; i < SORT_BUCKETS; i += 1024) hist[i] = 0;
+  __syncthreads();
+  int bucket[2];
+  for (int h = 0; h < 2; h++) {
+    const int64_t c = base + h * 1024 + tid;
+    bucket[h] = -1;
+    if (c < W.n) {
+      // class-0 cells by k_allot's tag: the list classes on the aux streams
+      // rewrite budget / mem_size of their own cells while this kernel runs
+      const bool c0 = W.aclass[c] == 0;
+      bucket[h] = c0 ? SORT_BUCKETS - 2 - min(W.budget[c], SORT_BUCKETS - 2) : SORT_BUCKETS - 1;
+      atomicAdd(&hist[bucket[h]], 1);
+    }
   }
   __syncthreads();
   if (tid < 64) {                              // exclusive scan of the buckets by one wave
@@ -523,40 +537,7 @@ __global__ __launch_bounds__(1024) void k_allot_sort(DevWorld W, const double* p
 // ---- budget-sorted class-0 windows ----
 // A wave runs until its longest slice ends, so the class-0 interpreter takes
 // its 64 organisms from a window of SORT_WIN cells sorted by budget
-// (descending; ties in cell order).  Execution order does not change any
-// organism's result (per-organism RNG streams, placement by priority), only
-// how many lanes idle.  One 1024-thread block sorts one window in LDS
-// (bitonic network over keys budget << 11 | (2047 - index)).
-__global__ __launch_bounds__(1024) void k_window_sort(DevWorld W) {
-  __shared__ uint32_t key[SORT_WIN];
-  const int64_t base = (int64_t)blockIdx.x * SORT_WIN;
-  for (int i = threadIdx.x; i < SORT_WIN; i += 1024) {
-    const int64_t c = base + i;
-    uint32_t b = 0;
-    // class-0 cells by k_allot's tag: the list classes on the aux streams
-    // rewrite budget / mem_size of their own cells while this kernel runs
-    if (c < W.n && W.aclass[c] == 0) b = (uint32_t)min(W.budget[c], 0xFFFFF);
-    key[i] = (b << 11) | (uint32_t)(SORT_WIN - 1 - i);
-  }
-  __syncthreads();
-  for (int k = 2; k <= SORT_WIN; k <<= 1) {
-    for (int j = k >> 1; j > 0; j >>= 1) {
-      for (int i = threadIdx.x; i < SORT_WIN; i += 1024) {
-        const int l = i ^ j;
-        if (l > i) {
-          const uint32_t a = key[i], b = key[l];
-          const bool desc = (i & k) == 0;          // descending runs first
-          if (desc ? (a < b) : (a > b)) { key[i] = b; key[l] = a; }
-        }
-      }
-      __syncthreads();
-    }
-  }
-  for (int i = threadIdx.x; i < SORT_WIN; i += 1024) {
-    const int64_t c = base + (SORT_WIN - 1 - (int64_t)(key[i] & (SORT_WIN - 1)));
-    if (base + i < W.n) W.order[base + i] = (int32_t)c;
-  }
-}
+// (k_window_count above).
 
 // ---- birth placement (cPopulation::PositionOffspring restated) ----
 // neighbour k of cell in fixed order NW N NE W E SW S SE (tools/cTopology.h).
@@ -1161,7 +1142,7 @@ void launch_merit_total(const DevWorld& W, hipStream_t s, double* totals, double
 __global__ __launch_bounds__(256) void k_reset_counts(DevWorld W) { reset_counts_block(W); }
 
 // single world: total merit, allotment, class lists and class-0 order in
-// two launches (k_merit_partial also zeroes the update's counters)
+// three launches (k_merit_partial also zeroes the update's counters)
 void launch_world_begin(const DevWorld& W, hipStream_t s, double* totals, double* scratch,
                         hipEvent_t lists_ready, uint32_t update) {
   const int64_t nb = (W.n + 255) / 256;
@@ -1169,10 +1150,12 @@ void launch_world_begin(const DevWorld& W, hipStream_t s, double* totals, double
   launch_resources_begin(W, s);   // ProcessPreUpdate + the update's first DoUpdates
   hipLaunchKernelGGL(k_merit_partial, dim3((unsigned)nb), dim3(256), 0, s, W, scratch, alive_partial,
                      (double*)nullptr, 1);
-  hipLaunchKernelGGL(k_allot_sort, dim3(nblk(W.n, SORT_WIN)), dim3(1024), 0, s, W, (const double*)scratch,
+  hipLaunchKernelGGL(k_allot_total, dim3(nblk(W.n, 2048)), dim3(1024), 0, s, W, (const double*)scratch,
                      (const int32_t*)alive_partial, nb, totals, update);
-  // the class lists are complete: the aux streams of the list classes start here
+  // the class lists are complete: the aux streams of the list classes start
+  // here, beside the window sort, so that their blocks take CUs before class 0
   hipEventRecord(lists_ready, s);
+  hipLaunchKernelGGL(k_window_count, dim3(nblk(W.n, SORT_WIN)), dim3(1024), 0, s, W);
 }
 
 void launch_world_pre(const DevWorld& W, hipStream_t s, const double* totals, hipEvent_t lists_ready,
@@ -1183,7 +1166,7 @@ void launch_world_pre(const DevWorld& W, hipStream_t s, const double* totals, hi
   // the class lists are complete: the aux streams of the list classes start
   // here, beside the window sort (launch_interpret_classes)
   hipEventRecord(lists_ready, s);
-  hipLaunchKernelGGL(k_window_sort, dim3(nblk(W.n, SORT_WIN)), dim3(1024), 0, s, W);
+  hipLaunchKernelGGL(k_window_count, dim3(nblk(W.n, SORT_WIN)), dim3(1024), 0, s, W);
 }
 
 static void launch_stats(const DevWorld& W, hipStream_t s, double* stats) {

@@ -374,10 +374,13 @@ __device__ __forceinline__ uint64_t gk_tape(const uint8_t* t, int len) {
 }
 
 __device__ __forceinline__ int head_adjust(int pos, int size) {
-  if ((unsigned)pos < (unsigned)size) return pos;
-  if (pos < 0) return 0;
-  if (pos < 2 * size) return pos - size;
-  return pos % size;
+  // wave-uniform test first: the common case (every active lane in range)
+  // falls through without entering the divergent adjustment
+  const bool out = (unsigned)pos >= (unsigned)size;
+  if (__builtin_expect(__ballot(out) != 0ull, 0)) {
+    if (out) pos = pos < 0 ? 0 : (pos < 2 * size ? pos - size : pos % size);
+  }
+  return pos;
 }
 // head_adjust of a position known to lie in [0, size] (one past a valid site)
 __device__ __forceinline__ int head_wrap(int pos, int size) {

@@ -480,8 +480,12 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
         rl = 0;
       }
       // TestCopyMut: no draw at rate 0 (main/cMutationRates.h:112)
-      if (mode != AVGPU_MODE_TEST && k_th_copy_mut && draw_p(k_th_copy_mut, W.p_copy_mut))
-        v = rand_code();
+      // (the rare mutated copy behind a wave-uniform test, so that the
+      // common path falls through instead of branching around it)
+      const bool cmut = mode != AVGPU_MODE_TEST && k_th_copy_mut && draw_p(k_th_copy_mut, W.p_copy_mut);
+      if (__builtin_expect(__ballot(cmut) != 0ull, 0)) {
+        if (cmut) v = rand_code();
+      }
       // the write head's executed flag: as read, or just set if it is the IP
       const int wex = (wh == ip) ? TF_EXEC : (dst_byte & TF_EXEC);
       T[wh] = (uint8_t)(wex | TF_COPIED | v);

@@ -1176,7 +1176,14 @@ static void launch_stats(const DevWorld& W, hipStream_t s, double* stats) {
   hipLaunchKernelGGL(k_stats_final, dim3(NPART + 1), dim3(256), 0, s, W, part, nb, stats);
 }
 
-static unsigned activate_grid(const DevWorld& W) { return (unsigned)std::min<int64_t>(W.rcap, 32768); }
+static unsigned activate_grid(const DevWorld& W) {
+  static int cap = -1;
+  if (cap < 0) {
+    const char* e = getenv("AVGPU_ACT_GRID");
+    cap = e ? std::max(64, atoi(e)) : 32768;
+  }
+  return (unsigned)std::min<int64_t>(W.rcap, cap);
+}
 // placement kernels stride over the queue; 8 blocks of 256 per CU cover it
 static unsigned place_grid(const DevWorld& W) { return (unsigned)std::min<int64_t>(nblk(W.rcap, 256), 2048); }
 

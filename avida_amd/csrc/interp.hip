@@ -1207,11 +1207,17 @@ __global__ __launch_bounds__(64, (S == CLASS0_SIZE) ? 2 : 1) void k_interpret(co
     interpret_chunk<S, REC>(Wp, 0, mode, first, count, chunk, lds32, sorted, 0, 64);
     return;
   }
-  // list classes: grid-stride over the list (its length is known on device only)
-  const int lcount = Wp->class_count[row];
-  for (int64_t chunk = blockIdx.x; chunk * lpw < lcount; chunk += gridDim.x) {
-    interpret_chunk<S, REC>(Wp, cls, mode, first, count, chunk, lds32, false, row, lpw);
-    __syncthreads();
+  // list classes: grid-stride over the list (its length is known on device
+  // only); with cls < 0, rows row and row + 1 in one launch (their organisms
+  // fit this class's tape slots: classes 2 + 3 beside class 0, spill rows 5 + 6)
+  const int nrows = cls < 0 ? 2 : 1;
+  for (int r = row; r < row + nrows; r++) {
+    const int rc = cls >= 0 ? cls : (r <= 3 ? r : r - 3);
+    const int lcount = Wp->class_count[r];
+    for (int64_t chunk = blockIdx.x; chunk * lpw < lcount; chunk += gridDim.x) {
+      interpret_chunk<S, REC>(Wp, rc, mode, first, count, chunk, lds32, false, r, lpw);
+      __syncthreads();
+    }
   }
 }
 
@@ -1274,6 +1280,10 @@ static void launch_classes(const DevWorld& W, const DevWorld* dW, int mode, hipS
     if (k == 1) hipLaunchKernelGGL((k_interpret<CLASS1_SIZE, REC>), dim3(lb), dim3(64), 0, st, dW, 1, 1, mode, first, count, 0, 64);
     if (k == 2) hipLaunchKernelGGL((k_interpret<CLASS2_SIZE, REC>), dim3(lb_c2), dim3(64), 0, st, dW, 2, 2, mode, first, count, 0, 64);
     if (k == 3) hipLaunchKernelGGL((k_interpret<CLASS3_SIZE, REC>), dim3(lb_c3), dim3(64), 0, st, dW, 3, 3, mode, first, count, 0, 64);
+    // classes 2 + 3 in one launch of class 3's slots: both start at the fork,
+    // before class 0's blocks fill the CUs (a class-3 block launched behind
+    // class 2 waited ~0.5 ms for a CU with all of its LDS free)
+    if (k == 23) hipLaunchKernelGGL((k_interpret<CLASS3_SIZE, REC>), dim3(lb_c2 + lb_c3), dim3(64), 0, st, dW, -1, 2, mode, first, count, 0, 64);
   };
   // Two aux streams (class 1; classes 2 + 3, which are short): with the
   // world's stream that is three HIP streams, so they keep distinct hardware
@@ -1302,11 +1312,10 @@ static void launch_classes(const DevWorld& W, const DevWorld* dW, int mode, hipS
   const int slpw = spill_lpw();
   hipLaunchKernelGGL((k_interpret<CLASS1_SIZE, REC>), dim3(lb_small), dim3(64), 0, s, dW, 1, 4, mode, first, count, 0, slpw);
   if (after_class && tall) hipEventRecord(after_class[1], s);
-  hipLaunchKernelGGL((k_interpret<CLASS2_SIZE, REC>), dim3(std::min(lb_small, 64u)), dim3(64), 0, s, dW, 2, 5, mode, first, count, 0, slpw);
-  if (after_class && tall) hipEventRecord(after_class[2], s);
-  hipLaunchKernelGGL((k_interpret<CLASS3_SIZE, REC>), dim3(std::min(lb_small, 64u)), dim3(64), 0, s, dW, 3, 6, mode, first, count, 0, slpw);
-  if (after_class && tall) hipEventRecord(after_class[3], s);
-  if (launches) *launches += 7;
+  // spill rows 5 + 6 (beyond classes 1 / 2) in one launch of class 3's slots
+  hipLaunchKernelGGL((k_interpret<CLASS3_SIZE, REC>), dim3(std::min(lb_small, 64u)), dim3(64), 0, s, dW, -1, 5, mode, first, count, 0, slpw);
+  if (after_class && tall) { hipEventRecord(after_class[2], s); hipEventRecord(after_class[3], s); }
+  if (launches) *launches += 5;
 }
 
 // RECORDED streams launch the REC instantiations (device.h DevWorld::rec)

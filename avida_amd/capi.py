@@ -157,7 +157,7 @@ EXPORTED = [
     "avgpu_tile_begin", "avgpu_tile_place", "avgpu_tile_finish", "avgpu_tile_res_bytes",
     "avgpu_set_tile_res_buffers", "avgpu_tile_res_cons", "avgpu_tile_res_settle",
     "avgpu_last_step_insts", "avgpu_last_kernel_ms", "avgpu_kernel_times", "avgpu_counters",
-    "avgpu_state_digests", "avgpu_set_rng_mode",
+    "avgpu_state_digests", "avgpu_set_rng_mode", "avgpu_run_serial_updates",
 ]
 
 
@@ -292,6 +292,7 @@ def bind_common(lib, prefix):
                                    C.POINTER(AvgpuTestResult), C.c_char_p, C.c_int,
                                    C.POINTER(C.c_uint8)]),
         "run_update": (C.c_int, [V, C.POINTER(AvgpuUpdateStats)]),
+        "run_serial_updates": (C.c_int, [V, C.c_int, C.POINTER(AvgpuUpdateStats)]),
         "run_updates": (C.c_int, [V, C.c_int, C.POINTER(AvgpuUpdateStats)]),
         "last_step_insts": (C.c_int, [V, C.POINTER(C.c_int64)]),
         "set_global_totals": (C.c_int, [V, C.c_double, I64]),

@@ -1,0 +1,173 @@
+// births.h -- offspring helpers shared by the placement kernels (world.hip)
+// and the serial world (interp.hip): the neighbourhood, the divide-mutation
+// edits, and ActivateOrganism / SetupOffspring of a record into a cell.
+// Paths are relative to avida-core/source/ of the reference.
+#pragma once
+#include "device.h"
+
+namespace {
+
+// ---- birth placement (cPopulation::PositionOffspring restated) ----
+// neighbour k of cell in fixed order NW N NE W E SW S SE (tools/cTopology.h).
+// Tiled worlds map the rows above / below the strip to the ghost rows
+// [n, n+X) / [n+X, n+2X) of occ / claim / owner.
+__device__ __forceinline__ int neighbours(const DevWorld& W, int cell, int* out) {
+  const int X = W.world_x, R = W.rows;
+  const int x = cell % X, y = cell / X;
+  int n = 0;
+  for (int dy = -1; dy <= 1; dy++)
+    for (int dx = -1; dx <= 1; dx++) {
+      if (dx == 0 && dy == 0) continue;
+      int nx = x + dx, ny = y + dy;
+      if (W.geometry == 1) {
+        if (nx < 0 || nx >= X) continue;
+      } else {
+        nx = (nx + X) % X;
+      }
+      if (ny >= 0 && ny < R) {
+        out[n++] = ny * X + nx;
+      } else if (!W.tiled) {
+        if (W.geometry == 1) continue;
+        ny = (ny + R) % R;
+        out[n++] = ny * X + nx;
+      } else {
+        const int gy = W.row0 + ny;
+        if (W.geometry == 1 && (gy < 0 || gy >= W.global_rows)) continue;
+        out[n++] = (int)W.n + (ny < 0 ? 0 : X) + nx;
+      }
+    }
+  return n;
+}
+
+// Divide_DoMutations' edits (cpu/cHardwareBase.cc:296-569), drawn in the
+// interpreter in the reference's order and stored with the birth record
+// (interp.hip): one wave per queued offspring that has any rewrites its
+// genome -- site j of the mutated child is traced back through the edits
+// (last first) to a site of the unmutated child or to a value an edit wrote.
+// Runs before placement, so halo records and activation see final genomes.
+__device__ __forceinline__ int mut_source(int j, const int* e, bool nopc, int& val) {
+  int src = j;
+  val = -1;
+#pragma unroll
+  for (int k = 4; k >= 0; k--) {
+    const int ew = e[k];
+    if (ew == 0 || val >= 0) continue;
+    const int kind = ew & 7, a = (ew >> 3) & 0xFFF, b = (ew >> 15) & 0xFFF;
+    if (kind == 2) {                         // point (E_POINT)
+      if (src == a) val = b;
+    } else if (kind == 3) {                  // insertion (E_INS)
+      if (src == a) val = b; else if (src > a) src--;
+    } else if (kind == 4) {                  // deletion (E_DEL)
+      if (src >= a) src++;
+    } else {                                 // slip from a to b (E_SLIP)
+      if (nopc && a > b && src >= a && src < 2 * a - b) val = AVGPU_H_NOP_C;
+      else if (src >= a) src = b + (src - a);
+    }
+  }
+  return src;
+}
+
+// The divide-mutation edits of record r applied to its child genome by one
+// wave (k_apply_mutations; the serial world per birth): a no-op when the
+// record has none.  child: LDS scratch of TAPE_SLOT + 16 bytes.
+__device__ __forceinline__ void apply_edits_wave(const DevWorld& W, int64_t r, uint8_t* child) {
+  const int lane = threadIdx.x & 63;
+  const bool nopc = W.slip_fill_mode == 4;
+  int e[5];
+#pragma unroll
+  for (int k = 0; k < 5; k++) e[k] = W.b_edit[(int64_t)k * W.rcap + r];
+  if ((e[0] | e[1] | e[2] | e[3] | e[4]) == 0) return;   // wave-uniform
+  const int len0 = W.b_len0[r], len = W.b_len[r];
+  uint32_t* g32 = reinterpret_cast<uint32_t*>(W.b_genome + r * TAPE_SLOT);
+  uint32_t* c32 = reinterpret_cast<uint32_t*>(child);
+  for (int w = lane; (w << 2) < len0; w += 64) c32[w] = g32[w];
+  __syncthreads();
+  for (int w = lane; (w << 2) < len; w += 64) {
+    uint32_t word = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const int j = 4 * w + k;
+      int val;
+      const int src = mut_source(j, e, nopc, val);
+      const uint32_t v = val >= 0 ? (uint32_t)val : (uint32_t)child[src];
+      word |= (j < len ? v : 0u) << (8 * k);
+    }
+    g32[w] = word;
+  }
+  __syncthreads();
+}
+
+// ActivateOrganism (main/cPopulation.cc:1320-1340) + SetupOffspring
+// (main/cPhenotype.cc:349-420) of one offspring into cell c by one wave.  The
+// organism is marked CTL_FRESH: its zero / default fields (registers, heads,
+// stacks, IO buffers, counters, task and reaction counts, bonus) are implied
+// by the bit instead of stored -- they sit in ~90 SoA rows, one scattered
+// store each -- and its first slice writes them back.  What is stored here,
+// one field per lane: the genome, its length and the phenotype it inherits.
+struct Child {
+  int len, gen, ccopied, exec, gest;
+  double merit, fitness;
+  uint32_t lo, hi, ctr;
+  const int32_t* ltask;   // the parent's last task counts, ltask[q * lstride]
+  int64_t lstride;
+};
+// Run by a group of G lanes (G = 64: a wave, 32: a half-wave); `lane` is the
+// lane's index inside its group.
+template <int G>
+__device__ __forceinline__ void setup_child(const DevWorld& W, int64_t c, const Child& b,
+                                            const uint32_t* src, int lane) {
+  static_assert(G == 32 || G == 64, "group = wave or half-wave");
+  const int64_t N = W.n;
+  const int len = b.len;
+  uint32_t* dst = reinterpret_cast<uint32_t*>(W.tape + c * TAPE_SLOT);
+  uint64_t gsum = 0;
+  for (int w = lane; w < (len + 3) / 4; w += G) {
+    const uint32_t v = src[w];
+    dst[w] = v;
+    gsum += gk_word(v, w, len);
+  }
+  for (int off = G / 2; off > 0; off >>= 1) gsum += __shfl_xor(gsum, off);
+  if (lane == 0) W.gkey[c] = gk_final(gsum, len);
+  switch (lane) {
+    case 0: W.ctl[c] = CTL_ALIVE | CTL_FRESH; break;
+    case 1: W.mem_size[c] = len; break;
+    case 2: {
+      int mx = 0;
+      if (W.death_method > 0) { mx = W.age_limit; if (W.death_method == 2) mx *= len; if (mx < 1) mx = 1; }
+      W.max_exec[c] = mx;
+      break; }
+    case 3: W.birth_len[c] = len; break;
+    case 4: W.merit[c] = b.merit; break;
+    case 5: W.fitness[c] = b.fitness; break;
+    case 6: W.credit[c] = 0.0; break;
+    case 7: W.gest_time[c] = b.gest; break;
+    case 8: W.generation[c] = b.gen; break;
+    case 9: W.copied[c] = b.ccopied; break;
+    case 10: W.executed[c] = b.exec; break;
+    case 11: {
+      uint32_t ctr = b.ctr;
+      // cEnvironment::SetupInputs random (main/cEnvironment.cc:1268-1271)
+      W.inputs[c] = (15 << 24) + (int)rng_below(b.lo, b.hi, ctr, 1u << 24);
+      W.inputs[N + c] = (51 << 24) + (int)rng_below(b.lo, b.hi, ctr, 1u << 24);
+      W.inputs[2 * N + c] = (85 << 24) + (int)rng_below(b.lo, b.hi, ctr, 1u << 24);
+      W.rng[c] = b.lo; W.rng[N + c] = b.hi; W.rng[2 * N + c] = ctr;
+      if (W.rec_off) W.rec_off[c] = -1;         // offspring: counter streams
+      break; }
+    default:                                   // last_task_count = the parent's (:447)
+      if (lane >= 12 && lane < 12 + AVGPU_NUM_LOGIC_TASKS)
+        W.last_task[(int64_t)(lane - 12) * N + c] = b.ltask[(int64_t)(lane - 12) * b.lstride];
+      break;
+  }
+}
+
+// the phenotype record r hands its offspring
+__device__ __forceinline__ Child child_of_record(const DevWorld& W, int64_t i) {
+  Child b;
+  b.len = W.b_len[i]; b.gen = W.b_gen[i]; b.ccopied = W.b_ccopied[i]; b.exec = W.b_exec[i];
+  b.gest = W.b_gest[i]; b.merit = W.b_merit[i]; b.fitness = W.b_fitness[i];
+  b.lo = W.b_rng[i]; b.hi = W.b_rng[W.rcap + i]; b.ctr = W.b_rng[2 * W.rcap + i];
+  b.ltask = W.b_ltask + i; b.lstride = W.rcap;
+  return b;
+}
+
+}  // namespace

@@ -656,6 +656,40 @@ int avgpu_run_update(avgpu_world* w, avgpu_update_stats* out) {
   return 0;
 }
 
+int avgpu_run_serial_updates(avgpu_world* w, int n, avgpu_update_stats* last) {
+  int rc = ready(w);
+  if (rc < 0) return rc;
+  if (n < 0) return fail(AVGPU_EINVAL, "n_updates < 0");
+  DevWorld& W = w->W;
+  if (W.rec) return fail(AVGPU_EUNSUPPORTED, "the serial world draws from counter streams only");
+  if (W.tiled) return fail(AVGPU_EUNSUPPORTED, "the serial world runs single worlds, not strip tiles");
+  if (!W.stree) {
+    int64_t size = 1;
+    while (size < W.n) size <<= 1;
+    W.stree_size = size;
+    if ((rc = w->alloc(&W.stree, (size_t)(2 * size))) < 0) return rc;
+    if ((rc = w->alloc(&W.spec, (size_t)W.n)) < 0) return rc;
+    if ((rc = w->alloc(&W.grng, 3)) < 0) return rc;
+    // the scheduler's stream (oracle World::global_rng): keyed by the seed
+    uint32_t g[3] = {0, 0, 0};
+    const uint64_t seed = (uint64_t)w->cfg.seed;
+    derive_key((uint32_t)seed, (uint32_t)(seed >> 32), 0x5CEDu, 0xC0FFEEu, g[0], g[1]);
+    HIPCHK(hipMemcpyAsync(W.grng, g, sizeof(g), hipMemcpyHostToDevice, w->stream));
+  }
+  for (int u = 0; u < n; u++) {
+    launch_reset_counts(W, w->stream);
+    launch_resources_begin(W, w->stream);
+    after_resources_begin(w);
+    if ((rc = push_world(w)) < 0) return rc;
+    launch_serial_update(W, w->d_W, w->stream);
+    launch_serial_post(W, w->stream, w->d_stats);
+    HIPCHK(hipGetLastError());
+    w->update++;
+  }
+  if (last) return avgpu_get_stats(w, last);
+  return 0;
+}
+
 int avgpu_run_updates(avgpu_world* w, int n, avgpu_update_stats* last) {
   for (int i = 0; i < n; i++) {
     int rc = avgpu_run_update(w, nullptr);

@@ -205,6 +205,13 @@ struct DevWorld {
   const double* rec;
   int64_t rec_n;
   int64_t* rec_off;
+  // the serial world (avgpu_run_serial_updates; allocated on its first use):
+  // merit sum tree (stree[1] the root, leaves at stree_size + cell), each
+  // organism's speculative-step credit, the world's scheduler stream
+  double* stree;
+  int64_t stree_size;
+  int32_t* spec;     // [n]
+  uint32_t* grng;    // [3] lo hi ctr
   uint32_t seed_lo, seed_hi;
   // Strip tiles (multi-GPU, DESIGN.md "Multi-GPU"): this world holds rows
   // [row0, row0+rows) of a world_x x global_rows torus / grid.  When tiled,
@@ -319,7 +326,7 @@ __device__ __forceinline__ void st_async_u8(void* p, uint32_t v) {
 
 // ---------------------------------------------------------------------------
 // RNG spec: identical arithmetic to the oracle's Stream.
-__device__ __forceinline__ uint32_t lowbias32(uint32_t x) {
+__host__ __device__ __forceinline__ uint32_t lowbias32(uint32_t x) {
   x ^= x >> 16; x *= 0x7feb352dU; x ^= x >> 15; x *= 0x846ca68bU; x ^= x >> 16;
   return x;
 }
@@ -335,8 +342,8 @@ __device__ __forceinline__ uint32_t rng_below(uint32_t lo, uint32_t hi, uint32_t
 __device__ __forceinline__ bool rng_p(uint32_t lo, uint32_t hi, uint32_t& ctr, uint64_t th) {
   return (uint64_t)rng_next(lo, hi, ctr) < th;
 }
-__device__ __forceinline__ void derive_key(uint32_t a_lo, uint32_t a_hi, uint32_t x, uint32_t y,
-                                           uint32_t& lo, uint32_t& hi) {
+__host__ __device__ __forceinline__ void derive_key(uint32_t a_lo, uint32_t a_hi, uint32_t x, uint32_t y,
+                                                    uint32_t& lo, uint32_t& hi) {
   lo = lowbias32(lowbias32(x ^ a_lo) + y);
   hi = lowbias32(lowbias32(y ^ a_hi) + x + 0x632BE5ABU);
 }
@@ -463,6 +470,9 @@ struct LaunchInfo {
 // dW: device copy of W (avgpu_world::push_world)
 // aux (optional): three streams on which the classes 1..3 of k_allot's
 // lists run concurrently with class 0 (ev_fork / ev_join[3] order them)
+void launch_serial_update(const DevWorld& W, const DevWorld* dW, hipStream_t s);
+void launch_serial_post(const DevWorld& W, hipStream_t s, double* stats);
+void launch_reset_counts(const DevWorld& W, hipStream_t s);
 void launch_interpret_classes(const DevWorld& W, const DevWorld* dW, int mode, hipStream_t s,
                               int64_t first, int64_t count, int* launches,
                               hipEvent_t* after_class = nullptr, bool sorted = false,

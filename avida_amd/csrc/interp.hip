@@ -21,6 +21,7 @@
 #include <cstdlib>
 
 #include "device.h"
+#include "births.h"
 
 #pragma clang fp contract(off)
 
@@ -107,11 +108,17 @@ __host__ __device__ constexpr int tape_stride(int S) { return S == CLASS0_SIZE ?
 enum { E_SLIP = 1, E_POINT = 2, E_INS = 3, E_DEL = 4 };
 __device__ __forceinline__ int edit_word(int kind, int a, int b) { return kind | (a << 3) | (b << 15); }
 
+// serial = 1: one step of the serial world (k_serial_update): lane 0 runs
+// cell `first` for the reference's ProcessStepSpeculative -- one instruction,
+// then up to 32 more until the next one is IO or h-divide, an offspring is
+// born or the organism dies (main/cPopulation.cc:5740-5788) -- and leaves its
+// offspring in the cell's primary record (placed by the caller).  Returns,
+// for the running lane: instructions executed | divides << 16 | birth << 24.
 template <int S, bool REC>
-__device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp, int cls, int mode,
-                                                int64_t first, int64_t count, int64_t chunk,
-                                                uint32_t* __restrict__ lds32, bool sorted, int row,
-                                                int lpw) {
+__device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, int cls, int mode,
+                                               int64_t first, int64_t count, int64_t chunk,
+                                               uint32_t* __restrict__ lds32, bool sorted, int row,
+                                               int lpw, int serial = 0) {
   const DevWorld& W = *Wp;
   // per-lane tape stride: a whole number of 16-byte quads (16-B LDS-DMA).
   // The fetch / label / search windows read up to 16 bytes past a site; what
@@ -163,7 +170,12 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
   const int64_t N = W.n;
   int cell = -1;
   int M = 0;
-  if (cls == 0) {
+  if (serial) {
+    if (lane == 0) {
+      cell = (int)first;
+      M = W.mem_size[cell];
+    }
+  } else if (cls == 0) {
     // dense sweep: in cell order, or (world updates) through the
     // budget-sorted windows of k_window_count
     const int64_t c = sorted ? (chunk * 64 + lane < count ? (int64_t)W.order[chunk * 64 + lane] : first + count)
@@ -178,7 +190,7 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
     // list rows: lpw entries per wave (lanes >= lpw idle)
     const int lcount = W.class_count[row];
     const int64_t base = chunk * lpw;
-    if (base >= lcount) return;
+    if (base >= lcount) return 0;
     const int idx = (int)base + lane;
     if (lane < lpw && idx < lcount) {
       cell = W.class_list[(int64_t)row * N + idx];
@@ -186,7 +198,7 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
     }
   }
   const bool active = cell >= 0;
-  if (!__any(active)) return;
+  if (!__any(active)) return 0;
   const bool fresh = active && (W.ctl[cell] & CTL_FRESH);
 #ifdef AVGPU_PHASE_CLOCKS
   const uint64_t clk0 = __builtin_amdgcn_s_memtime();
@@ -273,6 +285,7 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
 #pragma unroll
   for (int q = 0; q < AVGPU_MAX_REACTIONS; q++) rc[q] = 0;
   bool didv = false, prim = false, prim0 = false;
+  int sbirth = 0;                // serial step: an offspring is in the primary record
   int ndrop = 0, noversize = 0;
   if (active) {
     // written at birth (setup_child) or by the previous slice
@@ -282,6 +295,7 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
     budget = W.budget[cell];
     prim = (budget & BUDGET_PRIM) != 0;   // a spilled slice already used its primary record
     budget &= ~BUDGET_PRIM;
+    if (serial) { budget = 33; prim = false; }
     inp0 = W.inputs[cell]; inp1 = W.inputs[N + cell]; inp2 = W.inputs[2 * N + cell];
     dexe = W.executed[cell]; dcop = W.copied[cell]; dgen = W.generation[cell];
     bonus = W.default_bonus;
@@ -412,7 +426,10 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
                         alloc <= (int)(cur * k_size_range) && cur <= (int)(alloc * k_size_range);
         if (ok && nsz > S) { spill = true; ip = ipa; }
       }
-    if (!spill) {
+      // serial step: the speculative run ends before IO / h-divide
+      // (cHardwareCPU::SingleProcess stall instructions, cpu/cHardwareCPU.cc:961-968)
+      if (serial && executed > 0 && (op == AVGPU_H_IO || op == AVGPU_H_H_DIVIDE)) stop = true;
+    if (!spill && !stop) {
     stepped = true;
     cyc++;                                                    // IncCPUCyclesUsed :929
     tu++;                                                     // IncTimeUsed :930
@@ -934,6 +951,7 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
               }
               prim = true;
               }
+              if (serial && rec >= 0) { sbirth = 1; stop = true; }   // births end the step
               if (rec >= 0) {
                 uint32_t clo, chi;
                 derive_key(klo, khi, (uint32_t)nd, 0x1B873593U, clo, chi);
@@ -1122,6 +1140,7 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
       *reinterpret_cast<uint4*>(W.tape + (int64_t)c * TAPE_SLOT + q * 16) = v;
     }
   }
+  if (serial) return executed | (divides << 16) | (sbirth << 24);
   // ---- primary birth records -> birth queue (wavefront ballot + prefix) ----
   {
     const bool fresh = prim && !prim0;
@@ -1187,9 +1206,10 @@ __device__ __forceinline__ void interpret_chunk(const DevWorld* __restrict__ Wp,
     }
   }
 #endif
+  return 0;
 }
 
-// class 0 must keep 2 waves per SIMD (its LDS admits 5 blocks per CU): the
+// class 0 must keep 2 waves per SIMD (its LDS admits 7 blocks per CU): the
 // second bound caps it at 256 registers (VGPR + AGPR)
 template <int S, bool REC>
 __global__ __launch_bounds__(64, (S == CLASS0_SIZE) ? 2 : 1) void k_interpret(const DevWorld* __restrict__ Wp, int cls, int row, int mode,
@@ -1218,6 +1238,152 @@ __global__ __launch_bounds__(64, (S == CLASS0_SIZE) ? 2 : 1) void k_interpret(co
       interpret_chunk<S, REC>(Wp, rc, mode, first, count, chunk, lds32, false, r, lpw);
       __syncthreads();
     }
+  }
+}
+
+// ---- the serial world (oracle orc_run_serial_updates) ----
+// Avida2Driver::Run's update with the reference's own schedule: UD = 30 x
+// living organisms picks, each a merit-weighted draw of one cell from the
+// scheduler's stream (cPopulation::ScheduleOrganism over a cWeightedIndex sum
+// tree, tools/cWeightedIndex.cc:49-115); a picked organism with speculative
+// credit spends one, otherwise it runs ProcessStepSpeculative
+// (main/cPopulation.cc:5740-5788, interpret_chunk serial step) and an
+// offspring is placed at once (ActivateOffspring / PositionOffspring,
+// main/cPopulation.cc:621-952, :5185-5414) into a neighbour drawn from the
+// same stream.  One wave per world: the picks are sequential by definition;
+// the wave shares the tree walks, genome copies and the interpreter's staging.
+
+// the sum tree's leaf for x: the binary descent of SerialSched::find, five
+// levels per round -- lanes fetch the 62 nodes below p in parallel, then the
+// walk runs in registers (same comparisons and subtractions, same order)
+__device__ __forceinline__ int64_t stree_find(const double* tree, int64_t size, double x) {
+  const int lane = threadIdx.x & 63;
+  int depth = 0;
+  for (int64_t s = size; s > 1; s >>= 1) depth++;
+  int64_t p = 1;
+  int dp = 0;
+  while (dp < depth) {
+    const int lv = min(5, depth - dp);
+    const int h = lane + 2;                     // subtree heap index of this lane's node
+    const int d = 31 - __clz(h);
+    double v = 0.0;
+    if (h < (2 << lv) && d <= lv) v = tree[(p << d) + (h - (1 << d))];
+    int k = 1;
+    for (int l = 0; l < lv; l++) {
+      const double left = __shfl(v, 2 * k - 2);
+      if (x < left) {
+        k = 2 * k;
+      } else {
+        x = __dsub_rn(x, left);
+        k = 2 * k + 1;
+      }
+    }
+    p = (p << lv) + (k - (1 << lv));
+    dp += lv;
+  }
+  return p - size;
+}
+
+// SerialSched::set: leaf = v, then every node on its path to the root as the
+// sum of its two children (left + right); the siblings are fetched at once
+__device__ __forceinline__ void stree_set(double* tree, int64_t size, int64_t i, double v) {
+  const int lane = threadIdx.x & 63;
+  int depth = 0;
+  for (int64_t s = size; s > 1; s >>= 1) depth++;
+  const int64_t leaf = size + i;
+  double sib = 0.0;
+  if (lane < depth) sib = tree[(leaf >> lane) ^ 1];
+  double cur = v, mine = 0.0;
+  for (int k = 0; k < depth; k++) {
+    const double sk = __shfl(sib, k);
+    cur = ((leaf >> k) & 1) ? __dadd_rn(sk, cur) : __dadd_rn(cur, sk);
+    if (lane == k) mine = cur;
+  }
+  if (lane == 0) tree[leaf] = v;
+  if (lane < depth) tree[leaf >> (lane + 1)] = mine;
+  __threadfence_block();
+}
+
+template <int S>
+__global__ __launch_bounds__(64, 1) void k_serial_update(const DevWorld* __restrict__ Wp) {
+  constexpr int TAB_WORDS = 128 + 64 + 16 + 64 + AVGPU_MAX_REACTIONS * RT_STRIDE + 64;
+  __shared__ __attribute__((aligned(16))) uint32_t lds32[64 * tape_stride(S) / 4 + 2 * AVGPU_STACK_SIZE * 64 + TAB_WORDS];
+  __shared__ __attribute__((aligned(16))) uint8_t child[TAPE_SLOT + 16];
+  const DevWorld& W = *Wp;
+  const int lane = threadIdx.x;
+  const int64_t n = W.n, size = W.stree_size;
+  double* tree = W.stree;
+  // the tree over this update's merits (every cell's SerialSched::set)
+  int na = 0;
+  for (int64_t c = lane; c < size; c += 64) {
+    const bool live = c < n && (W.ctl[c] & CTL_ALIVE);
+    tree[size + c] = live ? W.merit[c] : 0.0;
+    na += live ? 1 : 0;
+  }
+  __threadfence_block();
+  for (int64_t lo = size >> 1; lo >= 1; lo >>= 1) {
+    for (int64_t q = lo + lane; q < 2 * lo; q += 64) tree[q] = __dadd_rn(tree[2 * q], tree[2 * q + 1]);
+    __threadfence_block();
+  }
+  for (int off = 32; off > 0; off >>= 1) na += __shfl_xor(na, off);
+  const int64_t ud = (int64_t)W.ave_time_slice * na;   // cWorld::CalculateUpdateSize
+  const uint32_t glo = W.grng[0], ghi = W.grng[1];
+  uint32_t gct = W.grng[2];
+  unsigned long long picks = 0, deaths = 0, divides = 0, births = 0;
+  for (int64_t i = 0; i < ud; i++) {
+    const double tot = tree[1];
+    if (!(tot > 0.0)) break;
+    const double x = __dmul_rn(__dmul_rn((double)rng_next(glo, ghi, gct), 1.0 / 4294967296.0), tot);
+    const int64_t c = stree_find(tree, size, x);
+    if (!(W.ctl[c] & CTL_ALIVE)) continue;
+    picks++;
+    const int sp = W.spec[c];
+    if (sp > 0) {                                 // a speculatively executed step
+      if (lane == 0) W.spec[c] = sp - 1;
+      __threadfence_block();
+      continue;
+    }
+    const int r = __shfl(interpret_chunk<S, false>(Wp, 1, AVGPU_MODE_WORLD, c, 1, 0, lds32, false, 0, 64, 1), 0);
+    __builtin_amdgcn_s_waitcnt(0);              // the step's stores (some outside the compiler's view)
+    __threadfence_block();
+    if (lane == 0) W.spec[c] = (r & 0xFFFF) - 1;
+    divides += (r >> 16) & 0xFF;
+    const bool alive = (W.ctl[c] & CTL_ALIVE) != 0;
+    if (!alive) { stree_set(tree, size, c, 0.0); deaths++; }
+    if ((r >> 24) & 1) {
+      stree_set(tree, size, c, alive ? W.merit[c] : 0.0);   // AdjustSchedule(parent) :933
+      apply_edits_wave(W, c, child);
+      // PositionOffspring: an empty neighbour if PREFER_EMPTY finds one,
+      // else any neighbour (or the parent's cell)
+      int nb[8];
+      const int nn = neighbours(W, (int)c, nb);
+      int cand[9];
+      int nc = 0;
+      if (W.prefer_empty)
+        for (int k = 0; k < nn; k++) if (!(W.ctl[nb[k]] & CTL_ALIVE)) cand[nc++] = nb[k];
+      if (nc == 0 && W.birth_method != 3) {
+        for (int k = 0; k < nn; k++) cand[nc++] = nb[k];
+        if (W.allow_parent) cand[nc++] = (int)c;
+      }
+      if (nc > 0) {
+        const int t = cand[rng_below(glo, ghi, gct, (uint32_t)nc)];
+        const bool killed = (W.ctl[t] & CTL_ALIVE) != 0;
+        const Child b = child_of_record(W, c);
+        setup_child<64>(W, t, b, reinterpret_cast<const uint32_t*>(W.b_genome + c * TAPE_SLOT), lane);
+        __threadfence_block();
+        if (lane == 0) W.spec[t] = 0;
+        stree_set(tree, size, t, b.merit);
+        births++;
+        deaths += killed ? 1 : 0;
+      }
+    }
+  }
+  if (lane == 0) {
+    W.grng[2] = gct;
+    count_add(W, CNT_INSTS, picks);
+    if (deaths) count_add(W, CNT_DEATHS, deaths);
+    if (divides) count_add(W, CNT_DIVIDES, divides);
+    if (births) count_add(W, CNT_BIRTHS, births);
   }
 }
 
@@ -1326,4 +1492,10 @@ void launch_interpret_classes(const DevWorld& W, const DevWorld* dW, int mode, h
     launch_classes<true>(W, dW, mode, s, first, count, launches, after_class, sorted, aux, ev_fork, ev_join);
   else
     launch_classes<false>(W, dW, mode, s, first, count, launches, after_class, sorted, aux, ev_fork, ev_join);
+}
+
+// one serial-world update (launch_world_post's statistics follow it)
+void launch_serial_update(const DevWorld& W, const DevWorld* dW, hipStream_t s) {
+  (void)W;
+  hipLaunchKernelGGL((k_serial_update<CLASS3_SIZE>), dim3(1), dim3(64), 0, s, dW);
 }

@@ -338,6 +338,21 @@ int avgpu_step(avgpu_world* w, int64_t first_cell, int64_t count,
  * main/cPopulation.cc:5185-5414), statistics. out may be NULL (no host sync). */
 int avgpu_run_update(avgpu_world* w, avgpu_update_stats* out);
 int avgpu_run_updates(avgpu_world* w, int n_updates, avgpu_update_stats* last);
+/* The serial world: n_updates updates under the reference's own schedule
+ * (Avida2Driver::Run with cPopulation::ScheduleOrganism's merit-weighted pick
+ * of one organism per step, main/cPopulation.cc:5698-5788, a cWeightedIndex
+ * sum tree, tools/cWeightedIndex.cc:49-115; ProcessStepSpeculative's
+ * run-ahead of up to 32 instructions, stopping before IO / h-divide,
+ * :5740-5788; every offspring placed at once, ActivateOffspring /
+ * PositionOffspring :621-952, :5185-5414).  The picks and placements draw
+ * from one scheduler stream keyed by the world seed;
+ * organisms keep their own streams.  One wave steps the world, so this mode
+ * is for reference-semantics runs of small worlds (statistical parity,
+ * replay), not throughput.  Counter streams only (AVGPU_EUNSUPPORTED under
+ * RECORDED streams) and single worlds (not strip tiles).  Statistics as
+ * avgpu_run_update: insts_executed counts the update's picks of living
+ * organisms, as cStats does. */
+int avgpu_run_serial_updates(avgpu_world* w, int n_updates, avgpu_update_stats* last);
 /* The same update split around an external all-reduce (multi-GPU tiles,
  * cMultiProcessWorld::CalculateUpdateSize main/cMultiProcessWorld.cc:375-405):
  * avgpu_update_totals writes the tile's {sum merit, organisms} into the

@@ -199,6 +199,12 @@ class Backend:
         self._call("run_update", self.h, C.byref(st))
         return st
 
+    def run_serial_update(self):
+        """one update of the serial world (reference schedule, births at once)"""
+        st = capi.AvgpuUpdateStats()
+        self._call("run_serial_updates", self.h, 1, C.byref(st))
+        return st
+
 
 def recalculate(backend: Backend, genomes, generations=3):
     """cTestCPU::TestGenome viability recursion (cpu/cTestCPU.cc:233-326) over a batch.

@@ -242,8 +242,10 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
   // i % QUADS), so each global_load_lds_dwordx4 moves 1 KiB with per-lane
   // sources; all copies are in flight together and retired by one wait ----
   typedef __attribute__((address_space(3))) void* lds_ptr_t;
+  // a serial step runs lane 0 only: its quads are the image's first QUADS
+  const int qits = serial ? (QUADS + 63) / 64 : QUADS;
 #pragma unroll 1
-  for (int it = 0; it < QUADS; it++) {
+  for (int it = 0; it < qits; it++) {
     const int i = it * 64 + lane;
     const int j = i / QUADS, q = i - j * QUADS;
     const int c = __shfl(cell, j);
@@ -1130,7 +1132,7 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
   }
   // tapes back to HBM: the same lane-linear quad image, 16 B per lane
 #pragma unroll 2
-  for (int it = 0; it < QUADS; it++) {
+  for (int it = 0; it < qits; it++) {
     const int i = it * 64 + lane;
     const int j = i / QUADS, q = i - j * QUADS;
     const int c = __shfl(cell, j);

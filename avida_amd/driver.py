@@ -32,8 +32,12 @@ class ProductWorld:
     """The world on the GPU through libavida_gpu.so (same methods as the
     tests' oracle Backend, so the driver runs on either)."""
 
-    def __init__(self, cfg, iset, env, ncells=0, device=0):
+    def __init__(self, cfg, iset, env, ncells=0, device=0, serial=False):
         self.lib, self.p = capi.load_product(), "avgpu_"
+        # serial=True: every update under the reference's own schedule
+        # (avgpu_run_serial_updates: per-step merit-weighted picks, births at
+        # once) instead of the batch update
+        self.serial = serial
         self.h = self.lib.avgpu_create(C.byref(cfg), device, ncells)
         if not self.h:
             raise RuntimeError(self.lib.avgpu_last_error().decode())
@@ -64,7 +68,10 @@ class ProductWorld:
 
     def run_update(self):
         st = capi.AvgpuUpdateStats()
-        self._call("run_update", self.h, C.byref(st))
+        if self.serial:
+            self._call("run_serial_updates", self.h, 1, C.byref(st))
+        else:
+            self._call("run_update", self.h, C.byref(st))
         return st
 
     def kill(self, cell):
@@ -242,8 +249,12 @@ def main(argv=None):
     ap.add_argument("-d", "--data", default="data")
     ap.add_argument("-u", "--max-updates", type=int, default=None)
     ap.add_argument("-s", "--seed", type=int, default=None)
+    ap.add_argument("--serial", action="store_true",
+                    help="the reference's own per-step schedule (avgpu_run_serial_updates) "
+                         "instead of the batch update")
     a = ap.parse_args(argv)
-    d = Driver(a.config, a.data, seed=a.seed)
+    mk = (lambda cfg, iset, env: ProductWorld(cfg, iset, env, serial=True)) if a.serial else None
+    d = Driver(a.config, a.data, make_world=mk, seed=a.seed)
     last = d.run(a.max_updates)
     print(f"ran updates 0..{last}", file=sys.stderr)
     d.world.close()

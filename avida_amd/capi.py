@@ -157,7 +157,7 @@ EXPORTED = [
     "avgpu_tile_begin", "avgpu_tile_place", "avgpu_tile_finish", "avgpu_tile_res_bytes",
     "avgpu_set_tile_res_buffers", "avgpu_tile_res_cons", "avgpu_tile_res_settle",
     "avgpu_last_step_insts", "avgpu_last_kernel_ms", "avgpu_kernel_times", "avgpu_counters",
-    "avgpu_state_digests", "avgpu_set_rng_mode", "avgpu_run_serial_updates",
+    "avgpu_state_digests", "avgpu_set_rng_mode", "avgpu_run_serial_updates", "avgpu_set_timing",
 ]
 
 
@@ -353,6 +353,7 @@ def load_product(path=None):
     lib.avgpu_last_kernel_ms.argtypes = [C.c_void_p, C.POINTER(C.c_double),
                                          C.POINTER(C.c_int64)]
     lib.avgpu_kernel_times.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_int64)]
+    lib.avgpu_set_timing.argtypes = [C.c_void_p, C.c_int]
     lib.avgpu_counters.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_int64), C.c_int]
     lib.avgpu_update_totals.argtypes = [C.c_void_p, C.c_void_p]
     lib.avgpu_update_run.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(AvgpuUpdateStats)]

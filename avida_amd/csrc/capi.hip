@@ -47,6 +47,9 @@ struct avgpu_world {
   static const int RING = 512;
   hipEvent_t ring[RING][NUM_CLASSES + 1] = {};
   int ring_head = 0, ring_count = 0;
+  // avgpu_set_timing: bracket every time_every-th interpretation (0: none)
+  int time_every = 1;
+  int64_t interp_calls = 0;
   double acc_ms = 0.0;
   double acc_class_ms[NUM_CLASSES] = {};
   int64_t acc_phases = 0;
@@ -359,13 +362,17 @@ int interpret(avgpu_world* w, int mode, int64_t first, int64_t count, bool sorte
   }
   int rc = drain_ring(w, avgpu_world::RING - 1);
   if (rc < 0) return rc;
+  const bool timed = w->time_every > 0 && (w->interp_calls++ % w->time_every) == 0;
   const int i = w->ring_head;
-  HIPCHK(hipEventRecord(w->ring[i][0], w->stream));
-  launch_interpret_classes(w->W, w->d_W, mode, w->stream, first, count, &launches, &w->ring[i][1], sorted,
+  if (timed) HIPCHK(hipEventRecord(w->ring[i][0], w->stream));
+  launch_interpret_classes(w->W, w->d_W, mode, w->stream, first, count, &launches,
+                           timed ? &w->ring[i][1] : nullptr, sorted,
                            sorted ? w->aux_stream : nullptr, w->ev_fork, w->ev_join);
   HIPCHK(hipGetLastError());
-  w->ring_head = (i + 1) % avgpu_world::RING;
-  w->ring_count++;
+  if (timed) {
+    w->ring_head = (i + 1) % avgpu_world::RING;
+    w->ring_count++;
+  }
   w->last_launches = launches;
   return 0;
 }
@@ -1283,6 +1290,13 @@ int avgpu_last_kernel_ms(avgpu_world* w, double* ms, int64_t* launches) {
   w->acc_ms = 0.0;
   w->acc_phases = 0;
   for (int k = 0; k < NUM_CLASSES; k++) w->acc_class_ms[k] = 0.0;
+  return 0;
+}
+
+int avgpu_set_timing(avgpu_world* w, int every) {
+  if (!w || every < 0) return fail(AVGPU_EINVAL, "every < 0");
+  w->time_every = every;
+  w->interp_calls = 0;
   return 0;
 }
 

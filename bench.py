@@ -244,6 +244,8 @@ def main():
                     help="untimed updates that age the seeded population before the warmup "
                          "(its organisms start in lock step; ~10 gestations spread them out)")
     ap.add_argument("--seed", type=int, default=101)
+    ap.add_argument("--time-every", type=int, default=1,
+                    help="bracket every k-th update's class-0 launch with HIP events (roofline timing)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--env", choices=["logic9", "resources"], default="logic9",
@@ -290,6 +292,8 @@ def main():
     h, cfg, n, tile = build_world(lib, capi, files, golden, args.side, args.seed, local, rank, world,
                                   on_tile, args.env)
     strips = tiles.StripWorld([tile], tiles.DistTransport(dist)) if tile else None
+
+    capi.check(lib, lib.avgpu_set_timing(h, args.time_every))
 
     def update():
         if strips:
@@ -379,8 +383,10 @@ def main():
     # slices * 2 * 224 B + tape sites staged in and written back * 1.25 B,
     # over its HIP-event-timed average duration on the world's stream.
     c0_ms = cms[0] / nph
-    c0_slices = d[capi.CNT_C0_SLICES] / nph
-    c0_sites = d[capi.CNT_C0_SITES] / nph
+    # counters run over every update of the timed region (one class-0 launch
+    # each); the events only over every time_every-th
+    c0_slices = d[capi.CNT_C0_SLICES] / args.steps
+    c0_sites = d[capi.CNT_C0_SITES] / args.steps
     bytes_per_launch = 2.0 * STATE_BYTES * c0_slices + SITE_BYTES * c0_sites
     achieved = bytes_per_launch / (c0_ms * 1e-3) / 1e9 if c0_ms > 0 else 0.0
     traffic, traffic_src, issue = None, None, None
@@ -391,7 +397,7 @@ def main():
             traffic = pmc["hbm_bytes_per_launch"]
             traffic_src = pmc["source"]
             issue = issue_roofline(pmc["counters_per_dispatch"], c0_ms,
-                                   d[capi.CNT_INSTS] / nph * c0_slices / max(1.0, d[capi.CNT_SLICES] / nph))
+                                   d[capi.CNT_INSTS] / args.steps * c0_slices / max(1.0, d[capi.CNT_SLICES] / args.steps))
     out = {
         "metric": METRIC,
         "value": value,
@@ -438,6 +444,8 @@ def main():
             "traffic_source": traffic_src,
             "kernel": "k_interpret<336> (LDS size class 0)",
             "kernel_ms": c0_ms,
+            "timed_launches": int(phases.value),
+            "time_every": args.time_every,
             "bytes_per_launch": bytes_per_launch,
             "slices_per_launch": c0_slices,
             "mean_sites_per_slice": c0_sites / max(1.0, 2.0 * c0_slices),

@@ -531,10 +531,14 @@ int avgpu_last_step_insts(avgpu_world* w, int64_t* insts);
  * every k_interpret launch sequence) accumulated since the previous call:
  * total milliseconds and number of interpret phases; resets the accumulator. */
 int avgpu_last_kernel_ms(avgpu_world* w, double* ms, int64_t* launches);
-/* The same accumulators split by interpreter size class (k_interpret<384>,
- * <768>, <1536>, <2048>): class_ms[4] milliseconds and the number of interpret
- * phases since the previous call; resets them (and avgpu_last_kernel_ms's). */
+/* The same accumulators split by interpreter size class (k_interpret<336>,
+ * <768>, <1536>, <2048>): class_ms[4] milliseconds and the number of timed
+ * interpret phases since the previous call; resets them (and
+ * avgpu_last_kernel_ms's). */
 int avgpu_kernel_times(avgpu_world* w, double* class_ms, int64_t* phases);
+/* Bracket only every `every`-th interpret phase with the timing events (each
+ * event record costs ~10 us of queue time); 0 = none, default 1. */
+int avgpu_set_timing(avgpu_world* w, int every);
 
 /* Device event counters (no reference equivalent: measurement only).
  * cumulative = 0: the last update (or avgpu_step); 1: summed over every

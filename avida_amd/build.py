@@ -43,5 +43,27 @@ def build(force: bool = False, verbose: bool = False, clocks: bool = False) -> s
     return out
 
 
+# the C++ host driver of strip-tiled worlds (RCCL between ranks)
+HOST_SRC = os.path.join(HERE, "host", "strips.cc")
+HOST_OUT = os.path.join(HERE, "bin", "avgpu_strips")
+
+
+def build_host(force: bool = False, verbose: bool = False) -> str:
+    lib = build(force=False, verbose=verbose)
+    if not force and os.path.exists(HOST_OUT) and \
+            os.path.getmtime(HOST_OUT) > max(os.path.getmtime(HOST_SRC), os.path.getmtime(lib)):
+        return HOST_OUT
+    os.makedirs(os.path.dirname(HOST_OUT), exist_ok=True)
+    cmd = [HIPCC, "-O2", "-std=c++17", "-Wno-unused-result", "-I", os.path.join(ROOT, "include"),
+           "-o", HOST_OUT + ".tmp", HOST_SRC, "-L", HERE, "-lavida_gpu", "-lrccl",
+           "-Wl,-rpath,$ORIGIN/..", "-Wl,-rpath,/opt/rocm/lib"]
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.run(cmd, check=True)
+    os.replace(HOST_OUT + ".tmp", HOST_OUT)
+    return HOST_OUT
+
+
 if __name__ == "__main__":
     build(force="--force" in sys.argv, verbose=True, clocks="--clocks" in sys.argv)
+    build_host(force="--force" in sys.argv, verbose=True)

@@ -114,12 +114,16 @@ __device__ __forceinline__ int edit_word(int kind, int a, int b) { return kind |
 // born or the organism dies (main/cPopulation.cc:5740-5788) -- and leaves its
 // offspring in the cell's primary record (placed by the caller).  Returns,
 // for the running lane: instructions executed | divides << 16 | birth << 24.
-template <int S, bool REC>
-__device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, int cls, int mode,
+// C0W: the class-0 sweep of a world update, with the class and the mode known
+// at compile time -- the test-CPU and list-row code drops out of the hot loop
+template <int S, bool REC, bool C0W = false>
+__device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, int cls_arg, int mode_arg,
                                                int64_t first, int64_t count, int64_t chunk,
                                                uint32_t* __restrict__ lds32, bool sorted, int row,
                                                int lpw, int serial = 0) {
   const DevWorld& W = *Wp;
+  const int cls = C0W ? 0 : cls_arg;
+  const int mode = C0W ? (int)AVGPU_MODE_WORLD : mode_arg;
   // per-lane tape stride: a whole number of 16-byte quads (16-B LDS-DMA).
   // The fetch / label / search windows read up to 16 bytes past a site; what
   // they read beyond the organism's memory is masked off.  Classes 1-3 keep a
@@ -1213,7 +1217,7 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
 
 // class 0 must keep 2 waves per SIMD (its LDS admits 7 blocks per CU): the
 // second bound caps it at 256 registers (VGPR + AGPR)
-template <int S, bool REC>
+template <int S, bool REC, bool C0W = false>
 __global__ __launch_bounds__(64, (S == CLASS0_SIZE) ? 2 : 1) void k_interpret(const DevWorld* __restrict__ Wp, int cls, int row, int mode,
                                                   int64_t first, int64_t count, int sorted, int lpw) {
   constexpr int TAB_WORDS = 128 + 64 + 16 + 64 + AVGPU_MAX_REACTIONS * RT_STRIDE + 64;
@@ -1226,9 +1230,10 @@ __global__ __launch_bounds__(64, (S == CLASS0_SIZE) ? 2 : 1) void k_interpret(co
     // dealt to the 8 XCDs round robin), so its state lines meet in one L2
     int64_t chunk = blockIdx.x;
     if (sorted && (gridDim.x & 7) == 0) chunk = (int64_t)(blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
-    interpret_chunk<S, REC>(Wp, 0, mode, first, count, chunk, lds32, sorted, 0, 64);
+    interpret_chunk<S, REC, C0W>(Wp, 0, mode, first, count, chunk, lds32, sorted, 0, 64);
     return;
   }
+  if (C0W) return;
   // list classes: grid-stride over the list (its length is known on device
   // only); with cls < 0, rows row and row + 1 in one launch (their organisms
   // fit this class's tape slots: classes 2 + 3 beside class 0, spill rows 5 + 6)
@@ -1468,7 +1473,10 @@ static void launch_classes(const DevWorld& W, const DevWorld* dW, int mode, hipS
     list(3, aux[1]);
     for (int k = 0; k < 2; k++) hipEventRecord(ev_join[k], aux[k]);
   }
-  hipLaunchKernelGGL((k_interpret<CLASS0_SIZE, REC>), dim3(blocks), dim3(64), 0, s, dW, 0, 0, mode, first, count, srt, 64);
+  if (mode == AVGPU_MODE_WORLD)
+    hipLaunchKernelGGL((k_interpret<CLASS0_SIZE, REC, true>), dim3(blocks), dim3(64), 0, s, dW, 0, 0, mode, first, count, srt, 64);
+  else
+    hipLaunchKernelGGL((k_interpret<CLASS0_SIZE, REC>), dim3(blocks), dim3(64), 0, s, dW, 0, 0, mode, first, count, srt, 64);
   if (after_class) hipEventRecord(after_class[0], s);
   if (aux) {
     for (int k = 0; k < 2; k++) hipStreamWaitEvent(s, ev_join[k], 0);

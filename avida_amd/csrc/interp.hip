@@ -115,8 +115,10 @@ __device__ __forceinline__ int edit_word(int kind, int a, int b) { return kind |
 // offspring in the cell's primary record (placed by the caller).  Returns,
 // for the running lane: instructions executed | divides << 16 | birth << 24.
 // C0W: the class-0 sweep of a world update, with the class and the mode known
-// at compile time -- the test-CPU and list-row code drops out of the hot loop
-template <int S, bool REC, bool C0W = false>
+// at compile time -- the test-CPU and list-row code drops out of the hot loop;
+// SIMPLE: the environment's reactions are the simple form (env_simple) with
+// no finite resource, so the general reaction path drops out as well
+template <int S, bool REC, bool C0W = false, bool SIMPLE = false>
 __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, int cls_arg, int mode_arg,
                                                int64_t first, int64_t count, int64_t chunk,
                                                uint32_t* __restrict__ lds32, bool sorted, int row,
@@ -364,9 +366,9 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
     if (REC && rbase) { const uint32_t v = (uint32_t)(rd() * (double)n); return v < n ? v : n - 1u; }
     return rng_below(klo, khi, kct, n);
   };
-  const int k_env_simple = W.env_simple, k_max_label_exe = W.max_label_exe;
+  const int k_env_simple = SIMPLE ? 1 : W.env_simple, k_max_label_exe = W.max_label_exe;
   const int k_env_resources = W.env_resources;
-  const uint32_t k_env_res_mask = W.env_res_mask;
+  const uint32_t k_env_res_mask = SIMPLE ? 0u : W.env_res_mask;
   const uint32_t k_env_react_mask = W.env_react_mask, k_env_once_mask = W.env_once_mask;
   // cInstSet::GetRandomInst (cpu/cInstSet.cc:83-88) from the LDS tables
   auto rand_code = [&]() -> uint8_t {
@@ -399,6 +401,7 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
   int pop = -1, pr = 0;                                       // parked op, its register
   const uint32_t* T32 = reinterpret_cast<const uint32_t*>(T);
   const int slow_batch = W.slow_batch;
+
   while (true) {
     const bool run = alive && budget > 0 && !stop && !spill && pop < 0;
     if (!__any(run || pop >= 0)) break;                       // wave-uniform loop
@@ -411,11 +414,11 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
     if (run) {
       // ---- SingleProcess (cpu/cHardwareCPU.cc:908-1058) ----
       const int ipa = head_adjust(ip, M);                     // ip.Adjust() :952
-      // fetch window: sites ipa .. ipa+4 in two independent word reads
-      const uint64_t fwin = ((uint64_t)T32[(ipa >> 2) + 1] << 32) | (uint64_t)T32[ipa >> 2];
-      // h-copy's two sites, read with the fetch (one LDS round trip per
-      // iteration instead of two); used only if the op is h-copy
+      // fetch window: sites ipa .. ipa+4 in two independent word reads, and
+      // h-copy's two sites read with it (one LDS round trip per iteration
+      // instead of two; used only if the op is h-copy)
       const int rha = head_adjust(rh, M), wha = head_adjust(wh, M);
+      const uint64_t fwin = ((uint64_t)T32[(ipa >> 2) + 1] << 32) | (uint64_t)T32[ipa >> 2];
       const int src_byte = T[rha], dst_byte = T[wha];
       const uint32_t fsh = (uint32_t)(ipa & 3) * 8u;
       const int cur_byte = (int)((fwin >> fsh) & 0xFFu);
@@ -1217,7 +1220,7 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
 
 // class 0 must keep 2 waves per SIMD (its LDS admits 7 blocks per CU): the
 // second bound caps it at 256 registers (VGPR + AGPR)
-template <int S, bool REC, bool C0W = false>
+template <int S, bool REC, bool C0W = false, bool SIMPLE = false>
 __global__ __launch_bounds__(64, (S == CLASS0_SIZE) ? 2 : 1) void k_interpret(const DevWorld* __restrict__ Wp, int cls, int row, int mode,
                                                   int64_t first, int64_t count, int sorted, int lpw) {
   constexpr int TAB_WORDS = 128 + 64 + 16 + 64 + AVGPU_MAX_REACTIONS * RT_STRIDE + 64;
@@ -1230,7 +1233,7 @@ __global__ __launch_bounds__(64, (S == CLASS0_SIZE) ? 2 : 1) void k_interpret(co
     // dealt to the 8 XCDs round robin), so its state lines meet in one L2
     int64_t chunk = blockIdx.x;
     if (sorted && (gridDim.x & 7) == 0) chunk = (int64_t)(blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
-    interpret_chunk<S, REC, C0W>(Wp, 0, mode, first, count, chunk, lds32, sorted, 0, 64);
+    interpret_chunk<S, REC, C0W, SIMPLE>(Wp, 0, mode, first, count, chunk, lds32, sorted, 0, 64);
     return;
   }
   if (C0W) return;
@@ -1473,7 +1476,9 @@ static void launch_classes(const DevWorld& W, const DevWorld* dW, int mode, hipS
     list(3, aux[1]);
     for (int k = 0; k < 2; k++) hipEventRecord(ev_join[k], aux[k]);
   }
-  if (mode == AVGPU_MODE_WORLD)
+  if (mode == AVGPU_MODE_WORLD && W.env_simple && W.env_res_mask == 0u)
+    hipLaunchKernelGGL((k_interpret<CLASS0_SIZE, REC, true, true>), dim3(blocks), dim3(64), 0, s, dW, 0, 0, mode, first, count, srt, 64);
+  else if (mode == AVGPU_MODE_WORLD)
     hipLaunchKernelGGL((k_interpret<CLASS0_SIZE, REC, true>), dim3(blocks), dim3(64), 0, s, dW, 0, 0, mode, first, count, srt, 64);
   else
     hipLaunchKernelGGL((k_interpret<CLASS0_SIZE, REC>), dim3(blocks), dim3(64), 0, s, dW, 0, 0, mode, first, count, srt, 64);

@@ -117,8 +117,10 @@ __device__ __forceinline__ int edit_word(int kind, int a, int b) { return kind |
 // C0W: the class-0 sweep of a world update, with the class and the mode known
 // at compile time -- the test-CPU and list-row code drops out of the hot loop;
 // SIMPLE: the environment's reactions are the simple form (env_simple) with
-// no finite resource, so the general reaction path drops out as well
-template <int S, bool REC, bool C0W = false, bool SIMPLE = false>
+// no finite resource, so the general reaction path drops out as well; DEF:
+// the allocation, divide and merit knobs at the reference's defaults
+// (def_knobs, capi.hip), so their other branches drop out
+template <int S, bool REC, bool C0W = false, bool SIMPLE = false, bool DEF = false>
 __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, int cls_arg, int mode_arg,
                                                int64_t first, int64_t count, int64_t chunk,
                                                uint32_t* __restrict__ lds32, bool sorted, int row,
@@ -339,7 +341,7 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
   // world scalars the loop uses, read once: through the descriptor pointer
   // each use was an s_load + lgkmcnt wait inside the loop
   const double k_size_range = W.size_range;
-  const int k_require_allocate = W.require_allocate, k_alloc_method = W.alloc_method;
+  const int k_require_allocate = DEF ? 1 : W.require_allocate, k_alloc_method = DEF ? 0 : W.alloc_method;
   const uint64_t k_th_copy_mut = W.th_copy_mut;
   const int k_rand_total = W.rand_total, k_n_ops = W.n_ops, k_n_react = W.n_react;
   // RECORDED streams (include/avida_gpu.h "random streams"): the organism's
@@ -366,7 +368,7 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
     if (REC && rbase) { const uint32_t v = (uint32_t)(rd() * (double)n); return v < n ? v : n - 1u; }
     return rng_below(klo, khi, kct, n);
   };
-  const int k_env_simple = SIMPLE ? 1 : W.env_simple, k_max_label_exe = W.max_label_exe;
+  const int k_env_simple = SIMPLE ? 1 : W.env_simple, k_max_label_exe = DEF ? 1 : W.max_label_exe;
   const int k_env_resources = W.env_resources;
   const uint32_t k_env_res_mask = SIMPLE ? 0u : W.env_res_mask;
   const uint32_t k_env_react_mask = W.env_react_mask, k_env_once_mask = W.env_once_mask;
@@ -720,8 +722,8 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
         const int min_size = max(AVGPU_MIN_GENOME, (int)(blen / k_size_range));
         const int max_size = min(AVGPU_MAX_GENOME, (int)(blen * k_size_range));
         bool ok = child >= min_size && child <= max_size && div >= min_size && div <= max_size;
-        if (ok && W.cfg_min_genome && (child < W.cfg_min_genome || div < W.cfg_min_genome)) ok = false;
-        if (ok && W.cfg_max_genome && (child > W.cfg_max_genome || div > W.cfg_max_genome)) ok = false;
+        if (!DEF && ok && W.cfg_min_genome && (child < W.cfg_min_genome || div < W.cfg_min_genome)) ok = false;
+        if (!DEF && ok && W.cfg_max_genome && (child > W.cfg_max_genome || div > W.cfg_max_genome)) ok = false;
         if (ok) { rq = RQ_DIVIDE; qa = div; qb = child; }
         CKC(4);
         break; }
@@ -844,16 +846,17 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
           // scheduling barriers, and the compiler re-issued each invariant
           // scalar load just before its use -- one load-to-use wait per field.
           double p_min_exe = W.min_exe_lines, p_min_cop = W.min_copied_lines, p_req = W.required_bonus;
-          double p_mdb = W.merit_default_bonus, p_defb = W.default_bonus;
-          int p_inherit = W.inherit_merit, p_bmm = W.base_merit_method, p_bcm = W.base_const_merit;
+          double p_mdb = DEF ? 0.0 : W.merit_default_bonus, p_defb = W.default_bonus;
+          int p_inherit = DEF ? 1 : W.inherit_merit, p_bmm = DEF ? 4 : W.base_merit_method;
+          int p_bcm = W.base_const_merit;
           double* g_merit = W.merit;
           double* g_fitness = W.fitness;
           int32_t* g_gest = W.gest_time;
           int32_t* g_ccop = W.child_copied;
           int32_t* g_exec = W.executed;
           int32_t* g_ltask = W.last_task;
-          OPQ(p_min_exe); OPQ(p_min_cop); OPQ(p_req); OPQ(p_mdb); OPQ(p_defb);
-          OPQ(p_inherit); OPQ(p_bmm); OPQ(p_bcm);
+          OPQ(p_min_exe); OPQ(p_min_cop); OPQ(p_req); OPQ(p_defb); OPQ(p_bcm);
+          if (!DEF) { OPQ(p_mdb); OPQ(p_inherit); OPQ(p_bmm); }
           OPQ(g_merit); OPQ(g_fitness); OPQ(g_gest); OPQ(g_ccop); OPQ(g_exec); OPQ(g_ltask);
           bool ok = exe >= (int)(div * p_min_exe) && cop >= (int)(child * p_min_cop);
           double bon = bonus;
@@ -910,11 +913,12 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
               // The offspring is this lane's child sites under up to 5 edits,
               // one fixed slot per kind (e0 .. e4, 0 = none) in the order applied.
               uint64_t t_slip = W.th_div_slip, t_mut = W.th_div_mut, t_ins = W.th_div_ins;
-              uint64_t t_del = W.th_div_del, t_uni = W.th_div_uni;
+              uint64_t t_del = W.th_div_del, t_uni = DEF ? 0ull : W.th_div_uni;
               double q_slip = W.p_div_slip, q_mut = W.p_div_mut, q_ins = W.p_div_ins;
               double q_del = W.p_div_del, q_uni = W.p_div_uni;
               int g_max = W.max_genome, g_min = W.min_genome;
-              OPQ(t_slip); OPQ(t_mut); OPQ(t_ins); OPQ(t_del); OPQ(t_uni);
+              OPQ(t_slip); OPQ(t_mut); OPQ(t_ins); OPQ(t_del);
+              if (!DEF) OPQ(t_uni);
               OPQ(q_slip); OPQ(q_mut); OPQ(q_ins); OPQ(q_del); OPQ(q_uni); OPQ(g_max); OPQ(g_min);
               if (draw_p(t_slip, q_slip)) {          // doSlipMutation :621-694
                 const int from = (int)draw_below((uint32_t)len + 1u);
@@ -1220,7 +1224,7 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
 
 // class 0 must keep 2 waves per SIMD (its LDS admits 7 blocks per CU): the
 // second bound caps it at 256 registers (VGPR + AGPR)
-template <int S, bool REC, bool C0W = false, bool SIMPLE = false>
+template <int S, bool REC, bool C0W = false, bool SIMPLE = false, bool DEF = false>
 __global__ __launch_bounds__(64, (S == CLASS0_SIZE) ? 2 : 1) void k_interpret(const DevWorld* __restrict__ Wp, int cls, int row, int mode,
                                                   int64_t first, int64_t count, int sorted, int lpw) {
   constexpr int TAB_WORDS = 128 + 64 + 16 + 64 + AVGPU_MAX_REACTIONS * RT_STRIDE + 64;
@@ -1233,7 +1237,7 @@ __global__ __launch_bounds__(64, (S == CLASS0_SIZE) ? 2 : 1) void k_interpret(co
     // dealt to the 8 XCDs round robin), so its state lines meet in one L2
     int64_t chunk = blockIdx.x;
     if (sorted && (gridDim.x & 7) == 0) chunk = (int64_t)(blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
-    interpret_chunk<S, REC, C0W, SIMPLE>(Wp, 0, mode, first, count, chunk, lds32, sorted, 0, 64);
+    interpret_chunk<S, REC, C0W, SIMPLE, DEF>(Wp, 0, mode, first, count, chunk, lds32, sorted, 0, 64);
     return;
   }
   if (C0W) return;
@@ -1423,6 +1427,14 @@ bool class_timing_all() {
   return v == 1;
 }
 
+// the knobs the DEF instantiation fixes, at the reference's defaults
+// (avgpu_cfg_defaults; main/cAvidaConfig.h)
+static bool def_knobs(const DevWorld& W) {
+  return W.alloc_method != 2 && W.require_allocate == 1 && W.max_label_exe == 1 && W.cfg_min_genome == 0 &&
+         W.cfg_max_genome == 0 && W.merit_default_bonus == 0.0 && W.inherit_merit == 1 &&
+         W.base_merit_method == 4 && W.th_div_uni == 0;
+}
+
 template <bool REC>
 static void launch_classes(const DevWorld& W, const DevWorld* dW, int mode, hipStream_t s,
                            int64_t first, int64_t count, int* launches, hipEvent_t* after_class,
@@ -1476,7 +1488,9 @@ static void launch_classes(const DevWorld& W, const DevWorld* dW, int mode, hipS
     list(3, aux[1]);
     for (int k = 0; k < 2; k++) hipEventRecord(ev_join[k], aux[k]);
   }
-  if (mode == AVGPU_MODE_WORLD && W.env_simple && W.env_res_mask == 0u)
+  if (mode == AVGPU_MODE_WORLD && W.env_simple && W.env_res_mask == 0u && def_knobs(W))
+    hipLaunchKernelGGL((k_interpret<CLASS0_SIZE, REC, true, true, true>), dim3(blocks), dim3(64), 0, s, dW, 0, 0, mode, first, count, srt, 64);
+  else if (mode == AVGPU_MODE_WORLD && W.env_simple && W.env_res_mask == 0u)
     hipLaunchKernelGGL((k_interpret<CLASS0_SIZE, REC, true, true>), dim3(blocks), dim3(64), 0, s, dW, 0, 0, mode, first, count, srt, 64);
   else if (mode == AVGPU_MODE_WORLD)
     hipLaunchKernelGGL((k_interpret<CLASS0_SIZE, REC, true>), dim3(blocks), dim3(64), 0, s, dW, 0, 0, mode, first, count, srt, 64);

@@ -340,10 +340,11 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
 
   // world scalars the loop uses, read once: through the descriptor pointer
   // each use was an s_load + lgkmcnt wait inside the loop
-  const double k_size_range = W.size_range;
+  const double k_size_range = DEF ? 2.0 : W.size_range;
   const int k_require_allocate = DEF ? 1 : W.require_allocate, k_alloc_method = DEF ? 0 : W.alloc_method;
   const uint64_t k_th_copy_mut = W.th_copy_mut;
   const int k_rand_total = W.rand_total, k_n_ops = W.n_ops, k_n_react = W.n_react;
+  const bool k_rand_lut = DEF || k_rand_total <= 256;   // GetRandomInst from the LUT
   // RECORDED streams (include/avida_gpu.h "random streams"): the organism's
   // k-th draw is rbase[k]; REC = false compiles the counter path only
   const double* rbase = nullptr;
@@ -375,7 +376,7 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
   // cInstSet::GetRandomInst (cpu/cInstSet.cc:83-88) from the LDS tables
   auto rand_code = [&]() -> uint8_t {
     const uint32_t r = draw_below((uint32_t)k_rand_total);
-    if (k_rand_total <= 256) return rlut[r];
+    if (k_rand_lut) return rlut[r];
     int i = 0;
     while (i < k_n_ops - 1 && tab_i32(rcum + i) <= (int32_t)r) i++;
     return (uint8_t)tab_u8(rcode + i);
@@ -845,8 +846,9 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
           // together and made opaque (OPQ): the asm stores below are
           // scheduling barriers, and the compiler re-issued each invariant
           // scalar load just before its use -- one load-to-use wait per field.
-          double p_min_exe = W.min_exe_lines, p_min_cop = W.min_copied_lines, p_req = W.required_bonus;
-          double p_mdb = DEF ? 0.0 : W.merit_default_bonus, p_defb = W.default_bonus;
+          double p_min_exe = DEF ? 0.5 : W.min_exe_lines, p_min_cop = DEF ? 0.5 : W.min_copied_lines;
+          double p_req = DEF ? 0.0 : W.required_bonus;
+          double p_mdb = DEF ? 0.0 : W.merit_default_bonus, p_defb = DEF ? 1.0 : W.default_bonus;
           int p_inherit = DEF ? 1 : W.inherit_merit, p_bmm = DEF ? 4 : W.base_merit_method;
           int p_bcm = W.base_const_merit;
           double* g_merit = W.merit;
@@ -855,8 +857,8 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
           int32_t* g_ccop = W.child_copied;
           int32_t* g_exec = W.executed;
           int32_t* g_ltask = W.last_task;
-          OPQ(p_min_exe); OPQ(p_min_cop); OPQ(p_req); OPQ(p_defb); OPQ(p_bcm);
-          if (!DEF) { OPQ(p_mdb); OPQ(p_inherit); OPQ(p_bmm); }
+          OPQ(p_bcm);
+          if (!DEF) { OPQ(p_min_exe); OPQ(p_min_cop); OPQ(p_req); OPQ(p_defb); OPQ(p_mdb); OPQ(p_inherit); OPQ(p_bmm); }
           OPQ(g_merit); OPQ(g_fitness); OPQ(g_gest); OPQ(g_ccop); OPQ(g_exec); OPQ(g_ltask);
           bool ok = exe >= (int)(div * p_min_exe) && cop >= (int)(child * p_min_cop);
           double bon = bonus;
@@ -1432,7 +1434,8 @@ bool class_timing_all() {
 static bool def_knobs(const DevWorld& W) {
   return W.alloc_method != 2 && W.require_allocate == 1 && W.max_label_exe == 1 && W.cfg_min_genome == 0 &&
          W.cfg_max_genome == 0 && W.merit_default_bonus == 0.0 && W.inherit_merit == 1 &&
-         W.base_merit_method == 4 && W.th_div_uni == 0;
+         W.base_merit_method == 4 && W.th_div_uni == 0 && W.size_range == 2.0 && W.min_exe_lines == 0.5 &&
+         W.min_copied_lines == 0.5 && W.required_bonus == 0.0 && W.default_bonus == 1.0 && W.rand_total <= 256;
 }
 
 template <bool REC>

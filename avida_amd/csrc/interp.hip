@@ -544,40 +544,35 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
       const int op = pop, r = pr;
       CKC(7);
       switch (op) {
-      case AVGPU_H_POP: {                                     // :2698, cCPUStack::Pop
+      case AVGPU_H_POP:                                       // :2698, cCPUStack::Pop
+      case AVGPU_H_PUSH: {                                    // :2705, cCPUStack::Push
+        // one case for both, so that a wave's pops and pushes share one pass
+        // over the register stacks: Push moves the pointer down and stores,
+        // Pop reads, clears and moves it up
+        const bool push = op == AVGPU_H_PUSH;
         const int k = (ctl & CTL_CURSTK) ? 1 : 0;
         int sp = k ? CTL_SP1(ctl) : CTL_SP0(ctl);
+        if (push) sp = (sp == 0) ? AVGPU_STACK_SIZE - 1 : sp - 1;
+        const int nv = push ? GETREG(r) : 0;
         int v = 0;
         if (VSTK) {
           const int idx = k * AVGPU_STACK_SIZE + sp;
 #pragma unroll
           for (int i = 0; i < 2 * AVGPU_STACK_SIZE; i++) {
             v = (i == idx) ? sv[i] : v;
-            sv[i] = (i == idx) ? 0 : sv[i];
+            sv[i] = (i == idx) ? nv : sv[i];
           }
         } else {
           int32_t* slot = stk + (k * AVGPU_STACK_SIZE + sp) * 64 + lane;
           v = *slot;
-          *slot = 0;
+          *slot = nv;
         }
-        sp = (sp + 1 == AVGPU_STACK_SIZE) ? 0 : sp + 1;
+        if (!push) {
+          sp = (sp + 1 == AVGPU_STACK_SIZE) ? 0 : sp + 1;
+          SETREG(r, v);
+        }
         ctl = k ? ((ctl & ~0xF0u) | ((uint32_t)sp << 4)) : ((ctl & ~0xFu) | (uint32_t)sp);
-        SETREG(r, v);
         CKC(0);
-        break; }
-      case AVGPU_H_PUSH: {                                    // :2705, cCPUStack::Push
-        const int k = (ctl & CTL_CURSTK) ? 1 : 0;
-        int sp = k ? CTL_SP1(ctl) : CTL_SP0(ctl);
-        sp = (sp == 0) ? AVGPU_STACK_SIZE - 1 : sp - 1;
-        if (VSTK) {
-          const int idx = k * AVGPU_STACK_SIZE + sp, val = GETREG(r);
-#pragma unroll
-          for (int i = 0; i < 2 * AVGPU_STACK_SIZE; i++) sv[i] = (i == idx) ? val : sv[i];
-        } else {
-          stk[(k * AVGPU_STACK_SIZE + sp) * 64 + lane] = GETREG(r);
-        }
-        ctl = k ? ((ctl & ~0xF0u) | ((uint32_t)sp << 4)) : ((ctl & ~0xFu) | (uint32_t)sp);
-        CKC(1);
         break; }
       case AVGPU_H_IO: {                                      // :4188 Inst_TaskIO
         const int out = GETREG(r);
@@ -589,11 +584,14 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
         const uint32_t b = num > 1 ? (uint32_t)in1 : 0u;
         const uint32_t c = num > 2 ? (uint32_t)in2 : 0u;
         const uint32_t o = (uint32_t)out;
-        // logic id (cTaskLib::SetupTests): per input combination p the
-        // output bits at the positions where the inputs spell p must agree
-        // ("ones" / "zeros" seen).  With three inputs and every combination
-        // present -- always, for SetupInputs' 0x0F/0x33/0x55 top bytes -- the
-        // id is the "ones" mask; otherwise the general rule below.
+        // logic id (cTaskLib::SetupTests, main/cTaskLib.cc:395-440): per input
+        // combination p the output bits where the inputs spell p are all 1
+        // (logic[p] = 1), all 0 (0), mixed (no id) or absent (-1); missing
+        // inputs repeat the lower half; id = sum logic[p] 2^p.  In bit masks:
+        // "ones" / "zeros" seen per p, present P = ones | zeros, and with
+        // every logic[p] in {-1, 0, 1}, id = ones - (~P & 0xFF).  With three
+        // inputs and every combination present -- always, for SetupInputs'
+        // 0x0F/0x33/0x55 top bytes -- that is just the "ones" mask.
         uint32_t ones = 0u, zeros = 0u;
 #pragma unroll
         for (int p = 0; p < 8; p++) {
@@ -601,27 +599,14 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
           ones |= min(o & m, 1u) << p;
           zeros |= min(~o & m, 1u) << p;
         }
-        uint32_t tmask = 0u;
-        if (num == 3 && (ones | zeros) == 0xFFu) {
-          tmask = (ones & zeros) ? 0u : lut[ones];
-        } else {
-          int lo[8];
-          bool bad = false;
-#pragma unroll
-          for (int p = 0; p < 8; p++) {
-            const uint32_t m = ((p & 1) ? a : ~a) & ((p & 2) ? b : ~b) & ((p & 4) ? c : ~c);
-            const uint32_t v = o & m;
-            lo[p] = (m == 0u) ? -1 : (v == m ? 1 : 0);
-            bad |= (m != 0u) && (v != m) && (v != 0u);
-          }
-          if (num < 1) lo[1] = lo[0];
-          if (num < 2) { lo[2] = lo[0]; lo[3] = lo[1]; }
-          if (num < 3) { lo[4] = lo[0]; lo[5] = lo[1]; lo[6] = lo[2]; lo[7] = lo[3]; }
-          int id = 0;
-#pragma unroll
-          for (int p = 0; p < 8; p++) id += lo[p] * (1 << p);
-          tmask = (!bad && id >= 0 && id < 256) ? lut[id] : 0u;
-        }
+        // a missing input is 0, so the combinations that need it are absent
+        // and their bits are clear: the copies below only fill empty bits
+        uint32_t lo = ones, pr = ones | zeros;
+        if (num < 1) { lo |= (lo & 1u) << 1; pr |= (pr & 1u) << 1; }
+        if (num < 2) { lo |= (lo & 3u) << 2; pr |= (pr & 3u) << 2; }
+        if (num < 3) { lo |= (lo & 15u) << 4; pr |= (pr & 15u) << 4; }
+        const int id = (int)lo - (int)(~pr & 0xFFu);
+        const uint32_t tmask = ((ones & zeros) == 0u && id >= 0) ? lut[id] : 0u;
         // cEnvironment::TestOutput / TestRequisites / DoProcesses
         // (main/cEnvironment.cc:1314-1406, :1408-1503, :1610-1760)
         if (tmask && k_env_simple) {

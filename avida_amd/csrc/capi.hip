@@ -102,15 +102,12 @@ int setup_world(avgpu_world* w, int64_t n, bool test_buffers) {
   const avgpu_cfg& c = w->cfg;
   int rc = 0;
 #define A(ptr, cnt) if ((rc = w->alloc(&W.ptr, (size_t)(cnt))) < 0) return rc
-  A(reg, 3 * n); A(head, 4 * n); A(ctl, n); A(rlabel, n); A(mem_size, n); A(cycles, n);
-  A(time_used, n); A(gest_start, n); A(max_exec, n); A(birth_len, n); A(gkey, n); A(rng, 3 * n);
+  A(xs, (size_t)n * XS_WORDS); A(ctl, n); A(mem_size, n); A(max_exec, n); A(birth_len, n); A(gkey, n); A(rng, 3 * n);
   A(budget, n); A(aclass, n); A(tape, (size_t)n * TAPE_SLOT);
-  A(stack, 2 * AVGPU_STACK_SIZE * n); A(inbuf, 3 * n); A(in_total, n); A(in_ptr, n);
-  A(outbuf, n); A(out_total, n); A(inputs, 3 * n);
-  A(cur_task, AVGPU_MAX_REACTIONS * n); A(last_task, AVGPU_MAX_REACTIONS * n);
+  A(inputs, 3 * n); A(last_task, AVGPU_MAX_REACTIONS * n);
   A(cur_react, AVGPU_MAX_REACTIONS * n);
-  A(cur_bonus, n); A(merit, n); A(fitness, n); A(credit, n); A(gest_time, n); A(num_div, n);
-  A(generation, n); A(copied, n); A(child_copied, n); A(executed, n); A(errors, n);
+  A(merit, n); A(fitness, n); A(credit, n); A(gest_time, n); A(num_div, n);
+  A(generation, n); A(copied, n); A(child_copied, n); A(executed, n);
   HIPCHK(hipMemsetAsync(W.aclass, ACLASS_NONE, n, w->stream));   // no slice allotted yet
   A(class_list, NUM_LISTS * n); A(order, n); A(class_count, 8); A(counters, CNT_WORDS);
   // birth records: one primary record per cell + overflow for further

@@ -58,17 +58,39 @@ enum { RT_TASK = 0, RT_TYPE = 1, RT_MIN = 2, RT_MAX = 3, RT_HASREQ = 4, RT_USED 
 // birth record is already in use (budgets are < 2^30: avgpu_step checks)
 #define BUDGET_PRIM 0x40000000
 
+// Per-cell execution record: the interpreter-private state of one organism
+// (the fields only a slice and the state import / export touch), XS_WORDS
+// int32 = 256 B per cell, 256-B aligned.  A slice reads and writes it with
+// 13 16-byte accesses per lane (words 0..51) instead of ~50 scattered 4-byte
+// SoA accesses -- in budget-sorted windows the lanes of a wave are scattered
+// cells, and every SoA store was a partial-line HBM write.  A fresh offspring
+// (CTL_FRESH) has none of it stored: its birth values are implied.
+enum : int {
+  XS_REG = 0,      // 3: registers AX BX CX
+  XS_HEAD = 3,     // 4: IP, read, write, flow
+  XS_RLABEL = 7,   // read_label: len (4b) | nop i at bits 4+2i
+  XS_CYCLES = 8,   // cpu_cycles_used
+  XS_TIME = 9,     // time_used
+  XS_GEST = 10,    // gestation_start
+  XS_ERRORS = 11,  // cur errors (faults)
+  XS_INBUF = 12,   // 3: input buffer, most recent first
+  XS_INTOT = 15,   // inputs received
+  XS_INPTR = 16,   // next input index
+  XS_OUTBUF = 17,  // last output
+  XS_OUTTOT = 18,  // outputs made
+  XS_BONUS = 20,   // 2: cur_bonus (double, 8-B aligned)
+  XS_TASK = 22,    // 9: cur_task_count of the logic-9 tasks
+  XS_STACK = 32,   // 20: stack k entry j at 32 + 10k + j
+  XS_USED = 52,
+  XS_WORDS = 64
+};
+
 struct DevWorld {
   int64_t n;  // cells
   // --- hot state (registers in the interpreter) ---
-  int32_t* reg;       // [3][n]
-  int32_t* head;      // [4][n]
+  int32_t* xs;        // [n][XS_WORDS] execution records (above)
   uint32_t* ctl;      // [n]  sp0 | sp1<<4 | cur_stack | mal_active | alive
-  uint32_t* rlabel;   // [n]  read_label: len (4b) | nop i at bits 4+2i
   int32_t* mem_size;  // [n]
-  int32_t* cycles;    // [n]  cpu_cycles_used
-  int32_t* time_used; // [n]
-  int32_t* gest_start;// [n]
   int32_t* max_exec;  // [n]
   int32_t* birth_len; // [n]  genome length at birth (cPhenotype::genome_length)
   uint64_t* gkey;     // [n]  genome key of the birth genome (systematics census)
@@ -82,18 +104,10 @@ struct DevWorld {
   // size must not be picked up by class 0 in the same update).
   uint8_t* aclass;
   uint8_t* tape;      // [n][TAPE_SLOT]
-  // --- cold state (touched in place by IO / stack / divide) ---
-  int32_t* stack;     // [2*10][n]
-  int32_t* inbuf;     // [3][n] most recent first
-  int32_t* in_total;  // [n]
-  int32_t* in_ptr;    // [n]
-  int32_t* outbuf;    // [n]
-  int32_t* out_total; // [n]
+  // --- cold state ---
   int32_t* inputs;    // [3][n] cell inputs
-  int32_t* cur_task;  // [16][n]
   int32_t* last_task; // [16][n]
   int32_t* cur_react; // [16][n]
-  double* cur_bonus;  // [n]
   double* merit;      // [n]
   double* fitness;    // [n]
   double* credit;     // [n]
@@ -103,7 +117,6 @@ struct DevWorld {
   int32_t* copied;    // [n]
   int32_t* child_copied; // [n]
   int32_t* executed;  // [n]
-  int32_t* errors;    // [n]
   // --- per-update work lists / queues ---
   // size-class lists: row k = 1..3 the organisms k_allot put in class k,
   // row 3 + k the organisms that spilled into class k during the update

@@ -262,14 +262,16 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
       __builtin_amdgcn_global_load_lds((void*)(W.tape + (int64_t)c * TAPE_SLOT + q * 16),
                                        (lds_ptr_t)(lds32 + it * 256), 16, 0, 0);
   }
+  // stacks: class 0's into VGPRs with the execution record below; the list
+  // classes' from the record into LDS, one word per lane and entry
+  int32_t* const xrec = W.xs + (int64_t)(cell < 0 ? 0 : cell) * XS_WORDS;
   int32_t sv[2 * AVGPU_STACK_SIZE];
 #pragma unroll
   for (int k = 0; k < 2 * AVGPU_STACK_SIZE; k++) {
     if (VSTK) {
-      sv[k] = (active && !fresh) ? W.stack[(int64_t)k * N + cell] : 0;
+      sv[k] = 0;
     } else if (active && !fresh) {
-      __builtin_amdgcn_global_load_lds((void*)(W.stack + (int64_t)k * N + cell),
-                                       (lds_ptr_t)(stk + k * 64), 4, 0, 0);
+      __builtin_amdgcn_global_load_lds((void*)(xrec + XS_STACK + k), (lds_ptr_t)(stk + k * 64), 4, 0, 0);
     } else {
       stk[k * 64 + lane] = 0;
     }
@@ -310,21 +312,28 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
     dexe = W.executed[cell]; dcop = W.copied[cell]; dgen = W.generation[cell];
     bonus = W.default_bonus;
   }
+  static_assert(AVGPU_NUM_LOGIC_TASKS == 9 && 2 * AVGPU_STACK_SIZE == 20, "execution record layout");
   if (active && !fresh) {
-    r0 = W.reg[cell]; r1 = W.reg[N + cell]; r2 = W.reg[2 * N + cell];
-    ip = W.head[cell]; rh = W.head[N + cell]; wh = W.head[2 * N + cell]; fh = W.head[3 * N + cell];
-    rl = W.rlabel[cell];
-    cyc = W.cycles[cell]; tu = W.time_used[cell]; gs = W.gest_start[cell];
-    errs = W.errors[cell];
-    in0 = W.inbuf[cell]; in1 = W.inbuf[N + cell]; in2 = W.inbuf[2 * N + cell];
-    intot = W.in_total[cell]; inptr = W.in_ptr[cell];
-    outv = W.outbuf[cell]; outtot = W.out_total[cell];
-    bonus = W.cur_bonus[cell];
+    // the execution record (device.h XS_*): 16-byte loads of its own lines
+    const int4* xr = reinterpret_cast<const int4*>(xrec);
+    const int4 x0 = xr[0], x1 = xr[1], x2 = xr[2], x3 = xr[3], x4 = xr[4], x5 = xr[5], x6 = xr[6], x7 = xr[7];
+    r0 = x0.x; r1 = x0.y; r2 = x0.z; ip = x0.w;
+    rh = x1.x; wh = x1.y; fh = x1.z; rl = (uint32_t)x1.w;
+    cyc = x2.x; tu = x2.y; gs = x2.z; errs = x2.w;
+    in0 = x3.x; in1 = x3.y; in2 = x3.z; intot = x3.w;
+    inptr = x4.x; outv = x4.y; outtot = x4.z;
+    bonus = __hiloint2double(x5.y, x5.x);
+    tc[0] = x5.z; tc[1] = x5.w; tc[2] = x6.x; tc[3] = x6.y; tc[4] = x6.z; tc[5] = x6.w;
+    tc[6] = x7.x; tc[7] = x7.y; tc[8] = x7.z;
+    if (VSTK) {
 #pragma unroll
-    for (int q = 0; q < AVGPU_NUM_LOGIC_TASKS; q++) {
-      tc[q] = W.cur_task[(int64_t)q * N + cell];
-      nzm |= (tc[q] > 0 ? 1u : 0u) << q;
+      for (int j = 0; j < 5; j++) {
+        const int4 v = xr[8 + j];
+        sv[4 * j] = v.x; sv[4 * j + 1] = v.y; sv[4 * j + 2] = v.z; sv[4 * j + 3] = v.w;
+      }
     }
+#pragma unroll
+    for (int q = 0; q < AVGPU_NUM_LOGIC_TASKS; q++) nzm |= (tc[q] > 0 ? 1u : 0u) << q;
     dnd = W.num_div[cell];
   }
   prim0 = prim;
@@ -1082,30 +1091,34 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
 #endif
   __syncthreads();
   if (active) {
-    W.reg[cell] = r0; W.reg[N + cell] = r1; W.reg[2 * N + cell] = r2;
-    W.head[cell] = ip; W.head[N + cell] = rh; W.head[2 * N + cell] = wh; W.head[3 * N + cell] = fh;
+    // the execution record: words 0..51 in 13 16-byte stores (whole 32-B
+    // sectors of the cell's own lines)
+    int4* xw = reinterpret_cast<int4*>(xrec);
+    const long long bb = __double_as_longlong(bonus);
+    xw[0] = make_int4(r0, r1, r2, ip);
+    xw[1] = make_int4(rh, wh, fh, (int)rl);
+    xw[2] = make_int4(cyc, tu, gs, errs);
+    xw[3] = make_int4(in0, in1, in2, intot);
+    xw[4] = make_int4(inptr, outv, outtot, 0);
+    xw[5] = make_int4((int)(uint32_t)bb, (int)(bb >> 32), tc[0], tc[1]);
+    xw[6] = make_int4(tc[2], tc[3], tc[4], tc[5]);
+    xw[7] = make_int4(tc[6], tc[7], tc[8], 0);
+#pragma unroll
+    for (int j = 0; j < 5; j++)
+      xw[8 + j] = VSTK ? make_int4(sv[4 * j], sv[4 * j + 1], sv[4 * j + 2], sv[4 * j + 3])
+                       : make_int4(stk[(4 * j) * 64 + lane], stk[(4 * j + 1) * 64 + lane],
+                                   stk[(4 * j + 2) * 64 + lane], stk[(4 * j + 3) * 64 + lane]);
     if (!alive) ctl &= ~CTL_ALIVE;
-    W.ctl[cell] = ctl & ~CTL_FRESH; W.rlabel[cell] = rl;
+    W.ctl[cell] = ctl & ~CTL_FRESH;
     W.mem_size[cell] = M;
-    W.cycles[cell] = cyc; W.time_used[cell] = tu; W.gest_start[cell] = gs;
     W.rng[2 * N + cell] = kct;
     W.budget[cell] = spill ? (budget | (prim ? BUDGET_PRIM : 0)) : 0;
-    W.errors[cell] = errs;
-    W.inbuf[cell] = in0; W.inbuf[N + cell] = in1; W.inbuf[2 * N + cell] = in2;
-    W.in_total[cell] = intot; W.in_ptr[cell] = inptr;
-    W.outbuf[cell] = outv; W.out_total[cell] = outtot;
-    W.cur_bonus[cell] = bonus;
-#pragma unroll
-    for (int q = 0; q < AVGPU_NUM_LOGIC_TASKS; q++) W.cur_task[(int64_t)q * N + cell] = tc[q];
     // merit, fitness, gestation time, copied / executed sizes and last-task
     // counts were stored at the divide (st_async)
     if (didv || fresh) { W.num_div[cell] = dnd; W.generation[cell] = dgen; }
     if (fresh) {
 #pragma unroll
-      for (int q = AVGPU_NUM_LOGIC_TASKS; q < AVGPU_MAX_REACTIONS; q++) {
-        W.cur_task[(int64_t)q * N + cell] = 0;
-        W.last_task[(int64_t)q * N + cell] = 0;
-      }
+      for (int q = AVGPU_NUM_LOGIC_TASKS; q < AVGPU_MAX_REACTIONS; q++) W.last_task[(int64_t)q * N + cell] = 0;
       if (!didv) W.child_copied[cell] = 0;   // last_task: the parent's, set at activation
     }
     // cur_reaction_count: reset at a divide, counted since (or added to the
@@ -1120,8 +1133,6 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
         *p = 0;
       }
     }
-#pragma unroll
-    for (int k = 0; k < 2 * AVGPU_STACK_SIZE; k++) W.stack[(int64_t)k * N + cell] = VSTK ? sv[k] : stk[k * 64 + lane];
     if (spill) {
       const int slot = atomicAdd(&W.class_count[3 + cls + 1], 1);     // spill row of class cls+1
       W.class_list[(int64_t)(3 + cls + 1) * N + slot] = cell;

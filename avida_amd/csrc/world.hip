@@ -67,13 +67,11 @@ __global__ void k_set_orgs(DevWorld W, int64_t first, int64_t count, const uint8
   const uint8_t* g = codes + offsets[i];
   uint8_t* t = W.tape + c * TAPE_SLOT;
   for (int k = 0; k < len; k++) t[k] = g[k] & CODE_MASK;
-  for (int k = 0; k < 3; k++) W.reg[k * N + c] = 0;
-  for (int k = 0; k < 4; k++) W.head[k * N + c] = 0;
-  for (int k = 0; k < 2 * AVGPU_STACK_SIZE; k++) W.stack[k * N + c] = 0;
+  // registers, heads, label, counters, buffers, task counts, stacks: zero
+  int32_t* x = W.xs + c * XS_WORDS;
+  for (int k = 0; k < XS_WORDS; k++) x[k] = 0;
   W.ctl[c] = CTL_ALIVE;
-  W.rlabel[c] = 0;
   W.mem_size[c] = len;
-  W.cycles[c] = 0; W.time_used[c] = 0; W.gest_start[c] = 0;
   int mx = 0;
   if (W.death_method > 0) {                 // cOrganism::initialize (main/cOrganism.cc:216-236)
     mx = W.age_limit;
@@ -99,18 +97,16 @@ __global__ void k_set_orgs(DevWorld W, int64_t first, int64_t count, const uint8
   if (W.spec) W.spec[c] = 0;           // serial world: no speculative credit yet
   W.inputs[c] = in0; W.inputs[N + c] = in1; W.inputs[2 * N + c] = in2;
   W.budget[c] = 0;
-  for (int k = 0; k < 3; k++) W.inbuf[k * N + c] = 0;
-  W.in_total[c] = 0; W.in_ptr[c] = 0; W.outbuf[c] = 0; W.out_total[c] = 0;
   for (int k = 0; k < AVGPU_MAX_REACTIONS; k++) {
-    W.cur_task[k * N + c] = 0; W.last_task[k * N + c] = 0; W.cur_react[k * N + c] = 0;
+    W.last_task[k * N + c] = 0; W.cur_react[k * N + c] = 0;
   }
   // cPhenotype::SetupInject (main/cPhenotype.cc:599-640)
-  W.cur_bonus[c] = W.default_bonus;
+  *reinterpret_cast<double*>(x + XS_BONUS) = W.default_bonus;
   W.merit[c] = (merits && merits[i] > 0.0) ? merits[i] : (double)len;
   W.fitness[c] = 0.0;
   W.credit[c] = 0.0;
   W.gest_time[c] = 0; W.num_div[c] = 0; W.generation[c] = 0;
-  W.copied[c] = len; W.child_copied[c] = 0; W.executed[c] = len; W.errors[c] = 0;
+  W.copied[c] = len; W.child_copied[c] = 0; W.executed[c] = len;
 }
 
 // the cHardwareBase inspection tuple of cell c (zero padding: the digest below
@@ -119,24 +115,25 @@ __device__ void build_state(const DevWorld& W, int64_t c, avgpu_cpu_state& s) {
   const int64_t N = W.n;
   memset(&s, 0, sizeof(s));
   const bool fresh = (W.ctl[c] & CTL_FRESH) != 0;   // birth values implied (setup_child)
+  const int32_t* x = W.xs + c * XS_WORDS;
   if (!fresh) {
-  for (int k = 0; k < 3; k++) s.reg[k] = W.reg[k * N + c];
-  for (int k = 0; k < 4; k++) s.head[k] = W.head[k * N + c];
+  for (int k = 0; k < 3; k++) s.reg[k] = x[XS_REG + k];
+  for (int k = 0; k < 4; k++) s.head[k] = x[XS_HEAD + k];
   for (int k = 0; k < 2; k++)
-    for (int j = 0; j < AVGPU_STACK_SIZE; j++) s.stack[k][j] = W.stack[(k * AVGPU_STACK_SIZE + j) * N + c];
+    for (int j = 0; j < AVGPU_STACK_SIZE; j++) s.stack[k][j] = x[XS_STACK + k * AVGPU_STACK_SIZE + j];
   }
   const uint32_t ctl = W.ctl[c];
   s.stack_ptr[0] = CTL_SP0(ctl); s.stack_ptr[1] = CTL_SP1(ctl);
   s.cur_stack = (ctl & CTL_CURSTK) ? 1 : 0;
   s.mal_active = (ctl & CTL_MAL) ? 1 : 0;
   s.alive = (ctl & CTL_ALIVE) ? 1 : 0;
-  const uint32_t rl = fresh ? 0u : W.rlabel[c];
+  const uint32_t rl = fresh ? 0u : (uint32_t)x[XS_RLABEL];
   s.read_label_len = rl & 15;
   for (int k = 0; k < (int)(rl & 15); k++) s.read_label[k] = (int8_t)((rl >> (4 + 2 * k)) & 3);
   s.mem_size = W.mem_size[c];
-  s.cpu_cycles_used = fresh ? 0 : W.cycles[c];
-  s.time_used = fresh ? 0 : W.time_used[c];
-  s.gestation_start = fresh ? 0 : W.gest_start[c];
+  s.cpu_cycles_used = fresh ? 0 : x[XS_CYCLES];
+  s.time_used = fresh ? 0 : x[XS_TIME];
+  s.gestation_start = fresh ? 0 : x[XS_GEST];
   s.gestation_time = W.gest_time[c];
   s.num_divides = fresh ? 0 : W.num_div[c];
   s.generation = W.generation[c];
@@ -146,22 +143,23 @@ __device__ void build_state(const DevWorld& W, int64_t c, avgpu_cpu_state& s) {
   s.executed_size = W.executed[c];
   s.max_executed = W.max_exec[c];
   s.birth_length = W.birth_len[c];
-  s.input_ptr = fresh ? 0 : W.in_ptr[c];
-  const int tot = fresh ? 0 : W.in_total[c];
-  for (int k = 0; k < 3; k++) s.input_buf[k] = (k < tot) ? W.inbuf[k * N + c] : 0;
+  s.input_ptr = fresh ? 0 : x[XS_INPTR];
+  const int tot = fresh ? 0 : x[XS_INTOT];
+  for (int k = 0; k < 3; k++) s.input_buf[k] = (k < tot) ? x[XS_INBUF + k] : 0;
   s.input_total = tot;
-  s.output_total = fresh ? 0 : W.out_total[c];
-  s.output_buf = s.output_total ? W.outbuf[c] : 0;
+  s.output_total = fresh ? 0 : x[XS_OUTTOT];
+  s.output_buf = s.output_total ? x[XS_OUTBUF] : 0;
   for (int k = 0; k < 3; k++) s.inputs[k] = W.inputs[k * N + c];
+  // task counts past the logic-9 tasks stay 0 (no reaction can count them)
   for (int k = 0; k < AVGPU_MAX_REACTIONS && !fresh; k++) {
-    s.cur_task_count[k] = W.cur_task[k * N + c];
+    s.cur_task_count[k] = k < AVGPU_NUM_LOGIC_TASKS ? x[XS_TASK + k] : 0;
     s.cur_reaction_count[k] = W.cur_react[k * N + c];
   }
   for (int k = 0; k < AVGPU_MAX_REACTIONS; k++)   // a fresh offspring's were set at activation
     s.last_task_count[k] = (fresh && k >= AVGPU_NUM_LOGIC_TASKS) ? 0 : W.last_task[k * N + c];
   s.rng_key_lo = W.rng[c]; s.rng_key_hi = W.rng[N + c]; s.rng_counter = W.rng[2 * N + c];
-  s.errors = fresh ? 0 : W.errors[c];
-  s.cur_bonus = fresh ? W.default_bonus : W.cur_bonus[c];
+  s.errors = fresh ? 0 : x[XS_ERRORS];
+  s.cur_bonus = fresh ? W.default_bonus : *reinterpret_cast<const double*>(x + XS_BONUS);
   s.merit = W.merit[c];
   s.fitness = W.fitness[c];
   s.credit = W.credit[c];
@@ -219,36 +217,39 @@ __global__ void k_set_states(DevWorld W, int64_t first, int64_t count, const avg
   const int64_t N = W.n;
   const int64_t c = first + i;
   const avgpu_cpu_state s = in[i];
-  for (int k = 0; k < 3; k++) W.reg[k * N + c] = s.reg[k];
-  for (int k = 0; k < 4; k++) W.head[k * N + c] = s.head[k];
+  int32_t* x = W.xs + c * XS_WORDS;
+  for (int k = 0; k < XS_WORDS; k++) x[k] = 0;
+  for (int k = 0; k < 3; k++) x[XS_REG + k] = s.reg[k];
+  for (int k = 0; k < 4; k++) x[XS_HEAD + k] = s.head[k];
   for (int k = 0; k < 2; k++)
-    for (int j = 0; j < AVGPU_STACK_SIZE; j++) W.stack[(k * AVGPU_STACK_SIZE + j) * N + c] = s.stack[k][j];
+    for (int j = 0; j < AVGPU_STACK_SIZE; j++) x[XS_STACK + k * AVGPU_STACK_SIZE + j] = s.stack[k][j];
   W.ctl[c] = (uint32_t)(s.stack_ptr[0] & 0xF) | ((uint32_t)(s.stack_ptr[1] & 0xF) << 4) |
              (s.cur_stack ? CTL_CURSTK : 0u) | (s.mal_active ? CTL_MAL : 0u) | (s.alive ? CTL_ALIVE : 0u);
   uint32_t rl = (uint32_t)(s.read_label_len & 15);
   for (int k = 0; k < (s.read_label_len & 15) && k < AVGPU_MAX_LABEL; k++)
     rl |= (uint32_t)(s.read_label[k] & 3) << (4 + 2 * k);
-  W.rlabel[c] = rl;
+  x[XS_RLABEL] = (int32_t)rl;
   W.mem_size[c] = s.mem_size;
-  W.cycles[c] = s.cpu_cycles_used; W.time_used[c] = s.time_used; W.gest_start[c] = s.gestation_start;
+  x[XS_CYCLES] = s.cpu_cycles_used; x[XS_TIME] = s.time_used; x[XS_GEST] = s.gestation_start;
   W.gest_time[c] = s.gestation_time; W.num_div[c] = s.num_divides; W.generation[c] = s.generation;
   W.birth_len[c] = s.birth_length;
   W.copied[c] = s.copied_size; W.child_copied[c] = s.child_copied_size; W.executed[c] = s.executed_size;
   W.max_exec[c] = s.max_executed;
-  W.in_ptr[c] = s.input_ptr;
-  for (int k = 0; k < 3; k++) W.inbuf[k * N + c] = s.input_buf[k];
-  W.in_total[c] = s.input_total;
-  W.outbuf[c] = s.output_buf; W.out_total[c] = s.output_total;
+  x[XS_INPTR] = s.input_ptr;
+  for (int k = 0; k < 3; k++) x[XS_INBUF + k] = s.input_buf[k];
+  x[XS_INTOT] = s.input_total;
+  x[XS_OUTBUF] = s.output_buf; x[XS_OUTTOT] = s.output_total;
   for (int k = 0; k < 3; k++) W.inputs[k * N + c] = s.inputs[k];
   for (int k = 0; k < AVGPU_MAX_REACTIONS; k++) {
-    W.cur_task[k * N + c] = s.cur_task_count[k];
+    if (k < AVGPU_NUM_LOGIC_TASKS) x[XS_TASK + k] = s.cur_task_count[k];
     W.last_task[k * N + c] = s.last_task_count[k];
     W.cur_react[k * N + c] = s.cur_reaction_count[k];
   }
   W.rng[c] = s.rng_key_lo; W.rng[N + c] = s.rng_key_hi; W.rng[2 * N + c] = s.rng_counter;
   if (W.rec_off) W.rec_off[c] = -1;   // restored organisms draw from counter streams
-  W.errors[c] = s.errors;
-  W.cur_bonus[c] = s.cur_bonus; W.merit[c] = s.merit; W.fitness[c] = s.fitness; W.credit[c] = s.credit;
+  x[XS_ERRORS] = s.errors;
+  *reinterpret_cast<double*>(x + XS_BONUS) = s.cur_bonus;
+  W.merit[c] = s.merit; W.fitness[c] = s.fitness; W.credit[c] = s.credit;
   W.budget[c] = 0;
   uint8_t* t = W.tape + c * TAPE_SLOT;
   const uint8_t* src = codes + i * cap;

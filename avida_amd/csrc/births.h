@@ -110,6 +110,7 @@ struct Child {
   uint32_t lo, hi, ctr;
   const int32_t* ltask;   // the parent's last task counts, ltask[q * lstride]
   int64_t lstride;
+  bool big;               // CTL_BIG class hint (SEQ_BIG of the record)
 };
 // Run by a group of G lanes (G = 64: a wave, 32: a half-wave); `lane` is the
 // lane's index inside its group.
@@ -129,7 +130,7 @@ __device__ __forceinline__ void setup_child(const DevWorld& W, int64_t c, const 
   for (int off = G / 2; off > 0; off >>= 1) gsum += __shfl_xor(gsum, off);
   if (lane == 0) W.gkey[c] = gk_final(gsum, len);
   switch (lane) {
-    case 0: W.ctl[c] = CTL_ALIVE | CTL_FRESH; break;
+    case 0: W.ctl[c] = CTL_ALIVE | CTL_FRESH | (b.big ? CTL_BIG : 0u); break;
     case 1: W.mem_size[c] = len; break;
     case 2: {
       int mx = 0;
@@ -160,6 +161,64 @@ __device__ __forceinline__ void setup_child(const DevWorld& W, int64_t c, const 
   }
 }
 
+// The same activation by ONE lane (k_activate: a lane per queued birth, so a
+// launch of ~1k waves covers a 60k-birth update with all of its record loads
+// in flight at once).  The genome moves in 16-byte quads; the bytes of the
+// last quad past the genome are written as 0 (sites >= mem_size are never
+// read before h-alloc fills them, and every export masks them).
+__device__ __forceinline__ void setup_child_lane(const DevWorld& W, int64_t c, const Child& b,
+                                                 const uint8_t* __restrict__ src) {
+  const int64_t N = W.n;
+  const int len = b.len;
+  const uint4* __restrict__ s4 = reinterpret_cast<const uint4*>(src);
+  uint4* __restrict__ d4 = reinterpret_cast<uint4*>(W.tape + c * TAPE_SLOT);
+  uint64_t gsum = 0;
+  const int nq = (len + 15) >> 4;
+  for (int k0 = 0; k0 < nq; k0 += 4) {
+    uint4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++)
+      if (k0 + u < nq) v[u] = s4[k0 + u];
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      if (k0 + u >= nq) break;
+      const int w = 4 * (k0 + u);
+      uint32_t x[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        const int keep = len - 4 * (w + j);     // sites of word w+j inside the genome
+        if (keep <= 0) x[j] = 0u;
+        else { if (keep < 4) x[j] &= (1u << (8 * keep)) - 1u; gsum += gk_word(x[j], w + j, len); }
+      }
+      d4[k0 + u] = make_uint4(x[0], x[1], x[2], x[3]);
+    }
+  }
+  W.gkey[c] = gk_final(gsum, len);
+  W.ctl[c] = CTL_ALIVE | CTL_FRESH | (b.big ? CTL_BIG : 0u);
+  W.mem_size[c] = len;
+  int mx = 0;
+  if (W.death_method > 0) { mx = W.age_limit; if (W.death_method == 2) mx *= len; if (mx < 1) mx = 1; }
+  W.max_exec[c] = mx;
+  W.birth_len[c] = len;
+  W.merit[c] = b.merit;
+  W.fitness[c] = b.fitness;
+  W.credit[c] = 0.0;
+  W.gest_time[c] = b.gest;
+  W.generation[c] = b.gen;
+  W.copied[c] = b.ccopied;
+  W.executed[c] = b.exec;
+  uint32_t ctr = b.ctr;
+  // cEnvironment::SetupInputs random (main/cEnvironment.cc:1268-1271)
+  W.inputs[c] = (15 << 24) + (int)rng_below(b.lo, b.hi, ctr, 1u << 24);
+  W.inputs[N + c] = (51 << 24) + (int)rng_below(b.lo, b.hi, ctr, 1u << 24);
+  W.inputs[2 * N + c] = (85 << 24) + (int)rng_below(b.lo, b.hi, ctr, 1u << 24);
+  W.rng[c] = b.lo; W.rng[N + c] = b.hi; W.rng[2 * N + c] = ctr;
+  if (W.rec_off) W.rec_off[c] = -1;             // offspring: counter streams
+#pragma unroll
+  for (int q = 0; q < AVGPU_NUM_LOGIC_TASKS; q++)   // last_task_count = the parent's (:447)
+    W.last_task[(int64_t)q * N + c] = b.ltask[(int64_t)q * b.lstride];
+}
+
 // the phenotype record r hands its offspring
 __device__ __forceinline__ Child child_of_record(const DevWorld& W, int64_t i) {
   Child b;
@@ -167,6 +226,7 @@ __device__ __forceinline__ Child child_of_record(const DevWorld& W, int64_t i) {
   b.gest = W.b_gest[i]; b.merit = W.b_merit[i]; b.fitness = W.b_fitness[i];
   b.lo = W.b_rng[i]; b.hi = W.b_rng[W.rcap + i]; b.ctr = W.b_rng[2 * W.rcap + i];
   b.ltask = W.b_ltask + i; b.lstride = W.rcap;
+  b.big = (W.b_seq[i] & SEQ_BIG) != 0u;
   return b;
 }
 

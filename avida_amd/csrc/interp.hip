@@ -985,7 +985,9 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
                 OPQ(b_fitness); OPQ(b_gen); OPQ(b_ccopied); OPQ(b_exec); OPQ(b_gest); OPQ(b_rng);
                 OPQ(b_state); OPQ(b_target); OPQ(b_ltask); OPQ(rcap);
                 st_async_u32(b_parent + rec, (uint32_t)cell);
-                st_async_u32(b_seq + rec, (uint32_t)nd);
+                // SEQ_BIG: the parent part re-allocates beyond class 0 (CTL_BIG)
+                const uint32_t big = need_of(div, 0u, k_size_range) > CLASS0_SIZE ? SEQ_BIG : 0u;
+                st_async_u32(b_seq + rec, (uint32_t)nd | big);
                 st_async_u32(b_len + rec, (uint32_t)len);
                 st_async_u32(b_len0 + rec, (uint32_t)child);   // k_apply_mutations edits the copy
                 st_async_u32(b_edit + rec, (uint32_t)e0);

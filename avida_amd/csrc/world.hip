@@ -700,29 +700,31 @@ __global__ __launch_bounds__(64) void k_apply_mutations(DevWorld W, int mblocks)
   for (int64_t q = blockIdx.x; q < nb; q += mblocks) apply_edits_wave(W, rec_of(W, q), child);
 }
 
-// One half-wave per queued birth (a genome of <= 128 sites is one 32-lane
-// pass, and the 21 stored fields fit 32 lanes): the winners of cells inside
-// the tile are activated; winners of ghost-row cells were shipped by
-// k_halo_pack.
+// One lane per queued birth: the winners of cells inside the tile are
+// activated; winners of ghost-row cells were shipped by k_halo_pack.  The
+// record's fields are loaded before the ownership test (independent loads
+// in flight together instead of a chain behind it).
 // last: (single world) the claim array of the last placement round, zeroed
 // at each record's target for the next update
 __global__ __launch_bounds__(64) void k_activate(DevWorld W, unsigned long long* last) {
   const int nb = queue_len(W);
-  const int lane = threadIdx.x & 31;
   unsigned long long born = 0, lost = 0;
-  for (int64_t q = 2 * (int64_t)blockIdx.x + (threadIdx.x >> 5); q < nb; q += 2 * (int64_t)gridDim.x) {
+  for (int64_t q = (int64_t)blockIdx.x * 64 + threadIdx.x; q < nb; q += (int64_t)gridDim.x * 64) {
     const int64_t i = rec_of(W, q);
     const int tgt = W.b_target[i];
-    if (last && lane == 0 && tgt >= 0) last[tgt] = 0ull;
-    const bool won = W.b_state[i] > 0 && tgt >= 0 && W.owner[tgt] == (int)i;
+    const int8_t st = W.b_state[i];
+    const Child b = child_of_record(W, i);
+    if (last && tgt >= 0) last[tgt] = 0ull;
+    const bool won = st > 0 && tgt >= 0 && W.owner[tgt] == (int)i;
     if (won && tgt >= W.n) continue;          // sent to the neighbouring tile
     if (!won) { lost++; continue; }
     born++;
-    setup_child<32>(W, tgt, child_of_record(W, i), reinterpret_cast<const uint32_t*>(W.b_genome + i * TAPE_SLOT),
-                    lane);
+    setup_child_lane(W, tgt, b, W.b_genome + i * TAPE_SLOT);
   }
-  born += __shfl_xor(born, 32);                 // both halves' lane 0
-  lost += __shfl_xor(lost, 32);
+  for (int off = 32; off > 0; off >>= 1) {
+    born += __shfl_xor(born, off);
+    lost += __shfl_xor(lost, off);
+  }
   if (threadIdx.x == 0) {
     if (born) count_add(W, CNT_BIRTHS, born);
     if (lost) count_add(W, CNT_DROPPED, lost);
@@ -799,7 +801,7 @@ __global__ __launch_bounds__(64) void k_activate_remote(DevWorld W, int d) {
     Child b;
     b.len = r.len; b.gen = r.gen; b.ccopied = r.ccopied; b.exec = r.exec; b.gest = r.gest;
     b.merit = r.merit; b.fitness = r.fitness; b.lo = r.rng_lo; b.hi = r.rng_hi; b.ctr = r.rng_ctr;
-    b.ltask = recs[q].last_task; b.lstride = 1;
+    b.ltask = recs[q].last_task; b.lstride = 1; b.big = false;
     setup_child<64>(W, c, b, reinterpret_cast<const uint32_t*>(arena + r.off), lane);
   }
   if (lane == 0) {
@@ -1034,8 +1036,18 @@ static unsigned activate_grid(const DevWorld& W) {
   }
   return (unsigned)std::min<int64_t>(W.rcap, cap);
 }
+// k_activate: a lane per birth; 2048 waves cover 131k queued births per pass
+static unsigned lane_grid(const DevWorld& W) { return (unsigned)std::min<int64_t>(nblk(W.rcap, 64), 2048); }
 // placement kernels stride over the queue; 8 blocks of 256 per CU cover it
-static unsigned place_grid(const DevWorld& W) { return (unsigned)std::min<int64_t>(nblk(W.rcap, 256), 2048); }
+// (AVGPU_PLACE_GRID overrides the cap for sweeps)
+static unsigned place_grid(const DevWorld& W) {
+  static int cap = -1;
+  if (cap < 0) {
+    const char* e = getenv("AVGPU_PLACE_GRID");
+    cap = e ? std::max(1, atoi(e)) : 2048;
+  }
+  return (unsigned)std::min<int64_t>(nblk(W.rcap, 256), cap);
+}
 
 static unsigned activate_grid(const DevWorld& W);
 static bool has_divide_mutations(const DevWorld& W) {
@@ -1075,7 +1087,7 @@ void launch_world_post(const DevWorld& W, hipStream_t s, double* stats) {
     hipLaunchKernelGGL(k_place_resolve, dim3(bb), dim3(256), 0, s, W, round, 0,
                        (const unsigned long long*)buf[round & 1]);
   }
-  hipLaunchKernelGGL(k_activate, dim3(activate_grid(W)), dim3(64), 0, s, W, buf[1]);
+  hipLaunchKernelGGL(k_activate, dim3(lane_grid(W)), dim3(64), 0, s, W, buf[1]);
   launch_stats(W, s, stats);
 }
 
@@ -1127,7 +1139,7 @@ void launch_tile_place(const DevWorld& W, hipStream_t s, int round, int phase) {
 }
 
 void launch_tile_finish(const DevWorld& W, hipStream_t s, double* stats) {
-  hipLaunchKernelGGL(k_activate, dim3(activate_grid(W)), dim3(64), 0, s, W, (unsigned long long*)nullptr);
+  hipLaunchKernelGGL(k_activate, dim3(lane_grid(W)), dim3(64), 0, s, W, (unsigned long long*)nullptr);
   for (int d = 0; d < 2; d++)
     hipLaunchKernelGGL(k_activate_remote, dim3((unsigned)std::max(1, std::min(W.world_x, 4096))), dim3(64),
                        0, s, W, d);

@@ -67,6 +67,15 @@ __device__ __forceinline__ int mut_source(int j, const int* e, bool nopc, int& v
   return src;
 }
 
+// LDS written by some lanes of a wave, then read by others: wait for the
+// wave's own LDS traffic (no block barrier -- the mutation waves of one
+// workgroup run different numbers of records)
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
 // The divide-mutation edits of record r applied to its child genome by one
 // wave (k_apply_mutations; the serial world per birth): a no-op when the
 // record has none.  child: LDS scratch of TAPE_SLOT + 16 bytes.
@@ -81,7 +90,7 @@ __device__ __forceinline__ void apply_edits_wave(const DevWorld& W, int64_t r, u
   uint32_t* g32 = reinterpret_cast<uint32_t*>(W.b_genome + r * TAPE_SLOT);
   uint32_t* c32 = reinterpret_cast<uint32_t*>(child);
   for (int w = lane; (w << 2) < len0; w += 64) c32[w] = g32[w];
-  __syncthreads();
+  wave_lds_sync();
   for (int w = lane; (w << 2) < len; w += 64) {
     uint32_t word = 0;
 #pragma unroll
@@ -94,7 +103,7 @@ __device__ __forceinline__ void apply_edits_wave(const DevWorld& W, int64_t r, u
     }
     g32[w] = word;
   }
-  __syncthreads();
+  wave_lds_sync();
 }
 
 // ActivateOrganism (main/cPopulation.cc:1320-1340) + SetupOffspring
@@ -110,7 +119,6 @@ struct Child {
   uint32_t lo, hi, ctr;
   const int32_t* ltask;   // the parent's last task counts, ltask[q * lstride]
   int64_t lstride;
-  bool big;               // CTL_BIG class hint (SEQ_BIG of the record)
 };
 // Run by a group of G lanes (G = 64: a wave, 32: a half-wave); `lane` is the
 // lane's index inside its group.
@@ -130,7 +138,7 @@ __device__ __forceinline__ void setup_child(const DevWorld& W, int64_t c, const 
   for (int off = G / 2; off > 0; off >>= 1) gsum += __shfl_xor(gsum, off);
   if (lane == 0) W.gkey[c] = gk_final(gsum, len);
   switch (lane) {
-    case 0: W.ctl[c] = CTL_ALIVE | CTL_FRESH | (b.big ? CTL_BIG : 0u); break;
+    case 0: W.ctl[c] = CTL_ALIVE | CTL_FRESH; break;
     case 1: W.mem_size[c] = len; break;
     case 2: {
       int mx = 0;
@@ -194,7 +202,7 @@ __device__ __forceinline__ void setup_child_lane(const DevWorld& W, int64_t c, c
     }
   }
   W.gkey[c] = gk_final(gsum, len);
-  W.ctl[c] = CTL_ALIVE | CTL_FRESH | (b.big ? CTL_BIG : 0u);
+  W.ctl[c] = CTL_ALIVE | CTL_FRESH;
   W.mem_size[c] = len;
   int mx = 0;
   if (W.death_method > 0) { mx = W.age_limit; if (W.death_method == 2) mx *= len; if (mx < 1) mx = 1; }
@@ -226,7 +234,6 @@ __device__ __forceinline__ Child child_of_record(const DevWorld& W, int64_t i) {
   b.gest = W.b_gest[i]; b.merit = W.b_merit[i]; b.fitness = W.b_fitness[i];
   b.lo = W.b_rng[i]; b.hi = W.b_rng[W.rcap + i]; b.ctr = W.b_rng[2 * W.rcap + i];
   b.ltask = W.b_ltask + i; b.lstride = W.rcap;
-  b.big = (W.b_seq[i] & SEQ_BIG) != 0u;
   return b;
 }
 

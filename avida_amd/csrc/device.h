@@ -32,14 +32,6 @@
 // (zero, default bonus) implicitly -- the SoA rows are stale until the
 // organism's first slice writes them back.  Every reader honours the bit.
 #define CTL_FRESH 0x800u
-// class hint (performance only, no semantics): the organism's parent kept a
-// part after its divide that re-allocates beyond class 0 (need_of > CLASS0_SIZE),
-// so this offspring likely will too at its first divide -- where a class-0
-// slice would stop and run the rest of its slice alone after class 0 (spill
-// row).  need_of puts it in class 1 from birth; its own divide clears the bit.
-#define CTL_BIG 0x1000u
-// b_seq bit of a birth record: hand CTL_BIG to the offspring (setup_child)
-#define SEQ_BIG 0x80000000u
 
 #define NUM_CLASSES 4
 #define ACLASS_NONE 0xFF
@@ -473,10 +465,9 @@ __device__ __forceinline__ int class_of(int need) {
 // tape capacity an organism may need this slice: its memory, or the size
 // h-alloc would grow it to when it has not allocated yet
 __device__ __forceinline__ int need_of(int m, uint32_t ctl, double size_range) {
-  const int hint = (ctl & CTL_BIG) ? CLASS0_SIZE + 1 : 0;
-  if (ctl & CTL_MAL) return max(m, hint);
+  if (ctl & CTL_MAL) return m;
   const int grown = m + min((int)(size_range * m), AVGPU_MAX_GENOME - m);
-  return max(grown > m ? grown : m, hint);
+  return grown > m ? grown : m;
 }
 
 // ---------------------------------------------------------------------------

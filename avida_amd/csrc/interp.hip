@@ -344,6 +344,7 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
 #endif
 
   bool alive = active && (ctl & CTL_ALIVE);
+  const bool alive0 = alive;
   bool stop = false, spill = false;
   int executed = 0, divides = 0;
 
@@ -985,9 +986,7 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
                 OPQ(b_fitness); OPQ(b_gen); OPQ(b_ccopied); OPQ(b_exec); OPQ(b_gest); OPQ(b_rng);
                 OPQ(b_state); OPQ(b_target); OPQ(b_ltask); OPQ(rcap);
                 st_async_u32(b_parent + rec, (uint32_t)cell);
-                // SEQ_BIG: the parent part re-allocates beyond class 0 (CTL_BIG)
-                const uint32_t big = need_of(div, 0u, k_size_range) > CLASS0_SIZE ? SEQ_BIG : 0u;
-                st_async_u32(b_seq + rec, (uint32_t)nd | big);
+                st_async_u32(b_seq + rec, (uint32_t)nd);
                 st_async_u32(b_len + rec, (uint32_t)len);
                 st_async_u32(b_len0 + rec, (uint32_t)child);   // k_apply_mutations edits the copy
                 st_async_u32(b_edit + rec, (uint32_t)e0);
@@ -1111,6 +1110,9 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
                        : make_int4(stk[(4 * j) * 64 + lane], stk[(4 * j + 1) * 64 + lane],
                                    stk[(4 * j + 2) * 64 + lane], stk[(4 * j + 3) * 64 + lane]);
     if (!alive) ctl &= ~CTL_ALIVE;
+    // a death frees the cell for this update's placement (k_allot_total
+    // marked the living cells occupied)
+    if (mode == AVGPU_MODE_WORLD && alive0 && !alive) W.occ[cell] = 0;
     W.ctl[cell] = ctl & ~CTL_FRESH;
     W.mem_size[cell] = M;
     W.rng[2 * N + cell] = kct;
@@ -1249,7 +1251,7 @@ __global__ __launch_bounds__(64, (S == CLASS0_SIZE) ? 2 : 1) void k_interpret(co
     const int rc = cls >= 0 ? cls : (r <= 3 ? r : r - 3);
     const int lcount = Wp->class_count[r];
     for (int64_t chunk = blockIdx.x; chunk * lpw < lcount; chunk += gridDim.x) {
-      interpret_chunk<S, REC>(Wp, rc, mode, first, count, chunk, lds32, false, r, lpw);
+      interpret_chunk<S, REC, false, SIMPLE, DEF>(Wp, rc, mode, first, count, chunk, lds32, false, r, lpw);
       __syncthreads();
     }
   }
@@ -1465,14 +1467,29 @@ static void launch_classes(const DevWorld& W, const DevWorld* dW, int mode, hipS
   // Organisms k_allot put in classes 1..3 (list rows 1..3) do not depend on
   // class 0; with an aux stream they run beside it and fill the CUs its tail
   // leaves idle.  Spills (rows 4..6) run after both, in class order.
+  // list classes and spill rows of a world update at the simple environment
+  // and default knobs: the same specialised interpreter as class 0's (SIMPLE,
+  // DEF) -- the spill rows run alone after class 0, latency-bound on their
+  // longest slice, so every instruction of the generic paths is on the
+  // update's critical path
+  const bool fast = mode == AVGPU_MODE_WORLD && W.env_simple && W.env_res_mask == 0u && def_knobs(W);
+  auto row = [&](int S, dim3 grid, hipStream_t st, int cls, int r, int lpw) {
+#define ROW_LAUNCH(SZ) \
+    do { if (fast) hipLaunchKernelGGL((k_interpret<SZ, REC, false, true, true>), grid, dim3(64), 0, st, dW, cls, r, mode, first, count, 0, lpw); \
+         else hipLaunchKernelGGL((k_interpret<SZ, REC>), grid, dim3(64), 0, st, dW, cls, r, mode, first, count, 0, lpw); } while (0)
+    if (S == CLASS1_SIZE) ROW_LAUNCH(CLASS1_SIZE);
+    else if (S == CLASS2_SIZE) ROW_LAUNCH(CLASS2_SIZE);
+    else ROW_LAUNCH(CLASS3_SIZE);
+#undef ROW_LAUNCH
+  };
   auto list = [&](int k, hipStream_t st) {
-    if (k == 1) hipLaunchKernelGGL((k_interpret<CLASS1_SIZE, REC>), dim3(lb), dim3(64), 0, st, dW, 1, 1, mode, first, count, 0, 64);
-    if (k == 2) hipLaunchKernelGGL((k_interpret<CLASS2_SIZE, REC>), dim3(lb_c2), dim3(64), 0, st, dW, 2, 2, mode, first, count, 0, 64);
-    if (k == 3) hipLaunchKernelGGL((k_interpret<CLASS3_SIZE, REC>), dim3(lb_c3), dim3(64), 0, st, dW, 3, 3, mode, first, count, 0, 64);
+    if (k == 1) row(CLASS1_SIZE, dim3(lb), st, 1, 1, 64);
+    if (k == 2) row(CLASS2_SIZE, dim3(lb_c2), st, 2, 2, 64);
+    if (k == 3) row(CLASS3_SIZE, dim3(lb_c3), st, 3, 3, 64);
     // classes 2 + 3 in one launch of class 3's slots: both start at the fork,
     // before class 0's blocks fill the CUs (a class-3 block launched behind
     // class 2 waited ~0.5 ms for a CU with all of its LDS free)
-    if (k == 23) hipLaunchKernelGGL((k_interpret<CLASS3_SIZE, REC>), dim3(lb_c2 + lb_c3), dim3(64), 0, st, dW, -1, 2, mode, first, count, 0, 64);
+    if (k == 23) row(CLASS3_SIZE, dim3(lb_c2 + lb_c3), st, -1, 2, 64);
   };
   // Two aux streams (class 1; classes 2 + 3, which are short): with the
   // world's stream that is three HIP streams, so they keep distinct hardware
@@ -1506,10 +1523,10 @@ static void launch_classes(const DevWorld& W, const DevWorld* dW, int mode, hipS
   // longest remaining slice; spread over waves (spill_lpw lanes each), a
   // wave's iterations no longer pay for its other lanes' divergent paths.
   const int slpw = spill_lpw();
-  hipLaunchKernelGGL((k_interpret<CLASS1_SIZE, REC>), dim3(lb_small), dim3(64), 0, s, dW, 1, 4, mode, first, count, 0, slpw);
+  row(CLASS1_SIZE, dim3(lb_small), s, 1, 4, slpw);
   if (after_class && tall) hipEventRecord(after_class[1], s);
   // spill rows 5 + 6 (beyond classes 1 / 2) in one launch of class 3's slots
-  hipLaunchKernelGGL((k_interpret<CLASS3_SIZE, REC>), dim3(std::min(lb_small, 64u)), dim3(64), 0, s, dW, -1, 5, mode, first, count, 0, slpw);
+  row(CLASS3_SIZE, dim3(std::min(lb_small, 64u)), s, -1, 5, slpw);
   if (after_class && tall) { hipEventRecord(after_class[2], s); hipEventRecord(after_class[3], s); }
   if (launches) *launches += 5;
 }

@@ -382,6 +382,11 @@ __global__ __launch_bounds__(256) void k_merit_final(const double* partial, cons
   }
 }
 
+__device__ __forceinline__ void occ_init_cell(const DevWorld& W, int64_t c) {
+  W.occ[c] = (c < W.n && (W.ctl[c] & CTL_ALIVE)) ? 1 : 0;
+  W.owner[c] = -1;
+}
+
 // cScheduler restated (DESIGN.md "Scheduler"): lambda = UD * merit / total.
 // Writes the cell's budget and class tag; returns the budget.
 __device__ __forceinline__ int allot_cell(const DevWorld& W, int64_t c, double sum, double alive, uint32_t update,
@@ -426,7 +431,10 @@ __global__ void k_allot(DevWorld W, const double* totals, uint32_t update) {
   const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   bool want = false;
   int cls = 0;
-  if (c < W.n) allot_cell(W, c, totals[0], totals[1], update, want, cls);
+  if (c < W.n) {
+    allot_cell(W, c, totals[0], totals[1], update, want, cls);
+    occ_init_cell(W, c);   // as in k_allot_total (tiles re-initialise with their ghost rows)
+  }
   const unsigned long long m = __ballot(want);
   if ((threadIdx.x & 63) == 0 && m) count_add(W, CNT_SLICES, (unsigned long long)__popcll(m));
   enqueue_class(W, (int)c, want, cls);
@@ -476,37 +484,23 @@ __global__ __launch_bounds__(1024) void k_allot_total(DevWorld W, const double* 
     const int64_t c = (int64_t)blockIdx.x * 2048 + h * 1024 + tid;
     bool want = false;
     int cls = 0;
-    if (c < W.n) allot_cell(W, c, sum, alive, update, want, cls);
+    if (c < W.n) {
+      allot_cell(W, c, sum, alive, update, want, cls);
+      // the placement occupancy of this update (k_occ_init's work): living
+      // cells are occupied; an organism that dies in its slice clears its
+      // cell (interpret_chunk's write-back), and no birth lands before placement
+      occ_init_cell(W, c);
+    }
     const unsigned long long m = __ballot(want);
     if ((tid & 63) == 0 && m) count_add(W, CNT_SLICES, (unsigned long long)__popcll(m));
     enqueue_class<16>(W, (int)c, want, cls);
   }
 }
 
-// The window's class-0 cells ordered by budget (descending) with a counting
-// sort (k_window_sort's job, one SORT_WIN window per block): which cell runs
-// in which wave changes no organism's result (per-organism streams, placement
-// by priority), it only groups similar slices, so the order inside a budget
-// is free (LDS atomics).
-__global__ __launch_bounds__(1024) void k_window_count(DevWorld W) {
-  __shared__ int hist[SORT_BUCKETS];
+// the window's order from its bucket histogram (block of 1024 threads, two
+// cells each): exclusive scan by one wave, then each cell's slot
+__device__ __forceinline__ void window_order(const DevWorld& W, int64_t base, int* hist, const int* bucket) {
   const int tid = threadIdx.x;
-  const int64_t base = (int64_t)blockIdx.x * SORT_WIN;
-  for (int i = tid; i < SORT_BUCKETS; i += 1024) hist[i] = 0;
-  __syncthreads();
-  int bucket[2];
-  for (int h = 0; h < 2; h++) {
-    const int64_t c = base + h * 1024 + tid;
-    bucket[h] = -1;
-    if (c < W.n) {
-      // class-0 cells by k_allot's tag: the list classes on the aux streams
-      // rewrite budget / mem_size of their own cells while this kernel runs
-      const bool c0 = W.aclass[c] == 0;
-      bucket[h] = c0 ? SORT_BUCKETS - 2 - min(W.budget[c], SORT_BUCKETS - 2) : SORT_BUCKETS - 1;
-      atomicAdd(&hist[bucket[h]], 1);
-    }
-  }
-  __syncthreads();
   if (tid < 64) {                              // exclusive scan of the buckets by one wave
     constexpr int PER = (SORT_BUCKETS + 63) / 64;
     int loc[PER], t = 0;
@@ -537,15 +531,38 @@ __global__ __launch_bounds__(1024) void k_window_count(DevWorld W) {
   }
 }
 
+// The window's class-0 cells ordered by budget (descending) with a counting
+// sort (k_window_sort's job, one SORT_WIN window per block): which cell runs
+// in which wave changes no organism's result (per-organism streams, placement
+// by priority), it only groups similar slices, so the order inside a budget
+// is free (LDS atomics).
+__global__ __launch_bounds__(1024) void k_window_count(DevWorld W) {
+  __shared__ int hist[SORT_BUCKETS];
+  const int tid = threadIdx.x;
+  const int64_t base = (int64_t)blockIdx.x * SORT_WIN;
+  for (int i = tid; i < SORT_BUCKETS; i += 1024) hist[i] = 0;
+  __syncthreads();
+  int bucket[2];
+  for (int h = 0; h < 2; h++) {
+    const int64_t c = base + h * 1024 + tid;
+    bucket[h] = -1;
+    if (c < W.n) {
+      // class-0 cells by k_allot's tag: the list classes on the aux streams
+      // rewrite budget / mem_size of their own cells while this kernel runs
+      const bool c0 = W.aclass[c] == 0;
+      bucket[h] = c0 ? SORT_BUCKETS - 2 - min(W.budget[c], SORT_BUCKETS - 2) : SORT_BUCKETS - 1;
+      atomicAdd(&hist[bucket[h]], 1);
+    }
+  }
+  __syncthreads();
+  window_order(W, base, hist, bucket);
+}
+
+
 // ---- budget-sorted class-0 windows ----
 // A wave runs until its longest slice ends, so the class-0 interpreter takes
 // its 64 organisms from a window of SORT_WIN cells sorted by budget
 // (k_window_count above).
-
-__device__ __forceinline__ void occ_init_cell(const DevWorld& W, int64_t c) {
-  W.occ[c] = (c < W.n && (W.ctl[c] & CTL_ALIVE)) ? 1 : 0;
-  W.owner[c] = -1;
-}
 
 __global__ void k_occ_init(DevWorld W) {
   const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -603,12 +620,45 @@ __device__ __forceinline__ void place_resolve_one(const DevWorld& W, int64_t i, 
   }
 }
 
+// divide-mutation scan: queue entries per wave (k_apply_mutations, k_place_pick_mut)
+#define MUT_PER_WAVE 8
 // grid-stride over the birth queue (its length is only known on the device)
 #define QUEUE_LOOP(i) \
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, _qn = queue_len(W); i < _qn; \
        i += (int64_t)gridDim.x * blockDim.x)
 __global__ void k_place_pick(DevWorld W, unsigned long long* claim, unsigned long long* prev) {
   QUEUE_LOOP(i) place_pick_one(W, i, claim, prev);
+}
+// Round 0 of a single world's placement with the divide mutations beside it:
+// blocks [0, pblocks) pick; the rest apply the edits (as k_apply_mutations,
+// 4 waves per block) -- placement reads no genome, so the two are independent
+// and share one launch instead of two latency-bound ones.
+__global__ __launch_bounds__(256) void k_place_pick_mut(DevWorld W, unsigned long long* claim, int pblocks) {
+  __shared__ uint8_t child[4][TAPE_SLOT + 16];
+  const int nb = queue_len(W);
+  if ((int)blockIdx.x < pblocks) {
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < nb; i += (int64_t)pblocks * 256)
+      place_pick_one(W, i, claim, nullptr);
+    return;
+  }
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t wave = (int64_t)(blockIdx.x - pblocks) * 4 + wv, nwaves = (int64_t)(gridDim.x - pblocks) * 4;
+  for (int64_t q0 = wave * MUT_PER_WAVE; q0 < nb; q0 += nwaves * MUT_PER_WAVE) {
+    const int64_t q = q0 + lane;
+    int64_t r = 0;
+    bool any = false;
+    if (lane < MUT_PER_WAVE && q < nb) {
+      r = rec_of(W, q);
+      int e = 0;
+#pragma unroll
+      for (int k = 0; k < 5; k++) e |= W.b_edit[(int64_t)k * W.rcap + r];
+      any = e != 0;
+    }
+    for (unsigned long long m = __ballot(any); m; m &= m - 1ull) {
+      const int L = __ffsll((long long)m) - 1;
+      apply_edits_wave(W, (int64_t)__shfl((long long)r, L), child[wv]);
+    }
+  }
 }
 __global__ void k_place_resolve(DevWorld W, int round, int which, const unsigned long long* claim) {
   QUEUE_LOOP(i) place_resolve_one(W, i, round, which, claim);
@@ -686,18 +736,30 @@ __global__ void k_halo_clear(DevWorld W) {
   W.claim[ghost_cell(W, d, x)] = 0ull;
 }
 
-// blocks [0, mblocks) apply the divide mutations; any further blocks
-// initialise the placement occupancy of the n cells (k_occ_init's work), so
-// that a single world's update needs one launch for both
-__global__ __launch_bounds__(64) void k_apply_mutations(DevWorld W, int mblocks) {
+// The divide mutations of the queued offspring: a wave per 8 queue entries --
+// lanes 0..7 read their records' edit words, and the wave rewrites, one after
+// the other, the genomes that have any (about one in ten births at the
+// default rates).  A wave per entry made ~60k short-lived waves for ~6k edits.
+__global__ __launch_bounds__(64) void k_apply_mutations(DevWorld W) {
   __shared__ uint8_t child[TAPE_SLOT + 16];
-  if ((int)blockIdx.x >= mblocks) {
-    const int64_t nthr = (int64_t)(gridDim.x - mblocks) * 64;
-    for (int64_t c = (int64_t)(blockIdx.x - mblocks) * 64 + threadIdx.x; c < W.n; c += nthr) occ_init_cell(W, c);
-    return;
-  }
   const int nb = queue_len(W);
-  for (int64_t q = blockIdx.x; q < nb; q += mblocks) apply_edits_wave(W, rec_of(W, q), child);
+  const int lane = threadIdx.x;
+  for (int64_t q0 = (int64_t)blockIdx.x * MUT_PER_WAVE; q0 < nb; q0 += (int64_t)gridDim.x * MUT_PER_WAVE) {
+    const int64_t q = q0 + lane;
+    int64_t r = 0;
+    bool any = false;
+    if (lane < MUT_PER_WAVE && q < nb) {
+      r = rec_of(W, q);
+      int e = 0;
+#pragma unroll
+      for (int k = 0; k < 5; k++) e |= W.b_edit[(int64_t)k * W.rcap + r];
+      any = e != 0;
+    }
+    for (unsigned long long m = __ballot(any); m; m &= m - 1ull) {
+      const int L = __ffsll((long long)m) - 1;
+      apply_edits_wave(W, (int64_t)__shfl((long long)r, L), child);
+    }
+  }
 }
 
 // One lane per queued birth: the winners of cells inside the tile are
@@ -801,7 +863,7 @@ __global__ __launch_bounds__(64) void k_activate_remote(DevWorld W, int d) {
     Child b;
     b.len = r.len; b.gen = r.gen; b.ccopied = r.ccopied; b.exec = r.exec; b.gest = r.gest;
     b.merit = r.merit; b.fitness = r.fitness; b.lo = r.rng_lo; b.hi = r.rng_hi; b.ctr = r.rng_ctr;
-    b.ltask = recs[q].last_task; b.lstride = 1; b.big = false;
+    b.ltask = recs[q].last_task; b.lstride = 1;
     setup_child<64>(W, c, b, reinterpret_cast<const uint32_t*>(arena + r.off), lane);
   }
   if (lane == 0) {
@@ -1006,6 +1068,8 @@ void launch_world_begin(const DevWorld& W, hipStream_t s, double* totals, double
                      (const int32_t*)alive_partial, nb, totals, update);
   // the class lists are complete: the aux streams of the list classes start
   // here, beside the window sort, so that their blocks take CUs before class 0
+  // (with the sort folded into k_allot_total they start together with class 0
+  // and end ~35 us after it: profiles/r02q_tail_per_update.txt)
   hipEventRecord(lists_ready, s);
   hipLaunchKernelGGL(k_window_count, dim3(nblk(W.n, SORT_WIN)), dim3(1024), 0, s, W);
 }
@@ -1053,9 +1117,9 @@ static unsigned activate_grid(const DevWorld& W);
 static bool has_divide_mutations(const DevWorld& W) {
   return (W.th_div_mut | W.th_div_ins | W.th_div_del | W.th_div_slip | W.th_div_uni) != 0;
 }
+static unsigned mut_grid(const DevWorld& W) { return (unsigned)std::min<int64_t>(nblk(W.rcap, MUT_PER_WAVE), 8192); }
 static void launch_apply_mutations(const DevWorld& W, hipStream_t s) {
-  if (has_divide_mutations(W))
-    hipLaunchKernelGGL(k_apply_mutations, dim3(activate_grid(W)), dim3(64), 0, s, W, (int)activate_grid(W));
+  if (has_divide_mutations(W)) hipLaunchKernelGGL(k_apply_mutations, dim3(mut_grid(W)), dim3(64), 0, s, W);
 }
 
 // after a serial-world update (its births are placed): resources, statistics
@@ -1072,18 +1136,17 @@ void launch_reset_counts(const DevWorld& W, hipStream_t s) {
 // claims into array k & 1 after zeroing its records' round k-1 claims; the
 // last round's are zeroed by k_activate): no clearing launch per round.
 void launch_world_post(const DevWorld& W, hipStream_t s, double* stats) {
-  if (has_divide_mutations(W)) {
-    const unsigned mb = activate_grid(W);
-    hipLaunchKernelGGL(k_apply_mutations, dim3(mb + 2048), dim3(64), 0, s, W, (int)mb);
-  } else {
-    hipLaunchKernelGGL(k_occ_init, dim3(nblk(W.n, 256)), dim3(256), 0, s, W);
-  }
+  // the occupancy was initialised by k_allot_total; the divide mutations
+  // ride in round 0's pick launch
   launch_resources_end(W, s);
   const unsigned bb = place_grid(W);
   unsigned long long* buf[2] = {W.claim, W.claim2};
   for (int round = 0; round < 4; round++) {
-    hipLaunchKernelGGL(k_place_pick, dim3(bb), dim3(256), 0, s, W, buf[round & 1],
-                       round ? buf[(round - 1) & 1] : (unsigned long long*)nullptr);
+    if (round == 0 && has_divide_mutations(W))
+      hipLaunchKernelGGL(k_place_pick_mut, dim3(bb + (mut_grid(W) + 3) / 4), dim3(256), 0, s, W, buf[0], (int)bb);
+    else
+      hipLaunchKernelGGL(k_place_pick, dim3(bb), dim3(256), 0, s, W, buf[round & 1],
+                         round ? buf[(round - 1) & 1] : (unsigned long long*)nullptr);
     hipLaunchKernelGGL(k_place_resolve, dim3(bb), dim3(256), 0, s, W, round, 0,
                        (const unsigned long long*)buf[round & 1]);
   }

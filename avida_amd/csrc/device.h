@@ -81,7 +81,8 @@ enum : int {
   XS_BONUS = 20,   // 2: cur_bonus (double, 8-B aligned)
   XS_TASK = 22,    // 9: cur_task_count of the logic-9 tasks
   XS_STACK = 32,   // 20: stack k entry j at 32 + 10k + j
-  XS_USED = 52,
+  XS_REACT = 52,   // 12: cur_reaction_count of reactions 0..11 (12..15 in cur_react rows)
+  XS_NREACT = 12,
   XS_WORDS = 64
 };
 
@@ -107,7 +108,7 @@ struct DevWorld {
   // --- cold state ---
   int32_t* inputs;    // [3][n] cell inputs
   int32_t* last_task; // [16][n]
-  int32_t* cur_react; // [16][n]
+  int32_t* cur_react; // [16][n]: rows XS_NREACT.. only (rows 0..11 live in the execution record)
   double* merit;      // [n]
   double* fitness;    // [n]
   double* credit;     // [n]

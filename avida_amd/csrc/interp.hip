@@ -292,7 +292,10 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
   // divide bookkeeping kept on chip so that no global load or store is
   // compiler-visible inside the loop (written back after it if a divide happened)
   int dexe = 0, dcop = 0, dnd = 0, dgen = 0;
-  int rc[AVGPU_MAX_REACTIONS];   // reaction counts since slice start / last reset
+  // cur_reaction_count: reactions 0..11 from the execution record (the
+  // running count), 12..15 counted since slice start / last reset (added to
+  // their cur_react rows at write-back)
+  int rc[AVGPU_MAX_REACTIONS];
   uint32_t nzm = 0;              // tasks with a non-zero count this gestation
 #pragma unroll
   for (int q = 0; q < AVGPU_MAX_REACTIONS; q++) rc[q] = 0;
@@ -331,6 +334,12 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
         const int4 v = xr[8 + j];
         sv[4 * j] = v.x; sv[4 * j + 1] = v.y; sv[4 * j + 2] = v.z; sv[4 * j + 3] = v.w;
       }
+    }
+    static_assert(XS_REACT == 52 && XS_NREACT == 12, "execution record: reaction counts");
+#pragma unroll
+    for (int j = 0; j < 3; j++) {
+      const int4 v = xr[13 + j];
+      rc[4 * j] = v.x; rc[4 * j + 1] = v.y; rc[4 * j + 2] = v.z; rc[4 * j + 3] = v.w;
     }
 #pragma unroll
     for (int q = 0; q < AVGPU_NUM_LOGIC_TASKS; q++) nzm |= (tc[q] > 0 ? 1u : 0u) << q;
@@ -897,7 +906,7 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
               st_async_u32(g_ltask + (int64_t)q * N + cell, (uint32_t)tc[q]);
             nzm = 0;
 #pragma unroll
-            for (int i = 0; i < AVGPU_MAX_REACTIONS; i++) rc[i] = 0;
+            for (int i = 0; i < AVGPU_MAX_REACTIONS; i++) rc[i] = i < k_n_react ? 0 : rc[i];
             len = child;
             if (mode == AVGPU_MODE_TEST) {
               st_async_u32(W.t_flags_len + cell, (uint32_t)div);
@@ -1109,6 +1118,8 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
       xw[8 + j] = VSTK ? make_int4(sv[4 * j], sv[4 * j + 1], sv[4 * j + 2], sv[4 * j + 3])
                        : make_int4(stk[(4 * j) * 64 + lane], stk[(4 * j + 1) * 64 + lane],
                                    stk[(4 * j + 2) * 64 + lane], stk[(4 * j + 3) * 64 + lane]);
+#pragma unroll
+    for (int j = 0; j < 3; j++) xw[13 + j] = make_int4(rc[4 * j], rc[4 * j + 1], rc[4 * j + 2], rc[4 * j + 3]);
     if (!alive) ctl &= ~CTL_ALIVE;
     // a death frees the cell for this update's placement (k_allot_total
     // marked the living cells occupied)
@@ -1128,7 +1139,7 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
     // cur_reaction_count: reset at a divide, counted since (or added to the
     // stored counts when no divide happened in this slice)
 #pragma unroll
-    for (int i = 0; i < AVGPU_MAX_REACTIONS; i++) {
+    for (int i = XS_NREACT; i < AVGPU_MAX_REACTIONS; i++) {
       int32_t* p = W.cur_react + (int64_t)i * N + cell;
       if (i < W.n_react) {
         if (didv || fresh) *p = rc[i];

@@ -98,7 +98,7 @@ __global__ void k_set_orgs(DevWorld W, int64_t first, int64_t count, const uint8
   W.inputs[c] = in0; W.inputs[N + c] = in1; W.inputs[2 * N + c] = in2;
   W.budget[c] = 0;
   for (int k = 0; k < AVGPU_MAX_REACTIONS; k++) {
-    W.last_task[k * N + c] = 0; W.cur_react[k * N + c] = 0;
+    W.last_task[k * N + c] = 0; W.cur_react[k * N + c] = 0;   // record words: zeroed above
   }
   // cPhenotype::SetupInject (main/cPhenotype.cc:599-640)
   *reinterpret_cast<double*>(x + XS_BONUS) = W.default_bonus;
@@ -153,7 +153,7 @@ __device__ void build_state(const DevWorld& W, int64_t c, avgpu_cpu_state& s) {
   // task counts past the logic-9 tasks stay 0 (no reaction can count them)
   for (int k = 0; k < AVGPU_MAX_REACTIONS && !fresh; k++) {
     s.cur_task_count[k] = k < AVGPU_NUM_LOGIC_TASKS ? x[XS_TASK + k] : 0;
-    s.cur_reaction_count[k] = W.cur_react[k * N + c];
+    s.cur_reaction_count[k] = k < XS_NREACT ? x[XS_REACT + k] : W.cur_react[k * N + c];
   }
   for (int k = 0; k < AVGPU_MAX_REACTIONS; k++)   // a fresh offspring's were set at activation
     s.last_task_count[k] = (fresh && k >= AVGPU_NUM_LOGIC_TASKS) ? 0 : W.last_task[k * N + c];
@@ -243,7 +243,8 @@ __global__ void k_set_states(DevWorld W, int64_t first, int64_t count, const avg
   for (int k = 0; k < AVGPU_MAX_REACTIONS; k++) {
     if (k < AVGPU_NUM_LOGIC_TASKS) x[XS_TASK + k] = s.cur_task_count[k];
     W.last_task[k * N + c] = s.last_task_count[k];
-    W.cur_react[k * N + c] = s.cur_reaction_count[k];
+    if (k < XS_NREACT) x[XS_REACT + k] = s.cur_reaction_count[k];
+    else W.cur_react[k * N + c] = s.cur_reaction_count[k];
   }
   W.rng[c] = s.rng_key_lo; W.rng[N + c] = s.rng_key_hi; W.rng[2 * N + c] = s.rng_counter;
   if (W.rec_off) W.rec_off[c] = -1;   // restored organisms draw from counter streams

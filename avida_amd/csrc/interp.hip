@@ -252,7 +252,11 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
   typedef __attribute__((address_space(3))) void* lds_ptr_t;
   // a serial step runs lane 0 only: its quads are the image's first QUADS
   const int qits = serial ? (QUADS + 63) / 64 : QUADS;
-#pragma unroll 1
+  // class 0: unrolled so that the shuffles of several quads are in flight
+  // together (one LDS round trip per quad otherwise); the list classes' 49 /
+  // 97 / 129-quad loops stay rolled (code size)
+  constexpr int QUNR = (S == CLASS0_SIZE) ? 7 : 1;
+#pragma unroll QUNR
   for (int it = 0; it < qits; it++) {
     const int i = it * 64 + lane;
     const int j = i / QUADS, q = i - j * QUADS;
@@ -1130,6 +1134,8 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
     W.budget[cell] = spill ? (budget | (prim ? BUDGET_PRIM : 0)) : 0;
     // merit, fitness, gestation time, copied / executed sizes and last-task
     // counts were stored at the divide (st_async)
+    // (a fresh organism's zero rows are stored here rather than at activation:
+    // k_activate is bound by its scattered stores, class 0 is not)
     if (didv || fresh) { W.num_div[cell] = dnd; W.generation[cell] = dgen; }
     if (fresh) {
 #pragma unroll
@@ -1155,7 +1161,7 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
     }
   }
   // tapes back to HBM: the same lane-linear quad image, 16 B per lane
-#pragma unroll 2
+#pragma unroll QUNR
   for (int it = 0; it < qits; it++) {
     const int i = it * 64 + lane;
     const int j = i / QUADS, q = i - j * QUADS;

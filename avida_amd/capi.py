@@ -21,7 +21,7 @@ MODE_WORLD, MODE_TEST, MODE_FROZEN = 0, 1, 2
 (CNT_INSTS, CNT_DEATHS, CNT_DIVIDES, CNT_BIRTHS, CNT_DROPPED, CNT_SPILLS, CNT_SLICES,
  CNT_LANESTEPS, CNT_C0_SLICES, CNT_C0_SITES, CNT_CLK_STAGE, CNT_CLK_LOOP, CNT_CLK_WB,
  CNT_ITERS, CNT_IT_FAST, CNT_IT_COPY, CNT_IT_SLOW, CNT_WAVES, CNT_HALO_SENT,
- CNT_HALO_LOST, CNT_REC_EXHAUSTED, CNT_OVERSIZE) = range(22)
+ CNT_HALO_LOST, CNT_REC_EXHAUSTED, CNT_OVERSIZE, CNT_SUB_OVERFLOW) = range(23)
 RNG_COUNTER, RNG_RECORDED = 0, 1
 NUM_COUNTERS = 48
 
@@ -50,6 +50,7 @@ class AvgpuCfg(C.Structure):
         ("seed", C.c_uint64),
         ("divide_slip_prob", C.c_double), ("divide_uniform_prob", C.c_double),
         ("slip_fill_mode", C.c_int32), ("pad_cfg", C.c_int32),
+        ("div_mut_prob", C.c_double),
     ]
 
 
@@ -162,7 +163,8 @@ EXPORTED = [
 
 
 # avida.cfg knobs that change the semantics of this path when non-zero and
-# that it does not implement (main/cAvidaConfig.h:309-361, 372): the per-site,
+# that it does not implement (main/cAvidaConfig.h:309-361, 372): the per-site
+# (other than DIV_MUT_PROB's substitutions),
 # Poisson, translocation, lateral-transfer, parent, point, inject and meta
 # mutations, copy uniform / slip, death on divide.  cfg_from_avida refuses a
 # config that sets any of them rather than run it with different semantics.
@@ -170,7 +172,7 @@ EXPORTED = [
 UNSUPPORTED_NONZERO = [
     "COPY_UNIFORM_PROB", "COPY_SLIP_PROB",
     "POINT_MUT_PROB", "POINT_INS_PROB", "POINT_DEL_PROB", "INST_POINT_MUT_PROB",
-    "DIV_MUT_PROB", "DIV_INS_PROB", "DIV_DEL_PROB", "DIV_UNIFORM_PROB", "DIV_SLIP_PROB",
+    "DIV_INS_PROB", "DIV_DEL_PROB", "DIV_UNIFORM_PROB", "DIV_SLIP_PROB",
     "DIV_TRANS_PROB", "DIV_LGT_PROB",
     "DIVIDE_TRANS_PROB", "DIVIDE_LGT_PROB",
     "DIVIDE_POISSON_MUT_MEAN", "DIVIDE_POISSON_INS_MEAN", "DIVIDE_POISSON_DEL_MEAN",
@@ -245,6 +247,7 @@ def cfg_from_avida(cfg, seed=None) -> AvgpuCfg:
     c.divide_slip_prob = float(g("DIVIDE_SLIP_PROB", 0.0))
     c.divide_uniform_prob = float(g("DIVIDE_UNIFORM_PROB", 0.0))
     c.slip_fill_mode = int(float(g("SLIP_FILL_MODE", 0)))
+    c.div_mut_prob = float(g("DIV_MUT_PROB", 0.0))
     return c
 
 

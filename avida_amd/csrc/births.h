@@ -43,7 +43,8 @@ __device__ __forceinline__ int neighbours(const DevWorld& W, int cell, int* out)
 // interpreter in the reference's order and stored with the birth record
 // (interp.hip): one wave per queued offspring that has any rewrites its
 // genome -- site j of the mutated child is traced back through the edits
-// (last first) to a site of the unmutated child or to a value an edit wrote.
+// (last first) to a site of the unmutated child or to a value an edit wrote;
+// DIV_MUT_PROB's substitutions (b_subs) overwrite their sites after that.
 // Runs before placement, so halo records and activation see final genomes.
 __device__ __forceinline__ int mut_source(int j, const int* e, bool nopc, int& val) {
   int src = j;
@@ -85,7 +86,9 @@ __device__ __forceinline__ void apply_edits_wave(const DevWorld& W, int64_t r, u
   int e[5];
 #pragma unroll
   for (int k = 0; k < 5; k++) e[k] = W.b_edit[(int64_t)k * W.rcap + r];
-  if ((e[0] | e[1] | e[2] | e[3] | e[4]) == 0) return;   // wave-uniform
+  int ns = 0, so = 0;        // DIV_MUT_PROB substitutions, applied last and in order
+  if (W.th_div_site) { ns = W.b_nsub[r]; so = W.b_subofs[r]; }
+  if ((e[0] | e[1] | e[2] | e[3] | e[4] | ns) == 0) return;   // wave-uniform
   const int len0 = W.b_len0[r], len = W.b_len[r];
   uint32_t* g32 = reinterpret_cast<uint32_t*>(W.b_genome + r * TAPE_SLOT);
   uint32_t* c32 = reinterpret_cast<uint32_t*>(child);
@@ -100,6 +103,14 @@ __device__ __forceinline__ void apply_edits_wave(const DevWorld& W, int64_t r, u
       const int src = mut_source(j, e, nopc, val);
       const uint32_t v = val >= 0 ? (uint32_t)val : (uint32_t)child[src];
       word |= (j < len ? v : 0u) << (8 * k);
+    }
+    for (int i = 0; i < ns; i++) {       // later substitutions of one site win
+      const int sub = W.b_subs[so + i];
+      const int site = sub & 0xFFFF;
+      if ((site >> 2) == w) {
+        const int sh = 8 * (site & 3);
+        word = (word & ~(0xFFu << sh)) | ((uint32_t)(sub >> 16) << sh);
+      }
     }
     g32[w] = word;
   }

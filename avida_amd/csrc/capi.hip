@@ -114,7 +114,17 @@ int setup_world(avgpu_world* w, int64_t n, bool test_buffers) {
   // offspring of one slice (device.h); test worlds never enqueue births
   W.rcap = n + (test_buffers ? 16 : std::max<int64_t>(4096, n / 4));
   const int64_t R = W.rcap;
-  A(b_count, 2); A(b_list, n); A(b_parent, R); A(b_seq, R); A(b_len, R); A(b_len0, R); A(b_edit, 5 * R);
+  A(b_count, 3); A(b_list, n); A(b_parent, R); A(b_seq, R); A(b_len, R); A(b_len0, R); A(b_edit, 5 * R);
+  // DIV_MUT_PROB arena: three times the largest expected substitutions per
+  // record plus 16 (offsets are int32); a fill past it is counted
+  // (AVGPU_CNT_SUB_OVERFLOW), never written
+  if (c.div_mut_prob > 0.0) {
+    const double p = std::min(1.0, c.div_mut_prob);
+    int64_t k = (int64_t)std::ceil(AVGPU_MAX_GENOME * p * 3.0) + 16;
+    k = std::min<int64_t>(k, (int64_t)INT32_MAX / R);
+    W.scap = R * k;
+    A(b_nsub, R); A(b_subofs, R); A(b_subs, W.scap);
+  }
   A(b_merit, R);
   A(b_fitness, R); A(b_gen, R); A(b_ccopied, R); A(b_exec, R);
   A(b_gest, R); A(b_ltask, AVGPU_NUM_LOGIC_TASKS * R); A(b_rng, 3 * R); A(b_target, R); A(b_state, R);
@@ -163,6 +173,8 @@ int setup_world(avgpu_world* w, int64_t n, bool test_buffers) {
   W.th_div_uni = th(c.divide_uniform_prob);
   W.p_copy_mut = c.copy_mut_prob; W.p_div_mut = c.divide_mut_prob; W.p_div_ins = c.divide_ins_prob;
   W.p_div_del = c.divide_del_prob; W.p_div_slip = c.divide_slip_prob; W.p_div_uni = c.divide_uniform_prob;
+  W.th_div_site = th(c.div_mut_prob);
+  W.p_div_site = c.div_mut_prob;
   W.slip_fill_mode = c.slip_fill_mode;
   W.rec = nullptr; W.rec_n = 0; W.rec_off = nullptr;
   W.seed_lo = (uint32_t)c.seed;
@@ -599,7 +611,7 @@ int avgpu_step(avgpu_world* w, int64_t first, int64_t count, const int32_t* budg
     HIPCHK(hipMemcpyAsync(d_b, budget, count * sizeof(int32_t), hipMemcpyHostToDevice, w->stream));
   }
   HIPCHK(hipMemsetAsync(w->W.counters, 0, NSHARD * CNT_STRIDE * sizeof(unsigned long long), w->stream));
-  HIPCHK(hipMemsetAsync(w->W.b_count, 0, 2 * sizeof(int32_t), w->stream));
+  HIPCHK(hipMemsetAsync(w->W.b_count, 0, 3 * sizeof(int32_t), w->stream));
   launch_classify_uniform(w->W, w->stream, first, count, d_b, budget_uniform);
   HIPCHK(hipGetLastError());
   rc = interpret(w, mode, first, count);

@@ -131,13 +131,21 @@ struct DevWorld {
   // Queue entry i < b_count[0] is record b_list[i]; entry b_count[0] + j is
   // record n + j (rec_of below).
   int64_t rcap;       // n + ocap
-  int32_t* b_count;   // [2] primary records listed, overflow records used
+  int32_t* b_count;   // [3] primary records listed, overflow records used, b_subs entries used
   int32_t* b_list;    // [n] primary record ids, appended per wave after the loop
   int32_t* b_parent;  // [rcap]
   uint32_t* b_seq;    // [rcap]
   int32_t* b_len;     // [rcap]  offspring length after the divide mutations
   int32_t* b_len0;    // [rcap]  the child's length before them (b_genome holds that child)
   int32_t* b_edit;    // [5][rcap] its divide-mutation edits (interp.hip edit_word; 0 = none)
+  // DIV_MUT_PROB's per-site substitutions of record r (only read when
+  // th_div_site != 0): b_nsub[r] entries from b_subs[b_subofs[r]], each
+  // site | code << 16, applied in order after the five edits; b_count[2] is
+  // the arena's fill of this update, scap its size
+  int32_t* b_nsub;    // [rcap]
+  int32_t* b_subofs;  // [rcap]
+  int32_t* b_subs;    // [scap]
+  int64_t scap;
   double* b_merit;    // [rcap]
   double* b_fitness;  // [rcap]
   int32_t* b_gen;     // [rcap]
@@ -212,6 +220,8 @@ struct DevWorld {
   // for RECORDED draws
   uint64_t th_copy_mut, th_div_mut, th_div_ins, th_div_del, th_div_slip, th_div_uni;
   double p_copy_mut, p_div_mut, p_div_ins, p_div_del, p_div_slip, p_div_uni;
+  uint64_t th_div_site;   // DIV_MUT_PROB (per-site substitutions on divide)
+  double p_div_site;
   int32_t slip_fill_mode;
   // RECORDED mode (avgpu_set_rng_mode): rec_n doubles; rec_off[c] = the start
   // of cell c's organism's segment, -1 = a counter stream.  rec == nullptr:
@@ -283,6 +293,7 @@ __host__ __device__ inline int64_t record_bytes(int x, int64_t arena) {
 #define CNT_HALO_SENT 18  /* offspring shipped to a neighbouring tile */
 #define CNT_HALO_LOST 19  /* offspring lost to a full halo arena (counted in DROPPED too) */
 #define CNT_REC_OVER 20   /* RECORDED draws past the end of the stream */
+#define CNT_SUB_OVERFLOW 22   /* DIV_MUT_PROB substitutions that found the b_subs arena full (must stay 0) */
 #define CNT_OVERSIZE 21   /* offspring a slip grew past AVGPU_MAX_GENOME (counted in DROPPED too) */
 // 32..37: AVGPU_PHASE_CLOCKS loop cycles by block (decode, fast, copy, switch,
 // wave phase, advance); 38..43: slow-switch cycles in pop, push, IO, h-alloc,

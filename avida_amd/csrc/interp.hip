@@ -849,6 +849,7 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
         }
         const int exe = wave_sum_i32(ne), cop = wave_sum_i32(nc);
         int okw = 0, rec = -1, len = 0, e0 = 0, e1 = 0, e2 = 0, e3 = 0, e4 = 0;   // edits: slip mut ins del uniform
+        int nsub = 0, sofs = 0;   // DIV_MUT_PROB substitutions in b_subs
         if (lane == L) {
           // The world parameters and phenotype arrays this block uses, loaded
           // together and made opaque (OPQ): the asm stores below are
@@ -960,6 +961,25 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
                   len++;
                 }
               }
+              // Divide Mutations (per site) (cpu/cHardwareBase.cc:447-460), only
+              // at a non-zero DIV_MUT_PROB: Binomial(len, p) as one P(p) per
+              // site (oracle divide_mutations), then a GetUInt(len) site and a
+              // GetRandomInst per substitution, kept in the b_subs arena (WORLD)
+              if (!DEF && W.th_div_site) {
+                const uint64_t t_site = W.th_div_site;
+                const double q_site = W.p_div_site;
+                for (int i = 0; i < len; i++) nsub += draw_p(t_site, q_site) ? 1 : 0;
+                if (nsub && mode == AVGPU_MODE_WORLD) sofs = atomicAdd(W.b_count + 2, nsub);
+                for (int i = 0; i < nsub; i++) {
+                  const int site = (int)draw_below((uint32_t)len);
+                  const int code = rand_code();
+                  if (mode == AVGPU_MODE_WORLD && (int64_t)sofs + i < W.scap) W.b_subs[sofs + i] = site | (code << 16);
+                }
+                if (mode == AVGPU_MODE_WORLD && (int64_t)sofs + nsub > W.scap) {
+                  count_add(W, CNT_SUB_OVERFLOW, (unsigned long long)nsub);
+                  nsub = 0;
+                }
+              }
               // record (WORLD): the cell's primary record for the slice's
               // first offspring, an overflow record (atomic) for any further
               // one; an offspring a slip grew past the largest genome is dropped
@@ -1007,6 +1027,10 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
                 st_async_u32(b_edit + 2 * rcap + rec, (uint32_t)e2);
                 st_async_u32(b_edit + 3 * rcap + rec, (uint32_t)e3);
                 st_async_u32(b_edit + 4 * rcap + rec, (uint32_t)e4);
+                if (!DEF && W.th_div_site) {
+                  W.b_nsub[rec] = nsub;
+                  W.b_subofs[rec] = sofs;
+                }
                 st_async_u64(b_merit + rec, (uint64_t)__double_as_longlong(merit));
                 st_async_u64(b_fitness + rec, (uint64_t)__double_as_longlong(fit));
                 st_async_u32(b_gen + rec, (uint32_t)gen);
@@ -1451,7 +1475,7 @@ bool class_timing_all() {
 static bool def_knobs(const DevWorld& W) {
   return W.alloc_method != 2 && W.require_allocate == 1 && W.max_label_exe == 1 && W.cfg_min_genome == 0 &&
          W.cfg_max_genome == 0 && W.merit_default_bonus == 0.0 && W.inherit_merit == 1 &&
-         W.base_merit_method == 4 && W.th_div_uni == 0 && W.size_range == 2.0 && W.min_exe_lines == 0.5 &&
+         W.base_merit_method == 4 && W.th_div_uni == 0 && W.th_div_site == 0 && W.size_range == 2.0 && W.min_exe_lines == 0.5 &&
          W.min_copied_lines == 0.5 && W.required_bonus == 0.0 && W.default_bonus == 1.0 && W.rand_total <= 256;
 }
 

@@ -315,7 +315,7 @@ __global__ void k_classify_uniform(DevWorld W, int64_t first, int64_t count, con
 // after the merits, the layout tiles exchange)
 __device__ __forceinline__ void reset_counts_block(const DevWorld& W) {
   for (int i = threadIdx.x; i < NSHARD * CNT_STRIDE; i += blockDim.x) W.counters[i] = 0ull;
-  if (threadIdx.x < 2) W.b_count[threadIdx.x] = 0;
+  if (threadIdx.x < 3) W.b_count[threadIdx.x] = 0;
   if (threadIdx.x < 8) W.class_count[threadIdx.x] = 0;
 }
 
@@ -653,6 +653,7 @@ __global__ __launch_bounds__(256) void k_place_pick_mut(DevWorld W, unsigned lon
       int e = 0;
 #pragma unroll
       for (int k = 0; k < 5; k++) e |= W.b_edit[(int64_t)k * W.rcap + r];
+      if (W.th_div_site) e |= W.b_nsub[r];
       any = e != 0;
     }
     for (unsigned long long m = __ballot(any); m; m &= m - 1ull) {
@@ -754,6 +755,7 @@ __global__ __launch_bounds__(64) void k_apply_mutations(DevWorld W) {
       int e = 0;
 #pragma unroll
       for (int k = 0; k < 5; k++) e |= W.b_edit[(int64_t)k * W.rcap + r];
+      if (W.th_div_site) e |= W.b_nsub[r];
       any = e != 0;
     }
     for (unsigned long long m = __ballot(any); m; m &= m - 1ull) {
@@ -1116,7 +1118,7 @@ static unsigned place_grid(const DevWorld& W) {
 
 static unsigned activate_grid(const DevWorld& W);
 static bool has_divide_mutations(const DevWorld& W) {
-  return (W.th_div_mut | W.th_div_ins | W.th_div_del | W.th_div_slip | W.th_div_uni) != 0;
+  return (W.th_div_mut | W.th_div_ins | W.th_div_del | W.th_div_slip | W.th_div_uni | W.th_div_site) != 0;
 }
 static unsigned mut_grid(const DevWorld& W) { return (unsigned)std::min<int64_t>(nblk(W.rcap, MUT_PER_WAVE), 8192); }
 static void launch_apply_mutations(const DevWorld& W, hipStream_t s) {

@@ -144,6 +144,9 @@ typedef struct avgpu_cfg {
   double divide_uniform_prob;      /* DIVIDE_UNIFORM_PROB */
   int32_t slip_fill_mode;          /* SLIP_FILL_MODE: 0 duplication, 4 nop-C (1-3 refused) */
   int32_t pad_cfg;
+  double div_mut_prob;             /* DIV_MUT_PROB: per-site substitutions on divide,
+                                      Binomial(offspring size, p) of them drawn after the
+                                      uniform mutation (cpu/cHardwareBase.cc:447-460) */
 } avgpu_cfg;
 
 /* One REACTION line of environment.cfg (main/cEnvironment.cc:1185-1211,
@@ -559,6 +562,7 @@ enum avgpu_counter {
   AVGPU_CNT_HALO_LOST = 19, /* offspring dropped because the halo arena was full */
   AVGPU_CNT_REC_EXHAUSTED = 20, /* RECORDED draws past the end of the stream */
   AVGPU_CNT_OVERSIZE = 21,  /* offspring longer than AVGPU_MAX_GENOME after a slip (dropped) */
+  AVGPU_CNT_SUB_OVERFLOW = 22, /* DIV_MUT_PROB substitutions not kept: the per-update arena was full (must be 0) */
   AVGPU_NUM_COUNTERS = 48   /* 32..47: AVGPU_PHASE_CLOCKS diagnostic builds */
 };
 int avgpu_counters(avgpu_world* w, int cumulative, int64_t* out, int n);

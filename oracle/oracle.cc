@@ -229,6 +229,7 @@ struct World {
   std::vector<Org> orgs;
   Prob p_copy_mut, p_copy_ins, p_copy_del;
   Prob p_div_mut, p_div_ins, p_div_del, p_div_slip, p_div_uni;
+  Prob p_div_site;           // DIV_MUT_PROB (per-site substitutions on divide)
   std::vector<double> rec;   // RECORDED mode: the host's stream (organisms point into it)
   // batch world
   std::vector<Birth> births;
@@ -457,7 +458,8 @@ struct Exec {
 
   // Divide_DoMutations (cpu/cHardwareBase.cc:296-569) in the reference's order
   // of draws: TestDivideSlip always draws (main/cMutationRates.h:128), the
-  // translocation / LGT / Poisson / per-site / parent kinds are refused when
+  // translocation / LGT / Poisson / parent kinds and the per-site insertions
+  // and deletions are refused when
   // non-zero (avida_amd/capi.py UNSUPPORTED_NONZERO) and draw nothing at zero,
   // TestDivideMut / Ins / Del always draw (:121-123; the size limits are
   // tested after the draw), TestDivideUniform draws only when non-zero (:124-127).
@@ -489,6 +491,21 @@ struct Exec {
       } else if ((int)child.size() != max_g) {
         const uint32_t site = r.uint_below((uint32_t)child.size() + 1);
         child.insert(child.begin() + site, (uint8_t)(mut - n_ops - 1));
+      }
+    }
+    // Divide Mutations (per site) (cpu/cHardwareBase.cc:447-460): only at a
+    // non-zero DIV_MUT_PROB; mut_multiplier 1 and maxmut INT_MAX on this path
+    // (Divide_Main :1806).  GetRandBinomial lives in Apto (absent here): it is
+    // restated as its exact form, one P(p) per offspring site, so the count is
+    // Binomial(size, p) and every draw comes from the organism's own stream.
+    // Then one GetUInt(size) site and one GetRandomInst per substitution.
+    if (w.p_div_site.p > 0.0) {
+      const int size = (int)child.size();
+      int num_mut = 0;
+      for (int i = 0; i < size; i++) num_mut += r.p(w.p_div_site) ? 1 : 0;
+      for (int i = 0; i < num_mut; i++) {
+        const uint32_t site = r.uint_below((uint32_t)size);
+        child[site] = (uint8_t)w.is.random_inst(r);
       }
     }
   }
@@ -984,6 +1001,7 @@ void* orc_create(const avgpu_cfg* cfg, int64_t ncells) {
   w->p_div_del = make_prob(cfg->divide_del_prob);
   w->p_div_slip = make_prob(cfg->divide_slip_prob);
   w->p_div_uni = make_prob(cfg->divide_uniform_prob);
+  w->p_div_site = make_prob(cfg->div_mut_prob);
   memset(&w->stats, 0, sizeof(w->stats));
   derive_key((uint32_t)cfg->seed, (uint32_t)(cfg->seed >> 32), 0x5CEDu, 0xC0FFEEu,
              &w->global_rng.lo, &w->global_rng.hi);

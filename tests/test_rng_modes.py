@@ -55,8 +55,31 @@ def test_recorded_draws_follow_reference_interface(golden):
     assert b.lib.orc_rec_exhausted() == 0
 
 
+def test_recorded_draws_per_site_divide_mutations(golden):
+    """DIV_MUT_PROB (cpu/cHardwareBase.cc:447-460) after the always-drawing
+    slip / mut / ins / del tests: Binomial(100, 0.5) as one P(0.5) per site
+    (u = 0.37 hits every time: 100 substitutions), then GetUInt(100) and
+    GetRandomInst per substitution -- 4 + 100 + 2 * 100 draws at the first
+    divide, with no copy-mutation draws at COPY_MUT_PROB 0 (they are skipped at
+    a zero rate, main/cMutationRates.h:111)."""
+    iset, env, cfg, anc = _ancestor(golden, {"COPY_MUT_PROB": 0.0, "DIVIDE_INS_PROB": 0.0,
+                                             "DIVIDE_DEL_PROB": 0.0, "DIV_MUT_PROB": 0.5,
+                                             "DEATH_METHOD": 0})
+    b = ol.Backend("oracle", cfg, iset, env, ncells=1)
+    b.set_orgs(0, [anc], deterministic=True)
+    b.set_rng_mode(capi.RNG_RECORDED, np.full(4096, 0.37))
+    for k in range(2000):
+        b.step(0, 1, uniform=1, mode=capi.MODE_FROZEN)
+        st, _, _ = b.states(0, 1, CAP)
+        if st[0].num_divides:
+            break
+    assert st[0].num_divides == 1
+    assert st[0].rng_counter == 4 + 100 + 2 * 100
+    assert b.lib.orc_rec_exhausted() == 0
+
+
 @pytest.mark.gpu
-@pytest.mark.parametrize("muts", ["copy", "all"])
+@pytest.mark.parametrize("muts", ["copy", "all", "site"])
 def test_recorded_stream_frozen_traces_gpu(golden, muts):
     """BASELINE configs[2] traces with mutations on, fed from one recorded
     stream: 3600 organisms of the detail-50000 population, each with its own
@@ -67,10 +90,12 @@ def test_recorded_stream_frozen_traces_gpu(golden, muts):
     ov = {"COPY_MUT_PROB": 0.02, "DIVIDE_INS_PROB": 0.05, "DIVIDE_DEL_PROB": 0.05, "DEATH_METHOD": 0}
     if muts == "all":
         ov.update({"DIVIDE_MUT_PROB": 0.1, "DIVIDE_SLIP_PROB": 0.05, "DIVIDE_UNIFORM_PROB": 0.05})
+    if muts == "site":      # per-site divide substitutions: one draw per offspring site
+        ov.update({"DIV_MUT_PROB": 0.02})
     iset, env, cfg = pu.load_env(golden, "instset-classic.cfg", ov)
     n = len(genomes)
     rng = np.random.default_rng(42)
-    per = 4500              # h-copy alone draws once per copy at a non-zero rate
+    per = 4500 if muts != "site" else 9000   # h-copy alone draws once per copy at a non-zero rate
     stream = rng.random(n * per)
     offsets = np.arange(n, dtype=np.int64) * per
     pair = [ol.Backend(k, cfg, iset, env, ncells=n) for k in ("oracle", "gpu")]
@@ -111,3 +136,28 @@ def test_divide_slip_uniform_world_gpu(golden, fill):
     assert nbad == 0, cells
     lens = {pair[0].states(c, 1)[0][0].birth_length for c in range(0, n, 7)}
     assert len(lens) > 5      # slips changed genome lengths
+
+
+@pytest.mark.gpu
+def test_per_site_divide_mutations_world_gpu(golden):
+    """World updates with DIV_MUT_PROB (per-site substitutions on divide,
+    cpu/cHardwareBase.cc:447-460) on top of the default mutations: GPU world
+    == oracle world, every cell digest, 120 updates; the substitution arena
+    never fills."""
+    ov = {"DIV_MUT_PROB": 0.02, "WORLD_X": 48, "WORLD_Y": 48}
+    iset, env, cfg, anc = _ancestor(golden, ov)
+    n = 48 * 48
+    pair = [ol.Backend(k, cfg, iset, env, ncells=n) for k in ("oracle", "gpu")]
+    g = pu.mutants_of(anc, iset, n // 4, rate=0.01, seed=11)
+    for b in pair:
+        b.set_orgs(0, g, deterministic=False)
+    births = 0
+    for u in range(120):
+        so, sg = pair[0].run_update(), pair[1].run_update()
+        for f in ("num_organisms", "insts_executed", "births", "deaths", "divides", "births_dropped"):
+            assert getattr(so, f) == getattr(sg, f), (u, f)
+        births += sg.births
+        assert pair[1].counters()[capi.CNT_SUB_OVERFLOW] == 0
+    nbad, cells = pu.compare_digests(pair[0].digests(), pair[1].digests())
+    assert nbad == 0, cells
+    assert births > 500

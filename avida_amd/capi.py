@@ -50,7 +50,7 @@ class AvgpuCfg(C.Structure):
         ("seed", C.c_uint64),
         ("divide_slip_prob", C.c_double), ("divide_uniform_prob", C.c_double),
         ("slip_fill_mode", C.c_int32), ("pad_cfg", C.c_int32),
-        ("div_mut_prob", C.c_double),
+        ("div_mut_prob", C.c_double), ("parent_mut_prob", C.c_double),
     ]
 
 
@@ -164,7 +164,7 @@ EXPORTED = [
 
 # avida.cfg knobs that change the semantics of this path when non-zero and
 # that it does not implement (main/cAvidaConfig.h:309-361, 372): the per-site
-# (other than DIV_MUT_PROB's substitutions),
+# (other than DIV_MUT_PROB's and PARENT_MUT_PROB's substitutions),
 # Poisson, translocation, lateral-transfer, parent, point, inject and meta
 # mutations, copy uniform / slip, death on divide.  cfg_from_avida refuses a
 # config that sets any of them rather than run it with different semantics.
@@ -178,7 +178,7 @@ UNSUPPORTED_NONZERO = [
     "DIVIDE_POISSON_MUT_MEAN", "DIVIDE_POISSON_INS_MEAN", "DIVIDE_POISSON_DEL_MEAN",
     "DIVIDE_POISSON_SLIP_MEAN", "DIVIDE_POISSON_TRANS_MEAN", "DIVIDE_POISSON_LGT_MEAN",
     "INJECT_MUT_PROB", "INJECT_INS_PROB", "INJECT_DEL_PROB",
-    "PARENT_MUT_PROB", "PARENT_INS_PROB", "PARENT_DEL_PROB",
+    "PARENT_INS_PROB", "PARENT_DEL_PROB",
     "META_COPY_MUT", "META_STD_DEV", "DEATH_PROB",
 ]
 # Knobs accepted without effect, with the reason.  SPECULATIVE only decides
@@ -248,6 +248,7 @@ def cfg_from_avida(cfg, seed=None) -> AvgpuCfg:
     c.divide_uniform_prob = float(g("DIVIDE_UNIFORM_PROB", 0.0))
     c.slip_fill_mode = int(float(g("SLIP_FILL_MODE", 0)))
     c.div_mut_prob = float(g("DIV_MUT_PROB", 0.0))
+    c.parent_mut_prob = float(g("PARENT_MUT_PROB", 0.0))
     return c
 
 

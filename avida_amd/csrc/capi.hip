@@ -175,6 +175,8 @@ int setup_world(avgpu_world* w, int64_t n, bool test_buffers) {
   W.p_div_del = c.divide_del_prob; W.p_div_slip = c.divide_slip_prob; W.p_div_uni = c.divide_uniform_prob;
   W.th_div_site = th(c.div_mut_prob);
   W.p_div_site = c.div_mut_prob;
+  W.th_par_site = th(c.parent_mut_prob);
+  W.p_par_site = c.parent_mut_prob;
   W.slip_fill_mode = c.slip_fill_mode;
   W.rec = nullptr; W.rec_n = 0; W.rec_off = nullptr;
   W.seed_lo = (uint32_t)c.seed;

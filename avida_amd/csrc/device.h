@@ -222,6 +222,8 @@ struct DevWorld {
   double p_copy_mut, p_div_mut, p_div_ins, p_div_del, p_div_slip, p_div_uni;
   uint64_t th_div_site;   // DIV_MUT_PROB (per-site substitutions on divide)
   double p_div_site;
+  uint64_t th_par_site;   // PARENT_MUT_PROB (per-site substitutions in the parent)
+  double p_par_site;
   int32_t slip_fill_mode;
   // RECORDED mode (avgpu_set_rng_mode): rec_n doubles; rec_off[c] = the start
   // of cell c's organism's segment, -1 = a counter stream.  rec == nullptr:

@@ -980,6 +980,20 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
                   nsub = 0;
                 }
               }
+              // Parent Substitution Mutations (per site) (cpu/cHardwareBase.cc:508-520)
+              // on the parent's sites [0, div) in this lane's LDS tape, code
+              // bits only (the flags are cleared below)
+              if (!DEF && W.th_par_site) {
+                const uint64_t t_par = W.th_par_site;
+                const double q_par = W.p_par_site;
+                int npar = 0;
+                for (int i = 0; i < div; i++) npar += draw_p(t_par, q_par) ? 1 : 0;
+                uint8_t* TLw = reinterpret_cast<uint8_t*>(TL32);
+                for (int i = 0; i < npar; i++) {
+                  const int site = (int)draw_below((uint32_t)div);
+                  TLw[site] = (uint8_t)((TLw[site] & ~CODE_MASK) | rand_code());
+                }
+              }
               // record (WORLD): the cell's primary record for the slice's
               // first offspring, an overflow record (atomic) for any further
               // one; an offspring a slip grew past the largest genome is dropped
@@ -1475,7 +1489,7 @@ bool class_timing_all() {
 static bool def_knobs(const DevWorld& W) {
   return W.alloc_method != 2 && W.require_allocate == 1 && W.max_label_exe == 1 && W.cfg_min_genome == 0 &&
          W.cfg_max_genome == 0 && W.merit_default_bonus == 0.0 && W.inherit_merit == 1 &&
-         W.base_merit_method == 4 && W.th_div_uni == 0 && W.th_div_site == 0 && W.size_range == 2.0 && W.min_exe_lines == 0.5 &&
+         W.base_merit_method == 4 && W.th_div_uni == 0 && W.th_div_site == 0 && W.th_par_site == 0 && W.size_range == 2.0 && W.min_exe_lines == 0.5 &&
          W.min_copied_lines == 0.5 && W.required_bonus == 0.0 && W.default_bonus == 1.0 && W.rand_total <= 256;
 }
 

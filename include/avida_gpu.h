@@ -147,6 +147,9 @@ typedef struct avgpu_cfg {
   double div_mut_prob;             /* DIV_MUT_PROB: per-site substitutions on divide,
                                       Binomial(offspring size, p) of them drawn after the
                                       uniform mutation (cpu/cHardwareBase.cc:447-460) */
+  double parent_mut_prob;          /* PARENT_MUT_PROB: per-site substitutions in the parent's
+                                      memory (cut to the divide point) after the offspring's
+                                      mutations (cpu/cHardwareBase.cc:508-520) */
 } avgpu_cfg;
 
 /* One REACTION line of environment.cfg (main/cEnvironment.cc:1185-1211,

@@ -230,6 +230,7 @@ struct World {
   Prob p_copy_mut, p_copy_ins, p_copy_del;
   Prob p_div_mut, p_div_ins, p_div_del, p_div_slip, p_div_uni;
   Prob p_div_site;           // DIV_MUT_PROB (per-site substitutions on divide)
+  Prob p_par_site;           // PARENT_MUT_PROB (per-site substitutions in the parent)
   std::vector<double> rec;   // RECORDED mode: the host's stream (organisms point into it)
   // batch world
   std::vector<Birth> births;
@@ -506,6 +507,18 @@ struct Exec {
       for (int i = 0; i < num_mut; i++) {
         const uint32_t site = r.uint_below((uint32_t)size);
         child[site] = (uint8_t)w.is.random_inst(r);
+      }
+    }
+    // Parent Substitution Mutations (per site) (cpu/cHardwareBase.cc:508-520):
+    // the parent's memory, already cut to the divide point (Divide_Main
+    // :1803-1806); the same Binomial restatement; flags are untouched
+    if (w.p_par_site.p > 0.0) {
+      const int size = (int)o.mem.size();
+      int num_mut = 0;
+      for (int i = 0; i < size; i++) num_mut += r.p(w.p_par_site) ? 1 : 0;
+      for (int i = 0; i < num_mut; i++) {
+        const uint32_t site = r.uint_below((uint32_t)size);
+        o.mem[site] = (uint8_t)w.is.random_inst(r);
       }
     }
   }
@@ -1002,6 +1015,7 @@ void* orc_create(const avgpu_cfg* cfg, int64_t ncells) {
   w->p_div_slip = make_prob(cfg->divide_slip_prob);
   w->p_div_uni = make_prob(cfg->divide_uniform_prob);
   w->p_div_site = make_prob(cfg->div_mut_prob);
+  w->p_par_site = make_prob(cfg->parent_mut_prob);
   memset(&w->stats, 0, sizeof(w->stats));
   derive_key((uint32_t)cfg->seed, (uint32_t)(cfg->seed >> 32), 0x5CEDu, 0xC0FFEEu,
              &w->global_rng.lo, &w->global_rng.hi);

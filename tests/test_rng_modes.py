@@ -78,6 +78,30 @@ def test_recorded_draws_per_site_divide_mutations(golden):
     assert b.lib.orc_rec_exhausted() == 0
 
 
+def test_recorded_draws_parent_mutations(golden):
+    """PARENT_MUT_PROB (cpu/cHardwareBase.cc:508-520) on the parent's memory,
+    cut to the divide point (Divide_Main :1803-1806): after the 4 always-drawing
+    divide tests, Binomial(100, 0.5) as 100 P(0.5) draws (all hit at u = 0.37),
+    then GetUInt(100) + GetRandomInst per substitution -- all of them on
+    site 37, which becomes the op GetRandomInst(0.37) picks."""
+    iset, env, cfg, anc = _ancestor(golden, {"COPY_MUT_PROB": 0.0, "DIVIDE_INS_PROB": 0.0,
+                                             "DIVIDE_DEL_PROB": 0.0, "PARENT_MUT_PROB": 0.5,
+                                             "DEATH_METHOD": 0})
+    b = ol.Backend("oracle", cfg, iset, env, ncells=1)
+    b.set_orgs(0, [anc], deterministic=True)
+    b.set_rng_mode(capi.RNG_RECORDED, np.full(4096, 0.37))
+    for k in range(2000):
+        b.step(0, 1, uniform=1, mode=capi.MODE_FROZEN)
+        st, ops, _ = b.states(0, 1, CAP)
+        if st[0].num_divides:
+            break
+    assert st[0].num_divides == 1
+    assert st[0].rng_counter == 4 + 100 + 2 * 100
+    assert st[0].mem_size == 100
+    # every GetUInt(100) at u = 0.37 picks site 37: only it changed
+    assert [i for i in range(100) if ops[i] != anc[i]] == [37]
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("muts", ["copy", "all", "site"])
 def test_recorded_stream_frozen_traces_gpu(golden, muts):
@@ -91,7 +115,7 @@ def test_recorded_stream_frozen_traces_gpu(golden, muts):
     if muts == "all":
         ov.update({"DIVIDE_MUT_PROB": 0.1, "DIVIDE_SLIP_PROB": 0.05, "DIVIDE_UNIFORM_PROB": 0.05})
     if muts == "site":      # per-site divide substitutions: one draw per offspring site
-        ov.update({"DIV_MUT_PROB": 0.02})
+        ov.update({"DIV_MUT_PROB": 0.02, "PARENT_MUT_PROB": 0.01})
     iset, env, cfg = pu.load_env(golden, "instset-classic.cfg", ov)
     n = len(genomes)
     rng = np.random.default_rng(42)
@@ -139,12 +163,13 @@ def test_divide_slip_uniform_world_gpu(golden, fill):
 
 
 @pytest.mark.gpu
-def test_per_site_divide_mutations_world_gpu(golden):
-    """World updates with DIV_MUT_PROB (per-site substitutions on divide,
-    cpu/cHardwareBase.cc:447-460) on top of the default mutations: GPU world
-    == oracle world, every cell digest, 120 updates; the substitution arena
-    never fills."""
-    ov = {"DIV_MUT_PROB": 0.02, "WORLD_X": 48, "WORLD_Y": 48}
+@pytest.mark.parametrize("knob", ["DIV_MUT_PROB", "PARENT_MUT_PROB"])
+def test_per_site_divide_mutations_world_gpu(golden, knob):
+    """World updates with DIV_MUT_PROB (per-site substitutions in the
+    offspring, cpu/cHardwareBase.cc:447-460) or PARENT_MUT_PROB (in the
+    parent, :508-520) on top of the default mutations: GPU world == oracle
+    world, every cell digest, 120 updates; the substitution arena never fills."""
+    ov = {knob: 0.02, "WORLD_X": 48, "WORLD_Y": 48}
     iset, env, cfg, anc = _ancestor(golden, ov)
     n = 48 * 48
     pair = [ol.Backend(k, cfg, iset, env, ncells=n) for k in ("oracle", "gpu")]

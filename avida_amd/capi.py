@@ -51,6 +51,8 @@ class AvgpuCfg(C.Structure):
         ("divide_slip_prob", C.c_double), ("divide_uniform_prob", C.c_double),
         ("slip_fill_mode", C.c_int32), ("pad_cfg", C.c_int32),
         ("div_mut_prob", C.c_double), ("parent_mut_prob", C.c_double),
+        ("divide_poisson_slip_mean", C.c_double), ("divide_poisson_mut_mean", C.c_double),
+        ("divide_poisson_ins_mean", C.c_double), ("divide_poisson_del_mean", C.c_double),
     ]
 
 
@@ -164,8 +166,9 @@ EXPORTED = [
 
 # avida.cfg knobs that change the semantics of this path when non-zero and
 # that it does not implement (main/cAvidaConfig.h:309-361, 372): the per-site
-# (other than DIV_MUT_PROB's and PARENT_MUT_PROB's substitutions),
-# Poisson, translocation, lateral-transfer, parent, point, inject and meta
+# (other than DIV_MUT_PROB's and PARENT_MUT_PROB's substitutions), the
+# Poisson translocation / LGT,
+# translocation, lateral-transfer, parent ins / del, point, inject and meta
 # mutations, copy uniform / slip, death on divide.  cfg_from_avida refuses a
 # config that sets any of them rather than run it with different semantics.
 # (COPY_INS_PROB / COPY_DEL_PROB travel in avgpu_cfg; avgpu_create refuses them.)
@@ -175,8 +178,7 @@ UNSUPPORTED_NONZERO = [
     "DIV_INS_PROB", "DIV_DEL_PROB", "DIV_UNIFORM_PROB", "DIV_SLIP_PROB",
     "DIV_TRANS_PROB", "DIV_LGT_PROB",
     "DIVIDE_TRANS_PROB", "DIVIDE_LGT_PROB",
-    "DIVIDE_POISSON_MUT_MEAN", "DIVIDE_POISSON_INS_MEAN", "DIVIDE_POISSON_DEL_MEAN",
-    "DIVIDE_POISSON_SLIP_MEAN", "DIVIDE_POISSON_TRANS_MEAN", "DIVIDE_POISSON_LGT_MEAN",
+    "DIVIDE_POISSON_TRANS_MEAN", "DIVIDE_POISSON_LGT_MEAN",
     "INJECT_MUT_PROB", "INJECT_INS_PROB", "INJECT_DEL_PROB",
     "PARENT_INS_PROB", "PARENT_DEL_PROB",
     "META_COPY_MUT", "META_STD_DEV", "DEATH_PROB",
@@ -249,6 +251,10 @@ def cfg_from_avida(cfg, seed=None) -> AvgpuCfg:
     c.slip_fill_mode = int(float(g("SLIP_FILL_MODE", 0)))
     c.div_mut_prob = float(g("DIV_MUT_PROB", 0.0))
     c.parent_mut_prob = float(g("PARENT_MUT_PROB", 0.0))
+    c.divide_poisson_slip_mean = float(g("DIVIDE_POISSON_SLIP_MEAN", 0.0))
+    c.divide_poisson_mut_mean = float(g("DIVIDE_POISSON_MUT_MEAN", 0.0))
+    c.divide_poisson_ins_mean = float(g("DIVIDE_POISSON_INS_MEAN", 0.0))
+    c.divide_poisson_del_mean = float(g("DIVIDE_POISSON_DEL_MEAN", 0.0))
     return c
 
 

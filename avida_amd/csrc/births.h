@@ -46,24 +46,33 @@ __device__ __forceinline__ int neighbours(const DevWorld& W, int cell, int* out)
 // (last first) to a site of the unmutated child or to a value an edit wrote;
 // DIV_MUT_PROB's substitutions (b_subs) overwrite their sites after that.
 // Runs before placement, so halo records and activation see final genomes.
-__device__ __forceinline__ int mut_source(int j, const int* e, bool nopc, int& val) {
+// one edit word undone: site src of the genome after the edit -> the site it
+// came from before it, or the value the edit wrote (val >= 0)
+__device__ __forceinline__ void edit_back(int ew, bool nopc, int& src, int& val) {
+  if (ew == 0 || val >= 0) return;
+  const int kind = ew & 7, a = (ew >> 3) & 0xFFF, b = (ew >> 15) & 0xFFF;
+  if (kind == 2) {                         // point (E_POINT)
+    if (src == a) val = b;
+  } else if (kind == 3) {                  // insertion (E_INS)
+    if (src == a) val = b; else if (src > a) src--;
+  } else if (kind == 4) {                  // deletion (E_DEL)
+    if (src >= a) src++;
+  } else {                                 // slip from a to b (E_SLIP)
+    if (nopc && a > b && src >= a && src < 2 * a - b) val = AVGPU_H_NOP_C;
+    else if (src >= a) src = b + (src - a);
+  }
+}
+// applied order: e0, Poisson slips, e1, Poisson substitutions, e2, Poisson
+// insertions, e3, Poisson deletions, e4 (pcnt[k] words at subs + pofs[k])
+__device__ __forceinline__ int mut_source(int j, const int* e, bool nopc, int& val, const int32_t* subs,
+                                          const int* pofs, const int* pcnt) {
   int src = j;
   val = -1;
 #pragma unroll
   for (int k = 4; k >= 0; k--) {
-    const int ew = e[k];
-    if (ew == 0 || val >= 0) continue;
-    const int kind = ew & 7, a = (ew >> 3) & 0xFFF, b = (ew >> 15) & 0xFFF;
-    if (kind == 2) {                         // point (E_POINT)
-      if (src == a) val = b;
-    } else if (kind == 3) {                  // insertion (E_INS)
-      if (src == a) val = b; else if (src > a) src--;
-    } else if (kind == 4) {                  // deletion (E_DEL)
-      if (src >= a) src++;
-    } else {                                 // slip from a to b (E_SLIP)
-      if (nopc && a > b && src >= a && src < 2 * a - b) val = AVGPU_H_NOP_C;
-      else if (src >= a) src = b + (src - a);
-    }
+    edit_back(e[k], nopc, src, val);
+    if (k > 0)
+      for (int i = pcnt[k - 1] - 1; i >= 0 && val < 0; i--) edit_back(subs[pofs[k - 1] + i], nopc, src, val);
   }
   return src;
 }
@@ -88,7 +97,15 @@ __device__ __forceinline__ void apply_edits_wave(const DevWorld& W, int64_t r, u
   for (int k = 0; k < 5; k++) e[k] = W.b_edit[(int64_t)k * W.rcap + r];
   int ns = 0, so = 0;        // DIV_MUT_PROB substitutions, applied last and in order
   if (W.th_div_site) { ns = W.b_nsub[r]; so = W.b_subofs[r]; }
-  if ((e[0] | e[1] | e[2] | e[3] | e[4] | ns) == 0) return;   // wave-uniform
+  int pofs[4] = {0, 0, 0, 0}, pcnt[4] = {0, 0, 0, 0}, np = 0;   // Poisson edits
+  if (W.pois_any)
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      pofs[k] = W.b_pofs[(int64_t)k * W.rcap + r];
+      pcnt[k] = W.b_pcnt[(int64_t)k * W.rcap + r];
+      np |= pcnt[k];
+    }
+  if ((e[0] | e[1] | e[2] | e[3] | e[4] | ns | np) == 0) return;   // wave-uniform
   const int len0 = W.b_len0[r], len = W.b_len[r];
   uint32_t* g32 = reinterpret_cast<uint32_t*>(W.b_genome + r * TAPE_SLOT);
   uint32_t* c32 = reinterpret_cast<uint32_t*>(child);
@@ -100,7 +117,7 @@ __device__ __forceinline__ void apply_edits_wave(const DevWorld& W, int64_t r, u
     for (int k = 0; k < 4; k++) {
       const int j = 4 * w + k;
       int val;
-      const int src = mut_source(j, e, nopc, val);
+      const int src = mut_source(j, e, nopc, val, W.b_subs, pofs, pcnt);
       const uint32_t v = val >= 0 ? (uint32_t)val : (uint32_t)child[src];
       word |= (j < len ? v : 0u) << (8 * k);
     }

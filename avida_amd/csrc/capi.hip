@@ -118,13 +118,22 @@ int setup_world(avgpu_world* w, int64_t n, bool test_buffers) {
   // DIV_MUT_PROB arena: three times the largest expected substitutions per
   // record plus 16 (offsets are int32); a fill past it is counted
   // (AVGPU_CNT_SUB_OVERFLOW), never written
-  if (c.div_mut_prob > 0.0) {
-    const double p = std::min(1.0, c.div_mut_prob);
-    int64_t k = (int64_t)std::ceil(AVGPU_MAX_GENOME * p * 3.0) + 16;
+  const double pmeans[4] = {c.divide_poisson_slip_mean, c.divide_poisson_mut_mean,
+                            c.divide_poisson_ins_mean, c.divide_poisson_del_mean};
+  const bool pois = pmeans[0] > 0.0 || pmeans[1] > 0.0 || pmeans[2] > 0.0 || pmeans[3] > 0.0;
+  if (c.div_mut_prob > 0.0 || pois) {
+    int64_t k = 16;
+    if (c.div_mut_prob > 0.0) k += (int64_t)std::ceil(AVGPU_MAX_GENOME * std::min(1.0, c.div_mut_prob) * 3.0);
+    for (int q = 0; q < 4; q++)      // Poisson edits: 3x the mean + 16 per kind
+      if (pmeans[q] > 0.0) k += (int64_t)std::ceil(3.0 * std::min(pmeans[q], 4096.0)) + 16;
     k = std::min<int64_t>(k, (int64_t)INT32_MAX / R);
     W.scap = R * k;
-    A(b_nsub, R); A(b_subofs, R); A(b_subs, W.scap);
+    A(b_subs, W.scap);
+    if (c.div_mut_prob > 0.0) { A(b_nsub, R); A(b_subofs, R); }
+    if (pois) { A(b_pofs, 4 * R); A(b_pcnt, 4 * R); }
   }
+  W.pois_any = pois ? 1 : 0;
+  for (int q = 0; q < 4; q++) W.pois_L[q] = pmeans[q] > 0.0 ? std::exp(-pmeans[q]) : 0.0;
   A(b_merit, R);
   A(b_fitness, R); A(b_gen, R); A(b_ccopied, R); A(b_exec, R);
   A(b_gest, R); A(b_ltask, AVGPU_NUM_LOGIC_TASKS * R); A(b_rng, 3 * R); A(b_target, R); A(b_state, R);
@@ -209,8 +218,14 @@ avgpu_world* create_world(const avgpu_cfg* cfg, int device, int64_t n, bool test
     fail(AVGPU_EUNSUPPORTED, "COPY_INS_PROB / COPY_DEL_PROB are not on the GPU path yet");
     return nullptr;
   }
-  if (cfg->divide_slip_prob > 0.0 && cfg->slip_fill_mode != 0 && cfg->slip_fill_mode != 4) {
+  if ((cfg->divide_slip_prob > 0.0 || cfg->divide_poisson_slip_mean > 0.0) && cfg->slip_fill_mode != 0 &&
+      cfg->slip_fill_mode != 4) {
     fail(AVGPU_EUNSUPPORTED, "SLIP_FILL_MODE 1-3 (nop-X, random, scrambled) are not on the GPU path");
+    return nullptr;
+  }
+  if (cfg->divide_poisson_slip_mean > 700.0 || cfg->divide_poisson_mut_mean > 700.0 ||
+      cfg->divide_poisson_ins_mean > 700.0 || cfg->divide_poisson_del_mean > 700.0) {
+    fail(AVGPU_EUNSUPPORTED, "DIVIDE_POISSON_*_MEAN above 700 (exp(-mean) underflows)");
     return nullptr;
   }
   if (cfg->divide_method != 1) {

@@ -146,6 +146,11 @@ struct DevWorld {
   int32_t* b_subofs;  // [rcap]
   int32_t* b_subs;    // [scap]
   int64_t scap;
+  // DIVIDE_POISSON_{SLIP,MUT,INS,DEL}_MEAN's edits of record r (read only when
+  // pois_any): kind k's b_pcnt[k][r] edit words from b_subs[b_pofs[k][r]],
+  // applied right after the fixed slot of the same kind
+  int32_t* b_pofs;    // [4][rcap]
+  int32_t* b_pcnt;    // [4][rcap]
   double* b_merit;    // [rcap]
   double* b_fitness;  // [rcap]
   int32_t* b_gen;     // [rcap]
@@ -224,6 +229,8 @@ struct DevWorld {
   double p_div_site;
   uint64_t th_par_site;   // PARENT_MUT_PROB (per-site substitutions in the parent)
   double p_par_site;
+  double pois_L[4];       // exp(-DIVIDE_POISSON_{SLIP,MUT,INS,DEL}_MEAN), 0 = off
+  int32_t pois_any;
   int32_t slip_fill_mode;
   // RECORDED mode (avgpu_set_rng_mode): rec_n doubles; rec_off[c] = the start
   // of cell c's organism's segment, -1 = a counter stream.  rec == nullptr:

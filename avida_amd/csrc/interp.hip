@@ -850,6 +850,7 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
         const int exe = wave_sum_i32(ne), cop = wave_sum_i32(nc);
         int okw = 0, rec = -1, len = 0, e0 = 0, e1 = 0, e2 = 0, e3 = 0, e4 = 0;   // edits: slip mut ins del uniform
         int nsub = 0, sofs = 0;   // DIV_MUT_PROB substitutions in b_subs
+        int pcnt[4] = {0, 0, 0, 0}, pofs[4] = {0, 0, 0, 0};   // Poisson edits in b_subs
         if (lane == L) {
           // The world parameters and phenotype arrays this block uses, loaded
           // together and made opaque (OPQ): the asm stores below are
@@ -931,24 +932,84 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
               OPQ(t_slip); OPQ(t_mut); OPQ(t_ins); OPQ(t_del);
               if (!DEF) OPQ(t_uni);
               OPQ(q_slip); OPQ(q_mut); OPQ(q_ins); OPQ(q_del); OPQ(q_uni); OPQ(g_max); OPQ(g_min);
+              // NumDividePoisson* (main/cMutationRates.h:137-144; Apto's
+              // GetRandPoisson restated as in the oracle: multiply uniforms
+              // until the product falls below exp(-mean)), each kind's edits
+              // right after its one-shot test, in an arena segment (WORLD)
+              const bool pois = !DEF && W.pois_any;
+              auto draw_u = [&]() -> double {
+                if (REC && rbase) return rd();
+                return (double)rng_next(klo, khi, kct) * 2.3283064365386963e-10;
+              };
+              auto npois = [&](int k) -> int {
+                const double Lk = W.pois_L[k];
+                if (!(Lk > 0.0)) return 0;
+                double x = draw_u();
+                int n = 0;
+                while (x >= Lk && n < 4096) { x = __dmul_rn(x, draw_u()); n++; }
+                if (n && mode == AVGPU_MODE_WORLD) pofs[k] = atomicAdd(W.b_count + 2, n);
+                return n;
+              };
+              auto pput = [&](int k, int i, int ew) {
+                if (mode == AVGPU_MODE_WORLD && (int64_t)pofs[k] + i < W.scap) W.b_subs[pofs[k] + i] = ew;
+              };
               if (draw_p(t_slip, q_slip)) {          // doSlipMutation :621-694
                 const int from = (int)draw_below((uint32_t)len + 1u);
                 const int to = from == 0 ? (int)draw_below((uint32_t)len) : (int)draw_below((uint32_t)len + 1u);
                 e0 = edit_word(E_SLIP, from, to);
                 len += from - to;
               }
+              if (pois) {                            // Poisson slips :318-320
+                const int n = npois(0);
+                for (int i = 0; i < n; i++) {
+                  const int from = (int)draw_below((uint32_t)len + 1u);
+                  const int to = from == 0 ? (int)draw_below((uint32_t)len) : (int)draw_below((uint32_t)len + 1u);
+                  pput(0, i, edit_word(E_SLIP, from, to));
+                  len += from - to;
+                }
+                pcnt[0] = n;
+              }
               if (draw_p(t_mut, q_mut)) {
                 const int line = (int)draw_below((uint32_t)len);
                 e1 = edit_word(E_POINT, line, rand_code());
+              }
+              if (pois) {                            // Poisson substitutions :383-391
+                const int n = npois(1);
+                for (int i = 0; i < n; i++) {
+                  const int line = (int)draw_below((uint32_t)len);
+                  pput(1, i, edit_word(E_POINT, line, rand_code()));
+                }
+                pcnt[1] = n;
               }
               if (draw_p(t_ins, q_ins) && len < g_max) {
                 const int line = (int)draw_below((uint32_t)len + 1u);
                 e2 = edit_word(E_INS, line, rand_code());
                 len++;
               }
+              if (pois) {                            // Poisson insertions :404-413
+                const int n = npois(2);
+                int used = 0;
+                for (int i = 0; i < n && len < g_max; i++) {
+                  const int line = (int)draw_below((uint32_t)len + 1u);
+                  pput(2, i, edit_word(E_INS, line, rand_code()));
+                  len++;
+                  used++;
+                }
+                pcnt[2] = used;
+              }
               if (draw_p(t_del, q_del) && len > g_min) {
                 e3 = edit_word(E_DEL, (int)draw_below((uint32_t)len), 0);
                 len--;
+              }
+              if (pois) {                            // Poisson deletions :426-435
+                const int n = npois(3);
+                int used = 0;
+                for (int i = 0; i < n && len > g_min; i++) {
+                  pput(3, i, edit_word(E_DEL, (int)draw_below((uint32_t)len), 0));
+                  len--;
+                  used++;
+                }
+                pcnt[3] = used;
               }
               if (t_uni && draw_p(t_uni, q_uni)) {   // doUniformMutation :572-595
                 const int mut = (int)draw_below((uint32_t)(2 * k_n_ops + 1));
@@ -980,6 +1041,12 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
                   nsub = 0;
                 }
               }
+              if (pois && mode == AVGPU_MODE_WORLD)
+                for (int k = 0; k < 4; k++)
+                  if ((int64_t)pofs[k] + pcnt[k] > W.scap) {
+                    count_add(W, CNT_SUB_OVERFLOW, (unsigned long long)pcnt[k]);
+                    pcnt[k] = 0;
+                  }
               // Parent Substitution Mutations (per site) (cpu/cHardwareBase.cc:508-520)
               // on the parent's sites [0, div) in this lane's LDS tape, code
               // bits only (the flags are cleared below)
@@ -1045,6 +1112,11 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
                   W.b_nsub[rec] = nsub;
                   W.b_subofs[rec] = sofs;
                 }
+                if (!DEF && W.pois_any)
+                  for (int k = 0; k < 4; k++) {
+                    W.b_pofs[(int64_t)k * rcap + rec] = pofs[k];
+                    W.b_pcnt[(int64_t)k * rcap + rec] = pcnt[k];
+                  }
                 st_async_u64(b_merit + rec, (uint64_t)__double_as_longlong(merit));
                 st_async_u64(b_fitness + rec, (uint64_t)__double_as_longlong(fit));
                 st_async_u32(b_gen + rec, (uint32_t)gen);
@@ -1489,7 +1561,7 @@ bool class_timing_all() {
 static bool def_knobs(const DevWorld& W) {
   return W.alloc_method != 2 && W.require_allocate == 1 && W.max_label_exe == 1 && W.cfg_min_genome == 0 &&
          W.cfg_max_genome == 0 && W.merit_default_bonus == 0.0 && W.inherit_merit == 1 &&
-         W.base_merit_method == 4 && W.th_div_uni == 0 && W.th_div_site == 0 && W.th_par_site == 0 && W.size_range == 2.0 && W.min_exe_lines == 0.5 &&
+         W.base_merit_method == 4 && W.th_div_uni == 0 && W.th_div_site == 0 && W.th_par_site == 0 && !W.pois_any && W.size_range == 2.0 && W.min_exe_lines == 0.5 &&
          W.min_copied_lines == 0.5 && W.required_bonus == 0.0 && W.default_bonus == 1.0 && W.rand_total <= 256;
 }
 

@@ -150,6 +150,12 @@ typedef struct avgpu_cfg {
   double parent_mut_prob;          /* PARENT_MUT_PROB: per-site substitutions in the parent's
                                       memory (cut to the divide point) after the offspring's
                                       mutations (cpu/cHardwareBase.cc:508-520) */
+  /* DIVIDE_POISSON_{SLIP,MUT,INS,DEL}_MEAN: Poisson-distributed numbers of
+   * slips / substitutions / insertions / deletions on divide, each right after
+   * its one-shot test (cpu/cHardwareBase.cc:318-320, :383-391, :404-413,
+   * :426-435; main/cMutationRates.h:137-144); means above 700 are refused */
+  double divide_poisson_slip_mean, divide_poisson_mut_mean;
+  double divide_poisson_ins_mean, divide_poisson_del_mean;
 } avgpu_cfg;
 
 /* One REACTION line of environment.cfg (main/cEnvironment.cc:1185-1211,

@@ -80,6 +80,21 @@ struct Stream {
     if (rec) { const uint32_t v = (uint32_t)(rd() * (double)n); return v < n ? v : n - 1; }
     return (uint32_t)(((uint64_t)next() * n) >> 32);
   }
+  // a uniform double: the recorded value, or the counter draw times 2^-32
+  double u() {
+    if (rec) return rd();
+    return (double)next() * 2.3283064365386963e-10;
+  }
+  // Apto::RNG::GetRandPoisson(mean) (Apto is absent; restated as the classic
+  // product-of-uniforms method of Avida's own cRandom: multiply uniforms until
+  // the product falls below exp(-mean), capped at 4096 events); L = exp(-mean)
+  // is computed once by the host (the device gets the same double)
+  uint32_t poisson(double L) {
+    double x = u();
+    uint32_t k = 0;
+    while (x >= L && k < 4096) { x = x * u(); k++; }
+    return k;
+  }
   // Apto::RNG::P(p): u < p
   bool p(const Prob& q) {
     if (rec) return rd() < q.p;
@@ -231,6 +246,7 @@ struct World {
   Prob p_div_mut, p_div_ins, p_div_del, p_div_slip, p_div_uni;
   Prob p_div_site;           // DIV_MUT_PROB (per-site substitutions on divide)
   Prob p_par_site;           // PARENT_MUT_PROB (per-site substitutions in the parent)
+  double pois_L[4] = {0, 0, 0, 0};   // exp(-DIVIDE_POISSON_{SLIP,MUT,INS,DEL}_MEAN); 0 = off
   std::vector<double> rec;   // RECORDED mode: the host's stream (organisms point into it)
   // batch world
   std::vector<Birth> births;
@@ -468,8 +484,15 @@ struct Exec {
     Stream& r = o.rng;
     int max_g = w.cfg.max_genome_size; if (!max_g || max_g > AVGPU_MAX_GENOME) max_g = AVGPU_MAX_GENOME;
     int min_g = w.cfg.min_genome_size; if (!min_g || min_g < AVGPU_MIN_GENOME) min_g = AVGPU_MIN_GENOME;
+    // NumDividePoisson* draws only at a non-zero mean (main/cMutationRates.h:137-144)
+    auto npois = [&](int k) -> uint32_t { return w.pois_L[k] > 0.0 ? r.poisson(w.pois_L[k]) : 0u; };
     if (r.p(w.p_div_slip)) slip_mutation(child, r);
+    for (uint32_t i = 0, n = npois(0); i < n; i++) slip_mutation(child, r);   // :318-320
     if (r.p(w.p_div_mut)) {
+      uint32_t line = r.uint_below((uint32_t)child.size());
+      child[line] = (uint8_t)w.is.random_inst(r);
+    }
+    for (uint32_t i = 0, n = npois(1); i < n; i++) {                         // :383-391
       uint32_t line = r.uint_below((uint32_t)child.size());
       child[line] = (uint8_t)w.is.random_inst(r);
     }
@@ -477,7 +500,17 @@ struct Exec {
       uint32_t line = r.uint_below((uint32_t)child.size() + 1);
       child.insert(child.begin() + line, (uint8_t)w.is.random_inst(r));
     }
+    for (uint32_t i = 0, n = npois(2); i < n; i++) {                         // :404-413
+      if ((int)child.size() >= max_g) break;
+      uint32_t line = r.uint_below((uint32_t)child.size() + 1);
+      child.insert(child.begin() + line, (uint8_t)w.is.random_inst(r));
+    }
     if (r.p(w.p_div_del) && (int)child.size() > min_g) {
+      uint32_t line = r.uint_below((uint32_t)child.size());
+      child.erase(child.begin() + line);
+    }
+    for (uint32_t i = 0, n = npois(3); i < n; i++) {                         // :426-435
+      if ((int)child.size() <= min_g) break;
       uint32_t line = r.uint_below((uint32_t)child.size());
       child.erase(child.begin() + line);
     }
@@ -1016,6 +1049,11 @@ void* orc_create(const avgpu_cfg* cfg, int64_t ncells) {
   w->p_div_uni = make_prob(cfg->divide_uniform_prob);
   w->p_div_site = make_prob(cfg->div_mut_prob);
   w->p_par_site = make_prob(cfg->parent_mut_prob);
+  {
+    const double means[4] = {cfg->divide_poisson_slip_mean, cfg->divide_poisson_mut_mean,
+                             cfg->divide_poisson_ins_mean, cfg->divide_poisson_del_mean};
+    for (int k = 0; k < 4; k++) w->pois_L[k] = means[k] > 0.0 ? std::exp(-means[k]) : 0.0;
+  }
   memset(&w->stats, 0, sizeof(w->stats));
   derive_key((uint32_t)cfg->seed, (uint32_t)(cfg->seed >> 32), 0x5CEDu, 0xC0FFEEu,
              &w->global_rng.lo, &w->global_rng.hi);

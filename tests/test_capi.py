@@ -71,7 +71,7 @@ def test_unsupported_mutation_knobs_are_refused(golden, tmp_path):
     """A reference avida.cfg that sets a mutation knob this path does not
     implement is refused, not run with different semantics (capi.UNSUPPORTED_NONZERO)."""
     from avida_amd import files
-    for key in ["DIV_INS_PROB", "PARENT_INS_PROB", "DIVIDE_POISSON_MUT_MEAN", "COPY_SLIP_PROB",
+    for key in ["DIV_INS_PROB", "PARENT_INS_PROB", "DIVIDE_POISSON_TRANS_MEAN", "COPY_SLIP_PROB",
                 "COPY_UNIFORM_PROB", "DIVIDE_TRANS_PROB"]:
         with pytest.raises(ValueError, match=key):
             capi.cfg_from_avida(files.read_avida_cfg(None, {key: 0.01}))

@@ -102,8 +102,33 @@ def test_recorded_draws_parent_mutations(golden):
     assert [i for i in range(100) if ops[i] != anc[i]] == [37]
 
 
+def test_recorded_draws_poisson_divide_mutations(golden):
+    """DIVIDE_POISSON_{SLIP,MUT,INS,DEL}_MEAN = 1 (cpu/cHardwareBase.cc:318-320,
+    :383-435): at u = 0.37 every Poisson count is 1 (0.37 >= exp(-1), then
+    0.37^2 < exp(-1): two uniforms), each right after its one-shot test --
+    slip 1 + 2 + (from, to) 2, mut 1 + 2 + (line, inst) 2, ins 1 + 2 + 2,
+    del 1 + 2 + (line) 1 = 19 draws at the first divide."""
+    iset, env, cfg, anc = _ancestor(golden, {"COPY_MUT_PROB": 0.0, "DIVIDE_INS_PROB": 0.0,
+                                             "DIVIDE_DEL_PROB": 0.0, "DEATH_METHOD": 0,
+                                             "DIVIDE_POISSON_SLIP_MEAN": 1.0,
+                                             "DIVIDE_POISSON_MUT_MEAN": 1.0,
+                                             "DIVIDE_POISSON_INS_MEAN": 1.0,
+                                             "DIVIDE_POISSON_DEL_MEAN": 1.0})
+    b = ol.Backend("oracle", cfg, iset, env, ncells=1)
+    b.set_orgs(0, [anc], deterministic=True)
+    b.set_rng_mode(capi.RNG_RECORDED, np.full(4096, 0.37))
+    for k in range(2000):
+        b.step(0, 1, uniform=1, mode=capi.MODE_FROZEN)
+        st, _, _ = b.states(0, 1, CAP)
+        if st[0].num_divides:
+            break
+    assert st[0].num_divides == 1
+    assert st[0].rng_counter == 19
+    assert b.lib.orc_rec_exhausted() == 0
+
+
 @pytest.mark.gpu
-@pytest.mark.parametrize("muts", ["copy", "all", "site"])
+@pytest.mark.parametrize("muts", ["copy", "all", "site", "poisson"])
 def test_recorded_stream_frozen_traces_gpu(golden, muts):
     """BASELINE configs[2] traces with mutations on, fed from one recorded
     stream: 3600 organisms of the detail-50000 population, each with its own
@@ -116,6 +141,9 @@ def test_recorded_stream_frozen_traces_gpu(golden, muts):
         ov.update({"DIVIDE_MUT_PROB": 0.1, "DIVIDE_SLIP_PROB": 0.05, "DIVIDE_UNIFORM_PROB": 0.05})
     if muts == "site":      # per-site divide substitutions: one draw per offspring site
         ov.update({"DIV_MUT_PROB": 0.02, "PARENT_MUT_PROB": 0.01})
+    if muts == "poisson":
+        ov.update({"DIVIDE_POISSON_SLIP_MEAN": 0.3, "DIVIDE_POISSON_MUT_MEAN": 1.5,
+                   "DIVIDE_POISSON_INS_MEAN": 0.8, "DIVIDE_POISSON_DEL_MEAN": 0.8})
     iset, env, cfg = pu.load_env(golden, "instset-classic.cfg", ov)
     n = len(genomes)
     rng = np.random.default_rng(42)
@@ -163,13 +191,18 @@ def test_divide_slip_uniform_world_gpu(golden, fill):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("knob", ["DIV_MUT_PROB", "PARENT_MUT_PROB"])
+@pytest.mark.parametrize("knob", ["DIV_MUT_PROB", "PARENT_MUT_PROB", "POISSON"])
 def test_per_site_divide_mutations_world_gpu(golden, knob):
     """World updates with DIV_MUT_PROB (per-site substitutions in the
     offspring, cpu/cHardwareBase.cc:447-460) or PARENT_MUT_PROB (in the
     parent, :508-520) on top of the default mutations: GPU world == oracle
-    world, every cell digest, 120 updates; the substitution arena never fills."""
+    world, every cell digest, 120 updates; the substitution arena never fills.
+    POISSON: the four DIVIDE_POISSON_*_MEAN knobs (:318-320, :383-435)."""
     ov = {knob: 0.02, "WORLD_X": 48, "WORLD_Y": 48}
+    if knob == "POISSON":
+        ov = {"DIVIDE_POISSON_SLIP_MEAN": 0.1, "DIVIDE_POISSON_MUT_MEAN": 1.0,
+              "DIVIDE_POISSON_INS_MEAN": 0.5, "DIVIDE_POISSON_DEL_MEAN": 0.5,
+              "WORLD_X": 48, "WORLD_Y": 48}
     iset, env, cfg, anc = _ancestor(golden, ov)
     n = 48 * 48
     pair = [ol.Backend(k, cfg, iset, env, ncells=n) for k in ("oracle", "gpu")]

@@ -62,10 +62,13 @@ def test_serial_world_from_ancestor(golden):
 def test_serial_world_dense_population(golden):
     """The bench's evolved logic-9 population (detail-50000.pop, classic
     instset) filling a 60x60 torus, with the divide slip, uniform and
-    per-site (DIV_MUT_PROB, PARENT_MUT_PROB) mutations on as well: 4 serial updates (~430k picks)."""
+    per-site (DIV_MUT_PROB, PARENT_MUT_PROB) and Poisson mutations on as well: 4 serial updates (~430k picks)."""
     iset, env, cfg = pu.load_env(golden, "instset-classic.cfg", seed=5,
                                  overrides={"DIVIDE_SLIP_PROB": 0.05, "DIVIDE_UNIFORM_PROB": 0.02,
-                                            "DIV_MUT_PROB": 0.005, "PARENT_MUT_PROB": 0.002})
+                                            "DIV_MUT_PROB": 0.005, "PARENT_MUT_PROB": 0.002,
+                                            "DIVIDE_POISSON_MUT_MEAN": 0.5,
+                                            "DIVIDE_POISSON_INS_MEAN": 0.2,
+                                            "DIVIDE_POISSON_DEL_MEAN": 0.2})
     n = cfg.world_x * cfg.world_y
     genomes = pu.pop_genomes(golden, iset)[:n]
     orc = ol.Backend("oracle", cfg, iset, env, ncells=n)

@@ -53,6 +53,8 @@ class AvgpuCfg(C.Structure):
         ("div_mut_prob", C.c_double), ("parent_mut_prob", C.c_double),
         ("divide_poisson_slip_mean", C.c_double), ("divide_poisson_mut_mean", C.c_double),
         ("divide_poisson_ins_mean", C.c_double), ("divide_poisson_del_mean", C.c_double),
+        ("div_ins_prob", C.c_double), ("div_del_prob", C.c_double),
+        ("div_uniform_prob", C.c_double), ("div_slip_prob", C.c_double),
     ]
 
 
@@ -165,17 +167,15 @@ EXPORTED = [
 
 
 # avida.cfg knobs that change the semantics of this path when non-zero and
-# that it does not implement (main/cAvidaConfig.h:309-361, 372): the per-site
-# (other than DIV_MUT_PROB's and PARENT_MUT_PROB's substitutions), the
-# Poisson translocation / LGT,
-# translocation, lateral-transfer, parent ins / del, point, inject and meta
-# mutations, copy uniform / slip, death on divide.  cfg_from_avida refuses a
-# config that sets any of them rather than run it with different semantics.
-# (COPY_INS_PROB / COPY_DEL_PROB travel in avgpu_cfg; avgpu_create refuses them.)
+# that it does not implement (main/cAvidaConfig.h:309-361, 372): translocation
+# and lateral-transfer mutations (one-shot, Poisson and per-site), parent
+# insertions / deletions, point, inject and meta mutations, copy uniform /
+# slip, death on divide.  cfg_from_avida refuses a config that sets any of
+# them rather than run it with different semantics.  (COPY_INS_PROB /
+# COPY_DEL_PROB travel in avgpu_cfg; avgpu_create refuses them.)
 UNSUPPORTED_NONZERO = [
     "COPY_UNIFORM_PROB", "COPY_SLIP_PROB",
     "POINT_MUT_PROB", "POINT_INS_PROB", "POINT_DEL_PROB", "INST_POINT_MUT_PROB",
-    "DIV_INS_PROB", "DIV_DEL_PROB", "DIV_UNIFORM_PROB", "DIV_SLIP_PROB",
     "DIV_TRANS_PROB", "DIV_LGT_PROB",
     "DIVIDE_TRANS_PROB", "DIVIDE_LGT_PROB",
     "DIVIDE_POISSON_TRANS_MEAN", "DIVIDE_POISSON_LGT_MEAN",
@@ -255,6 +255,10 @@ def cfg_from_avida(cfg, seed=None) -> AvgpuCfg:
     c.divide_poisson_mut_mean = float(g("DIVIDE_POISSON_MUT_MEAN", 0.0))
     c.divide_poisson_ins_mean = float(g("DIVIDE_POISSON_INS_MEAN", 0.0))
     c.divide_poisson_del_mean = float(g("DIVIDE_POISSON_DEL_MEAN", 0.0))
+    c.div_ins_prob = float(g("DIV_INS_PROB", 0.0))
+    c.div_del_prob = float(g("DIV_DEL_PROB", 0.0))
+    c.div_uniform_prob = float(g("DIV_UNIFORM_PROB", 0.0))
+    c.div_slip_prob = float(g("DIV_SLIP_PROB", 0.0))
     return c
 
 

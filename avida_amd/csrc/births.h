@@ -43,8 +43,8 @@ __device__ __forceinline__ int neighbours(const DevWorld& W, int cell, int* out)
 // interpreter in the reference's order and stored with the birth record
 // (interp.hip): one wave per queued offspring that has any rewrites its
 // genome -- site j of the mutated child is traced back through the edits
-// (last first) to a site of the unmutated child or to a value an edit wrote;
-// DIV_MUT_PROB's substitutions (b_subs) overwrite their sites after that.
+// (last first, the variable-count segments in b_subs included) to a site of
+// the unmutated child or to a value an edit wrote.
 // Runs before placement, so halo records and activation see final genomes.
 // one edit word undone: site src of the genome after the edit -> the site it
 // came from before it, or the value the edit wrote (val >= 0)
@@ -62,17 +62,20 @@ __device__ __forceinline__ void edit_back(int ew, bool nopc, int& src, int& val)
     else if (src >= a) src = b + (src - a);
   }
 }
-// applied order: e0, Poisson slips, e1, Poisson substitutions, e2, Poisson
-// insertions, e3, Poisson deletions, e4 (pcnt[k] words at subs + pofs[k])
+// applied order (device.h SEG_*): e0, segments 0-1, e1, segment 2, e2,
+// segment 3, e3, segment 4, e4, segments 5-8 (pcnt[k] words at subs + pofs[k])
 __device__ __forceinline__ int mut_source(int j, const int* e, bool nopc, int& val, const int32_t* subs,
                                           const int* pofs, const int* pcnt) {
+  constexpr int first[5] = {SEG_PSLIP, SEG_PMUT, SEG_PINS, SEG_PDEL, SEG_SMUT};
+  constexpr int last[5] = {SEG_SSLIP, SEG_PMUT, SEG_PINS, SEG_PDEL, SEG_SUNI};
   int src = j;
   val = -1;
 #pragma unroll
   for (int k = 4; k >= 0; k--) {
+#pragma unroll
+    for (int g = last[k]; g >= first[k]; g--)
+      for (int i = pcnt[g] - 1; i >= 0 && val < 0; i--) edit_back(subs[pofs[g] + i], nopc, src, val);
     edit_back(e[k], nopc, src, val);
-    if (k > 0)
-      for (int i = pcnt[k - 1] - 1; i >= 0 && val < 0; i--) edit_back(subs[pofs[k - 1] + i], nopc, src, val);
   }
   return src;
 }
@@ -95,17 +98,14 @@ __device__ __forceinline__ void apply_edits_wave(const DevWorld& W, int64_t r, u
   int e[5];
 #pragma unroll
   for (int k = 0; k < 5; k++) e[k] = W.b_edit[(int64_t)k * W.rcap + r];
-  int ns = 0, so = 0;        // DIV_MUT_PROB substitutions, applied last and in order
-  if (W.th_div_site) { ns = W.b_nsub[r]; so = W.b_subofs[r]; }
-  int pofs[4] = {0, 0, 0, 0}, pcnt[4] = {0, 0, 0, 0}, np = 0;   // Poisson edits
-  if (W.pois_any)
+  int pofs[NSEG], pcnt[NSEG], np = 0;   // variable-count edit segments
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
-      pofs[k] = W.b_pofs[(int64_t)k * W.rcap + r];
-      pcnt[k] = W.b_pcnt[(int64_t)k * W.rcap + r];
-      np |= pcnt[k];
-    }
-  if ((e[0] | e[1] | e[2] | e[3] | e[4] | ns | np) == 0) return;   // wave-uniform
+  for (int k = 0; k < NSEG; k++) {
+    pofs[k] = W.seg_any ? W.b_pofs[(int64_t)k * W.rcap + r] : 0;
+    pcnt[k] = W.seg_any ? W.b_pcnt[(int64_t)k * W.rcap + r] : 0;
+    np |= pcnt[k];
+  }
+  if ((e[0] | e[1] | e[2] | e[3] | e[4] | np) == 0) return;   // wave-uniform
   const int len0 = W.b_len0[r], len = W.b_len[r];
   uint32_t* g32 = reinterpret_cast<uint32_t*>(W.b_genome + r * TAPE_SLOT);
   uint32_t* c32 = reinterpret_cast<uint32_t*>(child);
@@ -120,14 +120,6 @@ __device__ __forceinline__ void apply_edits_wave(const DevWorld& W, int64_t r, u
       const int src = mut_source(j, e, nopc, val, W.b_subs, pofs, pcnt);
       const uint32_t v = val >= 0 ? (uint32_t)val : (uint32_t)child[src];
       word |= (j < len ? v : 0u) << (8 * k);
-    }
-    for (int i = 0; i < ns; i++) {       // later substitutions of one site win
-      const int sub = W.b_subs[so + i];
-      const int site = sub & 0xFFFF;
-      if ((site >> 2) == w) {
-        const int sh = 8 * (site & 3);
-        word = (word & ~(0xFFu << sh)) | ((uint32_t)(sub >> 16) << sh);
-      }
     }
     g32[w] = word;
   }

@@ -120,18 +120,23 @@ int setup_world(avgpu_world* w, int64_t n, bool test_buffers) {
   // (AVGPU_CNT_SUB_OVERFLOW), never written
   const double pmeans[4] = {c.divide_poisson_slip_mean, c.divide_poisson_mut_mean,
                             c.divide_poisson_ins_mean, c.divide_poisson_del_mean};
+  const double psite[5] = {c.div_mut_prob, c.div_ins_prob, c.div_del_prob, c.div_uniform_prob, c.div_slip_prob};
   const bool pois = pmeans[0] > 0.0 || pmeans[1] > 0.0 || pmeans[2] > 0.0 || pmeans[3] > 0.0;
-  if (c.div_mut_prob > 0.0 || pois) {
+  bool site = false;
+  for (int q = 0; q < 5; q++) site = site || psite[q] > 0.0;
+  if (pois || site) {
+    // arena words per record: 3x the largest expected count of each kind
+    // (per site: a 2048-site offspring) + 16 each; offsets are int32
     int64_t k = 16;
-    if (c.div_mut_prob > 0.0) k += (int64_t)std::ceil(AVGPU_MAX_GENOME * std::min(1.0, c.div_mut_prob) * 3.0);
-    for (int q = 0; q < 4; q++)      // Poisson edits: 3x the mean + 16 per kind
+    for (int q = 0; q < 5; q++)
+      if (psite[q] > 0.0) k += (int64_t)std::ceil(AVGPU_MAX_GENOME * std::min(1.0, psite[q]) * 3.0) + 16;
+    for (int q = 0; q < 4; q++)
       if (pmeans[q] > 0.0) k += (int64_t)std::ceil(3.0 * std::min(pmeans[q], 4096.0)) + 16;
     k = std::min<int64_t>(k, (int64_t)INT32_MAX / R);
     W.scap = R * k;
-    A(b_subs, W.scap);
-    if (c.div_mut_prob > 0.0) { A(b_nsub, R); A(b_subofs, R); }
-    if (pois) { A(b_pofs, 4 * R); A(b_pcnt, 4 * R); }
+    A(b_subs, W.scap); A(b_pofs, NSEG * R); A(b_pcnt, NSEG * R);
   }
+  W.seg_any = (pois || site) ? 1 : 0;
   W.pois_any = pois ? 1 : 0;
   for (int q = 0; q < 4; q++) W.pois_L[q] = pmeans[q] > 0.0 ? std::exp(-pmeans[q]) : 0.0;
   A(b_merit, R);
@@ -184,6 +189,10 @@ int setup_world(avgpu_world* w, int64_t n, bool test_buffers) {
   W.p_div_del = c.divide_del_prob; W.p_div_slip = c.divide_slip_prob; W.p_div_uni = c.divide_uniform_prob;
   W.th_div_site = th(c.div_mut_prob);
   W.p_div_site = c.div_mut_prob;
+  W.th_dsite[0] = th(c.div_ins_prob); W.p_dsite[0] = c.div_ins_prob;
+  W.th_dsite[1] = th(c.div_del_prob); W.p_dsite[1] = c.div_del_prob;
+  W.th_dsite[2] = th(c.div_uniform_prob); W.p_dsite[2] = c.div_uniform_prob;
+  W.th_dsite[3] = th(c.div_slip_prob); W.p_dsite[3] = c.div_slip_prob;
   W.th_par_site = th(c.parent_mut_prob);
   W.p_par_site = c.parent_mut_prob;
   W.slip_fill_mode = c.slip_fill_mode;
@@ -218,7 +227,8 @@ avgpu_world* create_world(const avgpu_cfg* cfg, int device, int64_t n, bool test
     fail(AVGPU_EUNSUPPORTED, "COPY_INS_PROB / COPY_DEL_PROB are not on the GPU path yet");
     return nullptr;
   }
-  if ((cfg->divide_slip_prob > 0.0 || cfg->divide_poisson_slip_mean > 0.0) && cfg->slip_fill_mode != 0 &&
+  if ((cfg->divide_slip_prob > 0.0 || cfg->divide_poisson_slip_mean > 0.0 || cfg->div_slip_prob > 0.0) &&
+      cfg->slip_fill_mode != 0 &&
       cfg->slip_fill_mode != 4) {
     fail(AVGPU_EUNSUPPORTED, "SLIP_FILL_MODE 1-3 (nop-X, random, scrambled) are not on the GPU path");
     return nullptr;

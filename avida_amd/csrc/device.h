@@ -138,19 +138,14 @@ struct DevWorld {
   int32_t* b_len;     // [rcap]  offspring length after the divide mutations
   int32_t* b_len0;    // [rcap]  the child's length before them (b_genome holds that child)
   int32_t* b_edit;    // [5][rcap] its divide-mutation edits (interp.hip edit_word; 0 = none)
-  // DIV_MUT_PROB's per-site substitutions of record r (only read when
-  // th_div_site != 0): b_nsub[r] entries from b_subs[b_subofs[r]], each
-  // site | code << 16, applied in order after the five edits; b_count[2] is
-  // the arena's fill of this update, scap its size
-  int32_t* b_nsub;    // [rcap]
-  int32_t* b_subofs;  // [rcap]
+  // variable-count divide-mutation edits of record r (only read when
+  // seg_any): segment k holds b_pcnt[k][r] edit words from
+  // b_subs[b_pofs[k][r]], applied at its place in Divide_DoMutations' order
+  // (SEG_* below); b_count[2] is the arena's fill of this update, scap its size
   int32_t* b_subs;    // [scap]
   int64_t scap;
-  // DIVIDE_POISSON_{SLIP,MUT,INS,DEL}_MEAN's edits of record r (read only when
-  // pois_any): kind k's b_pcnt[k][r] edit words from b_subs[b_pofs[k][r]],
-  // applied right after the fixed slot of the same kind
-  int32_t* b_pofs;    // [4][rcap]
-  int32_t* b_pcnt;    // [4][rcap]
+  int32_t* b_pofs;    // [NSEG][rcap]
+  int32_t* b_pcnt;    // [NSEG][rcap]
   double* b_merit;    // [rcap]
   double* b_fitness;  // [rcap]
   int32_t* b_gen;     // [rcap]
@@ -231,6 +226,9 @@ struct DevWorld {
   double p_par_site;
   double pois_L[4];       // exp(-DIVIDE_POISSON_{SLIP,MUT,INS,DEL}_MEAN), 0 = off
   int32_t pois_any;
+  uint64_t th_dsite[4];   // DIV_INS_PROB, DIV_DEL_PROB, DIV_UNIFORM_PROB, DIV_SLIP_PROB (per site)
+  double p_dsite[4];
+  int32_t seg_any;        // some variable-count kind is on (b_subs / b_pofs / b_pcnt allocated)
   int32_t slip_fill_mode;
   // RECORDED mode (avgpu_set_rng_mode): rec_n doubles; rec_off[c] = the start
   // of cell c's organism's segment, -1 = a counter stream.  rec == nullptr:
@@ -302,6 +300,11 @@ __host__ __device__ inline int64_t record_bytes(int x, int64_t arena) {
 #define CNT_HALO_SENT 18  /* offspring shipped to a neighbouring tile */
 #define CNT_HALO_LOST 19  /* offspring lost to a full halo arena (counted in DROPPED too) */
 #define CNT_REC_OVER 20   /* RECORDED draws past the end of the stream */
+// variable-count edit segments of a birth record, in the order applied:
+// e0 (slip), Poisson slips, per-site slips, e1 (mut), Poisson substitutions,
+// e2 (ins), Poisson insertions, e3 (del), Poisson deletions, e4 (uniform),
+// per-site substitutions, insertions, deletions, uniform mutations
+enum { SEG_PSLIP = 0, SEG_SSLIP, SEG_PMUT, SEG_PINS, SEG_PDEL, SEG_SMUT, SEG_SINS, SEG_SDEL, SEG_SUNI, NSEG };
 #define CNT_SUB_OVERFLOW 22   /* DIV_MUT_PROB substitutions that found the b_subs arena full (must stay 0) */
 #define CNT_OVERSIZE 21   /* offspring a slip grew past AVGPU_MAX_GENOME (counted in DROPPED too) */
 // 32..37: AVGPU_PHASE_CLOCKS loop cycles by block (decode, fast, copy, switch,

@@ -849,8 +849,7 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
         }
         const int exe = wave_sum_i32(ne), cop = wave_sum_i32(nc);
         int okw = 0, rec = -1, len = 0, e0 = 0, e1 = 0, e2 = 0, e3 = 0, e4 = 0;   // edits: slip mut ins del uniform
-        int nsub = 0, sofs = 0;   // DIV_MUT_PROB substitutions in b_subs
-        int pcnt[4] = {0, 0, 0, 0}, pofs[4] = {0, 0, 0, 0};   // Poisson edits in b_subs
+        int pcnt[NSEG] = {0}, pofs[NSEG] = {0};   // variable-count edit segments in b_subs (device.h)
         if (lane == L) {
           // The world parameters and phenotype arrays this block uses, loaded
           // together and made opaque (OPQ): the asm stores below are
@@ -936,6 +935,7 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
               // GetRandPoisson restated as in the oracle: multiply uniforms
               // until the product falls below exp(-mean)), each kind's edits
               // right after its one-shot test, in an arena segment (WORLD)
+              const bool segs = !DEF && W.seg_any;
               const bool pois = !DEF && W.pois_any;
               auto draw_u = [&]() -> double {
                 if (REC && rbase) return rd();
@@ -947,11 +947,39 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
                 double x = draw_u();
                 int n = 0;
                 while (x >= Lk && n < 4096) { x = __dmul_rn(x, draw_u()); n++; }
-                if (n && mode == AVGPU_MODE_WORLD) pofs[k] = atomicAdd(W.b_count + 2, n);
                 return n;
+              };
+              // GetRandBinomial(len, p): one P(p) per site (oracle binom)
+              auto nbinom = [&](uint64_t th, double p) -> int {
+                int n = 0;
+                for (int i = 0; i < len; i++) n += draw_p(th, p) ? 1 : 0;
+                return n;
+              };
+              // reserve n words of segment k / write its i-th edit (WORLD only)
+              auto preserve = [&](int k, int n) {
+                if (n > 0 && mode == AVGPU_MODE_WORLD) pofs[k] = atomicAdd(W.b_count + 2, n);
               };
               auto pput = [&](int k, int i, int ew) {
                 if (mode == AVGPU_MODE_WORLD && (int64_t)pofs[k] + i < W.scap) W.b_subs[pofs[k] + i] = ew;
+              };
+              auto slip_edit = [&]() -> int {   // doSlipMutation :621-694
+                const int from = (int)draw_below((uint32_t)len + 1u);
+                const int to = from == 0 ? (int)draw_below((uint32_t)len) : (int)draw_below((uint32_t)len + 1u);
+                len += from - to;
+                return edit_word(E_SLIP, from, to);
+              };
+              auto uniform_edit = [&]() -> int {   // doUniformMutation :572-595
+                const int mut = (int)draw_below((uint32_t)(2 * k_n_ops + 1));
+                int ew = 0;
+                if (mut < k_n_ops) {
+                  ew = edit_word(E_POINT, (int)draw_below((uint32_t)len), (int)tab_u8(rcode + mut));
+                } else if (mut == k_n_ops) {
+                  if (len != g_min) { ew = edit_word(E_DEL, (int)draw_below((uint32_t)len), 0); len--; }
+                } else if (len != g_max) {
+                  ew = edit_word(E_INS, (int)draw_below((uint32_t)len + 1u), (int)tab_u8(rcode + mut - k_n_ops - 1));
+                  len++;
+                }
+                return ew;
               };
               if (draw_p(t_slip, q_slip)) {          // doSlipMutation :621-694
                 const int from = (int)draw_below((uint32_t)len + 1u);
@@ -961,13 +989,15 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
               }
               if (pois) {                            // Poisson slips :318-320
                 const int n = npois(0);
-                for (int i = 0; i < n; i++) {
-                  const int from = (int)draw_below((uint32_t)len + 1u);
-                  const int to = from == 0 ? (int)draw_below((uint32_t)len) : (int)draw_below((uint32_t)len + 1u);
-                  pput(0, i, edit_word(E_SLIP, from, to));
-                  len += from - to;
-                }
-                pcnt[0] = n;
+                preserve(SEG_PSLIP, n);
+                for (int i = 0; i < n; i++) pput(SEG_PSLIP, i, slip_edit());
+                pcnt[SEG_PSLIP] = n;
+              }
+              if (segs && W.th_dsite[3]) {           // slips per site :323-327
+                const int n = nbinom(W.th_dsite[3], W.p_dsite[3]);
+                preserve(SEG_SSLIP, n);
+                for (int i = 0; i < n; i++) pput(SEG_SSLIP, i, slip_edit());
+                pcnt[SEG_SSLIP] = n;
               }
               if (draw_p(t_mut, q_mut)) {
                 const int line = (int)draw_below((uint32_t)len);
@@ -975,11 +1005,12 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
               }
               if (pois) {                            // Poisson substitutions :383-391
                 const int n = npois(1);
+                preserve(SEG_PMUT, n);
                 for (int i = 0; i < n; i++) {
                   const int line = (int)draw_below((uint32_t)len);
-                  pput(1, i, edit_word(E_POINT, line, rand_code()));
+                  pput(SEG_PMUT, i, edit_word(E_POINT, line, rand_code()));
                 }
-                pcnt[1] = n;
+                pcnt[SEG_PMUT] = n;
               }
               if (draw_p(t_ins, q_ins) && len < g_max) {
                 const int line = (int)draw_below((uint32_t)len + 1u);
@@ -988,14 +1019,15 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
               }
               if (pois) {                            // Poisson insertions :404-413
                 const int n = npois(2);
+                preserve(SEG_PINS, n);
                 int used = 0;
                 for (int i = 0; i < n && len < g_max; i++) {
                   const int line = (int)draw_below((uint32_t)len + 1u);
-                  pput(2, i, edit_word(E_INS, line, rand_code()));
+                  pput(SEG_PINS, i, edit_word(E_INS, line, rand_code()));
                   len++;
                   used++;
                 }
-                pcnt[2] = used;
+                pcnt[SEG_PINS] = used;
               }
               if (draw_p(t_del, q_del) && len > g_min) {
                 e3 = edit_word(E_DEL, (int)draw_below((uint32_t)len), 0);
@@ -1003,46 +1035,73 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
               }
               if (pois) {                            // Poisson deletions :426-435
                 const int n = npois(3);
+                preserve(SEG_PDEL, n);
                 int used = 0;
                 for (int i = 0; i < n && len > g_min; i++) {
-                  pput(3, i, edit_word(E_DEL, (int)draw_below((uint32_t)len), 0));
+                  pput(SEG_PDEL, i, edit_word(E_DEL, (int)draw_below((uint32_t)len), 0));
                   len--;
                   used++;
                 }
-                pcnt[3] = used;
+                pcnt[SEG_PDEL] = used;
               }
-              if (t_uni && draw_p(t_uni, q_uni)) {   // doUniformMutation :572-595
-                const int mut = (int)draw_below((uint32_t)(2 * k_n_ops + 1));
-                if (mut < k_n_ops) {
-                  e4 = edit_word(E_POINT, (int)draw_below((uint32_t)len), (int)tab_u8(rcode + mut));
-                } else if (mut == k_n_ops) {
-                  if (len != g_min) { e4 = edit_word(E_DEL, (int)draw_below((uint32_t)len), 0); len--; }
-                } else if (len != g_max) {
-                  e4 = edit_word(E_INS, (int)draw_below((uint32_t)len + 1u), (int)tab_u8(rcode + mut - k_n_ops - 1));
-                  len++;
-                }
-              }
-              // Divide Mutations (per site) (cpu/cHardwareBase.cc:447-460), only
-              // at a non-zero DIV_MUT_PROB: Binomial(len, p) as one P(p) per
-              // site (oracle divide_mutations), then a GetUInt(len) site and a
-              // GetRandomInst per substitution, kept in the b_subs arena (WORLD)
-              if (!DEF && W.th_div_site) {
-                const uint64_t t_site = W.th_div_site;
-                const double q_site = W.p_div_site;
-                for (int i = 0; i < len; i++) nsub += draw_p(t_site, q_site) ? 1 : 0;
-                if (nsub && mode == AVGPU_MODE_WORLD) sofs = atomicAdd(W.b_count + 2, nsub);
-                for (int i = 0; i < nsub; i++) {
+              if (t_uni && draw_p(t_uni, q_uni)) e4 = uniform_edit();
+              // the per-site kinds (cpu/cHardwareBase.cc:447-503), each only at
+              // a non-zero rate, in the reference's order: substitutions,
+              // insertions (all sites drawn, sorted, inserted from the highest
+              // down), deletions, uniform mutations
+              if (segs && W.th_div_site) {
+                const int n = nbinom(W.th_div_site, W.p_div_site);
+                preserve(SEG_SMUT, n);
+                for (int i = 0; i < n; i++) {
                   const int site = (int)draw_below((uint32_t)len);
-                  const int code = rand_code();
-                  if (mode == AVGPU_MODE_WORLD && (int64_t)sofs + i < W.scap) W.b_subs[sofs + i] = site | (code << 16);
+                  pput(SEG_SMUT, i, edit_word(E_POINT, site, rand_code()));
                 }
-                if (mode == AVGPU_MODE_WORLD && (int64_t)sofs + nsub > W.scap) {
-                  count_add(W, CNT_SUB_OVERFLOW, (unsigned long long)nsub);
-                  nsub = 0;
+                pcnt[SEG_SMUT] = n;
+              }
+              if (segs && W.th_dsite[0]) {
+                int n = nbinom(W.th_dsite[0], W.p_dsite[0]);
+                if (n + len > g_max) n = g_max - len;
+                if (n > 0) {
+                  preserve(SEG_SINS, n);
+                  const bool keep = mode == AVGPU_MODE_WORLD && (int64_t)pofs[SEG_SINS] + n <= W.scap;
+                  int32_t* seg = W.b_subs + pofs[SEG_SINS];
+                  for (int i = 0; i < n; i++) {
+                    const int site = (int)draw_below((uint32_t)len + 1u);
+                    if (keep) {                // insertion sort, highest first
+                      int j = i;
+                      while (j > 0 && seg[j - 1] < site) { seg[j] = seg[j - 1]; j--; }
+                      seg[j] = site;
+                    }
+                  }
+                  for (int i = 0; i < n; i++) {
+                    const int code = rand_code();
+                    if (keep) seg[i] = edit_word(E_INS, seg[i], code);
+                  }
+                  len += n;
+                  pcnt[SEG_SINS] = n;
                 }
               }
-              if (pois && mode == AVGPU_MODE_WORLD)
-                for (int k = 0; k < 4; k++)
+              if (segs && W.th_dsite[1]) {
+                int n = nbinom(W.th_dsite[1], W.p_dsite[1]);
+                if (len - n < g_min) n = len - g_min;
+                if (n > 0) {
+                  preserve(SEG_SDEL, n);
+                  for (int i = 0; i < n; i++) {
+                    pput(SEG_SDEL, i, edit_word(E_DEL, (int)draw_below((uint32_t)len), 0));
+                    len--;
+                  }
+                  pcnt[SEG_SDEL] = n;
+                }
+              }
+              if (segs && W.th_dsite[2]) {
+                const int n = nbinom(W.th_dsite[2], W.p_dsite[2]);
+                preserve(SEG_SUNI, n);
+                for (int i = 0; i < n; i++) pput(SEG_SUNI, i, uniform_edit());
+                pcnt[SEG_SUNI] = n;
+              }
+              if (segs && mode == AVGPU_MODE_WORLD)
+#pragma unroll
+                for (int k = 0; k < NSEG; k++)
                   if ((int64_t)pofs[k] + pcnt[k] > W.scap) {
                     count_add(W, CNT_SUB_OVERFLOW, (unsigned long long)pcnt[k]);
                     pcnt[k] = 0;
@@ -1108,12 +1167,9 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
                 st_async_u32(b_edit + 2 * rcap + rec, (uint32_t)e2);
                 st_async_u32(b_edit + 3 * rcap + rec, (uint32_t)e3);
                 st_async_u32(b_edit + 4 * rcap + rec, (uint32_t)e4);
-                if (!DEF && W.th_div_site) {
-                  W.b_nsub[rec] = nsub;
-                  W.b_subofs[rec] = sofs;
-                }
-                if (!DEF && W.pois_any)
-                  for (int k = 0; k < 4; k++) {
+                if (!DEF && W.seg_any)
+#pragma unroll
+                  for (int k = 0; k < NSEG; k++) {
                     W.b_pofs[(int64_t)k * rcap + rec] = pofs[k];
                     W.b_pcnt[(int64_t)k * rcap + rec] = pcnt[k];
                   }
@@ -1561,7 +1617,7 @@ bool class_timing_all() {
 static bool def_knobs(const DevWorld& W) {
   return W.alloc_method != 2 && W.require_allocate == 1 && W.max_label_exe == 1 && W.cfg_min_genome == 0 &&
          W.cfg_max_genome == 0 && W.merit_default_bonus == 0.0 && W.inherit_merit == 1 &&
-         W.base_merit_method == 4 && W.th_div_uni == 0 && W.th_div_site == 0 && W.th_par_site == 0 && !W.pois_any && W.size_range == 2.0 && W.min_exe_lines == 0.5 &&
+         W.base_merit_method == 4 && W.th_div_uni == 0 && !W.seg_any && W.th_par_site == 0 && W.size_range == 2.0 && W.min_exe_lines == 0.5 &&
          W.min_copied_lines == 0.5 && W.required_bonus == 0.0 && W.default_bonus == 1.0 && W.rand_total <= 256;
 }
 

@@ -653,9 +653,8 @@ __global__ __launch_bounds__(256) void k_place_pick_mut(DevWorld W, unsigned lon
       int e = 0;
 #pragma unroll
       for (int k = 0; k < 5; k++) e |= W.b_edit[(int64_t)k * W.rcap + r];
-      if (W.th_div_site) e |= W.b_nsub[r];
-      if (W.pois_any)
-        for (int k = 0; k < 4; k++) e |= W.b_pcnt[(int64_t)k * W.rcap + r];
+      if (W.seg_any)
+        for (int k = 0; k < NSEG; k++) e |= W.b_pcnt[(int64_t)k * W.rcap + r];
       any = e != 0;
     }
     for (unsigned long long m = __ballot(any); m; m &= m - 1ull) {
@@ -757,9 +756,8 @@ __global__ __launch_bounds__(64) void k_apply_mutations(DevWorld W) {
       int e = 0;
 #pragma unroll
       for (int k = 0; k < 5; k++) e |= W.b_edit[(int64_t)k * W.rcap + r];
-      if (W.th_div_site) e |= W.b_nsub[r];
-      if (W.pois_any)
-        for (int k = 0; k < 4; k++) e |= W.b_pcnt[(int64_t)k * W.rcap + r];
+      if (W.seg_any)
+        for (int k = 0; k < NSEG; k++) e |= W.b_pcnt[(int64_t)k * W.rcap + r];
       any = e != 0;
     }
     for (unsigned long long m = __ballot(any); m; m &= m - 1ull) {
@@ -1122,7 +1120,7 @@ static unsigned place_grid(const DevWorld& W) {
 
 static unsigned activate_grid(const DevWorld& W);
 static bool has_divide_mutations(const DevWorld& W) {
-  return (W.th_div_mut | W.th_div_ins | W.th_div_del | W.th_div_slip | W.th_div_uni | W.th_div_site) != 0 || W.pois_any;
+  return (W.th_div_mut | W.th_div_ins | W.th_div_del | W.th_div_slip | W.th_div_uni) != 0 || W.seg_any;
 }
 static unsigned mut_grid(const DevWorld& W) { return (unsigned)std::min<int64_t>(nblk(W.rcap, MUT_PER_WAVE), 8192); }
 static void launch_apply_mutations(const DevWorld& W, hipStream_t s) {

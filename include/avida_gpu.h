@@ -156,6 +156,10 @@ typedef struct avgpu_cfg {
    * :426-435; main/cMutationRates.h:137-144); means above 700 are refused */
   double divide_poisson_slip_mean, divide_poisson_mut_mean;
   double divide_poisson_ins_mean, divide_poisson_del_mean;
+  /* DIV_INS_PROB, DIV_DEL_PROB, DIV_UNIFORM_PROB, DIV_SLIP_PROB: per-site
+   * insertions / deletions / uniform mutations / slips on divide
+   * (cpu/cHardwareBase.cc:323-327, :463-503) */
+  double div_ins_prob, div_del_prob, div_uniform_prob, div_slip_prob;
 } avgpu_cfg;
 
 /* One REACTION line of environment.cfg (main/cEnvironment.cc:1185-1211,

@@ -246,6 +246,7 @@ struct World {
   Prob p_div_mut, p_div_ins, p_div_del, p_div_slip, p_div_uni;
   Prob p_div_site;           // DIV_MUT_PROB (per-site substitutions on divide)
   Prob p_par_site;           // PARENT_MUT_PROB (per-site substitutions in the parent)
+  Prob p_dsite[4];           // DIV_INS_PROB, DIV_DEL_PROB, DIV_UNIFORM_PROB, DIV_SLIP_PROB (per site)
   double pois_L[4] = {0, 0, 0, 0};   // exp(-DIVIDE_POISSON_{SLIP,MUT,INS,DEL}_MEAN); 0 = off
   std::vector<double> rec;   // RECORDED mode: the host's stream (organisms point into it)
   // batch world
@@ -486,8 +487,31 @@ struct Exec {
     int min_g = w.cfg.min_genome_size; if (!min_g || min_g < AVGPU_MIN_GENOME) min_g = AVGPU_MIN_GENOME;
     // NumDividePoisson* draws only at a non-zero mean (main/cMutationRates.h:137-144)
     auto npois = [&](int k) -> uint32_t { return w.pois_L[k] > 0.0 ? r.poisson(w.pois_L[k]) : 0u; };
+    // doUniformMutation (cpu/cHardwareBase.cc:572-595): op codes, not weighted
+    auto uniform_mutation = [&]() {
+      const int n_ops = w.is.n;
+      const int mut = (int)r.uint_below((uint32_t)(2 * n_ops + 1));
+      if (mut < n_ops) {
+        child[r.uint_below((uint32_t)child.size())] = (uint8_t)mut;
+      } else if (mut == n_ops) {
+        if ((int)child.size() != min_g) child.erase(child.begin() + r.uint_below((uint32_t)child.size()));
+      } else if ((int)child.size() != max_g) {
+        const uint32_t site = r.uint_below((uint32_t)child.size() + 1);
+        child.insert(child.begin() + site, (uint8_t)(mut - n_ops - 1));
+      }
+    };
+    // GetRandBinomial(size, p) restated as one P(p) per site (see DIV_MUT_PROB below)
+    auto binom = [&](const Prob& q, int size) -> int {
+      int n = 0;
+      for (int i = 0; i < size; i++) n += r.p(q) ? 1 : 0;
+      return n;
+    };
     if (r.p(w.p_div_slip)) slip_mutation(child, r);
     for (uint32_t i = 0, n = npois(0); i < n; i++) slip_mutation(child, r);   // :318-320
+    if (w.p_dsite[3].p > 0.0) {                                               // per site :323-327
+      const int n = binom(w.p_dsite[3], (int)child.size());
+      for (int i = 0; i < n; i++) slip_mutation(child, r);
+    }
     if (r.p(w.p_div_mut)) {
       uint32_t line = r.uint_below((uint32_t)child.size());
       child[line] = (uint8_t)w.is.random_inst(r);
@@ -514,19 +538,7 @@ struct Exec {
       uint32_t line = r.uint_below((uint32_t)child.size());
       child.erase(child.begin() + line);
     }
-    if (w.p_div_uni.p != 0.0 && r.p(w.p_div_uni)) {
-      // doUniformMutation (cpu/cHardwareBase.cc:572-595): op codes, not weighted
-      const int n_ops = w.is.n;
-      const int mut = (int)r.uint_below((uint32_t)(2 * n_ops + 1));
-      if (mut < n_ops) {
-        child[r.uint_below((uint32_t)child.size())] = (uint8_t)mut;
-      } else if (mut == n_ops) {
-        if ((int)child.size() != min_g) child.erase(child.begin() + r.uint_below((uint32_t)child.size()));
-      } else if ((int)child.size() != max_g) {
-        const uint32_t site = r.uint_below((uint32_t)child.size() + 1);
-        child.insert(child.begin() + site, (uint8_t)(mut - n_ops - 1));
-      }
-    }
+    if (w.p_div_uni.p != 0.0 && r.p(w.p_div_uni)) uniform_mutation();
     // Divide Mutations (per site) (cpu/cHardwareBase.cc:447-460): only at a
     // non-zero DIV_MUT_PROB; mut_multiplier 1 and maxmut INT_MAX on this path
     // (Divide_Main :1806).  GetRandBinomial lives in Apto (absent here): it is
@@ -541,6 +553,29 @@ struct Exec {
         const uint32_t site = r.uint_below((uint32_t)size);
         child[site] = (uint8_t)w.is.random_inst(r);
       }
+    }
+    // Insert Mutations (per site) (:463-485): all sites first, sorted, then
+    // inserted from the highest down, one GetRandomInst each
+    if (w.p_dsite[0].p > 0.0) {
+      int n = binom(w.p_dsite[0], (int)child.size());
+      if (n + (int)child.size() > max_g) n = max_g - (int)child.size();
+      if (n > 0) {
+        std::vector<int> sites(n);
+        for (int i = 0; i < n; i++) sites[i] = (int)r.uint_below((uint32_t)child.size() + 1);
+        std::sort(sites.begin(), sites.end());
+        for (int i = n - 1; i >= 0; i--) child.insert(child.begin() + sites[i], (uint8_t)w.is.random_inst(r));
+      }
+    }
+    // Delete Mutations (per site) (:473-488)
+    if (w.p_dsite[1].p > 0.0) {
+      int n = binom(w.p_dsite[1], (int)child.size());
+      if ((int)child.size() - n < min_g) n = (int)child.size() - min_g;
+      for (int i = 0; i < n; i++) child.erase(child.begin() + r.uint_below((uint32_t)child.size()));
+    }
+    // Uniform Mutations (per site) (:492-503)
+    if (w.p_dsite[2].p > 0.0) {
+      const int n = binom(w.p_dsite[2], (int)child.size());
+      for (int i = 0; i < n; i++) uniform_mutation();
     }
     // Parent Substitution Mutations (per site) (cpu/cHardwareBase.cc:508-520):
     // the parent's memory, already cut to the divide point (Divide_Main
@@ -1049,6 +1084,10 @@ void* orc_create(const avgpu_cfg* cfg, int64_t ncells) {
   w->p_div_uni = make_prob(cfg->divide_uniform_prob);
   w->p_div_site = make_prob(cfg->div_mut_prob);
   w->p_par_site = make_prob(cfg->parent_mut_prob);
+  w->p_dsite[0] = make_prob(cfg->div_ins_prob);
+  w->p_dsite[1] = make_prob(cfg->div_del_prob);
+  w->p_dsite[2] = make_prob(cfg->div_uniform_prob);
+  w->p_dsite[3] = make_prob(cfg->div_slip_prob);
   {
     const double means[4] = {cfg->divide_poisson_slip_mean, cfg->divide_poisson_mut_mean,
                              cfg->divide_poisson_ins_mean, cfg->divide_poisson_del_mean};

@@ -71,17 +71,17 @@ def test_unsupported_mutation_knobs_are_refused(golden, tmp_path):
     """A reference avida.cfg that sets a mutation knob this path does not
     implement is refused, not run with different semantics (capi.UNSUPPORTED_NONZERO)."""
     from avida_amd import files
-    for key in ["DIV_INS_PROB", "PARENT_INS_PROB", "DIVIDE_POISSON_TRANS_MEAN", "COPY_SLIP_PROB",
+    for key in ["DIV_TRANS_PROB", "PARENT_INS_PROB", "DIVIDE_POISSON_TRANS_MEAN", "COPY_SLIP_PROB",
                 "COPY_UNIFORM_PROB", "DIVIDE_TRANS_PROB"]:
         with pytest.raises(ValueError, match=key):
             capi.cfg_from_avida(files.read_avida_cfg(None, {key: 0.01}))
     # DIV_MUT_PROB (per-site substitutions on divide) is on the path
     assert capi.cfg_from_avida(files.read_avida_cfg(None, {"DIV_MUT_PROB": 0.003})).div_mut_prob == 0.003
     text = open(os.path.join(golden, "avida-default.cfg")).read().replace(
-        "DIV_INS_PROB 0.0", "DIV_INS_PROB 0.001")
+        "COPY_SLIP_PROB 0.0", "COPY_SLIP_PROB 0.001")
     p = tmp_path / "avida.cfg"
     p.write_text(text)
-    with pytest.raises(ValueError, match="DIV_INS_PROB"):
+    with pytest.raises(ValueError, match="COPY_SLIP_PROB"):
         capi.cfg_from_avida(files.read_avida_cfg(str(p)))
     # the reference's default config itself is accepted
     capi.cfg_from_avida(files.read_avida_cfg(os.path.join(golden, "avida-default.cfg")))

@@ -127,6 +127,30 @@ def test_recorded_draws_poisson_divide_mutations(golden):
     assert b.lib.orc_rec_exhausted() == 0
 
 
+def test_recorded_draws_per_site_ins_del_uniform_slip(golden):
+    """DIV_SLIP_PROB, DIV_INS_PROB, DIV_DEL_PROB, DIV_UNIFORM_PROB = 0.5
+    (cpu/cHardwareBase.cc:323-327, :463-503) at u = 0.37 on the 100-site
+    ancestor: 1 slip test, 100 + 100 x 2 per-site slips (from = to = 37: no
+    change), mut / ins / del tests 3, 100 + 100 insertion sites + 100
+    instructions, 200 deletion tests of which 192 fit above the 8-site minimum
+    (+192 sites), 8 uniform tests + 8 x 2 (op 19 < 26: a substitution) = 1020."""
+    iset, env, cfg, anc = _ancestor(golden, {"COPY_MUT_PROB": 0.0, "DIVIDE_INS_PROB": 0.0,
+                                             "DIVIDE_DEL_PROB": 0.0, "DEATH_METHOD": 0,
+                                             "DIV_SLIP_PROB": 0.5, "DIV_INS_PROB": 0.5,
+                                             "DIV_DEL_PROB": 0.5, "DIV_UNIFORM_PROB": 0.5})
+    b = ol.Backend("oracle", cfg, iset, env, ncells=1)
+    b.set_orgs(0, [anc], deterministic=True)
+    b.set_rng_mode(capi.RNG_RECORDED, np.full(4096, 0.37))
+    for k in range(2000):
+        b.step(0, 1, uniform=1, mode=capi.MODE_FROZEN)
+        st, _, _ = b.states(0, 1, CAP)
+        if st[0].num_divides:
+            break
+    assert st[0].num_divides == 1
+    assert st[0].rng_counter == 1 + 300 + 3 + 300 + 200 + 192 + 8 + 16
+    assert b.lib.orc_rec_exhausted() == 0
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("muts", ["copy", "all", "site", "poisson"])
 def test_recorded_stream_frozen_traces_gpu(golden, muts):
@@ -140,14 +164,15 @@ def test_recorded_stream_frozen_traces_gpu(golden, muts):
     if muts == "all":
         ov.update({"DIVIDE_MUT_PROB": 0.1, "DIVIDE_SLIP_PROB": 0.05, "DIVIDE_UNIFORM_PROB": 0.05})
     if muts == "site":      # per-site divide substitutions: one draw per offspring site
-        ov.update({"DIV_MUT_PROB": 0.02, "PARENT_MUT_PROB": 0.01})
+        ov.update({"DIV_MUT_PROB": 0.02, "PARENT_MUT_PROB": 0.01, "DIV_INS_PROB": 0.005,
+                   "DIV_DEL_PROB": 0.005, "DIV_UNIFORM_PROB": 0.005, "DIV_SLIP_PROB": 0.001})
     if muts == "poisson":
         ov.update({"DIVIDE_POISSON_SLIP_MEAN": 0.3, "DIVIDE_POISSON_MUT_MEAN": 1.5,
                    "DIVIDE_POISSON_INS_MEAN": 0.8, "DIVIDE_POISSON_DEL_MEAN": 0.8})
     iset, env, cfg = pu.load_env(golden, "instset-classic.cfg", ov)
     n = len(genomes)
     rng = np.random.default_rng(42)
-    per = 4500 if muts != "site" else 9000   # h-copy alone draws once per copy at a non-zero rate
+    per = 4500 if muts != "site" else 16000   # h-copy alone draws once per copy at a non-zero rate
     stream = rng.random(n * per)
     offsets = np.arange(n, dtype=np.int64) * per
     pair = [ol.Backend(k, cfg, iset, env, ncells=n) for k in ("oracle", "gpu")]
@@ -191,7 +216,7 @@ def test_divide_slip_uniform_world_gpu(golden, fill):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("knob", ["DIV_MUT_PROB", "PARENT_MUT_PROB", "POISSON"])
+@pytest.mark.parametrize("knob", ["DIV_MUT_PROB", "PARENT_MUT_PROB", "POISSON", "PER_SITE"])
 def test_per_site_divide_mutations_world_gpu(golden, knob):
     """World updates with DIV_MUT_PROB (per-site substitutions in the
     offspring, cpu/cHardwareBase.cc:447-460) or PARENT_MUT_PROB (in the
@@ -199,6 +224,9 @@ def test_per_site_divide_mutations_world_gpu(golden, knob):
     world, every cell digest, 120 updates; the substitution arena never fills.
     POISSON: the four DIVIDE_POISSON_*_MEAN knobs (:318-320, :383-435)."""
     ov = {knob: 0.02, "WORLD_X": 48, "WORLD_Y": 48}
+    if knob == "PER_SITE":   # per-site insertions, deletions, uniform mutations, slips (:323-327, :463-503)
+        ov = {"DIV_INS_PROB": 0.005, "DIV_DEL_PROB": 0.005, "DIV_UNIFORM_PROB": 0.005,
+              "DIV_SLIP_PROB": 0.001, "WORLD_X": 48, "WORLD_Y": 48}
     if knob == "POISSON":
         ov = {"DIVIDE_POISSON_SLIP_MEAN": 0.1, "DIVIDE_POISSON_MUT_MEAN": 1.0,
               "DIVIDE_POISSON_INS_MEAN": 0.5, "DIVIDE_POISSON_DEL_MEAN": 0.5,

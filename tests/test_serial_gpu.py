@@ -68,7 +68,9 @@ def test_serial_world_dense_population(golden):
                                             "DIV_MUT_PROB": 0.005, "PARENT_MUT_PROB": 0.002,
                                             "DIVIDE_POISSON_MUT_MEAN": 0.5,
                                             "DIVIDE_POISSON_INS_MEAN": 0.2,
-                                            "DIVIDE_POISSON_DEL_MEAN": 0.2})
+                                            "DIVIDE_POISSON_DEL_MEAN": 0.2,
+                                            "DIV_INS_PROB": 0.002, "DIV_DEL_PROB": 0.002,
+                                            "DIV_UNIFORM_PROB": 0.002, "DIV_SLIP_PROB": 0.0005})
     n = cfg.world_x * cfg.world_y
     genomes = pu.pop_genomes(golden, iset)[:n]
     orc = ol.Backend("oracle", cfg, iset, env, ncells=n)

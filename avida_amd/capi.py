@@ -55,6 +55,8 @@ class AvgpuCfg(C.Structure):
         ("divide_poisson_ins_mean", C.c_double), ("divide_poisson_del_mean", C.c_double),
         ("div_ins_prob", C.c_double), ("div_del_prob", C.c_double),
         ("div_uniform_prob", C.c_double), ("div_slip_prob", C.c_double),
+        ("divide_trans_prob", C.c_double), ("divide_poisson_trans_mean", C.c_double),
+        ("div_trans_prob", C.c_double),
     ]
 
 
@@ -167,8 +169,8 @@ EXPORTED = [
 
 
 # avida.cfg knobs that change the semantics of this path when non-zero and
-# that it does not implement (main/cAvidaConfig.h:309-361, 372): translocation
-# and lateral-transfer mutations (one-shot, Poisson and per-site), parent
+# that it does not implement (main/cAvidaConfig.h:309-361, 372):
+# lateral-transfer mutations (one-shot, Poisson and per-site), parent
 # insertions / deletions, point, inject and meta mutations, copy uniform /
 # slip, death on divide.  cfg_from_avida refuses a config that sets any of
 # them rather than run it with different semantics.  (COPY_INS_PROB /
@@ -176,9 +178,9 @@ EXPORTED = [
 UNSUPPORTED_NONZERO = [
     "COPY_UNIFORM_PROB", "COPY_SLIP_PROB",
     "POINT_MUT_PROB", "POINT_INS_PROB", "POINT_DEL_PROB", "INST_POINT_MUT_PROB",
-    "DIV_TRANS_PROB", "DIV_LGT_PROB",
-    "DIVIDE_TRANS_PROB", "DIVIDE_LGT_PROB",
-    "DIVIDE_POISSON_TRANS_MEAN", "DIVIDE_POISSON_LGT_MEAN",
+    "DIV_LGT_PROB",
+    "DIVIDE_LGT_PROB",
+    "DIVIDE_POISSON_LGT_MEAN",
     "INJECT_MUT_PROB", "INJECT_INS_PROB", "INJECT_DEL_PROB",
     "PARENT_INS_PROB", "PARENT_DEL_PROB",
     "META_COPY_MUT", "META_STD_DEV", "DEATH_PROB",
@@ -259,6 +261,12 @@ def cfg_from_avida(cfg, seed=None) -> AvgpuCfg:
     c.div_del_prob = float(g("DIV_DEL_PROB", 0.0))
     c.div_uniform_prob = float(g("DIV_UNIFORM_PROB", 0.0))
     c.div_slip_prob = float(g("DIV_SLIP_PROB", 0.0))
+    c.divide_trans_prob = float(g("DIVIDE_TRANS_PROB", 0.0))
+    c.divide_poisson_trans_mean = float(g("DIVIDE_POISSON_TRANS_MEAN", 0.0))
+    c.div_trans_prob = float(g("DIV_TRANS_PROB", 0.0))
+    if (c.divide_trans_prob or c.divide_poisson_trans_mean or c.div_trans_prob) and \
+            int(float(g("TRANS_FILL_MODE", 0))) != 0:
+        raise ValueError("TRANS_FILL_MODE 1 (scrambled) is not on this path")
     return c
 
 

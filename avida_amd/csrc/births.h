@@ -62,19 +62,37 @@ __device__ __forceinline__ void edit_back(int ew, bool nopc, int& src, int& val)
     else if (src >= a) src = b + (src - a);
   }
 }
+// a translocation undone (doTransMutation, cpu/cHardwareBase.cc:700-760,
+// duplication fill): w0 = E_TRANS | ins_loc << 3 | to << 15, w1 = from
+__device__ __forceinline__ void trans_back(int w0, int w1, int& src, int val) {
+  if (val >= 0) return;
+  const int ins = (w0 >> 3) & 0xFFF, to = (w0 >> 15) & 0xFFF, L = w1 - to;
+  if (L > 0) {
+    if (src >= ins + L) src -= L;
+    else if (src >= ins) src = to + (src - ins);
+  } else if (L < 0 && src >= ins) {
+    src -= L;
+  }
+}
 // applied order (device.h SEG_*): e0, segments 0-1, e1, segment 2, e2,
-// segment 3, e3, segment 4, e4, segments 5-8 (pcnt[k] words at subs + pofs[k])
+// the other segments (pcnt[k] words at subs + pofs[k])
 __device__ __forceinline__ int mut_source(int j, const int* e, bool nopc, int& val, const int32_t* subs,
                                           const int* pofs, const int* pcnt) {
   constexpr int first[5] = {SEG_PSLIP, SEG_PMUT, SEG_PINS, SEG_PDEL, SEG_SMUT};
-  constexpr int last[5] = {SEG_SSLIP, SEG_PMUT, SEG_PINS, SEG_PDEL, SEG_SUNI};
+  constexpr int last[5] = {SEG_STRANS, SEG_PMUT, SEG_PINS, SEG_PDEL, SEG_SUNI};
   int src = j;
   val = -1;
 #pragma unroll
   for (int k = 4; k >= 0; k--) {
 #pragma unroll
-    for (int g = last[k]; g >= first[k]; g--)
-      for (int i = pcnt[g] - 1; i >= 0 && val < 0; i--) edit_back(subs[pofs[g] + i], nopc, src, val);
+    for (int g = last[k]; g >= first[k]; g--) {
+      if (g >= SEG_TTRANS && g <= SEG_STRANS) {
+        for (int i = pcnt[g] - 2; i >= 0 && val < 0; i -= 2)
+          trans_back(subs[pofs[g] + i], subs[pofs[g] + i + 1], src, val);
+      } else {
+        for (int i = pcnt[g] - 1; i >= 0 && val < 0; i--) edit_back(subs[pofs[g] + i], nopc, src, val);
+      }
+    }
     edit_back(e[k], nopc, src, val);
   }
   return src;

@@ -118,27 +118,28 @@ int setup_world(avgpu_world* w, int64_t n, bool test_buffers) {
   // DIV_MUT_PROB arena: three times the largest expected substitutions per
   // record plus 16 (offsets are int32); a fill past it is counted
   // (AVGPU_CNT_SUB_OVERFLOW), never written
-  const double pmeans[4] = {c.divide_poisson_slip_mean, c.divide_poisson_mut_mean,
-                            c.divide_poisson_ins_mean, c.divide_poisson_del_mean};
-  const double psite[5] = {c.div_mut_prob, c.div_ins_prob, c.div_del_prob, c.div_uniform_prob, c.div_slip_prob};
-  const bool pois = pmeans[0] > 0.0 || pmeans[1] > 0.0 || pmeans[2] > 0.0 || pmeans[3] > 0.0;
-  bool site = false;
-  for (int q = 0; q < 5; q++) site = site || psite[q] > 0.0;
+  const double pmeans[5] = {c.divide_poisson_slip_mean, c.divide_poisson_mut_mean,
+                            c.divide_poisson_ins_mean, c.divide_poisson_del_mean, c.divide_poisson_trans_mean};
+  const double psite[6] = {c.div_mut_prob, c.div_ins_prob, c.div_del_prob, c.div_uniform_prob, c.div_slip_prob,
+                           c.div_trans_prob};
+  bool pois = false, site = c.divide_trans_prob > 0.0;
+  for (int q = 0; q < 5; q++) pois = pois || pmeans[q] > 0.0;
+  for (int q = 0; q < 6; q++) site = site || psite[q] > 0.0;
   if (pois || site) {
     // arena words per record: 3x the largest expected count of each kind
     // (per site: a 2048-site offspring) + 16 each; offsets are int32
-    int64_t k = 16;
+    int64_t k = 16 + 2;    // + the one-shot translocation's two words
+    for (int q = 0; q < 6; q++)
+      if (psite[q] > 0.0) k += (q == 5 ? 2 : 1) * ((int64_t)std::ceil(AVGPU_MAX_GENOME * std::min(1.0, psite[q]) * 3.0) + 16);
     for (int q = 0; q < 5; q++)
-      if (psite[q] > 0.0) k += (int64_t)std::ceil(AVGPU_MAX_GENOME * std::min(1.0, psite[q]) * 3.0) + 16;
-    for (int q = 0; q < 4; q++)
-      if (pmeans[q] > 0.0) k += (int64_t)std::ceil(3.0 * std::min(pmeans[q], 4096.0)) + 16;
+      if (pmeans[q] > 0.0) k += (q == 4 ? 2 : 1) * ((int64_t)std::ceil(3.0 * std::min(pmeans[q], 4096.0)) + 16);
     k = std::min<int64_t>(k, (int64_t)INT32_MAX / R);
     W.scap = R * k;
     A(b_subs, W.scap); A(b_pofs, NSEG * R); A(b_pcnt, NSEG * R);
   }
   W.seg_any = (pois || site) ? 1 : 0;
   W.pois_any = pois ? 1 : 0;
-  for (int q = 0; q < 4; q++) W.pois_L[q] = pmeans[q] > 0.0 ? std::exp(-pmeans[q]) : 0.0;
+  for (int q = 0; q < 5; q++) W.pois_L[q] = pmeans[q] > 0.0 ? std::exp(-pmeans[q]) : 0.0;
   A(b_merit, R);
   A(b_fitness, R); A(b_gen, R); A(b_ccopied, R); A(b_exec, R);
   A(b_gest, R); A(b_ltask, AVGPU_NUM_LOGIC_TASKS * R); A(b_rng, 3 * R); A(b_target, R); A(b_state, R);
@@ -193,6 +194,8 @@ int setup_world(avgpu_world* w, int64_t n, bool test_buffers) {
   W.th_dsite[1] = th(c.div_del_prob); W.p_dsite[1] = c.div_del_prob;
   W.th_dsite[2] = th(c.div_uniform_prob); W.p_dsite[2] = c.div_uniform_prob;
   W.th_dsite[3] = th(c.div_slip_prob); W.p_dsite[3] = c.div_slip_prob;
+  W.th_dsite[4] = th(c.div_trans_prob); W.p_dsite[4] = c.div_trans_prob;
+  W.th_dtrans = th(c.divide_trans_prob); W.p_dtrans = c.divide_trans_prob;
   W.th_par_site = th(c.parent_mut_prob);
   W.p_par_site = c.parent_mut_prob;
   W.slip_fill_mode = c.slip_fill_mode;
@@ -234,7 +237,8 @@ avgpu_world* create_world(const avgpu_cfg* cfg, int device, int64_t n, bool test
     return nullptr;
   }
   if (cfg->divide_poisson_slip_mean > 700.0 || cfg->divide_poisson_mut_mean > 700.0 ||
-      cfg->divide_poisson_ins_mean > 700.0 || cfg->divide_poisson_del_mean > 700.0) {
+      cfg->divide_poisson_ins_mean > 700.0 || cfg->divide_poisson_del_mean > 700.0 ||
+      cfg->divide_poisson_trans_mean > 700.0) {
     fail(AVGPU_EUNSUPPORTED, "DIVIDE_POISSON_*_MEAN above 700 (exp(-mean) underflows)");
     return nullptr;
   }

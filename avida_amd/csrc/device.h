@@ -224,10 +224,12 @@ struct DevWorld {
   double p_div_site;
   uint64_t th_par_site;   // PARENT_MUT_PROB (per-site substitutions in the parent)
   double p_par_site;
-  double pois_L[4];       // exp(-DIVIDE_POISSON_{SLIP,MUT,INS,DEL}_MEAN), 0 = off
+  double pois_L[5];       // exp(-DIVIDE_POISSON_{SLIP,MUT,INS,DEL,TRANS}_MEAN), 0 = off
   int32_t pois_any;
-  uint64_t th_dsite[4];   // DIV_INS_PROB, DIV_DEL_PROB, DIV_UNIFORM_PROB, DIV_SLIP_PROB (per site)
-  double p_dsite[4];
+  uint64_t th_dsite[5];   // DIV_INS_PROB, DIV_DEL_PROB, DIV_UNIFORM_PROB, DIV_SLIP_PROB, DIV_TRANS_PROB
+  double p_dsite[5];
+  uint64_t th_dtrans;     // DIVIDE_TRANS_PROB
+  double p_dtrans;
   int32_t seg_any;        // some variable-count kind is on (b_subs / b_pofs / b_pcnt allocated)
   int32_t slip_fill_mode;
   // RECORDED mode (avgpu_set_rng_mode): rec_n doubles; rec_off[c] = the start
@@ -301,10 +303,11 @@ __host__ __device__ inline int64_t record_bytes(int x, int64_t arena) {
 #define CNT_HALO_LOST 19  /* offspring lost to a full halo arena (counted in DROPPED too) */
 #define CNT_REC_OVER 20   /* RECORDED draws past the end of the stream */
 // variable-count edit segments of a birth record, in the order applied:
-// e0 (slip), Poisson slips, per-site slips, e1 (mut), Poisson substitutions,
+// e0 (slip), Poisson slips, per-site slips, translocations (one-shot, Poisson,
+// per site: two words each, see births.h), e1 (mut), Poisson substitutions,
 // e2 (ins), Poisson insertions, e3 (del), Poisson deletions, e4 (uniform),
 // per-site substitutions, insertions, deletions, uniform mutations
-enum { SEG_PSLIP = 0, SEG_SSLIP, SEG_PMUT, SEG_PINS, SEG_PDEL, SEG_SMUT, SEG_SINS, SEG_SDEL, SEG_SUNI, NSEG };
+enum { SEG_PSLIP = 0, SEG_SSLIP, SEG_TTRANS, SEG_PTRANS, SEG_STRANS, SEG_PMUT, SEG_PINS, SEG_PDEL, SEG_SMUT, SEG_SINS, SEG_SDEL, SEG_SUNI, NSEG };
 #define CNT_SUB_OVERFLOW 22   /* DIV_MUT_PROB substitutions that found the b_subs arena full (must stay 0) */
 #define CNT_OVERSIZE 21   /* offspring a slip grew past AVGPU_MAX_GENOME (counted in DROPPED too) */
 // 32..37: AVGPU_PHASE_CLOCKS loop cycles by block (decode, fast, copy, switch,

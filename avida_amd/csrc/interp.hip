@@ -105,7 +105,7 @@ __device__ __forceinline__ bool consume_resource(const DevWorld& W, const double
 __host__ __device__ constexpr int tape_stride(int S) { return S == CLASS0_SIZE ? S : S + 16; }
 
 // divide-mutation edits (Divide_DoMutations, applied in order): kind | a << 3 | b << 15
-enum { E_SLIP = 1, E_POINT = 2, E_INS = 3, E_DEL = 4 };
+enum { E_SLIP = 1, E_POINT = 2, E_INS = 3, E_DEL = 4, E_TRANS = 5 };
 __device__ __forceinline__ int edit_word(int kind, int a, int b) { return kind | (a << 3) | (b << 15); }
 
 // serial = 1: one step of the serial world (k_serial_update): lane 0 runs
@@ -998,6 +998,33 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
                 preserve(SEG_SSLIP, n);
                 for (int i = 0; i < n; i++) pput(SEG_SSLIP, i, slip_edit());
                 pcnt[SEG_SSLIP] = n;
+              }
+              // translocations (doTransMutation :700-760, duplication fill):
+              // from, to, then the insertion site on the size before it
+              auto trans_edit = [&](int k, int i) {
+                const int from = (int)draw_below((uint32_t)len + 1u);
+                const int to = from == 0 ? (int)draw_below((uint32_t)len) : (int)draw_below((uint32_t)len + 1u);
+                const int ins_loc = (int)draw_below((uint32_t)len + 1u);
+                pput(k, 2 * i, edit_word(E_TRANS, ins_loc, to));
+                pput(k, 2 * i + 1, from);
+                len += from - to;
+              };
+              if (segs && W.th_dtrans && draw_p(W.th_dtrans, W.p_dtrans)) {   // one-shot :331
+                preserve(SEG_TTRANS, 2);
+                trans_edit(SEG_TTRANS, 0);
+                pcnt[SEG_TTRANS] = 2;
+              }
+              if (pois) {                            // Poisson translocations :334-335
+                const int n = npois(4);
+                preserve(SEG_PTRANS, 2 * n);
+                for (int i = 0; i < n; i++) trans_edit(SEG_PTRANS, i);
+                pcnt[SEG_PTRANS] = 2 * n;
+              }
+              if (segs && W.th_dsite[4]) {           // translocations per site :338-342
+                const int n = nbinom(W.th_dsite[4], W.p_dsite[4]);
+                preserve(SEG_STRANS, 2 * n);
+                for (int i = 0; i < n; i++) trans_edit(SEG_STRANS, i);
+                pcnt[SEG_STRANS] = 2 * n;
               }
               if (draw_p(t_mut, q_mut)) {
                 const int line = (int)draw_below((uint32_t)len);

@@ -160,6 +160,10 @@ typedef struct avgpu_cfg {
    * insertions / deletions / uniform mutations / slips on divide
    * (cpu/cHardwareBase.cc:323-327, :463-503) */
   double div_ins_prob, div_del_prob, div_uniform_prob, div_slip_prob;
+  /* translocations (TRANS_FILL_MODE 0, duplication): DIVIDE_TRANS_PROB,
+   * DIVIDE_POISSON_TRANS_MEAN, DIV_TRANS_PROB (cpu/cHardwareBase.cc:331-343,
+   * doTransMutation :700-760) */
+  double divide_trans_prob, divide_poisson_trans_mean, div_trans_prob;
 } avgpu_cfg;
 
 /* One REACTION line of environment.cfg (main/cEnvironment.cc:1185-1211,

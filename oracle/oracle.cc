@@ -246,8 +246,9 @@ struct World {
   Prob p_div_mut, p_div_ins, p_div_del, p_div_slip, p_div_uni;
   Prob p_div_site;           // DIV_MUT_PROB (per-site substitutions on divide)
   Prob p_par_site;           // PARENT_MUT_PROB (per-site substitutions in the parent)
-  Prob p_dsite[4];           // DIV_INS_PROB, DIV_DEL_PROB, DIV_UNIFORM_PROB, DIV_SLIP_PROB (per site)
-  double pois_L[4] = {0, 0, 0, 0};   // exp(-DIVIDE_POISSON_{SLIP,MUT,INS,DEL}_MEAN); 0 = off
+  Prob p_dsite[5];           // DIV_INS_PROB, DIV_DEL_PROB, DIV_UNIFORM_PROB, DIV_SLIP_PROB, DIV_TRANS_PROB (per site)
+  Prob p_div_trans;          // DIVIDE_TRANS_PROB
+  double pois_L[5] = {0, 0, 0, 0, 0};   // + DIVIDE_POISSON_TRANS_MEAN   // exp(-DIVIDE_POISSON_{SLIP,MUT,INS,DEL}_MEAN); 0 = off
   std::vector<double> rec;   // RECORDED mode: the host's stream (organisms point into it)
   // batch world
   std::vector<Birth> births;
@@ -474,6 +475,25 @@ struct Exec {
     for (int i = ins; i < size - to; i++) g[from + i] = copy[to + i];
   }
 
+  // cHardwareBase::doTransMutation (cpu/cHardwareBase.cc:700-760), TRANS_FILL_MODE
+  // 0 (duplication; 1 is refused): copy[to, from) is inserted at ins_loc when
+  // from > to, copy[ins_loc, ins_loc + to - from) is cut when from < to
+  void trans_mutation(std::vector<uint8_t>& g, Stream& r) {
+    const std::vector<uint8_t> copy = g;
+    const int size = (int)copy.size();
+    const int from = (int)r.uint_below((uint32_t)size + 1);
+    const int to = (from == 0) ? (int)r.uint_below((uint32_t)size) : (int)r.uint_below((uint32_t)size + 1);
+    const int ins = from - to;
+    g.resize(size + ins);
+    const int ins_loc = (int)r.uint_below((uint32_t)size + 1);
+    if (ins > 0) {
+      for (int i = 0; i < ins; i++) g[ins_loc + i] = copy[to + i];
+      for (int i = ins_loc; i < size; i++) g[i + ins] = copy[i];
+    } else if (ins < 0) {
+      for (int i = ins_loc; i < (int)g.size(); i++) g[i] = copy[i - ins];
+    }
+  }
+
   // Divide_DoMutations (cpu/cHardwareBase.cc:296-569) in the reference's order
   // of draws: TestDivideSlip always draws (main/cMutationRates.h:128), the
   // translocation / LGT / Poisson / parent kinds and the per-site insertions
@@ -511,6 +531,14 @@ struct Exec {
     if (w.p_dsite[3].p > 0.0) {                                               // per site :323-327
       const int n = binom(w.p_dsite[3], (int)child.size());
       for (int i = 0; i < n; i++) slip_mutation(child, r);
+    }
+    // translocations (:331-343): one-shot (drawn only at a non-zero rate),
+    // Poisson, per site
+    if (w.p_div_trans.p != 0.0 && r.p(w.p_div_trans)) trans_mutation(child, r);
+    for (uint32_t i = 0, n = w.pois_L[4] > 0.0 ? r.poisson(w.pois_L[4]) : 0u; i < n; i++) trans_mutation(child, r);
+    if (w.p_dsite[4].p > 0.0) {
+      const int n = binom(w.p_dsite[4], (int)child.size());
+      for (int i = 0; i < n; i++) trans_mutation(child, r);
     }
     if (r.p(w.p_div_mut)) {
       uint32_t line = r.uint_below((uint32_t)child.size());
@@ -1088,6 +1116,9 @@ void* orc_create(const avgpu_cfg* cfg, int64_t ncells) {
   w->p_dsite[1] = make_prob(cfg->div_del_prob);
   w->p_dsite[2] = make_prob(cfg->div_uniform_prob);
   w->p_dsite[3] = make_prob(cfg->div_slip_prob);
+  w->p_dsite[4] = make_prob(cfg->div_trans_prob);
+  w->p_div_trans = make_prob(cfg->divide_trans_prob);
+  w->pois_L[4] = cfg->divide_poisson_trans_mean > 0.0 ? std::exp(-cfg->divide_poisson_trans_mean) : 0.0;
   {
     const double means[4] = {cfg->divide_poisson_slip_mean, cfg->divide_poisson_mut_mean,
                              cfg->divide_poisson_ins_mean, cfg->divide_poisson_del_mean};

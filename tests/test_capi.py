@@ -71,8 +71,8 @@ def test_unsupported_mutation_knobs_are_refused(golden, tmp_path):
     """A reference avida.cfg that sets a mutation knob this path does not
     implement is refused, not run with different semantics (capi.UNSUPPORTED_NONZERO)."""
     from avida_amd import files
-    for key in ["DIV_TRANS_PROB", "PARENT_INS_PROB", "DIVIDE_POISSON_TRANS_MEAN", "COPY_SLIP_PROB",
-                "COPY_UNIFORM_PROB", "DIVIDE_TRANS_PROB"]:
+    for key in ["DIV_LGT_PROB", "PARENT_INS_PROB", "DIVIDE_POISSON_LGT_MEAN", "COPY_SLIP_PROB",
+                "COPY_UNIFORM_PROB", "DIVIDE_LGT_PROB"]:
         with pytest.raises(ValueError, match=key):
             capi.cfg_from_avida(files.read_avida_cfg(None, {key: 0.01}))
     # DIV_MUT_PROB (per-site substitutions on divide) is on the path

@@ -151,6 +151,30 @@ def test_recorded_draws_per_site_ins_del_uniform_slip(golden):
     assert b.lib.orc_rec_exhausted() == 0
 
 
+def test_recorded_draws_translocations(golden):
+    """DIVIDE_TRANS_PROB 0.5, DIVIDE_POISSON_TRANS_MEAN 1, DIV_TRANS_PROB 0.5
+    (cpu/cHardwareBase.cc:331-343, doTransMutation :700-760) at u = 0.37: slip
+    test 1, one-shot test 1 + (from, to, insertion site) 3, Poisson count 2 +
+    3, 100 per-site tests + 100 x 3, mut / ins / del tests 3 = 413 draws."""
+    iset, env, cfg, anc = _ancestor(golden, {"COPY_MUT_PROB": 0.0, "DIVIDE_INS_PROB": 0.0,
+                                             "DIVIDE_DEL_PROB": 0.0, "DEATH_METHOD": 0,
+                                             "DIVIDE_TRANS_PROB": 0.5,
+                                             "DIVIDE_POISSON_TRANS_MEAN": 1.0,
+                                             "DIV_TRANS_PROB": 0.5})
+    b = ol.Backend("oracle", cfg, iset, env, ncells=1)
+    b.set_orgs(0, [anc], deterministic=True)
+    b.set_rng_mode(capi.RNG_RECORDED, np.full(4096, 0.37))
+    for k in range(2000):
+        b.step(0, 1, uniform=1, mode=capi.MODE_FROZEN)
+        st, _, _ = b.states(0, 1, CAP)
+        if st[0].num_divides:
+            break
+    assert st[0].num_divides == 1
+    assert st[0].rng_counter == 1 + 1 + 3 + 2 + 3 + 100 + 300 + 3
+    with pytest.raises(ValueError, match="TRANS_FILL_MODE"):
+        pu.load_env(golden, overrides={"DIVIDE_TRANS_PROB": 0.1, "TRANS_FILL_MODE": 1})
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("muts", ["copy", "all", "site", "poisson"])
 def test_recorded_stream_frozen_traces_gpu(golden, muts):
@@ -168,6 +192,7 @@ def test_recorded_stream_frozen_traces_gpu(golden, muts):
                    "DIV_DEL_PROB": 0.005, "DIV_UNIFORM_PROB": 0.005, "DIV_SLIP_PROB": 0.001})
     if muts == "poisson":
         ov.update({"DIVIDE_POISSON_SLIP_MEAN": 0.3, "DIVIDE_POISSON_MUT_MEAN": 1.5,
+                   "DIVIDE_TRANS_PROB": 0.05, "DIVIDE_POISSON_TRANS_MEAN": 0.1,
                    "DIVIDE_POISSON_INS_MEAN": 0.8, "DIVIDE_POISSON_DEL_MEAN": 0.8})
     iset, env, cfg = pu.load_env(golden, "instset-classic.cfg", ov)
     n = len(genomes)
@@ -216,7 +241,7 @@ def test_divide_slip_uniform_world_gpu(golden, fill):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("knob", ["DIV_MUT_PROB", "PARENT_MUT_PROB", "POISSON", "PER_SITE"])
+@pytest.mark.parametrize("knob", ["DIV_MUT_PROB", "PARENT_MUT_PROB", "POISSON", "PER_SITE", "TRANS"])
 def test_per_site_divide_mutations_world_gpu(golden, knob):
     """World updates with DIV_MUT_PROB (per-site substitutions in the
     offspring, cpu/cHardwareBase.cc:447-460) or PARENT_MUT_PROB (in the
@@ -227,6 +252,9 @@ def test_per_site_divide_mutations_world_gpu(golden, knob):
     if knob == "PER_SITE":   # per-site insertions, deletions, uniform mutations, slips (:323-327, :463-503)
         ov = {"DIV_INS_PROB": 0.005, "DIV_DEL_PROB": 0.005, "DIV_UNIFORM_PROB": 0.005,
               "DIV_SLIP_PROB": 0.001, "WORLD_X": 48, "WORLD_Y": 48}
+    if knob == "TRANS":      # translocations: one-shot, Poisson, per site (:331-343)
+        ov = {"DIVIDE_TRANS_PROB": 0.1, "DIVIDE_POISSON_TRANS_MEAN": 0.1, "DIV_TRANS_PROB": 0.0005,
+              "WORLD_X": 48, "WORLD_Y": 48}
     if knob == "POISSON":
         ov = {"DIVIDE_POISSON_SLIP_MEAN": 0.1, "DIVIDE_POISSON_MUT_MEAN": 1.0,
               "DIVIDE_POISSON_INS_MEAN": 0.5, "DIVIDE_POISSON_DEL_MEAN": 0.5,

@@ -21,7 +21,8 @@ MODE_WORLD, MODE_TEST, MODE_FROZEN = 0, 1, 2
 (CNT_INSTS, CNT_DEATHS, CNT_DIVIDES, CNT_BIRTHS, CNT_DROPPED, CNT_SPILLS, CNT_SLICES,
  CNT_LANESTEPS, CNT_C0_SLICES, CNT_C0_SITES, CNT_CLK_STAGE, CNT_CLK_LOOP, CNT_CLK_WB,
  CNT_ITERS, CNT_IT_FAST, CNT_IT_COPY, CNT_IT_SLOW, CNT_WAVES, CNT_HALO_SENT,
- CNT_HALO_LOST, CNT_REC_EXHAUSTED, CNT_OVERSIZE, CNT_SUB_OVERFLOW) = range(23)
+ CNT_HALO_LOST, CNT_REC_EXHAUSTED, CNT_OVERSIZE, CNT_SUB_OVERFLOW, CNT_MEM_CAP,
+ CNT_OVERWRITTEN) = range(25)
 RNG_COUNTER, RNG_RECORDED = 0, 1
 NUM_COUNTERS = 48
 
@@ -57,6 +58,27 @@ class AvgpuCfg(C.Structure):
         ("div_uniform_prob", C.c_double), ("div_slip_prob", C.c_double),
         ("divide_trans_prob", C.c_double), ("divide_poisson_trans_mean", C.c_double),
         ("div_trans_prob", C.c_double),
+        ("copy_uniform_prob", C.c_double), ("copy_slip_prob", C.c_double),
+        ("slip_copy_mode", C.c_int32), ("trans_fill_mode", C.c_int32),
+        ("parent_ins_prob", C.c_double), ("parent_del_prob", C.c_double),
+        # knobs the library refuses away from their defaults (avgpu_create)
+        ("point_mut_prob", C.c_double), ("point_ins_prob", C.c_double),
+        ("point_del_prob", C.c_double), ("inst_point_mut_prob", C.c_double),
+        ("div_lgt_prob", C.c_double), ("divide_lgt_prob", C.c_double),
+        ("divide_poisson_lgt_mean", C.c_double),
+        ("inject_mut_prob", C.c_double), ("inject_ins_prob", C.c_double),
+        ("inject_del_prob", C.c_double),
+        ("meta_copy_mut", C.c_double), ("meta_std_dev", C.c_double), ("death_prob", C.c_double),
+        ("age_deviation", C.c_int32), ("divide_failure_resets", C.c_int32),
+        ("special_mut_line", C.c_int32), ("population_cap", C.c_int32),
+        ("generation_inc_method", C.c_int32), ("reset_inputs_on_divide", C.c_int32),
+        ("epigenetic_method", C.c_int32), ("min_cycles", C.c_int32),
+        ("required_task", C.c_int32), ("immunity_task", C.c_int32),
+        ("required_reaction", C.c_int32), ("immunity_reaction", C.c_int32),
+        ("require_single_reaction", C.c_int32), ("max_unique_task_count", C.c_int32),
+        ("require_exact_copy", C.c_int32), ("fitness_method", C.c_int32),
+        ("juv_period", C.c_int32), ("no_mut_insts_len", C.c_int32),
+        ("test_fitness_measures", C.c_int32), ("pad_cfg2", C.c_int32),
     ]
 
 
@@ -131,7 +153,7 @@ class AvgpuUpdateStats(C.Structure):
         ("sum_genome_length", C.c_double), ("max_fitness", C.c_double),
         ("ave_generation", C.c_double), ("sum_mem_size", C.c_double),
         ("cum_insts_executed", C.c_int64), ("cum_births", C.c_int64), ("slices", C.c_int64),
-        ("lane_steps", C.c_int64),
+        ("lane_steps", C.c_int64), ("births_overwritten", C.c_int64),
     ]
 
 
@@ -154,7 +176,7 @@ def get_census(lib, prefix, handle, first, count):
 
 # C-ABI symbols declared in include/avida_gpu.h (checked by tests/test_capi.py)
 EXPORTED = [
-    "avgpu_last_error", "avgpu_cfg_defaults", "avgpu_create", "avgpu_destroy", "avgpu_sync",
+    "avgpu_last_error", "avgpu_cfg_defaults", "avgpu_check_cfg", "avgpu_create", "avgpu_destroy", "avgpu_sync",
     "avgpu_load_instset", "avgpu_load_env", "avgpu_load_resources", "avgpu_get_resources",
     "avgpu_set_resources", "avgpu_set_org", "avgpu_set_orgs", "avgpu_kill", "avgpu_set_states", "avgpu_set_clock",
     "avgpu_step", "avgpu_run_update", "avgpu_run_updates", "avgpu_update_totals",
@@ -164,27 +186,44 @@ EXPORTED = [
     "avgpu_tile_begin", "avgpu_tile_place", "avgpu_tile_finish", "avgpu_tile_res_bytes",
     "avgpu_set_tile_res_buffers", "avgpu_tile_res_cons", "avgpu_tile_res_settle",
     "avgpu_last_step_insts", "avgpu_last_kernel_ms", "avgpu_kernel_times", "avgpu_counters",
-    "avgpu_state_digests", "avgpu_set_rng_mode", "avgpu_run_serial_updates", "avgpu_set_timing",
+    "avgpu_state_digests", "avgpu_set_rng_mode", "avgpu_run_serial_updates", "avgpu_set_serial_streams",
+    "avgpu_set_timing",
 ]
 
 
-# avida.cfg knobs that change the semantics of this path when non-zero and
-# that it does not implement (main/cAvidaConfig.h:309-361, 372):
-# lateral-transfer mutations (one-shot, Poisson and per-site), parent
-# insertions / deletions, point, inject and meta mutations, copy uniform /
-# slip, death on divide.  cfg_from_avida refuses a config that sets any of
-# them rather than run it with different semantics.  (COPY_INS_PROB /
-# COPY_DEL_PROB travel in avgpu_cfg; avgpu_create refuses them.)
-UNSUPPORTED_NONZERO = [
-    "COPY_UNIFORM_PROB", "COPY_SLIP_PROB",
-    "POINT_MUT_PROB", "POINT_INS_PROB", "POINT_DEL_PROB", "INST_POINT_MUT_PROB",
-    "DIV_LGT_PROB",
-    "DIVIDE_LGT_PROB",
-    "DIVIDE_POISSON_LGT_MEAN",
-    "INJECT_MUT_PROB", "INJECT_INS_PROB", "INJECT_DEL_PROB",
-    "PARENT_INS_PROB", "PARENT_DEL_PROB",
-    "META_COPY_MUT", "META_STD_DEV", "DEATH_PROB",
+# avida.cfg knobs outside avgpu_cfg's implemented set travel in its refused
+# block (include/avida_gpu.h): the library itself refuses any of them set away
+# from the reference default (avgpu_create -> AVGPU_EUNSUPPORTED), so the
+# Python driver and a C++ caller are refused alike.  (cfg key, field, default,
+# kind) -- main/cAvidaConfig.h:309-420, :525-537, :546-559.
+REFUSED_KNOBS = [
+    ("POINT_MUT_PROB", "point_mut_prob", 0.0, float), ("POINT_INS_PROB", "point_ins_prob", 0.0, float),
+    ("POINT_DEL_PROB", "point_del_prob", 0.0, float),
+    ("INST_POINT_MUT_PROB", "inst_point_mut_prob", 0.0, float),
+    ("DIV_LGT_PROB", "div_lgt_prob", 0.0, float), ("DIVIDE_LGT_PROB", "divide_lgt_prob", 0.0, float),
+    ("DIVIDE_POISSON_LGT_MEAN", "divide_poisson_lgt_mean", 0.0, float),
+    ("INJECT_MUT_PROB", "inject_mut_prob", 0.0, float), ("INJECT_INS_PROB", "inject_ins_prob", 0.0, float),
+    ("INJECT_DEL_PROB", "inject_del_prob", 0.0, float),
+    ("META_COPY_MUT", "meta_copy_mut", 0.0, float), ("META_STD_DEV", "meta_std_dev", 0.0, float),
+    ("DEATH_PROB", "death_prob", 0.0, float),
+    ("AGE_DEVIATION", "age_deviation", 0, int), ("DIVIDE_FAILURE_RESETS", "divide_failure_resets", 0, int),
+    ("SPECIAL_MUT_LINE", "special_mut_line", -1, int), ("POPULATION_CAP", "population_cap", 0, int),
+    ("GENERATION_INC_METHOD", "generation_inc_method", 1, int),
+    ("RESET_INPUTS_ON_DIVIDE", "reset_inputs_on_divide", 0, int),
+    ("EPIGENETIC_METHOD", "epigenetic_method", 0, int), ("MIN_CYCLES", "min_cycles", 0, int),
+    ("REQUIRED_TASK", "required_task", -1, int), ("IMMUNITY_TASK", "immunity_task", -1, int),
+    ("REQUIRED_REACTION", "required_reaction", -1, int), ("IMMUNITY_REACTION", "immunity_reaction", -1, int),
+    ("REQUIRE_SINGLE_REACTION", "require_single_reaction", 0, int),
+    ("MAX_UNIQUE_TASK_COUNT", "max_unique_task_count", -1, int),
+    ("REQUIRE_EXACT_COPY", "require_exact_copy", 0, int), ("FITNESS_METHOD", "fitness_method", 0, int),
+    ("JUV_PERIOD", "juv_period", 0, int),
 ]
+# Divide_TestFitnessMeasures1 (cpu/cHardwareBase.cc:978-1085) runs a test CPU
+# on every offspring when any of these is set: avgpu_cfg.test_fitness_measures
+TEST_FITNESS_KNOBS = ["REVERT_FATAL", "REVERT_DETRIMENTAL", "REVERT_NEUTRAL", "REVERT_BENEFICIAL",
+                      "REVERT_TASKLOSS", "REVERT_EQUALS", "STERILIZE_FATAL", "STERILIZE_DETRIMENTAL",
+                      "STERILIZE_NEUTRAL", "STERILIZE_BENEFICIAL", "STERILIZE_TASKLOSS",
+                      "STERILIZE_UNSTABLE", "FAIL_IMPLICIT"]
 # Knobs accepted without effect, with the reason.  SPECULATIVE only decides
 # whether the reference's serial ProcessStep pre-executes up to 32 more
 # instructions of the picked organism (main/cPopulation.cc:5740-5788); the
@@ -192,27 +231,16 @@ UNSUPPORTED_NONZERO = [
 IGNORED = {"SPECULATIVE": "batched update: no serial schedule to speculate on"}
 
 
-def unsupported_knobs(cfg):
-    """Names of the UNSUPPORTED_NONZERO keys a files.AvidaConfig sets non-zero."""
-    bad = []
-    for k in UNSUPPORTED_NONZERO:
-        v = cfg.get(k, 0)
-        try:
-            nz = float(v) != 0.0
-        except (TypeError, ValueError):
-            nz = True
-        if nz:
-            bad.append(k)
-    return bad
+def _num(v, kind, default):
+    try:
+        return kind(float(v))
+    except (TypeError, ValueError):
+        return default
 
 
 def cfg_from_avida(cfg, seed=None) -> AvgpuCfg:
-    """Fill an AvgpuCfg from a files.AvidaConfig; raise ValueError for a knob
-    of UNSUPPORTED_NONZERO set non-zero."""
-    bad = unsupported_knobs(cfg)
-    if bad:
-        raise ValueError("avida.cfg sets mutation / death knobs this path does not implement: "
-                         + ", ".join(bad))
+    """Fill an AvgpuCfg from a files.AvidaConfig.  Every knob of the path is a
+    field; the library refuses (avgpu_create) what it does not implement."""
     g = cfg.get
     c = AvgpuCfg()
     c.world_x, c.world_y = g("WORLD_X"), g("WORLD_Y")
@@ -248,25 +276,35 @@ def cfg_from_avida(cfg, seed=None) -> AvgpuCfg:
     c.required_bonus = g("REQUIRED_BONUS")
     s = g("RANDOM_SEED") if seed is None else seed
     c.seed = int(s) & 0xFFFFFFFFFFFFFFFF if int(s) >= 0 else 0x1234ABCD
-    c.divide_slip_prob = float(g("DIVIDE_SLIP_PROB", 0.0))
-    c.divide_uniform_prob = float(g("DIVIDE_UNIFORM_PROB", 0.0))
-    c.slip_fill_mode = int(float(g("SLIP_FILL_MODE", 0)))
-    c.div_mut_prob = float(g("DIV_MUT_PROB", 0.0))
-    c.parent_mut_prob = float(g("PARENT_MUT_PROB", 0.0))
-    c.divide_poisson_slip_mean = float(g("DIVIDE_POISSON_SLIP_MEAN", 0.0))
-    c.divide_poisson_mut_mean = float(g("DIVIDE_POISSON_MUT_MEAN", 0.0))
-    c.divide_poisson_ins_mean = float(g("DIVIDE_POISSON_INS_MEAN", 0.0))
-    c.divide_poisson_del_mean = float(g("DIVIDE_POISSON_DEL_MEAN", 0.0))
-    c.div_ins_prob = float(g("DIV_INS_PROB", 0.0))
-    c.div_del_prob = float(g("DIV_DEL_PROB", 0.0))
-    c.div_uniform_prob = float(g("DIV_UNIFORM_PROB", 0.0))
-    c.div_slip_prob = float(g("DIV_SLIP_PROB", 0.0))
-    c.divide_trans_prob = float(g("DIVIDE_TRANS_PROB", 0.0))
-    c.divide_poisson_trans_mean = float(g("DIVIDE_POISSON_TRANS_MEAN", 0.0))
-    c.div_trans_prob = float(g("DIV_TRANS_PROB", 0.0))
-    if (c.divide_trans_prob or c.divide_poisson_trans_mean or c.div_trans_prob) and \
-            int(float(g("TRANS_FILL_MODE", 0))) != 0:
-        raise ValueError("TRANS_FILL_MODE 1 (scrambled) is not on this path")
+    f = lambda k, d=0.0: _num(g(k, d), float, d)   # noqa: E731
+    i = lambda k, d=0: _num(g(k, d), int, d)       # noqa: E731
+    c.divide_slip_prob = f("DIVIDE_SLIP_PROB")
+    c.divide_uniform_prob = f("DIVIDE_UNIFORM_PROB")
+    c.slip_fill_mode = i("SLIP_FILL_MODE")
+    c.div_mut_prob = f("DIV_MUT_PROB")
+    c.parent_mut_prob = f("PARENT_MUT_PROB")
+    c.divide_poisson_slip_mean = f("DIVIDE_POISSON_SLIP_MEAN")
+    c.divide_poisson_mut_mean = f("DIVIDE_POISSON_MUT_MEAN")
+    c.divide_poisson_ins_mean = f("DIVIDE_POISSON_INS_MEAN")
+    c.divide_poisson_del_mean = f("DIVIDE_POISSON_DEL_MEAN")
+    c.div_ins_prob = f("DIV_INS_PROB")
+    c.div_del_prob = f("DIV_DEL_PROB")
+    c.div_uniform_prob = f("DIV_UNIFORM_PROB")
+    c.div_slip_prob = f("DIV_SLIP_PROB")
+    c.divide_trans_prob = f("DIVIDE_TRANS_PROB")
+    c.divide_poisson_trans_mean = f("DIVIDE_POISSON_TRANS_MEAN")
+    c.div_trans_prob = f("DIV_TRANS_PROB")
+    c.copy_uniform_prob = f("COPY_UNIFORM_PROB")
+    c.copy_slip_prob = f("COPY_SLIP_PROB")
+    c.slip_copy_mode = i("SLIP_COPY_MODE")
+    c.trans_fill_mode = i("TRANS_FILL_MODE")
+    c.parent_ins_prob = f("PARENT_INS_PROB")
+    c.parent_del_prob = f("PARENT_DEL_PROB")
+    for key, field, default, kind in REFUSED_KNOBS:
+        setattr(c, field, _num(g(key, default), kind, default))
+    nmi = g("NO_MUT_INSTS", "")
+    c.no_mut_insts_len = len(str(nmi).strip()) if nmi not in (None, 0) else 0
+    c.test_fitness_measures = int(any(_num(g(k, 0), float, 1.0) != 0.0 for k in TEST_FITNESS_KNOBS))
     return c
 
 
@@ -343,6 +381,7 @@ def bind_common(lib, prefix):
         "set_genotype_keys": (C.c_int, [V, I64, I64, V]),
         "state_digests": (C.c_int, [V, I64, I64, V]),
         "set_rng_mode": (C.c_int, [V, C.c_int, V, I64, V]),
+        "set_serial_streams": (C.c_int, [V, V, I64, V, I64]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, p + name, None)
@@ -369,6 +408,7 @@ def load_product(path=None):
     lib.avgpu_create.restype = C.c_void_p
     lib.avgpu_create.argtypes = [C.POINTER(AvgpuCfg), C.c_int, C.c_int64]
     lib.avgpu_cfg_defaults.argtypes = [C.POINTER(AvgpuCfg)]
+    lib.avgpu_check_cfg.argtypes = [C.POINTER(AvgpuCfg)]
     lib.avgpu_sync.argtypes = [C.c_void_p]
     lib.avgpu_get_stats.argtypes = [C.c_void_p, C.POINTER(AvgpuUpdateStats)]
     lib.avgpu_stats_vector.argtypes = [C.c_void_p, C.POINTER(C.c_void_p)]

@@ -157,6 +157,8 @@ struct Child {
   uint32_t lo, hi, ctr;
   const int32_t* ltask;   // the parent's last task counts, ltask[q * lstride]
   int64_t lstride;
+  const int32_t* inputs = nullptr;   // the cell inputs, drawn by the caller (serial world), or
+                                     // nullptr: SetupInputs from the offspring's own stream
 };
 // Run by a group of G lanes (G = 64: a wave, 32: a half-wave); `lane` is the
 // lane's index inside its group.
@@ -194,9 +196,13 @@ __device__ __forceinline__ void setup_child(const DevWorld& W, int64_t c, const 
     case 11: {
       uint32_t ctr = b.ctr;
       // cEnvironment::SetupInputs random (main/cEnvironment.cc:1268-1271)
-      W.inputs[c] = (15 << 24) + (int)rng_below(b.lo, b.hi, ctr, 1u << 24);
-      W.inputs[N + c] = (51 << 24) + (int)rng_below(b.lo, b.hi, ctr, 1u << 24);
-      W.inputs[2 * N + c] = (85 << 24) + (int)rng_below(b.lo, b.hi, ctr, 1u << 24);
+      if (b.inputs) {
+        W.inputs[c] = b.inputs[0]; W.inputs[N + c] = b.inputs[1]; W.inputs[2 * N + c] = b.inputs[2];
+      } else {
+        W.inputs[c] = (15 << 24) + (int)rng_below(b.lo, b.hi, ctr, 1u << 24);
+        W.inputs[N + c] = (51 << 24) + (int)rng_below(b.lo, b.hi, ctr, 1u << 24);
+        W.inputs[2 * N + c] = (85 << 24) + (int)rng_below(b.lo, b.hi, ctr, 1u << 24);
+      }
       W.rng[c] = b.lo; W.rng[N + c] = b.hi; W.rng[2 * N + c] = ctr;
       if (W.rec_off) W.rec_off[c] = -1;         // offspring: counter streams
       break; }

@@ -76,6 +76,7 @@ struct avgpu_world {
   int64_t last_launches = 0;
   bool has_test_buffers = false;
   double* rec_buf = nullptr;    // RECORDED mode stream (avgpu_set_rng_mode)
+  double* srec_buf[2] = {nullptr, nullptr};   // the serial world's recorded streams
   // strip tiles
   int ntiles_last = 0;
   bool tile_buffers = false;
@@ -181,6 +182,11 @@ int setup_world(avgpu_world* w, int64_t n, bool test_buffers) {
     return (uint64_t)std::ceil(p * 4294967296.0);
   };
   W.th_copy_mut = th(c.copy_mut_prob);
+  W.th_copy_ins = th(c.copy_ins_prob); W.p_copy_ins = c.copy_ins_prob;
+  W.th_copy_del = th(c.copy_del_prob); W.p_copy_del = c.copy_del_prob;
+  W.th_copy_uni = th(c.copy_uniform_prob); W.p_copy_uni = c.copy_uniform_prob;
+  W.th_copy_slip = th(c.copy_slip_prob); W.p_copy_slip = c.copy_slip_prob;
+  W.copy_ext = (W.th_copy_ins || W.th_copy_del || W.th_copy_uni || W.th_copy_slip) ? 1 : 0;
   W.th_div_mut = th(c.divide_mut_prob);
   W.th_div_ins = th(c.divide_ins_prob);
   W.th_div_del = th(c.divide_del_prob);
@@ -198,6 +204,8 @@ int setup_world(avgpu_world* w, int64_t n, bool test_buffers) {
   W.th_dtrans = th(c.divide_trans_prob); W.p_dtrans = c.divide_trans_prob;
   W.th_par_site = th(c.parent_mut_prob);
   W.p_par_site = c.parent_mut_prob;
+  W.th_par_ins = th(c.parent_ins_prob); W.p_par_ins = c.parent_ins_prob;
+  W.th_par_del = th(c.parent_del_prob); W.p_par_del = c.parent_del_prob;
   W.slip_fill_mode = c.slip_fill_mode;
   W.rec = nullptr; W.rec_n = 0; W.rec_off = nullptr;
   W.seed_lo = (uint32_t)c.seed;
@@ -224,27 +232,65 @@ int setup_world(avgpu_world* w, int64_t n, bool test_buffers) {
   return 0;
 }
 
+// The avida.cfg values this path cannot run with the reference's semantics
+// (main/cAvidaConfig.h): an empty string when the configuration is on the
+// path, else the reason avgpu_create refuses it (AVGPU_EUNSUPPORTED).
+std::string unsupported_cfg(const avgpu_cfg& c) {
+  auto nz = [](double v) { return v != 0.0; };
+  const bool slips = nz(c.divide_slip_prob) || nz(c.divide_poisson_slip_mean) || nz(c.div_slip_prob);
+  if (slips && c.slip_fill_mode != 0 && c.slip_fill_mode != 4)
+    return "SLIP_FILL_MODE 1-3 (nop-X, random, scrambled)";
+  if (nz(c.copy_slip_prob) && c.slip_copy_mode != 0)
+    return "SLIP_COPY_MODE 1 (a slip of the whole memory at the write head)";
+  if ((nz(c.divide_trans_prob) || nz(c.divide_poisson_trans_mean) || nz(c.div_trans_prob)) && c.trans_fill_mode != 0)
+    return "TRANS_FILL_MODE 1 (scrambled)";
+  if (c.divide_poisson_slip_mean > 700.0 || c.divide_poisson_mut_mean > 700.0 ||
+      c.divide_poisson_ins_mean > 700.0 || c.divide_poisson_del_mean > 700.0 ||
+      c.divide_poisson_trans_mean > 700.0)
+    return "DIVIDE_POISSON_*_MEAN above 700 (exp(-mean) underflows)";
+  if (c.divide_method != 1) return "DIVIDE_METHOD other than 1 (split)";
+  if (c.world_geometry != 1 && c.world_geometry != 2) return "WORLD_GEOMETRY other than 1 (grid) or 2 (torus)";
+  if (c.slicing_method < 0 || c.slicing_method > 2) return "SLICING_METHOD other than 0, 1, 2";
+  if (c.base_merit_method < 0 || c.base_merit_method > 5) return "BASE_MERIT_METHOD other than 0..5";
+  if (c.birth_method != 0 && c.birth_method != 3)
+    return "BIRTH_METHOD other than 0 (random neighbour) and 3 (empty cells only)";
+  if (c.death_method < 0 || c.death_method > 2) return "DEATH_METHOD other than 0, 1, 2";
+  if (c.alloc_method != 0 && c.alloc_method != 2) return "ALLOC_METHOD other than 0 (default) and 2 (random)";
+  if (nz(c.point_mut_prob) || nz(c.point_ins_prob) || nz(c.point_del_prob) || nz(c.inst_point_mut_prob))
+    return "POINT_MUT_PROB / POINT_INS_PROB / POINT_DEL_PROB / INST_POINT_MUT_PROB (cosmic-ray mutations)";
+  if (nz(c.div_lgt_prob) || nz(c.divide_lgt_prob) || nz(c.divide_poisson_lgt_mean))
+    return "DIV_LGT_PROB / DIVIDE_LGT_PROB / DIVIDE_POISSON_LGT_MEAN (lateral gene transfer)";
+  if (nz(c.inject_mut_prob) || nz(c.inject_ins_prob) || nz(c.inject_del_prob)) return "INJECT_*_PROB";
+  if (nz(c.meta_copy_mut) || nz(c.meta_std_dev)) return "META_COPY_MUT / META_STD_DEV";
+  if (nz(c.death_prob)) return "DEATH_PROB";
+  if (c.age_deviation != 0) return "AGE_DEVIATION";
+  if (c.divide_failure_resets != 0) return "DIVIDE_FAILURE_RESETS";
+  if (c.special_mut_line >= 0) return "SPECIAL_MUT_LINE";
+  if (c.population_cap > 0) return "POPULATION_CAP";
+  if (c.generation_inc_method != 1) return "GENERATION_INC_METHOD other than 1";
+  if (c.reset_inputs_on_divide != 0) return "RESET_INPUTS_ON_DIVIDE";
+  if (c.epigenetic_method != 0) return "EPIGENETIC_METHOD";
+  if (c.min_cycles != 0) return "MIN_CYCLES";
+  if (c.required_task >= 0 || c.immunity_task >= 0 || c.required_reaction >= 0 || c.immunity_reaction >= 0 ||
+      c.require_single_reaction != 0 || c.max_unique_task_count >= 0)
+    return "REQUIRED_TASK / IMMUNITY_TASK / REQUIRED_REACTION / IMMUNITY_REACTION / REQUIRE_SINGLE_REACTION / "
+           "MAX_UNIQUE_TASK_COUNT";
+  if (c.require_exact_copy != 0) return "REQUIRE_EXACT_COPY";
+  if (c.fitness_method != 0) return "FITNESS_METHOD other than 0";
+  if (c.juv_period != 0) return "JUV_PERIOD";
+  if (c.no_mut_insts_len != 0) return "NO_MUT_INSTS";
+  if (c.test_fitness_measures != 0) return "REVERT_* / STERILIZE_* (Divide_TestFitnessMeasures1)";
+  return std::string();
+}
+
 avgpu_world* create_world(const avgpu_cfg* cfg, int device, int64_t n, bool test_buffers) {
   if (!cfg) { fail(AVGPU_EINVAL, "cfg is NULL"); return nullptr; }
-  if (cfg->copy_ins_prob > 0.0 || cfg->copy_del_prob > 0.0) {
-    fail(AVGPU_EUNSUPPORTED, "COPY_INS_PROB / COPY_DEL_PROB are not on the GPU path yet");
-    return nullptr;
-  }
-  if ((cfg->divide_slip_prob > 0.0 || cfg->divide_poisson_slip_mean > 0.0 || cfg->div_slip_prob > 0.0) &&
-      cfg->slip_fill_mode != 0 &&
-      cfg->slip_fill_mode != 4) {
-    fail(AVGPU_EUNSUPPORTED, "SLIP_FILL_MODE 1-3 (nop-X, random, scrambled) are not on the GPU path");
-    return nullptr;
-  }
-  if (cfg->divide_poisson_slip_mean > 700.0 || cfg->divide_poisson_mut_mean > 700.0 ||
-      cfg->divide_poisson_ins_mean > 700.0 || cfg->divide_poisson_del_mean > 700.0 ||
-      cfg->divide_poisson_trans_mean > 700.0) {
-    fail(AVGPU_EUNSUPPORTED, "DIVIDE_POISSON_*_MEAN above 700 (exp(-mean) underflows)");
-    return nullptr;
-  }
-  if (cfg->divide_method != 1) {
-    fail(AVGPU_EUNSUPPORTED, "only DIVIDE_METHOD 1 (split) is on the GPU path");
-    return nullptr;
+  {
+    const std::string why = unsupported_cfg(*cfg);
+    if (!why.empty()) {
+      fail(AVGPU_EUNSUPPORTED, why + " is not on the GPU path");
+      return nullptr;
+    }
   }
   if (hipSetDevice(device) != hipSuccess) { fail(AVGPU_EHIP, "hipSetDevice failed"); return nullptr; }
   avgpu_world* w = new avgpu_world();
@@ -437,10 +483,22 @@ void avgpu_cfg_defaults(avgpu_cfg* c) {
   c->divide_method = 1; c->max_label_exe_size = 1; c->birth_method = 0; c->prefer_empty = 1;
   c->allow_parent = 1; c->test_cpu_time_mod = 20; c->inherit_merit = 1;
   c->seed = 101;
+  // main/cAvidaConfig.h defaults of the refused knobs that are not 0
+  c->special_mut_line = -1; c->generation_inc_method = 1;
+  c->required_task = -1; c->immunity_task = -1;
+  c->required_reaction = -1; c->immunity_reaction = -1;
+  c->max_unique_task_count = -1;
 }
 
 avgpu_world* avgpu_create(const avgpu_cfg* cfg, int device, int64_t num_cells) {
   return create_world(cfg, device, num_cells, false);
+}
+
+int avgpu_check_cfg(const avgpu_cfg* cfg) {
+  if (!cfg) return fail(AVGPU_EINVAL, "cfg is NULL");
+  const std::string why = unsupported_cfg(*cfg);
+  if (!why.empty()) return fail(AVGPU_EUNSUPPORTED, why + " is not on the GPU path");
+  return 0;
 }
 
 int avgpu_destroy(avgpu_world* w) {
@@ -449,6 +507,7 @@ int avgpu_destroy(avgpu_world* w) {
   if (w->own_stream) hipStreamSynchronize(w->own_stream);
   for (void* p : w->allocs) hipFree(p);
   if (w->rec_buf) hipFree(w->rec_buf);
+  for (double* p : w->srec_buf) if (p) hipFree(p);
   if (w->ev0) hipEventDestroy(w->ev0);
   if (w->ev1) hipEventDestroy(w->ev1);
   for (int i = 0; i < avgpu_world::RING; i++) {
@@ -703,26 +762,67 @@ int avgpu_run_update(avgpu_world* w, avgpu_update_stats* out) {
   return 0;
 }
 
+// the serial world's state, allocated on first use: merit sum tree,
+// speculative credits, connection-list facings, the scheduler's and the
+// context's counter streams (keyed by the seed, as the oracle's)
+static int serial_alloc(avgpu_world* w) {
+  DevWorld& W = w->W;
+  if (W.stree) return 0;
+  int rc;
+  int64_t size = 1;
+  while (size < W.n) size <<= 1;
+  W.stree_size = size;
+  if ((rc = w->alloc(&W.stree, (size_t)(2 * size))) < 0) return rc;
+  if ((rc = w->alloc(&W.spec, (size_t)W.n)) < 0) return rc;
+  if ((rc = w->alloc(&W.face, (size_t)W.n)) < 0) return rc;
+  if ((rc = w->alloc(&W.grng, 3)) < 0) return rc;
+  if ((rc = w->alloc(&W.sctx, 3)) < 0) return rc;
+  uint32_t g[3] = {0, 0, 0}, x[3] = {0, 0, 0};
+  const uint64_t seed = (uint64_t)w->cfg.seed;
+  derive_key((uint32_t)seed, (uint32_t)(seed >> 32), 0x5CEDu, 0xC0FFEEu, g[0], g[1]);
+  derive_key((uint32_t)seed, (uint32_t)(seed >> 32), 0xC7C7u, 0x5EED5u, x[0], x[1]);
+  HIPCHK(hipMemcpyAsync(W.grng, g, sizeof(g), hipMemcpyHostToDevice, w->stream));
+  HIPCHK(hipMemcpyAsync(W.sctx, x, sizeof(x), hipMemcpyHostToDevice, w->stream));
+  HIPCHK(hipStreamSynchronize(w->stream));
+  return 0;
+}
+
+int avgpu_set_serial_streams(avgpu_world* w, const double* sched, int64_t n_sched, const double* ctx,
+                             int64_t n_ctx) {
+  if (!w) return fail(AVGPU_EINVAL, "NULL world");
+  if ((sched && n_sched <= 0) || (ctx && n_ctx <= 0)) return fail(AVGPU_EINVAL, "empty stream");
+  int rc = serial_alloc(w);
+  if (rc < 0) return rc;
+  DevWorld& W = w->W;
+  for (double** p : {&w->srec_buf[0], &w->srec_buf[1]})
+    if (*p) { hipFree(*p); *p = nullptr; }
+  W.srec_sched = nullptr; W.srec_sched_n = 0; W.srec_ctx = nullptr; W.srec_ctx_n = 0;
+  if (sched) {
+    HIPCHK(hipMalloc(&w->srec_buf[0], (size_t)n_sched * sizeof(double)));
+    HIPCHK(hipMemcpy(w->srec_buf[0], sched, (size_t)n_sched * sizeof(double), hipMemcpyHostToDevice));
+    W.srec_sched = w->srec_buf[0]; W.srec_sched_n = n_sched;
+  }
+  if (ctx) {
+    HIPCHK(hipMalloc(&w->srec_buf[1], (size_t)n_ctx * sizeof(double)));
+    HIPCHK(hipMemcpy(w->srec_buf[1], ctx, (size_t)n_ctx * sizeof(double), hipMemcpyHostToDevice));
+    W.srec_ctx = w->srec_buf[1]; W.srec_ctx_n = n_ctx;
+  }
+  // both positions restart at 0 (counter streams: their counters)
+  HIPCHK(hipMemsetAsync(W.grng + 2, 0, 4, w->stream));
+  HIPCHK(hipMemsetAsync(W.sctx + 2, 0, 4, w->stream));
+  HIPCHK(hipStreamSynchronize(w->stream));
+  return 0;
+}
+
 int avgpu_run_serial_updates(avgpu_world* w, int n, avgpu_update_stats* last) {
   int rc = ready(w);
   if (rc < 0) return rc;
   if (n < 0) return fail(AVGPU_EINVAL, "n_updates < 0");
   DevWorld& W = w->W;
-  if (W.rec) return fail(AVGPU_EUNSUPPORTED, "the serial world draws from counter streams only");
+  if (W.rec) return fail(AVGPU_EUNSUPPORTED, "the serial world takes its own two streams (avgpu_set_serial_streams), "
+                                             "not per-organism recorded streams");
   if (W.tiled) return fail(AVGPU_EUNSUPPORTED, "the serial world runs single worlds, not strip tiles");
-  if (!W.stree) {
-    int64_t size = 1;
-    while (size < W.n) size <<= 1;
-    W.stree_size = size;
-    if ((rc = w->alloc(&W.stree, (size_t)(2 * size))) < 0) return rc;
-    if ((rc = w->alloc(&W.spec, (size_t)W.n)) < 0) return rc;
-    if ((rc = w->alloc(&W.grng, 3)) < 0) return rc;
-    // the scheduler's stream (oracle World::global_rng): keyed by the seed
-    uint32_t g[3] = {0, 0, 0};
-    const uint64_t seed = (uint64_t)w->cfg.seed;
-    derive_key((uint32_t)seed, (uint32_t)(seed >> 32), 0x5CEDu, 0xC0FFEEu, g[0], g[1]);
-    HIPCHK(hipMemcpyAsync(W.grng, g, sizeof(g), hipMemcpyHostToDevice, w->stream));
-  }
+  if ((rc = serial_alloc(w)) < 0) return rc;
   for (int u = 0; u < n; u++) {
     launch_reset_counts(W, w->stream);
     launch_resources_begin(W, w->stream);
@@ -771,6 +871,7 @@ int avgpu_get_stats(avgpu_world* w, avgpu_update_stats* out) {
   out->cum_births = (int64_t)v[31];
   out->slices = (int64_t)v[32];
   out->lane_steps = (int64_t)v[33];
+  out->births_overwritten = (int64_t)v[34];
   return 0;
 }
 

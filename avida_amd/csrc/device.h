@@ -32,6 +32,8 @@
 // (zero, default bonus) implicitly -- the SoA rows are stale until the
 // organism's first slice writes them back.  Every reader honours the bit.
 #define CTL_FRESH 0x800u
+// serial world: died in a speculative step (m_spec_die); removed at its next pick
+#define CTL_SPECDIE 0x1000u
 
 #define NUM_CLASSES 4
 #define ACLASS_NONE 0xFF
@@ -220,10 +222,17 @@ struct DevWorld {
   // for RECORDED draws
   uint64_t th_copy_mut, th_div_mut, th_div_ins, th_div_del, th_div_slip, th_div_uni;
   double p_copy_mut, p_div_mut, p_div_ins, p_div_del, p_div_slip, p_div_uni;
+  // COPY_INS / COPY_DEL / COPY_UNIFORM / COPY_SLIP (SLIP_COPY_MODE 0) of
+  // Inst_HeadCopy; copy_ext: any of them non-zero
+  uint64_t th_copy_ins, th_copy_del, th_copy_uni, th_copy_slip;
+  double p_copy_ins, p_copy_del, p_copy_uni, p_copy_slip;
+  int32_t copy_ext;
   uint64_t th_div_site;   // DIV_MUT_PROB (per-site substitutions on divide)
   double p_div_site;
   uint64_t th_par_site;   // PARENT_MUT_PROB (per-site substitutions in the parent)
   double p_par_site;
+  uint64_t th_par_ins, th_par_del;   // PARENT_INS_PROB, PARENT_DEL_PROB (per site, in the parent)
+  double p_par_ins, p_par_del;
   double pois_L[5];       // exp(-DIVIDE_POISSON_{SLIP,MUT,INS,DEL,TRANS}_MEAN), 0 = off
   int32_t pois_any;
   uint64_t th_dsite[5];   // DIV_INS_PROB, DIV_DEL_PROB, DIV_UNIFORM_PROB, DIV_SLIP_PROB, DIV_TRANS_PROB
@@ -244,7 +253,15 @@ struct DevWorld {
   double* stree;
   int64_t stree_size;
   int32_t* spec;     // [n]
-  uint32_t* grng;    // [3] lo hi ctr
+  uint32_t* grng;    // [3] lo hi ctr: the scheduler's stream (picks)
+  uint32_t* sctx;    // [3] lo hi ctr: the context stream (every other draw of the serial world)
+  uint8_t* face;     // [n] connection-list rotation of each cell (cPopulationCell::Rotate)
+  // recorded serial streams (avgpu_set_serial_streams): the k-th pick / context
+  // draw is srec_sched[k] / srec_ctx[k] (the counters grng[2] / sctx[2])
+  const double* srec_sched;
+  int64_t srec_sched_n;
+  const double* srec_ctx;
+  int64_t srec_ctx_n;
   uint32_t seed_lo, seed_hi;
   // Strip tiles (multi-GPU, DESIGN.md "Multi-GPU"): this world holds rows
   // [row0, row0+rows) of a world_x x global_rows torus / grid.  When tiled,
@@ -310,6 +327,8 @@ __host__ __device__ inline int64_t record_bytes(int x, int64_t arena) {
 enum { SEG_PSLIP = 0, SEG_SSLIP, SEG_TTRANS, SEG_PTRANS, SEG_STRANS, SEG_PMUT, SEG_PINS, SEG_PDEL, SEG_SMUT, SEG_SINS, SEG_SDEL, SEG_SUNI, NSEG };
 #define CNT_SUB_OVERFLOW 22   /* DIV_MUT_PROB substitutions that found the b_subs arena full (must stay 0) */
 #define CNT_OVERSIZE 21   /* offspring a slip grew past AVGPU_MAX_GENOME (counted in DROPPED too) */
+#define CNT_MEM_CAP 23    /* copy insertions past AVGPU_MAX_GENOME sites / removals from one site (skipped) */
+#define CNT_OVERWRITTEN 24  /* offspring placed, then killed by a later birth into the same cell this update */
 // 32..37: AVGPU_PHASE_CLOCKS loop cycles by block (decode, fast, copy, switch,
 // wave phase, advance); 38..43: slow-switch cycles in pop, push, IO, h-alloc,
 // h-divide, h-search/if-label

@@ -108,12 +108,17 @@ __host__ __device__ constexpr int tape_stride(int S) { return S == CLASS0_SIZE ?
 enum { E_SLIP = 1, E_POINT = 2, E_INS = 3, E_DEL = 4, E_TRANS = 5 };
 __device__ __forceinline__ int edit_word(int kind, int a, int b) { return kind | (a << 3) | (b << 15); }
 
-// serial = 1: one step of the serial world (k_serial_update): lane 0 runs
-// cell `first` for the reference's ProcessStepSpeculative -- one instruction,
-// then up to 32 more until the next one is IO or h-divide, an offspring is
-// born or the organism dies (main/cPopulation.cc:5740-5788) -- and leaves its
-// offspring in the cell's primary record (placed by the caller).  Returns,
-// for the running lane: instructions executed | divides << 16 | birth << 24.
+// serial != 0: a step of the serial world (k_serial_update), lane 0 running
+// cell `first` for the reference's ProcessStepSpeculative
+// (main/cPopulation.cc:5740-5788) with every draw from the world's context
+// stream (DevWorld::sctx / srec_ctx) -- serial = 1: the one non-speculative
+// SingleProcess; an offspring is left in the cell's primary record, placed by
+// the caller at once (inside the h-divide, as ActivateOffspring does); serial
+// = 2: the speculative run, up to 32 instructions, each rejected before IO or
+// h-divide (cpu/cHardwareCPU.cc:961-968); one that reaches the age limit sets
+// m_spec_die (:1045-1049: not counted, the organism stays until its next
+// pick, CTL_SPECDIE).  Returns, for the running lane: instructions executed |
+// divides << 16 | birth << 24 | spec death << 25.
 // C0W: the class-0 sweep of a world update, with the class and the mode known
 // at compile time -- the test-CPU and list-row code drops out of the hot loop;
 // SIMPLE: the environment's reactions are the simple form (env_simple) with
@@ -286,6 +291,7 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
   // ---- hot state into registers ----
   int r0 = 0, r1 = 0, r2 = 0, ip = 0, rh = 0, wh = 0, fh = 0;
   uint32_t ctl = 0, rl = 0, klo = 0, khi = 0, kct = 0;
+  uint32_t olo = 0, ohi = 0;     // the organism's own key (its offspring's keys derive from it)
   int cyc = 0, tu = 0, gs = 0, mx = 0, blen = 0, budget = 0, errs = 0;
   int in0 = 0, in1 = 0, in2 = 0, intot = 0, inptr = 0, inp0 = 0, inp1 = 0, inp2 = 0;
   int outv = 0, outtot = 0;
@@ -305,16 +311,19 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
   for (int q = 0; q < AVGPU_MAX_REACTIONS; q++) rc[q] = 0;
   bool didv = false, prim = false, prim0 = false;
   int sbirth = 0;                // serial step: an offspring is in the primary record
+  int sdie = 0;                  // serial speculative run: m_spec_die
   int ndrop = 0, noversize = 0;
   if (active) {
     // written at birth (setup_child) or by the previous slice
     ctl = W.ctl[cell];
     mx = W.max_exec[cell]; blen = W.birth_len[cell];
     klo = W.rng[cell]; khi = W.rng[N + cell]; kct = W.rng[2 * N + cell];
+    olo = klo; ohi = khi;
+    if (serial) { klo = W.sctx[0]; khi = W.sctx[1]; kct = W.sctx[2]; }   // the context stream
     budget = W.budget[cell];
     prim = (budget & BUDGET_PRIM) != 0;   // a spilled slice already used its primary record
     budget &= ~BUDGET_PRIM;
-    if (serial) { budget = 33; prim = false; }
+    if (serial) { budget = serial == 1 ? 1 : 32; prim = false; }
     inp0 = W.inputs[cell]; inp1 = W.inputs[N + cell]; inp2 = W.inputs[2 * N + cell];
     dexe = W.executed[cell]; dcop = W.copied[cell]; dgen = W.generation[cell];
     bonus = W.default_bonus;
@@ -366,6 +375,9 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
   const double k_size_range = DEF ? 2.0 : W.size_range;
   const int k_require_allocate = DEF ? 1 : W.require_allocate, k_alloc_method = DEF ? 0 : W.alloc_method;
   const uint64_t k_th_copy_mut = W.th_copy_mut;
+  const int k_copy_ext = DEF ? 0 : W.copy_ext;
+  const uint64_t k_th_copy_ins = DEF ? 0ull : W.th_copy_ins, k_th_copy_del = DEF ? 0ull : W.th_copy_del;
+  const uint64_t k_th_copy_uni = DEF ? 0ull : W.th_copy_uni, k_th_copy_slip = DEF ? 0ull : W.th_copy_slip;
   const int k_rand_total = W.rand_total, k_n_ops = W.n_ops, k_n_react = W.n_react;
   const bool k_rand_lut = DEF || k_rand_total <= 256;   // GetRandomInst from the LUT
   // RECORDED streams (include/avida_gpu.h "random streams"): the organism's
@@ -374,8 +386,12 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
   int64_t rlim = 0;
   bool rover = false;
   if (REC && active) {
-    const int64_t off = W.rec_off[cell];
-    if (off >= 0) { rbase = W.rec + off; rlim = W.rec_n - off; }
+    if (serial) {
+      rbase = W.srec_ctx; rlim = W.srec_ctx_n;      // the serial world's recorded context stream
+    } else {
+      const int64_t off = W.rec_off[cell];
+      if (off >= 0) { rbase = W.rec + off; rlim = W.rec_n - off; }
+    }
   }
   // the reference's draws on a uniform u (Apto::RNG P / GetUInt)
   auto rd = [&]() -> double {
@@ -463,7 +479,7 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
       }
       // serial step: the speculative run ends before IO / h-divide
       // (cHardwareCPU::SingleProcess stall instructions, cpu/cHardwareCPU.cc:961-968)
-      if (serial && executed > 0 && (op == AVGPU_H_IO || op == AVGPU_H_H_DIVIDE)) stop = true;
+      if (serial == 2 && (op == AVGPU_H_IO || op == AVGPU_H_H_DIVIDE)) stop = true;
     if (!spill && !stop) {
     stepped = true;
     cyc++;                                                    // IncCPUCyclesUsed :929
@@ -524,6 +540,7 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
       rh = rha;
       wh = wha;
       int v = src_byte & CODE_MASK;
+      const uint32_t kct_h = kct, rl_h = rl;                  // rewound if the copy spills (below)
       // ReadInst (:1459-1466)
       if (v < 3) {
         const int len = rl & 15;
@@ -541,8 +558,79 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
       // the write head's executed flag: as read, or just set if it is the IP
       const int wex = (wh == ip) ? TF_EXEC : (dst_byte & TF_EXEC);
       T[wh] = (uint8_t)(wex | TF_COPIED | v);
-      rh = head_wrap(rh + 1, M);
-      wh = head_wrap(wh + 1, M);
+      // COPY_INS / DEL / UNIFORM / SLIP (:7153-7161, each drawing only at a
+      // non-zero rate, in that order): the memory grows or shrinks at the
+      // write head (cCPUMemory::Insert / Remove, cpu/cCPUMemory.cc:103-138;
+      // doUniformCopyMutation cpu/cHardwareBase.cc:597-612), or the read head
+      // jumps (SLIP_COPY_MODE 0).  A copy whose memory would outgrow this size
+      // class's LDS slot is rewound -- counter, label, written site, cycle --
+      // and the organism spills to the next class, which draws the same
+      // numbers again; at AVGPU_MAX_GENOME sites an insertion is skipped
+      // (counted), as in the oracle.
+      bool cspill = false;
+      if (!DEF && k_copy_ext && mode != AVGPU_MODE_TEST) {
+        int e_ins = -1, e_uni = -1, e_slip = -1;
+        bool e_del = false;
+        if (k_th_copy_ins && draw_p(k_th_copy_ins, W.p_copy_ins)) e_ins = rand_code();
+        if (k_th_copy_del) e_del = draw_p(k_th_copy_del, W.p_copy_del);
+        if (k_th_copy_uni && draw_p(k_th_copy_uni, W.p_copy_uni)) e_uni = (int)draw_below((uint32_t)(2 * k_n_ops + 1));
+        const bool e_slp = k_th_copy_slip && draw_p(k_th_copy_slip, W.p_copy_slip);
+        const bool ev = e_ins >= 0 || e_del || e_uni >= 0 || e_slp;
+        if (__builtin_expect(__ballot(ev) != 0ull, 0)) {
+          if (ev) {
+            // the size the memory passes through: a slot that cannot hold it
+            // (below the largest genome) makes the copy spill
+            int mx_sz = M + (e_ins >= 0 ? 1 : 0);
+            if (e_uni > k_n_ops) mx_sz = max(mx_sz, M + (e_ins >= 0 ? 1 : 0) - (e_del ? 1 : 0) + 1);
+            if (mx_sz > S && S < AVGPU_MAX_GENOME) {
+              T[wh] = (uint8_t)dst_byte;                       // undo the write, then the step
+              T[ipa] = (uint8_t)cur_byte;
+              kct = kct_h; rl = rl_h;
+              cyc--; tu--; executed--; budget++;
+              ip = ipa;
+              cspill = true;
+            } else {
+              int ncap = 0;
+              auto ins_at = [&](int pos, int code) {
+                if (M >= AVGPU_MAX_GENOME) { ncap++; return; }
+                for (int i = M; i > pos; i--) T[i] = T[i - 1];
+                T[pos] = (uint8_t)code;                        // new site: flags 0
+                M++;
+              };
+              auto del_at = [&](int pos) {
+                if (M <= 1) { ncap++; return; }
+                if (pos > M - 1) pos = M - 1;                  // Remove(size) drops the last site
+                for (int i = pos; i < M - 1; i++) T[i] = T[i + 1];
+                M--;
+              };
+              if (e_ins >= 0) ins_at(wh, e_ins);
+              if (e_del) del_at(wh);
+              if (e_uni >= 0) {
+                if (e_uni < k_n_ops) {
+                  if (wh < M) T[wh] = (uint8_t)((T[wh] & ~CODE_MASK) | (int)tab_u8(rcode + e_uni));   // SetInst
+                } else if (e_uni == k_n_ops) {
+                  del_at(wh);
+                } else {
+                  ins_at(wh, (int)tab_u8(rcode + e_uni - k_n_ops - 1));
+                }
+              }
+              if (e_slp) e_slip = (int)draw_below((uint32_t)M);   // read_head.Set(GetInt(size))
+              if (e_slip >= 0) rh = e_slip;
+              if (ncap) count_add(W, CNT_MEM_CAP, (unsigned long long)ncap);
+            }
+          }
+        }
+      }
+      if (cspill) {
+        spill = true;
+        stepped = false;
+      } else if (!DEF && k_copy_ext) {
+        rh = head_adjust(rh + 1, M);
+        wh = head_adjust(wh + 1, M);
+      } else {
+        rh = head_wrap(rh + 1, M);
+        wh = head_wrap(wh + 1, M);
+      }
     }
     CK(2);
     if (!(FAST_OPS & obit) && op != AVGPU_H_H_COPY) { pop = op; pr = r; stepped = false; }   // park
@@ -550,7 +638,10 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
     }  // run
     if (stepped && !stop) {
       if (adv) ip = head_wrap(ip + 1, M);                     // ip.Advance() :1013
-      if (mx > 0 && tu >= mx) alive = false;                  // death :1045-1049
+      if (mx > 0 && tu >= mx) {                               // death :1045-1049
+        if (serial == 2) { sdie = 1; stop = true; executed--; }   // m_spec_die: not counted
+        else alive = false;
+      }
     }
     // ---- slow phase ----
     const int npark = __popcll(__ballot(pop >= 0));
@@ -936,6 +1027,10 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
               // until the product falls below exp(-mean)), each kind's edits
               // right after its one-shot test, in an arena segment (WORLD)
               const bool segs = !DEF && W.seg_any;
+              // the longest the offspring gets while its edits apply: edit
+              // words hold 12-bit positions, so an offspring that passes 4095
+              // sites on the way is dropped as oversize (the oracle too)
+              int lmax = len;
               const bool pois = !DEF && W.pois_any;
               auto draw_u = [&]() -> double {
                 if (REC && rbase) return rd();
@@ -956,16 +1051,22 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
                 return n;
               };
               // reserve n words of segment k / write its i-th edit (WORLD only)
+              // (a full arena stops taking reservations, so its int32 fill
+              // cannot wrap: a reservation refused is placed at scap, i.e. it
+              // overflows below)
               auto preserve = [&](int k, int n) {
-                if (n > 0 && mode == AVGPU_MODE_WORLD) pofs[k] = atomicAdd(W.b_count + 2, n);
+                if (n > 0 && mode == AVGPU_MODE_WORLD)
+                  pofs[k] = (int64_t)__atomic_load_n(W.b_count + 2, __ATOMIC_RELAXED) >= W.scap
+                                ? (int)W.scap : atomicAdd(W.b_count + 2, n);
               };
               auto pput = [&](int k, int i, int ew) {
-                if (mode == AVGPU_MODE_WORLD && (int64_t)pofs[k] + i < W.scap) W.b_subs[pofs[k] + i] = ew;
+                if (mode == AVGPU_MODE_WORLD && pofs[k] >= 0 && (int64_t)pofs[k] + i < W.scap) W.b_subs[pofs[k] + i] = ew;
               };
               auto slip_edit = [&]() -> int {   // doSlipMutation :621-694
                 const int from = (int)draw_below((uint32_t)len + 1u);
                 const int to = from == 0 ? (int)draw_below((uint32_t)len) : (int)draw_below((uint32_t)len + 1u);
                 len += from - to;
+                lmax = max(lmax, len);
                 return edit_word(E_SLIP, from, to);
               };
               auto uniform_edit = [&]() -> int {   // doUniformMutation :572-595
@@ -978,6 +1079,7 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
                 } else if (len != g_max) {
                   ew = edit_word(E_INS, (int)draw_below((uint32_t)len + 1u), (int)tab_u8(rcode + mut - k_n_ops - 1));
                   len++;
+                  lmax = max(lmax, len);
                 }
                 return ew;
               };
@@ -986,6 +1088,7 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
                 const int to = from == 0 ? (int)draw_below((uint32_t)len) : (int)draw_below((uint32_t)len + 1u);
                 e0 = edit_word(E_SLIP, from, to);
                 len += from - to;
+                lmax = max(lmax, len);
               }
               if (pois) {                            // Poisson slips :318-320
                 const int n = npois(0);
@@ -1008,6 +1111,7 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
                 pput(k, 2 * i, edit_word(E_TRANS, ins_loc, to));
                 pput(k, 2 * i + 1, from);
                 len += from - to;
+                lmax = max(lmax, len);
               };
               if (segs && W.th_dtrans && draw_p(W.th_dtrans, W.p_dtrans)) {   // one-shot :331
                 preserve(SEG_TTRANS, 2);
@@ -1043,6 +1147,7 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
                 const int line = (int)draw_below((uint32_t)len + 1u);
                 e2 = edit_word(E_INS, line, rand_code());
                 len++;
+                lmax = max(lmax, len);
               }
               if (pois) {                            // Poisson insertions :404-413
                 const int n = npois(2);
@@ -1052,6 +1157,7 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
                   const int line = (int)draw_below((uint32_t)len + 1u);
                   pput(SEG_PINS, i, edit_word(E_INS, line, rand_code()));
                   len++;
+                  lmax = max(lmax, len);
                   used++;
                 }
                 pcnt[SEG_PINS] = used;
@@ -1105,6 +1211,7 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
                     if (keep) seg[i] = edit_word(E_INS, seg[i], code);
                   }
                   len += n;
+                  lmax = max(lmax, len);
                   pcnt[SEG_SINS] = n;
                 }
               }
@@ -1126,33 +1233,28 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
                 for (int i = 0; i < n; i++) pput(SEG_SUNI, i, uniform_edit());
                 pcnt[SEG_SUNI] = n;
               }
+              // a segment that did not fit the arena (its edits were not all
+              // written): the offspring cannot be rebuilt, so it is dropped
+              // (counted in CNT_SUB_OVERFLOW and CNT_DROPPED; tests require 0)
+              bool truncated = false;
               if (segs && mode == AVGPU_MODE_WORLD)
 #pragma unroll
                 for (int k = 0; k < NSEG; k++)
-                  if ((int64_t)pofs[k] + pcnt[k] > W.scap) {
+                  if (pcnt[k] > 0 && ((int64_t)pofs[k] < 0 || (int64_t)pofs[k] + pcnt[k] > W.scap)) {
                     count_add(W, CNT_SUB_OVERFLOW, (unsigned long long)pcnt[k]);
-                    pcnt[k] = 0;
+                    truncated = true;
                   }
-              // Parent Substitution Mutations (per site) (cpu/cHardwareBase.cc:508-520)
-              // on the parent's sites [0, div) in this lane's LDS tape, code
-              // bits only (the flags are cleared below)
-              if (!DEF && W.th_par_site) {
-                const uint64_t t_par = W.th_par_site;
-                const double q_par = W.p_par_site;
-                int npar = 0;
-                for (int i = 0; i < div; i++) npar += draw_p(t_par, q_par) ? 1 : 0;
-                uint8_t* TLw = reinterpret_cast<uint8_t*>(TL32);
-                for (int i = 0; i < npar; i++) {
-                  const int site = (int)draw_below((uint32_t)div);
-                  TLw[site] = (uint8_t)((TLw[site] & ~CODE_MASK) | rand_code());
-                }
-              }
+              // (the parent's own mutations -- Divide_DoMutations' last draws,
+              // cpu/cHardwareBase.cc:508-565 -- follow the child's copy-out below:
+              // insertions shift the sites the child still occupies)
               // record (WORLD): the cell's primary record for the slice's
               // first offspring, an overflow record (atomic) for any further
               // one; an offspring a slip grew past the largest genome is dropped
-              if (mode == AVGPU_MODE_WORLD && len > AVGPU_MAX_GENOME) {
+              if (mode == AVGPU_MODE_WORLD && (len > AVGPU_MAX_GENOME || lmax > 4095)) {
                 ndrop++;
                 noversize++;
+              } else if (mode == AVGPU_MODE_WORLD && truncated) {
+                ndrop++;
               } else if (mode == AVGPU_MODE_WORLD) {
               rec = cell;
               if (prim) {
@@ -1161,10 +1263,10 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
               }
               prim = true;
               }
-              if (serial && rec >= 0) { sbirth = 1; stop = true; }   // births end the step
+              if (serial && rec >= 0) sbirth = 1;      // placed by the caller before any speculation
               if (rec >= 0) {
                 uint32_t clo, chi;
-                derive_key(klo, khi, (uint32_t)nd, 0x1B873593U, clo, chi);
+                derive_key(olo, ohi, (uint32_t)nd, 0x1B873593U, clo, chi);
                 // the record arrays, loaded together (see OPQ above)
                 int32_t* b_parent = W.b_parent;
                 uint32_t* b_seq = W.b_seq;
@@ -1263,8 +1365,74 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
               st_async_u32(g + 4 * w, v & 0x3F3F3F3Fu & byte_mask(w << 2, 0, child));
             }
           }
+          // Parent Substitution / Insert / Deletion Mutations (per site)
+          // (cpu/cHardwareBase.cc:508-565) on the parent's memory, already cut
+          // to the divide point, in lane L's LDS tape: the last draws of
+          // Divide_DoMutations, so drawing them after the child's copy-out
+          // keeps the reference's order.  Insertions: all sites drawn
+          // (GetUInt(size + 1)), sorted, inserted from the highest down with
+          // a GetRandomInst each, capped at the largest genome; deletions capped
+          // at the smallest; new sites have flags 0 (cleared below anyway).  A
+          // parent that would outgrow this size class's slot keeps the
+          // insertions that fit (counted in CNT_MEM_CAP; the oracle has no
+          // slot, tests require 0).
+          if (!DEF && mode != AVGPU_MODE_TEST && lane == L && (W.th_par_site || W.th_par_ins || W.th_par_del)) {
+            int g_max = W.max_genome, g_min = W.min_genome;
+            if (W.th_par_site) {
+              int npar = 0;
+              for (int i = 0; i < M; i++) npar += draw_p(W.th_par_site, W.p_par_site) ? 1 : 0;
+              for (int i = 0; i < npar; i++) {
+                const int site = (int)draw_below((uint32_t)M);
+                T[site] = (uint8_t)((T[site] & ~CODE_MASK) | rand_code());
+              }
+            }
+            if (W.th_par_ins) {
+              int nins = 0;
+              for (int i = 0; i < M; i++) nins += draw_p(W.th_par_ins, W.p_par_ins) ? 1 : 0;
+              if (nins + M > g_max) nins = g_max - M;
+              if (nins > 0) {
+                // the sites, sorted, in the last 4 * nins bytes of the slot
+                // (the child's copy-out has read them; the growing parent
+                // stays below them: room)
+                int32_t* srt = reinterpret_cast<int32_t*>(T + S - 4 * nins);
+                const bool room = (int64_t)M + 5 * (int64_t)nins <= (int64_t)S;
+                for (int i = 0; i < nins; i++) {
+                  const int site = (int)draw_below((uint32_t)M + 1u);
+                  if (room) {
+                    int j = i;
+                    while (j > 0 && srt[j - 1] > site) { srt[j] = srt[j - 1]; j--; }
+                    srt[j] = site;
+                  }
+                }
+                int ncap = room ? 0 : nins;
+                if (room) {
+                  for (int i = nins - 1; i >= 0; i--) {
+                    const int pos = srt[i];
+                    const int code = rand_code();
+                    for (int k = M; k > pos; k--) T[k] = T[k - 1];
+                    T[pos] = (uint8_t)code;
+                    M++;
+                  }
+                } else {
+                  for (int i = 0; i < nins; i++) (void)rand_code();
+                }
+                if (ncap) count_add(W, CNT_MEM_CAP, (unsigned long long)ncap);
+              }
+            }
+            if (W.th_par_del) {
+              int ndel = 0;
+              for (int i = 0; i < M; i++) ndel += draw_p(W.th_par_del, W.p_par_del) ? 1 : 0;
+              if (M - ndel < g_min) ndel = M - g_min;
+              for (int i = 0; i < ndel; i++) {
+                const int site = (int)draw_below((uint32_t)M);
+                for (int k = site; k < M - 1; k++) T[k] = T[k + 1];
+                M--;
+              }
+            }
+          }
           // parent ClearFlags over its remaining sites, empty stacks
-          for (int w = lane; (w << 2) < div; w += 64) TL32[w] &= 0x3F3F3F3Fu;
+          const int pmem = __shfl(M, L);
+          for (int w = lane; (w << 2) < pmem; w += 64) TL32[w] &= 0x3F3F3F3Fu;
           if (VSTK) {
             if (lane == L) {
 #pragma unroll
@@ -1279,7 +1447,10 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
 
     if (sstep && !stop) {
       if (adv) ip = head_adjust(ip + 1, M);                   // ip.Advance() :1013
-      if (mx > 0 && tu >= mx) alive = false;                  // death :1045-1049
+      if (mx > 0 && tu >= mx) {                               // death :1045-1049
+        if (serial == 2) { sdie = 1; stop = true; executed--; }
+        else alive = false;
+      }
     }
     pop = -1;
     CK(4);
@@ -1321,9 +1492,10 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
     // a death frees the cell for this update's placement (k_allot_total
     // marked the living cells occupied)
     if (mode == AVGPU_MODE_WORLD && alive0 && !alive) W.occ[cell] = 0;
-    W.ctl[cell] = ctl & ~CTL_FRESH;
+    W.ctl[cell] = (ctl & ~CTL_FRESH) | (sdie ? CTL_SPECDIE : 0u);
     W.mem_size[cell] = M;
-    W.rng[2 * N + cell] = kct;
+    if (serial) W.sctx[2] = kct;                             // the context stream moved on
+    else W.rng[2 * N + cell] = kct;
     W.budget[cell] = spill ? (budget | (prim ? BUDGET_PRIM : 0)) : 0;
     // merit, fitness, gestation time, copied / executed sizes and last-task
     // counts were stored at the divide (st_async)
@@ -1365,7 +1537,7 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
       *reinterpret_cast<uint4*>(W.tape + (int64_t)c * TAPE_SLOT + q * 16) = v;
     }
   }
-  if (serial) return executed | (divides << 16) | (sbirth << 24);
+  if (serial) return executed | (divides << 16) | (sbirth << 24) | (sdie << 25);
   // ---- primary birth records -> birth queue (wavefront ballot + prefix) ----
   {
     const bool fresh = prim && !prim0;
@@ -1530,7 +1702,37 @@ __device__ __forceinline__ void stree_set(double* tree, int64_t size, int64_t i,
   __threadfence_block();
 }
 
-template <int S>
+// The reference's connection list of a cell (oracle conn_base;
+// tools/cTopology.h:40-55: Push() prepends, so the list runs W, SW, S, SE, E,
+// NE, N, NW; build_grid drops the wrapped entries, keeping the order)
+__device__ __forceinline__ int conn_base(const DevWorld& W, int cell, int* out) {
+  constexpr int DX[8] = {-1, -1, 0, 1, 1, 1, 0, -1}, DY[8] = {0, 1, 1, 1, 0, -1, -1, -1};
+  const int X = W.world_x, Y = W.world_y;
+  const int x = cell % X, y = cell / X;
+  int n = 0;
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    const int nx = x + DX[k], ny = y + DY[k];
+    if (W.geometry == 1 && (nx < 0 || nx >= X || ny < 0 || ny >= Y)) continue;
+    out[n++] = ((ny + Y) % Y) * X + (nx + X) % X;
+  }
+  return n;
+}
+
+// the serial world's context stream: GetUInt(n) of its next draw (counter, or
+// the recorded srec_ctx); ct is its position
+__device__ __forceinline__ uint32_t sctx_below(const DevWorld& W, uint32_t& ct, uint32_t n, bool& over) {
+  if (W.srec_ctx) {
+    double u = 0.0;
+    if ((int64_t)ct < W.srec_ctx_n) u = W.srec_ctx[ct]; else over = true;
+    ct++;
+    const uint32_t v = (uint32_t)(u * (double)n);
+    return v < n ? v : n - 1u;
+  }
+  return rng_below(W.sctx[0], W.sctx[1], ct, n);
+}
+
+template <int S, bool REC>
 __global__ __launch_bounds__(64, 1) void k_serial_update(const DevWorld* __restrict__ Wp) {
   constexpr int TAB_WORDS = 128 + 64 + 16 + 64 + AVGPU_MAX_REACTIONS * RT_STRIDE + 64;
   __shared__ __attribute__((aligned(16))) uint32_t lds32[64 * tape_stride(S) / 4 + 2 * AVGPU_STACK_SIZE * 64 + TAB_WORDS];
@@ -1555,13 +1757,22 @@ __global__ __launch_bounds__(64, 1) void k_serial_update(const DevWorld* __restr
   const int64_t ud = (int64_t)W.ave_time_slice * na;   // cWorld::CalculateUpdateSize
   const uint32_t glo = W.grng[0], ghi = W.grng[1];
   uint32_t gct = W.grng[2];
-  unsigned long long picks = 0, deaths = 0, divides = 0, births = 0;
+  unsigned long long picks = 0, deaths = 0, divides = 0, births = 0, dropped = 0, over = 0;
   for (int64_t i = 0; i < ud; i++) {
     const double tot = tree[1];
     if (!(tot > 0.0)) break;
-    const double x = __dmul_rn(__dmul_rn((double)rng_next(glo, ghi, gct), 1.0 / 4294967296.0), tot);
-    const int64_t c = stree_find(tree, size, x);
-    if (!(W.ctl[c] & CTL_ALIVE)) continue;
+    // the scheduler's draw (its own stream: main/cPopulation.cc:7341-7346)
+    double u;
+    if (W.srec_sched) {
+      u = (int64_t)gct < W.srec_sched_n ? W.srec_sched[gct] : 0.0;
+      over += (int64_t)gct < W.srec_sched_n ? 0 : 1;
+      gct++;
+    } else {
+      u = __dmul_rn((double)rng_next(glo, ghi, gct), 1.0 / 4294967296.0);
+    }
+    const int64_t c = stree_find(tree, size, __dmul_rn(u, tot));
+    const uint32_t ctl = W.ctl[c];
+    if (!(ctl & CTL_ALIVE)) continue;
     picks++;
     const int sp = W.spec[c];
     if (sp > 0) {                                 // a speculatively executed step
@@ -1569,40 +1780,88 @@ __global__ __launch_bounds__(64, 1) void k_serial_update(const DevWorld* __restr
       __threadfence_block();
       continue;
     }
-    const int r = __shfl(interpret_chunk<S, false>(Wp, 1, AVGPU_MODE_WORLD, c, 1, 0, lds32, false, 0, 64, 1), 0);
+    if (ctl & CTL_SPECDIE) {                      // SingleProcess: m_spec_die -> Die (cpu/cHardwareCPU.cc:917-921)
+      if (lane == 0) W.ctl[c] = ctl & ~(CTL_ALIVE | CTL_SPECDIE);
+      __threadfence_block();
+      stree_set(tree, size, c, 0.0);
+      deaths++;
+      continue;
+    }
+    // the one non-speculative SingleProcess
+    const int r = __shfl(interpret_chunk<S, REC>(Wp, 1, AVGPU_MODE_WORLD, c, 1, 0, lds32, false, 0, 64, 1), 0);
     __builtin_amdgcn_s_waitcnt(0);              // the step's stores (some outside the compiler's view)
     __threadfence_block();
-    if (lane == 0) W.spec[c] = (r & 0xFFFF) - 1;
     divides += (r >> 16) & 0xFF;
-    const bool alive = (W.ctl[c] & CTL_ALIVE) != 0;
-    if (!alive) { stree_set(tree, size, c, 0.0); deaths++; }
+    bool replaced = false;
     if ((r >> 24) & 1) {
-      stree_set(tree, size, c, alive ? W.merit[c] : 0.0);   // AdjustSchedule(parent) :933
+      // ActivateOffspring inside the h-divide (main/cPopulation.cc:621-960)
       apply_edits_wave(W, c, child);
-      // PositionOffspring: an empty neighbour if PREFER_EMPTY finds one,
-      // else any neighbour (or the parent's cell)
-      int nb[8];
-      const int nn = neighbours(W, (int)c, nb);
-      int cand[9];
-      int nc = 0;
-      if (W.prefer_empty)
-        for (int k = 0; k < nn; k++) if (!(W.ctl[nb[k]] & CTL_ALIVE)) cand[nc++] = nb[k];
-      if (nc == 0 && W.birth_method != 3) {
-        for (int k = 0; k < nn; k++) cand[nc++] = nb[k];
-        if (W.allow_parent) cand[nc++] = (int)c;
+      int t = -1, face_t = 0;
+      int32_t in3[3] = {0, 0, 0};
+      if (lane == 0) {
+        // PositionOffspring on the rotated connection list (oracle serial_target)
+        int base[8], conn[8], found[9];
+        const int nb = conn_base(W, (int)c, base);
+        const int f = nb ? W.face[c] % nb : 0;
+        for (int k = 0; k < nb; k++) conn[k] = base[(f + k) % nb];
+        int nf = 0;
+        if (W.prefer_empty)
+          for (int k = 0; k < nb; k++)
+            if (!(W.ctl[conn[k]] & CTL_ALIVE)) { for (int q = nf; q > 0; q--) found[q] = found[q - 1]; found[0] = conn[k]; nf++; }
+        if (nf == 0 && W.birth_method == 0) {
+          if (W.allow_parent) found[nf++] = (int)c;
+          for (int k = 0; k < nb; k++) found[nf++] = conn[k];
+        }
+        uint32_t ct = W.sctx[2];
+        bool ov = false;
+        t = nf == 0 ? (int)c : found[sctx_below(W, ct, (uint32_t)nf, ov)];
+        if (t == (int)c && !W.allow_parent) t = -1;            // target_cells[i] = -1 (:706-712)
+        if (t >= 0) {
+          // ActivateOrganism -> SetupInputs random (main/cEnvironment.cc:1268-1271)
+          in3[0] = (15 << 24) + (int)sctx_below(W, ct, 1u << 24, ov);
+          in3[1] = (51 << 24) + (int)sctx_below(W, ct, 1u << 24, ov);
+          in3[2] = (85 << 24) + (int)sctx_below(W, ct, 1u << 24, ov);
+          if (t != (int)c) {                                    // Rotate(parent_cell) (:935-944)
+            int tb[8];
+            const int ntb = conn_base(W, t, tb);
+            for (int k = 0; k < ntb; k++) if (tb[k] == (int)c) face_t = k;
+          }
+        }
+        W.sctx[2] = ct;
+        over += ov ? 1 : 0;
       }
-      if (nc > 0) {
-        const int t = cand[rng_below(glo, ghi, gct, (uint32_t)nc)];
+      t = __shfl(t, 0);
+#pragma unroll
+      for (int k = 0; k < 3; k++) in3[k] = __shfl(in3[k], 0);
+      if (t < 0) {
+        dropped++;
+      } else {
+        const bool parent_alive = t != (int)c;
         const bool killed = (W.ctl[t] & CTL_ALIVE) != 0;
-        const Child b = child_of_record(W, c);
+        if (parent_alive) stree_set(tree, size, c, W.merit[c]);   // AdjustSchedule(parent) :933
+        Child b = child_of_record(W, c);
+        b.inputs = in3;                                          // from the context stream (lane 0's)
         setup_child<64>(W, t, b, reinterpret_cast<const uint32_t*>(W.b_genome + c * TAPE_SLOT), lane);
         __threadfence_block();
-        if (lane == 0) W.spec[t] = 0;
+        if (lane == 0) {
+          W.spec[t] = 0;                                         // InsertOrganism resets the credit
+          if (parent_alive) W.face[t] = (uint8_t)face_t;
+        }
+        __threadfence_block();
         stree_set(tree, size, t, b.merit);
         births++;
         deaths += killed ? 1 : 0;
+        replaced = !parent_alive;
       }
     }
+    if (replaced) continue;                       // the parent died in its own step: no speculation
+    if (!(W.ctl[c] & CTL_ALIVE)) { stree_set(tree, size, c, 0.0); deaths++; continue; }
+    // the speculative run (ProcessStepSpeculative, main/cPopulation.cc:5758-5766)
+    const int r2 = __shfl(interpret_chunk<S, REC>(Wp, 1, AVGPU_MODE_WORLD, c, 1, 0, lds32, false, 0, 64, 2), 0);
+    __builtin_amdgcn_s_waitcnt(0);
+    __threadfence_block();
+    if (lane == 0) W.spec[c] = r2 & 0xFFFF;
+    __threadfence_block();
   }
   if (lane == 0) {
     W.grng[2] = gct;
@@ -1610,6 +1869,8 @@ __global__ __launch_bounds__(64, 1) void k_serial_update(const DevWorld* __restr
     if (deaths) count_add(W, CNT_DEATHS, deaths);
     if (divides) count_add(W, CNT_DIVIDES, divides);
     if (births) count_add(W, CNT_BIRTHS, births);
+    if (dropped) count_add(W, CNT_DROPPED, dropped);
+    if (over) count_add(W, CNT_REC_OVER, over);
   }
 }
 
@@ -1644,8 +1905,10 @@ bool class_timing_all() {
 static bool def_knobs(const DevWorld& W) {
   return W.alloc_method != 2 && W.require_allocate == 1 && W.max_label_exe == 1 && W.cfg_min_genome == 0 &&
          W.cfg_max_genome == 0 && W.merit_default_bonus == 0.0 && W.inherit_merit == 1 &&
-         W.base_merit_method == 4 && W.th_div_uni == 0 && !W.seg_any && W.th_par_site == 0 && W.size_range == 2.0 && W.min_exe_lines == 0.5 &&
-         W.min_copied_lines == 0.5 && W.required_bonus == 0.0 && W.default_bonus == 1.0 && W.rand_total <= 256;
+         W.base_merit_method == 4 && W.th_div_uni == 0 && !W.seg_any && W.th_par_site == 0 && W.th_par_ins == 0 &&
+         W.th_par_del == 0 && W.size_range == 2.0 && W.min_exe_lines == 0.5 &&
+         W.min_copied_lines == 0.5 && W.required_bonus == 0.0 && W.default_bonus == 1.0 && W.rand_total <= 256 &&
+         !W.copy_ext;
 }
 
 template <bool REC>
@@ -1753,6 +2016,6 @@ void launch_interpret_classes(const DevWorld& W, const DevWorld* dW, int mode, h
 
 // one serial-world update (launch_world_post's statistics follow it)
 void launch_serial_update(const DevWorld& W, const DevWorld* dW, hipStream_t s) {
-  (void)W;
-  hipLaunchKernelGGL((k_serial_update<CLASS3_SIZE>), dim3(1), dim3(64), 0, s, dW);
+  if (W.srec_ctx) hipLaunchKernelGGL((k_serial_update<CLASS3_SIZE, true>), dim3(1), dim3(64), 0, s, dW);
+  else hipLaunchKernelGGL((k_serial_update<CLASS3_SIZE, false>), dim3(1), dim3(64), 0, s, dW);
 }

@@ -593,10 +593,11 @@ __device__ __forceinline__ void place_pick_one(const DevWorld& W, int64_t i, uns
     for (int k = 0; k < nn; k++) cand[nc++] = nbr[k];
     if (W.allow_parent) cand[nc++] = parent;
   }
-  if (nc == 0) { W.b_state[r] = -1; return; }
   const uint32_t lo = W.b_rng[r], hi = W.b_rng[W.rcap + r];
   uint32_t ctr = W.b_rng[2 * W.rcap + r];
-  const int t = cand[rng_below(lo, hi, ctr, (uint32_t)nc)];
+  // no candidate (BIRTH_METHOD 3 without an empty neighbour): PositionOffspring
+  // returns the parent's cell, drawing nothing (main/cPopulation.cc:5407)
+  const int t = nc > 0 ? cand[rng_below(lo, hi, ctr, (uint32_t)nc)] : parent;
   // priority: draw, then the parent's GLOBAL cell id, so that tiles agree
   const unsigned long long prio = ((unsigned long long)rng_next(lo, hi, ctr) << 32) |
                                   ((unsigned long long)((W.cell0 + parent) & 0xFFFFFF) << 8) |
@@ -773,9 +774,18 @@ __global__ __launch_bounds__(64) void k_apply_mutations(DevWorld W) {
 // in flight together instead of a chain behind it).
 // last: (single world) the claim array of the last placement round, zeroed
 // at each record's target for the next update
+//
+// Every queued offspring has a target by now: PositionOffspring always returns
+// a cell (main/cPopulation.cc:5382-5413).  A birth still pending after the
+// last placement round lost that round's claim on its target to a birth of
+// higher priority; the reference would have placed both, one after the other,
+// and the later one (here: the higher priority, the cell's owner) kills the
+// earlier newborn.  So a birth either owns its cell at the update's end
+// (CNT_BIRTHS) or was placed and overwritten (CNT_OVERWRITTEN) -- never
+// "not placed".
 __global__ __launch_bounds__(64) void k_activate(DevWorld W, unsigned long long* last) {
   const int nb = queue_len(W);
-  unsigned long long born = 0, lost = 0;
+  unsigned long long born = 0, over = 0;
   for (int64_t q = (int64_t)blockIdx.x * 64 + threadIdx.x; q < nb; q += (int64_t)gridDim.x * 64) {
     const int64_t i = rec_of(W, q);
     const int tgt = W.b_target[i];
@@ -784,17 +794,17 @@ __global__ __launch_bounds__(64) void k_activate(DevWorld W, unsigned long long*
     if (last && tgt >= 0) last[tgt] = 0ull;
     const bool won = st > 0 && tgt >= 0 && W.owner[tgt] == (int)i;
     if (won && tgt >= W.n) continue;          // sent to the neighbouring tile
-    if (!won) { lost++; continue; }
+    if (!won) { over++; continue; }
     born++;
     setup_child_lane(W, tgt, b, W.b_genome + i * TAPE_SLOT);
   }
   for (int off = 32; off > 0; off >>= 1) {
     born += __shfl_xor(born, off);
-    lost += __shfl_xor(lost, off);
+    over += __shfl_xor(over, off);
   }
   if (threadIdx.x == 0) {
     if (born) count_add(W, CNT_BIRTHS, born);
-    if (lost) count_add(W, CNT_DROPPED, lost);
+    if (over) count_add(W, CNT_OVERWRITTEN, over);
   }
 }
 
@@ -863,7 +873,7 @@ __global__ __launch_bounds__(64) void k_activate_remote(DevWorld W, int d) {
     const HaloRec r = recs[q];
     if (r.len < 0) continue;                  // lost at the sender (counted there)
     const int64_t c = edge_cell(W, d, r.col);
-    if (W.owner[c] != REMOTE_OWNER(r.round)) { lost++; continue; }
+    if (W.owner[c] != REMOTE_OWNER(r.round)) { lost++; continue; }   // overwritten by a later winner
     born++;
     Child b;
     b.len = r.len; b.gen = r.gen; b.ccopied = r.ccopied; b.exec = r.exec; b.gest = r.gest;
@@ -873,7 +883,7 @@ __global__ __launch_bounds__(64) void k_activate_remote(DevWorld W, int d) {
   }
   if (lane == 0) {
     if (born) count_add(W, CNT_BIRTHS, born);
-    if (lost) count_add(W, CNT_DROPPED, lost);
+    if (lost) count_add(W, CNT_OVERWRITTEN, lost);
   }
 }
 
@@ -1002,6 +1012,7 @@ __global__ __launch_bounds__(256) void k_stats_final(DevWorld W, const double* p
     out[31] = (double)W.counters[CNT_CUM_BIRTHS];
     out[32] = (double)cs[0][CNT_SLICES];
     out[33] = (double)cs[0][CNT_LANESTEPS];
+    out[34] = (double)cs[0][CNT_OVERWRITTEN];
   }
 }
 

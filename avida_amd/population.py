@@ -2,7 +2,8 @@
 over the C-ABI (main/cPopulation.cc:6723-7000, :6294-6500).
 
 LoadPopulation (.pop genotype lists and .spop structured saves):
-  * every organism already in the world is killed (cellid_offset 0, :6731);
+  * every organism already in the world is killed when cellid_offset is 0
+    (:6731-6732); with an offset the file's organisms join the population;
   * genotype rows are processed in DESCENDING id order (sTmpGenotype's
     operator< compares id_num with >, :6683; Apto::QSort, :6857);
   * a structured file places each organism at cells[i] + offset, otherwise
@@ -75,11 +76,14 @@ def load_population(world, iset: files.InstSet, path, ncells, cellid_offset=0):
             if not 0 <= cell < ncells:
                 raise ValueError(f"{path}: cell {cell} outside the world")
             placed[cell] = (genome, merit)      # a later row on the same cell wins
-    # KillOrganism for every organism not replaced (the world is cleared first)
-    occ = np.nonzero(world.census()["genotype_key"] != 0)[0]
-    for c in occ:
-        if int(c) not in placed:
-            world.kill(int(c))
+    # KillOrganism for every organism not replaced: the world is cleared first
+    # only when cellid_offset is 0 (main/cPopulation.cc:6731-6732); with an
+    # offset the loaded organisms are added to the existing population
+    if cellid_offset == 0:
+        occ = np.nonzero(world.census()["genotype_key"] != 0)[0]
+        for c in occ:
+            if int(c) not in placed:
+                world.kill(int(c))
     cells = sorted(placed)
     for first, count, k in _runs(cells):
         chunk = cells[k:k + count]

@@ -39,6 +39,11 @@ METRIC = "organism-instructions/sec + updates/sec, 1M-org logic-9 world, 1/8 GPU
 STATE_BYTES = 224.0
 SITE_BYTES = 1.25
 HBM_PEAK_GBS = 8000.0         # MI355X_MICROARCH.md chip table (spec)
+# updates run before the timed region (+ the warmup): the timed world is aged,
+# not the freshly seeded lock-step one (tests/test_parity_full.py checks parity
+# in exactly this regime)
+BURN_IN = 150
+WARMUP = 5
 PMC_FILE = os.path.join(ROOT, "profiles", "pmc_k_interpret336.json")
 
 
@@ -193,6 +198,10 @@ def cpu_baseline_multi(golden, seconds, env_kind, procs):
     return {"value": sum(o["value"] for o in outs), "unit": "organism-instructions/s", "cores": procs,
             "kind": "port", "single_core_value": single["value"],
             "host_cpus": os.cpu_count(),
+            # the box gives one GPU's job a share of 16 host CPUs (gpurun's
+            # worker-pool rule); the whole host, linearly extrapolated from the
+            # single-core rate (independent worlds share nothing; an upper bound)
+            "all_host_cpus_extrapolated": single["value"] * (os.cpu_count() or 1),
             "label": "restatement (reference unbuildable here: its libs/apto submodule is absent)",
             "sample": f"{procs} independent oracle serial worlds (one process per host core, like the "
                       f"reference's heads_perf_1000u_rate rate_runner; {procs} of the box's "
@@ -240,7 +249,7 @@ def main():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--side", type=int, default=1024)
-    ap.add_argument("--burn-in", type=int, default=150,
+    ap.add_argument("--burn-in", type=int, default=BURN_IN,
                     help="untimed updates that age the seeded population before the warmup "
                          "(its organisms start in lock step; ~10 gestations spread them out)")
     ap.add_argument("--seed", type=int, default=101)
@@ -342,9 +351,12 @@ def main():
     tot_insts, tot_births, tot_orgs = vec[1].item(), vec[2].item(), vec[3].item()
     d = [cnt1[k] - cnt0[k] for k in range(capi.NUM_COUNTERS)]
     nph = max(1, phases.value)
-    # births the update could not place (queue overflow, no target) and
-    # slices handed to a larger LDS class, summed over ranks
-    extra = torch.tensor([float(d[capi.CNT_DROPPED]), float(d[capi.CNT_SPILLS])],
+    # offspring never placed (birth-queue overflow, oversize, full halo arena:
+    # placement itself places every birth), offspring placed and then
+    # overwritten by a later birth into the same cell, and slices handed to a
+    # larger LDS class, summed over ranks
+    extra = torch.tensor([float(d[capi.CNT_DROPPED]), float(d[capi.CNT_SPILLS]),
+                          float(d[capi.CNT_OVERWRITTEN])],
                          dtype=torch.float64, device="cuda")
     if dist:
         dist.all_reduce(extra)
@@ -424,24 +436,31 @@ def main():
             "organisms": int(tot_orgs),
             "updates_per_sec": args.steps / dt_max,
             "births_per_update": tot_births / args.steps,
-            "births_dropped_per_update": extra[0].item() / args.steps,
+            "births_never_placed_per_update": extra[0].item() / args.steps,
+            "births_overwritten_per_update": extra[2].item() / args.steps,
             "spills_per_update": extra[1].item() / args.steps,
             "insts_per_update": tot_insts / args.steps,
             "parallelism": f"strips{world}",
             "ranks": world,
             "long_run": long_run,
         },
+        # The resource that binds k_interpret<336> is instruction issue plus
+        # exposed latency, so the headline roofline is the VALU-issue one
+        # (PMC wave-instructions per launch over the live event-timed launch);
+        # the HBM roofline of the same launch (algorithmic bytes of SURVEY.md
+        # 8(d) over the same duration, PMC traffic) follows as "hbm".
         "roofline": {
-            "bound": "hbm",
-            # the HBM roofline is the contract's form; the resource that binds
-            # k_interpret is instruction issue + exposed latency ("issue" below)
-            "binding": "instruction issue + latency (see issue)",
-            "achieved": achieved,
-            "peak": HBM_PEAK_GBS,
-            "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS,
+            "bound": "issue",
+            "binding": "VALU instruction issue + exposed LDS / memory latency",
+            "achieved": issue["achieved"] if issue else None,
+            "peak": issue["peak"] if issue else None,
+            "unit": "wave-instructions/s",
+            "frac": issue["frac"] if issue else None,
             "traffic": traffic,
             "traffic_source": traffic_src,
+            "hbm": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                    "traffic_over_algorithmic": (traffic / bytes_per_launch) if traffic else None},
             "kernel": "k_interpret<336> (LDS size class 0)",
             "kernel_ms": c0_ms,
             "timed_launches": int(phases.value),

@@ -164,6 +164,47 @@ typedef struct avgpu_cfg {
    * DIVIDE_POISSON_TRANS_MEAN, DIV_TRANS_PROB (cpu/cHardwareBase.cc:331-343,
    * doTransMutation :700-760) */
   double divide_trans_prob, divide_poisson_trans_mean, div_trans_prob;
+  /* copy mutations of Inst_HeadCopy beyond COPY_MUT/INS/DEL_PROB
+   * (cpu/cHardwareCPU.cc:7153-7161): COPY_UNIFORM_PROB (doUniformCopyMutation,
+   * cpu/cHardwareBase.cc:597-612) and COPY_SLIP_PROB under SLIP_COPY_MODE 0
+   * (the read head jumps to GetInt(memory size)); SLIP_COPY_MODE 1 (a slip of
+   * the whole memory at the write head) is refused */
+  double copy_uniform_prob, copy_slip_prob;
+  int32_t slip_copy_mode;          /* SLIP_COPY_MODE */
+  int32_t trans_fill_mode;         /* TRANS_FILL_MODE: 0 duplication, 1 scrambled */
+  /* PARENT_INS_PROB / PARENT_DEL_PROB: per-site insertions / deletions in the
+   * parent's memory after its substitutions (cpu/cHardwareBase.cc:523-565) */
+  double parent_ins_prob, parent_del_prob;
+  /* ---- knobs this path does not implement: avgpu_create refuses any of them
+   * set away from the reference default (main/cAvidaConfig.h) with
+   * AVGPU_EUNSUPPORTED, so a C++ caller cannot run them with other semantics.
+   * avgpu_cfg_defaults writes the defaults. ---- */
+  double point_mut_prob, point_ins_prob, point_del_prob;   /* POINT_{MUT,INS,DEL}_PROB (0) */
+  double inst_point_mut_prob;                              /* INST_POINT_MUT_PROB (0) */
+  double div_lgt_prob, divide_lgt_prob, divide_poisson_lgt_mean;  /* lateral transfer (0) */
+  double inject_mut_prob, inject_ins_prob, inject_del_prob;       /* INJECT_*_PROB (0) */
+  double meta_copy_mut, meta_std_dev;                      /* META_COPY_MUT, META_STD_DEV (0) */
+  double death_prob;                                       /* DEATH_PROB (0) */
+  int32_t age_deviation;           /* AGE_DEVIATION (0) */
+  int32_t divide_failure_resets;   /* DIVIDE_FAILURE_RESETS (0) */
+  int32_t special_mut_line;        /* SPECIAL_MUT_LINE (-1) */
+  int32_t population_cap;          /* POPULATION_CAP (0) */
+  int32_t generation_inc_method;   /* GENERATION_INC_METHOD (1) */
+  int32_t reset_inputs_on_divide;  /* RESET_INPUTS_ON_DIVIDE (0) */
+  int32_t epigenetic_method;       /* EPIGENETIC_METHOD (0) */
+  int32_t min_cycles;              /* MIN_CYCLES (0) */
+  int32_t required_task, immunity_task;           /* REQUIRED_TASK, IMMUNITY_TASK (-1) */
+  int32_t required_reaction, immunity_reaction;   /* REQUIRED_REACTION, IMMUNITY_REACTION (-1) */
+  int32_t require_single_reaction; /* REQUIRE_SINGLE_REACTION (0) */
+  int32_t max_unique_task_count;   /* MAX_UNIQUE_TASK_COUNT (-1) */
+  int32_t require_exact_copy;      /* REQUIRE_EXACT_COPY (0) */
+  int32_t fitness_method;          /* FITNESS_METHOD (0) */
+  int32_t juv_period;              /* JUV_PERIOD (0) */
+  int32_t no_mut_insts_len;        /* strlen(NO_MUT_INSTS) (0) */
+  /* non-zero when any REVERT_* / STERILIZE_* probability or STERILIZE_UNSTABLE
+   * is set (Divide_TestFitnessMeasures1, cpu/cHardwareBase.cc:978-1085) */
+  int32_t test_fitness_measures;
+  int32_t pad_cfg2;
 } avgpu_cfg;
 
 /* One REACTION line of environment.cfg (main/cEnvironment.cc:1185-1211,
@@ -272,7 +313,7 @@ typedef struct avgpu_update_stats {
   int64_t num_organisms;
   int64_t insts_executed;      /* organism-instructions this update */
   int64_t births;              /* offspring placed this update */
-  int64_t births_dropped;      /* birth-queue overflow or placement failure */
+  int64_t births_dropped;      /* never placed: birth-queue overflow, oversize, halo arena full */
   int64_t deaths;              /* old-age deaths this update */
   int64_t divides;             /* successful divides this update */
   int64_t task_orgs[AVGPU_MAX_REACTIONS]; /* organisms whose last gestation did task t */
@@ -287,6 +328,8 @@ typedef struct avgpu_update_stats {
   int64_t cum_births;
   int64_t slices;              /* organism time slices interpreted this update */
   int64_t lane_steps;          /* 64 x longest lane per wave (SIMD lane-issue slots used) */
+  int64_t births_overwritten;  /* placed, then killed by a later birth into the same cell this update
+                                  (every successful divide is births + births_overwritten + births_dropped) */
 } avgpu_update_stats;
 
 typedef struct avgpu_world avgpu_world;   /* opaque handle */
@@ -298,6 +341,11 @@ void avgpu_cfg_defaults(avgpu_cfg* cfg);
  * main/cPopulation.cc:323-404): allocates SoA state for num_cells organisms
  * (world_x*world_y when num_cells <= 0) on HIP device `device`. */
 avgpu_world* avgpu_create(const avgpu_cfg* cfg, int device, int64_t num_cells);
+/* The configuration check avgpu_create runs first (no device needed): 0 when
+ * every knob is on this path, AVGPU_EUNSUPPORTED naming the first knob that is
+ * not (the refused block of avgpu_cfg, values outside the implemented ranges)
+ * -- cAvidaConfig's knobs, main/cAvidaConfig.h:283-559. */
+int avgpu_check_cfg(const avgpu_cfg* cfg);
 int avgpu_destroy(avgpu_world* w);
 int avgpu_sync(avgpu_world* w);
 
@@ -363,16 +411,29 @@ int avgpu_run_updates(avgpu_world* w, int n_updates, avgpu_update_stats* last);
  * of one organism per step, main/cPopulation.cc:5698-5788, a cWeightedIndex
  * sum tree, tools/cWeightedIndex.cc:49-115; ProcessStepSpeculative's
  * run-ahead of up to 32 instructions, stopping before IO / h-divide,
- * :5740-5788; every offspring placed at once, ActivateOffspring /
- * PositionOffspring :621-952, :5185-5414).  The picks and placements draw
- * from one scheduler stream keyed by the world seed;
- * organisms keep their own streams.  One wave steps the world, so this mode
- * is for reference-semantics runs of small worlds (statistical parity,
- * replay), not throughput.  Counter streams only (AVGPU_EUNSUPPORTED under
- * RECORDED streams) and single worlds (not strip tiles).  Statistics as
+ * :5740-5788; every offspring placed at once inside its h-divide,
+ * ActivateOffspring / PositionOffspring :621-952, :5185-5414, on the
+ * reference's rotated connection lists, tools/cTopology.h:40-55,
+ * main/cPopulationCell.cc:122-141).  The picks draw from the scheduler's
+ * stream, everything else from the world's context stream
+ * (avgpu_set_serial_streams).  One wave steps the world, so this mode is for
+ * reference-semantics runs of small worlds (statistical parity, replay), not
+ * throughput.  Not with per-organism RECORDED streams (AVGPU_EUNSUPPORTED) or
+ * strip tiles.  Statistics as
  * avgpu_run_update: insts_executed counts the update's picks of living
  * organisms, as cStats does. */
 int avgpu_run_serial_updates(avgpu_world* w, int n_updates, avgpu_update_stats* last);
+/* The serial world's two random streams, as the reference has them: the
+ * scheduler's own generator (Apto::Scheduler::Probabilistic over an AvidaRNG
+ * seeded from the world's, main/cPopulation.cc:7341-7346), drawn once per pick
+ * (x = u * total merit), and the world's context stream (ctx.GetRandom()),
+ * drawn by every organism instruction, PositionOffspring and the newborns'
+ * SetupInputs in execution order.  sched / ctx: recorded doubles (k-th draw =
+ * element k), or NULL for the counter stream keyed by the seed.  Both
+ * positions restart at 0.  Draws past the end of an array return 0 and count
+ * in AVGPU_CNT_REC_EXHAUSTED. */
+int avgpu_set_serial_streams(avgpu_world* w, const double* sched, int64_t n_sched, const double* ctx,
+                             int64_t n_ctx);
 /* The same update split around an external all-reduce (multi-GPU tiles,
  * cMultiProcessWorld::CalculateUpdateSize main/cMultiProcessWorld.cc:375-405):
  * avgpu_update_totals writes the tile's {sum merit, organisms} into the
@@ -568,7 +629,8 @@ enum avgpu_counter {
   AVGPU_CNT_DEATHS = 1,
   AVGPU_CNT_DIVIDES = 2,
   AVGPU_CNT_BIRTHS = 3,
-  AVGPU_CNT_DROPPED = 4,    /* offspring not placed */
+  AVGPU_CNT_DROPPED = 4,    /* offspring never placed: birth-queue overflow, a slip past
+                               AVGPU_MAX_GENOME, a full halo arena (placement itself places every birth) */
   AVGPU_CNT_SPILLS = 5,     /* slices handed to a larger LDS size class */
   AVGPU_CNT_SLICES = 6,     /* organisms with a non-zero allotment */
   AVGPU_CNT_LANESTEPS = 7,  /* 64 x longest lane per wave (lane efficiency = INSTS / this) */
@@ -580,6 +642,10 @@ enum avgpu_counter {
   AVGPU_CNT_REC_EXHAUSTED = 20, /* RECORDED draws past the end of the stream */
   AVGPU_CNT_OVERSIZE = 21,  /* offspring longer than AVGPU_MAX_GENOME after a slip (dropped) */
   AVGPU_CNT_SUB_OVERFLOW = 22, /* DIV_MUT_PROB substitutions not kept: the per-update arena was full (must be 0) */
+  AVGPU_CNT_OVERWRITTEN = 24, /* offspring placed, then replaced by a later birth into the same cell in
+                                 the same update (the reference kills such a newborn too) */
+  AVGPU_CNT_MEM_CAP = 23,   /* copy-time insertions skipped at AVGPU_MAX_GENOME memory sites (the
+                               reference has no cap) and removals from a one-site memory */
   AVGPU_NUM_COUNTERS = 48   /* 32..47: AVGPU_PHASE_CLOCKS diagnostic builds */
 };
 int avgpu_counters(avgpu_world* w, int cumulative, int64_t* out, int n);

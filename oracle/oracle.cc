@@ -212,6 +212,7 @@ struct Org {
   int cur_task[AVGPU_MAX_REACTIONS], last_task[AVGPU_MAX_REACTIONS];
   int cur_react[AVGPU_MAX_REACTIONS];
   bool to_die = false;
+  bool spec_die = false;   // serial world: died in a speculative step (m_spec_die), removed when next picked
   // batch-world bookkeeping
   Stream rng;
   double credit = 0.0;
@@ -242,10 +243,11 @@ struct World {
   std::vector<Reaction> react;
   int num_tasks_in_env = 0;
   std::vector<Org> orgs;
-  Prob p_copy_mut, p_copy_ins, p_copy_del;
+  Prob p_copy_mut, p_copy_ins, p_copy_del, p_copy_uni, p_copy_slip;
   Prob p_div_mut, p_div_ins, p_div_del, p_div_slip, p_div_uni;
   Prob p_div_site;           // DIV_MUT_PROB (per-site substitutions on divide)
   Prob p_par_site;           // PARENT_MUT_PROB (per-site substitutions in the parent)
+  Prob p_par_ins, p_par_del; // PARENT_INS_PROB, PARENT_DEL_PROB
   Prob p_dsite[5];           // DIV_INS_PROB, DIV_DEL_PROB, DIV_UNIFORM_PROB, DIV_SLIP_PROB, DIV_TRANS_PROB (per site)
   Prob p_div_trans;          // DIVIDE_TRANS_PROB
   double pois_L[5] = {0, 0, 0, 0, 0};   // + DIVIDE_POISSON_TRANS_MEAN   // exp(-DIVIDE_POISSON_{SLIP,MUT,INS,DEL}_MEAN); 0 = off
@@ -260,7 +262,10 @@ struct World {
   bool have_global = false;
   double global_merit = 0.0;
   int64_t global_orgs = 0;
-  Stream global_rng;   // serial world scheduler stream
+  Stream global_rng;   // serial world: the scheduler's own stream (main/cPopulation.cc:7341-7346)
+  Stream ctx_rng;      // serial world: the context stream every ctx.GetRandom() draw comes from
+  std::vector<double> srec_sched, srec_ctx;   // their recorded values (avgpu_set_serial_streams)
+  std::vector<uint8_t> face;   // serial world: each cell's connection-list rotation (cPopulationCell::Rotate)
   // strip tiles (avgpu_set_tile): rows [row0, row0+rows) of a world_x x
   // global_rows world; occ / claim / owner carry two ghost rows after n
   int64_t row0 = 0, rows = 0, global_rows = 0, cell0 = 0;
@@ -278,6 +283,8 @@ struct World {
   std::vector<int8_t> bstate;     // 0 pending, 1+k placed in round k, -1 failed
   int64_t t_insts = 0, t_deaths = 0, t_divides = 0, t_slices = 0, t_born = 0, t_dropped = 0;
   int64_t t_oversize = 0;   // offspring longer than AVGPU_MAX_GENOME after a slip (dropped at the divide)
+  int64_t t_memcap = 0;     // copy insertions past AVGPU_MAX_GENOME sites / removals from one site (skipped)
+  int64_t t_overwritten = 0;   // offspring placed, then killed by a later birth into the same cell
   // resources (avgpu_load_resources): literal restatement of cResourceCount /
   // cSpatialResCount, stepped once per update
   std::vector<avgpu_resource> res;
@@ -324,6 +331,10 @@ struct Exec {
   int mode;
   bool stop = false;   // TEST mode: gestation finished
   int64_t cur_cell = -1;  // the organism's cell (spatial resources)
+  // where the organism's ctx.GetRandom() draws come from: its own stream, or
+  // (serial world) the world's single context stream
+  Stream* ctx = nullptr;
+  Stream& rng() { return ctx ? *ctx : o.rng; }
 
   int size() const { return (int)o.mem.size(); }
   // cHeadCPU::GetNextInst (cpu/cHeadCPU.h:167-170)
@@ -408,7 +419,7 @@ struct Exec {
     o.mem.resize(new_size, 0);   // ALLOC_METHOD 0: new sites are op 0 (Allocate_Default :1698-1705)
     o.flg.resize(new_size, 0);
     if (w.cfg.alloc_method == 2) {  // ALLOC_METHOD_RANDOM (Allocate_Random :1688-1696)
-      for (int i = old_size; i < new_size; i++) o.mem[i] = (uint8_t)w.is.random_inst(o.rng);
+      for (int i = old_size; i < new_size; i++) o.mem[i] = (uint8_t)w.is.random_inst(rng());
     }
     o.mal_active = true;
     return true;
@@ -470,6 +481,7 @@ struct Exec {
     const int to = (from == 0) ? (int)r.uint_below((uint32_t)size) : (int)r.uint_below((uint32_t)size + 1);
     int ins = from - to;
     g.resize(size + ins);
+    lmax = std::max(lmax, (int)g.size());
     for (int i = 0; i < ins; i++) g[from + i] = w.cfg.slip_fill_mode == 4 ? (uint8_t)H_NOP_C : copy[to + i];
     if (ins < 0) ins = 0;
     for (int i = ins; i < size - to; i++) g[from + i] = copy[to + i];
@@ -485,6 +497,7 @@ struct Exec {
     const int to = (from == 0) ? (int)r.uint_below((uint32_t)size) : (int)r.uint_below((uint32_t)size + 1);
     const int ins = from - to;
     g.resize(size + ins);
+    lmax = std::max(lmax, (int)g.size());
     const int ins_loc = (int)r.uint_below((uint32_t)size + 1);
     if (ins > 0) {
       for (int i = 0; i < ins; i++) g[ins_loc + i] = copy[to + i];
@@ -501,8 +514,10 @@ struct Exec {
   // non-zero (avida_amd/capi.py UNSUPPORTED_NONZERO) and draw nothing at zero,
   // TestDivideMut / Ins / Del always draw (:121-123; the size limits are
   // tested after the draw), TestDivideUniform draws only when non-zero (:124-127).
+  int lmax = 0;   // the longest the offspring got during its divide mutations
   void divide_mutations(std::vector<uint8_t>& child) {
-    Stream& r = o.rng;
+    Stream& r = rng();
+    lmax = (int)child.size();
     int max_g = w.cfg.max_genome_size; if (!max_g || max_g > AVGPU_MAX_GENOME) max_g = AVGPU_MAX_GENOME;
     int min_g = w.cfg.min_genome_size; if (!min_g || min_g < AVGPU_MIN_GENOME) min_g = AVGPU_MIN_GENOME;
     // NumDividePoisson* draws only at a non-zero mean (main/cMutationRates.h:137-144)
@@ -518,6 +533,7 @@ struct Exec {
       } else if ((int)child.size() != max_g) {
         const uint32_t site = r.uint_below((uint32_t)child.size() + 1);
         child.insert(child.begin() + site, (uint8_t)(mut - n_ops - 1));
+        lmax = std::max(lmax, (int)child.size());
       }
     };
     // GetRandBinomial(size, p) restated as one P(p) per site (see DIV_MUT_PROB below)
@@ -551,11 +567,13 @@ struct Exec {
     if (r.p(w.p_div_ins) && (int)child.size() < max_g) {
       uint32_t line = r.uint_below((uint32_t)child.size() + 1);
       child.insert(child.begin() + line, (uint8_t)w.is.random_inst(r));
+      lmax = std::max(lmax, (int)child.size());
     }
     for (uint32_t i = 0, n = npois(2); i < n; i++) {                         // :404-413
       if ((int)child.size() >= max_g) break;
       uint32_t line = r.uint_below((uint32_t)child.size() + 1);
       child.insert(child.begin() + line, (uint8_t)w.is.random_inst(r));
+      lmax = std::max(lmax, (int)child.size());
     }
     if (r.p(w.p_div_del) && (int)child.size() > min_g) {
       uint32_t line = r.uint_below((uint32_t)child.size());
@@ -592,6 +610,7 @@ struct Exec {
         for (int i = 0; i < n; i++) sites[i] = (int)r.uint_below((uint32_t)child.size() + 1);
         std::sort(sites.begin(), sites.end());
         for (int i = n - 1; i >= 0; i--) child.insert(child.begin() + sites[i], (uint8_t)w.is.random_inst(r));
+        lmax = std::max(lmax, (int)child.size());
       }
     }
     // Delete Mutations (per site) (:473-488)
@@ -615,6 +634,32 @@ struct Exec {
       for (int i = 0; i < num_mut; i++) {
         const uint32_t site = r.uint_below((uint32_t)size);
         o.mem[site] = (uint8_t)w.is.random_inst(r);
+      }
+    }
+    // Parent Insert Mutations (per site) (:523-547): the count capped at the
+    // largest genome, every site drawn (GetUInt(size + 1)), sorted (Apto::QSort),
+    // inserted from the highest down, one GetRandomInst each; new sites flags 0
+    if (w.p_par_ins.p > 0.0) {
+      int n = binom(w.p_par_ins, (int)o.mem.size());
+      if (n + (int)o.mem.size() > max_g) n = max_g - (int)o.mem.size();
+      if (n > 0) {
+        std::vector<int> sites(n);
+        for (int i = 0; i < n; i++) sites[i] = (int)r.uint_below((uint32_t)o.mem.size() + 1);
+        std::sort(sites.begin(), sites.end());
+        for (int i = n - 1; i >= 0; i--) {
+          o.mem.insert(o.mem.begin() + sites[i], (uint8_t)w.is.random_inst(r));
+          o.flg.insert(o.flg.begin() + sites[i], 0);
+        }
+      }
+    }
+    // Parent Deletion Mutations (per site) (:550-565): capped at the smallest genome
+    if (w.p_par_del.p > 0.0) {
+      int n = binom(w.p_par_del, (int)o.mem.size());
+      if ((int)o.mem.size() - n < min_g) n = (int)o.mem.size() - min_g;
+      for (int i = 0; i < n; i++) {
+        const uint32_t site = r.uint_below((uint32_t)o.mem.size());
+        o.mem.erase(o.mem.begin() + site);
+        o.flg.erase(o.flg.begin() + site);
       }
     }
   }
@@ -684,8 +729,10 @@ struct Exec {
     // ActivateDivide: the on-divide DoOutput runs no reaction for logic-9
     // environments (every requisite has divide_only 0; TestRequisites :1408).
     divide_reset();
-    if (mode == AVGPU_MODE_WORLD && (int)child.size() > AVGPU_MAX_GENOME) {
-      w.t_oversize++;     // a slip outgrew the largest genome: the offspring is dropped
+    // a slip outgrew the largest genome (or passed 4095 sites on the way: the
+    // device's edit words hold 12-bit positions): the offspring is dropped
+    if (mode == AVGPU_MODE_WORLD && ((int)child.size() > AVGPU_MAX_GENOME || lmax > 4095)) {
+      w.t_oversize++;
     } else if (mode == AVGPU_MODE_WORLD) {
       Birth b;
       b.parent = cell;
@@ -825,21 +872,50 @@ struct Exec {
     // main/cMutationRates.cc:78-120)
     const bool muts = mode != AVGPU_MODE_TEST;
     // TestCopy*: no draw when the rate is 0 (main/cMutationRates.h:111-120)
-    if (muts && w.p_copy_mut.th && o.rng.p(w.p_copy_mut)) {
-      read_inst = w.is.random_inst(o.rng);
+    Stream& r = rng();
+    if (muts && w.p_copy_mut.th && r.p(w.p_copy_mut)) {
+      read_inst = w.is.random_inst(r);
       o.flg[wh] |= F_MUTATED | F_COPYMUT;
     }
     o.mem[wh] = (uint8_t)read_inst;
     o.flg[wh] |= F_COPIED;
-    if (muts && w.p_copy_ins.th && o.rng.p(w.p_copy_ins) && size() < AVGPU_MAX_GENOME) {
-      int ins = w.is.random_inst(o.rng);
-      o.mem.insert(o.mem.begin() + wh, (uint8_t)ins);
-      o.flg.insert(o.flg.begin() + wh, 0);
+    // cHeadCPU::InsertInst / RemoveInst at the write head (cpu/cHeadCPU.h:87-88
+    // -> cCPUMemory::Insert / Remove, cpu/cCPUMemory.cc:103-138: the new site
+    // has flags 0, later sites shift with their flags; no head moves).  The
+    // memory is capped at AVGPU_MAX_GENOME sites here (the reference has no
+    // cap): an insertion past it is skipped, its draws consumed, and counted
+    // (AVGPU_CNT_MEM_CAP); a removal from a one-site memory is skipped.
+    auto insert_at = [&](int pos, int op) {
+      if (size() >= AVGPU_MAX_GENOME) { w.t_memcap++; return; }
+      o.mem.insert(o.mem.begin() + pos, (uint8_t)op);
+      o.flg.insert(o.flg.begin() + pos, 0);
+    };
+    // After a deletion at the last site the write head sits one past the end:
+    // cCPUMemory::Remove(size) then drops the last site (its shift loop is
+    // empty, adjustCapacity shrinks) and SetInst writes outside the sequence
+    // (no visible effect).
+    auto remove_at = [&](int pos) {
+      if (size() <= 1) { w.t_memcap++; return; }
+      if (pos > size() - 1) pos = size() - 1;
+      o.mem.erase(o.mem.begin() + pos);
+      o.flg.erase(o.flg.begin() + pos);
+    };
+    // TestCopyIns, TestCopyDel, TestCopyUniform, TestCopySlip in that order
+    // (cpu/cHardwareCPU.cc:7153-7161), each drawing only at a non-zero rate
+    if (muts && w.p_copy_ins.th && r.p(w.p_copy_ins)) insert_at(wh, w.is.random_inst(r));
+    if (muts && w.p_copy_del.th && r.p(w.p_copy_del)) remove_at(wh);
+    if (muts && w.p_copy_uni.th && r.p(w.p_copy_uni)) {
+      // doUniformCopyMutation (cpu/cHardwareBase.cc:597-612; NO_MUT_INSTS empty):
+      // op codes, not weighted
+      const int n_ops = w.is.n;
+      const int mut = (int)r.uint_below((uint32_t)(2 * n_ops + 1));
+      if (mut < n_ops) { if (wh < size()) o.mem[wh] = (uint8_t)mut; }   // SetInst: flags kept
+      else if (mut == n_ops) remove_at(wh);
+      else insert_at(wh, mut - n_ops - 1);
     }
-    if (muts && w.p_copy_del.th && o.rng.p(w.p_copy_del) && size() > 1) {
-      o.mem.erase(o.mem.begin() + wh);
-      o.flg.erase(o.flg.begin() + wh);
-    }
+    // SLIP_COPY_MODE 0 (m_slip_read_head, cpu/cHardwareCPU.cc:785): the read
+    // head jumps to GetInt(memory size) (:7157-7158)
+    if (muts && w.p_copy_slip.th && r.p(w.p_copy_slip)) rh = adjust((int)r.uint_below((uint32_t)size()), size());
     rh = adjust(rh + 1, size());
     wh = adjust(wh + 1, size());
   }
@@ -1071,7 +1147,9 @@ int neighbours(const World& w, int64_t cell, int64_t* out) {
 
 // cPopulation::ActivateOrganism for a child (main/cPopulation.cc:1320-1340)
 // + cPhenotype::SetupOffspring (main/cPhenotype.cc:349-420)
-void activate_child(World& w, Birth& b, int64_t cell) {
+// ctx: the serial world's context stream (the three input draws of
+// SetupInputs come from it); nullptr: the offspring's own stream
+void activate_child(World& w, Birth& b, int64_t cell, Stream* ctx = nullptr) {
   Org& o = w.orgs[cell];
   setup_inject(w, o, b.genome.data(), (int)b.genome.size(), b.merit);
   o.merit = b.merit;
@@ -1083,9 +1161,10 @@ void activate_child(World& w, Birth& b, int64_t cell) {
   for (int t = 0; t < AVGPU_NUM_LOGIC_TASKS; t++) o.last_task[t] = b.last_task[t];
   o.rng = b.rng;
   // cEnvironment::SetupInputs random (main/cEnvironment.cc:1268-1271)
-  o.inputs[0] = (15 << 24) + (int)o.rng.uint_below(1u << 24);
-  o.inputs[1] = (51 << 24) + (int)o.rng.uint_below(1u << 24);
-  o.inputs[2] = (85 << 24) + (int)o.rng.uint_below(1u << 24);
+  Stream& r = ctx ? *ctx : o.rng;
+  o.inputs[0] = (15 << 24) + (int)r.uint_below(1u << 24);
+  o.inputs[1] = (51 << 24) + (int)r.uint_below(1u << 24);
+  o.inputs[2] = (85 << 24) + (int)r.uint_below(1u << 24);
 }
 
 }  // namespace
@@ -1105,6 +1184,8 @@ void* orc_create(const avgpu_cfg* cfg, int64_t ncells) {
   w->p_copy_mut = make_prob(cfg->copy_mut_prob);
   w->p_copy_ins = make_prob(cfg->copy_ins_prob);
   w->p_copy_del = make_prob(cfg->copy_del_prob);
+  w->p_copy_uni = make_prob(cfg->copy_uniform_prob);
+  w->p_copy_slip = make_prob(cfg->copy_slip_prob);
   w->p_div_mut = make_prob(cfg->divide_mut_prob);
   w->p_div_ins = make_prob(cfg->divide_ins_prob);
   w->p_div_del = make_prob(cfg->divide_del_prob);
@@ -1112,6 +1193,8 @@ void* orc_create(const avgpu_cfg* cfg, int64_t ncells) {
   w->p_div_uni = make_prob(cfg->divide_uniform_prob);
   w->p_div_site = make_prob(cfg->div_mut_prob);
   w->p_par_site = make_prob(cfg->parent_mut_prob);
+  w->p_par_ins = make_prob(cfg->parent_ins_prob);
+  w->p_par_del = make_prob(cfg->parent_del_prob);
   w->p_dsite[0] = make_prob(cfg->div_ins_prob);
   w->p_dsite[1] = make_prob(cfg->div_del_prob);
   w->p_dsite[2] = make_prob(cfg->div_uniform_prob);
@@ -1127,6 +1210,8 @@ void* orc_create(const avgpu_cfg* cfg, int64_t ncells) {
   memset(&w->stats, 0, sizeof(w->stats));
   derive_key((uint32_t)cfg->seed, (uint32_t)(cfg->seed >> 32), 0x5CEDu, 0xC0FFEEu,
              &w->global_rng.lo, &w->global_rng.hi);
+  derive_key((uint32_t)cfg->seed, (uint32_t)(cfg->seed >> 32), 0xC7C7u, 0x5EED5u,
+             &w->ctx_rng.lo, &w->ctx_rng.hi);
   return w;
 }
 
@@ -1741,6 +1826,8 @@ static void finish_stats(World& w, int64_t placed, int64_t dropped) {
   st.cum_insts_executed = w.cum_insts;
   st.cum_births = w.cum_births;
   st.slices = w.t_slices;
+  st.births_overwritten = w.t_overwritten;
+  w.t_overwritten = 0;
   w.update++;
 }
 
@@ -1758,8 +1845,9 @@ static void place_pick(World& w, int64_t i, const std::vector<uint8_t>& occ, std
     for (int k = 0; k < nn; k++) cand[nc++] = nb[k];
     if (w.cfg.allow_parent) cand[nc++] = b.parent;
   }
-  if (nc == 0) { state[i] = -1; return; }
-  b.target = cand[b.rng.uint_below((uint32_t)nc)];
+  // no candidate (BIRTH_METHOD 3 without an empty neighbour): PositionOffspring
+  // returns the parent's cell, drawing nothing (main/cPopulation.cc:5407)
+  b.target = nc > 0 ? cand[b.rng.uint_below((uint32_t)nc)] : b.parent;
   prio[i] = ((uint64_t)b.rng.next() << 32) | ((uint64_t)((w.cell0 + b.parent) & 0xFFFFFF) << 8) |
             (b.seq & 0xFF);
   if (prio[i] > claim[b.target]) claim[b.target] = prio[i];
@@ -1793,14 +1881,20 @@ static int run_update_impl(World& w) {
     }
     for (int64_t i = 0; i < nbirth; i++) if (w.births[i].target >= 0) claim[w.births[i].target] = 0;
   }
-  // 4. activation (the last round's winner owns the cell)
-  int64_t placed = 0, dropped = 0;
+  // 4. activation (the last round's winner owns the cell).  PositionOffspring
+  // always returns a cell (main/cPopulation.cc:5382-5413): a birth still
+  // pending after round 3 lost that round's claim on its target to a birth of
+  // higher priority, so the reference would have placed it there and the
+  // owner -- placed after it -- killed it.  Every birth is therefore placed:
+  // it owns its cell, or it was placed and overwritten.
+  int64_t placed = 0, overwritten = 0;
   for (int64_t i = 0; i < nbirth; i++) {
     Birth& b = w.births[i];
     if (state[i] == 1 && owner[b.target] == i) { activate_child(w, b, b.target); placed++; }
-    else dropped++;
+    else overwritten++;
   }
-  finish_stats(w, placed, dropped);
+  w.t_overwritten = overwritten;
+  finish_stats(w, placed, 0);
   return 0;
 }
 
@@ -2068,13 +2162,13 @@ int orc_tile_finish(void* h, avgpu_update_stats* out) {
   if (!tile_ok(w)) return fail(AVGPU_ESTATE, "not a strip tile with buffers");
   const int X = w.cfg.world_x;
   const int64_t nbirth = (int64_t)w.births.size();
-  int64_t placed = 0, dropped = w.t_dropped;
+  int64_t placed = 0, dropped = w.t_dropped, overwritten = 0;
   for (int64_t i = 0; i < nbirth; i++) {
     Birth& b = w.births[i];
     const bool won = w.bstate[i] > 0 && b.target >= 0 && w.owner[b.target] == i;
     if (won && b.target >= w.ncells) continue;   // shipped to the neighbour
     if (won) { activate_child(w, b, b.target); placed++; }
-    else dropped++;
+    else overwritten++;                          // placed, then overwritten (run_update_impl)
   }
   for (int d = 0; d < 2; d++) {
     const HaloHdr* hdr = reinterpret_cast<const HaloHdr*>(w.r_recv[d]);
@@ -2085,7 +2179,7 @@ int orc_tile_finish(void* h, avgpu_update_stats* out) {
       const HaloRec& r = recs[q];
       if (r.len < 0) continue;
       const int64_t c = edge_cell(w, d, r.col);
-      if (w.owner[c] != -2 - r.round) { dropped++; continue; }
+      if (w.owner[c] != -2 - r.round) { overwritten++; continue; }
       Birth b;
       b.parent = -1; b.seq = 0;
       b.genome.assign(arena + r.off, arena + r.off + r.len);
@@ -2097,6 +2191,7 @@ int orc_tile_finish(void* h, avgpu_update_stats* out) {
       placed++;
     }
   }
+  w.t_overwritten = overwritten;
   finish_stats(w, placed, dropped);
   if (out) *out = w.stats;
   return 0;
@@ -2131,28 +2226,107 @@ struct SerialSched {
   }
 };
 
-// returns 1 if the offspring was placed (2 if it replaced a living organism)
-static int serial_place(World& w, SerialSched& sch, Birth& b) {
-  int64_t nb[8];
-  const int nn = neighbours(w, b.parent, nb);
-  int64_t cand[9];
-  int nc = 0;
-  if (w.cfg.prefer_empty) for (int k = 0; k < nn; k++) if (!w.orgs[nb[k]].alive) cand[nc++] = nb[k];
-  if (nc == 0 && w.cfg.birth_method != 3) {
-    for (int k = 0; k < nn; k++) cand[nc++] = nb[k];
-    if (w.cfg.allow_parent) cand[nc++] = b.parent;
+// The reference's connection list of a cell (tools/cTopology.h:40-55
+// build_torus: eight Push()es, and tList::Push prepends, tools/tList.h:140-147,
+// so the list runs W, SW, S, SE, E, NE, N, NW -- (dx, dy) below; build_grid
+// :62-95 removes the wrapped entries, keeping the order), rotated by the cell's
+// facing (cPopulationCell::Rotate, main/cPopulationCell.cc:122-141: CircNext
+// until the given cell is first).
+static const int CONN_DX[8] = {-1, -1, 0, 1, 1, 1, 0, -1}, CONN_DY[8] = {0, 1, 1, 1, 0, -1, -1, -1};
+static int conn_base(const World& w, int64_t cell, int64_t* out) {
+  const int X = w.cfg.world_x, Y = w.cfg.world_y;
+  const int x = (int)(cell % X), y = (int)(cell / X);
+  int n = 0;
+  for (int k = 0; k < 8; k++) {
+    const int nx = x + CONN_DX[k], ny = y + CONN_DY[k];
+    if (w.cfg.world_geometry == 1 && (nx < 0 || nx >= X || ny < 0 || ny >= Y)) continue;
+    out[n++] = (int64_t)((ny + Y) % Y) * X + (nx + X) % X;
   }
-  if (nc == 0) return 0;
-  int64_t t = cand[w.global_rng.uint_below((uint32_t)nc)];
-  const int killed = w.orgs[t].alive ? 1 : 0;
-  activate_child(w, b, t);
-  w.orgs[t].spec_count = 0;
-  sch.set(t, w.orgs[t].merit);
-  return 1 + killed;
+  return n;
 }
 
+// PositionOffspring (main/cPopulation.cc:5353-5413) on the rotated list:
+// FindEmptyCell walks the list from its first cell and Push()es (prepends)
+// every empty one (:7361-7370), so the found list is the empty cells in
+// reverse list order; with none, BIRTH_METHOD 0 takes the whole list in order
+// (Append) with the parent pushed in front (ALLOW_PARENT); one GetUInt(size)
+// from the context stream picks.  No candidate: the parent's cell (no draw).
+static int64_t serial_target(World& w, int64_t parent) {
+  int64_t base[8], conn[8], found[9];
+  const int nb = conn_base(w, parent, base);
+  const int f = nb ? w.face[parent] % nb : 0;
+  for (int k = 0; k < nb; k++) conn[k] = base[(f + k) % nb];
+  int nf = 0;
+  if (w.cfg.prefer_empty)
+    for (int k = 0; k < nb; k++)
+      if (!w.orgs[conn[k]].alive) { for (int q = nf; q > 0; q--) found[q] = found[q - 1]; found[0] = conn[k]; nf++; }
+  if (nf == 0 && w.cfg.birth_method == 0) {
+    if (w.cfg.allow_parent) found[nf++] = parent;
+    for (int k = 0; k < nb; k++) found[nf++] = conn[k];
+  }
+  if (nf == 0) return parent;
+  return found[w.ctx_rng.uint_below((uint32_t)nf)];
+}
+
+// ActivateOffspring after the divide (main/cPopulation.cc:621-960): the
+// target cell, the kill of its occupant, ActivateOrganism with SetupInputs
+// from the context stream, the parent's and the child's scheduler weights,
+// and -- the parent still alive -- the child's cell rotated to face the
+// parent (:935-944).  Returns 0 dropped (BIRTH_METHOD 3, no empty cell, no
+// ALLOW_PARENT), 1 placed, 2 placed over a living organism, 3 over the parent.
+static int serial_place(World& w, SerialSched& sch, Birth& b) {
+  const int64_t t = serial_target(w, b.parent);
+  if (t == b.parent && !w.cfg.allow_parent) return 0;     // target_cells[i] = -1 (:706-712)
+  const bool parent_alive = t != b.parent;
+  if (parent_alive) sch.set(b.parent, w.orgs[b.parent].merit);   // AdjustSchedule(parent) :933
+  const int killed = w.orgs[t].alive ? 1 : 0;
+  activate_child(w, b, t, &w.ctx_rng);
+  w.orgs[t].spec_count = 0;                               // InsertOrganism (main/cPopulationCell.cc:270-271)
+  w.orgs[t].spec_die = false;
+  sch.set(t, w.orgs[t].merit);
+  if (parent_alive) {                                     // Rotate(parent_cell) :935-944
+    int64_t base[8];
+    const int nb = conn_base(w, t, base);
+    for (int k = 0; k < nb; k++) if (base[k] == b.parent) { w.face[t] = (uint8_t)k; break; }
+  }
+  return parent_alive ? 1 + killed : 3;
+}
+
+// avgpu_set_serial_streams restated: the scheduler's and the context's
+// recorded doubles (NULL / 0: counter streams)
+int orc_set_serial_streams(void* h, const double* sched, int64_t n_sched, const double* ctx, int64_t n_ctx) {
+  World& w = *(World*)h;
+  w.srec_sched.assign(sched ? sched : (const double*)nullptr, sched ? sched + n_sched : nullptr);
+  w.srec_ctx.assign(ctx ? ctx : (const double*)nullptr, ctx ? ctx + n_ctx : nullptr);
+  w.global_rng.rec = w.srec_sched.empty() ? nullptr : w.srec_sched.data();
+  w.global_rng.rec_len = (int64_t)w.srec_sched.size();
+  w.global_rng.ctr = 0;
+  w.ctx_rng.rec = w.srec_ctx.empty() ? nullptr : w.srec_ctx.data();
+  w.ctx_rng.rec_len = (int64_t)w.srec_ctx.size();
+  w.ctx_rng.ctr = 0;
+  return 0;
+}
+
+// The serial world: Avida2Driver::Run's update loop (targets/avida/
+// Avida2Driver.cc:91-163) with the reference's own schedule.
+//  * Two streams, as in the reference: the scheduler's own generator for the
+//    picks (Apto::Scheduler::Probabilistic over an AvidaRNG seeded from the
+//    world's, main/cPopulation.cc:7341-7346; restated as x = u * total merit
+//    and a cWeightedIndex-style sum-tree descent, tools/cWeightedIndex.cc:49-115)
+//    and ONE context stream for every other draw -- every organism's
+//    mutations, placement, the newborns' inputs -- in execution order.
+//  * ProcessStepSpeculative (main/cPopulation.cc:5740-5788): a cell with
+//    speculative credit spends one; otherwise one SingleProcess, then while it
+//    returns true up to 32 speculative ones, each rejected before a STALL
+//    instruction (IO, h-divide: cpu/cHardwareCPU.cc:961-968).  A speculative
+//    instruction that reaches the age limit sets m_spec_die (:1045-1049) and is
+//    not counted; the organism dies when next picked with no credit left
+//    (:917-921).  An organism replaced by its own offspring gets no speculation.
+//  * Offspring are placed inside the h-divide (ActivateOffspring), i.e.
+//    before the speculative run: rotated connection lists (serial_target).
 int orc_run_serial_updates(void* h, int n_updates, avgpu_update_stats* out) {
   World& w = *(World*)h;
+  if ((int64_t)w.face.size() != w.ncells) w.face.assign(w.ncells, 0);
   SerialSched sch;
   sch.init(w.ncells);
   for (int64_t c = 0; c < w.ncells; c++) sch.set(c, w.orgs[c].alive ? w.orgs[c].merit : 0.0);
@@ -2160,45 +2334,60 @@ int orc_run_serial_updates(void* h, int n_updates, avgpu_update_stats* out) {
     int64_t n_alive = 0;
     for (int64_t c = 0; c < w.ncells; c++) n_alive += w.orgs[c].alive;
     const int64_t ud = (int64_t)w.cfg.ave_time_slice * n_alive;   // cWorld::CalculateUpdateSize
-    int64_t insts = 0, births = 0, deaths = 0, divides = 0;
+    int64_t insts = 0, births = 0, deaths = 0, divides = 0, dropped = 0;
     res_begin(w);   // ProcessPreUpdate + the update's first DoUpdates
     for (int64_t i = 0; i < ud; i++) {
       const double tot = sch.tree[1];
       if (!(tot > 0.0)) break;
-      double x = (double)w.global_rng.next() * (1.0 / 4294967296.0) * tot;
+      const double x = w.global_rng.rec ? w.global_rng.u() * tot
+                                        : (double)w.global_rng.next() * (1.0 / 4294967296.0) * tot;
       int64_t c = sch.find(x);
       Org& o = w.orgs[c];
       if (!o.alive) continue;
       insts++;
       if (o.spec_count > 0) { o.spec_count--; continue; }
+      if (o.spec_die) {                        // SingleProcess: m_spec_die -> Die (:917-921)
+        o.alive = false; o.spec_die = false;
+        sch.set(c, 0.0);
+        deaths++;
+        continue;
+      }
       Exec ex{w, o, AVGPU_MODE_WORLD};
+      ex.ctx = &w.ctx_rng;
       w.births.clear();
       const int d0 = o.num_divides;
       ex.single_process(c);
-      // speculative run-ahead: up to 32 more, stopping before STALL insts
-      // (IO, h-divide: cpu/cHardwareCPU.cc:961-968)
+      divides += o.num_divides - d0;
+      bool replaced = false;
+      for (auto& b : w.births) {               // placed inside the h-divide
+        const int r = serial_place(w, sch, b);
+        births += r > 0;
+        deaths += r == 2 || r == 3;            // KillOrganism of the replaced occupant
+        dropped += r == 0;
+        replaced = replaced || r == 3;
+      }
+      w.births.clear();
+      if (replaced) continue;                  // the parent was killed in its own step
+      if (!o.alive) { sch.set(c, 0.0); deaths++; continue; }
+      // speculative run (SingleProcess(ctx, true) while it returns true)
       int spec = 0;
-      while (spec < 32 && o.alive && w.births.empty()) {
-        int hid = w.is.handler[o.mem[adjust(o.head[HEAD_IP], (int)o.mem.size())]];
-        if (hid == H_IO || hid == H_H_DIVIDE) break;
+      while (spec < 32) {
+        const int hid = w.is.handler[o.mem[adjust(o.head[HEAD_IP], (int)o.mem.size())]];
+        if (hid == H_IO || hid == H_H_DIVIDE) break;   // STALL: rejected, nothing counted
+        const int tu_max = o.max_executed;
         ex.single_process(c);
+        if (!o.alive) {                        // reached the age limit speculatively: m_spec_die
+          if (tu_max > 0) { o.alive = true; o.spec_die = true; }
+          break;
+        }
         spec++;
       }
       o.spec_count = spec;
-      divides += o.num_divides - d0;
-      if (!o.alive) { sch.set(c, 0.0); deaths++; }
-      for (auto& b : w.births) {
-        sch.set(c, o.alive ? o.merit : 0.0);   // AdjustSchedule(parent) :933
-        const int r = serial_place(w, sch, b);
-        births += r > 0;
-        deaths += r == 2;                       // KillOrganism of the replaced occupant
-      }
-      w.births.clear();
     }
     res_end(w);
     // cStats for the update (finish_stats advances the update counter)
     w.t_insts = insts; w.t_deaths = deaths; w.t_divides = divides; w.t_slices = 0;
-    finish_stats(w, births, 0);
+    finish_stats(w, births, dropped);
   }
   if (out) *out = w.stats;
   return 0;

@@ -140,10 +140,11 @@ class Backend:
             op = self._off.ctypes.data_as(C.c_void_p)
         self._call("set_rng_mode", self.h, mode, sp, n, op)
 
-    def counters(self):
-        """avgpu_counters of the last update (product only)"""
+    def counters(self, cumulative=0):
+        """avgpu_counters of the last update, or summed over every update
+        (cumulative=1) (product only)"""
         out = (C.c_int64 * capi.NUM_COUNTERS)()
-        self._call("counters", self.h, 0, out, capi.NUM_COUNTERS)
+        self._call("counters", self.h, cumulative, out, capi.NUM_COUNTERS)
         return list(out)
 
     def census(self, first=0, count=None):

@@ -67,21 +67,76 @@ def test_create_without_gpu_fails_loudly():
     assert lib.avgpu_last_error()
 
 
-def test_unsupported_mutation_knobs_are_refused(golden, tmp_path):
-    """A reference avida.cfg that sets a mutation knob this path does not
-    implement is refused, not run with different semantics (capi.UNSUPPORTED_NONZERO)."""
+# (avgpu_cfg field, value away from the reference default) for every knob of
+# the refused block and every value outside an implemented range: the C-ABI
+# itself must refuse each (avgpu_check_cfg / avgpu_create -> AVGPU_EUNSUPPORTED)
+REFUSED_C = [
+    ("point_mut_prob", "0.01"), ("point_ins_prob", "0.01"), ("point_del_prob", "0.01"),
+    ("inst_point_mut_prob", "0.01"), ("div_lgt_prob", "0.01"), ("divide_lgt_prob", "0.01"),
+    ("divide_poisson_lgt_mean", "1.0"), ("inject_mut_prob", "0.01"), ("inject_ins_prob", "0.01"),
+    ("inject_del_prob", "0.01"), ("meta_copy_mut", "0.1"), ("meta_std_dev", "0.1"),
+    ("death_prob", "0.1"), ("age_deviation", "3"), ("divide_failure_resets", "1"),
+    ("special_mut_line", "5"), ("population_cap", "100"), ("generation_inc_method", "0"),
+    ("reset_inputs_on_divide", "1"), ("epigenetic_method", "1"), ("min_cycles", "10"),
+    ("required_task", "2"), ("immunity_task", "2"), ("required_reaction", "2"),
+    ("immunity_reaction", "2"), ("require_single_reaction", "1"), ("max_unique_task_count", "3"),
+    ("require_exact_copy", "1"), ("fitness_method", "1"), ("juv_period", "5"),
+    ("no_mut_insts_len", "1"), ("test_fitness_measures", "1"),
+    ("divide_method", "0"), ("world_geometry", "3"), ("slicing_method", "3"),
+    ("base_merit_method", "6"), ("birth_method", "1"), ("death_method", "3"), ("alloc_method", "1"),
+]
+
+
+def test_c_abi_refuses_every_unimplemented_knob(tmp_path):
+    """Each knob set through the compiled header is refused by the library
+    (avgpu_check_cfg, the check avgpu_create runs first), naming the knob; the
+    defaults are accepted."""
+    build.build()
+    body = "\n".join(
+        f'  {{ avgpu_cfg c; avgpu_cfg_defaults(&c); c.{f} = {v}; int rc = avgpu_check_cfg(&c);'
+        f' printf("{f} %d %s\\n", rc, avgpu_last_error()); }}' for f, v in REFUSED_C)
+    src = tmp_path / "refuse.c"
+    src.write_text('#include "avida_gpu.h"\n#include <stdio.h>\nint main(void){\n'
+                   '  { avgpu_cfg c; avgpu_cfg_defaults(&c); printf("defaults %d\\n", avgpu_check_cfg(&c)); }\n'
+                   + body + "\n  return 0;\n}\n")
+    exe = tmp_path / "refuse"
+    libdir = os.path.dirname(capi.LIB_PATH)
+    subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe), "-L", libdir,
+                    "-lavida_gpu", f"-Wl,-rpath,{libdir}"], check=True)
+    lines = subprocess.check_output([str(exe)], text=True).strip().split("\n")
+    assert lines[0] == "defaults 0"
+    got = {ln.split()[0]: ln for ln in lines[1:]}
+    for f, _ in REFUSED_C:
+        rc = int(got[f].split()[1])
+        assert rc == -5, got[f]                      # AVGPU_EUNSUPPORTED
+        assert "not on the GPU path" in got[f], got[f]
+
+
+def test_python_config_reaches_the_refusal(golden, tmp_path):
+    """A reference avida.cfg that sets a knob this path does not implement
+    fills the avgpu_cfg field, and the library refuses it (no Python-only list)."""
     from avida_amd import files
-    for key in ["DIV_LGT_PROB", "PARENT_INS_PROB", "DIVIDE_POISSON_LGT_MEAN", "COPY_SLIP_PROB",
-                "COPY_UNIFORM_PROB", "DIVIDE_LGT_PROB"]:
-        with pytest.raises(ValueError, match=key):
-            capi.cfg_from_avida(files.read_avida_cfg(None, {key: 0.01}))
+    lib = capi.load_product()
+    for key, field in [("DIV_LGT_PROB", "div_lgt_prob"), ("DIVIDE_POISSON_LGT_MEAN", "divide_poisson_lgt_mean"),
+                       ("DIVIDE_LGT_PROB", "divide_lgt_prob"), ("DEATH_PROB", "death_prob"),
+                       ("POINT_MUT_PROB", "point_mut_prob")]:
+        c = capi.cfg_from_avida(files.read_avida_cfg(None, {key: 0.01}))
+        assert getattr(c, field) == 0.01
+        assert lib.avgpu_check_cfg(C.byref(c)) == -5
+        assert key.split("_")[0] in lib.avgpu_last_error().decode().upper()
+    c = capi.cfg_from_avida(files.read_avida_cfg(None, {"STERILIZE_UNSTABLE": 1}))
+    assert c.test_fitness_measures == 1 and lib.avgpu_check_cfg(C.byref(c)) == -5
+    c = capi.cfg_from_avida(files.read_avida_cfg(None, {"NO_MUT_INSTS": "abc"}))
+    assert c.no_mut_insts_len == 3 and lib.avgpu_check_cfg(C.byref(c)) == -5
     # DIV_MUT_PROB (per-site substitutions on divide) is on the path
-    assert capi.cfg_from_avida(files.read_avida_cfg(None, {"DIV_MUT_PROB": 0.003})).div_mut_prob == 0.003
+    c = capi.cfg_from_avida(files.read_avida_cfg(None, {"DIV_MUT_PROB": 0.003}))
+    assert c.div_mut_prob == 0.003 and lib.avgpu_check_cfg(C.byref(c)) == 0
     text = open(os.path.join(golden, "avida-default.cfg")).read().replace(
-        "COPY_SLIP_PROB 0.0", "COPY_SLIP_PROB 0.001")
+        "POINT_MUT_PROB 0.0", "POINT_MUT_PROB 0.001")
     p = tmp_path / "avida.cfg"
     p.write_text(text)
-    with pytest.raises(ValueError, match="COPY_SLIP_PROB"):
-        capi.cfg_from_avida(files.read_avida_cfg(str(p)))
+    c = capi.cfg_from_avida(files.read_avida_cfg(str(p)))
+    assert c.point_mut_prob == 0.001 and lib.avgpu_check_cfg(C.byref(c)) == -5
     # the reference's default config itself is accepted
-    capi.cfg_from_avida(files.read_avida_cfg(os.path.join(golden, "avida-default.cfg")))
+    c = capi.cfg_from_avida(files.read_avida_cfg(os.path.join(golden, "avida-default.cfg")))
+    assert lib.avgpu_check_cfg(C.byref(c)) == 0, lib.avgpu_last_error()

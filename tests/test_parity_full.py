@@ -62,7 +62,8 @@ def _assert_digests(a, b, what, ba=None, bb=None, first=0):
     assert nbad == 0, f"{what}: {nbad} cells differ, first {cells}"
 
 
-STAT_FIELDS = ("num_organisms", "insts_executed", "births", "deaths", "divides", "births_dropped")
+STAT_FIELDS = ("num_organisms", "insts_executed", "births", "deaths", "divides", "births_dropped",
+               "births_overwritten")
 
 
 @pytest.mark.timeout(900)
@@ -138,3 +139,58 @@ def test_config3_geometry_strips_equal_untiled(golden):
                 orc = None
     assert sent > 0, "no offspring crossed a strip edge"
     assert births > 1_000_000
+
+
+def _transfer(src, dst, n, chunk=1 << 16):
+    """every cell's state + tape of backend src into backend dst (set_states),
+    chunk by chunk, then the genotype keys and the update clock"""
+    cap = 1
+    for lo in range(0, n, chunk):
+        st = (capi.AvgpuCpuState * min(chunk, n - lo))()
+        src._call("get_states", src.h, lo, len(st), st, None, None, 0)
+        cap = max([cap] + [st[i].mem_size for i in range(len(st))])
+    for lo in range(0, n, chunk):
+        cnt = min(chunk, n - lo)
+        st = (capi.AvgpuCpuState * cnt)()
+        ops = (C.c_uint8 * (cnt * cap))()
+        fl = (C.c_uint8 * (cnt * cap))()
+        src._call("get_states", src.h, lo, cnt, st, ops, fl, cap)
+        dst._call("set_states", dst.h, lo, cnt, st, ops, fl, cap)
+    gk = np.ascontiguousarray(src.census()["genotype_key"], dtype=np.uint64)
+    dst._call("set_genotype_keys", dst.h, 0, n, gk.ctypes.data_as(C.c_void_p))
+    stats = capi.AvgpuUpdateStats()
+    src._call("get_stats", src.h, C.byref(stats))
+    dst._call("set_clock", dst.h, C.byref(stats))
+    return cap
+
+
+@pytest.mark.timeout(900)
+def test_config2_bench_regime_bit_exact(golden):
+    """Parity in the regime bench.py times (VERDICT r2 'next' #1): the
+    configs[2] world run on the GPU for bench.py's 150 burn-in updates -- an
+    aged world with size-class spills, list classes running beside class 0
+    on the aux streams, sorted windows -- is checkpointed cell by cell
+    (avgpu_get_states) into the oracle; both then run 3 more updates and
+    every counter and every cell digest must agree.  Every birth is placed
+    (births_dropped == 0: no queue overflow, no oversize offspring)."""
+    import bench
+    X = Y = 1024
+    cfg, iset, env, idx, gen, glen, gmer = _bench_seed(golden, X, Y)
+    gpu = ol.Backend("gpu", cfg, iset, env, ncells=X * Y)
+    _seed(gpu, 0, idx, gen, glen, gmer)
+    spills = 0
+    for u in range(bench.BURN_IN + bench.WARMUP):
+        s = gpu.run_update()
+        spills += gpu.counters()[capi.CNT_SPILLS]
+        assert s.births_dropped == 0, (u, s.births_dropped)
+    assert spills > 1000                         # the aged world spills out of class 0
+    orc = ol.Backend("oracle", cfg, iset, env, ncells=X * Y)
+    cap = _transfer(gpu, orc, X * Y)
+    _assert_digests(orc.digests(), gpu.digests(), "restored world", orc, gpu)
+    for u in range(3):
+        so, sg = orc.run_update(), gpu.run_update()
+        for f in STAT_FIELDS:
+            assert getattr(so, f) == getattr(sg, f), (u, f, getattr(so, f), getattr(sg, f))
+        assert sg.births_dropped == 0 and sg.births > 10_000 and sg.births_overwritten > 0
+        _assert_digests(orc.digests(), gpu.digests(), f"bench regime, update {bench.BURN_IN + bench.WARMUP + u}", orc, gpu)
+    assert cap > 336                             # organisms beyond class 0's slots took part

@@ -133,7 +133,8 @@ def test_gpu_strip_tiles_equal_single_world(golden, T, geometry):
         torch.cuda.synchronize()
         sent += sum(tu.records_sent(t) for _, t in pairs)
         tot = [tu.tile_stats(b) for b, _ in pairs]
-        for f in ("num_organisms", "insts_executed", "births", "deaths", "divides", "births_dropped"):
+        for f in ("num_organisms", "insts_executed", "births", "deaths", "divides", "births_dropped",
+                  "births_overwritten"):
             assert sum(getattr(s, f) for s in tot) == getattr(rstats[u], f), (u, f)
     a, oa, fa = ref.states(0, X * Y, CAP)
     per = X * Y // T

@@ -91,3 +91,23 @@ def test_save_load_roundtrip(golden, tmp_path):
     # every saved organism is back at its cell with its genotype's birth genome
     same = (c1["genotype_key"] == c2["genotype_key"]) | (c1["genotype_key"] == 0)
     assert same.mean() > 0.95      # organisms that copied over their own first sites excepted
+
+
+def test_load_with_offset_keeps_existing_population(golden):
+    """LoadPopulation with a non-zero cellid_offset adds the file's organisms
+    to the world: the clearing KillOrganism pass runs only at offset 0
+    (main/cPopulation.cc:6731-6732).  Offset 0 clears the world first.
+    detail-50000.pop (3599 organisms, no cells column) at offset 1 fills
+    cells 1 .. 3599; the organism already in cell 0 survives."""
+    iset, b = _world(golden, "instset-classic.cfg")
+    path = os.path.join(golden, "detail-50000.pop")
+    g0 = iset.parse_sequence(files.read_pop(path)[0].sequence)
+    b.set_orgs(0, [g0], deterministic=False)
+    placed = population.load_population(b, iset, path, 3600, cellid_offset=1)
+    assert placed == 3599
+    st, _, _ = b.states(0, 3600, 8)
+    assert all(st[c].alive for c in range(3600))            # cell 0 kept its organism
+    b.kill(5)
+    population.load_population(b, iset, path, 3600, cellid_offset=0)
+    st, _, _ = b.states(0, 3600, 8)
+    assert all(st[c].alive for c in range(3599)) and not st[3599].alive   # cleared, then cells 0..3598

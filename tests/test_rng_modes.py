@@ -10,6 +10,8 @@ recorded stream (FROZEN traces of the configs[2] population) and with the
 divide slip / uniform mutations in a world."""
 import os
 
+import ctypes as C
+
 import numpy as np
 import pytest
 
@@ -171,12 +173,130 @@ def test_recorded_draws_translocations(golden):
             break
     assert st[0].num_divides == 1
     assert st[0].rng_counter == 1 + 1 + 3 + 2 + 3 + 100 + 300 + 3
-    with pytest.raises(ValueError, match="TRANS_FILL_MODE"):
-        pu.load_env(golden, overrides={"DIVIDE_TRANS_PROB": 0.1, "TRANS_FILL_MODE": 1})
+    # TRANS_FILL_MODE 1 (scrambled) is refused by the library itself
+    _, _, cfg1 = pu.load_env(golden, overrides={"DIVIDE_TRANS_PROB": 0.1, "TRANS_FILL_MODE": 1})
+    lib = capi.load_product()
+    assert lib.avgpu_check_cfg(C.byref(cfg1)) == -5
+    assert "TRANS_FILL_MODE" in lib.avgpu_last_error().decode()
+
+
+def _u(k, n):
+    """the recorded double that GetUInt(n) / GetInt(n) turns into k"""
+    return (k + 0.5) / n
+
+
+def first_offspring(kind, golden, overrides, stream, side=3):
+    """Run a side x side world holding the default-heads ancestor in its
+    centre cell, the ancestor drawing from `stream` (RECORDED), until the first
+    birth; return (offspring op codes, parent op codes after the divide,
+    stream position of the parent)."""
+    iset, env, cfg, anc = _ancestor(golden, dict({"COPY_MUT_PROB": 0.0, "DIVIDE_INS_PROB": 0.0,
+                                                  "DIVIDE_DEL_PROB": 0.0, "DEATH_METHOD": 0,
+                                                  "WORLD_X": side, "WORLD_Y": side}, **overrides))
+    n = side * side
+    c0 = n // 2
+    b = ol.Backend(kind, cfg, iset, env, ncells=n)
+    try:
+        b.set_orgs(c0, [anc], deterministic=True)
+        offs = np.zeros(n, dtype=np.int64)
+        offs[:] = len(stream)                     # every other cell: an empty segment
+        offs[c0] = 0
+        b.set_rng_mode(capi.RNG_RECORDED, np.asarray(stream, dtype=np.float64), offsets=offs)
+        for _ in range(40):
+            s = b.run_update()
+            if s.births + s.births_overwritten:
+                break
+        st, ops, _ = b.states(0, n, CAP)
+        kids = [c for c in range(n) if c != c0 and st[c].alive]
+        assert len(kids) == 1, kids
+        k = kids[0]
+        child = bytes(ops[k * CAP:k * CAP + st[k].birth_length])
+        parent = bytes(ops[c0 * CAP:c0 * CAP + st[c0].mem_size])
+        return child, parent, st[c0].rng_counter, iset, anc
+    finally:
+        b.close()
+
+
+def _trans_cases():
+    """doTransMutation (cpu/cHardwareBase.cc:700-760) on the 100-site
+    ancestor, derived by hand: (from, to, ins_loc) -> offspring.
+    from > to: copy[to, from) is inserted at ins_loc (g[:ins] = copy[:ins],
+    g[ins:ins+L] = copy[to:from], then copy[ins:]); from < to: the size shrinks
+    by to - from and g[ins:] = copy[ins + to - from:]."""
+    def dup(a, f, t, i):
+        return a[:i] + a[t:f] + a[i:]
+
+    def cut(a, f, t, i):
+        return a[:i] + a[i + (t - f):]
+    return [((30, 10, 50), dup), ((10, 30, 40), cut), ((95, 2, 7), dup), ((3, 90, 5), cut)]
+
+
+@pytest.mark.parametrize("kind", ["oracle", pytest.param("gpu", marks=pytest.mark.gpu)])
+def test_translocation_offspring_content(golden, kind):
+    """Offspring of a recorded translocation, checked against the hand
+    derivation: the divide draws TestDivideSlip, the one-shot
+    TestDivideTrans hit, from, to (GetInt(size+1)), the insertion site
+    (GetInt(size+1)), then the mut / ins / del tests."""
+    for (f, t, i), make in _trans_cases():
+        stream = [0.9, 0.1, _u(f, 101), _u(t, 101), _u(i, 101), 0.9, 0.9, 0.9]
+        child, parent, pos, iset, anc = first_offspring(kind, golden, {"DIVIDE_TRANS_PROB": 1.0}, stream)
+        assert pos == 8
+        assert child == make(anc, f, t, i), (f, t, i)
+        assert parent[:100] == anc          # (it may have re-allocated since)
+
+
+def test_recorded_draws_parent_insertions_deletions(golden):
+    """PARENT_INS_PROB / PARENT_DEL_PROB 0.5 (cpu/cHardwareBase.cc:523-565) at
+    u = 0.37 on the 100-site ancestor: slip, mut, ins, del tests 4; 100
+    insertion tests (all hit) + 100 sites + 100 instructions (the parent grows
+    to 200); 200 deletion tests, capped at 200 - 8 = 192 deletions + 192 sites:
+    696 draws, and the parent is left with the 8-site minimum."""
+    iset, env, cfg, anc = _ancestor(golden, {"COPY_MUT_PROB": 0.0, "DIVIDE_INS_PROB": 0.0,
+                                             "DIVIDE_DEL_PROB": 0.0, "DEATH_METHOD": 0,
+                                             "PARENT_INS_PROB": 0.5, "PARENT_DEL_PROB": 0.5})
+    b = ol.Backend("oracle", cfg, iset, env, ncells=1)
+    b.set_orgs(0, [anc], deterministic=True)
+    b.set_rng_mode(capi.RNG_RECORDED, np.full(4096, 0.37))
+    for k in range(2000):
+        b.step(0, 1, uniform=1, mode=capi.MODE_FROZEN)
+        st, _, _ = b.states(0, 1, CAP)
+        if st[0].num_divides:
+            break
+    assert st[0].num_divides == 1
+    assert st[0].rng_counter == 4 + 300 + 200 + 192
+    assert st[0].mem_size == 8
+    assert b.lib.orc_rec_exhausted() == 0
+
+
+def test_copy_mutation_draw_order(golden):
+    """Inst_HeadCopy's copy mutations (cpu/cHardwareCPU.cc:7144-7161): per
+    h-copy TestCopyMut, then TestCopyIns [+ GetRandomInst], TestCopyDel,
+    TestCopyUniform [+ GetUInt(2n+1)], TestCopySlip [+ GetInt(size)], each
+    drawing only at a non-zero rate.  At u = 0.37 with every rate 0.5 every
+    test hits: a copy draws mut 2 + ins 2 + del 1 + uniform 2 + slip 2 = 9."""
+    iset, env, cfg, anc = _ancestor(golden, {"COPY_MUT_PROB": 0.5, "COPY_INS_PROB": 0.5,
+                                             "COPY_DEL_PROB": 0.5, "COPY_UNIFORM_PROB": 0.5,
+                                             "COPY_SLIP_PROB": 0.5, "DEATH_METHOD": 0})
+    b = ol.Backend("oracle", cfg, iset, env, ncells=1)
+    b.set_orgs(0, [anc], deterministic=True)
+    b.set_rng_mode(capi.RNG_RECORDED, np.full(100000, 0.37))
+    # the ancestor's first h-copy is its 90th instruction (Appendix B of SURVEY.md)
+    b.step(0, 1, uniform=89, mode=capi.MODE_FROZEN)
+    st0, _, _ = b.states(0, 1, CAP)
+    assert st0[0].rng_counter == 0
+    b.step(0, 1, uniform=1, mode=capi.MODE_FROZEN)
+    st, ops, fl = b.states(0, 1, CAP)
+    assert st[0].rng_counter == 9
+    # ins then del at the write head cancel; the uniform draw floor(0.37 * 53)
+    # = 19 < 26 substitutes op 19 in place; the slip moves the read head to
+    # floor(0.37 * 300) = 111, then Advance -> 112; the write head advances
+    assert st[0].mem_size == 300
+    assert st[0].head[1] == 112 and st[0].head[2] == 101
+    assert ops[100] == 19 and fl[100] & 1
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("muts", ["copy", "all", "site", "poisson"])
+@pytest.mark.parametrize("muts", ["copy", "all", "site", "poisson", "copyext"])
 def test_recorded_stream_frozen_traces_gpu(golden, muts):
     """BASELINE configs[2] traces with mutations on, fed from one recorded
     stream: 3600 organisms of the detail-50000 population, each with its own
@@ -189,7 +309,11 @@ def test_recorded_stream_frozen_traces_gpu(golden, muts):
         ov.update({"DIVIDE_MUT_PROB": 0.1, "DIVIDE_SLIP_PROB": 0.05, "DIVIDE_UNIFORM_PROB": 0.05})
     if muts == "site":      # per-site divide substitutions: one draw per offspring site
         ov.update({"DIV_MUT_PROB": 0.02, "PARENT_MUT_PROB": 0.01, "DIV_INS_PROB": 0.005,
-                   "DIV_DEL_PROB": 0.005, "DIV_UNIFORM_PROB": 0.005, "DIV_SLIP_PROB": 0.001})
+                   "DIV_DEL_PROB": 0.005, "DIV_UNIFORM_PROB": 0.005, "DIV_SLIP_PROB": 0.001,
+                   "PARENT_INS_PROB": 0.005, "PARENT_DEL_PROB": 0.005})
+    if muts == "copyext":   # copy insertions / deletions / uniform / slips (cpu/cHardwareCPU.cc:7153-7161)
+        ov.update({"COPY_INS_PROB": 0.02, "COPY_DEL_PROB": 0.02, "COPY_UNIFORM_PROB": 0.01,
+                   "COPY_SLIP_PROB": 0.005, "PARENT_MUT_PROB": 0.0})
     if muts == "poisson":
         ov.update({"DIVIDE_POISSON_SLIP_MEAN": 0.3, "DIVIDE_POISSON_MUT_MEAN": 1.5,
                    "DIVIDE_TRANS_PROB": 0.05, "DIVIDE_POISSON_TRANS_MEAN": 0.1,
@@ -197,7 +321,7 @@ def test_recorded_stream_frozen_traces_gpu(golden, muts):
     iset, env, cfg = pu.load_env(golden, "instset-classic.cfg", ov)
     n = len(genomes)
     rng = np.random.default_rng(42)
-    per = 4500 if muts != "site" else 16000   # h-copy alone draws once per copy at a non-zero rate
+    per = {"site": 16000, "copyext": 24000}.get(muts, 4500)   # h-copy draws per copy at non-zero rates
     stream = rng.random(n * per)
     offsets = np.arange(n, dtype=np.int64) * per
     pair = [ol.Backend(k, cfg, iset, env, ncells=n) for k in ("oracle", "gpu")]
@@ -232,7 +356,8 @@ def test_divide_slip_uniform_world_gpu(golden, fill):
         b.set_orgs(0, g, deterministic=False)
     for u in range(120):
         so, sg = pair[0].run_update(), pair[1].run_update()
-        for f in ("num_organisms", "insts_executed", "births", "deaths", "divides", "births_dropped"):
+        for f in ("num_organisms", "insts_executed", "births", "deaths", "divides", "births_dropped",
+                  "births_overwritten"):
             assert getattr(so, f) == getattr(sg, f), (u, f)
     nbad, cells = pu.compare_digests(pair[0].digests(), pair[1].digests())
     assert nbad == 0, cells
@@ -241,7 +366,8 @@ def test_divide_slip_uniform_world_gpu(golden, fill):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("knob", ["DIV_MUT_PROB", "PARENT_MUT_PROB", "POISSON", "PER_SITE", "TRANS"])
+@pytest.mark.parametrize("knob", ["DIV_MUT_PROB", "PARENT_MUT_PROB", "POISSON", "PER_SITE", "TRANS",
+                                  "PARENT_INDEL"])
 def test_per_site_divide_mutations_world_gpu(golden, knob):
     """World updates with DIV_MUT_PROB (per-site substitutions in the
     offspring, cpu/cHardwareBase.cc:447-460) or PARENT_MUT_PROB (in the
@@ -254,6 +380,9 @@ def test_per_site_divide_mutations_world_gpu(golden, knob):
               "DIV_SLIP_PROB": 0.001, "WORLD_X": 48, "WORLD_Y": 48}
     if knob == "TRANS":      # translocations: one-shot, Poisson, per site (:331-343)
         ov = {"DIVIDE_TRANS_PROB": 0.1, "DIVIDE_POISSON_TRANS_MEAN": 0.1, "DIV_TRANS_PROB": 0.0005,
+              "WORLD_X": 48, "WORLD_Y": 48}
+    if knob == "PARENT_INDEL":   # per-site insertions / deletions in the parent (:523-565)
+        ov = {"PARENT_INS_PROB": 0.01, "PARENT_DEL_PROB": 0.01, "PARENT_MUT_PROB": 0.005,
               "WORLD_X": 48, "WORLD_Y": 48}
     if knob == "POISSON":
         ov = {"DIVIDE_POISSON_SLIP_MEAN": 0.1, "DIVIDE_POISSON_MUT_MEAN": 1.0,
@@ -268,10 +397,52 @@ def test_per_site_divide_mutations_world_gpu(golden, knob):
     births = 0
     for u in range(120):
         so, sg = pair[0].run_update(), pair[1].run_update()
-        for f in ("num_organisms", "insts_executed", "births", "deaths", "divides", "births_dropped"):
+        for f in ("num_organisms", "insts_executed", "births", "deaths", "divides", "births_dropped",
+                  "births_overwritten"):
             assert getattr(so, f) == getattr(sg, f), (u, f)
         births += sg.births
         assert pair[1].counters()[capi.CNT_SUB_OVERFLOW] == 0
+        assert pair[1].counters()[capi.CNT_MEM_CAP] == 0
     nbad, cells = pu.compare_digests(pair[0].digests(), pair[1].digests())
     assert nbad == 0, cells
     assert births > 500
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("rec", [False, True])
+def test_copy_mutations_world_gpu(golden, rec):
+    """World updates with COPY_INS_PROB, COPY_DEL_PROB, COPY_UNIFORM_PROB and
+    COPY_SLIP_PROB (cpu/cHardwareCPU.cc:7153-7161) on top of the default
+    mutations: the memory grows and shrinks in the middle of h-copy, and a copy
+    that would outgrow its LDS size class is rewound and spills to the next
+    class.  GPU world == oracle world, every cell digest, 150 updates; rec:
+    every organism of the seeded world draws from a recorded stream."""
+    ov = {"COPY_INS_PROB": 0.03, "COPY_DEL_PROB": 0.02, "COPY_UNIFORM_PROB": 0.01,
+          "COPY_SLIP_PROB": 0.005, "WORLD_X": 48, "WORLD_Y": 48}
+    iset, env, cfg, anc = _ancestor(golden, ov)
+    n = 48 * 48
+    pair = [ol.Backend(k, cfg, iset, env, ncells=n) for k in ("oracle", "gpu")]
+    g = pu.mutants_of(anc, iset, n // 4, rate=0.01, seed=13)
+    if rec:
+        per = 60000
+        stream = np.random.default_rng(5).random(n * per)
+        offsets = np.arange(n, dtype=np.int64) * per
+    for b in pair:
+        b.set_orgs(0, g, deterministic=False)
+        if rec:
+            b.set_rng_mode(capi.RNG_RECORDED, stream, offsets)
+    births = 0
+    for u in range(150):
+        so, sg = pair[0].run_update(), pair[1].run_update()
+        for f in ("num_organisms", "insts_executed", "births", "deaths", "divides", "births_dropped",
+                  "births_overwritten"):
+            assert getattr(so, f) == getattr(sg, f), (u, f)
+        births += sg.births
+    nbad, cells = pu.compare_digests(pair[0].digests(), pair[1].digests())
+    assert nbad == 0, cells
+    c = pair[1].counters(cumulative=1)
+    assert births > 500
+    assert c[capi.CNT_SPILLS] > 0          # copies rewound into the next size class
+    assert c[capi.CNT_MEM_CAP] == 0
+    lens = {pair[0].states(k, 1)[0][0].birth_length for k in range(0, n, 7)}
+    assert len(lens) > 5

@@ -5,15 +5,16 @@ offspring placed at once (main/cPopulation.cc:5698-5788, :621-952) -- run by
 the product's interpreter on the GPU, against the oracle's restatement of the
 same loop (oracle/oracle.cc orc_run_serial_updates): every update's
 statistics and, at the end, every cell and every field bit for bit."""
+import ctypes as C
 import os
 
+import numpy as np
 import pytest
 
 from avida_amd import capi, files
 import oracle_lib as ol
 import parity_util as pu
 
-pytestmark = pytest.mark.gpu
 CAP = capi.MAX_GENOME
 # integer statistics bit for bit; the double sums over organisms within 1e-12
 # relative (the statistics kernels and the oracle add in different orders)
@@ -43,6 +44,7 @@ def _run(orc, gpu, updates):
     return last
 
 
+@pytest.mark.gpu
 def test_serial_world_from_ancestor(golden):
     """One ancestor on a 60x60 torus, default mutation rates, 120 serial
     updates: the colony grows through thousands of immediate placements."""
@@ -59,6 +61,7 @@ def test_serial_world_from_ancestor(golden):
     assert last.num_organisms > 20 and last.births > 0
 
 
+@pytest.mark.gpu
 def test_serial_world_dense_population(golden):
     """The bench's evolved logic-9 population (detail-50000.pop, classic
     instset) filling a 60x60 torus, with the divide slip, uniform and
@@ -81,11 +84,94 @@ def test_serial_world_dense_population(golden):
     _compare_states(orc, gpu, n)
 
 
+@pytest.mark.gpu
 def test_serial_world_refuses_recorded_streams(golden):
     iset, env, cfg = pu.load_env(golden, seed=3)
     gpu = ol.Backend("gpu", cfg, iset, env, ncells=cfg.world_x * cfg.world_y)
-    import numpy as np
     n = cfg.world_x * cfg.world_y
     gpu.set_rng_mode(capi.RNG_RECORDED, np.full(16, 0.5), np.zeros(n, dtype=np.int64))
-    with pytest.raises(RuntimeError, match="counter streams"):
+    with pytest.raises(RuntimeError, match="avgpu_set_serial_streams"):
         gpu.run_serial_update()
+
+
+def _set_streams(b, sched, ctx):
+    b._sched = np.ascontiguousarray(sched, dtype=np.float64)
+    b._ctx = np.ascontiguousarray(ctx, dtype=np.float64)
+    b._call("set_serial_streams", b.h, b._sched.ctypes.data_as(C.c_void_p), len(b._sched),
+            b._ctx.ctypes.data_as(C.c_void_p), len(b._ctx))
+
+
+@pytest.mark.gpu
+def test_serial_world_recorded_streams(golden):
+    """The serial world fed from two recorded streams -- the scheduler's picks
+    and the context stream every other draw comes from, as the reference has
+    them (main/cPopulation.cc:7341-7346) -- with copy and divide mutations on:
+    the dense evolved population for 7 serial updates, GPU == oracle every
+    update's statistics and every cell's state; no stream runs out."""
+    iset, env, cfg = pu.load_env(golden, "instset-classic.cfg", seed=9,
+                                 overrides={"COPY_MUT_PROB": 0.01, "DIVIDE_SLIP_PROB": 0.05,
+                                            "COPY_INS_PROB": 0.002, "COPY_DEL_PROB": 0.002})
+    n = cfg.world_x * cfg.world_y
+    genomes = pu.pop_genomes(golden, iset)[:n]
+    rng = np.random.default_rng(17)
+    sched, ctx = rng.random(400_000), rng.random(2_000_000)
+    orc = ol.Backend("oracle", cfg, iset, env, ncells=n)
+    gpu = ol.Backend("gpu", cfg, iset, env, ncells=n)
+    for b in (orc, gpu):
+        b.set_orgs(0, genomes, deterministic=False)
+        _set_streams(b, sched, ctx)
+    last = _run(orc, gpu, 7)
+    _compare_states(orc, gpu, n)
+    assert last.cum_births > 100            # the lock-step population's first births: update 5
+    assert gpu.counters()[capi.CNT_REC_EXHAUSTED] == 0
+
+
+def _placement_case(kind, golden, k1, k2):
+    """5x5 torus, the default-heads ancestor in cell 12, AGE_LIMIT 4 (it dies
+    400 instructions in, right after its first divide); recorded streams.  The
+    context stream: the four always-drawn divide tests (no hit), the
+    placement draw picking found-list index k1, the newborn's three inputs;
+    then the same for the child's own divide with index k2.  Returns the cells
+    of the child and of the grandchild."""
+    iset, env, cfg = pu.load_env(golden, seed=1, overrides={
+        "WORLD_X": 5, "WORLD_Y": 5, "COPY_MUT_PROB": 0.0, "AGE_LIMIT": 4})
+    b = ol.Backend(kind, cfg, iset, env, ncells=25)
+    anc = files.read_org(os.path.join(golden, "default-heads.org"), iset)
+    b.set_orgs(12, [anc], deterministic=True)
+    u = lambda k, n: (k + 0.5) / n          # noqa: E731  GetUInt(n) -> k
+    ctx = [0.99] * 4 + [u(k1, 8)] + [0.5] * 3 + [0.99] * 4 + [u(k2, 8)] + [0.5] * 3
+    _set_streams(b, np.random.default_rng(3).random(100_000), ctx + [0.99] * 64)
+    cells = [None, None]          # the newborn of generation 1 (child) and 2 (grandchild)
+    for _ in range(80):
+        b.run_serial_update()
+        st, _, _ = b.states(0, 25, 8)
+        for c in range(25):
+            g = st[c].generation
+            if st[c].alive and st[c].num_divides == 0 and g in (1, 2) and cells[g - 1] is None:
+                cells[g - 1] = c
+        if cells[1] is not None:
+            break
+    b.close()
+    return cells
+
+
+@pytest.mark.parametrize("kind", ["oracle", pytest.param("gpu", marks=pytest.mark.gpu)])
+def test_serial_placement_follows_reference_connection_lists(golden, kind):
+    """Hand-derived placement (PositionOffspring, main/cPopulation.cc:5353-5413,
+    on cTopology's lists).  Cell 12 = (2, 2) of a 5x5 torus: build_torus pushes
+    NW N NE E SE S SW W and Push prepends (tools/cTopology.h:40-55,
+    tools/tList.h:140-147), so its list is W11 SW16 S17 SE18 E13 NE8 N7 NW6;
+    FindEmptyCell prepends every empty cell (:7361-7370), so with all of them
+    empty the found list is 6 7 8 13 18 17 16 11 and GetUInt(8) = k picks
+    found[k].  The child in cell 6 = (1, 1) has the list W5 SW10 S11 SE12 E7
+    NE2 N1 NW0, rotated to face its parent 12 (cPopulationCell::Rotate,
+    main/cPopulationCell.cc:122-141): 12 7 2 1 0 5 10 11; the parent has died
+    by the child's divide, so every cell is empty and the found list is
+    11 10 5 0 1 2 7 12 (unrotated it would be 0 1 2 7 12 11 10 5)."""
+    found1 = [6, 7, 8, 13, 18, 17, 16, 11]
+    found2 = [11, 10, 5, 0, 1, 2, 7, 12]
+    for k1, k2 in [(0, 0), (0, 2), (0, 7)]:
+        assert _placement_case(kind, golden, k1, k2) == [found1[k1], found2[k2]], (k1, k2)
+    # a child in cell 13 = (3, 2): list W12 SW17 S18 SE19 E14 NE9 N8 NW7, the
+    # parent already first (no rotation): found 7 8 9 14 19 18 17 12
+    assert _placement_case(kind, golden, 3, 1) == [13, 8]

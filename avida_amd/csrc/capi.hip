@@ -70,6 +70,7 @@ struct avgpu_world {
   // device scratch
   double* d_totals = nullptr;   // [8 + partials]
   double* d_stats = nullptr;    // [32 + partials]
+  bool stats_stale = false;     // the last update ran without statistics (out == NULL)
   bool use_global = false;
   int64_t update = 0;
   float last_kernel_ms = 0.f;
@@ -147,6 +148,8 @@ int setup_world(avgpu_world* w, int64_t n, bool test_buffers) {
   A(b_prio, R); A(b_genome, (size_t)R * TAPE_SLOT);
   // placement scratch with two ghost rows (strip tiles)
   A(occ, n + 2 * c.world_x); A(claim, n + 2 * c.world_x); A(claim2, n); A(owner, n + 2 * c.world_x);
+  W.claim_r[0] = W.claim; W.claim_r[1] = W.claim2;
+  A(claim_r[2], n); A(claim_r[3], n); A(b_tgt, 4 * R);
   if (test_buffers) {
     A(t_flags, (size_t)n * TAPE_SLOT); A(t_flags_len, n); A(t_child, (size_t)n * TAPE_SLOT);
     A(t_child_len, n);
@@ -735,8 +738,11 @@ int avgpu_update_run(avgpu_world* w, const double* dev_totals, avgpu_update_stat
   HIPCHK(hipGetLastError());
   rc = interpret(w, AVGPU_MODE_WORLD, 0, w->W.n, true);
   if (rc < 0) return rc;
-  launch_world_post(w->W, w->stream, w->d_stats);
+  // statistics only when asked for: a run without them (out == NULL) leaves
+  // the reduction to avgpu_get_stats / avgpu_stats_vector, or skips it
+  launch_world_post(w->W, w->stream, w->d_stats, out != nullptr);
   HIPCHK(hipGetLastError());
+  w->stats_stale = out == nullptr;
   w->update++;
   if (out) return avgpu_get_stats(w, out);
   return 0;
@@ -755,8 +761,11 @@ int avgpu_run_update(avgpu_world* w, avgpu_update_stats* out) {
   HIPCHK(hipGetLastError());
   rc = interpret(w, AVGPU_MODE_WORLD, 0, w->W.n, true);
   if (rc < 0) return rc;
-  launch_world_post(w->W, w->stream, w->d_stats);
+  // statistics only when asked for: a run without them (out == NULL) leaves
+  // the reduction to avgpu_get_stats / avgpu_stats_vector, or skips it
+  launch_world_post(w->W, w->stream, w->d_stats, out != nullptr);
   HIPCHK(hipGetLastError());
+  w->stats_stale = out == nullptr;
   w->update++;
   if (out) return avgpu_get_stats(w, out);
   return 0;
@@ -831,6 +840,7 @@ int avgpu_run_serial_updates(avgpu_world* w, int n, avgpu_update_stats* last) {
     launch_serial_update(W, w->d_W, w->stream);
     launch_serial_post(W, w->stream, w->d_stats);
     HIPCHK(hipGetLastError());
+    w->stats_stale = false;
     w->update++;
   }
   if (last) return avgpu_get_stats(w, last);
@@ -849,6 +859,11 @@ int avgpu_run_updates(avgpu_world* w, int n, avgpu_update_stats* last) {
 int avgpu_get_stats(avgpu_world* w, avgpu_update_stats* out) {
   if (!w || !out) return fail(AVGPU_EINVAL, "args");
   double v[40];
+  if (w->stats_stale) {
+    launch_stats(w->W, w->stream, w->d_stats);
+    HIPCHK(hipGetLastError());
+    w->stats_stale = false;
+  }
   HIPCHK(hipMemcpyAsync(v, w->d_stats, sizeof(v), hipMemcpyDeviceToHost, w->stream));
   HIPCHK(hipStreamSynchronize(w->stream));
   memset(out, 0, sizeof(*out));
@@ -1026,6 +1041,9 @@ int avgpu_set_clock(avgpu_world* w, const avgpu_update_stats* last) {
   const unsigned long long cb = (unsigned long long)last->cum_births;
   HIPCHK(hipMemcpyAsync(w->W.counters + CNT_CUM_INSTS, &ci, sizeof(ci), hipMemcpyHostToDevice, w->stream));
   HIPCHK(hipMemcpyAsync(w->W.counters + CNT_CUM_BIRTHS, &cb, sizeof(cb), hipMemcpyHostToDevice, w->stream));
+  // the sums given are complete: the current shards are not folded in again
+  static const unsigned long long one = 1ull;
+  HIPCHK(hipMemcpyAsync(w->W.counters + CNT_CUM_FLAG, &one, sizeof(one), hipMemcpyHostToDevice, w->stream));
   HIPCHK(hipStreamSynchronize(w->stream));
   w->update = last->update + 1;
   return 0;
@@ -1101,6 +1119,11 @@ int avgpu_test_genomes(avgpu_world* w, int n, const uint8_t* genomes, const int3
 
 int avgpu_stats_vector(avgpu_world* w, void** dev_ptr) {
   if (!w || !dev_ptr) return fail(AVGPU_EINVAL, "args");
+  if (w->stats_stale) {           // the vector is complete once this stream reaches it
+    launch_stats(w->W, w->stream, w->d_stats);
+    HIPCHK(hipGetLastError());
+    w->stats_stale = false;
+  }
   *dev_ptr = w->d_stats;
   return 0;
 }
@@ -1395,7 +1418,8 @@ int avgpu_tile_begin(avgpu_world* w, const double* dev_gathered, int ntiles) {
 int avgpu_tile_place(avgpu_world* w, int round, int phase) {
   int rc = tile_ready(w);
   if (rc < 0) return rc;
-  if (round < 0 || round > 3 || phase < 0 || phase > 3) return fail(AVGPU_EINVAL, "round / phase");
+  if (round < 0 || round > 3 || phase < 0 || phase > 3 || (phase >= 2 && round != 3))
+    return fail(AVGPU_EINVAL, "round 0..3 with phase 0..1; phases 2, 3 after round 3");
   launch_tile_place(w->W, w->stream, round, phase);
   HIPCHK(hipGetLastError());
   return 0;
@@ -1404,8 +1428,9 @@ int avgpu_tile_place(avgpu_world* w, int round, int phase) {
 int avgpu_tile_finish(avgpu_world* w, avgpu_update_stats* out) {
   int rc = tile_ready(w);
   if (rc < 0) return rc;
-  launch_tile_finish(w->W, w->stream, w->d_stats);
+  launch_tile_finish(w->W, w->stream, w->d_stats, out != nullptr);
   HIPCHK(hipGetLastError());
+  w->stats_stale = out == nullptr;
   w->update++;
   if (out) return avgpu_get_stats(w, out);
   return 0;
@@ -1462,9 +1487,10 @@ int avgpu_counters(avgpu_world* w, int cumulative, int64_t* out, int n) {
   HIPCHK(hipStreamSynchronize(w->stream));
   for (int k = 0; k < n; k++) {
     unsigned long long s = 0;
-    if (cumulative) s = v[CNT_CUM_BASE + k];
-    else
+    // (an update run without statistics has its counts still in the shards)
+    if (!cumulative || v[CNT_CUM_FLAG] == 0ull)
       for (int sh = 0; sh < NSHARD; sh++) s += v[sh * CNT_STRIDE + k];
+    if (cumulative) s += v[CNT_CUM_BASE + k];
     out[k] = (int64_t)s;
   }
   return 0;

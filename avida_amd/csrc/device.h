@@ -163,7 +163,12 @@ struct DevWorld {
   // placement scratch, n cells + 2 ghost rows (strip tiles, below)
   uint8_t* occ;       // [n + 2X]
   unsigned long long* claim; // [n + 2X]
-  unsigned long long* claim2; // [n] odd placement rounds of a single world (launch_world_post)
+  unsigned long long* claim2; // [n] (claim_r[1])
+  // a single world's placement rounds 0..3 claim into their own arrays
+  // (k_place_round): claim_r[0] = claim, [1] = claim2, [2], [3] [n] each; all
+  // zero between updates
+  unsigned long long* claim_r[4];
+  int32_t* b_tgt;     // [4][rcap] the record's target in each placement round it claimed in
   int32_t* owner;     // [n + 2X]  record id, -1 none, REMOTE_OWNER(k) won by a halo birth in round k
   // test-CPU outputs
   uint8_t* t_flags;   // [n][TAPE_SLOT] executed flags snapshot ('+'/'-')
@@ -271,7 +276,8 @@ struct DevWorld {
   int32_t row0, global_rows, rows, tiled;
   int64_t cell0;          // row0 * world_x: global id of local cell 0 (RNG keys, priorities)
   // halo buffers per direction d (0: tile above, 1: tile below), registered by
-  // the host: HALO_BYTES(X) = X u64 claims then X u8 occupancy flags
+  // the host: halo_bytes(X) = X u64 claims on the receiver's edge row, X u64
+  // the sender's own claims on its edge row, X u8 edge-row occupancy
   uint8_t* h_send[2];
   uint8_t* h_recv[2];
   // birth-record buffers per direction: HaloHdr, X HaloRec, arena of r_arena bytes
@@ -281,7 +287,7 @@ struct DevWorld {
 };
 
 #define REMOTE_OWNER(k) (-2 - (k))
-__host__ __device__ inline int64_t halo_bytes(int x) { return ((int64_t)x * 9 + 15) / 16 * 16; }
+__host__ __device__ inline int64_t halo_bytes(int x) { return ((int64_t)x * 17 + 15) / 16 * 16; }
 struct HaloHdr { int32_t count, arena_used, overflow, pad; };
 // one offspring placed across a tile edge (the migrant record of
 // cMultiProcessWorld.cc:142-190, restated for strip tiles)
@@ -344,6 +350,9 @@ enum { SEG_PSLIP = 0, SEG_SSLIP, SEG_TTRANS, SEG_PTRANS, SEG_STRANS, SEG_PMUT, S
 #define CNT_WORDS (NSHARD * CNT_STRIDE + CNT_STRIDE)
 #define CNT_CUM_INSTS (CNT_CUM_BASE + CNT_INSTS)
 #define CNT_CUM_BIRTHS (CNT_CUM_BASE + CNT_BIRTHS)
+// 1 once this update's counts are in the running sums (k_stats_final); 0 after
+// reset_counts_block, which folds them in itself when statistics were skipped
+#define CNT_CUM_FLAG (CNT_CUM_BASE + CNT_STRIDE - 1)
 
 __device__ __forceinline__ int queue_len(const DevWorld& W) {
   const int64_t n = (int64_t)W.b_count[0] + (int64_t)min(W.b_count[1], (int)(W.rcap - W.n));
@@ -501,7 +510,13 @@ __device__ __forceinline__ void count_add(const DevWorld& W, int slot, unsigned 
 // LDS size classes of k_interpret (bytes of tape per lane)
 // (a block of class S uses 64 x tape_stride(S) B of LDS for tapes; class 0 is
 // sized so that 7 blocks fit a CU's 160 KiB with its two lookup tables)
+#ifdef AVGPU_C0_320
+// 320-site class-0 slots with the lookup tables in global memory: 64 x 320 B
+// is exactly a CU's 160 KiB / 8 blocks (A/B variant)
+#define CLASS0_SIZE 320
+#else
 #define CLASS0_SIZE 336
+#endif
 #define CLASS1_SIZE 768
 #define CLASS2_SIZE 1536
 #define CLASS3_SIZE 2048
@@ -557,7 +572,9 @@ void launch_resources_end(const DevWorld& W, hipStream_t s);
 void launch_resources_pack(const DevWorld& W, hipStream_t s);
 bool res_stepped(const DevWorld& W);   // launch_resources_begin wrote res_amount_alt
 void launch_resources_settle(const DevWorld& W, hipStream_t s, const unsigned long long* sum);
-void launch_world_post(const DevWorld& W, hipStream_t s, double* d_stats);
+void launch_world_post(const DevWorld& W, hipStream_t s, double* d_stats, bool eager);
+// the update's statistics into d_stats (k_stats_partial + k_stats_final)
+void launch_stats(const DevWorld& W, hipStream_t s, double* d_stats);
 void launch_classify_uniform(const DevWorld& W, hipStream_t s, int64_t first, int64_t count,
                              const int32_t* d_budget, int32_t uniform);
 void launch_set_orgs(const DevWorld& W, hipStream_t s, int64_t first, int64_t count,
@@ -576,4 +593,4 @@ void launch_tile_totals(const DevWorld& W, hipStream_t s, const double* d_gather
                         double* d_totals);
 void launch_tile_after_interpret(const DevWorld& W, hipStream_t s);
 void launch_tile_place(const DevWorld& W, hipStream_t s, int round, int phase);
-void launch_tile_finish(const DevWorld& W, hipStream_t s, double* d_stats);
+void launch_tile_finish(const DevWorld& W, hipStream_t s, double* d_stats, bool eager);

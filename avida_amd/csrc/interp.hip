@@ -164,6 +164,11 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
   typedef const __attribute__((address_space(3))) uint16_t lds_u16_t;
   typedef const __attribute__((address_space(3))) uint8_t lds_u8_t;
   lds_u16_t* lut = (lds_u16_t*)(tab);
+#ifdef AVGPU_C0_320
+  constexpr bool GLUT = (S == CLASS0_SIZE);   // no tables in LDS at all
+#else
+  constexpr bool GLUT = false;
+#endif
   const int32_t* rcum = GTAB ? W.rand_cum : reinterpret_cast<const int32_t*>(tab + 128);
   const uint8_t* rcode = GTAB ? W.rand_code : reinterpret_cast<const uint8_t*>(tab + 192);
   lds_u8_t* rlut = (lds_u8_t*)(tab + (GTAB ? 128 : 208));
@@ -234,7 +239,8 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
   const int m_in = M;
 
   // ---- block-shared tables ----
-  if (GTAB) {
+  if (GLUT) {
+  } else if (GTAB) {
     const uint32_t* g_lut = reinterpret_cast<const uint32_t*>(W.task_lut);
     tab[lane] = g_lut[lane];
     tab[64 + lane] = g_lut[64 + lane];
@@ -415,7 +421,7 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
   // cInstSet::GetRandomInst (cpu/cInstSet.cc:83-88) from the LDS tables
   auto rand_code = [&]() -> uint8_t {
     const uint32_t r = draw_below((uint32_t)k_rand_total);
-    if (k_rand_lut) return rlut[r];
+    if (k_rand_lut) return GLUT ? (uint8_t)ld_sync_u8(W.rand_lut + r) : rlut[r];
     int i = 0;
     while (i < k_n_ops - 1 && tab_i32(rcum + i) <= (int32_t)r) i++;
     return (uint8_t)tab_u8(rcode + i);
@@ -720,7 +726,9 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
         if (num < 2) { lo |= (lo & 3u) << 2; pr |= (pr & 3u) << 2; }
         if (num < 3) { lo |= (lo & 15u) << 4; pr |= (pr & 15u) << 4; }
         const int id = (int)lo - (int)(~pr & 0xFFu);
-        const uint32_t tmask = ((ones & zeros) == 0u && id >= 0) ? lut[id] : 0u;
+        uint32_t tmask = 0u;
+        if ((ones & zeros) == 0u && id >= 0)
+          tmask = GLUT ? (ld_sync_u32(W.task_lut + (id & ~1)) >> ((id & 1) * 16)) & 0xFFFFu : lut[id];
         // cEnvironment::TestOutput / TestRequisites / DoProcesses
         // (main/cEnvironment.cc:1314-1406, :1408-1503, :1610-1760)
         if (tmask && k_env_simple) {
@@ -1614,7 +1622,11 @@ __global__ __launch_bounds__(64, (S == CLASS0_SIZE) ? 2 : 1) void k_interpret(co
   constexpr int TAB_WORDS = 128 + 64 + 16 + 64 + AVGPU_MAX_REACTIONS * RT_STRIDE + 64;
   // class 0: stacks in VGPRs, tables in global memory -- only the tapes in LDS
   constexpr int STK = (S == CLASS0_SIZE) ? 0 : 2 * AVGPU_STACK_SIZE * 64;
+#ifdef AVGPU_C0_320
+  constexpr int TAB = (S == CLASS0_SIZE) ? 0 : TAB_WORDS;     // class 0: tapes only
+#else
   constexpr int TAB = (S == CLASS0_SIZE) ? 192 : TAB_WORDS;   // class 0: task LUT + random LUT
+#endif
   __shared__ __attribute__((aligned(16))) uint32_t lds32[64 * tape_stride(S) / 4 + STK + TAB];
   if (cls == 0) {
     // sorted windows: the 32 chunks of a window run on one XCD (blocks are

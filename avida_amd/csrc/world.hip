@@ -313,7 +313,28 @@ __global__ void k_classify_uniform(DevWorld W, int64_t first, int64_t count, con
 // (strip tiles hold whole 256-cell blocks, so the block partials of a tiled
 // world are the single world's partials; alive_d: alive counts as doubles
 // after the merits, the layout tiles exchange)
+// Before the shards are cleared, an update whose statistics were never asked
+// for (lazy: run with out == NULL, CNT_CUM_FLAG still 0) has its counts added
+// to the running sums here instead of in k_stats_final.  One block, >= 256
+// threads; the caller's condition is block-uniform.
 __device__ __forceinline__ void reset_counts_block(const DevWorld& W) {
+  constexpr int NG = 256 / CNT_STRIDE;
+  __shared__ unsigned long long cs[NG][CNT_STRIDE];
+  const bool fold = W.counters[CNT_CUM_FLAG] == 0ull;
+  if (threadIdx.x < 256) {
+    const int slot = threadIdx.x & (CNT_STRIDE - 1), g = threadIdx.x / CNT_STRIDE;
+    unsigned long long a = 0;
+    if (fold && slot != CNT_STRIDE - 1)
+      for (int sh = g; sh < NSHARD; sh += NG) a += W.counters[sh * CNT_STRIDE + slot];
+    cs[g][slot] = a;
+  }
+  __syncthreads();
+  if (threadIdx.x < CNT_STRIDE) {
+    unsigned long long t = 0;
+    for (int g = 0; g < NG; g++) t += cs[g][threadIdx.x];
+    if (threadIdx.x == CNT_STRIDE - 1) W.counters[CNT_CUM_FLAG] = 0ull;
+    else if (t) W.counters[CNT_CUM_BASE + threadIdx.x] += t;
+  }
   for (int i = threadIdx.x; i < NSHARD * CNT_STRIDE; i += blockDim.x) W.counters[i] = 0ull;
   if (threadIdx.x < 3) W.b_count[threadIdx.x] = 0;
   if (threadIdx.x < 8) W.class_count[threadIdx.x] = 0;
@@ -435,6 +456,7 @@ __global__ void k_allot(DevWorld W, const double* totals, uint32_t update) {
   if (c < W.n) {
     allot_cell(W, c, totals[0], totals[1], update, want, cls);
     occ_init_cell(W, c);   // as in k_allot_total (tiles re-initialise with their ghost rows)
+    W.claim_r[3][c] = 0ull;
   }
   const unsigned long long m = __ballot(want);
   if ((threadIdx.x & 63) == 0 && m) count_add(W, CNT_SLICES, (unsigned long long)__popcll(m));
@@ -491,6 +513,8 @@ __global__ __launch_bounds__(1024) void k_allot_total(DevWorld W, const double* 
       // cells are occupied; an organism that dies in its slice clears its
       // cell (interpret_chunk's write-back), and no birth lands before placement
       occ_init_cell(W, c);
+      // the previous update's round-3 claims (k_activate read them last)
+      W.claim_r[3][c] = 0ull;
     }
     const unsigned long long m = __ballot(want);
     if ((tid & 63) == 0 && m) count_add(W, CNT_SLICES, (unsigned long long)__popcll(m));
@@ -574,9 +598,14 @@ __global__ void k_occ_init(DevWorld W) {
 // claim / prev: this round's claim array and (single world) the previous
 // round's, whose entry at the record's last target is zeroed first -- the
 // rounds alternate between two arrays, so no clearing pass sits between them
+// occ_prev (fused single-world rounds, k_place_round): the previous round's
+// claim array -- a cell claimed there has a winner of that round, so it is
+// occupied for this round's pick whether or not that winner's resolve (in the
+// same launch) has marked occ yet; round: the claim's round (b_tgt row)
 __device__ __forceinline__ void place_pick_one(const DevWorld& W, int64_t i, unsigned long long* claim,
-                                               unsigned long long* prev) {
-  const int64_t r = rec_of(W, i);
+                                               unsigned long long* prev,
+                                               const unsigned long long* occ_prev = nullptr, int round = -1) {
+  const int64_t r = (round >= 0) ? i : rec_of(W, i);
   if (prev) {
     const int t0 = W.b_target[r];
     if (t0 >= 0) prev[t0] = 0ull;
@@ -588,7 +617,8 @@ __device__ __forceinline__ void place_pick_one(const DevWorld& W, int64_t i, uns
   int cand[9];
   int nc = 0;
   if (W.prefer_empty)
-    for (int k = 0; k < nn; k++) if (!W.occ[nbr[k]]) cand[nc++] = nbr[k];
+    for (int k = 0; k < nn; k++)
+      if (!W.occ[nbr[k]] && !(occ_prev && occ_prev[nbr[k]] != 0ull)) cand[nc++] = nbr[k];
   if (nc == 0 && W.birth_method != 3) {
     for (int k = 0; k < nn; k++) cand[nc++] = nbr[k];
     if (W.allow_parent) cand[nc++] = parent;
@@ -605,21 +635,8 @@ __device__ __forceinline__ void place_pick_one(const DevWorld& W, int64_t i, uns
   W.b_rng[2 * W.rcap + r] = ctr;
   W.b_target[r] = t;
   W.b_prio[r] = prio;
+  if (round >= 0) W.b_tgt[(int64_t)round * W.rcap + r] = t;
   atomicMax(&claim[t], prio);
-}
-
-// which: 0 every target, 1 targets inside the tile, 2 ghost-row targets
-__device__ __forceinline__ void place_resolve_one(const DevWorld& W, int64_t i, int round, int which,
-                                                  const unsigned long long* claim) {
-  const int64_t r = rec_of(W, i);
-  if (W.b_state[r] != 0) return;
-  const int t = W.b_target[r];
-  if ((which == 1 && t >= W.n) || (which == 2 && t < W.n)) return;
-  if (claim[t] == W.b_prio[r]) {
-    W.b_state[r] = (int8_t)(1 + round);
-    W.occ[t] = 1;
-    W.owner[t] = (int)r;
-  }
 }
 
 // divide-mutation scan: queue entries per wave (k_apply_mutations, k_place_pick_mut)
@@ -631,16 +648,44 @@ __device__ __forceinline__ void place_resolve_one(const DevWorld& W, int64_t i, 
 __global__ void k_place_pick(DevWorld W, unsigned long long* claim, unsigned long long* prev) {
   QUEUE_LOOP(i) place_pick_one(W, i, claim, prev);
 }
+// A single world's placement round m = 1..3 in one launch: the resolve of
+// round m-1 and the pick of round m.  Each round has its own claim array
+// (W.claim_r[m]), so round m-1's claims stay intact for the whole launch: a
+// record that won round m-1 takes its cell (occ, owner); one that lost picks
+// again, treating every cell claimed in round m-1 as occupied -- exactly the
+// occupancy the separate resolve launch would have left (every claimed cell
+// has a winner), so the result is the unfused pick / resolve pair's
+// (oracle run_update_impl) at half the launches.
+__global__ void k_place_round(DevWorld W, int m) {
+  const unsigned long long* prev = W.claim_r[m - 1];
+  unsigned long long* cur = W.claim_r[m];
+  QUEUE_LOOP(q) {
+    const int64_t r = rec_of(W, q);
+    if (W.b_state[r] != 0) continue;
+    const int t = W.b_target[r];
+    if (prev[t] == W.b_prio[r]) {              // won round m-1
+      W.b_state[r] = (int8_t)m;
+      W.occ[t] = 1;
+      W.owner[t] = (int)r;
+      continue;
+    }
+    place_pick_one(W, r, cur, nullptr, prev, m);
+  }
+}
 // Round 0 of a single world's placement with the divide mutations beside it:
 // blocks [0, pblocks) pick; the rest apply the edits (as k_apply_mutations,
 // 4 waves per block) -- placement reads no genome, so the two are independent
 // and share one launch instead of two latency-bound ones.
-__global__ __launch_bounds__(256) void k_place_pick_mut(DevWorld W, unsigned long long* claim, int pblocks) {
+// fused: the single world's round arrays (claim rows and b_tgt, k_place_round)
+__global__ __launch_bounds__(256) void k_place_pick_mut(DevWorld W, unsigned long long* claim, int pblocks,
+                                                        int fused) {
   __shared__ uint8_t child[4][TAPE_SLOT + 16];
   const int nb = queue_len(W);
   if ((int)blockIdx.x < pblocks) {
-    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < nb; i += (int64_t)pblocks * 256)
-      place_pick_one(W, i, claim, nullptr);
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < nb; i += (int64_t)pblocks * 256) {
+      if (fused) place_pick_one(W, rec_of(W, i), claim, nullptr, nullptr, 0);
+      else place_pick_one(W, i, claim, nullptr);
+    }
     return;
   }
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -664,16 +709,6 @@ __global__ __launch_bounds__(256) void k_place_pick_mut(DevWorld W, unsigned lon
     }
   }
 }
-__global__ void k_place_resolve(DevWorld W, int round, int which, const unsigned long long* claim) {
-  QUEUE_LOOP(i) place_resolve_one(W, i, round, which, claim);
-}
-__global__ void k_place_clear(DevWorld W) {
-  QUEUE_LOOP(i) {
-    const int t = W.b_target[rec_of(W, i)];
-    if (t >= 0) W.claim[t] = 0ull;
-  }
-}
-
 // ---- strip-tile halo (DESIGN.md "Multi-GPU") ----
 // Edge rows: top = local row 0, bottom = local row rows-1; ghost rows after n.
 __device__ __forceinline__ int64_t edge_cell(const DevWorld& W, int d, int x) {
@@ -682,58 +717,116 @@ __device__ __forceinline__ int64_t edge_cell(const DevWorld& W, int d, int x) {
 __device__ __forceinline__ int64_t ghost_cell(const DevWorld& W, int d, int x) {
   return W.n + (int64_t)d * W.world_x + x;
 }
+// Halo buffer (one per direction): [X u64] the sender's claims on the
+// receiver's edge row (its ghost row), [X u64] the sender's own claims on its
+// edge row (the receiver's ghost row), [X u8] the sender's edge-row occupancy.
+// A cell of an edge row is claimed only from the two strips it touches, so
+// after ONE exchange per placement round both strips know every claim on
+// both rows and resolve them alike (DESIGN.md "Multi-GPU").
 __device__ __forceinline__ unsigned long long* halo_claims(uint8_t* b) {
   return reinterpret_cast<unsigned long long*>(b);
 }
-__device__ __forceinline__ uint8_t* halo_occ(uint8_t* b, int X) { return b + (int64_t)X * 8; }
+__device__ __forceinline__ unsigned long long* halo_own(uint8_t* b, int X) {
+  return reinterpret_cast<unsigned long long*>(b) + X;
+}
+__device__ __forceinline__ uint8_t* halo_occ(uint8_t* b, int X) { return b + (int64_t)X * 16; }
 
-// what: 0 edge-row occupancy; 1 ghost-row claims; 2 merged edge-row claims + occupancy
+// what: 0 edge-row occupancy (after interpretation); 1 this round's claims
+// (on the ghost rows, on the own edge rows)
 __global__ void k_halo_export(DevWorld W, int what) {
   const int X = W.world_x;
   const int g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= 2 * X) return;
   const int d = g / X, x = g - d * X;
   uint8_t* b = W.h_send[d];
+  const int64_t c = edge_cell(W, d, x);
   if (what == 1) {
     halo_claims(b)[x] = W.claim[ghost_cell(W, d, x)];
+    halo_own(b, X)[x] = W.claim[c];
   } else {
-    const int64_t c = edge_cell(W, d, x);
     halo_occ(b, X)[x] = W.occ[c];
-    halo_claims(b)[x] = what == 2 ? W.claim[c] : 0ull;
+    halo_claims(b)[x] = 0ull;
+    halo_own(b, X)[x] = 0ull;
   }
 }
 
-// what 0: ghost occupancy from the neighbours' edge rows (before round 0);
-// what 1: merge the neighbours' claims on my edge rows and mark the cells a
-//         halo birth won (unique maximum priority) this round;
-// what 2: ghost rows take the neighbours' merged claims and occupancy.
-__global__ void k_halo_import(DevWorld W, int what, int round) {
+// ghost occupancy from the neighbours' edge rows (before round 0's pick)
+__global__ void k_halo_import_occ(DevWorld W) {
   const int X = W.world_x;
   const int g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= 2 * X) return;
   const int d = g / X, x = g - d * X;
-  uint8_t* b = W.h_recv[d];
-  if (what == 0) {
-    W.occ[ghost_cell(W, d, x)] = halo_occ(b, X)[x];
-  } else if (what == 1) {
-    const int64_t c = edge_cell(W, d, x);
-    const unsigned long long rc = halo_claims(b)[x];
-    unsigned long long m = W.claim[c];
-    if (rc > m) m = rc;
-    W.claim[c] = m;
-    if (rc != 0ull && m == rc) { W.owner[c] = REMOTE_OWNER(round); W.occ[c] = 1; }
-  } else {
-    const int64_t c = ghost_cell(W, d, x);
-    W.claim[c] = halo_claims(b)[x];
-    W.occ[c] = halo_occ(b, X)[x];
-  }
+  W.occ[ghost_cell(W, d, x)] = halo_occ(W.h_recv[d], X)[x];
 }
 
-// claims on the edge rows and ghost rows are cleared wholesale (remote
-// records claim there without being in this tile's queue)
-__global__ void k_halo_clear(DevWorld W) {
+// the claim of the round on cell t with the neighbours' claims merged in
+__device__ __forceinline__ unsigned long long merged_claim(const DevWorld& W, int64_t t) {
+  unsigned long long m = W.claim[t];
   const int X = W.world_x;
-  const int g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= W.n) {
+    const int64_t k = t - W.n;
+    const int d = (int)(k / X);
+    const unsigned long long o = halo_own(W.h_recv[d], X)[k - (int64_t)d * X];
+    return o > m ? o : m;
+  }
+  int d = -1, x = 0;
+  if (t < X) { d = 0; x = (int)t; }
+  else if (t >= W.n - X) { d = 1; x = (int)(t - (W.n - X)); }
+  if (d >= 0) {
+    const unsigned long long r = halo_claims(W.h_recv[d])[x];
+    if (r > m) m = r;
+  }
+  return m;
+}
+
+// One launch per placement round after its exchange: blocks [0, rblocks)
+// resolve this tile's records (targets inside the tile and on the ghost rows)
+// against the merged claims; the rest walk the 2 x X halo cells: an edge cell
+// whose maximum claim came from the neighbour is that round's remote winner's
+// (owner REMOTE_OWNER(round), occupied), a ghost cell with any claim is
+// occupied for the next round's pick (its winner is placed, here or there).
+__global__ void k_tile_resolve(DevWorld W, int round, int rblocks) {
+  if ((int)blockIdx.x < rblocks) {
+    const int nb = queue_len(W);
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nb;
+         i += (int64_t)rblocks * blockDim.x) {
+      const int64_t r = rec_of(W, i);
+      if (W.b_state[r] != 0) continue;
+      const int t = W.b_target[r];
+      if (merged_claim(W, t) == W.b_prio[r]) {
+        W.b_state[r] = (int8_t)(1 + round);
+        W.occ[t] = 1;
+        W.owner[t] = (int)r;
+      }
+    }
+    return;
+  }
+  const int X = W.world_x;
+  const int g = (blockIdx.x - rblocks) * blockDim.x + threadIdx.x;
+  if (g >= 2 * X) return;
+  const int d = g / X, x = g - d * X;
+  const int64_t c = edge_cell(W, d, x);
+  const unsigned long long rc = halo_claims(W.h_recv[d])[x];
+  if (rc != 0ull && rc > W.claim[c]) { W.owner[c] = REMOTE_OWNER(round); W.occ[c] = 1; }
+  const int64_t gc = ghost_cell(W, d, x);
+  if (W.claim[gc] != 0ull || halo_own(W.h_recv[d], X)[x] != 0ull) W.occ[gc] = 1;
+}
+
+// The round's claims cleared: blocks [0, rblocks) at this tile's records'
+// targets, the rest on the edge and ghost rows wholesale (remote records
+// claim there without being in this tile's queue).
+__global__ void k_tile_clear(DevWorld W, int rblocks) {
+  if ((int)blockIdx.x < rblocks) {
+    const int nb = queue_len(W);
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nb;
+         i += (int64_t)rblocks * blockDim.x) {
+      const int t = W.b_target[rec_of(W, i)];
+      if (t >= 0) W.claim[t] = 0ull;
+    }
+    return;
+  }
+  const int X = W.world_x;
+  const int g = (blockIdx.x - rblocks) * blockDim.x + threadIdx.x;
   if (g >= 2 * X) return;
   const int d = g / X, x = g - d * X;
   W.claim[edge_cell(W, d, x)] = 0ull;
@@ -783,7 +876,13 @@ __global__ __launch_bounds__(64) void k_apply_mutations(DevWorld W) {
 // earlier newborn.  So a birth either owns its cell at the update's end
 // (CNT_BIRTHS) or was placed and overwritten (CNT_OVERWRITTEN) -- never
 // "not placed".
-__global__ __launch_bounds__(64) void k_activate(DevWorld W, unsigned long long* last) {
+//
+// fused (single world, k_place_round): the resolve of round 3 happens here --
+// a record that won round 3 owns its cell; one that won an earlier round owns
+// it unless a round-3 claim landed there (claim_r[3] != 0: that claim's winner
+// is placed later and owns it).  Rounds 0-2's claims are cleared here by each
+// record; round 3's, which this launch reads, by k_stats_partial.
+__global__ __launch_bounds__(64) void k_activate(DevWorld W, unsigned long long* last, int fused) {
   const int nb = queue_len(W);
   unsigned long long born = 0, over = 0;
   for (int64_t q = (int64_t)blockIdx.x * 64 + threadIdx.x; q < nb; q += (int64_t)gridDim.x * 64) {
@@ -792,7 +891,20 @@ __global__ __launch_bounds__(64) void k_activate(DevWorld W, unsigned long long*
     const int8_t st = W.b_state[i];
     const Child b = child_of_record(W, i);
     if (last && tgt >= 0) last[tgt] = 0ull;
-    const bool won = st > 0 && tgt >= 0 && W.owner[tgt] == (int)i;
+    bool won;
+    if (fused) {
+      const unsigned long long c3 = tgt >= 0 ? W.claim_r[3][tgt] : 0ull;
+      if (st == 0) won = tgt >= 0 && c3 == W.b_prio[i];   // round 3's winner
+      else won = W.owner[tgt] == (int)i && c3 == 0ull;
+      const int lastr = st == 0 ? 3 : st - 1;              // the last round it claimed in
+      for (int k = 0; k < lastr && k < 3; k++) {
+        const int tk = W.b_tgt[(int64_t)k * W.rcap + i];
+        if (tk >= 0) W.claim_r[k][tk] = 0ull;
+      }
+      if (lastr < 3) W.claim_r[lastr][tgt] = 0ull;
+    } else {
+      won = st > 0 && tgt >= 0 && W.owner[tgt] == (int)i;
+    }
     if (won && tgt >= W.n) continue;          // sent to the neighbouring tile
     if (!won) { over++; continue; }
     born++;
@@ -994,11 +1106,16 @@ __global__ __launch_bounds__(256) void k_stats_final(DevWorld W, const double* p
     cs[g][slot] = a;
   }
   __syncthreads();
+  // the running sums take this update's counts once: here, or (statistics
+  // never asked for) in the next reset_counts_block
+  const bool fold = W.counters[CNT_CUM_FLAG] == 0ull;
+  __syncthreads();
   if (tid < CNT_STRIDE) {
     unsigned long long t = 0;
     for (int g = 0; g < NG; g++) t += cs[g][tid];
     cs[0][tid] = t;
-    W.counters[CNT_CUM_BASE + tid] += t;
+    if (tid == CNT_STRIDE - 1) W.counters[CNT_CUM_FLAG] = 1ull;
+    else if (fold) W.counters[CNT_CUM_BASE + tid] += t;
   }
   __syncthreads();
   if (tid == 0) {
@@ -1101,7 +1218,7 @@ void launch_world_pre(const DevWorld& W, hipStream_t s, const double* totals, hi
   hipLaunchKernelGGL(k_window_count, dim3(nblk(W.n, SORT_WIN)), dim3(1024), 0, s, W);
 }
 
-static void launch_stats(const DevWorld& W, hipStream_t s, double* stats) {
+void launch_stats(const DevWorld& W, hipStream_t s, double* stats) {
   const int64_t nb = (W.n + 255) / 256;
   double* part = stats + NSTAT;
   hipLaunchKernelGGL(k_stats_partial, dim3((unsigned)nb), dim3(256), 0, s, W, part);
@@ -1151,23 +1268,19 @@ void launch_reset_counts(const DevWorld& W, hipStream_t s) {
 // Placement rounds alternate between the claim arrays claim / claim2 (round k
 // claims into array k & 1 after zeroing its records' round k-1 claims; the
 // last round's are zeroed by k_activate): no clearing launch per round.
-void launch_world_post(const DevWorld& W, hipStream_t s, double* stats) {
+void launch_world_post(const DevWorld& W, hipStream_t s, double* stats, bool eager) {
   // the occupancy was initialised by k_allot_total; the divide mutations
   // ride in round 0's pick launch
   launch_resources_end(W, s);
+  // round 0's pick (with the divide mutations beside it), then three launches
+  // of resolve(m-1) + pick(m), then activation with round 3's resolve: 5
+  // launches instead of 9 (k_place_round)
   const unsigned bb = place_grid(W);
-  unsigned long long* buf[2] = {W.claim, W.claim2};
-  for (int round = 0; round < 4; round++) {
-    if (round == 0 && has_divide_mutations(W))
-      hipLaunchKernelGGL(k_place_pick_mut, dim3(bb + (mut_grid(W) + 3) / 4), dim3(256), 0, s, W, buf[0], (int)bb);
-    else
-      hipLaunchKernelGGL(k_place_pick, dim3(bb), dim3(256), 0, s, W, buf[round & 1],
-                         round ? buf[(round - 1) & 1] : (unsigned long long*)nullptr);
-    hipLaunchKernelGGL(k_place_resolve, dim3(bb), dim3(256), 0, s, W, round, 0,
-                       (const unsigned long long*)buf[round & 1]);
-  }
-  hipLaunchKernelGGL(k_activate, dim3(lane_grid(W)), dim3(64), 0, s, W, buf[1]);
-  launch_stats(W, s, stats);
+  const int pm = has_divide_mutations(W) ? (int)((mut_grid(W) + 3) / 4) : 0;
+  hipLaunchKernelGGL(k_place_pick_mut, dim3(bb + pm), dim3(256), 0, s, W, W.claim_r[0], (int)bb, 1);
+  for (int m = 1; m < 4; m++) hipLaunchKernelGGL(k_place_round, dim3(bb), dim3(256), 0, s, W, m);
+  hipLaunchKernelGGL(k_activate, dim3(lane_grid(W)), dim3(64), 0, s, W, (unsigned long long*)nullptr, 1);
+  if (eager) launch_stats(W, s, stats);
 }
 
 // ---- strip tiles: the same update split around the halo exchanges ----
@@ -1191,36 +1304,32 @@ void launch_tile_after_interpret(const DevWorld& W, hipStream_t s) {
   hipLaunchKernelGGL(k_halo_export, dim3(nblk(2 * (int64_t)W.world_x, 256)), dim3(256), 0, s, W, 0);
 }
 
-// phase 0: (round 0: ghost occupancy in) pick, ghost claims out
-// phase 1: neighbours' claims merged in, resolve inside the tile, edge rows out
-// phase 2: ghost rows in, resolve ghost targets, clear claims
-// phase 3: pack the ghost-row winners into the record buffers
+// phase 0: (round 0: ghost occupancy in) pick, the round's claims out
+// phase 1: (after the exchange) resolve against the merged claims, clear them
+// phase 2: (round 3) pack the ghost-row winners into the record buffers
+// phase 3: (round 3) activate this tile's own winners -- while the records
+//          travel; avgpu_tile_finish then activates the received ones
 void launch_tile_place(const DevWorld& W, hipStream_t s, int round, int phase) {
   const unsigned bb = place_grid(W);
   const unsigned hb = nblk(2 * (int64_t)W.world_x, 256);
   if (phase == 0) {
-    if (round == 0) hipLaunchKernelGGL(k_halo_import, dim3(hb), dim3(256), 0, s, W, 0, round);
+    if (round == 0) hipLaunchKernelGGL(k_halo_import_occ, dim3(hb), dim3(256), 0, s, W);
     hipLaunchKernelGGL(k_place_pick, dim3(bb), dim3(256), 0, s, W, W.claim, (unsigned long long*)nullptr);
     hipLaunchKernelGGL(k_halo_export, dim3(hb), dim3(256), 0, s, W, 1);
   } else if (phase == 1) {
-    hipLaunchKernelGGL(k_halo_import, dim3(hb), dim3(256), 0, s, W, 1, round);
-    hipLaunchKernelGGL(k_place_resolve, dim3(bb), dim3(256), 0, s, W, round, 1, (const unsigned long long*)W.claim);
-    hipLaunchKernelGGL(k_halo_export, dim3(hb), dim3(256), 0, s, W, 2);
+    hipLaunchKernelGGL(k_tile_resolve, dim3(bb + hb), dim3(256), 0, s, W, round, (int)bb);
+    hipLaunchKernelGGL(k_tile_clear, dim3(bb + hb), dim3(256), 0, s, W, (int)bb);
   } else if (phase == 2) {
-    hipLaunchKernelGGL(k_halo_import, dim3(hb), dim3(256), 0, s, W, 2, round);
-    hipLaunchKernelGGL(k_place_resolve, dim3(bb), dim3(256), 0, s, W, round, 2, (const unsigned long long*)W.claim);
-    hipLaunchKernelGGL(k_place_clear, dim3(bb), dim3(256), 0, s, W);
-    hipLaunchKernelGGL(k_halo_clear, dim3(hb), dim3(256), 0, s, W);
-  } else {
     for (int d = 0; d < 2; d++) hipMemsetAsync(W.r_send[d], 0, sizeof(HaloHdr), s);
     hipLaunchKernelGGL(k_halo_pack, dim3(activate_grid(W)), dim3(64), 0, s, W);
+  } else {
+    hipLaunchKernelGGL(k_activate, dim3(lane_grid(W)), dim3(64), 0, s, W, (unsigned long long*)nullptr, 0);
   }
 }
 
-void launch_tile_finish(const DevWorld& W, hipStream_t s, double* stats) {
-  hipLaunchKernelGGL(k_activate, dim3(lane_grid(W)), dim3(64), 0, s, W, (unsigned long long*)nullptr);
+void launch_tile_finish(const DevWorld& W, hipStream_t s, double* stats, bool eager) {
   for (int d = 0; d < 2; d++)
     hipLaunchKernelGGL(k_activate_remote, dim3((unsigned)std::max(1, std::min(W.world_x, 4096))), dim3(64),
                        0, s, W, d);
-  launch_stats(W, s, stats);
+  if (eager) launch_stats(W, s, stats);
 }

@@ -213,6 +213,10 @@ struct Transport {
   virtual ~Transport() = default;
   virtual void all_gather(std::vector<Tile>& t, hipStream_t s) = 0;
   virtual void exchange(std::vector<Tile>& t, Kind k, hipStream_t s) = 0;
+  // an exchange the stream's next kernels run beside: issued by
+  // exchange_begin, joined into s by exchange_end
+  virtual void exchange_begin(std::vector<Tile>& t, Kind k, hipStream_t s) { exchange(t, k, s); }
+  virtual void exchange_end(hipStream_t s) {}
   virtual void all_reduce_sum(std::vector<Tile>& t, hipStream_t s) = 0;
 };
 
@@ -259,7 +263,25 @@ struct Loopback : Transport {
 struct Rccl : Transport {
   ncclComm_t comm;
   int rank, world;
-  Rccl(ncclComm_t c, int r, int w) : comm(c), rank(r), world(w) {}
+  hipStream_t side = nullptr;           // the overlapped exchange's stream
+  hipEvent_t issued = nullptr, done = nullptr;
+  Rccl(ncclComm_t c, int r, int w) : comm(c), rank(r), world(w) {
+    HIP_OK(hipStreamCreateWithFlags(&side, hipStreamNonBlocking));
+    HIP_OK(hipEventCreateWithFlags(&issued, hipEventDisableTiming));
+    HIP_OK(hipEventCreateWithFlags(&done, hipEventDisableTiming));
+  }
+  ~Rccl() override {
+    hipEventDestroy(issued);
+    hipEventDestroy(done);
+    hipStreamDestroy(side);
+  }
+  void exchange_begin(std::vector<Tile>& t, Kind k, hipStream_t s) override {
+    HIP_OK(hipEventRecord(issued, s));
+    HIP_OK(hipStreamWaitEvent(side, issued, 0));
+    exchange(t, k, side);
+    HIP_OK(hipEventRecord(done, side));
+  }
+  void exchange_end(hipStream_t s) override { HIP_OK(hipStreamWaitEvent(s, done, 0)); }
   void all_gather(std::vector<Tile>& t, hipStream_t s) override {
     NCCL_OK(ncclAllGather(t[0].part, t[0].gathered, t[0].n_part, ncclFloat64, comm, s));
   }
@@ -325,15 +347,16 @@ void update(std::vector<Tile>& tiles, Transport& tr, hipStream_t s) {
   if (tiles[0].res_bytes > 0) tr.exchange(tiles, Kind::Resources, s);
   for (Tile& t : tiles) AV_OK(avgpu_tile_begin(t.h, t.gathered, ntiles_total));
   tr.exchange(tiles, Kind::Halo, s);
+  // one exchange per placement round (both strips resolve each edge cell alike)
   for (int rnd = 0; rnd < 4; rnd++) {
-    for (int phase = 0; phase < 2; phase++) {
-      for (Tile& t : tiles) AV_OK(avgpu_tile_place(t.h, rnd, phase));
-      tr.exchange(tiles, Kind::Halo, s);
-    }
-    for (Tile& t : tiles) AV_OK(avgpu_tile_place(t.h, rnd, 2));
+    for (Tile& t : tiles) AV_OK(avgpu_tile_place(t.h, rnd, 0));
+    tr.exchange(tiles, Kind::Halo, s);
+    for (Tile& t : tiles) AV_OK(avgpu_tile_place(t.h, rnd, 1));
   }
-  for (Tile& t : tiles) AV_OK(avgpu_tile_place(t.h, 3, 3));
-  tr.exchange(tiles, Kind::Records, s);
+  for (Tile& t : tiles) AV_OK(avgpu_tile_place(t.h, 3, 2));
+  tr.exchange_begin(tiles, Kind::Records, s);
+  for (Tile& t : tiles) AV_OK(avgpu_tile_place(t.h, 3, 3));   // own winners, beside the exchange
+  tr.exchange_end(s);
   for (Tile& t : tiles) AV_OK(avgpu_tile_finish(t.h, nullptr));
   int pools = 0;
   for (Tile& t : tiles) pools = avgpu_tile_res_cons(t.h, t.cons);

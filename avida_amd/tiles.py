@@ -10,8 +10,9 @@ tiled world equals the same update of the untiled world cell for cell
 include/avida_gpu.h ("strip tiles"):
 
     tile_partials -> all_gather -> tile_begin -> exchange(halo)
-    4 x [tile_place(r,0) -> exchange(halo) -> tile_place(r,1) -> exchange(halo) -> tile_place(r,2)]
-    tile_place(3,3) -> exchange(records) -> tile_finish
+    4 x [tile_place(r,0) -> exchange(halo) -> tile_place(r,1)]
+    tile_place(3,2) -> exchange(records) issued -> tile_place(3,3) (own
+    winners, while the records travel) -> wait(records) -> tile_finish
     with resources: exchange(resources) after the all_gather (edge rows of
     the spatial grids), all_reduce(consumption) + tile_res_settle at the end
 
@@ -91,6 +92,12 @@ class LoopbackTransport:
         for t in tiles:
             t.gathered.copy_(full)
 
+    def exchange_start(self, tiles, kind):
+        self.exchange(tiles, kind)
+
+    def exchange_wait(self, pending):
+        pass
+
     def exchange(self, tiles, kind):
         T = len(tiles)
         for i, t in enumerate(tiles):
@@ -129,6 +136,15 @@ class DistTransport:
         self.dist.all_reduce(t.cons, group=self.group)   # int64 sum == the uint64 sum mod 2^64
 
     def exchange(self, tiles, kind):
+        self.exchange_wait(self.exchange_start(tiles, kind))
+
+    def exchange_wait(self, pending):
+        for w in pending:
+            w.wait()
+
+    def exchange_start(self, tiles, kind):
+        """issue the neighbour exchange; the returned works are waited by
+        exchange_wait (on "nccl": kernels launched in between run beside it)"""
         (t,) = tiles
         send, recv = (getattr(t, n) for n in _buffers(kind))
         up = (self.rank - 1) % self.world
@@ -140,8 +156,7 @@ class DistTransport:
         # with the receive of the same edge.
         ops = [d.P2POp(d.isend, send[0], up, self.group), d.P2POp(d.isend, send[1], down, self.group),
                d.P2POp(d.irecv, recv[1], down, self.group), d.P2POp(d.irecv, recv[0], up, self.group)]
-        for w in d.batch_isend_irecv(ops):
-            w.wait()
+        return d.batch_isend_irecv(ops)
 
 
 class StripWorld:
@@ -162,16 +177,20 @@ class StripWorld:
         for t in tiles:
             t.call("tile_begin", C.c_void_p(t.gathered.data_ptr()), t.ntiles)
         self.tr.exchange(tiles, "halo")
+        # one exchange per placement round: the claims on both sides of each
+        # strip edge, resolved alike by the two strips
         for rnd in range(4):
-            for phase in (0, 1):
-                for t in tiles:
-                    t.call("tile_place", rnd, phase)
-                self.tr.exchange(tiles, "halo")
             for t in tiles:
-                t.call("tile_place", rnd, 2)
+                t.call("tile_place", rnd, 0)
+            self.tr.exchange(tiles, "halo")
+            for t in tiles:
+                t.call("tile_place", rnd, 1)
         for t in tiles:
-            t.call("tile_place", 3, 3)
-        self.tr.exchange(tiles, "records")
+            t.call("tile_place", 3, 2)
+        pending = self.tr.exchange_start(tiles, "records")
+        for t in tiles:
+            t.call("tile_place", 3, 3)     # this strip's own winners, beside the exchange
+        self.tr.exchange_wait(pending)
         for t in tiles:
             t.call("tile_finish", None)
         pools = [t.call("tile_res_cons", C.c_void_p(t.cons.data_ptr())) for t in tiles]

@@ -403,7 +403,9 @@ int avgpu_step(avgpu_world* w, int64_t first_cell, int64_t count,
 /* One whole update of Avida2Driver::Run (targets/avida/Avida2Driver.cc:91-163):
  * merit-weighted allotment of AVE_TIME_SLICE*N instructions (cScheduler),
  * interpretation, birth placement (cPopulation::PositionOffspring,
- * main/cPopulation.cc:5185-5414), statistics. out may be NULL (no host sync). */
+ * main/cPopulation.cc:5185-5414), statistics. out may be NULL: no host sync,
+ * and the update's statistics reduction is skipped until avgpu_get_stats /
+ * avgpu_stats_vector asks for it (cumulative counters stay exact either way). */
 int avgpu_run_update(avgpu_world* w, avgpu_update_stats* out);
 int avgpu_run_updates(avgpu_world* w, int n_updates, avgpu_update_stats* last);
 /* The serial world: n_updates updates under the reference's own schedule
@@ -535,6 +537,7 @@ int avgpu_test_genomes(avgpu_world* w, int n, const uint8_t* genomes, const int3
                        uint8_t* offspring);
 
 /* ---- statistics / multi-GPU plumbing ------------------------------------ */
+/* the last update's statistics (reduced here if that update ran with out == NULL) */
 int avgpu_get_stats(avgpu_world* w, avgpu_update_stats* out);
 /* device pointer of the 32-double reduction vector of the last update
  * (N, sum merit, executed, births, ...) for an external all-reduce
@@ -559,9 +562,10 @@ int avgpu_set_global_totals(avgpu_world* w, double total_merit, int64_t total_or
  *   avgpu_tile_begin(w, gathered, T)     exchange(halo)
  *   for round 0..3:
  *     avgpu_tile_place(w, round, 0)      exchange(halo)
- *     avgpu_tile_place(w, round, 1)      exchange(halo)
- *     avgpu_tile_place(w, round, 2)
- *   avgpu_tile_place(w, 3, 3)            exchange(records)
+ *     avgpu_tile_place(w, round, 1)
+ *   avgpu_tile_place(w, 3, 2)            exchange(records) issued ...
+ *   avgpu_tile_place(w, 3, 3)            ... and running beside this launch
+ *                                        wait(records)
  *   avgpu_tile_finish(w, stats)
  *   [avgpu_tile_res_cons(w, cons)        all_reduce(cons, sum): global pools,
  *    avgpu_tile_res_settle(w, cons)      when avgpu_tile_res_cons returned > 0]
@@ -587,9 +591,16 @@ int avgpu_tile_partials(avgpu_world* w, double* dev_out);
 /* global totals from the gathered partials (T x partials, tile order), then
  * allotment + interpretation of this tile, occupancy of its edge rows out */
 int avgpu_tile_begin(avgpu_world* w, const double* dev_gathered, int ntiles);
-/* placement round 0..3, phase 0..2; phase 3 packs the halo birth records */
+/* placement round 0..3: phase 0 picks and writes the round's claims (on the
+ * ghost rows and on the own edge rows) into the halo send buffers; phase 1,
+ * after the exchange, resolves every claim on this tile's cells and ghost
+ * rows (a cell of an edge row is claimed only from the two strips it touches,
+ * so both resolve it alike).  After round 3: phase 2 packs the ghost-row
+ * winners into the record buffers, phase 3 activates this tile's own winners
+ * (it reads no record buffer: it may run while the records travel). */
 int avgpu_tile_place(avgpu_world* w, int round, int phase);
-/* activation of this tile's winners and of the received records, statistics */
+/* activation of the received records; statistics (out may be NULL: see
+ * avgpu_run_update) */
 int avgpu_tile_finish(avgpu_world* w, avgpu_update_stats* out);
 /* spatial resources on strips: bytes of one resource-row buffer (n_spatial x
  * world_x doubles, 0 without spatial resources) and the 4 device buffers

@@ -285,6 +285,7 @@ struct World {
   int64_t t_oversize = 0;   // offspring longer than AVGPU_MAX_GENOME after a slip (dropped at the divide)
   int64_t t_memcap = 0;     // copy insertions past AVGPU_MAX_GENOME sites / removals from one site (skipped)
   int64_t t_overwritten = 0;   // offspring placed, then killed by a later birth into the same cell
+  int64_t t_placed = 0;        // strip tiles: this tile's own winners activated (avgpu_tile_place(3, 3))
   // resources (avgpu_load_resources): literal restatement of cResourceCount /
   // cSpatialResCount, stepped once per update
   std::vector<avgpu_resource> res;
@@ -1921,8 +1922,12 @@ int orc_set_global_totals(void* h, double merit, int64_t orgs) {
 // ---------------------------------------------------------------------------
 // Strip tiles (include/avida_gpu.h "strip tiles"; DESIGN.md "Multi-GPU"): the
 // same update as run_update_impl, split around the halo exchanges the host
-// performs.  Buffer layouts are the device's: halo = X u64 claims then X u8
-// occupancy flags; records = HaloHdr, X HaloRec, genome arena.
+// performs.  Buffer layouts are the device's: halo = X u64 claims on the
+// receiver's edge row, X u64 the sender's own claims on its edge row, X u8
+// edge-row occupancy; records = HaloHdr, X HaloRec, genome arena.  A cell of
+// an edge row is claimed only from the two strips it touches, so one exchange
+// per placement round gives both strips every claim on it: each resolves the
+// cell alike (the neighbour's own claims merged into the ghost row).
 namespace {
 struct HaloHdr { int32_t count, arena_used, overflow, pad; };
 struct HaloRec {
@@ -1933,9 +1938,10 @@ struct HaloRec {
   int32_t last_task[AVGPU_NUM_LOGIC_TASKS], pad2[3];
 };
 static_assert(sizeof(HaloRec) == 112, "HaloRec layout");
-int64_t halo_bytes_of(int x) { return ((int64_t)x * 9 + 15) / 16 * 16; }
+int64_t halo_bytes_of(int x) { return ((int64_t)x * 17 + 15) / 16 * 16; }
 uint64_t* hclaims(uint8_t* b) { return reinterpret_cast<uint64_t*>(b); }
-uint8_t* hocc(uint8_t* b, int x) { return b + (int64_t)x * 8; }
+uint64_t* hown(uint8_t* b, int x) { return reinterpret_cast<uint64_t*>(b) + x; }
+uint8_t* hocc(uint8_t* b, int x) { return b + (int64_t)x * 16; }
 int64_t edge_cell(const World& w, int d, int x) { return d == 0 ? x : (w.rows - 1) * w.cfg.world_x + x; }
 int64_t ghost_cell(const World& w, int d, int x) { return w.ncells + (int64_t)d * w.cfg.world_x + x; }
 bool tile_ok(World& w) { return w.tiled && w.h_send[0] && w.r_recv[1]; }
@@ -2075,13 +2081,17 @@ int orc_tile_begin(void* h, const double* gathered, int ntiles) {
     for (int x = 0; x < X; x++) {
       hocc(w.h_send[d], X)[x] = w.occ[edge_cell(w, d, x)];
       hclaims(w.h_send[d])[x] = 0;
+      hown(w.h_send[d], X)[x] = 0;
     }
+  w.t_placed = 0; w.t_overwritten = 0;
   return 0;
 }
 
 int orc_tile_place(void* h, int round, int phase) {
   World& w = *(World*)h;
   if (!tile_ok(w)) return fail(AVGPU_ESTATE, "not a strip tile with buffers");
+  if (round < 0 || round > 3 || phase < 0 || phase > 3 || (phase >= 2 && round != 3))
+    return fail(AVGPU_EINVAL, "round 0..3 with phase 0..1; phases 2, 3 after round 3");
   const int X = w.cfg.world_x;
   const int64_t nbirth = (int64_t)w.births.size();
   if (phase == 0) {
@@ -2091,43 +2101,42 @@ int orc_tile_place(void* h, int round, int phase) {
     for (int64_t i = 0; i < nbirth; i++)
       if (w.bstate[i] == 0) place_pick(w, i, w.occ, w.claim, w.prio, w.bstate);
     for (int d = 0; d < 2; d++)
-      for (int x = 0; x < X; x++) hclaims(w.h_send[d])[x] = w.claim[ghost_cell(w, d, x)];
+      for (int x = 0; x < X; x++) {
+        hclaims(w.h_send[d])[x] = w.claim[ghost_cell(w, d, x)];
+        hown(w.h_send[d], X)[x] = w.claim[edge_cell(w, d, x)];
+      }
   } else if (phase == 1) {
+    // merged claims: the neighbour's claims on my edge rows, its own claims on
+    // its edge rows (my ghost rows)
+    std::vector<uint64_t> merged(w.claim);
     for (int d = 0; d < 2; d++)
       for (int x = 0; x < X; x++) {
-        const int64_t c = edge_cell(w, d, x);
-        const uint64_t rc = hclaims(w.h_recv[d])[x];
-        if (rc > w.claim[c]) w.claim[c] = rc;
-        if (rc != 0 && w.claim[c] == rc) { w.owner[c] = -2 - round; w.occ[c] = 1; }
+        const int64_t c = edge_cell(w, d, x), g = ghost_cell(w, d, x);
+        const uint64_t rc = hclaims(w.h_recv[d])[x], oc = hown(w.h_recv[d], X)[x];
+        if (rc > merged[c]) { merged[c] = rc; w.owner[c] = -2 - round; w.occ[c] = 1; }
+        if (oc > merged[g]) merged[g] = oc;
+        if (merged[g] != 0) w.occ[g] = 1;     // its winner is placed, here or there
       }
     for (int64_t i = 0; i < nbirth; i++) {
-      if (w.bstate[i] != 0 || w.births[i].target >= w.ncells) continue;
+      if (w.bstate[i] != 0) continue;
       const int64_t t = w.births[i].target;
-      if (w.claim[t] == w.prio[i]) { w.bstate[i] = (int8_t)(1 + round); w.occ[t] = 1; w.owner[t] = i; }
+      if (merged[t] == w.prio[i]) { w.bstate[i] = (int8_t)(1 + round); w.occ[t] = 1; w.owner[t] = i; }
     }
-    for (int d = 0; d < 2; d++)
-      for (int x = 0; x < X; x++) {
-        const int64_t c = edge_cell(w, d, x);
-        hclaims(w.h_send[d])[x] = w.claim[c];
-        hocc(w.h_send[d], X)[x] = w.occ[c];
-      }
-  } else if (phase == 2) {
-    for (int d = 0; d < 2; d++)
-      for (int x = 0; x < X; x++) {
-        const int64_t c = ghost_cell(w, d, x);
-        w.claim[c] = hclaims(w.h_recv[d])[x];
-        w.occ[c] = hocc(w.h_recv[d], X)[x];
-      }
+    std::fill(w.claim.begin(), w.claim.end(), 0);
+  } else if (phase == 3) {
+    // this tile's own winners (the records travel meanwhile)
+    int64_t placed = 0, overwritten = 0;
     for (int64_t i = 0; i < nbirth; i++) {
-      if (w.bstate[i] != 0 || w.births[i].target < w.ncells) continue;
-      const int64_t t = w.births[i].target;
-      if (w.claim[t] == w.prio[i]) { w.bstate[i] = (int8_t)(1 + round); w.owner[t] = i; }
+      Birth& b = w.births[i];
+      const bool won = w.bstate[i] > 0 && b.target >= 0 && w.owner[b.target] == i;
+      if (won && b.target >= w.ncells) continue;   // shipped to the neighbour
+      if (won) { activate_child(w, b, b.target); placed++; }
+      else overwritten++;                          // placed, then overwritten (run_update_impl)
     }
-    for (int64_t i = 0; i < nbirth; i++) if (w.births[i].target >= 0) w.claim[w.births[i].target] = 0;
-    for (int d = 0; d < 2; d++)
-      for (int x = 0; x < X; x++) { w.claim[edge_cell(w, d, x)] = 0; w.claim[ghost_cell(w, d, x)] = 0; }
+    w.t_placed = placed;
+    w.t_overwritten = overwritten;
   } else {
-    // pack the last winner of every ghost cell (births in queue order)
+    // (phase 2) pack the last winner of every ghost cell (births in queue order)
     w.t_born = 0; w.t_dropped = 0;
     for (int d = 0; d < 2; d++) memset(w.r_send[d], 0, sizeof(HaloHdr));
     for (int64_t i = 0; i < nbirth; i++) {
@@ -2161,15 +2170,7 @@ int orc_tile_finish(void* h, avgpu_update_stats* out) {
   World& w = *(World*)h;
   if (!tile_ok(w)) return fail(AVGPU_ESTATE, "not a strip tile with buffers");
   const int X = w.cfg.world_x;
-  const int64_t nbirth = (int64_t)w.births.size();
-  int64_t placed = 0, dropped = w.t_dropped, overwritten = 0;
-  for (int64_t i = 0; i < nbirth; i++) {
-    Birth& b = w.births[i];
-    const bool won = w.bstate[i] > 0 && b.target >= 0 && w.owner[b.target] == i;
-    if (won && b.target >= w.ncells) continue;   // shipped to the neighbour
-    if (won) { activate_child(w, b, b.target); placed++; }
-    else overwritten++;                          // placed, then overwritten (run_update_impl)
-  }
+  int64_t placed = w.t_placed, dropped = w.t_dropped, overwritten = w.t_overwritten;
   for (int d = 0; d < 2; d++) {
     const HaloHdr* hdr = reinterpret_cast<const HaloHdr*>(w.r_recv[d]);
     const HaloRec* recs = reinterpret_cast<const HaloRec*>(w.r_recv[d] + sizeof(HaloHdr));

@@ -114,6 +114,40 @@ def test_world_updates_bit_exact(golden):
     assert so.num_organisms > 100
 
 
+def test_lazy_statistics_equal_eager(golden):
+    """An update run with out == NULL skips the statistics reduction (the bench
+    regime); the counts still reach the running sums (folded in by the next
+    update's counter reset) and avgpu_get_stats reduces on demand: the same
+    world run lazily equals the world run with statistics every update --
+    stats, per-update and cumulative counters, every cell."""
+    import ctypes as C
+    iset, env, cfg = pu.load_env(golden, seed=101)
+    n = cfg.world_x * cfg.world_y
+    eager = ol.Backend("gpu", cfg, iset, env, ncells=n)
+    lazy = ol.Backend("gpu", cfg, iset, env, ncells=n)
+    anc = files.read_org(os.path.join(golden, "default-heads.org"), iset)
+    for b in (eager, lazy):
+        b.set_orgs(n // 2 + 30, [anc], deterministic=False)
+    fields = [f for f, _ in capi.AvgpuUpdateStats._fields_]
+
+    def vals(st):
+        return [list(v) if hasattr(v, "__len__") else v for v in (getattr(st, f) for f in fields)]
+
+    for upd in range(120):
+        se = eager.run_update()
+        lazy._call("run_update", lazy.h, None)
+        if upd % 7 == 6 or upd > 110:
+            sl = capi.AvgpuUpdateStats()
+            lazy._call("get_stats", lazy.h, C.byref(sl))
+            assert vals(se) == vals(sl), upd
+            assert eager.counters(1) == lazy.counters(1), upd
+            assert eager.counters(0) == lazy.counters(0), upd
+        elif upd % 5 == 0:
+            assert eager.counters(1) == lazy.counters(1), upd      # shards still pending
+    assert se.num_organisms > 100 and se.cum_births > 100
+    assert (eager.digests() == lazy.digests()).all()
+
+
 @pytest.mark.parametrize("T,geometry", [(2, 2), (4, 2), (2, 1)])
 def test_gpu_strip_tiles_equal_single_world(golden, T, geometry):
     """Multi-GPU row on one GPU: T strips of one 64x64 world run

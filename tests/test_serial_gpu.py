@@ -114,7 +114,7 @@ def test_serial_world_recorded_streams(golden):
     n = cfg.world_x * cfg.world_y
     genomes = pu.pop_genomes(golden, iset)[:n]
     rng = np.random.default_rng(17)
-    sched, ctx = rng.random(400_000), rng.random(2_000_000)
+    sched, ctx = rng.random(800_000), rng.random(2_000_000)   # 7 x 108k picks
     orc = ol.Backend("oracle", cfg, iset, env, ncells=n)
     gpu = ol.Backend("gpu", cfg, iset, env, ncells=n)
     for b in (orc, gpu):
@@ -122,7 +122,7 @@ def test_serial_world_recorded_streams(golden):
         _set_streams(b, sched, ctx)
     last = _run(orc, gpu, 7)
     _compare_states(orc, gpu, n)
-    assert last.cum_births > 100            # the lock-step population's first births: update 5
+    assert last.cum_births > 10             # the lock-step population's first births: updates 5-6
     assert gpu.counters()[capi.CNT_REC_EXHAUSTED] == 0
 
 

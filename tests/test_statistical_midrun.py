@@ -17,14 +17,19 @@ merit, gestation time and fitness -- with the seed distribution:
 * the GPU serial world (avgpu_run_serial_updates: the same schedule run by
   the product's interpreter, bit-exact with the oracle's serial world --
   tests/test_serial_gpu.py): the same tolerance;
-* the GPU batch world (the product's update): at updates
-  10..30 within 8 % of the reference.  Update 5 is the documented exception:
-  the loaded population starts in lock step, ~45 % of it reaches its first
-  divide in the same update, and the batch model places those births at the
-  end of the update, where the reference places each one at once and kills a
-  neighbour that might have divided later in the update -- the batch world
-  shows ~40 % more completed gestations at update 5 (measured 2348 vs 1670
-  task organisms) and converges by update 10.
+* the GPU batch world (the product's update), 32 seeds:
+  |reference - mean| <= 3 sd + GAP * |reference|, GAP = 2.5 % the stated gap
+  of the batch model, measured once over the same 32 seeds on the oracle's
+  batch world (bit-identical to the GPU's; tools/midrun_gap.py,
+  profiles/r03_midrun_batch_gap_oracle32.txt: at most 1.7 % of the reference
+  beyond 3 sd, merit and fitness at update 20).  Update 5 is bounded
+  separately: the loaded population starts in lock step, ~45 % of it reaches
+  its first divide in the same update, and the batch model places those
+  births at the end of the update, where the reference places each one at
+  once and kills a neighbour that might have divided later in the update.
+  The batch world shows 40.7 % more completed gestations there (2349.6 vs
+  1670 task organisms; gestation and fitness alike), so the test requires
+  that excess to stay within 35..46 %; merit takes the general tolerance.
 """
 import ctypes as C
 import os
@@ -106,12 +111,20 @@ def test_gpu_serial_world_midrun(golden, tmp_path):
             assert abs(ref[u][k] - m[k]) <= tol, (u, name, ref[u][k], m[k], sd[k])
 
 
+GAP = 0.025                 # the batch model's gap beyond 3 sd (module docstring)
+LOCKSTEP = (0.35, 0.46)     # update 5: excess of completed gestations, (mean - ref) / ref
+
+
 @pytest.mark.gpu
 def test_gpu_batch_world_midrun(golden, tmp_path):
     ref = _ref(golden)
     res = _run(golden, tmp_path, lambda cfg, iset, env: driver.ProductWorld(cfg, iset, env), range(1, 33))
     for u in U:
-        m = res[u].mean(0)
+        m, sd = res[u].mean(0), res[u].std(0, ddof=1)
         for k, name in enumerate(COLS):
-            rel = abs(ref[u][k] - m[k]) / max(abs(ref[u][k]), 1e-12)
-            assert rel <= (0.45 if u == 5 else 0.08), (u, name, ref[u][k], m[k], rel)
+            if u == 5 and name != "merit":
+                excess = (m[k] - ref[u][k]) / abs(ref[u][k])
+                assert LOCKSTEP[0] <= excess <= LOCKSTEP[1], (u, name, ref[u][k], m[k], excess)
+            else:
+                tol = 3 * sd[k] + GAP * abs(ref[u][k])
+                assert abs(ref[u][k] - m[k]) <= tol, (u, name, ref[u][k], m[k], sd[k])

@@ -47,8 +47,9 @@ __device__ __forceinline__ int neighbours(const DevWorld& W, int cell, int* out)
 // the unmutated child or to a value an edit wrote.
 // Runs before placement, so halo records and activation see final genomes.
 // one edit word undone: site src of the genome after the edit -> the site it
-// came from before it, or the value the edit wrote (val >= 0)
-__device__ __forceinline__ void edit_back(int ew, bool nopc, int& src, int& val) {
+// came from before it, or the value the edit wrote (val >= 0); slips go
+// through slip_back
+__device__ __forceinline__ void edit_back(int ew, int& src, int& val) {
   if (ew == 0 || val >= 0) return;
   const int kind = ew & 7, a = (ew >> 3) & 0xFFF, b = (ew >> 15) & 0xFFF;
   if (kind == 2) {                         // point (E_POINT)
@@ -57,29 +58,46 @@ __device__ __forceinline__ void edit_back(int ew, bool nopc, int& src, int& val)
     if (src == a) val = b; else if (src > a) src--;
   } else if (kind == 4) {                  // deletion (E_DEL)
     if (src >= a) src++;
-  } else {                                 // slip from a to b (E_SLIP)
-    if (nopc && a > b && src >= a && src < 2 * a - b) val = AVGPU_H_NOP_C;
-    else if (src >= a) src = b + (src - a);
   }
 }
-// a translocation undone (doTransMutation, cpu/cHardwareBase.cc:700-760,
-// duplication fill): w0 = E_TRANS | ins_loc << 3 | to << 15, w1 = from
-__device__ __forceinline__ void trans_back(int w0, int w1, int& src, int val) {
+// a slip undone (doSlipMutation, cpu/cHardwareBase.cc:621-694) from a to b:
+// a site of the filled insertion [a, 2a - b) takes its SLIP_FILL_MODE fill --
+// 0 duplication (site b + k), 4 nop-C, and the data fills (fill != nullptr:
+// the slip's L words in the arena) 2 random codes, 3 scrambled source sites
+__device__ __forceinline__ void slip_back(int ew, int sfm, const int32_t* fill, int& src, int& val) {
+  if (ew == 0 || val >= 0) return;
+  const int a = (ew >> 3) & 0xFFF, b = (ew >> 15) & 0xFFF;
+  if (a > b && src >= a && src < 2 * a - b) {
+    if (sfm == 4) { val = AVGPU_H_NOP_C; return; }
+    if (sfm == 2 && fill) { val = fill[src - a]; return; }
+    if (sfm == 3 && fill) { src = fill[src - a]; return; }
+  }
+  if (src >= a) src = b + (src - a);
+}
+// a translocation undone (doTransMutation, cpu/cHardwareBase.cc:700-760):
+// w0 = E_TRANS | ins_loc << 3 | to << 15, w1 = from; fill (TRANS_FILL_MODE 1)
+// the inserted sites' source sites, scrambling and its read-backs resolved
+// by the interpreter
+__device__ __forceinline__ void trans_back(int w0, int w1, const int32_t* fill, int& src, int val) {
   if (val >= 0) return;
   const int ins = (w0 >> 3) & 0xFFF, to = (w0 >> 15) & 0xFFF, L = w1 - to;
   if (L > 0) {
     if (src >= ins + L) src -= L;
-    else if (src >= ins) src = to + (src - ins);
+    else if (src >= ins) src = fill ? fill[src - ins] : to + (src - ins);
   } else if (L < 0 && src >= ins) {
     src -= L;
   }
 }
-// applied order (device.h SEG_*): e0, segments 0-1, e1, segment 2, e2,
-// the other segments (pcnt[k] words at subs + pofs[k])
-__device__ __forceinline__ int mut_source(int j, const int* e, bool nopc, int& val, const int32_t* subs,
+// applied order (device.h SEG_*): e0, segments 0-5 (slips, translocations),
+// e1, segment 6, e2, the other segments (pcnt[k] words at subs + pofs[k]).
+// sfm / tfm: SLIP_FILL_MODE / TRANS_FILL_MODE; with a data fill (2, 3 / 1)
+// a slip takes two words (edit, fill offset) and a translocation three.
+__device__ __forceinline__ int mut_source(int j, const int* e, int sfm, int tfm, int& val, const int32_t* subs,
                                           const int* pofs, const int* pcnt) {
-  constexpr int first[5] = {SEG_PSLIP, SEG_PMUT, SEG_PINS, SEG_PDEL, SEG_SMUT};
+  constexpr int first[5] = {SEG_OSLIP, SEG_PMUT, SEG_PINS, SEG_PDEL, SEG_SMUT};
   constexpr int last[5] = {SEG_STRANS, SEG_PMUT, SEG_PINS, SEG_PDEL, SEG_SUNI};
+  const bool sdata = sfm == 2 || sfm == 3;
+  const int tw = tfm == 1 ? 3 : 2;
   int src = j;
   val = -1;
 #pragma unroll
@@ -87,13 +105,23 @@ __device__ __forceinline__ int mut_source(int j, const int* e, bool nopc, int& v
 #pragma unroll
     for (int g = last[k]; g >= first[k]; g--) {
       if (g >= SEG_TTRANS && g <= SEG_STRANS) {
-        for (int i = pcnt[g] - 2; i >= 0 && val < 0; i -= 2)
-          trans_back(subs[pofs[g] + i], subs[pofs[g] + i + 1], src, val);
+        for (int i = pcnt[g] - tw; i >= 0 && val < 0; i -= tw) {
+          const int fo = tw == 3 ? subs[pofs[g] + i + 2] : -1;
+          trans_back(subs[pofs[g] + i], subs[pofs[g] + i + 1], fo >= 0 ? subs + fo : nullptr, src, val);
+        }
+      } else if (g <= SEG_SSLIP && sdata) {
+        for (int i = pcnt[g] - 2; i >= 0 && val < 0; i -= 2) {
+          const int fo = subs[pofs[g] + i + 1];
+          slip_back(subs[pofs[g] + i], sfm, fo >= 0 ? subs + fo : nullptr, src, val);
+        }
+      } else if (g <= SEG_SSLIP) {
+        for (int i = pcnt[g] - 1; i >= 0 && val < 0; i--) slip_back(subs[pofs[g] + i], sfm, nullptr, src, val);
       } else {
-        for (int i = pcnt[g] - 1; i >= 0 && val < 0; i--) edit_back(subs[pofs[g] + i], nopc, src, val);
+        for (int i = pcnt[g] - 1; i >= 0 && val < 0; i--) edit_back(subs[pofs[g] + i], src, val);
       }
     }
-    edit_back(e[k], nopc, src, val);
+    if (k == 0) slip_back(e[0], sfm, nullptr, src, val);
+    else edit_back(e[k], src, val);
   }
   return src;
 }
@@ -112,7 +140,7 @@ __device__ __forceinline__ void wave_lds_sync() {
 // record has none.  child: LDS scratch of TAPE_SLOT + 16 bytes.
 __device__ __forceinline__ void apply_edits_wave(const DevWorld& W, int64_t r, uint8_t* child) {
   const int lane = threadIdx.x & 63;
-  const bool nopc = W.slip_fill_mode == 4;
+  const int sfm = W.slip_fill_mode, tfm = W.trans_fill_mode;
   int e[5];
 #pragma unroll
   for (int k = 0; k < 5; k++) e[k] = W.b_edit[(int64_t)k * W.rcap + r];
@@ -135,7 +163,7 @@ __device__ __forceinline__ void apply_edits_wave(const DevWorld& W, int64_t r, u
     for (int k = 0; k < 4; k++) {
       const int j = 4 * w + k;
       int val;
-      const int src = mut_source(j, e, nopc, val, W.b_subs, pofs, pcnt);
+      const int src = mut_source(j, e, sfm, tfm, val, W.b_subs, pofs, pcnt);
       const uint32_t v = val >= 0 ? (uint32_t)val : (uint32_t)child[src];
       word |= (j < len ? v : 0u) << (8 * k);
     }

@@ -124,17 +124,30 @@ int setup_world(avgpu_world* w, int64_t n, bool test_buffers) {
                             c.divide_poisson_ins_mean, c.divide_poisson_del_mean, c.divide_poisson_trans_mean};
   const double psite[6] = {c.div_mut_prob, c.div_ins_prob, c.div_del_prob, c.div_uniform_prob, c.div_slip_prob,
                            c.div_trans_prob};
-  bool pois = false, site = c.divide_trans_prob > 0.0;
+  // data fills (SLIP_FILL_MODE 2 / 3, TRANS_FILL_MODE 1) keep their draws in
+  // the arena, and the one-shot slip then goes there as a segment
+  const bool sdata = c.slip_fill_mode == 2 || c.slip_fill_mode == 3, tdata = c.trans_fill_mode == 1;
+  const double eslip = c.divide_slip_prob + c.divide_poisson_slip_mean + c.div_slip_prob * AVGPU_MAX_GENOME;
+  const double etrans = c.divide_trans_prob + c.divide_poisson_trans_mean + c.div_trans_prob * AVGPU_MAX_GENOME;
+  bool pois = false, site = c.divide_trans_prob > 0.0 || (sdata && eslip > 0.0);
   for (int q = 0; q < 5; q++) pois = pois || pmeans[q] > 0.0;
   for (int q = 0; q < 6; q++) site = site || psite[q] > 0.0;
   if (pois || site) {
     // arena words per record: 3x the largest expected count of each kind
     // (per site: a 2048-site offspring) + 16 each; offsets are int32
-    int64_t k = 16 + 2;    // + the one-shot translocation's two words
+    const int tw = tdata ? 3 : 2, sw = sdata ? 2 : 1;
+    int64_t k = 16 + tw + sw;    // + the one-shot translocation's and slip's words
     for (int q = 0; q < 6; q++)
-      if (psite[q] > 0.0) k += (q == 5 ? 2 : 1) * ((int64_t)std::ceil(AVGPU_MAX_GENOME * std::min(1.0, psite[q]) * 3.0) + 16);
+      if (psite[q] > 0.0)
+        k += (q == 5 ? tw : (q == 4 ? sw : 1)) * ((int64_t)std::ceil(AVGPU_MAX_GENOME * std::min(1.0, psite[q]) * 3.0) + 16);
     for (int q = 0; q < 5; q++)
-      if (pmeans[q] > 0.0) k += (q == 4 ? 2 : 1) * ((int64_t)std::ceil(3.0 * std::min(pmeans[q], 4096.0)) + 16);
+      if (pmeans[q] > 0.0) k += (q == 4 ? tw : (q == 0 ? sw : 1)) * ((int64_t)std::ceil(3.0 * std::min(pmeans[q], 4096.0)) + 16);
+    // fill words: a slip or translocation of an L-site insertion keeps L words
+    // + L/32 of bit set; E[L] <= a sixth of the offspring (from, to uniform),
+    // sized at 3x for an offspring of AVGPU_MAX_GENOME / 4 sites
+    const double efill = (AVGPU_MAX_GENOME / 4.0) / 6.0 * (1.0 + 1.0 / 32.0) + 2.0;
+    if (sdata && eslip > 0.0) k += (int64_t)std::ceil(3.0 * std::min(eslip, 4096.0) * efill) + 16;
+    if (tdata && etrans > 0.0) k += (int64_t)std::ceil(3.0 * std::min(etrans, 4096.0) * efill) + 16;
     k = std::min<int64_t>(k, (int64_t)INT32_MAX / R);
     W.scap = R * k;
     A(b_subs, W.scap); A(b_pofs, NSEG * R); A(b_pcnt, NSEG * R);
@@ -210,6 +223,7 @@ int setup_world(avgpu_world* w, int64_t n, bool test_buffers) {
   W.th_par_ins = th(c.parent_ins_prob); W.p_par_ins = c.parent_ins_prob;
   W.th_par_del = th(c.parent_del_prob); W.p_par_del = c.parent_del_prob;
   W.slip_fill_mode = c.slip_fill_mode;
+  W.trans_fill_mode = c.trans_fill_mode;
   W.rec = nullptr; W.rec_n = 0; W.rec_off = nullptr;
   W.seed_lo = (uint32_t)c.seed;
   W.seed_hi = (uint32_t)(c.seed >> 32);
@@ -241,12 +255,13 @@ int setup_world(avgpu_world* w, int64_t n, bool test_buffers) {
 std::string unsupported_cfg(const avgpu_cfg& c) {
   auto nz = [](double v) { return v != 0.0; };
   const bool slips = nz(c.divide_slip_prob) || nz(c.divide_poisson_slip_mean) || nz(c.div_slip_prob);
-  if (slips && c.slip_fill_mode != 0 && c.slip_fill_mode != 4)
-    return "SLIP_FILL_MODE 1-3 (nop-X, random, scrambled)";
+  if (slips && (c.slip_fill_mode < 0 || c.slip_fill_mode == 1 || c.slip_fill_mode > 4))
+    return "SLIP_FILL_MODE 1 (nop-X) or an unknown mode";
   if (nz(c.copy_slip_prob) && c.slip_copy_mode != 0)
     return "SLIP_COPY_MODE 1 (a slip of the whole memory at the write head)";
-  if ((nz(c.divide_trans_prob) || nz(c.divide_poisson_trans_mean) || nz(c.div_trans_prob)) && c.trans_fill_mode != 0)
-    return "TRANS_FILL_MODE 1 (scrambled)";
+  if ((nz(c.divide_trans_prob) || nz(c.divide_poisson_trans_mean) || nz(c.div_trans_prob)) &&
+      (c.trans_fill_mode < 0 || c.trans_fill_mode > 1))
+    return "TRANS_FILL_MODE other than 0 (duplication) / 1 (scrambled)";
   if (c.divide_poisson_slip_mean > 700.0 || c.divide_poisson_mut_mean > 700.0 ||
       c.divide_poisson_ins_mean > 700.0 || c.divide_poisson_del_mean > 700.0 ||
       c.divide_poisson_trans_mean > 700.0)

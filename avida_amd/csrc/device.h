@@ -246,6 +246,7 @@ struct DevWorld {
   double p_dtrans;
   int32_t seg_any;        // some variable-count kind is on (b_subs / b_pofs / b_pcnt allocated)
   int32_t slip_fill_mode;
+  int32_t trans_fill_mode;
   // RECORDED mode (avgpu_set_rng_mode): rec_n doubles; rec_off[c] = the start
   // of cell c's organism's segment, -1 = a counter stream.  rec == nullptr:
   // COUNTER mode everywhere (the REC-free interpreter instantiations run).
@@ -326,11 +327,15 @@ __host__ __device__ inline int64_t record_bytes(int x, int64_t arena) {
 #define CNT_HALO_LOST 19  /* offspring lost to a full halo arena (counted in DROPPED too) */
 #define CNT_REC_OVER 20   /* RECORDED draws past the end of the stream */
 // variable-count edit segments of a birth record, in the order applied:
-// e0 (slip), Poisson slips, per-site slips, translocations (one-shot, Poisson,
-// per site: two words each, see births.h), e1 (mut), Poisson substitutions,
-// e2 (ins), Poisson insertions, e3 (del), Poisson deletions, e4 (uniform),
-// per-site substitutions, insertions, deletions, uniform mutations
-enum { SEG_PSLIP = 0, SEG_SSLIP, SEG_TTRANS, SEG_PTRANS, SEG_STRANS, SEG_PMUT, SEG_PINS, SEG_PDEL, SEG_SMUT, SEG_SINS, SEG_SDEL, SEG_SUNI, NSEG };
+// e0 (slip) or, with a data fill (SLIP_FILL_MODE 2 / 3), the one-shot slip as
+// a segment, Poisson slips, per-site slips (two words each with a data fill:
+// edit, fill offset), translocations (one-shot, Poisson, per site: two words
+// each, three with TRANS_FILL_MODE 1; see births.h), e1 (mut), Poisson
+// substitutions, e2 (ins), Poisson insertions, e3 (del), Poisson deletions,
+// e4 (uniform), per-site substitutions, insertions, deletions, uniform
+// mutations.  Data fills (a slip's or translocation's L codes / source
+// sites) sit in the same arena, reserved per event.
+enum { SEG_OSLIP = 0, SEG_PSLIP, SEG_SSLIP, SEG_TTRANS, SEG_PTRANS, SEG_STRANS, SEG_PMUT, SEG_PINS, SEG_PDEL, SEG_SMUT, SEG_SINS, SEG_SDEL, SEG_SUNI, NSEG };
 #define CNT_SUB_OVERFLOW 22   /* DIV_MUT_PROB substitutions that found the b_subs arena full (must stay 0) */
 #define CNT_OVERSIZE 21   /* offspring a slip grew past AVGPU_MAX_GENOME (counted in DROPPED too) */
 #define CNT_MEM_CAP 23    /* copy insertions past AVGPU_MAX_GENOME sites / removals from one site (skipped) */
@@ -386,6 +391,18 @@ __device__ __forceinline__ uint32_t ld_sync_u32(const void* p) {
 __device__ __forceinline__ uint32_t ld_sync_u8(const void* p) {
   uint32_t v;
   asm volatile("global_load_ubyte %0, %1, off\n\ts_waitcnt vmcnt(0)" : "=v"(v) : "v"(p) : "memory");
+  return v;
+}
+// the same without the memory clobber: a read-only table load that orders
+// nothing else (it still waits for itself)
+__device__ __forceinline__ uint32_t ld_sync_ro_u32(const void* p) {
+  uint32_t v;
+  asm volatile("global_load_dword %0, %1, off\n\ts_waitcnt vmcnt(0)" : "=v"(v) : "v"(p));
+  return v;
+}
+__device__ __forceinline__ uint32_t ld_sync_ro_u8(const void* p) {
+  uint32_t v;
+  asm volatile("global_load_ubyte %0, %1, off\n\ts_waitcnt vmcnt(0)" : "=v"(v) : "v"(p));
   return v;
 }
 __device__ __forceinline__ void st_async_u8(void* p, uint32_t v) {
@@ -508,15 +525,10 @@ __device__ __forceinline__ void count_add(const DevWorld& W, int slot, unsigned 
 }
 
 // LDS size classes of k_interpret (bytes of tape per lane)
-// (a block of class S uses 64 x tape_stride(S) B of LDS for tapes; class 0 is
-// sized so that 7 blocks fit a CU's 160 KiB with its two lookup tables)
-#ifdef AVGPU_C0_320
-// 320-site class-0 slots with the lookup tables in global memory: 64 x 320 B
-// is exactly a CU's 160 KiB / 8 blocks (A/B variant)
+// (a block of class S uses 64 x tape_stride(S) B of LDS for tapes; class 0
+// holds nothing else: 64 x 320 B = 20 KiB, so 8 one-wave blocks fill a CU's
+// 160 KiB -- as many as its ~216 VGPRs admit)
 #define CLASS0_SIZE 320
-#else
-#define CLASS0_SIZE 336
-#endif
 #define CLASS1_SIZE 768
 #define CLASS2_SIZE 1536
 #define CLASS3_SIZE 2048

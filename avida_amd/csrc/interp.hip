@@ -137,8 +137,8 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
   // The fetch / label / search windows read up to 16 bytes past a site; what
   // they read beyond the organism's memory is masked off.  Classes 1-3 keep a
   // 16-byte pad; class 0 has none -- a window past lane L's slot reads lane
-  // L+1's tape (lane 63's: the lookup tables after the tapes) -- so that its
-  // block (tapes 21 KiB + tables 0.75 KiB) stays at 7 per CU.
+  // L+1's tape (lane 63's: past the block's LDS, which reads as 0) -- so that
+  // its block (tapes only, 20 KiB) fits 8 times in a CU.
   constexpr int STRIDE = tape_stride(S);
   constexpr int QUADS = STRIDE / 16;
   constexpr int TAPE_WORDS = 64 * STRIDE / 4;
@@ -152,23 +152,20 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
   uint8_t* lds = reinterpret_cast<uint8_t*>(lds32);
   int32_t* stk = reinterpret_cast<int32_t*>(lds32 + TAPE_WORDS);
   uint32_t* tab = lds32 + TAPE_WORDS + STK_WORDS;
-  // class 0 keeps only the two per-lane lookup tables in LDS after the tapes
-  // (task LUT 512 B + random-instruction LUT 256 B: 22.5 + 0.75 KiB per block,
-  // still 7 blocks per CU) -- a vector global load there made the IO path
-  // wait on vmcnt(0), i.e. for every store the wave still had in flight --
-  // and reads the rest from global memory through uniform (scalar) loads
+  // class 0 keeps no table in LDS: its 20 KiB are the tapes (8 blocks per CU;
+  // with the task and random-instruction LUTs beside 336-site tapes a block
+  // needed 22.25 KiB and 7 fitted, 4 % slower per update).  It reads them from
+  // global memory by loads that wait for themselves (a compiler-visible
+  // vector load made the IO path wait on vmcnt(0) at its join, i.e. for every
+  // store the wave still had in flight), the rest through uniform loads.
   constexpr bool GTAB = (S == CLASS0_SIZE);
-  // the two lookup tables are always in LDS; said so explicitly, or an access
+  constexpr bool GLUT = GTAB;
+  // the list classes' tables are in LDS; said so explicitly, or an access
   // through a generic pointer is a flat load, whose wait also drains every
   // outstanding global store of the wave
   typedef const __attribute__((address_space(3))) uint16_t lds_u16_t;
   typedef const __attribute__((address_space(3))) uint8_t lds_u8_t;
   lds_u16_t* lut = (lds_u16_t*)(tab);
-#ifdef AVGPU_C0_320
-  constexpr bool GLUT = (S == CLASS0_SIZE);   // no tables in LDS at all
-#else
-  constexpr bool GLUT = false;
-#endif
   const int32_t* rcum = GTAB ? W.rand_cum : reinterpret_cast<const int32_t*>(tab + 128);
   const uint8_t* rcode = GTAB ? W.rand_code : reinterpret_cast<const uint8_t*>(tab + 192);
   lds_u8_t* rlut = (lds_u8_t*)(tab + (GTAB ? 128 : 208));
@@ -239,13 +236,7 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
   const int m_in = M;
 
   // ---- block-shared tables ----
-  if (GLUT) {
-  } else if (GTAB) {
-    const uint32_t* g_lut = reinterpret_cast<const uint32_t*>(W.task_lut);
-    tab[lane] = g_lut[lane];
-    tab[64 + lane] = g_lut[64 + lane];
-    tab[128 + lane] = reinterpret_cast<const uint32_t*>(W.rand_lut)[lane];
-  } else {
+  if (!GTAB) {
     uint32_t* l32 = tab;
     const uint32_t* g_lut = reinterpret_cast<const uint32_t*>(W.task_lut);
     l32[lane] = g_lut[lane];
@@ -266,7 +257,7 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
   // class 0: unrolled so that the shuffles of several quads are in flight
   // together (one LDS round trip per quad otherwise); the list classes' 49 /
   // 97 / 129-quad loops stay rolled (code size)
-  constexpr int QUNR = (S == CLASS0_SIZE) ? 7 : 1;
+  constexpr int QUNR = (S == CLASS0_SIZE) ? (QUADS % 7 == 0 ? 7 : 5) : 1;
 #pragma unroll QUNR
   for (int it = 0; it < qits; it++) {
     const int i = it * 64 + lane;
@@ -421,7 +412,7 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
   // cInstSet::GetRandomInst (cpu/cInstSet.cc:83-88) from the LDS tables
   auto rand_code = [&]() -> uint8_t {
     const uint32_t r = draw_below((uint32_t)k_rand_total);
-    if (k_rand_lut) return GLUT ? (uint8_t)ld_sync_u8(W.rand_lut + r) : rlut[r];
+    if (k_rand_lut) return GLUT ? (uint8_t)ld_sync_ro_u8(W.rand_lut + r) : rlut[r];
     int i = 0;
     while (i < k_n_ops - 1 && tab_i32(rcum + i) <= (int32_t)r) i++;
     return (uint8_t)tab_u8(rcode + i);
@@ -728,7 +719,7 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
         const int id = (int)lo - (int)(~pr & 0xFFu);
         uint32_t tmask = 0u;
         if ((ones & zeros) == 0u && id >= 0)
-          tmask = GLUT ? (ld_sync_u32(W.task_lut + (id & ~1)) >> ((id & 1) * 16)) & 0xFFFFu : lut[id];
+          tmask = GLUT ? (ld_sync_ro_u32(W.task_lut + (id & ~1)) >> ((id & 1) * 16)) & 0xFFFFu : lut[id];
         // cEnvironment::TestOutput / TestRequisites / DoProcesses
         // (main/cEnvironment.cc:1314-1406, :1408-1503, :1610-1760)
         if (tmask && k_env_simple) {
@@ -1070,13 +1061,73 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
               auto pput = [&](int k, int i, int ew) {
                 if (mode == AVGPU_MODE_WORLD && pofs[k] >= 0 && (int64_t)pofs[k] + i < W.scap) W.b_subs[pofs[k] + i] = ew;
               };
-              auto slip_edit = [&]() -> int {   // doSlipMutation :621-694
+              // Data fills (SLIP_FILL_MODE 2 / 3, TRANS_FILL_MODE 1): after a
+              // slip's or translocation's from / to (/ ins_loc) draws, its L
+              // fill draws in the reference's order (:636-665, :721-741):
+              // GetRandomInst per site (2), or GetInt(L - i) per site with the
+              // scrambled walk over copied_so_far (3, translocation 1).  The
+              // interpreter resolves them into the arena (WORLD): codes, or
+              // the source site of each filled site in the sequence before the
+              // edit -- a scrambled translocation that reads a site it already
+              // filled takes that site's source.  A bit set of L bits after
+              // the L words marks the indices taken.  Other modes only draw.
+              const int sfm = DEF ? 0 : W.slip_fill_mode, tfm = DEF ? 0 : W.trans_fill_mode;
+              const bool sdata = sfm == 2 || sfm == 3, tdata = tfm == 1;
+              bool ftrunc = false;
+              auto fill_draws = [&](int kind, int L, int to, int ins_loc) -> int {
+                if (L <= 0) return -1;
+                const int nbw = kind == 2 ? 0 : (L + 31) >> 5;
+                int off = -1;
+                if (mode == AVGPU_MODE_WORLD) {
+                  if ((int64_t)__atomic_load_n(W.b_count + 2, __ATOMIC_RELAXED) < W.scap) {
+                    const int o = atomicAdd(W.b_count + 2, L + nbw);
+                    if ((int64_t)o + L + nbw <= W.scap) off = o;
+                  }
+                  if (off < 0) ftrunc = true;
+                }
+                int32_t* f = off >= 0 ? W.b_subs + off : nullptr;
+                uint32_t* bits = f ? reinterpret_cast<uint32_t*>(f + L) : nullptr;
+                if (bits)
+                  for (int q = 0; q < nbw; q++) bits[q] = 0u;
+                for (int i = 0; i < L; i++) {
+                  if (kind == 2) {
+                    const int v = rand_code();
+                    if (f) f[i] = v;
+                    continue;
+                  }
+                  int rem = (int)draw_below((uint32_t)(L - i));
+                  if (!f) continue;
+                  int wd = 0;                              // the rem-th index not taken
+                  while (true) {
+                    const int fr = 32 - __popc(bits[wd]);
+                    if (rem < fr) break;
+                    rem -= fr;
+                    wd++;
+                  }
+                  uint32_t z = ~bits[wd];
+                  for (int q = 0; q < rem; q++) z &= z - 1u;
+                  const int bit = __ffs((int)z) - 1;
+                  bits[wd] |= 1u << bit;
+                  int src = to + wd * 32 + bit;
+                  if (kind == 5 && src >= ins_loc && src < ins_loc + i) src = f[src - ins_loc];
+                  f[i] = src;
+                }
+                return off;
+              };
+              auto slip_edit = [&](int k, int i) {   // doSlipMutation :621-694 into segment k
                 const int from = (int)draw_below((uint32_t)len + 1u);
                 const int to = from == 0 ? (int)draw_below((uint32_t)len) : (int)draw_below((uint32_t)len + 1u);
+                if (sdata) {
+                  const int fo = fill_draws(sfm, from - to, to, 0);
+                  pput(k, 2 * i, edit_word(E_SLIP, from, to));
+                  pput(k, 2 * i + 1, fo);
+                } else {
+                  pput(k, i, edit_word(E_SLIP, from, to));
+                }
                 len += from - to;
                 lmax = max(lmax, len);
-                return edit_word(E_SLIP, from, to);
               };
+              const int sw = sdata ? 2 : 1, tw = tdata ? 3 : 2;   // words per slip / translocation
               auto uniform_edit = [&]() -> int {   // doUniformMutation :572-595
                 const int mut = (int)draw_below((uint32_t)(2 * k_n_ops + 1));
                 int ew = 0;
@@ -1092,51 +1143,59 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
                 return ew;
               };
               if (draw_p(t_slip, q_slip)) {          // doSlipMutation :621-694
-                const int from = (int)draw_below((uint32_t)len + 1u);
-                const int to = from == 0 ? (int)draw_below((uint32_t)len) : (int)draw_below((uint32_t)len + 1u);
-                e0 = edit_word(E_SLIP, from, to);
-                len += from - to;
-                lmax = max(lmax, len);
+                if (segs && sdata) {                   // as a segment, with its fill
+                  preserve(SEG_OSLIP, 2);
+                  slip_edit(SEG_OSLIP, 0);
+                  pcnt[SEG_OSLIP] = 2;
+                } else {
+                  const int from = (int)draw_below((uint32_t)len + 1u);
+                  const int to = from == 0 ? (int)draw_below((uint32_t)len) : (int)draw_below((uint32_t)len + 1u);
+                  if (sdata) fill_draws(sfm, from - to, to, 0);   // (no arena: the draws only)
+                  e0 = edit_word(E_SLIP, from, to);
+                  len += from - to;
+                  lmax = max(lmax, len);
+                }
               }
               if (pois) {                            // Poisson slips :318-320
                 const int n = npois(0);
-                preserve(SEG_PSLIP, n);
-                for (int i = 0; i < n; i++) pput(SEG_PSLIP, i, slip_edit());
-                pcnt[SEG_PSLIP] = n;
+                preserve(SEG_PSLIP, sw * n);
+                for (int i = 0; i < n; i++) slip_edit(SEG_PSLIP, i);
+                pcnt[SEG_PSLIP] = sw * n;
               }
               if (segs && W.th_dsite[3]) {           // slips per site :323-327
                 const int n = nbinom(W.th_dsite[3], W.p_dsite[3]);
-                preserve(SEG_SSLIP, n);
-                for (int i = 0; i < n; i++) pput(SEG_SSLIP, i, slip_edit());
-                pcnt[SEG_SSLIP] = n;
+                preserve(SEG_SSLIP, sw * n);
+                for (int i = 0; i < n; i++) slip_edit(SEG_SSLIP, i);
+                pcnt[SEG_SSLIP] = sw * n;
               }
-              // translocations (doTransMutation :700-760, duplication fill):
-              // from, to, then the insertion site on the size before it
+              // translocations (doTransMutation :700-760): from, to, then the
+              // insertion site on the size before it, then the fill's draws
               auto trans_edit = [&](int k, int i) {
                 const int from = (int)draw_below((uint32_t)len + 1u);
                 const int to = from == 0 ? (int)draw_below((uint32_t)len) : (int)draw_below((uint32_t)len + 1u);
                 const int ins_loc = (int)draw_below((uint32_t)len + 1u);
-                pput(k, 2 * i, edit_word(E_TRANS, ins_loc, to));
-                pput(k, 2 * i + 1, from);
+                pput(k, tw * i, edit_word(E_TRANS, ins_loc, to));
+                pput(k, tw * i + 1, from);
+                if (tdata) pput(k, tw * i + 2, fill_draws(5, from - to, to, ins_loc));
                 len += from - to;
                 lmax = max(lmax, len);
               };
               if (segs && W.th_dtrans && draw_p(W.th_dtrans, W.p_dtrans)) {   // one-shot :331
-                preserve(SEG_TTRANS, 2);
+                preserve(SEG_TTRANS, tw);
                 trans_edit(SEG_TTRANS, 0);
-                pcnt[SEG_TTRANS] = 2;
+                pcnt[SEG_TTRANS] = tw;
               }
               if (pois) {                            // Poisson translocations :334-335
                 const int n = npois(4);
-                preserve(SEG_PTRANS, 2 * n);
+                preserve(SEG_PTRANS, tw * n);
                 for (int i = 0; i < n; i++) trans_edit(SEG_PTRANS, i);
-                pcnt[SEG_PTRANS] = 2 * n;
+                pcnt[SEG_PTRANS] = tw * n;
               }
               if (segs && W.th_dsite[4]) {           // translocations per site :338-342
                 const int n = nbinom(W.th_dsite[4], W.p_dsite[4]);
-                preserve(SEG_STRANS, 2 * n);
+                preserve(SEG_STRANS, tw * n);
                 for (int i = 0; i < n; i++) trans_edit(SEG_STRANS, i);
-                pcnt[SEG_STRANS] = 2 * n;
+                pcnt[SEG_STRANS] = tw * n;
               }
               if (draw_p(t_mut, q_mut)) {
                 const int line = (int)draw_below((uint32_t)len);
@@ -1245,6 +1304,7 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
               // written): the offspring cannot be rebuilt, so it is dropped
               // (counted in CNT_SUB_OVERFLOW and CNT_DROPPED; tests require 0)
               bool truncated = false;
+              if (ftrunc) { count_add(W, CNT_SUB_OVERFLOW, 1ull); truncated = true; }   // a fill found the arena full
               if (segs && mode == AVGPU_MODE_WORLD)
 #pragma unroll
                 for (int k = 0; k < NSEG; k++)
@@ -1622,11 +1682,7 @@ __global__ __launch_bounds__(64, (S == CLASS0_SIZE) ? 2 : 1) void k_interpret(co
   constexpr int TAB_WORDS = 128 + 64 + 16 + 64 + AVGPU_MAX_REACTIONS * RT_STRIDE + 64;
   // class 0: stacks in VGPRs, tables in global memory -- only the tapes in LDS
   constexpr int STK = (S == CLASS0_SIZE) ? 0 : 2 * AVGPU_STACK_SIZE * 64;
-#ifdef AVGPU_C0_320
   constexpr int TAB = (S == CLASS0_SIZE) ? 0 : TAB_WORDS;     // class 0: tapes only
-#else
-  constexpr int TAB = (S == CLASS0_SIZE) ? 192 : TAB_WORDS;   // class 0: task LUT + random LUT
-#endif
   __shared__ __attribute__((aligned(16))) uint32_t lds32[64 * tape_stride(S) / 4 + STK + TAB];
   if (cls == 0) {
     // sorted windows: the 32 chunks of a window run on one XCD (blocks are
@@ -1989,7 +2045,12 @@ static void launch_classes(const DevWorld& W, const DevWorld* dW, int mode, hipS
     list(1, aux[0]);
     list(2, aux[1]);
     list(3, aux[1]);
-    for (int k = 0; k < 2; k++) hipEventRecord(ev_join[k], aux[k]);
+    // one join for the world's stream: aux 0 takes in aux 1 (classes 2 + 3,
+    // short) off the critical path; each wait queued on the world's stream
+    // costs ~10 us of dead time there even when its event has long completed
+    hipEventRecord(ev_join[1], aux[1]);
+    hipStreamWaitEvent(aux[0], ev_join[1], 0);
+    hipEventRecord(ev_join[0], aux[0]);
   }
   if (mode == AVGPU_MODE_WORLD && W.env_simple && W.env_res_mask == 0u && def_knobs(W))
     hipLaunchKernelGGL((k_interpret<CLASS0_SIZE, REC, true, true, true>), dim3(blocks), dim3(64), 0, s, dW, 0, 0, mode, first, count, srt, 64);
@@ -2000,15 +2061,21 @@ static void launch_classes(const DevWorld& W, const DevWorld* dW, int mode, hipS
   else
     hipLaunchKernelGGL((k_interpret<CLASS0_SIZE, REC>), dim3(blocks), dim3(64), 0, s, dW, 0, 0, mode, first, count, srt, 64);
   if (after_class) hipEventRecord(after_class[0], s);
-  if (aux) {
-    for (int k = 0; k < 2; k++) hipStreamWaitEvent(s, ev_join[k], 0);
-  } else
-    for (int k = 1; k <= 3; k++) list(k, s);
   // Spill rows run after class 0, alone on the chip and latency-bound on their
   // longest remaining slice; spread over waves (spill_lpw lanes each), a
   // wave's iterations no longer pay for its other lanes' divergent paths.
+  // Row 4 holds only class-0 organisms (those that outgrew its slots), so it
+  // starts right behind class 0, and the joins with the aux streams (their
+  // lists ended inside class 0) are queued while it runs instead of in front
+  // of it (~17 us per update of event waits on the critical path).
   const int slpw = spill_lpw();
-  row(CLASS1_SIZE, dim3(lb_small), s, 1, 4, slpw);
+  if (aux) {
+    row(CLASS1_SIZE, dim3(lb_small), s, 1, 4, slpw);
+    hipStreamWaitEvent(s, ev_join[0], 0);
+  } else {
+    for (int k = 1; k <= 3; k++) list(k, s);
+    row(CLASS1_SIZE, dim3(lb_small), s, 1, 4, slpw);
+  }
   if (after_class && tall) hipEventRecord(after_class[1], s);
   // spill rows 5 + 6 (beyond classes 1 / 2) in one launch of class 3's slots
   row(CLASS3_SIZE, dim3(std::min(lb_small, 64u)), s, -1, 5, slpw);

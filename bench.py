@@ -44,14 +44,14 @@ HBM_PEAK_GBS = 8000.0         # MI355X_MICROARCH.md chip table (spec)
 # in exactly this regime)
 BURN_IN = 150
 WARMUP = 5
-PMC_FILE = os.path.join(ROOT, "profiles", "pmc_k_interpret336.json")
+PMC_FILE = os.path.join(ROOT, "profiles", "pmc_k_interpret320.json")
 
 
 
 def issue_roofline(cnt, c0_ms, c0_insts):
-    """Instruction-issue roofline of k_interpret<336> (the second roofline the
+    """Instruction-issue roofline of k_interpret<320> (the second roofline the
     north star asks for). PMC wave-instruction counts per class-0 dispatch
-    (profiles/pmc_k_interpret336.json, same world) over this run's live
+    (profiles/pmc_k_interpret320.json, same world) over this run's live
     HIP-event duration of that kernel. VALU peak: a wave64 VALU instruction
     occupies its SIMD-32 for 2 cycles (MI355X_MICROARCH.md, wave scheduling),
     4 SIMDs x 256 CUs x 2.4 GHz / 2 = 1.23e12 wave-instructions/s; SALU peak:
@@ -390,7 +390,7 @@ def main():
             dist.destroy_process_group()
         return
     value = tot_insts / dt_max
-    # roofline of the dominant kernel k_interpret<336> (LDS size class 0, one
+    # roofline of the dominant kernel k_interpret<320> (LDS size class 0, one
     # launch per update), this rank: algorithmic bytes per launch =
     # slices * 2 * 224 B + tape sites staged in and written back * 1.25 B,
     # over its HIP-event-timed average duration on the world's stream.
@@ -444,7 +444,7 @@ def main():
             "ranks": world,
             "long_run": long_run,
         },
-        # The resource that binds k_interpret<336> is instruction issue plus
+        # The resource that binds k_interpret<320> is instruction issue plus
         # exposed latency, so the headline roofline is the VALU-issue one
         # (PMC wave-instructions per launch over the live event-timed launch);
         # the HBM roofline of the same launch (algorithmic bytes of SURVEY.md
@@ -461,7 +461,7 @@ def main():
             "hbm": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                     "traffic_over_algorithmic": (traffic / bytes_per_launch) if traffic else None},
-            "kernel": "k_interpret<336> (LDS size class 0)",
+            "kernel": "k_interpret<320> (LDS size class 0)",
             "kernel_ms": c0_ms,
             "timed_launches": int(phases.value),
             "time_every": args.time_every,

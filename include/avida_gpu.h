@@ -142,7 +142,8 @@ typedef struct avgpu_cfg {
   uint64_t seed;                   /* RANDOM_SEED (counter-RNG key) */
   double divide_slip_prob;         /* DIVIDE_SLIP_PROB (TestDivideSlip always draws) */
   double divide_uniform_prob;      /* DIVIDE_UNIFORM_PROB */
-  int32_t slip_fill_mode;          /* SLIP_FILL_MODE: 0 duplication, 4 nop-C (1-3 refused) */
+  int32_t slip_fill_mode;          /* SLIP_FILL_MODE: 0 duplication, 2 random, 3 scrambled,
+                                      4 nop-C (1, nop-X, refused) */
   int32_t pad_cfg;
   double div_mut_prob;             /* DIV_MUT_PROB: per-site substitutions on divide,
                                       Binomial(offspring size, p) of them drawn after the
@@ -160,7 +161,7 @@ typedef struct avgpu_cfg {
    * insertions / deletions / uniform mutations / slips on divide
    * (cpu/cHardwareBase.cc:323-327, :463-503) */
   double div_ins_prob, div_del_prob, div_uniform_prob, div_slip_prob;
-  /* translocations (TRANS_FILL_MODE 0, duplication): DIVIDE_TRANS_PROB,
+  /* translocations (TRANS_FILL_MODE below): DIVIDE_TRANS_PROB,
    * DIVIDE_POISSON_TRANS_MEAN, DIV_TRANS_PROB (cpu/cHardwareBase.cc:331-343,
    * doTransMutation :700-760) */
   double divide_trans_prob, divide_poisson_trans_mean, div_trans_prob;
@@ -623,7 +624,7 @@ int avgpu_last_step_insts(avgpu_world* w, int64_t* insts);
  * every k_interpret launch sequence) accumulated since the previous call:
  * total milliseconds and number of interpret phases; resets the accumulator. */
 int avgpu_last_kernel_ms(avgpu_world* w, double* ms, int64_t* launches);
-/* The same accumulators split by interpreter size class (k_interpret<336>,
+/* The same accumulators split by interpreter size class (k_interpret<320>,
  * <768>, <1536>, <2048>): class_ms[4] milliseconds and the number of timed
  * interpret phases since the previous call; resets them (and
  * avgpu_last_kernel_ms's). */

@@ -473,8 +473,30 @@ struct Exec {
     else o.generation++;
   }
 
+  // the op code of nop-C in this instruction set (cInstSet::GetInst("nop-C"))
+  uint8_t nop_c_op() const {
+    for (int i = 0; i < w.is.n; i++) if (w.is.nopmod[i] == 2) return (uint8_t)i;
+    return 2;
+  }
+  // The scrambled fills' index pick (cpu/cHardwareBase.cc:652-664, :727-739):
+  // GetInt(L - i), then the walk over copied_so_far that skips the indices
+  // already taken -- the draw-th index not yet copied.
+  static int scrambled_index(std::vector<bool>& taken, int draw) {
+    int copy_index = draw, test = 0, passed = draw;
+    while (passed >= 0) {
+      if (taken[test]) copy_index++;
+      else passed--;
+      test++;
+    }
+    taken[copy_index] = true;
+    return copy_index;
+  }
+
   // cHardwareBase::doSlipMutation (cpu/cHardwareBase.cc:621-694), SLIP_FILL_MODE
-  // 0 (duplication) and 4 (nop-C; the device refuses 1-3)
+  // 0 duplication, 2 random instructions, 3 scrambled duplication, 4 nop-C
+  // (1, nop-X, is refused).  The scrambled fill reads genome[to + k] of the
+  // sequence being filled: [to, from) is never written by the fill, so that is
+  // the copy's.
   void slip_mutation(std::vector<uint8_t>& g, Stream& r) {
     const std::vector<uint8_t> copy = g;
     const int size = (int)copy.size();
@@ -483,14 +505,23 @@ struct Exec {
     int ins = from - to;
     g.resize(size + ins);
     lmax = std::max(lmax, (int)g.size());
-    for (int i = 0; i < ins; i++) g[from + i] = w.cfg.slip_fill_mode == 4 ? (uint8_t)H_NOP_C : copy[to + i];
+    const int mode = w.cfg.slip_fill_mode;
+    std::vector<bool> taken(ins > 0 ? ins : 0, false);
+    for (int i = 0; i < ins; i++) {
+      if (mode == 2) g[from + i] = (uint8_t)w.is.random_inst(r);
+      else if (mode == 3) g[from + i] = g[to + scrambled_index(taken, (int)r.uint_below((uint32_t)(ins - i)))];
+      else if (mode == 4) g[from + i] = nop_c_op();
+      else g[from + i] = copy[to + i];
+    }
     if (ins < 0) ins = 0;
     for (int i = ins; i < size - to; i++) g[from + i] = copy[to + i];
   }
 
   // cHardwareBase::doTransMutation (cpu/cHardwareBase.cc:700-760), TRANS_FILL_MODE
-  // 0 (duplication; 1 is refused): copy[to, from) is inserted at ins_loc when
-  // from > to, copy[ins_loc, ins_loc + to - from) is cut when from < to
+  // 0 duplication, 1 scrambled: copy[to, from) is inserted at ins_loc when
+  // from > to, copy[ins_loc, ins_loc + to - from) is cut when from < to.  The
+  // scrambled fill reads genome[to + k] of the sequence being filled, which may
+  // be a site this fill already wrote (ins_loc inside [to, from)).
   void trans_mutation(std::vector<uint8_t>& g, Stream& r) {
     const std::vector<uint8_t> copy = g;
     const int size = (int)copy.size();
@@ -501,7 +532,13 @@ struct Exec {
     lmax = std::max(lmax, (int)g.size());
     const int ins_loc = (int)r.uint_below((uint32_t)size + 1);
     if (ins > 0) {
-      for (int i = 0; i < ins; i++) g[ins_loc + i] = copy[to + i];
+      if (w.cfg.trans_fill_mode == 1) {
+        std::vector<bool> taken(ins, false);
+        for (int i = 0; i < ins; i++)
+          g[ins_loc + i] = g[to + scrambled_index(taken, (int)r.uint_below((uint32_t)(ins - i)))];
+      } else {
+        for (int i = 0; i < ins; i++) g[ins_loc + i] = copy[to + i];
+      }
       for (int i = ins_loc; i < size; i++) g[i + ins] = copy[i];
     } else if (ins < 0) {
       for (int i = ins_loc; i < (int)g.size(); i++) g[i] = copy[i - ins];
@@ -509,12 +546,14 @@ struct Exec {
   }
 
   // Divide_DoMutations (cpu/cHardwareBase.cc:296-569) in the reference's order
-  // of draws: TestDivideSlip always draws (main/cMutationRates.h:128), the
-  // translocation / LGT / Poisson / parent kinds and the per-site insertions
-  // and deletions are refused when
-  // non-zero (avida_amd/capi.py UNSUPPORTED_NONZERO) and draw nothing at zero,
+  // of draws: TestDivideSlip always draws (main/cMutationRates.h:128);
   // TestDivideMut / Ins / Del always draw (:121-123; the size limits are
-  // tested after the draw), TestDivideUniform draws only when non-zero (:124-127).
+  // tested after the draw); TestDivideUniform and every variable-count kind --
+  // Poisson (:318-435), per site (:323-327, :447-503), translocations
+  // (:331-343) -- draw only at a non-zero rate or mean; the parent's own
+  // substitutions, insertions and deletions (:509-563) come last, in
+  // divide() on the parent's memory.  LGT (:345-357) is refused by the
+  // library (avgpu_check_cfg) and never reaches this code.
   int lmax = 0;   // the longest the offspring got during its divide mutations
   void divide_mutations(std::vector<uint8_t>& child) {
     Stream& r = rng();

@@ -173,11 +173,94 @@ def test_recorded_draws_translocations(golden):
             break
     assert st[0].num_divides == 1
     assert st[0].rng_counter == 1 + 1 + 3 + 2 + 3 + 100 + 300 + 3
-    # TRANS_FILL_MODE 1 (scrambled) is refused by the library itself
-    _, _, cfg1 = pu.load_env(golden, overrides={"DIVIDE_TRANS_PROB": 0.1, "TRANS_FILL_MODE": 1})
+    # TRANS_FILL_MODE 1 (scrambled) is on the path; an unknown mode and
+    # SLIP_FILL_MODE 1 (nop-X) are refused by the library itself
     lib = capi.load_product()
-    assert lib.avgpu_check_cfg(C.byref(cfg1)) == -5
+    _, _, cfg1 = pu.load_env(golden, overrides={"DIVIDE_TRANS_PROB": 0.1, "TRANS_FILL_MODE": 1})
+    assert lib.avgpu_check_cfg(C.byref(cfg1)) == 0
+    _, _, cfg2 = pu.load_env(golden, overrides={"DIVIDE_TRANS_PROB": 0.1, "TRANS_FILL_MODE": 2})
+    assert lib.avgpu_check_cfg(C.byref(cfg2)) == -5
     assert "TRANS_FILL_MODE" in lib.avgpu_last_error().decode()
+    _, _, cfg3 = pu.load_env(golden, overrides={"DIVIDE_SLIP_PROB": 0.1, "SLIP_FILL_MODE": 1})
+    assert lib.avgpu_check_cfg(C.byref(cfg3)) == -5
+    assert "SLIP_FILL_MODE" in lib.avgpu_last_error().decode()
+
+
+def test_recorded_draws_fill_modes(golden):
+    """The data fills draw once per filled site, after from / to (/ ins_loc):
+    SLIP_FILL_MODE 2 GetRandomInst, SLIP_FILL_MODE 3 and TRANS_FILL_MODE 1
+    GetInt(L - i) (cpu/cHardwareBase.cc:636-665, :721-741).  At u = 0.37 on
+    the 100-site ancestor: from = floor(0.37 * 101) = 37, to = 37 (L = 0, no
+    fill) -- so the stream puts from = 60, to = 20 (L = 40) instead."""
+    for ov, head, fills in [({"DIVIDE_SLIP_PROB": 1.0, "SLIP_FILL_MODE": 2}, [0.1, _u(60, 101), _u(20, 101)], 40),
+                            ({"DIVIDE_SLIP_PROB": 1.0, "SLIP_FILL_MODE": 3}, [0.1, _u(60, 101), _u(20, 101)], 40),
+                            ({"DIVIDE_TRANS_PROB": 1.0, "TRANS_FILL_MODE": 1},
+                             [0.9, 0.1, _u(60, 101), _u(20, 101), _u(5, 101)], 40)]:
+        iset, env, cfg, anc = _ancestor(golden, dict({"COPY_MUT_PROB": 0.0, "DIVIDE_INS_PROB": 0.0,
+                                                      "DIVIDE_DEL_PROB": 0.0, "DEATH_METHOD": 0}, **ov))
+        b = ol.Backend("oracle", cfg, iset, env, ncells=1)
+        b.set_orgs(0, [anc], deterministic=True)
+        b.set_rng_mode(capi.RNG_RECORDED, np.array(head + [0.37] * 4000))
+        for k in range(2000):
+            b.step(0, 1, uniform=1, mode=capi.MODE_FROZEN)
+            st, _, _ = b.states(0, 1, CAP)
+            if st[0].num_divides:
+                break
+        assert st[0].num_divides == 1
+        assert st[0].rng_counter == len(head) + fills + 3, ov      # + mut / ins / del tests
+        b.close()
+
+
+def _scramble(draws):
+    """the copied_so_far walk of doSlipMutation / doTransMutation
+    (cpu/cHardwareBase.cc:652-664): each draw picks the draw-th index not
+    taken yet"""
+    free = list(range(len(draws)))
+    return [free.pop(d) for d in draws]
+
+
+def _fill_cases(anc, nops):
+    """(overrides, stream, expected offspring), derived by hand from
+    doSlipMutation / doTransMutation on the 100-site ancestor."""
+    cases = []
+    # slip from 30 to 25 (L = 5): child = a[:30] + fill + a[30:]
+    codes = [5, 17, 0, 25, 9]
+    cases.append(({"DIVIDE_SLIP_PROB": 1.0, "SLIP_FILL_MODE": 2},
+                  [0.1, _u(30, 101), _u(25, 101)] + [_u(c, nops) for c in codes] + [0.9] * 3,
+                  anc[:30] + bytes(codes) + anc[30:]))
+    draws = [4, 0, 2, 0, 0]                  # -> indices 4, 0, 3, 1, 2
+    assert _scramble(draws) == [4, 0, 3, 1, 2]
+    cases.append(({"DIVIDE_SLIP_PROB": 1.0, "SLIP_FILL_MODE": 3},
+                  [0.1, _u(30, 101), _u(25, 101)] + [_u(d, 5 - i) for i, d in enumerate(draws)] + [0.9] * 3,
+                  anc[:30] + bytes(anc[25 + k] for k in [4, 0, 3, 1, 2]) + anc[30:]))
+    # translocation from 30 to 10 (L = 20) inserted at 15, scrambled with every
+    # draw 0 (indices in order): site 15 + i reads the sequence being filled at
+    # 10 + i, which for i >= 5 is a site this fill already wrote -- the fill is
+    # a[10:15] four times; then a[15:] after it
+    cases.append(({"DIVIDE_TRANS_PROB": 1.0, "TRANS_FILL_MODE": 1},
+                  [0.9, 0.1, _u(30, 101), _u(10, 101), _u(15, 101)] + [_u(0, 20 - i) for i in range(20)] + [0.9] * 3,
+                  anc[:15] + anc[10:15] * 4 + anc[15:]))
+    # scrambled without overlap: from 60 to 50 (L = 10) at 5
+    draws = [9, 0, 7, 1, 5, 0, 3, 2, 1, 0]
+    cases.append(({"DIVIDE_TRANS_PROB": 1.0, "TRANS_FILL_MODE": 1},
+                  [0.9, 0.1, _u(60, 101), _u(50, 101), _u(5, 101)] + [_u(d, 10 - i) for i, d in enumerate(draws)]
+                  + [0.9] * 3,
+                  anc[:5] + bytes(anc[50 + k] for k in _scramble(draws)) + anc[5:]))
+    return cases
+
+
+@pytest.mark.parametrize("kind", ["oracle", pytest.param("gpu", marks=pytest.mark.gpu)])
+def test_fill_mode_offspring_content(golden, kind):
+    """Offspring of recorded slips with SLIP_FILL_MODE 2 (random instructions)
+    and 3 (scrambled), and of scrambled translocations (TRANS_FILL_MODE 1,
+    including the read-back of sites the fill already wrote), against the
+    hand derivations of _fill_cases."""
+    iset = files.read_instset(os.path.join(golden, "instset-heads.cfg"))
+    anc = files.read_org(os.path.join(golden, "default-heads.org"), iset)
+    for ov, stream, want in _fill_cases(anc, len(iset.names)):
+        child, parent, pos, _, _ = first_offspring(kind, golden, ov, stream)
+        assert pos == len(stream), ov
+        assert child == want, (ov, list(child), list(want))
 
 
 def _u(k, n):
@@ -341,13 +424,17 @@ def test_recorded_stream_frozen_traces_gpu(golden, muts):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("fill", [0, 4])
+@pytest.mark.parametrize("fill", [0, 2, 3, 4])
 def test_divide_slip_uniform_world_gpu(golden, fill):
-    """World updates with DIVIDE_SLIP_PROB (SLIP_FILL_MODE 0 duplication / 4
-    nop-C) and DIVIDE_UNIFORM_PROB on top of the default mutations: GPU world
-    == oracle world, every cell digest, 120 updates."""
+    """World updates with DIVIDE_SLIP_PROB (SLIP_FILL_MODE 0 duplication, 2
+    random, 3 scrambled, 4 nop-C) and DIVIDE_UNIFORM_PROB on top of the default
+    mutations (with 2 / 3 also Poisson and per-site slips and scrambled
+    translocations): GPU world == oracle world, every cell digest, 120 updates."""
     ov = {"DIVIDE_SLIP_PROB": 0.1, "DIVIDE_UNIFORM_PROB": 0.1, "SLIP_FILL_MODE": fill,
           "WORLD_X": 48, "WORLD_Y": 48}
+    if fill in (2, 3):
+        ov.update({"DIVIDE_POISSON_SLIP_MEAN": 0.05, "DIV_SLIP_PROB": 0.0005,
+                   "DIVIDE_TRANS_PROB": 0.05, "TRANS_FILL_MODE": 1})
     iset, env, cfg, anc = _ancestor(golden, ov)
     n = 48 * 48
     pair = [ol.Backend(k, cfg, iset, env, ncells=n) for k in ("oracle", "gpu")]

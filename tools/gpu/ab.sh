@@ -1,7 +1,8 @@
 #!/bin/bash
 # A/B bench of variant libraries (avida_amd/libavida_gpu_<V>.so) on one box:
-#   run_ab.sh TAG V1 V2 ...   ("main" = the in-tree product library)
+#   tools/gpu/ab.sh TAG V1 V2 ...   ("main" = the in-tree product library)
 set -o pipefail
+cd "$(dirname "$0")/../.."
 mkdir -p gpurun_out
 TAG=$1; shift
 for V in "$@"; do

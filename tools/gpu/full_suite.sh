@@ -1,6 +1,7 @@
 #!/bin/bash
 # full GPU suite, phase clocks, bench (no CPU leg)
 set -o pipefail
+cd "$(dirname "$0")/../.."
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 TAG=${1:-r03}

@@ -1,7 +1,8 @@
 #!/bin/bash
 # selected GPU tests, bench, kernel-trace stats + per-update tail breakdown
-#   run_r03t.sh TAG [pytest -k expression]
+#   tools/gpu/tests_bench_trace.sh TAG [pytest -k expression]
 set -o pipefail
+cd "$(dirname "$0")/../.."
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 TAG=${1:-r03}

@@ -5,7 +5,7 @@ phase-clock points of interp.hip, compiled only with -DAVGPU_ISA_MARKS):
 
   hipcc -O3 --offload-arch=gfx950 -std=c++17 -ffp-contract=off \
       -DAVGPU_ISA_MARKS --offload-device-only -S -o marks.s avida_amd/csrc/interp.hip
-  python tools/isa_sections.py marks.s [336] [0] [Lb1ELb1ELb1]
+  python tools/isa_sections.py marks.s [320] [0] [Lb1ELb1ELb1]
 
 Counts are static (instructions between a marker and the next one in layout
 order), not executed counts: a section the compiler splits across blocks is
@@ -39,7 +39,7 @@ def classify(line):
 
 def main():
     path = sys.argv[1]
-    size = sys.argv[2] if len(sys.argv) > 2 else "336"
+    size = sys.argv[2] if len(sys.argv) > 2 else "320"
     rec = sys.argv[3] if len(sys.argv) > 3 else "0"
     flags = sys.argv[4] if len(sys.argv) > 4 else ""   # e.g. "Lb1ELb1ELb1" for the C0W/SIMPLE/DEF kernel
     text = open(path).read()

@@ -4,7 +4,7 @@ updates are the GPU's bit for bit)
 
 A class-0 slice spills when an h-alloc would grow the memory past
 CLASS0_SIZE; the slice then ends in the spill row after class 0, so from the
-end-of-update state: need_of(start) <= 336 and memory(end) > 336.  For those
+end-of-update state: need_of(start) <= 320 and memory(end) > 320.  For those
 organisms and for all other class-0 slices this prints the read head at the
 start of the update, to test "read head > CLASS0_SIZE / 3" as a predictor.
 
@@ -49,10 +49,10 @@ def main():
             s0, s1 = st0[c], st1[c]
             if not (s0.alive and s1.alive) or s1.birth_length != s0.birth_length:
                 continue
-            if need_of(s0.mem_size, s0.mal_active) > 336:
+            if need_of(s0.mem_size, s0.mal_active) > 320:
                 continue
             rec = (s0.head[1], s0.mem_size, s0.mal_active, s0.birth_length, s1.mem_size)
-            (spilled if s1.mem_size > 336 else quiet).append(rec)
+            (spilled if s1.mem_size > 320 else quiet).append(rec)
     sp, qu = np.array(spilled).reshape(-1, 5), np.array(quiet).reshape(-1, 5)
     print(f"{ups} updates of a {side}x{side} world after {burn}: class-0 slices {len(sp) + len(qu)}, "
           f"spilled {len(sp)} ({len(sp) / ups:.1f} per update)")

@@ -160,9 +160,12 @@ int setup_world(avgpu_world* w, int64_t n, bool test_buffers) {
   A(b_gest, R); A(b_ltask, AVGPU_NUM_LOGIC_TASKS * R); A(b_rng, 3 * R); A(b_target, R); A(b_state, R);
   A(b_prio, R); A(b_genome, (size_t)R * TAPE_SLOT);
   // placement scratch with two ghost rows (strip tiles)
-  A(occ, n + 2 * c.world_x); A(claim, n + 2 * c.world_x); A(claim2, n); A(owner, n + 2 * c.world_x);
+  // occupancy, owners and the four placement rounds' claims, each with the two
+  // ghost rows a strip tile keeps after its n cells
+  const int64_t ng = n + 2 * (int64_t)c.world_x;
+  A(occ, ng); A(claim, ng); A(claim2, ng); A(owner, ng);
   W.claim_r[0] = W.claim; W.claim_r[1] = W.claim2;
-  A(claim_r[2], n); A(claim_r[3], n); A(b_tgt, 4 * R);
+  A(claim_r[2], ng); A(claim_r[3], ng); A(b_tgt, 4 * R);
   if (test_buffers) {
     A(t_flags, (size_t)n * TAPE_SLOT); A(t_flags_len, n); A(t_child, (size_t)n * TAPE_SLOT);
     A(t_child_len, n);
@@ -1419,7 +1422,8 @@ int avgpu_tile_begin(avgpu_world* w, const double* dev_gathered, int ntiles) {
     return fail(AVGPU_ESTATE, "spatial resources need avgpu_set_tile_res_buffers");
   if (!dev_gathered || ntiles < 1) return fail(AVGPU_EINVAL, "gathered partials");
   launch_tile_totals(w->W, w->stream, dev_gathered, ntiles, w->d_totals);
-  launch_world_pre(w->W, w->stream, w->d_totals, w->ev_fork, (uint32_t)w->update);
+  // (the counters were cleared by avgpu_tile_partials' launch)
+  launch_world_pre(w->W, w->stream, w->d_totals, w->ev_fork, (uint32_t)w->update, false);
   after_resources_begin(w);
   HIPCHK(hipGetLastError());
   rc = interpret(w, AVGPU_MODE_WORLD, 0, w->W.n, true);
@@ -1433,8 +1437,8 @@ int avgpu_tile_begin(avgpu_world* w, const double* dev_gathered, int ntiles) {
 int avgpu_tile_place(avgpu_world* w, int round, int phase) {
   int rc = tile_ready(w);
   if (rc < 0) return rc;
-  if (round < 0 || round > 3 || phase < 0 || phase > 3 || (phase >= 2 && round != 3))
-    return fail(AVGPU_EINVAL, "round 0..3 with phase 0..1; phases 2, 3 after round 3");
+  if (round < 0 || round > 3 || phase < 0 || phase > 2 || (phase >= 1 && round != 3))
+    return fail(AVGPU_EINVAL, "round 0..3 with phase 0; phases 1, 2 after round 3");
   launch_tile_place(w->W, w->stream, round, phase);
   HIPCHK(hipGetLastError());
   return 0;

@@ -163,10 +163,11 @@ struct DevWorld {
   // placement scratch, n cells + 2 ghost rows (strip tiles, below)
   uint8_t* occ;       // [n + 2X]
   unsigned long long* claim; // [n + 2X]
-  unsigned long long* claim2; // [n] (claim_r[1])
-  // a single world's placement rounds 0..3 claim into their own arrays
-  // (k_place_round): claim_r[0] = claim, [1] = claim2, [2], [3] [n] each; all
-  // zero between updates
+  unsigned long long* claim2; // [n + 2X] (claim_r[1])
+  // placement rounds 0..3 claim into their own arrays (k_place_round,
+  // k_tile_round): claim_r[0] = claim, [1] = claim2, [2], [3], [n + 2X] each;
+  // all zero between updates (records clear theirs at activation, k_allot
+  // round 3's, k_tile_prep the ghost rows)
   unsigned long long* claim_r[4];
   int32_t* b_tgt;     // [4][rcap] the record's target in each placement round it claimed in
   int32_t* owner;     // [n + 2X]  record id, -1 none, REMOTE_OWNER(k) won by a halo birth in round k
@@ -277,8 +278,9 @@ struct DevWorld {
   int32_t row0, global_rows, rows, tiled;
   int64_t cell0;          // row0 * world_x: global id of local cell 0 (RNG keys, priorities)
   // halo buffers per direction d (0: tile above, 1: tile below), registered by
-  // the host: halo_bytes(X) = X u64 claims on the receiver's edge row, X u64
-  // the sender's own claims on its edge row, X u8 edge-row occupancy
+  // the host: halo_bytes(X) = per round parity X u64 claims on the receiver's
+  // edge row and X u64 the sender's own claims on its edge row, then X u8
+  // edge-row occupancy (world.hip halo_cl / halo_occ)
   uint8_t* h_send[2];
   uint8_t* h_recv[2];
   // birth-record buffers per direction: HaloHdr, X HaloRec, arena of r_arena bytes
@@ -288,7 +290,7 @@ struct DevWorld {
 };
 
 #define REMOTE_OWNER(k) (-2 - (k))
-__host__ __device__ inline int64_t halo_bytes(int x) { return ((int64_t)x * 17 + 15) / 16 * 16; }
+__host__ __device__ inline int64_t halo_bytes(int x) { return ((int64_t)x * 33 + 15) / 16 * 16; }
 struct HaloHdr { int32_t count, arena_used, overflow, pad; };
 // one offspring placed across a tile edge (the migrant record of
 // cMultiProcessWorld.cc:142-190, restated for strip tiles)
@@ -574,7 +576,7 @@ bool class_timing_all();   // AVGPU_CLASS_TIMING (interp.hip)
 void launch_world_begin(const DevWorld& W, hipStream_t s, double* d_totals, double* d_scratch,
                         hipEvent_t lists_ready, uint32_t update);
 void launch_world_pre(const DevWorld& W, hipStream_t s, const double* d_totals, hipEvent_t lists_ready,
-                      uint32_t update);
+                      uint32_t update, bool reset = true);
 // allotment draw of organism (lo, hi) in update u (oracle allot_draw)
 __device__ __forceinline__ uint32_t allot_draw(uint32_t lo, uint32_t hi, uint32_t update) {
   return lowbias32(lowbias32(update * 0x85EBCA6BU + hi) ^ lo ^ 0x27D4EB2FU);

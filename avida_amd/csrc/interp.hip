@@ -1358,7 +1358,7 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
                 st_async_u32(b_parent + rec, (uint32_t)cell);
                 st_async_u32(b_seq + rec, (uint32_t)nd);
                 st_async_u32(b_len + rec, (uint32_t)len);
-                st_async_u32(b_len0 + rec, (uint32_t)child);   // k_apply_mutations edits the copy
+                st_async_u32(b_len0 + rec, (uint32_t)child);   // the placement launch edits the copy
                 st_async_u32(b_edit + rec, (uint32_t)e0);
                 st_async_u32(b_edit + rcap + rec, (uint32_t)e1);
                 st_async_u32(b_edit + 2 * rcap + rec, (uint32_t)e2);
@@ -1421,7 +1421,7 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
             }
           } else if (mode == AVGPU_MODE_WORLD && rec >= 0) {
             // the unmutated child, 4 sites per lane; its divide mutations are
-            // applied by k_apply_mutations (world.hip) before placement, from
+            // applied by k_place_pick_mut / k_tile_prep (world.hip) before placement, from
             // the edits stored with the record -- keeping the per-site edit
             // composition out of this kernel's registers
             uint8_t* g = W.b_genome + (int64_t)rec * TAPE_SLOT;

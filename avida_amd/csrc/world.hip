@@ -3,8 +3,8 @@
 //   k_get_states     cHardwareBase inspection API (trace tuple gather)
 //   k_classify_*     budget + LDS size-class lists for k_interpret
 //   k_merit_*        deterministic total merit (scheduler input)
-//   k_allot          merit-weighted time slicing (cScheduler restated)
-//   k_place_*        cPopulation::PositionOffspring in conflict-resolving rounds
+//   k_allot_total    merit-weighted time slicing (cScheduler restated)
+//   k_place_*, k_tile_*  cPopulation::PositionOffspring in conflict-resolving rounds
 //   k_activate       cPopulation::ActivateOrganism + cPhenotype::SetupOffspring
 //   k_stats          cStats reduction inputs
 // Paths are relative to avida-core/source/ of the reference.
@@ -378,12 +378,26 @@ __global__ __launch_bounds__(256) void k_merit_final(const double* partial, cons
   long long c = 0;
   double acc = 0.0;
   const int64_t total = TILES ? nb * ntiles : nb;
-  for (int64_t b = threadIdx.x; b < total; b += 256) {
-    if (TILES) {
-      const int64_t k = b / nb, j = b - k * nb;
-      acc = __dadd_rn(acc, gathered[k * 2 * nb + j]);
-      c += (long long)gathered[k * 2 * nb + nb + j];
-    } else {
+  if (TILES) {
+    // entry b = tile k, block j of the gathered vector, walked without a
+    // division per entry; the loads of 8 entries go out before their adds
+    int64_t k = threadIdx.x / nb, j = threadIdx.x - k * nb;
+    for (int64_t b0 = threadIdx.x; b0 < total; b0 += 256 * 8) {
+      double v[8], a[8];
+#pragma unroll
+      for (int u = 0; u < 8; u++) {
+        const bool in = b0 + 256 * u < total;
+        v[u] = in ? gathered[k * 2 * nb + j] : 0.0;
+        a[u] = in ? gathered[k * 2 * nb + nb + j] : 0.0;
+        j += 256;
+        while (j >= nb) { j -= nb; k++; }
+      }
+#pragma unroll
+      for (int u = 0; u < 8; u++)
+        if (b0 + 256 * u < total) { acc = __dadd_rn(acc, v[u]); c += (long long)a[u]; }
+    }
+  } else {
+    for (int64_t b = threadIdx.x; b < total; b += 256) {
       c += alive_partial[b];
       acc = __dadd_rn(acc, partial[b]);
     }
@@ -449,32 +463,23 @@ __device__ __forceinline__ int allot_cell(const DevWorld& W, int64_t c, double s
   }
 }
 
-__global__ void k_allot(DevWorld W, const double* totals, uint32_t update) {
-  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  bool want = false;
-  int cls = 0;
-  if (c < W.n) {
-    allot_cell(W, c, totals[0], totals[1], update, want, cls);
-    occ_init_cell(W, c);   // as in k_allot_total (tiles re-initialise with their ghost rows)
-    W.claim_r[3][c] = 0ull;
-  }
-  const unsigned long long m = __ballot(want);
-  if ((threadIdx.x & 63) == 0 && m) count_add(W, CNT_SLICES, (unsigned long long)__popcll(m));
-  enqueue_class(W, (int)c, want, cls);
-}
 
 // A single world's allotment with its total merit (k_merit_final + k_allot
 // in one launch): blocks of 1024 threads, two cells per thread.  Each block
 // first recomputes the total merit from the block partials of k_merit_partial
 // in k_merit_final's fixed order (lane t sums partials t, t+256, ..., then the
 // pairwise tree), so every block holds the same bits; block 0 stores them.
+// partial == nullptr (strip tiles): the totals are already in `totals`
+// (k_merit_final<true> over the gathered partials of every strip)
 __global__ __launch_bounds__(1024) void k_allot_total(DevWorld W, const double* partial,
                                                       const int32_t* alive_partial, int64_t nb,
                                                       double* totals, uint32_t update) {
   __shared__ double s_sum[256];
   __shared__ long long s_cnt[256];
   const int tid = threadIdx.x;
-  if (tid < 256) {
+  if (!partial) {
+    if (tid == 0) { s_sum[0] = totals[0]; s_cnt[0] = (long long)totals[1]; }
+  } else if (tid < 256) {
     double acc = 0.0;
     long long cnt = 0;
     for (int64_t b0 = tid; b0 < nb; b0 += 256 * 8) {
@@ -494,15 +499,17 @@ __global__ __launch_bounds__(1024) void k_allot_total(DevWorld W, const double* 
     s_cnt[tid] = cnt;
   }
   __syncthreads();
-  for (int stride = 128; stride >= 1; stride >>= 1) {
-    if (tid < stride) {
-      s_sum[tid] = __dadd_rn(s_sum[tid], s_sum[tid + stride]);
-      s_cnt[tid] += s_cnt[tid + stride];
+  if (partial) {
+    for (int stride = 128; stride >= 1; stride >>= 1) {
+      if (tid < stride) {
+        s_sum[tid] = __dadd_rn(s_sum[tid], s_sum[tid + stride]);
+        s_cnt[tid] += s_cnt[tid + stride];
+      }
+      __syncthreads();
     }
-    __syncthreads();
   }
   const double sum = s_sum[0], alive = (double)s_cnt[0];
-  if (blockIdx.x == 0 && tid == 0) { totals[0] = sum; totals[1] = alive; }
+  if (partial && blockIdx.x == 0 && tid == 0) { totals[0] = sum; totals[1] = alive; }
   for (int h = 0; h < 2; h++) {
     const int64_t c = (int64_t)blockIdx.x * 2048 + h * 1024 + tid;
     bool want = false;
@@ -589,10 +596,60 @@ __global__ __launch_bounds__(1024) void k_window_count(DevWorld W) {
 // its 64 organisms from a window of SORT_WIN cells sorted by budget
 // (k_window_count above).
 
-__global__ void k_occ_init(DevWorld W) {
-  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int64_t ext = W.n + (W.tiled ? 2 * (int64_t)W.world_x : 0);
-  if (c < ext) occ_init_cell(W, c);
+// ---- strip-tile halo (DESIGN.md "Multi-GPU") ----
+// Edge rows: top = local row 0, bottom = local row rows-1; ghost rows after n.
+__device__ __forceinline__ int64_t edge_cell(const DevWorld& W, int d, int x) {
+  return d == 0 ? (int64_t)x : (int64_t)(W.rows - 1) * W.world_x + x;
+}
+__device__ __forceinline__ int64_t ghost_cell(const DevWorld& W, int d, int x) {
+  return W.n + (int64_t)d * W.world_x + x;
+}
+// Halo buffer (one per direction): per round parity p = round & 1, [X u64]
+// the sender's claims on the receiver's edge row (its ghost row, k = 0) and
+// [X u64] the sender's own claims on its edge row (the receiver's ghost row,
+// k = 1); then [X u8] the sender's edge-row occupancy after interpretation.
+// A cell of an edge row is claimed only from the two strips it touches, so
+// after ONE exchange per placement round both strips know every claim on
+// both rows and resolve them alike; the parities let round m + 1's claims
+// go out while round m's are still being read (DESIGN.md "Multi-GPU").
+__device__ __forceinline__ unsigned long long* halo_cl(uint8_t* b, int X, int p, int k) {
+  return reinterpret_cast<unsigned long long*>(b) + (int64_t)(2 * p + k) * X;
+}
+__device__ __forceinline__ uint8_t* halo_occ(uint8_t* b, int X) { return b + (int64_t)X * 32; }
+// which halo slot a cell maps to: d = direction, x = column, k = 0 for a
+// ghost cell (my claims on the neighbour's edge), 1 for an edge cell
+__device__ __forceinline__ bool halo_slot(const DevWorld& W, int64_t c, int& d, int& x, bool& ghost) {
+  const int X = W.world_x;
+  if (c >= W.n) { const int64_t k = c - W.n; d = (int)(k / X); x = (int)(k - (int64_t)d * X); ghost = true; return true; }
+  ghost = false;
+  if (c < X) { d = 0; x = (int)c; return true; }
+  if (c >= W.n - X) { d = 1; x = (int)(c - (W.n - X)); return true; }
+  return false;
+}
+// a tile's cell is taken for round m's pick: occupied before round m - 1's
+// resolve, or claimed in round m - 1 -- here, or by the neighbour on my edge
+// row / on its own edge row (my ghost row): every claimed cell gets a winner,
+// so this is the occupancy round m - 1's resolve leaves, read before that
+// resolve (in the same launch) has written it.  Round 0 reads the ghost
+// rows' occupancy straight from the received halo.
+__device__ __forceinline__ bool tile_taken(const DevWorld& W, int64_t c, int m) {
+  int d, x;
+  bool ghost;
+  const bool h = halo_slot(W, c, d, x, ghost);
+  if (m == 0) return (h && ghost) ? halo_occ(W.h_recv[d], W.world_x)[x] != 0 : W.occ[c] != 0;
+  if (W.occ[c] || W.claim_r[m - 1][c] != 0ull) return true;
+  return h && halo_cl(W.h_recv[d], W.world_x, (m - 1) & 1, ghost ? 1 : 0)[x] != 0ull;
+}
+// round m's merged claim on cell t: mine, the neighbour's
+__device__ __forceinline__ unsigned long long tile_merged(const DevWorld& W, int64_t t, int m) {
+  unsigned long long v = W.claim_r[m][t];
+  int d, x;
+  bool ghost;
+  if (halo_slot(W, t, d, x, ghost)) {
+    const unsigned long long o = halo_cl(W.h_recv[d], W.world_x, m & 1, ghost ? 1 : 0)[x];
+    if (o > v) v = o;
+  }
+  return v;
 }
 
 // claim / prev: this round's claim array and (single world) the previous
@@ -602,9 +659,13 @@ __global__ void k_occ_init(DevWorld W) {
 // claim array -- a cell claimed there has a winner of that round, so it is
 // occupied for this round's pick whether or not that winner's resolve (in the
 // same launch) has marked occ yet; round: the claim's round (b_tgt row)
+// tile_m >= 0 (strip tiles, k_tile_round): occupancy by tile_taken, and a
+// claim on an edge or ghost cell also goes into the halo send slot of its
+// round's parity (atomicMax: the exchange after the launch carries it)
 __device__ __forceinline__ void place_pick_one(const DevWorld& W, int64_t i, unsigned long long* claim,
                                                unsigned long long* prev,
-                                               const unsigned long long* occ_prev = nullptr, int round = -1) {
+                                               const unsigned long long* occ_prev = nullptr, int round = -1,
+                                               int tile_m = -1) {
   const int64_t r = (round >= 0) ? i : rec_of(W, i);
   if (prev) {
     const int t0 = W.b_target[r];
@@ -618,7 +679,8 @@ __device__ __forceinline__ void place_pick_one(const DevWorld& W, int64_t i, uns
   int nc = 0;
   if (W.prefer_empty)
     for (int k = 0; k < nn; k++)
-      if (!W.occ[nbr[k]] && !(occ_prev && occ_prev[nbr[k]] != 0ull)) cand[nc++] = nbr[k];
+      if (tile_m >= 0 ? !tile_taken(W, nbr[k], tile_m)
+                      : (!W.occ[nbr[k]] && !(occ_prev && occ_prev[nbr[k]] != 0ull))) cand[nc++] = nbr[k];
   if (nc == 0 && W.birth_method != 3) {
     for (int k = 0; k < nn; k++) cand[nc++] = nbr[k];
     if (W.allow_parent) cand[nc++] = parent;
@@ -637,17 +699,19 @@ __device__ __forceinline__ void place_pick_one(const DevWorld& W, int64_t i, uns
   W.b_prio[r] = prio;
   if (round >= 0) W.b_tgt[(int64_t)round * W.rcap + r] = t;
   atomicMax(&claim[t], prio);
+  if (tile_m >= 0) {
+    int d, x;
+    bool ghost;
+    if (halo_slot(W, t, d, x, ghost)) atomicMax(&halo_cl(W.h_send[d], W.world_x, tile_m & 1, ghost ? 0 : 1)[x], prio);
+  }
 }
 
-// divide-mutation scan: queue entries per wave (k_apply_mutations, k_place_pick_mut)
+// divide-mutation scan: queue entries per wave (k_place_pick_mut, k_tile_prep)
 #define MUT_PER_WAVE 8
 // grid-stride over the birth queue (its length is only known on the device)
 #define QUEUE_LOOP(i) \
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, _qn = queue_len(W); i < _qn; \
        i += (int64_t)gridDim.x * blockDim.x)
-__global__ void k_place_pick(DevWorld W, unsigned long long* claim, unsigned long long* prev) {
-  QUEUE_LOOP(i) place_pick_one(W, i, claim, prev);
-}
 // A single world's placement round m = 1..3 in one launch: the resolve of
 // round m-1 and the pick of round m.  Each round has its own claim array
 // (W.claim_r[m]), so round m-1's claims stay intact for the whole launch: a
@@ -673,7 +737,8 @@ __global__ void k_place_round(DevWorld W, int m) {
   }
 }
 // Round 0 of a single world's placement with the divide mutations beside it:
-// blocks [0, pblocks) pick; the rest apply the edits (as k_apply_mutations,
+// blocks [0, pblocks) pick; the rest apply the edits (a wave per 8 queue
+// entries, rewriting the ~10 % of genomes that have edits one after the other;
 // 4 waves per block) -- placement reads no genome, so the two are independent
 // and share one launch instead of two latency-bound ones.
 // fused: the single world's round arrays (claim rows and b_tgt, k_place_round)
@@ -709,155 +774,108 @@ __global__ __launch_bounds__(256) void k_place_pick_mut(DevWorld W, unsigned lon
     }
   }
 }
-// ---- strip-tile halo (DESIGN.md "Multi-GPU") ----
-// Edge rows: top = local row 0, bottom = local row rows-1; ghost rows after n.
-__device__ __forceinline__ int64_t edge_cell(const DevWorld& W, int d, int x) {
-  return d == 0 ? (int64_t)x : (int64_t)(W.rows - 1) * W.world_x + x;
-}
-__device__ __forceinline__ int64_t ghost_cell(const DevWorld& W, int d, int x) {
-  return W.n + (int64_t)d * W.world_x + x;
-}
-// Halo buffer (one per direction): [X u64] the sender's claims on the
-// receiver's edge row (its ghost row), [X u64] the sender's own claims on its
-// edge row (the receiver's ghost row), [X u8] the sender's edge-row occupancy.
-// A cell of an edge row is claimed only from the two strips it touches, so
-// after ONE exchange per placement round both strips know every claim on
-// both rows and resolve them alike (DESIGN.md "Multi-GPU").
-__device__ __forceinline__ unsigned long long* halo_claims(uint8_t* b) {
-  return reinterpret_cast<unsigned long long*>(b);
-}
-__device__ __forceinline__ unsigned long long* halo_own(uint8_t* b, int X) {
-  return reinterpret_cast<unsigned long long*>(b) + X;
-}
-__device__ __forceinline__ uint8_t* halo_occ(uint8_t* b, int X) { return b + (int64_t)X * 16; }
 
-// what: 0 edge-row occupancy (after interpretation); 1 this round's claims
-// (on the ghost rows, on the own edge rows)
-__global__ void k_halo_export(DevWorld W, int what) {
-  const int X = W.world_x;
-  const int g = blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= 2 * X) return;
-  const int d = g / X, x = g - d * X;
-  uint8_t* b = W.h_send[d];
-  const int64_t c = edge_cell(W, d, x);
-  if (what == 1) {
-    halo_claims(b)[x] = W.claim[ghost_cell(W, d, x)];
-    halo_own(b, X)[x] = W.claim[c];
-  } else {
-    halo_occ(b, X)[x] = W.occ[c];
-    halo_claims(b)[x] = 0ull;
-    halo_own(b, X)[x] = 0ull;
-  }
-}
 
-// ghost occupancy from the neighbours' edge rows (before round 0's pick)
-__global__ void k_halo_import_occ(DevWorld W) {
-  const int X = W.world_x;
-  const int g = blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= 2 * X) return;
-  const int d = g / X, x = g - d * X;
-  W.occ[ghost_cell(W, d, x)] = halo_occ(W.h_recv[d], X)[x];
-}
-
-// the claim of the round on cell t with the neighbours' claims merged in
-__device__ __forceinline__ unsigned long long merged_claim(const DevWorld& W, int64_t t) {
-  unsigned long long m = W.claim[t];
-  const int X = W.world_x;
-  if (t >= W.n) {
-    const int64_t k = t - W.n;
-    const int d = (int)(k / X);
-    const unsigned long long o = halo_own(W.h_recv[d], X)[k - (int64_t)d * X];
-    return o > m ? o : m;
-  }
-  int d = -1, x = 0;
-  if (t < X) { d = 0; x = (int)t; }
-  else if (t >= W.n - X) { d = 1; x = (int)(t - (W.n - X)); }
-  if (d >= 0) {
-    const unsigned long long r = halo_claims(W.h_recv[d])[x];
-    if (r > m) m = r;
-  }
-  return m;
-}
-
-// One launch per placement round after its exchange: blocks [0, rblocks)
-// resolve this tile's records (targets inside the tile and on the ghost rows)
-// against the merged claims; the rest walk the 2 x X halo cells: an edge cell
-// whose maximum claim came from the neighbour is that round's remote winner's
-// (owner REMOTE_OWNER(round), occupied), a ghost cell with any claim is
-// occupied for the next round's pick (its winner is placed, here or there).
-__global__ void k_tile_resolve(DevWorld W, int round, int rblocks) {
-  if ((int)blockIdx.x < rblocks) {
+// ---- strip tiles' placement: one launch per round (DESIGN.md "Multi-GPU") ----
+// k_tile_prep, after interpretation: blocks [0, mblocks) apply the divide
+// mutations (as k_place_pick_mut's extra blocks); the rest walk the 2 x X
+// halo cells: the ghost rows empty (occ, owner, every round's claims), the
+// edge rows' occupancy into the send buffers and both parities' claim slots
+// zeroed.  (k_allot initialised the tile's own cells.)
+__global__ __launch_bounds__(256) void k_tile_prep(DevWorld W, int mblocks) {
+  __shared__ uint8_t child[4][TAPE_SLOT + 16];
+  if ((int)blockIdx.x < mblocks) {
     const int nb = queue_len(W);
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nb;
-         i += (int64_t)rblocks * blockDim.x) {
-      const int64_t r = rec_of(W, i);
-      if (W.b_state[r] != 0) continue;
-      const int t = W.b_target[r];
-      if (merged_claim(W, t) == W.b_prio[r]) {
-        W.b_state[r] = (int8_t)(1 + round);
-        W.occ[t] = 1;
-        W.owner[t] = (int)r;
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int64_t wave = (int64_t)blockIdx.x * 4 + wv, nwaves = (int64_t)mblocks * 4;
+    for (int64_t q0 = wave * MUT_PER_WAVE; q0 < nb; q0 += nwaves * MUT_PER_WAVE) {
+      const int64_t q = q0 + lane;
+      int64_t r = 0;
+      bool any = false;
+      if (lane < MUT_PER_WAVE && q < nb) {
+        r = rec_of(W, q);
+        int e = 0;
+#pragma unroll
+        for (int k = 0; k < 5; k++) e |= W.b_edit[(int64_t)k * W.rcap + r];
+        if (W.seg_any)
+          for (int k = 0; k < NSEG; k++) e |= W.b_pcnt[(int64_t)k * W.rcap + r];
+        any = e != 0;
+      }
+      for (unsigned long long m = __ballot(any); m; m &= m - 1ull) {
+        const int L = __ffsll((long long)m) - 1;
+        apply_edits_wave(W, (int64_t)__shfl((long long)r, L), child[wv]);
       }
     }
     return;
   }
   const int X = W.world_x;
-  const int g = (blockIdx.x - rblocks) * blockDim.x + threadIdx.x;
+  const int g = (blockIdx.x - mblocks) * blockDim.x + threadIdx.x;
   if (g >= 2 * X) return;
   const int d = g / X, x = g - d * X;
-  const int64_t c = edge_cell(W, d, x);
-  const unsigned long long rc = halo_claims(W.h_recv[d])[x];
-  if (rc != 0ull && rc > W.claim[c]) { W.owner[c] = REMOTE_OWNER(round); W.occ[c] = 1; }
   const int64_t gc = ghost_cell(W, d, x);
-  if (W.claim[gc] != 0ull || halo_own(W.h_recv[d], X)[x] != 0ull) W.occ[gc] = 1;
+  W.occ[gc] = 0;
+  W.owner[gc] = -1;
+#pragma unroll
+  for (int k = 0; k < 4; k++) W.claim_r[k][gc] = 0ull;
+  uint8_t* b = W.h_send[d];
+  halo_occ(b, X)[x] = W.occ[edge_cell(W, d, x)];
+#pragma unroll
+  for (int k = 0; k < 4; k++) halo_cl(b, X, k >> 1, k & 1)[x] = 0ull;
 }
 
-// The round's claims cleared: blocks [0, rblocks) at this tile's records'
-// targets, the rest on the edge and ghost rows wholesale (remote records
-// claim there without being in this tile's queue).
-__global__ void k_tile_clear(DevWorld W, int rblocks) {
+// Round m of a tile's placement, after round m - 1's exchange: blocks
+// [0, rblocks) take the records -- resolve round m - 1 against the merged
+// claims (a winner takes its cell), then a pending record picks for round m
+// (tile_taken: the occupancy that resolve leaves); the rest walk the halo
+// cells -- round 0 imports the ghost rows' occupancy, later rounds mark round
+// m - 1's remote winners on the edge rows (owner REMOTE_OWNER(m - 1)) and the
+// claimed ghost cells occupied, and clear the send parity of round m + 1
+// (its last contents, round m - 1's, went out before this launch).
+// m = 4: the last resolve only (records + halo cells), and the record
+// buffers' headers cleared for k_halo_pack.
+__global__ __launch_bounds__(256) void k_tile_round(DevWorld W, int m, int rblocks) {
+  const int X = W.world_x;
   if ((int)blockIdx.x < rblocks) {
     const int nb = queue_len(W);
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nb;
-         i += (int64_t)rblocks * blockDim.x) {
-      const int t = W.b_target[rec_of(W, i)];
-      if (t >= 0) W.claim[t] = 0ull;
+    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < nb; q += (int64_t)rblocks * blockDim.x) {
+      const int64_t r = rec_of(W, q);
+      if (W.b_state[r] != 0) continue;
+      if (m > 0) {
+        const int t = W.b_target[r];
+        if (tile_merged(W, t, m - 1) == W.b_prio[r]) {   // won round m - 1
+          W.b_state[r] = (int8_t)m;
+          W.occ[t] = 1;
+          W.owner[t] = (int)r;
+          continue;
+        }
+      }
+      if (m < 4) place_pick_one(W, r, W.claim_r[m], nullptr, nullptr, m, m);
     }
     return;
   }
-  const int X = W.world_x;
   const int g = (blockIdx.x - rblocks) * blockDim.x + threadIdx.x;
+  if (m == 4 && g < 2) {
+    HaloHdr* hdr = reinterpret_cast<HaloHdr*>(W.r_send[g]);
+    hdr->count = 0;
+    hdr->arena_used = 0;
+    hdr->overflow = 0;
+  }
   if (g >= 2 * X) return;
   const int d = g / X, x = g - d * X;
-  W.claim[edge_cell(W, d, x)] = 0ull;
-  W.claim[ghost_cell(W, d, x)] = 0ull;
-}
-
-// The divide mutations of the queued offspring: a wave per 8 queue entries --
-// lanes 0..7 read their records' edit words, and the wave rewrites, one after
-// the other, the genomes that have any (about one in ten births at the
-// default rates).  A wave per entry made ~60k short-lived waves for ~6k edits.
-__global__ __launch_bounds__(64) void k_apply_mutations(DevWorld W) {
-  __shared__ uint8_t child[TAPE_SLOT + 16];
-  const int nb = queue_len(W);
-  const int lane = threadIdx.x;
-  for (int64_t q0 = (int64_t)blockIdx.x * MUT_PER_WAVE; q0 < nb; q0 += (int64_t)gridDim.x * MUT_PER_WAVE) {
-    const int64_t q = q0 + lane;
-    int64_t r = 0;
-    bool any = false;
-    if (lane < MUT_PER_WAVE && q < nb) {
-      r = rec_of(W, q);
-      int e = 0;
-#pragma unroll
-      for (int k = 0; k < 5; k++) e |= W.b_edit[(int64_t)k * W.rcap + r];
-      if (W.seg_any)
-        for (int k = 0; k < NSEG; k++) e |= W.b_pcnt[(int64_t)k * W.rcap + r];
-      any = e != 0;
-    }
-    for (unsigned long long m = __ballot(any); m; m &= m - 1ull) {
-      const int L = __ffsll((long long)m) - 1;
-      apply_edits_wave(W, (int64_t)__shfl((long long)r, L), child);
-    }
+  const int64_t gc = ghost_cell(W, d, x);
+  if (m == 0) {
+    W.occ[gc] = halo_occ(W.h_recv[d], X)[x];
+    return;
+  }
+  const int p = (m - 1) & 1;
+  const int64_t c = edge_cell(W, d, x);
+  const unsigned long long rc = halo_cl(W.h_recv[d], X, p, 0)[x];
+  if (rc != 0ull && rc > W.claim_r[m - 1][c]) { W.owner[c] = REMOTE_OWNER(m - 1); W.occ[c] = 1; }
+  if (W.claim_r[m - 1][gc] != 0ull || halo_cl(W.h_recv[d], X, p, 1)[x] != 0ull) W.occ[gc] = 1;
+  if (m == 1 || m == 2) {                      // round m + 1's send parity = round m - 1's
+    uint8_t* b = W.h_send[d];
+    halo_cl(b, X, p, 0)[x] = 0ull;
+    halo_cl(b, X, p, 1)[x] = 0ull;
   }
 }
 
@@ -882,6 +900,9 @@ __global__ __launch_bounds__(64) void k_apply_mutations(DevWorld W) {
 // it unless a round-3 claim landed there (claim_r[3] != 0: that claim's winner
 // is placed later and owns it).  Rounds 0-2's claims are cleared here by each
 // record; round 3's, which this launch reads, by k_stats_partial.
+// fused 2 (strip tiles, k_tile_round): the owners are final (round 3 was
+// resolved before the halo records were packed), the claims are cleared as
+// in the fused single world
 __global__ __launch_bounds__(64) void k_activate(DevWorld W, unsigned long long* last, int fused) {
   const int nb = queue_len(W);
   unsigned long long born = 0, over = 0;
@@ -893,10 +914,14 @@ __global__ __launch_bounds__(64) void k_activate(DevWorld W, unsigned long long*
     if (last && tgt >= 0) last[tgt] = 0ull;
     bool won;
     if (fused) {
-      const unsigned long long c3 = tgt >= 0 ? W.claim_r[3][tgt] : 0ull;
-      if (st == 0) won = tgt >= 0 && c3 == W.b_prio[i];   // round 3's winner
-      else won = W.owner[tgt] == (int)i && c3 == 0ull;
-      const int lastr = st == 0 ? 3 : st - 1;              // the last round it claimed in
+      if (fused == 2) {
+        won = st > 0 && tgt >= 0 && W.owner[tgt] == (int)i;
+      } else {
+        const unsigned long long c3 = tgt >= 0 ? W.claim_r[3][tgt] : 0ull;
+        if (st == 0) won = tgt >= 0 && c3 == W.b_prio[i];   // round 3's winner
+        else won = W.owner[tgt] == (int)i && c3 == 0ull;
+      }
+      const int lastr = (st == 0 || st > 4) ? 3 : st - 1;  // the last round it claimed in
       for (int k = 0; k < lastr && k < 3; k++) {
         const int tk = W.b_tgt[(int64_t)k * W.rcap + i];
         if (tk >= 0) W.claim_r[k][tk] = 0ull;
@@ -922,15 +947,25 @@ __global__ __launch_bounds__(64) void k_activate(DevWorld W, unsigned long long*
 
 // Winners of ghost-row cells -> record buffer of that direction (one wave per
 // queued birth; one record per ghost cell at most: its last winner here).
+// The lanes of a wave test 64 queued births at once; the wave then packs the
+// few that won a ghost cell one after the other (a wave per queued birth
+// spent ~40 us per update on the test alone).
 __global__ __launch_bounds__(64) void k_halo_pack(DevWorld W) {
   const int nb = queue_len(W);
   const int lane = threadIdx.x;
   const int X = W.world_x;
   unsigned long long sent = 0, lost = 0;
-  for (int64_t q = blockIdx.x; q < nb; q += gridDim.x) {
-    const int64_t i = rec_of(W, q);
+  for (int64_t q0 = (int64_t)blockIdx.x * 64; q0 < nb; q0 += (int64_t)gridDim.x * 64) {
+    const int64_t q = q0 + lane;
+    int64_t mine = -1;
+    if (q < nb) {
+      const int64_t i = rec_of(W, q);
+      const int tgt = W.b_target[i];
+      if (W.b_state[i] > 0 && tgt >= W.n && W.owner[tgt] == (int)i) mine = i;
+    }
+    for (unsigned long long m = __ballot(mine >= 0); m; m &= m - 1ull) {
+    const int64_t i = (int64_t)__shfl((long long)mine, __ffsll((long long)m) - 1);
     const int tgt = W.b_target[i];
-    if (W.b_state[i] <= 0 || tgt < W.n || W.owner[tgt] != (int)i) continue;
     const int d = (tgt - (int)W.n) / X, col = (tgt - (int)W.n) - d * X;
     const int len = W.b_len[i];
     HaloHdr* hdr = reinterpret_cast<HaloHdr*>(W.r_send[d]);
@@ -964,6 +999,7 @@ __global__ __launch_bounds__(64) void k_halo_pack(DevWorld W) {
     } else {
       lost++;
     }
+    }
   }
   if (lane == 0) {
     if (sent) count_add(W, CNT_HALO_SENT, sent);
@@ -973,15 +1009,19 @@ __global__ __launch_bounds__(64) void k_halo_pack(DevWorld W) {
 
 // Records received from direction d: the offspring owns its target cell when
 // it was that cell's last winner (owner == REMOTE_OWNER(its round)).
-__global__ __launch_bounds__(64) void k_activate_remote(DevWorld W, int d) {
+__global__ __launch_bounds__(64) void k_activate_remote(DevWorld W) {
   const int lane = threadIdx.x;
   const int X = W.world_x;
+  // blocks [0, G/2) take the records from above, the rest those from below
+  const int half = gridDim.x >> 1;
+  const int d = (int)blockIdx.x >= half ? 1 : 0;
+  const int b0 = (int)blockIdx.x - d * half;
   const HaloHdr* hdr = reinterpret_cast<const HaloHdr*>(W.r_recv[d]);
   const HaloRec* recs = reinterpret_cast<const HaloRec*>(W.r_recv[d] + sizeof(HaloHdr));
   const uint8_t* arena = W.r_recv[d] + sizeof(HaloHdr) + (int64_t)X * sizeof(HaloRec);
   const int nrec = min(hdr->count, X);
   unsigned long long born = 0, lost = 0;
-  for (int q = blockIdx.x; q < nrec; q += gridDim.x) {
+  for (int q = b0; q < nrec; q += half) {
     const HaloRec r = recs[q];
     if (r.len < 0) continue;                  // lost at the sender (counted there)
     const int64_t c = edge_cell(W, d, r.col);
@@ -1207,11 +1247,14 @@ void launch_world_begin(const DevWorld& W, hipStream_t s, double* totals, double
   hipLaunchKernelGGL(k_window_count, dim3(nblk(W.n, SORT_WIN)), dim3(1024), 0, s, W);
 }
 
+// reset: clear the update's counters here (a strip tile's k_merit_partial in
+// avgpu_tile_partials already did)
 void launch_world_pre(const DevWorld& W, hipStream_t s, const double* totals, hipEvent_t lists_ready,
-                      uint32_t update) {
+                      uint32_t update, bool reset) {
   launch_resources_begin(W, s);   // ProcessPreUpdate + the update's first DoUpdates
-  hipLaunchKernelGGL(k_reset_counts, dim3(1), dim3(256), 0, s, W);
-  hipLaunchKernelGGL(k_allot, dim3(nblk(W.n, 256)), dim3(256), 0, s, W, totals, update);
+  if (reset) hipLaunchKernelGGL(k_reset_counts, dim3(1), dim3(256), 0, s, W);
+  hipLaunchKernelGGL(k_allot_total, dim3(nblk(W.n, 2048)), dim3(1024), 0, s, W, (const double*)nullptr,
+                     (const int32_t*)nullptr, (int64_t)0, const_cast<double*>(totals), update);
   // the class lists are complete: the aux streams of the list classes start
   // here, beside the window sort (launch_interpret_classes)
   hipEventRecord(lists_ready, s);
@@ -1225,14 +1268,6 @@ void launch_stats(const DevWorld& W, hipStream_t s, double* stats) {
   hipLaunchKernelGGL(k_stats_final, dim3(NPART + 1), dim3(256), 0, s, W, part, nb, stats);
 }
 
-static unsigned activate_grid(const DevWorld& W) {
-  static int cap = -1;
-  if (cap < 0) {
-    const char* e = getenv("AVGPU_ACT_GRID");
-    cap = e ? std::max(64, atoi(e)) : 32768;
-  }
-  return (unsigned)std::min<int64_t>(W.rcap, cap);
-}
 // k_activate: a lane per birth; 2048 waves cover 131k queued births per pass
 static unsigned lane_grid(const DevWorld& W) { return (unsigned)std::min<int64_t>(nblk(W.rcap, 64), 2048); }
 // placement kernels stride over the queue; 8 blocks of 256 per CU cover it
@@ -1246,14 +1281,10 @@ static unsigned place_grid(const DevWorld& W) {
   return (unsigned)std::min<int64_t>(nblk(W.rcap, 256), cap);
 }
 
-static unsigned activate_grid(const DevWorld& W);
 static bool has_divide_mutations(const DevWorld& W) {
   return (W.th_div_mut | W.th_div_ins | W.th_div_del | W.th_div_slip | W.th_div_uni) != 0 || W.seg_any;
 }
 static unsigned mut_grid(const DevWorld& W) { return (unsigned)std::min<int64_t>(nblk(W.rcap, MUT_PER_WAVE), 8192); }
-static void launch_apply_mutations(const DevWorld& W, hipStream_t s) {
-  if (has_divide_mutations(W)) hipLaunchKernelGGL(k_apply_mutations, dim3(mut_grid(W)), dim3(64), 0, s, W);
-}
 
 // after a serial-world update (its births are placed): resources, statistics
 void launch_serial_post(const DevWorld& W, hipStream_t s, double* stats) {
@@ -1284,10 +1315,11 @@ void launch_world_post(const DevWorld& W, hipStream_t s, double* stats, bool eag
 }
 
 // ---- strip tiles: the same update split around the halo exchanges ----
+// (a strip tile's partials start its update: block 0 also clears the counters)
 void launch_tile_partials(const DevWorld& W, hipStream_t s, double* out) {
   const int64_t nb = (W.n + 255) / 256;
   hipLaunchKernelGGL(k_merit_partial, dim3((unsigned)nb), dim3(256), 0, s, W, out, (int32_t*)nullptr,
-                     out + nb, 0);
+                     out + nb, W.tiled ? 1 : 0);
 }
 
 void launch_tile_totals(const DevWorld& W, hipStream_t s, const double* gathered, int ntiles,
@@ -1297,39 +1329,34 @@ void launch_tile_totals(const DevWorld& W, hipStream_t s, const double* gathered
                      (const int32_t*)nullptr, gathered, nb, ntiles, totals, 0);
 }
 
-// after interpretation: occupancy (cells + ghost rows) and the edge-row export
+// after interpretation: the divide mutations, the ghost rows emptied and the
+// edge-row occupancy out (one launch, k_tile_prep)
 void launch_tile_after_interpret(const DevWorld& W, hipStream_t s) {
-  launch_apply_mutations(W, s);
-  hipLaunchKernelGGL(k_occ_init, dim3(nblk(W.n + 2 * (int64_t)W.world_x, 256)), dim3(256), 0, s, W);
-  hipLaunchKernelGGL(k_halo_export, dim3(nblk(2 * (int64_t)W.world_x, 256)), dim3(256), 0, s, W, 0);
+  const unsigned hb = nblk(2 * (int64_t)W.world_x, 256);
+  const int mb = has_divide_mutations(W) ? (int)((mut_grid(W) + 3) / 4) : 0;
+  hipLaunchKernelGGL(k_tile_prep, dim3(mb + hb), dim3(256), 0, s, W, mb);
 }
 
-// phase 0: (round 0: ghost occupancy in) pick, the round's claims out
-// phase 1: (after the exchange) resolve against the merged claims, clear them
-// phase 2: (round 3) pack the ghost-row winners into the record buffers
-// phase 3: (round 3) activate this tile's own winners -- while the records
+// phase 0: round `round` (k_tile_round: resolve round - 1, pick round)
+// phase 1: (round 3) the last resolve, then the ghost-row winners packed into
+//          the record buffers
+// phase 2: (round 3) this tile's own winners activated -- while the records
 //          travel; avgpu_tile_finish then activates the received ones
 void launch_tile_place(const DevWorld& W, hipStream_t s, int round, int phase) {
   const unsigned bb = place_grid(W);
   const unsigned hb = nblk(2 * (int64_t)W.world_x, 256);
   if (phase == 0) {
-    if (round == 0) hipLaunchKernelGGL(k_halo_import_occ, dim3(hb), dim3(256), 0, s, W);
-    hipLaunchKernelGGL(k_place_pick, dim3(bb), dim3(256), 0, s, W, W.claim, (unsigned long long*)nullptr);
-    hipLaunchKernelGGL(k_halo_export, dim3(hb), dim3(256), 0, s, W, 1);
+    hipLaunchKernelGGL(k_tile_round, dim3(bb + hb), dim3(256), 0, s, W, round, (int)bb);
   } else if (phase == 1) {
-    hipLaunchKernelGGL(k_tile_resolve, dim3(bb + hb), dim3(256), 0, s, W, round, (int)bb);
-    hipLaunchKernelGGL(k_tile_clear, dim3(bb + hb), dim3(256), 0, s, W, (int)bb);
-  } else if (phase == 2) {
-    for (int d = 0; d < 2; d++) hipMemsetAsync(W.r_send[d], 0, sizeof(HaloHdr), s);
-    hipLaunchKernelGGL(k_halo_pack, dim3(activate_grid(W)), dim3(64), 0, s, W);
+    hipLaunchKernelGGL(k_tile_round, dim3(bb + hb), dim3(256), 0, s, W, 4, (int)bb);
+    hipLaunchKernelGGL(k_halo_pack, dim3(lane_grid(W)), dim3(64), 0, s, W);
   } else {
-    hipLaunchKernelGGL(k_activate, dim3(lane_grid(W)), dim3(64), 0, s, W, (unsigned long long*)nullptr, 0);
+    hipLaunchKernelGGL(k_activate, dim3(lane_grid(W)), dim3(64), 0, s, W, (unsigned long long*)nullptr, 2);
   }
 }
 
 void launch_tile_finish(const DevWorld& W, hipStream_t s, double* stats, bool eager) {
-  for (int d = 0; d < 2; d++)
-    hipLaunchKernelGGL(k_activate_remote, dim3((unsigned)std::max(1, std::min(W.world_x, 4096))), dim3(64),
-                       0, s, W, d);
+  const unsigned rb = (unsigned)std::max(1, std::min(W.world_x, 4096));
+  hipLaunchKernelGGL(k_activate_remote, dim3(2 * rb), dim3(64), 0, s, W);
   if (eager) launch_stats(W, s, stats);
 }

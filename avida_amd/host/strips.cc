@@ -347,15 +347,15 @@ void update(std::vector<Tile>& tiles, Transport& tr, hipStream_t s) {
   if (tiles[0].res_bytes > 0) tr.exchange(tiles, Kind::Resources, s);
   for (Tile& t : tiles) AV_OK(avgpu_tile_begin(t.h, t.gathered, ntiles_total));
   tr.exchange(tiles, Kind::Halo, s);
-  // one exchange per placement round (both strips resolve each edge cell alike)
+  // one launch and one exchange per placement round (both strips resolve each
+  // edge cell alike, at the start of the next round's launch)
   for (int rnd = 0; rnd < 4; rnd++) {
     for (Tile& t : tiles) AV_OK(avgpu_tile_place(t.h, rnd, 0));
     tr.exchange(tiles, Kind::Halo, s);
-    for (Tile& t : tiles) AV_OK(avgpu_tile_place(t.h, rnd, 1));
   }
-  for (Tile& t : tiles) AV_OK(avgpu_tile_place(t.h, 3, 2));
+  for (Tile& t : tiles) AV_OK(avgpu_tile_place(t.h, 3, 1));   // last resolve, records packed
   tr.exchange_begin(tiles, Kind::Records, s);
-  for (Tile& t : tiles) AV_OK(avgpu_tile_place(t.h, 3, 3));   // own winners, beside the exchange
+  for (Tile& t : tiles) AV_OK(avgpu_tile_place(t.h, 3, 2));   // own winners, beside the exchange
   tr.exchange_end(s);
   for (Tile& t : tiles) AV_OK(avgpu_tile_finish(t.h, nullptr));
   int pools = 0;

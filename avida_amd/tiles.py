@@ -10,8 +10,8 @@ tiled world equals the same update of the untiled world cell for cell
 include/avida_gpu.h ("strip tiles"):
 
     tile_partials -> all_gather -> tile_begin -> exchange(halo)
-    4 x [tile_place(r,0) -> exchange(halo) -> tile_place(r,1)]
-    tile_place(3,2) -> exchange(records) issued -> tile_place(3,3) (own
+    4 x [tile_place(r, 0) -> exchange(halo)]
+    tile_place(3, 1) -> exchange(records) issued -> tile_place(3, 2) (own
     winners, while the records travel) -> wait(records) -> tile_finish
     with resources: exchange(resources) after the all_gather (edge rows of
     the spatial grids), all_reduce(consumption) + tile_res_settle at the end
@@ -177,19 +177,18 @@ class StripWorld:
         for t in tiles:
             t.call("tile_begin", C.c_void_p(t.gathered.data_ptr()), t.ntiles)
         self.tr.exchange(tiles, "halo")
-        # one exchange per placement round: the claims on both sides of each
-        # strip edge, resolved alike by the two strips
+        # one launch and one exchange per placement round: round r's launch
+        # resolves round r - 1 with the claims both strips sent and picks
+        # round r; the claims on both sides of each strip edge go out together
         for rnd in range(4):
             for t in tiles:
                 t.call("tile_place", rnd, 0)
             self.tr.exchange(tiles, "halo")
-            for t in tiles:
-                t.call("tile_place", rnd, 1)
         for t in tiles:
-            t.call("tile_place", 3, 2)
+            t.call("tile_place", 3, 1)     # round 3 resolved, the halo offspring packed
         pending = self.tr.exchange_start(tiles, "records")
         for t in tiles:
-            t.call("tile_place", 3, 3)     # this strip's own winners, beside the exchange
+            t.call("tile_place", 3, 2)     # this strip's own winners, beside the exchange
         self.tr.exchange_wait(pending)
         for t in tiles:
             t.call("tile_finish", None)

@@ -563,9 +563,8 @@ int avgpu_set_global_totals(avgpu_world* w, double total_merit, int64_t total_or
  *   avgpu_tile_begin(w, gathered, T)     exchange(halo)
  *   for round 0..3:
  *     avgpu_tile_place(w, round, 0)      exchange(halo)
- *     avgpu_tile_place(w, round, 1)
- *   avgpu_tile_place(w, 3, 2)            exchange(records) issued ...
- *   avgpu_tile_place(w, 3, 3)            ... and running beside this launch
+ *   avgpu_tile_place(w, 3, 1)            exchange(records) issued ...
+ *   avgpu_tile_place(w, 3, 2)            ... and running beside this launch
  *                                        wait(records)
  *   avgpu_tile_finish(w, stats)
  *   [avgpu_tile_res_cons(w, cons)        all_reduce(cons, sum): global pools,
@@ -592,13 +591,14 @@ int avgpu_tile_partials(avgpu_world* w, double* dev_out);
 /* global totals from the gathered partials (T x partials, tile order), then
  * allotment + interpretation of this tile, occupancy of its edge rows out */
 int avgpu_tile_begin(avgpu_world* w, const double* dev_gathered, int ntiles);
-/* placement round 0..3: phase 0 picks and writes the round's claims (on the
- * ghost rows and on the own edge rows) into the halo send buffers; phase 1,
- * after the exchange, resolves every claim on this tile's cells and ghost
- * rows (a cell of an edge row is claimed only from the two strips it touches,
- * so both resolve it alike).  After round 3: phase 2 packs the ghost-row
- * winners into the record buffers, phase 3 activates this tile's own winners
- * (it reads no record buffer: it may run while the records travel). */
+/* placement round 0..3, phase 0: one launch that resolves round - 1 with the
+ * claims both strips sent (a cell of an edge row is claimed only from the two
+ * strips it touches, so both resolve it alike) and picks round `round`,
+ * writing its claims on the ghost rows and on the own edge rows into the halo
+ * send buffers.  After round 3: phase 1 resolves round 3 and packs the
+ * ghost-row winners into the record buffers, phase 2 activates this tile's
+ * own winners (it reads no record buffer: it may run while the records
+ * travel). */
 int avgpu_tile_place(avgpu_world* w, int round, int phase);
 /* activation of the received records; statistics (out may be NULL: see
  * avgpu_run_update) */

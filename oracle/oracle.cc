@@ -277,7 +277,7 @@ struct World {
   uint8_t* r_recv[2] = {nullptr, nullptr};
   // per-update placement state of the tiled path
   std::vector<uint8_t> occ;
-  std::vector<uint64_t> claim;
+  std::vector<uint64_t> claim_r[4];   // each placement round's claims
   std::vector<int64_t> owner;     // birth index, -1 none, -2-k won by a halo birth in round k
   std::vector<uint64_t> prio;
   std::vector<int8_t> bstate;     // 0 pending, 1+k placed in round k, -1 failed
@@ -285,7 +285,7 @@ struct World {
   int64_t t_oversize = 0;   // offspring longer than AVGPU_MAX_GENOME after a slip (dropped at the divide)
   int64_t t_memcap = 0;     // copy insertions past AVGPU_MAX_GENOME sites / removals from one site (skipped)
   int64_t t_overwritten = 0;   // offspring placed, then killed by a later birth into the same cell
-  int64_t t_placed = 0;        // strip tiles: this tile's own winners activated (avgpu_tile_place(3, 3))
+  int64_t t_placed = 0;        // strip tiles: this tile's own winners activated (avgpu_tile_place(3, 2))
   // resources (avgpu_load_resources): literal restatement of cResourceCount /
   // cSpatialResCount, stepped once per update
   std::vector<avgpu_resource> res;
@@ -1961,12 +1961,13 @@ int orc_set_global_totals(void* h, double merit, int64_t orgs) {
 // ---------------------------------------------------------------------------
 // Strip tiles (include/avida_gpu.h "strip tiles"; DESIGN.md "Multi-GPU"): the
 // same update as run_update_impl, split around the halo exchanges the host
-// performs.  Buffer layouts are the device's: halo = X u64 claims on the
-// receiver's edge row, X u64 the sender's own claims on its edge row, X u8
-// edge-row occupancy; records = HaloHdr, X HaloRec, genome arena.  A cell of
-// an edge row is claimed only from the two strips it touches, so one exchange
-// per placement round gives both strips every claim on it: each resolves the
-// cell alike (the neighbour's own claims merged into the ghost row).
+// performs.  Buffer layouts are the device's: halo = per round parity X u64
+// claims on the receiver's edge row and X u64 the sender's own claims on its
+// edge row, then X u8 edge-row occupancy; records = HaloHdr, X HaloRec,
+// genome arena.  A cell of an edge row is claimed only from the two strips it
+// touches, so one exchange per placement round gives both strips every claim
+// on it: each resolves the cell alike (the neighbour's own claims merged into
+// the ghost row), at the start of the next round's call.
 namespace {
 struct HaloHdr { int32_t count, arena_used, overflow, pad; };
 struct HaloRec {
@@ -1977,10 +1978,11 @@ struct HaloRec {
   int32_t last_task[AVGPU_NUM_LOGIC_TASKS], pad2[3];
 };
 static_assert(sizeof(HaloRec) == 112, "HaloRec layout");
-int64_t halo_bytes_of(int x) { return ((int64_t)x * 17 + 15) / 16 * 16; }
-uint64_t* hclaims(uint8_t* b) { return reinterpret_cast<uint64_t*>(b); }
-uint64_t* hown(uint8_t* b, int x) { return reinterpret_cast<uint64_t*>(b) + x; }
-uint8_t* hocc(uint8_t* b, int x) { return b + (int64_t)x * 16; }
+int64_t halo_bytes_of(int x) { return ((int64_t)x * 33 + 15) / 16 * 16; }
+// per round parity p: k = 0 the sender's claims on the receiver's edge row
+// (its ghost row), k = 1 its own claims on its edge row; then the occupancy
+uint64_t* hcl(uint8_t* b, int x, int p, int k) { return reinterpret_cast<uint64_t*>(b) + (int64_t)(2 * p + k) * x; }
+uint8_t* hocc(uint8_t* b, int x) { return b + (int64_t)x * 32; }
 int64_t edge_cell(const World& w, int d, int x) { return d == 0 ? x : (w.rows - 1) * w.cfg.world_x + x; }
 int64_t ghost_cell(const World& w, int d, int x) { return w.ncells + (int64_t)d * w.cfg.world_x + x; }
 bool tile_ok(World& w) { return w.tiled && w.h_send[0] && w.r_recv[1]; }
@@ -2112,57 +2114,83 @@ int orc_tile_begin(void* h, const double* gathered, int ntiles) {
   const int64_t ext = w.ncells + 2 * X, nbirth = (int64_t)w.births.size();
   w.occ.assign(ext, 0);
   for (int64_t c = 0; c < w.ncells; c++) w.occ[c] = w.orgs[c].alive ? 1 : 0;
-  w.claim.assign(ext, 0);
+  for (int k = 0; k < 4; k++) w.claim_r[k].assign(ext, 0);
   w.owner.assign(ext, -1);
   w.prio.assign(nbirth, 0);
   w.bstate.assign(nbirth, 0);
   for (int d = 0; d < 2; d++)
     for (int x = 0; x < X; x++) {
       hocc(w.h_send[d], X)[x] = w.occ[edge_cell(w, d, x)];
-      hclaims(w.h_send[d])[x] = 0;
-      hown(w.h_send[d], X)[x] = 0;
+      for (int k = 0; k < 4; k++) hcl(w.h_send[d], X, k >> 1, k & 1)[x] = 0;
     }
   w.t_placed = 0; w.t_overwritten = 0;
   return 0;
 }
 
+namespace {
+// the halo slot of a cell: direction, column, ghost row (else edge row)
+bool tile_slot(const World& w, int64_t c, int& d, int& x, bool& ghost) {
+  const int X = w.cfg.world_x;
+  if (c >= w.ncells) { d = (int)((c - w.ncells) / X); x = (int)((c - w.ncells) % X); ghost = true; return true; }
+  ghost = false;
+  if (c < X) { d = 0; x = (int)c; return true; }
+  if (c >= w.ncells - X) { d = 1; x = (int)(c - (w.ncells - X)); return true; }
+  return false;
+}
+// round m's resolve with the merged claims (mine, the neighbour's): winners
+// take their cells (state m + 1); an edge cell whose maximum came from the
+// neighbour is that round's remote winner's; a claimed ghost cell is occupied
+void tile_resolve(World& w, int m) {
+  const int X = w.cfg.world_x, p = m & 1;
+  const std::vector<uint64_t>& cl = w.claim_r[m];
+  for (int64_t i = 0; i < (int64_t)w.births.size(); i++) {
+    if (w.bstate[i] != 0) continue;
+    const int64_t t = w.births[i].target;
+    uint64_t v = cl[t];
+    int d, x;
+    bool ghost;
+    if (tile_slot(w, t, d, x, ghost)) v = std::max(v, hcl(w.h_recv[d], X, p, ghost ? 1 : 0)[x]);
+    if (v == w.prio[i]) { w.bstate[i] = (int8_t)(1 + m); w.occ[t] = 1; w.owner[t] = i; }
+  }
+  for (int d = 0; d < 2; d++)
+    for (int x = 0; x < X; x++) {
+      const int64_t c = edge_cell(w, d, x), g = ghost_cell(w, d, x);
+      const uint64_t rc = hcl(w.h_recv[d], X, p, 0)[x];
+      if (rc != 0 && rc > cl[c]) { w.owner[c] = -2 - m; w.occ[c] = 1; }
+      if (cl[g] != 0 || hcl(w.h_recv[d], X, p, 1)[x] != 0) w.occ[g] = 1;
+    }
+}
+}  // namespace
+
 int orc_tile_place(void* h, int round, int phase) {
   World& w = *(World*)h;
   if (!tile_ok(w)) return fail(AVGPU_ESTATE, "not a strip tile with buffers");
-  if (round < 0 || round > 3 || phase < 0 || phase > 3 || (phase >= 2 && round != 3))
-    return fail(AVGPU_EINVAL, "round 0..3 with phase 0..1; phases 2, 3 after round 3");
+  if (round < 0 || round > 3 || phase < 0 || phase > 2 || (phase >= 1 && round != 3))
+    return fail(AVGPU_EINVAL, "round 0..3 with phase 0; phases 1, 2 after round 3");
   const int X = w.cfg.world_x;
   const int64_t nbirth = (int64_t)w.births.size();
   if (phase == 0) {
     if (round == 0)
       for (int d = 0; d < 2; d++)
         for (int x = 0; x < X; x++) w.occ[ghost_cell(w, d, x)] = hocc(w.h_recv[d], X)[x];
-    for (int64_t i = 0; i < nbirth; i++)
-      if (w.bstate[i] == 0) place_pick(w, i, w.occ, w.claim, w.prio, w.bstate);
+    else
+      tile_resolve(w, round - 1);
+    // this round's claims: the arrays and the halo send slots of its parity
+    const int p = round & 1;
     for (int d = 0; d < 2; d++)
-      for (int x = 0; x < X; x++) {
-        hclaims(w.h_send[d])[x] = w.claim[ghost_cell(w, d, x)];
-        hown(w.h_send[d], X)[x] = w.claim[edge_cell(w, d, x)];
-      }
-  } else if (phase == 1) {
-    // merged claims: the neighbour's claims on my edge rows, its own claims on
-    // its edge rows (my ghost rows)
-    std::vector<uint64_t> merged(w.claim);
-    for (int d = 0; d < 2; d++)
-      for (int x = 0; x < X; x++) {
-        const int64_t c = edge_cell(w, d, x), g = ghost_cell(w, d, x);
-        const uint64_t rc = hclaims(w.h_recv[d])[x], oc = hown(w.h_recv[d], X)[x];
-        if (rc > merged[c]) { merged[c] = rc; w.owner[c] = -2 - round; w.occ[c] = 1; }
-        if (oc > merged[g]) merged[g] = oc;
-        if (merged[g] != 0) w.occ[g] = 1;     // its winner is placed, here or there
-      }
+      for (int x = 0; x < X; x++) { hcl(w.h_send[d], X, p, 0)[x] = 0; hcl(w.h_send[d], X, p, 1)[x] = 0; }
     for (int64_t i = 0; i < nbirth; i++) {
       if (w.bstate[i] != 0) continue;
+      place_pick(w, i, w.occ, w.claim_r[round], w.prio, w.bstate);
+      int d, x;
+      bool ghost;
       const int64_t t = w.births[i].target;
-      if (merged[t] == w.prio[i]) { w.bstate[i] = (int8_t)(1 + round); w.occ[t] = 1; w.owner[t] = i; }
+      if (tile_slot(w, t, d, x, ghost)) {
+        uint64_t& slot = hcl(w.h_send[d], X, p, ghost ? 0 : 1)[x];
+        slot = std::max(slot, w.prio[i]);
+      }
     }
-    std::fill(w.claim.begin(), w.claim.end(), 0);
-  } else if (phase == 3) {
+  } else if (phase == 2) {
     // this tile's own winners (the records travel meanwhile)
     int64_t placed = 0, overwritten = 0;
     for (int64_t i = 0; i < nbirth; i++) {
@@ -2175,7 +2203,8 @@ int orc_tile_place(void* h, int round, int phase) {
     w.t_placed = placed;
     w.t_overwritten = overwritten;
   } else {
-    // (phase 2) pack the last winner of every ghost cell (births in queue order)
+    tile_resolve(w, 3);
+    // then pack the last winner of every ghost cell (births in queue order)
     w.t_born = 0; w.t_dropped = 0;
     for (int d = 0; d < 2; d++) memset(w.r_send[d], 0, sizeof(HaloHdr));
     for (int64_t i = 0; i < nbirth; i++) {

@@ -302,10 +302,14 @@ __device__ __forceinline__ void setup_child_lane(const DevWorld& W, int64_t c, c
 // the phenotype record r hands its offspring
 __device__ __forceinline__ Child child_of_record(const DevWorld& W, int64_t i) {
   Child b;
-  b.len = W.b_len[i]; b.gen = W.b_gen[i]; b.ccopied = W.b_ccopied[i]; b.exec = W.b_exec[i];
-  b.gest = W.b_gest[i]; b.merit = W.b_merit[i]; b.fitness = W.b_fitness[i];
-  b.lo = W.b_rng[i]; b.hi = W.b_rng[W.rcap + i]; b.ctr = W.b_rng[2 * W.rcap + i];
-  b.ltask = W.b_ltask + i; b.lstride = W.rcap;
+  const int4* row = reinterpret_cast<const int4*>(W.b_inh + i * BI_WORDS);
+  const int4 q0 = row[0], q1 = row[1], q2 = row[2];       // 16-B loads of the record's row
+  static_assert(BI_MERIT == 0 && BI_GEN == 4 && BI_RLO == 8 && BI_LTASK == 12, "b_inh row layout");
+  b.len = W.b_len[i];
+  b.merit = __hiloint2double(q0.y, q0.x); b.fitness = __hiloint2double(q0.w, q0.z);
+  b.gen = q1.x; b.ccopied = q1.y; b.exec = q1.z; b.gest = q1.w;
+  b.lo = (uint32_t)q2.x; b.hi = (uint32_t)q2.y; b.ctr = (uint32_t)q2.z;
+  b.ltask = W.b_inh + i * BI_WORDS + BI_LTASK; b.lstride = 1;
   return b;
 }
 

@@ -155,9 +155,7 @@ int setup_world(avgpu_world* w, int64_t n, bool test_buffers) {
   W.seg_any = (pois || site) ? 1 : 0;
   W.pois_any = pois ? 1 : 0;
   for (int q = 0; q < 5; q++) W.pois_L[q] = pmeans[q] > 0.0 ? std::exp(-pmeans[q]) : 0.0;
-  A(b_merit, R);
-  A(b_fitness, R); A(b_gen, R); A(b_ccopied, R); A(b_exec, R);
-  A(b_gest, R); A(b_ltask, AVGPU_NUM_LOGIC_TASKS * R); A(b_rng, 3 * R); A(b_target, R); A(b_state, R);
+  A(b_inh, (size_t)BI_WORDS * R); A(b_target, R); A(b_state, R);
   A(b_prio, R); A(b_genome, (size_t)R * TAPE_SLOT);
   // placement scratch with two ghost rows (strip tiles)
   // occupancy, owners and the four placement rounds' claims, each with the two

@@ -16,6 +16,11 @@
 #include "../../include/avida_gpu.h"
 
 #define TAPE_SLOT 2048
+// birth record row b_inh[r * BI_WORDS ..]: merit, fitness (doubles), generation,
+// copied size, executed size, gestation time, the offspring's RNG key and
+// counter, the parent's last task counts
+enum { BI_MERIT = 0, BI_FITNESS = 2, BI_GEN = 4, BI_CCOPIED = 5, BI_EXEC = 6, BI_GEST = 7,
+       BI_RLO = 8, BI_RHI = 9, BI_RCTR = 10, BI_LTASK = 12, BI_WORDS = 32 };
 #define CODE_MASK 0x3F
 #define TF_COPIED 0x40
 #define TF_EXEC 0x80
@@ -148,14 +153,12 @@ struct DevWorld {
   int64_t scap;
   int32_t* b_pofs;    // [NSEG][rcap]
   int32_t* b_pcnt;    // [NSEG][rcap]
-  double* b_merit;    // [rcap]
-  double* b_fitness;  // [rcap]
-  int32_t* b_gen;     // [rcap]
-  int32_t* b_ccopied; // [rcap]
-  int32_t* b_exec;    // [rcap]
-  int32_t* b_gest;    // [rcap]
-  int32_t* b_ltask;   // [9][rcap] the parent's last task counts (cPhenotype::SetupOffspring :447)
-  uint32_t* b_rng;    // [3][rcap]
+  // what the offspring of record r inherits (cPhenotype::SetupOffspring,
+  // main/cPhenotype.cc:349-447), one 128-B row per record (BI_* below):
+  // written with 16-B stores at the divide, read with 16-B loads at
+  // activation -- as [field][rcap] rows every field was a scattered 4-B
+  // access whose line held no other field of the record
+  int32_t* b_inh;     // [rcap][BI_WORDS]
   int32_t* b_target;  // [rcap]
   int8_t* b_state;    // [rcap]  0 pending, 1+k placed in round k, -1 failed
   unsigned long long* b_prio; // [rcap]
@@ -406,6 +409,46 @@ __device__ __forceinline__ uint32_t ld_sync_ro_u8(const void* p) {
   uint32_t v;
   asm volatile("global_load_ubyte %0, %1, off\n\ts_waitcnt vmcnt(0)" : "=v"(v) : "v"(p));
   return v;
+}
+// Read-only tables read through the scalar cache (s_load, counted by lgkmcnt):
+// a vector load in the interpreter's loop waits on vmcnt, which also counts
+// every store the wave still has in flight (the divide's record stores).
+typedef const __attribute__((address_space(4))) double const_f64_t;
+// p[0] at a wave-uniform address
+__device__ __forceinline__ double ld_uniform_f64(const double* p) {
+  return *(const_f64_t*)p;
+}
+// tab[idx] for a per-lane idx: one scalar load per distinct index among the
+// active lanes (waterfall)
+__device__ __forceinline__ uint32_t sgather_u8(const uint8_t* tab, uint32_t idx) {
+  uint32_t out = 0;
+  bool todo = true;
+  while (todo) {
+    const uint32_t u = __builtin_amdgcn_readfirstlane(idx);
+    if (idx == u) {
+      // the address made explicitly scalar (an "s" operand computed by VALU
+      // was otherwise handed over in a VGPR)
+      const uint64_t a = (uint64_t)(tab + (u & ~3u));
+      // (readfirstlane returns int: each half through uint32_t, no sign extension)
+      const uint64_t sa = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(a >> 32)) << 32) |
+                          (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)a);
+      uint32_t w;
+      asm volatile("s_load_dword %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(w) : "s"(sa));
+      out = (w >> ((u & 3u) * 8u)) & 0xFFu;
+      todo = false;
+    }
+  }
+  return out;
+}
+// one 16-B store of four words (p 16-byte aligned).  A store of more than 8
+// bytes leaves a hazard on its data VGPRs: a VALU write to them right after
+// the store can change what is stored.  The compiler pads its own stores; an
+// asm store must carry the wait states itself (without them the rows came out
+// corrupted, nondeterministically).
+__device__ __forceinline__ void st_async_b128(void* p, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  const u32x4 v = {a, b, c, d};
+  asm volatile("global_store_dwordx4 %0, %1, off\n\ts_waitcnt expcnt(0)\n\ts_nop 2" ::"v"(p), "v"(v));
 }
 __device__ __forceinline__ void st_async_u8(void* p, uint32_t v) {
   asm volatile("global_store_byte %0, %1, off\n\ts_waitcnt expcnt(0)" ::"v"(p), "v"(v));

@@ -412,7 +412,7 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
   // cInstSet::GetRandomInst (cpu/cInstSet.cc:83-88) from the LDS tables
   auto rand_code = [&]() -> uint8_t {
     const uint32_t r = draw_below((uint32_t)k_rand_total);
-    if (k_rand_lut) return GLUT ? (uint8_t)ld_sync_ro_u8(W.rand_lut + r) : rlut[r];
+    if (k_rand_lut) return GLUT ? (uint8_t)sgather_u8(W.rand_lut, r) : rlut[r];
     int i = 0;
     while (i < k_n_ops - 1 && tab_i32(rcum + i) <= (int32_t)r) i++;
     return (uint8_t)tab_u8(rcode + i);
@@ -438,6 +438,14 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
   // lane can step any more.  Each organism still executes its own
   // instructions in order -- only the interleaving across lanes changes.
   int pop = -1, pr = 0;                                       // parked op, its register
+  int io_id = -2;                                             // IO's logic id (-1: none; -2: no IO this step)
+  // class 0's task LUT (256 x u16) spread over the wave: lane j holds entries 4j .. 4j+3
+  uint32_t tl0 = 0u, tl1 = 0u;
+  if (GLUT) {
+    const uint32_t* g_lut = reinterpret_cast<const uint32_t*>(W.task_lut);
+    tl0 = g_lut[2 * lane];
+    tl1 = g_lut[2 * lane + 1];
+  }
   const uint32_t* T32 = reinterpret_cast<const uint32_t*>(T);
   const int slow_batch = W.slow_batch;
 
@@ -629,8 +637,37 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
         wh = head_wrap(wh + 1, M);
       }
     }
+    // if-label (:6914 Inst_IfLabel) from the fetch window when its label ends
+    // inside the window (the copy loop's short labels): no park, no label
+    // read.  The window holds sites ipa+1 .. ipa+avail; a label that may run
+    // past them parks and reads its own 16-byte window in the slow phase.
+    bool lab_done = false;
+    if (op == AVGPU_H_IF_LABEL && k_max_label_exe == 1) {
+      const int base = ip + 1;
+      const int avail = 7 - (ipa & 3);
+      const uint64_t w = fwin >> (fsh + 8u);                // site base in byte 0
+      const uint64_t cl = w & 0x3F3F3F3F3F3F3F3Full;
+      const uint64_t nl = (cl + 0x7D7D7D7D7D7D7D7Dull) & 0x8080808080808080ull;   // non-nop bytes
+      const int run = nl ? (int)(__ffsll((long long)nl) - 8) >> 3 : 8;
+      const int lim = min(AVGPU_MAX_LABEL, M - base);
+      if (run < avail || lim <= avail) {
+        lab_done = true;
+        const int len = max(min(run, lim), 0);
+        uint64_t v = cl & 0x0303030303030303ull;
+        v = (v | (v >> 6)) & 0x000F000F000F000Full;
+        v = (v | (v >> 12)) & 0x000000FF000000FFull;
+        v = (v | (v >> 24)) & 0xFFFFull;
+        const uint32_t lmask = (1u << (2 * len)) - 1u;
+        const uint32_t lab = (uint32_t)v & lmask;
+        const uint32_t dl = lab & 0x55555u, dh = (lab >> 1) & 0x55555u;
+        const uint32_t rot = ((~dl & ~dh & 0x55555u) | (dl << 1)) & lmask;   // Rotate(1, NUM_NOPS)
+        if (len > 0) T[base] = (uint8_t)((uint32_t)w | TF_EXEC);         // the label's first site (MAX_LABEL_EXE_SIZE 1)
+        ip += len;
+        if (((uint32_t)len | (rot << 4)) != rl) ip = head_wrap(ip + 1, M);
+      }
+    }
     CK(2);
-    if (!(FAST_OPS & obit) && op != AVGPU_H_H_COPY) { pop = op; pr = r; stepped = false; }   // park
+    if (!(FAST_OPS & obit) && op != AVGPU_H_H_COPY && !lab_done) { pop = op; pr = r; stepped = false; }   // park
     }  // !spill
     }  // run
     if (stepped && !stop) {
@@ -717,79 +754,9 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
         if (num < 2) { lo |= (lo & 3u) << 2; pr |= (pr & 3u) << 2; }
         if (num < 3) { lo |= (lo & 15u) << 4; pr |= (pr & 15u) << 4; }
         const int id = (int)lo - (int)(~pr & 0xFFu);
-        uint32_t tmask = 0u;
-        if ((ones & zeros) == 0u && id >= 0)
-          tmask = GLUT ? (ld_sync_ro_u32(W.task_lut + (id & ~1)) >> ((id & 1) * 16)) & 0xFFFFu : lut[id];
-        // cEnvironment::TestOutput / TestRequisites / DoProcesses
-        // (main/cEnvironment.cc:1314-1406, :1408-1503, :1610-1760)
-        if (tmask && k_env_simple) {
-          // reaction i rewards task i, requisites at most "max_count=1"
-          // (capi.hip avgpu_load_env): the firing set is a bit operation and
-          // the bonus factors multiply in reaction order (ascending bits)
-          const uint32_t done = tmask & k_env_react_mask & ~(k_env_once_mask & nzm);
-          if (done) {
-            double mult = 1.0, addb = 0.0;
-            uint32_t paid = done;
-            {
-            for (uint32_t d = done; d; d &= d - 1u) {
-              const int t = __ffs(d) - 1;
-              if ((k_env_res_mask >> t) & 1u) {                 // finite resource (general path below)
-                if (!consume_resource(W, W.react_res + t * RR_STRIDE, N, cell, mult, addb)) paid &= ~(1u << t);
-              } else {
-                mult = __dmul_rn(mult, tmul[t]);
-                addb = __dadd_rn(addb, tadd[t]);
-              }
-            }
-            }
-#pragma unroll
-            for (int q = 0; q < AVGPU_NUM_LOGIC_TASKS; q++) {
-              tc[q] += (done >> q) & 1u;
-              rc[q] += (paid >> q) & 1u;
-            }
-            nzm |= done;
-            bonus = __dadd_rn(__dmul_rn(bonus, mult), addb);   // cPhenotype.cc:1645-1646
-          }
-        } else if (tmask) {
-          uint32_t done = 0;
-          double mult = 1.0, addb = 0.0;
-#pragma unroll
-          for (int i = 0; i < AVGPU_MAX_REACTIONS; i++) {
-            if (i >= k_n_react) break;
-            const int32_t* rt = rtab + i * RT_STRIDE;         // uniform LDS reads
-            const int t = rt[RT_TASK];
-            int cnt = 0;
-#pragma unroll
-            for (int q = 0; q < AVGPU_NUM_LOGIC_TASKS; q++) cnt = (q == t) ? tc[q] : cnt;
-            const bool fire = rt[RT_USED] && ((tmask >> t) & 1u) &&
-                              !(rt[RT_HASREQ] && (cnt < rt[RT_MIN] || cnt >= rt[RT_MAX]));
-            if (fire) {
-              done |= 1u << t;                                // MarkTask precedes the processes
-              const double* rr = W.react_res + i * RR_STRIDE; // uniform (scalar) loads
-              if (!k_env_resources || rr[RR_RES] == 0.0) {    // infinite resource
-                if (rt[RT_TYPE] == AVGPU_PROC_ADD)
-                  addb = __dadd_rn(addb, *reinterpret_cast<const double*>(rt + RT_ADD));
-                else
-                  mult = __dmul_rn(mult, *reinterpret_cast<const double*>(rt + RT_MULT));
-                rc[i]++;
-              } else if (consume_resource(W, rr, N, cell, mult, addb)) {
-                rc[i]++;
-              }
-            }
-          }
-          if (done) {
-#pragma unroll
-            for (int q = 0; q < AVGPU_NUM_LOGIC_TASKS; q++) tc[q] += (done >> q) & 1u;
-            nzm |= done;
-            bonus = __dadd_rn(__dmul_rn(bonus, mult), addb);   // cPhenotype.cc:1645-1646
-          }
-        }
-        // GetNextInput (main/cOrganism.h:249 -> cPopulationCell.h:214-218) + DoInput
-        const int p = inptr >= 3 ? 0 : inptr;
-        const int in = p == 0 ? inp0 : (p == 1 ? inp1 : inp2);
-        inptr = p + 1;
-        in2 = in1; in1 = in0; in0 = in;
-        intot++;
-        SETREG(r, in);
+        // the task lookup, the rewards and the input follow the switch, with
+        // the whole wave converged (io_id: the logic id, or -1 for none)
+        io_id = ((ones & zeros) == 0u && id >= 0) ? id : -1;
         CKC(2);
         break; }
       case AVGPU_H_H_ALLOC: {                                 // :3294 Inst_MaxAlloc -> Allocate_Main :1707
@@ -851,7 +818,10 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
         uint32_t lab = (uint32_t)v | ((uint32_t)(ch & 3u) << 16) | ((uint32_t)((ch >> 8) & 3u) << 18);
         const uint32_t lmask = (1u << (2 * len)) - 1u;
         lab &= lmask;
-        for (int k = 0; k < min(len, k_max_label_exe); k++) T[base + k] |= TF_EXEC;
+        // executed flags of the label's first sites, from the window's own bytes
+        // (no LDS read-modify-write round trip)
+        for (int k = 0; k < min(len, k_max_label_exe); k++)
+          T[base + k] = (uint8_t)(((k < 8 ? (lo64 >> (8 * k)) : (hi64 >> (8 * (k - 8)))) & 0xFFull) | TF_EXEC);
         ip += len;
         // Rotate(1, NUM_NOPS): per 2-bit digit 0->1, 1->2, 2->0
         const uint32_t dl = lab & 0x55555u, dh = (lab >> 1) & 0x55555u;
@@ -871,6 +841,98 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
       default:
         break;
     }
+    }
+    // ---- IO, second half (converged): cTaskLib's logic id -> task mask,
+    // cEnvironment::TestOutput / TestRequisites / DoProcesses
+    // (main/cEnvironment.cc:1314-1406, :1408-1503, :1610-1760), then
+    // GetNextInput + DoInput.  Class 0 holds its task LUT spread over the
+    // wave's lanes (tl0 / tl1) and reads it by lane shuffles, and reads the
+    // per-task bonus factors as wave-uniform scalar loads: a vector load here
+    // waited (vmcnt) for every store the wave still had in flight.
+    if (__ballot(io_id >= -1) != 0ull) {
+      const bool io = io_id >= -1;
+      uint32_t tmask = 0u;
+      if (GLUT) {
+        const int sl = io_id >= 0 ? (io_id >> 2) : 0;
+        const uint32_t a0 = (uint32_t)__shfl((int)tl0, sl), a1 = (uint32_t)__shfl((int)tl1, sl);
+        const uint32_t wv = (io_id & 2) ? a1 : a0;
+        tmask = io_id >= 0 ? (wv >> ((io_id & 1) * 16)) & 0xFFFFu : 0u;
+      } else if (io_id >= 0) {
+        tmask = lut[io_id];
+      }
+      if (k_env_simple) {
+        // reaction i rewards task i, requisites at most "max_count=1"
+        // (capi.hip avgpu_load_env): the firing set is a bit operation and
+        // the bonus factors multiply in reaction order (ascending bits)
+        const uint32_t done = io ? (tmask & k_env_react_mask & ~(k_env_once_mask & nzm)) : 0u;
+        if (__ballot(done != 0u) != 0ull) {
+          double mult = 1.0, addb = 0.0;
+          uint32_t paid = done;
+          for (int t = 0; t < AVGPU_NUM_LOGIC_TASKS; t++) {   // wave-uniform t
+            const bool dt = (done >> t) & 1u;
+            if (__ballot(dt) == 0ull) continue;
+            if ((k_env_res_mask >> t) & 1u) {                 // finite resource
+              if (dt && !consume_resource(W, W.react_res + t * RR_STRIDE, N, cell, mult, addb)) paid &= ~(1u << t);
+            } else {
+              const double fm = GTAB ? ld_uniform_f64(tmul + t) : tmul[t];
+              const double fa = GTAB ? ld_uniform_f64(tadd + t) : tadd[t];
+              if (dt) { mult = __dmul_rn(mult, fm); addb = __dadd_rn(addb, fa); }
+            }
+          }
+          if (done) {
+#pragma unroll
+            for (int q = 0; q < AVGPU_NUM_LOGIC_TASKS; q++) {
+              tc[q] += (done >> q) & 1u;
+              rc[q] += (paid >> q) & 1u;
+            }
+            nzm |= done;
+            bonus = __dadd_rn(__dmul_rn(bonus, mult), addb);   // cPhenotype.cc:1645-1646
+          }
+        }
+      } else if (io && tmask) {
+        uint32_t done = 0;
+        double mult = 1.0, addb = 0.0;
+#pragma unroll
+        for (int i = 0; i < AVGPU_MAX_REACTIONS; i++) {
+          if (i >= k_n_react) break;
+          const int32_t* rt = rtab + i * RT_STRIDE;           // uniform LDS reads
+          const int t = rt[RT_TASK];
+          int cnt = 0;
+#pragma unroll
+          for (int q = 0; q < AVGPU_NUM_LOGIC_TASKS; q++) cnt = (q == t) ? tc[q] : cnt;
+          const bool fire = rt[RT_USED] && ((tmask >> t) & 1u) &&
+                            !(rt[RT_HASREQ] && (cnt < rt[RT_MIN] || cnt >= rt[RT_MAX]));
+          if (fire) {
+            done |= 1u << t;                                  // MarkTask precedes the processes
+            const double* rr = W.react_res + i * RR_STRIDE;   // uniform (scalar) loads
+            if (!k_env_resources || rr[RR_RES] == 0.0) {      // infinite resource
+              if (rt[RT_TYPE] == AVGPU_PROC_ADD)
+                addb = __dadd_rn(addb, *reinterpret_cast<const double*>(rt + RT_ADD));
+              else
+                mult = __dmul_rn(mult, *reinterpret_cast<const double*>(rt + RT_MULT));
+              rc[i]++;
+            } else if (consume_resource(W, rr, N, cell, mult, addb)) {
+              rc[i]++;
+            }
+          }
+        }
+        if (done) {
+#pragma unroll
+          for (int q = 0; q < AVGPU_NUM_LOGIC_TASKS; q++) tc[q] += (done >> q) & 1u;
+          nzm |= done;
+          bonus = __dadd_rn(__dmul_rn(bonus, mult), addb);     // cPhenotype.cc:1645-1646
+        }
+      }
+      if (io) {
+        // GetNextInput (main/cOrganism.h:249 -> cPopulationCell.h:214-218) + DoInput
+        const int p = inptr >= 3 ? 0 : inptr;
+        const int in = p == 0 ? inp0 : (p == 1 ? inp1 : inp2);
+        inptr = p + 1;
+        in2 = in1; in1 = in0; in0 = in;
+        intot++;
+        SETREG(pr, in);
+      }
+      io_id = -2;
     }
     CK(3);
 
@@ -937,7 +999,9 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
           ne += __popc(v & (TF_EXEC * 0x01010101u) & byte_mask(w << 2, 0, div));
           nc += __popc(v & (TF_COPIED * 0x01010101u) & byte_mask(w << 2, div, div + child));
         }
-        const int exe = wave_sum_i32(ne), cop = wave_sum_i32(nc);
+        // both counts (<= AVGPU_MAX_GENOME each) in one reduction: halves of one word
+        const int both = wave_sum_i32(ne | (nc << 16));
+        const int exe = both & 0xFFFF, cop = both >> 16;
         int okw = 0, rec = -1, len = 0, e0 = 0, e1 = 0, e2 = 0, e3 = 0, e4 = 0;   // edits: slip mut ins del uniform
         int pcnt[NSEG] = {0}, pofs[NSEG] = {0};   // variable-count edit segments in b_subs (device.h)
         if (lane == L) {
@@ -1341,20 +1405,12 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
                 int32_t* b_len = W.b_len;
                 int32_t* b_len0 = W.b_len0;
                 int32_t* b_edit = W.b_edit;
-                double* b_merit = W.b_merit;
-                double* b_fitness = W.b_fitness;
-                int32_t* b_gen = W.b_gen;
-                int32_t* b_ccopied = W.b_ccopied;
-                int32_t* b_exec = W.b_exec;
-                int32_t* b_gest = W.b_gest;
-                uint32_t* b_rng = W.b_rng;
                 int8_t* b_state = W.b_state;
                 int32_t* b_target = W.b_target;
-                int32_t* b_ltask = W.b_ltask;
+                int32_t* b_inh = W.b_inh;
                 int64_t rcap = W.rcap;
-                OPQ(b_parent); OPQ(b_seq); OPQ(b_len); OPQ(b_len0); OPQ(b_edit); OPQ(b_merit);
-                OPQ(b_fitness); OPQ(b_gen); OPQ(b_ccopied); OPQ(b_exec); OPQ(b_gest); OPQ(b_rng);
-                OPQ(b_state); OPQ(b_target); OPQ(b_ltask); OPQ(rcap);
+                OPQ(b_parent); OPQ(b_seq); OPQ(b_len); OPQ(b_len0); OPQ(b_edit);
+                OPQ(b_state); OPQ(b_target); OPQ(b_inh); OPQ(rcap);
                 st_async_u32(b_parent + rec, (uint32_t)cell);
                 st_async_u32(b_seq + rec, (uint32_t)nd);
                 st_async_u32(b_len + rec, (uint32_t)len);
@@ -1370,20 +1426,17 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
                     W.b_pofs[(int64_t)k * rcap + rec] = pofs[k];
                     W.b_pcnt[(int64_t)k * rcap + rec] = pcnt[k];
                   }
-                st_async_u64(b_merit + rec, (uint64_t)__double_as_longlong(merit));
-                st_async_u64(b_fitness + rec, (uint64_t)__double_as_longlong(fit));
-                st_async_u32(b_gen + rec, (uint32_t)gen);
-                st_async_u32(b_ccopied + rec, (uint32_t)cop);
-                st_async_u32(b_exec + rec, (uint32_t)exe);
-                st_async_u32(b_gest + rec, (uint32_t)gt);
-                st_async_u32(b_rng + rec, clo);
-                st_async_u32(b_rng + rcap + rec, chi);
-                st_async_u32(b_rng + 2 * rcap + rec, 0u);
+                // the inherited phenotype: one 128-B row, 16-B stores (device.h BI_*)
+                int32_t* irow = b_inh + (int64_t)rec * BI_WORDS;
+                const long long mb = __double_as_longlong(merit), fb = __double_as_longlong(fit);
+                st_async_b128(irow, (uint32_t)mb, (uint32_t)(mb >> 32), (uint32_t)fb, (uint32_t)(fb >> 32));
+                st_async_b128(irow + 4, (uint32_t)gen, (uint32_t)cop, (uint32_t)exe, (uint32_t)gt);
+                st_async_b128(irow + 8, clo, chi, 0u, 0u);
+                st_async_b128(irow + 12, (uint32_t)tc[0], (uint32_t)tc[1], (uint32_t)tc[2], (uint32_t)tc[3]);
+                st_async_b128(irow + 16, (uint32_t)tc[4], (uint32_t)tc[5], (uint32_t)tc[6], (uint32_t)tc[7]);
+                st_async_b128(irow + 20, (uint32_t)tc[8], 0u, 0u, 0u);
                 st_async_u8(b_state + rec, 0u);
                 st_async_u32(b_target + rec, 0xFFFFFFFFu);
-#pragma unroll
-                for (int q = 0; q < AVGPU_NUM_LOGIC_TASKS; q++)   // SetupOffspring copies them (:447)
-                  st_async_u32(b_ltask + (int64_t)q * rcap + rec, (uint32_t)tc[q]);
               }
             }
 #pragma unroll
@@ -2078,6 +2131,9 @@ static void launch_classes(const DevWorld& W, const DevWorld* dW, int mode, hipS
   }
   if (after_class && tall) hipEventRecord(after_class[1], s);
   // spill rows 5 + 6 (beyond classes 1 / 2) in one launch of class 3's slots
+  // (all three spill rows in one class-3 launch after the join measured 8 us
+  // slower per update than these two launches: row 4's organisms ran slower
+  // in class 3's slots than the saved launch gap)
   row(CLASS3_SIZE, dim3(std::min(lb_small, 64u)), s, -1, 5, slpw);
   if (after_class && tall) { hipEventRecord(after_class[2], s); hipEventRecord(after_class[3], s); }
   if (launches) *launches += 5;

@@ -342,27 +342,37 @@ __device__ __forceinline__ void reset_counts_block(const DevWorld& W) {
 
 // reset: block 0 also zeroes the update's counters, birth-queue and class-list
 // lengths (k_reset_counts' work; the previous update's statistics have read them)
+// One wave per 256-cell block b (partial[b]): the pairwise tree of strides
+// 128, 64, ..., 1 (s[t] += s[t + stride]), the oracle's tree_merit_sum order.
+// Lane l loads cells l, l+64, l+128, l+192 and forms the stride-128 and -64
+// sums itself; strides 32 .. 1 are lane shuffles -- the same additions in the
+// same order, without the LDS tree's 8 barriers.  Four blocks per workgroup.
 __global__ __launch_bounds__(256) void k_merit_partial(DevWorld W, double* partial, int32_t* alive_partial,
                                                        double* alive_d, int reset) {
-  __shared__ double s[256];
-  __shared__ int a[256];
   if (reset && blockIdx.x == 0) reset_counts_block(W);
-  const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  const bool live = c < W.n && (W.ctl[c] & CTL_ALIVE);
-  s[threadIdx.x] = live ? W.merit[c] : 0.0;
-  a[threadIdx.x] = live ? 1 : 0;
-  __syncthreads();
-  for (int stride = 128; stride >= 1; stride >>= 1) {
-    if ((int)threadIdx.x < stride) {
-      s[threadIdx.x] = __dadd_rn(s[threadIdx.x], s[threadIdx.x + stride]);
-      a[threadIdx.x] += a[threadIdx.x + stride];
-    }
-    __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t nb = (W.n + 255) / 256;
+  if (b >= nb) return;
+  double m[4];
+  int a = 0;
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const int64_t c = b * 256 + lane + 64 * k;
+    const bool live = c < W.n && (W.ctl[c] & CTL_ALIVE);
+    m[k] = live ? W.merit[c] : 0.0;
+    a += live ? 1 : 0;
   }
-  if (threadIdx.x == 0) {
-    partial[blockIdx.x] = s[0];
-    if (alive_partial) alive_partial[blockIdx.x] = a[0];
-    if (alive_d) alive_d[blockIdx.x] = (double)a[0];
+  double z = __dadd_rn(__dadd_rn(m[0], m[2]), __dadd_rn(m[1], m[3]));
+  for (int off = 32; off >= 1; off >>= 1) {
+    const double o = __shfl_down(z, off);
+    z = __dadd_rn(z, o);                       // lanes < off hold the tree's s[t]
+    a += __shfl_down(a, off);
+  }
+  if (lane == 0) {
+    partial[b] = z;
+    if (alive_partial) alive_partial[b] = a;
+    if (alive_d) alive_d[b] = (double)a;
   }
 }
 
@@ -685,8 +695,9 @@ __device__ __forceinline__ void place_pick_one(const DevWorld& W, int64_t i, uns
     for (int k = 0; k < nn; k++) cand[nc++] = nbr[k];
     if (W.allow_parent) cand[nc++] = parent;
   }
-  const uint32_t lo = W.b_rng[r], hi = W.b_rng[W.rcap + r];
-  uint32_t ctr = W.b_rng[2 * W.rcap + r];
+  int32_t* const inh = W.b_inh + (int64_t)r * BI_WORDS;
+  const uint32_t lo = (uint32_t)inh[BI_RLO], hi = (uint32_t)inh[BI_RHI];
+  uint32_t ctr = (uint32_t)inh[BI_RCTR];
   // no candidate (BIRTH_METHOD 3 without an empty neighbour): PositionOffspring
   // returns the parent's cell, drawing nothing (main/cPopulation.cc:5407)
   const int t = nc > 0 ? cand[rng_below(lo, hi, ctr, (uint32_t)nc)] : parent;
@@ -694,7 +705,7 @@ __device__ __forceinline__ void place_pick_one(const DevWorld& W, int64_t i, uns
   const unsigned long long prio = ((unsigned long long)rng_next(lo, hi, ctr) << 32) |
                                   ((unsigned long long)((W.cell0 + parent) & 0xFFFFFF) << 8) |
                                   (unsigned long long)(W.b_seq[r] & 0xFF);
-  W.b_rng[2 * W.rcap + r] = ctr;
+  inh[BI_RCTR] = (int32_t)ctr;
   W.b_target[r] = t;
   W.b_prio[r] = prio;
   if (round >= 0) W.b_tgt[(int64_t)round * W.rcap + r] = t;
@@ -982,11 +993,12 @@ __global__ __launch_bounds__(64) void k_halo_pack(DevWorld W) {
     if (lane == 0) {
       HaloRec r;
       r.col = col; r.round = W.b_state[i] - 1; r.len = fits ? len : -1;
-      r.gen = W.b_gen[i]; r.ccopied = W.b_ccopied[i]; r.exec = W.b_exec[i]; r.gest = W.b_gest[i];
-      r.rng_lo = W.b_rng[i]; r.rng_hi = W.b_rng[W.rcap + i]; r.rng_ctr = W.b_rng[2 * W.rcap + i];
-      r.off = off; r.pad = 0; r.merit = W.b_merit[i]; r.fitness = W.b_fitness[i];
+      const Child b = child_of_record(W, i);
+      r.gen = b.gen; r.ccopied = b.ccopied; r.exec = b.exec; r.gest = b.gest;
+      r.rng_lo = b.lo; r.rng_hi = b.hi; r.rng_ctr = b.ctr;
+      r.off = off; r.pad = 0; r.merit = b.merit; r.fitness = b.fitness;
 #pragma unroll
-      for (int t = 0; t < AVGPU_NUM_LOGIC_TASKS; t++) r.last_task[t] = W.b_ltask[(int64_t)t * W.rcap + i];
+      for (int t = 0; t < AVGPU_NUM_LOGIC_TASKS; t++) r.last_task[t] = b.ltask[t];
       r.pad2[0] = r.pad2[1] = r.pad2[2] = 0;
       recs[slot] = r;
       if (!fits) atomicAdd(&hdr->overflow, 1);
@@ -1218,7 +1230,7 @@ void launch_classify_uniform(const DevWorld& W, hipStream_t s, int64_t first, in
 void launch_merit_total(const DevWorld& W, hipStream_t s, double* totals, double* scratch) {
   const int64_t nb = (W.n + 255) / 256;
   int32_t* alive_partial = reinterpret_cast<int32_t*>(scratch + nb);
-  hipLaunchKernelGGL(k_merit_partial, dim3((unsigned)nb), dim3(256), 0, s, W, scratch, alive_partial,
+  hipLaunchKernelGGL(k_merit_partial, dim3((unsigned)((nb + 3) / 4)), dim3(256), 0, s, W, scratch, alive_partial,
                      (double*)nullptr, 0);
   hipLaunchKernelGGL(k_merit_final<false>, dim3(1), dim3(256), 0, s, scratch, alive_partial,
                      (const double*)nullptr, nb, 1, totals, 0);
@@ -1235,7 +1247,7 @@ void launch_world_begin(const DevWorld& W, hipStream_t s, double* totals, double
   const int64_t nb = (W.n + 255) / 256;
   int32_t* alive_partial = reinterpret_cast<int32_t*>(scratch + nb);
   launch_resources_begin(W, s);   // ProcessPreUpdate + the update's first DoUpdates
-  hipLaunchKernelGGL(k_merit_partial, dim3((unsigned)nb), dim3(256), 0, s, W, scratch, alive_partial,
+  hipLaunchKernelGGL(k_merit_partial, dim3((unsigned)((nb + 3) / 4)), dim3(256), 0, s, W, scratch, alive_partial,
                      (double*)nullptr, 1);
   hipLaunchKernelGGL(k_allot_total, dim3(nblk(W.n, 2048)), dim3(1024), 0, s, W, (const double*)scratch,
                      (const int32_t*)alive_partial, nb, totals, update);
@@ -1318,7 +1330,7 @@ void launch_world_post(const DevWorld& W, hipStream_t s, double* stats, bool eag
 // (a strip tile's partials start its update: block 0 also clears the counters)
 void launch_tile_partials(const DevWorld& W, hipStream_t s, double* out) {
   const int64_t nb = (W.n + 255) / 256;
-  hipLaunchKernelGGL(k_merit_partial, dim3((unsigned)nb), dim3(256), 0, s, W, out, (int32_t*)nullptr,
+  hipLaunchKernelGGL(k_merit_partial, dim3((unsigned)((nb + 3) / 4)), dim3(256), 0, s, W, out, (int32_t*)nullptr,
                      out + nb, W.tiled ? 1 : 0);
 }
 

@@ -19,8 +19,10 @@
 // birth record row b_inh[r * BI_WORDS ..]: merit, fitness (doubles), generation,
 // copied size, executed size, gestation time, the offspring's RNG key and
 // counter, the parent's last task counts
+// (BI_FINAL = 1: the divide left the offspring's fitness and key and the
+// parent's phenotype to finalize_record, world.hip)
 enum { BI_MERIT = 0, BI_FITNESS = 2, BI_GEN = 4, BI_CCOPIED = 5, BI_EXEC = 6, BI_GEST = 7,
-       BI_RLO = 8, BI_RHI = 9, BI_RCTR = 10, BI_LTASK = 12, BI_WORDS = 32 };
+       BI_RLO = 8, BI_RHI = 9, BI_RCTR = 10, BI_FINAL = 11, BI_LTASK = 12, BI_WORDS = 32 };
 #define CODE_MASK 0x3F
 #define TF_COPIED 0x40
 #define TF_EXEC 0x80

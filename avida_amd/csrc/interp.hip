@@ -1044,14 +1044,27 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
             double merit = __dmul_rn(base, bon);
             if (p_inherit == 0) merit = base;
             const int gt = tu - gs;
-            const double fit = __ddiv_rn(__dmul_rn(base, bon), (double)gt);
-            // write-only phenotype fields go out now (fire and forget) rather
-            // than being held in registers to the end of the slice
-            st_async_u64(g_merit + cell, (uint64_t)__double_as_longlong(merit));
-            st_async_u64(g_fitness + cell, (uint64_t)__double_as_longlong(fit));
-            st_async_u32(g_gest + cell, (uint32_t)gt);
-            st_async_u32(g_ccop + cell, (uint32_t)cop);       // SetLinesCopied
-            st_async_u32(g_exec + cell, (uint32_t)exe);
+            // The parent's phenotype (merit, fitness, gestation time, copied /
+            // executed size, last task counts) and the offspring's fitness and
+            // RNG key: a world slice at the default knobs leaves them to
+            // finalize_record (world.hip, placement round 0: SIMT over the
+            // records, where here one lane at a time ran them with the wave
+            // waiting); otherwise, or without a record, they are stored here.
+            const bool defer = DEF && mode == AVGPU_MODE_WORLD && !serial;
+            auto parent_phenotype = [&]() {
+              const double fit = __ddiv_rn(__dmul_rn(base, bon), (double)gt);
+              // write-only fields go out now (fire and forget) rather than
+              // being held in registers to the end of the slice
+              st_async_u64(g_merit + cell, (uint64_t)__double_as_longlong(merit));
+              st_async_u64(g_fitness + cell, (uint64_t)__double_as_longlong(fit));
+              st_async_u32(g_gest + cell, (uint32_t)gt);
+              st_async_u32(g_ccop + cell, (uint32_t)cop);     // SetLinesCopied
+              st_async_u32(g_exec + cell, (uint32_t)exe);
+#pragma unroll
+              for (int q = 0; q < AVGPU_NUM_LOGIC_TASKS; q++)
+                st_async_u32(g_ltask + (int64_t)q * N + cell, (uint32_t)tc[q]);
+            };
+            if (!defer) parent_phenotype();
             gs = tu;
             dnd = nd;
             const int gen = dgen + 1;
@@ -1060,9 +1073,6 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
             errs = 0;
             bonus = p_defb;
             cyc = 0;
-#pragma unroll
-            for (int q = 0; q < AVGPU_NUM_LOGIC_TASKS; q++)
-              st_async_u32(g_ltask + (int64_t)q * N + cell, (uint32_t)tc[q]);
             nzm = 0;
 #pragma unroll
             for (int i = 0; i < AVGPU_MAX_REACTIONS; i++) rc[i] = i < k_n_react ? 0 : rc[i];
@@ -1396,9 +1406,10 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
               prim = true;
               }
               if (serial && rec >= 0) sbirth = 1;      // placed by the caller before any speculation
+              if (defer && rec < 0) parent_phenotype();   // no record to carry it
               if (rec >= 0) {
-                uint32_t clo, chi;
-                derive_key(olo, ohi, (uint32_t)nd, 0x1B873593U, clo, chi);
+                uint32_t clo = 0u, chi = 0u;
+                if (!defer) derive_key(olo, ohi, (uint32_t)nd, 0x1B873593U, clo, chi);
                 // the record arrays, loaded together (see OPQ above)
                 int32_t* b_parent = W.b_parent;
                 uint32_t* b_seq = W.b_seq;
@@ -1427,11 +1438,13 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
                     W.b_pcnt[(int64_t)k * rcap + rec] = pcnt[k];
                   }
                 // the inherited phenotype: one 128-B row, 16-B stores (device.h BI_*)
+                // (deferred: fitness and key left to finalize_record, BI_FINAL = 1)
                 int32_t* irow = b_inh + (int64_t)rec * BI_WORDS;
-                const long long mb = __double_as_longlong(merit), fb = __double_as_longlong(fit);
+                const long long mb = __double_as_longlong(merit);
+                const long long fb = defer ? 0ll : __double_as_longlong(__ddiv_rn(__dmul_rn(base, bon), (double)gt));
                 st_async_b128(irow, (uint32_t)mb, (uint32_t)(mb >> 32), (uint32_t)fb, (uint32_t)(fb >> 32));
                 st_async_b128(irow + 4, (uint32_t)gen, (uint32_t)cop, (uint32_t)exe, (uint32_t)gt);
-                st_async_b128(irow + 8, clo, chi, 0u, 0u);
+                st_async_b128(irow + 8, clo, chi, 0u, defer ? 1u : 0u);
                 st_async_b128(irow + 12, (uint32_t)tc[0], (uint32_t)tc[1], (uint32_t)tc[2], (uint32_t)tc[3]);
                 st_async_b128(irow + 16, (uint32_t)tc[4], (uint32_t)tc[5], (uint32_t)tc[6], (uint32_t)tc[7]);
                 st_async_b128(irow + 20, (uint32_t)tc[8], 0u, 0u, 0u);
@@ -1623,6 +1636,9 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
     // (a fresh organism's zero rows are stored here rather than at activation:
     // k_activate is bound by its scattered stores, class 0 is not)
     if (didv || fresh) { W.num_div[cell] = dnd; W.generation[cell] = dgen; }
+    // (a deferred divide's executed size: a spill row continuing this slice
+    // in the same update reads it at its staging)
+    if (didv) W.executed[cell] = dexe;
     if (fresh) {
 #pragma unroll
       for (int q = AVGPU_NUM_LOGIC_TASKS; q < AVGPU_MAX_REACTIONS; q++) W.last_task[(int64_t)q * N + cell] = 0;

@@ -672,11 +672,47 @@ __device__ __forceinline__ unsigned long long tile_merged(const DevWorld& W, int
 // tile_m >= 0 (strip tiles, k_tile_round): occupancy by tile_taken, and a
 // claim on an edge or ghost cell also goes into the halo send slot of its
 // round's parity (atomicMax: the exchange after the launch carries it)
+// The rest of a deferred divide (interp.hip, BI_FINAL), run once per record
+// by placement round 0 before its draws: the offspring's fitness
+// (cPhenotype::DivideReset, merit / gestation time) and RNG key (derived from
+// the parent's key and divide count), and -- from the record of the parent's
+// last divide of the update, the one whose sequence number is its final
+// num_div -- the parent's merit, fitness, gestation time, copied / executed
+// sizes and last task counts (main/cPhenotype.cc:824-1000).
+__device__ __forceinline__ void finalize_record(const DevWorld& W, int64_t r) {
+  int32_t* row = W.b_inh + r * BI_WORDS;
+  if (row[BI_FINAL] == 0) return;
+  const int4 q0 = reinterpret_cast<const int4*>(row)[0], q1 = reinterpret_cast<const int4*>(row)[1];
+  const double merit = __hiloint2double(q0.y, q0.x);
+  const int gt = q1.w;
+  const double fit = __ddiv_rn(merit, (double)gt);
+  const int parent = W.b_parent[r];
+  const uint32_t seq = W.b_seq[r];
+  uint32_t clo, chi;
+  derive_key(W.rng[parent], W.rng[W.n + parent], seq, 0x1B873593U, clo, chi);
+  const long long fb = __double_as_longlong(fit);
+  row[BI_FITNESS] = (int32_t)fb;
+  row[BI_FITNESS + 1] = (int32_t)(fb >> 32);
+  row[BI_RLO] = (int32_t)clo;
+  row[BI_RHI] = (int32_t)chi;
+  row[BI_FINAL] = 0;
+  if ((int)seq == W.num_div[parent]) {
+    W.merit[parent] = merit;
+    W.fitness[parent] = fit;
+    W.gest_time[parent] = gt;
+    W.child_copied[parent] = q1.y;
+    W.executed[parent] = q1.z;
+#pragma unroll
+    for (int q = 0; q < AVGPU_NUM_LOGIC_TASKS; q++) W.last_task[(int64_t)q * W.n + parent] = row[BI_LTASK + q];
+  }
+}
+
 __device__ __forceinline__ void place_pick_one(const DevWorld& W, int64_t i, unsigned long long* claim,
                                                unsigned long long* prev,
                                                const unsigned long long* occ_prev = nullptr, int round = -1,
                                                int tile_m = -1) {
   const int64_t r = (round >= 0) ? i : rec_of(W, i);
+  if (round <= 0) finalize_record(W, r);      // round 0: the record's first touch after its divide
   if (prev) {
     const int t0 = W.b_target[r];
     if (t0 >= 0) prev[t0] = 0ull;

@@ -217,7 +217,7 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
   const bool fresh = active && (W.ctl[cell] & CTL_FRESH);
 #ifdef AVGPU_PHASE_CLOCKS
   const uint64_t clk0 = __builtin_amdgcn_s_memtime();
-  int it_fast = 0, it_copy = 0, it_slow = 0;
+  int it_fast = 0, it_copy = 0, it_slow = 0, it_loop = 0;   // it_loop: loop iterations (wave-uniform)
   // loop cycles by block: decode, fast, copy, switch, wave phase, advance
   uint64_t cb[6] = {0, 0, 0, 0, 0, 0};
   uint64_t clast = 0;
@@ -362,9 +362,12 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
   const uint64_t clk1 = __builtin_amdgcn_s_memtime();
 #endif
 
-  bool alive = active && (ctl & CTL_ALIVE);
-  const bool alive0 = alive;
-  bool stop = false, spill = false;
+  // the lane's run state as bits of one int (F_DEAD | F_STOP | F_SPILL): as
+  // three bools, each was a lane mask in SGPRs that every join of the
+  // divergent loop body merged with its own s_andn2 / s_and / s_or triple
+  enum { F_DEAD = 1, F_STOP = 2, F_SPILL = 4 };
+  int fl = (active && (ctl & CTL_ALIVE)) ? 0 : F_DEAD;
+  const bool alive0 = fl == 0;
   int executed = 0, divides = 0;
 
   // world scalars the loop uses, read once: through the descriptor pointer
@@ -441,19 +444,24 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
   int io_id = -2;                                             // IO's logic id (-1: none; -2: no IO this step)
   // class 0's task LUT (256 x u16) spread over the wave: lane j holds entries 4j .. 4j+3
   uint32_t tl0 = 0u, tl1 = 0u;
+  // and its per-task bonus factors / addends (32 doubles): lane j holds word j,
+  // read by v_readlane at a wave-uniform task index
+  uint32_t ttab = 0u;
   if (GLUT) {
     const uint32_t* g_lut = reinterpret_cast<const uint32_t*>(W.task_lut);
     tl0 = g_lut[2 * lane];
     tl1 = g_lut[2 * lane + 1];
+    ttab = reinterpret_cast<const uint32_t*>(W.task_tab)[lane];
   }
   const uint32_t* T32 = reinterpret_cast<const uint32_t*>(T);
   const int slow_batch = W.slow_batch;
 
   while (true) {
-    const bool run = alive && budget > 0 && !stop && !spill && pop < 0;
+    const bool run = fl == 0 && budget > 0 && pop < 0;
     if (!__any(run || pop >= 0)) break;                       // wave-uniform loop
 #ifdef AVGPU_PHASE_CLOCKS
     if (clast == 0) clast = __builtin_amdgcn_s_memtime();
+    it_loop++;
     CK(5);
 #endif
     bool adv = true;                                          // m_advance_ip
@@ -480,12 +488,12 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
         const bool ok = !(k_require_allocate && (ctl & CTL_MAL)) && alloc >= 1 &&
                         nsz <= AVGPU_MAX_GENOME && nsz >= AVGPU_MIN_GENOME &&
                         alloc <= (int)(cur * k_size_range) && cur <= (int)(alloc * k_size_range);
-        if (ok && nsz > S) { spill = true; ip = ipa; }
+        if (ok && nsz > S) { fl |= F_SPILL; ip = ipa; }
       }
       // serial step: the speculative run ends before IO / h-divide
       // (cHardwareCPU::SingleProcess stall instructions, cpu/cHardwareCPU.cc:961-968)
-      if (serial == 2 && (op == AVGPU_H_IO || op == AVGPU_H_H_DIVIDE)) stop = true;
-    if (!spill && !stop) {
+      if (serial == 2 && (op == AVGPU_H_IO || op == AVGPU_H_H_DIVIDE)) fl |= F_STOP;
+    if (fl == 0) {
     stepped = true;
     cyc++;                                                    // IncCPUCyclesUsed :929
     tu++;                                                     // IncTimeUsed :930
@@ -627,7 +635,7 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
         }
       }
       if (cspill) {
-        spill = true;
+        fl |= F_SPILL;
         stepped = false;
       } else if (!DEF && k_copy_ext) {
         rh = head_adjust(rh + 1, M);
@@ -670,17 +678,17 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
     if (!(FAST_OPS & obit) && op != AVGPU_H_H_COPY && !lab_done) { pop = op; pr = r; stepped = false; }   // park
     }  // !spill
     }  // run
-    if (stepped && !stop) {
+    if (stepped && !(fl & F_STOP)) {
       if (adv) ip = head_wrap(ip + 1, M);                     // ip.Advance() :1013
       if (mx > 0 && tu >= mx) {                               // death :1045-1049
-        if (serial == 2) { sdie = 1; stop = true; executed--; }   // m_spec_die: not counted
-        else alive = false;
+        if (serial == 2) { sdie = 1; fl |= F_STOP; executed--; }   // m_spec_die: not counted
+        else fl |= F_DEAD;
       }
     }
     // ---- slow phase ----
     const int npark = __popcll(__ballot(pop >= 0));
     if (npark == 0) continue;
-    if (npark < slow_batch && __any(alive && budget > 0 && !stop && !spill && pop < 0)) continue;
+    if (npark < slow_batch && __any(fl == 0 && budget > 0 && pop < 0)) continue;
 #ifdef AVGPU_PHASE_CLOCKS
     it_slow++;
 #endif
@@ -846,9 +854,10 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
     // cEnvironment::TestOutput / TestRequisites / DoProcesses
     // (main/cEnvironment.cc:1314-1406, :1408-1503, :1610-1760), then
     // GetNextInput + DoInput.  Class 0 holds its task LUT spread over the
-    // wave's lanes (tl0 / tl1) and reads it by lane shuffles, and reads the
-    // per-task bonus factors as wave-uniform scalar loads: a vector load here
-    // waited (vmcnt) for every store the wave still had in flight.
+    // wave's lanes (tl0 / tl1) and reads it by lane shuffles, and its per-task
+    // bonus factors (ttab) by v_readlane at a wave-uniform task: a vector load
+    // here waited (vmcnt) for every store the wave still had in flight, and a
+    // scalar load per task present cost a memory round trip each.
     if (__ballot(io_id >= -1) != 0ull) {
       const bool io = io_id >= -1;
       uint32_t tmask = 0u;
@@ -874,8 +883,10 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
             if ((k_env_res_mask >> t) & 1u) {                 // finite resource
               if (dt && !consume_resource(W, W.react_res + t * RR_STRIDE, N, cell, mult, addb)) paid &= ~(1u << t);
             } else {
-              const double fm = GTAB ? ld_uniform_f64(tmul + t) : tmul[t];
-              const double fa = GTAB ? ld_uniform_f64(tadd + t) : tadd[t];
+              const double fm = GTAB ? __hiloint2double(__builtin_amdgcn_readlane((int)ttab, 2 * t + 1),
+                                                        __builtin_amdgcn_readlane((int)ttab, 2 * t)) : tmul[t];
+              const double fa = GTAB ? __hiloint2double(__builtin_amdgcn_readlane((int)ttab, 33 + 2 * t),
+                                                        __builtin_amdgcn_readlane((int)ttab, 32 + 2 * t)) : tadd[t];
               if (dt) { mult = __dmul_rn(mult, fm); addb = __dadd_rn(addb, fa); }
             }
           }
@@ -1080,7 +1091,7 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
             if (mode == AVGPU_MODE_TEST) {
               st_async_u32(W.t_flags_len + cell, (uint32_t)div);
               st_async_u32(W.t_child_len + cell, (uint32_t)child);
-              stop = true;
+              fl |= F_STOP;
             } else {
               // Divide_DoMutations (cpu/cHardwareBase.cc:296-569) in the
               // reference's order of draws (oracle divide_mutations): slip,
@@ -1579,11 +1590,11 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
       }
     }
 
-    if (sstep && !stop) {
+    if (sstep && !(fl & F_STOP)) {
       if (adv) ip = head_adjust(ip + 1, M);                   // ip.Advance() :1013
       if (mx > 0 && tu >= mx) {                               // death :1045-1049
-        if (serial == 2) { sdie = 1; stop = true; executed--; }
-        else alive = false;
+        if (serial == 2) { sdie = 1; fl |= F_STOP; executed--; }
+        else fl |= F_DEAD;
       }
     }
     pop = -1;
@@ -1622,6 +1633,8 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
                                    stk[(4 * j + 2) * 64 + lane], stk[(4 * j + 3) * 64 + lane]);
 #pragma unroll
     for (int j = 0; j < 3; j++) xw[13 + j] = make_int4(rc[4 * j], rc[4 * j + 1], rc[4 * j + 2], rc[4 * j + 3]);
+    const bool alive = !(fl & F_DEAD);
+    const bool spill = (fl & F_SPILL) != 0;
     if (!alive) ctl &= ~CTL_ALIVE;
     // a death frees the cell for this update's placement (k_allot_total
     // marked the living cells occupied)
@@ -1688,7 +1701,7 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
   }
   // counters: one atomic per wave
   unsigned long long e = (unsigned long long)executed;
-  int dead = (active && !alive) ? 1 : 0;
+  int dead = (active && (fl & F_DEAD)) ? 1 : 0;
   int dv = divides;
   int mxe = executed;
   int sl = active ? 1 : 0;
@@ -1730,7 +1743,7 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
       count_add(W, CNT_CLK_STAGE, clk1 - clk0);
       count_add(W, CNT_CLK_LOOP, clk2 - clk1);
       count_add(W, CNT_CLK_WB, clk3 - clk2);
-      count_add(W, CNT_ITERS, (unsigned long long)mxe);
+      count_add(W, CNT_ITERS, (unsigned long long)it_loop);
       count_add(W, CNT_IT_FAST, (unsigned long long)it_fast);
       count_add(W, CNT_IT_COPY, (unsigned long long)it_copy);
       count_add(W, CNT_IT_SLOW, (unsigned long long)it_slow);

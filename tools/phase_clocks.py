@@ -4,7 +4,8 @@ Loads the AVGPU_PHASE_CLOCKS build (avida_amd/libavida_gpu_clk.so, built by
 `python avida_amd/build.py --clocks`), runs the bench world for a few updates
 and prints, per wave: s_memtime cycles spent staging (LDS-DMA of tapes +
 stacks + state loads), in the interpreter loop, and writing back; loop
-iterations; and how many iterations entered the branch-free block, the h-copy
+iterations (CNT_ITERS counts real loop iterations, parked lanes
+included); and how many iterations entered the branch-free block, the h-copy
 block and the switch (divergence: one iteration can enter several)."""
 import ctypes as C
 import json

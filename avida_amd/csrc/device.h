@@ -20,7 +20,7 @@
 // copied size, executed size, gestation time, the offspring's RNG key and
 // counter, the parent's last task counts
 // (BI_FINAL = 1: the divide left the offspring's fitness and key and the
-// parent's phenotype to finalize_record, world.hip)
+// parent's phenotype to finalize_key / finalize_phenotype, world.hip)
 enum { BI_MERIT = 0, BI_FITNESS = 2, BI_GEN = 4, BI_CCOPIED = 5, BI_EXEC = 6, BI_GEST = 7,
        BI_RLO = 8, BI_RHI = 9, BI_RCTR = 10, BI_FINAL = 11, BI_LTASK = 12, BI_WORDS = 32 };
 #define CODE_MASK 0x3F

@@ -1058,7 +1058,7 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
             // The parent's phenotype (merit, fitness, gestation time, copied /
             // executed size, last task counts) and the offspring's fitness and
             // RNG key: a world slice at the default knobs leaves them to
-            // finalize_record (world.hip, placement round 0: SIMT over the
+            // finalize_key / finalize_phenotype (world.hip, placement round 0: SIMT over the
             // records, where here one lane at a time ran them with the wave
             // waiting); otherwise, or without a record, they are stored here.
             const bool defer = DEF && mode == AVGPU_MODE_WORLD && !serial;
@@ -1449,7 +1449,7 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
                     W.b_pcnt[(int64_t)k * rcap + rec] = pcnt[k];
                   }
                 // the inherited phenotype: one 128-B row, 16-B stores (device.h BI_*)
-                // (deferred: fitness and key left to finalize_record, BI_FINAL = 1)
+                // (deferred: fitness and key left to world.hip's finalize_*, BI_FINAL = 1)
                 int32_t* irow = b_inh + (int64_t)rec * BI_WORDS;
                 const long long mb = __double_as_longlong(merit);
                 const long long fb = defer ? 0ll : __double_as_longlong(__ddiv_rn(__dmul_rn(base, bon), (double)gt));

@@ -672,31 +672,37 @@ __device__ __forceinline__ unsigned long long tile_merged(const DevWorld& W, int
 // tile_m >= 0 (strip tiles, k_tile_round): occupancy by tile_taken, and a
 // claim on an edge or ghost cell also goes into the halo send slot of its
 // round's parity (atomicMax: the exchange after the launch carries it)
-// The rest of a deferred divide (interp.hip, BI_FINAL), run once per record
-// by placement round 0 before its draws: the offspring's fitness
-// (cPhenotype::DivideReset, merit / gestation time) and RNG key (derived from
-// the parent's key and divide count), and -- from the record of the parent's
-// last divide of the update, the one whose sequence number is its final
-// num_div -- the parent's merit, fitness, gestation time, copied / executed
-// sizes and last task counts (main/cPhenotype.cc:824-1000).
-__device__ __forceinline__ void finalize_record(const DevWorld& W, int64_t r) {
+// The rest of a deferred divide (interp.hip, BI_FINAL), in two halves that
+// run side by side in placement round 0's launch.  The offspring's RNG key
+// (derived from the parent's key and divide count) is the pick's, which draws
+// from it (finalize_key); the offspring's fitness (cPhenotype::DivideReset,
+// merit / gestation time) and -- from the record of the parent's last divide
+// of the update, the one whose sequence number is its final num_div -- the
+// parent's merit, fitness, gestation time, copied / executed sizes and last
+// task counts (main/cPhenotype.cc:824-1000) are the extra blocks'
+// (finalize_phenotype), off the pick's dependency chain.  BI_FINAL stays set
+// (a row is rewritten whole by its next divide): both halves test it.
+__device__ __forceinline__ void finalize_key(const DevWorld& W, int64_t r, int parent) {
   int32_t* row = W.b_inh + r * BI_WORDS;
   if (row[BI_FINAL] == 0) return;
+  uint32_t clo, chi;
+  derive_key(W.rng[parent], W.rng[W.n + parent], W.b_seq[r], 0x1B873593U, clo, chi);
+  row[BI_RLO] = (int32_t)clo;
+  row[BI_RHI] = (int32_t)chi;
+}
+__device__ __forceinline__ void finalize_phenotype(const DevWorld& W, int64_t r) {
+  int32_t* row = W.b_inh + r * BI_WORDS;
   const int4 q0 = reinterpret_cast<const int4*>(row)[0], q1 = reinterpret_cast<const int4*>(row)[1];
+  const int fin = row[BI_FINAL];
+  if (fin == 0) return;
   const double merit = __hiloint2double(q0.y, q0.x);
   const int gt = q1.w;
   const double fit = __ddiv_rn(merit, (double)gt);
-  const int parent = W.b_parent[r];
-  const uint32_t seq = W.b_seq[r];
-  uint32_t clo, chi;
-  derive_key(W.rng[parent], W.rng[W.n + parent], seq, 0x1B873593U, clo, chi);
   const long long fb = __double_as_longlong(fit);
   row[BI_FITNESS] = (int32_t)fb;
   row[BI_FITNESS + 1] = (int32_t)(fb >> 32);
-  row[BI_RLO] = (int32_t)clo;
-  row[BI_RHI] = (int32_t)chi;
-  row[BI_FINAL] = 0;
-  if ((int)seq == W.num_div[parent]) {
+  const int parent = W.b_parent[r];
+  if ((int)W.b_seq[r] == W.num_div[parent]) {
     W.merit[parent] = merit;
     W.fitness[parent] = fit;
     W.gest_time[parent] = gt;
@@ -712,13 +718,13 @@ __device__ __forceinline__ void place_pick_one(const DevWorld& W, int64_t i, uns
                                                const unsigned long long* occ_prev = nullptr, int round = -1,
                                                int tile_m = -1) {
   const int64_t r = (round >= 0) ? i : rec_of(W, i);
-  if (round <= 0) finalize_record(W, r);      // round 0: the record's first touch after its divide
   if (prev) {
     const int t0 = W.b_target[r];
     if (t0 >= 0) prev[t0] = 0ull;
   }
   if (W.b_state[r] != 0) return;
   const int parent = W.b_parent[r];
+  if (round <= 0) finalize_key(W, r, parent);   // round 0: the record's first draws
   int nbr[8];
   const int nn = neighbours(W, parent, nbr);
   int cand[9];
@@ -790,7 +796,7 @@ __global__ void k_place_round(DevWorld W, int m) {
 // and share one launch instead of two latency-bound ones.
 // fused: the single world's round arrays (claim rows and b_tgt, k_place_round)
 __global__ __launch_bounds__(256) void k_place_pick_mut(DevWorld W, unsigned long long* claim, int pblocks,
-                                                        int fused) {
+                                                        int fused, int fblocks) {
   __shared__ uint8_t child[4][TAPE_SLOT + 16];
   const int nb = queue_len(W);
   if ((int)blockIdx.x < pblocks) {
@@ -800,6 +806,12 @@ __global__ __launch_bounds__(256) void k_place_pick_mut(DevWorld W, unsigned lon
     }
     return;
   }
+  if ((int)blockIdx.x < pblocks + fblocks) {   // deferred divides' phenotype half
+    for (int64_t i = (int64_t)(blockIdx.x - pblocks) * 256 + threadIdx.x; i < nb; i += (int64_t)fblocks * 256)
+      finalize_phenotype(W, rec_of(W, i));
+    return;
+  }
+  pblocks += fblocks;
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int64_t wave = (int64_t)(blockIdx.x - pblocks) * 4 + wv, nwaves = (int64_t)(gridDim.x - pblocks) * 4;
   for (int64_t q0 = wave * MUT_PER_WAVE; q0 < nb; q0 += nwaves * MUT_PER_WAVE) {
@@ -828,9 +840,16 @@ __global__ __launch_bounds__(256) void k_place_pick_mut(DevWorld W, unsigned lon
 // mutations (as k_place_pick_mut's extra blocks); the rest walk the 2 x X
 // halo cells: the ghost rows empty (occ, owner, every round's claims), the
 // edge rows' occupancy into the send buffers and both parities' claim slots
-// zeroed.  (k_allot initialised the tile's own cells.)
-__global__ __launch_bounds__(256) void k_tile_prep(DevWorld W, int mblocks) {
+// zeroed; fblocks more run the deferred divides' phenotype half
+// (finalize_phenotype).  (k_allot initialised the tile's own cells.)
+__global__ __launch_bounds__(256) void k_tile_prep(DevWorld W, int mblocks, int fblocks) {
   __shared__ uint8_t child[4][TAPE_SLOT + 16];
+  if ((int)blockIdx.x >= mblocks && (int)blockIdx.x < mblocks + fblocks) {
+    const int nb = queue_len(W);
+    for (int64_t i = (int64_t)(blockIdx.x - mblocks) * 256 + threadIdx.x; i < nb; i += (int64_t)fblocks * 256)
+      finalize_phenotype(W, rec_of(W, i));
+    return;
+  }
   if ((int)blockIdx.x < mblocks) {
     const int nb = queue_len(W);
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -856,7 +875,7 @@ __global__ __launch_bounds__(256) void k_tile_prep(DevWorld W, int mblocks) {
     return;
   }
   const int X = W.world_x;
-  const int g = (blockIdx.x - mblocks) * blockDim.x + threadIdx.x;
+  const int g = (blockIdx.x - mblocks - fblocks) * blockDim.x + threadIdx.x;
   if (g >= 2 * X) return;
   const int d = g / X, x = g - d * X;
   const int64_t gc = ghost_cell(W, d, x);
@@ -1356,7 +1375,8 @@ void launch_world_post(const DevWorld& W, hipStream_t s, double* stats, bool eag
   // launches instead of 9 (k_place_round)
   const unsigned bb = place_grid(W);
   const int pm = has_divide_mutations(W) ? (int)((mut_grid(W) + 3) / 4) : 0;
-  hipLaunchKernelGGL(k_place_pick_mut, dim3(bb + pm), dim3(256), 0, s, W, W.claim_r[0], (int)bb, 1);
+  const int pf = (int)std::min<unsigned>(bb, 256u);   // finalize_phenotype blocks
+  hipLaunchKernelGGL(k_place_pick_mut, dim3(bb + pf + pm), dim3(256), 0, s, W, W.claim_r[0], (int)bb, 1, pf);
   for (int m = 1; m < 4; m++) hipLaunchKernelGGL(k_place_round, dim3(bb), dim3(256), 0, s, W, m);
   hipLaunchKernelGGL(k_activate, dim3(lane_grid(W)), dim3(64), 0, s, W, (unsigned long long*)nullptr, 1);
   if (eager) launch_stats(W, s, stats);
@@ -1382,7 +1402,8 @@ void launch_tile_totals(const DevWorld& W, hipStream_t s, const double* gathered
 void launch_tile_after_interpret(const DevWorld& W, hipStream_t s) {
   const unsigned hb = nblk(2 * (int64_t)W.world_x, 256);
   const int mb = has_divide_mutations(W) ? (int)((mut_grid(W) + 3) / 4) : 0;
-  hipLaunchKernelGGL(k_tile_prep, dim3(mb + hb), dim3(256), 0, s, W, mb);
+  const int fb = (int)std::min<unsigned>(place_grid(W), 256u);   // finalize_phenotype blocks
+  hipLaunchKernelGGL(k_tile_prep, dim3(mb + fb + hb), dim3(256), 0, s, W, mb, fb);
 }
 
 // phase 0: round `round` (k_tile_round: resolve round - 1, pick round)

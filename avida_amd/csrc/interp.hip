@@ -877,12 +877,26 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
         if (__ballot(done != 0u) != 0ull) {
           double mult = 1.0, addb = 0.0;
           uint32_t paid = done;
+          if (k_env_res_mask != 0u) {
+            // finite resources: each lane walks its own tasks, so that a
+            // wave's resource loads go out together (one memory round trip
+            // per task rank, not one per distinct task of the wave)
+            if (done) {
+              for (uint32_t d = done; d; d &= d - 1u) {
+                const int t = __ffs(d) - 1;
+                if ((k_env_res_mask >> t) & 1u) {
+                  if (!consume_resource(W, W.react_res + t * RR_STRIDE, N, cell, mult, addb)) paid &= ~(1u << t);
+                } else {
+                  mult = __dmul_rn(mult, tmul[t]);
+                  addb = __dadd_rn(addb, tadd[t]);
+                }
+              }
+            }
+          } else
           for (int t = 0; t < AVGPU_NUM_LOGIC_TASKS; t++) {   // wave-uniform t
             const bool dt = (done >> t) & 1u;
             if (__ballot(dt) == 0ull) continue;
-            if ((k_env_res_mask >> t) & 1u) {                 // finite resource
-              if (dt && !consume_resource(W, W.react_res + t * RR_STRIDE, N, cell, mult, addb)) paid &= ~(1u << t);
-            } else {
+            {
               const double fm = GTAB ? __hiloint2double(__builtin_amdgcn_readlane((int)ttab, 2 * t + 1),
                                                         __builtin_amdgcn_readlane((int)ttab, 2 * t)) : tmul[t];
               const double fa = GTAB ? __hiloint2double(__builtin_amdgcn_readlane((int)ttab, 33 + 2 * t),

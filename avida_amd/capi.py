@@ -128,7 +128,7 @@ class AvgpuCpuState(C.Structure):
         ("last_task_count", C.c_int32 * MAX_REACTIONS),
         ("cur_reaction_count", C.c_int32 * MAX_REACTIONS),
         ("rng_counter", C.c_uint32), ("rng_key_lo", C.c_uint32), ("rng_key_hi", C.c_uint32),
-        ("errors", C.c_int32), ("pad1", C.c_int32),
+        ("errors", C.c_int32), ("head_start", C.c_uint32),
         ("cur_bonus", C.c_double), ("merit", C.c_double), ("fitness", C.c_double),
         ("credit", C.c_double),
     ]
@@ -153,7 +153,8 @@ class AvgpuUpdateStats(C.Structure):
         ("sum_genome_length", C.c_double), ("max_fitness", C.c_double),
         ("ave_generation", C.c_double), ("sum_mem_size", C.c_double),
         ("cum_insts_executed", C.c_int64), ("cum_births", C.c_int64), ("slices", C.c_int64),
-        ("lane_steps", C.c_int64), ("births_overwritten", C.c_int64),
+        ("lane_steps", C.c_int64), ("births_overwritten", C.c_int64), ("births_cancelled", C.c_int64),
+        ("seed", C.c_uint64),
     ]
 
 

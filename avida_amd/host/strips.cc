@@ -347,10 +347,13 @@ void update(std::vector<Tile>& tiles, Transport& tr, hipStream_t s) {
   if (tiles[0].res_bytes > 0) tr.exchange(tiles, Kind::Resources, s);
   for (Tile& t : tiles) AV_OK(avgpu_tile_begin(t.h, t.gathered, ntiles_total));
   tr.exchange(tiles, Kind::Halo, s);
+  // round 0's picks and kill times, then the cancellations and round 0's
+  // claims (phase 3, with the neighbours' kill times on the edge rows); then
   // one launch and one exchange per placement round (both strips resolve each
   // edge cell alike, at the start of the next round's launch)
-  for (int rnd = 0; rnd < 4; rnd++) {
-    for (Tile& t : tiles) AV_OK(avgpu_tile_place(t.h, rnd, 0));
+  const int steps[5][2] = {{0, 0}, {0, 3}, {1, 0}, {2, 0}, {3, 0}};
+  for (const auto& st : steps) {
+    for (Tile& t : tiles) AV_OK(avgpu_tile_place(t.h, st[0], st[1]));
     tr.exchange(tiles, Kind::Halo, s);
   }
   for (Tile& t : tiles) AV_OK(avgpu_tile_place(t.h, 3, 1));   // last resolve, records packed

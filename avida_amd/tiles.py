@@ -10,7 +10,9 @@ tiled world equals the same update of the untiled world cell for cell
 include/avida_gpu.h ("strip tiles"):
 
     tile_partials -> all_gather -> tile_begin -> exchange(halo)
-    4 x [tile_place(r, 0) -> exchange(halo)]
+    tile_place(0, 0) (picks, kill times) -> exchange(halo)
+    tile_place(0, 3) (cancellations, round-0 claims) -> exchange(halo)
+    3 x [tile_place(r, 0) -> exchange(halo)]
     tile_place(3, 1) -> exchange(records) issued -> tile_place(3, 2) (own
     winners, while the records travel) -> wait(records) -> tile_finish
     with resources: exchange(resources) after the all_gather (edge rows of
@@ -177,12 +179,15 @@ class StripWorld:
         for t in tiles:
             t.call("tile_begin", C.c_void_p(t.gathered.data_ptr()), t.ntiles)
         self.tr.exchange(tiles, "halo")
-        # one launch and one exchange per placement round: round r's launch
-        # resolves round r - 1 with the claims both strips sent and picks
-        # round r; the claims on both sides of each strip edge go out together
-        for rnd in range(4):
+        # round 0: the picks and their kill times, then (with the neighbours'
+        # kill times on the edge rows) the cancellations and round 0's
+        # claims; then one launch and one exchange per placement round: round
+        # r's launch resolves round r - 1 with the claims both strips sent and
+        # picks round r; the claims on both sides of each strip edge go out
+        # together
+        for rnd, phase in ((0, 0), (0, 3), (1, 0), (2, 0), (3, 0)):
             for t in tiles:
-                t.call("tile_place", rnd, 0)
+                t.call("tile_place", rnd, phase)
             self.tr.exchange(tiles, "halo")
         for t in tiles:
             t.call("tile_place", 3, 1)     # round 3 resolved, the halo offspring packed

@@ -284,7 +284,8 @@ typedef struct avgpu_cpu_state {
   uint32_t rng_counter;                /* draws consumed from this organism's stream */
   uint32_t rng_key_lo, rng_key_hi;
   int32_t errors;                      /* cPhenotype::cur_num_errors (faults) */
-  int32_t pad1;                        /* explicit: the record's bytes are digested (avgpu_state_digests) */
+  uint32_t head_start;                 /* 2^16 - birth time of an offspring not yet allotted (its first
+                                          allotment weights its merit by 1 + head_start / 2^16); 0 otherwise */
   double cur_bonus;
   double merit;
   double fitness;
@@ -329,8 +330,12 @@ typedef struct avgpu_update_stats {
   int64_t cum_births;
   int64_t slices;              /* organism time slices interpreted this update */
   int64_t lane_steps;          /* 64 x longest lane per wave (SIMD lane-issue slots used) */
-  int64_t births_overwritten;  /* placed, then killed by a later birth into the same cell this update
-                                  (every successful divide is births + births_overwritten + births_dropped) */
+  int64_t births_overwritten;  /* placed, then killed by a later birth into the same cell this update */
+  int64_t births_cancelled;    /* never placed: an earlier birth into the parent's cell killed the parent
+                                  before this divide (every successful divide is births +
+                                  births_overwritten + births_cancelled + births_dropped) */
+  uint64_t seed;               /* the world's RANDOM_SEED, the key of the scheduler's draws: a checkpoint
+                                  carries it and avgpu_set_clock restores it with the clock */
 } avgpu_update_stats;
 
 typedef struct avgpu_world avgpu_world;   /* opaque handle */

@@ -216,6 +216,7 @@ struct Org {
   // batch-world bookkeeping
   Stream rng;
   double credit = 0.0;
+  uint32_t hstart = 0;   // head start: 2^16 - birth time, for the first allotment after birth (sched_weight)
   int spec_count = 0;
   // test-CPU outputs
   std::vector<uint8_t> offspring;
@@ -234,6 +235,7 @@ struct Birth {
   Stream rng;     // the child's stream
   int64_t target = -1;
   bool placed = false;
+  uint32_t t = 0;   // birth time in the update, 1/2^16 (birth_time)
 };
 
 struct World {
@@ -278,13 +280,16 @@ struct World {
   // per-update placement state of the tiled path
   std::vector<uint8_t> occ;
   std::vector<uint64_t> claim_r[4];   // each placement round's claims
-  std::vector<int64_t> owner;     // birth index, -1 none, -2-k won by a halo birth in round k
-  std::vector<uint64_t> prio;
-  std::vector<int8_t> bstate;     // 0 pending, 1+k placed in round k, -1 failed
+  std::vector<int64_t> tgt_r[4];      // each record's target in each round it picked in
+  std::vector<int64_t> owner;     // birth index, -1 none, remote_owner(m, t) won by a halo birth
+  std::vector<uint32_t> killt;    // per cell: 2^16 - the earliest kill pick's birth time, 0 none
+  std::vector<uint64_t> prio;     // each record's claim key in its current round
+  std::vector<int8_t> bstate;     // BS_* (place_pick)
   int64_t t_insts = 0, t_deaths = 0, t_divides = 0, t_slices = 0, t_born = 0, t_dropped = 0;
   int64_t t_oversize = 0;   // offspring longer than AVGPU_MAX_GENOME after a slip (dropped at the divide)
   int64_t t_memcap = 0;     // copy insertions past AVGPU_MAX_GENOME sites / removals from one site (skipped)
   int64_t t_overwritten = 0;   // offspring placed, then killed by a later birth into the same cell
+  int64_t t_cancelled = 0;     // records whose parent's cell got an offspring before their divide
   int64_t t_placed = 0;        // strip tiles: this tile's own winners activated (avgpu_tile_place(3, 2))
   // resources (avgpu_load_resources): literal restatement of cResourceCount /
   // cSpatialResCount, stepped once per update
@@ -324,6 +329,18 @@ static double det_exp2(double x) {
   double y = 1.0;
   for (int k = 22; k >= 1; k--) y = 1.0 + y * (t / (double)k);
   return std::ldexp(y, (int)n);
+}
+
+// Square root from IEEE adds / multiplies / divisions only (the device's
+// det_sqrt, device.h): exponent halved exactly, then 6 Newton steps -- the
+// same operations on both sides, so the bits agree.
+static double det_sqrt(double x) {
+  if (!(x > 0.0)) return 0.0;
+  int e;
+  const double m = std::frexp(x, &e);          // x = m 2^e, m in [0.5, 1)
+  double y = std::ldexp(m + 0.5, e / 2 - (e & 1 && e < 0 ? 1 : 0));
+  for (int k = 0; k < 6; k++) y = 0.5 * (y + x / y);
+  return y;
 }
 
 struct Exec {
@@ -1110,6 +1127,7 @@ void dump_state(const World& w, const Org& o, avgpu_cpu_state* s, uint8_t* ops, 
   s->merit = o.merit;
   s->fitness = o.fitness;
   s->credit = o.credit;
+  s->head_start = o.hstart;
   (void)w;
   if (ops && flags) {
     for (int i = 0; i < cap; i++) {
@@ -1120,35 +1138,158 @@ void dump_state(const World& w, const Org& o, avgpu_cpu_state* s, uint8_t* ops, 
   }
 }
 
-// Deterministic total merit: fixed 256-cell blocks, pairwise tree, then block
-// partials in order (the same order the device reduction uses).
-// Level 2: 256 lanes, lane t sums partials t, t+256, t+512, ... in order, then
-// the same pairwise tree over the 256 lane sums (DESIGN.md "Scheduler").
-double tree_merit_sum(const World& w, int64_t* n_alive) {
-  int64_t nb = (w.ncells + 255) / 256;
-  std::vector<double> part(nb);
-  int64_t cnt = 0;
-  for (int64_t b = 0; b < nb; b++) {
-    double s[256];
-    for (int i = 0; i < 256; i++) {
-      int64_t c = b * 256 + i;
-      s[i] = (c < w.ncells && w.orgs[c].alive) ? w.orgs[c].merit : 0.0;
-      if (c < w.ncells && w.orgs[c].alive) cnt++;
+// The scheduler weight of a living organism: its merit, raised for its first
+// allotment after birth by the share of the birth update it did not run
+// (hstart / 2^16, DESIGN.md 5 "head start"): the reference places an
+// offspring inside its parent's divide and schedules it for the rest of that
+// update; the batch update places it at the update's end and gives it that
+// share in the next.  hstart 0 -> the merit itself.
+static inline double sched_weight(const Org& o) {
+  return o.hstart ? o.merit * (1.0 + (double)o.hstart * (1.0 / 65536.0)) : o.merit;
+}
+
+// ---------------------------------------------------------------------------
+// The scheduler (SLICING_METHOD 1, the default: Apto::Scheduler::Probabilistic,
+// main/cPopulation.cc:7341-7346): each update the reference makes
+// UD = AVE_TIME_SLICE x N picks (cWorld::CalculateUpdateSize,
+// main/cWorld.cc:247-250), each one instruction of an organism drawn with
+// probability weight / total weight -- so the update's instruction counts are
+// Multinomial(UD, weights).  The batch update draws exactly that, in parallel,
+// by splitting UD down a fixed binary tree of the cells with a Binomial at
+// every node:
+//   * 256-cell blocks; a block's partial is the pairwise tree of strides 128,
+//     64, ..., 1 over its cells' weights (s[t] += s[t + stride]): node (k, t)
+//     of level k covers the block's cells = t (mod 2^k);
+//   * the top tree over the blocks (global order, padded to a power of two
+//     with zeros): node i of level l = left + right, children 2i, 2i + 1;
+//   * top down: the root holds UD; a node holding n gives its left child
+//     Binomial(n, S_left / S_node) (binom_draw) and its right child the rest,
+//     down to the blocks and inside each block down to the cells.
+// The sums are the same additions in the same order on both sides, and every
+// node draws from its own stateless word (node_draw), so the budgets do not
+// depend on execution order or on how the world is cut into strips.
+static double pow_int(double q, int64_t n) {
+  double r = 1.0, b = q;
+  while (n) { if (n & 1) r = r * b; b = b * b; n >>= 1; }
+  return r;
+}
+
+// Binomial(n, p) from one 32-bit word h (the device's binom_draw, device.h):
+// on the smaller side pp = min(p, 1 - p), mean n pp < 12 by inversion
+// (f_0 = (1 - pp)^n by squaring, f_{k+1} = f_k (n - k) pp / ((1 - pp)(k + 1)));
+// otherwise normal with the binomial's skew (Cornish-Fisher), z the centred
+// sum of 12 16-bit uniforms from h (Irwin-Hall), clamped to [0, n].
+static int64_t binom_draw(int64_t n, double p, uint32_t h) {
+  if (n <= 0 || !(p > 0.0)) return 0;
+  if (p >= 1.0) return n;
+  const bool flip = p > 0.5;
+  const double pp = flip ? 1.0 - p : p, q = 1.0 - pp;
+  const double mean = (double)n * pp;
+  int64_t k;
+  if (mean < 12.0) {
+    const double u = ((double)h + 0.5) * 2.3283064365386962890625e-10;
+    const double r = pp / q;
+    double f = pow_int(q, n);
+    double F = f;
+    k = 0;
+    while (F < u && k < n && k < 256) { f = (f * ((double)(n - k) * r)) / (double)(k + 1); k++; F = F + f; }
+  } else {
+    uint32_t x = h;
+    double sum = 0.0;
+    for (int i = 0; i < 6; i++) {
+      x = lowbias32(x + 0x9E3779B9U);
+      sum = sum + (double)(x & 0xFFFFu) + (double)(x >> 16);
     }
-    for (int stride = 128; stride >= 1; stride >>= 1)
-      for (int i = 0; i < stride; i++) s[i] = s[i] + s[i + stride];
-    part[b] = s[0];
+    const double z = (sum + 6.0) * 1.52587890625e-05 - 6.0;
+    const double sd = det_sqrt(mean * q);
+    const double v = mean + sd * z + ((q - pp) * (z * z - 1.0)) / 6.0 + 0.5;
+    k = v < 1.0 ? 0 : (int64_t)std::floor(v);
+    if (k > n) k = n;
   }
-  double lane[256];
+  return flip ? n - k : k;
+}
+
+// the word of tree node `node` in update u (salt: top tree / block trees)
+static inline uint32_t node_draw(const World& w, uint32_t update, uint32_t salt, uint64_t node) {
+  const uint32_t slo = (uint32_t)w.cfg.seed, shi = (uint32_t)(w.cfg.seed >> 32);
+  return lowbias32(lowbias32(lowbias32(update * 0x85EBCA6BU + shi) ^ (uint32_t)node ^ salt) +
+                   (uint32_t)(node >> 32) + slo);
+}
+enum : uint32_t { SALT_TOP = 0x7A11C0DEu, SALT_BLOCK = 0x51CEB10Cu };
+
+// a block's partial: the stride tree over its cells' weights (levels kept)
+static double block_levels(const World& w, int64_t b, double lv[9][256]) {
   for (int t = 0; t < 256; t++) {
-    double acc = 0.0;
-    for (int64_t b = t; b < nb; b += 256) acc = acc + part[b];
-    lane[t] = acc;
+    const int64_t c = b * 256 + t;
+    lv[8][t] = (c < w.ncells && w.orgs[c].alive) ? sched_weight(w.orgs[c]) : 0.0;
   }
-  for (int stride = 128; stride >= 1; stride >>= 1)
-    for (int i = 0; i < stride; i++) lane[i] = lane[i] + lane[i + stride];
+  for (int k = 7; k >= 0; k--)
+    for (int t = 0; t < (1 << k); t++) lv[k][t] = lv[k + 1][t] + lv[k + 1][t + (1 << k)];
+  return lv[0][0];
+}
+
+// the top tree over block partials `leaf` (global block order): returns the
+// root (the total weight) and, when n_root >= 0, splits n_root down to the
+// blocks [b0, b0 + nloc) into cnt
+static double top_tree(const World& w, const std::vector<double>& leaf, int64_t n_root, int64_t b0, int64_t nloc,
+                       std::vector<int64_t>* cnt) {
+  int L = 0;
+  while (((int64_t)1 << L) < (int64_t)leaf.size()) L++;
+  std::vector<std::vector<double>> lv(L + 1);
+  lv[L].assign((size_t)1 << L, 0.0);
+  for (size_t i = 0; i < leaf.size(); i++) lv[L][i] = leaf[i];
+  for (int l = L - 1; l >= 0; l--) {
+    lv[l].resize((size_t)1 << l);
+    for (size_t i = 0; i < lv[l].size(); i++) lv[l][i] = lv[l + 1][2 * i] + lv[l + 1][2 * i + 1];
+  }
+  if (cnt) {
+    std::vector<int64_t> c(1, n_root);
+    for (int l = 0; l < L; l++) {
+      std::vector<int64_t> nc((size_t)2 << l, 0);
+      for (size_t i = 0; i < c.size(); i++) {
+        const int64_t left = binom_draw(c[i], lv[l + 1][2 * i] / lv[l][i],
+                                        node_draw(w, (uint32_t)w.update, SALT_TOP, ((uint64_t)1 << l) + i));
+        nc[2 * i] = left;
+        nc[2 * i + 1] = c[i] - left;
+      }
+      c.swap(nc);
+    }
+    cnt->assign(nloc, 0);
+    for (int64_t j = 0; j < nloc; j++) (*cnt)[j] = c[b0 + j];
+  }
+  return lv[0][0];
+}
+
+// a block's count split down its stride tree into its cells' budgets
+static void block_split(const World& w, int64_t b, int64_t n, int32_t* budget) {
+  double lv[9][256];
+  block_levels(w, b, lv);
+  int64_t cnt[256];
+  cnt[0] = n;
+  const uint64_t gb = (uint64_t)(w.cell0 / 256 + b);
+  for (int k = 0; k < 8; k++)
+    for (int t = 0; t < (1 << k); t++) {
+      const int64_t c0 = cnt[t];
+      const int64_t left = binom_draw(c0, lv[k + 1][t] / lv[k][t],
+                                      node_draw(w, (uint32_t)w.update, SALT_BLOCK, (gb << 9) | ((1u << k) + t)));
+      cnt[t] = left;
+      cnt[t + (1 << k)] = c0 - left;
+    }
+  for (int t = 0; t < 256; t++) {
+    const int64_t c = b * 256 + t;
+    if (c < w.ncells) budget[c] = (int32_t)cnt[t];
+  }
+}
+
+// this world's block partials and living organisms (the strip tiles' partials)
+static void world_partials(const World& w, std::vector<double>& part, int64_t* n_alive) {
+  const int64_t nb = (w.ncells + 255) / 256;
+  part.resize(nb);
+  double lv[9][256];
+  for (int64_t b = 0; b < nb; b++) part[b] = block_levels(w, b, lv);
+  int64_t cnt = 0;
+  for (int64_t c = 0; c < w.ncells; c++) cnt += w.orgs[c].alive ? 1 : 0;
   *n_alive = cnt;
-  return lane[0];
 }
 
 // torus / grid neighbourhood (tools/cTopology.h:40-55 build_torus/build_grid),
@@ -1586,6 +1727,7 @@ int orc_set_states(void* h, int64_t first, int64_t count, const avgpu_cpu_state*
     o.rng.rec = nullptr; o.rng.rec_len = 0;   // restored organisms draw from counter streams
     o.errors = s.errors;
     o.cur_bonus = s.cur_bonus; o.merit = s.merit; o.fitness = s.fitness; o.credit = s.credit;
+    o.hstart = s.head_start;
   }
   return 0;
 }
@@ -1595,6 +1737,8 @@ int orc_set_clock(void* h, const avgpu_update_stats* last) {
   w.update = last->update + 1;
   w.cum_insts = last->cum_insts_executed;
   w.cum_births = last->cum_births;
+  w.cfg.seed = last->seed;
+  w.stats.seed = last->seed;
   return 0;
 }
 
@@ -1795,28 +1939,40 @@ static void res_end(World& w) {
 }
 
 // 1. allotment (cScheduler restated; DESIGN.md "Scheduler") + 2. interpretation
-static void allot_interpret(World& w, double sum_merit, int64_t n_alive) {
-  const int64_t ud = (int64_t)w.cfg.ave_time_slice * n_alive;
+// PROBABILISTIC: the update's picks split down the cell tree (block_split);
+// INTEGRATED: lambda = UD * weight / total weight with a credit carry;
+// CONSTANT: AVE_TIME_SLICE.  A divide stamps its birth record
+// with its time in the update, t = k / (b + 1) in 1/2^16 (k: the slice's
+// instructions up to and including the h-divide, b: the slice's budget) --
+// the expected position of the k-th of b instructions spread uniformly over
+// the update, which is how the reference's one-instruction picks interleave
+// organisms (main/cPopulation.cc:5698-5701).
+static inline uint32_t birth_time(int k, int budget) {
+  return (uint32_t)(((double)k * 65536.0) / (double)((int64_t)budget + 1));
+}
+
+// blk: each of this world's blocks' share of the update's picks (top_tree),
+// total: the total weight, ud: the update size (INTEGRATED's lambda =
+// ud * weight / total)
+static void allot_interpret(World& w, const std::vector<int64_t>& blk, double total, double ud) {
   std::vector<int32_t> budget(w.ncells, 0);
+  const bool consts = w.cfg.slicing_method == AVGPU_SLICE_CONSTANT || !(total > 0.0);
+  if (!consts && w.cfg.slicing_method != AVGPU_SLICE_INTEGRATED)
+    for (int64_t b = 0; b < (int64_t)blk.size(); b++) block_split(w, b, blk[b], budget.data());
   for (int64_t c = 0; c < w.ncells; c++) {
     Org& o = w.orgs[c];
-    if (!o.alive) continue;
-    if (w.cfg.slicing_method == AVGPU_SLICE_CONSTANT || !(sum_merit > 0.0)) {
+    if (!o.alive) { budget[c] = 0; continue; }
+    const double wt = sched_weight(o);
+    o.hstart = 0;                               // consumed by this allotment
+    if (consts) {
       budget[c] = w.cfg.ave_time_slice;
-      continue;
-    }
-    double lam = ((double)ud * o.merit) / sum_merit;
-    if (lam > 1.0e8) lam = 1.0e8;
-    if (w.cfg.slicing_method == AVGPU_SLICE_INTEGRATED) {
+    } else if (w.cfg.slicing_method == AVGPU_SLICE_INTEGRATED) {
+      double lam = (ud * wt) / total;
+      if (lam > 1.0e8) lam = 1.0e8;
       o.credit = o.credit + lam;
       double fl = std::floor(o.credit);
       budget[c] = (int32_t)fl;
       o.credit = o.credit - fl;
-    } else {
-      double fl = std::floor(lam);
-      double frac = lam - fl;
-      const uint64_t th = make_prob(frac).th;
-      budget[c] = (int32_t)fl + ((uint64_t)allot_draw(o.rng.lo, o.rng.hi, (uint32_t)w.update) < th ? 1 : 0);
     }
   }
   w.t_slices = 0;
@@ -1828,7 +1984,11 @@ static void allot_interpret(World& w, double sum_merit, int64_t n_alive) {
     if (!o.alive) continue;
     Exec ex{w, o, AVGPU_MODE_WORLD};
     int d0 = o.num_divides;
-    for (int k = 0; k < budget[c] && o.alive; k++) { ex.single_process(c); insts++; }
+    for (int k = 0; k < budget[c] && o.alive; k++) {
+      const size_t nb0 = w.births.size();
+      ex.single_process(c); insts++;
+      if (w.births.size() != nb0) w.births.back().t = birth_time(k + 1, budget[c]);
+    }
     divides += o.num_divides - d0;
     if (!o.alive) deaths++;
   }
@@ -1867,74 +2027,194 @@ static void finish_stats(World& w, int64_t placed, int64_t dropped) {
   st.cum_births = w.cum_births;
   st.slices = w.t_slices;
   st.births_overwritten = w.t_overwritten;
+  st.births_cancelled = w.t_cancelled;
+  st.seed = w.cfg.seed;
   w.t_overwritten = 0;
+  w.t_cancelled = 0;
   w.update++;
 }
 
-// placement pick for birth i (PositionOffspring restated, main/cPopulation.cc:5353-5413)
-static void place_pick(World& w, int64_t i, const std::vector<uint8_t>& occ, std::vector<uint64_t>& claim,
-                       std::vector<uint64_t>& prio, std::vector<int8_t>& state) {
+extern "C++" {
+// ---------------------------------------------------------------------------
+// 3. Time-ordered placement.  The reference places each
+// offspring inside its parent's h-divide (ActivateOffspring,
+// main/cPopulation.cc:621-952 -> PositionOffspring :5185-5414), so an
+// organism whose cell receives an offspring before its own divide never
+// divides, an earlier birth takes an empty cell before a later one, and a
+// later birth into an occupied cell kills whatever is there.  The batch update
+// restates that order from the records' birth times t:
+//   launch 0  every record picks a target (PositionOffspring: an empty
+//             neighbour, else any neighbour or the parent); a pick whose
+//             target is taken is a kill, and the cell's kill time is the
+//             earliest such t (killt = 2^16 - t, max-reduced);
+//   launch 0b a record whose parent's cell was killed before its own time
+//             (killt[parent] > 2^16 - t) is cancelled -- its parent died
+//             before dividing; the rest claim their targets;
+//   launch m  (1..3) round m-1 resolved: the maximum claim wins.  Claim keys
+//             order empty-cell claims earliest first and kill claims latest
+//             first, so an empty cell goes to its earliest claimer and a kill
+//             target to its latest -- the earlier kills were placed and
+//             overwritten, as in the reference.  A winner owns its cell
+//             unless the cell's owner from an earlier round is later in time
+//             (that owner overwrote it).  A lost empty claim picks again
+//             (cells claimed in round m-1 count as taken); a lost kill claim
+//             is placed and overwritten;
+//   activation round 3 resolved the same way; every owner is activated.
+// claim key: [63:48] time key (kill: t, empty: 0xFFFF - t), [47] kill,
+// [46:32] the pick's draw >> 17, [31:8] the parent's GLOBAL cell id (tiles
+// agree), [7:0] its divide number -- unique per record.
+static inline uint64_t claim_key(uint32_t t, bool kill, uint32_t draw, int64_t gparent, uint32_t seq) {
+  const uint64_t tk = kill ? (uint64_t)(t & 0xFFFFu) : (uint64_t)(0xFFFFu - (t & 0xFFFFu));
+  return (tk << 48) | ((uint64_t)(kill ? 1 : 0) << 47) | ((uint64_t)(draw >> 17) << 32) |
+         ((uint64_t)(gparent & 0xFFFFFF) << 8) | (uint64_t)(seq & 0xFF);
+}
+static inline bool key_kill(uint64_t k) { return ((k >> 47) & 1ull) != 0; }
+static inline uint32_t key_time(uint64_t k) {
+  const uint32_t tk = (uint32_t)(k >> 48);
+  return key_kill(k) ? tk : 0xFFFFu - tk;
+}
+// record states (Birth index i -> bstate[i])
+enum : int8_t { BS_PENDING = 0, BS_WON = 1 /* 1 + round */, BS_KILL_LOST = 8 /* 8 + round */,
+                BS_CANCELLED = -1, BS_NO_CELL = -2 };
+// owner: >= 0 a record of this world, -1 none, <= -2 a neighbouring strip's
+// offspring that won round m at time t (strip tiles)
+static inline int64_t remote_owner(int m, uint32_t t) { return -2 - ((int64_t)m + 4 * (int64_t)t); }
+static inline uint32_t owner_time(const World& w, int64_t o) {
+  return o >= 0 ? w.births[o].t : (uint32_t)((-2 - o) >> 2);
+}
+// a cell's owner after a round-m winner with time t: it replaces the owner
+// unless the owner is later in time
+static inline bool takes_cell(const World& w, int64_t owner, uint32_t t) {
+  return owner == -1 || owner_time(w, owner) <= t;
+}
+
+// PositionOffspring for record i in round m (main/cPopulation.cc:5353-5413):
+// an empty neighbour (not taken) when PREFER_EMPTY, else any of the eight
+// neighbours or the parent (ALLOW_PARENT).  BIRTH_METHOD 3 with no empty
+// neighbour: PositionOffspring returns the parent's cell without a draw
+// (:5407) and ActivateOffspring places the offspring there only if
+// ALLOW_PARENT (:706-713); otherwise it is never placed (BS_NO_CELL).
+// Writes the record's target and key (and w.tgt_r[m][i]); returns false for
+// no cell.
+template <class Taken>
+static bool place_pick(World& w, int64_t i, int m, Taken taken) {
   Birth& b = w.births[i];
   int64_t nb[8];
   const int nn = neighbours(w, b.parent, nb);
   int64_t cand[9];
   int nc = 0;
   if (w.cfg.prefer_empty)
-    for (int k = 0; k < nn; k++) if (!occ[nb[k]]) cand[nc++] = nb[k];
+    for (int k = 0; k < nn; k++) if (!taken(nb[k])) cand[nc++] = nb[k];
   if (nc == 0 && w.cfg.birth_method != 3) {
     for (int k = 0; k < nn; k++) cand[nc++] = nb[k];
     if (w.cfg.allow_parent) cand[nc++] = b.parent;
   }
-  // no candidate (BIRTH_METHOD 3 without an empty neighbour): PositionOffspring
-  // returns the parent's cell, drawing nothing (main/cPopulation.cc:5407)
+  if (nc == 0 && !w.cfg.allow_parent) { b.target = -1; w.bstate[i] = BS_NO_CELL; return false; }
   b.target = nc > 0 ? cand[b.rng.uint_below((uint32_t)nc)] : b.parent;
-  prio[i] = ((uint64_t)b.rng.next() << 32) | ((uint64_t)((w.cell0 + b.parent) & 0xFFFFFF) << 8) |
-            (b.seq & 0xFF);
-  if (prio[i] > claim[b.target]) claim[b.target] = prio[i];
+  w.prio[i] = claim_key(b.t, taken(b.target), b.rng.next(), w.cell0 + b.parent, b.seq);
+  w.tgt_r[m][i] = b.target;
+  return true;
 }
 
-// ---------------------------------------------------------------------------
+static void place_reset(World& w, int64_t ext) {
+  const int64_t nbirth = (int64_t)w.births.size();
+  w.occ.assign(ext, 0);
+  for (int64_t c = 0; c < w.ncells; c++) w.occ[c] = w.orgs[c].alive ? 1 : 0;
+  for (int k = 0; k < 4; k++) { w.claim_r[k].assign(ext, 0); w.tgt_r[k].assign(nbirth, -1); }
+  w.owner.assign(ext, -1);
+  w.killt.assign(w.ncells, 0);
+  w.prio.assign(nbirth, 0);
+  w.bstate.assign(nbirth, BS_PENDING);
+}
+
+// launch 0b, one record: cancelled if its parent's cell was killed earlier
+// (kt: the cell's merged kill time), else it claims its round-0 target
+static inline bool place_cancelled(const World& w, int64_t i, uint32_t kt) {
+  return kt > 0x10000u - w.births[i].t;
+}
+
+// the single world's activation: round 3 resolved, owners activated, the
+// rest counted (main/cPopulation.cc:5382-5413: PositionOffspring always
+// returns a cell, so a record that is neither cancelled nor without a cell
+// was placed -- it owns its cell, or a later birth overwrote it)
+static void place_finish_single(World& w) {
+  const int64_t nbirth = (int64_t)w.births.size();
+  int64_t placed = 0, overwritten = 0, cancelled = 0, dropped = 0;
+  for (int64_t i = 0; i < nbirth; i++) {
+    Birth& b = w.births[i];
+    const int8_t st = w.bstate[i];
+    bool own = false;
+    if (st == BS_PENDING) {
+      own = w.claim_r[3][b.target] == w.prio[i] && takes_cell(w, w.owner[b.target], b.t);
+    } else if (st >= BS_WON && st < BS_WON + 4) {
+      const uint64_t c3 = w.claim_r[3][b.target];
+      own = w.owner[b.target] == i && !(c3 != 0 && key_time(c3) >= b.t);
+    }
+    if (own) { activate_child(w, b, b.target); w.orgs[b.target].hstart = 0x10000u - b.t; placed++; }
+    else if (st == BS_CANCELLED) cancelled++;
+    else if (st == BS_NO_CELL) dropped++;
+    else overwritten++;
+  }
+  w.t_overwritten = overwritten;
+  w.t_cancelled = cancelled;
+  finish_stats(w, placed, dropped);
+}
+
+}  // extern "C++"
+
 // Batch-synchronous world update: the exact semantics the device implements
 // (DESIGN.md "Update semantics"): allot -> interpret -> place births -> stats.
 static int run_update_impl(World& w) {
   int64_t n_alive = 0;
-  double sum_merit = tree_merit_sum(w, &n_alive);
-  if (w.have_global) { sum_merit = w.global_merit; n_alive = w.global_orgs; }
+  std::vector<double> part;
+  world_partials(w, part, &n_alive);
+  const double local = top_tree(w, part, -1, 0, 0, nullptr);
+  const double ave = (double)w.cfg.ave_time_slice;
+  double total = local, ud = ave * (double)n_alive;
+  int64_t n_root = (int64_t)w.cfg.ave_time_slice * n_alive;
+  if (w.have_global) {   // cMultiProcessWorld::CalculateUpdateSize (main/cMultiProcessWorld.cc:396-405)
+    total = w.global_merit;
+    ud = ave * (double)w.global_orgs;
+    n_root = total > 0.0 ? (int64_t)((local / total) * ave * (double)w.global_orgs) : 0;
+  }
+  std::vector<int64_t> blk;
+  top_tree(w, part, n_root, 0, (int64_t)part.size(), &blk);
   res_begin(w);
-  allot_interpret(w, sum_merit, n_alive);
+  allot_interpret(w, blk, total, ud);
   res_end(w);
-  // 3. placement rounds
   const int64_t nbirth = (int64_t)w.births.size();
-  std::vector<uint8_t> occ(w.ncells);
-  for (int64_t c = 0; c < w.ncells; c++) occ[c] = w.orgs[c].alive ? 1 : 0;
-  std::vector<uint64_t> claim(w.ncells, 0);
-  std::vector<int64_t> owner(w.ncells, -1);
-  std::vector<uint64_t> prio(nbirth, 0);
-  std::vector<int8_t> state(nbirth, 0);   // 0 pending, 1 placed, -1 failed
-  for (int round = 0; round < 4; round++) {
-    for (int64_t i = 0; i < nbirth; i++)
-      if (state[i] == 0) place_pick(w, i, occ, claim, prio, state);
-    for (int64_t i = 0; i < nbirth; i++) {
-      if (state[i] != 0) continue;
-      Birth& b = w.births[i];
-      if (claim[b.target] == prio[i]) { state[i] = 1; occ[b.target] = 1; owner[b.target] = i; }
-    }
-    for (int64_t i = 0; i < nbirth; i++) if (w.births[i].target >= 0) claim[w.births[i].target] = 0;
-  }
-  // 4. activation (the last round's winner owns the cell).  PositionOffspring
-  // always returns a cell (main/cPopulation.cc:5382-5413): a birth still
-  // pending after round 3 lost that round's claim on its target to a birth of
-  // higher priority, so the reference would have placed it there and the
-  // owner -- placed after it -- killed it.  Every birth is therefore placed:
-  // it owns its cell, or it was placed and overwritten.
-  int64_t placed = 0, overwritten = 0;
+  place_reset(w, w.ncells);
+  // launch 0: picks, kill times
   for (int64_t i = 0; i < nbirth; i++) {
-    Birth& b = w.births[i];
-    if (state[i] == 1 && owner[b.target] == i) { activate_child(w, b, b.target); placed++; }
-    else overwritten++;
+    if (!place_pick(w, i, 0, [&](int64_t c) { return w.occ[c] != 0; })) continue;
+    const Birth& b = w.births[i];
+    if (key_kill(w.prio[i])) w.killt[b.target] = std::max(w.killt[b.target], 0x10000u - b.t);
   }
-  w.t_overwritten = overwritten;
-  finish_stats(w, placed, 0);
+  // launch 0b: cancellations, round-0 claims
+  for (int64_t i = 0; i < nbirth; i++) {
+    if (w.bstate[i] != BS_PENDING) continue;
+    const Birth& b = w.births[i];
+    if (place_cancelled(w, i, w.killt[b.parent])) { w.bstate[i] = BS_CANCELLED; continue; }
+    w.claim_r[0][b.target] = std::max(w.claim_r[0][b.target], w.prio[i]);
+  }
+  // launches 1..3: resolve round m-1, pick round m
+  for (int m = 1; m < 4; m++) {
+    const std::vector<uint64_t>& prev = w.claim_r[m - 1];
+    for (int64_t i = 0; i < nbirth; i++) {
+      if (w.bstate[i] != BS_PENDING) continue;
+      Birth& b = w.births[i];
+      if (prev[b.target] == w.prio[i]) {
+        w.bstate[i] = (int8_t)(BS_WON + m - 1);
+        w.occ[b.target] = 1;
+        if (takes_cell(w, w.owner[b.target], b.t)) w.owner[b.target] = i;
+        continue;
+      }
+      if (key_kill(w.prio[i])) { w.bstate[i] = (int8_t)(BS_KILL_LOST + m - 1); continue; }
+      if (!place_pick(w, i, m, [&](int64_t c) { return w.occ[c] != 0 || prev[c] != 0; })) continue;
+      w.claim_r[m][b.target] = std::max(w.claim_r[m][b.target], w.prio[i]);
+    }
+  }
+  place_finish_single(w);
   return 0;
 }
 
@@ -1973,16 +2253,21 @@ struct HaloHdr { int32_t count, arena_used, overflow, pad; };
 struct HaloRec {
   int32_t col, round, len, gen, ccopied, exec, gest;
   uint32_t rng_lo, rng_hi, rng_ctr;
-  int32_t off, pad;
+  int32_t off;
+  uint32_t t;         // the offspring's birth time (owner bookkeeping, head start)
   double merit, fitness;
   int32_t last_task[AVGPU_NUM_LOGIC_TASKS], pad2[3];
 };
 static_assert(sizeof(HaloRec) == 112, "HaloRec layout");
-int64_t halo_bytes_of(int x) { return ((int64_t)x * 33 + 15) / 16 * 16; }
 // per round parity p: k = 0 the sender's claims on the receiver's edge row
-// (its ghost row), k = 1 its own claims on its edge row; then the occupancy
+// (its ghost row), k = 1 its own claims on its edge row; then the occupancy;
+// then (round 0's picks) the kill times of the sender's picks on the
+// receiver's edge row (u32, 2^16 - t, max-reduced)
+int64_t halo_kt_off(int x) { return ((int64_t)x * 33 + 3) / 4 * 4; }
+int64_t halo_bytes_of(int x) { return (halo_kt_off(x) + 4 * (int64_t)x + 15) / 16 * 16; }
 uint64_t* hcl(uint8_t* b, int x, int p, int k) { return reinterpret_cast<uint64_t*>(b) + (int64_t)(2 * p + k) * x; }
 uint8_t* hocc(uint8_t* b, int x) { return b + (int64_t)x * 32; }
+uint32_t* hkt(uint8_t* b, int x) { return reinterpret_cast<uint32_t*>(b + halo_kt_off(x)); }
 int64_t edge_cell(const World& w, int d, int x) { return d == 0 ? x : (w.rows - 1) * w.cfg.world_x + x; }
 int64_t ghost_cell(const World& w, int d, int x) { return w.ncells + (int64_t)d * w.cfg.world_x + x; }
 bool tile_ok(World& w) { return w.tiled && w.h_send[0] && w.r_recv[1]; }
@@ -2057,22 +2342,15 @@ int orc_set_tile_buffers(void* h, void* hs0, void* hs1, void* hr0, void* hr1, vo
   return 0;
 }
 
-// the 256-cell block partials of tree_merit_sum (level 1), then alive counts
+// the 256-cell block partials of the scheduler tree (block_levels), then alive counts
 int orc_tile_partials(void* h, double* out) {
   World& w = *(World*)h;
   const int64_t nb = (w.ncells + 255) / 256;
+  double lv[9][256];
   for (int64_t b = 0; b < nb; b++) {
-    double s[256];
+    out[b] = block_levels(w, b, lv);
     int64_t cnt = 0;
-    for (int i = 0; i < 256; i++) {
-      const int64_t c = b * 256 + i;
-      const bool live = c < w.ncells && w.orgs[c].alive;
-      s[i] = live ? w.orgs[c].merit : 0.0;
-      cnt += live;
-    }
-    for (int stride = 128; stride >= 1; stride >>= 1)
-      for (int i = 0; i < stride; i++) s[i] = s[i] + s[i + stride];
-    out[b] = s[0];
+    for (int i = 0; i < 256; i++) cnt += (b * 256 + i < w.ncells && w.orgs[b * 256 + i].alive) ? 1 : 0;
     out[nb + b] = (double)cnt;
   }
   // edge rows of the spatial amounts for the neighbours' flow step
@@ -2092,36 +2370,27 @@ int orc_tile_partials(void* h, double* out) {
 int orc_tile_begin(void* h, const double* gathered, int ntiles) {
   World& w = *(World*)h;
   if (!tile_ok(w)) return fail(AVGPU_ESTATE, "not a strip tile with buffers");
-  // tree_merit_sum level 2 over the gathered partials (tile order = block order)
-  const int64_t nb = (w.ncells + 255) / 256, total = nb * ntiles;
-  double lane[256];
+  // the top tree over every strip's block partials (tile order = block order)
+  const int64_t nb = (w.ncells + 255) / 256;
+  std::vector<double> leaf((size_t)(nb * ntiles));
   int64_t cnt = 0;
-  for (int t = 0; t < 256; t++) {
-    double acc = 0.0;
-    for (int64_t g = t; g < total; g += 256) {
-      const int64_t k = g / nb, j = g % nb;
-      acc = acc + gathered[k * 2 * nb + j];
+  for (int k = 0; k < ntiles; k++)
+    for (int64_t j = 0; j < nb; j++) {
+      leaf[k * nb + j] = gathered[k * 2 * nb + j];
       cnt += (int64_t)gathered[k * 2 * nb + nb + j];
     }
-    lane[t] = acc;
-  }
-  for (int stride = 128; stride >= 1; stride >>= 1)
-    for (int i = 0; i < stride; i++) lane[i] = lane[i] + lane[i + stride];
+  std::vector<int64_t> blk;
+  const double total = top_tree(w, leaf, (int64_t)w.cfg.ave_time_slice * cnt, w.cell0 / 256, nb, &blk);
   if (w.n_spatial && !w.rs_recv[0]) return fail(AVGPU_ESTATE, "spatial resources need the tile resource buffers");
   res_begin(w);
-  allot_interpret(w, lane[0], cnt);
+  allot_interpret(w, blk, total, (double)w.cfg.ave_time_slice * (double)cnt);
   const int X = w.cfg.world_x;
-  const int64_t ext = w.ncells + 2 * X, nbirth = (int64_t)w.births.size();
-  w.occ.assign(ext, 0);
-  for (int64_t c = 0; c < w.ncells; c++) w.occ[c] = w.orgs[c].alive ? 1 : 0;
-  for (int k = 0; k < 4; k++) w.claim_r[k].assign(ext, 0);
-  w.owner.assign(ext, -1);
-  w.prio.assign(nbirth, 0);
-  w.bstate.assign(nbirth, 0);
+  place_reset(w, w.ncells + 2 * X);
   for (int d = 0; d < 2; d++)
     for (int x = 0; x < X; x++) {
       hocc(w.h_send[d], X)[x] = w.occ[edge_cell(w, d, x)];
       for (int k = 0; k < 4; k++) hcl(w.h_send[d], X, k >> 1, k & 1)[x] = 0;
+      hkt(w.h_send[d], X)[x] = 0;
     }
   w.t_placed = 0; w.t_overwritten = 0;
   return 0;
@@ -2137,79 +2406,146 @@ bool tile_slot(const World& w, int64_t c, int& d, int& x, bool& ghost) {
   if (c >= w.ncells - X) { d = 1; x = (int)(c - (w.ncells - X)); return true; }
   return false;
 }
-// round m's resolve with the merged claims (mine, the neighbour's): winners
-// take their cells (state m + 1); an edge cell whose maximum came from the
-// neighbour is that round's remote winner's; a claimed ghost cell is occupied
-void tile_resolve(World& w, int m) {
-  const int X = w.cfg.world_x, p = m & 1;
-  const std::vector<uint64_t>& cl = w.claim_r[m];
-  for (int64_t i = 0; i < (int64_t)w.births.size(); i++) {
-    if (w.bstate[i] != 0) continue;
-    const int64_t t = w.births[i].target;
-    uint64_t v = cl[t];
-    int d, x;
-    bool ghost;
-    if (tile_slot(w, t, d, x, ghost)) v = std::max(v, hcl(w.h_recv[d], X, p, ghost ? 1 : 0)[x]);
-    if (v == w.prio[i]) { w.bstate[i] = (int8_t)(1 + m); w.occ[t] = 1; w.owner[t] = i; }
-  }
+// a tile's cell taken for round m's pick (the device's tile_taken): round 0
+// the occupancy (ghost rows: the neighbour's edge occupancy, imported); later
+// rounds also every cell claimed in round m - 1, here or by the neighbour
+bool tile_taken(const World& w, int64_t c, int m) {
+  if (w.occ[c]) return true;
+  if (m == 0) return false;
+  if (w.claim_r[m - 1][c] != 0) return true;
+  int d, x;
+  bool ghost;
+  return tile_slot(w, c, d, x, ghost) && hcl(w.h_recv[d], w.cfg.world_x, (m - 1) & 1, ghost ? 1 : 0)[x] != 0;
+}
+// round m's merged claim on cell t: mine, the neighbour's
+uint64_t tile_merged(const World& w, int64_t t, int m) {
+  uint64_t v = w.claim_r[m][t];
+  int d, x;
+  bool ghost;
+  if (tile_slot(w, t, d, x, ghost)) v = std::max(v, hcl(w.h_recv[d], w.cfg.world_x, m & 1, ghost ? 1 : 0)[x]);
+  return v;
+}
+// launch m = 1..4 of a tile (the device's k_tile_round): round m - 1
+// resolved with the merged claims -- the halo cells' remote winners (an edge
+// or ghost cell whose maximum came from the neighbour: owner
+// remote_owner(m - 1, t) by the time rule, occupied), this tile's winners
+// (takes_cell), lost kill claims placed and overwritten -- then (m < 4) the
+// pending records pick round m
+void tile_launch(World& w, int m) {
+  const int X = w.cfg.world_x, p = (m - 1) & 1;
+  const std::vector<uint64_t>& cl = w.claim_r[m - 1];
   for (int d = 0; d < 2; d++)
     for (int x = 0; x < X; x++) {
       const int64_t c = edge_cell(w, d, x), g = ghost_cell(w, d, x);
-      const uint64_t rc = hcl(w.h_recv[d], X, p, 0)[x];
-      if (rc != 0 && rc > cl[c]) { w.owner[c] = -2 - m; w.occ[c] = 1; }
-      if (cl[g] != 0 || hcl(w.h_recv[d], X, p, 1)[x] != 0) w.occ[g] = 1;
+      const uint64_t rc = hcl(w.h_recv[d], X, p, 0)[x], rg = hcl(w.h_recv[d], X, p, 1)[x];
+      if (rc != 0 && rc > cl[c]) {
+        if (takes_cell(w, w.owner[c], key_time(rc))) w.owner[c] = remote_owner(m - 1, key_time(rc));
+        w.occ[c] = 1;
+      }
+      if (rg != 0 && rg > cl[g] && takes_cell(w, w.owner[g], key_time(rg)))
+        w.owner[g] = remote_owner(m - 1, key_time(rg));
+      if (cl[g] != 0 || rg != 0) w.occ[g] = 1;
     }
+  const int64_t nbirth = (int64_t)w.births.size();
+  for (int64_t i = 0; i < nbirth; i++) {
+    if (w.bstate[i] != BS_PENDING) continue;
+    Birth& b = w.births[i];
+    if (tile_merged(w, b.target, m - 1) == w.prio[i]) {
+      w.bstate[i] = (int8_t)(BS_WON + m - 1);
+      w.occ[b.target] = 1;
+      if (takes_cell(w, w.owner[b.target], b.t)) w.owner[b.target] = i;
+      continue;
+    }
+    if (key_kill(w.prio[i])) { w.bstate[i] = (int8_t)(BS_KILL_LOST + m - 1); continue; }
+    if (m == 4) continue;
+    if (!place_pick(w, i, m, [&](int64_t c) { return tile_taken(w, c, m); })) continue;
+    w.claim_r[m][b.target] = std::max(w.claim_r[m][b.target], w.prio[i]);
+    int d, x;
+    bool ghost;
+    if (tile_slot(w, b.target, d, x, ghost)) {
+      uint64_t& slot = hcl(w.h_send[d], X, m & 1, ghost ? 0 : 1)[x];
+      slot = std::max(slot, w.prio[i]);
+    }
+  }
 }
 }  // namespace
 
+// phase 0, round 0: picks and kill times (own cells; picks on a ghost row go
+// to the neighbour in the halo's kill-time slots); phase 3 (after that
+// exchange): cancellations with the merged kill times, round 0's claims;
+// phase 0, rounds 1..3: tile_launch; phase 1: round 3 resolved, the ghost
+// cells' owners packed; phase 2: this tile's owners activated
 int orc_tile_place(void* h, int round, int phase) {
   World& w = *(World*)h;
   if (!tile_ok(w)) return fail(AVGPU_ESTATE, "not a strip tile with buffers");
-  if (round < 0 || round > 3 || phase < 0 || phase > 2 || (phase >= 1 && round != 3))
-    return fail(AVGPU_EINVAL, "round 0..3 with phase 0; phases 1, 2 after round 3");
+  if (round < 0 || round > 3 || phase < 0 || phase > 3 || (phase >= 1 && phase <= 2 && round != 3) ||
+      (phase == 3 && round != 0))
+    return fail(AVGPU_EINVAL, "round 0..3 with phase 0, round 0 with phase 3; phases 1, 2 after round 3");
   const int X = w.cfg.world_x;
   const int64_t nbirth = (int64_t)w.births.size();
-  if (phase == 0) {
-    if (round == 0)
-      for (int d = 0; d < 2; d++)
-        for (int x = 0; x < X; x++) w.occ[ghost_cell(w, d, x)] = hocc(w.h_recv[d], X)[x];
-    else
-      tile_resolve(w, round - 1);
-    // this round's claims: the arrays and the halo send slots of its parity
-    const int p = round & 1;
+  if (phase == 0 && round == 0) {
     for (int d = 0; d < 2; d++)
-      for (int x = 0; x < X; x++) { hcl(w.h_send[d], X, p, 0)[x] = 0; hcl(w.h_send[d], X, p, 1)[x] = 0; }
+      for (int x = 0; x < X; x++) w.occ[ghost_cell(w, d, x)] = hocc(w.h_recv[d], X)[x];
     for (int64_t i = 0; i < nbirth; i++) {
-      if (w.bstate[i] != 0) continue;
-      place_pick(w, i, w.occ, w.claim_r[round], w.prio, w.bstate);
+      if (!place_pick(w, i, 0, [&](int64_t c) { return tile_taken(w, c, 0); })) continue;
+      const Birth& b = w.births[i];
+      if (!key_kill(w.prio[i])) continue;
       int d, x;
       bool ghost;
-      const int64_t t = w.births[i].target;
-      if (tile_slot(w, t, d, x, ghost)) {
-        uint64_t& slot = hcl(w.h_send[d], X, p, ghost ? 0 : 1)[x];
+      if (b.target >= w.ncells && tile_slot(w, b.target, d, x, ghost)) {
+        uint32_t& k = hkt(w.h_send[d], X)[x];
+        k = std::max(k, 0x10000u - b.t);
+      } else {
+        w.killt[b.target] = std::max(w.killt[b.target], 0x10000u - b.t);
+      }
+    }
+  } else if (phase == 3) {
+    for (int64_t i = 0; i < nbirth; i++) {
+      if (w.bstate[i] != BS_PENDING) continue;
+      const Birth& b = w.births[i];
+      uint32_t kt = w.killt[b.parent];
+      int d, x;
+      bool ghost;
+      if (tile_slot(w, b.parent, d, x, ghost)) kt = std::max(kt, hkt(w.h_recv[d], X)[x]);
+      if (place_cancelled(w, i, kt)) { w.bstate[i] = BS_CANCELLED; continue; }
+      w.claim_r[0][b.target] = std::max(w.claim_r[0][b.target], w.prio[i]);
+      if (tile_slot(w, b.target, d, x, ghost)) {
+        uint64_t& slot = hcl(w.h_send[d], X, 0, ghost ? 0 : 1)[x];
         slot = std::max(slot, w.prio[i]);
       }
     }
+  } else if (phase == 0) {
+    // this round's send slots (their last contents, round - 2's, went out)
+    const int p = round & 1;
+    for (int d = 0; d < 2; d++)
+      for (int x = 0; x < X; x++) { hcl(w.h_send[d], X, p, 0)[x] = 0; hcl(w.h_send[d], X, p, 1)[x] = 0; }
+    tile_launch(w, round);
   } else if (phase == 2) {
     // this tile's own winners (the records travel meanwhile)
-    int64_t placed = 0, overwritten = 0;
+    int64_t placed = 0, overwritten = 0, cancelled = 0, nocell = 0;
     for (int64_t i = 0; i < nbirth; i++) {
       Birth& b = w.births[i];
-      const bool won = w.bstate[i] > 0 && b.target >= 0 && w.owner[b.target] == i;
+      const int8_t st = w.bstate[i];
+      const bool won = st >= BS_WON && st < BS_WON + 4 && w.owner[b.target] == i;
       if (won && b.target >= w.ncells) continue;   // shipped to the neighbour
-      if (won) { activate_child(w, b, b.target); placed++; }
+      if (won) { activate_child(w, b, b.target); w.orgs[b.target].hstart = 0x10000u - b.t; placed++; }
+      else if (st == BS_CANCELLED) cancelled++;
+      else if (st == BS_NO_CELL) nocell++;
       else overwritten++;                          // placed, then overwritten (run_update_impl)
     }
     w.t_placed = placed;
     w.t_overwritten = overwritten;
+    w.t_cancelled = cancelled;
+    w.t_dropped += nocell;
   } else {
-    tile_resolve(w, 3);
-    // then pack the last winner of every ghost cell (births in queue order)
+    tile_launch(w, 4);
+    // then pack the owner of every ghost cell (births in queue order)
     w.t_born = 0; w.t_dropped = 0;
     for (int d = 0; d < 2; d++) memset(w.r_send[d], 0, sizeof(HaloHdr));
     for (int64_t i = 0; i < nbirth; i++) {
       const Birth& b = w.births[i];
-      if (w.bstate[i] <= 0 || b.target < w.ncells || w.owner[b.target] != i) continue;
+      const int8_t st = w.bstate[i];
+      if (st < BS_WON || st >= BS_WON + 4 || b.target < w.ncells || w.owner[b.target] != i) continue;
       const int d = (int)((b.target - w.ncells) / X), col = (int)((b.target - w.ncells) % X);
       HaloHdr* hdr = reinterpret_cast<HaloHdr*>(w.r_send[d]);
       HaloRec* recs = reinterpret_cast<HaloRec*>(w.r_send[d] + sizeof(HaloHdr));
@@ -2220,10 +2556,10 @@ int orc_tile_place(void* h, int round, int phase) {
       hdr->arena_used += (len + 3) & ~3;
       const bool fits = (int64_t)off + len <= w.r_arena;
       HaloRec r;
-      r.col = col; r.round = w.bstate[i] - 1; r.len = fits ? len : -1;
+      r.col = col; r.round = st - BS_WON; r.len = fits ? len : -1;
       r.gen = b.generation; r.ccopied = b.child_copied; r.exec = b.executed; r.gest = b.gestation_time;
       r.rng_lo = b.rng.lo; r.rng_hi = b.rng.hi; r.rng_ctr = b.rng.ctr;
-      r.off = off; r.pad = 0; r.merit = b.merit; r.fitness = b.fitness;
+      r.off = off; r.t = b.t; r.merit = b.merit; r.fitness = b.fitness;
       for (int t = 0; t < AVGPU_NUM_LOGIC_TASKS; t++) r.last_task[t] = b.last_task[t];
       r.pad2[0] = r.pad2[1] = r.pad2[2] = 0;
       recs[slot] = r;
@@ -2248,7 +2584,7 @@ int orc_tile_finish(void* h, avgpu_update_stats* out) {
       const HaloRec& r = recs[q];
       if (r.len < 0) continue;
       const int64_t c = edge_cell(w, d, r.col);
-      if (w.owner[c] != -2 - r.round) { overwritten++; continue; }
+      if (w.owner[c] != remote_owner(r.round, r.t)) { overwritten++; continue; }
       Birth b;
       b.parent = -1; b.seq = 0;
       b.genome.assign(arena + r.off, arena + r.off + r.len);
@@ -2257,6 +2593,7 @@ int orc_tile_finish(void* h, avgpu_update_stats* out) {
       for (int t = 0; t < AVGPU_NUM_LOGIC_TASKS; t++) b.last_task[t] = r.last_task[t];
       b.rng.lo = r.rng_lo; b.rng.hi = r.rng_hi; b.rng.ctr = r.rng_ctr;
       activate_child(w, b, c);
+      w.orgs[c].hstart = 0x10000u - r.t;
       placed++;
     }
   }

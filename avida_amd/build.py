@@ -31,14 +31,29 @@ def needs_build(out: str = OUT) -> bool:
 
 
 def build(force: bool = False, verbose: bool = False, clocks: bool = False) -> str:
+    """Each source compiled on its own (in parallel), then one shared link."""
+    from concurrent.futures import ThreadPoolExecutor
     out = OUT_CLK if clocks else OUT
     if not force and not needs_build(out):
         return out
     extra = ["-DAVGPU_PHASE_CLOCKS"] if clocks else []
-    cmd = [HIPCC, *FLAGS, *extra, "-o", out + ".tmp", *[os.path.join(CSRC, s) for s in SOURCES]]
+    cflags = [f for f in FLAGS if f != "-shared"]
+    objs = [out + "." + os.path.splitext(src)[0] + ".o" for src in SOURCES]
+
+    def compile_one(k):
+        cmd = [HIPCC, *cflags, *extra, "-c", "-o", objs[k], os.path.join(CSRC, SOURCES[k])]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        subprocess.run(cmd, check=True)
+
+    with ThreadPoolExecutor(len(SOURCES)) as ex:
+        list(ex.map(compile_one, range(len(SOURCES))))
+    cmd = [HIPCC, "--offload-arch=gfx950", "-fPIC", "-shared", "-o", out + ".tmp", *objs]
     if verbose:
-        print(" ".join(cmd))
+        print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
+    for o in objs:
+        os.remove(o)
     os.replace(out + ".tmp", out)
     return out
 

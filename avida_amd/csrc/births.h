@@ -187,6 +187,7 @@ struct Child {
   int64_t lstride;
   const int32_t* inputs = nullptr;   // the cell inputs, drawn by the caller (serial world), or
                                      // nullptr: SetupInputs from the offspring's own stream
+  uint32_t hs = 0;                   // head start (CTL_HS: 2^16 - birth time; 0 in the serial world)
 };
 // Run by a group of G lanes (G = 64: a wave, 32: a half-wave); `lane` is the
 // lane's index inside its group.
@@ -206,7 +207,7 @@ __device__ __forceinline__ void setup_child(const DevWorld& W, int64_t c, const 
   for (int off = G / 2; off > 0; off >>= 1) gsum += __shfl_xor(gsum, off);
   if (lane == 0) W.gkey[c] = gk_final(gsum, len);
   switch (lane) {
-    case 0: W.ctl[c] = CTL_ALIVE | CTL_FRESH; break;
+    case 0: W.ctl[c] = CTL_ALIVE | CTL_FRESH | (b.hs << CTL_HS_SHIFT); break;
     case 1: W.mem_size[c] = len; break;
     case 2: {
       int mx = 0;
@@ -274,7 +275,7 @@ __device__ __forceinline__ void setup_child_lane(const DevWorld& W, int64_t c, c
     }
   }
   W.gkey[c] = gk_final(gsum, len);
-  W.ctl[c] = CTL_ALIVE | CTL_FRESH;
+  W.ctl[c] = CTL_ALIVE | CTL_FRESH | (b.hs << CTL_HS_SHIFT);
   W.mem_size[c] = len;
   int mx = 0;
   if (W.death_method > 0) { mx = W.age_limit; if (W.death_method == 2) mx *= len; if (mx < 1) mx = 1; }
@@ -309,6 +310,7 @@ __device__ __forceinline__ Child child_of_record(const DevWorld& W, int64_t i) {
   b.merit = __hiloint2double(q0.y, q0.x); b.fitness = __hiloint2double(q0.w, q0.z);
   b.gen = q1.x; b.ccopied = q1.y; b.exec = q1.z; b.gest = q1.w;
   b.lo = (uint32_t)q2.x; b.hi = (uint32_t)q2.y; b.ctr = (uint32_t)q2.z;
+  b.hs = 0x10000u - BI_TIME(q2.w);
   b.ltask = W.b_inh + i * BI_WORDS + BI_LTASK; b.lstride = 1;
   return b;
 }

@@ -161,7 +161,7 @@ int setup_world(avgpu_world* w, int64_t n, bool test_buffers) {
   // occupancy, owners and the four placement rounds' claims, each with the two
   // ghost rows a strip tile keeps after its n cells
   const int64_t ng = n + 2 * (int64_t)c.world_x;
-  A(occ, ng); A(claim, ng); A(claim2, ng); A(owner, ng);
+  A(occ, ng); A(claim, ng); A(claim2, ng); A(owner, ng); A(killt, n); A(sdone, n);
   W.claim_r[0] = W.claim; W.claim_r[1] = W.claim2;
   A(claim_r[2], ng); A(claim_r[3], ng); A(b_tgt, 4 * R);
   if (test_buffers) {
@@ -175,6 +175,13 @@ int setup_world(avgpu_world* w, int64_t n, bool test_buffers) {
   if ((rc = w->alloc(&w->d_W, 1))) return rc;
   const int64_t nb = (n + 255) / 256;
   if ((rc = w->alloc(&w->d_totals, (size_t)(8 + 2 * nb)))) return rc;
+  // the scheduler's tree: block counts, the top tree's levels (a strip tile
+  // regrows them for the whole world at avgpu_tile_begin)
+  if ((rc = w->alloc(&W.blk_count, (size_t)nb))) return rc;
+  W.tree_cap = 1;
+  while (W.tree_cap < nb) W.tree_cap <<= 1;
+  if ((rc = w->alloc(&W.tree_scr, (size_t)(2 * W.tree_cap)))) return rc;
+  if ((rc = w->alloc(&W.tree_cnt, (size_t)(2 * W.tree_cap)))) return rc;
   if ((rc = w->alloc(&w->d_stats, (size_t)(40 + 24 * nb)))) return rc;
 #undef A
   w->has_test_buffers = test_buffers;
@@ -719,8 +726,9 @@ int avgpu_step(avgpu_world* w, int64_t first, int64_t count, const int32_t* budg
     HIPCHK(hipMalloc(&d_b, count * sizeof(int32_t)));
     HIPCHK(hipMemcpyAsync(d_b, budget, count * sizeof(int32_t), hipMemcpyHostToDevice, w->stream));
   }
-  HIPCHK(hipMemsetAsync(w->W.counters, 0, NSHARD * CNT_STRIDE * sizeof(unsigned long long), w->stream));
-  HIPCHK(hipMemsetAsync(w->W.b_count, 0, 3 * sizeof(int32_t), w->stream));
+  // the update's counters and queue lengths cleared -- an earlier update run
+  // without statistics has its counts folded into the running sums first
+  launch_reset_counts(w->W, w->stream);
   launch_classify_uniform(w->W, w->stream, first, count, d_b, budget_uniform);
   HIPCHK(hipGetLastError());
   rc = interpret(w, mode, first, count);
@@ -749,7 +757,11 @@ int avgpu_update_run(avgpu_world* w, const double* dev_totals, avgpu_update_stat
   int rc = ready(w);
   if (rc < 0) return rc;
   if (!dev_totals) return fail(AVGPU_EINVAL, "dev_totals is NULL");
-  launch_world_pre(w->W, w->stream, dev_totals, w->ev_fork, (uint32_t)w->update);
+  // every world's {total weight, organisms} -> this world's share of the
+  // picks (cMultiProcessWorld::CalculateUpdateSize) and its allotment
+  if (dev_totals != w->d_totals)
+    HIPCHK(hipMemcpyAsync(w->d_totals, dev_totals, 2 * sizeof(double), hipMemcpyDeviceToDevice, w->stream));
+  launch_world_pre(w->W, w->stream, w->d_totals, w->d_totals + 8, w->ev_fork, (uint32_t)w->update);
   after_resources_begin(w);
   HIPCHK(hipGetLastError());
   rc = interpret(w, AVGPU_MODE_WORLD, 0, w->W.n, true);
@@ -903,6 +915,8 @@ int avgpu_get_stats(avgpu_world* w, avgpu_update_stats* out) {
   out->slices = (int64_t)v[32];
   out->lane_steps = (int64_t)v[33];
   out->births_overwritten = (int64_t)v[34];
+  out->births_cancelled = (int64_t)v[35];
+  out->seed = w->cfg.seed;
   return 0;
 }
 
@@ -1062,6 +1076,10 @@ int avgpu_set_clock(avgpu_world* w, const avgpu_update_stats* last) {
   HIPCHK(hipMemcpyAsync(w->W.counters + CNT_CUM_FLAG, &one, sizeof(one), hipMemcpyHostToDevice, w->stream));
   HIPCHK(hipStreamSynchronize(w->stream));
   w->update = last->update + 1;
+  // the scheduler's key (the world's RANDOM_SEED) comes with the clock
+  w->cfg.seed = last->seed;
+  w->W.seed_lo = (uint32_t)last->seed;
+  w->W.seed_hi = (uint32_t)(last->seed >> 32);
   return 0;
 }
 
@@ -1419,9 +1437,21 @@ int avgpu_tile_begin(avgpu_world* w, const double* dev_gathered, int ntiles) {
   if (w->W.n_spatial && !w->W.rs_recv[0])
     return fail(AVGPU_ESTATE, "spatial resources need avgpu_set_tile_res_buffers");
   if (!dev_gathered || ntiles < 1) return fail(AVGPU_EINVAL, "gathered partials");
-  launch_tile_totals(w->W, w->stream, dev_gathered, ntiles, w->d_totals);
+  // the scheduler's top tree spans every strip's blocks
+  {
+    int64_t P = 1;
+    const int64_t nbt = ((w->W.n + 255) / 256) * (int64_t)ntiles;
+    while (P < nbt) P <<= 1;
+    if (P > w->W.tree_cap) {   // (the smaller buffers stay in the world's allocations)
+      if ((rc = w->alloc(&w->W.tree_scr, (size_t)(2 * P))) < 0) return rc;
+      if ((rc = w->alloc(&w->W.tree_cnt, (size_t)(2 * P))) < 0) return rc;
+      w->W.tree_cap = P;
+      const int prc = push_world(w);
+      if (prc < 0) return prc;
+    }
+  }
   // (the counters were cleared by avgpu_tile_partials' launch)
-  launch_world_pre(w->W, w->stream, w->d_totals, w->ev_fork, (uint32_t)w->update, false);
+  launch_tile_pre(w->W, w->stream, dev_gathered, ntiles, w->d_totals, w->ev_fork, (uint32_t)w->update);
   after_resources_begin(w);
   HIPCHK(hipGetLastError());
   rc = interpret(w, AVGPU_MODE_WORLD, 0, w->W.n, true);
@@ -1435,8 +1465,9 @@ int avgpu_tile_begin(avgpu_world* w, const double* dev_gathered, int ntiles) {
 int avgpu_tile_place(avgpu_world* w, int round, int phase) {
   int rc = tile_ready(w);
   if (rc < 0) return rc;
-  if (round < 0 || round > 3 || phase < 0 || phase > 2 || (phase >= 1 && round != 3))
-    return fail(AVGPU_EINVAL, "round 0..3 with phase 0; phases 1, 2 after round 3");
+  if (round < 0 || round > 3 || phase < 0 || phase > 3 || (phase >= 1 && phase <= 2 && round != 3) ||
+      (phase == 3 && round != 0))
+    return fail(AVGPU_EINVAL, "round 0..3 with phase 0, round 0 with phase 3; phases 1, 2 after round 3");
   launch_tile_place(w->W, w->stream, round, phase);
   HIPCHK(hipGetLastError());
   return 0;

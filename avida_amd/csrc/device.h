@@ -19,10 +19,12 @@
 // birth record row b_inh[r * BI_WORDS ..]: merit, fitness (doubles), generation,
 // copied size, executed size, gestation time, the offspring's RNG key and
 // counter, the parent's last task counts
-// (BI_FINAL = 1: the divide left the offspring's fitness and key and the
-// parent's phenotype to finalize_key / finalize_phenotype, world.hip)
+// (BI_FINAL bit 0 = 1: the divide left the offspring's fitness and key and the
+// parent's phenotype to finalize_key / finalize_phenotype, world.hip; bits
+// 16..31 the offspring's birth time in the update, 1/2^16 -- DESIGN.md 5)
 enum { BI_MERIT = 0, BI_FITNESS = 2, BI_GEN = 4, BI_CCOPIED = 5, BI_EXEC = 6, BI_GEST = 7,
        BI_RLO = 8, BI_RHI = 9, BI_RCTR = 10, BI_FINAL = 11, BI_LTASK = 12, BI_WORDS = 32 };
+#define BI_TIME(w) ((uint32_t)(w) >> 16)
 #define CODE_MASK 0x3F
 #define TF_COPIED 0x40
 #define TF_EXEC 0x80
@@ -41,6 +43,12 @@ enum { BI_MERIT = 0, BI_FITNESS = 2, BI_GEN = 4, BI_CCOPIED = 5, BI_EXEC = 6, BI
 #define CTL_FRESH 0x800u
 // serial world: died in a speculative step (m_spec_die); removed at its next pick
 #define CTL_SPECDIE 0x1000u
+// head start of an offspring not yet allotted (17 bits: 2^16 - its birth
+// time, 1..2^16; 0 = none): its first allotment weights its merit by
+// 1 + hs / 2^16 (sched_weight), then clears it
+#define CTL_HS_SHIFT 14
+#define CTL_HS(c) (((c) >> CTL_HS_SHIFT) & 0x1FFFFu)
+#define CTL_HS_MASK (0x1FFFFu << CTL_HS_SHIFT)
 
 #define NUM_CLASSES 4
 #define ACLASS_NONE 0xFF
@@ -162,8 +170,8 @@ struct DevWorld {
   // access whose line held no other field of the record
   int32_t* b_inh;     // [rcap][BI_WORDS]
   int32_t* b_target;  // [rcap]
-  int8_t* b_state;    // [rcap]  0 pending, 1+k placed in round k, -1 failed
-  unsigned long long* b_prio; // [rcap]
+  int8_t* b_state;    // [rcap]  BS_* (world.hip)
+  unsigned long long* b_prio; // [rcap] claim key of the record's current round (world.hip claim_key)
   uint8_t* b_genome;  // [rcap][TAPE_SLOT]
   // placement scratch, n cells + 2 ghost rows (strip tiles, below)
   uint8_t* occ;       // [n + 2X]
@@ -175,7 +183,16 @@ struct DevWorld {
   // round 3's, k_tile_prep the ghost rows)
   unsigned long long* claim_r[4];
   int32_t* b_tgt;     // [4][rcap] the record's target in each placement round it claimed in
-  int32_t* owner;     // [n + 2X]  record id, -1 none, REMOTE_OWNER(k) won by a halo birth in round k
+  int32_t* owner;     // [n + 2X]  record id, -1 none, REMOTE_OWNER(k, t) won by a halo birth in round k
+  uint32_t* killt;    // [n] 2^16 - the earliest birth time of a round-0 pick that kills the cell's
+                      // organism, 0 none (placement launch 0 -> the cancellations of launch 0b)
+  // the scheduler's tree (k_block_counts -> k_allot): each 256-cell block's
+  // share of the update's picks, then the tree's levels (scratch)
+  int64_t* blk_count; // [nb]
+  double* tree_scr;   // [2 * P] levels of the top tree over the block partials (P = pow2 >= blocks)
+  int64_t* tree_cnt;  // [2 * P] their counts
+  int64_t tree_cap;   // P of the allocation (strip tiles: >= every strip's blocks)
+  int32_t* sdone;     // [n] instructions a spilled slice ran before it spilled (birth times)
   // test-CPU outputs
   uint8_t* t_flags;   // [n][TAPE_SLOT] executed flags snapshot ('+'/'-')
   int32_t* t_flags_len; // [n]
@@ -294,15 +311,22 @@ struct DevWorld {
   int64_t r_arena;
 };
 
-#define REMOTE_OWNER(k) (-2 - (k))
-__host__ __device__ inline int64_t halo_bytes(int x) { return ((int64_t)x * 33 + 15) / 16 * 16; }
+// owner of a cell won by a neighbouring strip's offspring in round k at birth time t
+#define REMOTE_OWNER(k, t) (-2 - ((k) + 4 * (int)(t)))
+// halo buffer: per round parity X u64 claims on the receiver's edge row and X
+// u64 the sender's own claims on its edge row, X u8 edge-row occupancy, then
+// (round 0's picks) X u32 kill times of the sender's picks on the receiver's
+// edge row (2^16 - t, max-reduced)
+__host__ __device__ inline int64_t halo_kt_off(int x) { return ((int64_t)x * 33 + 3) / 4 * 4; }
+__host__ __device__ inline int64_t halo_bytes(int x) { return (halo_kt_off(x) + 4 * (int64_t)x + 15) / 16 * 16; }
 struct HaloHdr { int32_t count, arena_used, overflow, pad; };
 // one offspring placed across a tile edge (the migrant record of
 // cMultiProcessWorld.cc:142-190, restated for strip tiles)
 struct HaloRec {
   int32_t col, round, len, gen, ccopied, exec, gest;
   uint32_t rng_lo, rng_hi, rng_ctr;
-  int32_t off, pad;
+  int32_t off;
+  uint32_t t;         // birth time (owner bookkeeping, head start)
   double merit, fitness;
   int32_t last_task[AVGPU_NUM_LOGIC_TASKS], pad2[3];   // the parent's (SetupOffspring)
 };
@@ -347,6 +371,8 @@ enum { SEG_OSLIP = 0, SEG_PSLIP, SEG_SSLIP, SEG_TTRANS, SEG_PTRANS, SEG_STRANS, 
 #define CNT_OVERSIZE 21   /* offspring a slip grew past AVGPU_MAX_GENOME (counted in DROPPED too) */
 #define CNT_MEM_CAP 23    /* copy insertions past AVGPU_MAX_GENOME sites / removals from one site (skipped) */
 #define CNT_OVERWRITTEN 24  /* offspring placed, then killed by a later birth into the same cell this update */
+#define CNT_CANCELLED 25  /* records whose parent's cell got an offspring before their divide (never placed) */
+#define CNT_BAD_RECORD 26 /* record / cell fields out of range where used as an index (guarded; must be 0) */
 // 32..37: AVGPU_PHASE_CLOCKS loop cycles by block (decode, fast, copy, switch,
 // wave phase, advance); 38..43: slow-switch cycles in pop, push, IO, h-alloc,
 // h-divide, h-search/if-label
@@ -547,6 +573,72 @@ __device__ __forceinline__ double det_exp2(double x) {
   return ldexp(y, (int)n);
 }
 
+// square root from IEEE adds / multiplies / divisions (oracle det_sqrt): the
+// exponent halved exactly, then 6 Newton steps
+__device__ __forceinline__ double det_sqrt(double x) {
+  if (!(x > 0.0)) return 0.0;
+  int e;
+  const double m = frexp(x, &e);
+  double y = ldexp(__dadd_rn(m, 0.5), e / 2 - ((e & 1) && e < 0 ? 1 : 0));
+  for (int k = 0; k < 6; k++) y = __dmul_rn(0.5, __dadd_rn(y, __ddiv_rn(x, y)));
+  return y;
+}
+__device__ __forceinline__ double pow_int(double q, int64_t n) {
+  double r = 1.0, b = q;
+  while (n) { if (n & 1) r = __dmul_rn(r, b); b = __dmul_rn(b, b); n >>= 1; }
+  return r;
+}
+// Binomial(n, p) from one 32-bit word h (oracle binom_draw: inversion below a
+// mean of 12 on the smaller side, else normal with the binomial's skew, z the
+// centred sum of 12 16-bit uniforms)
+__device__ __forceinline__ int64_t binom_draw(int64_t n, double p, uint32_t h) {
+  if (n <= 0 || !(p > 0.0)) return 0;
+  if (p >= 1.0) return n;
+  const bool flip = p > 0.5;
+  const double pp = flip ? __dsub_rn(1.0, p) : p, q = __dsub_rn(1.0, pp);
+  const double mean = __dmul_rn((double)n, pp);
+  int64_t k;
+  if (mean < 12.0) {
+    const double u = __dmul_rn(__dadd_rn((double)h, 0.5), 2.3283064365386962890625e-10);
+    const double r = __ddiv_rn(pp, q);
+    double f = pow_int(q, n);
+    double F = f;
+    k = 0;
+    while (F < u && k < n && k < 256) {
+      f = __ddiv_rn(__dmul_rn(f, __dmul_rn((double)(n - k), r)), (double)(k + 1));
+      k++;
+      F = __dadd_rn(F, f);
+    }
+  } else {
+    uint32_t x = h;
+    double sum = 0.0;
+    for (int i = 0; i < 6; i++) {
+      x = lowbias32(x + 0x9E3779B9U);
+      sum = __dadd_rn(__dadd_rn(sum, (double)(x & 0xFFFFu)), (double)(x >> 16));
+    }
+    const double z = __dsub_rn(__dmul_rn(__dadd_rn(sum, 6.0), 1.52587890625e-05), 6.0);
+    const double sd = det_sqrt(__dmul_rn(mean, q));
+    const double skew = __ddiv_rn(__dmul_rn(__dsub_rn(q, pp), __dsub_rn(__dmul_rn(z, z), 1.0)), 6.0);
+    const double v = __dadd_rn(__dadd_rn(__dadd_rn(mean, __dmul_rn(sd, z)), skew), 0.5);
+    k = v < 1.0 ? 0 : (int64_t)floor(v);
+    if (k > n) k = n;
+  }
+  return flip ? n - k : k;
+}
+// the word of scheduler-tree node `node` in update u (oracle node_draw)
+#define SALT_TOP 0x7A11C0DEu
+#define SALT_BLOCK 0x51CEB10Cu
+__device__ __forceinline__ uint32_t node_draw(uint32_t slo, uint32_t shi, uint32_t update, uint32_t salt,
+                                              uint64_t node) {
+  return lowbias32(lowbias32(lowbias32(update * 0x85EBCA6BU + shi) ^ (uint32_t)node ^ salt) +
+                   (uint32_t)(node >> 32) + slo);
+}
+// the scheduler weight of a living organism (oracle sched_weight)
+__device__ __forceinline__ double sched_weight(double merit, uint32_t ctl) {
+  const uint32_t hs = CTL_HS(ctl);
+  return hs ? __dmul_rn(merit, __dadd_rn(1.0, __dmul_rn((double)hs, 1.0 / 65536.0))) : merit;
+}
+
 // CalcSizeMerit (main/cPhenotype.cc:1760-1816)
 __device__ __forceinline__ int size_merit(int method, int base_const, int glen, int copied, int exe) {
   int s;
@@ -620,8 +712,10 @@ void launch_interpret_classes(const DevWorld& W, const DevWorld* dW, int mode, h
 bool class_timing_all();   // AVGPU_CLASS_TIMING (interp.hip)
 void launch_world_begin(const DevWorld& W, hipStream_t s, double* d_totals, double* d_scratch,
                         hipEvent_t lists_ready, uint32_t update);
-void launch_world_pre(const DevWorld& W, hipStream_t s, const double* d_totals, hipEvent_t lists_ready,
+void launch_world_pre(const DevWorld& W, hipStream_t s, double* d_totals, double* d_scratch, hipEvent_t lists_ready,
                       uint32_t update, bool reset = true);
+void launch_tile_pre(const DevWorld& W, hipStream_t s, const double* d_gathered, int ntiles, double* d_totals,
+                     hipEvent_t lists_ready, uint32_t update);
 // allotment draw of organism (lo, hi) in update u (oracle allot_draw)
 __device__ __forceinline__ uint32_t allot_draw(uint32_t lo, uint32_t hi, uint32_t update) {
   return lowbias32(lowbias32(update * 0x85EBCA6BU + hi) ^ lo ^ 0x27D4EB2FU);
@@ -648,8 +742,6 @@ void launch_get_census(const DevWorld& W, hipStream_t s, int64_t first, int64_t 
 void launch_merit_total(const DevWorld& W, hipStream_t s, double* d_totals, double* d_scratch);
 // strip tiles
 void launch_tile_partials(const DevWorld& W, hipStream_t s, double* d_out);
-void launch_tile_totals(const DevWorld& W, hipStream_t s, const double* d_gathered, int ntiles,
-                        double* d_totals);
 void launch_tile_after_interpret(const DevWorld& W, hipStream_t s);
 void launch_tile_place(const DevWorld& W, hipStream_t s, int round, int phase);
 void launch_tile_finish(const DevWorld& W, hipStream_t s, double* d_stats, bool eager);

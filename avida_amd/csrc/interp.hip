@@ -289,7 +289,7 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
   int r0 = 0, r1 = 0, r2 = 0, ip = 0, rh = 0, wh = 0, fh = 0;
   uint32_t ctl = 0, rl = 0, klo = 0, khi = 0, kct = 0;
   uint32_t olo = 0, ohi = 0;     // the organism's own key (its offspring's keys derive from it)
-  int cyc = 0, tu = 0, gs = 0, mx = 0, blen = 0, budget = 0, errs = 0;
+  int cyc = 0, tu = 0, gs = 0, mx = 0, blen = 0, budget = 0, errs = 0, sdone = 0;
   int in0 = 0, in1 = 0, in2 = 0, intot = 0, inptr = 0, inp0 = 0, inp1 = 0, inp2 = 0;
   int outv = 0, outtot = 0;
   double bonus = 0.0;
@@ -320,6 +320,9 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
     budget = W.budget[cell];
     prim = (budget & BUDGET_PRIM) != 0;   // a spilled slice already used its primary record
     budget &= ~BUDGET_PRIM;
+    // a spill row continues a slice: the instructions it ran before it spilled
+    // (birth times count from the slice's start)
+    if (row > NUM_CLASSES - 1) sdone = W.sdone[cell];
     if (serial) { budget = serial == 1 ? 1 : 32; prim = false; }
     inp0 = W.inputs[cell]; inp1 = W.inputs[N + cell]; inp2 = W.inputs[2 * N + cell];
     dexe = W.executed[cell]; dcop = W.copied[cell]; dgen = W.generation[cell];
@@ -1463,13 +1466,18 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
                     W.b_pcnt[(int64_t)k * rcap + rec] = pcnt[k];
                   }
                 // the inherited phenotype: one 128-B row, 16-B stores (device.h BI_*)
-                // (deferred: fitness and key left to world.hip's finalize_*, BI_FINAL = 1)
+                // (deferred: fitness and key left to world.hip's finalize_*, BI_FINAL bit 0)
                 int32_t* irow = b_inh + (int64_t)rec * BI_WORDS;
                 const long long mb = __double_as_longlong(merit);
                 const long long fb = defer ? 0ll : __double_as_longlong(__ddiv_rn(__dmul_rn(base, bon), (double)gt));
                 st_async_b128(irow, (uint32_t)mb, (uint32_t)(mb >> 32), (uint32_t)fb, (uint32_t)(fb >> 32));
                 st_async_b128(irow + 4, (uint32_t)gen, (uint32_t)cop, (uint32_t)exe, (uint32_t)gt);
-                st_async_b128(irow + 8, clo, chi, 0u, defer ? 1u : 0u);
+                // birth time t = k / (b + 1) in 1/2^16 (oracle birth_time): k the
+                // slice's instructions so far, the h-divide included; b its budget
+                const int kdone = sdone + executed;
+                const uint32_t tb = (uint32_t)__ddiv_rn(__dmul_rn((double)kdone, 65536.0),
+                                                        (double)((int64_t)kdone + budget + 1));
+                st_async_b128(irow + 8, clo, chi, 0u, (defer ? 1u : 0u) | (tb << 16));
                 st_async_b128(irow + 12, (uint32_t)tc[0], (uint32_t)tc[1], (uint32_t)tc[2], (uint32_t)tc[3]);
                 st_async_b128(irow + 16, (uint32_t)tc[4], (uint32_t)tc[5], (uint32_t)tc[6], (uint32_t)tc[7]);
                 st_async_b128(irow + 20, (uint32_t)tc[8], 0u, 0u, 0u);
@@ -1658,6 +1666,7 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
     if (serial) W.sctx[2] = kct;                             // the context stream moved on
     else W.rng[2 * N + cell] = kct;
     W.budget[cell] = spill ? (budget | (prim ? BUDGET_PRIM : 0)) : 0;
+    if (spill && mode == AVGPU_MODE_WORLD) W.sdone[cell] = sdone + executed;
     // merit, fitness, gestation time, copied / executed sizes and last-task
     // counts were stored at the divide (st_async)
     // (a fresh organism's zero rows are stored here rather than at activation:
@@ -2005,6 +2014,7 @@ __global__ __launch_bounds__(64, 1) void k_serial_update(const DevWorld* __restr
         if (parent_alive) stree_set(tree, size, c, W.merit[c]);   // AdjustSchedule(parent) :933
         Child b = child_of_record(W, c);
         b.inputs = in3;                                          // from the context stream (lane 0's)
+        b.hs = 0;                                                // placed at once: no head start
         setup_child<64>(W, t, b, reinterpret_cast<const uint32_t*>(W.b_genome + c * TAPE_SLOT), lane);
         __threadfence_block();
         if (lane == 0) {
@@ -2109,7 +2119,9 @@ static void launch_classes(const DevWorld& W, const DevWorld* dW, int mode, hipS
   // DEF) -- the spill rows run alone after class 0, latency-bound on their
   // longest slice, so every instruction of the generic paths is on the
   // update's critical path
-  const bool fast = mode == AVGPU_MODE_WORLD && W.env_simple && W.env_res_mask == 0u && def_knobs(W);
+  // (DEF defers the divide's phenotype work to placement round 0: only world
+  // updates run placement -- avgpu_step(MODE_WORLD) takes the general path)
+  const bool fast = sorted && mode == AVGPU_MODE_WORLD && W.env_simple && W.env_res_mask == 0u && def_knobs(W);
   auto row = [&](int S, dim3 grid, hipStream_t st, int cls, int r, int lpw) {
 #define ROW_LAUNCH(SZ) \
     do { if (fast) hipLaunchKernelGGL((k_interpret<SZ, REC, false, true, true>), grid, dim3(64), 0, st, dW, cls, r, mode, first, count, 0, lpw); \
@@ -2148,7 +2160,7 @@ static void launch_classes(const DevWorld& W, const DevWorld* dW, int mode, hipS
     hipStreamWaitEvent(aux[0], ev_join[1], 0);
     hipEventRecord(ev_join[0], aux[0]);
   }
-  if (mode == AVGPU_MODE_WORLD && W.env_simple && W.env_res_mask == 0u && def_knobs(W))
+  if (fast)
     hipLaunchKernelGGL((k_interpret<CLASS0_SIZE, REC, true, true, true>), dim3(blocks), dim3(64), 0, s, dW, 0, 0, mode, first, count, srt, 64);
   else if (mode == AVGPU_MODE_WORLD && W.env_simple && W.env_res_mask == 0u)
     hipLaunchKernelGGL((k_interpret<CLASS0_SIZE, REC, true, true>), dim3(blocks), dim3(64), 0, s, dW, 0, 0, mode, first, count, srt, 64);

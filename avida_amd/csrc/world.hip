@@ -3,7 +3,8 @@
 //   k_get_states     cHardwareBase inspection API (trace tuple gather)
 //   k_classify_*     budget + LDS size-class lists for k_interpret
 //   k_merit_*        deterministic total merit (scheduler input)
-//   k_allot_total    merit-weighted time slicing (cScheduler restated)
+//   k_block_counts, k_allot  the scheduler (cScheduler restated): the update's picks
+//                    split down a binary tree of the cells
 //   k_place_*, k_tile_*  cPopulation::PositionOffspring in conflict-resolving rounds
 //   k_activate       cPopulation::ActivateOrganism + cPhenotype::SetupOffspring
 //   k_stats          cStats reduction inputs
@@ -163,6 +164,7 @@ __device__ void build_state(const DevWorld& W, int64_t c, avgpu_cpu_state& s) {
   s.merit = W.merit[c];
   s.fitness = W.fitness[c];
   s.credit = W.credit[c];
+  s.head_start = CTL_HS(ctl);
 }
 
 __global__ void k_get_states(DevWorld W, int64_t first, int64_t count, avgpu_cpu_state* out,
@@ -224,7 +226,8 @@ __global__ void k_set_states(DevWorld W, int64_t first, int64_t count, const avg
   for (int k = 0; k < 2; k++)
     for (int j = 0; j < AVGPU_STACK_SIZE; j++) x[XS_STACK + k * AVGPU_STACK_SIZE + j] = s.stack[k][j];
   W.ctl[c] = (uint32_t)(s.stack_ptr[0] & 0xF) | ((uint32_t)(s.stack_ptr[1] & 0xF) << 4) |
-             (s.cur_stack ? CTL_CURSTK : 0u) | (s.mal_active ? CTL_MAL : 0u) | (s.alive ? CTL_ALIVE : 0u);
+             (s.cur_stack ? CTL_CURSTK : 0u) | (s.mal_active ? CTL_MAL : 0u) | (s.alive ? CTL_ALIVE : 0u) |
+             ((s.head_start & 0x1FFFFu) << CTL_HS_SHIFT);
   uint32_t rl = (uint32_t)(s.read_label_len & 15);
   for (int k = 0; k < (s.read_label_len & 15) && k < AVGPU_MAX_LABEL; k++)
     rl |= (uint32_t)(s.read_label[k] & 3) << (4 + 2 * k);
@@ -359,8 +362,9 @@ __global__ __launch_bounds__(256) void k_merit_partial(DevWorld W, double* parti
 #pragma unroll
   for (int k = 0; k < 4; k++) {
     const int64_t c = b * 256 + lane + 64 * k;
-    const bool live = c < W.n && (W.ctl[c] & CTL_ALIVE);
-    m[k] = live ? W.merit[c] : 0.0;
+    const uint32_t ctl = c < W.n ? W.ctl[c] : 0u;
+    const bool live = (ctl & CTL_ALIVE) != 0;
+    m[k] = live ? sched_weight(W.merit[c], ctl) : 0.0;   // the scheduler weight (oracle block_levels)
     a += live ? 1 : 0;
   }
   double z = __dadd_rn(__dadd_rn(m[0], m[2]), __dadd_rn(m[1], m[3]));
@@ -376,56 +380,91 @@ __global__ __launch_bounds__(256) void k_merit_partial(DevWorld W, double* parti
   }
 }
 
-// totals[0] = sum merit, totals[1] = alive count.  Lane t sums partials
-// t, t+256, ... in order, then the fixed pairwise tree (oracle: tree_merit_sum).
-// Tiled: the partials of tile k are gathered[k*2*nb ..], alive counts after them.
-template <bool TILES>
-__global__ __launch_bounds__(256) void k_merit_final(const double* partial, const int32_t* alive_partial,
-                                                     const double* gathered, int64_t nb, int ntiles,
-                                                     double* totals, int use_global) {
-  __shared__ double s[256];
-  __shared__ long long cnt[256];
-  long long c = 0;
-  double acc = 0.0;
-  const int64_t total = TILES ? nb * ntiles : nb;
-  if (TILES) {
-    // entry b = tile k, block j of the gathered vector, walked without a
-    // division per entry; the loads of 8 entries go out before their adds
-    int64_t k = threadIdx.x / nb, j = threadIdx.x - k * nb;
-    for (int64_t b0 = threadIdx.x; b0 < total; b0 += 256 * 8) {
-      double v[8], a[8];
-#pragma unroll
-      for (int u = 0; u < 8; u++) {
-        const bool in = b0 + 256 * u < total;
-        v[u] = in ? gathered[k * 2 * nb + j] : 0.0;
-        a[u] = in ? gathered[k * 2 * nb + nb + j] : 0.0;
-        j += 256;
-        while (j >= nb) { j -= nb; k++; }
+// ---- the scheduler: PROBABILISTIC slicing as the reference's picks ----
+// (oracle/oracle.cc block_levels / top_tree / block_split) The
+// update's UD = AVE_TIME_SLICE x N picks are split down a fixed binary tree
+// with a Binomial at every node: the top tree over the 256-cell blocks'
+// partials (k_block_counts, one workgroup), then each block's stride tree
+// down to its cells (k_allot).
+//
+// k_block_counts: heap-ordered top tree in tree_scr (node h = (1 << l) + i,
+// children 2h, 2h + 1; leaves at P + block, zero-padded to P = 2^L), built
+// bottom up, split top down in tree_cnt.  mode 0: this world's partials
+// (part doubles, alive int32); mode 1: a strip's gathered vector (tile k's
+// block j at gathered[k * 2 nb + j], its alive count nb after); mode 2: this
+// world's partials with the totals of every world handed in (totals[0..1]:
+// cMultiProcessWorld::CalculateUpdateSize, main/cMultiProcessWorld.cc:
+// 396-405 -- this world's picks = (int)((local / total) * AVE_TIME_SLICE *
+// N_total)); mode 3: the totals only (totals[0..1] = root, N).
+// totals[2] = the weight total INTEGRATED divides by, totals[3] = UD.
+__global__ __launch_bounds__(1024) void k_block_counts(DevWorld W, const double* part, const int32_t* alive_part,
+                                                       int64_t nb, int ntiles, int L, double* totals,
+                                                       uint32_t update, int mode) {
+  __shared__ long long s_cnt[1024];
+  __shared__ long long s_root;
+  const int tid = threadIdx.x;
+  const int64_t P = (int64_t)1 << L, nbt = mode == 1 ? nb * ntiles : nb;
+  double* scr = W.tree_scr;
+  int64_t* cnt = W.tree_cnt;
+  long long a = 0;
+  for (int64_t g = tid; g < P; g += 1024) {
+    double v = 0.0;
+    if (g < nbt) {
+      if (mode == 1) {
+        const int64_t k = g / nb, j = g - k * nb;
+        v = part[k * 2 * nb + j];
+        a += (long long)part[k * 2 * nb + nb + j];
+      } else {
+        v = part[g];
+        a += alive_part[g];
       }
-#pragma unroll
-      for (int u = 0; u < 8; u++)
-        if (b0 + 256 * u < total) { acc = __dadd_rn(acc, v[u]); c += (long long)a[u]; }
     }
-  } else {
-    for (int64_t b = threadIdx.x; b < total; b += 256) {
-      c += alive_partial[b];
-      acc = __dadd_rn(acc, partial[b]);
-    }
+    scr[P + g] = v;
   }
-  cnt[threadIdx.x] = c;
-  s[threadIdx.x] = acc;
+  s_cnt[tid] = a;
   __syncthreads();
-  for (int stride = 128; stride >= 1; stride >>= 1) {
-    if ((int)threadIdx.x < stride) {
-      s[threadIdx.x] = __dadd_rn(s[threadIdx.x], s[threadIdx.x + stride]);
-      cnt[threadIdx.x] += cnt[threadIdx.x + stride];
+  for (int l = L - 1; l >= 0; l--) {
+    const int64_t w0 = (int64_t)1 << l;
+    for (int64_t i = tid; i < w0; i += 1024) scr[w0 + i] = __dadd_rn(scr[2 * (w0 + i)], scr[2 * (w0 + i) + 1]);
+    __syncthreads();
+  }
+  if (tid == 0) {
+    long long n = 0;
+    for (int i = 0; i < 1024; i++) n += s_cnt[i];
+    const double root = scr[1];
+    const double ave = (double)W.ave_time_slice;
+    long long nroot = (long long)W.ave_time_slice * n;
+    if (mode == 2) {
+      const double tot = totals[0];
+      nroot = tot > 0.0 ? (long long)__dmul_rn(__dmul_rn(__ddiv_rn(root, tot), ave), totals[1]) : 0;
+      totals[2] = tot;
+      totals[3] = __dmul_rn(ave, totals[1]);
+    } else {
+      totals[0] = root;
+      totals[1] = (double)n;
+      totals[2] = root;
+      totals[3] = __dmul_rn(ave, (double)n);
+    }
+    s_root = nroot;
+    cnt[1] = nroot;
+  }
+  __syncthreads();
+  if (mode == 3) return;
+  for (int l = 0; l < L; l++) {
+    const int64_t w0 = (int64_t)1 << l;
+    for (int64_t i = tid; i < w0; i += 1024) {
+      const int64_t h = w0 + i, n = cnt[h];
+      const int64_t left = binom_draw(n, __ddiv_rn(scr[2 * h], scr[h]),
+                                      node_draw(W.seed_lo, W.seed_hi, update, SALT_TOP, (uint64_t)h));
+      cnt[2 * h] = left;
+      cnt[2 * h + 1] = n - left;
     }
     __syncthreads();
   }
-  if (threadIdx.x == 0 && !use_global) {
-    totals[0] = s[0];
-    totals[1] = (double)cnt[0];
-  }
+  const int64_t b0 = mode == 1 ? W.cell0 / 256 : 0;
+  const int64_t nloc = (W.n + 255) / 256;
+  for (int64_t j = tid; j < nloc; j += 1024) W.blk_count[j] = cnt[P + b0 + j];
+  (void)s_root;
 }
 
 __device__ __forceinline__ void occ_init_cell(const DevWorld& W, int64_t c) {
@@ -433,110 +472,88 @@ __device__ __forceinline__ void occ_init_cell(const DevWorld& W, int64_t c) {
   W.owner[c] = -1;
 }
 
-// cScheduler restated (DESIGN.md "Scheduler"): lambda = UD * merit / total.
-// Writes the cell's budget and class tag; returns the budget.
-__device__ __forceinline__ int allot_cell(const DevWorld& W, int64_t c, double sum, double alive, uint32_t update,
-                                          bool& want, int& cls) {
-  want = false;
-  cls = 0;
-  {
-    int b = 0;
-    if (W.ctl[c] & CTL_ALIVE) {
-      const int64_t ud = (int64_t)W.ave_time_slice * (int64_t)alive;
-      if (W.slicing == AVGPU_SLICE_CONSTANT || !(sum > 0.0)) {
-        b = W.ave_time_slice;
-      } else {
-        double lam = __ddiv_rn(__dmul_rn((double)ud, W.merit[c]), sum);
-        if (lam > 1.0e8) lam = 1.0e8;
-        if (W.slicing == AVGPU_SLICE_INTEGRATED) {
-          double cr = __dadd_rn(W.credit[c], lam);
-          const double fl = floor(cr);
-          b = (int)fl;
-          W.credit[c] = __dsub_rn(cr, fl);
-        } else {
-          const double fl = floor(lam);
-          const double frac = __dsub_rn(lam, fl);
-          // P(frac) on the stateless allotment draw (the organism's own
-          // stream carries only the reference's ctx.GetRandom() calls)
-          const double t = __dmul_rn(frac, 4294967296.0);
-          const uint64_t th = (uint64_t)ceil(t);
-          const bool extra = (uint64_t)allot_draw(W.rng[c], W.rng[W.n + c], update) < th;
-          b = (int)fl + (extra ? 1 : 0);
-        }
-      }
-      want = b > 0;
-      if (want) cls = class_of(need_of_cell(W, (int)c));
-    }
-    W.budget[c] = b;
-    W.aclass[c] = want ? (uint8_t)cls : (uint8_t)ACLASS_NONE;
-    return b;
+// k_allot: one 256-cell block per workgroup.  The block's stride tree over its
+// cells' weights (levels in LDS: level k of 2^k nodes at offset 2^k - 1, node
+// (k, t) = the cells = t mod 2^k, the additions of k_merit_partial), then its
+// count blk_count[b] split top down to the cells (PROBABILISTIC);
+// INTEGRATED: lambda = UD * weight / total with a credit carry; CONSTANT (or
+// no weight at all): AVE_TIME_SLICE.  Each cell's head start is consumed here.
+// Also the cell's budget and class tag, the placement occupancy of this
+// update (living cells occupied; an organism that dies in its slice clears
+// its cell at write-back), its kill time, the previous update's round-3
+// claim, and the class lists.
+__global__ __launch_bounds__(256) void k_allot(DevWorld W, const double* totals, uint32_t update) {
+  __shared__ double lv[511];
+  __shared__ long long cn[256];
+  const int t = threadIdx.x;
+  const int64_t b = blockIdx.x;
+  const int64_t c = b * 256 + t;
+  const bool in = c < W.n;
+  const uint32_t ctl = in ? W.ctl[c] : 0u;
+  const bool alive = (ctl & CTL_ALIVE) != 0;
+  double merit = alive ? W.merit[c] : 0.0;
+  if (alive && !(merit >= 0.0 && merit < 1.0e300)) {   // a corrupt merit is counted, not scheduled
+    count_add(W, CNT_BAD_RECORD, 1ull);
+    merit = 0.0;
   }
-}
-
-
-// A single world's allotment with its total merit (k_merit_final + k_allot
-// in one launch): blocks of 1024 threads, two cells per thread.  Each block
-// first recomputes the total merit from the block partials of k_merit_partial
-// in k_merit_final's fixed order (lane t sums partials t, t+256, ..., then the
-// pairwise tree), so every block holds the same bits; block 0 stores them.
-// partial == nullptr (strip tiles): the totals are already in `totals`
-// (k_merit_final<true> over the gathered partials of every strip)
-__global__ __launch_bounds__(1024) void k_allot_total(DevWorld W, const double* partial,
-                                                      const int32_t* alive_partial, int64_t nb,
-                                                      double* totals, uint32_t update) {
-  __shared__ double s_sum[256];
-  __shared__ long long s_cnt[256];
-  const int tid = threadIdx.x;
-  if (!partial) {
-    if (tid == 0) { s_sum[0] = totals[0]; s_cnt[0] = (long long)totals[1]; }
-  } else if (tid < 256) {
-    double acc = 0.0;
-    long long cnt = 0;
-    for (int64_t b0 = tid; b0 < nb; b0 += 256 * 8) {
-      double v[8];
-      int a[8];
-#pragma unroll
-      for (int k = 0; k < 8; k++) {
-        const int64_t b = b0 + 256 * k;
-        v[k] = b < nb ? partial[b] : 0.0;
-        a[k] = b < nb ? alive_partial[b] : 0;
-      }
-#pragma unroll
-      for (int k = 0; k < 8; k++)
-        if (b0 + 256 * k < nb) { acc = __dadd_rn(acc, v[k]); cnt += a[k]; }
+  const double wt = alive ? sched_weight(merit, ctl) : 0.0;
+  const double total = totals[2];
+  const bool consts = W.slicing == AVGPU_SLICE_CONSTANT || !(total > 0.0);
+  const bool prob = !consts && W.slicing != AVGPU_SLICE_INTEGRATED;
+  if (prob) {                                  // block-uniform
+    lv[255 + t] = wt;
+    __syncthreads();
+    for (int k = 7; k >= 0; k--) {
+      const int o = (1 << k) - 1, oc = (2 << k) - 1;
+      if (t < (1 << k)) lv[o + t] = __dadd_rn(lv[oc + t], lv[oc + t + (1 << k)]);
+      __syncthreads();
     }
-    s_sum[tid] = acc;
-    s_cnt[tid] = cnt;
-  }
-  __syncthreads();
-  if (partial) {
-    for (int stride = 128; stride >= 1; stride >>= 1) {
-      if (tid < stride) {
-        s_sum[tid] = __dadd_rn(s_sum[tid], s_sum[tid + stride]);
-        s_cnt[tid] += s_cnt[tid + stride];
+    if (t == 0) cn[0] = W.blk_count[b];
+    __syncthreads();
+    const uint64_t gb = (uint64_t)(W.cell0 / 256 + b);
+    for (int k = 0; k < 8; k++) {
+      if (t < (1 << k)) {
+        const int o = (1 << k) - 1, oc = (2 << k) - 1;
+        const long long c0 = cn[t];
+        const long long left = binom_draw(c0, __ddiv_rn(lv[oc + t], lv[o + t]),
+                                          node_draw(W.seed_lo, W.seed_hi, update, SALT_BLOCK,
+                                                    (gb << 9) | (uint64_t)((1 << k) + t)));
+        cn[t] = left;
+        cn[t + (1 << k)] = c0 - left;
       }
       __syncthreads();
     }
   }
-  const double sum = s_sum[0], alive = (double)s_cnt[0];
-  if (partial && blockIdx.x == 0 && tid == 0) { totals[0] = sum; totals[1] = alive; }
-  for (int h = 0; h < 2; h++) {
-    const int64_t c = (int64_t)blockIdx.x * 2048 + h * 1024 + tid;
-    bool want = false;
-    int cls = 0;
-    if (c < W.n) {
-      allot_cell(W, c, sum, alive, update, want, cls);
-      // the placement occupancy of this update (k_occ_init's work): living
-      // cells are occupied; an organism that dies in its slice clears its
-      // cell (interpret_chunk's write-back), and no birth lands before placement
-      occ_init_cell(W, c);
-      // the previous update's round-3 claims (k_activate read them last)
-      W.claim_r[3][c] = 0ull;
+  bool want = false;
+  int cls = 0;
+  if (in) {
+    int bud = 0;
+    if (alive) {
+      if (consts) {
+        bud = W.ave_time_slice;
+      } else if (prob) {
+        bud = (int)min(cn[t], (long long)(BUDGET_PRIM - 1));   // budgets are < 2^30 (device.h)
+      } else {
+        double lam = __ddiv_rn(__dmul_rn(totals[3], wt), total);
+        if (lam > 1.0e8) lam = 1.0e8;
+        const double cr = __dadd_rn(W.credit[c], lam);
+        const double fl = floor(cr);
+        bud = (int)fl;
+        W.credit[c] = __dsub_rn(cr, fl);
+      }
+      if (ctl & CTL_HS_MASK) W.ctl[c] = ctl & ~CTL_HS_MASK;   // the head start is used up
+      want = bud > 0;
+      if (want) cls = class_of(need_of_cell(W, (int)c));
     }
-    const unsigned long long m = __ballot(want);
-    if ((tid & 63) == 0 && m) count_add(W, CNT_SLICES, (unsigned long long)__popcll(m));
-    enqueue_class<16>(W, (int)c, want, cls);
+    W.budget[c] = bud;
+    W.aclass[c] = want ? (uint8_t)cls : (uint8_t)ACLASS_NONE;
+    occ_init_cell(W, c);
+    W.killt[c] = 0u;
+    W.claim_r[3][c] = 0ull;   // the previous update's round-3 claims (k_activate read them last)
   }
+  const unsigned long long m = __ballot(want);
+  if ((t & 63) == 0 && m) count_add(W, CNT_SLICES, (unsigned long long)__popcll(m));
+  enqueue_class<4>(W, (int)c, want, cls);
 }
 
 // the window's order from its bucket histogram (block of 1024 threads, two
@@ -626,6 +643,8 @@ __device__ __forceinline__ unsigned long long* halo_cl(uint8_t* b, int X, int p,
   return reinterpret_cast<unsigned long long*>(b) + (int64_t)(2 * p + k) * X;
 }
 __device__ __forceinline__ uint8_t* halo_occ(uint8_t* b, int X) { return b + (int64_t)X * 32; }
+// round 0's kill times of the sender's picks on the receiver's edge row
+__device__ __forceinline__ uint32_t* halo_kt(uint8_t* b, int X) { return reinterpret_cast<uint32_t*>(b + halo_kt_off(X)); }
 // which halo slot a cell maps to: d = direction, x = column, k = 0 for a
 // ghost cell (my claims on the neighbour's edge), 1 for an edge cell
 __device__ __forceinline__ bool halo_slot(const DevWorld& W, int64_t c, int& d, int& x, bool& ghost) {
@@ -662,16 +681,6 @@ __device__ __forceinline__ unsigned long long tile_merged(const DevWorld& W, int
   return v;
 }
 
-// claim / prev: this round's claim array and (single world) the previous
-// round's, whose entry at the record's last target is zeroed first -- the
-// rounds alternate between two arrays, so no clearing pass sits between them
-// occ_prev (fused single-world rounds, k_place_round): the previous round's
-// claim array -- a cell claimed there has a winner of that round, so it is
-// occupied for this round's pick whether or not that winner's resolve (in the
-// same launch) has marked occ yet; round: the claim's round (b_tgt row)
-// tile_m >= 0 (strip tiles, k_tile_round): occupancy by tile_taken, and a
-// claim on an edge or ghost cell also goes into the halo send slot of its
-// round's parity (atomicMax: the exchange after the launch carries it)
 // The rest of a deferred divide (interp.hip, BI_FINAL), in two halves that
 // run side by side in placement round 0's launch.  The offspring's RNG key
 // (derived from the parent's key and divide count) is the pick's, which draws
@@ -684,7 +693,7 @@ __device__ __forceinline__ unsigned long long tile_merged(const DevWorld& W, int
 // (a row is rewritten whole by its next divide): both halves test it.
 __device__ __forceinline__ void finalize_key(const DevWorld& W, int64_t r, int parent) {
   int32_t* row = W.b_inh + r * BI_WORDS;
-  if (row[BI_FINAL] == 0) return;
+  if ((row[BI_FINAL] & 1) == 0) return;
   uint32_t clo, chi;
   derive_key(W.rng[parent], W.rng[W.n + parent], W.b_seq[r], 0x1B873593U, clo, chi);
   row[BI_RLO] = (int32_t)clo;
@@ -694,7 +703,7 @@ __device__ __forceinline__ void finalize_phenotype(const DevWorld& W, int64_t r)
   int32_t* row = W.b_inh + r * BI_WORDS;
   const int4 q0 = reinterpret_cast<const int4*>(row)[0], q1 = reinterpret_cast<const int4*>(row)[1];
   const int fin = row[BI_FINAL];
-  if (fin == 0) return;
+  if ((fin & 1) == 0) return;
   const double merit = __hiloint2double(q0.y, q0.x);
   const int gt = q1.w;
   const double fit = __ddiv_rn(merit, (double)gt);
@@ -713,50 +722,92 @@ __device__ __forceinline__ void finalize_phenotype(const DevWorld& W, int64_t r)
   }
 }
 
-__device__ __forceinline__ void place_pick_one(const DevWorld& W, int64_t i, unsigned long long* claim,
-                                               unsigned long long* prev,
-                                               const unsigned long long* occ_prev = nullptr, int round = -1,
-                                               int tile_m = -1) {
-  const int64_t r = (round >= 0) ? i : rec_of(W, i);
-  if (prev) {
-    const int t0 = W.b_target[r];
-    if (t0 >= 0) prev[t0] = 0ull;
-  }
-  if (W.b_state[r] != 0) return;
+// ---- time-ordered placement (oracle/oracle.cc "3. Time-ordered placement";
+// DESIGN.md 5) ----
+// claim key: [63:48] time key (kill: t, empty: 0xFFFF - t), [47] kill,
+// [46:32] the pick's draw >> 17, [31:8] the parent's GLOBAL cell id (tiles
+// agree), [7:0] its divide number
+__device__ __forceinline__ unsigned long long claim_key(uint32_t t, bool kill, uint32_t draw, int64_t gparent,
+                                                        uint32_t seq) {
+  const unsigned long long tk = kill ? (unsigned long long)(t & 0xFFFFu) : (unsigned long long)(0xFFFFu - (t & 0xFFFFu));
+  return (tk << 48) | ((unsigned long long)(kill ? 1 : 0) << 47) | ((unsigned long long)(draw >> 17) << 32) |
+         ((unsigned long long)(gparent & 0xFFFFFF) << 8) | (unsigned long long)(seq & 0xFF);
+}
+__device__ __forceinline__ bool key_kill(unsigned long long k) { return ((k >> 47) & 1ull) != 0ull; }
+__device__ __forceinline__ uint32_t key_time(unsigned long long k) {
+  const uint32_t tk = (uint32_t)(k >> 48);
+  return key_kill(k) ? tk : 0xFFFFu - tk;
+}
+// record states (b_state)
+enum : int8_t { BS_PENDING = 0, BS_WON = 1 /* 1 + round */, BS_KILL_LOST = 8 /* 8 + round */,
+                BS_CANCELLED = -1, BS_NO_CELL = -2 /* - round: found no cell in that round */ };
+__device__ __forceinline__ uint32_t rec_time(const DevWorld& W, int64_t r) {
+  return BI_TIME(W.b_inh[r * BI_WORDS + BI_FINAL]);
+}
+__device__ __forceinline__ uint32_t owner_time(const DevWorld& W, int o) {
+  return o >= 0 ? rec_time(W, o) : (uint32_t)((-2 - o) >> 2);
+}
+// a round's winner with time t takes its cell unless the cell's owner from an
+// earlier round is later in time (that owner overwrote it)
+__device__ __forceinline__ bool takes_cell(const DevWorld& W, int owner, uint32_t t) {
+  return owner == -1 || owner_time(W, owner) <= t;
+}
+// the last round a record claimed in (-1: none) -- its claims are cleared at
+// activation (round k's at b_tgt[k])
+__device__ __forceinline__ int last_claim_round(int st) {
+  if (st == BS_PENDING) return 3;
+  if (st >= BS_WON && st < BS_WON + 4) return st - BS_WON;
+  if (st >= BS_KILL_LOST && st < BS_KILL_LOST + 4) return st - BS_KILL_LOST;
+  if (st <= BS_NO_CELL) return BS_NO_CELL - st - 1;
+  return -1;
+}
+
+// PositionOffspring for record r in round m (main/cPopulation.cc:5353-5413):
+// an empty neighbour (not taken) when PREFER_EMPTY, else any of the eight
+// neighbours or the parent (ALLOW_PARENT); BIRTH_METHOD 3 with no empty
+// neighbour: the parent's cell without a draw (:5407), placed only if
+// ALLOW_PARENT (ActivateOffspring :706-713), else never (BS_NO_CELL).  The
+// key records whether the target is taken (a kill).  taken(c): the round's
+// occupancy -- round 0 occ (tiles: the ghost rows' received occupancy), round
+// m > 0 also every cell claimed in round m - 1 (tile_m >= 0: here or by the
+// neighbour, tile_taken).  Returns false for no cell.
+__device__ __forceinline__ bool tile_taken(const DevWorld& W, int64_t c, int m);
+template <bool TILE>
+__device__ __forceinline__ bool place_pick_one(const DevWorld& W, int64_t r, int m) {
   const int parent = W.b_parent[r];
-  if (round <= 0) finalize_key(W, r, parent);   // round 0: the record's first draws
+  if (m == 0) finalize_key(W, r, parent);   // round 0: the record's first draws
+  const unsigned long long* prev = m > 0 ? W.claim_r[m - 1] : nullptr;
+  auto taken = [&](int c) -> bool {
+    if (TILE) return tile_taken(W, c, m);
+    return W.occ[c] != 0 || (prev && prev[c] != 0ull);
+  };
   int nbr[8];
   const int nn = neighbours(W, parent, nbr);
   int cand[9];
   int nc = 0;
   if (W.prefer_empty)
     for (int k = 0; k < nn; k++)
-      if (tile_m >= 0 ? !tile_taken(W, nbr[k], tile_m)
-                      : (!W.occ[nbr[k]] && !(occ_prev && occ_prev[nbr[k]] != 0ull))) cand[nc++] = nbr[k];
+      if (!taken(nbr[k])) cand[nc++] = nbr[k];
   if (nc == 0 && W.birth_method != 3) {
     for (int k = 0; k < nn; k++) cand[nc++] = nbr[k];
     if (W.allow_parent) cand[nc++] = parent;
   }
+  if (nc == 0 && !W.allow_parent) {
+    W.b_target[r] = -1;
+    W.b_state[r] = (int8_t)(BS_NO_CELL - m);
+    return false;
+  }
   int32_t* const inh = W.b_inh + (int64_t)r * BI_WORDS;
   const uint32_t lo = (uint32_t)inh[BI_RLO], hi = (uint32_t)inh[BI_RHI];
   uint32_t ctr = (uint32_t)inh[BI_RCTR];
-  // no candidate (BIRTH_METHOD 3 without an empty neighbour): PositionOffspring
-  // returns the parent's cell, drawing nothing (main/cPopulation.cc:5407)
   const int t = nc > 0 ? cand[rng_below(lo, hi, ctr, (uint32_t)nc)] : parent;
-  // priority: draw, then the parent's GLOBAL cell id, so that tiles agree
-  const unsigned long long prio = ((unsigned long long)rng_next(lo, hi, ctr) << 32) |
-                                  ((unsigned long long)((W.cell0 + parent) & 0xFFFFFF) << 8) |
-                                  (unsigned long long)(W.b_seq[r] & 0xFF);
+  const unsigned long long key = claim_key(BI_TIME(inh[BI_FINAL]), taken(t), rng_next(lo, hi, ctr),
+                                           W.cell0 + parent, W.b_seq[r]);
   inh[BI_RCTR] = (int32_t)ctr;
   W.b_target[r] = t;
-  W.b_prio[r] = prio;
-  if (round >= 0) W.b_tgt[(int64_t)round * W.rcap + r] = t;
-  atomicMax(&claim[t], prio);
-  if (tile_m >= 0) {
-    int d, x;
-    bool ghost;
-    if (halo_slot(W, t, d, x, ghost)) atomicMax(&halo_cl(W.h_send[d], W.world_x, tile_m & 1, ghost ? 0 : 1)[x], prio);
-  }
+  W.b_prio[r] = key;
+  W.b_tgt[(int64_t)m * W.rcap + r] = t;
+  return true;
 }
 
 // divide-mutation scan: queue entries per wave (k_place_pick_mut, k_tile_prep)
@@ -765,44 +816,60 @@ __device__ __forceinline__ void place_pick_one(const DevWorld& W, int64_t i, uns
 #define QUEUE_LOOP(i) \
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, _qn = queue_len(W); i < _qn; \
        i += (int64_t)gridDim.x * blockDim.x)
-// A single world's placement round m = 1..3 in one launch: the resolve of
-// round m-1 and the pick of round m.  Each round has its own claim array
-// (W.claim_r[m]), so round m-1's claims stay intact for the whole launch: a
-// record that won round m-1 takes its cell (occ, owner); one that lost picks
-// again, treating every cell claimed in round m-1 as occupied -- exactly the
-// occupancy the separate resolve launch would have left (every claimed cell
-// has a winner), so the result is the unfused pick / resolve pair's
-// (oracle run_update_impl) at half the launches.
+// A single world's placement launch m = 1..3: round m - 1 resolved and round m
+// picked (oracle run_update_impl).  Each round has its own claim array, so
+// round m - 1's claims stay intact for the whole launch: a record whose key is
+// the maximum won -- it occupies its cell and owns it unless the cell's owner
+// from an earlier round is later in time; a lost kill claim was placed and
+// overwritten by the later winner; a lost empty claim picks again, treating
+// every cell claimed in round m - 1 as taken (each has a winner).
 __global__ void k_place_round(DevWorld W, int m) {
   const unsigned long long* prev = W.claim_r[m - 1];
   unsigned long long* cur = W.claim_r[m];
   QUEUE_LOOP(q) {
     const int64_t r = rec_of(W, q);
-    if (W.b_state[r] != 0) continue;
+    if (W.b_state[r] != BS_PENDING) continue;
     const int t = W.b_target[r];
-    if (prev[t] == W.b_prio[r]) {              // won round m-1
-      W.b_state[r] = (int8_t)m;
+    const unsigned long long key = W.b_prio[r];
+    if (prev[t] == key) {                      // won round m-1
+      W.b_state[r] = (int8_t)(BS_WON + m - 1);
       W.occ[t] = 1;
-      W.owner[t] = (int)r;
+      if (takes_cell(W, W.owner[t], rec_time(W, r))) W.owner[t] = (int)r;
       continue;
     }
-    place_pick_one(W, r, cur, nullptr, prev, m);
+    if (key_kill(key)) { W.b_state[r] = (int8_t)(BS_KILL_LOST + m - 1); continue; }
+    if (place_pick_one<false>(W, r, m)) atomicMax(&cur[W.b_target[r]], W.b_prio[r]);
   }
 }
-// Round 0 of a single world's placement with the divide mutations beside it:
-// blocks [0, pblocks) pick; the rest apply the edits (a wave per 8 queue
-// entries, rewriting the ~10 % of genomes that have edits one after the other;
-// 4 waves per block) -- placement reads no genome, so the two are independent
-// and share one launch instead of two latency-bound ones.
-// fused: the single world's round arrays (claim rows and b_tgt, k_place_round)
-__global__ __launch_bounds__(256) void k_place_pick_mut(DevWorld W, unsigned long long* claim, int pblocks,
-                                                        int fused, int fblocks) {
+// Launch 0b of a single world: a record whose parent's cell was killed before
+// its own birth time (a round-0 pick of an earlier birth landed there:
+// killt[parent] > 2^16 - t) is cancelled -- the reference would have killed
+// its parent before this divide; the others claim their round-0 targets.
+__global__ void k_place_claim0(DevWorld W) {
+  QUEUE_LOOP(q) {
+    const int64_t r = rec_of(W, q);
+    if (W.b_state[r] != BS_PENDING) continue;
+    const int p = W.b_parent[r];
+    if (W.killt[p] > 0x10000u - rec_time(W, r)) { W.b_state[r] = BS_CANCELLED; continue; }
+    atomicMax(&W.claim_r[0][W.b_target[r]], W.b_prio[r]);
+  }
+}
+// Launch 0 of a single world's placement with the divide mutations beside it:
+// blocks [0, pblocks) pick round 0 (a pick whose target is occupied is a kill:
+// the cell's kill time, atomicMax of 2^16 - t); the next fblocks finalize the
+// deferred divides' phenotype; the rest apply the edits (a wave per 8 queue
+// entries, rewriting the ~10 % of genomes that have edits one after the
+// other; 4 waves per block) -- placement reads no genome, so they are
+// independent and share one launch instead of several latency-bound ones.
+__global__ __launch_bounds__(256) void k_place_pick_mut(DevWorld W, int pblocks, int fblocks) {
   __shared__ uint8_t child[4][TAPE_SLOT + 16];
   const int nb = queue_len(W);
   if ((int)blockIdx.x < pblocks) {
     for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < nb; i += (int64_t)pblocks * 256) {
-      if (fused) place_pick_one(W, rec_of(W, i), claim, nullptr, nullptr, 0);
-      else place_pick_one(W, i, claim, nullptr);
+      const int64_t r = rec_of(W, i);
+      if (!place_pick_one<false>(W, r, 0)) continue;
+      const unsigned long long key = W.b_prio[r];
+      if (key_kill(key)) atomicMax(&W.killt[W.b_target[r]], 0x10000u - key_time(key));
     }
     return;
   }
@@ -887,35 +954,65 @@ __global__ __launch_bounds__(256) void k_tile_prep(DevWorld W, int mblocks, int 
   halo_occ(b, X)[x] = W.occ[edge_cell(W, d, x)];
 #pragma unroll
   for (int k = 0; k < 4; k++) halo_cl(b, X, k >> 1, k & 1)[x] = 0ull;
+  halo_kt(b, X)[x] = 0u;
 }
 
-// Round m of a tile's placement, after round m - 1's exchange: blocks
-// [0, rblocks) take the records -- resolve round m - 1 against the merged
-// claims (a winner takes its cell), then a pending record picks for round m
-// (tile_taken: the occupancy that resolve leaves); the rest walk the halo
-// cells -- round 0 imports the ghost rows' occupancy, later rounds mark round
-// m - 1's remote winners on the edge rows (owner REMOTE_OWNER(m - 1)) and the
-// claimed ghost cells occupied, and clear the send parity of round m + 1
-// (its last contents, round m - 1's, went out before this launch).
-// m = 4: the last resolve only (records + halo cells), and the record
-// buffers' headers cleared for k_halo_pack.
+// Launch m of a tile's placement (oracle orc_tile_place / tile_launch), after
+// the previous exchange: blocks [0, rblocks) take the records, the rest walk
+// the 2 x X halo cells.
+// m = 0: round 0's picks with their kill times (own cells: killt; ghost
+//   cells: the halo's kill-time slots, read by the neighbour's launch 0b);
+//   the halo cells import the ghost rows' occupancy.
+// m = 1..3: round m - 1 resolved against the merged claims -- a halo cell
+//   whose maximum came from the neighbour (an edge cell: its claims on my edge
+//   row; a ghost cell: its own claims on its edge row) is that round's remote
+//   winner's (owner REMOTE_OWNER(m - 1, t), by the time rule) and occupied;
+//   a claimed ghost cell is occupied; a record that won takes its cell by the
+//   time rule, a lost kill claim was placed and overwritten, a lost empty
+//   claim picks round m (tile_taken: the occupancy that resolve leaves) --
+//   and the send parity of round m + 1 is cleared (its last contents, round
+//   m - 1's, went out before this launch).
+// m = 4: the last resolve only, and the record buffers' headers cleared for
+//   k_halo_pack.
 __global__ __launch_bounds__(256) void k_tile_round(DevWorld W, int m, int rblocks) {
   const int X = W.world_x;
   if ((int)blockIdx.x < rblocks) {
     const int nb = queue_len(W);
     for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < nb; q += (int64_t)rblocks * blockDim.x) {
       const int64_t r = rec_of(W, q);
-      if (W.b_state[r] != 0) continue;
-      if (m > 0) {
+      if (W.b_state[r] != BS_PENDING) continue;
+      if (m == 0) {
+        if (!place_pick_one<true>(W, r, 0)) continue;
+        const unsigned long long key = W.b_prio[r];
+        if (!key_kill(key)) continue;
         const int t = W.b_target[r];
-        if (tile_merged(W, t, m - 1) == W.b_prio[r]) {   // won round m - 1
-          W.b_state[r] = (int8_t)m;
-          W.occ[t] = 1;
-          W.owner[t] = (int)r;
-          continue;
+        const uint32_t kv = 0x10000u - key_time(key);
+        if (t >= W.n) {
+          const int64_t k = t - W.n;
+          const int d = (int)(k / X), x = (int)(k - (int64_t)d * X);
+          atomicMax(&halo_kt(W.h_send[d], X)[x], kv);
+        } else {
+          atomicMax(&W.killt[t], kv);
         }
+        continue;
       }
-      if (m < 4) place_pick_one(W, r, W.claim_r[m], nullptr, nullptr, m, m);
+      const int t = W.b_target[r];
+      const unsigned long long key = W.b_prio[r];
+      if (tile_merged(W, t, m - 1) == key) {   // won round m - 1
+        W.b_state[r] = (int8_t)(BS_WON + m - 1);
+        W.occ[t] = 1;
+        if (takes_cell(W, W.owner[t], rec_time(W, r))) W.owner[t] = (int)r;
+        continue;
+      }
+      if (key_kill(key)) { W.b_state[r] = (int8_t)(BS_KILL_LOST + m - 1); continue; }
+      if (m < 4 && place_pick_one<true>(W, r, m)) {
+        const int nt = W.b_target[r];
+        const unsigned long long nk = W.b_prio[r];
+        atomicMax(&W.claim_r[m][nt], nk);
+        int d, x;
+        bool ghost;
+        if (halo_slot(W, nt, d, x, ghost)) atomicMax(&halo_cl(W.h_send[d], X, m & 1, ghost ? 0 : 1)[x], nk);
+      }
     }
     return;
   }
@@ -935,79 +1032,110 @@ __global__ __launch_bounds__(256) void k_tile_round(DevWorld W, int m, int rbloc
   }
   const int p = (m - 1) & 1;
   const int64_t c = edge_cell(W, d, x);
-  const unsigned long long rc = halo_cl(W.h_recv[d], X, p, 0)[x];
-  if (rc != 0ull && rc > W.claim_r[m - 1][c]) { W.owner[c] = REMOTE_OWNER(m - 1); W.occ[c] = 1; }
-  if (W.claim_r[m - 1][gc] != 0ull || halo_cl(W.h_recv[d], X, p, 1)[x] != 0ull) W.occ[gc] = 1;
+  const unsigned long long rc = halo_cl(W.h_recv[d], X, p, 0)[x], rg = halo_cl(W.h_recv[d], X, p, 1)[x];
+  const unsigned long long lg = W.claim_r[m - 1][gc];
+  if (rc != 0ull && rc > W.claim_r[m - 1][c]) {
+    const uint32_t tr = key_time(rc);
+    if (takes_cell(W, W.owner[c], tr)) W.owner[c] = REMOTE_OWNER(m - 1, tr);
+    W.occ[c] = 1;
+  }
+  if (rg != 0ull && rg > lg) {
+    const uint32_t tr = key_time(rg);
+    if (takes_cell(W, W.owner[gc], tr)) W.owner[gc] = REMOTE_OWNER(m - 1, tr);
+  }
+  if (lg != 0ull || rg != 0ull) W.occ[gc] = 1;
   if (m == 1 || m == 2) {                      // round m + 1's send parity = round m - 1's
     uint8_t* b = W.h_send[d];
     halo_cl(b, X, p, 0)[x] = 0ull;
     halo_cl(b, X, p, 1)[x] = 0ull;
   }
 }
+// Launch 0b of a tile (after the kill times' exchange): a record whose
+// parent's cell was killed earlier -- by a pick here or, on an edge row, by
+// the neighbour's (the halo's kill-time slot) -- is cancelled; the others
+// claim their round-0 targets (and the halo send slots of parity 0).
+__global__ __launch_bounds__(256) void k_tile_claim0(DevWorld W) {
+  const int X = W.world_x;
+  QUEUE_LOOP(q) {
+    const int64_t r = rec_of(W, q);
+    if (W.b_state[r] != BS_PENDING) continue;
+    const int p = W.b_parent[r];
+    uint32_t kt = W.killt[p];
+    int d, x;
+    bool ghost;
+    if (halo_slot(W, p, d, x, ghost)) kt = max(kt, halo_kt(W.h_recv[d], X)[x]);
+    if (kt > 0x10000u - rec_time(W, r)) { W.b_state[r] = BS_CANCELLED; continue; }
+    const int t = W.b_target[r];
+    const unsigned long long key = W.b_prio[r];
+    atomicMax(&W.claim_r[0][t], key);
+    if (halo_slot(W, t, d, x, ghost)) atomicMax(&halo_cl(W.h_send[d], X, 0, ghost ? 0 : 1)[x], key);
+  }
+}
 
-// One lane per queued birth: the winners of cells inside the tile are
-// activated; winners of ghost-row cells were shipped by k_halo_pack.  The
-// record's fields are loaded before the ownership test (independent loads
-// in flight together instead of a chain behind it).
-// last: (single world) the claim array of the last placement round, zeroed
-// at each record's target for the next update
-//
-// Every queued offspring has a target by now: PositionOffspring always returns
-// a cell (main/cPopulation.cc:5382-5413).  A birth still pending after the
-// last placement round lost that round's claim on its target to a birth of
-// higher priority; the reference would have placed both, one after the other,
-// and the later one (here: the higher priority, the cell's owner) kills the
-// earlier newborn.  So a birth either owns its cell at the update's end
-// (CNT_BIRTHS) or was placed and overwritten (CNT_OVERWRITTEN) -- never
-// "not placed".
-//
-// fused (single world, k_place_round): the resolve of round 3 happens here --
-// a record that won round 3 owns its cell; one that won an earlier round owns
-// it unless a round-3 claim landed there (claim_r[3] != 0: that claim's winner
-// is placed later and owns it).  Rounds 0-2's claims are cleared here by each
-// record; round 3's, which this launch reads, by k_stats_partial.
-// fused 2 (strip tiles, k_tile_round): the owners are final (round 3 was
-// resolved before the halo records were packed), the claims are cleared as
-// in the fused single world
-__global__ __launch_bounds__(64) void k_activate(DevWorld W, unsigned long long* last, int fused) {
+// One lane per queued birth: the owners of cells inside this world are
+// activated (ActivateOrganism + SetupOffspring; owners of ghost-row cells were
+// shipped by k_halo_pack), with the head start 2^16 - t for their first
+// allotment.  The record's fields are loaded before the ownership test
+// (independent loads in flight together instead of a chain behind it).
+// fused 1 (single world): round 3 is resolved here -- a round-3 winner owns
+// its cell unless the owner from an earlier round is later in time; an
+// earlier round's owner keeps it unless a round-3 winner (necessarily a
+// kill claim: the cell was taken) is not earlier than it.  fused 2 (strip
+// tiles): the owners are final (k_tile_round resolved round 3).  Either way
+// each record clears the claims it made (round 3's, which this launch reads,
+// are cleared by k_allot).  A record that does not own its cell was placed
+// and overwritten (CNT_OVERWRITTEN), unless it was cancelled
+// (CNT_CANCELLED: its parent died first) or found no cell (CNT_DROPPED).
+__global__ __launch_bounds__(64) void k_activate(DevWorld W, int fused) {
   const int nb = queue_len(W);
-  unsigned long long born = 0, over = 0;
+  const int64_t ncell = W.n + (W.tiled ? 2 * (int64_t)W.world_x : 0);
+  unsigned long long born = 0, over = 0, canc = 0, nocell = 0, bad = 0;
   for (int64_t q = (int64_t)blockIdx.x * 64 + threadIdx.x; q < nb; q += (int64_t)gridDim.x * 64) {
     const int64_t i = rec_of(W, q);
     const int tgt = W.b_target[i];
     const int8_t st = W.b_state[i];
     const Child b = child_of_record(W, i);
-    if (last && tgt >= 0) last[tgt] = 0ull;
-    bool won;
-    if (fused) {
-      if (fused == 2) {
-        won = st > 0 && tgt >= 0 && W.owner[tgt] == (int)i;
-      } else {
-        const unsigned long long c3 = tgt >= 0 ? W.claim_r[3][tgt] : 0ull;
-        if (st == 0) won = tgt >= 0 && c3 == W.b_prio[i];   // round 3's winner
-        else won = W.owner[tgt] == (int)i && c3 == 0ull;
-      }
-      const int lastr = (st == 0 || st > 4) ? 3 : st - 1;  // the last round it claimed in
-      for (int k = 0; k < lastr && k < 3; k++) {
-        const int tk = W.b_tgt[(int64_t)k * W.rcap + i];
-        if (tk >= 0) W.claim_r[k][tk] = 0ull;
-      }
-      if (lastr < 3) W.claim_r[lastr][tgt] = 0ull;
-    } else {
-      won = st > 0 && tgt >= 0 && W.owner[tgt] == (int)i;
+    const int lastr = last_claim_round(st);
+    // the record's claims, round k's at b_tgt[k] (the last one its target);
+    // a target out of range is a corrupt record: counted, never written
+    bool ok = true;
+    for (int k = 0; k <= lastr && k < 3; k++) {
+      const int tk = (k == lastr && tgt >= 0) ? tgt : W.b_tgt[(int64_t)k * W.rcap + i];
+      if (tk >= 0 && (int64_t)tk < ncell) W.claim_r[k][tk] = 0ull;
+      else ok = false;
+    }
+    if (st == BS_CANCELLED) { canc++; continue; }
+    if (st <= BS_NO_CELL) { nocell++; continue; }
+    if (!ok || tgt < 0 || (int64_t)tgt >= ncell) { bad++; continue; }
+    const uint32_t t = 0x10000u - b.hs;
+    bool won = false;
+    if (fused == 2) {
+      won = st >= BS_WON && st < BS_WON + 4 && W.owner[tgt] == (int)i;
+    } else if (st == BS_PENDING) {
+      won = W.claim_r[3][tgt] == W.b_prio[i] && takes_cell(W, W.owner[tgt], t);
+    } else if (st >= BS_WON && st < BS_WON + 4) {
+      const unsigned long long c3 = W.claim_r[3][tgt];
+      won = W.owner[tgt] == (int)i && !(c3 != 0ull && key_time(c3) >= t);
     }
     if (won && tgt >= W.n) continue;          // sent to the neighbouring tile
     if (!won) { over++; continue; }
+    if (b.len < 0 || b.len > AVGPU_MAX_GENOME) { bad++; continue; }
     born++;
     setup_child_lane(W, tgt, b, W.b_genome + i * TAPE_SLOT);
   }
   for (int off = 32; off > 0; off >>= 1) {
     born += __shfl_xor(born, off);
     over += __shfl_xor(over, off);
+    canc += __shfl_xor(canc, off);
+    nocell += __shfl_xor(nocell, off);
+    bad += __shfl_xor(bad, off);
   }
   if (threadIdx.x == 0) {
     if (born) count_add(W, CNT_BIRTHS, born);
     if (over) count_add(W, CNT_OVERWRITTEN, over);
+    if (canc) count_add(W, CNT_CANCELLED, canc);
+    if (nocell) count_add(W, CNT_DROPPED, nocell);
+    if (bad) count_add(W, CNT_BAD_RECORD, bad);
   }
 }
 
@@ -1027,7 +1155,8 @@ __global__ __launch_bounds__(64) void k_halo_pack(DevWorld W) {
     if (q < nb) {
       const int64_t i = rec_of(W, q);
       const int tgt = W.b_target[i];
-      if (W.b_state[i] > 0 && tgt >= W.n && W.owner[tgt] == (int)i) mine = i;
+      const int8_t st = W.b_state[i];
+      if (st >= BS_WON && st < BS_WON + 4 && tgt >= W.n && W.owner[tgt] == (int)i) mine = i;
     }
     for (unsigned long long m = __ballot(mine >= 0); m; m &= m - 1ull) {
     const int64_t i = (int64_t)__shfl((long long)mine, __ffsll((long long)m) - 1);
@@ -1047,11 +1176,11 @@ __global__ __launch_bounds__(64) void k_halo_pack(DevWorld W) {
     const bool fits = (int64_t)off + len <= W.r_arena;
     if (lane == 0) {
       HaloRec r;
-      r.col = col; r.round = W.b_state[i] - 1; r.len = fits ? len : -1;
+      r.col = col; r.round = W.b_state[i] - BS_WON; r.len = fits ? len : -1;
       const Child b = child_of_record(W, i);
       r.gen = b.gen; r.ccopied = b.ccopied; r.exec = b.exec; r.gest = b.gest;
       r.rng_lo = b.lo; r.rng_hi = b.hi; r.rng_ctr = b.ctr;
-      r.off = off; r.pad = 0; r.merit = b.merit; r.fitness = b.fitness;
+      r.off = off; r.t = 0x10000u - b.hs; r.merit = b.merit; r.fitness = b.fitness;
 #pragma unroll
       for (int t = 0; t < AVGPU_NUM_LOGIC_TASKS; t++) r.last_task[t] = b.ltask[t];
       r.pad2[0] = r.pad2[1] = r.pad2[2] = 0;
@@ -1092,10 +1221,11 @@ __global__ __launch_bounds__(64) void k_activate_remote(DevWorld W) {
     const HaloRec r = recs[q];
     if (r.len < 0) continue;                  // lost at the sender (counted there)
     const int64_t c = edge_cell(W, d, r.col);
-    if (W.owner[c] != REMOTE_OWNER(r.round)) { lost++; continue; }   // overwritten by a later winner
+    if (W.owner[c] != REMOTE_OWNER(r.round, r.t)) { lost++; continue; }   // overwritten by a later winner
     born++;
     Child b;
     b.len = r.len; b.gen = r.gen; b.ccopied = r.ccopied; b.exec = r.exec; b.gest = r.gest;
+    b.hs = 0x10000u - r.t;
     b.merit = r.merit; b.fitness = r.fitness; b.lo = r.rng_lo; b.hi = r.rng_hi; b.ctr = r.rng_ctr;
     b.ltask = recs[q].last_task; b.lstride = 1;
     setup_child<64>(W, c, b, reinterpret_cast<const uint32_t*>(arena + r.off), lane);
@@ -1237,6 +1367,7 @@ __global__ __launch_bounds__(256) void k_stats_final(DevWorld W, const double* p
     out[32] = (double)cs[0][CNT_SLICES];
     out[33] = (double)cs[0][CNT_LANESTEPS];
     out[34] = (double)cs[0][CNT_OVERWRITTEN];
+    out[35] = (double)cs[0][CNT_CANCELLED];
   }
 }
 
@@ -1280,23 +1411,42 @@ void launch_classify_uniform(const DevWorld& W, hipStream_t s, int64_t first, in
                      budget, uniform);
 }
 
-// totals: [0] sum merit, [1] organisms (deterministic order; DESIGN.md "Scheduler").
+static int tree_levels(int64_t nbt) {
+  int L = 0;
+  while (((int64_t)1 << L) < nbt) L++;
+  return L;
+}
+
+// totals: [0] total weight, [1] organisms (mode 3 of k_block_counts).
 // scratch: (n+255)/256 doubles + as many int32 partials
 void launch_merit_total(const DevWorld& W, hipStream_t s, double* totals, double* scratch) {
   const int64_t nb = (W.n + 255) / 256;
   int32_t* alive_partial = reinterpret_cast<int32_t*>(scratch + nb);
   hipLaunchKernelGGL(k_merit_partial, dim3((unsigned)((nb + 3) / 4)), dim3(256), 0, s, W, scratch, alive_partial,
                      (double*)nullptr, 0);
-  hipLaunchKernelGGL(k_merit_final<false>, dim3(1), dim3(256), 0, s, scratch, alive_partial,
-                     (const double*)nullptr, nb, 1, totals, 0);
+  hipLaunchKernelGGL(k_block_counts, dim3(1), dim3(1024), 0, s, W, (const double*)scratch,
+                     (const int32_t*)alive_partial, nb, 1, tree_levels(nb), totals, 0u, 3);
 }
 
 // the update's counters, birth-queue and class-list lengths, zeroed by one
 // launch instead of three fill packets (~10 us each on the queue)
 __global__ __launch_bounds__(256) void k_reset_counts(DevWorld W) { reset_counts_block(W); }
 
-// single world: total merit, allotment, class lists and class-0 order in
-// three launches (k_merit_partial also zeroes the update's counters)
+// the allotment of a world whose block counts are in W.blk_count: budgets,
+// class lists, occupancy; then the class-0 order
+static void launch_allot(const DevWorld& W, hipStream_t s, const double* totals, hipEvent_t lists_ready,
+                         uint32_t update) {
+  hipLaunchKernelGGL(k_allot, dim3(nblk(W.n, 256)), dim3(256), 0, s, W, totals, update);
+  // the class lists are complete: the aux streams of the list classes start
+  // here, beside the window sort, so that their blocks take CUs before class 0
+  // (with the sort folded into the allotment they start together with class 0
+  // and end ~35 us after it: profiles/r02q_tail_per_update.txt)
+  hipEventRecord(lists_ready, s);
+  hipLaunchKernelGGL(k_window_count, dim3(nblk(W.n, SORT_WIN)), dim3(1024), 0, s, W);
+}
+
+// single world: block partials (k_merit_partial also zeroes the update's
+// counters), the scheduler's top tree, the allotment, the class-0 order
 void launch_world_begin(const DevWorld& W, hipStream_t s, double* totals, double* scratch,
                         hipEvent_t lists_ready, uint32_t update) {
   const int64_t nb = (W.n + 255) / 256;
@@ -1304,28 +1454,36 @@ void launch_world_begin(const DevWorld& W, hipStream_t s, double* totals, double
   launch_resources_begin(W, s);   // ProcessPreUpdate + the update's first DoUpdates
   hipLaunchKernelGGL(k_merit_partial, dim3((unsigned)((nb + 3) / 4)), dim3(256), 0, s, W, scratch, alive_partial,
                      (double*)nullptr, 1);
-  hipLaunchKernelGGL(k_allot_total, dim3(nblk(W.n, 2048)), dim3(1024), 0, s, W, (const double*)scratch,
-                     (const int32_t*)alive_partial, nb, totals, update);
-  // the class lists are complete: the aux streams of the list classes start
-  // here, beside the window sort, so that their blocks take CUs before class 0
-  // (with the sort folded into k_allot_total they start together with class 0
-  // and end ~35 us after it: profiles/r02q_tail_per_update.txt)
-  hipEventRecord(lists_ready, s);
-  hipLaunchKernelGGL(k_window_count, dim3(nblk(W.n, SORT_WIN)), dim3(1024), 0, s, W);
+  hipLaunchKernelGGL(k_block_counts, dim3(1), dim3(1024), 0, s, W, (const double*)scratch,
+                     (const int32_t*)alive_partial, nb, 1, tree_levels(nb), totals, update, 0);
+  launch_allot(W, s, totals, lists_ready, update);
 }
 
-// reset: clear the update's counters here (a strip tile's k_merit_partial in
-// avgpu_tile_partials already did)
-void launch_world_pre(const DevWorld& W, hipStream_t s, const double* totals, hipEvent_t lists_ready,
+// a world whose totals were handed in (avgpu_update_totals + an all-reduce of
+// every world's {total weight, organisms}, in totals[0..1]): its block
+// partials, then this world's picks by cMultiProcessWorld's formula
+// (k_block_counts mode 2).  reset: clear the update's counters here.
+void launch_world_pre(const DevWorld& W, hipStream_t s, double* totals, double* scratch, hipEvent_t lists_ready,
                       uint32_t update, bool reset) {
+  const int64_t nb = (W.n + 255) / 256;
+  int32_t* alive_partial = reinterpret_cast<int32_t*>(scratch + nb);
   launch_resources_begin(W, s);   // ProcessPreUpdate + the update's first DoUpdates
-  if (reset) hipLaunchKernelGGL(k_reset_counts, dim3(1), dim3(256), 0, s, W);
-  hipLaunchKernelGGL(k_allot_total, dim3(nblk(W.n, 2048)), dim3(1024), 0, s, W, (const double*)nullptr,
-                     (const int32_t*)nullptr, (int64_t)0, const_cast<double*>(totals), update);
-  // the class lists are complete: the aux streams of the list classes start
-  // here, beside the window sort (launch_interpret_classes)
-  hipEventRecord(lists_ready, s);
-  hipLaunchKernelGGL(k_window_count, dim3(nblk(W.n, SORT_WIN)), dim3(1024), 0, s, W);
+  hipLaunchKernelGGL(k_merit_partial, dim3((unsigned)((nb + 3) / 4)), dim3(256), 0, s, W, scratch, alive_partial,
+                     (double*)nullptr, reset ? 1 : 0);
+  hipLaunchKernelGGL(k_block_counts, dim3(1), dim3(1024), 0, s, W, (const double*)scratch,
+                     (const int32_t*)alive_partial, nb, 1, tree_levels(nb), totals, update, 2);
+  launch_allot(W, s, totals, lists_ready, update);
+}
+
+// a strip tile: the top tree over every strip's gathered partials (mode 1),
+// then the allotment (its partials' launch cleared the counters)
+void launch_tile_pre(const DevWorld& W, hipStream_t s, const double* gathered, int ntiles, double* totals,
+                     hipEvent_t lists_ready, uint32_t update) {
+  const int64_t nb = (W.n + 255) / 256;
+  launch_resources_begin(W, s);
+  hipLaunchKernelGGL(k_block_counts, dim3(1), dim3(1024), 0, s, W, gathered, (const int32_t*)nullptr, nb, ntiles,
+                     tree_levels(nb * ntiles), totals, update, 1);
+  launch_allot(W, s, totals, lists_ready, update);
 }
 
 void launch_stats(const DevWorld& W, hipStream_t s, double* stats) {
@@ -1376,9 +1534,10 @@ void launch_world_post(const DevWorld& W, hipStream_t s, double* stats, bool eag
   const unsigned bb = place_grid(W);
   const int pm = has_divide_mutations(W) ? (int)((mut_grid(W) + 3) / 4) : 0;
   const int pf = (int)std::min<unsigned>(bb, 256u);   // finalize_phenotype blocks
-  hipLaunchKernelGGL(k_place_pick_mut, dim3(bb + pf + pm), dim3(256), 0, s, W, W.claim_r[0], (int)bb, 1, pf);
+  hipLaunchKernelGGL(k_place_pick_mut, dim3(bb + pf + pm), dim3(256), 0, s, W, (int)bb, pf);
+  hipLaunchKernelGGL(k_place_claim0, dim3(bb), dim3(256), 0, s, W);
   for (int m = 1; m < 4; m++) hipLaunchKernelGGL(k_place_round, dim3(bb), dim3(256), 0, s, W, m);
-  hipLaunchKernelGGL(k_activate, dim3(lane_grid(W)), dim3(64), 0, s, W, (unsigned long long*)nullptr, 1);
+  hipLaunchKernelGGL(k_activate, dim3(lane_grid(W)), dim3(64), 0, s, W, 1);
   if (eager) launch_stats(W, s, stats);
 }
 
@@ -1390,13 +1549,6 @@ void launch_tile_partials(const DevWorld& W, hipStream_t s, double* out) {
                      out + nb, W.tiled ? 1 : 0);
 }
 
-void launch_tile_totals(const DevWorld& W, hipStream_t s, const double* gathered, int ntiles,
-                        double* totals) {
-  const int64_t nb = (W.n + 255) / 256;
-  hipLaunchKernelGGL(k_merit_final<true>, dim3(1), dim3(256), 0, s, (const double*)nullptr,
-                     (const int32_t*)nullptr, gathered, nb, ntiles, totals, 0);
-}
-
 // after interpretation: the divide mutations, the ghost rows emptied and the
 // edge-row occupancy out (one launch, k_tile_prep)
 void launch_tile_after_interpret(const DevWorld& W, hipStream_t s) {
@@ -1406,7 +1558,9 @@ void launch_tile_after_interpret(const DevWorld& W, hipStream_t s) {
   hipLaunchKernelGGL(k_tile_prep, dim3(mb + fb + hb), dim3(256), 0, s, W, mb, fb);
 }
 
-// phase 0: round `round` (k_tile_round: resolve round - 1, pick round)
+// phase 0: round 0's picks and kill times, or (round 1..3) k_tile_round:
+//          resolve round - 1, pick round
+// phase 3: (round 0) the cancellations and round 0's claims (k_tile_claim0)
 // phase 1: (round 3) the last resolve, then the ghost-row winners packed into
 //          the record buffers
 // phase 2: (round 3) this tile's own winners activated -- while the records
@@ -1416,11 +1570,13 @@ void launch_tile_place(const DevWorld& W, hipStream_t s, int round, int phase) {
   const unsigned hb = nblk(2 * (int64_t)W.world_x, 256);
   if (phase == 0) {
     hipLaunchKernelGGL(k_tile_round, dim3(bb + hb), dim3(256), 0, s, W, round, (int)bb);
+  } else if (phase == 3) {
+    hipLaunchKernelGGL(k_tile_claim0, dim3(bb), dim3(256), 0, s, W);
   } else if (phase == 1) {
     hipLaunchKernelGGL(k_tile_round, dim3(bb + hb), dim3(256), 0, s, W, 4, (int)bb);
     hipLaunchKernelGGL(k_halo_pack, dim3(lane_grid(W)), dim3(64), 0, s, W);
   } else {
-    hipLaunchKernelGGL(k_activate, dim3(lane_grid(W)), dim3(64), 0, s, W, (unsigned long long*)nullptr, 2);
+    hipLaunchKernelGGL(k_activate, dim3(lane_grid(W)), dim3(64), 0, s, W, 2);
   }
 }
 

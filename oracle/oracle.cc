@@ -1277,7 +1277,7 @@ static void block_split(const World& w, int64_t b, int64_t n, int32_t* budget) {
     }
   for (int t = 0; t < 256; t++) {
     const int64_t c = b * 256 + t;
-    if (c < w.ncells) budget[c] = (int32_t)cnt[t];
+    if (c < w.ncells) budget[c] = (int32_t)std::min<int64_t>(cnt[t], (1 << 30) - 1);   // the device's budget range
   }
 }
 
@@ -2075,7 +2075,7 @@ static inline uint32_t key_time(uint64_t k) {
 }
 // record states (Birth index i -> bstate[i])
 enum : int8_t { BS_PENDING = 0, BS_WON = 1 /* 1 + round */, BS_KILL_LOST = 8 /* 8 + round */,
-                BS_CANCELLED = -1, BS_NO_CELL = -2 };
+                BS_CANCELLED = -1, BS_NO_CELL = -2 /* - round */ };
 // owner: >= 0 a record of this world, -1 none, <= -2 a neighbouring strip's
 // offspring that won round m at time t (strip tiles)
 static inline int64_t remote_owner(int m, uint32_t t) { return -2 - ((int64_t)m + 4 * (int64_t)t); }
@@ -2109,7 +2109,7 @@ static bool place_pick(World& w, int64_t i, int m, Taken taken) {
     for (int k = 0; k < nn; k++) cand[nc++] = nb[k];
     if (w.cfg.allow_parent) cand[nc++] = b.parent;
   }
-  if (nc == 0 && !w.cfg.allow_parent) { b.target = -1; w.bstate[i] = BS_NO_CELL; return false; }
+  if (nc == 0 && !w.cfg.allow_parent) { b.target = -1; w.bstate[i] = (int8_t)(BS_NO_CELL - m); return false; }
   b.target = nc > 0 ? cand[b.rng.uint_below((uint32_t)nc)] : b.parent;
   w.prio[i] = claim_key(b.t, taken(b.target), b.rng.next(), w.cell0 + b.parent, b.seq);
   w.tgt_r[m][i] = b.target;
@@ -2152,7 +2152,7 @@ static void place_finish_single(World& w) {
     }
     if (own) { activate_child(w, b, b.target); w.orgs[b.target].hstart = 0x10000u - b.t; placed++; }
     else if (st == BS_CANCELLED) cancelled++;
-    else if (st == BS_NO_CELL) dropped++;
+    else if (st <= BS_NO_CELL) dropped++;
     else overwritten++;
   }
   w.t_overwritten = overwritten;
@@ -2530,7 +2530,7 @@ int orc_tile_place(void* h, int round, int phase) {
       if (won && b.target >= w.ncells) continue;   // shipped to the neighbour
       if (won) { activate_child(w, b, b.target); w.orgs[b.target].hstart = 0x10000u - b.t; placed++; }
       else if (st == BS_CANCELLED) cancelled++;
-      else if (st == BS_NO_CELL) nocell++;
+      else if (st <= BS_NO_CELL) nocell++;
       else overwritten++;                          // placed, then overwritten (run_update_impl)
     }
     w.t_placed = placed;

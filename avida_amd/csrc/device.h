@@ -573,16 +573,6 @@ __device__ __forceinline__ double det_exp2(double x) {
   return ldexp(y, (int)n);
 }
 
-// square root from IEEE adds / multiplies / divisions (oracle det_sqrt): the
-// exponent halved exactly, then 6 Newton steps
-__device__ __forceinline__ double det_sqrt(double x) {
-  if (!(x > 0.0)) return 0.0;
-  int e;
-  const double m = frexp(x, &e);
-  double y = ldexp(__dadd_rn(m, 0.5), e / 2 - ((e & 1) && e < 0 ? 1 : 0));
-  for (int k = 0; k < 6; k++) y = __dmul_rn(0.5, __dadd_rn(y, __ddiv_rn(x, y)));
-  return y;
-}
 __device__ __forceinline__ double pow_int(double q, int64_t n) {
   double r = 1.0, b = q;
   while (n) { if (n & 1) r = __dmul_rn(r, b); b = __dmul_rn(b, b); n >>= 1; }
@@ -617,7 +607,7 @@ __device__ __forceinline__ int64_t binom_draw(int64_t n, double p, uint32_t h) {
       sum = __dadd_rn(__dadd_rn(sum, (double)(x & 0xFFFFu)), (double)(x >> 16));
     }
     const double z = __dsub_rn(__dmul_rn(__dadd_rn(sum, 6.0), 1.52587890625e-05), 6.0);
-    const double sd = det_sqrt(__dmul_rn(mean, q));
+    const double sd = __dsqrt_rn(__dmul_rn(mean, q));   // IEEE, correctly rounded (oracle std::sqrt)
     const double skew = __ddiv_rn(__dmul_rn(__dsub_rn(q, pp), __dsub_rn(__dmul_rn(z, z), 1.0)), 6.0);
     const double v = __dadd_rn(__dadd_rn(__dadd_rn(mean, __dmul_rn(sd, z)), skew), 0.5);
     k = v < 1.0 ? 0 : (int64_t)floor(v);
@@ -705,7 +695,7 @@ void launch_interpret_classes(const DevWorld& W, const DevWorld* dW, int mode, h
                               hipEvent_t* ev_join = nullptr);
 // class-0 windows: k_allot's budgets sorted (descending) inside windows of
 // SORT_WIN cells, so that a wave's 64 organisms get similar time slices
-#define SORT_WIN 2048
+#define SORT_WIN 8192
 // k_allot_sort's buckets: budgets 0 .. SORT_BUCKETS-3 (larger ones share the
 // last of them), then one bucket for the window's cells that are not class 0
 #define SORT_BUCKETS 258

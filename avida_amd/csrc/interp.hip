@@ -1539,10 +1539,7 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
           // keeps the reference's order.  Insertions: all sites drawn
           // (GetUInt(size + 1)), sorted, inserted from the highest down with
           // a GetRandomInst each, capped at the largest genome; deletions capped
-          // at the smallest; new sites have flags 0 (cleared below anyway).  A
-          // parent that would outgrow this size class's slot keeps the
-          // insertions that fit (counted in CNT_MEM_CAP; the oracle has no
-          // slot, tests require 0).
+          // at the smallest; new sites have flags 0 (cleared below anyway).
           if (!DEF && mode != AVGPU_MODE_TEST && lane == L && (W.th_par_site || W.th_par_ins || W.th_par_del)) {
             int g_max = W.max_genome, g_min = W.min_genome;
             if (W.th_par_site) {
@@ -1557,33 +1554,31 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
               int nins = 0;
               for (int i = 0; i < M; i++) nins += draw_p(W.th_par_ins, W.p_par_ins) ? 1 : 0;
               if (nins + M > g_max) nins = g_max - M;
+              // the sorted sites sit in the last 4 * nins bytes of the slot
+              // and the parent grows below them: M + 5 * nins <= S.  A parent
+              // near its slot's end keeps the insertions that fit (the rest
+              // counted in CNT_MEM_CAP; the oracle has no slot, tests require 0)
+              const int nfit = (S - M) / 5;
+              if (nins > nfit) {
+                count_add(W, CNT_MEM_CAP, (unsigned long long)(nins - nfit));
+                nins = nfit;
+              }
               if (nins > 0) {
-                // the sites, sorted, in the last 4 * nins bytes of the slot
-                // (the child's copy-out has read them; the growing parent
-                // stays below them: room)
+                // (the child's copy-out has read those bytes)
                 int32_t* srt = reinterpret_cast<int32_t*>(T + S - 4 * nins);
-                const bool room = (int64_t)M + 5 * (int64_t)nins <= (int64_t)S;
                 for (int i = 0; i < nins; i++) {
                   const int site = (int)draw_below((uint32_t)M + 1u);
-                  if (room) {
-                    int j = i;
-                    while (j > 0 && srt[j - 1] > site) { srt[j] = srt[j - 1]; j--; }
-                    srt[j] = site;
-                  }
+                  int j = i;
+                  while (j > 0 && srt[j - 1] > site) { srt[j] = srt[j - 1]; j--; }
+                  srt[j] = site;
                 }
-                int ncap = room ? 0 : nins;
-                if (room) {
-                  for (int i = nins - 1; i >= 0; i--) {
-                    const int pos = srt[i];
-                    const int code = rand_code();
-                    for (int k = M; k > pos; k--) T[k] = T[k - 1];
-                    T[pos] = (uint8_t)code;
-                    M++;
-                  }
-                } else {
-                  for (int i = 0; i < nins; i++) (void)rand_code();
+                for (int i = nins - 1; i >= 0; i--) {
+                  const int pos = srt[i];
+                  const int code = rand_code();
+                  for (int k = M; k > pos; k--) T[k] = T[k - 1];
+                  T[pos] = (uint8_t)code;
+                  M++;
                 }
-                if (ncap) count_add(W, CNT_MEM_CAP, (unsigned long long)ncap);
               }
             }
             if (W.th_par_del) {

@@ -423,14 +423,17 @@ __global__ __launch_bounds__(1024) void k_block_counts(DevWorld W, const double*
   }
   s_cnt[tid] = a;
   __syncthreads();
+  for (int st = 512; st >= 1; st >>= 1) {      // living organisms (integer: any order)
+    if (tid < st) s_cnt[tid] += s_cnt[tid + st];
+    __syncthreads();
+  }
   for (int l = L - 1; l >= 0; l--) {
     const int64_t w0 = (int64_t)1 << l;
     for (int64_t i = tid; i < w0; i += 1024) scr[w0 + i] = __dadd_rn(scr[2 * (w0 + i)], scr[2 * (w0 + i) + 1]);
     __syncthreads();
   }
   if (tid == 0) {
-    long long n = 0;
-    for (int i = 0; i < 1024; i++) n += s_cnt[i];
+    const long long n = s_cnt[0];
     const double root = scr[1];
     const double ave = (double)W.ave_time_slice;
     long long nroot = (long long)W.ave_time_slice * n;
@@ -472,10 +475,13 @@ __device__ __forceinline__ void occ_init_cell(const DevWorld& W, int64_t c) {
   W.owner[c] = -1;
 }
 
-// k_allot: one 256-cell block per workgroup.  The block's stride tree over its
-// cells' weights (levels in LDS: level k of 2^k nodes at offset 2^k - 1, node
-// (k, t) = the cells = t mod 2^k, the additions of k_merit_partial), then its
-// count blk_count[b] split top down to the cells (PROBABILISTIC);
+// k_allot: one wave per 256-cell block, four blocks per workgroup.  Lane l
+// holds cells l, l + 64, l + 128, l + 192.  The block's stride tree over its
+// cells' weights (node (k, t) = the cells = t mod 2^k, the additions of
+// k_merit_partial): levels 7 and 6 in the lane, levels 5..0 by shuffles; then
+// its count blk_count[b] split top down (PROBABILISTIC): levels 0..5 across
+// the lanes (lane t holds node (k, t), the right child's count goes to lane
+// t + 2^k by shuffle), levels 6 and 7 in the lane -- no barrier, no LDS.
 // INTEGRATED: lambda = UD * weight / total with a credit carry; CONSTANT (or
 // no weight at all): AVE_TIME_SLICE.  Each cell's head start is consumed here.
 // Also the cell's budget and class tag, the placement occupancy of this
@@ -483,81 +489,106 @@ __device__ __forceinline__ void occ_init_cell(const DevWorld& W, int64_t c) {
 // its cell at write-back), its kill time, the previous update's round-3
 // claim, and the class lists.
 __global__ __launch_bounds__(256) void k_allot(DevWorld W, const double* totals, uint32_t update) {
-  __shared__ double lv[511];
-  __shared__ long long cn[256];
-  const int t = threadIdx.x;
-  const int64_t b = blockIdx.x;
-  const int64_t c = b * 256 + t;
-  const bool in = c < W.n;
-  const uint32_t ctl = in ? W.ctl[c] : 0u;
-  const bool alive = (ctl & CTL_ALIVE) != 0;
-  double merit = alive ? W.merit[c] : 0.0;
-  if (alive && !(merit >= 0.0 && merit < 1.0e300)) {   // a corrupt merit is counted, not scheduled
-    count_add(W, CNT_BAD_RECORD, 1ull);
-    merit = 0.0;
-  }
-  const double wt = alive ? sched_weight(merit, ctl) : 0.0;
+  const int lane = threadIdx.x & 63;
+  const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t nb = (W.n + 255) / 256;
   const double total = totals[2];
   const bool consts = W.slicing == AVGPU_SLICE_CONSTANT || !(total > 0.0);
   const bool prob = !consts && W.slicing != AVGPU_SLICE_INTEGRATED;
-  if (prob) {                                  // block-uniform
-    lv[255 + t] = wt;
-    __syncthreads();
-    for (int k = 7; k >= 0; k--) {
-      const int o = (1 << k) - 1, oc = (2 << k) - 1;
-      if (t < (1 << k)) lv[o + t] = __dadd_rn(lv[oc + t], lv[oc + t + (1 << k)]);
-      __syncthreads();
+  uint32_t ctl[4];
+  double wt[4];
+  bool alive[4];
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    const int64_t c = b * 256 + lane + 64 * j;
+    ctl[j] = (b < nb && c < W.n) ? W.ctl[c] : 0u;
+    alive[j] = (ctl[j] & CTL_ALIVE) != 0;
+    double m = alive[j] ? W.merit[c] : 0.0;
+    if (alive[j] && !(m >= 0.0 && m < 1.0e300)) {   // a corrupt merit is counted, not scheduled
+      count_add(W, CNT_BAD_RECORD, 1ull);
+      m = 0.0;
     }
-    if (t == 0) cn[0] = W.blk_count[b];
-    __syncthreads();
-    const uint64_t gb = (uint64_t)(W.cell0 / 256 + b);
-    for (int k = 0; k < 8; k++) {
-      if (t < (1 << k)) {
-        const int o = (1 << k) - 1, oc = (2 << k) - 1;
-        const long long c0 = cn[t];
-        const long long left = binom_draw(c0, __ddiv_rn(lv[oc + t], lv[o + t]),
-                                          node_draw(W.seed_lo, W.seed_hi, update, SALT_BLOCK,
-                                                    (gb << 9) | (uint64_t)((1 << k) + t)));
-        cn[t] = left;
-        cn[t + (1 << k)] = c0 - left;
-      }
-      __syncthreads();
-    }
+    wt[j] = alive[j] ? sched_weight(m, ctl[j]) : 0.0;
   }
-  bool want = false;
-  int cls = 0;
-  if (in) {
+  long long cnt[4] = {0, 0, 0, 0};
+  if (prob && b < nb) {                        // wave-uniform
+    const uint64_t gb = (uint64_t)(W.cell0 / 256 + b);
+    const uint32_t slo = W.seed_lo, shi = W.seed_hi;
+    // bottom up: L7[l] = x[l] + x[l+128], L7[l+64] = x[l+64] + x[l+192], L6[l] = L7[l] + L7[l+64]
+    const double l7a = __dadd_rn(wt[0], wt[2]), l7b = __dadd_rn(wt[1], wt[3]);
+    const double l6 = __dadd_rn(l7a, l7b);
+    double lv[7];                                // lv[k] = L_k[lane] (k = 0..6; lanes >= 2^k: unused)
+    lv[6] = l6;
+#pragma unroll
+    for (int k = 5; k >= 0; k--) {
+      const double o = __shfl_down(lv[k + 1], 1 << k);
+      lv[k] = __dadd_rn(lv[k + 1], o);
+    }
+    // top down: lane t < 2^k holds count(k, t)
+    long long c = lane == 0 ? (long long)W.blk_count[b] : 0;
+#pragma unroll
+    for (int k = 0; k < 6; k++) {
+      long long left = 0;
+      const bool act = lane < (1 << k);
+      if (act)
+        left = binom_draw(c, __ddiv_rn(lv[k + 1], lv[k]),
+                          node_draw(slo, shi, update, SALT_BLOCK, (gb << 9) | (uint64_t)((1 << k) + lane)));
+      const long long right = c - left;
+      const long long got = __shfl_up(right, 1 << k);   // lane t + 2^k takes node (k, t)'s right child
+      if (act) c = left;
+      else if (lane < (2 << k)) c = got;
+    }
+    // level 6 (node (6, l) -> (7, l), (7, l + 64)) and level 7 (-> the cells)
+    const long long l6l = binom_draw(c, __ddiv_rn(l7a, l6),
+                                     node_draw(slo, shi, update, SALT_BLOCK, (gb << 9) | (uint64_t)(64 + lane)));
+    const long long c7a = l6l, c7b = c - l6l;
+    const long long x0 = binom_draw(c7a, __ddiv_rn(wt[0], l7a),
+                                    node_draw(slo, shi, update, SALT_BLOCK, (gb << 9) | (uint64_t)(128 + lane)));
+    const long long x1 = binom_draw(c7b, __ddiv_rn(wt[1], l7b),
+                                    node_draw(slo, shi, update, SALT_BLOCK, (gb << 9) | (uint64_t)(192 + lane)));
+    cnt[0] = x0; cnt[2] = c7a - x0; cnt[1] = x1; cnt[3] = c7b - x1;
+  }
+  bool want[4] = {false, false, false, false};
+  int cls[4] = {0, 0, 0, 0};
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    const int64_t c = b * 256 + lane + 64 * j;
+    if (b >= nb || c >= W.n) continue;
     int bud = 0;
-    if (alive) {
+    if (alive[j]) {
       if (consts) {
         bud = W.ave_time_slice;
       } else if (prob) {
-        bud = (int)min(cn[t], (long long)(BUDGET_PRIM - 1));   // budgets are < 2^30 (device.h)
+        bud = (int)min(cnt[j], (long long)(BUDGET_PRIM - 1));   // budgets are < 2^30 (device.h)
       } else {
-        double lam = __ddiv_rn(__dmul_rn(totals[3], wt), total);
+        double lam = __ddiv_rn(__dmul_rn(totals[3], wt[j]), total);
         if (lam > 1.0e8) lam = 1.0e8;
         const double cr = __dadd_rn(W.credit[c], lam);
         const double fl = floor(cr);
         bud = (int)fl;
         W.credit[c] = __dsub_rn(cr, fl);
       }
-      if (ctl & CTL_HS_MASK) W.ctl[c] = ctl & ~CTL_HS_MASK;   // the head start is used up
-      want = bud > 0;
-      if (want) cls = class_of(need_of_cell(W, (int)c));
+      if (ctl[j] & CTL_HS_MASK) W.ctl[c] = ctl[j] & ~CTL_HS_MASK;   // the head start is used up
+      want[j] = bud > 0;
+      if (want[j]) cls[j] = class_of(need_of_cell(W, (int)c));
     }
     W.budget[c] = bud;
-    W.aclass[c] = want ? (uint8_t)cls : (uint8_t)ACLASS_NONE;
+    W.aclass[c] = want[j] ? (uint8_t)cls[j] : (uint8_t)ACLASS_NONE;
     occ_init_cell(W, c);
     W.killt[c] = 0u;
     W.claim_r[3][c] = 0ull;   // the previous update's round-3 claims (k_activate read them last)
   }
-  const unsigned long long m = __ballot(want);
-  if ((t & 63) == 0 && m) count_add(W, CNT_SLICES, (unsigned long long)__popcll(m));
-  enqueue_class<4>(W, (int)c, want, cls);
+  unsigned long long ns = 0;
+#pragma unroll
+  for (int j = 0; j < 4; j++) ns += (unsigned long long)__popcll(__ballot(want[j]));
+  if (lane == 0 && ns) count_add(W, CNT_SLICES, ns);
+#pragma unroll
+  for (int j = 0; j < 4; j++) enqueue_class<4>(W, (int)(b * 256 + lane + 64 * j), want[j], cls[j]);
 }
 
-// the window's order from its bucket histogram (block of 1024 threads, two
-// cells each): exclusive scan by one wave, then each cell's slot
+// the window's order from its bucket histogram (block of 1024 threads,
+// WIN_CPT cells each): exclusive scan by one wave, then each cell's slot
+#define WIN_CPT (SORT_WIN / 1024)
 __device__ __forceinline__ void window_order(const DevWorld& W, int64_t base, int* hist, const int* bucket) {
   const int tid = threadIdx.x;
   if (tid < 64) {                              // exclusive scan of the buckets by one wave
@@ -583,7 +614,8 @@ __device__ __forceinline__ void window_order(const DevWorld& W, int64_t base, in
     }
   }
   __syncthreads();
-  for (int h = 0; h < 2; h++) {
+#pragma unroll
+  for (int h = 0; h < WIN_CPT; h++) {
     if (bucket[h] < 0) continue;
     const int pos = atomicAdd(&hist[bucket[h]], 1);
     W.order[base + pos] = (int32_t)(base + h * 1024 + tid);
@@ -591,18 +623,22 @@ __device__ __forceinline__ void window_order(const DevWorld& W, int64_t base, in
 }
 
 // The window's class-0 cells ordered by budget (descending) with a counting
-// sort (k_window_sort's job, one SORT_WIN window per block): which cell runs
-// in which wave changes no organism's result (per-organism streams, placement
-// by priority), it only groups similar slices, so the order inside a budget
-// is free (LDS atomics).
+// sort (one SORT_WIN window per block): which cell runs in which wave changes
+// no organism's result (per-organism streams, placement by birth time and
+// key), it only groups similar slices, so the order inside a budget is free
+// (LDS atomics).  A wave loses about (window's budget range) / (2 x its
+// waves) per lane to the spread of its budgets: 8192-cell windows (128
+// waves) instead of 2048 took the lane efficiency of the bench's
+// multinomial budgets from 0.94 to 0.98 (tools/budget_spread.py).
 __global__ __launch_bounds__(1024) void k_window_count(DevWorld W) {
   __shared__ int hist[SORT_BUCKETS];
   const int tid = threadIdx.x;
   const int64_t base = (int64_t)blockIdx.x * SORT_WIN;
   for (int i = tid; i < SORT_BUCKETS; i += 1024) hist[i] = 0;
   __syncthreads();
-  int bucket[2];
-  for (int h = 0; h < 2; h++) {
+  int bucket[WIN_CPT];
+#pragma unroll
+  for (int h = 0; h < WIN_CPT; h++) {
     const int64_t c = base + h * 1024 + tid;
     bucket[h] = -1;
     if (c < W.n) {
@@ -1220,6 +1256,13 @@ __global__ __launch_bounds__(64) void k_activate_remote(DevWorld W) {
   for (int q = b0; q < nrec; q += half) {
     const HaloRec r = recs[q];
     if (r.len < 0) continue;                  // lost at the sender (counted there)
+    // fields used as indices / lengths are checked: a record the exchange
+    // delivered damaged is counted (CNT_BAD_RECORD), never followed
+    if (r.col < 0 || r.col >= X || r.len > AVGPU_MAX_GENOME || r.off < 0 || (r.off & 3) ||
+        (int64_t)r.off + r.len > W.r_arena || r.round < 0 || r.round > 3) {
+      if (lane == 0) count_add(W, CNT_BAD_RECORD, 1ull);
+      continue;
+    }
     const int64_t c = edge_cell(W, d, r.col);
     if (W.owner[c] != REMOTE_OWNER(r.round, r.t)) { lost++; continue; }   // overwritten by a later winner
     born++;
@@ -1436,7 +1479,7 @@ __global__ __launch_bounds__(256) void k_reset_counts(DevWorld W) { reset_counts
 // class lists, occupancy; then the class-0 order
 static void launch_allot(const DevWorld& W, hipStream_t s, const double* totals, hipEvent_t lists_ready,
                          uint32_t update) {
-  hipLaunchKernelGGL(k_allot, dim3(nblk(W.n, 256)), dim3(256), 0, s, W, totals, update);
+  hipLaunchKernelGGL(k_allot, dim3(nblk(W.n, 1024)), dim3(256), 0, s, W, totals, update);
   // the class lists are complete: the aux streams of the list classes start
   // here, beside the window sort, so that their blocks take CUs before class 0
   // (with the sort folded into the allotment they start together with class 0

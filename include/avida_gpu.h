@@ -646,8 +646,8 @@ enum avgpu_counter {
   AVGPU_CNT_DEATHS = 1,
   AVGPU_CNT_DIVIDES = 2,
   AVGPU_CNT_BIRTHS = 3,
-  AVGPU_CNT_DROPPED = 4,    /* offspring never placed: birth-queue overflow, a slip past
-                               AVGPU_MAX_GENOME, a full halo arena (placement itself places every birth) */
+  AVGPU_CNT_DROPPED = 4,    /* offspring never placed for capacity: birth-queue overflow, a slip past
+                               AVGPU_MAX_GENOME, a full halo arena, BIRTH_METHOD 3 without a cell */
   AVGPU_CNT_SPILLS = 5,     /* slices handed to a larger LDS size class */
   AVGPU_CNT_SLICES = 6,     /* organisms with a non-zero allotment */
   AVGPU_CNT_LANESTEPS = 7,  /* 64 x longest lane per wave (lane efficiency = INSTS / this) */
@@ -663,6 +663,10 @@ enum avgpu_counter {
                                  the same update (the reference kills such a newborn too) */
   AVGPU_CNT_MEM_CAP = 23,   /* copy-time insertions skipped at AVGPU_MAX_GENOME memory sites (the
                                reference has no cap) and removals from a one-site memory */
+  AVGPU_CNT_CANCELLED = 25, /* births whose parent's cell got an earlier offspring before the divide
+                               (the reference's parent died first: never placed) */
+  AVGPU_CNT_BAD_RECORD = 26, /* record or cell fields out of range where used as an index or length
+                                (guarded, counted, never used; must be 0) */
   AVGPU_NUM_COUNTERS = 48   /* 32..47: AVGPU_PHASE_CLOCKS diagnostic builds */
 };
 int avgpu_counters(avgpu_world* w, int cumulative, int64_t* out, int n);

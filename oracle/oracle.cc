@@ -290,6 +290,7 @@ struct World {
   int64_t t_memcap = 0;     // copy insertions past AVGPU_MAX_GENOME sites / removals from one site (skipped)
   int64_t t_overwritten = 0;   // offspring placed, then killed by a later birth into the same cell
   int64_t t_cancelled = 0;     // records whose parent's cell got an offspring before their divide
+  std::vector<int32_t> last_budget;   // the last allotment's budgets (orc_last_budgets, diagnostics)
   int64_t t_placed = 0;        // strip tiles: this tile's own winners activated (avgpu_tile_place(3, 2))
   // resources (avgpu_load_resources): literal restatement of cResourceCount /
   // cSpatialResCount, stepped once per update
@@ -329,18 +330,6 @@ static double det_exp2(double x) {
   double y = 1.0;
   for (int k = 22; k >= 1; k--) y = 1.0 + y * (t / (double)k);
   return std::ldexp(y, (int)n);
-}
-
-// Square root from IEEE adds / multiplies / divisions only (the device's
-// det_sqrt, device.h): exponent halved exactly, then 6 Newton steps -- the
-// same operations on both sides, so the bits agree.
-static double det_sqrt(double x) {
-  if (!(x > 0.0)) return 0.0;
-  int e;
-  const double m = std::frexp(x, &e);          // x = m 2^e, m in [0.5, 1)
-  double y = std::ldexp(m + 0.5, e / 2 - (e & 1 && e < 0 ? 1 : 0));
-  for (int k = 0; k < 6; k++) y = 0.5 * (y + x / y);
-  return y;
 }
 
 struct Exec {
@@ -1178,7 +1167,9 @@ static double pow_int(double q, int64_t n) {
 // on the smaller side pp = min(p, 1 - p), mean n pp < 12 by inversion
 // (f_0 = (1 - pp)^n by squaring, f_{k+1} = f_k (n - k) pp / ((1 - pp)(k + 1)));
 // otherwise normal with the binomial's skew (Cornish-Fisher), z the centred
-// sum of 12 16-bit uniforms from h (Irwin-Hall), clamped to [0, n].
+// sum of 12 16-bit uniforms from h (Irwin-Hall), clamped to [0, n].  IEEE
+// adds, multiplies, divisions and square roots only (all correctly rounded on
+// both sides, no fused multiply-add).
 static int64_t binom_draw(int64_t n, double p, uint32_t h) {
   if (n <= 0 || !(p > 0.0)) return 0;
   if (p >= 1.0) return n;
@@ -1201,7 +1192,7 @@ static int64_t binom_draw(int64_t n, double p, uint32_t h) {
       sum = sum + (double)(x & 0xFFFFu) + (double)(x >> 16);
     }
     const double z = (sum + 6.0) * 1.52587890625e-05 - 6.0;
-    const double sd = det_sqrt(mean * q);
+    const double sd = std::sqrt(mean * q);   // IEEE, correctly rounded (the device's __dsqrt_rn)
     const double v = mean + sd * z + ((q - pp) * (z * z - 1.0)) / 6.0 + 0.5;
     k = v < 1.0 ? 0 : (int64_t)std::floor(v);
     if (k > n) k = n;
@@ -1977,6 +1968,7 @@ static void allot_interpret(World& w, const std::vector<int64_t>& blk, double to
   }
   w.t_slices = 0;
   for (int64_t c = 0; c < w.ncells; c++) w.t_slices += budget[c] > 0;
+  w.last_budget = budget;
   w.births.clear();
   int64_t insts = 0, deaths = 0, divides = 0;
   for (int64_t c = 0; c < w.ncells; c++) {
@@ -2604,6 +2596,13 @@ int orc_tile_finish(void* h, avgpu_update_stats* out) {
 }
 
 int orc_get_stats(void* h, avgpu_update_stats* out) { *out = ((World*)h)->stats; return 0; }
+
+// the last allotment's budgets (diagnostics: tools/budget_spread.py)
+int orc_last_budgets(void* h, int32_t* out) {
+  const World& w = *(World*)h;
+  for (size_t c = 0; c < w.last_budget.size(); c++) out[c] = w.last_budget[c];
+  return (int)w.last_budget.size();
+}
 
 // ---------------------------------------------------------------------------
 // Reference-style serial world (the CPU baseline): Avida2Driver::Run's update

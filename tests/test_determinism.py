@@ -14,6 +14,7 @@ side.)
 """
 import pytest
 
+from avida_amd import capi
 import oracle_lib as ol
 import parity_util as pu
 from test_parity_full import _bench_seed, _seed
@@ -30,7 +31,9 @@ def _run(golden, X, Y, updates, lazy):
         b._call("run_update", b.h, None)
     stats.append(b.run_update())
     d = b.digests(0, X * Y)
+    bad = b.counters(cumulative=1)[capi.CNT_BAD_RECORD]
     b.close()
+    assert bad == 0, f"{bad} record / cell fields out of range (AVGPU_CNT_BAD_RECORD)"
     return d, stats
 
 

@@ -194,3 +194,4 @@ def test_config2_bench_regime_bit_exact(golden):
         assert sg.births_dropped == 0 and sg.births > 10_000 and sg.births_overwritten > 0
         _assert_digests(orc.digests(), gpu.digests(), f"bench regime, update {bench.BURN_IN + bench.WARMUP + u}", orc, gpu)
     assert cap > 320                             # organisms beyond class 0's slots took part
+    assert gpu.counters(cumulative=1)[capi.CNT_BAD_RECORD] == 0   # no guarded field ever out of range

@@ -578,9 +578,17 @@ __device__ __forceinline__ double pow_int(double q, int64_t n) {
   while (n) { if (n & 1) r = __dmul_rn(r, b); b = __dmul_rn(b, b); n >>= 1; }
   return r;
 }
+// 1/k for k = 1..64 (oracle INV_K)
+__constant__ const double INV_K[65] = {0.0,
+  1.0 / 1, 1.0 / 2, 1.0 / 3, 1.0 / 4, 1.0 / 5, 1.0 / 6, 1.0 / 7, 1.0 / 8, 1.0 / 9, 1.0 / 10, 1.0 / 11, 1.0 / 12,
+  1.0 / 13, 1.0 / 14, 1.0 / 15, 1.0 / 16, 1.0 / 17, 1.0 / 18, 1.0 / 19, 1.0 / 20, 1.0 / 21, 1.0 / 22, 1.0 / 23,
+  1.0 / 24, 1.0 / 25, 1.0 / 26, 1.0 / 27, 1.0 / 28, 1.0 / 29, 1.0 / 30, 1.0 / 31, 1.0 / 32, 1.0 / 33, 1.0 / 34,
+  1.0 / 35, 1.0 / 36, 1.0 / 37, 1.0 / 38, 1.0 / 39, 1.0 / 40, 1.0 / 41, 1.0 / 42, 1.0 / 43, 1.0 / 44, 1.0 / 45,
+  1.0 / 46, 1.0 / 47, 1.0 / 48, 1.0 / 49, 1.0 / 50, 1.0 / 51, 1.0 / 52, 1.0 / 53, 1.0 / 54, 1.0 / 55, 1.0 / 56,
+  1.0 / 57, 1.0 / 58, 1.0 / 59, 1.0 / 60, 1.0 / 61, 1.0 / 62, 1.0 / 63, 1.0 / 64};
 // Binomial(n, p) from one 32-bit word h (oracle binom_draw: inversion below a
-// mean of 12 on the smaller side, else normal with the binomial's skew, z the
-// centred sum of 12 16-bit uniforms)
+// mean of 6 on the smaller side, else normal with the binomial's skew, z the
+// centred, scaled sum of 4 16-bit uniforms)
 __device__ __forceinline__ int64_t binom_draw(int64_t n, double p, uint32_t h) {
   if (n <= 0 || !(p > 0.0)) return 0;
   if (p >= 1.0) return n;
@@ -588,27 +596,26 @@ __device__ __forceinline__ int64_t binom_draw(int64_t n, double p, uint32_t h) {
   const double pp = flip ? __dsub_rn(1.0, p) : p, q = __dsub_rn(1.0, pp);
   const double mean = __dmul_rn((double)n, pp);
   int64_t k;
-  if (mean < 12.0) {
+  if (mean < 6.0) {
     const double u = __dmul_rn(__dadd_rn((double)h, 0.5), 2.3283064365386962890625e-10);
     const double r = __ddiv_rn(pp, q);
     double f = pow_int(q, n);
     double F = f;
     k = 0;
-    while (F < u && k < n && k < 256) {
-      f = __ddiv_rn(__dmul_rn(f, __dmul_rn((double)(n - k), r)), (double)(k + 1));
+    while (F < u && k < n && k < 64) {
+      f = __dmul_rn(__dmul_rn(f, __dmul_rn((double)(n - k), r)), INV_K[k + 1]);
       k++;
       F = __dadd_rn(F, f);
     }
   } else {
-    uint32_t x = h;
-    double sum = 0.0;
-    for (int i = 0; i < 6; i++) {
-      x = lowbias32(x + 0x9E3779B9U);
-      sum = __dadd_rn(__dadd_rn(sum, (double)(x & 0xFFFFu)), (double)(x >> 16));
-    }
-    const double z = __dsub_rn(__dmul_rn(__dadd_rn(sum, 6.0), 1.52587890625e-05), 6.0);
+    uint32_t x = lowbias32(h + 0x9E3779B9U);
+    uint32_t sum = (x & 0xFFFFu) + (x >> 16);
+    x = lowbias32(x + 0x9E3779B9U);
+    sum += (x & 0xFFFFu) + (x >> 16);
+    const double z = __dmul_rn(__dsub_rn(__dmul_rn(__dadd_rn((double)sum, 2.0), 1.52587890625e-05), 2.0),
+                               1.7320508075688772);
     const double sd = __dsqrt_rn(__dmul_rn(mean, q));   // IEEE, correctly rounded (oracle std::sqrt)
-    const double skew = __ddiv_rn(__dmul_rn(__dsub_rn(q, pp), __dsub_rn(__dmul_rn(z, z), 1.0)), 6.0);
+    const double skew = __dmul_rn(__dmul_rn(__dsub_rn(q, pp), __dsub_rn(__dmul_rn(z, z), 1.0)), 0.16666666666666666);
     const double v = __dadd_rn(__dadd_rn(__dadd_rn(mean, __dmul_rn(sd, z)), skew), 0.5);
     k = v < 1.0 ? 0 : (int64_t)floor(v);
     if (k > n) k = n;
@@ -655,9 +662,10 @@ __device__ __forceinline__ void count_add(const DevWorld& W, int slot, unsigned 
 
 // LDS size classes of k_interpret (bytes of tape per lane)
 // (a block of class S uses 64 x tape_stride(S) B of LDS for tapes; class 0
-// holds nothing else: 64 x 320 B = 20 KiB, so 8 one-wave blocks fill a CU's
-// 160 KiB -- as many as its ~216 VGPRs admit)
-#define CLASS0_SIZE 320
+// holds nothing else: 64 x 316 B = 19.75 KiB, so 8 one-wave blocks fit a
+// CU's 160 KiB -- as many as its ~216 VGPRs admit; 316 B = 79 dwords, odd,
+// so equal offsets of the 64 lanes fall in 64 different banks)
+#define CLASS0_SIZE 316
 #define CLASS1_SIZE 768
 #define CLASS2_SIZE 1536
 #define CLASS3_SIZE 2048

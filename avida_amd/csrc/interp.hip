@@ -140,7 +140,12 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
   // L+1's tape (lane 63's: past the block's LDS, which reads as 0) -- so that
   // its block (tapes only, 20 KiB) fits 8 times in a CU.
   constexpr int STRIDE = tape_stride(S);
-  constexpr int QUADS = STRIDE / 16;
+  // staging granule: 16-B quads, or dwords for class 0, whose 316-B stride
+  // (79 dwords, odd) puts the 64 lanes' equal tape offsets in 64 different
+  // LDS banks (a 320-B stride, 80 = 16 mod 64 dwords, put them in 4:
+  // 16-way conflicts whenever the lanes of a wave run clones in step)
+  constexpr int GRAN = (STRIDE % 16 == 0) ? 16 : 4;
+  constexpr int QUADS = STRIDE / GRAN;
   constexpr int TAPE_WORDS = 64 * STRIDE / 4;
   // class 0 keeps the two stacks in VGPRs (sv[]): without their 5 KiB of LDS a
   // block needs 26 KiB and 6 blocks fit a CU instead of 5
@@ -248,25 +253,28 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
     l32[272 + AVGPU_MAX_REACTIONS * RT_STRIDE + lane] = reinterpret_cast<const uint32_t*>(W.task_tab)[lane];
   }
   // ---- stage tapes and stacks into LDS by LDS-DMA.  The 64 tapes form one
-  // lane-linear image of 64 x QUADS quads (quad i = organism i / QUADS, part
-  // i % QUADS), so each global_load_lds_dwordx4 moves 1 KiB with per-lane
-  // sources; all copies are in flight together and retired by one wait ----
+  // lane-linear image of 64 x QUADS granules (granule i = organism i / QUADS,
+  // part i % QUADS), so each global_load_lds moves 64 granules (1 KiB of
+  // quads, 256 B of dwords) with per-lane sources; all copies are in flight
+  // together and retired by one wait ----
   typedef __attribute__((address_space(3))) void* lds_ptr_t;
   // a serial step runs lane 0 only: its quads are the image's first QUADS
   const int qits = serial ? (QUADS + 63) / 64 : QUADS;
   // class 0: unrolled so that the shuffles of several quads are in flight
   // together (one LDS round trip per quad otherwise); the list classes' 49 /
   // 97 / 129-quad loops stay rolled (code size)
-  constexpr int QUNR = (S == CLASS0_SIZE) ? (QUADS % 7 == 0 ? 7 : 5) : 1;
+  constexpr int QUNR = (S == CLASS0_SIZE) ? 8 : 1;
 #pragma unroll QUNR
   for (int it = 0; it < qits; it++) {
     const int i = it * 64 + lane;
     const int j = i / QUADS, q = i - j * QUADS;
     const int c = __shfl(cell, j);
     const int m = __shfl(M, j);
-    if (c >= 0 && q * 16 < m)
-      __builtin_amdgcn_global_load_lds((void*)(W.tape + (int64_t)c * TAPE_SLOT + q * 16),
-                                       (lds_ptr_t)(lds32 + it * 256), 16, 0, 0);
+    if (c >= 0 && q * GRAN < m) {
+      void* src = (void*)(W.tape + (int64_t)c * TAPE_SLOT + q * GRAN);
+      if constexpr (GRAN == 16) __builtin_amdgcn_global_load_lds(src, (lds_ptr_t)(lds32 + it * 256), 16, 0, 0);
+      else __builtin_amdgcn_global_load_lds(src, (lds_ptr_t)(lds32 + it * 64), 4, 0, 0);
+    }
   }
   // stacks: class 0's into VGPRs with the execution record below; the list
   // classes' from the record into LDS, one word per lane and entry
@@ -1693,16 +1701,20 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
       count_add(W, CNT_SPILLS, 1ull);
     }
   }
-  // tapes back to HBM: the same lane-linear quad image, 16 B per lane
+  // tapes back to HBM: the same lane-linear image, one granule per lane
 #pragma unroll QUNR
   for (int it = 0; it < qits; it++) {
     const int i = it * 64 + lane;
     const int j = i / QUADS, q = i - j * QUADS;
     const int c = __shfl(cell, j);
     const int m = __shfl(M, j);
-    if (c >= 0 && q * 16 < m) {
-      const uint4 v = reinterpret_cast<const uint4*>(lds32)[i];
-      *reinterpret_cast<uint4*>(W.tape + (int64_t)c * TAPE_SLOT + q * 16) = v;
+    if (c >= 0 && q * GRAN < m) {
+      if (GRAN == 16) {
+        const uint4 v = reinterpret_cast<const uint4*>(lds32)[i];
+        *reinterpret_cast<uint4*>(W.tape + (int64_t)c * TAPE_SLOT + q * 16) = v;
+      } else {
+        *reinterpret_cast<uint32_t*>(W.tape + (int64_t)c * TAPE_SLOT + q * 4) = lds32[i];
+      }
     }
   }
   if (serial) return executed | (divides << 16) | (sbirth << 24) | (sdie << 25);

@@ -397,15 +397,20 @@ __global__ __launch_bounds__(256) void k_merit_partial(DevWorld W, double* parti
 // 396-405 -- this world's picks = (int)((local / total) * AVE_TIME_SLICE *
 // N_total)); mode 3: the totals only (totals[0..1] = root, N).
 // totals[2] = the weight total INTEGRATED divides by, totals[3] = UD.
+// LDS: the whole tree in the workgroup's LDS (P <= TREE_LDS_P: 2 x 4096 doubles
+// + counts = 128 KiB of gfx950's 160), else in W.tree_scr / tree_cnt
+#define TREE_LDS_P 4096
+template <bool LDS>
 __global__ __launch_bounds__(1024) void k_block_counts(DevWorld W, const double* part, const int32_t* alive_part,
                                                        int64_t nb, int ntiles, int L, double* totals,
                                                        uint32_t update, int mode) {
   __shared__ long long s_cnt[1024];
-  __shared__ long long s_root;
+  __shared__ double l_scr[LDS ? 2 * TREE_LDS_P : 1];
+  __shared__ long long l_cnt[LDS ? 2 * TREE_LDS_P : 1];
   const int tid = threadIdx.x;
   const int64_t P = (int64_t)1 << L, nbt = mode == 1 ? nb * ntiles : nb;
-  double* scr = W.tree_scr;
-  int64_t* cnt = W.tree_cnt;
+  double* scr = LDS ? l_scr : W.tree_scr;
+  long long* cnt = LDS ? l_cnt : reinterpret_cast<long long*>(W.tree_cnt);
   long long a = 0;
   for (int64_t g = tid; g < P; g += 1024) {
     double v = 0.0;
@@ -448,7 +453,6 @@ __global__ __launch_bounds__(1024) void k_block_counts(DevWorld W, const double*
       totals[2] = root;
       totals[3] = __dmul_rn(ave, (double)n);
     }
-    s_root = nroot;
     cnt[1] = nroot;
   }
   __syncthreads();
@@ -456,9 +460,10 @@ __global__ __launch_bounds__(1024) void k_block_counts(DevWorld W, const double*
   for (int l = 0; l < L; l++) {
     const int64_t w0 = (int64_t)1 << l;
     for (int64_t i = tid; i < w0; i += 1024) {
-      const int64_t h = w0 + i, n = cnt[h];
-      const int64_t left = binom_draw(n, __ddiv_rn(scr[2 * h], scr[h]),
-                                      node_draw(W.seed_lo, W.seed_hi, update, SALT_TOP, (uint64_t)h));
+      const int64_t h = w0 + i;
+      const long long n = cnt[h];
+      const long long left = binom_draw(n, __ddiv_rn(scr[2 * h], scr[h]),
+                                        node_draw(W.seed_lo, W.seed_hi, update, SALT_TOP, (uint64_t)h));
       cnt[2 * h] = left;
       cnt[2 * h + 1] = n - left;
     }
@@ -467,7 +472,6 @@ __global__ __launch_bounds__(1024) void k_block_counts(DevWorld W, const double*
   const int64_t b0 = mode == 1 ? W.cell0 / 256 : 0;
   const int64_t nloc = (W.n + 255) / 256;
   for (int64_t j = tid; j < nloc; j += 1024) W.blk_count[j] = cnt[P + b0 + j];
-  (void)s_root;
 }
 
 __device__ __forceinline__ void occ_init_cell(const DevWorld& W, int64_t c) {
@@ -1454,6 +1458,14 @@ void launch_classify_uniform(const DevWorld& W, hipStream_t s, int64_t first, in
                      budget, uniform);
 }
 
+static void launch_block_counts(const DevWorld& W, hipStream_t s, const double* part, const int32_t* alive,
+                                int64_t nb, int ntiles, int L, double* totals, uint32_t update, int mode) {
+  if (((int64_t)1 << L) <= TREE_LDS_P)
+    hipLaunchKernelGGL(k_block_counts<true>, dim3(1), dim3(1024), 0, s, W, part, alive, nb, ntiles, L, totals, update, mode);
+  else
+    hipLaunchKernelGGL(k_block_counts<false>, dim3(1), dim3(1024), 0, s, W, part, alive, nb, ntiles, L, totals, update, mode);
+}
+
 static int tree_levels(int64_t nbt) {
   int L = 0;
   while (((int64_t)1 << L) < nbt) L++;
@@ -1467,8 +1479,7 @@ void launch_merit_total(const DevWorld& W, hipStream_t s, double* totals, double
   int32_t* alive_partial = reinterpret_cast<int32_t*>(scratch + nb);
   hipLaunchKernelGGL(k_merit_partial, dim3((unsigned)((nb + 3) / 4)), dim3(256), 0, s, W, scratch, alive_partial,
                      (double*)nullptr, 0);
-  hipLaunchKernelGGL(k_block_counts, dim3(1), dim3(1024), 0, s, W, (const double*)scratch,
-                     (const int32_t*)alive_partial, nb, 1, tree_levels(nb), totals, 0u, 3);
+  launch_block_counts(W, s, scratch, alive_partial, nb, 1, tree_levels(nb), totals, 0u, 3);
 }
 
 // the update's counters, birth-queue and class-list lengths, zeroed by one
@@ -1497,8 +1508,7 @@ void launch_world_begin(const DevWorld& W, hipStream_t s, double* totals, double
   launch_resources_begin(W, s);   // ProcessPreUpdate + the update's first DoUpdates
   hipLaunchKernelGGL(k_merit_partial, dim3((unsigned)((nb + 3) / 4)), dim3(256), 0, s, W, scratch, alive_partial,
                      (double*)nullptr, 1);
-  hipLaunchKernelGGL(k_block_counts, dim3(1), dim3(1024), 0, s, W, (const double*)scratch,
-                     (const int32_t*)alive_partial, nb, 1, tree_levels(nb), totals, update, 0);
+  launch_block_counts(W, s, scratch, alive_partial, nb, 1, tree_levels(nb), totals, update, 0);
   launch_allot(W, s, totals, lists_ready, update);
 }
 
@@ -1513,8 +1523,7 @@ void launch_world_pre(const DevWorld& W, hipStream_t s, double* totals, double* 
   launch_resources_begin(W, s);   // ProcessPreUpdate + the update's first DoUpdates
   hipLaunchKernelGGL(k_merit_partial, dim3((unsigned)((nb + 3) / 4)), dim3(256), 0, s, W, scratch, alive_partial,
                      (double*)nullptr, reset ? 1 : 0);
-  hipLaunchKernelGGL(k_block_counts, dim3(1), dim3(1024), 0, s, W, (const double*)scratch,
-                     (const int32_t*)alive_partial, nb, 1, tree_levels(nb), totals, update, 2);
+  launch_block_counts(W, s, scratch, alive_partial, nb, 1, tree_levels(nb), totals, update, 2);
   launch_allot(W, s, totals, lists_ready, update);
 }
 
@@ -1524,8 +1533,7 @@ void launch_tile_pre(const DevWorld& W, hipStream_t s, const double* gathered, i
                      hipEvent_t lists_ready, uint32_t update) {
   const int64_t nb = (W.n + 255) / 256;
   launch_resources_begin(W, s);
-  hipLaunchKernelGGL(k_block_counts, dim3(1), dim3(1024), 0, s, W, gathered, (const int32_t*)nullptr, nb, ntiles,
-                     tree_levels(nb * ntiles), totals, update, 1);
+  launch_block_counts(W, s, gathered, nullptr, nb, ntiles, tree_levels(nb * ntiles), totals, update, 1);
   launch_allot(W, s, totals, lists_ready, update);
 }
 

@@ -271,9 +271,9 @@ struct Rccl : Transport {
     HIP_OK(hipEventCreateWithFlags(&done, hipEventDisableTiming));
   }
   ~Rccl() override {
-    hipEventDestroy(issued);
-    hipEventDestroy(done);
-    hipStreamDestroy(side);
+    (void)hipEventDestroy(issued);
+    (void)hipEventDestroy(done);
+    (void)hipStreamDestroy(side);
   }
   void exchange_begin(std::vector<Tile>& t, Kind k, hipStream_t s) override {
     HIP_OK(hipEventRecord(issued, s));

@@ -385,6 +385,28 @@ def main():
             dist.all_reduce(lins)
         long_run = {"updates": args.long_updates, "value": lins.item() / ldt.item(),
                     "ms_per_step": ldt.item() * 1e3 / args.long_updates}
+    stats_run = None
+    if args.long_updates > 0 and world == 1:
+        # the timed updates skip the statistics reduction the reference runs
+        # every update (cPopulation::UpdateOrganismStats, main/cPopulation.cc:6245;
+        # DESIGN.md 5 "lazy statistics"): the same updates with it, stream-ordered
+        # (avgpu_stats_vector enqueues the reduction, no host copy)
+        nst = 20
+        ss0 = capi.AvgpuUpdateStats()
+        capi.check(lib, lib.avgpu_get_stats(h, C.byref(ss0)))
+        ptr = C.c_void_p()
+        torch.cuda.synchronize()
+        q0 = time.perf_counter()
+        for _ in range(nst):
+            update()
+            capi.check(lib, lib.avgpu_stats_vector(h, C.byref(ptr)))
+        torch.cuda.synchronize()
+        qdt = time.perf_counter() - q0
+        ss1 = capi.AvgpuUpdateStats()
+        capi.check(lib, lib.avgpu_get_stats(h, C.byref(ss1)))
+        stats_run = {"updates": nst, "value": (ss1.cum_insts_executed - ss0.cum_insts_executed) / qdt,
+                     "ms_per_step": qdt * 1e3 / nst,
+                     "stats_ms_per_update": qdt * 1e3 / nst - dt_max * 1e3 / args.steps}
     if rank != 0:
         if dist:
             dist.destroy_process_group()
@@ -443,6 +465,10 @@ def main():
             "parallelism": f"strips{world}",
             "ranks": world,
             "long_run": long_run,
+            # the timed updates run without the per-update statistics reduction;
+            # stats_every_update_run: the same updates with it (its cost per update)
+            "stats_every_update": False,
+            "stats_every_update_run": stats_run,
         },
         # The resource that binds k_interpret<320> is instruction issue plus
         # exposed latency, so the headline roofline is the VALU-issue one

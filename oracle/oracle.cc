@@ -1163,13 +1163,23 @@ static double pow_int(double q, int64_t n) {
   return r;
 }
 
+// 1/k for k = 1..64, correctly rounded (the same doubles on both sides)
+static const double INV_K[65] = {0.0,
+  1.0 / 1, 1.0 / 2, 1.0 / 3, 1.0 / 4, 1.0 / 5, 1.0 / 6, 1.0 / 7, 1.0 / 8, 1.0 / 9, 1.0 / 10, 1.0 / 11, 1.0 / 12,
+  1.0 / 13, 1.0 / 14, 1.0 / 15, 1.0 / 16, 1.0 / 17, 1.0 / 18, 1.0 / 19, 1.0 / 20, 1.0 / 21, 1.0 / 22, 1.0 / 23,
+  1.0 / 24, 1.0 / 25, 1.0 / 26, 1.0 / 27, 1.0 / 28, 1.0 / 29, 1.0 / 30, 1.0 / 31, 1.0 / 32, 1.0 / 33, 1.0 / 34,
+  1.0 / 35, 1.0 / 36, 1.0 / 37, 1.0 / 38, 1.0 / 39, 1.0 / 40, 1.0 / 41, 1.0 / 42, 1.0 / 43, 1.0 / 44, 1.0 / 45,
+  1.0 / 46, 1.0 / 47, 1.0 / 48, 1.0 / 49, 1.0 / 50, 1.0 / 51, 1.0 / 52, 1.0 / 53, 1.0 / 54, 1.0 / 55, 1.0 / 56,
+  1.0 / 57, 1.0 / 58, 1.0 / 59, 1.0 / 60, 1.0 / 61, 1.0 / 62, 1.0 / 63, 1.0 / 64};
+
 // Binomial(n, p) from one 32-bit word h (the device's binom_draw, device.h):
-// on the smaller side pp = min(p, 1 - p), mean n pp < 12 by inversion
-// (f_0 = (1 - pp)^n by squaring, f_{k+1} = f_k (n - k) pp / ((1 - pp)(k + 1)));
-// otherwise normal with the binomial's skew (Cornish-Fisher), z the centred
-// sum of 12 16-bit uniforms from h (Irwin-Hall), clamped to [0, n].  IEEE
-// adds, multiplies, divisions and square roots only (all correctly rounded on
-// both sides, no fused multiply-add).
+// on the smaller side pp = min(p, 1 - p), mean n pp < 6 by inversion
+// (f_0 = (1 - pp)^n by squaring, f_{k+1} = f_k (n - k) (pp / (1 - pp)) / (k + 1),
+// at most 64 steps); otherwise normal with the binomial's skew
+// (Cornish-Fisher: mean + sd z + (1 - 2 pp)(z^2 - 1) / 6, rounded), z the
+// centred, scaled sum of 4 16-bit uniforms from h (Irwin-Hall), clamped to
+// [0, n].  IEEE adds, multiplies, divisions and square roots only (correctly
+// rounded on both sides, no fused multiply-add).
 static int64_t binom_draw(int64_t n, double p, uint32_t h) {
   if (n <= 0 || !(p > 0.0)) return 0;
   if (p >= 1.0) return n;
@@ -1177,23 +1187,21 @@ static int64_t binom_draw(int64_t n, double p, uint32_t h) {
   const double pp = flip ? 1.0 - p : p, q = 1.0 - pp;
   const double mean = (double)n * pp;
   int64_t k;
-  if (mean < 12.0) {
+  if (mean < 6.0) {
     const double u = ((double)h + 0.5) * 2.3283064365386962890625e-10;
     const double r = pp / q;
     double f = pow_int(q, n);
     double F = f;
     k = 0;
-    while (F < u && k < n && k < 256) { f = (f * ((double)(n - k) * r)) / (double)(k + 1); k++; F = F + f; }
+    while (F < u && k < n && k < 64) { f = (f * ((double)(n - k) * r)) * INV_K[k + 1]; k++; F = F + f; }
   } else {
-    uint32_t x = h;
-    double sum = 0.0;
-    for (int i = 0; i < 6; i++) {
-      x = lowbias32(x + 0x9E3779B9U);
-      sum = sum + (double)(x & 0xFFFFu) + (double)(x >> 16);
-    }
-    const double z = (sum + 6.0) * 1.52587890625e-05 - 6.0;
+    uint32_t x = lowbias32(h + 0x9E3779B9U);
+    uint32_t sum = (x & 0xFFFFu) + (x >> 16);
+    x = lowbias32(x + 0x9E3779B9U);
+    sum += (x & 0xFFFFu) + (x >> 16);
+    const double z = (((double)sum + 2.0) * 1.52587890625e-05 - 2.0) * 1.7320508075688772;
     const double sd = std::sqrt(mean * q);   // IEEE, correctly rounded (the device's __dsqrt_rn)
-    const double v = mean + sd * z + ((q - pp) * (z * z - 1.0)) / 6.0 + 0.5;
+    const double v = mean + sd * z + ((q - pp) * (z * z - 1.0)) * 0.16666666666666666 + 0.5;
     k = v < 1.0 ? 0 : (int64_t)std::floor(v);
     if (k > n) k = n;
   }

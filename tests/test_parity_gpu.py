@@ -90,10 +90,14 @@ def test_ancestor_mutants_fuzz(golden):
     _run_compare(orc, gpu, len(g), [250, 750, 2000])
 
 
+@pytest.mark.timeout(900)
 def test_world_updates_bit_exact(golden):
-    """Full batch-synchronous updates (allot, interpret with copy/divide
-    mutations, birth placement, activation) from one injected ancestor on a
-    60x60 torus: GPU world == oracle world, every cell, every field."""
+    """BASELINE.json configs[0] at its stated length: the default avida.cfg
+    world (60x60 torus, heads_default, logic-9, default mutation rates), the
+    default-heads ancestor injected once, 1000 full batch-synchronous updates
+    (allot, interpret with copy/divide mutations, time-ordered placement,
+    activation): every update's counters equal, then GPU world == oracle
+    world, every cell, every field, and the cell digests."""
     iset, env, cfg = pu.load_env(golden, seed=101)
     n = cfg.world_x * cfg.world_y
     orc = ol.Backend("oracle", cfg, iset, env, ncells=n)
@@ -102,16 +106,21 @@ def test_world_updates_bit_exact(golden):
     center = (cfg.world_y // 2) * cfg.world_x + cfg.world_x // 2
     for b in (orc, gpu):
         b.set_orgs(center, [anc], deterministic=False)
-    for upd in range(150):
+    for upd in range(1000):
         so = orc.run_update()
         sg = gpu.run_update()
-        for f in ("num_organisms", "insts_executed", "births", "deaths", "divides"):
+        for f in ("num_organisms", "insts_executed", "births", "deaths", "divides", "births_dropped",
+                  "births_overwritten", "births_cancelled", "cum_insts_executed", "cum_births"):
             assert getattr(so, f) == getattr(sg, f), (upd, f, getattr(so, f), getattr(sg, f))
+        assert list(so.task_orgs) == list(sg.task_orgs), upd
     a, oa, fa = orc.states(0, n, CAP)
     b, ob, fb = gpu.states(0, n, CAP)
     bad = pu.diff_states(a, b, oa, ob, fa, fb, CAP)
     assert not bad, f"{len(bad)} mismatches: {bad[:5]}"
-    assert so.num_organisms > 100
+    nbad, cells = pu.compare_digests(orc.digests(0, n), gpu.digests(0, n))
+    assert nbad == 0, f"{nbad} cell digests differ, first {cells}"
+    assert so.num_organisms > 3000 and so.update == 999
+    assert gpu.counters(cumulative=1)[capi.CNT_BAD_RECORD] == 0
 
 
 def test_lazy_statistics_equal_eager(golden):

@@ -14,7 +14,7 @@ import re
 from collections import defaultdict
 
 
-def summarize(pattern, regex=r"k_interpret<320[,>]|k_interpretILi320"):
+def summarize(pattern, regex=r"k_interpret<(316|320)[,>]|k_interpretILi(316|320)"):
     vals = defaultdict(list)
     for f in sorted(glob.glob(pattern, recursive=True)):
         with open(f) as fh:
@@ -28,7 +28,7 @@ def summarize(pattern, regex=r"k_interpret<320[,>]|k_interpretILi320"):
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("pattern")
-    ap.add_argument("regex", nargs="?", default=r"k_interpret<320[,>]|k_interpretILi320")
+    ap.add_argument("regex", nargs="?", default=r"k_interpret<(316|320)[,>]|k_interpretILi(316|320)")
     ap.add_argument("--json")
     ap.add_argument("--world", default="1024x1024")
     ap.add_argument("--source", default="")

@@ -8,7 +8,7 @@ from collections import defaultdict
 def main():
     rows = list(csv.DictReader(open(sys.argv[1])))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-    idx = [i for i, r in enumerate(rows) if "k_interpret<320" in r["Kernel_Name"]]
+    idx = [i for i, r in enumerate(rows) if ("k_interpret<316" in r["Kernel_Name"] or "k_interpret<320" in r["Kernel_Name"])]
     acc = defaultdict(float)
     gaps = aux_over = 0.0
     steps = 0

@@ -8,7 +8,7 @@ def main():
     rows = list(csv.DictReader(open(sys.argv[1])))
     step = int(sys.argv[2]) if len(sys.argv) > 2 else 15
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-    c0 = [i for i, r in enumerate(rows) if "k_interpret<320" in r["Kernel_Name"]]
+    c0 = [i for i, r in enumerate(rows) if ("k_interpret<316" in r["Kernel_Name"] or "k_interpret<320" in r["Kernel_Name"])]
     t0 = int(rows[c0[step - 1]]["End_Timestamp"])
     tail = 0
     for r in rows[c0[step - 1] + 1:c0[step] + 1]:

@@ -662,10 +662,12 @@ __device__ __forceinline__ void count_add(const DevWorld& W, int slot, unsigned 
 
 // LDS size classes of k_interpret (bytes of tape per lane)
 // (a block of class S uses 64 x tape_stride(S) B of LDS for tapes; class 0
-// holds nothing else: 64 x 316 B = 19.75 KiB, so 8 one-wave blocks fit a
-// CU's 160 KiB -- as many as its ~216 VGPRs admit; 316 B = 79 dwords, odd,
-// so equal offsets of the 64 lanes fall in 64 different banks)
-#define CLASS0_SIZE 316
+// holds nothing else: 64 x 320 B = 20 KiB, so 8 one-wave blocks fill a CU's
+// 160 KiB -- as many as its ~216 VGPRs admit.  A 316-B stride (79 dwords:
+// equal offsets of the 64 lanes in 64 banks) cut the bank conflicts from 47
+// to 22 % of LDS cycles but needs dword LDS-DMA staging: class 0 1.12 ->
+// 1.50 ms per launch, A/B on one box, profiles/r04c_*)
+#define CLASS0_SIZE 320
 #define CLASS1_SIZE 768
 #define CLASS2_SIZE 1536
 #define CLASS3_SIZE 2048

@@ -140,10 +140,8 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
   // L+1's tape (lane 63's: past the block's LDS, which reads as 0) -- so that
   // its block (tapes only, 20 KiB) fits 8 times in a CU.
   constexpr int STRIDE = tape_stride(S);
-  // staging granule: 16-B quads, or dwords for class 0, whose 316-B stride
-  // (79 dwords, odd) puts the 64 lanes' equal tape offsets in 64 different
-  // LDS banks (a 320-B stride, 80 = 16 mod 64 dwords, put them in 4:
-  // 16-way conflicts whenever the lanes of a wave run clones in step)
+  // staging granule: 16-B quads (dwords for a stride that is not a whole
+  // number of quads; device.h CLASS0_SIZE on why class 0 is not)
   constexpr int GRAN = (STRIDE % 16 == 0) ? 16 : 4;
   constexpr int QUADS = STRIDE / GRAN;
   constexpr int TAPE_WORDS = 64 * STRIDE / 4;
@@ -263,7 +261,7 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
   // class 0: unrolled so that the shuffles of several quads are in flight
   // together (one LDS round trip per quad otherwise); the list classes' 49 /
   // 97 / 129-quad loops stay rolled (code size)
-  constexpr int QUNR = (S == CLASS0_SIZE) ? 8 : 1;
+  constexpr int QUNR = (S == CLASS0_SIZE) ? (QUADS % 7 == 0 ? 7 : 5) : 1;
 #pragma unroll QUNR
   for (int it = 0; it < qits; it++) {
     const int i = it * 64 + lane;

@@ -52,6 +52,49 @@ __device__ __forceinline__ void enqueue_class(const DevWorld& W, int cell, bool 
   }
 }
 
+// The same for CPT cells per thread (cells[j], j-major order inside the
+// block): one global atomic per class and block for all of them.
+template <int WAVES, int CPT>
+__device__ __forceinline__ void enqueue_class_multi(const DevWorld& W, const int* cell, const bool* want,
+                                                    const int* cls) {
+  __shared__ int s_pc[NUM_CLASSES][WAVES], s_base[NUM_CLASSES];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  unsigned long long masks[NUM_CLASSES][CPT];
+  __syncthreads();                             // s_pc / s_base free (repeat calls)
+#pragma unroll
+  for (int k = 1; k < NUM_CLASSES; k++) {
+    int n = 0;
+#pragma unroll
+    for (int j = 0; j < CPT; j++) {
+      masks[k][j] = __ballot(want[j] && cls[j] == k);
+      n += __popcll(masks[k][j]);
+    }
+    if (lane == 0) s_pc[k][wv] = n;
+  }
+  __syncthreads();
+  if (threadIdx.x > 0 && threadIdx.x < NUM_CLASSES) {
+    const int k = threadIdx.x;
+    int tot = 0;
+    for (int w = 0; w < WAVES; w++) tot += s_pc[k][w];
+    s_base[k] = tot ? atomicAdd(&W.class_count[k], tot) : 0;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 1; k < NUM_CLASSES; k++) {
+    int woff = 0;
+    for (int w = 0; w < wv; w++) woff += s_pc[k][w];
+    int jbase = 0;
+#pragma unroll
+    for (int j = 0; j < CPT; j++) {
+      if (want[j] && cls[j] == k) {
+        const int rank = __popcll(masks[k][j] & ((1ull << lane) - 1ull));
+        W.class_list[(int64_t)k * W.n + s_base[k] + woff + jbase + rank] = cell[j];
+      }
+      jbase += __popcll(masks[k][j]);
+    }
+  }
+}
+
 __device__ __forceinline__ int need_of_cell(const DevWorld& W, int cell) {
   return ::need_of(W.mem_size[cell], W.ctl[cell], W.size_range);
 }
@@ -327,8 +370,13 @@ __device__ __forceinline__ void reset_counts_block(const DevWorld& W) {
   if (threadIdx.x < 256) {
     const int slot = threadIdx.x & (CNT_STRIDE - 1), g = threadIdx.x / CNT_STRIDE;
     unsigned long long a = 0;
-    if (fold && slot != CNT_STRIDE - 1)
-      for (int sh = g; sh < NSHARD; sh += NG) a += W.counters[sh * CNT_STRIDE + slot];
+    if (fold && slot != CNT_STRIDE - 1) {
+      unsigned long long v[NSHARD / NG];         // all loads in flight together (this block is
+#pragma unroll                                   // the launch's long pole: ~16 L2 round trips)
+      for (int k = 0; k < NSHARD / NG; k++) v[k] = W.counters[(g + k * NG) * CNT_STRIDE + slot];
+#pragma unroll
+      for (int k = 0; k < NSHARD / NG; k++) a += v[k];
+    }
     cs[g][slot] = a;
   }
   __syncthreads();
@@ -479,7 +527,7 @@ __device__ __forceinline__ void occ_init_cell(const DevWorld& W, int64_t c) {
   W.owner[c] = -1;
 }
 
-// k_allot: one wave per 256-cell block, four blocks per workgroup.  Lane l
+// k_allot: one wave per 256-cell block, 16 blocks per workgroup.  Lane l
 // holds cells l, l + 64, l + 128, l + 192.  The block's stride tree over its
 // cells' weights (node (k, t) = the cells = t mod 2^k, the additions of
 // k_merit_partial): levels 7 and 6 in the lane, levels 5..0 by shuffles; then
@@ -492,9 +540,9 @@ __device__ __forceinline__ void occ_init_cell(const DevWorld& W, int64_t c) {
 // update (living cells occupied; an organism that dies in its slice clears
 // its cell at write-back), its kill time, the previous update's round-3
 // claim, and the class lists.
-__global__ __launch_bounds__(256) void k_allot(DevWorld W, const double* totals, uint32_t update) {
+__global__ __launch_bounds__(1024) void k_allot(DevWorld W, const double* totals, uint32_t update) {
   const int lane = threadIdx.x & 63;
-  const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t b = (int64_t)blockIdx.x * 16 + (threadIdx.x >> 6);
   const int64_t nb = (W.n + 255) / 256;
   const double total = totals[2];
   const bool consts = W.slicing == AVGPU_SLICE_CONSTANT || !(total > 0.0);
@@ -586,8 +634,10 @@ __global__ __launch_bounds__(256) void k_allot(DevWorld W, const double* totals,
 #pragma unroll
   for (int j = 0; j < 4; j++) ns += (unsigned long long)__popcll(__ballot(want[j]));
   if (lane == 0 && ns) count_add(W, CNT_SLICES, ns);
+  int cells[4];
 #pragma unroll
-  for (int j = 0; j < 4; j++) enqueue_class<4>(W, (int)(b * 256 + lane + 64 * j), want[j], cls[j]);
+  for (int j = 0; j < 4; j++) cells[j] = (int)(b * 256 + lane + 64 * j);
+  enqueue_class_multi<16, 4>(W, cells, want, cls);
 }
 
 // the window's order from its bucket histogram (block of 1024 threads,
@@ -1490,7 +1540,10 @@ __global__ __launch_bounds__(256) void k_reset_counts(DevWorld W) { reset_counts
 // class lists, occupancy; then the class-0 order
 static void launch_allot(const DevWorld& W, hipStream_t s, const double* totals, hipEvent_t lists_ready,
                          uint32_t update) {
-  hipLaunchKernelGGL(k_allot, dim3(nblk(W.n, 1024)), dim3(256), 0, s, W, totals, update);
+  // (16 blocks per workgroup: the class lists take one global atomic per
+  // class and 4096 cells -- with 1024-cell workgroups those atomics on three
+  // addresses serialised to ~50 us per update, profiles/r04c_tail_per_update.txt)
+  hipLaunchKernelGGL(k_allot, dim3(nblk(W.n, 4096)), dim3(1024), 0, s, W, totals, update);
   // the class lists are complete: the aux streams of the list classes start
   // here, beside the window sort, so that their blocks take CUs before class 0
   // (with the sort folded into the allotment they start together with class 0

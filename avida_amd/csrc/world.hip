@@ -683,7 +683,9 @@ __device__ __forceinline__ void window_order(const DevWorld& W, int64_t base, in
 // (LDS atomics).  A wave loses about (window's budget range) / (2 x its
 // waves) per lane to the spread of its budgets: 8192-cell windows (128
 // waves) instead of 2048 took the lane efficiency of the bench's
-// multinomial budgets from 0.94 to 0.98 (tools/budget_spread.py).
+// multinomial budgets from 0.94 to 0.98 (tools/budget_spread.py); 16384
+// (256 waves) measured 1.299 ms/step against 1.326-1.389 for 8192 on the
+// same box (profiles/r04e_ab.txt).
 __global__ __launch_bounds__(1024) void k_window_count(DevWorld W) {
   __shared__ int hist[SORT_BUCKETS];
   const int tid = threadIdx.x;
@@ -951,11 +953,14 @@ __global__ void k_place_claim0(DevWorld W) {
 // entries, rewriting the ~10 % of genomes that have edits one after the
 // other; 4 waves per block) -- placement reads no genome, so they are
 // independent and share one launch instead of several latency-bound ones.
-__global__ __launch_bounds__(256) void k_place_pick_mut(DevWorld W, int pblocks, int fblocks) {
+// (boff / nblocks: the launch's first logical block and the logical grid, for
+// the AVGPU_SPLIT_PICK_MUT diagnostic build that times the three parts apart)
+__global__ __launch_bounds__(256) void k_place_pick_mut(DevWorld W, int pblocks, int fblocks, int boff, int nblocks) {
   __shared__ uint8_t child[4][TAPE_SLOT + 16];
   const int nb = queue_len(W);
-  if ((int)blockIdx.x < pblocks) {
-    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < nb; i += (int64_t)pblocks * 256) {
+  const int bid = (int)blockIdx.x + boff;
+  if (bid < pblocks) {
+    for (int64_t i = (int64_t)bid * 256 + threadIdx.x; i < nb; i += (int64_t)pblocks * 256) {
       const int64_t r = rec_of(W, i);
       if (!place_pick_one<false>(W, r, 0)) continue;
       const unsigned long long key = W.b_prio[r];
@@ -963,14 +968,14 @@ __global__ __launch_bounds__(256) void k_place_pick_mut(DevWorld W, int pblocks,
     }
     return;
   }
-  if ((int)blockIdx.x < pblocks + fblocks) {   // deferred divides' phenotype half
-    for (int64_t i = (int64_t)(blockIdx.x - pblocks) * 256 + threadIdx.x; i < nb; i += (int64_t)fblocks * 256)
+  if (bid < pblocks + fblocks) {               // deferred divides' phenotype half
+    for (int64_t i = (int64_t)(bid - pblocks) * 256 + threadIdx.x; i < nb; i += (int64_t)fblocks * 256)
       finalize_phenotype(W, rec_of(W, i));
     return;
   }
   pblocks += fblocks;
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int64_t wave = (int64_t)(blockIdx.x - pblocks) * 4 + wv, nwaves = (int64_t)(gridDim.x - pblocks) * 4;
+  const int64_t wave = (int64_t)(bid - pblocks) * 4 + wv, nwaves = (int64_t)(nblocks - pblocks) * 4;
   for (int64_t q0 = wave * MUT_PER_WAVE; q0 < nb; q0 += nwaves * MUT_PER_WAVE) {
     const int64_t q = q0 + lane;
     int64_t r = 0;
@@ -1638,7 +1643,14 @@ void launch_world_post(const DevWorld& W, hipStream_t s, double* stats, bool eag
   const unsigned bb = place_grid(W);
   const int pm = has_divide_mutations(W) ? (int)((mut_grid(W) + 3) / 4) : 0;
   const int pf = (int)std::min<unsigned>(bb, 256u);   // finalize_phenotype blocks
-  hipLaunchKernelGGL(k_place_pick_mut, dim3(bb + pf + pm), dim3(256), 0, s, W, (int)bb, pf);
+  const int nbk = (int)bb + pf + pm;
+#ifdef AVGPU_SPLIT_PICK_MUT
+  hipLaunchKernelGGL(k_place_pick_mut, dim3(bb), dim3(256), 0, s, W, (int)bb, pf, 0, nbk);
+  hipLaunchKernelGGL(k_place_pick_mut, dim3(pf), dim3(256), 0, s, W, (int)bb, pf, (int)bb, nbk);
+  if (pm) hipLaunchKernelGGL(k_place_pick_mut, dim3(pm), dim3(256), 0, s, W, (int)bb, pf, (int)bb + pf, nbk);
+#else
+  hipLaunchKernelGGL(k_place_pick_mut, dim3(nbk), dim3(256), 0, s, W, (int)bb, pf, 0, nbk);
+#endif
   hipLaunchKernelGGL(k_place_claim0, dim3(bb), dim3(256), 0, s, W);
   for (int m = 1; m < 4; m++) hipLaunchKernelGGL(k_place_round, dim3(bb), dim3(256), 0, s, W, m);
   hipLaunchKernelGGL(k_activate, dim3(lane_grid(W)), dim3(64), 0, s, W, 1);

@@ -25,6 +25,8 @@ def main():
             name = r["Kernel_Name"].replace("void ", "").replace("(anonymous namespace)::", "").split("(")[0]
             if name.startswith("k_interpret"):
                 name = "spill " + name
+            if name == "k_place_pick_mut":   # the split diagnostic build launches its parts apart
+                name += " [%d blocks]" % (int(r["Grid_Size_X"]) // int(r["Workgroup_Size_X"]))
             acc[name] += (e - s) / 1e3
             t = e
         gaps += max(0, int(rows[b]["Start_Timestamp"]) - t) / 1e3

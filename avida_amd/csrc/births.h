@@ -138,12 +138,13 @@ __device__ __forceinline__ void wave_lds_sync() {
 // The divide-mutation edits of record r applied to its child genome by one
 // wave (k_apply_mutations; the serial world per birth): a no-op when the
 // record has none.  child: LDS scratch of TAPE_SLOT + 16 bytes.
-__device__ __forceinline__ void apply_edits_wave(const DevWorld& W, int64_t r, uint8_t* child) {
+// apply_edits_core: the same with the record's five edit words and lengths
+// already in hand (the mutation scan loads them with the queue entry, so a
+// genome costs one dependent round trip -- its own words -- instead of three)
+__device__ __forceinline__ void apply_edits_core(const DevWorld& W, int64_t r, const int* e, int len0, int len,
+                                                 uint8_t* child) {
   const int lane = threadIdx.x & 63;
   const int sfm = W.slip_fill_mode, tfm = W.trans_fill_mode;
-  int e[5];
-#pragma unroll
-  for (int k = 0; k < 5; k++) e[k] = W.b_edit[(int64_t)k * W.rcap + r];
   int pofs[NSEG], pcnt[NSEG], np = 0;   // variable-count edit segments
 #pragma unroll
   for (int k = 0; k < NSEG; k++) {
@@ -152,7 +153,6 @@ __device__ __forceinline__ void apply_edits_wave(const DevWorld& W, int64_t r, u
     np |= pcnt[k];
   }
   if ((e[0] | e[1] | e[2] | e[3] | e[4] | np) == 0) return;   // wave-uniform
-  const int len0 = W.b_len0[r], len = W.b_len[r];
   uint32_t* g32 = reinterpret_cast<uint32_t*>(W.b_genome + r * TAPE_SLOT);
   uint32_t* c32 = reinterpret_cast<uint32_t*>(child);
   for (int w = lane; (w << 2) < len0; w += 64) c32[w] = g32[w];
@@ -170,6 +170,12 @@ __device__ __forceinline__ void apply_edits_wave(const DevWorld& W, int64_t r, u
     g32[w] = word;
   }
   wave_lds_sync();
+}
+__device__ __forceinline__ void apply_edits_wave(const DevWorld& W, int64_t r, uint8_t* child) {
+  int e[5];
+#pragma unroll
+  for (int k = 0; k < 5; k++) e[k] = W.b_edit[(int64_t)k * W.rcap + r];
+  apply_edits_core(W, r, e, W.b_len0[r], W.b_len[r], child);
 }
 
 // ActivateOrganism (main/cPopulation.cc:1320-1340) + SetupOffspring

@@ -141,10 +141,16 @@ __device__ __forceinline__ void cswap(int64_t (&key)[8], double (&val)[8]) {
 // every cell whose pointer 3..6 is c, added in increasing (computing cell, k)
 // order of global cell ids like the reference's loop over i (an 8-entry
 // sorting network keeps the order in registers) -- then StateAll.
+// the spatial resources one launch steps: blockIdx.y = index into r[]
+// (the resources own disjoint grids, so their steps are independent)
+struct ResIds {
+  int r[AVGPU_MAX_RESOURCES];
+};
 template <bool FUSED>
-__global__ void k_res_step(DevWorld W, int r) {
+__global__ void k_res_step(DevWorld W, ResIds ids) {
   const int c = (int)(blockIdx.x * blockDim.x + threadIdx.x);   // n < 2^31 (avgpu_load_resources)
   if (c >= W.n) return;
+  const int r = ids.r[blockIdx.y];
   const ResParam P = W.res_param[r];
   const int X = W.world_x, Y = W.world_y;
   const double* amt = W.res_amount + (int64_t)P.slot * W.n;
@@ -263,18 +269,28 @@ static inline unsigned rblk(int64_t n) { return (unsigned)((n + 255) / 256); }
 
 void launch_resources_begin(const DevWorld& W, hipStream_t s) {
   if (W.n_res == 0) return;
-  // spatial resources: one step of the reference's DoSpatialUpdates, in
-  // resource order (each resource owns its own grid); none in update 0.  The
+  // spatial resources: one step of the reference's DoSpatialUpdates (each
+  // resource owns its own grid, so the order across resources is free); none
+  // in update 0.  Every resource without CELL entries steps in ONE launch
+  // (blockIdx.y = resource); one with them goes through the rates kernels
+  // (res_delta is shared scratch, so those run one resource at a time).  The
   // caller swaps res_amount / res_amount_alt afterwards (res_stepped).
-  for (int r = 0; r < W.n_res && !W.res_first; r++) {
-    if (!W.res_spatial_host[r]) continue;
-    if (W.res_cells_host[r]) {
-      hipLaunchKernelGGL(k_res_spatial_rates, dim3(rblk(W.n)), dim3(256), 0, s, W, r);
-      hipLaunchKernelGGL(k_res_cell_rates, dim3(1), dim3(64), 0, s, W, r);
-      hipLaunchKernelGGL(k_res_step<false>, dim3(rblk(W.n)), dim3(256), 0, s, W, r);
-    } else {
-      hipLaunchKernelGGL(k_res_step<true>, dim3(rblk(W.n)), dim3(256), 0, s, W, r);
+  if (!W.res_first) {
+    ResIds fused{};
+    int nf = 0;
+    for (int r = 0; r < W.n_res; r++) {
+      if (!W.res_spatial_host[r]) continue;
+      if (W.res_cells_host[r]) {
+        ResIds one{};
+        one.r[0] = r;
+        hipLaunchKernelGGL(k_res_spatial_rates, dim3(rblk(W.n)), dim3(256), 0, s, W, r);
+        hipLaunchKernelGGL(k_res_cell_rates, dim3(1), dim3(64), 0, s, W, r);
+        hipLaunchKernelGGL(k_res_step<false>, dim3(rblk(W.n)), dim3(256), 0, s, W, one);
+      } else {
+        fused.r[nf++] = r;
+      }
     }
+    if (nf) hipLaunchKernelGGL(k_res_step<true>, dim3(rblk(W.n), nf), dim3(256), 0, s, W, fused);
   }
   hipLaunchKernelGGL(k_res_global_begin, dim3(1), dim3(64), 0, s, W, (int)W.res_first);
 }

@@ -114,7 +114,7 @@ __global__ void k_set_orgs(DevWorld W, int64_t first, int64_t count, const uint8
   // registers, heads, label, counters, buffers, task counts, stacks: zero
   int32_t* x = W.xs + c * XS_WORDS;
   for (int k = 0; k < XS_WORDS; k++) x[k] = 0;
-  W.ctl[c] = CTL_ALIVE;
+  W.ctl[c] = CTL_ALIVE | CTL_HICLEAN;      // (codes only: no flags)
   W.mem_size[c] = len;
   int mx = 0;
   if (W.death_method > 0) {                 // cOrganism::initialize (main/cOrganism.cc:216-236)
@@ -791,26 +791,33 @@ __device__ __forceinline__ void finalize_key(const DevWorld& W, int64_t r, int p
   row[BI_RLO] = (int32_t)clo;
   row[BI_RHI] = (int32_t)chi;
 }
+// (every load it needs is issued before the first test: the record's row, its
+// parent and sequence number, then the parent's divide count -- a chain of
+// three dependent loads after the queue entry)
 __device__ __forceinline__ void finalize_phenotype(const DevWorld& W, int64_t r) {
+  static_assert(BI_LTASK == 12 && BI_FINAL == 11 && AVGPU_NUM_LOGIC_TASKS <= 12, "row quads");
   int32_t* row = W.b_inh + r * BI_WORDS;
-  const int4 q0 = reinterpret_cast<const int4*>(row)[0], q1 = reinterpret_cast<const int4*>(row)[1];
-  const int fin = row[BI_FINAL];
-  if ((fin & 1) == 0) return;
+  const int4* q = reinterpret_cast<const int4*>(row);
+  const int4 q0 = q[0], q1 = q[1], q2 = q[2], q3 = q[3], q4 = q[4], q5 = q[5];
+  const int parent = W.b_parent[r];
+  const int seq = (int)W.b_seq[r];
+  if ((q2.w & 1) == 0) return;                 // BI_FINAL
+  const int nd = W.num_div[parent];
   const double merit = __hiloint2double(q0.y, q0.x);
   const int gt = q1.w;
   const double fit = __ddiv_rn(merit, (double)gt);
   const long long fb = __double_as_longlong(fit);
   row[BI_FITNESS] = (int32_t)fb;
   row[BI_FITNESS + 1] = (int32_t)(fb >> 32);
-  const int parent = W.b_parent[r];
-  if ((int)W.b_seq[r] == W.num_div[parent]) {
+  if (seq == nd) {
     W.merit[parent] = merit;
     W.fitness[parent] = fit;
     W.gest_time[parent] = gt;
     W.child_copied[parent] = q1.y;
     W.executed[parent] = q1.z;
+    const int lt[12] = {q3.x, q3.y, q3.z, q3.w, q4.x, q4.y, q4.z, q4.w, q5.x, q5.y, q5.z, q5.w};
 #pragma unroll
-    for (int q = 0; q < AVGPU_NUM_LOGIC_TASKS; q++) W.last_task[(int64_t)q * W.n + parent] = row[BI_LTASK + q];
+    for (int k = 0; k < AVGPU_NUM_LOGIC_TASKS; k++) W.last_task[(int64_t)k * W.n + parent] = lt[k];
   }
 }
 
@@ -902,12 +909,46 @@ __device__ __forceinline__ bool place_pick_one(const DevWorld& W, int64_t r, int
   return true;
 }
 
-// divide-mutation scan: queue entries per wave (k_place_pick_mut, k_tile_prep)
-#define MUT_PER_WAVE 8
 // grid-stride over the birth queue (its length is only known on the device)
 #define QUEUE_LOOP(i) \
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, _qn = queue_len(W); i < _qn; \
        i += (int64_t)gridDim.x * blockDim.x)
+// The divide mutations (k_place_pick_mut, k_tile_prep): wave w of nwaves
+// scans MUT_PER_WAVE queue entries at a time -- lane k loads entry k's five
+// edit words and both lengths -- and applies the ~10 % that have edits one
+// after the other, each from the words already in hand (apply_edits_core).
+// (One entry per wave over 65536 waves instead cost 71 us for the fused
+// launch against 59: profiles/r04g_tail_per_update.txt.)
+#define MUT_PER_WAVE 8
+__device__ __forceinline__ void mutation_waves(const DevWorld& W, int64_t wave, int64_t nwaves, uint8_t* child) {
+  const int nb = queue_len(W);
+  const int lane = threadIdx.x & 63;
+  for (int64_t q0 = wave * MUT_PER_WAVE; q0 < nb; q0 += nwaves * MUT_PER_WAVE) {
+    const int64_t q = q0 + lane;
+    int64_t r = 0;
+    int e[5] = {0, 0, 0, 0, 0}, l0 = 0, l1 = 0;
+    bool any = false;
+    if (lane < MUT_PER_WAVE && q < nb) {
+      r = rec_of(W, q);
+#pragma unroll
+      for (int k = 0; k < 5; k++) e[k] = W.b_edit[(int64_t)k * W.rcap + r];
+      l0 = W.b_len0[r];
+      l1 = W.b_len[r];
+      int x = e[0] | e[1] | e[2] | e[3] | e[4];
+      if (W.seg_any)
+        for (int k = 0; k < NSEG; k++) x |= W.b_pcnt[(int64_t)k * W.rcap + r];
+      any = x != 0;
+    }
+    for (unsigned long long m = __ballot(any); m; m &= m - 1ull) {
+      const int L = __ffsll((long long)m) - 1;
+      int eL[5];
+#pragma unroll
+      for (int k = 0; k < 5; k++) eL[k] = __shfl(e[k], L);
+      apply_edits_core(W, (int64_t)__shfl((long long)r, L), eL, __shfl(l0, L), __shfl(l1, L), child);
+    }
+  }
+}
+
 // A single world's placement launch m = 1..3: round m - 1 resolved and round m
 // picked (oracle run_update_impl).  Each round has its own claim array, so
 // round m - 1's claims stay intact for the whole launch: a record whose key is
@@ -974,26 +1015,8 @@ __global__ __launch_bounds__(256) void k_place_pick_mut(DevWorld W, int pblocks,
     return;
   }
   pblocks += fblocks;
-  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int64_t wave = (int64_t)(bid - pblocks) * 4 + wv, nwaves = (int64_t)(nblocks - pblocks) * 4;
-  for (int64_t q0 = wave * MUT_PER_WAVE; q0 < nb; q0 += nwaves * MUT_PER_WAVE) {
-    const int64_t q = q0 + lane;
-    int64_t r = 0;
-    bool any = false;
-    if (lane < MUT_PER_WAVE && q < nb) {
-      r = rec_of(W, q);
-      int e = 0;
-#pragma unroll
-      for (int k = 0; k < 5; k++) e |= W.b_edit[(int64_t)k * W.rcap + r];
-      if (W.seg_any)
-        for (int k = 0; k < NSEG; k++) e |= W.b_pcnt[(int64_t)k * W.rcap + r];
-      any = e != 0;
-    }
-    for (unsigned long long m = __ballot(any); m; m &= m - 1ull) {
-      const int L = __ffsll((long long)m) - 1;
-      apply_edits_wave(W, (int64_t)__shfl((long long)r, L), child[wv]);
-    }
-  }
+  const int wv = threadIdx.x >> 6;
+  mutation_waves(W, (int64_t)(bid - pblocks) * 4 + wv, (int64_t)(nblocks - pblocks) * 4, child[wv]);
 }
 
 
@@ -1013,27 +1036,8 @@ __global__ __launch_bounds__(256) void k_tile_prep(DevWorld W, int mblocks, int 
     return;
   }
   if ((int)blockIdx.x < mblocks) {
-    const int nb = queue_len(W);
-    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int64_t wave = (int64_t)blockIdx.x * 4 + wv, nwaves = (int64_t)mblocks * 4;
-    for (int64_t q0 = wave * MUT_PER_WAVE; q0 < nb; q0 += nwaves * MUT_PER_WAVE) {
-      const int64_t q = q0 + lane;
-      int64_t r = 0;
-      bool any = false;
-      if (lane < MUT_PER_WAVE && q < nb) {
-        r = rec_of(W, q);
-        int e = 0;
-#pragma unroll
-        for (int k = 0; k < 5; k++) e |= W.b_edit[(int64_t)k * W.rcap + r];
-        if (W.seg_any)
-          for (int k = 0; k < NSEG; k++) e |= W.b_pcnt[(int64_t)k * W.rcap + r];
-        any = e != 0;
-      }
-      for (unsigned long long m = __ballot(any); m; m &= m - 1ull) {
-        const int L = __ffsll((long long)m) - 1;
-        apply_edits_wave(W, (int64_t)__shfl((long long)r, L), child[wv]);
-      }
-    }
+    const int wv = threadIdx.x >> 6;
+    mutation_waves(W, (int64_t)blockIdx.x * 4 + wv, (int64_t)mblocks * 4, child[wv]);
     return;
   }
   const int X = W.world_x;

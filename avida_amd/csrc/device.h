@@ -43,10 +43,6 @@ enum { BI_MERIT = 0, BI_FITNESS = 2, BI_GEN = 4, BI_CCOPIED = 5, BI_EXEC = 6, BI
 #define CTL_FRESH 0x800u
 // serial world: died in a speculative step (m_spec_die); removed at its next pick
 #define CTL_SPECDIE 0x1000u
-// no site at or above CLASS0_LDS carries the executed flag (set by a divide's
-// ClearFlags, cleared when such a site is flagged): class 0 then knows a
-// copy's destination flags there without reading its HBM part (interp.hip)
-#define CTL_HICLEAN 0x2000u
 // head start of an offspring not yet allotted (17 bits: 2^16 - its birth
 // time, 1..2^16; 0 = none): its first allotment weights its merit by
 // 1 + hs / 2^16 (sched_weight), then clears it
@@ -670,15 +666,11 @@ __device__ __forceinline__ void count_add(const DevWorld& W, int slot, unsigned 
 // 160 KiB -- as many as its ~216 VGPRs admit.  A 316-B stride (79 dwords:
 // equal offsets of the 64 lanes in 64 banks) cut the bank conflicts from 47
 // to 22 % of LDS cycles but needs dword LDS-DMA staging: class 0 1.12 ->
-// 1.50 ms per launch, A/B on one box, profiles/r04c_*)
+// 1.50 ms per launch, A/B on one box, profiles/r04c_*).  A split
+// slot -- 208 sites in LDS, the rest in the HBM tape, 13 KiB per wave -- for 3
+// waves per SIMD was bit-exact but slower, 1.36 against 1.02 ms: 3 waves cap
+// the kernel at 168 VGPRs and the spills land in the loop (profiles/r04k_*)
 #define CLASS0_SIZE 320
-// class 0 keeps an organism's sites [0, CLASS0_LDS) in its lane's LDS slot and
-// the rest of its memory in the cell's HBM tape: 64 x 208 B = 13 KiB per
-// one-wave block, 12 blocks (3 waves per SIMD) per CU where whole 320-B slots
-// admitted 8.  A typical class-0 organism (parent part <= 104 sites) runs,
-// copies and divides inside the LDS part; only h-alloc's fill above it goes
-// to HBM (interp.hip "split memory")
-#define CLASS0_LDS 208
 #define CLASS1_SIZE 768
 #define CLASS2_SIZE 1536
 #define CLASS3_SIZE 2048

@@ -102,9 +102,7 @@ __device__ __forceinline__ bool consume_resource(const DevWorld& W, const double
   return true;
 }
 
-// bytes of LDS tape per lane: class 0 its split memory's LDS part (device.h
-// CLASS0_LDS), the list classes their whole slot and a 16-byte pad
-__host__ __device__ constexpr int tape_stride(int S) { return S == CLASS0_SIZE ? CLASS0_LDS : S + 16; }
+__host__ __device__ constexpr int tape_stride(int S) { return S == CLASS0_SIZE ? S : S + 16; }
 
 // divide-mutation edits (Divide_DoMutations, applied in order): kind | a << 3 | b << 15
 enum { E_SLIP = 1, E_POINT = 2, E_INS = 3, E_DEL = 4, E_TRANS = 5 };
@@ -144,15 +142,6 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
   // L+1's tape (lane 63's: past the block's LDS, which reads as 0) -- so that
   // its block (tapes only, 20 KiB) fits 8 times in a CU.
   constexpr int STRIDE = tape_stride(S);
-  // Split memory (class 0): an organism's sites [0, P) are in its lane's LDS
-  // slot, sites [P, M) in the cell's HBM tape, written there by fire-and-forget
-  // byte stores and read only on rare paths, by loads that wait for
-  // themselves (a compiler-visible load in the loop would make its wait drain
-  // every store the wave has in flight).  The list classes hold whole slots.
-  constexpr int P = (S == CLASS0_SIZE) ? CLASS0_LDS : S;
-  constexpr bool SPLIT = P < S;
-  constexpr int PW = P / 4;
-  static_assert(P % 16 == 0 && (!SPLIT || STRIDE == P), "split memory: whole quads per lane");
   // staging granule: 16-B quads (dwords for a stride that is not a whole
   // number of quads; device.h CLASS0_SIZE on why class 0 is not)
   constexpr int GRAN = (STRIDE % 16 == 0) ? 16 : 4;
@@ -329,11 +318,9 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
   int sbirth = 0;                // serial step: an offspring is in the primary record
   int sdie = 0;                  // serial speculative run: m_spec_die
   int ndrop = 0, noversize = 0;
-  bool hic = true;               // CTL_HICLEAN: no executed flag at or above CLASS0_LDS
   if (active) {
     // written at birth (setup_child) or by the previous slice
     ctl = W.ctl[cell];
-    hic = fresh || (ctl & CTL_HICLEAN) != 0u;
     mx = W.max_exec[cell]; blen = W.birth_len[cell];
     klo = W.rng[cell]; khi = W.rng[N + cell]; kct = W.rng[2 * N + cell];
     olo = klo; ohi = khi;
@@ -479,40 +466,6 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
   }
   const uint32_t* T32 = reinterpret_cast<const uint32_t*>(T);
   const int slow_batch = W.slow_batch;
-  // the split memory's sites, any position (slow paths; SPLIT false: LDS only).
-  // A byte written at or above CLASS0_LDS with its executed flag clears hic,
-  // in every class, so that the bit is exact wherever the organism runs next.
-  auto gsite = [&](int c, int i) -> uint8_t* { return W.tape + (int64_t)c * TAPE_SLOT + i; };
-  auto tget = [&](int i) -> int { return (!SPLIT || i < P) ? (int)T[i] : (int)ld_sync_u8(gsite(cell, i)); };
-  auto tput = [&](int i, int v) {
-    if (!SPLIT || i < P) T[i] = (uint8_t)v;
-    else st_async_u8(gsite(cell, i), (uint32_t)v);
-    if (i >= CLASS0_LDS && (v & TF_EXEC)) hic = false;
-  };
-  // the same on the hot path, branch free for the wave: the LDS store always
-  // goes out (to the block's spare word when the site is in the HBM part),
-  // the HBM store only behind a wave-uniform test (as an exec-masked if /
-  // else, each write site cost ~10 scalar instructions per iteration)
-  uint8_t* const spare = lds + 64 * STRIDE;
-  auto tput_hot = [&](int i, int v) {
-    const bool hi = SPLIT && i >= P;
-    *(hi ? spare : T + i) = (uint8_t)v;
-    if (SPLIT && __builtin_expect(__ballot(hi) != 0ull, 0)) {
-      if (hi) st_async_u8(gsite(cell, i), (uint32_t)v);
-    }
-    hic = hic && !(i >= CLASS0_LDS && (v & TF_EXEC));
-  };
-  // words w0 .. w0 + 3 of the lane's memory (a label window), the HBM part's
-  // words reloaded when the window reaches it
-  auto twin4 = [&](int w0, uint32_t& a, uint32_t& b, uint32_t& c, uint32_t& d) {
-    a = T32[w0]; b = T32[w0 + 1]; c = T32[w0 + 2]; d = T32[w0 + 3];
-    if (SPLIT && w0 + 3 >= PW && M > P) {
-      if (w0 >= PW) a = ld_sync_u32(gsite(cell, 4 * w0));
-      if (w0 + 1 >= PW) b = ld_sync_u32(gsite(cell, 4 * w0 + 4));
-      if (w0 + 2 >= PW) c = ld_sync_u32(gsite(cell, 4 * w0 + 8));
-      d = ld_sync_u32(gsite(cell, 4 * w0 + 12));
-    }
-  };
 
   while (true) {
     const bool run = fl == 0 && budget > 0 && pop < 0;
@@ -531,16 +484,7 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
       // h-copy's two sites read with it (one LDS round trip per iteration
       // instead of two; used only if the op is h-copy)
       const int rha = head_adjust(rh, M), wha = head_adjust(wh, M);
-      uint32_t fw0 = T32[ipa >> 2], fw1 = T32[(ipa >> 2) + 1];
-      const bool fhi = SPLIT && ipa >= P - 4 && M > P;           // the window reaches the HBM part
-      if (SPLIT && __builtin_expect(__ballot(fhi) != 0ull, 0)) {
-        if (fhi) {
-          if ((ipa >> 2) >= PW) fw0 = ld_sync_u32(gsite(cell, ipa & ~3));
-          fw1 = ld_sync_u32(gsite(cell, (ipa & ~3) + 4));
-        }
-      }
-      const uint64_t fwin = ((uint64_t)fw1 << 32) | (uint64_t)fw0;
-      // (split memory: LDS reads of sites >= P are junk, replaced in h-copy)
+      const uint64_t fwin = ((uint64_t)T32[(ipa >> 2) + 1] << 32) | (uint64_t)T32[ipa >> 2];
       const int src_byte = T[rha], dst_byte = T[wha];
       const uint32_t fsh = (uint32_t)(ipa & 3) * 8u;
       const int cur_byte = (int)((fwin >> fsh) & 0xFFu);
@@ -565,7 +509,7 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
     cyc++;                                                    // IncCPUCyclesUsed :929
     tu++;                                                     // IncTimeUsed :930
     ip = ipa;
-    tput_hot(ip, cur_byte | TF_EXEC);                         // SetFlagExecuted :996
+    T[ip] = (uint8_t)(cur_byte | TF_EXEC);                    // SetFlagExecuted :996
     executed++;
     budget--;
     const int nbyte = (int)((fwin >> (fsh + 8u)) & 0xFFu);
@@ -575,7 +519,7 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
     const uint32_t obit = 1u << op;
     const bool mod = ((MOD_OPS & obit) != 0u) && nxt < 3;
     const int r = mod ? nxt : (int)((DEF_OPS >> (2 * op)) & 3ull);
-    if (mod) { ip = ip + 1; tput_hot(ip, nbyte | TF_EXEC); }
+    if (mod) { ip = ip + 1; T[ip] = (uint8_t)(nbyte | TF_EXEC); }
 #ifdef AVGPU_PHASE_CLOCKS
     it_fast += __ballot((FAST_OPS & obit) != 0u) != 0ull;
     it_copy += __ballot(op == AVGPU_H_H_COPY) != 0ull;
@@ -619,16 +563,7 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
     if (op == AVGPU_H_H_COPY) {                               // :7130 Inst_HeadCopy
       rh = rha;
       wh = wha;
-      // split memory: a source in the HBM part is read from there; the
-      // destination's executed flag is known clear there while hic holds
-      // (its whole byte is needed only to undo a spilling copy)
-      int sb = src_byte, db = dst_byte;
-      const bool shi = SPLIT && rha >= P, dhi = SPLIT && wha >= P;
-      if (SPLIT && __builtin_expect(__ballot(shi || dhi) != 0ull, 0)) {
-        if (shi) sb = (int)ld_sync_u8(gsite(cell, rha));
-        if (dhi) db = (hic && (DEF || !k_copy_ext)) ? 0 : (int)ld_sync_u8(gsite(cell, wha));
-      }
-      int v = sb & CODE_MASK;
+      int v = src_byte & CODE_MASK;
       const uint32_t kct_h = kct, rl_h = rl;                  // rewound if the copy spills (below)
       // ReadInst (:1459-1466)
       if (v < 3) {
@@ -645,8 +580,8 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
         if (cmut) v = rand_code();
       }
       // the write head's executed flag: as read, or just set if it is the IP
-      const int wex = (wh == ip) ? TF_EXEC : (db & TF_EXEC);
-      tput_hot(wh, wex | TF_COPIED | v);
+      const int wex = (wh == ip) ? TF_EXEC : (dst_byte & TF_EXEC);
+      T[wh] = (uint8_t)(wex | TF_COPIED | v);
       // COPY_INS / DEL / UNIFORM / SLIP (:7153-7161, each drawing only at a
       // non-zero rate, in that order): the memory grows or shrinks at the
       // write head (cCPUMemory::Insert / Remove, cpu/cCPUMemory.cc:103-138;
@@ -672,8 +607,8 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
             int mx_sz = M + (e_ins >= 0 ? 1 : 0);
             if (e_uni > k_n_ops) mx_sz = max(mx_sz, M + (e_ins >= 0 ? 1 : 0) - (e_del ? 1 : 0) + 1);
             if (mx_sz > S && S < AVGPU_MAX_GENOME) {
-              tput(wh, db);                                    // undo the write, then the step
-              tput(ipa, cur_byte);
+              T[wh] = (uint8_t)dst_byte;                       // undo the write, then the step
+              T[ipa] = (uint8_t)cur_byte;
               kct = kct_h; rl = rl_h;
               cyc--; tu--; executed--; budget++;
               ip = ipa;
@@ -682,21 +617,21 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
               int ncap = 0;
               auto ins_at = [&](int pos, int code) {
                 if (M >= AVGPU_MAX_GENOME) { ncap++; return; }
-                for (int i = M; i > pos; i--) tput(i, tget(i - 1));
-                tput(pos, code);                               // new site: flags 0
+                for (int i = M; i > pos; i--) T[i] = T[i - 1];
+                T[pos] = (uint8_t)code;                        // new site: flags 0
                 M++;
               };
               auto del_at = [&](int pos) {
                 if (M <= 1) { ncap++; return; }
                 if (pos > M - 1) pos = M - 1;                  // Remove(size) drops the last site
-                for (int i = pos; i < M - 1; i++) tput(i, tget(i + 1));
+                for (int i = pos; i < M - 1; i++) T[i] = T[i + 1];
                 M--;
               };
               if (e_ins >= 0) ins_at(wh, e_ins);
               if (e_del) del_at(wh);
               if (e_uni >= 0) {
                 if (e_uni < k_n_ops) {
-                  if (wh < M) tput(wh, (tget(wh) & ~CODE_MASK) | (int)tab_u8(rcode + e_uni));   // SetInst
+                  if (wh < M) T[wh] = (uint8_t)((T[wh] & ~CODE_MASK) | (int)tab_u8(rcode + e_uni));   // SetInst
                 } else if (e_uni == k_n_ops) {
                   del_at(wh);
                 } else {
@@ -745,7 +680,7 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
         const uint32_t lab = (uint32_t)v & lmask;
         const uint32_t dl = lab & 0x55555u, dh = (lab >> 1) & 0x55555u;
         const uint32_t rot = ((~dl & ~dh & 0x55555u) | (dl << 1)) & lmask;   // Rotate(1, NUM_NOPS)
-        if (len > 0) tput_hot(base, (int)(((uint32_t)w & 0xFFu) | TF_EXEC));   // the label's first site (MAX_LABEL_EXE_SIZE 1)
+        if (len > 0) T[base] = (uint8_t)((uint32_t)w | TF_EXEC);         // the label's first site (MAX_LABEL_EXE_SIZE 1)
         ip += len;
         if (((uint32_t)len | (rot << 4)) != rl) ip = head_wrap(ip + 1, M);
       }
@@ -853,7 +788,7 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
                         alloc <= (int)(cur * k_size_range) && cur <= (int)(alloc * k_size_range);
         if (!ok) { errs++; break; }                           // cOrganism::Fault
         if (k_alloc_method == 2) {
-          for (int i = cur; i < nsz; i++) tput(i, rand_code());
+          for (int i = cur; i < nsz; i++) T[i] = rand_code();
         } else {
           rq = RQ_FILL; qa = cur; qb = nsz;                   // new sites = op 0 (wave fill below)
         }
@@ -885,10 +820,8 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
         const int base = ip + 1;
         const int w0 = base >> 2;
         const uint32_t bsh = (uint32_t)(base & 3) * 8u;
-        uint32_t lw0, lw1, lw2, lw3;
-        twin4(w0, lw0, lw1, lw2, lw3);
-        uint64_t lo64 = ((uint64_t)lw1 << 32) | (uint64_t)lw0;
-        uint64_t hi64 = ((uint64_t)lw3 << 32) | (uint64_t)lw2;
+        uint64_t lo64 = ((uint64_t)T32[w0 + 1] << 32) | (uint64_t)T32[w0];
+        uint64_t hi64 = ((uint64_t)T32[w0 + 3] << 32) | (uint64_t)T32[w0 + 2];
         if (bsh) { lo64 = (lo64 >> bsh) | (hi64 << (64u - bsh)); hi64 >>= bsh; }
         const uint64_t K3F = 0x3F3F3F3F3F3F3F3Full, K7D = 0x7D7D7D7D7D7D7D7Dull, K80 = 0x8080808080808080ull;
         const uint64_t cl = lo64 & K3F, ch = hi64 & K3F;
@@ -907,7 +840,7 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
         // executed flags of the label's first sites, from the window's own bytes
         // (no LDS read-modify-write round trip)
         for (int k = 0; k < min(len, k_max_label_exe); k++)
-          tput(base + k, (int)(((k < 8 ? (lo64 >> (8 * k)) : (hi64 >> (8 * (k - 8)))) & 0xFFull) | TF_EXEC));
+          T[base + k] = (uint8_t)(((k < 8 ? (lo64 >> (8 * k)) : (hi64 >> (8 * (k - 8)))) & 0xFFull) | TF_EXEC);
         ip += len;
         // Rotate(1, NUM_NOPS): per 2-bit digit 0->1, 1->2, 2->0
         const uint32_t dl = lab & 0x55555u, dh = (lab >> 1) & 0x55555u;
@@ -1048,19 +981,11 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
       const int a = __shfl(qa, L), b = __shfl(qb, L);
       uint32_t* TL32 = lds32 + L * (STRIDE / 4);
       const uint8_t* TL = lds + L * STRIDE;
-      // lane L's memory word w / site i wherever it lives (split memory)
-      const int cL = __shfl(cell, L);
-      auto tlw = [&](int w) -> uint32_t { return (!SPLIT || w < PW) ? TL32[w] : ld_sync_u32(gsite(cL, 4 * w)); };
-      auto tlb = [&](int i) -> uint32_t { return (!SPLIT || i < P) ? (uint32_t)TL[i] : ld_sync_u8(gsite(cL, i)); };
       if (kind == RQ_FILL) {
-        // Allocate_Main: new sites [a, b) get op 0 (ALLOC_METHOD 0/1); in the
-        // HBM part a word wholly at or above a is stored whole (its bytes past
-        // b are past the memory)
+        // Allocate_Main: new sites [a, b) get op 0 (ALLOC_METHOD 0/1)
         for (int w = (a >> 2) + lane; (w << 2) < b; w += 64) {
           const uint32_t keep = byte_mask(w << 2, a, b);
-          if (!SPLIT || w < PW) TL32[w] = (TL32[w] & ~keep) | (fill4 & keep);
-          else if ((w << 2) >= a) st_async_u32(gsite(cL, 4 * w), fill4);
-          else st_async_u32(gsite(cL, 4 * w), (tlw(w) & ~keep) | (fill4 & keep));
+          TL32[w] = (TL32[w] & ~keep) | (fill4 & keep);
         }
       } else if (kind == RQ_SEARCH) {
         // FindLabel(0) -> FindLabel_Forward(label, memory, 0) (:1177-1295).
@@ -1074,7 +999,7 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
         const int len = a;
         const uint32_t rot = (uint32_t)b;
         const int ML = __shfl(M, L);
-        const bool run0_ok = len < ML && (tlb(len) & CODE_MASK) < 3;
+        const bool run0_ok = len < ML && (TL[len] & CODE_MASK) < 3;
         int fpos = -1;
         for (int base = 0; base < ML && fpos < 0; base += 64) {
           const int j = base + lane;
@@ -1082,8 +1007,8 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
           if (m) {
             const int st = j - len + 1;
             const int w0 = st >> 2;
-            const uint64_t lo64 = ((uint64_t)tlw(w0 + 1) << 32) | (uint64_t)tlw(w0);
-            const uint64_t hi64 = ((uint64_t)tlw(w0 + 3) << 32) | (uint64_t)tlw(w0 + 2);
+            const uint64_t lo64 = ((uint64_t)TL32[w0 + 1] << 32) | (uint64_t)TL32[w0];
+            const uint64_t hi64 = ((uint64_t)TL32[w0 + 3] << 32) | (uint64_t)TL32[w0 + 2];
             const int b0 = st & 3;
             for (int i = 0; i < len; i++) {
               const int k = b0 + i;
@@ -1106,7 +1031,7 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
         // calcExecutedSize (cpu/cHardwareBase.cc:130-138), calcCopiedSize (cpu/cHardwareCPU.cc:1765-1772)
         int ne = 0, nc = 0;
         for (int w = lane; (w << 2) < div + child; w += 64) {
-          const uint32_t v = tlw(w);
+          const uint32_t v = TL32[w];
           ne += __popc(v & (TF_EXEC * 0x01010101u) & byte_mask(w << 2, 0, div));
           nc += __popc(v & (TF_COPIED * 0x01010101u) & byte_mask(w << 2, div, div + child));
         }
@@ -1592,13 +1517,13 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
               uint32_t wd = 0;
 #pragma unroll
               for (int q = 0; q < 4; q++)
-                wd |= (uint32_t)((tlb(4 * w + q) & TF_EXEC) ? '+' : '-') << (8 * q);
+                wd |= (uint32_t)((TL[4 * w + q] & TF_EXEC) ? '+' : '-') << (8 * q);
               st_async_u32(fl + 4 * w, wd);
             }
             for (int w = lane; (w << 2) < child; w += 64) {
               uint32_t wd = 0;
 #pragma unroll
-              for (int q = 0; q < 4; q++) wd |= (uint32_t)(tlb(div + 4 * w + q) & CODE_MASK) << (8 * q);
+              for (int q = 0; q < 4; q++) wd |= (uint32_t)(TL[div + 4 * w + q] & CODE_MASK) << (8 * q);
               st_async_u32(ch + 4 * w, wd);
             }
           } else if (mode == AVGPU_MODE_WORLD && rec >= 0) {
@@ -1610,7 +1535,7 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
             const uint32_t dsh = (uint32_t)(div & 3) * 8u;
             for (int w = lane; (w << 2) < child; w += 64) {
               const int a = (div >> 2) + w;                 // aligned words around sites div+4w ..
-              const uint32_t lo = tlw(a), hi = tlw(a + 1);
+              const uint32_t lo = TL32[a], hi = TL32[a + 1];
               const uint32_t v = dsh ? ((lo >> dsh) | (hi << (32u - dsh))) : lo;
               st_async_u32(g + 4 * w, v & 0x3F3F3F3Fu & byte_mask(w << 2, 0, child));
             }
@@ -1630,7 +1555,7 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
               for (int i = 0; i < M; i++) npar += draw_p(W.th_par_site, W.p_par_site) ? 1 : 0;
               for (int i = 0; i < npar; i++) {
                 const int site = (int)draw_below((uint32_t)M);
-                tput(site, (tget(site) & ~CODE_MASK) | rand_code());
+                T[site] = (uint8_t)((T[site] & ~CODE_MASK) | rand_code());
               }
             }
             if (W.th_par_ins) {
@@ -1647,10 +1572,8 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
                 nins = nfit;
               }
               if (nins > 0) {
-                // (the child's copy-out has read those bytes; split memory:
-                // in the HBM tape, clear of the memory's M + nins sites there)
-                int32_t* srt = SPLIT ? reinterpret_cast<int32_t*>(gsite(cell, S - 4 * nins))
-                                     : reinterpret_cast<int32_t*>(T + S - 4 * nins);
+                // (the child's copy-out has read those bytes)
+                int32_t* srt = reinterpret_cast<int32_t*>(T + S - 4 * nins);
                 for (int i = 0; i < nins; i++) {
                   const int site = (int)draw_below((uint32_t)M + 1u);
                   int j = i;
@@ -1660,8 +1583,8 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
                 for (int i = nins - 1; i >= 0; i--) {
                   const int pos = srt[i];
                   const int code = rand_code();
-                  for (int k = M; k > pos; k--) tput(k, tget(k - 1));
-                  tput(pos, code);
+                  for (int k = M; k > pos; k--) T[k] = T[k - 1];
+                  T[pos] = (uint8_t)code;
                   M++;
                 }
               }
@@ -1672,18 +1595,14 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
               if (M - ndel < g_min) ndel = M - g_min;
               for (int i = 0; i < ndel; i++) {
                 const int site = (int)draw_below((uint32_t)M);
-                for (int k = site; k < M - 1; k++) tput(k, tget(k + 1));
+                for (int k = site; k < M - 1; k++) T[k] = T[k + 1];
                 M--;
               }
             }
           }
           // parent ClearFlags over its remaining sites, empty stacks
           const int pmem = __shfl(M, L);
-          for (int w = lane; (w << 2) < pmem; w += 64) {
-            if (!SPLIT || w < PW) TL32[w] &= 0x3F3F3F3Fu;
-            else st_async_u32(gsite(cL, 4 * w), tlw(w) & 0x3F3F3F3Fu);
-          }
-          if (lane == L) hic = true;                          // every executed flag cleared
+          for (int w = lane; (w << 2) < pmem; w += 64) TL32[w] &= 0x3F3F3F3Fu;
           if (VSTK) {
             if (lane == L) {
 #pragma unroll
@@ -1745,7 +1664,7 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
     // a death frees the cell for this update's placement (k_allot_total
     // marked the living cells occupied)
     if (mode == AVGPU_MODE_WORLD && alive0 && !alive) W.occ[cell] = 0;
-    W.ctl[cell] = (ctl & ~(CTL_FRESH | CTL_HICLEAN)) | (sdie ? CTL_SPECDIE : 0u) | (hic ? CTL_HICLEAN : 0u);
+    W.ctl[cell] = (ctl & ~CTL_FRESH) | (sdie ? CTL_SPECDIE : 0u);
     W.mem_size[cell] = M;
     if (serial) W.sctx[2] = kct;                             // the context stream moved on
     else W.rng[2 * N + cell] = kct;
@@ -1870,14 +1789,13 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
 // class 0 must keep 2 waves per SIMD (its LDS admits 7 blocks per CU): the
 // second bound caps it at 256 registers (VGPR + AGPR)
 template <int S, bool REC, bool C0W = false, bool SIMPLE = false, bool DEF = false, bool RES = false>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((S == CLASS0_SIZE) ? 3 : 1))) void k_interpret(const DevWorld* __restrict__ Wp, int cls, int row, int mode,
+__global__ __launch_bounds__(64, (S == CLASS0_SIZE) ? 2 : 1) void k_interpret(const DevWorld* __restrict__ Wp, int cls, int row, int mode,
                                                   int64_t first, int64_t count, int sorted, int lpw) {
   constexpr int TAB_WORDS = 128 + 64 + 16 + 64 + AVGPU_MAX_REACTIONS * RT_STRIDE + 64;
   // class 0: stacks in VGPRs, tables in global memory -- only the tapes in LDS
   constexpr int STK = (S == CLASS0_SIZE) ? 0 : 2 * AVGPU_STACK_SIZE * 64;
   constexpr int TAB = (S == CLASS0_SIZE) ? 0 : TAB_WORDS;     // class 0: tapes only
-  // (+ 4 words: the spare word tput_hot writes for a site in class 0's HBM part)
-  __shared__ __attribute__((aligned(16))) uint32_t lds32[64 * tape_stride(S) / 4 + 4 + STK + TAB];
+  __shared__ __attribute__((aligned(16))) uint32_t lds32[64 * tape_stride(S) / 4 + STK + TAB];
   if (cls == 0) {
     // sorted windows: the 32 chunks of a window run on one XCD (blocks are
     // dealt to the 8 XCDs round robin), so its state lines meet in one L2

@@ -114,7 +114,7 @@ __global__ void k_set_orgs(DevWorld W, int64_t first, int64_t count, const uint8
   // registers, heads, label, counters, buffers, task counts, stacks: zero
   int32_t* x = W.xs + c * XS_WORDS;
   for (int k = 0; k < XS_WORDS; k++) x[k] = 0;
-  W.ctl[c] = CTL_ALIVE | CTL_HICLEAN;      // (codes only: no flags)
+  W.ctl[c] = CTL_ALIVE;
   W.mem_size[c] = len;
   int mx = 0;
   if (W.death_method > 0) {                 // cOrganism::initialize (main/cOrganism.cc:216-236)
@@ -913,39 +913,52 @@ __device__ __forceinline__ bool place_pick_one(const DevWorld& W, int64_t r, int
 #define QUEUE_LOOP(i) \
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, _qn = queue_len(W); i < _qn; \
        i += (int64_t)gridDim.x * blockDim.x)
-// The divide mutations (k_place_pick_mut, k_tile_prep): wave w of nwaves
-// scans MUT_PER_WAVE queue entries at a time -- lane k loads entry k's five
-// edit words and both lengths -- and applies the ~10 % that have edits one
-// after the other, each from the words already in hand (apply_edits_core).
-// (One entry per wave over 65536 waves instead cost 71 us for the fused
-// launch against 59: profiles/r04g_tail_per_update.txt.)
+// The divide mutations (k_place_pick_mut, k_tile_prep), by 256-thread blocks:
+// block b of nb scans MUT_PER_BLOCK queue entries at a time -- lane k of each
+// wave loads one entry's five edit words and both lengths -- and lists the
+// ~10 % that have edits in LDS; the block's four waves then apply the list
+// round robin, each genome from the words in hand (apply_edits_core).  A
+// wave that applied its own 8 entries' edits ran up to ~5 genomes one after
+// the other (the launch's longest wave, 36 us: profiles/r04f_split_*); the
+// block's pool of 32 caps a wave at ~2.  (One entry per wave over 65536
+// waves instead: 71 us for the fused launch, profiles/r04g_*.)
 #define MUT_PER_WAVE 8
-__device__ __forceinline__ void mutation_waves(const DevWorld& W, int64_t wave, int64_t nwaves, uint8_t* child) {
+#define MUT_PER_BLOCK (4 * MUT_PER_WAVE)
+__device__ __forceinline__ void mutation_block(const DevWorld& W, int64_t blk, int64_t nblk,
+                                               uint8_t (*child)[TAPE_SLOT + 16]) {
+  __shared__ int ml[MUT_PER_BLOCK][8];   // record (2 words), e0..e4, len0 | len << 16
+  __shared__ int mn;
   const int nb = queue_len(W);
-  const int lane = threadIdx.x & 63;
-  for (int64_t q0 = wave * MUT_PER_WAVE; q0 < nb; q0 += nwaves * MUT_PER_WAVE) {
-    const int64_t q = q0 + lane;
-    int64_t r = 0;
-    int e[5] = {0, 0, 0, 0, 0}, l0 = 0, l1 = 0;
-    bool any = false;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  for (int64_t q0 = blk * MUT_PER_BLOCK; q0 < nb; q0 += nblk * MUT_PER_BLOCK) {   // block-uniform
+    if (threadIdx.x == 0) mn = 0;
+    __syncthreads();
+    const int64_t q = q0 + wv * MUT_PER_WAVE + lane;
     if (lane < MUT_PER_WAVE && q < nb) {
-      r = rec_of(W, q);
+      const int64_t r = rec_of(W, q);
+      int e[5];
 #pragma unroll
       for (int k = 0; k < 5; k++) e[k] = W.b_edit[(int64_t)k * W.rcap + r];
-      l0 = W.b_len0[r];
-      l1 = W.b_len[r];
+      const int l0 = W.b_len0[r], l1 = W.b_len[r];
       int x = e[0] | e[1] | e[2] | e[3] | e[4];
       if (W.seg_any)
         for (int k = 0; k < NSEG; k++) x |= W.b_pcnt[(int64_t)k * W.rcap + r];
-      any = x != 0;
-    }
-    for (unsigned long long m = __ballot(any); m; m &= m - 1ull) {
-      const int L = __ffsll((long long)m) - 1;
-      int eL[5];
+      if (x) {
+        const int i = atomicAdd(&mn, 1);
+        ml[i][0] = (int)(uint32_t)r; ml[i][1] = (int)(r >> 32);
 #pragma unroll
-      for (int k = 0; k < 5; k++) eL[k] = __shfl(e[k], L);
-      apply_edits_core(W, (int64_t)__shfl((long long)r, L), eL, __shfl(l0, L), __shfl(l1, L), child);
+        for (int k = 0; k < 5; k++) ml[i][2 + k] = e[k];
+        ml[i][7] = l0 | (l1 << 16);
+      }
     }
+    __syncthreads();
+    const int n = mn;
+    for (int i = wv; i < n; i += 4) {
+      const int64_t r = (int64_t)(uint32_t)ml[i][0] | ((int64_t)ml[i][1] << 32);
+      const int e[5] = {ml[i][2], ml[i][3], ml[i][4], ml[i][5], ml[i][6]};
+      apply_edits_core(W, r, e, ml[i][7] & 0xFFFF, ml[i][7] >> 16, child[wv]);
+    }
+    __syncthreads();
   }
 }
 
@@ -1015,8 +1028,7 @@ __global__ __launch_bounds__(256) void k_place_pick_mut(DevWorld W, int pblocks,
     return;
   }
   pblocks += fblocks;
-  const int wv = threadIdx.x >> 6;
-  mutation_waves(W, (int64_t)(bid - pblocks) * 4 + wv, (int64_t)(nblocks - pblocks) * 4, child[wv]);
+  mutation_block(W, bid - pblocks, nblocks - pblocks, child);
 }
 
 
@@ -1036,8 +1048,7 @@ __global__ __launch_bounds__(256) void k_tile_prep(DevWorld W, int mblocks, int 
     return;
   }
   if ((int)blockIdx.x < mblocks) {
-    const int wv = threadIdx.x >> 6;
-    mutation_waves(W, (int64_t)blockIdx.x * 4 + wv, (int64_t)mblocks * 4, child[wv]);
+    mutation_block(W, blockIdx.x, mblocks, child);
     return;
   }
   const int X = W.world_x;

@@ -701,7 +701,9 @@ __global__ __launch_bounds__(1024) void k_window_count(DevWorld W) {
       // class-0 cells by k_allot's tag: the list classes on the aux streams
       // rewrite budget / mem_size of their own cells while this kernel runs
       const bool c0 = W.aclass[c] == 0;
-      bucket[h] = c0 ? SORT_BUCKETS - 2 - min(W.budget[c], SORT_BUCKETS - 2) : SORT_BUCKETS - 1;
+      // (clamped both ways: a bucket outside the histogram would place the
+      // cell outside its window of W.order)
+      bucket[h] = c0 ? SORT_BUCKETS - 2 - min(max(W.budget[c], 0), SORT_BUCKETS - 2) : SORT_BUCKETS - 1;
       atomicAdd(&hist[bucket[h]], 1);
     }
   }
@@ -1227,9 +1229,9 @@ __global__ __launch_bounds__(64) void k_activate(DevWorld W, int fused) {
       const unsigned long long c3 = W.claim_r[3][tgt];
       won = W.owner[tgt] == (int)i && !(c3 != 0ull && key_time(c3) >= t);
     }
-    if (won && tgt >= W.n) continue;          // sent to the neighbouring tile
     if (!won) { over++; continue; }
-    if (b.len < 0 || b.len > AVGPU_MAX_GENOME) { bad++; continue; }
+    if (b.len < 0 || b.len > AVGPU_MAX_GENOME) { bad++; continue; }   // (k_halo_pack skips it too)
+    if (tgt >= W.n) continue;                 // sent to the neighbouring tile
     born++;
     setup_child_lane(W, tgt, b, W.b_genome + i * TAPE_SLOT);
   }
@@ -1266,7 +1268,11 @@ __global__ __launch_bounds__(64) void k_halo_pack(DevWorld W) {
       const int64_t i = rec_of(W, q);
       const int tgt = W.b_target[i];
       const int8_t st = W.b_state[i];
-      if (st >= BS_WON && st < BS_WON + 4 && tgt >= W.n && W.owner[tgt] == (int)i) mine = i;
+      // (a target past the ghost rows or a length out of range is a corrupt
+      // record: counted in k_activate, which sees the same fields, never sent)
+      if (st >= BS_WON && st < BS_WON + 4 && tgt >= W.n && (int64_t)tgt < W.n + 2 * (int64_t)X &&
+          W.b_len[i] >= 0 && W.b_len[i] <= AVGPU_MAX_GENOME && W.owner[tgt] == (int)i)
+        mine = i;
     }
     for (unsigned long long m = __ballot(mine >= 0); m; m &= m - 1ull) {
     const int64_t i = (int64_t)__shfl((long long)mine, __ffsll((long long)m) - 1);

@@ -131,3 +131,28 @@ def test_print_status_format(golden):
     # h-alloc grew the memory to 300 and put its old size in AX
     assert t1[0].startswith("2 IP:1 (") and t1[1].startswith("AX:100 [0x64]")
     assert t1[5].startswith("  Mem (300):")
+
+
+@pytest.mark.parametrize("allow_parent", [0, 1])
+def test_birth_method3_full_grid_oracle(golden, allow_parent):
+    """The oracle's BIRTH_METHOD 3 on a full 16x16 grid (no empty neighbour
+    anywhere): ALLOW_PARENT 0 drops every offspring and the parents live
+    (cPopulation::ActivateOffspring, main/cPopulation.cc:706-713); ALLOW_PARENT
+    1 puts each offspring into its parent's cell (PositionOffspring :5407)."""
+    import parity_util as pu
+    ov = {"WORLD_X": 16, "WORLD_Y": 16, "BIRTH_METHOD": 3, "ALLOW_PARENT": allow_parent}
+    iset, env, cfg = pu.load_env(golden, overrides=ov, seed=29)
+    n = cfg.world_x * cfg.world_y
+    orc = ol.Backend("oracle", cfg, iset, env, ncells=n)
+    anc = files.read_org(os.path.join(golden, "default-heads.org"), iset)
+    orc.set_orgs(0, [anc] * n, deterministic=False)
+    dropped = births = 0
+    for _ in range(30):
+        s = orc.run_update()
+        dropped += s.births_dropped
+        births += s.births
+        assert s.num_organisms == n and s.deaths == 0
+    if allow_parent:
+        assert births > 0 and dropped == 0
+    else:
+        assert dropped > 0 and births == 0

@@ -353,3 +353,38 @@ def test_trace_every_instruction(golden):
         orc.step(0, n, uniform=1, mode=capi.MODE_FROZEN)
         gpu.step(0, n, uniform=1, mode=capi.MODE_FROZEN)
     assert sum(a[i].num_divides for i in range(n)) > 0
+
+
+@pytest.mark.parametrize("allow_parent", [0, 1])
+def test_birth_method3_full_grid(golden, allow_parent):
+    """BIRTH_METHOD 3 (an empty neighbour, else the parent's cell without a
+    draw; cPopulation::PositionOffspring, main/cPopulation.cc:5407) on a full
+    grid: with ALLOW_PARENT 0 the offspring is never placed and the parent
+    lives (ActivateOffspring :706-713, BS_NO_CELL, counted as dropped); with
+    ALLOW_PARENT 1 it replaces its parent.  Every update's counters equal,
+    then every cell and digest, GPU world == oracle world."""
+    ov = {"WORLD_X": 32, "WORLD_Y": 32, "BIRTH_METHOD": 3, "ALLOW_PARENT": allow_parent}
+    iset, env, cfg = pu.load_env(golden, overrides=ov, seed=29)
+    n = cfg.world_x * cfg.world_y
+    orc = ol.Backend("oracle", cfg, iset, env, ncells=n)
+    gpu = ol.Backend("gpu", cfg, iset, env, ncells=n)
+    anc = files.read_org(os.path.join(golden, "default-heads.org"), iset)
+    for b in (orc, gpu):
+        b.set_orgs(0, [anc] * n, deterministic=False)
+    dropped = births = 0
+    for upd in range(40):
+        so, sg = orc.run_update(), gpu.run_update()
+        for f in ("num_organisms", "insts_executed", "births", "deaths", "divides", "births_dropped",
+                  "births_overwritten", "births_cancelled"):
+            assert getattr(so, f) == getattr(sg, f), (upd, f, getattr(so, f), getattr(sg, f))
+        dropped += so.births_dropped
+        births += so.births
+    if allow_parent:
+        assert births > 0 and dropped == 0
+    else:
+        assert dropped > 0 and births == 0   # the grid stays full of the ancestors
+    a, oa, fa = orc.states(0, n, CAP)
+    b, ob, fb = gpu.states(0, n, CAP)
+    bad = pu.diff_states(a, b, oa, ob, fa, fb, CAP)
+    assert not bad, f"{len(bad)} mismatches: {bad[:5]}"
+    assert gpu.counters(cumulative=1)[capi.CNT_BAD_RECORD] == 0

@@ -1,11 +1,11 @@
 // resources.hip -- environment resources around the interpreter (config 5):
-//   k_res_step<true>     one cSpatialResCount step of a resource, fused:
-//                        Source + Sink (main/cSpatialResCount.cc:341-394),
+//   k_res_step_tiled     one cSpatialResCount step of every resource without
+//                        CELL entries, fused: Source + Sink (main/cSpatialResCount.cc:341-394),
 //                        FlowAll / FlowMatter (:323-338, main/cResourceCount.cc:40-110),
-//                        StateAll (:307-314), double-buffered
+//                        StateAll (:307-314), double-buffered, by LDS tiles
 //   k_res_spatial_rates  Source + Sink into res_delta  } resources with CELL
 //   k_res_cell_rates     CellInflow + CellOutflow      } entries: then
-//                        (:356-404), list order        } k_res_step<false>
+//                        (:356-404), list order        } k_res_step
 //   k_res_global_begin   DoNonSpatialUpdates over one update   (main/cResourceCount.cc:757-827)
 //   k_res_global_end     the update's consumption of global resources
 //   k_res_pack / k_res_settle   strip tiles: edge rows out; summed consumption in
@@ -146,32 +146,30 @@ __device__ __forceinline__ void cswap(int64_t (&key)[8], double (&val)[8]) {
 struct ResIds {
   int r[AVGPU_MAX_RESOURCES];
 };
-template <bool FUSED>
-__global__ void k_res_step(DevWorld W, ResIds ids) {
-  const int c = (int)(blockIdx.x * blockDim.x + threadIdx.x);   // n < 2^31 (avgpu_load_resources)
-  if (c >= W.n) return;
-  const int r = ids.r[blockIdx.y];
-  const ResParam P = W.res_param[r];
-  const int X = W.world_x, Y = W.world_y;
-  const double* amt = W.res_amount + (int64_t)P.slot * W.n;
-  const int ly = (int)((unsigned)c / (unsigned)X), x = c - ly * X, y = W.row0 + ly;
-  const double a_c = amt[c];
-  double d;
-  if (FUSED) {
-    d = 0.0;
-    const int nin = P.in_all ? 1 : cover(y, P.in_y1, P.in_y2, Y) * cover(x, P.in_x1, P.in_x2, X);
-    for (int k = 0; k < nin; k++) d = __dadd_rn(d, P.in_share);
-    if (P.has_sink) {
-      const int nout = P.out_all ? 1 : cover(y, P.out_y1, P.out_y2, Y) * cover(x, P.out_x1, P.out_x2, X);
-      const double dec = fmax(__dmul_rn(a_c, P.sink_frac), 0.0);
-      for (int k = 0; k < nout; k++) d = __dadd_rn(d, -dec);
-    }
-  } else {
-    d = W.res_delta[c];
+
+// Source + Sink of cell (x, y) (main/cSpatialResCount.cc:341-394): the rate
+// the flows are added to
+__device__ __forceinline__ double res_source_sink(const ResParam& P, double a_c, int x, int y, int X, int Y) {
+  double d = 0.0;
+  const int nin = P.in_all ? 1 : cover(y, P.in_y1, P.in_y2, Y) * cover(x, P.in_x1, P.in_x2, X);
+  for (int k = 0; k < nin; k++) d = __dadd_rn(d, P.in_share);
+  if (P.has_sink) {
+    const int nout = P.out_all ? 1 : cover(y, P.out_y1, P.out_y2, Y) * cover(x, P.out_x1, P.out_x2, X);
+    const double dec = fmax(__dmul_rn(a_c, P.sink_frac), 0.0);
+    for (int k = 0; k < nout; k++) d = __dadd_rn(d, -dec);
   }
-  if (P.flows && x >= 1 && x <= X - 2 && y >= 1 && y <= Y - 2) {
-    // interior cell (either geometry): all eight flows exist and the order of
-    // their computing cells is fixed -- NW, N, NE (row above), W, then c
+  return d;
+}
+
+// FlowAll's terms of cell c = (x, y) onto its rate d, read from the amounts in
+// memory: an interior cell's eight flows in their fixed order (NW, N, NE, W
+// computing cells, then c's own E, SE, S, SW), a world-edge cell's through
+// an 8-entry sorting network in increasing (computing cell, k) order of
+// global cell ids like the reference's loop over i
+__device__ __forceinline__ double res_flows(const DevWorld& W, const ResParam& P, const double* amt, int c, int x,
+                                            int y, double a_c, double d) {
+  const int X = W.world_x, Y = W.world_y;
+  if (x >= 1 && x <= X - 2 && y >= 1 && y <= Y - 2) {
     const double a_nw = res_at(W, amt, P.slot, x - 1, y - 1), a_n = res_at(W, amt, P.slot, x, y - 1);
     const double a_ne = res_at(W, amt, P.slot, x + 1, y - 1), a_w = amt[c - 1];
     d = __dadd_rn(d, flow_amt(P, a_nw, a_c, 1, 1, true));
@@ -182,39 +180,121 @@ __global__ void k_res_step(DevWorld W, ResIds ids) {
     d = __dadd_rn(d, -flow_amt(P, a_c, res_at(W, amt, P.slot, x + 1, y + 1), 1, 1, true));
     d = __dadd_rn(d, -flow_amt(P, a_c, res_at(W, amt, P.slot, x, y + 1), 0, 1, false));
     d = __dadd_rn(d, -flow_amt(P, a_c, res_at(W, amt, P.slot, x - 1, y + 1), -1, 1, true));
-  } else if (P.flows) {
-    const int64_t gc = (int64_t)y * X + x;
-    int64_t key[8];
-    double val[8];
-#pragma unroll
-    for (int k = 3; k <= 6; k++) {                     // own pointers: slots 0..3
-      const int dx = (k == 3 || k == 4) ? 1 : (k == 5 ? 0 : -1), dy = (k == 3) ? 0 : 1;
-      int nx, ny;
-      const bool ok = res_ptr(P.geometry, X, Y, x, y, k, nx, ny);
-      key[k - 3] = ok ? gc * 8 + k : INT64_MAX;
-      val[k - 3] = ok ? -flow_amt(P, a_c, res_at(W, amt, P.slot, nx, ny), dx, dy, k == 4 || k == 6) : 0.0;
-    }
-#pragma unroll
-    for (int k = 3; k <= 6; k++) {                     // cells whose pointer k is c: slots 4..7
-      const int dx = (k == 3 || k == 4) ? 1 : (k == 5 ? 0 : -1), dy = (k == 3) ? 0 : 1;
-      const int jx = wrap1(x - dx, X), jy = wrap1(y - dy, Y);
-      int nx, ny;
-      const bool ok = res_ptr(P.geometry, X, Y, jx, jy, k, nx, ny) && nx == x && ny == y;
-      key[k + 1] = ok ? ((int64_t)jy * X + jx) * 8 + k : INT64_MAX;
-      val[k + 1] = ok ? flow_amt(P, res_at(W, amt, P.slot, jx, jy), a_c, dx, dy, k == 4 || k == 6) : 0.0;
-    }
-    // Batcher odd-even merge sort of 8 (19 compare-exchanges)
-    cswap<0, 1>(key, val); cswap<2, 3>(key, val); cswap<4, 5>(key, val); cswap<6, 7>(key, val);
-    cswap<0, 2>(key, val); cswap<1, 3>(key, val); cswap<4, 6>(key, val); cswap<5, 7>(key, val);
-    cswap<1, 2>(key, val); cswap<5, 6>(key, val);
-    cswap<0, 4>(key, val); cswap<1, 5>(key, val); cswap<2, 6>(key, val); cswap<3, 7>(key, val);
-    cswap<2, 4>(key, val); cswap<3, 5>(key, val);
-    cswap<1, 2>(key, val); cswap<3, 4>(key, val); cswap<5, 6>(key, val);
-#pragma unroll
-    for (int a = 0; a < 8; a++)
-      if (key[a] != INT64_MAX) d = __dadd_rn(d, val[a]);
+    return d;
   }
+  const int64_t gc = (int64_t)y * X + x;
+  int64_t key[8];
+  double val[8];
+#pragma unroll
+  for (int k = 3; k <= 6; k++) {                     // own pointers: slots 0..3
+    const int dx = (k == 3 || k == 4) ? 1 : (k == 5 ? 0 : -1), dy = (k == 3) ? 0 : 1;
+    int nx, ny;
+    const bool ok = res_ptr(P.geometry, X, Y, x, y, k, nx, ny);
+    key[k - 3] = ok ? gc * 8 + k : INT64_MAX;
+    val[k - 3] = ok ? -flow_amt(P, a_c, res_at(W, amt, P.slot, nx, ny), dx, dy, k == 4 || k == 6) : 0.0;
+  }
+#pragma unroll
+  for (int k = 3; k <= 6; k++) {                     // cells whose pointer k is c: slots 4..7
+    const int dx = (k == 3 || k == 4) ? 1 : (k == 5 ? 0 : -1), dy = (k == 3) ? 0 : 1;
+    const int jx = wrap1(x - dx, X), jy = wrap1(y - dy, Y);
+    int nx, ny;
+    const bool ok = res_ptr(P.geometry, X, Y, jx, jy, k, nx, ny) && nx == x && ny == y;
+    key[k + 1] = ok ? ((int64_t)jy * X + jx) * 8 + k : INT64_MAX;
+    val[k + 1] = ok ? flow_amt(P, res_at(W, amt, P.slot, jx, jy), a_c, dx, dy, k == 4 || k == 6) : 0.0;
+  }
+  // Batcher odd-even merge sort of 8 (19 compare-exchanges)
+  cswap<0, 1>(key, val); cswap<2, 3>(key, val); cswap<4, 5>(key, val); cswap<6, 7>(key, val);
+  cswap<0, 2>(key, val); cswap<1, 3>(key, val); cswap<4, 6>(key, val); cswap<5, 7>(key, val);
+  cswap<1, 2>(key, val); cswap<5, 6>(key, val);
+  cswap<0, 4>(key, val); cswap<1, 5>(key, val); cswap<2, 6>(key, val); cswap<3, 7>(key, val);
+  cswap<2, 4>(key, val); cswap<3, 5>(key, val);
+  cswap<1, 2>(key, val); cswap<3, 4>(key, val); cswap<5, 6>(key, val);
+#pragma unroll
+  for (int a = 0; a < 8; a++)
+    if (key[a] != INT64_MAX) d = __dadd_rn(d, val[a]);
+  return d;
+}
+
+// One DoSpatialUpdates step of resource r for cell c, double-buffered
+// (res_amount -> res_amount_alt), for a resource with CELL entries: its rate
+// is res_delta (k_res_spatial_rates + k_res_cell_rates), then FlowAll, then
+// StateAll.
+__global__ void k_res_step(DevWorld W, ResIds ids) {
+  const int c = (int)(blockIdx.x * blockDim.x + threadIdx.x);   // n < 2^31 (avgpu_load_resources)
+  if (c >= W.n) return;
+  const int r = ids.r[blockIdx.y];
+  const ResParam P = W.res_param[r];
+  const int X = W.world_x;
+  const double* amt = W.res_amount + (int64_t)P.slot * W.n;
+  const int ly = (int)((unsigned)c / (unsigned)X), x = c - ly * X, y = W.row0 + ly;
+  const double a_c = amt[c];
+  double d = W.res_delta[c];
+  if (P.flows) d = res_flows(W, P, amt, c, x, y, a_c, d);
   W.res_amount_alt[(int64_t)P.slot * W.n + c] = __dadd_rn(a_c, d);
+}
+
+// The same step for the resources without CELL entries (Source + Sink fused),
+// by tiles of RT_X x RT_Y cells: the tile's amounts and a one-cell rim are
+// staged in LDS, every flow the tile's interior cells need is computed ONCE
+// -- the outgoing E, SE, S, SW flows of the tile's cells and of the rim's
+// cells above and beside it -- and each interior cell adds its eight in the
+// fixed order (the per-cell kernel computed each flow twice, once at each
+// end: the step is FP64-VALU bound, 4 divisions by sqrt(2) per cell and
+// flow set).  The same flow_amt on the same amounts: bit for bit the
+// per-cell result.  World-edge cells take res_flows' sorted path.
+#define RT_X 64
+#define RT_Y 8
+__global__ __launch_bounds__(256) void k_res_step_tiled(DevWorld W, ResIds ids) {
+  __shared__ double A[RT_Y + 2][RT_X + 4];        // local rows ty0-1 .. ty0+RT_Y, columns tx0-2 .. tx0+RT_X+1
+  __shared__ double F[4][RT_Y + 1][RT_X + 2];     // E, SE, S, SW of rows ty0-1 .. ty0+RT_Y-1, columns tx0-1 .. tx0+RT_X
+  const int r = ids.r[blockIdx.y];
+  const ResParam P = W.res_param[r];
+  const int X = W.world_x, Y = W.world_y, rows = W.rows;
+  const int tiles_x = (X + RT_X - 1) / RT_X;
+  const int tx0 = (int)(blockIdx.x % (unsigned)tiles_x) * RT_X, ty0 = (int)(blockIdx.x / (unsigned)tiles_x) * RT_Y;
+  const double* amt = W.res_amount + (int64_t)P.slot * W.n;
+  for (int i = threadIdx.x; i < (RT_Y + 2) * (RT_X + 4); i += 256) {
+    const int iy = i / (RT_X + 4), ix = i - iy * (RT_X + 4);
+    const int ly = ty0 - 1 + iy;                  // -1 .. rows: this world's rows and the two beside them
+    double v = 0.0;
+    if (ly >= -1 && ly <= rows) v = res_at(W, amt, P.slot, amod(tx0 - 2 + ix, X), amod(W.row0 + ly, Y));
+    A[iy][ix] = v;
+  }
+  __syncthreads();
+  if (P.flows) {
+    for (int i = threadIdx.x; i < (RT_Y + 1) * (RT_X + 2); i += 256) {
+      const int fy = i / (RT_X + 2), fx = i - fy * (RT_X + 2);
+      const double a = A[fy][fx + 1];
+      F[0][fy][fx] = flow_amt(P, a, A[fy][fx + 2], 1, 0, false);
+      F[1][fy][fx] = flow_amt(P, a, A[fy + 1][fx + 2], 1, 1, true);
+      F[2][fy][fx] = flow_amt(P, a, A[fy + 1][fx + 1], 0, 1, false);
+      F[3][fy][fx] = flow_amt(P, a, A[fy + 1][fx], -1, 1, true);
+    }
+    __syncthreads();
+  }
+  for (int i = threadIdx.x; i < RT_X * RT_Y; i += 256) {
+    const int ty = i / RT_X, tx = i - ty * RT_X;
+    const int lx = tx0 + tx, ly = ty0 + ty;
+    if (lx >= X || ly >= rows) continue;
+    const int c = ly * X + lx, y = W.row0 + ly;
+    const double a_c = A[ty + 1][tx + 2];
+    double d = res_source_sink(P, a_c, lx, y, X, Y);
+    if (P.flows) {
+      if (lx >= 1 && lx <= X - 2 && y >= 1 && y <= Y - 2) {
+        d = __dadd_rn(d, F[1][ty][tx]);          // NW's SE
+        d = __dadd_rn(d, F[2][ty][tx + 1]);      // N's S
+        d = __dadd_rn(d, F[3][ty][tx + 2]);      // NE's SW
+        d = __dadd_rn(d, F[0][ty + 1][tx]);      // W's E
+        d = __dadd_rn(d, -F[0][ty + 1][tx + 1]);
+        d = __dadd_rn(d, -F[1][ty + 1][tx + 1]);
+        d = __dadd_rn(d, -F[2][ty + 1][tx + 1]);
+        d = __dadd_rn(d, -F[3][ty + 1][tx + 1]);
+      } else {
+        d = res_flows(W, P, amt, c, lx, y, a_c, d);
+      }
+    }
+    W.res_amount_alt[(int64_t)P.slot * W.n + c] = __dadd_rn(a_c, d);
+  }
 }
 
 // one update of DoNonSpatialUpdates (main/cResourceCount.cc:814-827): 10000
@@ -285,12 +365,13 @@ void launch_resources_begin(const DevWorld& W, hipStream_t s) {
         one.r[0] = r;
         hipLaunchKernelGGL(k_res_spatial_rates, dim3(rblk(W.n)), dim3(256), 0, s, W, r);
         hipLaunchKernelGGL(k_res_cell_rates, dim3(1), dim3(64), 0, s, W, r);
-        hipLaunchKernelGGL(k_res_step<false>, dim3(rblk(W.n)), dim3(256), 0, s, W, one);
+        hipLaunchKernelGGL(k_res_step, dim3(rblk(W.n)), dim3(256), 0, s, W, one);
       } else {
         fused.r[nf++] = r;
       }
     }
-    if (nf) hipLaunchKernelGGL(k_res_step<true>, dim3(rblk(W.n), nf), dim3(256), 0, s, W, fused);
+    const unsigned tiles = (unsigned)(((W.world_x + RT_X - 1) / RT_X) * ((W.rows + RT_Y - 1) / RT_Y));
+    if (nf) hipLaunchKernelGGL(k_res_step_tiled, dim3(tiles, nf), dim3(256), 0, s, W, fused);
   }
   hipLaunchKernelGGL(k_res_global_begin, dim3(1), dim3(64), 0, s, W, (int)W.res_first);
 }

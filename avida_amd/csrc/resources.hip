@@ -1,11 +1,12 @@
 // resources.hip -- environment resources around the interpreter (config 5):
-//   k_res_step_tiled     one cSpatialResCount step of every resource without
-//                        CELL entries, fused: Source + Sink (main/cSpatialResCount.cc:341-394),
-//                        FlowAll / FlowMatter (:323-338, main/cResourceCount.cc:40-110),
-//                        StateAll (:307-314), double-buffered, by LDS tiles
+//   k_res_step<true>     one cSpatialResCount step of every resource without
+//                        CELL entries (one launch), fused: Source + Sink
+//                        (main/cSpatialResCount.cc:341-394), FlowAll / FlowMatter
+//                        (:323-338, main/cResourceCount.cc:40-110), StateAll
+//                        (:307-314), double-buffered
 //   k_res_spatial_rates  Source + Sink into res_delta  } resources with CELL
 //   k_res_cell_rates     CellInflow + CellOutflow      } entries: then
-//                        (:356-404), list order        } k_res_step
+//                        (:356-404), list order        } k_res_step<false>
 //   k_res_global_begin   DoNonSpatialUpdates over one update   (main/cResourceCount.cc:757-827)
 //   k_res_global_end     the update's consumption of global resources
 //   k_res_pack / k_res_settle   strip tiles: edge rows out; summed consumption in
@@ -216,9 +217,14 @@ __device__ __forceinline__ double res_flows(const DevWorld& W, const ResParam& P
 }
 
 // One DoSpatialUpdates step of resource r for cell c, double-buffered
-// (res_amount -> res_amount_alt), for a resource with CELL entries: its rate
-// is res_delta (k_res_spatial_rates + k_res_cell_rates), then FlowAll, then
-// StateAll.
+// (res_amount -> res_amount_alt): the cell's rate is Source + Sink (FUSED; or
+// res_delta after k_res_spatial_rates + k_res_cell_rates when r has CELL
+// entries), then FlowAll (res_flows), then StateAll.  Every resource without
+// CELL entries steps in one launch (blockIdx.y).  (A tiled variant that staged
+// a 64 x 8 tile and its rim in LDS and computed each flow once instead of at
+// both ends ran at 306 against 138 us per update for the 9 resources of
+// configs[4]: profiles/r04o_res_step_tiled.txt.)
+template <bool FUSED>
 __global__ void k_res_step(DevWorld W, ResIds ids) {
   const int c = (int)(blockIdx.x * blockDim.x + threadIdx.x);   // n < 2^31 (avgpu_load_resources)
   if (c >= W.n) return;
@@ -228,73 +234,9 @@ __global__ void k_res_step(DevWorld W, ResIds ids) {
   const double* amt = W.res_amount + (int64_t)P.slot * W.n;
   const int ly = (int)((unsigned)c / (unsigned)X), x = c - ly * X, y = W.row0 + ly;
   const double a_c = amt[c];
-  double d = W.res_delta[c];
+  double d = FUSED ? res_source_sink(P, a_c, x, y, X, W.world_y) : W.res_delta[c];
   if (P.flows) d = res_flows(W, P, amt, c, x, y, a_c, d);
   W.res_amount_alt[(int64_t)P.slot * W.n + c] = __dadd_rn(a_c, d);
-}
-
-// The same step for the resources without CELL entries (Source + Sink fused),
-// by tiles of RT_X x RT_Y cells: the tile's amounts and a one-cell rim are
-// staged in LDS, every flow the tile's interior cells need is computed ONCE
-// -- the outgoing E, SE, S, SW flows of the tile's cells and of the rim's
-// cells above and beside it -- and each interior cell adds its eight in the
-// fixed order (the per-cell kernel computed each flow twice, once at each
-// end: the step is FP64-VALU bound, 4 divisions by sqrt(2) per cell and
-// flow set).  The same flow_amt on the same amounts: bit for bit the
-// per-cell result.  World-edge cells take res_flows' sorted path.
-#define RT_X 64
-#define RT_Y 8
-__global__ __launch_bounds__(256) void k_res_step_tiled(DevWorld W, ResIds ids) {
-  __shared__ double A[RT_Y + 2][RT_X + 4];        // local rows ty0-1 .. ty0+RT_Y, columns tx0-2 .. tx0+RT_X+1
-  __shared__ double F[4][RT_Y + 1][RT_X + 2];     // E, SE, S, SW of rows ty0-1 .. ty0+RT_Y-1, columns tx0-1 .. tx0+RT_X
-  const int r = ids.r[blockIdx.y];
-  const ResParam P = W.res_param[r];
-  const int X = W.world_x, Y = W.world_y, rows = W.rows;
-  const int tiles_x = (X + RT_X - 1) / RT_X;
-  const int tx0 = (int)(blockIdx.x % (unsigned)tiles_x) * RT_X, ty0 = (int)(blockIdx.x / (unsigned)tiles_x) * RT_Y;
-  const double* amt = W.res_amount + (int64_t)P.slot * W.n;
-  for (int i = threadIdx.x; i < (RT_Y + 2) * (RT_X + 4); i += 256) {
-    const int iy = i / (RT_X + 4), ix = i - iy * (RT_X + 4);
-    const int ly = ty0 - 1 + iy;                  // -1 .. rows: this world's rows and the two beside them
-    double v = 0.0;
-    if (ly >= -1 && ly <= rows) v = res_at(W, amt, P.slot, amod(tx0 - 2 + ix, X), amod(W.row0 + ly, Y));
-    A[iy][ix] = v;
-  }
-  __syncthreads();
-  if (P.flows) {
-    for (int i = threadIdx.x; i < (RT_Y + 1) * (RT_X + 2); i += 256) {
-      const int fy = i / (RT_X + 2), fx = i - fy * (RT_X + 2);
-      const double a = A[fy][fx + 1];
-      F[0][fy][fx] = flow_amt(P, a, A[fy][fx + 2], 1, 0, false);
-      F[1][fy][fx] = flow_amt(P, a, A[fy + 1][fx + 2], 1, 1, true);
-      F[2][fy][fx] = flow_amt(P, a, A[fy + 1][fx + 1], 0, 1, false);
-      F[3][fy][fx] = flow_amt(P, a, A[fy + 1][fx], -1, 1, true);
-    }
-    __syncthreads();
-  }
-  for (int i = threadIdx.x; i < RT_X * RT_Y; i += 256) {
-    const int ty = i / RT_X, tx = i - ty * RT_X;
-    const int lx = tx0 + tx, ly = ty0 + ty;
-    if (lx >= X || ly >= rows) continue;
-    const int c = ly * X + lx, y = W.row0 + ly;
-    const double a_c = A[ty + 1][tx + 2];
-    double d = res_source_sink(P, a_c, lx, y, X, Y);
-    if (P.flows) {
-      if (lx >= 1 && lx <= X - 2 && y >= 1 && y <= Y - 2) {
-        d = __dadd_rn(d, F[1][ty][tx]);          // NW's SE
-        d = __dadd_rn(d, F[2][ty][tx + 1]);      // N's S
-        d = __dadd_rn(d, F[3][ty][tx + 2]);      // NE's SW
-        d = __dadd_rn(d, F[0][ty + 1][tx]);      // W's E
-        d = __dadd_rn(d, -F[0][ty + 1][tx + 1]);
-        d = __dadd_rn(d, -F[1][ty + 1][tx + 1]);
-        d = __dadd_rn(d, -F[2][ty + 1][tx + 1]);
-        d = __dadd_rn(d, -F[3][ty + 1][tx + 1]);
-      } else {
-        d = res_flows(W, P, amt, c, lx, y, a_c, d);
-      }
-    }
-    W.res_amount_alt[(int64_t)P.slot * W.n + c] = __dadd_rn(a_c, d);
-  }
 }
 
 // one update of DoNonSpatialUpdates (main/cResourceCount.cc:814-827): 10000
@@ -365,13 +307,12 @@ void launch_resources_begin(const DevWorld& W, hipStream_t s) {
         one.r[0] = r;
         hipLaunchKernelGGL(k_res_spatial_rates, dim3(rblk(W.n)), dim3(256), 0, s, W, r);
         hipLaunchKernelGGL(k_res_cell_rates, dim3(1), dim3(64), 0, s, W, r);
-        hipLaunchKernelGGL(k_res_step, dim3(rblk(W.n)), dim3(256), 0, s, W, one);
+        hipLaunchKernelGGL(k_res_step<false>, dim3(rblk(W.n)), dim3(256), 0, s, W, one);
       } else {
         fused.r[nf++] = r;
       }
     }
-    const unsigned tiles = (unsigned)(((W.world_x + RT_X - 1) / RT_X) * ((W.rows + RT_Y - 1) / RT_Y));
-    if (nf) hipLaunchKernelGGL(k_res_step_tiled, dim3(tiles, nf), dim3(256), 0, s, W, fused);
+    if (nf) hipLaunchKernelGGL(k_res_step<true>, dim3(rblk(W.n), nf), dim3(256), 0, s, W, fused);
   }
   hipLaunchKernelGGL(k_res_global_begin, dim3(1), dim3(64), 0, s, W, (int)W.res_first);
 }

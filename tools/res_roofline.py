@@ -22,7 +22,7 @@ def main():
         avg_ns = float(r["AverageNs"])
         b = 16.0 * cells * nres
         gbs = b / (avg_ns * 1e-9) / 1e9
-        key = re.search(r"k_res_step<[^>]*>", name).group(0)
+        key = re.search(r"k_res_step\w*(<[^>]*>)?", name).group(0)
         out[key] = {
             "calls": int(r["Calls"]), "avg_us": avg_ns / 1e3, "bytes_per_launch": b,
             "achieved_GBs": gbs, "peak_GBs": peak, "frac": gbs / peak}

@@ -505,9 +505,16 @@ __global__ __launch_bounds__(1024) void k_block_counts(DevWorld W, const double*
   }
   __syncthreads();
   if (mode == 3) return;
+  // top down, only the nodes over this world's blocks [b0, b0 + nloc) (a
+  // node's count depends on its ancestors' alone): a strip of T splits its
+  // own subtree and the path to it, not the whole gathered world's tree
+  // (T x the work; 65536 blocks at configs[3])
+  const int64_t b0 = mode == 1 ? W.cell0 / 256 : 0;
+  const int64_t nloc = (W.n + 255) / 256;
   for (int l = 0; l < L; l++) {
     const int64_t w0 = (int64_t)1 << l;
-    for (int64_t i = tid; i < w0; i += 1024) {
+    const int64_t ilo = b0 >> (L - l), ihi = (b0 + nloc - 1) >> (L - l);
+    for (int64_t i = ilo + tid; i <= ihi; i += 1024) {
       const int64_t h = w0 + i;
       const long long n = cnt[h];
       const long long left = binom_draw(n, __ddiv_rn(scr[2 * h], scr[h]),
@@ -517,8 +524,6 @@ __global__ __launch_bounds__(1024) void k_block_counts(DevWorld W, const double*
     }
     __syncthreads();
   }
-  const int64_t b0 = mode == 1 ? W.cell0 / 256 : 0;
-  const int64_t nloc = (W.n + 255) / 256;
   for (int64_t j = tid; j < nloc; j += 1024) W.blk_count[j] = cnt[P + b0 + j];
 }
 

@@ -566,7 +566,9 @@ int avgpu_set_global_totals(avgpu_world* w, double total_merit, int64_t total_or
  *   avgpu_tile_partials(w, part)         all_gather(part) in tile order
  *                                        [exchange(resource rows): spatial resources]
  *   avgpu_tile_begin(w, gathered, T)     exchange(halo)
- *   for round 0..3:
+ *   avgpu_tile_place(w, 0, 0)            exchange(halo)
+ *   avgpu_tile_place(w, 0, 3)            exchange(halo)
+ *   for round 1..3:
  *     avgpu_tile_place(w, round, 0)      exchange(halo)
  *   avgpu_tile_place(w, 3, 1)            exchange(records) issued ...
  *   avgpu_tile_place(w, 3, 2)            ... and running beside this launch
@@ -600,10 +602,14 @@ int avgpu_tile_begin(avgpu_world* w, const double* dev_gathered, int ntiles);
  * claims both strips sent (a cell of an edge row is claimed only from the two
  * strips it touches, so both resolve it alike) and picks round `round`,
  * writing its claims on the ghost rows and on the own edge rows into the halo
- * send buffers.  After round 3: phase 1 resolves round 3 and packs the
- * ghost-row winners into the record buffers, phase 2 activates this tile's
- * own winners (it reads no record buffer: it may run while the records
- * travel). */
+ * send buffers.  Round 0, phase 0 picks and sends the kill times of its picks
+ * on the ghost rows; round 0, phase 3 (after that exchange) cancels the
+ * births whose parent's cell a pick of an earlier birth kills, here or from
+ * the neighbour, and claims the others' round-0 targets (time-ordered
+ * placement).  After round 3: phase 1 resolves round 3 and packs
+ * the ghost-row winners into the record buffers, phase 2 activates this
+ * tile's own winners (it reads no record buffer: it may run while the
+ * records travel). */
 int avgpu_tile_place(avgpu_world* w, int round, int phase);
 /* activation of the received records; statistics (out may be NULL: see
  * avgpu_run_update) */

@@ -446,12 +446,33 @@ __global__ __launch_bounds__(256) void k_merit_partial(DevWorld W, double* parti
 // N_total)); mode 3: the totals only (totals[0..1] = root, N).
 // totals[2] = the weight total INTEGRATED divides by, totals[3] = UD.
 // LDS: the whole tree in the workgroup's LDS (P <= TREE_LDS_P: 2 x 4096 doubles
-// + counts = 128 KiB of gfx950's 160), else in W.tree_scr / tree_cnt
+// + counts = 128 KiB of gfx950's 160).  A larger tree (strips of a world of
+// more than 4096 blocks: the weak-scaling bench at N >= 2, configs[3]) is
+// cut at the level of its 4096-block subtrees ("chunks"): k_tree_up builds
+// every chunk's sums (a workgroup each), k_block_counts runs the tree above
+// the chunk roots (chunked = 1: its leaves are the chunk roots, its output
+// the chunk roots' counts), k_tree_down splits each chunk over this world's
+// blocks (a workgroup each).  The same pairwise sums, the same draws at the
+// same heap nodes: the same counts as one tree (oracle top_tree).  (One
+// workgroup over a 65536-block tree in global memory took 124 us.)
 #define TREE_LDS_P 4096
+#define TREE_C_LOG 12
+// leaf g of the block level (0 past the blocks); alive count into a
+__device__ __forceinline__ double tree_leaf(const double* part, const int32_t* alive_part, int64_t nb, int64_t nbt,
+                                            int mode, int64_t g, long long& a) {
+  if (g >= nbt) return 0.0;
+  if (mode == 1) {
+    const int64_t k = g / nb, j = g - k * nb;
+    a += (long long)part[k * 2 * nb + nb + j];
+    return part[k * 2 * nb + j];
+  }
+  a += alive_part[g];
+  return part[g];
+}
 template <bool LDS>
 __global__ __launch_bounds__(1024) void k_block_counts(DevWorld W, const double* part, const int32_t* alive_part,
                                                        int64_t nb, int ntiles, int L, double* totals,
-                                                       uint32_t update, int mode) {
+                                                       uint32_t update, int mode, int chunked) {
   __shared__ long long s_cnt[1024];
   __shared__ double l_scr[LDS ? 2 * TREE_LDS_P : 1];
   __shared__ long long l_cnt[LDS ? 2 * TREE_LDS_P : 1];
@@ -461,16 +482,12 @@ __global__ __launch_bounds__(1024) void k_block_counts(DevWorld W, const double*
   long long* cnt = LDS ? l_cnt : reinterpret_cast<long long*>(W.tree_cnt);
   long long a = 0;
   for (int64_t g = tid; g < P; g += 1024) {
-    double v = 0.0;
-    if (g < nbt) {
-      if (mode == 1) {
-        const int64_t k = g / nb, j = g - k * nb;
-        v = part[k * 2 * nb + j];
-        a += (long long)part[k * 2 * nb + nb + j];
-      } else {
-        v = part[g];
-        a += alive_part[g];
-      }
+    double v;
+    if (chunked) {                              // the chunk roots of k_tree_up
+      v = W.tree_scr[g];
+      a += W.tree_cnt[g];
+    } else {
+      v = tree_leaf(part, alive_part, nb, nbt, mode, g, a);
     }
     scr[P + g] = v;
   }
@@ -508,12 +525,14 @@ __global__ __launch_bounds__(1024) void k_block_counts(DevWorld W, const double*
   // top down, only the nodes over this world's blocks [b0, b0 + nloc) (a
   // node's count depends on its ancestors' alone): a strip of T splits its
   // own subtree and the path to it, not the whole gathered world's tree
-  // (T x the work; 65536 blocks at configs[3])
+  // (chunked: the leaves are chunks, the range in chunks)
+  const int sh = chunked ? TREE_C_LOG : 0;
   const int64_t b0 = mode == 1 ? W.cell0 / 256 : 0;
   const int64_t nloc = (W.n + 255) / 256;
+  const int64_t lo = b0 >> sh, hi = (b0 + nloc - 1) >> sh;
   for (int l = 0; l < L; l++) {
     const int64_t w0 = (int64_t)1 << l;
-    const int64_t ilo = b0 >> (L - l), ihi = (b0 + nloc - 1) >> (L - l);
+    const int64_t ilo = lo >> (L - l), ihi = hi >> (L - l);
     for (int64_t i = ilo + tid; i <= ihi; i += 1024) {
       const int64_t h = w0 + i;
       const long long n = cnt[h];
@@ -524,7 +543,81 @@ __global__ __launch_bounds__(1024) void k_block_counts(DevWorld W, const double*
     }
     __syncthreads();
   }
-  for (int64_t j = tid; j < nloc; j += 1024) W.blk_count[j] = cnt[P + b0 + j];
+  if (chunked) {
+    for (int64_t j = lo + tid; j <= hi; j += 1024) W.tree_cnt[P + j] = cnt[P + j];
+  } else {
+    for (int64_t j = tid; j < nloc; j += 1024) W.blk_count[j] = cnt[P + b0 + j];
+  }
+}
+
+// a chunk's subtree sums in LDS (t[1 .. 2 C), leaves at C + i), its alive count
+__device__ __forceinline__ long long chunk_sums(double* t, long long* s_cnt, const double* part,
+                                                const int32_t* alive_part, int64_t nb, int64_t nbt, int mode,
+                                                int64_t k) {
+  constexpr int C = 1 << TREE_C_LOG;
+  const int tid = threadIdx.x;
+  long long a = 0;
+  for (int i = tid; i < C; i += 1024) t[C + i] = tree_leaf(part, alive_part, nb, nbt, mode, k * C + i, a);
+  s_cnt[tid] = a;
+  __syncthreads();
+  for (int st = 512; st >= 1; st >>= 1) {
+    if (tid < st) s_cnt[tid] += s_cnt[tid + st];
+    __syncthreads();
+  }
+  for (int l = TREE_C_LOG - 1; l >= 0; l--) {
+    const int w0 = 1 << l;
+    for (int i = tid; i < w0; i += 1024) t[w0 + i] = __dadd_rn(t[2 * (w0 + i)], t[2 * (w0 + i) + 1]);
+    __syncthreads();
+  }
+  return s_cnt[0];
+}
+// chunk k = blockIdx.x: its root's sum -> tree_scr[k], its organisms -> tree_cnt[k]
+__global__ __launch_bounds__(1024) void k_tree_up(DevWorld W, const double* part, const int32_t* alive_part,
+                                                  int64_t nb, int ntiles, int mode) {
+  __shared__ double t[2 << TREE_C_LOG];
+  __shared__ long long s_cnt[1024];
+  const int64_t nbt = mode == 1 ? nb * ntiles : nb;
+  const long long a = chunk_sums(t, s_cnt, part, alive_part, nb, nbt, mode, blockIdx.x);
+  if (threadIdx.x == 0) {
+    W.tree_scr[blockIdx.x] = t[1];
+    W.tree_cnt[blockIdx.x] = a;
+  }
+}
+// chunk k = k0 + blockIdx.x of this world's range: its count (tree_cnt[K + k],
+// k_block_counts chunked) split down its subtree over this world's blocks;
+// node i of local level l is heap node (K + k) 2^l + i
+__global__ __launch_bounds__(1024) void k_tree_down(DevWorld W, const double* part, const int32_t* alive_part,
+                                                    int64_t nb, int ntiles, int mode, int64_t K, uint32_t update) {
+  constexpr int C = 1 << TREE_C_LOG;
+  __shared__ double t[2 * C];
+  __shared__ long long c[2 * C];
+  __shared__ long long s_cnt[1024];
+  const int tid = threadIdx.x;
+  const int64_t nbt = mode == 1 ? nb * ntiles : nb;
+  const int64_t b0 = mode == 1 ? W.cell0 / 256 : 0;
+  const int64_t nloc = (W.n + 255) / 256;
+  const int64_t k = (b0 >> TREE_C_LOG) + blockIdx.x;
+  chunk_sums(t, s_cnt, part, alive_part, nb, nbt, mode, k);
+  if (tid == 0) c[1] = W.tree_cnt[K + k];
+  __syncthreads();
+  // this world's blocks inside the chunk: local leaves [lo, hi]
+  const int64_t g0 = k * C;
+  const int lo = (int)(max(b0, g0) - g0), hi = (int)(min(b0 + nloc, g0 + C) - 1 - g0);
+  for (int l = 0; l < TREE_C_LOG; l++) {
+    const int w0 = 1 << l;
+    const int ilo = lo >> (TREE_C_LOG - l), ihi = hi >> (TREE_C_LOG - l);
+    for (int i = ilo + tid; i <= ihi; i += 1024) {
+      const int h = w0 + i;
+      const long long n = c[h];
+      const uint64_t H = (uint64_t)(K + k) * (uint64_t)w0 + (uint64_t)i;
+      const long long left = binom_draw(n, __ddiv_rn(t[2 * h], t[h]),
+                                        node_draw(W.seed_lo, W.seed_hi, update, SALT_TOP, H));
+      c[2 * h] = left;
+      c[2 * h + 1] = n - left;
+    }
+    __syncthreads();
+  }
+  for (int i = lo + tid; i <= hi; i += 1024) W.blk_count[g0 + i - b0] = c[C + i];
 }
 
 __device__ __forceinline__ void occ_init_cell(const DevWorld& W, int64_t c) {
@@ -1541,10 +1634,22 @@ void launch_classify_uniform(const DevWorld& W, hipStream_t s, int64_t first, in
 
 static void launch_block_counts(const DevWorld& W, hipStream_t s, const double* part, const int32_t* alive,
                                 int64_t nb, int ntiles, int L, double* totals, uint32_t update, int mode) {
-  if (((int64_t)1 << L) <= TREE_LDS_P)
-    hipLaunchKernelGGL(k_block_counts<true>, dim3(1), dim3(1024), 0, s, W, part, alive, nb, ntiles, L, totals, update, mode);
-  else
-    hipLaunchKernelGGL(k_block_counts<false>, dim3(1), dim3(1024), 0, s, W, part, alive, nb, ntiles, L, totals, update, mode);
+  if (((int64_t)1 << L) <= TREE_LDS_P) {
+    hipLaunchKernelGGL(k_block_counts<true>, dim3(1), dim3(1024), 0, s, W, part, alive, nb, ntiles, L, totals, update,
+                       mode, 0);
+    return;
+  }
+  const int Lt = L - TREE_C_LOG;
+  const int64_t K = (int64_t)1 << Lt;
+  hipLaunchKernelGGL(k_tree_up, dim3((unsigned)K), dim3(1024), 0, s, W, part, alive, nb, ntiles, mode);
+  // the K chunk roots' tree in LDS: K <= 4096 for any world of < 2^31 cells
+  // (2^23 blocks at most, so K <= 2^11)
+  hipLaunchKernelGGL(k_block_counts<true>, dim3(1), dim3(1024), 0, s, W, part, alive, nb, ntiles, Lt, totals,
+                     update, mode, 1);
+  if (mode == 3) return;
+  const int64_t b0 = mode == 1 ? W.cell0 / 256 : 0, nloc = (W.n + 255) / 256;
+  const int64_t nk = ((b0 + nloc - 1) >> TREE_C_LOG) - (b0 >> TREE_C_LOG) + 1;
+  hipLaunchKernelGGL(k_tree_down, dim3((unsigned)nk), dim3(1024), 0, s, W, part, alive, nb, ntiles, mode, K, update);
 }
 
 static int tree_levels(int64_t nbt) {

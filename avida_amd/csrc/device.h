@@ -708,7 +708,7 @@ void launch_interpret_classes(const DevWorld& W, const DevWorld* dW, int mode, h
                               hipEvent_t* ev_join = nullptr);
 // class-0 windows: k_allot's budgets sorted (descending) inside windows of
 // SORT_WIN cells, so that a wave's 64 organisms get similar time slices
-#define SORT_WIN 16384
+#define SORT_WIN 32768
 // k_allot_sort's buckets: budgets 0 .. SORT_BUCKETS-3 (larger ones share the
 // last of them), then one bucket for the window's cells that are not class 0
 #define SORT_BUCKETS 258

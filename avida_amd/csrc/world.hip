@@ -783,7 +783,9 @@ __device__ __forceinline__ void window_order(const DevWorld& W, int64_t base, in
 // waves) instead of 2048 took the lane efficiency of the bench's
 // multinomial budgets from 0.94 to 0.98 (tools/budget_spread.py); 16384
 // (256 waves) measured 1.299 ms/step against 1.326-1.389 for 8192 on the
-// same box (profiles/r04e_ab.txt).
+// same box (profiles/r04e_ab.txt), 32768 1.276-1.280 against 1.307 for 16384
+// (class 0 0.945 vs 0.990 ms; 65536: 0.924 ms, but this kernel's 16
+// workgroups cost more than that gains: profiles/r04w_ab.txt).
 __global__ __launch_bounds__(1024) void k_window_count(DevWorld W) {
   __shared__ int hist[SORT_BUCKETS];
   const int tid = threadIdx.x;

@@ -50,7 +50,7 @@ class AvgpuCfg(C.Structure):
         ("merit_default_bonus", C.c_double), ("required_bonus", C.c_double),
         ("seed", C.c_uint64),
         ("divide_slip_prob", C.c_double), ("divide_uniform_prob", C.c_double),
-        ("slip_fill_mode", C.c_int32), ("pad_cfg", C.c_int32),
+        ("slip_fill_mode", C.c_int32), ("sub_updates", C.c_int32),
         ("div_mut_prob", C.c_double), ("parent_mut_prob", C.c_double),
         ("divide_poisson_slip_mean", C.c_double), ("divide_poisson_mut_mean", C.c_double),
         ("divide_poisson_ins_mean", C.c_double), ("divide_poisson_del_mean", C.c_double),

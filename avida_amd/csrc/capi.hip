@@ -275,6 +275,8 @@ std::string unsupported_cfg(const avgpu_cfg& c) {
       c.divide_poisson_trans_mean > 700.0)
     return "DIVIDE_POISSON_*_MEAN above 700 (exp(-mean) underflows)";
   if (c.divide_method != 1) return "DIVIDE_METHOD other than 1 (split)";
+  if (c.sub_updates < 0 || c.sub_updates > 64) return "sub_updates outside 0..64";
+  if (c.sub_updates > 1 && c.slicing_method != 1) return "sub_updates > 1 with SLICING_METHOD other than 1";
   if (c.world_geometry != 1 && c.world_geometry != 2) return "WORLD_GEOMETRY other than 1 (grid) or 2 (torus)";
   if (c.slicing_method < 0 || c.slicing_method > 2) return "SLICING_METHOD other than 0, 1, 2";
   if (c.base_merit_method < 0 || c.base_merit_method > 5) return "BASE_MERIT_METHOD other than 0..5";
@@ -757,6 +759,8 @@ int avgpu_update_run(avgpu_world* w, const double* dev_totals, avgpu_update_stat
   int rc = ready(w);
   if (rc < 0) return rc;
   if (!dev_totals) return fail(AVGPU_EINVAL, "dev_totals is NULL");
+  if (w->cfg.sub_updates > 1)
+    return fail(AVGPU_EUNSUPPORTED, "sub_updates > 1 needs the world's own totals (no handed-in totals, no strips)");
   // every world's {total weight, organisms} -> this world's share of the
   // picks (cMultiProcessWorld::CalculateUpdateSize) and its allotment
   if (dev_totals != w->d_totals)
@@ -783,16 +787,21 @@ int avgpu_run_update(avgpu_world* w, avgpu_update_stats* out) {
     w->use_global = false;
     return avgpu_update_run(w, w->d_totals, out);
   }
-  // total merit, allotment, class lists and the class-0 order: two launches
-  launch_world_begin(w->W, w->stream, w->d_totals, w->d_totals + 8, w->ev_fork, (uint32_t)w->update);
-  after_resources_begin(w);
-  HIPCHK(hipGetLastError());
-  rc = interpret(w, AVGPU_MODE_WORLD, 0, w->W.n, true);
-  if (rc < 0) return rc;
-  // statistics only when asked for: a run without them (out == NULL) leaves
-  // the reduction to avgpu_get_stats / avgpu_stats_vector, or skips it
-  launch_world_post(w->W, w->stream, w->d_stats, out != nullptr);
-  HIPCHK(hipGetLastError());
+  // K sub-updates (avgpu_cfg.sub_updates), each: total merit,
+  // allotment, class lists and the class-0 order; interpretation; placement
+  const int K = w->cfg.sub_updates > 1 ? w->cfg.sub_updates : 1;
+  for (int sub = 0; sub < K; sub++) {
+    launch_world_begin(w->W, w->stream, w->d_totals, w->d_totals + 8, w->ev_fork,
+                       (uint32_t)w->update * (uint32_t)K + (uint32_t)sub, sub, K);
+    if (sub == 0) after_resources_begin(w);
+    HIPCHK(hipGetLastError());
+    rc = interpret(w, AVGPU_MODE_WORLD, 0, w->W.n, true);
+    if (rc < 0) return rc;
+    // statistics only when asked for: a run without them (out == NULL) leaves
+    // the reduction to avgpu_get_stats / avgpu_stats_vector, or skips it
+    launch_world_post(w->W, w->stream, w->d_stats, out != nullptr && sub == K - 1);
+    HIPCHK(hipGetLastError());
+  }
   w->stats_stale = out == nullptr;
   w->update++;
   if (out) return avgpu_get_stats(w, out);
@@ -1328,6 +1337,7 @@ int avgpu_get_resources(avgpu_world* w, double* levels, double* spatial) {
 
 // ---- strip tiles (DESIGN.md "Multi-GPU") ----
 int avgpu_set_tile(avgpu_world* w, int64_t row0, int64_t arena_bytes) {
+  if (w && w->cfg.sub_updates > 1) return fail(AVGPU_EUNSUPPORTED, "sub_updates > 1 on strip tiles");
   if (!w) return fail(AVGPU_EINVAL, "NULL world");
   DevWorld& W = w->W;
   const int64_t X = W.world_x;

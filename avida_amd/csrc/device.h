@@ -713,8 +713,15 @@ void launch_interpret_classes(const DevWorld& W, const DevWorld* dW, int mode, h
 // last of them), then one bucket for the window's cells that are not class 0
 #define SORT_BUCKETS 258
 bool class_timing_all();   // AVGPU_CLASS_TIMING (interp.hip)
+// sub-update `sub` of `nsub` (avgpu_cfg.sub_updates): the
+// resources step and the update's counters are reset at sub 0 only; the key
+// of the scheduler's node draws is update x nsub + sub (the caller's `update`)
 void launch_world_begin(const DevWorld& W, hipStream_t s, double* d_totals, double* d_scratch,
-                        hipEvent_t lists_ready, uint32_t update);
+                        hipEvent_t lists_ready, uint32_t update, int sub = 0, int nsub = 1);
+// a sub-update's share of the update's picks n (oracle sub_share)
+__host__ __device__ __forceinline__ long long sub_share(long long n, int s, int K) {
+  return K == 1 ? n : (n * (s + 1)) / K - (n * s) / K;
+}
 void launch_world_pre(const DevWorld& W, hipStream_t s, double* d_totals, double* d_scratch, hipEvent_t lists_ready,
                       uint32_t update, bool reset = true);
 void launch_tile_pre(const DevWorld& W, hipStream_t s, const double* d_gathered, int ntiles, double* d_totals,

@@ -363,6 +363,10 @@ __global__ void k_classify_uniform(DevWorld W, int64_t first, int64_t count, con
 // for (lazy: run with out == NULL, CNT_CUM_FLAG still 0) has its counts added
 // to the running sums here instead of in k_stats_final.  One block, >= 256
 // threads; the caller's condition is block-uniform.
+__device__ __forceinline__ void reset_queues_block(const DevWorld& W) {
+  if (threadIdx.x < 3) W.b_count[threadIdx.x] = 0;
+  if (threadIdx.x < 8) W.class_count[threadIdx.x] = 0;
+}
 __device__ __forceinline__ void reset_counts_block(const DevWorld& W) {
   constexpr int NG = 256 / CNT_STRIDE;
   __shared__ unsigned long long cs[NG][CNT_STRIDE];
@@ -391,8 +395,10 @@ __device__ __forceinline__ void reset_counts_block(const DevWorld& W) {
   if (threadIdx.x < 8) W.class_count[threadIdx.x] = 0;
 }
 
-// reset: block 0 also zeroes the update's counters, birth-queue and class-list
-// lengths (k_reset_counts' work; the previous update's statistics have read them)
+// reset 1: block 0 also zeroes the update's counters, birth-queue and class-list
+// lengths (k_reset_counts' work; the previous update's statistics have read them);
+// reset 2 (a later sub-update): the queue and list lengths only, the counters
+// go on adding up the update
 // One wave per 256-cell block b (partial[b]): the pairwise tree of strides
 // 128, 64, ..., 1 (s[t] += s[t + stride]), the oracle's tree_merit_sum order.
 // Lane l loads cells l, l+64, l+128, l+192 and forms the stride-128 and -64
@@ -400,7 +406,8 @@ __device__ __forceinline__ void reset_counts_block(const DevWorld& W) {
 // same order, without the LDS tree's 8 barriers.  Four blocks per workgroup.
 __global__ __launch_bounds__(256) void k_merit_partial(DevWorld W, double* partial, int32_t* alive_partial,
                                                        double* alive_d, int reset) {
-  if (reset && blockIdx.x == 0) reset_counts_block(W);
+  if (reset == 1 && blockIdx.x == 0) reset_counts_block(W);
+  if (reset == 2 && blockIdx.x == 0) reset_queues_block(W);
   const int lane = threadIdx.x & 63;
   const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int64_t nb = (W.n + 255) / 256;
@@ -472,7 +479,8 @@ __device__ __forceinline__ double tree_leaf(const double* part, const int32_t* a
 template <bool LDS>
 __global__ __launch_bounds__(1024) void k_block_counts(DevWorld W, const double* part, const int32_t* alive_part,
                                                        int64_t nb, int ntiles, int L, double* totals,
-                                                       uint32_t update, int mode, int chunked) {
+                                                       uint32_t update, int mode, int chunked, int sub,
+                                                       int nsub) {
   __shared__ long long s_cnt[1024];
   __shared__ double l_scr[LDS ? 2 * TREE_LDS_P : 1];
   __shared__ long long l_cnt[LDS ? 2 * TREE_LDS_P : 1];
@@ -506,7 +514,7 @@ __global__ __launch_bounds__(1024) void k_block_counts(DevWorld W, const double*
     const long long n = s_cnt[0];
     const double root = scr[1];
     const double ave = (double)W.ave_time_slice;
-    long long nroot = (long long)W.ave_time_slice * n;
+    long long nroot = sub_share((long long)W.ave_time_slice * n, sub, nsub);
     if (mode == 2) {
       const double tot = totals[0];
       nroot = tot > 0.0 ? (long long)__dmul_rn(__dmul_rn(__ddiv_rn(root, tot), ave), totals[1]) : 0;
@@ -1635,10 +1643,11 @@ void launch_classify_uniform(const DevWorld& W, hipStream_t s, int64_t first, in
 }
 
 static void launch_block_counts(const DevWorld& W, hipStream_t s, const double* part, const int32_t* alive,
-                                int64_t nb, int ntiles, int L, double* totals, uint32_t update, int mode) {
+                                int64_t nb, int ntiles, int L, double* totals, uint32_t update, int mode,
+                                int sub = 0, int nsub = 1) {
   if (((int64_t)1 << L) <= TREE_LDS_P) {
     hipLaunchKernelGGL(k_block_counts<true>, dim3(1), dim3(1024), 0, s, W, part, alive, nb, ntiles, L, totals, update,
-                       mode, 0);
+                       mode, 0, sub, nsub);
     return;
   }
   const int Lt = L - TREE_C_LOG;
@@ -1647,7 +1656,7 @@ static void launch_block_counts(const DevWorld& W, hipStream_t s, const double* 
   // the K chunk roots' tree in LDS: K <= 4096 for any world of < 2^31 cells
   // (2^23 blocks at most, so K <= 2^11)
   hipLaunchKernelGGL(k_block_counts<true>, dim3(1), dim3(1024), 0, s, W, part, alive, nb, ntiles, Lt, totals,
-                     update, mode, 1);
+                     update, mode, 1, sub, nsub);
   if (mode == 3) return;
   const int64_t b0 = mode == 1 ? W.cell0 / 256 : 0, nloc = (W.n + 255) / 256;
   const int64_t nk = ((b0 + nloc - 1) >> TREE_C_LOG) - (b0 >> TREE_C_LOG) + 1;
@@ -1693,13 +1702,13 @@ static void launch_allot(const DevWorld& W, hipStream_t s, const double* totals,
 // single world: block partials (k_merit_partial also zeroes the update's
 // counters), the scheduler's top tree, the allotment, the class-0 order
 void launch_world_begin(const DevWorld& W, hipStream_t s, double* totals, double* scratch,
-                        hipEvent_t lists_ready, uint32_t update) {
+                        hipEvent_t lists_ready, uint32_t update, int sub, int nsub) {
   const int64_t nb = (W.n + 255) / 256;
   int32_t* alive_partial = reinterpret_cast<int32_t*>(scratch + nb);
-  launch_resources_begin(W, s);   // ProcessPreUpdate + the update's first DoUpdates
+  if (sub == 0) launch_resources_begin(W, s);   // ProcessPreUpdate + the update's first DoUpdates
   hipLaunchKernelGGL(k_merit_partial, dim3((unsigned)((nb + 3) / 4)), dim3(256), 0, s, W, scratch, alive_partial,
-                     (double*)nullptr, 1);
-  launch_block_counts(W, s, scratch, alive_partial, nb, 1, tree_levels(nb), totals, update, 0);
+                     (double*)nullptr, sub == 0 ? 1 : 2);
+  launch_block_counts(W, s, scratch, alive_partial, nb, 1, tree_levels(nb), totals, update, 0, sub, nsub);
   launch_allot(W, s, totals, lists_ready, update);
 }
 

@@ -144,7 +144,12 @@ typedef struct avgpu_cfg {
   double divide_uniform_prob;      /* DIVIDE_UNIFORM_PROB */
   int32_t slip_fill_mode;          /* SLIP_FILL_MODE: 0 duplication, 2 random, 3 scrambled,
                                       4 nop-C (1, nop-X, refused) */
-  int32_t pad_cfg;
+  int32_t sub_updates;             /* batch-model fidelity, no reference knob (DESIGN.md 5
+                                      "Sub-updates"): an update's AVE_TIME_SLICE x N picks
+                                      are made in K = sub_updates batch steps, the scheduler
+                                      weights re-read before each; 0 or 1: one step.  K > 1
+                                      needs SLICING_METHOD 1 and a single world (no strips,
+                                      no handed-in totals) */
   double div_mut_prob;             /* DIV_MUT_PROB: per-site substitutions on divide,
                                       Binomial(offspring size, p) of them drawn after the
                                       uniform mutation (cpu/cHardwareBase.cc:447-460) */

@@ -286,6 +286,7 @@ struct World {
   std::vector<uint64_t> prio;     // each record's claim key in its current round
   std::vector<int8_t> bstate;     // BS_* (place_pick)
   int64_t t_insts = 0, t_deaths = 0, t_divides = 0, t_slices = 0, t_born = 0, t_dropped = 0;
+  uint32_t sched_key = 0;  // the scheduler's node-draw key: update x K + sub-update (sub_share)
   int64_t t_oversize = 0;   // offspring longer than AVGPU_MAX_GENOME after a slip (dropped at the divide)
   int64_t t_memcap = 0;     // copy insertions past AVGPU_MAX_GENOME sites / removals from one site (skipped)
   int64_t t_overwritten = 0;   // offspring placed, then killed by a later birth into the same cell
@@ -1247,7 +1248,7 @@ static double top_tree(const World& w, const std::vector<double>& leaf, int64_t 
       std::vector<int64_t> nc((size_t)2 << l, 0);
       for (size_t i = 0; i < c.size(); i++) {
         const int64_t left = binom_draw(c[i], lv[l + 1][2 * i] / lv[l][i],
-                                        node_draw(w, (uint32_t)w.update, SALT_TOP, ((uint64_t)1 << l) + i));
+                                        node_draw(w, w.sched_key, SALT_TOP, ((uint64_t)1 << l) + i));
         nc[2 * i] = left;
         nc[2 * i + 1] = c[i] - left;
       }
@@ -1270,7 +1271,7 @@ static void block_split(const World& w, int64_t b, int64_t n, int32_t* budget) {
     for (int t = 0; t < (1 << k); t++) {
       const int64_t c0 = cnt[t];
       const int64_t left = binom_draw(c0, lv[k + 1][t] / lv[k][t],
-                                      node_draw(w, (uint32_t)w.update, SALT_BLOCK, (gb << 9) | ((1u << k) + t)));
+                                      node_draw(w, w.sched_key, SALT_BLOCK, (gb << 9) | ((1u << k) + t)));
       cnt[t] = left;
       cnt[t + (1 << k)] = c0 - left;
     }
@@ -2137,7 +2138,7 @@ static inline bool place_cancelled(const World& w, int64_t i, uint32_t kt) {
 // rest counted (main/cPopulation.cc:5382-5413: PositionOffspring always
 // returns a cell, so a record that is neither cancelled nor without a cell
 // was placed -- it owns its cell, or a later birth overwrote it)
-static void place_finish_single(World& w) {
+static void place_finish_single(World& w, int64_t& placed_out, int64_t& dropped_out) {
   const int64_t nbirth = (int64_t)w.births.size();
   int64_t placed = 0, overwritten = 0, cancelled = 0, dropped = 0;
   for (int64_t i = 0; i < nbirth; i++) {
@@ -2155,66 +2156,93 @@ static void place_finish_single(World& w) {
     else if (st <= BS_NO_CELL) dropped++;
     else overwritten++;
   }
-  w.t_overwritten = overwritten;
-  w.t_cancelled = cancelled;
-  finish_stats(w, placed, dropped);
+  w.t_overwritten += overwritten;
+  w.t_cancelled += cancelled;
+  placed_out += placed;
+  dropped_out += dropped;
 }
 
 }  // extern "C++"
 
+// Sub-updates (avgpu_cfg.sub_updates = K, DESIGN.md 5 "Sub-updates"): the
+// update's UD picks are made in K consecutive batch steps of
+// floor(UD (s + 1) / K) - floor(UD s / K) picks each, the weights re-read
+// before each one -- the reference re-weights its scheduler at every divide
+// (cPopulation::ActivateOffspring -> AdjustSchedule, main/cPopulation.cc:
+// 621-952), so K steps bring the batch model's weight refresh K times closer
+// to it.  Resources step once per update (at sub-update 0); global
+// consumption settles after each sub-update; K = 1 is the plain batch update.
+static inline int sub_updates_of(const avgpu_cfg& c) { return c.sub_updates > 1 ? c.sub_updates : 1; }
+static inline int64_t sub_share(int64_t n, int s, int K) {
+  return K == 1 ? n : (n * (s + 1)) / K - (n * s) / K;
+}
+
 // Batch-synchronous world update: the exact semantics the device implements
 // (DESIGN.md "Update semantics"): allot -> interpret -> place births -> stats.
 static int run_update_impl(World& w) {
-  int64_t n_alive = 0;
-  std::vector<double> part;
-  world_partials(w, part, &n_alive);
-  const double local = top_tree(w, part, -1, 0, 0, nullptr);
-  const double ave = (double)w.cfg.ave_time_slice;
-  double total = local, ud = ave * (double)n_alive;
-  int64_t n_root = (int64_t)w.cfg.ave_time_slice * n_alive;
-  if (w.have_global) {   // cMultiProcessWorld::CalculateUpdateSize (main/cMultiProcessWorld.cc:396-405)
-    total = w.global_merit;
-    ud = ave * (double)w.global_orgs;
-    n_root = total > 0.0 ? (int64_t)((local / total) * ave * (double)w.global_orgs) : 0;
-  }
-  std::vector<int64_t> blk;
-  top_tree(w, part, n_root, 0, (int64_t)part.size(), &blk);
-  res_begin(w);
-  allot_interpret(w, blk, total, ud);
-  res_end(w);
-  const int64_t nbirth = (int64_t)w.births.size();
-  place_reset(w, w.ncells);
-  // launch 0: picks, kill times
-  for (int64_t i = 0; i < nbirth; i++) {
-    if (!place_pick(w, i, 0, [&](int64_t c) { return w.occ[c] != 0; })) continue;
-    const Birth& b = w.births[i];
-    if (key_kill(w.prio[i])) w.killt[b.target] = std::max(w.killt[b.target], 0x10000u - b.t);
-  }
-  // launch 0b: cancellations, round-0 claims
-  for (int64_t i = 0; i < nbirth; i++) {
-    if (w.bstate[i] != BS_PENDING) continue;
-    const Birth& b = w.births[i];
-    if (place_cancelled(w, i, w.killt[b.parent])) { w.bstate[i] = BS_CANCELLED; continue; }
-    w.claim_r[0][b.target] = std::max(w.claim_r[0][b.target], w.prio[i]);
-  }
-  // launches 1..3: resolve round m-1, pick round m
-  for (int m = 1; m < 4; m++) {
-    const std::vector<uint64_t>& prev = w.claim_r[m - 1];
+  const int K = sub_updates_of(w.cfg);
+  if (K > 1 && w.have_global)
+    return fail(AVGPU_EUNSUPPORTED, "sub_updates > 1 needs the world's own totals (no handed-in totals, no strips)");
+  int64_t placed = 0, dropped = 0, insts = 0, deaths = 0, divides = 0, slices = 0;
+  w.t_overwritten = 0;
+  w.t_cancelled = 0;
+  for (int sub = 0; sub < K; sub++) {
+    w.sched_key = (uint32_t)w.update * (uint32_t)K + (uint32_t)sub;
+    int64_t n_alive = 0;
+    std::vector<double> part;
+    world_partials(w, part, &n_alive);
+    const double local = top_tree(w, part, -1, 0, 0, nullptr);
+    const double ave = (double)w.cfg.ave_time_slice;
+    double total = local, ud = ave * (double)n_alive;
+    int64_t n_root = (int64_t)w.cfg.ave_time_slice * n_alive;
+    if (w.have_global) {   // cMultiProcessWorld::CalculateUpdateSize (main/cMultiProcessWorld.cc:396-405)
+      total = w.global_merit;
+      ud = ave * (double)w.global_orgs;
+      n_root = total > 0.0 ? (int64_t)((local / total) * ave * (double)w.global_orgs) : 0;
+    }
+    n_root = sub_share(n_root, sub, K);
+    std::vector<int64_t> blk;
+    top_tree(w, part, n_root, 0, (int64_t)part.size(), &blk);
+    if (sub == 0) res_begin(w);   // resources step once per update, at its start
+    allot_interpret(w, blk, total, ud);
+    insts += w.t_insts; deaths += w.t_deaths; divides += w.t_divides; slices += w.t_slices;
+    res_end(w);
+    const int64_t nbirth = (int64_t)w.births.size();
+    place_reset(w, w.ncells);
+    // launch 0: picks, kill times
+    for (int64_t i = 0; i < nbirth; i++) {
+      if (!place_pick(w, i, 0, [&](int64_t c) { return w.occ[c] != 0; })) continue;
+      const Birth& b = w.births[i];
+      if (key_kill(w.prio[i])) w.killt[b.target] = std::max(w.killt[b.target], 0x10000u - b.t);
+    }
+    // launch 0b: cancellations, round-0 claims
     for (int64_t i = 0; i < nbirth; i++) {
       if (w.bstate[i] != BS_PENDING) continue;
-      Birth& b = w.births[i];
-      if (prev[b.target] == w.prio[i]) {
-        w.bstate[i] = (int8_t)(BS_WON + m - 1);
-        w.occ[b.target] = 1;
-        if (takes_cell(w, w.owner[b.target], b.t)) w.owner[b.target] = i;
-        continue;
-      }
-      if (key_kill(w.prio[i])) { w.bstate[i] = (int8_t)(BS_KILL_LOST + m - 1); continue; }
-      if (!place_pick(w, i, m, [&](int64_t c) { return w.occ[c] != 0 || prev[c] != 0; })) continue;
-      w.claim_r[m][b.target] = std::max(w.claim_r[m][b.target], w.prio[i]);
+      const Birth& b = w.births[i];
+      if (place_cancelled(w, i, w.killt[b.parent])) { w.bstate[i] = BS_CANCELLED; continue; }
+      w.claim_r[0][b.target] = std::max(w.claim_r[0][b.target], w.prio[i]);
     }
+    // launches 1..3: resolve round m-1, pick round m
+    for (int m = 1; m < 4; m++) {
+      const std::vector<uint64_t>& prev = w.claim_r[m - 1];
+      for (int64_t i = 0; i < nbirth; i++) {
+        if (w.bstate[i] != BS_PENDING) continue;
+        Birth& b = w.births[i];
+        if (prev[b.target] == w.prio[i]) {
+          w.bstate[i] = (int8_t)(BS_WON + m - 1);
+          w.occ[b.target] = 1;
+          if (takes_cell(w, w.owner[b.target], b.t)) w.owner[b.target] = i;
+          continue;
+        }
+        if (key_kill(w.prio[i])) { w.bstate[i] = (int8_t)(BS_KILL_LOST + m - 1); continue; }
+        if (!place_pick(w, i, m, [&](int64_t c) { return w.occ[c] != 0 || prev[c] != 0; })) continue;
+        w.claim_r[m][b.target] = std::max(w.claim_r[m][b.target], w.prio[i]);
+      }
+    }
+    place_finish_single(w, placed, dropped);
   }
-  place_finish_single(w);
+  w.t_insts = insts; w.t_deaths = deaths; w.t_divides = divides; w.t_slices = slices;
+  finish_stats(w, placed, dropped);
   return 0;
 }
 
@@ -2370,6 +2398,8 @@ int orc_tile_partials(void* h, double* out) {
 int orc_tile_begin(void* h, const double* gathered, int ntiles) {
   World& w = *(World*)h;
   if (!tile_ok(w)) return fail(AVGPU_ESTATE, "not a strip tile with buffers");
+  if (sub_updates_of(w.cfg) > 1) return fail(AVGPU_EUNSUPPORTED, "sub_updates > 1 on strip tiles");
+  w.sched_key = (uint32_t)w.update;
   // the top tree over every strip's block partials (tile order = block order)
   const int64_t nb = (w.ncells + 255) / 256;
   std::vector<double> leaf((size_t)(nb * ntiles));

@@ -6,12 +6,18 @@ where the values do not depend on the reference's RNG stream, the same
 numbers (update 0: 100 injected organisms, ResA 20 and the global pool
 98.5913; the never-consumed global pool at every printed update).  Update 0's
 instruction count is 3000 in the reference, whose scheduler draws UD = 30 x 100
-picks; the batch update draws each organism's count, Poisson(30) (DESIGN.md
-5), so the total is 3000 in expectation -- within 4 sd here -- and ResB, which
-NAND consumes, follows the organisms' instruction counts.
+picks; the batch update splits exactly UD picks down its multinomial tree
+(DESIGN.md 5), so every update executes AVE_TIME_SLICE x (organisms at its
+start) instructions -- 3000 at update 0 -- with one batch step or with
+sub-updates (the steps' shares sum to UD).  Later updates can fall short of
+it by the picks an organism still had when it died in its slice (AGE_LIMIT):
+the reference gives those picks to the living, the batch budgets were drawn
+at the update's start.
 Update 0's births / deaths differ by design: the reference counts the 101
 injections as births (and the replaced first organism as a death)."""
 import os
+
+import pytest
 
 from avida_amd import datafiles, driver
 import oracle_lib as ol
@@ -25,10 +31,14 @@ def _header(path):
     return [l for l in open(path) if l.startswith("#")][2:]   # after the title and the time stamp
 
 
-def test_driver_spatial_res_100u(golden, tmp_path):
+@pytest.mark.parametrize("sub_updates", [1, 3])
+def test_driver_spatial_res_100u(golden, tmp_path, sub_updates):
     ref = os.path.join(golden, "spatial_res_100u")
-    d = driver.Driver(os.path.join(ref, "config"), str(tmp_path),
-                      make_world=lambda cfg, iset, env: ol.Backend("oracle", cfg, iset, env))
+
+    def mk(cfg, iset, env):
+        cfg.sub_updates = sub_updates
+        return ol.Backend("oracle", cfg, iset, env)
+    d = driver.Driver(os.path.join(ref, "config"), str(tmp_path), make_world=mk)
     last = d.run()
     assert last == 100                                  # "u 100 Exit"
     for name in ("count.dat", "average.dat", "tasks.dat", "time.dat", "resource.dat"):
@@ -39,7 +49,8 @@ def test_driver_spatial_res_100u(golden, tmp_path):
     assert [res[u][2] for u in range(0, 101, 10)] == [want[u][2] for u in range(0, 101, 10)]
     cnt, wcnt = _rows(os.path.join(tmp_path, "count.dat")), _rows(os.path.join(ref, "count.dat"))
     assert cnt[0][1] == wcnt[0][1]                      # organisms
-    assert abs(int(cnt[0][0]) - int(wcnt[0][0])) <= 4 * 3000 ** 0.5   # insts executed
+    assert int(cnt[0][0]) == int(wcnt[0][0]) == 3000    # insts executed: exactly UD
+    assert all(int(r[0]) <= 3000 for r in cnt.values())      # 100 cells: UD <= 3000
     tasks = _rows(os.path.join(tmp_path, "tasks.dat"))
     assert tasks[0] == ["0"] * 9
     time_ = _rows(os.path.join(tmp_path, "time.dat"))

@@ -258,6 +258,48 @@ def test_world_updates_resources_bit_exact(golden, variant):
     assert so.num_organisms > 200
 
 
+@pytest.mark.parametrize("variant", ["logic9", "9r"])
+def test_world_subupdates_bit_exact(golden, variant):
+    """sub_updates = 3 (DESIGN.md 5 "Sub-updates": an update's picks in three
+    batch steps, the scheduler weights re-read before each, resources stepped
+    once per update, global consumption settled after each step): GPU world ==
+    oracle world, every update's counters (summed over the steps), every
+    resource level, then every cell, field and digest."""
+    if variant == "logic9":
+        iset, env, cfg = pu.load_env(golden, seed=31)
+        anc = files.read_org(os.path.join(golden, "default-heads.org"), iset)
+        orgs, merits, updates = [anc], None, 400
+    else:
+        env, anc = _resource_env(golden, variant)
+        iset = files.read_instset(os.path.join(golden, "resources_9r", "instset-heads.cfg"))
+        cfg = capi.cfg_from_avida(files.read_avida_cfg(None, {"WORLD_X": 48, "WORLD_Y": 40}), seed=23)
+        orgs, merits, updates = [anc] * 200, [100.0] * 200, 60
+    cfg.sub_updates = 3
+    n = cfg.world_x * cfg.world_y
+    orc = ol.Backend("oracle", cfg, iset, env, ncells=n)
+    gpu = ol.Backend("gpu", cfg, iset, env, ncells=n)
+    for b in (orc, gpu):
+        b.set_orgs(0 if merits else n // 2 + cfg.world_x // 2, orgs, merits, deterministic=False)
+    for upd in range(updates):
+        so = orc.run_update()
+        sg = gpu.run_update()
+        for f in ("num_organisms", "insts_executed", "births", "deaths", "divides", "births_dropped",
+                  "births_overwritten", "births_cancelled", "cum_insts_executed", "cum_births", "slices"):
+            assert getattr(so, f) == getattr(sg, f), (upd, f, getattr(so, f), getattr(sg, f))
+        assert list(so.task_orgs) == list(sg.task_orgs), upd
+        if variant != "logic9":
+            assert orc.resources(spatial=True) == gpu.resources(spatial=True), upd
+    # the update's picks are UD = AVE_TIME_SLICE x N split over the steps
+    assert so.num_organisms > 100
+    a, oa, fa = orc.states(0, n, CAP)
+    b, ob, fb = gpu.states(0, n, CAP)
+    bad = pu.diff_states(a, b, oa, ob, fa, fb, CAP)
+    assert not bad, f"{len(bad)} mismatches: {bad[:5]}"
+    nbad, cells = pu.compare_digests(orc.digests(0, n), gpu.digests(0, n))
+    assert nbad == 0, f"{nbad} cell digests differ, first {cells}"
+    assert gpu.counters(cumulative=1)[capi.CNT_BAD_RECORD] == 0
+
+
 @pytest.mark.parametrize("T,geometry", [(2, 2), (4, 1)])
 def test_gpu_strip_tiles_with_resources(golden, T, geometry):
     """Config 5's path on one GPU: T strips with spatial resources (flows,

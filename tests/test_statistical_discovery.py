@@ -1,28 +1,20 @@
-"""Task-discovery statistics: the reference's discovery
-updates must lie inside the 2.5-97.5 % quantiles of the seeds' discovery
-updates -- a statistic of WHEN evolution finds (or spreads) a task, not just
-of how many organisms do it.  Both references print tasks.dat every 10
-updates, so the seeds are read on the same grid.
+"""Task-discovery statistics on resources_9r: for each
+task and each threshold T in (10, 50, 100), the first printed update at which
+T organisms do it -- 27 crossing updates of the reference
+(tests/golden/resources_9r/tasks.dat; the 9task ancestor does all nine
+tasks) -- must lie inside the 2.5-97.5 % quantiles of the seeds' crossing
+updates.  Run over 32 seeds on the GPU batch world (the metric's world) and
+on the oracle (bit-identical to it, tests/test_parity_gpu.py).
 
-* spatial_res_100u (the classic ancestor does Not, Nand, OrNot): the first
-  printed update with an Or organism -- the reference's run discovers Or by
-  update 20 (tests/golden/spatial_res_100u/tasks.dat).  Seeds that never
-  discover Or within 100 updates count as infinity (the distribution is
-  bimodal, test_statistical_spatial.py), so the upper quantile may be
-  infinite; the lower one must not exceed 20.
-* resources_9r (the 9task ancestor does all nine tasks): for each task and
-  each threshold T in (10, 50, 100), the first printed update at which T
-  organisms do it -- 27 crossing updates of the reference
-  (tests/golden/resources_9r/tasks.dat).
-
-Run over SEEDS >= 32 seeds on the GPU batch world (the metric's world) and
-on the oracle (bit-identical to it, tests/test_parity_gpu.py)."""
+spatial_res_100u's discovery statistics (Or, two-sample against the serial
+world) are in test_statistical_spatial.py.
+"""
 import os
 
 import numpy as np
 import pytest
 
-from avida_amd import capi, driver, files
+from avida_amd import capi, files
 import oracle_lib as ol
 
 SEEDS = range(1, 33)
@@ -44,24 +36,6 @@ def _inside(name, ref, samples):
     s = np.asarray(samples, dtype=float)
     lo, hi = np.quantile(s, 0.025, method="inverted_cdf"), np.quantile(s, 0.975, method="inverted_cdf")
     assert lo <= ref <= hi, f"{name}: reference {ref} outside the seeds' [{lo}, {hi}] ({sorted(s)})"
-
-
-def spatial_discovery(golden, tmp_path, make_world):
-    cfg = os.path.join(golden, "spatial_res_100u", "config")
-    disc = []
-    for s in SEEDS:
-        d = str(tmp_path / f"s{s}")
-        drv = driver.Driver(cfg, d, make_world=make_world, seed=s)
-        assert drv.run() == 100
-        drv.world.close()
-        t = _rows(os.path.join(d, "tasks.dat"))
-        disc.append(_first([(u, t[u][4]) for u in U if u in t], lambda v: v > 0))   # column 4: Or
-    ref = _rows(os.path.join(golden, "spatial_res_100u", "tasks.dat"))
-    ref_disc = _first([(u, ref[u][4]) for u in U], lambda v: v > 0)
-    assert ref_disc == 20
-    _inside("Or discovery", ref_disc, disc)
-    assert any(np.isfinite(disc)) and min(disc) <= ref_disc
-    return disc
 
 
 def resources_crossings(golden, kind):
@@ -92,17 +66,8 @@ def resources_crossings(golden, kind):
     assert checked == 27
 
 
-def test_discovery_spatial_oracle(golden, tmp_path):
-    spatial_discovery(golden, tmp_path, lambda cfg, iset, env: ol.Backend("oracle", cfg, iset, env))
-
-
 def test_discovery_resources_9r_oracle(golden):
     resources_crossings(golden, "oracle")
-
-
-@pytest.mark.gpu
-def test_discovery_spatial_gpu(golden, tmp_path):
-    spatial_discovery(golden, tmp_path, lambda cfg, iset, env: driver.ProductWorld(cfg, iset, env))
 
 
 @pytest.mark.gpu

@@ -395,6 +395,14 @@ def bind_common(lib, prefix):
 _lib = None
 
 
+def lib_build_hash(path=None):
+    """the first 16 hex digits of the SHA-256 of the library file: which
+    build a measurement (profiles/pmc_k_interpret320.json) belongs to"""
+    import hashlib
+    with open(path or LIB_PATH, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()[:16]
+
+
 def load_product(path=None):
     """Load the in-tree HIP library; raise if it is missing (no fallback).
     `path` selects a diagnostic build (tools/phase_clocks.py); it is not cached."""

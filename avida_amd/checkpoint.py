@@ -14,7 +14,11 @@ avgpu_cpu_state records), `tape` (one byte per site: op | copied << 6 |
 executed << 7, `cap` bytes per cell), `stats` (raw avgpu_update_stats),
 `levels` / `grids` (resources), `gkeys` (the census genotype keys of the
 birth genomes, which the tape no longer holds once an organism copied into
-its own sites; avgpu_set_genotype_keys).
+its own sites; avgpu_set_genotype_keys), `version` and the byte sizes of the
+two raw structures (`state_size`, `stats_size`).  A file from before a
+structure grew (round 4 added births_cancelled and seed to the stats) loads
+with the missing tail zeroed; a zero seed then leaves the world's configured
+RANDOM_SEED in place (avgpu_set_clock).
 """
 from __future__ import annotations
 
@@ -23,6 +27,8 @@ import ctypes as C
 import numpy as np
 
 from . import capi
+
+VERSION = 2
 
 
 def _call(lib, prefix, name, *args):
@@ -54,7 +60,17 @@ def save(lib, prefix, handle, ncells, nres, path):
     gkeys = capi.get_census(lib, prefix, handle, 0, ncells)["genotype_key"]
     np.savez_compressed(path, states=np.frombuffer(st, dtype=np.uint8), tape=tape.astype(np.uint8), gkeys=gkeys,
                         cap=np.int64(cap), stats=np.frombuffer(stats, dtype=np.uint8),
-                        levels=levels[:nres], grids=grids[:nres * ncells], ncells=np.int64(ncells))
+                        levels=levels[:nres], grids=grids[:nres * ncells], ncells=np.int64(ncells),
+                        version=np.int64(VERSION), state_size=np.int64(C.sizeof(capi.AvgpuCpuState)),
+                        stats_size=np.int64(C.sizeof(capi.AvgpuUpdateStats)))
+
+
+def _struct(cls, raw, what):
+    """a raw structure of an older (shorter) layout, its missing tail zeroed"""
+    size = C.sizeof(cls)
+    if len(raw) > size:
+        raise ValueError(f"checkpoint {what} record is {len(raw)} B, this build's is {size} B (newer file?)")
+    return cls.from_buffer_copy(raw + b"\0" * (size - len(raw)))
 
 
 def load(lib, prefix, handle, path):
@@ -62,7 +78,13 @@ def load(lib, prefix, handle, path):
     instruction set and environment (resources loaded)."""
     z = np.load(path, allow_pickle=False)
     ncells, cap = int(z["ncells"]), int(z["cap"])
-    st = (capi.AvgpuCpuState * ncells).from_buffer_copy(z["states"].tobytes())
+    if "version" in z.files and int(z["version"]) > VERSION:
+        raise ValueError(f"checkpoint version {int(z['version'])} is newer than this reader ({VERSION})")
+    raw = z["states"].tobytes()
+    ssz = int(z["state_size"]) if "state_size" in z.files else C.sizeof(capi.AvgpuCpuState)
+    if ssz != C.sizeof(capi.AvgpuCpuState) or len(raw) != ssz * ncells:
+        raise ValueError(f"checkpoint state records are {ssz} B, this build's are {C.sizeof(capi.AvgpuCpuState)} B")
+    st = (capi.AvgpuCpuState * ncells).from_buffer_copy(raw)
     tape = z["tape"]
     ops = np.ascontiguousarray(tape & 0x3F)
     fl = np.ascontiguousarray(((tape >> 6) & 0x01) | (((tape >> 7) & 0x01) << 2))
@@ -71,7 +93,7 @@ def load(lib, prefix, handle, path):
     if "gkeys" in z.files:                     # genotype keys of the birth genomes
         gk = np.ascontiguousarray(z["gkeys"], dtype=np.uint64)
         _call(lib, prefix, "set_genotype_keys", handle, 0, ncells, gk.ctypes.data_as(C.c_void_p))
-    stats = capi.AvgpuUpdateStats.from_buffer_copy(z["stats"].tobytes())
+    stats = _struct(capi.AvgpuUpdateStats, z["stats"].tobytes(), "stats")
     _call(lib, prefix, "set_clock", handle, C.byref(stats))
     levels = np.ascontiguousarray(z["levels"], dtype=np.float64)
     if len(levels):

@@ -1085,10 +1085,14 @@ int avgpu_set_clock(avgpu_world* w, const avgpu_update_stats* last) {
   HIPCHK(hipMemcpyAsync(w->W.counters + CNT_CUM_FLAG, &one, sizeof(one), hipMemcpyHostToDevice, w->stream));
   HIPCHK(hipStreamSynchronize(w->stream));
   w->update = last->update + 1;
-  // the scheduler's key (the world's RANDOM_SEED) comes with the clock
-  w->cfg.seed = last->seed;
-  w->W.seed_lo = (uint32_t)last->seed;
-  w->W.seed_hi = (uint32_t)(last->seed >> 32);
+  // the scheduler's key (the world's RANDOM_SEED) comes with the clock; a
+  // zero seed (stats from an older checkpoint, or not from avgpu_get_stats)
+  // keeps the configured one
+  if (last->seed != 0) {
+    w->cfg.seed = last->seed;
+    w->W.seed_lo = (uint32_t)last->seed;
+    w->W.seed_hi = (uint32_t)(last->seed >> 32);
+  }
   return 0;
 }
 

@@ -630,10 +630,16 @@ __device__ __forceinline__ uint32_t node_draw(uint32_t slo, uint32_t shi, uint32
   return lowbias32(lowbias32(lowbias32(update * 0x85EBCA6BU + shi) ^ (uint32_t)node ^ salt) +
                    (uint32_t)(node >> 32) + slo);
 }
-// the scheduler weight of a living organism (oracle sched_weight)
+// a merit the scheduler can weigh: finite and not negative (NaN, -x and inf
+// are never scheduled; large finite merits of multiplicative environments are)
+__device__ __forceinline__ bool merit_ok(double m) { return m >= 0.0 && m <= 1.7976931348623157e308; }
+// the scheduler weight of a living organism (oracle sched_weight): the same
+// in k_merit_partial's partials and k_allot's leaves
 __device__ __forceinline__ double sched_weight(double merit, uint32_t ctl) {
+  if (!merit_ok(merit)) return 0.0;
   const uint32_t hs = CTL_HS(ctl);
-  return hs ? __dmul_rn(merit, __dadd_rn(1.0, __dmul_rn((double)hs, 1.0 / 65536.0))) : merit;
+  const double w = hs ? __dmul_rn(merit, __dadd_rn(1.0, __dmul_rn((double)hs, 1.0 / 65536.0))) : merit;
+  return merit_ok(w) ? w : 0.0;
 }
 
 // CalcSizeMerit (main/cPhenotype.cc:1760-1816)

@@ -661,11 +661,8 @@ __global__ __launch_bounds__(1024) void k_allot(DevWorld W, const double* totals
     const int64_t c = b * 256 + lane + 64 * j;
     ctl[j] = (b < nb && c < W.n) ? W.ctl[c] : 0u;
     alive[j] = (ctl[j] & CTL_ALIVE) != 0;
-    double m = alive[j] ? W.merit[c] : 0.0;
-    if (alive[j] && !(m >= 0.0 && m < 1.0e300)) {   // a corrupt merit is counted, not scheduled
-      count_add(W, CNT_BAD_RECORD, 1ull);
-      m = 0.0;
-    }
+    const double m = alive[j] ? W.merit[c] : 0.0;
+    if (alive[j] && !merit_ok(m)) count_add(W, CNT_BAD_RECORD, 1ull);   // counted; sched_weight gives it 0
     wt[j] = alive[j] ? sched_weight(m, ctl[j]) : 0.0;
   }
   long long cnt[4] = {0, 0, 0, 0};

@@ -122,7 +122,8 @@ def environment(files, golden, kind, X, Y):
     return files.read_environment(os.path.join(golden, "environment-logic9.cfg"))
 
 
-def build_world(lib, capi, files, golden, side, seed, device, rank, world, on_tile=None, env_kind="logic9"):
+def build_world(lib, capi, files, golden, side, seed, device, rank, world, on_tile=None, env_kind="logic9",
+                sub_updates=1):
     """One 1024x1024 strip per rank of a side x (side*world) torus (world = 1:
     the untiled side x side world).  on_tile(h) places the strip before the
     organisms are injected (their RNG streams are keyed by global cell id)."""
@@ -130,6 +131,7 @@ def build_world(lib, capi, files, golden, side, seed, device, rank, world, on_ti
     env = environment(files, golden, env_kind, side, side * world)
     cfg = capi.cfg_from_avida(files.read_avida_cfg(None, {"WORLD_X": side, "WORLD_Y": side * world}),
                               seed=seed)
+    cfg.sub_updates = sub_updates
     n = side * side
     h = lib.avgpu_create(C.byref(cfg), device, n)
     if not h:
@@ -263,6 +265,9 @@ def main():
     ap.add_argument("--cpu-procs", type=int, default=0,
                     help="CPU baseline processes (0: min(16, host CPUs) -- 16 is a GPU box's share)")
     ap.add_argument("--cpu-worker", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--sub-updates", type=int, default=1,
+                    help="batch steps per update (avgpu_cfg.sub_updates, DESIGN.md 5): 1 is the "
+                         "product's update; K > 1 re-reads the scheduler weights K times per update")
     ap.add_argument("--long-updates", type=int, default=200,
                     help="after the K timed steps, a second untimed-by-contract run of this many "
                          "updates reported as config.long_run (stability cross-check; 0 = off)")
@@ -299,7 +304,7 @@ def main():
         return tiles.Tile(lib, "avgpu_", h, rank * args.side, world, "cuda")
 
     h, cfg, n, tile = build_world(lib, capi, files, golden, args.side, args.seed, local, rank, world,
-                                  on_tile, args.env)
+                                  on_tile, args.env, args.sub_updates)
     strips = tiles.StripWorld([tile], tiles.DistTransport(dist)) if tile else None
 
     capi.check(lib, lib.avgpu_set_timing(h, args.time_every))
@@ -418,20 +423,28 @@ def main():
     # over its HIP-event-timed average duration on the world's stream.
     c0_ms = cms[0] / nph
     # counters run over every update of the timed region (one class-0 launch
-    # each); the events only over every time_every-th
-    c0_slices = d[capi.CNT_C0_SLICES] / args.steps
-    c0_sites = d[capi.CNT_C0_SITES] / args.steps
+    # per batch step, sub_updates steps per update); the events only over
+    # every time_every-th launch
+    launches = args.steps * max(1, args.sub_updates)
+    c0_slices = d[capi.CNT_C0_SLICES] / launches
+    c0_sites = d[capi.CNT_C0_SITES] / launches
     bytes_per_launch = 2.0 * STATE_BYTES * c0_slices + SITE_BYTES * c0_sites
     achieved = bytes_per_launch / (c0_ms * 1e-3) / 1e9 if c0_ms > 0 else 0.0
     traffic, traffic_src, issue = None, None, None
     if os.path.exists(PMC_FILE):
         with open(PMC_FILE) as f:
             pmc = json.load(f)
-        if pmc.get("world") == f"{args.side}x{args.side}" and args.env == "logic9":
-            traffic = pmc["hbm_bytes_per_launch"]
-            traffic_src = pmc["source"]
-            issue = issue_roofline(pmc["counters_per_dispatch"], c0_ms,
-                                   d[capi.CNT_INSTS] / args.steps * c0_slices / max(1.0, d[capi.CNT_SLICES] / args.steps))
+        same_build = pmc.get("lib_sha16") == capi.lib_build_hash()
+        if pmc.get("world") == f"{args.side}x{args.side}" and args.env == "logic9" and args.sub_updates <= 1:
+            if same_build:
+                traffic = pmc["hbm_bytes_per_launch"]
+                traffic_src = pmc["source"]
+                issue = issue_roofline(pmc["counters_per_dispatch"], c0_ms,
+                                       d[capi.CNT_INSTS] / args.steps * c0_slices /
+                                       max(1.0, d[capi.CNT_SLICES] / args.steps))
+            else:     # counters of another build of the library: not paired with this run's timing
+                traffic_src = (f"none: {PMC_FILE} holds counters of library build {pmc.get('lib_sha16')}, "
+                               f"this is {capi.lib_build_hash()} (rerun tools/pmc_passes.sh)")
     out = {
         "metric": METRIC,
         "value": value,
@@ -464,6 +477,7 @@ def main():
             "insts_per_update": tot_insts / args.steps,
             "parallelism": f"strips{world}",
             "ranks": world,
+            "sub_updates": max(1, args.sub_updates),
             "long_run": long_run,
             # the timed updates run without the per-update statistics reduction;
             # stats_every_update_run: the same updates with it (its cost per update)

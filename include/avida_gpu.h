@@ -449,10 +449,13 @@ int avgpu_set_serial_streams(avgpu_world* w, const double* sched, int64_t n_sche
                              int64_t n_ctx);
 /* The same update split around an external all-reduce (multi-GPU tiles,
  * cMultiProcessWorld::CalculateUpdateSize main/cMultiProcessWorld.cc:375-405):
- * avgpu_update_totals writes the tile's {sum merit, organisms} into the
- * 2-double device buffer dev_totals; after the caller sums it over ranks
- * (RCCL all-reduce, stream-ordered), avgpu_update_run allots
- * AVE_TIME_SLICE * N_global instructions in proportion to merit / global merit. */
+ * avgpu_update_totals writes the tile's {sum of scheduler weights, organisms}
+ * into the 2-double device buffer dev_totals; after the caller sums it over
+ * ranks (RCCL all-reduce, stream-ordered), avgpu_update_run allots
+ * AVE_TIME_SLICE * N_global instructions in proportion to weight / global
+ * weight.  The scheduler weight is the merit, times 1 + head start / 2^16 for
+ * a newborn's first allotment, not the plain merit: a host that
+ * hands in sum(merit) gives the world a different share of the picks. */
 int avgpu_update_totals(avgpu_world* w, double* dev_totals);
 int avgpu_update_run(avgpu_world* w, const double* dev_totals, avgpu_update_stats* out);
 /* Run the handle's work on an external HIP stream (e.g. the framework's
@@ -537,7 +540,9 @@ int avgpu_set_genotype_keys(avgpu_world* w, int64_t first_cell, int64_t count, c
 int avgpu_set_states(avgpu_world* w, int64_t first, int64_t count, const avgpu_cpu_state* states,
                      const uint8_t* mem_ops, const uint8_t* mem_flags, int mem_cap);
 /* checkpoint / resume: the update counter and cumulative counters of
- * avgpu_get_stats (`last` = the stats of the checkpointed world's last update) */
+ * avgpu_get_stats (`last` = the stats of the checkpointed world's last update),
+ * and its seed (the scheduler's key) unless last->seed is 0, which keeps the
+ * world's configured seed */
 int avgpu_set_clock(avgpu_world* w, const avgpu_update_stats* last);
 /* Batched cTestCPU::TestGenome (cpu/cTestCPU.cc:190-326), one gestation
  * each, deterministic inputs, mutations off. executed_flags (n*flags_cap)
@@ -555,6 +560,9 @@ int avgpu_get_stats(avgpu_world* w, avgpu_update_stats* out);
  * (RCCL, cMultiProcessWorld.cc:375-405); avgpu_set_global_merit feeds the
  * reduced totals back before the next allotment. */
 int avgpu_stats_vector(avgpu_world* w, void** dev_ptr);
+/* total_merit: the SUM OF SCHEDULER WEIGHTS over every world (as
+ * avgpu_update_totals computes it, head starts included), total_orgs: the
+ * living organisms of every world */
 int avgpu_set_global_totals(avgpu_world* w, double total_merit, int64_t total_orgs);
 /* ---- strip tiles: one global world over several GPUs --------------------
  * Replaces the reference's only multi-process world, cMultiProcessWorld

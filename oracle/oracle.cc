@@ -1134,8 +1134,13 @@ void dump_state(const World& w, const Org& o, avgpu_cpu_state* s, uint8_t* ops, 
 // offspring inside its parent's divide and schedules it for the rest of that
 // update; the batch update places it at the update's end and gives it that
 // share in the next.  hstart 0 -> the merit itself.
+// A merit that is NaN, negative or infinite is never scheduled (weight 0),
+// nor is a weight that overflows; the device's merit_ok / sched_weight.
+static inline bool merit_ok(double m) { return m >= 0.0 && m <= 1.7976931348623157e308; }
 static inline double sched_weight(const Org& o) {
-  return o.hstart ? o.merit * (1.0 + (double)o.hstart * (1.0 / 65536.0)) : o.merit;
+  if (!merit_ok(o.merit)) return 0.0;
+  const double w = o.hstart ? o.merit * (1.0 + (double)o.hstart * (1.0 / 65536.0)) : o.merit;
+  return merit_ok(w) ? w : 0.0;
 }
 
 // ---------------------------------------------------------------------------
@@ -1737,8 +1742,10 @@ int orc_set_clock(void* h, const avgpu_update_stats* last) {
   w.update = last->update + 1;
   w.cum_insts = last->cum_insts_executed;
   w.cum_births = last->cum_births;
-  w.cfg.seed = last->seed;
-  w.stats.seed = last->seed;
+  if (last->seed != 0) {   // zero: stats of an older checkpoint -- the configured seed stays
+    w.cfg.seed = last->seed;
+    w.stats.seed = last->seed;
+  }
   return 0;
 }
 

@@ -39,7 +39,13 @@ if __name__ == "__main__":
     if a.json:
         fetch = avg.get("FETCH_SIZE", 0.0) * 1024.0
         write = avg.get("WRITE_SIZE", 0.0) * 1024.0
-        out = {"kernel": a.regex, "world": a.world, "source": a.source,
+        import os
+        import sys
+        sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        from avida_amd import capi
+        # the library build the counters belong to: bench.py pairs them only
+        # with timings of the same build
+        out = {"kernel": a.regex, "world": a.world, "source": a.source, "lib_sha16": capi.lib_build_hash(),
                "fetch_size_bytes": fetch, "write_size_bytes": write,
                "hbm_bytes_per_launch": 2.0 * fetch + write,
                "counters_per_dispatch": avg}

@@ -232,6 +232,7 @@ int setup_world(avgpu_world* w, int64_t n, bool test_buffers) {
   W.th_par_del = th(c.parent_del_prob); W.p_par_del = c.parent_del_prob;
   W.slip_fill_mode = c.slip_fill_mode;
   W.trans_fill_mode = c.trans_fill_mode;
+  W.slip_copy_mode = c.slip_copy_mode;
   W.rec = nullptr; W.rec_n = 0; W.rec_off = nullptr;
   W.seed_lo = (uint32_t)c.seed;
   W.seed_hi = (uint32_t)(c.seed >> 32);
@@ -265,8 +266,11 @@ std::string unsupported_cfg(const avgpu_cfg& c) {
   const bool slips = nz(c.divide_slip_prob) || nz(c.divide_poisson_slip_mean) || nz(c.div_slip_prob);
   if (slips && (c.slip_fill_mode < 0 || c.slip_fill_mode == 1 || c.slip_fill_mode > 4))
     return "SLIP_FILL_MODE 1 (nop-X) or an unknown mode";
-  if (nz(c.copy_slip_prob) && c.slip_copy_mode != 0)
-    return "SLIP_COPY_MODE 1 (a slip of the whole memory at the write head)";
+  if (nz(c.copy_slip_prob) && c.slip_copy_mode != 0 && c.slip_copy_mode != 1)
+    return "SLIP_COPY_MODE other than 0 (read-head jump) and 1 (memory slip)";
+  if (nz(c.copy_slip_prob) && c.slip_copy_mode == 1 && c.slip_fill_mode != 0 && c.slip_fill_mode != 2 &&
+      c.slip_fill_mode != 4)
+    return "SLIP_COPY_MODE 1 with SLIP_FILL_MODE other than 0 (duplication), 2 (random), 4 (nop-C)";
   if ((nz(c.divide_trans_prob) || nz(c.divide_poisson_trans_mean) || nz(c.div_trans_prob)) &&
       (c.trans_fill_mode < 0 || c.trans_fill_mode > 1))
     return "TRANS_FILL_MODE other than 0 (duplication) / 1 (scrambled)";

@@ -270,6 +270,7 @@ struct DevWorld {
   int32_t seg_any;        // some variable-count kind is on (b_subs / b_pofs / b_pcnt allocated)
   int32_t slip_fill_mode;
   int32_t trans_fill_mode;
+  int32_t slip_copy_mode;   // SLIP_COPY_MODE: 0 the read head jumps, 1 a slip of the whole memory
   // RECORDED mode (avgpu_set_rng_mode): rec_n doubles; rec_off[c] = the start
   // of cell c's organism's segment, -1 = a counter stream.  rec == nullptr:
   // COUNTER mode everywhere (the REC-free interpreter instantiations run).

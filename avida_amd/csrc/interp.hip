@@ -389,6 +389,7 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
   const int k_copy_ext = DEF ? 0 : W.copy_ext;
   const uint64_t k_th_copy_ins = DEF ? 0ull : W.th_copy_ins, k_th_copy_del = DEF ? 0ull : W.th_copy_del;
   const uint64_t k_th_copy_uni = DEF ? 0ull : W.th_copy_uni, k_th_copy_slip = DEF ? 0ull : W.th_copy_slip;
+  const int k_slip_whole = DEF ? 0 : W.slip_copy_mode;
   const int k_rand_total = W.rand_total, k_n_ops = W.n_ops, k_n_react = W.n_react;
   const bool k_rand_lut = DEF || k_rand_total <= 256;   // GetRandomInst from the LUT
   // RECORDED streams (include/avida_gpu.h "random streams"): the organism's
@@ -606,6 +607,19 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
             // (below the largest genome) makes the copy spill
             int mx_sz = M + (e_ins >= 0 ? 1 : 0);
             if (e_uni > k_n_ops) mx_sz = max(mx_sz, M + (e_ins >= 0 ? 1 : 0) - (e_del ? 1 : 0) + 1);
+            // SLIP_COPY_MODE 1 (oracle slip_memory): the slip's `to` is the
+            // next draw, from the size the edits above leave (their caps
+            // included); its result size joins the check
+            int s_to = -1;
+            if (e_slp && k_slip_whole) {
+              int Mp = M;
+              if (e_ins >= 0 && Mp < AVGPU_MAX_GENOME) Mp++;
+              if (e_del && Mp > 1) Mp--;
+              if (e_uni == k_n_ops && Mp > 1) Mp--;
+              else if (e_uni > k_n_ops && Mp < AVGPU_MAX_GENOME) Mp++;
+              s_to = (int)draw_below((uint32_t)(wh == 0 ? Mp : Mp + 1));
+              if (Mp + wh - s_to <= AVGPU_MAX_GENOME) mx_sz = max(mx_sz, Mp + wh - s_to);
+            }
             if (mx_sz > S && S < AVGPU_MAX_GENOME) {
               T[wh] = (uint8_t)dst_byte;                       // undo the write, then the step
               T[ipa] = (uint8_t)cur_byte;
@@ -638,8 +652,29 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
                   ins_at(wh, (int)tab_u8(rcode + e_uni - k_n_ops - 1));
                 }
               }
-              if (e_slp) e_slip = (int)draw_below((uint32_t)M);   // read_head.Set(GetInt(size))
+              if (e_slp && !k_slip_whole) e_slip = (int)draw_below((uint32_t)M);   // read_head.Set(GetInt(size))
               if (e_slip >= 0) rh = e_slip;
+              if (s_to >= 0) {                                 // the memory slip at the write head
+                const int from = wh, ins = from - s_to, Mn = M + ins;
+                if (Mn > AVGPU_MAX_GENOME) {
+                  ncap++;
+                } else if (ins > 0) {                          // only codes move; flags stay per position
+                  for (int j = Mn - 1; j >= from + ins; j--) {
+                    const int cd = T[j - ins] & CODE_MASK;
+                    T[j] = (uint8_t)(j < M ? ((T[j] & ~CODE_MASK) | cd) : cd);
+                  }
+                  const int sfm = W.slip_fill_mode;
+                  for (int i = 0; i < ins; i++) {
+                    const int j = from + i;
+                    const int cd = sfm == 0 ? (T[s_to + i] & CODE_MASK) : sfm == 2 ? rand_code() : 2;   // nop-C
+                    T[j] = (uint8_t)(j < M ? ((T[j] & ~CODE_MASK) | cd) : cd);
+                  }
+                  M = Mn;
+                } else if (ins < 0) {
+                  for (int j = from; j < Mn; j++) T[j] = (uint8_t)((T[j] & ~CODE_MASK) | (T[j - ins] & CODE_MASK));
+                  M = Mn;
+                }
+              }
               if (ncap) count_add(W, CNT_MEM_CAP, (unsigned long long)ncap);
             }
           }

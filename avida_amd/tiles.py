@@ -161,6 +161,49 @@ class DistTransport:
         return d.batch_isend_irecv(ops)
 
 
+class StagedTransport(DistTransport):
+    """DistTransport over a host-only backend ("gloo") for device strips:
+    every collective step copies the device buffers to host tensors (the copy
+    waits for the strip's stream, on which the product library runs),
+    exchanges them, and copies the result back before the next launch.  This
+    is how two ranks that share ONE GPU -- which RCCL refuses -- run the
+    product's strips across processes (tests/test_tiles_mp_gpu.py); on a node
+    with a GPU per rank, DistTransport over "nccl" keeps everything on the
+    device."""
+
+    def all_gather(self, tiles):
+        (t,) = tiles
+        host = t.part.cpu()
+        out = [torch.empty_like(host) for _ in range(self.world)]
+        self.dist.all_gather(out, host, group=self.group)
+        t.gathered.copy_(torch.cat(out))
+
+    def all_reduce_sum(self, tiles):
+        (t,) = tiles
+        host = t.cons.cpu()
+        self.dist.all_reduce(host, group=self.group)
+        t.cons.copy_(host)
+
+    def exchange_start(self, tiles, kind):
+        (t,) = tiles
+        send, recv = (getattr(t, n) for n in _buffers(kind))
+        hs = [b.cpu() for b in send]
+        hr = [torch.empty_like(hs[0]) for _ in range(2)]
+        up = (self.rank - 1) % self.world
+        down = (self.rank + 1) % self.world
+        d = self.dist
+        ops = [d.P2POp(d.isend, hs[0], up, self.group), d.P2POp(d.isend, hs[1], down, self.group),
+               d.P2POp(d.irecv, hr[1], down, self.group), d.P2POp(d.irecv, hr[0], up, self.group)]
+        return d.batch_isend_irecv(ops), hs, hr, recv
+
+    def exchange_wait(self, pending):
+        works, _, hr, recv = pending
+        for w in works:
+            w.wait()
+        for k in range(2):
+            recv[k].copy_(hr[k])
+
+
 class StripWorld:
     """Runs updates of the strips this process holds (`tiles`, in global row
     order) with `transport` doing the collective steps."""

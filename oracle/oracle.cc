@@ -905,6 +905,35 @@ struct Exec {
     return o.inputs[o.input_ptr++];
   }
 
+  // doSlipMutation(ctx, m_memory, write head) (cpu/cHardwareBase.cc:621-694)
+  // on the organism's whole memory -- SLIP_COPY_MODE 1's copy slip
+  // (cpu/cHardwareCPU.cc:7157-7161): `to` = GetInt(size) when from is 0, else
+  // GetInt(size + 1); the memory is resized by from - to (cCPUMemory::Resize,
+  // cpu/cCPUMemory.cc:66-77: new sites op 0 / flags 0, a shrink keeps the
+  // leading flags) and the sites from `from` on are rewritten -- the
+  // insertion [from, from + (from - to)) filled per SLIP_FILL_MODE (0: the
+  // duplicated sites [to, from); 2: GetRandomInst each; 4: nop-C), then the
+  // old sites from `to` on.  Only the instructions move: every site keeps the
+  // flags of its position (the slip writes InstructionSequence elements, not
+  // the cCPUMemory flag array).  A slip that would take the memory past
+  // AVGPU_MAX_GENOME sites is skipped after its draw and counted
+  // (AVGPU_CNT_MEM_CAP).  SLIP_FILL_MODE 1 (nop-X) and 3 are refused with
+  // SLIP_COPY_MODE 1 (avgpu_check_cfg).
+  void slip_memory(Stream& r, int from) {
+    const int M = size();
+    const int to = (int)(from == 0 ? r.uint_below((uint32_t)M) : r.uint_below((uint32_t)M + 1u));
+    const int ins = from - to, Mn = M + ins;
+    if (Mn > AVGPU_MAX_GENOME) { w.t_memcap++; return; }
+    const std::vector<uint8_t> copy = o.mem;
+    o.mem.resize(Mn, 0);
+    o.flg.resize(Mn, 0);
+    for (int i = 0; i < ins; i++) {
+      const int sfm = w.cfg.slip_fill_mode;
+      o.mem[from + i] = sfm == 0 ? copy[to + i] : sfm == 2 ? (uint8_t)w.is.random_inst(r) : (uint8_t)2;   // nop-C
+    }
+    for (int i = std::max(ins, 0); i < M - to; i++) o.mem[from + i] = copy[to + i];
+  }
+
   // Inst_HeadCopy (cpu/cHardwareCPU.cc:7130-7167)
   void h_copy() {
     const int sz = size();
@@ -961,8 +990,12 @@ struct Exec {
       else insert_at(wh, mut - n_ops - 1);
     }
     // SLIP_COPY_MODE 0 (m_slip_read_head, cpu/cHardwareCPU.cc:785): the read
-    // head jumps to GetInt(memory size) (:7157-7158)
-    if (muts && w.p_copy_slip.th && r.p(w.p_copy_slip)) rh = adjust((int)r.uint_below((uint32_t)size()), size());
+    // head jumps to GetInt(memory size) (:7157-7158); SLIP_COPY_MODE 1: a slip
+    // of the whole memory at the write head (:7160, slip_memory)
+    if (muts && w.p_copy_slip.th && r.p(w.p_copy_slip)) {
+      if (w.cfg.slip_copy_mode == 0) rh = adjust((int)r.uint_below((uint32_t)size()), size());
+      else slip_memory(r, wh);
+    }
     rh = adjust(rh + 1, size());
     wh = adjust(wh + 1, size());
   }

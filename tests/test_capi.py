@@ -84,6 +84,7 @@ REFUSED_C = [
     ("no_mut_insts_len", "1"), ("test_fitness_measures", "1"),
     ("divide_method", "0"), ("world_geometry", "3"), ("slicing_method", "3"),
     ("base_merit_method", "6"), ("birth_method", "1"), ("death_method", "3"), ("alloc_method", "1"),
+    ("sub_updates", "65"),
 ]
 
 
@@ -128,6 +129,17 @@ def test_python_config_reaches_the_refusal(golden, tmp_path):
     assert c.test_fitness_measures == 1 and lib.avgpu_check_cfg(C.byref(c)) == -5
     c = capi.cfg_from_avida(files.read_avida_cfg(None, {"NO_MUT_INSTS": "abc"}))
     assert c.no_mut_insts_len == 3 and lib.avgpu_check_cfg(C.byref(c)) == -5
+    # SLIP_COPY_MODE 1 (memory slips) runs with fill modes 0 / 2 / 4; 3 and 1 are refused
+    for fill, rc in ((0, 0), (2, 0), (4, 0), (3, -5), (1, -5)):
+        c = capi.cfg_from_avida(files.read_avida_cfg(None, {"COPY_SLIP_PROB": 0.01, "SLIP_COPY_MODE": 1,
+                                                            "SLIP_FILL_MODE": fill}))
+        assert lib.avgpu_check_cfg(C.byref(c)) == rc, fill
+    # sub-updates need the probabilistic scheduler
+    c = capi.cfg_from_avida(files.read_avida_cfg(None, {"SLICING_METHOD": 2}))
+    c.sub_updates = 3
+    assert lib.avgpu_check_cfg(C.byref(c)) == -5 and "sub_updates" in lib.avgpu_last_error().decode()
+    c.slicing_method = 1
+    assert lib.avgpu_check_cfg(C.byref(c)) == 0
     # DIV_MUT_PROB (per-site substitutions on divide) is on the path
     c = capi.cfg_from_avida(files.read_avida_cfg(None, {"DIV_MUT_PROB": 0.003}))
     assert c.div_mut_prob == 0.003 and lib.avgpu_check_cfg(C.byref(c)) == 0

@@ -141,6 +141,15 @@ def test_config3_geometry_strips_equal_untiled(golden):
     assert births > 1_000_000
 
 
+def _resources_np(b, nres, n):
+    """(levels, grids [nres][n]) of a backend as numpy arrays"""
+    lv = np.zeros(max(1, nres))
+    gr = np.zeros(max(1, nres * n))
+    b._call("get_resources", b.h, lv.ctypes.data_as(C.POINTER(C.c_double)),
+            gr.ctypes.data_as(C.POINTER(C.c_double)))
+    return lv[:nres], gr[:nres * n].reshape(nres, n)
+
+
 def _transfer(src, dst, n, chunk=1 << 16):
     """every cell's state + tape of backend src into backend dst (set_states),
     chunk by chunk, then the genotype keys and the update clock"""
@@ -195,3 +204,44 @@ def test_config2_bench_regime_bit_exact(golden):
         _assert_digests(orc.digests(), gpu.digests(), f"bench regime, update {bench.BURN_IN + bench.WARMUP + u}", orc, gpu)
     assert cap > 320                             # organisms beyond class 0's slots took part
     assert gpu.counters(cumulative=1)[capi.CNT_BAD_RECORD] == 0   # no guarded field ever out of range
+
+
+@pytest.mark.timeout(1100)
+def test_config4_bench_regime_bit_exact(golden):
+    """configs[4] at its own workload: bench.py --env
+    resources -- the 1024x1024 world with one diffusing spatial torus resource
+    per logic-9 reaction (inflow / outflow everywhere, diffusion 1) -- run on
+    the GPU for the bench's burn-in + warmup updates, then checkpointed cell by
+    cell AND resource grid by grid into the oracle; both run 3 more updates
+    and every counter, every cell digest, every resource level and every
+    per-cell amount must agree bit for bit."""
+    import bench
+    X = Y = 1024
+    n = X * Y
+    cfg, iset, _, idx, gen, glen, gmer = _bench_seed(golden, X, Y)
+    env = files.parse_environment(bench.resource_env_text(X, Y))
+    nres = len(env.resources)
+    gpu = ol.Backend("gpu", cfg, iset, env, ncells=n)
+    _seed(gpu, 0, idx, gen, glen, gmer)
+    for u in range(bench.BURN_IN + bench.WARMUP):
+        s = gpu.run_update()
+        assert s.births_dropped == 0, (u, s.births_dropped)
+    orc = ol.Backend("oracle", cfg, iset, env, ncells=n)
+    _transfer(gpu, orc, n)
+    lv, gr = _resources_np(gpu, nres, n)
+    orc._call("set_resources", orc.h, lv.ctypes.data_as(C.POINTER(C.c_double)),
+              np.ascontiguousarray(gr).ctypes.data_as(C.POINTER(C.c_double)))
+    _assert_digests(orc.digests(), gpu.digests(), "restored world", orc, gpu)
+    for u in range(3):
+        so, sg = orc.run_update(), gpu.run_update()
+        for f in STAT_FIELDS:
+            assert getattr(so, f) == getattr(sg, f), (u, f, getattr(so, f), getattr(sg, f))
+        assert list(so.task_orgs) == list(sg.task_orgs), u
+        assert sg.births_dropped == 0 and sg.births > 10_000
+        _assert_digests(orc.digests(), gpu.digests(), f"configs[4] bench regime, update {u}", orc, gpu)
+        lo, go = _resources_np(orc, nres, n)
+        lg, gg = _resources_np(gpu, nres, n)
+        assert np.array_equal(lo, lg), (u, lo, lg)
+        bad = np.argwhere(go != gg)
+        assert len(bad) == 0, f"update {u}: {len(bad)} resource cells differ, first {bad[:3].tolist()}"
+    assert gr.sum() > 0 and gpu.counters(cumulative=1)[capi.CNT_BAD_RECORD] == 0

@@ -300,8 +300,8 @@ def test_world_subupdates_bit_exact(golden, variant):
     assert gpu.counters(cumulative=1)[capi.CNT_BAD_RECORD] == 0
 
 
-@pytest.mark.parametrize("T,geometry", [(2, 2), (4, 1)])
-def test_gpu_strip_tiles_with_resources(golden, T, geometry):
+@pytest.mark.parametrize("T,geometry,env_kind", [(2, 2, "tile"), (4, 1, "tile"), (4, 2, "bench")])
+def test_gpu_strip_tiles_with_resources(golden, T, geometry, env_kind):
     """Config 5's path on one GPU: T strips with spatial resources (flows,
     inflow box and CELL list across strip edges, edge rows exchanged) and a
     consumed global pool (consumption all-reduced) == the untiled oracle world:
@@ -311,7 +311,11 @@ def test_gpu_strip_tiles_with_resources(golden, T, geometry):
     import tile_util as tu
     from test_tiles import resource_grids_match
     X, Y, U = 64, 64, 30
-    env = tu.resource_env(golden)
+    if env_kind == "bench":          # configs[4]'s environment (bench.py --env resources)
+        import bench
+        env = files.parse_environment(bench.resource_env_text(X, Y))
+    else:
+        env = tu.resource_env(golden)
     per_update = []
     ref, rstats = tu.single("oracle", golden, X, Y, U, geometry=geometry, env=env,
                             on_update=lambda u, b: per_update.append(b.resources(spatial=True)))

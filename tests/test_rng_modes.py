@@ -378,6 +378,73 @@ def test_copy_mutation_draw_order(golden):
     assert ops[100] == 19 and fl[100] & 1
 
 
+def _slip_memory_expected(ops, fl, M, frm, to, fill, rand_code=None):
+    """doSlipMutation on the whole memory (cpu/cHardwareBase.cc:621-694),
+    restated independently of the oracle: (ops, flags) after the slip.  Only
+    the instructions move; flags stay with positions (new positions: 0)."""
+    copy = list(ops[:M])
+    ins = frm - to
+    Mn = M + ins
+    new = copy[:min(M, Mn)] + [0] * max(0, Mn - M)
+    for i in range(max(ins, 0)):
+        new[frm + i] = copy[to + i] if fill == 0 else (2 if fill == 4 else rand_code(i))
+    for i in range(max(ins, 0), M - to):
+        new[frm + i] = copy[to + i]
+    flags = list(fl[:min(M, Mn)]) + [0] * max(0, Mn - M)
+    return new, flags
+
+
+def _first_copy_state(kind, golden, stream, fill):
+    """the ancestor (COPY_SLIP_PROB 0.5, SLIP_COPY_MODE 1, every other
+    mutation off) just before its first h-copy (its 90th instruction, SURVEY.md
+    Appendix B) and just after it, fed from `stream`"""
+    iset, env, cfg, anc = _ancestor(golden, {"COPY_MUT_PROB": 0.0, "DIVIDE_INS_PROB": 0.0,
+                                             "DIVIDE_DEL_PROB": 0.0, "COPY_SLIP_PROB": 0.5,
+                                             "SLIP_COPY_MODE": 1, "SLIP_FILL_MODE": fill,
+                                             "DEATH_METHOD": 0})
+    b = ol.Backend(kind, cfg, iset, env, ncells=1)
+    b.set_orgs(0, [anc], deterministic=True)
+    b.set_rng_mode(capi.RNG_RECORDED, np.asarray(stream, dtype=np.float64))
+    b.step(0, 1, uniform=89, mode=capi.MODE_FROZEN)
+    before = b.states(0, 1, CAP)
+    b.step(0, 1, uniform=1, mode=capi.MODE_FROZEN)
+    after = b.states(0, 1, CAP)
+    b.close()
+    return iset, before, after
+
+
+@pytest.mark.parametrize("kind", ["oracle", pytest.param("gpu", marks=pytest.mark.gpu)])
+@pytest.mark.parametrize("second,fill", [(0.37, 0), (0.1, 0), (0.1, 4), (0.0, 2)])
+def test_copy_slip_memory_kat(golden, kind, second, fill):
+    """SLIP_COPY_MODE 1 (cpu/cHardwareCPU.cc:785, :7157-7161): the copy slip
+    is doSlipMutation of the whole memory at the write head.  The first
+    h-copy of the ancestor (memory 300 after h-alloc, read head 0, write head
+    100) with draws [0.37 (TestCopySlip hits), `second` (to = GetInt(301))]:
+    0.37 -> to 111, a deletion of sites 100..110 (memory 289); 0.1 -> to 30,
+    sites 30..99 duplicated at 100 (memory 370), SLIP_FILL_MODE 4 fills them
+    with nop-C instead; 0.0 -> to 0, SLIP_FILL_MODE 2 draws one GetRandomInst
+    per inserted site (memory 400).  Expected memory and flags restated in
+    the test; then both heads advance (read 1, write 101)."""
+    stream = [0.37, second] + [0.61] * 200
+    iset, (st0, o0, f0), (st, o1, f1) = _first_copy_state(kind, golden, stream, fill)
+    M = st0[0].mem_size
+    assert M == 300 and st0[0].head[1] == 0 and st0[0].head[2] == 100
+    ops, fl = list(o0[:M]), list(f0[:M])
+    ops[100] = ops[0]                              # the copy itself (COPY_MUT 0)
+    fl[100] |= 1                                   # copied flag (cpu/cHeadCPU SetFlagCopied)
+    to = int(second * 301)
+    # GetRandomInst of u = 0.61: the op whose cumulative redundancy first exceeds 0.61 * total
+    cum = np.cumsum(iset.redundancy)
+    rnd = int(np.searchsorted(cum, 0.61 * cum[-1], side="right"))
+    want_ops, want_fl = _slip_memory_expected(ops, fl, M, 100, to, fill, lambda i: rnd)
+    Mn = len(want_ops)
+    assert st[0].mem_size == Mn == M + 100 - to
+    assert list(o1[:Mn]) == want_ops
+    assert [x & 1 for x in f1[:Mn]] == [x & 1 for x in want_fl]       # copied flags stay per position
+    assert st[0].head[1] == 1 and st[0].head[2] == 101
+    assert st[0].rng_counter == 2 + (100 - to if fill == 2 else 0)
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("muts", ["copy", "all", "site", "poisson", "copyext"])
 def test_recorded_stream_frozen_traces_gpu(golden, muts):
@@ -496,8 +563,9 @@ def test_per_site_divide_mutations_world_gpu(golden, knob):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("rec", [False, True])
-def test_copy_mutations_world_gpu(golden, rec):
+@pytest.mark.parametrize("rec,slip_mode,fill", [(False, 0, 0), (True, 0, 0), (False, 1, 0), (True, 1, 2),
+                                                (False, 1, 4)])
+def test_copy_mutations_world_gpu(golden, rec, slip_mode, fill):
     """World updates with COPY_INS_PROB, COPY_DEL_PROB, COPY_UNIFORM_PROB and
     COPY_SLIP_PROB (cpu/cHardwareCPU.cc:7153-7161) on top of the default
     mutations: the memory grows and shrinks in the middle of h-copy, and a copy
@@ -505,7 +573,8 @@ def test_copy_mutations_world_gpu(golden, rec):
     class.  GPU world == oracle world, every cell digest, 150 updates; rec:
     every organism of the seeded world draws from a recorded stream."""
     ov = {"COPY_INS_PROB": 0.03, "COPY_DEL_PROB": 0.02, "COPY_UNIFORM_PROB": 0.01,
-          "COPY_SLIP_PROB": 0.005, "WORLD_X": 48, "WORLD_Y": 48}
+          "COPY_SLIP_PROB": 0.005, "WORLD_X": 48, "WORLD_Y": 48,
+          "SLIP_COPY_MODE": slip_mode, "SLIP_FILL_MODE": fill}   # mode 1: memory slips (cpu/cHardwareBase.cc:621)
     iset, env, cfg, anc = _ancestor(golden, ov)
     n = 48 * 48
     pair = [ol.Backend(k, cfg, iset, env, ncells=n) for k in ("oracle", "gpu")]
@@ -530,6 +599,6 @@ def test_copy_mutations_world_gpu(golden, rec):
     c = pair[1].counters(cumulative=1)
     assert births > 500
     assert c[capi.CNT_SPILLS] > 0          # copies rewound into the next size class
-    assert c[capi.CNT_MEM_CAP] == 0
+    assert slip_mode == 1 or c[capi.CNT_MEM_CAP] == 0
     lens = {pair[0].states(k, 1)[0][0].birth_length for k in range(0, n, 7)}
     assert len(lens) > 5

@@ -44,13 +44,13 @@ def test_oracle_tiles_loopback_equal_single_world(golden, T, geometry):
     assert sent > 0, "no offspring crossed a strip edge: the test exercised nothing"
 
 
-def _rank_main(rank, world_size, golden, port, out_dir, with_res):
+def _rank_main(rank, world_size, golden, port, out_dir, with_res, staged=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world_size)
     X, Y, U = 32, 32, 20
     env = tu.resource_env(golden) if with_res else None
     b, t = tu.make_tile("oracle", golden, X, Y, world_size, rank, env=env)
-    sw = tiles.StripWorld([t], tiles.DistTransport(dist))
+    sw = tiles.StripWorld([t], (tiles.StagedTransport if staged else tiles.DistTransport)(dist))
     births = 0
     for _ in range(U):
         sw.update()
@@ -62,14 +62,14 @@ def _rank_main(rank, world_size, golden, port, out_dir, with_res):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("with_res", [False, True])
-def test_oracle_tiles_gloo_two_ranks(golden, tmp_path, with_res):
+@pytest.mark.parametrize("with_res,staged", [(False, False), (True, False), (True, True)])
+def test_oracle_tiles_gloo_two_ranks(golden, tmp_path, with_res, staged):
     X, Y, U, T = 32, 32, 20, 2
     import socket
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
-    mp.spawn(_rank_main, args=(T, golden, port, str(tmp_path), with_res), nprocs=T, join=True)
+    mp.spawn(_rank_main, args=(T, golden, port, str(tmp_path), with_res, staged), nprocs=T, join=True)
     env = tu.resource_env(golden) if with_res else None
     ref, _ = tu.single("oracle", golden, X, Y, U, env=env)
     a, oa, fa = ref.states(0, X * Y, CAP)

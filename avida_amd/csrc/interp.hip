@@ -228,7 +228,7 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
   uint64_t clast = 0;
   // slow-switch cycles by case: pop, push, IO, h-alloc, h-divide, h-search,
   // if-label, and the stretch from the copy block to the switch
-  uint64_t cc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  uint64_t cc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};   // + IO's second half: task lookup, rewards
 #define CK(k) do { const uint64_t _n = __builtin_amdgcn_s_memtime(); cb[k] += _n - clast; clast = _n; } while (0)
 #define CKC(k) do { const uint64_t _n = __builtin_amdgcn_s_memtime(); cc[k] += _n - clast; clast = _n; } while (0)
 #elif defined(AVGPU_ISA_MARKS)
@@ -424,6 +424,8 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
   const int k_env_resources = W.env_resources;
   const uint32_t k_env_res_mask = (SIMPLE && !RES) ? 0u : W.env_res_mask;
   const uint32_t k_env_react_mask = W.env_react_mask, k_env_once_mask = W.env_once_mask;
+  const int k_task_exp = (SIMPLE && !RES) ? W.task_exp_ok : 0;
+  const uint32_t k_texp[3] = {W.task_exp[0], W.task_exp[1], W.task_exp[2]};
   // cInstSet::GetRandomInst (cpu/cInstSet.cc:83-88) from the LDS tables
   auto rand_code = [&]() -> uint8_t {
     const uint32_t r = draw_below((uint32_t)k_rand_total);
@@ -915,12 +917,28 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
       } else if (io_id >= 0) {
         tmask = lut[io_id];
       }
+      CKC(8);
       if (k_env_simple) {
         // reaction i rewards task i, requisites at most "max_count=1"
         // (capi.hip avgpu_load_env): the firing set is a bit operation and
         // the bonus factors multiply in reaction order (ascending bits)
         const uint32_t done = io ? (tmask & k_env_react_mask & ~(k_env_once_mask & nzm)) : 0u;
-        if (__ballot(done != 0u) != 0ull) {
+        if (k_task_exp) {
+          // every reward 2^e_t, no addend: bonus x prod 2^e_t = ldexp(bonus,
+          // sum e_t) exactly (capi.hip load_env)
+          if (done) {
+            int E = 0;
+#pragma unroll
+            for (int q = 0; q < AVGPU_NUM_LOGIC_TASKS; q++) {
+              const int e = (int)(int8_t)(uint8_t)(k_texp[q >> 2] >> (8 * (q & 3)));
+              E += ((done >> q) & 1u) ? e : 0;
+              tc[q] += (done >> q) & 1u;
+              rc[q] += (done >> q) & 1u;
+            }
+            nzm |= done;
+            bonus = ldexp(bonus, E);                           // cPhenotype.cc:1645-1646
+          }
+        } else if (__ballot(done != 0u) != 0ull) {
           double mult = 1.0, addb = 0.0;
           uint32_t paid = done;
           if (k_env_res_mask != 0u) {
@@ -994,6 +1012,7 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
           bonus = __dadd_rn(__dmul_rn(bonus, mult), addb);     // cPhenotype.cc:1645-1646
         }
       }
+      CKC(9);
       if (io) {
         // GetNextInput (main/cOrganism.h:249 -> cPopulationCell.h:214-218) + DoInput
         const int p = inptr >= 3 ? 0 : inptr;
@@ -1814,7 +1833,7 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
       count_add(W, CNT_IT_SLOW, (unsigned long long)it_slow);
       count_add(W, CNT_WAVES, 1ull);
       for (int k = 0; k < 6; k++) count_add(W, CNT_CB0 + k, cb[k]);
-      for (int k = 0; k < 8; k++) count_add(W, CNT_CASE0 + k, cc[k]);
+      for (int k = 0; k < 10; k++) count_add(W, CNT_CASE0 + k, cc[k]);
     }
   }
 #endif

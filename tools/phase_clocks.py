@@ -55,7 +55,8 @@ def main():
         "loop_cycles_per_iter_by_block": {k: tot[32 + i] / it for i, k in enumerate(
             ["decode", "fast", "copy", "switch", "wave_phase", "advance"])},
         "slow_phase_cycles_per_iter_by_case": {k: tot[38 + i] / it for i, k in enumerate(
-            ["pop", "push", "io", "h_alloc", "h_divide", "h_search", "if_label", "pre_switch"])},
+            ["pop", "push", "io", "h_alloc", "h_divide", "h_search", "if_label", "pre_switch",
+             "io2_task_lookup", "io2_rewards"])},
     }
     lib.avgpu_destroy(h)
     print(json.dumps(out, indent=1))

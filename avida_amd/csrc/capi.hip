@@ -678,20 +678,6 @@ int avgpu_load_env(avgpu_world* w, int nreact, const avgpu_reaction* r) {
   W.env_res_mask = simple ? res_mask : 0u;   // the simple path indexes reactions by task
   HIPCHK(hipMemcpyAsync(W.react_res, rr, sizeof(rr), hipMemcpyHostToDevice, w->stream));
   W.env_simple = simple ? 1 : 0;
-  // rewards that are exact powers of two with no addend: bonus x (product of
-  // the factors) = ldexp(bonus, sum of the exponents), bit for bit (each
-  // product of powers of two is exact; |sum| <= 9 x 63 stays in range)
-  bool p2 = simple && res_mask == 0u;
-  uint32_t tex[3] = {0u, 0u, 0u};
-  for (int t = 0; t < AVGPU_NUM_LOGIC_TASKS && p2; t++) {
-    if (!((rmask >> t) & 1u)) continue;                  // never rewarded: exponent 0
-    int e = 0;
-    const double fr = std::frexp(ttab[t], &e);
-    if (ttab[16 + t] != 0.0 || fr != 0.5 || e - 1 < -63 || e - 1 > 63) { p2 = false; break; }
-    tex[t / 4] |= (uint32_t)((e - 1) & 0xFF) << (8 * (t % 4));
-  }
-  W.task_exp_ok = p2 ? 1 : 0;
-  for (int k = 0; k < 3; k++) W.task_exp[k] = p2 ? tex[k] : 0u;
   W.env_react_mask = rmask;
   W.env_once_mask = omask;
   HIPCHK(hipMemcpyAsync(W.task_tab, ttab, sizeof(ttab), hipMemcpyHostToDevice, w->stream));

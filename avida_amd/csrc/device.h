@@ -271,11 +271,6 @@ struct DevWorld {
   int32_t slip_fill_mode;
   int32_t trans_fill_mode;
   int32_t slip_copy_mode;   // SLIP_COPY_MODE: 0 the read head jumps, 1 a slip of the whole memory
-  // simple environment whose every reward is an exact power of two with no
-  // addend (logic-9's pow processes): task t's exponent is the signed byte t
-  // of task_exp[] and the IO path adds exponents (interp.hip, capi.hip load_env)
-  int32_t task_exp_ok;
-  uint32_t task_exp[3];
   // RECORDED mode (avgpu_set_rng_mode): rec_n doubles; rec_off[c] = the start
   // of cell c's organism's segment, -1 = a counter stream.  rec == nullptr:
   // COUNTER mode everywhere (the REC-free interpreter instantiations run).

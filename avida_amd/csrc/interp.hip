@@ -424,8 +424,6 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
   const int k_env_resources = W.env_resources;
   const uint32_t k_env_res_mask = (SIMPLE && !RES) ? 0u : W.env_res_mask;
   const uint32_t k_env_react_mask = W.env_react_mask, k_env_once_mask = W.env_once_mask;
-  const int k_task_exp = (SIMPLE && !RES) ? W.task_exp_ok : 0;
-  const uint32_t k_texp[3] = {W.task_exp[0], W.task_exp[1], W.task_exp[2]};
   // cInstSet::GetRandomInst (cpu/cInstSet.cc:83-88) from the LDS tables
   auto rand_code = [&]() -> uint8_t {
     const uint32_t r = draw_below((uint32_t)k_rand_total);
@@ -923,22 +921,7 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
         // (capi.hip avgpu_load_env): the firing set is a bit operation and
         // the bonus factors multiply in reaction order (ascending bits)
         const uint32_t done = io ? (tmask & k_env_react_mask & ~(k_env_once_mask & nzm)) : 0u;
-        if (k_task_exp) {
-          // every reward 2^e_t, no addend: bonus x prod 2^e_t = ldexp(bonus,
-          // sum e_t) exactly (capi.hip load_env)
-          if (done) {
-            int E = 0;
-#pragma unroll
-            for (int q = 0; q < AVGPU_NUM_LOGIC_TASKS; q++) {
-              const int e = (int)(int8_t)(uint8_t)(k_texp[q >> 2] >> (8 * (q & 3)));
-              E += ((done >> q) & 1u) ? e : 0;
-              tc[q] += (done >> q) & 1u;
-              rc[q] += (done >> q) & 1u;
-            }
-            nzm |= done;
-            bonus = ldexp(bonus, E);                           // cPhenotype.cc:1645-1646
-          }
-        } else if (__ballot(done != 0u) != 0ull) {
+        if (__ballot(done != 0u) != 0ull) {
           double mult = 1.0, addb = 0.0;
           uint32_t paid = done;
           if (k_env_res_mask != 0u) {

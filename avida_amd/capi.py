@@ -128,7 +128,7 @@ class AvgpuCpuState(C.Structure):
         ("last_task_count", C.c_int32 * MAX_REACTIONS),
         ("cur_reaction_count", C.c_int32 * MAX_REACTIONS),
         ("rng_counter", C.c_uint32), ("rng_key_lo", C.c_uint32), ("rng_key_hi", C.c_uint32),
-        ("errors", C.c_int32), ("head_start", C.c_uint32),
+        ("errors", C.c_int32), ("head_start", C.c_uint32), ("age", C.c_int32), ("pad1", C.c_int32),
         ("cur_bonus", C.c_double), ("merit", C.c_double), ("fitness", C.c_double),
         ("credit", C.c_double),
     ]

@@ -28,7 +28,10 @@ import numpy as np
 
 from . import capi
 
-VERSION = 2
+VERSION = 3
+# round 5 added `age` (+ a pad word) before cur_bonus: an older state record
+# gets them inserted as zeros (age 0: as if every organism had just divided)
+_AGE_OFF = capi.AvgpuCpuState.age.offset
 
 
 def _call(lib, prefix, name, *args):
@@ -81,9 +84,14 @@ def load(lib, prefix, handle, path):
     if "version" in z.files and int(z["version"]) > VERSION:
         raise ValueError(f"checkpoint version {int(z['version'])} is newer than this reader ({VERSION})")
     raw = z["states"].tobytes()
-    ssz = int(z["state_size"]) if "state_size" in z.files else C.sizeof(capi.AvgpuCpuState)
-    if ssz != C.sizeof(capi.AvgpuCpuState) or len(raw) != ssz * ncells:
-        raise ValueError(f"checkpoint state records are {ssz} B, this build's are {C.sizeof(capi.AvgpuCpuState)} B")
+    size = C.sizeof(capi.AvgpuCpuState)
+    ssz = int(z["state_size"]) if "state_size" in z.files else len(raw) // max(1, ncells)
+    if ssz == size - 8 and len(raw) == ssz * ncells:       # before `age` (version <= 2)
+        raw = b"".join(raw[k * ssz:k * ssz + _AGE_OFF] + b"\0" * 8 + raw[k * ssz + _AGE_OFF:(k + 1) * ssz]
+                       for k in range(ncells))
+        ssz = size
+    if ssz != size or len(raw) != ssz * ncells:
+        raise ValueError(f"checkpoint state records are {ssz} B, this build's are {size} B")
     st = (capi.AvgpuCpuState * ncells).from_buffer_copy(raw)
     tape = z["tape"]
     ops = np.ascontiguousarray(tape & 0x3F)

@@ -104,7 +104,7 @@ int setup_world(avgpu_world* w, int64_t n, bool test_buffers) {
   const avgpu_cfg& c = w->cfg;
   int rc = 0;
 #define A(ptr, cnt) if ((rc = w->alloc(&W.ptr, (size_t)(cnt))) < 0) return rc
-  A(xs, (size_t)n * XS_WORDS); A(ctl, n); A(mem_size, n); A(max_exec, n); A(birth_len, n); A(gkey, n); A(rng, 3 * n);
+  A(xs, (size_t)n * XS_WORDS); A(ctl, n); A(mem_size, n); A(max_exec, n); A(age, n); A(birth_len, n); A(gkey, n); A(rng, 3 * n);
   A(budget, n); A(aclass, n); A(tape, (size_t)n * TAPE_SLOT);
   A(inputs, 3 * n); A(last_task, AVGPU_MAX_REACTIONS * n);
   A(cur_react, AVGPU_MAX_REACTIONS * n);
@@ -284,8 +284,10 @@ std::string unsupported_cfg(const avgpu_cfg& c) {
   if (c.world_geometry != 1 && c.world_geometry != 2) return "WORLD_GEOMETRY other than 1 (grid) or 2 (torus)";
   if (c.slicing_method < 0 || c.slicing_method > 2) return "SLICING_METHOD other than 0, 1, 2";
   if (c.base_merit_method < 0 || c.base_merit_method > 5) return "BASE_MERIT_METHOD other than 0..5";
-  if (c.birth_method != 0 && c.birth_method != 3)
-    return "BIRTH_METHOD other than 0 (random neighbour) and 3 (empty cells only)";
+  if (c.birth_method < 0 || c.birth_method > 3)
+    return "BIRTH_METHOD other than 0 (random neighbour), 1 (oldest), 2 (highest age / merit), 3 (empty only)";
+  if ((c.birth_method == 1 || c.birth_method == 2) && !c.prefer_empty)
+    return "BIRTH_METHOD 1 / 2 without PREFER_EMPTY (the reference reads the organism of an empty cell)";
   if (c.death_method < 0 || c.death_method > 2) return "DEATH_METHOD other than 0, 1, 2";
   if (c.alloc_method != 0 && c.alloc_method != 2) return "ALLOC_METHOD other than 0 (default) and 2 (random)";
   if (nz(c.point_mut_prob) || nz(c.point_ins_prob) || nz(c.point_del_prob) || nz(c.inst_point_mut_prob))
@@ -872,9 +874,12 @@ int avgpu_run_serial_updates(avgpu_world* w, int n, avgpu_update_stats* last) {
   if (W.rec) return fail(AVGPU_EUNSUPPORTED, "the serial world takes its own two streams (avgpu_set_serial_streams), "
                                              "not per-organism recorded streams");
   if (W.tiled) return fail(AVGPU_EUNSUPPORTED, "the serial world runs single worlds, not strip tiles");
+  if (W.birth_method == 1 || W.birth_method == 2)
+    return fail(AVGPU_EUNSUPPORTED, "BIRTH_METHOD 1 / 2 run on the batch world, not the serial world");
   if ((rc = serial_alloc(w)) < 0) return rc;
   for (int u = 0; u < n; u++) {
     launch_reset_counts(W, w->stream);
+    launch_age_tick(W, w->stream);
     launch_resources_begin(W, w->stream);
     after_resources_begin(w);
     if ((rc = push_world(w)) < 0) return rc;
@@ -1346,6 +1351,8 @@ int avgpu_get_resources(avgpu_world* w, double* levels, double* spatial) {
 // ---- strip tiles (DESIGN.md "Multi-GPU") ----
 int avgpu_set_tile(avgpu_world* w, int64_t row0, int64_t arena_bytes) {
   if (w && w->cfg.sub_updates > 1) return fail(AVGPU_EUNSUPPORTED, "sub_updates > 1 on strip tiles");
+  if (w && (w->cfg.birth_method == 1 || w->cfg.birth_method == 2))
+    return fail(AVGPU_EUNSUPPORTED, "BIRTH_METHOD 1 / 2 on strip tiles (the ghost rows carry no age or merit)");
   if (!w) return fail(AVGPU_EINVAL, "NULL world");
   DevWorld& W = w->W;
   const int64_t X = W.world_x;

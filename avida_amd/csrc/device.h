@@ -110,6 +110,7 @@ struct DevWorld {
   uint32_t* ctl;      // [n]  sp0 | sp1<<4 | cur_stack | mal_active | alive
   int32_t* mem_size;  // [n]
   int32_t* max_exec;  // [n]
+  int32_t* age;       // [n] cPhenotype::age during the update (k_allot ticks it; -1 injected, 0 born / divided)
   int32_t* birth_len; // [n]  genome length at birth (cPhenotype::genome_length)
   uint64_t* gkey;     // [n]  genome key of the birth genome (systematics census)
   uint32_t* rng;      // [3][n] key_lo, key_hi, ctr
@@ -720,6 +721,7 @@ void launch_interpret_classes(const DevWorld& W, const DevWorld* dW, int mode, h
 // last of them), then one bucket for the window's cells that are not class 0
 #define SORT_BUCKETS 258
 bool class_timing_all();   // AVGPU_CLASS_TIMING (interp.hip)
+void launch_age_tick(const DevWorld& W, hipStream_t s);
 // sub-update `sub` of `nsub` (avgpu_cfg.sub_updates): the
 // resources step and the update's counters are reset at sub 0 only; the key
 // of the scheduler's node draws is update x nsub + sub (the caller's `update`)

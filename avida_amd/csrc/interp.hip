@@ -1712,6 +1712,7 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
     // (a fresh organism's zero rows are stored here rather than at activation:
     // k_activate is bound by its scattered stores, class 0 is not)
     if (didv || fresh) { W.num_div[cell] = dnd; W.generation[cell] = dgen; }
+    if (didv) W.age[cell] = 0;                               // DivideReset (main/cPhenotype.cc:950)
     // (a deferred divide's executed size: a spill row continuing this slice
     // in the same update reads it at its staging)
     if (didv) W.executed[cell] = dexe;

@@ -124,6 +124,7 @@ __global__ void k_set_orgs(DevWorld W, int64_t first, int64_t count, const uint8
   }
   W.max_exec[c] = mx;
   W.birth_len[c] = len;
+  W.age[c] = -1;                            // injected between updates: age 0 during the next one
   W.gkey[c] = gk_tape(t, len);
   // stream key (DESIGN.md RNG spec)
   uint32_t lo, hi, ctr = 0;
@@ -208,6 +209,7 @@ __device__ void build_state(const DevWorld& W, int64_t c, avgpu_cpu_state& s) {
   s.fitness = W.fitness[c];
   s.credit = W.credit[c];
   s.head_start = CTL_HS(ctl);
+  s.age = W.age[c] + 1;                     // as UpdateOrganismStats leaves it at the update's end
 }
 
 __global__ void k_get_states(DevWorld W, int64_t first, int64_t count, avgpu_cpu_state* out,
@@ -262,6 +264,7 @@ __global__ void k_set_states(DevWorld W, int64_t first, int64_t count, const avg
   const int64_t N = W.n;
   const int64_t c = first + i;
   const avgpu_cpu_state s = in[i];
+  W.age[c] = s.age - 1;
   int32_t* x = W.xs + c * XS_WORDS;
   for (int k = 0; k < XS_WORDS; k++) x[k] = 0;
   for (int k = 0; k < 3; k++) x[XS_REG + k] = s.reg[k];
@@ -646,7 +649,7 @@ __device__ __forceinline__ void occ_init_cell(const DevWorld& W, int64_t c) {
 // update (living cells occupied; an organism that dies in its slice clears
 // its cell at write-back), its kill time, the previous update's round-3
 // claim, and the class lists.
-__global__ __launch_bounds__(1024) void k_allot(DevWorld W, const double* totals, uint32_t update) {
+__global__ __launch_bounds__(1024) void k_allot(DevWorld W, const double* totals, uint32_t update, int tick) {
   const int lane = threadIdx.x & 63;
   const int64_t b = (int64_t)blockIdx.x * 16 + (threadIdx.x >> 6);
   const int64_t nb = (W.n + 255) / 256;
@@ -724,6 +727,7 @@ __global__ __launch_bounds__(1024) void k_allot(DevWorld W, const double* totals
         W.credit[c] = __dsub_rn(cr, fl);
       }
       if (ctl[j] & CTL_HS_MASK) W.ctl[c] = ctl[j] & ~CTL_HS_MASK;   // the head start is used up
+      if (tick) W.age[c] += 1;     // cPhenotype::IncAge at the previous update's end (oracle age_tick)
       want[j] = bud > 0;
       if (want[j]) cls[j] = class_of(need_of_cell(W, (int)c));
     }
@@ -978,6 +982,16 @@ __device__ __forceinline__ int last_claim_round(int st) {
 // m > 0 also every cell claimed in round m - 1 (tile_m >= 0: here or by the
 // neighbour, tile_taken).  Returns false for no cell.
 __device__ __forceinline__ bool tile_taken(const DevWorld& W, int64_t c, int m);
+// BIRTH_METHOD 1: the cell's organism's age; 2: cOrganism::CalcMeritRatio
+// (main/cOrganism.cc:703-708, age / merit, or the age without a positive
+// merit); an empty cell (a newborn's to be) 0 (oracle position_value)
+__device__ __forceinline__ double position_value(const DevWorld& W, int c) {
+  if (c >= W.n || !(W.ctl[c] & CTL_ALIVE)) return 0.0;
+  const double age = (double)W.age[c];
+  if (W.birth_method == 1) return age;
+  const double m = W.merit[c];
+  return m > 0.0 ? __ddiv_rn(age, m) : age;
+}
 template <bool TILE>
 __device__ __forceinline__ bool place_pick_one(const DevWorld& W, int64_t r, int m) {
   const int parent = W.b_parent[r];
@@ -994,7 +1008,18 @@ __device__ __forceinline__ bool place_pick_one(const DevWorld& W, int64_t r, int
   if (W.prefer_empty)
     for (int k = 0; k < nn; k++)
       if (!taken(nbr[k])) cand[nc++] = nbr[k];
-  if (nc == 0 && W.birth_method != 3) {
+  if (nc == 0 && (W.birth_method == 1 || W.birth_method == 2)) {
+    // PositionAge / PositionMerit (main/cPopulation.cc:5416-5470): the parent
+    // first, valued -1 without ALLOW_PARENT; a neighbour of a larger value
+    // replaces the list, one of an equal value joins it (oracle place_pick)
+    double best = W.allow_parent ? position_value(W, parent) : -1.0;
+    cand[nc++] = parent;
+    for (int k = 0; k < nn; k++) {
+      const double v = position_value(W, nbr[k]);
+      if (v > best) { best = v; nc = 0; cand[nc++] = nbr[k]; }
+      else if (v == best) cand[nc++] = nbr[k];
+    }
+  } else if (nc == 0 && W.birth_method != 3) {
     for (int k = 0; k < nn; k++) cand[nc++] = nbr[k];
     if (W.allow_parent) cand[nc++] = parent;
   }
@@ -1683,11 +1708,11 @@ __global__ __launch_bounds__(256) void k_reset_counts(DevWorld W) { reset_counts
 // the allotment of a world whose block counts are in W.blk_count: budgets,
 // class lists, occupancy; then the class-0 order
 static void launch_allot(const DevWorld& W, hipStream_t s, const double* totals, hipEvent_t lists_ready,
-                         uint32_t update) {
+                         uint32_t update, int tick = 1) {
   // (16 blocks per workgroup: the class lists take one global atomic per
   // class and 4096 cells -- with 1024-cell workgroups those atomics on three
   // addresses serialised to ~50 us per update, profiles/r04c_tail_per_update.txt)
-  hipLaunchKernelGGL(k_allot, dim3(nblk(W.n, 4096)), dim3(1024), 0, s, W, totals, update);
+  hipLaunchKernelGGL(k_allot, dim3(nblk(W.n, 4096)), dim3(1024), 0, s, W, totals, update, tick);
   // the class lists are complete: the aux streams of the list classes start
   // here, beside the window sort, so that their blocks take CUs before class 0
   // (with the sort folded into the allotment they start together with class 0
@@ -1706,7 +1731,7 @@ void launch_world_begin(const DevWorld& W, hipStream_t s, double* totals, double
   hipLaunchKernelGGL(k_merit_partial, dim3((unsigned)((nb + 3) / 4)), dim3(256), 0, s, W, scratch, alive_partial,
                      (double*)nullptr, sub == 0 ? 1 : 2);
   launch_block_counts(W, s, scratch, alive_partial, nb, 1, tree_levels(nb), totals, update, 0, sub, nsub);
-  launch_allot(W, s, totals, lists_ready, update);
+  launch_allot(W, s, totals, lists_ready, update, sub == 0 ? 1 : 0);
 }
 
 // a world whose totals were handed in (avgpu_update_totals + an all-reduce of
@@ -1763,6 +1788,15 @@ static unsigned mut_grid(const DevWorld& W) { return (unsigned)std::min<int64_t>
 void launch_serial_post(const DevWorld& W, hipStream_t s, double* stats) {
   launch_resources_end(W, s);
   launch_stats(W, s, stats);
+}
+
+// the serial world's cPhenotype::IncAge tick (k_allot's, for the batch update)
+__global__ void k_age_tick(DevWorld W) {
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c < W.n && (W.ctl[c] & CTL_ALIVE)) W.age[c] += 1;
+}
+void launch_age_tick(const DevWorld& W, hipStream_t s) {
+  hipLaunchKernelGGL(k_age_tick, dim3(nblk(W.n, 256)), dim3(256), 0, s, W);
 }
 
 void launch_reset_counts(const DevWorld& W, hipStream_t s) {

@@ -291,6 +291,11 @@ typedef struct avgpu_cpu_state {
   int32_t errors;                      /* cPhenotype::cur_num_errors (faults) */
   uint32_t head_start;                 /* 2^16 - birth time of an offspring not yet allotted (its first
                                           allotment weights its merit by 1 + head_start / 2^16); 0 otherwise */
+  int32_t age;                         /* cPhenotype::age: updates since birth or the last divide, as the
+                                          reference's UpdateOrganismStats leaves it at the end of the last
+                                          update (main/cPopulation.cc:6021, main/cPhenotype.cc:950) --
+                                          BIRTH_METHOD 1 (PositionAge) and 2 (PositionMerit) compare it */
+  int32_t pad1;
   double cur_bonus;
   double merit;
   double fitness;

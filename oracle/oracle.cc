@@ -216,6 +216,7 @@ struct Org {
   // batch-world bookkeeping
   Stream rng;
   double credit = 0.0;
+  int age = 0;           // cPhenotype::age during the update (BIRTH_METHOD 1 / 2; age_tick)
   uint32_t hstart = 0;   // head start: 2^16 - birth time, for the first allotment after birth (sched_weight)
   int spec_count = 0;
   // test-CPU outputs
@@ -475,6 +476,7 @@ struct Exec {
     o.cur_bonus = w.cfg.default_bonus;
     o.cpu_cycles_used = 0;
     o.errors = 0;
+    o.age = 0;   // DivideReset (main/cPhenotype.cc:950)
     o.num_divides++;
     if (mode == AVGPU_MODE_TEST) o.generation++;  // TestDivideReset :1160; world: GENERATION_INC_METHOD 1
     else o.generation++;
@@ -1086,6 +1088,7 @@ struct Exec {
 void setup_inject(World& w, Org& o, const uint8_t* genome, int len, double merit) {
   o = Org();
   o.alive = true;
+  o.age = -1;   // injected between updates: age 0 during the next one (age_tick)
   o.genome.assign(genome, genome + len);
   o.mem = o.genome;
   o.flg.assign(len, 0);
@@ -1151,6 +1154,7 @@ void dump_state(const World& w, const Org& o, avgpu_cpu_state* s, uint8_t* ops, 
   s->fitness = o.fitness;
   s->credit = o.credit;
   s->head_start = o.hstart;
+  s->age = o.age + 1;   // as the reference's UpdateOrganismStats leaves it (age_tick)
   (void)w;
   if (ops && flags) {
     for (int i = 0; i < cap; i++) {
@@ -1379,6 +1383,7 @@ void activate_child(World& w, Birth& b, int64_t cell, Stream* ctx = nullptr) {
   o.generation = b.generation;
   for (int t = 0; t < AVGPU_NUM_LOGIC_TASKS; t++) o.last_task[t] = b.last_task[t];
   o.rng = b.rng;
+  o.age = 0;   // cPhenotype::SetupOffspring (main/cPhenotype.cc:705): 0 for the rest of its birth update
   // cEnvironment::SetupInputs random (main/cEnvironment.cc:1268-1271)
   Stream& r = ctx ? *ctx : o.rng;
   o.inputs[0] = (15 << 24) + (int)r.uint_below(1u << 24);
@@ -1766,6 +1771,7 @@ int orc_set_states(void* h, int64_t first, int64_t count, const avgpu_cpu_state*
     o.errors = s.errors;
     o.cur_bonus = s.cur_bonus; o.merit = s.merit; o.fitness = s.fitness; o.credit = s.credit;
     o.hstart = s.head_start;
+    o.age = s.age - 1;
   }
   return 0;
 }
@@ -2137,6 +2143,18 @@ static inline bool takes_cell(const World& w, int64_t owner, uint32_t t) {
 // ALLOW_PARENT (:706-713); otherwise it is never placed (BS_NO_CELL).
 // Writes the record's target and key (and w.tgt_r[m][i]); returns false for
 // no cell.
+// A cell's value for BIRTH_METHOD 1 (its organism's age) or 2
+// (cOrganism::CalcMeritRatio, main/cOrganism.cc:703-708: age / merit, or the
+// age without a positive merit) at the batch step's end; an empty cell (a
+// newborn's to be) is worth 0.
+static double position_value(const World& w, int64_t c) {
+  if (c >= w.ncells || !w.orgs[c].alive) return 0.0;
+  const Org& o = w.orgs[c];
+  const double age = (double)o.age;
+  if (w.cfg.birth_method == 1) return age;
+  return o.merit > 0.0 ? age / o.merit : age;
+}
+
 template <class Taken>
 static bool place_pick(World& w, int64_t i, int m, Taken taken) {
   Birth& b = w.births[i];
@@ -2146,7 +2164,18 @@ static bool place_pick(World& w, int64_t i, int m, Taken taken) {
   int nc = 0;
   if (w.cfg.prefer_empty)
     for (int k = 0; k < nn; k++) if (!taken(nb[k])) cand[nc++] = nb[k];
-  if (nc == 0 && w.cfg.birth_method != 3) {
+  if (nc == 0 && (w.cfg.birth_method == 1 || w.cfg.birth_method == 2)) {
+    // PositionAge / PositionMerit (main/cPopulation.cc:5416-5470): the parent
+    // first, valued -1 without ALLOW_PARENT; each neighbour of a larger value
+    // replaces the list, one of an equal value joins it
+    double best = w.cfg.allow_parent ? position_value(w, b.parent) : -1.0;
+    cand[nc++] = b.parent;
+    for (int k = 0; k < nn; k++) {
+      const double v = position_value(w, nb[k]);
+      if (v > best) { best = v; nc = 0; cand[nc++] = nb[k]; }
+      else if (v == best) cand[nc++] = nb[k];
+    }
+  } else if (nc == 0 && w.cfg.birth_method != 3) {
     for (int k = 0; k < nn; k++) cand[nc++] = nb[k];
     if (w.cfg.allow_parent) cand[nc++] = b.parent;
   }
@@ -2212,6 +2241,14 @@ static void place_finish_single(World& w, int64_t& placed_out, int64_t& dropped_
 // 621-952), so K steps bring the batch model's weight refresh K times closer
 // to it.  Resources step once per update (at sub-update 0); global
 // consumption settles after each sub-update; K = 1 is the plain batch update.
+// cPhenotype::IncAge for every living organism (UpdateOrganismStats,
+// main/cPopulation.cc:6021, at the end of each update): here at the start of
+// the next, so that Org::age is the reference's age DURING the update --
+// injected organisms start at -1, newborns and dividers are set to 0.
+static void age_tick(World& w) {
+  for (int64_t c = 0; c < w.ncells; c++) if (w.orgs[c].alive) w.orgs[c].age++;
+}
+
 static inline int sub_updates_of(const avgpu_cfg& c) { return c.sub_updates > 1 ? c.sub_updates : 1; }
 static inline int64_t sub_share(int64_t n, int s, int K) {
   return K == 1 ? n : (n * (s + 1)) / K - (n * s) / K;
@@ -2244,6 +2281,7 @@ static int run_update_impl(World& w) {
     std::vector<int64_t> blk;
     top_tree(w, part, n_root, 0, (int64_t)part.size(), &blk);
     if (sub == 0) res_begin(w);   // resources step once per update, at its start
+    if (sub == 0) age_tick(w);
     allot_interpret(w, blk, total, ud);
     insts += w.t_insts; deaths += w.t_deaths; divides += w.t_divides; slices += w.t_slices;
     res_end(w);
@@ -2343,6 +2381,8 @@ bool tile_ok(World& w) { return w.tiled && w.h_send[0] && w.r_recv[1]; }
 
 int orc_set_tile(void* h, int64_t row0, int64_t arena) {
   World& w = *(World*)h;
+  if (w.cfg.birth_method == 1 || w.cfg.birth_method == 2)
+    return fail(AVGPU_EUNSUPPORTED, "BIRTH_METHOD 1 / 2 on strip tiles (the ghost rows carry no age or merit)");
   const int64_t X = w.cfg.world_x;
   if (X <= 0 || w.ncells % X) return fail(AVGPU_EINVAL, "tile cells must be whole rows of WORLD_X");
   const int64_t rows = w.ncells / X;
@@ -2440,6 +2480,7 @@ int orc_tile_begin(void* h, const double* gathered, int ntiles) {
   if (!tile_ok(w)) return fail(AVGPU_ESTATE, "not a strip tile with buffers");
   if (sub_updates_of(w.cfg) > 1) return fail(AVGPU_EUNSUPPORTED, "sub_updates > 1 on strip tiles");
   w.sched_key = (uint32_t)w.update;
+  age_tick(w);
   // the top tree over every strip's block partials (tile order = block order)
   const int64_t nb = (w.ncells + 255) / 256;
   std::vector<double> leaf((size_t)(nb * ntiles));
@@ -2809,6 +2850,8 @@ int orc_set_serial_streams(void* h, const double* sched, int64_t n_sched, const 
 //    before the speculative run: rotated connection lists (serial_target).
 int orc_run_serial_updates(void* h, int n_updates, avgpu_update_stats* out) {
   World& w = *(World*)h;
+  if (w.cfg.birth_method == 1 || w.cfg.birth_method == 2)
+    return fail(AVGPU_EUNSUPPORTED, "BIRTH_METHOD 1 / 2 run on the batch world, not the serial world");
   if ((int64_t)w.face.size() != w.ncells) w.face.assign(w.ncells, 0);
   SerialSched sch;
   sch.init(w.ncells);
@@ -2818,6 +2861,7 @@ int orc_run_serial_updates(void* h, int n_updates, avgpu_update_stats* out) {
     for (int64_t c = 0; c < w.ncells; c++) n_alive += w.orgs[c].alive;
     const int64_t ud = (int64_t)w.cfg.ave_time_slice * n_alive;   // cWorld::CalculateUpdateSize
     int64_t insts = 0, births = 0, deaths = 0, divides = 0, dropped = 0;
+    age_tick(w);
     res_begin(w);   // ProcessPreUpdate + the update's first DoUpdates
     for (int64_t i = 0; i < ud; i++) {
       const double tot = sch.tree[1];

@@ -66,3 +66,39 @@ def resume_case(kind_a, kind_b, golden, env_kind, tmp_path, u1=20, u2=15):
 @pytest.mark.parametrize("env_kind", ["logic9", "resources"])
 def test_oracle_checkpoint_resume(golden, tmp_path, env_kind):
     resume_case("oracle", "oracle", golden, env_kind, tmp_path)
+
+
+def test_older_checkpoint_formats_load(golden, tmp_path):
+    """A checkpoint written before round 4 (stats without births_cancelled /
+    seed) and round 5 (state records without `age`) loads: the missing
+    fields are zero -- the world's configured seed stays, every organism's
+    age is 0 -- and the world continues."""
+    import ctypes as C
+    import numpy as np
+    n = 32 * 32
+    a = _world("oracle", golden, "logic9")
+    for _ in range(10):
+        a.run_update()
+    path = os.path.join(tmp_path, "w.npz")
+    a.checkpoint(path)
+    z = dict(np.load(path, allow_pickle=False))
+    size = C.sizeof(capi.AvgpuCpuState)
+    off = capi.AvgpuCpuState.age.offset
+    raw = z["states"].tobytes()
+    old = b"".join(raw[k * size:k * size + off] + raw[k * size + off + 8:(k + 1) * size] for k in range(n))
+    z["states"] = np.frombuffer(old, dtype=np.uint8)
+    z["stats"] = z["stats"][:C.sizeof(capi.AvgpuUpdateStats) - 16]      # no births_cancelled, seed
+    for k in ("version", "state_size", "stats_size"):
+        z.pop(k)
+    old_path = os.path.join(tmp_path, "old.npz")
+    np.savez_compressed(old_path, **z)
+    b = _world("oracle", golden, "logic9", seed=5)
+    last = b.restore(old_path)
+    assert last.update == 9 and last.seed == 0 and last.births_cancelled == 0
+    st, _, _ = b.states(0, n, CAP)
+    assert all(st[i].age == 0 for i in range(n))
+    sa, _, _ = a.states(0, n, CAP)
+    assert [sa[i].merit for i in range(n)] == [st[i].merit for i in range(n)]
+    for _ in range(5):
+        b.run_update()
+    assert b.run_update().num_organisms > 0

@@ -241,7 +241,7 @@ __device__ __forceinline__ void setup_child(const DevWorld& W, int64_t c, const 
       W.rng[c] = b.lo; W.rng[N + c] = b.hi; W.rng[2 * N + c] = ctr;
       if (W.rec_off) W.rec_off[c] = -1;         // offspring: counter streams
       break; }
-    case 12 + AVGPU_NUM_LOGIC_TASKS: W.age[c] = 0; break;   // SetupOffspring (main/cPhenotype.cc:705)
+    case 12 + AVGPU_NUM_LOGIC_TASKS: if (W.track_age) W.age[c] = 0; break;   // SetupOffspring (main/cPhenotype.cc:705)
     default:                                   // last_task_count = the parent's (:447)
       if (lane >= 12 && lane < 12 + AVGPU_NUM_LOGIC_TASKS)
         W.last_task[(int64_t)(lane - 12) * N + c] = b.ltask[(int64_t)(lane - 12) * b.lstride];
@@ -288,7 +288,7 @@ __device__ __forceinline__ void setup_child_lane(const DevWorld& W, int64_t c, c
   if (W.death_method > 0) { mx = W.age_limit; if (W.death_method == 2) mx *= len; if (mx < 1) mx = 1; }
   W.max_exec[c] = mx;
   W.birth_len[c] = len;
-  W.age[c] = 0;                                // SetupOffspring (main/cPhenotype.cc:705)
+  if (W.track_age) W.age[c] = 0;               // SetupOffspring (main/cPhenotype.cc:705)
   W.merit[c] = b.merit;
   W.fitness[c] = b.fitness;
   W.credit[c] = 0.0;

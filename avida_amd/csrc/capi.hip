@@ -233,6 +233,7 @@ int setup_world(avgpu_world* w, int64_t n, bool test_buffers) {
   W.slip_fill_mode = c.slip_fill_mode;
   W.trans_fill_mode = c.trans_fill_mode;
   W.slip_copy_mode = c.slip_copy_mode;
+  W.track_age = (c.birth_method == 1 || c.birth_method == 2) ? 1 : 0;
   W.rec = nullptr; W.rec_n = 0; W.rec_off = nullptr;
   W.seed_lo = (uint32_t)c.seed;
   W.seed_hi = (uint32_t)(c.seed >> 32);

@@ -110,7 +110,8 @@ struct DevWorld {
   uint32_t* ctl;      // [n]  sp0 | sp1<<4 | cur_stack | mal_active | alive
   int32_t* mem_size;  // [n]
   int32_t* max_exec;  // [n]
-  int32_t* age;       // [n] cPhenotype::age during the update (k_allot ticks it; -1 injected, 0 born / divided)
+  int32_t* age;       // [n] cPhenotype::age during the update (k_allot ticks it; -1 injected, 0 born / divided),
+                      // kept only when track_age (BIRTH_METHOD 1 / 2, its one consumer on this path)
   int32_t* birth_len; // [n]  genome length at birth (cPhenotype::genome_length)
   uint64_t* gkey;     // [n]  genome key of the birth genome (systematics census)
   uint32_t* rng;      // [3][n] key_lo, key_hi, ctr
@@ -247,6 +248,7 @@ struct DevWorld {
   int32_t cfg_min_genome, cfg_max_genome;  // raw MIN_GENOME_SIZE / MAX_GENOME_SIZE
   int32_t death_method, age_limit;
   int32_t prefer_empty, allow_parent, birth_method;
+  int32_t track_age;  // BIRTH_METHOD 1 / 2: the age row is maintained
   // P(p) = u < p: counter threshold ceil(p 2^32), and p itself
   // for RECORDED draws
   uint64_t th_copy_mut, th_div_mut, th_div_ins, th_div_del, th_div_slip, th_div_uni;

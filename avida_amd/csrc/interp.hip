@@ -1712,7 +1712,7 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
     // (a fresh organism's zero rows are stored here rather than at activation:
     // k_activate is bound by its scattered stores, class 0 is not)
     if (didv || fresh) { W.num_div[cell] = dnd; W.generation[cell] = dgen; }
-    if (didv) W.age[cell] = 0;                               // DivideReset (main/cPhenotype.cc:950)
+    if (!DEF && didv && W.track_age) W.age[cell] = 0;        // DivideReset (main/cPhenotype.cc:950)
     // (a deferred divide's executed size: a spill row continuing this slice
     // in the same update reads it at its staging)
     if (didv) W.executed[cell] = dexe;
@@ -2127,7 +2127,7 @@ static bool def_knobs(const DevWorld& W) {
          W.base_merit_method == 4 && W.th_div_uni == 0 && !W.seg_any && W.th_par_site == 0 && W.th_par_ins == 0 &&
          W.th_par_del == 0 && W.size_range == 2.0 && W.min_exe_lines == 0.5 &&
          W.min_copied_lines == 0.5 && W.required_bonus == 0.0 && W.default_bonus == 1.0 && W.rand_total <= 256 &&
-         !W.copy_ext;
+         !W.copy_ext && !W.track_age;
 }
 
 template <bool REC>

@@ -124,7 +124,7 @@ __global__ void k_set_orgs(DevWorld W, int64_t first, int64_t count, const uint8
   }
   W.max_exec[c] = mx;
   W.birth_len[c] = len;
-  W.age[c] = -1;                            // injected between updates: age 0 during the next one
+  if (W.track_age) W.age[c] = -1;          // injected between updates: age 0 during the next one
   W.gkey[c] = gk_tape(t, len);
   // stream key (DESIGN.md RNG spec)
   uint32_t lo, hi, ctr = 0;
@@ -209,7 +209,7 @@ __device__ void build_state(const DevWorld& W, int64_t c, avgpu_cpu_state& s) {
   s.fitness = W.fitness[c];
   s.credit = W.credit[c];
   s.head_start = CTL_HS(ctl);
-  s.age = W.age[c] + 1;                     // as UpdateOrganismStats leaves it at the update's end
+  s.age = W.track_age ? W.age[c] + 1 : 0;   // as UpdateOrganismStats leaves it at the update's end
 }
 
 __global__ void k_get_states(DevWorld W, int64_t first, int64_t count, avgpu_cpu_state* out,
@@ -264,7 +264,7 @@ __global__ void k_set_states(DevWorld W, int64_t first, int64_t count, const avg
   const int64_t N = W.n;
   const int64_t c = first + i;
   const avgpu_cpu_state s = in[i];
-  W.age[c] = s.age - 1;
+  if (W.track_age) W.age[c] = s.age - 1;
   int32_t* x = W.xs + c * XS_WORDS;
   for (int k = 0; k < XS_WORDS; k++) x[k] = 0;
   for (int k = 0; k < 3; k++) x[XS_REG + k] = s.reg[k];
@@ -727,7 +727,7 @@ __global__ __launch_bounds__(1024) void k_allot(DevWorld W, const double* totals
         W.credit[c] = __dsub_rn(cr, fl);
       }
       if (ctl[j] & CTL_HS_MASK) W.ctl[c] = ctl[j] & ~CTL_HS_MASK;   // the head start is used up
-      if (tick) W.age[c] += 1;     // cPhenotype::IncAge at the previous update's end (oracle age_tick)
+      if (tick && W.track_age) W.age[c] += 1;   // cPhenotype::IncAge at the previous update's end (oracle age_tick)
       want[j] = bud > 0;
       if (want[j]) cls[j] = class_of(need_of_cell(W, (int)c));
     }
@@ -1793,7 +1793,7 @@ void launch_serial_post(const DevWorld& W, hipStream_t s, double* stats) {
 // the serial world's cPhenotype::IncAge tick (k_allot's, for the batch update)
 __global__ void k_age_tick(DevWorld W) {
   const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (c < W.n && (W.ctl[c] & CTL_ALIVE)) W.age[c] += 1;
+  if (c < W.n && W.track_age && (W.ctl[c] & CTL_ALIVE)) W.age[c] += 1;
 }
 void launch_age_tick(const DevWorld& W, hipStream_t s) {
   hipLaunchKernelGGL(k_age_tick, dim3(nblk(W.n, 256)), dim3(256), 0, s, W);

@@ -312,6 +312,7 @@ struct World {
 thread_local std::string g_err;
 static int g_trace = getenv("ORACLE_TRACE") ? 1 : 0;
 static int64_t g_op_hist[64];   // executed instructions per handler (instruction-mix statistics)
+static inline bool tracks_age(const World& w) { return w.cfg.birth_method == 1 || w.cfg.birth_method == 2; }
 int fail(int code, const std::string& msg) { g_err = msg; return code; }
 
 // cHeadCPU::Adjust / fullAdjust (cpu/cHeadCPU.h:63, cpu/cHeadCPU.cc:27-50)
@@ -1154,7 +1155,10 @@ void dump_state(const World& w, const Org& o, avgpu_cpu_state* s, uint8_t* ops, 
   s->fitness = o.fitness;
   s->credit = o.credit;
   s->head_start = o.hstart;
-  s->age = o.age + 1;   // as the reference's UpdateOrganismStats leaves it (age_tick)
+  // as the reference's UpdateOrganismStats leaves it (age_tick); kept only
+  // for BIRTH_METHOD 1 / 2, its one consumer on this path (the device's
+  // track_age), 0 otherwise
+  s->age = tracks_age(w) ? o.age + 1 : 0;
   (void)w;
   if (ops && flags) {
     for (int i = 0; i < cap; i++) {
@@ -1771,7 +1775,7 @@ int orc_set_states(void* h, int64_t first, int64_t count, const avgpu_cpu_state*
     o.errors = s.errors;
     o.cur_bonus = s.cur_bonus; o.merit = s.merit; o.fitness = s.fitness; o.credit = s.credit;
     o.hstart = s.head_start;
-    o.age = s.age - 1;
+    if (tracks_age(w)) o.age = s.age - 1;
   }
   return 0;
 }
@@ -2246,6 +2250,7 @@ static void place_finish_single(World& w, int64_t& placed_out, int64_t& dropped_
 // the next, so that Org::age is the reference's age DURING the update --
 // injected organisms start at -1, newborns and dividers are set to 0.
 static void age_tick(World& w) {
+  if (!tracks_age(w)) return;
   for (int64_t c = 0; c < w.ncells; c++) if (w.orgs[c].alive) w.orgs[c].age++;
 }
 

@@ -110,8 +110,6 @@ struct DevWorld {
   uint32_t* ctl;      // [n]  sp0 | sp1<<4 | cur_stack | mal_active | alive
   int32_t* mem_size;  // [n]
   int32_t* max_exec;  // [n]
-  int32_t* age;       // [n] cPhenotype::age during the update (k_allot ticks it; -1 injected, 0 born / divided),
-                      // kept only when track_age (BIRTH_METHOD 1 / 2, its one consumer on this path)
   int32_t* birth_len; // [n]  genome length at birth (cPhenotype::genome_length)
   uint64_t* gkey;     // [n]  genome key of the birth genome (systematics census)
   uint32_t* rng;      // [3][n] key_lo, key_hi, ctr
@@ -248,7 +246,6 @@ struct DevWorld {
   int32_t cfg_min_genome, cfg_max_genome;  // raw MIN_GENOME_SIZE / MAX_GENOME_SIZE
   int32_t death_method, age_limit;
   int32_t prefer_empty, allow_parent, birth_method;
-  int32_t track_age;  // BIRTH_METHOD 1 / 2: the age row is maintained
   // P(p) = u < p: counter threshold ceil(p 2^32), and p itself
   // for RECORDED draws
   uint64_t th_copy_mut, th_div_mut, th_div_ins, th_div_del, th_div_slip, th_div_uni;
@@ -313,6 +310,10 @@ struct DevWorld {
   uint8_t* r_send[2];
   uint8_t* r_recv[2];
   int64_t r_arena;
+  // (appended, so that the hot fields keep their offsets in the scalar loads)
+  int32_t* age;       // [n] cPhenotype::age during the update (k_allot ticks it; -1 injected, 0 born / divided),
+                      // kept only when track_age (BIRTH_METHOD 1 / 2, its one consumer on this path)
+  int32_t track_age;  // BIRTH_METHOD 1 / 2: the age row is maintained
 };
 
 // owner of a cell won by a neighbouring strip's offspring in round k at birth time t
@@ -723,6 +724,7 @@ void launch_interpret_classes(const DevWorld& W, const DevWorld* dW, int mode, h
 // last of them), then one bucket for the window's cells that are not class 0
 #define SORT_BUCKETS 258
 bool class_timing_all();   // AVGPU_CLASS_TIMING (interp.hip)
+bool mix_lists();          // list classes inside class 0's launch (interp.hip; AVGPU_NO_MIX=1 off)
 void launch_age_tick(const DevWorld& W, hipStream_t s);
 // sub-update `sub` of `nsub` (avgpu_cfg.sub_updates): the
 // resources step and the update's counters are reset at sub 0 only; the key

@@ -127,11 +127,16 @@ __device__ __forceinline__ int edit_word(int kind, int a, int b) { return kind |
 // (def_knobs, capi.hip), so their other branches drop out; RES: with SIMPLE,
 // the simple reactions consume finite resources (configs[4]) -- without it
 // the resource walk drops out of the simple path
-template <int S, bool REC, bool C0W = false, bool SIMPLE = false, bool DEF = false, bool RES = false>
+// MIX: a list-class chunk run in class 0's 320-site block (k_interpret's
+// mixed launch): each organism takes kslot consecutive 320-B slots (class 1:
+// 3, class 2: 5, class 3: 7), 64 / kslot organisms per block; the slot size,
+// the staging granules per organism and the spill capacity are runtime
+template <int S, bool REC, bool C0W = false, bool SIMPLE = false, bool DEF = false, bool RES = false,
+          bool MIX = false>
 __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, int cls_arg, int mode_arg,
                                                int64_t first, int64_t count, int64_t chunk,
                                                uint32_t* __restrict__ lds32, bool sorted, int row,
-                                               int lpw, int serial = 0) {
+                                               int lpw, int serial = 0, int kslot = 1) {
   const DevWorld& W = *Wp;
   const int cls = C0W ? 0 : cls_arg;
   const int mode = C0W ? (int)AVGPU_MODE_WORLD : mode_arg;
@@ -141,12 +146,16 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
   // 16-byte pad; class 0 has none -- a window past lane L's slot reads lane
   // L+1's tape (lane 63's: past the block's LDS, which reads as 0) -- so that
   // its block (tapes only, 20 KiB) fits 8 times in a CU.
-  constexpr int STRIDE = tape_stride(S);
+  constexpr int STRIDE0 = tape_stride(S);
   // staging granule: 16-B quads (dwords for a stride that is not a whole
   // number of quads; device.h CLASS0_SIZE on why class 0 is not)
-  constexpr int GRAN = (STRIDE % 16 == 0) ? 16 : 4;
-  constexpr int QUADS = STRIDE / GRAN;
-  constexpr int TAPE_WORDS = 64 * STRIDE / 4;
+  constexpr int GRAN = (STRIDE0 % 16 == 0) ? 16 : 4;
+  constexpr int QUADS0 = STRIDE0 / GRAN;
+  constexpr int TAPE_WORDS = 64 * STRIDE0 / 4;
+  // per-organism slot, granules and capacity (MIX: kslot slots of S sites)
+  const int STRIDE = MIX ? STRIDE0 * kslot : STRIDE0;
+  const int QUADS = MIX ? QUADS0 * kslot : QUADS0;
+  const int Scap = MIX ? min(S * kslot, AVGPU_MAX_GENOME) : S;
   // class 0 keeps the two stacks in VGPRs (sv[]): without their 5 KiB of LDS a
   // block needs 26 KiB and 6 blocks fit a CU instead of 5
   constexpr bool VSTK = (S == CLASS0_SIZE);
@@ -259,11 +268,11 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
   // together and retired by one wait ----
   typedef __attribute__((address_space(3))) void* lds_ptr_t;
   // a serial step runs lane 0 only: its quads are the image's first QUADS
-  const int qits = serial ? (QUADS + 63) / 64 : QUADS;
+  const int qits = serial ? (QUADS0 + 63) / 64 : QUADS0;   // MIX: the same 64 x QUADS0 granule image
   // class 0: unrolled so that the shuffles of several quads are in flight
   // together (one LDS round trip per quad otherwise); the list classes' 49 /
   // 97 / 129-quad loops stay rolled (code size)
-  constexpr int QUNR = (S == CLASS0_SIZE) ? (QUADS % 7 == 0 ? 7 : 5) : 1;
+  constexpr int QUNR = (S == CLASS0_SIZE) ? (QUADS0 % 7 == 0 ? 7 : 5) : 1;
 #pragma unroll QUNR
   for (int it = 0; it < qits; it++) {
     const int i = it * 64 + lane;
@@ -291,7 +300,9 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
     }
   }
 
-  uint8_t* T = lds + lane * STRIDE;
+  // (MIX: lanes past the block's 64 / kslot organisms never touch their tape;
+  // they point at lane 0's)
+  uint8_t* T = lds + ((MIX && lane * kslot >= 64) ? 0 : lane) * STRIDE;
 
   // ---- hot state into registers ----
   int r0 = 0, r1 = 0, r2 = 0, ip = 0, rh = 0, wh = 0, fh = 0;
@@ -500,7 +511,7 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
         const bool ok = !(k_require_allocate && (ctl & CTL_MAL)) && alloc >= 1 &&
                         nsz <= AVGPU_MAX_GENOME && nsz >= AVGPU_MIN_GENOME &&
                         alloc <= (int)(cur * k_size_range) && cur <= (int)(alloc * k_size_range);
-        if (ok && nsz > S) { fl |= F_SPILL; ip = ipa; }
+        if (ok && nsz > Scap) { fl |= F_SPILL; ip = ipa; }
       }
       // serial step: the speculative run ends before IO / h-divide
       // (cHardwareCPU::SingleProcess stall instructions, cpu/cHardwareCPU.cc:961-968)
@@ -620,7 +631,7 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
               s_to = (int)draw_below((uint32_t)(wh == 0 ? Mp : Mp + 1));
               if (Mp + wh - s_to <= AVGPU_MAX_GENOME) mx_sz = max(mx_sz, Mp + wh - s_to);
             }
-            if (mx_sz > S && S < AVGPU_MAX_GENOME) {
+            if (mx_sz > Scap && Scap < AVGPU_MAX_GENOME) {
               T[wh] = (uint8_t)dst_byte;                       // undo the write, then the step
               T[ipa] = (uint8_t)cur_byte;
               kct = kct_h; rl = rl_h;
@@ -1603,14 +1614,14 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
               // and the parent grows below them: M + 5 * nins <= S.  A parent
               // near its slot's end keeps the insertions that fit (the rest
               // counted in CNT_MEM_CAP; the oracle has no slot, tests require 0)
-              const int nfit = (S - M) / 5;
+              const int nfit = (Scap - M) / 5;
               if (nins > nfit) {
                 count_add(W, CNT_MEM_CAP, (unsigned long long)(nins - nfit));
                 nins = nfit;
               }
               if (nins > 0) {
                 // (the child's copy-out has read those bytes)
-                int32_t* srt = reinterpret_cast<int32_t*>(T + S - 4 * nins);
+                int32_t* srt = reinterpret_cast<int32_t*>(T + Scap - 4 * nins);
                 for (int i = 0; i < nins; i++) {
                   const int site = (int)draw_below((uint32_t)M + 1u);
                   int j = i;
@@ -1826,19 +1837,45 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
 
 // class 0 must keep 2 waves per SIMD (its LDS admits 7 blocks per CU): the
 // second bound caps it at 256 registers (VGPR + AGPR)
+// The mixed class-0 launch (nmix > 0, world updates): its first nmix blocks
+// run the list classes 1 / 2 / 3 in class-0 blocks (MIX_B1 / MIX_B2 / MIX_B3
+// blocks, each a grid-stride over its list in chunks of 64 / kslot
+// organisms), the rest are class 0 -- one launch, so the list classes need no
+// aux stream, no fork / join events and no head start on class 0.
+#define MIX_B1 512
+#define MIX_B2 16
+#define MIX_B3 8
+#define MIX_BLOCKS (MIX_B1 + MIX_B2 + MIX_B3)
+static_assert(MIX_BLOCKS % 8 == 0, "class 0's XCD mapping needs whole rounds of 8 blocks");
 template <int S, bool REC, bool C0W = false, bool SIMPLE = false, bool DEF = false, bool RES = false>
 __global__ __launch_bounds__(64, (S == CLASS0_SIZE) ? 2 : 1) void k_interpret(const DevWorld* __restrict__ Wp, int cls, int row, int mode,
-                                                  int64_t first, int64_t count, int sorted, int lpw) {
+                                                  int64_t first, int64_t count, int sorted, int lpw, int nmix = 0) {
   constexpr int TAB_WORDS = 128 + 64 + 16 + 64 + AVGPU_MAX_REACTIONS * RT_STRIDE + 64;
   // class 0: stacks in VGPRs, tables in global memory -- only the tapes in LDS
   constexpr int STK = (S == CLASS0_SIZE) ? 0 : 2 * AVGPU_STACK_SIZE * 64;
   constexpr int TAB = (S == CLASS0_SIZE) ? 0 : TAB_WORDS;     // class 0: tapes only
   __shared__ __attribute__((aligned(16))) uint32_t lds32[64 * tape_stride(S) / 4 + STK + TAB];
   if (cls == 0) {
+    if (S == CLASS0_SIZE && C0W && (int)blockIdx.x < nmix) {
+      const int b = blockIdx.x;
+      const int lc = b < MIX_B1 ? 1 : (b < MIX_B1 + MIX_B2 ? 2 : 3);
+      const int b0 = lc == 1 ? 0 : (lc == 2 ? MIX_B1 : MIX_B1 + MIX_B2);
+      const int nb = lc == 1 ? MIX_B1 : (lc == 2 ? MIX_B2 : MIX_B3);
+      const int kslot = lc == 1 ? 3 : (lc == 2 ? 5 : 7);      // 960 / 1600 / 2240 B >= 768 / 1536 / 2048 sites
+      const int per = 64 / kslot;
+      const int lcount = Wp->class_count[lc];
+      for (int64_t chunk = b - b0; chunk * per < lcount; chunk += nb) {
+        interpret_chunk<S, REC, false, SIMPLE, DEF, RES, true>(Wp, lc, mode, first, count, chunk, lds32, false, lc,
+                                                                per, 0, kslot);
+        __syncthreads();
+      }
+      return;
+    }
     // sorted windows: the 32 chunks of a window run on one XCD (blocks are
     // dealt to the 8 XCDs round robin), so its state lines meet in one L2
-    int64_t chunk = blockIdx.x;
-    if (sorted && (gridDim.x & 7) == 0) chunk = (int64_t)(blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
+    const int64_t bx = (int64_t)blockIdx.x - nmix, gx = (int64_t)gridDim.x - nmix;
+    int64_t chunk = bx;
+    if (sorted && (gx & 7) == 0) chunk = (bx & 7) * (gx >> 3) + (bx >> 3);
     interpret_chunk<S, REC, C0W, SIMPLE, DEF, RES>(Wp, 0, mode, first, count, chunk, lds32, sorted, 0, 64);
     return;
   }
@@ -2121,6 +2158,16 @@ bool class_timing_all() {
 
 // the knobs the DEF instantiation fixes, at the reference's defaults
 // (avgpu_cfg_defaults; main/cAvidaConfig.h)
+// AVGPU_NO_MIX=1: the list classes on their own aux-stream launches (A/B)
+bool mix_lists() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("AVGPU_NO_MIX");
+    v = (e && atoi(e) == 1) ? 0 : 1;
+  }
+  return v == 1;
+}
+
 static bool def_knobs(const DevWorld& W) {
   return W.alloc_method != 2 && W.require_allocate == 1 && W.max_label_exe == 1 && W.cfg_min_genome == 0 &&
          W.cfg_max_genome == 0 && W.merit_default_bonus == 0.0 && W.inherit_merit == 1 &&
@@ -2195,7 +2242,12 @@ static void launch_classes(const DevWorld& W, const DevWorld* dW, int mode, hipS
   // lists start after k_allot, beside k_window_count, so that they take their
   // CUs before class 0 and end well inside it (forked after the sort they only
   // got CUs as class-0 waves retired and ended ~40-55 us after class 0).
-  if (aux) {
+  // the list classes inside class 0's launch (MIX_BLOCKS leading blocks):
+  // sorted world updates, unless AVGPU_NO_MIX=1 (A/B)
+  const bool mix = aux && mix_lists();
+  const int nmix = mix ? MIX_BLOCKS : 0;
+  const unsigned cblocks = blocks + (unsigned)nmix;
+  if (aux && !mix) {
     // ev_fork: recorded by launch_world_pre right after k_allot built the lists
     for (int k = 0; k < 2; k++) hipStreamWaitEvent(aux[k], ev_fork, 0);
     list(1, aux[0]);
@@ -2209,13 +2261,13 @@ static void launch_classes(const DevWorld& W, const DevWorld* dW, int mode, hipS
     hipEventRecord(ev_join[0], aux[0]);
   }
   if (fast && res)
-    hipLaunchKernelGGL((k_interpret<CLASS0_SIZE, REC, true, true, true, true>), dim3(blocks), dim3(64), 0, s, dW, 0, 0, mode, first, count, srt, 64);
+    hipLaunchKernelGGL((k_interpret<CLASS0_SIZE, REC, true, true, true, true>), dim3(cblocks), dim3(64), 0, s, dW, 0, 0, mode, first, count, srt, 64, nmix);
   else if (fast)
-    hipLaunchKernelGGL((k_interpret<CLASS0_SIZE, REC, true, true, true>), dim3(blocks), dim3(64), 0, s, dW, 0, 0, mode, first, count, srt, 64);
+    hipLaunchKernelGGL((k_interpret<CLASS0_SIZE, REC, true, true, true>), dim3(cblocks), dim3(64), 0, s, dW, 0, 0, mode, first, count, srt, 64, nmix);
   else if (mode == AVGPU_MODE_WORLD && W.env_simple && W.env_res_mask == 0u)
-    hipLaunchKernelGGL((k_interpret<CLASS0_SIZE, REC, true, true>), dim3(blocks), dim3(64), 0, s, dW, 0, 0, mode, first, count, srt, 64);
+    hipLaunchKernelGGL((k_interpret<CLASS0_SIZE, REC, true, true>), dim3(cblocks), dim3(64), 0, s, dW, 0, 0, mode, first, count, srt, 64, nmix);
   else if (mode == AVGPU_MODE_WORLD)
-    hipLaunchKernelGGL((k_interpret<CLASS0_SIZE, REC, true>), dim3(blocks), dim3(64), 0, s, dW, 0, 0, mode, first, count, srt, 64);
+    hipLaunchKernelGGL((k_interpret<CLASS0_SIZE, REC, true>), dim3(cblocks), dim3(64), 0, s, dW, 0, 0, mode, first, count, srt, 64, nmix);
   else
     hipLaunchKernelGGL((k_interpret<CLASS0_SIZE, REC>), dim3(blocks), dim3(64), 0, s, dW, 0, 0, mode, first, count, srt, 64);
   if (after_class) hipEventRecord(after_class[0], s);
@@ -2227,7 +2279,9 @@ static void launch_classes(const DevWorld& W, const DevWorld* dW, int mode, hipS
   // lists ended inside class 0) are queued while it runs instead of in front
   // of it (~17 us per update of event waits on the critical path).
   const int slpw = spill_lpw();
-  if (aux) {
+  if (mix) {
+    row(CLASS1_SIZE, dim3(lb_small), s, 1, 4, slpw);   // no join: the lists ran in class 0's launch
+  } else if (aux) {
     row(CLASS1_SIZE, dim3(lb_small), s, 1, 4, slpw);
     hipStreamWaitEvent(s, ev_join[0], 0);
   } else {

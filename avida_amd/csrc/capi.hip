@@ -111,7 +111,7 @@ int setup_world(avgpu_world* w, int64_t n, bool test_buffers) {
   A(merit, n); A(fitness, n); A(credit, n); A(gest_time, n); A(num_div, n);
   A(generation, n); A(copied, n); A(child_copied, n); A(executed, n);
   HIPCHK(hipMemsetAsync(W.aclass, ACLASS_NONE, n, w->stream));   // no slice allotted yet
-  A(class_list, NUM_LISTS * n); A(order, n); A(class_count, 8); A(counters, CNT_WORDS);
+  A(class_list, NUM_LISTS * n); A(order, n); A(sub_hist, (size_t)((n + 4095) / 4096) * SORT_BUCKETS); A(class_count, 8); A(counters, CNT_WORDS);
   // birth records: one primary record per cell + overflow for further
   // offspring of one slice (device.h); test worlds never enqueue births
   W.rcap = n + (test_buffers ? 16 : std::max<int64_t>(4096, n / 4));

@@ -314,6 +314,9 @@ struct DevWorld {
   int32_t* age;       // [n] cPhenotype::age during the update (k_allot ticks it; -1 injected, 0 born / divided),
                       // kept only when track_age (BIRTH_METHOD 1 / 2, its one consumer on this path)
   int32_t track_age;  // BIRTH_METHOD 1 / 2: the age row is maintained
+  // the class-0 order's bucket histogram of each 4096-cell sub-window
+  // (k_allot's workgroups write it, k_window_order scans it): [nsub][SORT_BUCKETS]
+  int32_t* sub_hist;
 };
 
 // owner of a cell won by a neighbouring strip's offspring in round k at birth time t

@@ -206,7 +206,7 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
     }
   } else if (cls == 0) {
     // dense sweep: in cell order, or (world updates) through the
-    // budget-sorted windows of k_window_count
+    // budget-sorted windows of k_window_order
     const int64_t c = sorted ? (chunk * 64 + lane < count ? (int64_t)W.order[chunk * 64 + lane] : first + count)
                              : first + chunk * 64 + lane;
     // the cell's slice is class 0 by k_allot's tag (device.h aclass), not by
@@ -2239,7 +2239,7 @@ static void launch_classes(const DevWorld& W, const DevWorld* dW, int mode, hipS
   // world's stream that is three HIP streams, so they keep distinct hardware
   // queues (GPU_MAX_HW_QUEUES = 4); a third aux stream shared a queue with
   // the world's stream and serialised class 3 in front of class 0.  The aux
-  // lists start after k_allot, beside k_window_count, so that they take their
+  // lists start after k_allot, beside the window sort, so that they take their
   // CUs before class 0 and end well inside it (forked after the sort they only
   // got CUs as class-0 waves retired and ended ~40-55 us after class 0).
   // the list classes inside class 0's launch (MIX_BLOCKS leading blocks):

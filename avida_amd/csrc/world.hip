@@ -649,6 +649,12 @@ __device__ __forceinline__ void occ_init_cell(const DevWorld& W, int64_t c) {
 // update (living cells occupied; an organism that dies in its slice clears
 // its cell at write-back), its kill time, the previous update's round-3
 // claim, and the class lists.
+// a cell's bucket of the class-0 order: class-0 slices by budget, descending
+// (clamped both ways: a bucket outside the histogram would place the cell
+// outside its window of W.order), every other cell in the last bucket
+__device__ __forceinline__ int window_bucket(bool c0, int budget) {
+  return c0 ? SORT_BUCKETS - 2 - min(max(budget, 0), SORT_BUCKETS - 2) : SORT_BUCKETS - 1;
+}
 __global__ __launch_bounds__(1024) void k_allot(DevWorld W, const double* totals, uint32_t update, int tick) {
   const int lane = threadIdx.x & 63;
   const int64_t b = (int64_t)blockIdx.x * 16 + (threadIdx.x >> 6);
@@ -745,20 +751,30 @@ __global__ __launch_bounds__(1024) void k_allot(DevWorld W, const double* totals
 #pragma unroll
   for (int j = 0; j < 4; j++) cells[j] = (int)(b * 256 + lane + 64 * j);
   enqueue_class_multi<16, 4>(W, cells, want, cls);
+  // this 4096-cell sub-window's histogram of the class-0 order's buckets
+  // (k_window_order; the bucket rule of window_bucket)
+  __shared__ int sh[SORT_BUCKETS];
+  for (int i = threadIdx.x; i < SORT_BUCKETS; i += 1024) sh[i] = 0;
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    const int64_t c = b * 256 + lane + 64 * j;
+    if (b < nb && c < W.n) atomicAdd(&sh[window_bucket(want[j] && cls[j] == 0, W.budget[c])], 1);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < SORT_BUCKETS; i += 1024) W.sub_hist[(int64_t)blockIdx.x * SORT_BUCKETS + i] = sh[i];
 }
 
-// the window's order from its bucket histogram (block of 1024 threads,
-// WIN_CPT cells each): exclusive scan by one wave, then each cell's slot
-#define WIN_CPT (SORT_WIN / 1024)
-__device__ __forceinline__ void window_order(const DevWorld& W, int64_t base, int* hist, const int* bucket) {
+// exclusive scan of the SORT_BUCKETS counts in h, in place, by one wave
+__device__ __forceinline__ void bucket_scan(int* h) {
   const int tid = threadIdx.x;
-  if (tid < 64) {                              // exclusive scan of the buckets by one wave
+  if (tid < 64) {
     constexpr int PER = (SORT_BUCKETS + 63) / 64;
     int loc[PER], t = 0;
 #pragma unroll
     for (int k = 0; k < PER; k++) {
       const int i = tid * PER + k;
-      loc[k] = i < SORT_BUCKETS ? hist[i] : 0;
+      loc[k] = i < SORT_BUCKETS ? h[i] : 0;
       t += loc[k];
     }
     int incl = t;
@@ -770,61 +786,64 @@ __device__ __forceinline__ void window_order(const DevWorld& W, int64_t base, in
 #pragma unroll
     for (int k = 0; k < PER; k++) {
       const int i = tid * PER + k;
-      if (i < SORT_BUCKETS) hist[i] = run;
+      if (i < SORT_BUCKETS) h[i] = run;
       run += loc[k];
     }
   }
-  __syncthreads();
-#pragma unroll
-  for (int h = 0; h < WIN_CPT; h++) {
-    if (bucket[h] < 0) continue;
-    const int pos = atomicAdd(&hist[bucket[h]], 1);
-    W.order[base + pos] = (int32_t)(base + h * 1024 + tid);
-  }
 }
 
-// The window's class-0 cells ordered by budget (descending) with a counting
-// sort (one SORT_WIN window per block): which cell runs in which wave changes
-// no organism's result (per-organism streams, placement by birth time and
-// key), it only groups similar slices, so the order inside a budget is free
-// (LDS atomics).  A wave loses about (window's budget range) / (2 x its
-// waves) per lane to the spread of its budgets: 8192-cell windows (128
-// waves) instead of 2048 took the lane efficiency of the bench's
-// multinomial budgets from 0.94 to 0.98 (tools/budget_spread.py); 16384
-// (256 waves) measured 1.299 ms/step against 1.326-1.389 for 8192 on the
-// same box (profiles/r04e_ab.txt), 32768 1.276-1.280 against 1.307 for 16384
-// (class 0 0.945 vs 0.990 ms; 65536: 0.924 ms, but this kernel's 16
-// workgroups cost more than that gains: profiles/r04w_ab.txt).
-__global__ __launch_bounds__(1024) void k_window_count(DevWorld W) {
-  __shared__ int hist[SORT_BUCKETS];
+// The class-0 order: each SORT_WIN window's class-0 cells by budget
+// (descending), a counting sort.  Which cell runs in which wave changes no
+// organism's result (per-organism streams, placement by birth time and key),
+// it only groups similar slices, so the order inside a budget is free (LDS
+// atomics).  A wave loses about (window's budget range) / (2 x its waves) per
+// lane to the spread of its budgets: 8192-cell windows (128 waves) took the
+// lane efficiency of the multinomial budgets from 0.94 to 0.98
+// (tools/budget_spread.py), 32768 cells measured fastest (HISTORY.md,
+// profiles/r04w_ab.txt).
+// One 1024-thread block per 4096-cell sub-window (the blocks of k_allot,
+// which left each sub-window's bucket histogram in sub_hist): the window's
+// bucket starts plus the counts of its earlier sub-windows, then this
+// sub-window's cells by LDS atomics.  (One block per 32768-cell window, all
+// of its 32768 LDS atomics on ~25 busy buckets, took 33 us: the list classes
+// used that as their head start before they ran inside class 0's launch.)
+__global__ __launch_bounds__(1024) void k_window_order(DevWorld W) {
+  constexpr int SUBS = SORT_WIN / 4096;
+  __shared__ int start[SORT_BUCKETS];
   const int tid = threadIdx.x;
-  const int64_t base = (int64_t)blockIdx.x * SORT_WIN;
-  for (int i = tid; i < SORT_BUCKETS; i += 1024) hist[i] = 0;
-  __syncthreads();
-  int bucket[WIN_CPT];
-#pragma unroll
-  for (int h = 0; h < WIN_CPT; h++) {
-    const int64_t c = base + h * 1024 + tid;
-    bucket[h] = -1;
-    if (c < W.n) {
-      // class-0 cells by k_allot's tag: the list classes on the aux streams
-      // rewrite budget / mem_size of their own cells while this kernel runs
-      const bool c0 = W.aclass[c] == 0;
-      // (clamped both ways: a bucket outside the histogram would place the
-      // cell outside its window of W.order)
-      bucket[h] = c0 ? SORT_BUCKETS - 2 - min(max(W.budget[c], 0), SORT_BUCKETS - 2) : SORT_BUCKETS - 1;
-      atomicAdd(&hist[bucket[h]], 1);
+  const int64_t sub = blockIdx.x;
+  const int64_t s0 = (sub / SUBS) * SUBS, nsub = (W.n + 4095) / 4096;
+  int before = 0;
+  if (tid < SORT_BUCKETS) {
+    int tot = 0;
+    for (int64_t k = s0; k < s0 + SUBS && k < nsub; k++) {
+      const int v = W.sub_hist[k * SORT_BUCKETS + tid];
+      tot += v;
+      if (k < sub) before += v;
     }
+    start[tid] = tot;
   }
   __syncthreads();
-  window_order(W, base, hist, bucket);
+  bucket_scan(start);
+  __syncthreads();
+  if (tid < SORT_BUCKETS) start[tid] += before;
+  __syncthreads();
+  const int64_t wbase = (sub / SUBS) * SORT_WIN;
+#pragma unroll
+  for (int h = 0; h < 4; h++) {
+    const int64_t c = sub * 4096 + h * 1024 + tid;
+    if (c < W.n) {
+      const int pos = atomicAdd(&start[window_bucket(W.aclass[c] == 0, W.budget[c])], 1);
+      W.order[wbase + pos] = (int32_t)c;
+    }
+  }
 }
 
 
 // ---- budget-sorted class-0 windows ----
 // A wave runs until its longest slice ends, so the class-0 interpreter takes
 // its 64 organisms from a window of SORT_WIN cells sorted by budget
-// (k_window_count above).
+// (k_window_order above).
 
 // ---- strip-tile halo (DESIGN.md "Multi-GPU") ----
 // Edge rows: top = local row 0, bottom = local row rows-1; ghost rows after n.
@@ -1720,7 +1739,7 @@ static void launch_allot(const DevWorld& W, hipStream_t s, const double* totals,
   // lists inside class 0's launch (mix_lists) there is no fork: an event
   // record here left ~14 us of dead time on the world's stream
   if (!mix_lists()) hipEventRecord(lists_ready, s);
-  hipLaunchKernelGGL(k_window_count, dim3(nblk(W.n, SORT_WIN)), dim3(1024), 0, s, W);
+  hipLaunchKernelGGL(k_window_order, dim3(nblk(W.n, 4096)), dim3(1024), 0, s, W);
 }
 
 // single world: block partials (k_merit_partial also zeroes the update's

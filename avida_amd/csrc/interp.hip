@@ -136,7 +136,7 @@ template <int S, bool REC, bool C0W = false, bool SIMPLE = false, bool DEF = fal
 __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, int cls_arg, int mode_arg,
                                                int64_t first, int64_t count, int64_t chunk,
                                                uint32_t* __restrict__ lds32, bool sorted, int row,
-                                               int lpw, int serial = 0, int kslot = 1) {
+                                               int lpw, int serial = 0, int kslot = 1, int direct = -2) {
   const DevWorld& W = *Wp;
   const int cls = C0W ? 0 : cls_arg;
   const int mode = C0W ? (int)AVGPU_MODE_WORLD : mode_arg;
@@ -214,6 +214,13 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
     if (c < first + count && W.aclass[c] == 0) {
       cell = (int)c;
       M = W.mem_size[c];
+    }
+  } else if (MIX && direct != -2) {
+    // the organisms a class-0 wave spilled, continued by the same wave
+    // (k_interpret): the lane's cell, -1 for none
+    if (direct >= 0) {
+      cell = direct;
+      M = W.mem_size[direct];
     }
   } else {
     // list rows: lpw entries per wave (lanes >= lpw idle)
@@ -1745,8 +1752,12 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
       }
     }
     if (spill) {
-      const int slot = atomicAdd(&W.class_count[3 + cls + 1], 1);     // spill row of class cls+1
-      W.class_list[(int64_t)(3 + cls + 1) * N + slot] = cell;
+      // a class-0 world slice continues in the same wave (k_interpret), the
+      // others in the spill row of class cls+1
+      if (!(C0W && cls == 0)) {
+        const int slot = atomicAdd(&W.class_count[3 + cls + 1], 1);
+        W.class_list[(int64_t)(3 + cls + 1) * N + slot] = cell;
+      }
       count_add(W, CNT_SPILLS, 1ull);
     }
   }
@@ -1832,7 +1843,8 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
     }
   }
 #endif
-  return 0;
+  // a class-0 world slice that spilled: its cell + 1, for the wave to continue
+  return (C0W && cls == 0 && active && (fl & F_SPILL)) ? cell + 1 : 0;
 }
 
 // class 0 must keep 2 waves per SIMD (its LDS admits 7 blocks per CU): the
@@ -1876,7 +1888,36 @@ __global__ __launch_bounds__(64, (S == CLASS0_SIZE) ? 2 : 1) void k_interpret(co
     const int64_t bx = (int64_t)blockIdx.x - nmix, gx = (int64_t)gridDim.x - nmix;
     int64_t chunk = bx;
     if (sorted && (gx & 7) == 0) chunk = (bx & 7) * (gx >> 3) + (bx >> 3);
-    interpret_chunk<S, REC, C0W, SIMPLE, DEF, RES>(Wp, 0, mode, first, count, chunk, lds32, sorted, 0, 64);
+    const int sp = interpret_chunk<S, REC, C0W, SIMPLE, DEF, RES>(Wp, 0, mode, first, count, chunk, lds32, sorted,
+                                                                  0, 64) - 1;
+    if (S == CLASS0_SIZE && C0W) {
+      // Organisms whose h-alloc (or copy) outgrew their 320-site slot: this
+      // wave continues them at once in 3-slot (960-site) lanes of its own
+      // block's LDS -- their state was written back by this wave, so a
+      // workgroup-scope fence makes it visible to the re-staging -- instead of
+      // a spill row after class 0 (~55 organisms per update, 66 us after
+      // class 0, latency-bound on the longest).  A slice that outgrows 960
+      // sites goes on to the class-2 spill row.
+      uint64_t m = __ballot(sp >= 0);
+      if (m) {
+        const int nsp = __popcll(m);
+        int mine = -1;
+        for (int j = 0; m; j++, m &= m - 1) {
+          const int c = __shfl(sp, __ffsll((long long)m) - 1);
+          if ((int)threadIdx.x == j) mine = c;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+        __syncthreads();
+        constexpr int PER3 = 64 / 3;
+        for (int g = 0; g < nsp; g += PER3) {
+          const int d = __shfl(mine, (g + (int)threadIdx.x) & 63);
+          const int direct = ((int)threadIdx.x < PER3 && g + (int)threadIdx.x < nsp) ? d : -1;
+          interpret_chunk<S, REC, false, SIMPLE, DEF, RES, true>(Wp, 1, mode, first, count, 0, lds32, false, 4,
+                                                                  PER3, 0, 3, direct);
+          __syncthreads();
+        }
+      }
+    }
     return;
   }
   if (C0W) return;
@@ -2279,14 +2320,17 @@ static void launch_classes(const DevWorld& W, const DevWorld* dW, int mode, hipS
   // lists ended inside class 0) are queued while it runs instead of in front
   // of it (~17 us per update of event waits on the critical path).
   const int slpw = spill_lpw();
+  // row 4 (class 0's spills): a world launch's class-0 waves continue their
+  // own spills (k_interpret, C0W), other launches run the row
+  const bool c0w = mode == AVGPU_MODE_WORLD;
   if (mix) {
-    row(CLASS1_SIZE, dim3(lb_small), s, 1, 4, slpw);   // no join: the lists ran in class 0's launch
+    // no join: the lists ran in class 0's launch
   } else if (aux) {
-    row(CLASS1_SIZE, dim3(lb_small), s, 1, 4, slpw);
+    if (!c0w) row(CLASS1_SIZE, dim3(lb_small), s, 1, 4, slpw);
     hipStreamWaitEvent(s, ev_join[0], 0);
   } else {
     for (int k = 1; k <= 3; k++) list(k, s);
-    row(CLASS1_SIZE, dim3(lb_small), s, 1, 4, slpw);
+    if (!c0w) row(CLASS1_SIZE, dim3(lb_small), s, 1, 4, slpw);
   }
   if (after_class && tall) hipEventRecord(after_class[1], s);
   // spill rows 5 + 6 (beyond classes 1 / 2) in one launch of class 3's slots

@@ -102,6 +102,118 @@ __device__ __forceinline__ bool consume_resource(const DevWorld& W, const double
   return true;
 }
 
+// The branch-free ops -- register ALU, swap, conditionals, head moves -- of
+// one instruction (op with its register / head r); returns m_advance_ip.
+__device__ __forceinline__ bool fast_op(const int op, const int r, int& r0, int& r1, int& r2, int& ip, int& rh,
+                                        int& wh, int& fh, uint32_t& ctl, const int M) {
+  const int rn = (r == 2) ? 0 : r + 1;                    // FindNextRegister :1676
+  const int ra = (r == 0) ? r0 : ((r == 1) ? r1 : r2);
+  const int rb = (rn == 0) ? r0 : ((rn == 1) ? r1 : r2);
+  int res = ~(r1 & r2);                                                  // nand :3018
+  res = (op == AVGPU_H_ADD) ? (int)((uint32_t)r1 + (uint32_t)r2) : res;  // add :2959
+  res = (op == AVGPU_H_SUB) ? (int)((uint32_t)r1 - (uint32_t)r2) : res;  // sub :2968
+  res = (op == AVGPU_H_INC) ? (int)((uint32_t)ra + 1u) : res;            // inc :2864
+  res = (op == AVGPU_H_DEC) ? (int)((uint32_t)ra - 1u) : res;            // dec :2871
+  res = (op == AVGPU_H_SHIFT_R) ? (ra >> 1) : res;                       // shift-r :2806
+  res = (op == AVGPU_H_SHIFT_L) ? (int)((uint32_t)ra << 1) : res;        // shift-l :2813
+  res = (op == AVGPU_H_SWAP) ? rb : res;                                 // swap :2742
+  const bool wr = (WR_OPS & (1u << op)) != 0u;
+  const bool sw = op == AVGPU_H_SWAP;
+  // head ops: head id = nop-mod or IP (mov-head :6809, jmp-head :6859, get-head :6907)
+  const int hv = (r == 0) ? ip : ((r == 1) ? rh : wh);
+  const bool hw = op == AVGPU_H_MOV_HEAD || op == AVGPU_H_JMP_HEAD;
+  int hnew = fh;                                                         // mov-head: Set(FLOW), no adjust
+  if (op == AVGPU_H_JMP_HEAD) hnew = head_adjust((int)((uint32_t)hv + (uint32_t)r2), M);
+  r0 = (wr && r == 0) ? res : ((sw && rn == 0) ? ra : r0);
+  r1 = (wr && r == 1) ? res : ((sw && rn == 1) ? ra : r1);
+  r2 = (wr && r == 2) ? res : ((sw && rn == 2) ? ra : r2);
+  r2 = (op == AVGPU_H_GET_HEAD) ? hv : r2;
+  rh = (hw && r == 1) ? hnew : rh;
+  wh = (hw && r == 2) ? hnew : wh;
+  if (op == AVGPU_H_SET_FLOW) fh = head_adjust(ra, M);                   // set-flow :7270
+  if (hw && r == 0) ip = hnew;
+  // if-n-equ :2190 / if-less :2235 skip the next instruction
+  const bool skip = (op == AVGPU_H_IF_N_EQU && ra == rb) || (op == AVGPU_H_IF_LESS && ra >= rb);
+  if (skip) ip = head_wrap(ip + 1, M);
+  ctl ^= (op == AVGPU_H_SWAP_STK) ? CTL_CURSTK : 0u;                     // swap-stk :2739
+  return !(op == AVGPU_H_MOV_HEAD && r == 0);
+}
+
+// configs[4]'s deferred rewards (interpret_chunk's IO block): up to 3 queued
+// events of 9 task bits per lane, the count in bits 30..31.  Applies every
+// lane's events in order, each rank by rank -- every lane takes its lowest
+// remaining task, so an organism applies its tasks in ascending order with
+// consume_resource's arithmetic; a reaction's settings and its resource's
+// grid row come by scalar loads, one step per distinct task of the rank, and
+// the rank's cell levels go out together.  Runs with the whole wave.
+template <bool GTAB>
+__device__ __forceinline__ void res_flush(const DevWorld& W, const int64_t N, const int64_t cell, uint32_t& rpq,
+                                          double& bonus, int (&rc)[AVGPU_MAX_REACTIONS], const uint32_t ttab,
+                                          const double* tmul, const double* tadd, const uint32_t k_env_res_mask) {
+  while (__ballot(rpq != 0u) != 0ull) {
+    const uint32_t ev = rpq & 0x1FFu;
+    double mult = 1.0, addb = 0.0;
+    uint32_t paid = ev, rem = ev;
+    while (__ballot(rem != 0u) != 0ull) {
+      const bool has = rem != 0u;
+      const int t = has ? __ffs(rem) - 1 : 0;
+      const bool isres = has && ((k_env_res_mask >> t) & 1u);
+      // (the lane shuffles run with the whole wave active: a ds_bpermute
+      // reads 0 from an inactive source lane)
+      const double fm = GTAB ? __hiloint2double(__shfl((int)ttab, 2 * t + 1), __shfl((int)ttab, 2 * t)) : 1.0;
+      const double fa = GTAB ? __hiloint2double(__shfl((int)ttab, 33 + 2 * t), __shfl((int)ttab, 32 + 2 * t)) : 0.0;
+      if (has && !isres) {
+        mult = __dmul_rn(mult, GTAB ? fm : tmul[t]);
+        addb = __dadd_rn(addb, GTAB ? fa : tadd[t]);
+      }
+      double frac = 0.0, rmin = 0.0, rmax = 0.0, rval = 0.0;
+      double* lvp = nullptr;
+      int rty = 0, rslot = 0;
+      bool rdepl = false, rsp = false;
+      for (uint64_t need = __ballot(isres); need;) {
+        const int tu = __builtin_amdgcn_readlane(t, __ffsll((long long)need) - 1);
+        const double* rr = W.react_res + tu * RR_STRIDE;     // wave-uniform: scalar loads
+        const int slot = (int)rr[RR_RES] - 1;
+        const bool sp = rr[RR_SPATIAL] != 0.0;
+        const bool mine = isres && t == tu;
+        if (mine) {
+          frac = rr[RR_FRAC]; rmin = rr[RR_MIN]; rmax = rr[RR_MAX]; rval = rr[RR_VALUE];
+          rty = (int)rr[RR_TYPE]; rdepl = rr[RR_DEPL] != 0.0; rsp = sp; rslot = slot;
+          lvp = sp ? W.res_amount + (int64_t)W.res_param[slot].slot * N + cell : W.res_global + slot;
+        }
+        need &= ~__ballot(mine);
+      }
+      if (isres) {
+        const double level = *lvp;
+        double consumed = (level == 0.0) ? 0.0 : __dmul_rn(level, frac);
+        if (consumed > rmax) consumed = rmax;
+        if (consumed < rmin) consumed = 0.0;
+        if (consumed == 0.0) {
+          paid &= ~(1u << t);
+        } else {
+          consumed = fmin(consumed, level);
+          if (rdepl) {
+            if (rsp) *lvp = __dsub_rn(level, consumed);
+            else atomicAdd(W.res_cons + rslot, (unsigned long long)__dmul_rn(consumed, RES_FIX));
+          }
+          const double bon = __dmul_rn(consumed, rval);
+          if (rty == AVGPU_PROC_ADD) addb = __dadd_rn(addb, bon);
+          else if (rty == AVGPU_PROC_MULT) mult = __dmul_rn(mult, bon);
+          else mult = __dmul_rn(mult, det_exp2(bon));
+        }
+      }
+      rem &= rem - 1u;
+    }
+    if (ev) {
+#pragma unroll
+      for (int q = 0; q < AVGPU_NUM_LOGIC_TASKS; q++) rc[q] += (paid >> q) & 1u;
+      bonus = __dadd_rn(__dmul_rn(bonus, mult), addb);         // cPhenotype.cc:1645-1646
+    }
+    const uint32_t n = rpq >> 30;
+    rpq = n > 1u ? (((rpq & 0x07FFFFFFu) >> 9) | ((n - 1u) << 30)) : 0u;
+  }
+}
+
 __host__ __device__ constexpr int tape_stride(int S) { return S == CLASS0_SIZE ? S : S + 16; }
 
 // divide-mutation edits (Divide_DoMutations, applied in order): kind | a << 3 | b << 15
@@ -485,6 +597,7 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
   }
   const uint32_t* T32 = reinterpret_cast<const uint32_t*>(T);
   const int slow_batch = W.slow_batch;
+  uint32_t rpq = 0u;        // configs[4]'s queued reward events (res_flush)
 
   while (true) {
     const bool run = fl == 0 && budget > 0 && pop < 0;
@@ -544,40 +657,7 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
     it_copy += __ballot(op == AVGPU_H_H_COPY) != 0ull;
 #endif
     CK(0);
-    if (FAST_OPS & obit) {
-      // ---- branch-free ops: register ALU, swap, conditionals, head moves ----
-      const int rn = (r == 2) ? 0 : r + 1;                    // FindNextRegister :1676
-      const int ra = (r == 0) ? r0 : ((r == 1) ? r1 : r2);
-      const int rb = (rn == 0) ? r0 : ((rn == 1) ? r1 : r2);
-      int res = ~(r1 & r2);                                                  // nand :3018
-      res = (op == AVGPU_H_ADD) ? (int)((uint32_t)r1 + (uint32_t)r2) : res;  // add :2959
-      res = (op == AVGPU_H_SUB) ? (int)((uint32_t)r1 - (uint32_t)r2) : res;  // sub :2968
-      res = (op == AVGPU_H_INC) ? (int)((uint32_t)ra + 1u) : res;            // inc :2864
-      res = (op == AVGPU_H_DEC) ? (int)((uint32_t)ra - 1u) : res;            // dec :2871
-      res = (op == AVGPU_H_SHIFT_R) ? (ra >> 1) : res;                       // shift-r :2806
-      res = (op == AVGPU_H_SHIFT_L) ? (int)((uint32_t)ra << 1) : res;        // shift-l :2813
-      res = (op == AVGPU_H_SWAP) ? rb : res;                                 // swap :2742
-      const bool wr = (WR_OPS & obit) != 0u;
-      const bool sw = op == AVGPU_H_SWAP;
-      // head ops: head id = nop-mod or IP (mov-head :6809, jmp-head :6859, get-head :6907)
-      const int hv = (r == 0) ? ip : ((r == 1) ? rh : wh);
-      const bool hw = op == AVGPU_H_MOV_HEAD || op == AVGPU_H_JMP_HEAD;
-      int hnew = fh;                                                         // mov-head: Set(FLOW), no adjust
-      if (op == AVGPU_H_JMP_HEAD) hnew = head_adjust((int)((uint32_t)hv + (uint32_t)r2), M);
-      r0 = (wr && r == 0) ? res : ((sw && rn == 0) ? ra : r0);
-      r1 = (wr && r == 1) ? res : ((sw && rn == 1) ? ra : r1);
-      r2 = (wr && r == 2) ? res : ((sw && rn == 2) ? ra : r2);
-      r2 = (op == AVGPU_H_GET_HEAD) ? hv : r2;
-      rh = (hw && r == 1) ? hnew : rh;
-      wh = (hw && r == 2) ? hnew : wh;
-      if (op == AVGPU_H_SET_FLOW) fh = head_adjust(ra, M);                   // set-flow :7270
-      if (hw && r == 0) ip = hnew;
-      adv = !(op == AVGPU_H_MOV_HEAD && r == 0);
-      // if-n-equ :2190 / if-less :2235 skip the next instruction
-      const bool skip = (op == AVGPU_H_IF_N_EQU && ra == rb) || (op == AVGPU_H_IF_LESS && ra >= rb);
-      if (skip) ip = head_wrap(ip + 1, M);
-      ctl ^= (op == AVGPU_H_SWAP_STK) ? CTL_CURSTK : 0u;                     // swap-stk :2739
-    }
+    if (FAST_OPS & obit) adv = fast_op(op, r, r0, r1, r2, ip, rh, wh, fh, ctl, M);
     CK(1);
     if (op == AVGPU_H_H_COPY) {                               // :7130 Inst_HeadCopy
       rh = rha;
@@ -938,25 +1018,26 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
         // reaction i rewards task i, requisites at most "max_count=1"
         // (capi.hip avgpu_load_env): the firing set is a bit operation and
         // the bonus factors multiply in reaction order (ascending bits)
-        const uint32_t done = io ? (tmask & k_env_react_mask & ~(k_env_once_mask & nzm)) : 0u;
+        uint32_t done = io ? (tmask & k_env_react_mask & ~(k_env_once_mask & nzm)) : 0u;
         if (__ballot(done != 0u) != 0ull) {
           double mult = 1.0, addb = 0.0;
           uint32_t paid = done;
           if (k_env_res_mask != 0u) {
-            // finite resources: each lane walks its own tasks, so that a
-            // wave's resource loads go out together (one memory round trip
-            // per task rank, not one per distinct task of the wave)
+            // finite resources (configs[4]): the event is queued and its
+            // bonus, reaction counts and consumption applied at the next
+            // flush (res_flush: before a divide of the lane, when its queue is
+            // full, at the slice's end) -- nothing else reads them, and only
+            // this organism draws on its cell in the slice, so the order of
+            // every level, bonus and count is unchanged; the wave pays one
+            // memory round trip per flushed rank instead of one per IO
             if (done) {
-              for (uint32_t d = done; d; d &= d - 1u) {
-                const int t = __ffs(d) - 1;
-                if ((k_env_res_mask >> t) & 1u) {
-                  if (!consume_resource(W, W.react_res + t * RR_STRIDE, N, cell, mult, addb)) paid &= ~(1u << t);
-                } else {
-                  mult = __dmul_rn(mult, tmul[t]);
-                  addb = __dadd_rn(addb, tadd[t]);
-                }
-              }
+              const uint32_t n = rpq >> 30;
+              rpq = (rpq & 0x07FFFFFFu) | (done << (9 * n)) | ((n + 1u) << 30);
+#pragma unroll
+              for (int q = 0; q < AVGPU_NUM_LOGIC_TASKS; q++) tc[q] += (done >> q) & 1u;
+              nzm |= done;
             }
+            done = 0u;
           } else
           for (int t = 0; t < AVGPU_NUM_LOGIC_TASKS; t++) {   // wave-uniform t
             const bool dt = (done >> t) & 1u;
@@ -1027,6 +1108,9 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
     }
     CK(3);
 
+    // a divide reads the bonus and resets the counts: apply its queued rewards first
+    if (k_env_res_mask != 0u && __ballot(rpq != 0u && (rq == RQ_DIVIDE || (rpq >> 30) == 3u)) != 0ull)
+      res_flush<GTAB>(W, N, cell, rpq, bonus, rc, ttab, tmul, tadd, k_env_res_mask);
     // ---- wave phase: serve the posted requests, one lane at a time ----
     unsigned long long pend = __ballot(rq != RQ_NONE);
     while (pend) {
@@ -1688,6 +1772,7 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
 #undef GETHEAD
 #undef SETHEAD
 
+  if (k_env_res_mask != 0u) res_flush<GTAB>(W, N, cell, rpq, bonus, rc, ttab, tmul, tadd, k_env_res_mask);
   // ---- write back ----
 #ifdef AVGPU_PHASE_CLOCKS
   const uint64_t clk2 = __builtin_amdgcn_s_memtime();

@@ -1,5 +1,5 @@
 """Write a trimmed copy of interp.hip that instantiates only the class-0
-world kernel (C0W, SIMPLE, DEF), for fast ISA / register-count experiments:
+world kernel of the bench (REC, C0W, SIMPLE, DEF), for fast ISA / register-count experiments:
 
   python tools/isa/c0_only.py /tmp/isa/c0.hip [extra #define lines...]
   hipcc -O3 --offload-arch=gfx950 -std=c++17 -ffp-contract=off \
@@ -14,8 +14,8 @@ cut = src.index("}  // namespace\n")
 body = src[:cut]
 tail = """
 void c0_launch(const DevWorld* dW) {
-  hipLaunchKernelGGL((k_interpret<CLASS0_SIZE, false, true, true, true>), dim3(1), dim3(64), 0, 0, dW, 0, 0,
-                     (int)AVGPU_MODE_WORLD, (int64_t)0, (int64_t)0, 1, 64);
+  hipLaunchKernelGGL((k_interpret<CLASS0_SIZE, true, true, true, true, false>), dim3(1), dim3(64), 0, 0, dW, 0, 0,
+                     (int)AVGPU_MODE_WORLD, (int64_t)0, (int64_t)0, 1, 64, 0);
 }
 }  // namespace
 void c0_entry(const DevWorld* dW) { c0_launch(dW); }

@@ -675,7 +675,7 @@ enum avgpu_counter {
   AVGPU_CNT_SPILLS = 5,     /* slices handed to a larger LDS size class */
   AVGPU_CNT_SLICES = 6,     /* organisms with a non-zero allotment */
   AVGPU_CNT_LANESTEPS = 7,  /* 64 x longest lane per wave (lane efficiency = INSTS / this) */
-  AVGPU_CNT_C0_SLICES = 8,  /* slices run by the class-0 (<=384 sites) launch */
+  AVGPU_CNT_C0_SLICES = 8,  /* slices run by the class-0 launch (its windows, the list-class blocks inside it, its in-wave spill continuations) */
   AVGPU_CNT_C0_SITES = 9,   /* tape sites that launch staged in plus wrote back */
   /* 10..17: per-phase clocks of diagnostic (AVGPU_PHASE_CLOCKS) builds */
   AVGPU_CNT_HALO_SENT = 18, /* offspring shipped to a neighbouring tile */

@@ -164,6 +164,7 @@ int setup_world(avgpu_world* w, int64_t n, bool test_buffers) {
   A(occ, ng); A(claim, ng); A(claim2, ng); A(owner, ng); A(killt, n); A(sdone, n);
   W.claim_r[0] = W.claim; W.claim_r[1] = W.claim2;
   A(claim_r[2], ng); A(claim_r[3], ng); A(b_tgt, 4 * R);
+  if (c.birth_method == 4) { A(e_list, n); A(e_blk, (n + 255) / 256 + 1); }
   if (test_buffers) {
     A(t_flags, (size_t)n * TAPE_SLOT); A(t_flags_len, n); A(t_child, (size_t)n * TAPE_SLOT);
     A(t_child_len, n);
@@ -285,8 +286,9 @@ std::string unsupported_cfg(const avgpu_cfg& c) {
   if (c.world_geometry != 1 && c.world_geometry != 2) return "WORLD_GEOMETRY other than 1 (grid) or 2 (torus)";
   if (c.slicing_method < 0 || c.slicing_method > 2) return "SLICING_METHOD other than 0, 1, 2";
   if (c.base_merit_method < 0 || c.base_merit_method > 5) return "BASE_MERIT_METHOD other than 0..5";
-  if (c.birth_method < 0 || c.birth_method > 3)
-    return "BIRTH_METHOD other than 0 (random neighbour), 1 (oldest), 2 (highest age / merit), 3 (empty only)";
+  if (c.birth_method < 0 || c.birth_method > 4)
+    return "BIRTH_METHOD other than 0 (random neighbour), 1 (oldest), 2 (highest age / merit), 3 (empty only), "
+           "4 (whole-world soup)";
   if ((c.birth_method == 1 || c.birth_method == 2) && !c.prefer_empty)
     return "BIRTH_METHOD 1 / 2 without PREFER_EMPTY (the reference reads the organism of an empty cell)";
   if (c.death_method < 0 || c.death_method > 2) return "DEATH_METHOD other than 0, 1, 2";
@@ -875,8 +877,8 @@ int avgpu_run_serial_updates(avgpu_world* w, int n, avgpu_update_stats* last) {
   if (W.rec) return fail(AVGPU_EUNSUPPORTED, "the serial world takes its own two streams (avgpu_set_serial_streams), "
                                              "not per-organism recorded streams");
   if (W.tiled) return fail(AVGPU_EUNSUPPORTED, "the serial world runs single worlds, not strip tiles");
-  if (W.birth_method == 1 || W.birth_method == 2)
-    return fail(AVGPU_EUNSUPPORTED, "BIRTH_METHOD 1 / 2 run on the batch world, not the serial world");
+  if (W.birth_method == 1 || W.birth_method == 2 || W.birth_method == 4)
+    return fail(AVGPU_EUNSUPPORTED, "BIRTH_METHOD 1 / 2 / 4 run on the batch world, not the serial world");
   if ((rc = serial_alloc(w)) < 0) return rc;
   for (int u = 0; u < n; u++) {
     launch_reset_counts(W, w->stream);
@@ -1354,6 +1356,8 @@ int avgpu_set_tile(avgpu_world* w, int64_t row0, int64_t arena_bytes) {
   if (w && w->cfg.sub_updates > 1) return fail(AVGPU_EUNSUPPORTED, "sub_updates > 1 on strip tiles");
   if (w && (w->cfg.birth_method == 1 || w->cfg.birth_method == 2))
     return fail(AVGPU_EUNSUPPORTED, "BIRTH_METHOD 1 / 2 on strip tiles (the ghost rows carry no age or merit)");
+  if (w && w->cfg.birth_method == 4)
+    return fail(AVGPU_EUNSUPPORTED, "BIRTH_METHOD 4 on strip tiles (a soup birth may land in any strip)");
   if (!w) return fail(AVGPU_EINVAL, "NULL world");
   DevWorld& W = w->W;
   const int64_t X = W.world_x;

@@ -317,6 +317,8 @@ struct DevWorld {
   // the class-0 order's bucket histogram of each 4096-cell sub-window
   // (k_allot's workgroups write it, k_window_order scans it): [nsub][SORT_BUCKETS]
   int32_t* sub_hist;
+  int32_t* e_list;    // BIRTH_METHOD 4 + PREFER_EMPTY: the cells empty at placement start, ascending
+  int32_t* e_blk;     // its per-256-cell counts, then their exclusive offsets (e_blk[nb]: the total)
 };
 
 // owner of a cell won by a neighbouring strip's offspring in round k at birth time t

@@ -1011,6 +1011,14 @@ __device__ __forceinline__ double position_value(const DevWorld& W, int c) {
   const double m = W.merit[c];
   return m > 0.0 ? __ddiv_rn(age, m) : age;
 }
+// BIRTH_METHOD 4 (POSITION_OFFSPRING_FULL_SOUP_RANDOM, main/cPopulation.cc:
+// 5297-5310; oracle soup_target): with PREFER_EMPTY a cell drawn uniformly
+// among those empty at placement start (e_list) that this round has not
+// taken, by up to SOUP_TRIES draws (FindRandEmptyCell, :5650-5668), else --
+// a full world, or every empty cell claimed by earlier births -- GetUInt(size);
+// without PREFER_EMPTY GetUInt(size), redrawn while it is the parent and
+// ALLOW_PARENT is 0.  Single worlds only (capi refuses strip tiles).
+#define SOUP_TRIES 64
 template <bool TILE>
 __device__ __forceinline__ bool place_pick_one(const DevWorld& W, int64_t r, int m) {
   const int parent = W.b_parent[r];
@@ -1020,6 +1028,37 @@ __device__ __forceinline__ bool place_pick_one(const DevWorld& W, int64_t r, int
     if (TILE) return tile_taken(W, c, m);
     return W.occ[c] != 0 || (prev && prev[c] != 0ull);
   };
+  if (!TILE && W.birth_method == 4) {
+    int32_t* const inh = W.b_inh + (int64_t)r * BI_WORDS;
+    const uint32_t lo = (uint32_t)inh[BI_RLO], hi = (uint32_t)inh[BI_RHI];
+    uint32_t ctr = (uint32_t)inh[BI_RCTR];
+    const uint32_t n = (uint32_t)W.n;
+    int t = -1;
+    if (W.prefer_empty) {
+      const uint32_t ne = (uint32_t)W.e_blk[(W.n + 255) / 256];
+      for (int k = 0; k < SOUP_TRIES && ne > 0u && t < 0; k++) {
+        const int c = W.e_list[rng_below(lo, hi, ctr, ne)];
+        if (!taken(c)) t = c;
+      }
+      if (t < 0) t = (int)rng_below(lo, hi, ctr, n);
+    } else {
+      t = (int)rng_below(lo, hi, ctr, n);
+      while (!W.allow_parent && n > 1u && t == parent) t = (int)rng_below(lo, hi, ctr, n);
+    }
+    if (t == parent && !W.allow_parent) {              // ActivateOffspring drops it (:706-713)
+      inh[BI_RCTR] = (int32_t)ctr;
+      W.b_target[r] = -1;
+      W.b_state[r] = (int8_t)(BS_NO_CELL - m);
+      return false;
+    }
+    const unsigned long long key = claim_key(BI_TIME(inh[BI_FINAL]), taken(t), rng_next(lo, hi, ctr),
+                                             W.cell0 + parent, W.b_seq[r]);
+    inh[BI_RCTR] = (int32_t)ctr;
+    W.b_target[r] = t;
+    W.b_prio[r] = key;
+    W.b_tgt[(int64_t)m * W.rcap + r] = t;
+    return true;
+  }
   int nbr[8];
   const int nn = neighbours(W, parent, nbr);
   int cand[9];
@@ -1064,6 +1103,54 @@ __device__ __forceinline__ bool place_pick_one(const DevWorld& W, int64_t r, int
 #define QUEUE_LOOP(i) \
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, _qn = queue_len(W); i < _qn; \
        i += (int64_t)gridDim.x * blockDim.x)
+// BIRTH_METHOD 4 + PREFER_EMPTY: the cells empty at placement start (after
+// the slices' deaths), ascending -- FindRandEmptyCell's candidates (oracle
+// place_reset): per-256-cell counts, one block's exclusive scan over them
+// (e_blk[nb]: the total), the scatter
+__global__ __launch_bounds__(256) void k_empty_count(DevWorld W) {
+  __shared__ int ws[4];
+  const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const bool e = c < W.n && W.occ[c] == 0;
+  const int cnt = __popcll(__ballot(e));
+  if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = cnt;
+  __syncthreads();
+  if (threadIdx.x == 0) W.e_blk[blockIdx.x] = ws[0] + ws[1] + ws[2] + ws[3];
+}
+__global__ __launch_bounds__(1024) void k_empty_scan(DevWorld W, int nb) {
+  __shared__ int part[1024];
+  const int per = (nb + 1023) / 1024;
+  const int b0 = (int)threadIdx.x * per, b1 = min(nb, b0 + per);
+  int sum = 0;
+  for (int b = b0; b < b1; b++) sum += W.e_blk[b];
+  part[threadIdx.x] = sum;
+  __syncthreads();
+  for (int off = 1; off < 1024; off <<= 1) {          // inclusive scan of the runs' sums
+    const int v = (int)threadIdx.x >= off ? part[threadIdx.x - off] : 0;
+    __syncthreads();
+    part[threadIdx.x] += v;
+    __syncthreads();
+  }
+  int run = threadIdx.x > 0 ? part[threadIdx.x - 1] : 0;
+  for (int b = b0; b < b1; b++) {
+    const int v = W.e_blk[b];
+    W.e_blk[b] = run;
+    run += v;
+  }
+  if (threadIdx.x == 1023) W.e_blk[nb] = part[1023];
+}
+__global__ __launch_bounds__(256) void k_empty_scatter(DevWorld W) {
+  __shared__ int ws[4];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const bool e = c < W.n && W.occ[c] == 0;
+  const unsigned long long m = __ballot(e);
+  if (lane == 0) ws[wv] = __popcll(m);
+  __syncthreads();
+  int base = W.e_blk[blockIdx.x];
+  for (int k = 0; k < wv; k++) base += ws[k];
+  if (e) W.e_list[base + __popcll(m & ((1ull << lane) - 1ull))] = (int)c;
+}
+
 // The divide mutations (k_place_pick_mut, k_tile_prep), by 256-thread blocks:
 // block b of nb scans MUT_PER_BLOCK queue entries at a time -- lane k of each
 // wave loads one entry's five edit words and both lengths -- and lists the
@@ -1838,6 +1925,12 @@ void launch_world_post(const DevWorld& W, hipStream_t s, double* stats, bool eag
   const int pm = has_divide_mutations(W) ? (int)((mut_grid(W) + 3) / 4) : 0;
   const int pf = (int)std::min<unsigned>(bb, 256u);   // finalize_phenotype blocks
   const int nbk = (int)bb + pf + pm;
+  if (W.birth_method == 4 && W.prefer_empty) {      // the soup's empty cells (k_empty_*)
+    const int eb = (int)nblk(W.n, 256);
+    hipLaunchKernelGGL(k_empty_count, dim3(eb), dim3(256), 0, s, W);
+    hipLaunchKernelGGL(k_empty_scan, dim3(1), dim3(1024), 0, s, W, eb);
+    hipLaunchKernelGGL(k_empty_scatter, dim3(eb), dim3(256), 0, s, W);
+  }
 #ifdef AVGPU_SPLIT_PICK_MUT
   hipLaunchKernelGGL(k_place_pick_mut, dim3(bb), dim3(256), 0, s, W, (int)bb, pf, 0, nbk);
   hipLaunchKernelGGL(k_place_pick_mut, dim3(pf), dim3(256), 0, s, W, (int)bb, pf, (int)bb, nbk);

@@ -130,7 +130,7 @@ typedef struct avgpu_cfg {
   int32_t alloc_method;            /* ALLOC_METHOD (0 default inst, 2 random) */
   int32_t divide_method;           /* DIVIDE_METHOD (1 split) */
   int32_t max_label_exe_size;      /* MAX_LABEL_EXE_SIZE */
-  int32_t birth_method;            /* BIRTH_METHOD (0 random nbhd, 3 empty only) */
+  int32_t birth_method;            /* BIRTH_METHOD 0 random neighbour, 1 oldest, 2 age / merit, 3 empty only, 4 whole-world soup */
   int32_t prefer_empty;            /* PREFER_EMPTY */
   int32_t allow_parent;            /* ALLOW_PARENT */
   int32_t test_cpu_time_mod;       /* TEST_CPU_TIME_MOD */

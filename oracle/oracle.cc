@@ -286,6 +286,7 @@ struct World {
   std::vector<uint32_t> killt;    // per cell: 2^16 - the earliest kill pick's birth time, 0 none
   std::vector<uint64_t> prio;     // each record's claim key in its current round
   std::vector<int8_t> bstate;     // BS_* (place_pick)
+  std::vector<int64_t> empty_cells;   // BIRTH_METHOD 4: the cells empty at placement start, ascending
   int64_t t_insts = 0, t_deaths = 0, t_divides = 0, t_slices = 0, t_born = 0, t_dropped = 0;
   uint32_t sched_key = 0;  // the scheduler's node-draw key: update x K + sub-update (sub_share)
   int64_t t_oversize = 0;   // offspring longer than AVGPU_MAX_GENOME after a slip (dropped at the divide)
@@ -2159,9 +2160,42 @@ static double position_value(const World& w, int64_t c) {
   return o.merit > 0.0 ? age / o.merit : age;
 }
 
+// BIRTH_METHOD 4 (POSITION_OFFSPRING_FULL_SOUP_RANDOM, main/cPopulation.cc:
+// 5297-5310): with PREFER_EMPTY, FindRandEmptyCell (:5650-5668) -- a cell drawn
+// uniformly among the empty ones; here the cells empty at the batch step's end
+// (empty_cells, ascending) that this round has not taken, by up to SOUP_TRIES
+// draws; none (a full world, or every empty cell claimed by earlier births):
+// GetUInt(size) over the whole world.  Without PREFER_EMPTY: GetUInt(size),
+// redrawn while it is the parent and ALLOW_PARENT is 0.  The parent's cell
+// without ALLOW_PARENT: ActivateOffspring drops the offspring (:706-713).
+static constexpr int SOUP_TRIES = 64;
+template <class Taken>
+static int64_t soup_target(World& w, Birth& b, Taken taken) {
+  const uint32_t n = (uint32_t)w.ncells;
+  if (w.cfg.prefer_empty) {
+    const uint32_t ne = (uint32_t)w.empty_cells.size();
+    for (int k = 0; k < SOUP_TRIES && ne > 0; k++) {
+      const int64_t c = w.empty_cells[b.rng.uint_below(ne)];
+      if (!taken(c)) return c;
+    }
+    return b.rng.uint_below(n);
+  }
+  int64_t c = b.rng.uint_below(n);
+  while (!w.cfg.allow_parent && n > 1 && c == b.parent) c = b.rng.uint_below(n);
+  return c;
+}
+
 template <class Taken>
 static bool place_pick(World& w, int64_t i, int m, Taken taken) {
   Birth& b = w.births[i];
+  if (w.cfg.birth_method == 4) {
+    const int64_t t = soup_target(w, b, taken);
+    if (t == b.parent && !w.cfg.allow_parent) { b.target = -1; w.bstate[i] = (int8_t)(BS_NO_CELL - m); return false; }
+    b.target = t;
+    w.prio[i] = claim_key(b.t, taken(t), b.rng.next(), w.cell0 + b.parent, b.seq);
+    w.tgt_r[m][i] = t;
+    return true;
+  }
   int64_t nb[8];
   const int nn = neighbours(w, b.parent, nb);
   int64_t cand[9];
@@ -2194,6 +2228,9 @@ static void place_reset(World& w, int64_t ext) {
   const int64_t nbirth = (int64_t)w.births.size();
   w.occ.assign(ext, 0);
   for (int64_t c = 0; c < w.ncells; c++) w.occ[c] = w.orgs[c].alive ? 1 : 0;
+  w.empty_cells.clear();
+  if (w.cfg.birth_method == 4 && w.cfg.prefer_empty)
+    for (int64_t c = 0; c < w.ncells; c++) if (!w.occ[c]) w.empty_cells.push_back(c);
   for (int k = 0; k < 4; k++) { w.claim_r[k].assign(ext, 0); w.tgt_r[k].assign(nbirth, -1); }
   w.owner.assign(ext, -1);
   w.killt.assign(w.ncells, 0);
@@ -2388,6 +2425,8 @@ int orc_set_tile(void* h, int64_t row0, int64_t arena) {
   World& w = *(World*)h;
   if (w.cfg.birth_method == 1 || w.cfg.birth_method == 2)
     return fail(AVGPU_EUNSUPPORTED, "BIRTH_METHOD 1 / 2 on strip tiles (the ghost rows carry no age or merit)");
+  if (w.cfg.birth_method == 4)
+    return fail(AVGPU_EUNSUPPORTED, "BIRTH_METHOD 4 on strip tiles (a soup birth may land in any strip)");
   const int64_t X = w.cfg.world_x;
   if (X <= 0 || w.ncells % X) return fail(AVGPU_EINVAL, "tile cells must be whole rows of WORLD_X");
   const int64_t rows = w.ncells / X;
@@ -2855,8 +2894,8 @@ int orc_set_serial_streams(void* h, const double* sched, int64_t n_sched, const 
 //    before the speculative run: rotated connection lists (serial_target).
 int orc_run_serial_updates(void* h, int n_updates, avgpu_update_stats* out) {
   World& w = *(World*)h;
-  if (w.cfg.birth_method == 1 || w.cfg.birth_method == 2)
-    return fail(AVGPU_EUNSUPPORTED, "BIRTH_METHOD 1 / 2 run on the batch world, not the serial world");
+  if (w.cfg.birth_method == 1 || w.cfg.birth_method == 2 || w.cfg.birth_method == 4)
+    return fail(AVGPU_EUNSUPPORTED, "BIRTH_METHOD 1 / 2 / 4 run on the batch world, not the serial world");
   if ((int64_t)w.face.size() != w.ncells) w.face.assign(w.ncells, 0);
   SerialSched sch;
   sch.init(w.ncells);

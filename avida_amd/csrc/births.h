@@ -254,15 +254,34 @@ __device__ __forceinline__ void setup_child(const DevWorld& W, int64_t c, const 
 // in flight at once).  The genome moves in 16-byte quads; the bytes of the
 // last quad past the genome are written as 0 (sites >= mem_size are never
 // read before h-alloc fills them, and every export masks them).
+// one 16-B quad k of an offspring's genome into the cell's tape: the sites
+// past len cleared, the genotype key's words summed
+__device__ __forceinline__ void child_quad(uint4 v, int k, int len, uint4* __restrict__ d4, uint64_t& gsum) {
+  const int w = 4 * k;
+  uint32_t x[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    const int keep = len - 4 * (w + j);     // sites of word w+j inside the genome
+    if (keep <= 0) x[j] = 0u;
+    else { if (keep < 4) x[j] &= (1u << (8 * keep)) - 1u; gsum += gk_word(x[j], w + j, len); }
+  }
+  d4[k] = make_uint4(x[0], x[1], x[2], x[3]);
+}
+// PRE: the genome's first PRE quads are already in registers (pre), loaded by
+// the caller before it knew whether the record won its cell
+template <int PRE = 0>
 __device__ __forceinline__ void setup_child_lane(const DevWorld& W, int64_t c, const Child& b,
-                                                 const uint8_t* __restrict__ src) {
+                                                 const uint8_t* __restrict__ src, const uint4* pre = nullptr) {
   const int64_t N = W.n;
   const int len = b.len;
   const uint4* __restrict__ s4 = reinterpret_cast<const uint4*>(src);
   uint4* __restrict__ d4 = reinterpret_cast<uint4*>(W.tape + c * TAPE_SLOT);
   uint64_t gsum = 0;
   const int nq = (len + 15) >> 4;
-  for (int k0 = 0; k0 < nq; k0 += 4) {
+#pragma unroll
+  for (int u = 0; u < PRE; u++)
+    if (u < nq) child_quad(pre[u], u, len, d4, gsum);
+  for (int k0 = PRE; k0 < nq; k0 += 4) {
     uint4 v[4];
 #pragma unroll
     for (int u = 0; u < 4; u++)
@@ -270,15 +289,7 @@ __device__ __forceinline__ void setup_child_lane(const DevWorld& W, int64_t c, c
 #pragma unroll
     for (int u = 0; u < 4; u++) {
       if (k0 + u >= nq) break;
-      const int w = 4 * (k0 + u);
-      uint32_t x[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
-#pragma unroll
-      for (int j = 0; j < 4; j++) {
-        const int keep = len - 4 * (w + j);     // sites of word w+j inside the genome
-        if (keep <= 0) x[j] = 0u;
-        else { if (keep < 4) x[j] &= (1u << (8 * keep)) - 1u; gsum += gk_word(x[j], w + j, len); }
-      }
-      d4[k0 + u] = make_uint4(x[0], x[1], x[2], x[3]);
+      child_quad(v[u], k0 + u, len, d4, gsum);
     }
   }
   W.gkey[c] = gk_final(gsum, len);

@@ -77,14 +77,31 @@ __global__ void k_res_cell_rates(DevWorld W, int r) {
   }
 }
 
+// x / c correctly rounded for a constant c with r = RN(1 / c): y = RN(x r) is
+// a faithful quotient, the residual x - c y is exact by FMA, and
+// RN(y + r (x - c y)) = RN(x / c) (Markstein's correction) away from
+// underflow and overflow -- tiny, huge and non-finite x take the full
+// division (zero: x r, which keeps the sign).  3 FP64 operations instead of
+// __ddiv_rn's scaled Newton sequence; tests/test_res_division.py checks the
+// identity on 2e7 quotients per c (4e8 when it was written).
+__device__ __forceinline__ double div_const(double x, double c, double r) {
+  const double ax = fabs(x);
+  if (ax == 0.0) return __dmul_rn(x, r);                    // +-0 (equal amounts: a common flow)
+  if (!(ax >= 0x1p-900 && ax <= 0x1p+900)) return __ddiv_rn(x, c);
+  const double y = __dmul_rn(x, r);
+  const double e = __fma_rn(-c, y, x);
+  return __fma_rn(e, r, y);
+}
+constexpr double SQRT2 = 1.4142135623730951, R_SQRT2 = 1.0 / 1.4142135623730951, R_3 = 1.0 / 3.0;
+
 // FlowMatter (main/cResourceCount.cc:40-110) from elem1 = a1 to elem2 = a2.
 // Exact rewrites: x / 16 == x * 0.0625 and x / 2 == x * 0.5 (power-of-two
 // divisors: the same real value, so the same rounding), and with zero gravity
 // the reference's (-a2 * 0) / 3 is the signed zero (-a2 * 0) itself.
 __device__ __forceinline__ double gravity_term(double a1, double a2, int dist, double g) {
   if (g == 0.0) return __dmul_rn(-a2, 0.0);
-  if ((dist > 0 && g > 0.0) || (dist < 0 && g < 0.0)) return __ddiv_rn(__dmul_rn(a1, fabs(g)), 3.0);
-  return __ddiv_rn(__dmul_rn(-a2, fabs(g)), 3.0);
+  if ((dist > 0 && g > 0.0) || (dist < 0 && g < 0.0)) return div_const(__dmul_rn(a1, fabs(g)), 3.0, R_3);
+  return div_const(__dmul_rn(-a2, fabs(g)), 3.0, R_3);
 }
 
 __device__ __forceinline__ double flow_amt(const ResParam& P, double a1, double a2, int xdist, int ydist,
@@ -101,7 +118,7 @@ __device__ __forceinline__ double flow_amt(const ResParam& P, double a1, double 
   }
   const double num = __dadd_rn(__dadd_rn(__dadd_rn(xd, yd), xg), yg);
   const double q = diagonal ? __dmul_rn(num, 0.5) : num;        // / (|xdist| + |ydist|)
-  return diagonal ? __ddiv_rn(q, 1.4142135623730951) : q;       // / dist (sqrt(2.0) or 1)
+  return diagonal ? div_const(q, SQRT2, R_SQRT2) : q;           // / dist (sqrt(2.0) or 1)
 }
 
 // pointer k = 3..6 of cell (x, y): E, SE, S, SW (cSpatialResCount::SetPointers)
@@ -226,7 +243,11 @@ __device__ __forceinline__ double res_flows(const DevWorld& W, const ResParam& P
 // configs[4]: profiles/r04o_res_step_tiled.txt.)
 template <bool FUSED>
 __global__ void k_res_step(DevWorld W, ResIds ids) {
-  const int c = (int)(blockIdx.x * blockDim.x + threadIdx.x);   // n < 2^31 (avgpu_load_resources)
+  // blocks are dealt to the 8 XCDs round robin: XCD k takes the k-th eighth
+  // of the rows, so the rows above and below a block are in its own L2
+  unsigned bx = blockIdx.x;
+  if ((gridDim.x & 7u) == 0u) bx = (bx & 7u) * (gridDim.x >> 3) + (bx >> 3);
+  const int c = (int)(bx * blockDim.x + threadIdx.x);   // n < 2^31 (avgpu_load_resources)
   if (c >= W.n) return;
   const int r = ids.r[blockIdx.y];
   const ResParam P = W.res_param[r];

@@ -285,11 +285,18 @@ def main():
         cpu = cpu_baseline_multi(golden, args.cpu_seconds, args.env, procs)
 
     import torch
-    torch.cuda.set_device(local)
+    # AVGPU_BENCH_STAGED=1: a rehearsal of the multi-GPU bench on fewer GPUs --
+    # ranks may share a device, exchanges over gloo staged through host
+    # tensors (tiles.StagedTransport; RCCL refuses two ranks on one device).
+    # Its line says so in config.transport and is no scaling measurement.
+    staged = os.environ.get("AVGPU_BENCH_STAGED") == "1" and world > 1
+    rdev = "cpu" if staged else "cuda"      # the timing / counter reductions' tensors
+    device = local % max(1, torch.cuda.device_count()) if staged else local
+    torch.cuda.set_device(device)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl")
+        dist.init_process_group("gloo" if staged else "nccl")
         assert dist.get_world_size() == world == args.gpus
 
     from avida_amd import capi, files, tiles
@@ -303,9 +310,10 @@ def main():
             return None
         return tiles.Tile(lib, "avgpu_", h, rank * args.side, world, "cuda")
 
-    h, cfg, n, tile = build_world(lib, capi, files, golden, args.side, args.seed, local, rank, world,
+    h, cfg, n, tile = build_world(lib, capi, files, golden, args.side, args.seed, device, rank, world,
                                   on_tile, args.env, args.sub_updates)
-    strips = tiles.StripWorld([tile], tiles.DistTransport(dist)) if tile else None
+    transport = (tiles.StagedTransport(dist) if staged else tiles.DistTransport(dist)) if tile else None
+    strips = tiles.StripWorld([tile], transport) if tile else None
 
     capi.check(lib, lib.avgpu_set_timing(h, args.time_every))
 
@@ -345,7 +353,7 @@ def main():
     births = s1.cum_births - s0.cum_births
     dt = t1 - t0
     vec = torch.tensor([dt, float(insts), float(births), float(s1.num_organisms)],
-                       dtype=torch.float64, device="cuda")
+                       dtype=torch.float64, device=rdev)
     if dist:
         mx = vec.clone()
         dist.all_reduce(mx, op=dist.ReduceOp.MAX)
@@ -362,7 +370,7 @@ def main():
     # larger LDS class, summed over ranks
     extra = torch.tensor([float(d[capi.CNT_DROPPED]), float(d[capi.CNT_SPILLS]),
                           float(d[capi.CNT_OVERWRITTEN])],
-                         dtype=torch.float64, device="cuda")
+                         dtype=torch.float64, device=rdev)
     if dist:
         dist.all_reduce(extra)
     long_run = None
@@ -380,11 +388,11 @@ def main():
         torch.cuda.synchronize()
         if dist:
             dist.barrier()
-        ldt = torch.tensor([time.perf_counter() - l0], dtype=torch.float64, device="cuda")
+        ldt = torch.tensor([time.perf_counter() - l0], dtype=torch.float64, device=rdev)
         ls1 = capi.AvgpuUpdateStats()
         capi.check(lib, lib.avgpu_get_stats(h, C.byref(ls1)))
         lins = torch.tensor([float(ls1.cum_insts_executed - ls0.cum_insts_executed)],
-                            dtype=torch.float64, device="cuda")
+                            dtype=torch.float64, device=rdev)
         if dist:
             dist.all_reduce(ldt, op=dist.ReduceOp.MAX)
             dist.all_reduce(lins)
@@ -483,6 +491,8 @@ def main():
             "spills_per_update": extra[1].item() / args.steps,
             "insts_per_update": tot_insts / args.steps,
             "parallelism": f"strips{world}",
+            "transport": ("gloo-staged rehearsal (ranks share GPUs; not a scaling measurement)" if staged
+                          else ("rccl" if world > 1 else "none")),
             "ranks": world,
             "sub_updates": max(1, args.sub_updates),
             "long_run": long_run,

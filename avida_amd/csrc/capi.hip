@@ -164,7 +164,16 @@ int setup_world(avgpu_world* w, int64_t n, bool test_buffers) {
   A(occ, ng); A(claim, ng); A(claim2, ng); A(owner, ng); A(killt, n); A(sdone, n);
   W.claim_r[0] = W.claim; W.claim_r[1] = W.claim2;
   A(claim_r[2], ng); A(claim_r[3], ng); A(b_tgt, 4 * R);
-  if (c.birth_method == 4) { A(e_list, n); A(e_blk, (n + 255) / 256 + 1); }
+  if (c.birth_method == 4) {
+    A(e_list, n); A(e_blk, (n + 255) / 256 + 1); A(soup_perm, n);
+    std::vector<int32_t> iota((size_t)n);
+    for (int64_t i = 0; i < n; i++) iota[(size_t)i] = (int32_t)i;
+    // on the world's stream, after alloc's zeroing memset (a plain hipMemcpy
+    // runs on the null stream, which does not wait for the non-blocking one)
+    HIPCHK(hipMemcpyAsync(W.soup_perm, iota.data(), (size_t)n * sizeof(int32_t), hipMemcpyHostToDevice,
+                          w->stream));
+    HIPCHK(hipStreamSynchronize(w->stream));
+  }
   if (test_buffers) {
     A(t_flags, (size_t)n * TAPE_SLOT); A(t_flags_len, n); A(t_child, (size_t)n * TAPE_SLOT);
     A(t_child_len, n);
@@ -877,8 +886,8 @@ int avgpu_run_serial_updates(avgpu_world* w, int n, avgpu_update_stats* last) {
   if (W.rec) return fail(AVGPU_EUNSUPPORTED, "the serial world takes its own two streams (avgpu_set_serial_streams), "
                                              "not per-organism recorded streams");
   if (W.tiled) return fail(AVGPU_EUNSUPPORTED, "the serial world runs single worlds, not strip tiles");
-  if (W.birth_method == 1 || W.birth_method == 2 || W.birth_method == 4)
-    return fail(AVGPU_EUNSUPPORTED, "BIRTH_METHOD 1 / 2 / 4 run on the batch world, not the serial world");
+  if (W.birth_method == 1 || W.birth_method == 2)
+    return fail(AVGPU_EUNSUPPORTED, "BIRTH_METHOD 1 / 2 run on the batch world, not the serial world");
   if ((rc = serial_alloc(w)) < 0) return rc;
   for (int u = 0; u < n; u++) {
     launch_reset_counts(W, w->stream);

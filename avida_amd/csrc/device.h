@@ -319,6 +319,7 @@ struct DevWorld {
   int32_t* sub_hist;
   int32_t* e_list;    // BIRTH_METHOD 4 + PREFER_EMPTY: the cells empty at placement start, ascending
   int32_t* e_blk;     // its per-256-cell counts, then their exclusive offsets (e_blk[nb]: the total)
+  int32_t* soup_perm; // serial world, BIRTH_METHOD 4: the reference's empty_cell_id_array (0..N-1 at creation)
 };
 
 // owner of a cell won by a neighbouring strip's offspring in round k at birth time t

@@ -2177,25 +2177,60 @@ __global__ __launch_bounds__(64, 1) void k_serial_update(const DevWorld* __restr
     if ((r >> 24) & 1) {
       // ActivateOffspring inside the h-divide (main/cPopulation.cc:621-960)
       apply_edits_wave(W, c, child);
-      int t = -1, face_t = 0;
+      int t = -1, face_t = -1;
       int32_t in3[3] = {0, 0, 0};
+      int alive_n = 0;
+      if (W.birth_method == 4 && W.prefer_empty) {   // num_organisms, for FindRandEmptyCell
+        int a = 0;
+        for (int64_t q = lane; q < W.n; q += 64) a += (W.ctl[q] & CTL_ALIVE) ? 1 : 0;
+        alive_n = wave_sum_i32(a);
+      }
       if (lane == 0) {
-        // PositionOffspring on the rotated connection list (oracle serial_target)
-        int base[8], conn[8], found[9];
-        const int nb = conn_base(W, (int)c, base);
-        const int f = nb ? W.face[c] % nb : 0;
-        for (int k = 0; k < nb; k++) conn[k] = base[(f + k) % nb];
-        int nf = 0;
-        if (W.prefer_empty)
-          for (int k = 0; k < nb; k++)
-            if (!(W.ctl[conn[k]] & CTL_ALIVE)) { for (int q = nf; q > 0; q--) found[q] = found[q - 1]; found[0] = conn[k]; nf++; }
-        if (nf == 0 && W.birth_method == 0) {
-          if (W.allow_parent) found[nf++] = (int)c;
-          for (int k = 0; k < nb; k++) found[nf++] = conn[k];
-        }
         uint32_t ct = W.sctx[2];
         bool ov = false;
-        t = nf == 0 ? (int)c : found[sctx_below(W, ct, (uint32_t)nf, ov)];
+        if (W.birth_method == 4) {
+          // FULL_SOUP_RANDOM (oracle serial_soup): FindRandEmptyCell on the
+          // persistent empty_cell_id_array, else GetUInt(size)
+          const uint32_t n = (uint32_t)W.n;
+          t = -1;
+          if (W.prefer_empty) {
+            if (alive_n < (int)n) {
+              uint32_t ws = n;
+              uint32_t idx = sctx_below(W, ct, ws, ov);
+              int cc = W.soup_perm[idx];
+              bool found = true;
+              while (W.ctl[cc] & CTL_ALIVE) {
+                --ws;
+                const int sw = W.soup_perm[ws];
+                W.soup_perm[ws] = cc;
+                W.soup_perm[idx] = sw;
+                if (ws == 1) { found = false; break; }
+                idx = sctx_below(W, ct, ws, ov);
+                cc = W.soup_perm[idx];
+              }
+              if (found) t = cc;
+            }
+            if (t < 0) t = (int)sctx_below(W, ct, n, ov);
+          } else {
+            t = (int)sctx_below(W, ct, n, ov);
+            while (!W.allow_parent && n > 1u && t == (int)c) t = (int)sctx_below(W, ct, n, ov);
+          }
+        } else {
+          // PositionOffspring on the rotated connection list (oracle serial_target)
+          int base[8], conn[8], found[9];
+          const int nb = conn_base(W, (int)c, base);
+          const int f = nb ? W.face[c] % nb : 0;
+          for (int k = 0; k < nb; k++) conn[k] = base[(f + k) % nb];
+          int nf = 0;
+          if (W.prefer_empty)
+            for (int k = 0; k < nb; k++)
+              if (!(W.ctl[conn[k]] & CTL_ALIVE)) { for (int q = nf; q > 0; q--) found[q] = found[q - 1]; found[0] = conn[k]; nf++; }
+          if (nf == 0 && W.birth_method == 0) {
+            if (W.allow_parent) found[nf++] = (int)c;
+            for (int k = 0; k < nb; k++) found[nf++] = conn[k];
+          }
+          t = nf == 0 ? (int)c : found[sctx_below(W, ct, (uint32_t)nf, ov)];
+        }
         if (t == (int)c && !W.allow_parent) t = -1;            // target_cells[i] = -1 (:706-712)
         if (t >= 0) {
           // ActivateOrganism -> SetupInputs random (main/cEnvironment.cc:1268-1271)
@@ -2203,9 +2238,9 @@ __global__ __launch_bounds__(64, 1) void k_serial_update(const DevWorld* __restr
           in3[1] = (51 << 24) + (int)sctx_below(W, ct, 1u << 24, ov);
           in3[2] = (85 << 24) + (int)sctx_below(W, ct, 1u << 24, ov);
           if (t != (int)c) {                                    // Rotate(parent_cell) (:935-944)
-            int tb[8];
+            int tb[8];                                          // (not adjacent: a full turn, no change)
             const int ntb = conn_base(W, t, tb);
-            for (int k = 0; k < ntb; k++) if (tb[k] == (int)c) face_t = k;
+            for (int k = 0; k < ntb; k++) if (tb[k] == (int)c && face_t < 0) face_t = k;
           }
         }
         W.sctx[2] = ct;
@@ -2227,7 +2262,7 @@ __global__ __launch_bounds__(64, 1) void k_serial_update(const DevWorld* __restr
         __threadfence_block();
         if (lane == 0) {
           W.spec[t] = 0;                                         // InsertOrganism resets the credit
-          if (parent_alive) W.face[t] = (uint8_t)face_t;
+          if (parent_alive && face_t >= 0) W.face[t] = (uint8_t)face_t;
         }
         __threadfence_block();
         stree_set(tree, size, t, b.merit);

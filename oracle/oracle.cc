@@ -269,6 +269,7 @@ struct World {
   Stream ctx_rng;      // serial world: the context stream every ctx.GetRandom() draw comes from
   std::vector<double> srec_sched, srec_ctx;   // their recorded values (avgpu_set_serial_streams)
   std::vector<uint8_t> face;   // serial world: each cell's connection-list rotation (cPopulationCell::Rotate)
+  std::vector<int64_t> soup_cells;   // serial world, BIRTH_METHOD 4: cPopulation::empty_cell_id_array
   // strip tiles (avgpu_set_tile): rows [row0, row0+rows) of a world_x x
   // global_rows world; occ / claim / owner carry two ghost rows after n
   int64_t row0 = 0, rows = 0, global_rows = 0, cell0 = 0;
@@ -2819,7 +2820,44 @@ static int conn_base(const World& w, int64_t cell, int64_t* out) {
 // reverse list order; with none, BIRTH_METHOD 0 takes the whole list in order
 // (Append) with the parent pushed in front (ALLOW_PARENT); one GetUInt(size)
 // from the context stream picks.  No candidate: the parent's cell (no draw).
+// BIRTH_METHOD 4 in the serial world: PositionOffspring's FULL_SOUP_RANDOM
+// (main/cPopulation.cc:5297-5310) with FindRandEmptyCell (:5650-5668) on the
+// reference's persistent empty_cell_id_array (0..N-1 at setup, :338-340):
+// a full world (num_organisms >= size) or a walk that runs out of cells ->
+// GetUInt(size); each occupied draw is swapped behind the shrinking range,
+// and the swaps persist.  Without PREFER_EMPTY GetUInt(size), redrawn while
+// it is the parent and ALLOW_PARENT is 0.  Every draw from the context stream.
+static int64_t serial_soup(World& w, int64_t parent) {
+  const uint32_t n = (uint32_t)w.ncells;
+  if ((int64_t)w.soup_cells.size() != w.ncells) {
+    w.soup_cells.resize(w.ncells);
+    for (int64_t c = 0; c < w.ncells; c++) w.soup_cells[c] = c;
+  }
+  if (w.cfg.prefer_empty) {
+    int64_t alive = 0;
+    for (int64_t c = 0; c < w.ncells; c++) alive += w.orgs[c].alive ? 1 : 0;
+    if (alive < (int64_t)n) {
+      uint32_t ws = n;
+      uint32_t idx = w.ctx_rng.uint_below(ws);
+      int64_t c = w.soup_cells[idx];
+      bool found = true;
+      while (w.orgs[c].alive) {
+        std::swap(w.soup_cells[idx], w.soup_cells[--ws]);
+        if (ws == 1) { found = false; break; }
+        idx = w.ctx_rng.uint_below(ws);
+        c = w.soup_cells[idx];
+      }
+      if (found) return c;
+    }
+    return w.ctx_rng.uint_below(n);
+  }
+  int64_t c = w.ctx_rng.uint_below(n);
+  while (!w.cfg.allow_parent && n > 1 && c == parent) c = w.ctx_rng.uint_below(n);
+  return c;
+}
+
 static int64_t serial_target(World& w, int64_t parent) {
+  if (w.cfg.birth_method == 4) return serial_soup(w, parent);
   int64_t base[8], conn[8], found[9];
   const int nb = conn_base(w, parent, base);
   const int f = nb ? w.face[parent] % nb : 0;
@@ -2894,8 +2932,8 @@ int orc_set_serial_streams(void* h, const double* sched, int64_t n_sched, const 
 //    before the speculative run: rotated connection lists (serial_target).
 int orc_run_serial_updates(void* h, int n_updates, avgpu_update_stats* out) {
   World& w = *(World*)h;
-  if (w.cfg.birth_method == 1 || w.cfg.birth_method == 2 || w.cfg.birth_method == 4)
-    return fail(AVGPU_EUNSUPPORTED, "BIRTH_METHOD 1 / 2 / 4 run on the batch world, not the serial world");
+  if (w.cfg.birth_method == 1 || w.cfg.birth_method == 2)
+    return fail(AVGPU_EUNSUPPORTED, "BIRTH_METHOD 1 / 2 run on the batch world, not the serial world");
   if ((int64_t)w.face.size() != w.ncells) w.face.assign(w.ncells, 0);
   SerialSched sch;
   sch.init(w.ncells);

@@ -11,10 +11,18 @@ KAT: one ancestor about to divide in an otherwise empty 9x9 grid; over many
 seeds its offspring lands in every part of the grid, a neighbour about as
 often as 8 of the 80 empty cells predict, never in the parent's cell.  World:
 a 32x32 grid grown from 12 mutants until it is full, GPU == oracle bit for
-bit under every PREFER_EMPTY / ALLOW_PARENT combination."""
+bit under every PREFER_EMPTY / ALLOW_PARENT combination.  The serial world
+(the reference's schedule) places soup births with FindRandEmptyCell on the
+reference's persistent empty-cell array (oracle serial_soup, interp.hip
+k_serial_update): GPU == oracle, and the batch world's growth is compared
+with it over many seeds (two-sample tests)."""
 import ctypes as C
+import multiprocessing
 import os
+import sys
+from concurrent.futures import ProcessPoolExecutor
 
+import numpy as np
 import pytest
 
 from avida_amd import capi, files
@@ -82,16 +90,13 @@ def test_soup_random_kat(golden):
 
 
 def test_soup_refused_where_unbuilt(golden):
-    """the serial world and strip tiles refuse BIRTH_METHOD 4 (a soup birth
-    may land in any strip; the serial world has no FindRandEmptyCell array);
-    BIRTH_METHOD 5 (FULL_SOUP_ELDEST) stays refused by the library"""
+    """strip tiles refuse BIRTH_METHOD 4 (a soup birth may land in any
+    strip); BIRTH_METHOD 5 (FULL_SOUP_ELDEST) stays refused by the library"""
     ov = dict(OV, WORLD_X=8, WORLD_Y=8, BIRTH_METHOD=4)
     iset, env, cfg = pu.load_env(golden, overrides=ov, seed=3)
     anc = files.read_org(os.path.join(golden, "default-heads.org"), iset)
     b = ol.Backend("oracle", cfg, iset, env, ncells=64)
     b.set_orgs(0, [anc] * 4, deterministic=False)
-    with pytest.raises(RuntimeError):
-        b.run_serial_update()
     with pytest.raises(RuntimeError):
         b._call("set_tile", b.h, C.c_int64(0), C.c_int64(1 << 20))
     b.close()
@@ -152,3 +157,82 @@ def test_soup_world_gpu(golden, prefer_empty, allow_parent):
     assert not bad, f"{len(bad)} mismatches: {bad[:5]}"
     nbad, cells = pu.compare_digests(orc.digests(), gpu.digests())
     assert nbad == 0, cells
+
+
+def _serial_pair(golden, prefer_empty, allow_parent, side=16, seed=29):
+    ov = {"WORLD_X": side, "WORLD_Y": side, "BIRTH_METHOD": 4, "PREFER_EMPTY": prefer_empty,
+          "ALLOW_PARENT": allow_parent}
+    iset, env, cfg = pu.load_env(golden, overrides=ov, seed=seed)
+    n = cfg.world_x * cfg.world_y
+    anc = files.read_org(os.path.join(golden, "default-heads.org"), iset)
+    g = pu.mutants_of(anc, iset, 6, rate=0.02, seed=7)
+    return iset, env, cfg, n, g
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("prefer_empty,allow_parent", [(1, 0), (1, 1), (0, 0), (0, 1)])
+def test_soup_serial_world_gpu(golden, prefer_empty, allow_parent):
+    """the serial world with soup births, 6 mutants on a 16x16 grid, 90
+    updates (it fills; then FindRandEmptyCell sees a full world): every
+    update's counters, then every cell and field, GPU == oracle"""
+    iset, env, cfg, n, g = _serial_pair(golden, prefer_empty, allow_parent)
+    orc = ol.Backend("oracle", cfg, iset, env, ncells=n)
+    gpu = ol.Backend("gpu", cfg, iset, env, ncells=n)
+    for b in (orc, gpu):
+        b.set_orgs(0, g, deterministic=False)
+    births = 0
+    for upd in range(90):
+        so, sg = orc.run_serial_update(), gpu.run_serial_update()
+        for f in ("num_organisms", "insts_executed", "births", "deaths", "divides", "births_dropped"):
+            assert getattr(so, f) == getattr(sg, f), (upd, f, getattr(so, f), getattr(sg, f))
+        births += so.births
+    assert births > 150
+    a, oa, fa = orc.states(0, n, CAP)
+    b, ob, fb = gpu.states(0, n, CAP)
+    bad = pu.diff_states(a, b, oa, ob, fa, fb, CAP)
+    assert not bad, f"{len(bad)} mismatches: {bad[:5]}"
+
+
+def _growth(args):
+    """organisms at updates 10, 20, ..., 100 of one seed (a worker process)"""
+    root, seed, serial = args
+    for p in (root, os.path.join(root, "tests")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    import oracle_lib as olw
+    import parity_util as puw
+    from avida_amd import files as fw
+    golden = os.path.join(root, "tests", "golden")
+    ov = {"WORLD_X": 32, "WORLD_Y": 32, "BIRTH_METHOD": 4, "PREFER_EMPTY": 1, "ALLOW_PARENT": 1}
+    iset, env, cfg = puw.load_env(golden, overrides=ov, seed=seed)
+    anc = fw.read_org(os.path.join(golden, "default-heads.org"), iset)
+    b = olw.Backend("oracle", cfg, iset, env, ncells=1024)
+    b.set_orgs(0, [anc] * 8, deterministic=False)
+    out = []
+    for u in range(100):
+        s = b.run_serial_update() if serial else b.run_update()
+        if u % 10 == 9:
+            out.append(s.num_organisms)
+    b.close()
+    return out
+
+
+def test_soup_batch_growth_matches_serial():
+    """8 ancestors on a 32x32 grid with soup births, 40 seeds per world: the
+    batch world's population at updates 50..100 against the serial world's
+    (the reference's schedule), Welch t and KS two-sample tests, Bonferroni at
+    a family-wise 0.01 (measured with 48 seeds: means within 0.3 sd of the
+    serial world's at every printed update)."""
+    from scipy import stats
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    seeds = range(1, 41)
+    with ProcessPoolExecutor(8, mp_context=multiprocessing.get_context("forkserver")) as ex:
+        ser = np.array(list(ex.map(_growth, [(root, s, True) for s in seeds])))
+        bat = np.array(list(ex.map(_growth, [(root, s + 1000, False) for s in seeds])))
+    cols = range(4, 10)                  # updates 50, 60, ..., 100
+    alpha = 0.01 / (2 * len(cols))
+    for k in cols:
+        pt = stats.ttest_ind(bat[:, k], ser[:, k], equal_var=False).pvalue
+        pk = stats.ks_2samp(bat[:, k], ser[:, k]).pvalue
+        assert pt > alpha and pk > alpha, (10 * (k + 1), bat[:, k].mean(), ser[:, k].mean(), pt, pk)
+    assert ser[:, -1].mean() > 300

@@ -295,9 +295,9 @@ std::string unsupported_cfg(const avgpu_cfg& c) {
   if (c.world_geometry != 1 && c.world_geometry != 2) return "WORLD_GEOMETRY other than 1 (grid) or 2 (torus)";
   if (c.slicing_method < 0 || c.slicing_method > 2) return "SLICING_METHOD other than 0, 1, 2";
   if (c.base_merit_method < 0 || c.base_merit_method > 5) return "BASE_MERIT_METHOD other than 0..5";
-  if (c.birth_method < 0 || c.birth_method > 4)
+  if (c.birth_method < 0 || c.birth_method > 5)
     return "BIRTH_METHOD other than 0 (random neighbour), 1 (oldest), 2 (highest age / merit), 3 (empty only), "
-           "4 (whole-world soup)";
+           "4 (whole-world soup), 5 (eldest, serial world)";
   if ((c.birth_method == 1 || c.birth_method == 2) && !c.prefer_empty)
     return "BIRTH_METHOD 1 / 2 without PREFER_EMPTY (the reference reads the organism of an empty cell)";
   if (c.death_method < 0 || c.death_method > 2) return "DEATH_METHOD other than 0, 1, 2";
@@ -776,6 +776,8 @@ int avgpu_update_totals(avgpu_world* w, double* dev_totals) {
 int avgpu_update_run(avgpu_world* w, const double* dev_totals, avgpu_update_stats* out) {
   int rc = ready(w);
   if (rc < 0) return rc;
+  if (w->cfg.birth_method == 5)
+    return fail(AVGPU_EUNSUPPORTED, "BIRTH_METHOD 5 (the reaper queue) runs on the serial world only");
   if (!dev_totals) return fail(AVGPU_EINVAL, "dev_totals is NULL");
   if (w->cfg.sub_updates > 1)
     return fail(AVGPU_EUNSUPPORTED, "sub_updates > 1 needs the world's own totals (no handed-in totals, no strips)");
@@ -801,6 +803,8 @@ int avgpu_update_run(avgpu_world* w, const double* dev_totals, avgpu_update_stat
 int avgpu_run_update(avgpu_world* w, avgpu_update_stats* out) {
   int rc = ready(w);
   if (rc < 0) return rc;
+  if (w->cfg.birth_method == 5)
+    return fail(AVGPU_EUNSUPPORTED, "BIRTH_METHOD 5 (the reaper queue) runs on the serial world only");
   if (w->use_global) {                 // totals handed in (avgpu_update_totals / tiles)
     w->use_global = false;
     return avgpu_update_run(w, w->d_totals, out);
@@ -841,6 +845,24 @@ static int serial_alloc(avgpu_world* w) {
   if ((rc = w->alloc(&W.face, (size_t)W.n)) < 0) return rc;
   if ((rc = w->alloc(&W.grng, 3)) < 0) return rc;
   if ((rc = w->alloc(&W.sctx, 3)) < 0) return rc;
+  if (w->cfg.birth_method == 5) {
+    // the reaper queue (oracle reaper_setup): Setup's cells 0..N-1, then the
+    // living cells in ascending order, each pushed at the front
+    const int64_t cap = 2 * W.n + 64;
+    if ((rc = w->alloc(&W.reaper, (size_t)cap)) < 0) return rc;
+    if ((rc = w->alloc(&W.reaper_ix, 2)) < 0) return rc;
+    W.reaper_cap = cap;
+    HIPCHK(hipStreamSynchronize(w->stream));
+    std::vector<uint32_t> ctl((size_t)W.n);
+    HIPCHK(hipMemcpy(ctl.data(), W.ctl, (size_t)W.n * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    std::vector<int32_t> q((size_t)cap, 0);
+    int64_t f = cap;
+    for (int64_t c = 0; c < W.n; c++) q[(size_t)(f++ % cap)] = (int32_t)c;
+    for (int64_t c = 0; c < W.n; c++) if (ctl[(size_t)c] & CTL_ALIVE) q[(size_t)(f++ % cap)] = (int32_t)c;
+    const int64_t ix[2] = {cap, f};
+    HIPCHK(hipMemcpy(W.reaper, q.data(), (size_t)cap * sizeof(int32_t), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(W.reaper_ix, ix, sizeof(ix), hipMemcpyHostToDevice));
+  }
   uint32_t g[3] = {0, 0, 0}, x[3] = {0, 0, 0};
   const uint64_t seed = (uint64_t)w->cfg.seed;
   derive_key((uint32_t)seed, (uint32_t)(seed >> 32), 0x5CEDu, 0xC0FFEEu, g[0], g[1]);
@@ -1365,8 +1387,8 @@ int avgpu_set_tile(avgpu_world* w, int64_t row0, int64_t arena_bytes) {
   if (w && w->cfg.sub_updates > 1) return fail(AVGPU_EUNSUPPORTED, "sub_updates > 1 on strip tiles");
   if (w && (w->cfg.birth_method == 1 || w->cfg.birth_method == 2))
     return fail(AVGPU_EUNSUPPORTED, "BIRTH_METHOD 1 / 2 on strip tiles (the ghost rows carry no age or merit)");
-  if (w && w->cfg.birth_method == 4)
-    return fail(AVGPU_EUNSUPPORTED, "BIRTH_METHOD 4 on strip tiles (a soup birth may land in any strip)");
+  if (w && (w->cfg.birth_method == 4 || w->cfg.birth_method == 5))
+    return fail(AVGPU_EUNSUPPORTED, "BIRTH_METHOD 4 / 5 on strip tiles (a soup birth may land in any strip)");
   if (!w) return fail(AVGPU_EINVAL, "NULL world");
   DevWorld& W = w->W;
   const int64_t X = W.world_x;

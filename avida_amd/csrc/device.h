@@ -320,6 +320,9 @@ struct DevWorld {
   int32_t* e_list;    // BIRTH_METHOD 4 + PREFER_EMPTY: the cells empty at placement start, ascending
   int32_t* e_blk;     // its per-256-cell counts, then their exclusive offsets (e_blk[nb]: the total)
   int32_t* soup_perm; // serial world, BIRTH_METHOD 4: the reference's empty_cell_id_array (0..N-1 at creation)
+  int32_t* reaper;    // serial world, BIRTH_METHOD 5: the reaper queue, a ring of reaper_cap cells
+  int64_t* reaper_ix; // [0] its rear (oldest) position, [1] one past its front (newest)
+  int64_t reaper_cap;
 };
 
 // owner of a cell won by a neighbouring strip's offspring in round k at birth time t

@@ -2215,6 +2215,18 @@ __global__ __launch_bounds__(64, 1) void k_serial_update(const DevWorld* __restr
             t = (int)sctx_below(W, ct, n, ov);
             while (!W.allow_parent && n > 1u && t == (int)c) t = (int)sctx_below(W, ct, n, ov);
           }
+        } else if (W.birth_method == 5) {
+          // FULL_SOUP_ELDEST (oracle serial_eldest): the reaper queue's rear
+          // cell; the parent's, without ALLOW_PARENT, goes back to the rear
+          const int64_t C = W.reaper_cap;
+          int64_t R = W.reaper_ix[0];
+          t = W.reaper[R % C];
+          R++;
+          if (!W.allow_parent && t == (int)c && R < W.reaper_ix[1]) {
+            t = W.reaper[R % C];                                  // PopRear, then PushRear(parent)
+            W.reaper[R % C] = (int)c;                             // into the slot it freed
+          }
+          W.reaper_ix[0] = R;
         } else {
           // PositionOffspring on the rotated connection list (oracle serial_target)
           int base[8], conn[8], found[9];
@@ -2263,6 +2275,11 @@ __global__ __launch_bounds__(64, 1) void k_serial_update(const DevWorld* __restr
         if (lane == 0) {
           W.spec[t] = 0;                                         // InsertOrganism resets the credit
           if (parent_alive && face_t >= 0) W.face[t] = (uint8_t)face_t;
+          if (W.birth_method == 5) {                             // ActivateOrganism: Push(target) (:1358-1361)
+            const int64_t F = W.reaper_ix[1];
+            W.reaper[F % W.reaper_cap] = t;
+            W.reaper_ix[1] = F + 1;
+          }
         }
         __threadfence_block();
         stree_set(tree, size, t, b.merit);

@@ -30,6 +30,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <string>
+#include <deque>
 #include <vector>
 
 namespace {
@@ -270,6 +271,8 @@ struct World {
   std::vector<double> srec_sched, srec_ctx;   // their recorded values (avgpu_set_serial_streams)
   std::vector<uint8_t> face;   // serial world: each cell's connection-list rotation (cPopulationCell::Rotate)
   std::vector<int64_t> soup_cells;   // serial world, BIRTH_METHOD 4: cPopulation::empty_cell_id_array
+  std::deque<int64_t> reaper;        // serial world, BIRTH_METHOD 5: cPopulation::reaper_queue (front: newest)
+  bool reaper_init = false;
   // strip tiles (avgpu_set_tile): rows [row0, row0+rows) of a world_x x
   // global_rows world; occ / claim / owner carry two ghost rows after n
   int64_t row0 = 0, rows = 0, global_rows = 0, cell0 = 0;
@@ -2300,6 +2303,8 @@ static inline int64_t sub_share(int64_t n, int s, int K) {
 // Batch-synchronous world update: the exact semantics the device implements
 // (DESIGN.md "Update semantics"): allot -> interpret -> place births -> stats.
 static int run_update_impl(World& w) {
+  if (w.cfg.birth_method == 5)
+    return fail(AVGPU_EUNSUPPORTED, "BIRTH_METHOD 5 (the reaper queue) runs on the serial world only");
   const int K = sub_updates_of(w.cfg);
   if (K > 1 && w.have_global)
     return fail(AVGPU_EUNSUPPORTED, "sub_updates > 1 needs the world's own totals (no handed-in totals, no strips)");
@@ -2426,8 +2431,8 @@ int orc_set_tile(void* h, int64_t row0, int64_t arena) {
   World& w = *(World*)h;
   if (w.cfg.birth_method == 1 || w.cfg.birth_method == 2)
     return fail(AVGPU_EUNSUPPORTED, "BIRTH_METHOD 1 / 2 on strip tiles (the ghost rows carry no age or merit)");
-  if (w.cfg.birth_method == 4)
-    return fail(AVGPU_EUNSUPPORTED, "BIRTH_METHOD 4 on strip tiles (a soup birth may land in any strip)");
+  if (w.cfg.birth_method == 4 || w.cfg.birth_method == 5)
+    return fail(AVGPU_EUNSUPPORTED, "BIRTH_METHOD 4 / 5 on strip tiles (a soup birth may land in any strip)");
   const int64_t X = w.cfg.world_x;
   if (X <= 0 || w.ncells % X) return fail(AVGPU_EINVAL, "tile cells must be whole rows of WORLD_X");
   const int64_t rows = w.ncells / X;
@@ -2856,8 +2861,35 @@ static int64_t serial_soup(World& w, int64_t parent) {
   return c;
 }
 
+// BIRTH_METHOD 5 in the serial world: FULL_SOUP_ELDEST (main/cPopulation.cc:
+// 5312-5319) -- the cell of the reaper queue's rear entry (PopRear; the
+// parent's, without ALLOW_PARENT, is pushed back to the rear and the next one
+// taken); ActivateOrganism pushes every newborn's cell at the front (:1358-
+// 1361).  Deaths leave the queue alone, so a cell may be in it more than once.
+// The queue is the reference's Setup order (cells 0..N-1 pushed, :343-347)
+// followed by the living cells in ascending order (their injections, each
+// an ActivateOrganism), built at the first serial update.
+static void reaper_setup(World& w) {
+  if (w.reaper_init) return;
+  w.reaper_init = true;
+  w.reaper.clear();
+  for (int64_t c = 0; c < w.ncells; c++) w.reaper.push_front(c);
+  for (int64_t c = 0; c < w.ncells; c++) if (w.orgs[c].alive) w.reaper.push_front(c);
+}
+static int64_t serial_eldest(World& w, int64_t parent) {
+  int64_t c = w.reaper.back();
+  w.reaper.pop_back();
+  if (!w.cfg.allow_parent && c == parent && !w.reaper.empty()) {
+    c = w.reaper.back();
+    w.reaper.pop_back();
+    w.reaper.push_back(parent);
+  }
+  return c;
+}
+
 static int64_t serial_target(World& w, int64_t parent) {
   if (w.cfg.birth_method == 4) return serial_soup(w, parent);
+  if (w.cfg.birth_method == 5) return serial_eldest(w, parent);
   int64_t base[8], conn[8], found[9];
   const int nb = conn_base(w, parent, base);
   const int f = nb ? w.face[parent] % nb : 0;
@@ -2887,6 +2919,7 @@ static int serial_place(World& w, SerialSched& sch, Birth& b) {
   if (parent_alive) sch.set(b.parent, w.orgs[b.parent].merit);   // AdjustSchedule(parent) :933
   const int killed = w.orgs[t].alive ? 1 : 0;
   activate_child(w, b, t, &w.ctx_rng);
+  if (w.cfg.birth_method == 5) w.reaper.push_front(t);   // ActivateOrganism (:1358-1361)
   w.orgs[t].spec_count = 0;                               // InsertOrganism (main/cPopulationCell.cc:270-271)
   w.orgs[t].spec_die = false;
   sch.set(t, w.orgs[t].merit);
@@ -2935,6 +2968,7 @@ int orc_run_serial_updates(void* h, int n_updates, avgpu_update_stats* out) {
   if (w.cfg.birth_method == 1 || w.cfg.birth_method == 2)
     return fail(AVGPU_EUNSUPPORTED, "BIRTH_METHOD 1 / 2 run on the batch world, not the serial world");
   if ((int64_t)w.face.size() != w.ncells) w.face.assign(w.ncells, 0);
+  if (w.cfg.birth_method == 5) reaper_setup(w);
   SerialSched sch;
   sch.init(w.ncells);
   for (int64_t c = 0; c < w.ncells; c++) sch.set(c, w.orgs[c].alive ? w.orgs[c].merit : 0.0);

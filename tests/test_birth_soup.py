@@ -91,7 +91,7 @@ def test_soup_random_kat(golden):
 
 def test_soup_refused_where_unbuilt(golden):
     """strip tiles refuse BIRTH_METHOD 4 (a soup birth may land in any
-    strip); BIRTH_METHOD 5 (FULL_SOUP_ELDEST) stays refused by the library"""
+    strip); the library refuses BIRTH_METHOD 6 and beyond"""
     ov = dict(OV, WORLD_X=8, WORLD_Y=8, BIRTH_METHOD=4)
     iset, env, cfg = pu.load_env(golden, overrides=ov, seed=3)
     anc = files.read_org(os.path.join(golden, "default-heads.org"), iset)
@@ -103,7 +103,7 @@ def test_soup_refused_where_unbuilt(golden):
     lib = capi.load_product()
     c = capi.cfg_from_avida(files.read_avida_cfg(None, {"BIRTH_METHOD": 4}))
     assert lib.avgpu_check_cfg(C.byref(c)) == 0
-    c = capi.cfg_from_avida(files.read_avida_cfg(None, {"BIRTH_METHOD": 5}))
+    c = capi.cfg_from_avida(files.read_avida_cfg(None, {"BIRTH_METHOD": 6}))
     assert lib.avgpu_check_cfg(C.byref(c)) == -5
 
 

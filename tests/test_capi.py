@@ -83,7 +83,7 @@ REFUSED_C = [
     ("require_exact_copy", "1"), ("fitness_method", "1"), ("juv_period", "5"),
     ("no_mut_insts_len", "1"), ("test_fitness_measures", "1"),
     ("divide_method", "0"), ("world_geometry", "3"), ("slicing_method", "3"),
-    ("base_merit_method", "6"), ("birth_method", "5"), ("death_method", "3"), ("alloc_method", "1"),
+    ("base_merit_method", "6"), ("birth_method", "6"), ("death_method", "3"), ("alloc_method", "1"),
     ("sub_updates", "65"),
 ]
 

@@ -154,7 +154,8 @@ class AvgpuUpdateStats(C.Structure):
         ("ave_generation", C.c_double), ("sum_mem_size", C.c_double),
         ("cum_insts_executed", C.c_int64), ("cum_births", C.c_int64), ("slices", C.c_int64),
         ("lane_steps", C.c_int64), ("births_overwritten", C.c_int64), ("births_cancelled", C.c_int64),
-        ("seed", C.c_uint64),
+        ("seed", C.c_uint64), ("sched_pred", C.c_int64), ("sched_pred_n", C.c_int64), ("sub_steps", C.c_int64),
+        ("sched_carry", C.c_int64), ("insts_wasted", C.c_int64),
     ]
 
 
@@ -184,7 +185,7 @@ EXPORTED = [
     "avgpu_update_run", "avgpu_set_stream", "avgpu_get_states", "avgpu_get_census", "avgpu_set_genotype_keys",
     "avgpu_test_genomes", "avgpu_get_stats", "avgpu_stats_vector", "avgpu_set_global_totals",
     "avgpu_set_tile", "avgpu_tile_buffer_bytes", "avgpu_set_tile_buffers", "avgpu_tile_partials",
-    "avgpu_tile_begin", "avgpu_tile_place", "avgpu_tile_finish", "avgpu_tile_res_bytes",
+    "avgpu_tile_begin", "avgpu_tile_steps", "avgpu_tile_begin_step", "avgpu_tile_place", "avgpu_tile_finish", "avgpu_tile_res_bytes",
     "avgpu_set_tile_res_buffers", "avgpu_tile_res_cons", "avgpu_tile_res_settle",
     "avgpu_last_step_insts", "avgpu_last_kernel_ms", "avgpu_kernel_times", "avgpu_counters",
     "avgpu_state_digests", "avgpu_set_rng_mode", "avgpu_run_serial_updates", "avgpu_set_serial_streams",
@@ -364,6 +365,8 @@ def bind_common(lib, prefix):
         "set_tile_buffers": (C.c_int, [V] + [V] * 8),
         "tile_partials": (C.c_int, [V, V]),
         "tile_begin": (C.c_int, [V, V, C.c_int]),
+        "tile_steps": (C.c_int, [V, V, C.c_int, C.POINTER(C.c_int)]),
+        "tile_begin_step": (C.c_int, [V, V, C.c_int, C.c_int, C.c_int]),
         "tile_place": (C.c_int, [V, C.c_int, C.c_int]),
         "tile_finish": (C.c_int, [V, C.POINTER(AvgpuUpdateStats)]),
         "tile_res_bytes": (C.c_int, [V, C.POINTER(I64)]),

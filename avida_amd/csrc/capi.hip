@@ -81,6 +81,17 @@ struct avgpu_world {
   // strip tiles
   int ntiles_last = 0;
   bool tile_buffers = false;
+  // batch steps: the last update's predictor and organisms
+  // (mapped host memory the update's last step writes, ev_pred after it), the
+  // host's copy, the steps the last update ran; strips: the current step
+  long long* h_pred = nullptr;
+  long long* d_pred = nullptr;   // its device address
+  hipEvent_t ev_pred = nullptr;
+  bool pred_pending = false;
+  long long pred_acc = 0, pred_n = 0;
+  int last_k = 1;
+  int tile_sub = 0, tile_k = 1, tile_sub_next = 0;
+  uint32_t tile_key = 0;
 
   template <typename T>
   int alloc(T** p, size_t count) {
@@ -161,7 +172,7 @@ int setup_world(avgpu_world* w, int64_t n, bool test_buffers) {
   // occupancy, owners and the four placement rounds' claims, each with the two
   // ghost rows a strip tile keeps after its n cells
   const int64_t ng = n + 2 * (int64_t)c.world_x;
-  A(occ, ng); A(claim, ng); A(claim2, ng); A(owner, ng); A(killt, n); A(sdone, n);
+  A(occ, ng); A(claim, ng); A(claim2, ng); A(owner, ng); A(killt, n); A(sdone, n); A(ran, n); A(sched, 4);
   W.claim_r[0] = W.claim; W.claim_r[1] = W.claim2;
   A(claim_r[2], ng); A(claim_r[3], ng); A(b_tgt, 4 * R);
   if (c.birth_method == 4) {
@@ -185,6 +196,7 @@ int setup_world(avgpu_world* w, int64_t n, bool test_buffers) {
   if ((rc = w->alloc(&w->d_W, 1))) return rc;
   const int64_t nb = (n + 255) / 256;
   if ((rc = w->alloc(&w->d_totals, (size_t)(8 + 2 * nb)))) return rc;
+  W.totals = w->d_totals;
   // the scheduler's tree: block counts, the top tree's levels (a strip tile
   // regrows them for the whole world at avgpu_tile_begin)
   if ((rc = w->alloc(&W.blk_count, (size_t)nb))) return rc;
@@ -357,9 +369,13 @@ avgpu_world* create_world(const avgpu_cfg* cfg, int device, int64_t n, bool test
       hipEventCreateWithFlags(&w->ev_join[0], hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&w->ev_join[1], hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&w->ev_join[2], hipEventDisableTiming) != hipSuccess ||
-      hipEventCreate(&w->ev0) != hipSuccess || hipEventCreate(&w->ev1) != hipSuccess) {
+      hipEventCreate(&w->ev0) != hipSuccess || hipEventCreate(&w->ev1) != hipSuccess ||
+      hipEventCreateWithFlags(&w->ev_pred, hipEventDisableTiming) != hipSuccess ||
+      hipHostMalloc((void**)&w->h_pred, 2 * sizeof(long long), hipHostMallocMapped) != hipSuccess ||
+      hipHostGetDevicePointer((void**)&w->d_pred, w->h_pred, 0) != hipSuccess) {
     delete w; fail(AVGPU_EHIP, "stream/event creation failed"); return nullptr;
   }
+  w->h_pred[0] = w->h_pred[1] = 0;
   w->stream = w->own_stream;
   for (int i = 0; i < avgpu_world::RING; i++) {
     for (int k = 0; k <= NUM_CLASSES; k++)
@@ -511,6 +527,20 @@ int interpret(avgpu_world* w, int mode, int64_t first, int64_t count, bool sorte
 
 int update_run(avgpu_world* w, const double* dev_totals, avgpu_update_stats* out);
 
+// An update's batch steps (oracle choose_k): avgpu_cfg.sub_updates
+// when set; else, with E the last step's predictor in mean weights per
+// organism (the total weight's expected move within the update), one step for
+// E <= 0.1 and ceil(E / 0.05) steps (2 .. ADAPT_KMAX) above.
+constexpr int ADAPT_KMAX = 16;
+int choose_k(const avgpu_cfg& c, long long pred, long long n, bool handed_in) {
+  if (c.sub_updates > 0) return c.sub_updates;
+  if (handed_in || c.slicing_method != AVGPU_SLICE_PROBABILISTIC) return 1;
+  const double a = (double)(pred < 0 ? -pred : pred);
+  if (!(n > 0 && a > 104857.6 * (double)n)) return 1;
+  const int k = (int)std::ceil(a / (52428.8 * (double)n));
+  return std::max(2, std::min(k, ADAPT_KMAX));
+}
+
 }  // namespace
 
 // ===========================================================================
@@ -566,6 +596,8 @@ int avgpu_destroy(avgpu_world* w) {
     if (w->ev_join[k]) hipEventDestroy(w->ev_join[k]);
   }
   if (w->ev_fork) hipEventDestroy(w->ev_fork);
+  if (w->ev_pred) hipEventDestroy(w->ev_pred);
+  if (w->h_pred) hipHostFree(w->h_pred);
   delete w;
   return 0;
 }
@@ -780,20 +812,25 @@ int avgpu_update_run(avgpu_world* w, const double* dev_totals, avgpu_update_stat
     return fail(AVGPU_EUNSUPPORTED, "BIRTH_METHOD 5 (the reaper queue) runs on the serial world only");
   if (!dev_totals) return fail(AVGPU_EINVAL, "dev_totals is NULL");
   if (w->cfg.sub_updates > 1)
-    return fail(AVGPU_EUNSUPPORTED, "sub_updates > 1 needs the world's own totals (no handed-in totals, no strips)");
+    return fail(AVGPU_EUNSUPPORTED, "sub_updates > 1 needs the world's own totals (no handed-in totals)");
   // every world's {total weight, organisms} -> this world's share of the
-  // picks (cMultiProcessWorld::CalculateUpdateSize) and its allotment
+  // picks (cMultiProcessWorld::CalculateUpdateSize) and its allotment; one
+  // batch step (choose_k: handed-in totals)
   if (dev_totals != w->d_totals)
     HIPCHK(hipMemcpyAsync(w->d_totals, dev_totals, 2 * sizeof(double), hipMemcpyDeviceToDevice, w->stream));
+  w->pred_pending = false;
   launch_world_pre(w->W, w->stream, w->d_totals, w->d_totals + 8, w->ev_fork, (uint32_t)w->update);
   after_resources_begin(w);
   HIPCHK(hipGetLastError());
   rc = interpret(w, AVGPU_MODE_WORLD, 0, w->W.n, true);
   if (rc < 0) return rc;
+  launch_world_post(w->W, w->stream, (uint32_t)w->update, 0, 1);
+  launch_newborns(w->W, w->d_W, w->stream);
   // statistics only when asked for: a run without them (out == NULL) leaves
   // the reduction to avgpu_get_stats / avgpu_stats_vector, or skips it
-  launch_world_post(w->W, w->stream, w->d_stats, out != nullptr);
+  launch_world_end(w->W, w->stream, w->d_stats, out != nullptr);
   HIPCHK(hipGetLastError());
+  w->last_k = 1;
   w->stats_stale = out == nullptr;
   w->update++;
   if (out) return avgpu_get_stats(w, out);
@@ -809,21 +846,36 @@ int avgpu_run_update(avgpu_world* w, avgpu_update_stats* out) {
     w->use_global = false;
     return avgpu_update_run(w, w->d_totals, out);
   }
-  // K sub-updates (avgpu_cfg.sub_updates), each: total merit,
-  // allotment, class lists and the class-0 order; interpretation; placement
-  const int K = w->cfg.sub_updates > 1 ? w->cfg.sub_updates : 1;
+  // K batch steps (choose_k: avgpu_cfg.sub_updates, or the
+  // last update's predictor), each: total merit, allotment, class lists and
+  // the class-0 order; interpretation; placement; the newborn pass.  The
+  // predictor comes back by mapped memory from the last step's placement:
+  // the host waits for it (here, at the next update) while the GPU runs the
+  // rest of that update.
+  if (w->pred_pending) {
+    HIPCHK(hipEventSynchronize(w->ev_pred));
+    w->pred_acc = w->h_pred[0];
+    w->pred_n = w->h_pred[1];
+    w->pred_pending = false;
+  }
+  const int K = choose_k(w->cfg, w->pred_acc, w->pred_n, false);
   for (int sub = 0; sub < K; sub++) {
-    launch_world_begin(w->W, w->stream, w->d_totals, w->d_totals + 8, w->ev_fork,
-                       (uint32_t)w->update * (uint32_t)K + (uint32_t)sub, sub, K);
+    const uint32_t key = (uint32_t)w->update * (uint32_t)K + (uint32_t)sub;
+    launch_world_begin(w->W, w->stream, w->d_totals, w->d_totals + 8, w->ev_fork, key, sub, K);
     if (sub == 0) after_resources_begin(w);
     HIPCHK(hipGetLastError());
     rc = interpret(w, AVGPU_MODE_WORLD, 0, w->W.n, true);
     if (rc < 0) return rc;
+    const bool last = sub == K - 1;
+    launch_world_post(w->W, w->stream, key, sub, K, last ? w->d_pred : nullptr, last ? w->ev_pred : nullptr);
+    launch_newborns(w->W, w->d_W, w->stream);
     // statistics only when asked for: a run without them (out == NULL) leaves
     // the reduction to avgpu_get_stats / avgpu_stats_vector, or skips it
-    launch_world_post(w->W, w->stream, w->d_stats, out != nullptr && sub == K - 1);
+    launch_world_end(w->W, w->stream, w->d_stats, out != nullptr && last);
     HIPCHK(hipGetLastError());
   }
+  w->pred_pending = true;
+  w->last_k = K;
   w->stats_stale = out == nullptr;
   w->update++;
   if (out) return avgpu_get_stats(w, out);
@@ -969,6 +1021,11 @@ int avgpu_get_stats(avgpu_world* w, avgpu_update_stats* out) {
   out->births_overwritten = (int64_t)v[34];
   out->births_cancelled = (int64_t)v[35];
   out->seed = w->cfg.seed;
+  out->insts_wasted = (int64_t)v[36];
+  memcpy(&out->sched_pred, v + 37, 8);        // (int64 bits)
+  memcpy(&out->sched_carry, v + 38, 8);
+  out->sched_pred_n = (int64_t)v[39];
+  out->sub_steps = w->last_k;
   return 0;
 }
 
@@ -1136,6 +1193,15 @@ int avgpu_set_clock(avgpu_world* w, const avgpu_update_stats* last) {
     w->W.seed_lo = (uint32_t)last->seed;
     w->W.seed_hi = (uint32_t)(last->seed >> 32);
   }
+  // the batch-step predictor and the pick carry
+  w->pred_acc = last->sched_pred;
+  w->pred_n = last->sched_pred_n;
+  w->pred_pending = false;
+  const long long sv[3] = {last->sched_pred, 0, last->sched_carry};
+  HIPCHK(hipMemcpyAsync(w->W.sched, sv, sizeof(sv), hipMemcpyHostToDevice, w->stream));
+  const double nv = (double)last->sched_pred_n;
+  HIPCHK(hipMemcpyAsync(w->d_totals + 1, &nv, sizeof(nv), hipMemcpyHostToDevice, w->stream));
+  HIPCHK(hipStreamSynchronize(w->stream));
   return 0;
 }
 
@@ -1323,6 +1389,11 @@ int avgpu_load_resources(avgpu_world* w, int nres, const avgpu_resource* res, in
     HIPCHK(hipMalloc(&W.res_delta, (size_t)n * sizeof(double)));
     w->allocs.push_back(W.res_delta);
   }
+  if (nres && !W.cons) {   // each cell's consumption in a step (newborn credit)
+    HIPCHK(hipMalloc(&W.cons, (size_t)AVGPU_MAX_RESOURCES * n * sizeof(double)));
+    w->allocs.push_back(W.cons);
+    HIPCHK(hipMemsetAsync(W.cons, 0, (size_t)AVGPU_MAX_RESOURCES * n * sizeof(double), w->stream));
+  }
   if (ncell) {
     if (W.res_cells) hipFree(W.res_cells);
     HIPCHK(hipMalloc(&W.res_cells, ncell * sizeof(avgpu_cell_resource)));
@@ -1384,7 +1455,6 @@ int avgpu_get_resources(avgpu_world* w, double* levels, double* spatial) {
 
 // ---- strip tiles (DESIGN.md "Multi-GPU") ----
 int avgpu_set_tile(avgpu_world* w, int64_t row0, int64_t arena_bytes) {
-  if (w && w->cfg.sub_updates > 1) return fail(AVGPU_EUNSUPPORTED, "sub_updates > 1 on strip tiles");
   if (w && (w->cfg.birth_method == 1 || w->cfg.birth_method == 2))
     return fail(AVGPU_EUNSUPPORTED, "BIRTH_METHOD 1 / 2 on strip tiles (the ghost rows carry no age or merit)");
   if (w && (w->cfg.birth_method == 4 || w->cfg.birth_method == 5))
@@ -1451,7 +1521,7 @@ int avgpu_tile_res_settle(avgpu_world* w, const uint64_t* dev_sum) {
 
 int avgpu_tile_buffer_bytes(avgpu_world* w, int64_t* partial_bytes, int64_t* halo_b, int64_t* record_b) {
   if (!w) return fail(AVGPU_EINVAL, "NULL world");
-  if (partial_bytes) *partial_bytes = 2 * ((w->W.n + 255) / 256) * (int64_t)sizeof(double);
+  if (partial_bytes) *partial_bytes = tile_part_stride((w->W.n + 255) / 256) * (int64_t)sizeof(double);
   if (halo_b) *halo_b = halo_bytes(w->W.world_x);
   if (record_b) *record_b = record_bytes(w->W.world_x, w->W.r_arena);
   return 0;
@@ -1486,18 +1556,47 @@ int avgpu_tile_partials(avgpu_world* w, double* dev_out) {
   int rc = ready(w);
   if (rc < 0) return rc;
   if (!dev_out) return fail(AVGPU_EINVAL, "dev_out is NULL");
-  launch_tile_partials(w->W, w->stream, dev_out);
+  // a strip's first step of an update clears the update's counters, a later
+  // step its queues only (the counts add up over the update)
+  launch_tile_partials(w->W, w->stream, dev_out, w->W.tiled ? (w->tile_sub_next == 0 ? 1 : 2) : 0);
   if (w->W.tiled) launch_resources_pack(w->W, w->stream);
   HIPCHK(hipGetLastError());
   return 0;
 }
 
-int avgpu_tile_begin(avgpu_world* w, const double* dev_gathered, int ntiles) {
+// the update's batch steps from every strip's predictor (the gathered
+// partials' tails) and the organisms of the last step (the same on every strip)
+int avgpu_tile_steps(avgpu_world* w, const double* dev_gathered, int ntiles, int* k_out) {
+  int rc = tile_ready(w);
+  if (rc < 0) return rc;
+  if (!dev_gathered || ntiles < 1 || !k_out) return fail(AVGPU_EINVAL, "gathered partials / k_out");
+  const int64_t nb = (w->W.n + 255) / 256, stride = tile_part_stride(nb);
+  std::vector<double> tail((size_t)(2 * ntiles));
+  for (int k = 0; k < ntiles; k++)
+    HIPCHK(hipMemcpyAsync(tail.data() + 2 * k, dev_gathered + k * stride + 2 * nb, 2 * sizeof(double),
+                          hipMemcpyDeviceToHost, w->stream));
+  double n = 0.0;
+  HIPCHK(hipMemcpyAsync(&n, w->d_totals + 1, sizeof(double), hipMemcpyDeviceToHost, w->stream));
+  HIPCHK(hipStreamSynchronize(w->stream));
+  long long sum = 0;
+  for (int k = 0; k < ntiles; k++) {
+    long long v;
+    memcpy(&v, tail.data() + 2 * k, 8);
+    sum += v;
+  }
+  *k_out = choose_k(w->cfg, sum, (long long)n, false);
+  return 0;
+}
+
+int avgpu_tile_begin_step(avgpu_world* w, const double* dev_gathered, int ntiles, int sub, int K) {
   int rc = tile_ready(w);
   if (rc < 0) return rc;
   if (w->W.n_spatial && !w->W.rs_recv[0])
     return fail(AVGPU_ESTATE, "spatial resources need avgpu_set_tile_res_buffers");
   if (!dev_gathered || ntiles < 1) return fail(AVGPU_EINVAL, "gathered partials");
+  if (K < 1 || K > 64 || sub < 0 || sub >= K) return fail(AVGPU_EINVAL, "batch step sub of K");
+  if (K > 1 && w->cfg.slicing_method != AVGPU_SLICE_PROBABILISTIC)
+    return fail(AVGPU_EUNSUPPORTED, "batch steps > 1 need SLICING_METHOD 1");
   // the scheduler's top tree spans every strip's blocks
   {
     int64_t P = 1;
@@ -1511,16 +1610,23 @@ int avgpu_tile_begin(avgpu_world* w, const double* dev_gathered, int ntiles) {
       if (prc < 0) return prc;
     }
   }
-  // (the counters were cleared by avgpu_tile_partials' launch)
-  launch_tile_pre(w->W, w->stream, dev_gathered, ntiles, w->d_totals, w->ev_fork, (uint32_t)w->update);
-  after_resources_begin(w);
+  // (the counters were cleared by avgpu_tile_partials' launch at step 0)
+  const uint32_t key = (uint32_t)w->update * (uint32_t)K + (uint32_t)sub;
+  launch_tile_pre(w->W, w->stream, dev_gathered, ntiles, w->d_totals, w->ev_fork, key, sub, K);
+  if (sub == 0) after_resources_begin(w);
   HIPCHK(hipGetLastError());
   rc = interpret(w, AVGPU_MODE_WORLD, 0, w->W.n, true);
   if (rc < 0) return rc;
   launch_tile_after_interpret(w->W, w->stream);
   HIPCHK(hipGetLastError());
   w->ntiles_last = ntiles;
+  w->tile_sub = sub; w->tile_k = K; w->tile_key = key;
+  w->tile_sub_next = sub + 1 < K ? sub + 1 : 0;
   return 0;
+}
+
+int avgpu_tile_begin(avgpu_world* w, const double* dev_gathered, int ntiles) {
+  return avgpu_tile_begin_step(w, dev_gathered, ntiles, 0, 1);
 }
 
 int avgpu_tile_place(avgpu_world* w, int round, int phase) {
@@ -1529,7 +1635,7 @@ int avgpu_tile_place(avgpu_world* w, int round, int phase) {
   if (round < 0 || round > 3 || phase < 0 || phase > 3 || (phase >= 1 && phase <= 2 && round != 3) ||
       (phase == 3 && round != 0))
     return fail(AVGPU_EINVAL, "round 0..3 with phase 0, round 0 with phase 3; phases 1, 2 after round 3");
-  launch_tile_place(w->W, w->stream, round, phase);
+  launch_tile_place(w->W, w->stream, round, phase, w->tile_key, w->tile_sub, w->tile_k);
   HIPCHK(hipGetLastError());
   return 0;
 }
@@ -1537,9 +1643,16 @@ int avgpu_tile_place(avgpu_world* w, int round, int phase) {
 int avgpu_tile_finish(avgpu_world* w, avgpu_update_stats* out) {
   int rc = tile_ready(w);
   if (rc < 0) return rc;
-  launch_tile_finish(w->W, w->stream, w->d_stats, out != nullptr);
+  // the received offspring, the step's newborn pass; after the update's last
+  // step its statistics
+  launch_tile_finish(w->W, w->stream, w->tile_key, w->tile_sub, w->tile_k);
+  launch_newborns(w->W, w->d_W, w->stream);
+  HIPCHK(hipGetLastError());
+  if (w->tile_sub + 1 < w->tile_k) return 0;
+  if (out) launch_stats(w->W, w->stream, w->d_stats);
   HIPCHK(hipGetLastError());
   w->stats_stale = out == nullptr;
+  w->last_k = w->tile_k;
   w->update++;
   if (out) return avgpu_get_stats(w, out);
   return 0;

@@ -323,8 +323,19 @@ struct DevWorld {
   int32_t* reaper;    // serial world, BIRTH_METHOD 5: the reaper queue, a ring of reaper_cap cells
   int64_t* reaper_ix; // [0] its rear (oldest) position, [1] one past its front (newest)
   int64_t reaper_cap;
+  // the batch step's newborns and sub-steps:
+  int32_t* ran;       // [n] instructions each cell's organism ran in this step's main pass (k_allot zeroes)
+  double* cons;       // [n_res][n] its depletable consumption in that pass (k_allot zeroes; env_resources)
+  // [0] the sub-step predictor of this step's main pass (2^-20 mean weights,
+  // k_block_counts zeroes it), [1] this step's pick carry (newborn picks beyond
+  // their victims' leftovers, k_activate), [2] the carry not yet taken
+  long long* sched;
+  const double* totals;   // the step's totals (k_block_counts): [1] organisms, [2] weight total, [3] UD
 };
 
+// a strip's partials vector (avgpu_tile_partials): nb block partials, nb alive
+// counts, its sub-step predictor and its pick carry (int64 bits)
+__host__ __device__ inline int64_t tile_part_stride(int64_t nb) { return 2 * nb + 2; }
 // owner of a cell won by a neighbouring strip's offspring in round k at birth time t
 #define REMOTE_OWNER(k, t) (-2 - ((k) + 4 * (int)(t)))
 // halo buffer: per round parity X u64 claims on the receiver's edge row and X
@@ -387,6 +398,7 @@ enum { SEG_OSLIP = 0, SEG_PSLIP, SEG_SSLIP, SEG_TTRANS, SEG_PTRANS, SEG_STRANS, 
 #define CNT_OVERWRITTEN 24  /* offspring placed, then killed by a later birth into the same cell this update */
 #define CNT_CANCELLED 25  /* records whose parent's cell got an offspring before their divide (never placed) */
 #define CNT_BAD_RECORD 26 /* record / cell fields out of range where used as an index (guarded; must be 0) */
+#define CNT_WASTED 27     /* instructions replaced organisms ran after their newborns' birth times */
 // 32..37: AVGPU_PHASE_CLOCKS loop cycles by block (decode, fast, copy, switch,
 // wave phase, advance); 38..43: slow-switch cycles in pop, push, IO, h-alloc,
 // h-divide, h-search/if-label
@@ -639,6 +651,7 @@ __device__ __forceinline__ int64_t binom_draw(int64_t n, double p, uint32_t h) {
 // the word of scheduler-tree node `node` in update u (oracle node_draw)
 #define SALT_TOP 0x7A11C0DEu
 #define SALT_BLOCK 0x51CEB10Cu
+#define SALT_NEWBORN 0x4E3B0A17u
 __device__ __forceinline__ uint32_t node_draw(uint32_t slo, uint32_t shi, uint32_t update, uint32_t salt,
                                               uint64_t node) {
   return lowbias32(lowbias32(lowbias32(update * 0x85EBCA6BU + shi) ^ (uint32_t)node ^ salt) +
@@ -747,7 +760,7 @@ __host__ __device__ __forceinline__ long long sub_share(long long n, int s, int 
 void launch_world_pre(const DevWorld& W, hipStream_t s, double* d_totals, double* d_scratch, hipEvent_t lists_ready,
                       uint32_t update, bool reset = true);
 void launch_tile_pre(const DevWorld& W, hipStream_t s, const double* d_gathered, int ntiles, double* d_totals,
-                     hipEvent_t lists_ready, uint32_t update);
+                     hipEvent_t lists_ready, uint32_t update, int sub = 0, int nsub = 1);
 // allotment draw of organism (lo, hi) in update u (oracle allot_draw)
 __device__ __forceinline__ uint32_t allot_draw(uint32_t lo, uint32_t hi, uint32_t update) {
   return lowbias32(lowbias32(update * 0x85EBCA6BU + hi) ^ lo ^ 0x27D4EB2FU);
@@ -757,7 +770,15 @@ void launch_resources_end(const DevWorld& W, hipStream_t s);
 void launch_resources_pack(const DevWorld& W, hipStream_t s);
 bool res_stepped(const DevWorld& W);   // launch_resources_begin wrote res_amount_alt
 void launch_resources_settle(const DevWorld& W, hipStream_t s, const unsigned long long* sum);
-void launch_world_post(const DevWorld& W, hipStream_t s, double* d_stats, bool eager);
+// placement and activation of batch step `sub` of `nsub` (key: its scheduler
+// key), the newborns listed for the newborn pass; then launch_world_end
+// pred_out (mapped host memory, the update's last step): the predictor and
+// its organisms, ev_pred recorded after them
+void launch_world_post(const DevWorld& W, hipStream_t s, uint32_t key, int sub, int nsub,
+                       long long* pred_out = nullptr, hipEvent_t ev_pred = nullptr);
+void launch_world_end(const DevWorld& W, hipStream_t s, double* d_stats, bool eager);
+// the newborn pass of a batch step (interp.hip): the organisms k_activate listed
+void launch_newborns(const DevWorld& W, const DevWorld* dW, hipStream_t s);
 // the update's statistics into d_stats (k_stats_partial + k_stats_final)
 void launch_stats(const DevWorld& W, hipStream_t s, double* d_stats);
 void launch_classify_uniform(const DevWorld& W, hipStream_t s, int64_t first, int64_t count,
@@ -773,7 +794,7 @@ void launch_state_digest(const DevWorld& W, hipStream_t s, int64_t first, int64_
 void launch_get_census(const DevWorld& W, hipStream_t s, int64_t first, int64_t count, avgpu_census* d_out);
 void launch_merit_total(const DevWorld& W, hipStream_t s, double* d_totals, double* d_scratch);
 // strip tiles
-void launch_tile_partials(const DevWorld& W, hipStream_t s, double* d_out);
+void launch_tile_partials(const DevWorld& W, hipStream_t s, double* d_out, int reset);
 void launch_tile_after_interpret(const DevWorld& W, hipStream_t s);
-void launch_tile_place(const DevWorld& W, hipStream_t s, int round, int phase);
-void launch_tile_finish(const DevWorld& W, hipStream_t s, double* d_stats, bool eager);
+void launch_tile_place(const DevWorld& W, hipStream_t s, int round, int phase, uint32_t key, int sub, int nsub);
+void launch_tile_finish(const DevWorld& W, hipStream_t s, uint32_t key, int sub, int nsub);

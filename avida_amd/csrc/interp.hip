@@ -80,7 +80,7 @@ __device__ __forceinline__ int wave_sum_i32(int v) {
 // update's global level (consumption summed in 2^-32 units, subtracted at the
 // update's end).  Returns whether the process paid (rc counts it).
 __device__ __forceinline__ bool consume_resource(const DevWorld& W, const double* rr, int64_t N, int64_t cell,
-                                                 double& mult, double& addb) {
+                                                 double& mult, double& addb, bool wcons) {
   const int slot = (int)rr[RR_RES] - 1;
   const bool spatial = rr[RR_SPATIAL] != 0.0;
   double* cellp = W.res_amount + (int64_t)W.res_param[slot].slot * N + cell;
@@ -93,6 +93,9 @@ __device__ __forceinline__ bool consume_resource(const DevWorld& W, const double
   if (rr[RR_DEPL] != 0.0) {
     if (spatial) *cellp = __dsub_rn(level, consumed);
     else atomicAdd(W.res_cons + slot, (unsigned long long)__dmul_rn(consumed, RES_FIX));
+    // the cell's consumption this step (a newborn that replaces the organism
+    // gives back its share after the birth: world.hip newborn_credit)
+    if (wcons) { double* cp = W.cons + (int64_t)slot * N + cell; *cp = __dadd_rn(*cp, consumed); }
   }
   const double bon = __dmul_rn(consumed, rr[RR_VALUE]);
   const int ty = (int)rr[RR_TYPE];
@@ -149,7 +152,8 @@ __device__ __forceinline__ bool fast_op(const int op, const int r, int& r0, int&
 template <bool GTAB>
 __device__ __forceinline__ void res_flush(const DevWorld& W, const int64_t N, const int64_t cell, uint32_t& rpq,
                                           double& bonus, int (&rc)[AVGPU_MAX_REACTIONS], const uint32_t ttab,
-                                          const double* tmul, const double* tadd, const uint32_t k_env_res_mask) {
+                                          const double* tmul, const double* tadd, const uint32_t k_env_res_mask,
+                                          const bool wcons) {
   while (__ballot(rpq != 0u) != 0ull) {
     const uint32_t ev = rpq & 0x1FFu;
     double mult = 1.0, addb = 0.0;
@@ -195,6 +199,7 @@ __device__ __forceinline__ void res_flush(const DevWorld& W, const int64_t N, co
           if (rdepl) {
             if (rsp) *lvp = __dsub_rn(level, consumed);
             else atomicAdd(W.res_cons + rslot, (unsigned long long)__dmul_rn(consumed, RES_FIX));
+            if (wcons) { double* cp = W.cons + (int64_t)rslot * N + cell; *cp = __dadd_rn(*cp, consumed); }
           }
           const double bon = __dmul_rn(consumed, rval);
           if (rty == AVGPU_PROC_ADD) addb = __dadd_rn(addb, bon);
@@ -215,6 +220,34 @@ __device__ __forceinline__ void res_flush(const DevWorld& W, const int64_t N, co
 }
 
 __host__ __device__ constexpr int tape_stride(int S) { return S == CLASS0_SIZE ? S : S + 16; }
+
+// The adaptive sub-step predictor's term of one organism at the end of its
+// slice (oracle pred_term, the same IEEE operations): an
+// organism expected to divide within the next update's share of picks moves
+// the total weight by its merit's change plus its offspring against an
+// average victim from that point on, in mean weights, 2^-20 fixed point.
+__device__ __forceinline__ long long pred_term(const DevWorld& W, int cell, int tu, int gs, int blen, int dcop,
+                                               int dexe, double bonus) {
+  const double total = W.totals[2], n = W.totals[1];
+  if (!(total > 0.0) || !(n > 0.0)) return 0;
+  const double wbar = __ddiv_rn(total, n);
+  const double wi = W.merit[cell];
+  if (!(wi > 0.0) || !(wi <= 1.7976931348623157e308) || !(wbar > 0.0)) return 0;
+  const double e = __ddiv_rn(__dmul_rn((double)W.ave_time_slice, wi), wbar);
+  const int gt = W.gest_time[cell];
+  const int G = gt > 0 ? gt : blen;
+  const double r = (double)(G - (tu - gs));
+  if (!(r <= __dmul_rn(e, 1.25))) return 0;
+  const double t = r <= 0.0 ? 0.0 : fmin(__ddiv_rn(r, e), 1.0);
+  int sz = blen;
+  if (sz > dcop) sz = dcop;
+  if (sz > dexe) sz = dexe;
+  const double m = gt > 0 ? wi : __dmul_rn((double)sz, bonus);
+  double term = __ddiv_rn(__dmul_rn(__dadd_rn(__dsub_rn(m, wi), __dsub_rn(m, wbar)), __dsub_rn(1.0, t)), wbar);
+  if (!(term <= 1.0e6)) term = 1.0e6;
+  if (!(term >= -1.0e6)) term = -1.0e6;
+  return (long long)__dmul_rn(term, 1048576.0);
+}
 
 // divide-mutation edits (Divide_DoMutations, applied in order): kind | a << 3 | b << 15
 enum { E_SLIP = 1, E_POINT = 2, E_INS = 3, E_DEL = 4, E_TRANS = 5 };
@@ -243,12 +276,18 @@ __device__ __forceinline__ int edit_word(int kind, int a, int b) { return kind |
 // mixed launch): each organism takes kslot consecutive 320-B slots (class 1:
 // 3, class 2: 5, class 3: 7), 64 / kslot organisms per block; the slot size,
 // the staging granules per organism and the spill capacity are runtime
+// NB: the newborn pass of a batch step (oracle newborn_pass):
+// class 0 takes its organisms from list row 0 (k_activate), and a viable
+// h-divide is not run -- its cycle is taken back and the slice ends before it.
+// pred: a world update's main pass, whose slices add their sub-step
+// predictor terms (pred_term) to W.sched[0].
 template <int S, bool REC, bool C0W = false, bool SIMPLE = false, bool DEF = false, bool RES = false,
-          bool MIX = false>
+          bool MIX = false, bool NB = false>
 __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, int cls_arg, int mode_arg,
                                                int64_t first, int64_t count, int64_t chunk,
                                                uint32_t* __restrict__ lds32, bool sorted, int row,
-                                               int lpw, int serial = 0, int kslot = 1, int direct = -2) {
+                                               int lpw, int serial = 0, int kslot = 1, int direct = -2,
+                                               bool pred = false) {
   const DevWorld& W = *Wp;
   const int cls = C0W ? 0 : cls_arg;
   const int mode = C0W ? (int)AVGPU_MODE_WORLD : mode_arg;
@@ -314,6 +353,13 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
   if (serial) {
     if (lane == 0) {
       cell = (int)first;
+      M = W.mem_size[cell];
+    }
+  } else if (NB && cls == 0) {
+    // the newborn pass's class-0 organisms: list row 0 (k_activate)
+    const int64_t idx = chunk * 64 + lane;
+    if (idx < W.class_count[0]) {
+      cell = W.class_list[idx];
       M = W.mem_size[cell];
     }
   } else if (cls == 0) {
@@ -1082,7 +1128,7 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
               else
                 mult = __dmul_rn(mult, *reinterpret_cast<const double*>(rt + RT_MULT));
               rc[i]++;
-            } else if (consume_resource(W, rr, N, cell, mult, addb)) {
+            } else if (consume_resource(W, rr, N, cell, mult, addb, mode == AVGPU_MODE_WORLD)) {
               rc[i]++;
             }
           }
@@ -1110,7 +1156,7 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
 
     // a divide reads the bonus and resets the counts: apply its queued rewards first
     if (k_env_res_mask != 0u && __ballot(rpq != 0u && (rq == RQ_DIVIDE || (rpq >> 30) == 3u)) != 0ull)
-      res_flush<GTAB>(W, N, cell, rpq, bonus, rc, ttab, tmul, tadd, k_env_res_mask);
+      res_flush<GTAB>(W, N, cell, rpq, bonus, rc, ttab, tmul, tadd, k_env_res_mask, mode == AVGPU_MODE_WORLD);
     // ---- wave phase: serve the posted requests, one lane at a time ----
     unsigned long long pend = __ballot(rq != RQ_NONE);
     while (pend) {
@@ -1208,6 +1254,14 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
             double off_merit = __dmul_rn(base0, b0);
             if (p_inherit == 0) off_merit = base0;
             if (off_merit == 0.0) ok = false;
+          }
+          if (NB && ok) {
+            // the newborn pass ends before a viable divide: the instruction's
+            // cycle is taken back (its executed flag stays -- it is set again
+            // when the divide runs) and the slice stops with the IP on it
+            ok = false;
+            fl |= F_STOP;
+            cyc--; tu--; executed--;
           }
           if (ok) {
             okw = 1;
@@ -1772,7 +1826,8 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
 #undef GETHEAD
 #undef SETHEAD
 
-  if (k_env_res_mask != 0u) res_flush<GTAB>(W, N, cell, rpq, bonus, rc, ttab, tmul, tadd, k_env_res_mask);
+  if (k_env_res_mask != 0u)
+    res_flush<GTAB>(W, N, cell, rpq, bonus, rc, ttab, tmul, tadd, k_env_res_mask, mode == AVGPU_MODE_WORLD);
   // ---- write back ----
 #ifdef AVGPU_PHASE_CLOCKS
   const uint64_t clk2 = __builtin_amdgcn_s_memtime();
@@ -1810,6 +1865,9 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
     else W.rng[2 * N + cell] = kct;
     W.budget[cell] = spill ? (budget | (prim ? BUDGET_PRIM : 0)) : 0;
     if (spill && mode == AVGPU_MODE_WORLD) W.sdone[cell] = sdone + executed;
+    // the slice's instructions (a newborn replacing this organism gives the
+    // step back the share after its birth: world.hip newborn_setup)
+    if (!NB && !spill && mode == AVGPU_MODE_WORLD && !serial) W.ran[cell] = sdone + executed;
     // merit, fitness, gestation time, copied / executed sizes and last-task
     // counts were stored at the divide (st_async)
     // (a fresh organism's zero rows are stored here rather than at activation:
@@ -1873,6 +1931,15 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
       base = __shfl(base, 0);
       if (fresh) W.b_list[base + (int)__popcll(bm & ((1ull << lane) - 1ull))] = cell;
     }
+  }
+  // the sub-step predictor (oracle pred_term): an organism that ran this
+  // step's main pass to its slice's end, alive, without a divide in it
+  if (pred) {
+    long long pt = 0;
+    if (active && !(fl & (F_DEAD | F_SPILL)) && alive0 && gs <= tu - executed - sdone)
+      pt = pred_term(W, cell, tu, gs, blen, dcop, dexe, bonus);
+    for (int off = 32; off > 0; off >>= 1) pt += __shfl_xor(pt, off);
+    if (lane == 0 && pt) atomicAdd(reinterpret_cast<unsigned long long*>(W.sched), (unsigned long long)pt);
   }
   // counters: one atomic per wave
   unsigned long long e = (unsigned long long)executed;
@@ -1944,14 +2011,19 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
 #define MIX_B3 8
 #define MIX_BLOCKS (MIX_B1 + MIX_B2 + MIX_B3)
 static_assert(MIX_BLOCKS % 8 == 0, "class 0's XCD mapping needs whole rounds of 8 blocks");
-template <int S, bool REC, bool C0W = false, bool SIMPLE = false, bool DEF = false, bool RES = false>
+// `sorted`: bit 0 the class-0 sweep follows the budget-sorted windows, bit 1
+// a world update's main pass (its slices add the sub-step predictor); NB: the
+// newborn pass (class 0 over list row 0, a grid-stride)
+template <int S, bool REC, bool C0W = false, bool SIMPLE = false, bool DEF = false, bool RES = false, bool NB = false>
 __global__ __launch_bounds__(64, (S == CLASS0_SIZE) ? 2 : 1) void k_interpret(const DevWorld* __restrict__ Wp, int cls, int row, int mode,
-                                                  int64_t first, int64_t count, int sorted, int lpw, int nmix = 0) {
+                                                  int64_t first, int64_t count, int sorted_arg, int lpw, int nmix = 0) {
   constexpr int TAB_WORDS = 128 + 64 + 16 + 64 + AVGPU_MAX_REACTIONS * RT_STRIDE + 64;
   // class 0: stacks in VGPRs, tables in global memory -- only the tapes in LDS
   constexpr int STK = (S == CLASS0_SIZE) ? 0 : 2 * AVGPU_STACK_SIZE * 64;
   constexpr int TAB = (S == CLASS0_SIZE) ? 0 : TAB_WORDS;     // class 0: tapes only
   __shared__ __attribute__((aligned(16))) uint32_t lds32[64 * tape_stride(S) / 4 + STK + TAB];
+  const int sorted = sorted_arg & 1;
+  const bool pred = (sorted_arg & 2) != 0;
   if (cls == 0) {
     if (S == CLASS0_SIZE && C0W && (int)blockIdx.x < nmix) {
       const int b = blockIdx.x;
@@ -1962,47 +2034,60 @@ __global__ __launch_bounds__(64, (S == CLASS0_SIZE) ? 2 : 1) void k_interpret(co
       const int per = 64 / kslot;
       const int lcount = Wp->class_count[lc];
       for (int64_t chunk = b - b0; chunk * per < lcount; chunk += nb) {
-        interpret_chunk<S, REC, false, SIMPLE, DEF, RES, true>(Wp, lc, mode, first, count, chunk, lds32, false, lc,
-                                                                per, 0, kslot);
+        interpret_chunk<S, REC, false, SIMPLE, DEF, RES, true, NB>(Wp, lc, mode, first, count, chunk, lds32, false, lc,
+                                                                    per, 0, kslot, -2, pred);
+        __syncthreads();
+      }
+      return;
+    }
+    const int64_t bx = (int64_t)blockIdx.x - nmix, gx = (int64_t)gridDim.x - nmix;
+    // one class-0 chunk, then (world slices) the wave's own spills
+    auto run_chunk = [&](int64_t chunk) {
+      const int sp = interpret_chunk<S, REC, C0W, SIMPLE, DEF, RES, false, NB>(Wp, 0, mode, first, count, chunk, lds32,
+                                                                               sorted, 0, 64, 0, 1, -2, pred) - 1;
+      if (S == CLASS0_SIZE && C0W) {
+        // Organisms whose h-alloc (or copy) outgrew their 320-site slot: this
+        // wave continues them at once in 3-slot (960-site) lanes of its own
+        // block's LDS -- their state was written back by this wave, so a
+        // workgroup-scope fence makes it visible to the re-staging -- instead of
+        // a spill row after class 0 (~55 organisms per update, 66 us after
+        // class 0, latency-bound on the longest).  A slice that outgrows 960
+        // sites goes on to the class-2 spill row.
+        uint64_t m = __ballot(sp >= 0);
+        if (m) {
+          const int nsp = __popcll(m);
+          int mine = -1;
+          for (int j = 0; m; j++, m &= m - 1) {
+            const int c = __shfl(sp, __ffsll((long long)m) - 1);
+            if ((int)threadIdx.x == j) mine = c;
+          }
+          __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+          __syncthreads();
+          constexpr int PER3 = 64 / 3;
+          for (int g = 0; g < nsp; g += PER3) {
+            const int d = __shfl(mine, (g + (int)threadIdx.x) & 63);
+            const int direct = ((int)threadIdx.x < PER3 && g + (int)threadIdx.x < nsp) ? d : -1;
+            interpret_chunk<S, REC, false, SIMPLE, DEF, RES, true, NB>(Wp, 1, mode, first, count, 0, lds32, false, 4,
+                                                                        PER3, 0, 3, direct, pred);
+            __syncthreads();
+          }
+        }
+      }
+    };
+    if (NB) {
+      // the newborn pass: a grid-stride over list row 0
+      const int ncount = Wp->class_count[0];
+      for (int64_t chunk = bx; chunk * 64 < ncount; chunk += gx) {
+        run_chunk(chunk);
         __syncthreads();
       }
       return;
     }
     // sorted windows: the 32 chunks of a window run on one XCD (blocks are
     // dealt to the 8 XCDs round robin), so its state lines meet in one L2
-    const int64_t bx = (int64_t)blockIdx.x - nmix, gx = (int64_t)gridDim.x - nmix;
     int64_t chunk = bx;
     if (sorted && (gx & 7) == 0) chunk = (bx & 7) * (gx >> 3) + (bx >> 3);
-    const int sp = interpret_chunk<S, REC, C0W, SIMPLE, DEF, RES>(Wp, 0, mode, first, count, chunk, lds32, sorted,
-                                                                  0, 64) - 1;
-    if (S == CLASS0_SIZE && C0W) {
-      // Organisms whose h-alloc (or copy) outgrew their 320-site slot: this
-      // wave continues them at once in 3-slot (960-site) lanes of its own
-      // block's LDS -- their state was written back by this wave, so a
-      // workgroup-scope fence makes it visible to the re-staging -- instead of
-      // a spill row after class 0 (~55 organisms per update, 66 us after
-      // class 0, latency-bound on the longest).  A slice that outgrows 960
-      // sites goes on to the class-2 spill row.
-      uint64_t m = __ballot(sp >= 0);
-      if (m) {
-        const int nsp = __popcll(m);
-        int mine = -1;
-        for (int j = 0; m; j++, m &= m - 1) {
-          const int c = __shfl(sp, __ffsll((long long)m) - 1);
-          if ((int)threadIdx.x == j) mine = c;
-        }
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-        __syncthreads();
-        constexpr int PER3 = 64 / 3;
-        for (int g = 0; g < nsp; g += PER3) {
-          const int d = __shfl(mine, (g + (int)threadIdx.x) & 63);
-          const int direct = ((int)threadIdx.x < PER3 && g + (int)threadIdx.x < nsp) ? d : -1;
-          interpret_chunk<S, REC, false, SIMPLE, DEF, RES, true>(Wp, 1, mode, first, count, 0, lds32, false, 4,
-                                                                  PER3, 0, 3, direct);
-          __syncthreads();
-        }
-      }
-    }
+    run_chunk(chunk);
     return;
   }
   if (C0W) return;
@@ -2014,7 +2099,8 @@ __global__ __launch_bounds__(64, (S == CLASS0_SIZE) ? 2 : 1) void k_interpret(co
     const int rc = cls >= 0 ? cls : (r <= 3 ? r : r - 3);
     const int lcount = Wp->class_count[r];
     for (int64_t chunk = blockIdx.x; chunk * lpw < lcount; chunk += gridDim.x) {
-      interpret_chunk<S, REC, false, SIMPLE, DEF, RES>(Wp, rc, mode, first, count, chunk, lds32, false, r, lpw);
+      interpret_chunk<S, REC, false, SIMPLE, DEF, RES, false, NB>(Wp, rc, mode, first, count, chunk, lds32, false, r,
+                                                                   lpw, 0, 1, -2, pred);
       __syncthreads();
     }
   }
@@ -2355,13 +2441,20 @@ static bool def_knobs(const DevWorld& W) {
          !W.copy_ext && !W.track_age;
 }
 
-template <bool REC>
+// NB: the newborn pass of a world update (launch_newborns): the same launches
+// over the organisms k_activate listed -- class 0 from list row 0 by a
+// grid-stride of NB_BLOCKS blocks, the list classes in its leading blocks,
+// then the spill rows.  A world update's main pass (sorted) adds the sub-step
+// predictor (bit 1 of the kernels' `sorted` argument).
+#define NB_BLOCKS 2048
+template <bool REC, bool NB>
 static void launch_classes(const DevWorld& W, const DevWorld* dW, int mode, hipStream_t s,
                            int64_t first, int64_t count, int* launches, hipEvent_t* after_class,
                            bool sorted, hipStream_t* aux, hipEvent_t ev_fork, hipEvent_t* ev_join) {
-  const int srt = (sorted && first == 0 && count == W.n) ? 1 : 0;
+  const int pfl = (!NB && sorted && mode == AVGPU_MODE_WORLD) ? 2 : 0;
+  const int srt = ((!NB && sorted && first == 0 && count == W.n) ? 1 : 0) | pfl;
   const bool tall = class_timing_all();
-  const unsigned blocks = (unsigned)((count + 63) / 64);
+  const unsigned blocks = NB ? (unsigned)NB_BLOCKS : (unsigned)((count + 63) / 64);
   // list classes: a capped grid strides over the list (length known on the
   // device only).  The caps follow the blocks a CU holds (LDS: 3 of class 1,
   // 1 of classes 2 / 3) and the lists' usual lengths (class 1 ~1 %, classes
@@ -2392,13 +2485,13 @@ static void launch_classes(const DevWorld& W, const DevWorld* dW, int mode, hipS
   // (DEF defers the divide's phenotype work to placement round 0: only world
   // updates run placement -- avgpu_step(MODE_WORLD) takes the general path)
   // (RES: the same with finite resources behind the simple reactions, configs[4])
-  const bool fast = sorted && mode == AVGPU_MODE_WORLD && W.env_simple && def_knobs(W);
+  const bool fast = (NB || sorted) && mode == AVGPU_MODE_WORLD && W.env_simple && def_knobs(W);
   const bool res = W.env_res_mask != 0u;
   auto row = [&](int S, dim3 grid, hipStream_t st, int cls, int r, int lpw) {
 #define ROW_LAUNCH(SZ) \
-    do { if (fast && res) hipLaunchKernelGGL((k_interpret<SZ, REC, false, true, true, true>), grid, dim3(64), 0, st, dW, cls, r, mode, first, count, 0, lpw); \
-         else if (fast) hipLaunchKernelGGL((k_interpret<SZ, REC, false, true, true>), grid, dim3(64), 0, st, dW, cls, r, mode, first, count, 0, lpw); \
-         else hipLaunchKernelGGL((k_interpret<SZ, REC>), grid, dim3(64), 0, st, dW, cls, r, mode, first, count, 0, lpw); } while (0)
+    do { if (fast && res) hipLaunchKernelGGL((k_interpret<SZ, REC, false, true, true, true, NB>), grid, dim3(64), 0, st, dW, cls, r, mode, first, count, pfl, lpw); \
+         else if (fast) hipLaunchKernelGGL((k_interpret<SZ, REC, false, true, true, false, NB>), grid, dim3(64), 0, st, dW, cls, r, mode, first, count, pfl, lpw); \
+         else hipLaunchKernelGGL((k_interpret<SZ, REC, false, false, false, false, NB>), grid, dim3(64), 0, st, dW, cls, r, mode, first, count, pfl, lpw); } while (0)
     if (S == CLASS1_SIZE) ROW_LAUNCH(CLASS1_SIZE);
     else if (S == CLASS2_SIZE) ROW_LAUNCH(CLASS2_SIZE);
     else ROW_LAUNCH(CLASS3_SIZE);
@@ -2422,10 +2515,10 @@ static void launch_classes(const DevWorld& W, const DevWorld* dW, int mode, hipS
   // got CUs as class-0 waves retired and ended ~40-55 us after class 0).
   // the list classes inside class 0's launch (MIX_BLOCKS leading blocks):
   // sorted world updates, unless AVGPU_NO_MIX=1 (A/B)
-  const bool mix = aux && mix_lists();
+  const bool mix = NB || (aux && mix_lists());
   const int nmix = mix ? MIX_BLOCKS : 0;
   const unsigned cblocks = blocks + (unsigned)nmix;
-  if (aux && !mix) {
+  if (!NB && aux && !mix) {
     // ev_fork: recorded by launch_world_pre right after k_allot built the lists
     for (int k = 0; k < 2; k++) hipStreamWaitEvent(aux[k], ev_fork, 0);
     list(1, aux[0]);
@@ -2439,14 +2532,14 @@ static void launch_classes(const DevWorld& W, const DevWorld* dW, int mode, hipS
     hipEventRecord(ev_join[0], aux[0]);
   }
   if (fast && res)
-    hipLaunchKernelGGL((k_interpret<CLASS0_SIZE, REC, true, true, true, true>), dim3(cblocks), dim3(64), 0, s, dW, 0, 0, mode, first, count, srt, 64, nmix);
+    hipLaunchKernelGGL((k_interpret<CLASS0_SIZE, REC, true, true, true, true, NB>), dim3(cblocks), dim3(64), 0, s, dW, 0, 0, mode, first, count, srt, 64, nmix);
   else if (fast)
-    hipLaunchKernelGGL((k_interpret<CLASS0_SIZE, REC, true, true, true>), dim3(cblocks), dim3(64), 0, s, dW, 0, 0, mode, first, count, srt, 64, nmix);
+    hipLaunchKernelGGL((k_interpret<CLASS0_SIZE, REC, true, true, true, false, NB>), dim3(cblocks), dim3(64), 0, s, dW, 0, 0, mode, first, count, srt, 64, nmix);
   else if (mode == AVGPU_MODE_WORLD && W.env_simple && W.env_res_mask == 0u)
-    hipLaunchKernelGGL((k_interpret<CLASS0_SIZE, REC, true, true>), dim3(cblocks), dim3(64), 0, s, dW, 0, 0, mode, first, count, srt, 64, nmix);
+    hipLaunchKernelGGL((k_interpret<CLASS0_SIZE, REC, true, true, false, false, NB>), dim3(cblocks), dim3(64), 0, s, dW, 0, 0, mode, first, count, srt, 64, nmix);
   else if (mode == AVGPU_MODE_WORLD)
-    hipLaunchKernelGGL((k_interpret<CLASS0_SIZE, REC, true>), dim3(cblocks), dim3(64), 0, s, dW, 0, 0, mode, first, count, srt, 64, nmix);
-  else
+    hipLaunchKernelGGL((k_interpret<CLASS0_SIZE, REC, true, false, false, false, NB>), dim3(cblocks), dim3(64), 0, s, dW, 0, 0, mode, first, count, srt, 64, nmix);
+  else if (!NB)
     hipLaunchKernelGGL((k_interpret<CLASS0_SIZE, REC>), dim3(blocks), dim3(64), 0, s, dW, 0, 0, mode, first, count, srt, 64);
   if (after_class) hipEventRecord(after_class[0], s);
   // Spill rows run after class 0, alone on the chip and latency-bound on their
@@ -2484,9 +2577,17 @@ void launch_interpret_classes(const DevWorld& W, const DevWorld* dW, int mode, h
                               int64_t first, int64_t count, int* launches, hipEvent_t* after_class,
                               bool sorted, hipStream_t* aux, hipEvent_t ev_fork, hipEvent_t* ev_join) {
   if (W.rec)
-    launch_classes<true>(W, dW, mode, s, first, count, launches, after_class, sorted, aux, ev_fork, ev_join);
+    launch_classes<true, false>(W, dW, mode, s, first, count, launches, after_class, sorted, aux, ev_fork, ev_join);
   else
-    launch_classes<false>(W, dW, mode, s, first, count, launches, after_class, sorted, aux, ev_fork, ev_join);
+    launch_classes<false, false>(W, dW, mode, s, first, count, launches, after_class, sorted, aux, ev_fork, ev_join);
+}
+
+// the newborn pass of a world update's batch step (after k_activate)
+void launch_newborns(const DevWorld& W, const DevWorld* dW, hipStream_t s) {
+  if (W.rec)
+    launch_classes<true, true>(W, dW, AVGPU_MODE_WORLD, s, 0, W.n, nullptr, nullptr, false, nullptr, nullptr, nullptr);
+  else
+    launch_classes<false, true>(W, dW, AVGPU_MODE_WORLD, s, 0, W.n, nullptr, nullptr, false, nullptr, nullptr, nullptr);
 }
 
 // one serial-world update (launch_world_post's statistics follow it)

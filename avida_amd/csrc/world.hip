@@ -411,6 +411,12 @@ __global__ __launch_bounds__(256) void k_merit_partial(DevWorld W, double* parti
                                                        double* alive_d, int reset) {
   if (reset == 1 && blockIdx.x == 0) reset_counts_block(W);
   if (reset == 2 && blockIdx.x == 0) reset_queues_block(W);
+  // a strip's partials end with its last step's predictor and pick carry
+  // (the oracle's orc_tile_partials; summed on every strip after the gather)
+  if (alive_d && blockIdx.x == 0 && threadIdx.x < 2) {
+    const int64_t nbl = (W.n + 255) / 256;
+    partial[2 * nbl + threadIdx.x] = __longlong_as_double(W.sched[threadIdx.x]);
+  }
   const int lane = threadIdx.x & 63;
   const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int64_t nb = (W.n + 255) / 256;
@@ -467,14 +473,15 @@ __global__ __launch_bounds__(256) void k_merit_partial(DevWorld W, double* parti
 // workgroup over a 65536-block tree in global memory took 124 us.)
 #define TREE_LDS_P 4096
 #define TREE_C_LOG 12
+
 // leaf g of the block level (0 past the blocks); alive count into a
 __device__ __forceinline__ double tree_leaf(const double* part, const int32_t* alive_part, int64_t nb, int64_t nbt,
                                             int mode, int64_t g, long long& a) {
   if (g >= nbt) return 0.0;
   if (mode == 1) {
     const int64_t k = g / nb, j = g - k * nb;
-    a += (long long)part[k * 2 * nb + nb + j];
-    return part[k * 2 * nb + j];
+    a += (long long)part[k * tile_part_stride(nb) + nb + j];
+    return part[k * tile_part_stride(nb) + j];
   }
   a += alive_part[g];
   return part[g];
@@ -528,6 +535,23 @@ __global__ __launch_bounds__(1024) void k_block_counts(DevWorld W, const double*
       totals[1] = (double)n;
       totals[2] = root;
       totals[3] = __dmul_rn(ave, (double)n);
+    }
+    if (mode != 3) {
+      // the picks the last step's newborns ran beyond their victims'
+      // leftovers come out of this step (oracle take_carry): a strip sums
+      // every strip's carry from the gathered partials
+      long long fresh = W.sched[1];
+      if (mode == 1) {
+        fresh = 0;
+        for (int k = 0; k < ntiles; k++) fresh += __double_as_longlong(part[k * tile_part_stride(nb) + 2 * nb + 1]);
+      }
+      long long rem = W.sched[2] + fresh;
+      const long long take = min(max(rem, -nroot), nroot);
+      rem -= take;
+      nroot -= take;
+      W.sched[1] = 0;
+      W.sched[2] = rem;
+      W.sched[0] = 0;                         // this step's predictor (interp.hip pred_term)
     }
     cnt[1] = nroot;
   }
@@ -739,6 +763,9 @@ __global__ __launch_bounds__(1024) void k_allot(DevWorld W, const double* totals
     }
     W.budget[c] = bud;
     W.aclass[c] = want[j] ? (uint8_t)cls[j] : (uint8_t)ACLASS_NONE;
+    W.ran[c] = 0;
+    if (W.env_resources)
+      for (int r = 0; r < W.n_res; r++) W.cons[(int64_t)r * W.n + c] = 0.0;
     occ_init_cell(W, c);
     W.killt[c] = 0u;
     W.claim_r[3][c] = 0ull;   // the previous update's round-3 claims (k_activate read them last)
@@ -1229,7 +1256,15 @@ __global__ void k_place_round(DevWorld W, int m) {
 // its own birth time (a round-0 pick of an earlier birth landed there:
 // killt[parent] > 2^16 - t) is cancelled -- the reference would have killed
 // its parent before this divide; the others claim their round-0 targets.
-__global__ void k_place_claim0(DevWorld W) {
+__global__ void k_place_claim0(DevWorld W, long long* pred_out) {
+  // the list rows are free after the main pass: the newborn pass's (k_activate)
+  if (blockIdx.x == 0 && threadIdx.x < NUM_LISTS) W.class_count[threadIdx.x] = 0;
+  // the update's last step: its predictor and organisms to the host (mapped
+  // memory), which chooses the next update's steps from them
+  if (pred_out && blockIdx.x == 0 && threadIdx.x == 0) {
+    pred_out[0] = W.sched[0];
+    pred_out[1] = (long long)W.totals[1];
+  }
   QUEUE_LOOP(q) {
     const int64_t r = rec_of(W, q);
     if (W.b_state[r] != BS_PENDING) continue;
@@ -1404,6 +1439,7 @@ __global__ __launch_bounds__(256) void k_tile_round(DevWorld W, int m, int rbloc
 // claim their round-0 targets (and the halo send slots of parity 0).
 __global__ __launch_bounds__(256) void k_tile_claim0(DevWorld W) {
   const int X = W.world_x;
+  if (blockIdx.x == 0 && threadIdx.x < NUM_LISTS) W.class_count[threadIdx.x] = 0;
   QUEUE_LOOP(q) {
     const int64_t r = rec_of(W, q);
     if (W.b_state[r] != BS_PENDING) continue;
@@ -1417,6 +1453,64 @@ __global__ __launch_bounds__(256) void k_tile_claim0(DevWorld W) {
     const unsigned long long key = W.b_prio[r];
     atomicMax(&W.claim_r[0][t], key);
     if (halo_slot(W, t, d, x, ghost)) atomicMax(&halo_cl(W.h_send[d], X, 0, ghost ? 0 : 1)[x], key);
+  }
+}
+
+// ---- the batch step's newborns (oracle newborn_pass) ----
+// An activated offspring first gives back (1 - t) of what its cell's replaced
+// organism consumed in the step's main pass, then runs its own share of the
+// step's remaining picks: Binomial(round(UD_s (1 - t)), merit / total) from a
+// stateless draw of its global cell, in the newborn pass (interp.hip NB).
+// The picks beyond what the replaced organism had left ((1 - t) of the
+// instructions it ran) are the step's carry, taken from the next allotment.
+__device__ __forceinline__ double nb_frac(uint32_t t) { return __dmul_rn((double)(0x10000u - t), 1.0 / 65536.0); }
+__device__ __forceinline__ long long newborn_budget(const DevWorld& W, int64_t c, uint32_t t, double merit,
+                                                    uint32_t key, long long uds, double total) {
+  if (!(total > 0.0) || uds <= 0) return 0;
+  const long long n = (long long)floor(__dadd_rn(__dmul_rn((double)uds, nb_frac(t)), 0.5));
+  const double p = __ddiv_rn(merit_ok(merit) ? merit : 0.0, total);
+  const long long b = binom_draw(n, p, node_draw(W.seed_lo, W.seed_hi, key, SALT_NEWBORN, (uint64_t)(W.cell0 + c)));
+  return min(b, (long long)(BUDGET_PRIM - 1));
+}
+__device__ __forceinline__ void newborn_credit(const DevWorld& W, int64_t c, uint32_t t) {
+  const double f = nb_frac(t);
+  for (int r = 0; r < W.n_res; r++) {
+    const double v = W.cons[(int64_t)r * W.n + c];
+    if (v == 0.0) continue;
+    const double back = __dmul_rn(v, f);
+    const ResParam& q = W.res_param[r];
+    if (q.geometry != AVGPU_RES_GLOBAL) {
+      double* p = W.res_amount + (int64_t)q.slot * W.n + c;
+      *p = __dadd_rn(*p, back);
+    } else {
+      atomicAdd(W.res_cons + r, 0ull - (unsigned long long)__dmul_rn(back, RES_FIX));
+    }
+  }
+}
+// one newborn in cell c: credit, budget, carry; returns its list row (-1: no slice)
+__device__ __forceinline__ int newborn_setup(const DevWorld& W, int64_t c, uint32_t t, double merit, int len,
+                                             uint32_t key, long long uds, double total, long long& carry,
+                                             unsigned long long& wasted) {
+  if (W.env_resources) newborn_credit(W, c, t);
+  const long long left = (long long)__dmul_rn((double)W.ran[c], nb_frac(t));
+  const long long bud = newborn_budget(W, c, t, merit, key, uds, total);
+  carry += bud - left;
+  wasted += (unsigned long long)left;
+  W.budget[c] = (int32_t)bud;
+  return bud > 0 ? class_of(::need_of(len, CTL_ALIVE, W.size_range)) : -1;
+}
+// the wave's newborns into the newborn pass's lists (row 0: class 0, rows
+// 1..3 the list classes), one atomic per row and wave
+__device__ __forceinline__ void newborn_enqueue(const DevWorld& W, int cell, int row) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int k = 0; k < NUM_CLASSES; k++) {
+    const unsigned long long m = __ballot(row == k);
+    if (!m) continue;
+    int base = 0;
+    if (lane == 0) base = atomicAdd(&W.class_count[k], (int)__popcll(m));
+    base = __shfl(base, 0);
+    if (row == k) W.class_list[(int64_t)k * W.n + base + (int)__popcll(m & ((1ull << lane) - 1ull))] = cell;
   }
 }
 
@@ -1434,48 +1528,62 @@ __global__ __launch_bounds__(256) void k_tile_claim0(DevWorld W) {
 // are cleared by k_allot).  A record that does not own its cell was placed
 // and overwritten (CNT_OVERWRITTEN), unless it was cancelled
 // (CNT_CANCELLED: its parent died first) or found no cell (CNT_DROPPED).
-__global__ __launch_bounds__(64) void k_activate(DevWorld W, int fused) {
+__global__ __launch_bounds__(64) void k_activate(DevWorld W, int fused, uint32_t key, int sub, int nsub) {
   const int nb = queue_len(W);
   const int64_t ncell = W.n + (W.tiled ? 2 * (int64_t)W.world_x : 0);
-  unsigned long long born = 0, over = 0, canc = 0, nocell = 0, bad = 0;
-  for (int64_t q = (int64_t)blockIdx.x * 64 + threadIdx.x; q < nb; q += (int64_t)gridDim.x * 64) {
-    const int64_t i = rec_of(W, q);
-    // the genome's first 128 B, loaded before the claims decide whether the
-    // record won (a dependent round trip less for the ~95 % that do)
-    const uint4* g4 = reinterpret_cast<const uint4*>(W.b_genome + i * TAPE_SLOT);
-    uint4 pre[8];
+  const int lane = threadIdx.x & 63;
+  const double total = W.totals[2];
+  const long long uds = sub_share((long long)W.totals[3], sub, nsub);
+  unsigned long long born = 0, over = 0, canc = 0, nocell = 0, bad = 0, wasted = 0, nbs = 0;
+  long long carry = 0;
+  for (int64_t q0 = (int64_t)blockIdx.x * 64; q0 < nb; q0 += (int64_t)gridDim.x * 64) {
+    const int64_t q = q0 + lane;
+    int nrow = -1, ncell_nb = 0;
+    do {
+      if (q >= nb) break;
+      const int64_t i = rec_of(W, q);
+      // the genome's first 128 B, loaded before the claims decide whether the
+      // record won (a dependent round trip less for the ~95 % that do)
+      const uint4* g4 = reinterpret_cast<const uint4*>(W.b_genome + i * TAPE_SLOT);
+      uint4 pre[8];
 #pragma unroll
-    for (int u = 0; u < 8; u++) pre[u] = g4[u];
-    const int tgt = W.b_target[i];
-    const int8_t st = W.b_state[i];
-    const Child b = child_of_record(W, i);
-    const int lastr = last_claim_round(st);
-    // the record's claims, round k's at b_tgt[k] (the last one its target);
-    // a target out of range is a corrupt record: counted, never written
-    bool ok = true;
-    for (int k = 0; k <= lastr && k < 3; k++) {
-      const int tk = (k == lastr && tgt >= 0) ? tgt : W.b_tgt[(int64_t)k * W.rcap + i];
-      if (tk >= 0 && (int64_t)tk < ncell) W.claim_r[k][tk] = 0ull;
-      else ok = false;
-    }
-    if (st == BS_CANCELLED) { canc++; continue; }
-    if (st <= BS_NO_CELL) { nocell++; continue; }
-    if (!ok || tgt < 0 || (int64_t)tgt >= ncell) { bad++; continue; }
-    const uint32_t t = 0x10000u - b.hs;
-    bool won = false;
-    if (fused == 2) {
-      won = st >= BS_WON && st < BS_WON + 4 && W.owner[tgt] == (int)i;
-    } else if (st == BS_PENDING) {
-      won = W.claim_r[3][tgt] == W.b_prio[i] && takes_cell(W, W.owner[tgt], t);
-    } else if (st >= BS_WON && st < BS_WON + 4) {
-      const unsigned long long c3 = W.claim_r[3][tgt];
-      won = W.owner[tgt] == (int)i && !(c3 != 0ull && key_time(c3) >= t);
-    }
-    if (!won) { over++; continue; }
-    if (b.len < 0 || b.len > AVGPU_MAX_GENOME) { bad++; continue; }   // (k_halo_pack skips it too)
-    if (tgt >= W.n) continue;                 // sent to the neighbouring tile
-    born++;
-    setup_child_lane<8>(W, tgt, b, W.b_genome + i * TAPE_SLOT, pre);
+      for (int u = 0; u < 8; u++) pre[u] = g4[u];
+      const int tgt = W.b_target[i];
+      const int8_t st = W.b_state[i];
+      Child b = child_of_record(W, i);
+      const int lastr = last_claim_round(st);
+      // the record's claims, round k's at b_tgt[k] (the last one its target);
+      // a target out of range is a corrupt record: counted, never written
+      bool ok = true;
+      for (int k = 0; k <= lastr && k < 3; k++) {
+        const int tk = (k == lastr && tgt >= 0) ? tgt : W.b_tgt[(int64_t)k * W.rcap + i];
+        if (tk >= 0 && (int64_t)tk < ncell) W.claim_r[k][tk] = 0ull;
+        else ok = false;
+      }
+      if (st == BS_CANCELLED) { canc++; break; }
+      if (st <= BS_NO_CELL) { nocell++; break; }
+      if (!ok || tgt < 0 || (int64_t)tgt >= ncell) { bad++; break; }
+      const uint32_t t = 0x10000u - b.hs;
+      bool won = false;
+      if (fused == 2) {
+        won = st >= BS_WON && st < BS_WON + 4 && W.owner[tgt] == (int)i;
+      } else if (st == BS_PENDING) {
+        won = W.claim_r[3][tgt] == W.b_prio[i] && takes_cell(W, W.owner[tgt], t);
+      } else if (st >= BS_WON && st < BS_WON + 4) {
+        const unsigned long long c3 = W.claim_r[3][tgt];
+        won = W.owner[tgt] == (int)i && !(c3 != 0ull && key_time(c3) >= t);
+      }
+      if (!won) { over++; break; }
+      if (b.len < 0 || b.len > AVGPU_MAX_GENOME) { bad++; break; }   // (k_halo_pack skips it too)
+      if (tgt >= W.n) break;                   // sent to the neighbouring tile
+      born++;
+      b.hs = 0;                                // it runs its share of this step instead (newborn pass)
+      setup_child_lane<8>(W, tgt, b, W.b_genome + i * TAPE_SLOT, pre);
+      nrow = newborn_setup(W, tgt, t, b.merit, b.len, key, uds, total, carry, wasted);
+      ncell_nb = tgt;
+    } while (0);
+    nbs += nrow >= 0 ? 1ull : 0ull;
+    newborn_enqueue(W, ncell_nb, nrow);
   }
   for (int off = 32; off > 0; off >>= 1) {
     born += __shfl_xor(born, off);
@@ -1483,6 +1591,9 @@ __global__ __launch_bounds__(64) void k_activate(DevWorld W, int fused) {
     canc += __shfl_xor(canc, off);
     nocell += __shfl_xor(nocell, off);
     bad += __shfl_xor(bad, off);
+    wasted += __shfl_xor(wasted, off);
+    nbs += __shfl_xor(nbs, off);
+    carry += __shfl_xor(carry, off);
   }
   if (threadIdx.x == 0) {
     if (born) count_add(W, CNT_BIRTHS, born);
@@ -1490,6 +1601,9 @@ __global__ __launch_bounds__(64) void k_activate(DevWorld W, int fused) {
     if (canc) count_add(W, CNT_CANCELLED, canc);
     if (nocell) count_add(W, CNT_DROPPED, nocell);
     if (bad) count_add(W, CNT_BAD_RECORD, bad);
+    if (wasted) count_add(W, CNT_WASTED, wasted);
+    if (nbs) count_add(W, CNT_SLICES, nbs);
+    if (carry) atomicAdd(reinterpret_cast<unsigned long long*>(W.sched + 1), (unsigned long long)carry);
   }
 }
 
@@ -1563,8 +1677,12 @@ __global__ __launch_bounds__(64) void k_halo_pack(DevWorld W) {
 
 // Records received from direction d: the offspring owns its target cell when
 // it was that cell's last winner (owner == REMOTE_OWNER(its round)).
-__global__ __launch_bounds__(64) void k_activate_remote(DevWorld W) {
+__global__ __launch_bounds__(64) void k_activate_remote(DevWorld W, uint32_t key, int sub, int nsub) {
   const int lane = threadIdx.x;
+  const double total = W.totals[2];
+  const long long uds = sub_share((long long)W.totals[3], sub, nsub);
+  long long carry = 0;
+  unsigned long long wasted = 0, nbs = 0;
   const int X = W.world_x;
   // blocks [0, G/2) take the records from above, the rest those from below
   const int half = gridDim.x >> 1;
@@ -1590,14 +1708,25 @@ __global__ __launch_bounds__(64) void k_activate_remote(DevWorld W) {
     born++;
     Child b;
     b.len = r.len; b.gen = r.gen; b.ccopied = r.ccopied; b.exec = r.exec; b.gest = r.gest;
-    b.hs = 0x10000u - r.t;
+    b.hs = 0;                                  // it runs its share of this step (newborn pass)
     b.merit = r.merit; b.fitness = r.fitness; b.lo = r.rng_lo; b.hi = r.rng_hi; b.ctr = r.rng_ctr;
     b.ltask = recs[q].last_task; b.lstride = 1;
     setup_child<64>(W, c, b, reinterpret_cast<const uint32_t*>(arena + r.off), lane);
+    if (lane == 0) {
+      const int row = newborn_setup(W, c, r.t, r.merit, r.len, key, uds, total, carry, wasted);
+      if (row >= 0) {
+        nbs++;
+        const int slot = atomicAdd(&W.class_count[row], 1);
+        W.class_list[(int64_t)row * W.n + slot] = (int)c;
+      }
+    }
   }
   if (lane == 0) {
     if (born) count_add(W, CNT_BIRTHS, born);
     if (lost) count_add(W, CNT_OVERWRITTEN, lost);
+    if (wasted) count_add(W, CNT_WASTED, wasted);
+    if (nbs) count_add(W, CNT_SLICES, nbs);
+    if (carry) atomicAdd(reinterpret_cast<unsigned long long*>(W.sched + 1), (unsigned long long)carry);
   }
 }
 
@@ -1733,6 +1862,10 @@ __global__ __launch_bounds__(256) void k_stats_final(DevWorld W, const double* p
     out[33] = (double)cs[0][CNT_LANESTEPS];
     out[34] = (double)cs[0][CNT_OVERWRITTEN];
     out[35] = (double)cs[0][CNT_CANCELLED];
+    out[36] = (double)cs[0][CNT_WASTED];
+    out[37] = __longlong_as_double(W.sched[0]);             // the predictor (bits)
+    out[38] = __longlong_as_double(W.sched[1] + W.sched[2]); // the pick carry (bits)
+    out[39] = W.totals[1];                                  // the organisms it is relative to
   }
 }
 
@@ -1866,11 +1999,11 @@ void launch_world_pre(const DevWorld& W, hipStream_t s, double* totals, double* 
 // a strip tile: the top tree over every strip's gathered partials (mode 1),
 // then the allotment (its partials' launch cleared the counters)
 void launch_tile_pre(const DevWorld& W, hipStream_t s, const double* gathered, int ntiles, double* totals,
-                     hipEvent_t lists_ready, uint32_t update) {
+                     hipEvent_t lists_ready, uint32_t update, int sub, int nsub) {
   const int64_t nb = (W.n + 255) / 256;
-  launch_resources_begin(W, s);
-  launch_block_counts(W, s, gathered, nullptr, nb, ntiles, tree_levels(nb * ntiles), totals, update, 1);
-  launch_allot(W, s, totals, lists_ready, update);
+  if (sub == 0) launch_resources_begin(W, s);
+  launch_block_counts(W, s, gathered, nullptr, nb, ntiles, tree_levels(nb * ntiles), totals, update, 1, sub, nsub);
+  launch_allot(W, s, totals, lists_ready, update, sub == 0 ? 1 : 0);
 }
 
 void launch_stats(const DevWorld& W, hipStream_t s, double* stats) {
@@ -1920,10 +2053,10 @@ void launch_reset_counts(const DevWorld& W, hipStream_t s) {
 // Placement rounds alternate between the claim arrays claim / claim2 (round k
 // claims into array k & 1 after zeroing its records' round k-1 claims; the
 // last round's are zeroed by k_activate): no clearing launch per round.
-void launch_world_post(const DevWorld& W, hipStream_t s, double* stats, bool eager) {
+void launch_world_post(const DevWorld& W, hipStream_t s, uint32_t key, int sub, int nsub, long long* pred_out,
+                       hipEvent_t ev_pred) {
   // the occupancy was initialised by k_allot_total; the divide mutations
   // ride in round 0's pick launch
-  launch_resources_end(W, s);
   // round 0's pick (with the divide mutations beside it), then three launches
   // of resolve(m-1) + pick(m), then activation with round 3's resolve: 5
   // launches instead of 9 (k_place_round)
@@ -1944,18 +2077,25 @@ void launch_world_post(const DevWorld& W, hipStream_t s, double* stats, bool eag
 #else
   hipLaunchKernelGGL(k_place_pick_mut, dim3(nbk), dim3(256), 0, s, W, (int)bb, pf, 0, nbk);
 #endif
-  hipLaunchKernelGGL(k_place_claim0, dim3(bb), dim3(256), 0, s, W);
+  hipLaunchKernelGGL(k_place_claim0, dim3(bb), dim3(256), 0, s, W, pred_out);
+  if (pred_out && ev_pred) hipEventRecord(ev_pred, s);
   for (int m = 1; m < 4; m++) hipLaunchKernelGGL(k_place_round, dim3(bb), dim3(256), 0, s, W, m);
-  hipLaunchKernelGGL(k_activate, dim3(lane_grid(W)), dim3(64), 0, s, W, 1);
+  hipLaunchKernelGGL(k_activate, dim3(lane_grid(W)), dim3(64), 0, s, W, 1, key, sub, nsub);
+}
+
+// after the newborn pass (interp.hip): the step's global consumption settled,
+// then (eager) the update's statistics
+void launch_world_end(const DevWorld& W, hipStream_t s, double* stats, bool eager) {
+  launch_resources_end(W, s);
   if (eager) launch_stats(W, s, stats);
 }
 
 // ---- strip tiles: the same update split around the halo exchanges ----
 // (a strip tile's partials start its update: block 0 also clears the counters)
-void launch_tile_partials(const DevWorld& W, hipStream_t s, double* out) {
+void launch_tile_partials(const DevWorld& W, hipStream_t s, double* out, int reset) {
   const int64_t nb = (W.n + 255) / 256;
   hipLaunchKernelGGL(k_merit_partial, dim3((unsigned)((nb + 3) / 4)), dim3(256), 0, s, W, out, (int32_t*)nullptr,
-                     out + nb, W.tiled ? 1 : 0);
+                     out + nb, reset);
 }
 
 // after interpretation: the divide mutations, the ghost rows emptied and the
@@ -1974,7 +2114,7 @@ void launch_tile_after_interpret(const DevWorld& W, hipStream_t s) {
 //          the record buffers
 // phase 2: (round 3) this tile's own winners activated -- while the records
 //          travel; avgpu_tile_finish then activates the received ones
-void launch_tile_place(const DevWorld& W, hipStream_t s, int round, int phase) {
+void launch_tile_place(const DevWorld& W, hipStream_t s, int round, int phase, uint32_t key, int sub, int nsub) {
   const unsigned bb = place_grid(W);
   const unsigned hb = nblk(2 * (int64_t)W.world_x, 256);
   if (phase == 0) {
@@ -1985,12 +2125,11 @@ void launch_tile_place(const DevWorld& W, hipStream_t s, int round, int phase) {
     hipLaunchKernelGGL(k_tile_round, dim3(bb + hb), dim3(256), 0, s, W, 4, (int)bb);
     hipLaunchKernelGGL(k_halo_pack, dim3(lane_grid(W)), dim3(64), 0, s, W);
   } else {
-    hipLaunchKernelGGL(k_activate, dim3(lane_grid(W)), dim3(64), 0, s, W, 2);
+    hipLaunchKernelGGL(k_activate, dim3(lane_grid(W)), dim3(64), 0, s, W, 2, key, sub, nsub);
   }
 }
 
-void launch_tile_finish(const DevWorld& W, hipStream_t s, double* stats, bool eager) {
+void launch_tile_finish(const DevWorld& W, hipStream_t s, uint32_t key, int sub, int nsub) {
   const unsigned rb = (unsigned)std::max(1, std::min(W.world_x, 4096));
-  hipLaunchKernelGGL(k_activate_remote, dim3(2 * rb), dim3(64), 0, s, W);
-  if (eager) launch_stats(W, s, stats);
+  hipLaunchKernelGGL(k_activate_remote, dim3(2 * rb), dim3(64), 0, s, W, key, sub, nsub);
 }

@@ -117,7 +117,7 @@ class StatsRecorder:
         f = self._file(name, ["Avida count data", self._stamp()], COUNT_COLS)
         a = self.arbiter
         ng, nt = (a.num_genotypes(), a.num_threshold()) if a is not None else (0, 0)
-        f.row([s.update, s.insts_executed, n, ng, nt, 0, 0, 0, s.births, s.deaths, 0, 0, 0, n, 0, 0])
+        f.row([s.update, s.insts_executed - s.insts_wasted, n, ng, nt, 0, 0, 0, s.births, s.deaths, 0, 0, 0, n, 0, 0])
 
     def print_dominant(self, name="dominant.dat"):
         """cActionPrintDominantData (actions/PrintActions.cc:5405-5440): the
@@ -152,7 +152,7 @@ class StatsRecorder:
     def print_time(self, name="time.dat"):
         s = self.last
         f = self._file(name, ["Avida time data", self._stamp()], TIME_COLS)
-        f.row([s.update, self.avida_time, s.ave_generation, s.insts_executed])
+        f.row([s.update, self.avida_time, s.ave_generation, s.insts_executed - s.insts_wasted])
 
     def print_resource(self, levels, name="resource.dat"):
         f = self._file(name, ["Avida resource data", self._stamp(),

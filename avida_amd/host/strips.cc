@@ -337,35 +337,44 @@ void attach(Tile& t, int ntiles) {
   t.cons = dalloc<uint64_t>(AVGPU_MAX_RESOURCES);
 }
 
-// the per-update schedule of include/avida_gpu.h ("strip tiles")
+// the per-update schedule of include/avida_gpu.h ("strip tiles"): the
+// update's batch steps K from the gathered predictors (avgpu_tile_steps, the
+// same on every strip), then per step the placement protocol
 void update(std::vector<Tile>& tiles, Transport& tr, hipStream_t s) {
-  const int T = (int)tiles.size();
-  int ntiles_total = T;
+  int ntiles_total = (int)tiles.size();
   if (auto* r = dynamic_cast<Rccl*>(&tr)) ntiles_total = r->world;
   for (Tile& t : tiles) AV_OK(avgpu_tile_partials(t.h, t.part));
   tr.all_gather(tiles, s);
-  if (tiles[0].res_bytes > 0) tr.exchange(tiles, Kind::Resources, s);
-  for (Tile& t : tiles) AV_OK(avgpu_tile_begin(t.h, t.gathered, ntiles_total));
-  tr.exchange(tiles, Kind::Halo, s);
-  // round 0's picks and kill times, then the cancellations and round 0's
-  // claims (phase 3, with the neighbours' kill times on the edge rows); then
-  // one launch and one exchange per placement round (both strips resolve each
-  // edge cell alike, at the start of the next round's launch)
-  const int steps[5][2] = {{0, 0}, {0, 3}, {1, 0}, {2, 0}, {3, 0}};
-  for (const auto& st : steps) {
-    for (Tile& t : tiles) AV_OK(avgpu_tile_place(t.h, st[0], st[1]));
+  int K = 1;
+  AV_OK(avgpu_tile_steps(tiles[0].h, tiles[0].gathered, ntiles_total, &K));
+  for (int sub = 0; sub < K; sub++) {
+    if (sub > 0) {
+      for (Tile& t : tiles) AV_OK(avgpu_tile_partials(t.h, t.part));
+      tr.all_gather(tiles, s);
+    }
+    if (sub == 0 && tiles[0].res_bytes > 0) tr.exchange(tiles, Kind::Resources, s);
+    for (Tile& t : tiles) AV_OK(avgpu_tile_begin_step(t.h, t.gathered, ntiles_total, sub, K));
     tr.exchange(tiles, Kind::Halo, s);
-  }
-  for (Tile& t : tiles) AV_OK(avgpu_tile_place(t.h, 3, 1));   // last resolve, records packed
-  tr.exchange_begin(tiles, Kind::Records, s);
-  for (Tile& t : tiles) AV_OK(avgpu_tile_place(t.h, 3, 2));   // own winners, beside the exchange
-  tr.exchange_end(s);
-  for (Tile& t : tiles) AV_OK(avgpu_tile_finish(t.h, nullptr));
-  int pools = 0;
-  for (Tile& t : tiles) pools = avgpu_tile_res_cons(t.h, t.cons);
-  if (pools > 0) {
-    tr.all_reduce_sum(tiles, s);
-    for (Tile& t : tiles) AV_OK(avgpu_tile_res_settle(t.h, t.cons));
+    // round 0's picks and kill times, then the cancellations and round 0's
+    // claims (phase 3, with the neighbours' kill times on the edge rows); then
+    // one launch and one exchange per placement round (both strips resolve each
+    // edge cell alike, at the start of the next round's launch)
+    const int steps[5][2] = {{0, 0}, {0, 3}, {1, 0}, {2, 0}, {3, 0}};
+    for (const auto& st : steps) {
+      for (Tile& t : tiles) AV_OK(avgpu_tile_place(t.h, st[0], st[1]));
+      tr.exchange(tiles, Kind::Halo, s);
+    }
+    for (Tile& t : tiles) AV_OK(avgpu_tile_place(t.h, 3, 1));   // last resolve, records packed
+    tr.exchange_begin(tiles, Kind::Records, s);
+    for (Tile& t : tiles) AV_OK(avgpu_tile_place(t.h, 3, 2));   // own winners, beside the exchange
+    tr.exchange_end(s);
+    for (Tile& t : tiles) AV_OK(avgpu_tile_finish(t.h, nullptr));   // remote offspring, newborn pass
+    int pools = 0;
+    for (Tile& t : tiles) pools = avgpu_tile_res_cons(t.h, t.cons);
+    if (pools > 0) {
+      tr.all_reduce_sum(tiles, s);
+      for (Tile& t : tiles) AV_OK(avgpu_tile_res_settle(t.h, t.cons));
+    }
   }
 }
 

@@ -9,7 +9,8 @@ tiled world equals the same update of the untiled world cell for cell
 (DESIGN.md "Multi-GPU").  The per-update schedule is the one documented in
 include/avida_gpu.h ("strip tiles"):
 
-    tile_partials -> all_gather -> tile_begin -> exchange(halo)
+    tile_partials -> all_gather -> tile_steps (K) -> per batch step s < K:
+    [s > 0: tile_partials -> all_gather] -> tile_begin_step -> exchange(halo)
     tile_place(0, 0) (picks, kill times) -> exchange(halo)
     tile_place(0, 3) (cancellations, round-0 claims) -> exchange(halo)
     3 x [tile_place(r, 0) -> exchange(halo)]
@@ -217,10 +218,24 @@ class StripWorld:
         for t in tiles:
             t.call("tile_partials", C.c_void_p(t.part.data_ptr()))
         self.tr.all_gather(tiles)
-        if tiles[0].has_res_rows:
+        # the update's batch steps: the same K on every strip (the gathered
+        # predictors are the same bytes everywhere)
+        k = C.c_int(1)
+        tiles[0].call("tile_steps", C.c_void_p(tiles[0].gathered.data_ptr()), tiles[0].ntiles, C.byref(k))
+        self.steps = k.value
+        for sub in range(k.value):
+            if sub > 0:
+                for t in tiles:
+                    t.call("tile_partials", C.c_void_p(t.part.data_ptr()))
+                self.tr.all_gather(tiles)
+            self._step(sub, k.value)
+
+    def _step(self, sub, nsteps):
+        tiles = self.tiles
+        if tiles[0].has_res_rows and sub == 0:    # the spatial step runs at step 0
             self.tr.exchange(tiles, "resources")
         for t in tiles:
-            t.call("tile_begin", C.c_void_p(t.gathered.data_ptr()), t.ntiles)
+            t.call("tile_begin_step", C.c_void_p(t.gathered.data_ptr()), t.ntiles, sub, nsteps)
         self.tr.exchange(tiles, "halo")
         # round 0: the picks and their kill times, then (with the neighbours'
         # kill times on the edge rows) the cancellations and round 0's

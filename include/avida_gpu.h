@@ -144,12 +144,16 @@ typedef struct avgpu_cfg {
   double divide_uniform_prob;      /* DIVIDE_UNIFORM_PROB */
   int32_t slip_fill_mode;          /* SLIP_FILL_MODE: 0 duplication, 2 random, 3 scrambled,
                                       4 nop-C (1, nop-X, refused) */
-  int32_t sub_updates;             /* batch-model fidelity, no reference knob (DESIGN.md 5
-                                      "Sub-updates"): an update's AVE_TIME_SLICE x N picks
-                                      are made in K = sub_updates batch steps, the scheduler
-                                      weights re-read before each; 0 or 1: one step.  K > 1
-                                      needs SLICING_METHOD 1 and a single world (no strips,
-                                      no handed-in totals) */
+  int32_t sub_updates;             /* batch steps per update, no reference knob (DESIGN.md
+                                      4.2): an update's AVE_TIME_SLICE x N picks are made in
+                                      K batch steps, the scheduler weights re-read before
+                                      each.  0 (default): adaptive -- 6 steps in an update
+                                      whose total weight the previous step's predictor
+                                      (avgpu_update_stats.sched_pred) expects to move by
+                                      more than a tenth (a cohort dividing together), else
+                                      1; K > 0: always K.  K > 1 needs SLICING_METHOD 1 and
+                                      the world's own totals (strips take it through
+                                      avgpu_tile_steps / avgpu_tile_begin_step) */
   double div_mut_prob;             /* DIV_MUT_PROB: per-site substitutions on divide,
                                       Binomial(offspring size, p) of them drawn after the
                                       uniform mutation (cpu/cHardwareBase.cc:447-460) */
@@ -346,6 +350,17 @@ typedef struct avgpu_update_stats {
                                   births_overwritten + births_cancelled + births_dropped) */
   uint64_t seed;               /* the world's RANDOM_SEED, the key of the scheduler's draws: a checkpoint
                                   carries it and avgpu_set_clock restores it with the clock */
+  int64_t sched_pred;          /* the adaptive sub-step predictor of the update's last batch step
+                                  (2^-20 mean weights) and the living organisms it is relative to:
+                                  the next update's step count follows from them (cfg.sub_updates
+                                  0); avgpu_set_clock restores them */
+  int64_t sched_pred_n;
+  int64_t sub_steps;           /* batch steps this update ran */
+  int64_t sched_carry;         /* picks the newborns ran beyond what the organisms they replaced had
+                                  left, still to come out of the next allotment;
+                                  avgpu_set_clock restores it */
+  int64_t insts_wasted;        /* instructions the replaced organisms ran after their newborns' birth
+                                  times (counted in insts_executed) */
 } avgpu_update_stats;
 
 typedef struct avgpu_world avgpu_world;   /* opaque handle */
@@ -582,8 +597,13 @@ int avgpu_set_global_totals(avgpu_world* w, double total_merit, int64_t total_or
  * halo_recv_down from the tile below (same for records):
  *
  *   avgpu_tile_partials(w, part)         all_gather(part) in tile order
- *                                        [exchange(resource rows): spatial resources]
- *   avgpu_tile_begin(w, gathered, T)     exchange(halo)
+ *   avgpu_tile_steps(w, gathered, T, &K) (the update's batch steps; the same K on
+ *                                        every tile)
+ *   for step s = 0 .. K-1:
+ *    [s > 0: avgpu_tile_partials, all_gather(part)]
+ *    [exchange(resource rows): spatial resources]
+ *    avgpu_tile_begin_step(w, gathered, T, s, K)
+ *                                        exchange(halo)
  *   avgpu_tile_place(w, 0, 0)            exchange(halo)
  *   avgpu_tile_place(w, 0, 3)            exchange(halo)
  *   for round 1..3:
@@ -591,7 +611,7 @@ int avgpu_set_global_totals(avgpu_world* w, double total_merit, int64_t total_or
  *   avgpu_tile_place(w, 3, 1)            exchange(records) issued ...
  *   avgpu_tile_place(w, 3, 2)            ... and running beside this launch
  *                                        wait(records)
- *   avgpu_tile_finish(w, stats)
+ *   avgpu_tile_finish(w, stats)          (the step's newborns; stats after the last step)
  *   [avgpu_tile_res_cons(w, cons)        all_reduce(cons, sum): global pools,
  *    avgpu_tile_res_settle(w, cons)      when avgpu_tile_res_cons returned > 0]
  *
@@ -611,10 +631,17 @@ int avgpu_tile_buffer_bytes(avgpu_world* w, int64_t* partial_bytes, int64_t* hal
 int avgpu_set_tile_buffers(avgpu_world* w, void* halo_send_up, void* halo_send_down,
                            void* halo_recv_up, void* halo_recv_down, void* rec_send_up,
                            void* rec_send_down, void* rec_recv_up, void* rec_recv_down);
-/* per-256-cell merit partials, then alive counts (doubles), for the all-gather */
+/* per-256-cell merit partials, then alive counts (doubles), then the tile's
+ * sub-step predictor (int64 bits), for the all-gather */
 int avgpu_tile_partials(avgpu_world* w, double* dev_out);
-/* global totals from the gathered partials (T x partials, tile order), then
- * allotment + interpretation of this tile, occupancy of its edge rows out */
+/* the update's batch steps K from every tile's predictor in the gathered
+ * partials (the single world's rule over the same integer sum; synchronises
+ * with the handle's stream) */
+int avgpu_tile_steps(avgpu_world* w, const double* dev_gathered, int ntiles, int* k_out);
+/* batch step s of K: global totals from the gathered partials (T x partials,
+ * tile order), then allotment + interpretation of this tile, occupancy of its
+ * edge rows out.  avgpu_tile_begin = step 0 of 1. */
+int avgpu_tile_begin_step(avgpu_world* w, const double* dev_gathered, int ntiles, int sub, int k);
 int avgpu_tile_begin(avgpu_world* w, const double* dev_gathered, int ntiles);
 /* placement round 0..3, phase 0: one launch that resolves round - 1 with the
  * claims both strips sent (a cell of an edge row is claimed only from the two

@@ -312,6 +312,29 @@ struct World {
   int n_spatial = 0;
   double* rs_send[2] = {nullptr, nullptr};
   double* rs_recv[2] = {nullptr, nullptr};
+  // the birth-step model: each cell's depletable consumption
+  // in this batch step's main pass, [resource][cell] (credited back when an
+  // offspring replaces the organism); the step's newborns (cell, birth time)
+  std::vector<std::vector<double>> cons_cell;
+  std::vector<std::pair<int64_t, uint32_t>> newborns;
+  // the adaptive sub-step predictor: the last batch step's sum
+  // (2^-20 units) and the living organisms it was relative to; the batch
+  // steps the last update ran
+  int64_t pred_acc = 0, pred_n = 0;
+  int64_t last_k = 1;
+  // the picks the last batch step's newborns took beyond what the organisms
+  // they replaced left (newborn_pass), taken from the next step's allotment;
+  // each cell's instructions in this step's main pass
+  int64_t carry_rem = 0, carry_new = 0;   // the carry not yet taken (all strips alike); this step's own
+  int64_t t_wasted = 0;                    // the replaced organisms' instructions after their newborns' times
+  std::vector<int32_t> ran;
+  // strip tiles: the current batch step (avgpu_tile_begin_step) and the
+  // update's counts summed over its steps
+  int step_sub = 0, step_k = 1;
+  int64_t step_uds = 0;
+  double step_total = 0.0;
+  int64_t acc_placed = 0, acc_dropped = 0, acc_insts = 0, acc_deaths = 0, acc_divides = 0, acc_slices = 0;
+  int64_t acc_overwritten = 0, acc_cancelled = 0;
 };
 
 thread_local std::string g_err;
@@ -345,6 +368,9 @@ struct Exec {
   Org& o;
   int mode;
   bool stop = false;   // TEST mode: gestation finished
+  // the newborn pass (newborn_pass): a viable h-divide is not run -- the
+  // instruction's cycle is taken back and the slice ends before it
+  bool nb_stop = false, nb_halted = false;
   int64_t cur_cell = -1;  // the organism's cell (spatial resources)
   // where the organism's ctx.GetRandom() draws come from: its own stream, or
   // (serial world) the world's single context stream
@@ -766,6 +792,7 @@ struct Exec {
       for (int i = 0; i < 4; i++) o.head[i] = adjust(o.head[i], size());
       return false;
     }
+    if (nb_stop) { nb_halted = true; return false; }
     o.executed_size = exe;       // SetLinesExecuted
     o.child_copied_size = cop;   // SetLinesCopied
     std::vector<uint8_t> child(o.mem.begin() + div_point, o.mem.begin() + div_point + child_size);
@@ -893,6 +920,7 @@ struct Exec {
       if (r.depletable) {
         if (spatial) w.res_amount[res][cur_cell] = level + (-consumed);   // ModifyCell: Rate + State
         else w.res_cons[res] += (uint64_t)(consumed * 4294967296.0);
+        if (mode == AVGPU_MODE_WORLD) w.cons_cell[res][cur_cell] += consumed;   // (newborn credit)
       }
       const double bonus = consumed * r.value;
       if (r.type == AVGPU_PROC_ADD) add += bonus;
@@ -1083,6 +1111,7 @@ struct Exec {
       default: break;
     }
     if (stop) return;
+    if (nb_halted) { o.cpu_cycles_used--; o.time_used--; return; }   // (its executed flag stays: set again when it runs)
     if (o.advance_ip) advance_ip();
     // death (:1045-1049)
     if ((o.max_executed > 0 && o.time_used >= o.max_executed) || o.to_die) o.alive = false;
@@ -1499,6 +1528,7 @@ static void res_init(World& w) {
   w.res_delta.assign(nres, {});
   w.res_global.assign(nres, 0.0);
   w.res_cons.assign(nres, 0);
+  w.cons_cell.assign(nres, std::vector<double>(n, 0.0));
   w.res_first = true;
   for (int r = 0; r < nres; r++) {
     const avgpu_resource& q = w.res[r];
@@ -1794,6 +1824,11 @@ int orc_set_clock(void* h, const avgpu_update_stats* last) {
     w.cfg.seed = last->seed;
     w.stats.seed = last->seed;
   }
+  // the adaptive sub-step predictor the next update decides by (0: one step)
+  w.pred_acc = last->sched_pred;
+  w.pred_n = last->sched_pred_n;
+  w.carry_rem = last->sched_carry;
+  w.carry_new = 0;
   return 0;
 }
 
@@ -1995,7 +2030,7 @@ static void res_end(World& w) {
 
 // 1. allotment (cScheduler restated; DESIGN.md "Scheduler") + 2. interpretation
 // PROBABILISTIC: the update's picks split down the cell tree (block_split);
-// INTEGRATED: lambda = UD * weight / total weight with a credit carry;
+// INTEGRATED: lambda = UD * weight / total with a credit carry;
 // CONSTANT: AVE_TIME_SLICE.  A divide stamps its birth record
 // with its time in the update, t = k / (b + 1) in 1/2^16 (k: the slice's
 // instructions up to and including the h-divide, b: the slice's budget) --
@@ -2006,10 +2041,41 @@ static inline uint32_t birth_time(int k, int budget) {
   return (uint32_t)(((double)k * 65536.0) / (double)((int64_t)budget + 1));
 }
 
+// The adaptive sub-step predictor, one organism's term at the
+// end of its slice: an organism expected to reach its divide within the next
+// update's share of picks (its gestation time, or for one that never divided
+// its genome length, against the cycles of its current gestation) changes the
+// scheduler's total weight by its merit's change at the divide plus its
+// offspring against an average victim, from that point of the update on --
+// the within-update weight change the batch step reads only once
+// (main/cPopulation.cc:610-615 AdjustSchedule at every divide).  In units of
+// the mean weight, 2^-20 fixed point (an order-free sum).  Organisms that
+// divided in this slice are left out (their next divide is a gestation away).
+// The device's pred_term (interp.hip) is the same arithmetic.
+static int64_t pred_term(const World& w, const Org& o, double total, int64_t nalive) {
+  const double wbar = total / (double)nalive;
+  const double wi = o.merit;
+  if (!(wi > 0.0) || !(wi <= 1.7976931348623157e308) || !(wbar > 0.0)) return 0;
+  const double e = ((double)w.cfg.ave_time_slice * wi) / wbar;
+  const int G = o.gestation_time > 0 ? o.gestation_time : o.genome_length;
+  const double r = (double)(G - (o.time_used - o.gestation_start));
+  if (!(r <= e * 1.25)) return 0;
+  const double t = r <= 0.0 ? 0.0 : std::fmin(r / e, 1.0);
+  int sz = o.genome_length;
+  if (sz > o.copied_size) sz = o.copied_size;
+  if (sz > o.executed_size) sz = o.executed_size;
+  const double m = o.gestation_time > 0 ? wi : (double)sz * o.cur_bonus;
+  double term = (((m - wi) + (m - wbar)) * (1.0 - t)) / wbar;
+  if (!(term <= 1.0e6)) term = 1.0e6;
+  if (!(term >= -1.0e6)) term = -1.0e6;
+  return (int64_t)(term * 1048576.0);
+}
+
 // blk: each of this world's blocks' share of the update's picks (top_tree),
 // total: the total weight, ud: the update size (INTEGRATED's lambda =
-// ud * weight / total)
-static void allot_interpret(World& w, const std::vector<int64_t>& blk, double total, double ud) {
+// ud * weight / total), nalive: the living organisms the weights are over
+// (the predictor's mean weight)
+static void allot_interpret(World& w, const std::vector<int64_t>& blk, double total, double ud, int64_t nalive) {
   std::vector<int32_t> budget(w.ncells, 0);
   const bool consts = w.cfg.slicing_method == AVGPU_SLICE_CONSTANT || !(total > 0.0);
   if (!consts && w.cfg.slicing_method != AVGPU_SLICE_INTEGRATED)
@@ -2034,21 +2100,85 @@ static void allot_interpret(World& w, const std::vector<int64_t>& blk, double to
   for (int64_t c = 0; c < w.ncells; c++) w.t_slices += budget[c] > 0;
   w.last_budget = budget;
   w.births.clear();
+  for (auto& v : w.cons_cell) std::fill(v.begin(), v.end(), 0.0);
+  w.pred_acc = 0;
+  w.pred_n = nalive;
+  w.ran.assign(w.ncells, 0);
   int64_t insts = 0, deaths = 0, divides = 0;
   for (int64_t c = 0; c < w.ncells; c++) {
     Org& o = w.orgs[c];
     if (!o.alive) continue;
     Exec ex{w, o, AVGPU_MODE_WORLD};
     int d0 = o.num_divides;
+    const int tu0 = o.time_used;
     for (int k = 0; k < budget[c] && o.alive; k++) {
       const size_t nb0 = w.births.size();
       ex.single_process(c); insts++;
+      w.ran[c]++;
       if (w.births.size() != nb0) w.births.back().t = birth_time(k + 1, budget[c]);
     }
     divides += o.num_divides - d0;
     if (!o.alive) deaths++;
+    else if (budget[c] > 0 && o.gestation_start <= tu0 && total > 0.0 && nalive > 0)
+      w.pred_acc += pred_term(w, o, total, nalive);
   }
   w.t_insts = insts; w.t_deaths = deaths; w.t_divides = divides;
+}
+
+// The newborns of a batch step (the reference places an
+// offspring inside its parent's divide and schedules it for the rest of that
+// update, main/cPopulation.cc:621-952): each activated offspring first gives
+// back what the organism it replaced consumed in this step's main pass after
+// the birth -- (1 - t) of the cell's depletable consumption -- and then runs
+// its own share of the step's remaining picks, Binomial(round(UD_s (1 - t)),
+// weight / total) from a stateless node draw of its global cell, stopping
+// before an h-divide (its offspring would need a placement this step has
+// already done).  The device's k_activate / newborn pass (world.hip,
+// interp.hip NB) run the same.
+enum : uint32_t { SALT_NEWBORN = 0x4E3B0A17u };
+static int64_t newborn_budget(const World& w, int64_t cell, uint32_t t, int64_t uds, double total) {
+  const Org& o = w.orgs[cell];
+  if (!(total > 0.0) || uds <= 0) return 0;
+  const double f = (double)(0x10000u - t) * (1.0 / 65536.0);
+  const int64_t n = (int64_t)std::floor((double)uds * f + 0.5);
+  const double p = sched_weight(o) / total;
+  int64_t b = binom_draw(n, p, node_draw(w, w.sched_key, SALT_NEWBORN, (uint64_t)(w.cell0 + cell)));
+  return std::min<int64_t>(b, (1 << 30) - 1);
+}
+static void newborn_credit(World& w, int64_t cell, uint32_t t) {
+  const double f = (double)(0x10000u - t) * (1.0 / 65536.0);
+  for (size_t r = 0; r < w.res.size(); r++) {
+    const double v = w.cons_cell[r][cell];
+    if (v == 0.0) continue;
+    const double back = v * f;
+    if (w.res[r].geometry != AVGPU_RES_GLOBAL) w.res_amount[r][cell] = w.res_amount[r][cell] + back;
+    else w.res_cons[r] -= (uint64_t)(back * 4294967296.0);
+  }
+}
+static void newborn_pass(World& w, int64_t uds, double total) {
+  int64_t insts = 0, deaths = 0;
+  for (const auto& nb : w.newborns) {
+    const int64_t c = nb.first;
+    if (!w.res.empty()) newborn_credit(w, c, nb.second);
+    Org& o = w.orgs[c];
+    const int64_t bud = newborn_budget(w, c, nb.second, uds, total);
+    const int64_t left = (int64_t)((double)w.ran[c] * ((double)(0x10000u - nb.second) * (1.0 / 65536.0)));
+    w.carry_new += bud - left;
+    w.t_wasted += left;
+    if (bud <= 0) continue;
+    w.t_slices++;
+    Exec ex{w, o, AVGPU_MODE_WORLD};
+    ex.nb_stop = true;
+    for (int64_t k = 0; k < bud && o.alive; k++) {
+      ex.single_process(c);
+      if (ex.nb_halted) break;
+      insts++;
+    }
+    if (!o.alive) deaths++;
+  }
+  w.newborns.clear();
+  w.t_insts += insts;
+  w.t_deaths += deaths;
 }
 
 // 5. statistics (main/cStats.cc:1081-1100 inputs)
@@ -2085,6 +2215,12 @@ static void finish_stats(World& w, int64_t placed, int64_t dropped) {
   st.births_overwritten = w.t_overwritten;
   st.births_cancelled = w.t_cancelled;
   st.seed = w.cfg.seed;
+  st.sched_pred = w.pred_acc;
+  st.sched_pred_n = w.pred_n;
+  st.sub_steps = w.last_k;
+  st.sched_carry = w.carry_rem + w.carry_new;
+  st.insts_wasted = w.t_wasted;
+  w.t_wasted = 0;
   w.t_overwritten = 0;
   w.t_cancelled = 0;
   w.update++;
@@ -2265,7 +2401,7 @@ static void place_finish_single(World& w, int64_t& placed_out, int64_t& dropped_
       const uint64_t c3 = w.claim_r[3][b.target];
       own = w.owner[b.target] == i && !(c3 != 0 && key_time(c3) >= b.t);
     }
-    if (own) { activate_child(w, b, b.target); w.orgs[b.target].hstart = 0x10000u - b.t; placed++; }
+    if (own) { activate_child(w, b, b.target); w.newborns.push_back({b.target, b.t}); placed++; }
     else if (st == BS_CANCELLED) cancelled++;
     else if (st <= BS_NO_CELL) dropped++;
     else overwritten++;
@@ -2278,14 +2414,17 @@ static void place_finish_single(World& w, int64_t& placed_out, int64_t& dropped_
 
 }  // extern "C++"
 
-// Sub-updates (avgpu_cfg.sub_updates = K, DESIGN.md 5 "Sub-updates"): the
-// update's UD picks are made in K consecutive batch steps of
-// floor(UD (s + 1) / K) - floor(UD s / K) picks each, the weights re-read
-// before each one -- the reference re-weights its scheduler at every divide
-// (cPopulation::ActivateOffspring -> AdjustSchedule, main/cPopulation.cc:
-// 621-952), so K steps bring the batch model's weight refresh K times closer
-// to it.  Resources step once per update (at sub-update 0); global
-// consumption settles after each sub-update; K = 1 is the plain batch update.
+// Sub-steps: an update's UD picks are made in K consecutive
+// batch steps of floor(UD (s + 1) / K) - floor(UD s / K) picks each, the
+// weights re-read before each one -- the reference re-weights its scheduler
+// at every divide (cPopulation::ActivateOffspring -> AdjustSchedule,
+// main/cPopulation.cc:621-952).  avgpu_cfg.sub_updates = K > 0 fixes K;
+// 0 (the default) chooses it per update from the previous step's predictor
+// (pred_term): more steps the more the total weight is expected to move
+// within the update (a cohort reaching its divides together: the lock-step
+// start of injected or loaded organisms), one step below a tenth.  Resources
+// step once per update (at sub-step 0); global consumption settles after each
+// step.
 // cPhenotype::IncAge for every living organism (UpdateOrganismStats,
 // main/cPopulation.cc:6021, at the end of each update): here at the start of
 // the next, so that Org::age is the reference's age DURING the update --
@@ -2295,19 +2434,47 @@ static void age_tick(World& w) {
   for (int64_t c = 0; c < w.ncells; c++) if (w.orgs[c].alive) w.orgs[c].age++;
 }
 
-static inline int sub_updates_of(const avgpu_cfg& c) { return c.sub_updates > 1 ? c.sub_updates : 1; }
 static inline int64_t sub_share(int64_t n, int s, int K) {
   return K == 1 ? n : (n * (s + 1)) / K - (n * s) / K;
 }
+// The picks the last batch step's newborns ran beyond what the organisms they
+// replaced had left after their births (newborn_pass) come out of the next
+// step's allotment, so that an update's picks stay the reference's UD
+// (newborns into empty cells take picks from the living there, as the
+// reference's scheduler gives a newborn its share of the remaining picks);
+// a negative carry (victims left more) adds picks.  `fresh`: the summed new
+// carry of every strip (the single world's own); returns the picks to take
+// from the step's n_root (at most n_root either way; the rest waits).
+static int64_t take_carry(World& w, int64_t fresh, int64_t n_root) {
+  w.carry_rem += fresh;
+  w.carry_new = 0;
+  const int64_t take = std::min(std::max<int64_t>(w.carry_rem, -n_root), n_root);
+  w.carry_rem -= take;
+  return take;
+}
+// the update's batch steps (the device's choose_k, capi.hip): sub_updates
+// when set; else, with E = |predictor| in mean weights per organism, one step
+// for E <= 0.1 and ceil(E / 0.05) steps (2 .. ADAPT_KMAX) above -- the
+// within-step weight change each step leaves is then about 0.05
+static constexpr int ADAPT_KMAX = 16;
+static int choose_k(const avgpu_cfg& c, int64_t pred, int64_t n, bool handed_in) {
+  if (c.sub_updates > 0) return c.sub_updates;
+  if (handed_in || c.slicing_method != AVGPU_SLICE_PROBABILISTIC) return 1;
+  const double a = (double)(pred < 0 ? -pred : pred);
+  if (!(n > 0 && a > 104857.6 * (double)n)) return 1;
+  const int k = (int)std::ceil(a / (52428.8 * (double)n));
+  return std::max(2, std::min(k, ADAPT_KMAX));
+}
 
 // Batch-synchronous world update: the exact semantics the device implements
-// (DESIGN.md "Update semantics"): allot -> interpret -> place births -> stats.
+// (DESIGN.md "Update semantics"): allot -> interpret -> place births ->
+// newborns -> stats.
 static int run_update_impl(World& w) {
   if (w.cfg.birth_method == 5)
     return fail(AVGPU_EUNSUPPORTED, "BIRTH_METHOD 5 (the reaper queue) runs on the serial world only");
-  const int K = sub_updates_of(w.cfg);
+  const int K = choose_k(w.cfg, w.pred_acc, w.pred_n, w.have_global);
   if (K > 1 && w.have_global)
-    return fail(AVGPU_EUNSUPPORTED, "sub_updates > 1 needs the world's own totals (no handed-in totals, no strips)");
+    return fail(AVGPU_EUNSUPPORTED, "sub_updates > 1 needs the world's own totals (no handed-in totals)");
   int64_t placed = 0, dropped = 0, insts = 0, deaths = 0, divides = 0, slices = 0;
   w.t_overwritten = 0;
   w.t_cancelled = 0;
@@ -2319,20 +2486,22 @@ static int run_update_impl(World& w) {
     const double local = top_tree(w, part, -1, 0, 0, nullptr);
     const double ave = (double)w.cfg.ave_time_slice;
     double total = local, ud = ave * (double)n_alive;
+    int64_t n_all = n_alive;
     int64_t n_root = (int64_t)w.cfg.ave_time_slice * n_alive;
     if (w.have_global) {   // cMultiProcessWorld::CalculateUpdateSize (main/cMultiProcessWorld.cc:396-405)
       total = w.global_merit;
       ud = ave * (double)w.global_orgs;
+      n_all = w.global_orgs;
       n_root = total > 0.0 ? (int64_t)((local / total) * ave * (double)w.global_orgs) : 0;
     }
     n_root = sub_share(n_root, sub, K);
+    n_root -= take_carry(w, w.carry_new, n_root);
     std::vector<int64_t> blk;
     top_tree(w, part, n_root, 0, (int64_t)part.size(), &blk);
     if (sub == 0) res_begin(w);   // resources step once per update, at its start
     if (sub == 0) age_tick(w);
-    allot_interpret(w, blk, total, ud);
+    allot_interpret(w, blk, total, ud, n_all);
     insts += w.t_insts; deaths += w.t_deaths; divides += w.t_divides; slices += w.t_slices;
-    res_end(w);
     const int64_t nbirth = (int64_t)w.births.size();
     place_reset(w, w.ncells);
     // launch 0: picks, kill times
@@ -2366,8 +2535,14 @@ static int run_update_impl(World& w) {
       }
     }
     place_finish_single(w, placed, dropped);
+    // the newborns' credit and their share of the step (newborn_pass)
+    w.t_insts = 0; w.t_deaths = 0; w.t_slices = 0;
+    newborn_pass(w, sub_share((int64_t)ud, sub, K), total);
+    insts += w.t_insts; deaths += w.t_deaths; slices += w.t_slices;
+    res_end(w);
   }
   w.t_insts = insts; w.t_deaths = deaths; w.t_divides = divides; w.t_slices = slices;
+  w.last_k = K;
   finish_stats(w, placed, dropped);
   return 0;
 }
@@ -2483,7 +2658,7 @@ int orc_tile_res_settle(void* h, const uint64_t* sum) {
 int orc_tile_buffer_bytes(void* h, int64_t* part, int64_t* halo, int64_t* rec) {
   World& w = *(World*)h;
   const int X = w.cfg.world_x;
-  if (part) *part = 2 * ((w.ncells + 255) / 256) * 8;
+  if (part) *part = (2 * ((w.ncells + 255) / 256) + 2) * 8;
   if (halo) *halo = halo_bytes_of(X);
   if (rec) *rec = (int64_t)sizeof(HaloHdr) + (int64_t)X * (int64_t)sizeof(HaloRec) + w.r_arena;
   return 0;
@@ -2511,6 +2686,10 @@ int orc_tile_partials(void* h, double* out) {
     for (int i = 0; i < 256; i++) cnt += (b * 256 + i < w.ncells && w.orgs[b * 256 + i].alive) ? 1 : 0;
     out[nb + b] = (double)cnt;
   }
+  // the predictor of the strip's last batch step (its bits), summed by
+  // avgpu_tile_steps on every strip
+  memcpy(out + 2 * nb, &w.pred_acc, 8);
+  memcpy(out + 2 * nb + 1, &w.carry_new, 8);
   // edge rows of the spatial amounts for the neighbours' flow step
   const int X = w.cfg.world_x;
   if (w.tiled && w.rs_send[0])
@@ -2525,26 +2704,55 @@ int orc_tile_partials(void* h, double* out) {
   return 0;
 }
 
-int orc_tile_begin(void* h, const double* gathered, int ntiles) {
+// the update's batch steps from every strip's predictor in the gathered
+// partials (the single world's choose_k over the same integer sum)
+int orc_tile_steps(void* h, const double* gathered, int ntiles, int* k_out) {
+  World& w = *(World*)h;
+  const int64_t nb = (w.ncells + 255) / 256, stride = 2 * nb + 2;
+  int64_t sum = 0;
+  for (int k = 0; k < ntiles; k++) {
+    int64_t v;
+    memcpy(&v, gathered + k * stride + 2 * nb, 8);
+    sum += v;
+  }
+  if (k_out) *k_out = choose_k(w.cfg, sum, w.pred_n, false);
+  return 0;
+}
+
+int orc_tile_begin_step(void* h, const double* gathered, int ntiles, int sub, int K) {
   World& w = *(World*)h;
   if (!tile_ok(w)) return fail(AVGPU_ESTATE, "not a strip tile with buffers");
-  if (sub_updates_of(w.cfg) > 1) return fail(AVGPU_EUNSUPPORTED, "sub_updates > 1 on strip tiles");
-  w.sched_key = (uint32_t)w.update;
-  age_tick(w);
+  if (K < 1 || sub < 0 || sub >= K) return fail(AVGPU_EINVAL, "batch step sub of K");
+  w.sched_key = (uint32_t)w.update * (uint32_t)K + (uint32_t)sub;
+  if (sub == 0) {
+    age_tick(w);
+    w.acc_placed = w.acc_dropped = w.acc_insts = w.acc_deaths = w.acc_divides = w.acc_slices = 0;
+    w.acc_overwritten = w.acc_cancelled = 0;
+  }
   // the top tree over every strip's block partials (tile order = block order)
-  const int64_t nb = (w.ncells + 255) / 256;
+  const int64_t nb = (w.ncells + 255) / 256, stride = 2 * nb + 2;
   std::vector<double> leaf((size_t)(nb * ntiles));
-  int64_t cnt = 0;
-  for (int k = 0; k < ntiles; k++)
+  int64_t cnt = 0, fresh = 0;
+  for (int k = 0; k < ntiles; k++) {
     for (int64_t j = 0; j < nb; j++) {
-      leaf[k * nb + j] = gathered[k * 2 * nb + j];
-      cnt += (int64_t)gathered[k * 2 * nb + nb + j];
+      leaf[k * nb + j] = gathered[k * stride + j];
+      cnt += (int64_t)gathered[k * stride + nb + j];
     }
+    int64_t v;
+    memcpy(&v, gathered + k * stride + 2 * nb + 1, 8);
+    fresh += v;
+  }
   std::vector<int64_t> blk;
-  const double total = top_tree(w, leaf, (int64_t)w.cfg.ave_time_slice * cnt, w.cell0 / 256, nb, &blk);
+  const int64_t ud = (int64_t)w.cfg.ave_time_slice * cnt;
+  int64_t n_root = sub_share(ud, sub, K);
+  n_root -= take_carry(w, fresh, n_root);
+  const double total = top_tree(w, leaf, n_root, w.cell0 / 256, nb, &blk);
   if (w.n_spatial && !w.rs_recv[0]) return fail(AVGPU_ESTATE, "spatial resources need the tile resource buffers");
-  res_begin(w);
-  allot_interpret(w, blk, total, (double)w.cfg.ave_time_slice * (double)cnt);
+  if (sub == 0) res_begin(w);
+  allot_interpret(w, blk, total, (double)w.cfg.ave_time_slice * (double)cnt, cnt);
+  w.step_sub = sub; w.step_k = K;
+  w.step_uds = sub_share(ud, sub, K);
+  w.step_total = total;
   const int X = w.cfg.world_x;
   place_reset(w, w.ncells + 2 * X);
   for (int d = 0; d < 2; d++)
@@ -2553,9 +2761,11 @@ int orc_tile_begin(void* h, const double* gathered, int ntiles) {
       for (int k = 0; k < 4; k++) hcl(w.h_send[d], X, k >> 1, k & 1)[x] = 0;
       hkt(w.h_send[d], X)[x] = 0;
     }
-  w.t_placed = 0; w.t_overwritten = 0;
+  w.t_placed = 0; w.t_overwritten = 0; w.t_dropped = 0;
   return 0;
 }
+
+int orc_tile_begin(void* h, const double* gathered, int ntiles) { return orc_tile_begin_step(h, gathered, ntiles, 0, 1); }
 
 namespace {
 // the halo slot of a cell: direction, column, ghost row (else edge row)
@@ -2689,7 +2899,7 @@ int orc_tile_place(void* h, int round, int phase) {
       const int8_t st = w.bstate[i];
       const bool won = st >= BS_WON && st < BS_WON + 4 && w.owner[b.target] == i;
       if (won && b.target >= w.ncells) continue;   // shipped to the neighbour
-      if (won) { activate_child(w, b, b.target); w.orgs[b.target].hstart = 0x10000u - b.t; placed++; }
+      if (won) { activate_child(w, b, b.target); w.newborns.push_back({b.target, b.t}); placed++; }
       else if (st == BS_CANCELLED) cancelled++;
       else if (st <= BS_NO_CELL) nocell++;
       else overwritten++;                          // placed, then overwritten (run_update_impl)
@@ -2754,12 +2964,24 @@ int orc_tile_finish(void* h, avgpu_update_stats* out) {
       for (int t = 0; t < AVGPU_NUM_LOGIC_TASKS; t++) b.last_task[t] = r.last_task[t];
       b.rng.lo = r.rng_lo; b.rng.hi = r.rng_hi; b.rng.ctr = r.rng_ctr;
       activate_child(w, b, c);
-      w.orgs[c].hstart = 0x10000u - r.t;
+      w.newborns.push_back({c, r.t});
       placed++;
     }
   }
-  w.t_overwritten = overwritten;
-  finish_stats(w, placed, dropped);
+  // the step's newborns, the update's counts over its steps
+  const int64_t mi = w.t_insts, md = w.t_deaths, ms = w.t_slices;
+  w.t_insts = 0; w.t_deaths = 0; w.t_slices = 0;
+  newborn_pass(w, w.step_uds, w.step_total);
+  w.acc_insts += mi + w.t_insts; w.acc_deaths += md + w.t_deaths; w.acc_slices += ms + w.t_slices;
+  w.acc_divides += w.t_divides;
+  w.acc_placed += placed; w.acc_dropped += dropped;
+  w.acc_overwritten += overwritten; w.acc_cancelled += w.t_cancelled;
+  if (w.step_sub == w.step_k - 1) {
+    w.t_insts = w.acc_insts; w.t_deaths = w.acc_deaths; w.t_slices = w.acc_slices; w.t_divides = w.acc_divides;
+    w.t_overwritten = w.acc_overwritten; w.t_cancelled = w.acc_cancelled;
+    w.last_k = w.step_k;
+    finish_stats(w, w.acc_placed, w.acc_dropped);
+  }
   if (out) *out = w.stats;
   return 0;
 }

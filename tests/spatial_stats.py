@@ -11,9 +11,13 @@ for one of the worlds:
 * "serial"   -- the oracle's serial world: the reference's own schedule (a
                 merit-weighted pick per instruction, speculative run-ahead,
                 births placed inside the divide; DESIGN.md 5c);
-* "batchK"   -- the batch world with K sub-updates per update (K = 1: the
-                product's update, the bench's; DESIGN.md 5), on the oracle;
+* "batchK"   -- the batch world with avgpu_cfg.sub_updates = K (K = 0: the
+                product's default, adaptive batch steps), on
+                the oracle;
 * "gpuK"     -- the same batch world on the GPU (libavida_gpu.so).
+
+Also recorded: average.dat's merit, gestation time and fitness at the printed
+updates.
 """
 from __future__ import annotations
 
@@ -75,8 +79,13 @@ def _make(kind):
     return mk
 
 
+AVG = (0, 1, 2)                # average.dat columns Merit, Gestation Time, Fitness
+AVG_NAMES = ("merit", "gestation", "fitness")
+
+
 def run_seed(kind, seed):
-    """(Or count after each update 0..100, printed columns [10][6])"""
+    """(Or count after each update 0..100, printed columns [10][6],
+    average.dat columns [10][3])"""
     from avida_amd import driver
     with tempfile.TemporaryDirectory() as d:
         drv = driver.Driver(CFG, d, make_world=_make(kind), seed=seed)
@@ -84,16 +93,30 @@ def run_seed(kind, seed):
         tr = list(drv.world.trace)
         drv.world.close()
         t, r = rows(os.path.join(d, "tasks.dat")), rows(os.path.join(d, "resource.dat"))
-    return tr, [[t[u][c] for c in TASKS] + [r[u][c] for c in RES] for u in PRINTED]
+        a = rows(os.path.join(d, "average.dat"))
+    return (tr, [[t[u][c] for c in TASKS] + [r[u][c] for c in RES] for u in PRINTED],
+            [[a[u][c] for c in AVG] for u in PRINTED])
 
 
 def _one(args):
     return run_seed(*args)
 
 
-@functools.lru_cache(maxsize=None)
 def runs(kind, nseeds, workers=8):
-    """seeds 1..nseeds of a world: (traces [n][101], printed [n][10][6]).
+    """seeds 1..nseeds of a world: (traces [n][101], printed [n][10][6])"""
+    tr, pr, _ = _runs(kind, nseeds, workers)
+    return tr, pr
+
+
+def average_runs(kind, nseeds, workers=8):
+    """seeds 1..nseeds: (traces [n][101], average.dat columns [n][10][3])"""
+    tr, _, av = _runs(kind, nseeds, workers)
+    return tr, av
+
+
+@functools.lru_cache(maxsize=None)
+def _runs(kind, nseeds, workers=8):
+    """seeds 1..nseeds of a world: (traces, printed, averages).
     Oracle worlds run in the workers of a fork server (a fresh process: no
     GPU context is inherited), GPU worlds in threads of this process (each
     world has its own HIP stream)."""
@@ -104,7 +127,8 @@ def runs(kind, nseeds, workers=8):
     else:
         with ProcessPoolExecutor(workers, mp_context=multiprocessing.get_context("forkserver")) as ex:
             out = list(ex.map(_one, args, chunksize=8))
-    return np.array([o[0] for o in out]), np.array([o[1] for o in out], dtype=float)
+    return (np.array([o[0] for o in out]), np.array([o[1] for o in out], dtype=float),
+            np.array([o[2] for o in out], dtype=float))
 
 
 def discovery(traces):
@@ -139,6 +163,22 @@ def trajectory_tests(a_pr, b_pr):
             x, y = a_pr[:, j, c], b_pr[:, j, c]
             p = 1.0 if (np.all(x == x[0]) and np.all(y == x[0])) else float(stats.ks_2samp(x, y).pvalue)
             out.append((f"{name} at update {u}", p))
+    return out
+
+
+def average_tests(a_av, b_av):
+    """Welch t and two-sample KS of average.dat's merit, gestation time and
+    fitness at every printed update: [(name, p)] (60 tests)"""
+    from scipy import stats
+    out = []
+    for j, u in enumerate(PRINTED):
+        for c, name in enumerate(AVG_NAMES):
+            x, y = a_av[:, j, c], b_av[:, j, c]
+            if np.all(x == x[0]) and np.all(y == x[0]):
+                out += [(f"{name} at update {u} (Welch)", 1.0), (f"{name} at update {u} (KS)", 1.0)]
+                continue
+            out.append((f"{name} at update {u} (Welch)", float(stats.ttest_ind(x, y, equal_var=False).pvalue)))
+            out.append((f"{name} at update {u} (KS)", float(stats.ks_2samp(x, y).pvalue)))
     return out
 
 

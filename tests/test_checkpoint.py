@@ -70,7 +70,7 @@ def test_oracle_checkpoint_resume(golden, tmp_path, env_kind):
 
 def test_older_checkpoint_formats_load(golden, tmp_path):
     """A checkpoint written before round 4 (stats without births_cancelled /
-    seed) and round 5 (state records without `age`) loads: the missing
+    seed, or round 6's sub-step predictor and pick carry) and round 5 (state records without `age`) loads: the missing
     fields are zero -- the world's configured seed stays, every organism's
     age is 0 -- and the world continues."""
     import ctypes as C
@@ -87,7 +87,7 @@ def test_older_checkpoint_formats_load(golden, tmp_path):
     raw = z["states"].tobytes()
     old = b"".join(raw[k * size:k * size + off] + raw[k * size + off + 8:(k + 1) * size] for k in range(n))
     z["states"] = np.frombuffer(old, dtype=np.uint8)
-    z["stats"] = z["stats"][:C.sizeof(capi.AvgpuUpdateStats) - 16]      # no births_cancelled, seed
+    z["stats"] = z["stats"][:capi.AvgpuUpdateStats.births_cancelled.offset]   # no births_cancelled, seed, ...
     for k in ("version", "state_size", "stats_size"):
         z.pop(k)
     old_path = os.path.join(tmp_path, "old.npz")

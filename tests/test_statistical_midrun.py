@@ -17,12 +17,14 @@ merit, gestation time and fitness -- with the seed distribution:
 * the GPU serial world (avgpu_run_serial_updates: the same schedule run by
   the product's interpreter, bit-exact with the oracle's serial world --
   tests/test_serial_gpu.py): the same tolerance;
-* the batch world (the product's update, DESIGN.md section 5: the
+* the batch world (the product's update, DESIGN.md 4: the
   scheduler's multinomial picks, time-ordered placement with cancelled
-  divides, the newborns' head start), on the oracle and on the GPU (bit for
-  bit the same world), 32 seeds: the same tolerance, 3 sd + 1 %, at every
-  printed update -- update 5 included, where the loaded population reaches
-  its first divides in lock step.
+  divides, the newborn pass, adaptive batch steps), on the oracle and on the
+  GPU (bit for bit the same world), 32 seeds: the same tolerance, 3 sd + 1 %,
+  at every printed update -- update 5 included, where the loaded population
+  reaches its first divides in lock step;
+* the product world against the serial world, two-sample tests over 192
+  seeds each (test_product_world_vs_serial_world_midrun).
 """
 import ctypes as C
 import os
@@ -123,3 +125,21 @@ def test_oracle_batch_world_midrun(golden, tmp_path):
 def test_gpu_batch_world_midrun(golden, tmp_path):
     _check_batch(_ref(golden), _run(golden, tmp_path, lambda cfg, iset, env: driver.ProductWorld(cfg, iset, env),
                                     range(1, 33)))
+
+
+def test_product_world_vs_serial_world_midrun():
+    """The product's world (the batch world at its default: adaptive batch
+    steps, the newborn pass) against the reference's
+    schedule (the oracle's serial world), 192 seeds each: Welch t and KS of
+    the nine task-organism counts and average merit, gestation time and
+    fitness at every printed update 5..30, Bonferroni at a family-wise 0.01.
+    The loaded population divides in lock-step waves (updates 5-6, 11-12,
+    17-18, ...): measured at 256 seeds the smallest p is 7e-4 (update 5,
+    threshold 7e-5)."""
+    import midrun_stats as ms
+    b = ms.runs("batch0", 192)
+    s = ms.runs("serial", 192)
+    res = ms.two_sample_tests(b, s)
+    thr = 0.01 / len(res)
+    bad = [(n, p) for n, p in res if p <= thr]
+    assert not bad, f"p <= {thr:.2e}: {bad}"

@@ -22,7 +22,7 @@ MODE_WORLD, MODE_TEST, MODE_FROZEN = 0, 1, 2
  CNT_LANESTEPS, CNT_C0_SLICES, CNT_C0_SITES, CNT_CLK_STAGE, CNT_CLK_LOOP, CNT_CLK_WB,
  CNT_ITERS, CNT_IT_FAST, CNT_IT_COPY, CNT_IT_SLOW, CNT_WAVES, CNT_HALO_SENT,
  CNT_HALO_LOST, CNT_REC_EXHAUSTED, CNT_OVERSIZE, CNT_SUB_OVERFLOW, CNT_MEM_CAP,
- CNT_OVERWRITTEN, CNT_CANCELLED, CNT_BAD_RECORD) = range(27)
+ CNT_OVERWRITTEN, CNT_CANCELLED, CNT_BAD_RECORD, CNT_WASTED, CNT_STEPS) = range(29)
 RNG_COUNTER, RNG_RECORDED = 0, 1
 NUM_COUNTERS = 48
 

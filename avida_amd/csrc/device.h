@@ -399,6 +399,7 @@ enum { SEG_OSLIP = 0, SEG_PSLIP, SEG_SSLIP, SEG_TTRANS, SEG_PTRANS, SEG_STRANS, 
 #define CNT_CANCELLED 25  /* records whose parent's cell got an offspring before their divide (never placed) */
 #define CNT_BAD_RECORD 26 /* record / cell fields out of range where used as an index (guarded; must be 0) */
 #define CNT_WASTED 27     /* instructions replaced organisms ran after their newborns' birth times */
+#define CNT_STEPS 28      /* batch steps (k_block_counts, one per step) */
 // 32..37: AVGPU_PHASE_CLOCKS loop cycles by block (decode, fast, copy, switch,
 // wave phase, advance); 38..43: slow-switch cycles in pop, push, IO, h-alloc,
 // h-divide, h-search/if-label

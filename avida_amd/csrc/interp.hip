@@ -1968,7 +1968,7 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
     if (ndrop) count_add(W, CNT_DROPPED, (unsigned long long)ndrop);
     if (nover) count_add(W, CNT_OVERSIZE, (unsigned long long)nover);
     if (REC && nrover) count_add(W, CNT_REC_OVER, (unsigned long long)nrover);
-    if (S == CLASS0_SIZE) {   // everything the class-0 launch runs: its windows, list blocks, in-wave spills
+    if (S == CLASS0_SIZE && !NB) {   // everything the class-0 launch runs: its windows, list blocks, in-wave spills
       count_add(W, CNT_C0_SLICES, (unsigned long long)sl);
       count_add(W, CNT_C0_SITES, (unsigned long long)sites);
     }

@@ -552,6 +552,7 @@ __global__ __launch_bounds__(1024) void k_block_counts(DevWorld W, const double*
       W.sched[1] = 0;
       W.sched[2] = rem;
       W.sched[0] = 0;                         // this step's predictor (interp.hip pred_term)
+      count_add(W, CNT_STEPS, 1ull);
     }
     cnt[1] = nroot;
   }

@@ -381,6 +381,7 @@ void update(std::vector<Tile>& tiles, Transport& tr, hipStream_t s) {
 struct Args {
   std::string config = ".";
   int side = 1024, strips = 1, updates = 50, burn_in = 150, gpus = 1;
+  int sub_updates = 0;       // avgpu_cfg.sub_updates (0: adaptive batch steps)
   uint64_t seed = 101;
   bool untiled = false;
   bool rccl = false;         // RCCL even for one rank
@@ -399,12 +400,14 @@ Args parse(int argc, char** argv) {
     else if (k == "--burn-in") a.burn_in = atoi(val().c_str());
     else if (k == "--seed") a.seed = strtoull(val().c_str(), nullptr, 10);
     else if (k == "--gpus") a.gpus = atoi(val().c_str());
+    else if (k == "--sub-updates") a.sub_updates = atoi(val().c_str());
     else if (k == "--untiled") a.untiled = true;
     else if (k == "--rccl") a.rccl = true;
     else if (k == "--independent") a.independent = true;
     else if (k == "--help" || k == "-h") {
       printf("usage: avgpu_strips --config DIR [--side N] [--strips T] [--updates U] [--burn-in B]\n"
-             "                    [--seed S] [--gpus N] [--untiled] [--rccl] [--independent]\n");
+             "                    [--seed S] [--gpus N] [--untiled] [--rccl] [--independent]\n"
+             "                    [--sub-updates K]\n");
       exit(0);
     } else die("unknown option " + k);
   }
@@ -503,6 +506,7 @@ int main(int argc, char** argv) {
   cfg.world_x = (int32_t)side;
   cfg.world_y = (int32_t)(side * T);
   cfg.seed = a.seed + (a.independent ? (uint64_t)rank : 0);   // independent worlds: a run per seed
+  cfg.sub_updates = a.sub_updates;
 
   std::vector<Tile> tiles(local_tiles);
   for (int k = 0; k < local_tiles; k++) {

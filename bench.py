@@ -123,7 +123,7 @@ def environment(files, golden, kind, X, Y):
 
 
 def build_world(lib, capi, files, golden, side, seed, device, rank, world, on_tile=None, env_kind="logic9",
-                sub_updates=1):
+                sub_updates=0):
     """One 1024x1024 strip per rank of a side x (side*world) torus (world = 1:
     the untiled side x side world).  on_tile(h) places the strip before the
     organisms are injected (their RNG streams are keyed by global cell id)."""
@@ -265,9 +265,10 @@ def main():
     ap.add_argument("--cpu-procs", type=int, default=0,
                     help="CPU baseline processes (0: min(16, host CPUs) -- 16 is a GPU box's share)")
     ap.add_argument("--cpu-worker", action="store_true", help=argparse.SUPPRESS)
-    ap.add_argument("--sub-updates", type=int, default=1,
-                    help="batch steps per update (avgpu_cfg.sub_updates, DESIGN.md 5): 1 is the "
-                         "product's update; K > 1 re-reads the scheduler weights K times per update")
+    ap.add_argument("--sub-updates", type=int, default=0,
+                    help="batch steps per update (avgpu_cfg.sub_updates, DESIGN.md 4.2): 0 is the "
+                         "product's default (adaptive: more steps in an update whose total weight "
+                         "is expected to move); K > 0 always K steps")
     ap.add_argument("--long-updates", type=int, default=200,
                     help="after the K timed steps, a second untimed-by-contract run of this many "
                          "updates reported as config.long_run (stability cross-check; 0 = off)")
@@ -317,6 +318,16 @@ def main():
 
     capi.check(lib, lib.avgpu_set_timing(h, args.time_every))
 
+    def ref_insts():
+        """cumulative organism-instructions of the reference's semantics:
+        executed, less those replaced organisms ran after their newborns'
+        births"""
+        st = capi.AvgpuUpdateStats()
+        capi.check(lib, lib.avgpu_get_stats(h, C.byref(st)))
+        cnt = (C.c_int64 * capi.NUM_COUNTERS)()
+        capi.check(lib, lib.avgpu_counters(h, 1, cnt, capi.NUM_COUNTERS))
+        return st.cum_insts_executed - cnt[capi.CNT_WASTED]
+
     def update():
         if strips:
             strips.update()      # halo-birth exchange + gathered scheduler totals over RCCL
@@ -349,7 +360,11 @@ def main():
     capi.check(lib, lib.avgpu_kernel_times(h, cms, C.byref(phases)))
     cnt1 = (C.c_int64 * capi.NUM_COUNTERS)()
     capi.check(lib, lib.avgpu_counters(h, 1, cnt1, capi.NUM_COUNTERS))
-    insts = s1.cum_insts_executed - s0.cum_insts_executed
+    d = [cnt1[k] - cnt0[k] for k in range(capi.NUM_COUNTERS)]
+    # the organism-instructions of the reference's semantics: every executed
+    # instruction (main pass + newborn pass) but those an organism ran after
+    # the birth of the offspring that replaced it
+    insts = (s1.cum_insts_executed - s0.cum_insts_executed) - d[capi.CNT_WASTED]
     births = s1.cum_births - s0.cum_births
     dt = t1 - t0
     vec = torch.tensor([dt, float(insts), float(births), float(s1.num_organisms)],
@@ -362,14 +377,13 @@ def main():
     else:
         dt_max = vec[0].item()
     tot_insts, tot_births, tot_orgs = vec[1].item(), vec[2].item(), vec[3].item()
-    d = [cnt1[k] - cnt0[k] for k in range(capi.NUM_COUNTERS)]
     nph = max(1, phases.value)
     # offspring never placed (birth-queue overflow, oversize, full halo arena:
     # placement itself places every birth), offspring placed and then
     # overwritten by a later birth into the same cell, and slices handed to a
     # larger LDS class, summed over ranks
     extra = torch.tensor([float(d[capi.CNT_DROPPED]), float(d[capi.CNT_SPILLS]),
-                          float(d[capi.CNT_OVERWRITTEN])],
+                          float(d[capi.CNT_OVERWRITTEN]), float(d[capi.CNT_WASTED])],
                          dtype=torch.float64, device=rdev)
     if dist:
         dist.all_reduce(extra)
@@ -377,8 +391,7 @@ def main():
     if args.long_updates > 0:
         # stability cross-check outside the contract's timed region: the same
         # updates, many more of them, under the same barrier / max-over-ranks clock
-        ls0 = capi.AvgpuUpdateStats()
-        capi.check(lib, lib.avgpu_get_stats(h, C.byref(ls0)))
+        li0 = ref_insts()
         if dist:
             dist.barrier()
         torch.cuda.synchronize()
@@ -389,9 +402,7 @@ def main():
         if dist:
             dist.barrier()
         ldt = torch.tensor([time.perf_counter() - l0], dtype=torch.float64, device=rdev)
-        ls1 = capi.AvgpuUpdateStats()
-        capi.check(lib, lib.avgpu_get_stats(h, C.byref(ls1)))
-        lins = torch.tensor([float(ls1.cum_insts_executed - ls0.cum_insts_executed)],
+        lins = torch.tensor([float(ref_insts() - li0)],
                             dtype=torch.float64, device=rdev)
         if dist:
             dist.all_reduce(ldt, op=dist.ReduceOp.MAX)
@@ -407,8 +418,7 @@ def main():
         # (its cost: 20 updates without it, then 20 with it, back to back, so
         # that the population's drift since the timed region cancels)
         nst = 20
-        ss0 = capi.AvgpuUpdateStats()
-        capi.check(lib, lib.avgpu_get_stats(h, C.byref(ss0)))
+        si0 = ref_insts()
         ptr = C.c_void_p()
         torch.cuda.synchronize()
         p0 = time.perf_counter()
@@ -422,9 +432,7 @@ def main():
             capi.check(lib, lib.avgpu_stats_vector(h, C.byref(ptr)))
         torch.cuda.synchronize()
         qdt = time.perf_counter() - q0
-        ss1 = capi.AvgpuUpdateStats()
-        capi.check(lib, lib.avgpu_get_stats(h, C.byref(ss1)))
-        stats_run = {"updates": nst, "value": (ss1.cum_insts_executed - ss0.cum_insts_executed) / (pdt + qdt),
+        stats_run = {"updates": nst, "value": (ref_insts() - si0) / (pdt + qdt),
                      "ms_per_step": qdt * 1e3 / nst, "ms_per_step_without": pdt * 1e3 / nst,
                      "stats_ms_per_update": (qdt - pdt) * 1e3 / nst}
     if rank != 0:
@@ -438,9 +446,9 @@ def main():
     # over its HIP-event-timed average duration on the world's stream.
     c0_ms = cms[0] / nph
     # counters run over every update of the timed region (one class-0 launch
-    # per batch step, sub_updates steps per update); the events only over
-    # every time_every-th launch
-    launches = args.steps * max(1, args.sub_updates)
+    # per batch step -- the newborn pass's is not counted); the events only
+    # over every time_every-th launch
+    launches = max(1, d[capi.CNT_STEPS])
     c0_slices = d[capi.CNT_C0_SLICES] / launches
     c0_sites = d[capi.CNT_C0_SITES] / launches
     bytes_per_launch = 2.0 * STATE_BYTES * c0_slices + SITE_BYTES * c0_sites
@@ -450,7 +458,7 @@ def main():
         with open(PMC_FILE) as f:
             pmc = json.load(f)
         same_build = pmc.get("lib_sha16") == capi.lib_build_hash()
-        if pmc.get("world") == f"{args.side}x{args.side}" and args.env == "logic9" and args.sub_updates <= 1:
+        if pmc.get("world") == f"{args.side}x{args.side}" and args.env == "logic9":
             if same_build:
                 traffic = pmc["hbm_bytes_per_launch"]
                 traffic_src = pmc["source"]
@@ -490,11 +498,13 @@ def main():
             "births_overwritten_per_update": extra[2].item() / args.steps,
             "spills_per_update": extra[1].item() / args.steps,
             "insts_per_update": tot_insts / args.steps,
+            "insts_wasted_per_update": extra[3].item() / args.steps,
             "parallelism": f"strips{world}",
             "transport": ("gloo-staged rehearsal (ranks share GPUs; not a scaling measurement)" if staged
                           else ("rccl" if world > 1 else "none")),
             "ranks": world,
-            "sub_updates": max(1, args.sub_updates),
+            "sub_updates": args.sub_updates,
+            "batch_steps_per_update": d[capi.CNT_STEPS] / args.steps,
             "long_run": long_run,
             # the timed updates run without the per-update statistics reduction;
             # stats_every_update_run: the same updates with it (its cost per update)

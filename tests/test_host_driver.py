@@ -37,7 +37,8 @@ def test_host_driver_strips_equal_untiled():
     assert loop["digest_rank0"] == flat["digest_rank0"], (loop, flat)
     assert loop["organisms"] == flat["organisms"]
     # one rank of cMultiProcessWorld-style independent worlds: RCCL all-reduce
-    # of the scheduler totals on the world's stream, == the untiled world
-    one = _run(*common, "--strips", "1", "--untiled")
-    rccl = _run(*common, "--rccl", "--independent")
+    # of the scheduler totals on the world's stream, == the untiled world (one
+    # batch step per update: handed-in totals take no adaptive steps)
+    one = _run(*common, "--strips", "1", "--untiled", "--sub-updates", "1")
+    rccl = _run(*common, "--rccl", "--independent", "--sub-updates", "1")
     assert rccl["ranks"] == 1 and rccl["digest_rank0"] == one["digest_rank0"], (rccl, one)

@@ -88,7 +88,7 @@ struct avgpu_world {
   long long* d_pred = nullptr;   // its device address
   hipEvent_t ev_pred = nullptr;
   bool pred_pending = false;
-  long long pred_acc = 0, pred_n = 0;
+  long long pred_acc = 0, pred_n = 0, pred_cnt = 0;
   int last_k = 1;
   int tile_sub = 0, tile_k = 1, tile_sub_next = 0;
   uint32_t tile_key = 0;
@@ -172,7 +172,7 @@ int setup_world(avgpu_world* w, int64_t n, bool test_buffers) {
   // occupancy, owners and the four placement rounds' claims, each with the two
   // ghost rows a strip tile keeps after its n cells
   const int64_t ng = n + 2 * (int64_t)c.world_x;
-  A(occ, ng); A(claim, ng); A(claim2, ng); A(owner, ng); A(killt, n); A(sdone, n); A(ran, n); A(sched, 4);
+  A(occ, ng); A(claim, ng); A(claim2, ng); A(owner, ng); A(killt, n); A(sdone, n); A(ran, n); A(sched, 8);
   W.claim_r[0] = W.claim; W.claim_r[1] = W.claim2;
   A(claim_r[2], ng); A(claim_r[3], ng); A(b_tgt, 4 * R);
   if (c.birth_method == 4) {
@@ -204,7 +204,7 @@ int setup_world(avgpu_world* w, int64_t n, bool test_buffers) {
   while (W.tree_cap < nb) W.tree_cap <<= 1;
   if ((rc = w->alloc(&W.tree_scr, (size_t)(2 * W.tree_cap)))) return rc;
   if ((rc = w->alloc(&W.tree_cnt, (size_t)(2 * W.tree_cap)))) return rc;
-  if ((rc = w->alloc(&w->d_stats, (size_t)(40 + 24 * nb)))) return rc;
+  if ((rc = w->alloc(&w->d_stats, (size_t)(41 + 24 * nb)))) return rc;
 #undef A
   w->has_test_buffers = test_buffers;
   // config scalars
@@ -371,11 +371,11 @@ avgpu_world* create_world(const avgpu_cfg* cfg, int device, int64_t n, bool test
       hipEventCreateWithFlags(&w->ev_join[2], hipEventDisableTiming) != hipSuccess ||
       hipEventCreate(&w->ev0) != hipSuccess || hipEventCreate(&w->ev1) != hipSuccess ||
       hipEventCreateWithFlags(&w->ev_pred, hipEventDisableTiming) != hipSuccess ||
-      hipHostMalloc((void**)&w->h_pred, 2 * sizeof(long long), hipHostMallocMapped) != hipSuccess ||
+      hipHostMalloc((void**)&w->h_pred, 3 * sizeof(long long), hipHostMallocMapped) != hipSuccess ||
       hipHostGetDevicePointer((void**)&w->d_pred, w->h_pred, 0) != hipSuccess) {
     delete w; fail(AVGPU_EHIP, "stream/event creation failed"); return nullptr;
   }
-  w->h_pred[0] = w->h_pred[1] = 0;
+  w->h_pred[0] = w->h_pred[1] = w->h_pred[2] = 0;
   w->stream = w->own_stream;
   for (int i = 0; i < avgpu_world::RING; i++) {
     for (int k = 0; k <= NUM_CLASSES; k++)
@@ -528,17 +528,21 @@ int interpret(avgpu_world* w, int mode, int64_t first, int64_t count, bool sorte
 int update_run(avgpu_world* w, const double* dev_totals, avgpu_update_stats* out);
 
 // An update's batch steps (oracle choose_k): avgpu_cfg.sub_updates
-// when set; else, with E the last step's predictor in mean weights per
-// organism (the total weight's expected move within the update), one step for
-// E <= 0.1 and ceil(E / 0.05) steps (2 .. ADAPT_KMAX) above.
+// when set; else the more of two rules over the last step's predictor: with E
+// its weight term in mean weights per organism (the total weight's expected
+// move within the update), ceil(E / 0.05) steps above E = 0.1; with D the
+// fraction of organisms it expects to divide within the update (a cohort in
+// lock step), ceil(D / 0.15) steps above D = 0.3; one step otherwise, at most
+// ADAPT_KMAX.
 constexpr int ADAPT_KMAX = 16;
-int choose_k(const avgpu_cfg& c, long long pred, long long n, bool handed_in) {
+int choose_k(const avgpu_cfg& c, long long pred, long long n, bool handed_in, long long cnt) {
   if (c.sub_updates > 0) return c.sub_updates;
-  if (handed_in || c.slicing_method != AVGPU_SLICE_PROBABILISTIC) return 1;
-  const double a = (double)(pred < 0 ? -pred : pred);
-  if (!(n > 0 && a > 104857.6 * (double)n)) return 1;
-  const int k = (int)std::ceil(a / (52428.8 * (double)n));
-  return std::max(2, std::min(k, ADAPT_KMAX));
+  if (handed_in || c.slicing_method != AVGPU_SLICE_PROBABILISTIC || n <= 0) return 1;
+  const double a = (double)(pred < 0 ? -pred : pred), dn = (double)n;
+  int k = 1;
+  if (a > 104857.6 * dn) k = std::max(k, (int)std::ceil(a / (52428.8 * dn)));
+  if ((double)cnt > 0.3 * dn) k = std::max(k, (int)std::ceil((double)cnt / (0.15 * dn)));
+  return std::min(k, ADAPT_KMAX);
 }
 
 }  // namespace
@@ -856,9 +860,10 @@ int avgpu_run_update(avgpu_world* w, avgpu_update_stats* out) {
     HIPCHK(hipEventSynchronize(w->ev_pred));
     w->pred_acc = w->h_pred[0];
     w->pred_n = w->h_pred[1];
+    w->pred_cnt = w->h_pred[2];
     w->pred_pending = false;
   }
-  const int K = choose_k(w->cfg, w->pred_acc, w->pred_n, false);
+  const int K = choose_k(w->cfg, w->pred_acc, w->pred_n, false, w->pred_cnt);
   for (int sub = 0; sub < K; sub++) {
     const uint32_t key = (uint32_t)w->update * (uint32_t)K + (uint32_t)sub;
     launch_world_begin(w->W, w->stream, w->d_totals, w->d_totals + 8, w->ev_fork, key, sub, K);
@@ -990,7 +995,7 @@ int avgpu_run_updates(avgpu_world* w, int n, avgpu_update_stats* last) {
 
 int avgpu_get_stats(avgpu_world* w, avgpu_update_stats* out) {
   if (!w || !out) return fail(AVGPU_EINVAL, "args");
-  double v[40];
+  double v[41];
   if (w->stats_stale) {
     launch_stats(w->W, w->stream, w->d_stats);
     HIPCHK(hipGetLastError());
@@ -1025,6 +1030,7 @@ int avgpu_get_stats(avgpu_world* w, avgpu_update_stats* out) {
   memcpy(&out->sched_pred, v + 37, 8);        // (int64 bits)
   memcpy(&out->sched_carry, v + 38, 8);
   out->sched_pred_n = (int64_t)v[39];
+  memcpy(&out->sched_pred_cnt, v + 40, 8);
   out->sub_steps = w->last_k;
   return 0;
 }
@@ -1196,8 +1202,9 @@ int avgpu_set_clock(avgpu_world* w, const avgpu_update_stats* last) {
   // the batch-step predictor and the pick carry
   w->pred_acc = last->sched_pred;
   w->pred_n = last->sched_pred_n;
+  w->pred_cnt = last->sched_pred_cnt;
   w->pred_pending = false;
-  const long long sv[3] = {last->sched_pred, 0, last->sched_carry};
+  const long long sv[4] = {last->sched_pred, 0, last->sched_carry, last->sched_pred_cnt};
   HIPCHK(hipMemcpyAsync(w->W.sched, sv, sizeof(sv), hipMemcpyHostToDevice, w->stream));
   const double nv = (double)last->sched_pred_n;
   HIPCHK(hipMemcpyAsync(w->d_totals + 1, &nv, sizeof(nv), hipMemcpyHostToDevice, w->stream));
@@ -1571,20 +1578,22 @@ int avgpu_tile_steps(avgpu_world* w, const double* dev_gathered, int ntiles, int
   if (rc < 0) return rc;
   if (!dev_gathered || ntiles < 1 || !k_out) return fail(AVGPU_EINVAL, "gathered partials / k_out");
   const int64_t nb = (w->W.n + 255) / 256, stride = tile_part_stride(nb);
-  std::vector<double> tail((size_t)(2 * ntiles));
+  std::vector<double> tail((size_t)(3 * ntiles));
   for (int k = 0; k < ntiles; k++)
-    HIPCHK(hipMemcpyAsync(tail.data() + 2 * k, dev_gathered + k * stride + 2 * nb, 2 * sizeof(double),
+    HIPCHK(hipMemcpyAsync(tail.data() + 3 * k, dev_gathered + k * stride + 2 * nb, 3 * sizeof(double),
                           hipMemcpyDeviceToHost, w->stream));
   double n = 0.0;
   HIPCHK(hipMemcpyAsync(&n, w->d_totals + 1, sizeof(double), hipMemcpyDeviceToHost, w->stream));
   HIPCHK(hipStreamSynchronize(w->stream));
-  long long sum = 0;
+  long long sum = 0, cnt = 0;
   for (int k = 0; k < ntiles; k++) {
-    long long v;
-    memcpy(&v, tail.data() + 2 * k, 8);
+    long long v, c;
+    memcpy(&v, tail.data() + 3 * k, 8);
+    memcpy(&c, tail.data() + 3 * k + 2, 8);
     sum += v;
+    cnt += c;
   }
-  *k_out = choose_k(w->cfg, sum, (long long)n, false);
+  *k_out = choose_k(w->cfg, sum, (long long)n, false, cnt);
   return 0;
 }
 

@@ -328,14 +328,18 @@ struct DevWorld {
   double* cons;       // [n_res][n] its depletable consumption in that pass (k_allot zeroes; env_resources)
   // [0] the sub-step predictor of this step's main pass (2^-20 mean weights,
   // k_block_counts zeroes it), [1] this step's pick carry (newborn picks beyond
-  // their victims' leftovers, k_activate), [2] the carry not yet taken
+  // their victims' leftovers, k_activate), [2] the carry not yet taken (taken
+  // at an update's first step), [3] the organisms of this step's main pass
+  // expected to divide within the next update (zeroed with [0]), [4] the
+  // update's UD (AVE_TIME_SLICE x the organisms at its first step)
   long long* sched;
   const double* totals;   // the step's totals (k_block_counts): [1] organisms, [2] weight total, [3] UD
 };
 
 // a strip's partials vector (avgpu_tile_partials): nb block partials, nb alive
-// counts, its sub-step predictor and its pick carry (int64 bits)
-__host__ __device__ inline int64_t tile_part_stride(int64_t nb) { return 2 * nb + 2; }
+// counts, its sub-step predictor, its pick carry and its predictor's divide
+// count (int64 bits)
+__host__ __device__ inline int64_t tile_part_stride(int64_t nb) { return 2 * nb + 3; }
 // owner of a cell won by a neighbouring strip's offspring in round k at birth time t
 #define REMOTE_OWNER(k, t) (-2 - ((k) + 4 * (int)(t)))
 // halo buffer: per round parity X u64 claims on the receiver's edge row and X

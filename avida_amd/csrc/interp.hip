@@ -223,11 +223,12 @@ __host__ __device__ constexpr int tape_stride(int S) { return S == CLASS0_SIZE ?
 
 // The adaptive sub-step predictor's term of one organism at the end of its
 // slice (oracle pred_term, the same IEEE operations): an
-// organism expected to divide within the next update's share of picks moves
-// the total weight by its merit's change plus its offspring against an
-// average victim from that point on, in mean weights, 2^-20 fixed point.
+// organism expected to divide within the next update's share of picks is
+// counted (imm) and moves the total weight by twice its merit's change at the
+// divide (its own and its offspring's, which replaces a relative of about its
+// old merit) from that point on, in mean weights, 2^-20 fixed point.
 __device__ __forceinline__ long long pred_term(const DevWorld& W, int cell, int tu, int gs, int blen, int dcop,
-                                               int dexe, double bonus) {
+                                               int dexe, double bonus, bool& imm) {
   const double total = W.totals[2], n = W.totals[1];
   if (!(total > 0.0) || !(n > 0.0)) return 0;
   const double wbar = __ddiv_rn(total, n);
@@ -238,12 +239,13 @@ __device__ __forceinline__ long long pred_term(const DevWorld& W, int cell, int 
   const int G = gt > 0 ? gt : blen;
   const double r = (double)(G - (tu - gs));
   if (!(r <= __dmul_rn(e, 1.25))) return 0;
+  imm = true;
   const double t = r <= 0.0 ? 0.0 : fmin(__ddiv_rn(r, e), 1.0);
   int sz = blen;
   if (sz > dcop) sz = dcop;
   if (sz > dexe) sz = dexe;
   const double m = gt > 0 ? wi : __dmul_rn((double)sz, bonus);
-  double term = __ddiv_rn(__dmul_rn(__dadd_rn(__dsub_rn(m, wi), __dsub_rn(m, wbar)), __dsub_rn(1.0, t)), wbar);
+  double term = __ddiv_rn(__dmul_rn(__dadd_rn(__dsub_rn(m, wi), __dsub_rn(m, wi)), __dsub_rn(1.0, t)), wbar);
   if (!(term <= 1.0e6)) term = 1.0e6;
   if (!(term >= -1.0e6)) term = -1.0e6;
   return (long long)__dmul_rn(term, 1048576.0);
@@ -280,7 +282,8 @@ __device__ __forceinline__ int edit_word(int kind, int a, int b) { return kind |
 // class 0 takes its organisms from list row 0 (k_activate), and a viable
 // h-divide is not run -- its cycle is taken back and the slice ends before it.
 // pred: a world update's main pass, whose slices add their sub-step
-// predictor terms (pred_term) to W.sched[0].
+// predictor terms (pred_term) to W.sched[0] and count the organisms expected
+// to divide within the next update into W.sched[3].
 template <int S, bool REC, bool C0W = false, bool SIMPLE = false, bool DEF = false, bool RES = false,
           bool MIX = false, bool NB = false>
 __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, int cls_arg, int mode_arg,
@@ -1936,10 +1939,13 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
   // step's main pass to its slice's end, alive, without a divide in it
   if (pred) {
     long long pt = 0;
+    bool imm = false;
     if (active && !(fl & (F_DEAD | F_SPILL)) && alive0 && gs <= tu - executed - sdone)
-      pt = pred_term(W, cell, tu, gs, blen, dcop, dexe, bonus);
+      pt = pred_term(W, cell, tu, gs, blen, dcop, dexe, bonus, imm);
     for (int off = 32; off > 0; off >>= 1) pt += __shfl_xor(pt, off);
+    const unsigned long long ni = __popcll(__ballot(imm));
     if (lane == 0 && pt) atomicAdd(reinterpret_cast<unsigned long long*>(W.sched), (unsigned long long)pt);
+    if (lane == 0 && ni) atomicAdd(reinterpret_cast<unsigned long long*>(W.sched + 3), ni);
   }
   // counters: one atomic per wave
   unsigned long long e = (unsigned long long)executed;

@@ -411,11 +411,12 @@ __global__ __launch_bounds__(256) void k_merit_partial(DevWorld W, double* parti
                                                        double* alive_d, int reset) {
   if (reset == 1 && blockIdx.x == 0) reset_counts_block(W);
   if (reset == 2 && blockIdx.x == 0) reset_queues_block(W);
-  // a strip's partials end with its last step's predictor and pick carry
-  // (the oracle's orc_tile_partials; summed on every strip after the gather)
-  if (alive_d && blockIdx.x == 0 && threadIdx.x < 2) {
+  // a strip's partials end with its last step's predictor, pick carry and
+  // divide count (the oracle's orc_tile_partials; summed on every strip after
+  // the gather)
+  if (alive_d && blockIdx.x == 0 && threadIdx.x < 3) {
     const int64_t nbl = (W.n + 255) / 256;
-    partial[2 * nbl + threadIdx.x] = __longlong_as_double(W.sched[threadIdx.x]);
+    partial[2 * nbl + threadIdx.x] = __longlong_as_double(W.sched[threadIdx.x == 2 ? 3 : threadIdx.x]);
   }
   const int lane = threadIdx.x & 63;
   const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -524,7 +525,10 @@ __global__ __launch_bounds__(1024) void k_block_counts(DevWorld W, const double*
     const long long n = s_cnt[0];
     const double root = scr[1];
     const double ave = (double)W.ave_time_slice;
-    long long nroot = sub_share((long long)W.ave_time_slice * n, sub, nsub);
+    // the update's UD = AVE_TIME_SLICE x the organisms at its start
+    // (cAvidaDriver's update loop; W.sched[4]), a step's share of that
+    if (sub == 0 && mode != 2) W.sched[4] = (long long)W.ave_time_slice * n;
+    long long nroot = sub_share(W.sched[4], sub, nsub);
     if (mode == 2) {
       const double tot = totals[0];
       nroot = tot > 0.0 ? (long long)__dmul_rn(__dmul_rn(__ddiv_rn(root, tot), ave), totals[1]) : 0;
@@ -534,24 +538,27 @@ __global__ __launch_bounds__(1024) void k_block_counts(DevWorld W, const double*
       totals[0] = root;
       totals[1] = (double)n;
       totals[2] = root;
-      totals[3] = __dmul_rn(ave, (double)n);
+      totals[3] = (double)W.sched[4];
     }
     if (mode != 3) {
-      // the picks the last step's newborns ran beyond their victims'
-      // leftovers come out of this step (oracle take_carry): a strip sums
-      // every strip's carry from the gathered partials
+      // the picks the last steps' newborns ran beyond their victims'
+      // leftovers come out of an update's first step (oracle take_carry): a
+      // strip sums every strip's carry from the gathered partials
       long long fresh = W.sched[1];
       if (mode == 1) {
         fresh = 0;
         for (int k = 0; k < ntiles; k++) fresh += __double_as_longlong(part[k * tile_part_stride(nb) + 2 * nb + 1]);
       }
       long long rem = W.sched[2] + fresh;
-      const long long take = min(max(rem, -nroot), nroot);
-      rem -= take;
-      nroot -= take;
+      if (sub == 0) {
+        const long long take = min(max(rem, -nroot), nroot);
+        rem -= take;
+        nroot -= take;
+      }
       W.sched[1] = 0;
       W.sched[2] = rem;
       W.sched[0] = 0;                         // this step's predictor (interp.hip pred_term)
+      W.sched[3] = 0;
       count_add(W, CNT_STEPS, 1ull);
     }
     cnt[1] = nroot;
@@ -1265,6 +1272,7 @@ __global__ void k_place_claim0(DevWorld W, long long* pred_out) {
   if (pred_out && blockIdx.x == 0 && threadIdx.x == 0) {
     pred_out[0] = W.sched[0];
     pred_out[1] = (long long)W.totals[1];
+    pred_out[2] = W.sched[3];
   }
   QUEUE_LOOP(q) {
     const int64_t r = rec_of(W, q);
@@ -1736,7 +1744,7 @@ __global__ __launch_bounds__(64) void k_activate_remote(DevWorld W, uint32_t key
 // 6 generation 7 memory size 8..16 task organisms
 #define NPART 24
 #define NUSED (8 + AVGPU_NUM_LOGIC_TASKS)
-#define NSTAT 40
+#define NSTAT 41
 __device__ __forceinline__ double wave_sum(double v) {
   for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
   return v;
@@ -1867,6 +1875,7 @@ __global__ __launch_bounds__(256) void k_stats_final(DevWorld W, const double* p
     out[37] = __longlong_as_double(W.sched[0]);             // the predictor (bits)
     out[38] = __longlong_as_double(W.sched[1] + W.sched[2]); // the pick carry (bits)
     out[39] = W.totals[1];                                  // the organisms it is relative to
+    out[40] = __longlong_as_double(W.sched[3]);             // the predictor's divide count (bits)
   }
 }
 

@@ -147,11 +147,12 @@ typedef struct avgpu_cfg {
   int32_t sub_updates;             /* batch steps per update, no reference knob (DESIGN.md
                                       4.2): an update's AVE_TIME_SLICE x N picks are made in
                                       K batch steps, the scheduler weights re-read before
-                                      each.  0 (default): adaptive -- 6 steps in an update
-                                      whose total weight the previous step's predictor
-                                      (avgpu_update_stats.sched_pred) expects to move by
-                                      more than a tenth (a cohort dividing together), else
-                                      1; K > 0: always K.  K > 1 needs SLICING_METHOD 1 and
+                                      each.  0 (default): adaptive -- from the previous
+                                      step's predictor (avgpu_update_stats.sched_pred*),
+                                      more steps the more the total weight is expected to
+                                      move within the update or the more organisms are
+                                      expected to divide in it (a cohort in lock step),
+                                      else 1; K > 0: always K.  K > 1 needs SLICING_METHOD 1 and
                                       the world's own totals (strips take it through
                                       avgpu_tile_steps / avgpu_tile_begin_step) */
   double div_mut_prob;             /* DIV_MUT_PROB: per-site substitutions on divide,
@@ -361,6 +362,8 @@ typedef struct avgpu_update_stats {
                                   avgpu_set_clock restores it */
   int64_t insts_wasted;        /* instructions the replaced organisms ran after their newborns' birth
                                   times (counted in insts_executed) */
+  int64_t sched_pred_cnt;      /* organisms the predictor expects to divide within the next update
+                                  (avgpu_set_clock restores it) */
 } avgpu_update_stats;
 
 typedef struct avgpu_world avgpu_world;   /* opaque handle */

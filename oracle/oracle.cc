@@ -320,7 +320,7 @@ struct World {
   // the adaptive sub-step predictor: the last batch step's sum
   // (2^-20 units) and the living organisms it was relative to; the batch
   // steps the last update ran
-  int64_t pred_acc = 0, pred_n = 0;
+  int64_t pred_acc = 0, pred_n = 0, pred_cnt = 0;
   int64_t last_k = 1;
   // the picks the last batch step's newborns took beyond what the organisms
   // they replaced left (newborn_pass), taken from the next step's allotment;
@@ -332,6 +332,7 @@ struct World {
   // update's counts summed over its steps
   int step_sub = 0, step_k = 1;
   int64_t step_uds = 0;
+  int64_t upd_ud = 0;      // the update's picks UD, fixed at its first batch step
   double step_total = 0.0;
   int64_t acc_placed = 0, acc_dropped = 0, acc_insts = 0, acc_deaths = 0, acc_divides = 0, acc_slices = 0;
   int64_t acc_overwritten = 0, acc_cancelled = 0;
@@ -1829,6 +1830,7 @@ int orc_set_clock(void* h, const avgpu_update_stats* last) {
   w.pred_n = last->sched_pred_n;
   w.carry_rem = last->sched_carry;
   w.carry_new = 0;
+  w.pred_cnt = last->sched_pred_cnt;
   return 0;
 }
 
@@ -2044,15 +2046,18 @@ static inline uint32_t birth_time(int k, int budget) {
 // The adaptive sub-step predictor, one organism's term at the
 // end of its slice: an organism expected to reach its divide within the next
 // update's share of picks (its gestation time, or for one that never divided
-// its genome length, against the cycles of its current gestation) changes the
-// scheduler's total weight by its merit's change at the divide plus its
-// offspring against an average victim, from that point of the update on --
-// the within-update weight change the batch step reads only once
+// its genome length, against the cycles of its current gestation) is counted
+// (the divide density), and it changes the scheduler's total weight by its
+// merit's change at the divide (its size times its bonus so far, for one
+// that never divided; else its merit stays) and by as much again through its
+// offspring, which takes the merit to a neighbour's cell (a relative's, of
+// about its old merit) -- from that point of the update on: the
+// within-update weight change the batch step reads only once
 // (main/cPopulation.cc:610-615 AdjustSchedule at every divide).  In units of
 // the mean weight, 2^-20 fixed point (an order-free sum).  Organisms that
 // divided in this slice are left out (their next divide is a gestation away).
 // The device's pred_term (interp.hip) is the same arithmetic.
-static int64_t pred_term(const World& w, const Org& o, double total, int64_t nalive) {
+static int64_t pred_term(const World& w, const Org& o, double total, int64_t nalive, int64_t& cnt) {
   const double wbar = total / (double)nalive;
   const double wi = o.merit;
   if (!(wi > 0.0) || !(wi <= 1.7976931348623157e308) || !(wbar > 0.0)) return 0;
@@ -2060,12 +2065,13 @@ static int64_t pred_term(const World& w, const Org& o, double total, int64_t nal
   const int G = o.gestation_time > 0 ? o.gestation_time : o.genome_length;
   const double r = (double)(G - (o.time_used - o.gestation_start));
   if (!(r <= e * 1.25)) return 0;
+  cnt++;
   const double t = r <= 0.0 ? 0.0 : std::fmin(r / e, 1.0);
   int sz = o.genome_length;
   if (sz > o.copied_size) sz = o.copied_size;
   if (sz > o.executed_size) sz = o.executed_size;
   const double m = o.gestation_time > 0 ? wi : (double)sz * o.cur_bonus;
-  double term = (((m - wi) + (m - wbar)) * (1.0 - t)) / wbar;
+  double term = (((m - wi) + (m - wi)) * (1.0 - t)) / wbar;
   if (!(term <= 1.0e6)) term = 1.0e6;
   if (!(term >= -1.0e6)) term = -1.0e6;
   return (int64_t)(term * 1048576.0);
@@ -2102,6 +2108,7 @@ static void allot_interpret(World& w, const std::vector<int64_t>& blk, double to
   w.births.clear();
   for (auto& v : w.cons_cell) std::fill(v.begin(), v.end(), 0.0);
   w.pred_acc = 0;
+  w.pred_cnt = 0;
   w.pred_n = nalive;
   w.ran.assign(w.ncells, 0);
   int64_t insts = 0, deaths = 0, divides = 0;
@@ -2120,7 +2127,7 @@ static void allot_interpret(World& w, const std::vector<int64_t>& blk, double to
     divides += o.num_divides - d0;
     if (!o.alive) deaths++;
     else if (budget[c] > 0 && o.gestation_start <= tu0 && total > 0.0 && nalive > 0)
-      w.pred_acc += pred_term(w, o, total, nalive);
+      w.pred_acc += pred_term(w, o, total, nalive, w.pred_cnt);
   }
   w.t_insts = insts; w.t_deaths = deaths; w.t_divides = divides;
 }
@@ -2219,6 +2226,7 @@ static void finish_stats(World& w, int64_t placed, int64_t dropped) {
   st.sched_pred_n = w.pred_n;
   st.sub_steps = w.last_k;
   st.sched_carry = w.carry_rem + w.carry_new;
+  st.sched_pred_cnt = w.pred_cnt;
   st.insts_wasted = w.t_wasted;
   w.t_wasted = 0;
   w.t_overwritten = 0;
@@ -2439,31 +2447,37 @@ static inline int64_t sub_share(int64_t n, int s, int K) {
 }
 // The picks the last batch step's newborns ran beyond what the organisms they
 // replaced had left after their births (newborn_pass) come out of the next
-// step's allotment, so that an update's picks stay the reference's UD
+// update's first step's allotment (taken within the update, from steps whose
+// weights are older than the births, it starved the organisms that had not
+// divided yet), so that the updates' picks stay the reference's UD
 // (newborns into empty cells take picks from the living there, as the
 // reference's scheduler gives a newborn its share of the remaining picks);
 // a negative carry (victims left more) adds picks.  `fresh`: the summed new
 // carry of every strip (the single world's own); returns the picks to take
 // from the step's n_root (at most n_root either way; the rest waits).
-static int64_t take_carry(World& w, int64_t fresh, int64_t n_root) {
+static int64_t take_carry(World& w, int64_t fresh, int64_t n_root, bool first) {
   w.carry_rem += fresh;
   w.carry_new = 0;
+  if (!first) return 0;
   const int64_t take = std::min(std::max<int64_t>(w.carry_rem, -n_root), n_root);
   w.carry_rem -= take;
   return take;
 }
 // the update's batch steps (the device's choose_k, capi.hip): sub_updates
-// when set; else, with E = |predictor| in mean weights per organism, one step
-// for E <= 0.1 and ceil(E / 0.05) steps (2 .. ADAPT_KMAX) above -- the
-// within-step weight change each step leaves is then about 0.05
+// when set; else the more of two rules, each one step up to its threshold:
+// with E = |predictor| in mean weights per organism (the total weight's
+// expected move within the update), ceil(E / 0.05) steps above E = 0.1; with
+// D the fraction of organisms expected to divide within it (a cohort in lock
+// step), ceil(D / 0.15) steps above D = 0.3; at most ADAPT_KMAX
 static constexpr int ADAPT_KMAX = 16;
-static int choose_k(const avgpu_cfg& c, int64_t pred, int64_t n, bool handed_in) {
+static int choose_k(const avgpu_cfg& c, int64_t pred, int64_t n, bool handed_in, int64_t cnt) {
   if (c.sub_updates > 0) return c.sub_updates;
-  if (handed_in || c.slicing_method != AVGPU_SLICE_PROBABILISTIC) return 1;
-  const double a = (double)(pred < 0 ? -pred : pred);
-  if (!(n > 0 && a > 104857.6 * (double)n)) return 1;
-  const int k = (int)std::ceil(a / (52428.8 * (double)n));
-  return std::max(2, std::min(k, ADAPT_KMAX));
+  if (handed_in || c.slicing_method != AVGPU_SLICE_PROBABILISTIC || n <= 0) return 1;
+  const double a = (double)(pred < 0 ? -pred : pred), dn = (double)n;
+  int k = 1;
+  if (a > 104857.6 * dn) k = std::max(k, (int)std::ceil(a / (52428.8 * dn)));
+  if ((double)cnt > 0.3 * dn) k = std::max(k, (int)std::ceil((double)cnt / (0.15 * dn)));
+  return std::min(k, ADAPT_KMAX);
 }
 
 // Batch-synchronous world update: the exact semantics the device implements
@@ -2472,7 +2486,7 @@ static int choose_k(const avgpu_cfg& c, int64_t pred, int64_t n, bool handed_in)
 static int run_update_impl(World& w) {
   if (w.cfg.birth_method == 5)
     return fail(AVGPU_EUNSUPPORTED, "BIRTH_METHOD 5 (the reaper queue) runs on the serial world only");
-  const int K = choose_k(w.cfg, w.pred_acc, w.pred_n, w.have_global);
+  const int K = choose_k(w.cfg, w.pred_acc, w.pred_n, w.have_global, w.pred_cnt);
   if (K > 1 && w.have_global)
     return fail(AVGPU_EUNSUPPORTED, "sub_updates > 1 needs the world's own totals (no handed-in totals)");
   int64_t placed = 0, dropped = 0, insts = 0, deaths = 0, divides = 0, slices = 0;
@@ -2485,9 +2499,12 @@ static int run_update_impl(World& w) {
     world_partials(w, part, &n_alive);
     const double local = top_tree(w, part, -1, 0, 0, nullptr);
     const double ave = (double)w.cfg.ave_time_slice;
-    double total = local, ud = ave * (double)n_alive;
+    // the update's UD = AVE_TIME_SLICE x the organisms at its start
+    // (cAvidaDriver's update loop), its later steps' shares of that
+    if (sub == 0) w.upd_ud = (int64_t)w.cfg.ave_time_slice * n_alive;
+    double total = local, ud = (double)w.upd_ud;
     int64_t n_all = n_alive;
-    int64_t n_root = (int64_t)w.cfg.ave_time_slice * n_alive;
+    int64_t n_root = w.upd_ud;
     if (w.have_global) {   // cMultiProcessWorld::CalculateUpdateSize (main/cMultiProcessWorld.cc:396-405)
       total = w.global_merit;
       ud = ave * (double)w.global_orgs;
@@ -2495,7 +2512,7 @@ static int run_update_impl(World& w) {
       n_root = total > 0.0 ? (int64_t)((local / total) * ave * (double)w.global_orgs) : 0;
     }
     n_root = sub_share(n_root, sub, K);
-    n_root -= take_carry(w, w.carry_new, n_root);
+    n_root -= take_carry(w, w.carry_new, n_root, sub == 0);
     std::vector<int64_t> blk;
     top_tree(w, part, n_root, 0, (int64_t)part.size(), &blk);
     if (sub == 0) res_begin(w);   // resources step once per update, at its start
@@ -2658,7 +2675,7 @@ int orc_tile_res_settle(void* h, const uint64_t* sum) {
 int orc_tile_buffer_bytes(void* h, int64_t* part, int64_t* halo, int64_t* rec) {
   World& w = *(World*)h;
   const int X = w.cfg.world_x;
-  if (part) *part = (2 * ((w.ncells + 255) / 256) + 2) * 8;
+  if (part) *part = (2 * ((w.ncells + 255) / 256) + 3) * 8;
   if (halo) *halo = halo_bytes_of(X);
   if (rec) *rec = (int64_t)sizeof(HaloHdr) + (int64_t)X * (int64_t)sizeof(HaloRec) + w.r_arena;
   return 0;
@@ -2690,6 +2707,7 @@ int orc_tile_partials(void* h, double* out) {
   // avgpu_tile_steps on every strip
   memcpy(out + 2 * nb, &w.pred_acc, 8);
   memcpy(out + 2 * nb + 1, &w.carry_new, 8);
+  memcpy(out + 2 * nb + 2, &w.pred_cnt, 8);
   // edge rows of the spatial amounts for the neighbours' flow step
   const int X = w.cfg.world_x;
   if (w.tiled && w.rs_send[0])
@@ -2708,14 +2726,16 @@ int orc_tile_partials(void* h, double* out) {
 // partials (the single world's choose_k over the same integer sum)
 int orc_tile_steps(void* h, const double* gathered, int ntiles, int* k_out) {
   World& w = *(World*)h;
-  const int64_t nb = (w.ncells + 255) / 256, stride = 2 * nb + 2;
-  int64_t sum = 0;
+  const int64_t nb = (w.ncells + 255) / 256, stride = 2 * nb + 3;
+  int64_t sum = 0, cnt = 0;
   for (int k = 0; k < ntiles; k++) {
-    int64_t v;
+    int64_t v, c;
     memcpy(&v, gathered + k * stride + 2 * nb, 8);
+    memcpy(&c, gathered + k * stride + 2 * nb + 2, 8);
     sum += v;
+    cnt += c;
   }
-  if (k_out) *k_out = choose_k(w.cfg, sum, w.pred_n, false);
+  if (k_out) *k_out = choose_k(w.cfg, sum, w.pred_n, false, cnt);
   return 0;
 }
 
@@ -2730,7 +2750,7 @@ int orc_tile_begin_step(void* h, const double* gathered, int ntiles, int sub, in
     w.acc_overwritten = w.acc_cancelled = 0;
   }
   // the top tree over every strip's block partials (tile order = block order)
-  const int64_t nb = (w.ncells + 255) / 256, stride = 2 * nb + 2;
+  const int64_t nb = (w.ncells + 255) / 256, stride = 2 * nb + 3;
   std::vector<double> leaf((size_t)(nb * ntiles));
   int64_t cnt = 0, fresh = 0;
   for (int k = 0; k < ntiles; k++) {
@@ -2743,13 +2763,14 @@ int orc_tile_begin_step(void* h, const double* gathered, int ntiles, int sub, in
     fresh += v;
   }
   std::vector<int64_t> blk;
-  const int64_t ud = (int64_t)w.cfg.ave_time_slice * cnt;
+  if (sub == 0) w.upd_ud = (int64_t)w.cfg.ave_time_slice * cnt;
+  const int64_t ud = w.upd_ud;
   int64_t n_root = sub_share(ud, sub, K);
-  n_root -= take_carry(w, fresh, n_root);
+  n_root -= take_carry(w, fresh, n_root, sub == 0);
   const double total = top_tree(w, leaf, n_root, w.cell0 / 256, nb, &blk);
   if (w.n_spatial && !w.rs_recv[0]) return fail(AVGPU_ESTATE, "spatial resources need the tile resource buffers");
   if (sub == 0) res_begin(w);
-  allot_interpret(w, blk, total, (double)w.cfg.ave_time_slice * (double)cnt, cnt);
+  allot_interpret(w, blk, total, (double)ud, cnt);
   w.step_sub = sub; w.step_k = K;
   w.step_uds = sub_share(ud, sub, K);
   w.step_total = total;

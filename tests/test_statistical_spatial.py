@@ -15,10 +15,11 @@ The product's world is the batch world at its default, avgpu_cfg.sub_updates
 = 0: each batch step's newborns run their share of the
 step's remaining picks after placement (a replaced organism's consumption
 after the birth given back, the picks beyond what it had left carried into
-the next step), and an update takes more batch steps the more its sub-step
-predictor expects the total weight to move (the lock-step start of the 100
-ancestors) -- the bench's own world runs the same code with one step.  No
-effect-size carve-out, no update excluded:
+the next update), and an update takes more batch steps the more its sub-step
+predictor expects the total weight to move or the more organisms it expects
+to divide in it (the lock-step start of the 100 ancestors) -- the bench's own
+world runs the same code and takes one step per update (bench.py
+batch_steps_per_update).  No effect-size carve-out, no update excluded:
 
 * task discovery: Fisher's exact test on the fraction of seeds with an Or
   organism by updates 20 / 30 / 50 / 100 and a KS test of the Or count at
@@ -33,8 +34,9 @@ effect-size carve-out, no update excluded:
   run): an early, strong Or sweep, around the 97th percentile.
 
 Measured (1024 seeds, this build; tools/piece_stats.py): smallest
-trajectory / discovery p 0.067 (threshold 0.01 / 65 = 1.5e-4), largest
-|Cohen's d| 0.08.  The GPU batch world is the oracle's bit for bit (checked
+trajectory / discovery p 0.011 (OrNot at update 30; threshold 0.01 / 65 =
+1.5e-4), largest |Cohen's d| 0.12; the reference run's mid-ranks 0.018 ..
+0.995.  The GPU batch world is the oracle's bit for bit (checked
 per seed below), so its statistics are these.
 """
 import numpy as np

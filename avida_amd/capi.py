@@ -144,6 +144,13 @@ class AvgpuTestResult(C.Structure):
     ]
 
 
+class AvgpuSerialState(C.Structure):
+    """avgpu_serial_state (include/avida_gpu.h): the serial world's stream
+    positions, reaper queue length and whether it has started"""
+    _fields_ = [("sched_pos", C.c_int64), ("ctx_pos", C.c_int64), ("reaper_len", C.c_int64),
+                ("started", C.c_int32), ("pad_", C.c_int32)]
+
+
 class AvgpuUpdateStats(C.Structure):
     _fields_ = [
         ("update", C.c_int64), ("num_organisms", C.c_int64), ("insts_executed", C.c_int64),
@@ -189,7 +196,7 @@ EXPORTED = [
     "avgpu_set_tile_res_buffers", "avgpu_tile_res_cons", "avgpu_tile_res_settle",
     "avgpu_last_step_insts", "avgpu_last_kernel_ms", "avgpu_kernel_times", "avgpu_counters",
     "avgpu_state_digests", "avgpu_set_rng_mode", "avgpu_run_serial_updates", "avgpu_set_serial_streams",
-    "avgpu_set_timing",
+    "avgpu_get_serial_state", "avgpu_set_serial_state", "avgpu_set_timing",
 ]
 
 
@@ -386,6 +393,8 @@ def bind_common(lib, prefix):
         "state_digests": (C.c_int, [V, I64, I64, V]),
         "set_rng_mode": (C.c_int, [V, C.c_int, V, I64, V]),
         "set_serial_streams": (C.c_int, [V, V, I64, V, I64]),
+        "get_serial_state": (C.c_int, [V, C.POINTER(AvgpuSerialState), V, V, V, V, I64]),
+        "set_serial_state": (C.c_int, [V, C.POINTER(AvgpuSerialState), V, V, V, V]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, p + name, None)

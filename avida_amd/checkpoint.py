@@ -14,7 +14,11 @@ avgpu_cpu_state records), `tape` (one byte per site: op | copied << 6 |
 executed << 7, `cap` bytes per cell), `stats` (raw avgpu_update_stats),
 `levels` / `grids` (resources), `gkeys` (the census genotype keys of the
 birth genomes, which the tape no longer holds once an organism copied into
-its own sites; avgpu_set_genotype_keys), `version` and the byte sizes of the
+its own sites; avgpu_set_genotype_keys), `serial` / `spec` / `face` /
+`soup_perm` / `reaper` (the serial world's own state, avgpu_get_serial_state:
+its two streams' positions, speculative credits, connection-list rotations,
+BIRTH_METHOD 4's empty_cell_id_array and 5's reaper queue, rear first),
+`version` and the byte sizes of the
 two raw structures (`state_size`, `stats_size`).  A file from before a
 structure grew (round 4 added births_cancelled and seed to the stats) loads
 with the missing tail zeroed; a zero seed then leaves the world's configured
@@ -28,7 +32,7 @@ import numpy as np
 
 from . import capi
 
-VERSION = 3
+VERSION = 4
 # round 5 added `age` (+ a pad word) before cur_bonus: an older state record
 # gets them inserted as zeros (age 0: as if every organism had just divided)
 _AGE_OFF = capi.AvgpuCpuState.age.offset
@@ -61,7 +65,17 @@ def save(lib, prefix, handle, ncells, nres, path):
         _call(lib, prefix, "get_resources", handle, levels.ctypes.data_as(C.POINTER(C.c_double)),
               grids.ctypes.data_as(C.POINTER(C.c_double)))
     gkeys = capi.get_census(lib, prefix, handle, 0, ncells)["genotype_key"]
+    ser = capi.AvgpuSerialState()
+    spec = np.zeros(ncells, dtype=np.int32)
+    face = np.zeros(ncells, dtype=np.uint8)
+    soup = np.zeros(ncells, dtype=np.int32)
+    reaper = np.zeros(2 * ncells + 64, dtype=np.int32)
+    _call(lib, prefix, "get_serial_state", handle, C.byref(ser), spec.ctypes.data_as(C.c_void_p),
+          face.ctypes.data_as(C.c_void_p), soup.ctypes.data_as(C.c_void_p), reaper.ctypes.data_as(C.c_void_p),
+          len(reaper))
     np.savez_compressed(path, states=np.frombuffer(st, dtype=np.uint8), tape=tape.astype(np.uint8), gkeys=gkeys,
+                        serial=np.frombuffer(ser, dtype=np.uint8), spec=spec, face=face, soup_perm=soup,
+                        reaper=reaper[:max(0, ser.reaper_len)],
                         cap=np.int64(cap), stats=np.frombuffer(stats, dtype=np.uint8),
                         levels=levels[:nres], grids=grids[:nres * ncells], ncells=np.int64(ncells),
                         version=np.int64(VERSION), state_size=np.int64(C.sizeof(capi.AvgpuCpuState)),
@@ -101,6 +115,11 @@ def load(lib, prefix, handle, path):
     if "gkeys" in z.files:                     # genotype keys of the birth genomes
         gk = np.ascontiguousarray(z["gkeys"], dtype=np.uint64)
         _call(lib, prefix, "set_genotype_keys", handle, 0, ncells, gk.ctypes.data_as(C.c_void_p))
+    if "serial" in z.files:                    # the serial world's own state (version >= 4)
+        ser = _struct(capi.AvgpuSerialState, z["serial"].tobytes(), "serial state")
+        arrs = [np.ascontiguousarray(z[k], dtype=t) for k, t in
+                (("spec", np.int32), ("face", np.uint8), ("soup_perm", np.int32), ("reaper", np.int32))]
+        _call(lib, prefix, "set_serial_state", handle, C.byref(ser), *[a.ctypes.data_as(C.c_void_p) for a in arrs])
     stats = _struct(capi.AvgpuUpdateStats, z["stats"].tobytes(), "stats")
     _call(lib, prefix, "set_clock", handle, C.byref(stats))
     levels = np.ascontiguousarray(z["levels"], dtype=np.float64)

@@ -31,6 +31,19 @@ int fail(int code, const std::string& msg) {
     hipError_t _e = (x);                                                            \
     if (_e != hipSuccess) return fail(AVGPU_EHIP, std::string(#x ": ") + hipGetErrorString(_e)); \
   } while (0)
+// A copy / fill of an API call on the world's stream, complete on return.  The
+// world's streams are non-blocking: a null-stream hipMemcpy / hipMemset would
+// neither wait for the kernels queued on them nor be waited for by them.
+#define COPY_SYNC(ww, dst, src, bytes, kind)                                        \
+  do {                                                                              \
+    HIPCHK(hipMemcpyAsync((dst), (src), (bytes), (kind), (ww)->stream));           \
+    HIPCHK(hipStreamSynchronize((ww)->stream));                                     \
+  } while (0)
+#define SET_SYNC(ww, dst, val, bytes)                                               \
+  do {                                                                              \
+    HIPCHK(hipMemsetAsync((dst), (val), (bytes), (ww)->stream));                    \
+    HIPCHK(hipStreamSynchronize((ww)->stream));                                     \
+  } while (0)
 
 }  // namespace
 
@@ -88,6 +101,7 @@ struct avgpu_world {
   long long* d_pred = nullptr;   // its device address
   hipEvent_t ev_pred = nullptr;
   bool pred_pending = false;
+  bool reaper_rebuild = false;  // the serial reaper queue is built again at the next serial update
   long long pred_acc = 0, pred_n = 0, pred_cnt = 0;
   int last_k = 1;
   int tile_sub = 0, tile_k = 1, tile_sub_next = 0;
@@ -399,12 +413,15 @@ int copy_tables(avgpu_world* dst, const avgpu_world* src) {
   D.n_ops = S.n_ops; D.rand_total = S.rand_total; D.fill_code = S.fill_code;
   D.n_react = S.n_react;
   D.env_simple = S.env_simple; D.env_react_mask = S.env_react_mask; D.env_once_mask = S.env_once_mask;
-  HIPCHK(hipMemcpy(D.task_tab, S.task_tab, 32 * sizeof(double), hipMemcpyDeviceToDevice));
-  HIPCHK(hipMemcpy(D.react_tab, S.react_tab, AVGPU_MAX_REACTIONS * RT_STRIDE * sizeof(int32_t),
-                   hipMemcpyDeviceToDevice));
-  HIPCHK(hipMemcpy(D.rand_lut, S.rand_lut, 256, hipMemcpyDeviceToDevice));
-  HIPCHK(hipMemcpy(D.rand_cum, S.rand_cum, 64 * sizeof(int32_t), hipMemcpyDeviceToDevice));
-  HIPCHK(hipMemcpy(D.rand_code, S.rand_code, 64, hipMemcpyDeviceToDevice));
+  // the source's tables as its stream leaves them, into the destination on its own
+  HIPCHK(hipStreamSynchronize(src->stream));
+  HIPCHK(hipMemcpyAsync(D.task_tab, S.task_tab, 32 * sizeof(double), hipMemcpyDeviceToDevice, dst->stream));
+  HIPCHK(hipMemcpyAsync(D.react_tab, S.react_tab, AVGPU_MAX_REACTIONS * RT_STRIDE * sizeof(int32_t),
+                        hipMemcpyDeviceToDevice, dst->stream));
+  HIPCHK(hipMemcpyAsync(D.rand_lut, S.rand_lut, 256, hipMemcpyDeviceToDevice, dst->stream));
+  HIPCHK(hipMemcpyAsync(D.rand_cum, S.rand_cum, 64 * sizeof(int32_t), hipMemcpyDeviceToDevice, dst->stream));
+  HIPCHK(hipMemcpyAsync(D.rand_code, S.rand_code, 64, hipMemcpyDeviceToDevice, dst->stream));
+  HIPCHK(hipStreamSynchronize(dst->stream));
   dst->n_ops = src->n_ops;
   memcpy(dst->op2code, src->op2code, sizeof(dst->op2code));
   memcpy(dst->code2op, src->code2op, sizeof(dst->code2op));
@@ -441,10 +458,67 @@ int translate_genomes(avgpu_world* w, const uint8_t* genomes, const int32_t* len
   return 0;
 }
 
+// the serial world's reaper queue (W.reaper: a ring of reaper_cap cells,
+// positions [reaper_ix[0], reaper_ix[1]) from the rear), rear first
+int reaper_read(avgpu_world* w, std::vector<int32_t>& q) {
+  const DevWorld& W = w->W;
+  int64_t ix[2];
+  COPY_SYNC(w, ix, W.reaper_ix, sizeof(ix), hipMemcpyDeviceToHost);
+  std::vector<int32_t> ring((size_t)W.reaper_cap);
+  COPY_SYNC(w, ring.data(), W.reaper, ring.size() * sizeof(int32_t), hipMemcpyDeviceToHost);
+  if (ix[1] < ix[0] || ix[1] - ix[0] > W.reaper_cap) return fail(AVGPU_ESTATE, "reaper queue indices");
+  q.clear();
+  for (int64_t p = ix[0]; p < ix[1]; p++) q.push_back(ring[(size_t)(p % W.reaper_cap)]);
+  return 0;
+}
+int reaper_write(avgpu_world* w, const std::vector<int32_t>& q) {
+  const DevWorld& W = w->W;
+  if ((int64_t)q.size() > W.reaper_cap) return fail(AVGPU_EUNSUPPORTED, "reaper queue longer than 2n + 64");
+  std::vector<int32_t> ring((size_t)W.reaper_cap, 0);
+  std::copy(q.begin(), q.end(), ring.begin());
+  const int64_t ix[2] = {W.reaper_cap, W.reaper_cap + (int64_t)q.size()};   // position cap + k = slot k
+  COPY_SYNC(w, W.reaper, ring.data(), ring.size() * sizeof(int32_t), hipMemcpyHostToDevice);
+  COPY_SYNC(w, W.reaper_ix, ix, sizeof(ix), hipMemcpyHostToDevice);
+  return 0;
+}
+
+// the queue as the reference has it after Setup and the injections of the
+// living cells (oracle reaper_setup): cells 0..N-1 pushed, then every living
+// cell in ascending order
+int reaper_build(avgpu_world* w) {
+  const DevWorld& W = w->W;
+  std::vector<uint32_t> ctl((size_t)W.n);
+  COPY_SYNC(w, ctl.data(), W.ctl, (size_t)W.n * sizeof(uint32_t), hipMemcpyDeviceToHost);
+  std::vector<int32_t> q;
+  for (int64_t c = 0; c < W.n; c++) q.push_back((int32_t)c);
+  for (int64_t c = 0; c < W.n; c++) if (ctl[(size_t)c] & CTL_ALIVE) q.push_back((int32_t)c);
+  w->reaper_rebuild = false;
+  return reaper_write(w, q);
+}
+
 int set_orgs_impl(avgpu_world* w, int64_t first, int64_t count, const uint8_t* genomes,
                   const int32_t* lens, const double* merits, const int32_t* inputs, int det) {
   if (first < 0 || count < 0 || first + count > w->W.n) return fail(AVGPU_EINVAL, "cell range");
   if (count == 0) return 0;
+  // a serial BIRTH_METHOD 5 world whose reaper queue exists: the injections'
+  // queue entries (oracle reaper_inject; InjectGenome main/cPopulation.cc:
+  // 6964-6968, ActivateOrganism :1358-1361), on the host (injection is rare)
+  if (w->W.reaper && w->cfg.birth_method == 5 && !w->reaper_rebuild) {
+    std::vector<uint32_t> ctl((size_t)count);
+    COPY_SYNC(w, ctl.data(), w->W.ctl + first, (size_t)count * sizeof(uint32_t), hipMemcpyDeviceToHost);
+    std::vector<int32_t> q;
+    int qrc = reaper_read(w, q);
+    if (qrc < 0) return qrc;
+    for (int64_t i = 0; i < count; i++) {
+      const int32_t c = (int32_t)(first + i);
+      if (ctl[(size_t)i] & CTL_ALIVE) {
+        for (size_t k = q.size(); k-- > 0;)      // the first entry from the front (the newest end)
+          if (q[k] == c) { q.erase(q.begin() + (std::ptrdiff_t)k); break; }
+      }
+      q.push_back(c);
+    }
+    if ((qrc = reaper_write(w, q)) < 0) return qrc;
+  }
   std::vector<uint8_t> codes;
   std::vector<int32_t> offsets;
   int rc = translate_genomes(w, genomes, lens, count, codes, offsets);
@@ -755,10 +829,9 @@ int avgpu_set_orgs(avgpu_world* w, int64_t first, int64_t count, const uint8_t* 
 int avgpu_kill(avgpu_world* w, int64_t cell) {
   if (!w || cell < 0 || cell >= w->W.n) return fail(AVGPU_EINVAL, "cell");
   uint32_t ctl = 0;
-  HIPCHK(hipStreamSynchronize(w->stream));
-  HIPCHK(hipMemcpy(&ctl, w->W.ctl + cell, 4, hipMemcpyDeviceToHost));
+  COPY_SYNC(w, &ctl, w->W.ctl + cell, 4, hipMemcpyDeviceToHost);
   ctl &= ~CTL_ALIVE;
-  HIPCHK(hipMemcpy(w->W.ctl + cell, &ctl, 4, hipMemcpyHostToDevice));
+  COPY_SYNC(w, w->W.ctl + cell, &ctl, 4, hipMemcpyHostToDevice);
   return 0;
 }
 
@@ -909,16 +982,7 @@ static int serial_alloc(avgpu_world* w) {
     if ((rc = w->alloc(&W.reaper, (size_t)cap)) < 0) return rc;
     if ((rc = w->alloc(&W.reaper_ix, 2)) < 0) return rc;
     W.reaper_cap = cap;
-    HIPCHK(hipStreamSynchronize(w->stream));
-    std::vector<uint32_t> ctl((size_t)W.n);
-    HIPCHK(hipMemcpy(ctl.data(), W.ctl, (size_t)W.n * sizeof(uint32_t), hipMemcpyDeviceToHost));
-    std::vector<int32_t> q((size_t)cap, 0);
-    int64_t f = cap;
-    for (int64_t c = 0; c < W.n; c++) q[(size_t)(f++ % cap)] = (int32_t)c;
-    for (int64_t c = 0; c < W.n; c++) if (ctl[(size_t)c] & CTL_ALIVE) q[(size_t)(f++ % cap)] = (int32_t)c;
-    const int64_t ix[2] = {cap, f};
-    HIPCHK(hipMemcpy(W.reaper, q.data(), (size_t)cap * sizeof(int32_t), hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(W.reaper_ix, ix, sizeof(ix), hipMemcpyHostToDevice));
+    if ((rc = reaper_build(w)) < 0) return rc;
   }
   uint32_t g[3] = {0, 0, 0}, x[3] = {0, 0, 0};
   const uint64_t seed = (uint64_t)w->cfg.seed;
@@ -937,23 +1001,117 @@ int avgpu_set_serial_streams(avgpu_world* w, const double* sched, int64_t n_sche
   int rc = serial_alloc(w);
   if (rc < 0) return rc;
   DevWorld& W = w->W;
+  HIPCHK(hipStreamSynchronize(w->stream));   // no queued serial update still reads them
   for (double** p : {&w->srec_buf[0], &w->srec_buf[1]})
     if (*p) { hipFree(*p); *p = nullptr; }
   W.srec_sched = nullptr; W.srec_sched_n = 0; W.srec_ctx = nullptr; W.srec_ctx_n = 0;
   if (sched) {
     HIPCHK(hipMalloc(&w->srec_buf[0], (size_t)n_sched * sizeof(double)));
-    HIPCHK(hipMemcpy(w->srec_buf[0], sched, (size_t)n_sched * sizeof(double), hipMemcpyHostToDevice));
+    COPY_SYNC(w, w->srec_buf[0], sched, (size_t)n_sched * sizeof(double), hipMemcpyHostToDevice);
     W.srec_sched = w->srec_buf[0]; W.srec_sched_n = n_sched;
   }
   if (ctx) {
     HIPCHK(hipMalloc(&w->srec_buf[1], (size_t)n_ctx * sizeof(double)));
-    HIPCHK(hipMemcpy(w->srec_buf[1], ctx, (size_t)n_ctx * sizeof(double), hipMemcpyHostToDevice));
+    COPY_SYNC(w, w->srec_buf[1], ctx, (size_t)n_ctx * sizeof(double), hipMemcpyHostToDevice);
     W.srec_ctx = w->srec_buf[1]; W.srec_ctx_n = n_ctx;
   }
   // both positions restart at 0 (counter streams: their counters)
   HIPCHK(hipMemsetAsync(W.grng + 2, 0, 4, w->stream));
   HIPCHK(hipMemsetAsync(W.sctx + 2, 0, 4, w->stream));
   HIPCHK(hipStreamSynchronize(w->stream));
+  return 0;
+}
+
+int avgpu_get_serial_state(avgpu_world* w, avgpu_serial_state* st, int32_t* spec, uint8_t* face,
+                           int32_t* soup_perm, int32_t* reaper, int64_t reaper_cap) {
+  if (!w) return fail(AVGPU_EINVAL, "NULL world");
+  const DevWorld& W = w->W;
+  const int64_t n = W.n;
+  const bool started = W.stree != nullptr;     // serial_alloc ran (a serial update, or a set state)
+  uint32_t g[3] = {0, 0, 0}, x[3] = {0, 0, 0};
+  if (started) {
+    COPY_SYNC(w, g, W.grng, sizeof(g), hipMemcpyDeviceToHost);
+    COPY_SYNC(w, x, W.sctx, sizeof(x), hipMemcpyDeviceToHost);
+  }
+  std::vector<int32_t> q;
+  const bool have_q = W.reaper && !w->reaper_rebuild;
+  if (have_q) {
+    int rc = reaper_read(w, q);
+    if (rc < 0) return rc;
+  }
+  if (st) {
+    memset(st, 0, sizeof(*st));
+    st->sched_pos = g[2];
+    st->ctx_pos = x[2];
+    st->reaper_len = have_q ? (int64_t)q.size() : -1;
+    st->started = started ? 1 : 0;
+  }
+  if (spec) {
+    std::vector<uint32_t> ctl((size_t)n);
+    COPY_SYNC(w, ctl.data(), W.ctl, (size_t)n * sizeof(uint32_t), hipMemcpyDeviceToHost);
+    if (started) COPY_SYNC(w, spec, W.spec, (size_t)n * sizeof(int32_t), hipMemcpyDeviceToHost);
+    for (int64_t c = 0; c < n; c++)
+      spec[c] = (started ? (spec[c] & 0xFFFF) : 0) | ((ctl[(size_t)c] & CTL_SPECDIE) ? 1 << 16 : 0);
+  }
+  if (face) {
+    if (started) COPY_SYNC(w, face, W.face, (size_t)n, hipMemcpyDeviceToHost);
+    else memset(face, 0, (size_t)n);
+  }
+  if (soup_perm) {
+    if (W.soup_perm) COPY_SYNC(w, soup_perm, W.soup_perm, (size_t)n * sizeof(int32_t), hipMemcpyDeviceToHost);
+    else for (int64_t c = 0; c < n; c++) soup_perm[c] = (int32_t)c;
+  }
+  if (reaper && !q.empty()) {
+    if (reaper_cap < (int64_t)q.size()) return fail(AVGPU_EINVAL, "reaper buffer too small");
+    std::copy(q.begin(), q.end(), reaper);
+  }
+  return 0;
+}
+
+int avgpu_set_serial_state(avgpu_world* w, const avgpu_serial_state* st, const int32_t* spec, const uint8_t* face,
+                           const int32_t* soup_perm, const int32_t* reaper) {
+  if (!w || !st) return fail(AVGPU_EINVAL, "serial state");
+  if (!st->started) return 0;
+  DevWorld& W = w->W;
+  const int64_t n = W.n, len = st->reaper_len;
+  if (soup_perm) {
+    std::vector<char> seen((size_t)n, 0);
+    for (int64_t c = 0; c < n; c++) {
+      if (soup_perm[c] < 0 || soup_perm[c] >= n || seen[(size_t)soup_perm[c]])
+        return fail(AVGPU_EINVAL, "soup_perm is not a permutation of the cells");
+      seen[(size_t)soup_perm[c]] = 1;
+    }
+  }
+  if (len > 2 * n + 64) return fail(AVGPU_EINVAL, "reaper queue longer than 2n + 64");
+  if (len > 0 && !reaper) return fail(AVGPU_EINVAL, "reaper queue");
+  for (int64_t k = 0; k < len; k++)
+    if (reaper[k] < 0 || reaper[k] >= n) return fail(AVGPU_EINVAL, "reaper queue cell out of range");
+  int rc = serial_alloc(w);
+  if (rc < 0) return rc;
+  const uint32_t gp = (uint32_t)st->sched_pos, xp = (uint32_t)st->ctx_pos;
+  COPY_SYNC(w, W.grng + 2, &gp, 4, hipMemcpyHostToDevice);
+  COPY_SYNC(w, W.sctx + 2, &xp, 4, hipMemcpyHostToDevice);
+  if (spec) {
+    std::vector<int32_t> cr((size_t)n);
+    std::vector<uint32_t> ctl((size_t)n);
+    COPY_SYNC(w, ctl.data(), W.ctl, (size_t)n * sizeof(uint32_t), hipMemcpyDeviceToHost);
+    for (int64_t c = 0; c < n; c++) {
+      cr[(size_t)c] = spec[c] & 0xFFFF;
+      ctl[(size_t)c] = (ctl[(size_t)c] & ~CTL_SPECDIE) | (((spec[c] >> 16) & 1) ? CTL_SPECDIE : 0u);
+    }
+    COPY_SYNC(w, W.spec, cr.data(), (size_t)n * sizeof(int32_t), hipMemcpyHostToDevice);
+    COPY_SYNC(w, W.ctl, ctl.data(), (size_t)n * sizeof(uint32_t), hipMemcpyHostToDevice);
+  }
+  if (face) COPY_SYNC(w, W.face, face, (size_t)n, hipMemcpyHostToDevice);
+  if (soup_perm && W.soup_perm) COPY_SYNC(w, W.soup_perm, soup_perm, (size_t)n * sizeof(int32_t), hipMemcpyHostToDevice);
+  if (W.reaper) {
+    if (len < 0) {
+      w->reaper_rebuild = true;                      // built again at the next serial update
+    } else {
+      w->reaper_rebuild = false;
+      if ((rc = reaper_write(w, std::vector<int32_t>(reaper, reaper + len))) < 0) return rc;
+    }
+  }
   return 0;
 }
 
@@ -968,6 +1126,7 @@ int avgpu_run_serial_updates(avgpu_world* w, int n, avgpu_update_stats* last) {
   if (W.birth_method == 1 || W.birth_method == 2)
     return fail(AVGPU_EUNSUPPORTED, "BIRTH_METHOD 1 / 2 run on the batch world, not the serial world");
   if ((rc = serial_alloc(w)) < 0) return rc;
+  if (w->reaper_rebuild && (rc = reaper_build(w)) < 0) return rc;
   for (int u = 0; u < n; u++) {
     launch_reset_counts(W, w->stream);
     launch_age_tick(W, w->stream);
@@ -1068,7 +1227,7 @@ int avgpu_set_rng_mode(avgpu_world* w, int mode, const double* stream, int64_t n
   if (mode == AVGPU_RNG_COUNTER) {
     W.rec = nullptr;
     W.rec_n = 0;
-    if (W.rec_off) HIPCHK(hipMemset(W.rec_off, 0xFF, W.n * sizeof(int64_t)));   // -1: counter streams
+    if (W.rec_off) SET_SYNC(w, W.rec_off, 0xFF, W.n * sizeof(int64_t));   // -1: counter streams
     return 0;
   }
   if (mode != AVGPU_RNG_RECORDED || !stream || n <= 0) return fail(AVGPU_EINVAL, "rng mode / stream");
@@ -1080,16 +1239,16 @@ int avgpu_set_rng_mode(avgpu_world* w, int mode, const double* stream, int64_t n
     }
   if (w->rec_buf) { hipFree(w->rec_buf); w->rec_buf = nullptr; }
   HIPCHK(hipMalloc(&w->rec_buf, n * sizeof(double)));
-  HIPCHK(hipMemcpy(w->rec_buf, stream, n * sizeof(double), hipMemcpyHostToDevice));
+  COPY_SYNC(w, w->rec_buf, stream, n * sizeof(double), hipMemcpyHostToDevice);
   if (!W.rec_off) {
     HIPCHK(hipMalloc(&W.rec_off, W.n * sizeof(int64_t)));
     w->allocs.push_back(W.rec_off);
   }
-  HIPCHK(hipMemcpy(W.rec_off, off.data(), W.n * sizeof(int64_t), hipMemcpyHostToDevice));
+  COPY_SYNC(w, W.rec_off, off.data(), W.n * sizeof(int64_t), hipMemcpyHostToDevice);
   W.rec = w->rec_buf;
   W.rec_n = n;
   // every organism's position in its segment starts at 0
-  HIPCHK(hipMemset(W.rng + 2 * W.n, 0, W.n * sizeof(uint32_t)));
+  SET_SYNC(w, W.rng + 2 * W.n, 0, W.n * sizeof(uint32_t));
   return 0;
 }
 
@@ -1198,6 +1357,16 @@ int avgpu_set_clock(avgpu_world* w, const avgpu_update_stats* last) {
     w->cfg.seed = last->seed;
     w->W.seed_lo = (uint32_t)last->seed;
     w->W.seed_hi = (uint32_t)(last->seed >> 32);
+    // the serial world's two streams are keyed by the seed too (serial_alloc;
+    // their positions stay)
+    if (w->W.grng) {
+      uint32_t g[2], x[2];
+      derive_key((uint32_t)last->seed, (uint32_t)(last->seed >> 32), 0x5CEDu, 0xC0FFEEu, g[0], g[1]);
+      derive_key((uint32_t)last->seed, (uint32_t)(last->seed >> 32), 0xC7C7u, 0x5EED5u, x[0], x[1]);
+      HIPCHK(hipMemcpyAsync(w->W.grng, g, sizeof(g), hipMemcpyHostToDevice, w->stream));
+      HIPCHK(hipMemcpyAsync(w->W.sctx, x, sizeof(x), hipMemcpyHostToDevice, w->stream));
+      HIPCHK(hipStreamSynchronize(w->stream));
+    }
   }
   // the batch-step predictor and the pick carry
   w->pred_acc = last->sched_pred;
@@ -1234,10 +1403,18 @@ int avgpu_test_genomes(avgpu_world* w, int n, const uint8_t* genomes, const int3
   }
   std::vector<uint8_t> tflags((size_t)n * TAPE_SLOT), tchild((size_t)n * TAPE_SLOT);
   std::vector<int32_t> tflen(n), tclen(n);
-  hipMemcpy(tflags.data(), t->W.t_flags, tflags.size(), hipMemcpyDeviceToHost);
-  hipMemcpy(tchild.data(), t->W.t_child, tchild.size(), hipMemcpyDeviceToHost);
-  hipMemcpy(tflen.data(), t->W.t_flags_len, n * 4, hipMemcpyDeviceToHost);
-  hipMemcpy(tclen.data(), t->W.t_child_len, n * 4, hipMemcpyDeviceToHost);
+  // (checked: a failed copy would hand back uninitialised flags and offspring)
+  const hipError_t ce[4] = {
+      hipMemcpyAsync(tflags.data(), t->W.t_flags, tflags.size(), hipMemcpyDeviceToHost, t->stream),
+      hipMemcpyAsync(tchild.data(), t->W.t_child, tchild.size(), hipMemcpyDeviceToHost, t->stream),
+      hipMemcpyAsync(tflen.data(), t->W.t_flags_len, n * 4, hipMemcpyDeviceToHost, t->stream),
+      hipMemcpyAsync(tclen.data(), t->W.t_child_len, n * 4, hipMemcpyDeviceToHost, t->stream)};
+  const hipError_t se = hipStreamSynchronize(t->stream);
+  for (hipError_t e : {ce[0], ce[1], ce[2], ce[3], se})
+    if (e != hipSuccess) {
+      avgpu_destroy(t);
+      return fail(AVGPU_EHIP, std::string("test_genomes copy: ") + hipGetErrorString(e));
+    }
   size_t off = 0;
   for (int i = 0; i < n; i++) {
     avgpu_test_result& r = results[i];
@@ -1310,7 +1487,7 @@ static int res_seed(avgpu_world* w) {
   const int64_t n = W.n, nglobal = (int64_t)W.world_x * W.world_y;
   const int nres = (int)w->res_spec.size();
   ResParam P[AVGPU_MAX_RESOURCES];
-  HIPCHK(hipMemcpy(P, W.res_param, sizeof(P), hipMemcpyDeviceToHost));
+  COPY_SYNC(w, P, W.res_param, sizeof(P), hipMemcpyDeviceToHost);
   double glob[AVGPU_MAX_RESOURCES];
   memset(glob, 0, sizeof(glob));
   if (W.n_spatial) {
@@ -1418,19 +1595,18 @@ int avgpu_load_resources(avgpu_world* w, int nres, const avgpu_resource* res, in
 int avgpu_set_resources(avgpu_world* w, const double* levels, const double* spatial) {
   if (!w || !levels) return fail(AVGPU_EINVAL, "args");
   DevWorld& W = w->W;
-  HIPCHK(hipStreamSynchronize(w->stream));
   double glob[AVGPU_MAX_RESOURCES];
   ResParam P[AVGPU_MAX_RESOURCES];
-  HIPCHK(hipMemcpy(glob, W.res_global, sizeof(glob), hipMemcpyDeviceToHost));
-  HIPCHK(hipMemcpy(P, W.res_param, sizeof(P), hipMemcpyDeviceToHost));
+  COPY_SYNC(w, glob, W.res_global, sizeof(glob), hipMemcpyDeviceToHost);
+  COPY_SYNC(w, P, W.res_param, sizeof(P), hipMemcpyDeviceToHost);
   for (int r = 0; r < W.n_res; r++) {
     if (P[r].slot < 0) { glob[r] = levels[r]; continue; }
     if (!spatial) return fail(AVGPU_EINVAL, "spatial resources need their grids");
-    HIPCHK(hipMemcpy(W.res_amount + (size_t)P[r].slot * W.n, spatial + (size_t)r * W.n, W.n * sizeof(double),
-                     hipMemcpyHostToDevice));
+    COPY_SYNC(w, W.res_amount + (size_t)P[r].slot * W.n, spatial + (size_t)r * W.n, W.n * sizeof(double),
+              hipMemcpyHostToDevice);
   }
-  HIPCHK(hipMemcpy(W.res_global, glob, sizeof(glob), hipMemcpyHostToDevice));
-  HIPCHK(hipMemset(W.res_cons, 0, AVGPU_MAX_RESOURCES * sizeof(unsigned long long)));
+  COPY_SYNC(w, W.res_global, glob, sizeof(glob), hipMemcpyHostToDevice);
+  SET_SYNC(w, W.res_cons, 0, AVGPU_MAX_RESOURCES * sizeof(unsigned long long));
   W.res_first = 0;
   return 0;
 }
@@ -1438,11 +1614,10 @@ int avgpu_set_resources(avgpu_world* w, const double* levels, const double* spat
 int avgpu_get_resources(avgpu_world* w, double* levels, double* spatial) {
   if (!w || !levels) return fail(AVGPU_EINVAL, "args");
   DevWorld& W = w->W;
-  HIPCHK(hipStreamSynchronize(w->stream));
   double glob[AVGPU_MAX_RESOURCES];
   ResParam P[AVGPU_MAX_RESOURCES];
-  HIPCHK(hipMemcpy(glob, W.res_global, sizeof(glob), hipMemcpyDeviceToHost));
-  HIPCHK(hipMemcpy(P, W.res_param, sizeof(P), hipMemcpyDeviceToHost));
+  COPY_SYNC(w, glob, W.res_global, sizeof(glob), hipMemcpyDeviceToHost);
+  COPY_SYNC(w, P, W.res_param, sizeof(P), hipMemcpyDeviceToHost);
   std::vector<double> row(W.n);
   for (int r = 0; r < W.n_res; r++) {
     if (P[r].slot < 0) {
@@ -1450,8 +1625,8 @@ int avgpu_get_resources(avgpu_world* w, double* levels, double* spatial) {
       if (spatial) memset(spatial + (size_t)r * W.n, 0, W.n * sizeof(double));
       continue;
     }
-    HIPCHK(hipMemcpy(row.data(), W.res_amount + (size_t)P[r].slot * W.n, W.n * sizeof(double),
-                     hipMemcpyDeviceToHost));
+    COPY_SYNC(w, row.data(), W.res_amount + (size_t)P[r].slot * W.n, W.n * sizeof(double),
+              hipMemcpyDeviceToHost);
     double sum = 0.0;                                   // cStats::PrintResourceData order
     for (int64_t c = 0; c < W.n; c++) sum += row[c];
     levels[r] = sum;

@@ -666,12 +666,14 @@ __device__ __forceinline__ uint32_t node_draw(uint32_t slo, uint32_t shi, uint32
 // are never scheduled; large finite merits of multiplicative environments are)
 __device__ __forceinline__ bool merit_ok(double m) { return m >= 0.0 && m <= 1.7976931348623157e308; }
 // the scheduler weight of a living organism (oracle sched_weight): the same
-// in k_merit_partial's partials and k_allot's leaves
+// in k_merit_partial's partials and k_allot's leaves; at most 2^990, so that
+// the scheduler's sums over up to 2^33 organisms stay finite
+#define WEIGHT_CAP 0x1p990
 __device__ __forceinline__ double sched_weight(double merit, uint32_t ctl) {
   if (!merit_ok(merit)) return 0.0;
   const uint32_t hs = CTL_HS(ctl);
   const double w = hs ? __dmul_rn(merit, __dadd_rn(1.0, __dmul_rn((double)hs, 1.0 / 65536.0))) : merit;
-  return merit_ok(w) ? w : 0.0;
+  return merit_ok(w) ? fmin(w, WEIGHT_CAP) : 0.0;
 }
 
 // CalcSizeMerit (main/cPhenotype.cc:1760-1816)

@@ -2341,7 +2341,9 @@ __global__ __launch_bounds__(64, 1) void k_serial_update(const DevWorld* __restr
           in3[0] = (15 << 24) + (int)sctx_below(W, ct, 1u << 24, ov);
           in3[1] = (51 << 24) + (int)sctx_below(W, ct, 1u << 24, ov);
           in3[2] = (85 << 24) + (int)sctx_below(W, ct, 1u << 24, ov);
-          if (t != (int)c) {                                    // Rotate(parent_cell) (:935-944)
+          // Rotate(parent_cell) (:935-944), for the local birth methods only
+          // (birth_method < NUM_LOCAL_POSITION_OFFSPRING = 4, :938)
+          if (t != (int)c && W.birth_method < 4) {
             int tb[8];                                          // (not adjacent: a full turn, no change)
             const int ntb = conn_base(W, t, tb);
             for (int k = 0; k < ntb; k++) if (tb[k] == (int)c && face_t < 0) face_t = k;

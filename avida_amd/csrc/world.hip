@@ -1047,13 +1047,13 @@ __device__ __forceinline__ double position_value(const DevWorld& W, int c) {
   return m > 0.0 ? __ddiv_rn(age, m) : age;
 }
 // BIRTH_METHOD 4 (POSITION_OFFSPRING_FULL_SOUP_RANDOM, main/cPopulation.cc:
-// 5297-5310; oracle soup_target): with PREFER_EMPTY a cell drawn uniformly
-// among those empty at placement start (e_list) that this round has not
-// taken, by up to SOUP_TRIES draws (FindRandEmptyCell, :5650-5668), else --
-// a full world, or every empty cell claimed by earlier births -- GetUInt(size);
-// without PREFER_EMPTY GetUInt(size), redrawn while it is the parent and
-// ALLOW_PARENT is 0.  Single worlds only (capi refuses strip tiles).
-#define SOUP_TRIES 64
+// 5297-5310; oracle soup_target): with PREFER_EMPTY one draw among the cells
+// empty at placement start that this round has not taken (e_list, compacted
+// before every round by k_empty_*: FindRandEmptyCell, :5650-5668, draws
+// uniformly among the empty cells), else -- a full world, or every empty cell
+// claimed by earlier births -- GetUInt(size); without PREFER_EMPTY
+// GetUInt(size), redrawn while it is the parent and ALLOW_PARENT is 0.
+// Single worlds only (capi refuses strip tiles).
 template <bool TILE>
 __device__ __forceinline__ bool place_pick_one(const DevWorld& W, int64_t r, int m) {
   const int parent = W.b_parent[r];
@@ -1071,11 +1071,7 @@ __device__ __forceinline__ bool place_pick_one(const DevWorld& W, int64_t r, int
     int t = -1;
     if (W.prefer_empty) {
       const uint32_t ne = (uint32_t)W.e_blk[(W.n + 255) / 256];
-      for (int k = 0; k < SOUP_TRIES && ne > 0u && t < 0; k++) {
-        const int c = W.e_list[rng_below(lo, hi, ctr, ne)];
-        if (!taken(c)) t = c;
-      }
-      if (t < 0) t = (int)rng_below(lo, hi, ctr, n);
+      t = ne > 0u ? W.e_list[rng_below(lo, hi, ctr, ne)] : (int)rng_below(lo, hi, ctr, n);
     } else {
       t = (int)rng_below(lo, hi, ctr, n);
       while (!W.allow_parent && n > 1u && t == parent) t = (int)rng_below(lo, hi, ctr, n);
@@ -1138,14 +1134,19 @@ __device__ __forceinline__ bool place_pick_one(const DevWorld& W, int64_t r, int
 #define QUEUE_LOOP(i) \
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, _qn = queue_len(W); i < _qn; \
        i += (int64_t)gridDim.x * blockDim.x)
-// BIRTH_METHOD 4 + PREFER_EMPTY: the cells empty at placement start (after
-// the slices' deaths), ascending -- FindRandEmptyCell's candidates (oracle
-// place_reset): per-256-cell counts, one block's exclusive scan over them
-// (e_blk[nb]: the total), the scatter
-__global__ __launch_bounds__(256) void k_empty_count(DevWorld W) {
+// BIRTH_METHOD 4 + PREFER_EMPTY: round m's candidates, ascending -- the cells
+// empty at placement start (after the slices' deaths) and, for m > 0, not
+// claimed in round m - 1 (FindRandEmptyCell's; oracle place_reset /
+// soup_round_cells): per-256-cell counts, one block's exclusive scan over them
+// (e_blk[nb]: the total), the scatter.  (Before round m's launch, occ holds
+// the winners up to round m - 2; round m - 1's are in its claims.)
+__device__ __forceinline__ bool soup_free(const DevWorld& W, int64_t c, int m) {
+  return c < W.n && W.occ[c] == 0 && (m == 0 || W.claim_r[m - 1][c] == 0ull);
+}
+__global__ __launch_bounds__(256) void k_empty_count(DevWorld W, int m) {
   __shared__ int ws[4];
   const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  const bool e = c < W.n && W.occ[c] == 0;
+  const bool e = soup_free(W, c, m);
   const int cnt = __popcll(__ballot(e));
   if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = cnt;
   __syncthreads();
@@ -1173,17 +1174,17 @@ __global__ __launch_bounds__(1024) void k_empty_scan(DevWorld W, int nb) {
   }
   if (threadIdx.x == 1023) W.e_blk[nb] = part[1023];
 }
-__global__ __launch_bounds__(256) void k_empty_scatter(DevWorld W) {
+__global__ __launch_bounds__(256) void k_empty_scatter(DevWorld W, int m) {
   __shared__ int ws[4];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  const bool e = c < W.n && W.occ[c] == 0;
-  const unsigned long long m = __ballot(e);
-  if (lane == 0) ws[wv] = __popcll(m);
+  const bool e = soup_free(W, c, m);
+  const unsigned long long bm = __ballot(e);
+  if (lane == 0) ws[wv] = __popcll(bm);
   __syncthreads();
   int base = W.e_blk[blockIdx.x];
   for (int k = 0; k < wv; k++) base += ws[k];
-  if (e) W.e_list[base + __popcll(m & ((1ull << lane) - 1ull))] = (int)c;
+  if (e) W.e_list[base + __popcll(bm & ((1ull << lane) - 1ull))] = (int)c;
 }
 
 // The divide mutations (k_place_pick_mut, k_tile_prep), by 256-thread blocks:
@@ -1477,7 +1478,7 @@ __device__ __forceinline__ long long newborn_budget(const DevWorld& W, int64_t c
                                                     uint32_t key, long long uds, double total) {
   if (!(total > 0.0) || uds <= 0) return 0;
   const long long n = (long long)floor(__dadd_rn(__dmul_rn((double)uds, nb_frac(t)), 0.5));
-  const double p = __ddiv_rn(merit_ok(merit) ? merit : 0.0, total);
+  const double p = __ddiv_rn(sched_weight(merit, 0u), total);   // (oracle: sched_weight, no head start)
   const long long b = binom_draw(n, p, node_draw(W.seed_lo, W.seed_hi, key, SALT_NEWBORN, (uint64_t)(W.cell0 + c)));
   return min(b, (long long)(BUDGET_PRIM - 1));
 }
@@ -2074,12 +2075,14 @@ void launch_world_post(const DevWorld& W, hipStream_t s, uint32_t key, int sub, 
   const int pm = has_divide_mutations(W) ? (int)((mut_grid(W) + 3) / 4) : 0;
   const int pf = (int)std::min<unsigned>(bb, 256u);   // finalize_phenotype blocks
   const int nbk = (int)bb + pf + pm;
-  if (W.birth_method == 4 && W.prefer_empty) {      // the soup's empty cells (k_empty_*)
+  const bool soup = W.birth_method == 4 && W.prefer_empty;
+  auto soup_cells = [&](int m) {                    // the soup's candidates of round m (k_empty_*)
     const int eb = (int)nblk(W.n, 256);
-    hipLaunchKernelGGL(k_empty_count, dim3(eb), dim3(256), 0, s, W);
+    hipLaunchKernelGGL(k_empty_count, dim3(eb), dim3(256), 0, s, W, m);
     hipLaunchKernelGGL(k_empty_scan, dim3(1), dim3(1024), 0, s, W, eb);
-    hipLaunchKernelGGL(k_empty_scatter, dim3(eb), dim3(256), 0, s, W);
-  }
+    hipLaunchKernelGGL(k_empty_scatter, dim3(eb), dim3(256), 0, s, W, m);
+  };
+  if (soup) soup_cells(0);
 #ifdef AVGPU_SPLIT_PICK_MUT
   hipLaunchKernelGGL(k_place_pick_mut, dim3(bb), dim3(256), 0, s, W, (int)bb, pf, 0, nbk);
   hipLaunchKernelGGL(k_place_pick_mut, dim3(pf), dim3(256), 0, s, W, (int)bb, pf, (int)bb, nbk);
@@ -2089,7 +2092,10 @@ void launch_world_post(const DevWorld& W, hipStream_t s, uint32_t key, int sub, 
 #endif
   hipLaunchKernelGGL(k_place_claim0, dim3(bb), dim3(256), 0, s, W, pred_out);
   if (pred_out && ev_pred) hipEventRecord(ev_pred, s);
-  for (int m = 1; m < 4; m++) hipLaunchKernelGGL(k_place_round, dim3(bb), dim3(256), 0, s, W, m);
+  for (int m = 1; m < 4; m++) {
+    if (soup) soup_cells(m);
+    hipLaunchKernelGGL(k_place_round, dim3(bb), dim3(256), 0, s, W, m);
+  }
   hipLaunchKernelGGL(k_activate, dim3(lane_grid(W)), dim3(64), 0, s, W, 1, key, sub, nsub);
 }
 

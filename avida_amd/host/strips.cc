@@ -577,11 +577,11 @@ int main(int argc, char** argv) {
   double v[4] = {dt, (double)(i1 - i0), (double)orgs, (double)dig};
   if (multi) {
     double* d = dalloc<double>(4);
-    HIP_OK(hipMemcpy(d, v, sizeof(v), hipMemcpyHostToDevice));
+    HIP_OK(hipMemcpyAsync(d, v, sizeof(v), hipMemcpyHostToDevice, s));
     NCCL_OK(ncclAllReduce(d + 1, d + 1, 2, ncclFloat64, ncclSum, comm, s));
     NCCL_OK(ncclAllReduce(d, d, 1, ncclFloat64, ncclMax, comm, s));
+    HIP_OK(hipMemcpyAsync(v, d, 3 * sizeof(double), hipMemcpyDeviceToHost, s));
     HIP_OK(hipStreamSynchronize(s));
-    HIP_OK(hipMemcpy(v, d, 3 * sizeof(double), hipMemcpyDeviceToHost));
   }
   if (rank == 0)
     printf("{\"tool\": \"avgpu_strips\", \"ranks\": %d, \"strips\": %d, \"untiled\": %s, \"side\": %lld, "

@@ -470,6 +470,36 @@ int avgpu_run_serial_updates(avgpu_world* w, int n_updates, avgpu_update_stats* 
  * in AVGPU_CNT_REC_EXHAUSTED. */
 int avgpu_set_serial_streams(avgpu_world* w, const double* sched, int64_t n_sched, const double* ctx,
                              int64_t n_ctx);
+/* The serial world's own state beyond the organisms' (checkpoint / resume):
+ * the two streams' positions (draws taken; recorded streams index their
+ * arrays), every cell's speculative credit and m_spec_die
+ * (ProcessStepSpeculative, main/cPopulation.cc:5740-5788; spec[c] = credit |
+ * die << 16) and connection-list rotation (cPopulationCell::Rotate, face[c]),
+ * and the persistent placement queues: soup_perm (n cells) -- BIRTH_METHOD 4's
+ * empty_cell_id_array, whose swaps persist across placements (:338-340,
+ * :5650-5668), the identity before its first use; reaper -- BIRTH_METHOD 5's
+ * reaper_queue (Setup's cells, then every activated cell pushed at the front,
+ * :343-347, :1358-1361), rear (eldest, the next PopRear) first, reaper_len -1
+ * before it exists (it is built at the first serial update from the living
+ * cells).  started = 0: no serial update has run (everything at its start).
+ * get: any array may be NULL (reaper needs reaper_cap >= reaper_len, at most
+ * 2n + 64).  set: after avgpu_set_states; started = 0 leaves the world alone;
+ * NULL arrays keep theirs; reaper_len < 0 builds the queue again at the next
+ * serial update.  Injection (avgpu_set_orgs / avgpu_set_org) into a serial
+ * BIRTH_METHOD 5 world whose queue exists takes an occupied cell's entry out
+ * (the first from the front, :6964-6968) and pushes the cell at the front, as
+ * the reference's InjectGenome + ActivateOrganism do. */
+typedef struct avgpu_serial_state {
+  int64_t sched_pos;   /* draws taken from the scheduler's stream */
+  int64_t ctx_pos;     /* draws taken from the context stream */
+  int64_t reaper_len;  /* BIRTH_METHOD 5's queue length; -1: not built */
+  int32_t started;     /* 1: the world has run a serial update (or had its state set) */
+  int32_t pad_;
+} avgpu_serial_state;
+int avgpu_get_serial_state(avgpu_world* w, avgpu_serial_state* st, int32_t* spec, uint8_t* face,
+                           int32_t* soup_perm, int32_t* reaper, int64_t reaper_cap);
+int avgpu_set_serial_state(avgpu_world* w, const avgpu_serial_state* st, const int32_t* spec, const uint8_t* face,
+                           const int32_t* soup_perm, const int32_t* reaper);
 /* The same update split around an external all-reduce (multi-GPU tiles,
  * cMultiProcessWorld::CalculateUpdateSize main/cMultiProcessWorld.cc:375-405):
  * avgpu_update_totals writes the tile's {sum of scheduler weights, organisms}

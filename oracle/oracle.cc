@@ -1211,12 +1211,16 @@ void dump_state(const World& w, const Org& o, avgpu_cpu_state* s, uint8_t* ops, 
 // update; the batch update places it at the update's end and gives it that
 // share in the next.  hstart 0 -> the merit itself.
 // A merit that is NaN, negative or infinite is never scheduled (weight 0),
-// nor is a weight that overflows; the device's merit_ok / sched_weight.
+// nor is a weight that overflows; a weight is at most 2^990, so that the
+// scheduler's sums over up to 2^33 organisms stay finite (a few merits near
+// DBL_MAX would sum to inf and zero every draw); the device's merit_ok /
+// sched_weight.
+static constexpr double WEIGHT_CAP = 0x1p990;
 static inline bool merit_ok(double m) { return m >= 0.0 && m <= 1.7976931348623157e308; }
 static inline double sched_weight(const Org& o) {
   if (!merit_ok(o.merit)) return 0.0;
   const double w = o.hstart ? o.merit * (1.0 + (double)o.hstart * (1.0 / 65536.0)) : o.merit;
-  return merit_ok(w) ? w : 0.0;
+  return merit_ok(w) ? std::min(w, WEIGHT_CAP) : 0.0;
 }
 
 // ---------------------------------------------------------------------------
@@ -1618,6 +1622,7 @@ int orc_load_env(void* h, int n, const avgpu_reaction* r) {
   return 0;
 }
 
+static void reaper_inject(World& w, int64_t c, bool was_alive);
 int orc_set_orgs(void* h, int64_t first, int64_t count, const uint8_t* genomes, const int32_t* lens,
                  const double* merits, const int32_t* inputs, int deterministic) {
   World& w = *(World*)h;
@@ -1625,6 +1630,7 @@ int orc_set_orgs(void* h, int64_t first, int64_t count, const uint8_t* genomes, 
   for (int64_t i = 0; i < count; i++) {
     int64_t c = first + i;
     Org& o = w.orgs[c];
+    reaper_inject(w, c, o.alive);
     setup_inject(w, o, genomes + off, lens[i], merits ? merits[i] : 0.0);
     off += lens[i];
     derive_key((uint32_t)w.cfg.seed, (uint32_t)(w.cfg.seed >> 32), (uint32_t)(w.cell0 + c), 0xA5A5A5A5U,
@@ -1824,6 +1830,11 @@ int orc_set_clock(void* h, const avgpu_update_stats* last) {
   if (last->seed != 0) {   // zero: stats of an older checkpoint -- the configured seed stays
     w.cfg.seed = last->seed;
     w.stats.seed = last->seed;
+    // the serial world's two streams are keyed by the seed too (positions stay)
+    derive_key((uint32_t)w.cfg.seed, (uint32_t)(w.cfg.seed >> 32), 0x5CEDu, 0xC0FFEEu,
+               &w.global_rng.lo, &w.global_rng.hi);
+    derive_key((uint32_t)w.cfg.seed, (uint32_t)(w.cfg.seed >> 32), 0xC7C7u, 0x5EED5u,
+               &w.ctx_rng.lo, &w.ctx_rng.hi);
   }
   // the adaptive sub-step predictor the next update decides by (0: one step)
   w.pred_acc = last->sched_pred;
@@ -2310,22 +2321,19 @@ static double position_value(const World& w, int64_t c) {
 
 // BIRTH_METHOD 4 (POSITION_OFFSPRING_FULL_SOUP_RANDOM, main/cPopulation.cc:
 // 5297-5310): with PREFER_EMPTY, FindRandEmptyCell (:5650-5668) -- a cell drawn
-// uniformly among the empty ones; here the cells empty at the batch step's end
-// (empty_cells, ascending) that this round has not taken, by up to SOUP_TRIES
-// draws; none (a full world, or every empty cell claimed by earlier births):
-// GetUInt(size) over the whole world.  Without PREFER_EMPTY: GetUInt(size),
-// redrawn while it is the parent and ALLOW_PARENT is 0.  The parent's cell
-// without ALLOW_PARENT: ActivateOffspring drops the offspring (:706-713).
-static constexpr int SOUP_TRIES = 64;
-template <class Taken>
-static int64_t soup_target(World& w, Birth& b, Taken taken) {
+// uniformly among the empty ones (the reference swap-removes the occupied
+// entries it draws and draws again); here one draw among the cells empty at
+// the batch step's end that this round has not taken (empty_cells, ascending,
+// recompacted before every round: soup_round_cells); none (a full world, or
+// every empty cell claimed by earlier births): GetUInt(size) over the whole
+// world.  Without PREFER_EMPTY: GetUInt(size), redrawn while it is the parent
+// and ALLOW_PARENT is 0.  The parent's cell without ALLOW_PARENT:
+// ActivateOffspring drops the offspring (:706-713).
+static int64_t soup_target(World& w, Birth& b) {
   const uint32_t n = (uint32_t)w.ncells;
   if (w.cfg.prefer_empty) {
     const uint32_t ne = (uint32_t)w.empty_cells.size();
-    for (int k = 0; k < SOUP_TRIES && ne > 0; k++) {
-      const int64_t c = w.empty_cells[b.rng.uint_below(ne)];
-      if (!taken(c)) return c;
-    }
+    if (ne > 0) return w.empty_cells[b.rng.uint_below(ne)];
     return b.rng.uint_below(n);
   }
   int64_t c = b.rng.uint_below(n);
@@ -2337,7 +2345,7 @@ template <class Taken>
 static bool place_pick(World& w, int64_t i, int m, Taken taken) {
   Birth& b = w.births[i];
   if (w.cfg.birth_method == 4) {
-    const int64_t t = soup_target(w, b, taken);
+    const int64_t t = soup_target(w, b);
     if (t == b.parent && !w.cfg.allow_parent) { b.target = -1; w.bstate[i] = (int8_t)(BS_NO_CELL - m); return false; }
     b.target = t;
     w.prio[i] = claim_key(b.t, taken(t), b.rng.next(), w.cell0 + b.parent, b.seq);
@@ -2370,6 +2378,15 @@ static bool place_pick(World& w, int64_t i, int m, Taken taken) {
   w.prio[i] = claim_key(b.t, taken(b.target), b.rng.next(), w.cell0 + b.parent, b.seq);
   w.tgt_r[m][i] = b.target;
   return true;
+}
+
+// round m > 0's soup candidates: the cells still empty and not claimed in
+// round m - 1 (the device's k_empty_* with m)
+static void soup_round_cells(World& w, int m) {
+  if (w.cfg.birth_method != 4 || !w.cfg.prefer_empty) return;
+  const std::vector<uint64_t>& prev = w.claim_r[m - 1];
+  w.empty_cells.clear();
+  for (int64_t c = 0; c < w.ncells; c++) if (!w.occ[c] && !prev[c]) w.empty_cells.push_back(c);
 }
 
 static void place_reset(World& w, int64_t ext) {
@@ -2537,6 +2554,7 @@ static int run_update_impl(World& w) {
     // launches 1..3: resolve round m-1, pick round m
     for (int m = 1; m < 4; m++) {
       const std::vector<uint64_t>& prev = w.claim_r[m - 1];
+      soup_round_cells(w, m);
       for (int64_t i = 0; i < nbirth; i++) {
         if (w.bstate[i] != BS_PENDING) continue;
         Birth& b = w.births[i];
@@ -3119,6 +3137,17 @@ static void reaper_setup(World& w) {
   for (int64_t c = 0; c < w.ncells; c++) w.reaper.push_front(c);
   for (int64_t c = 0; c < w.ncells; c++) if (w.orgs[c].alive) w.reaper.push_front(c);
 }
+// an injection into cell c once the queue exists: an occupied cell's entry
+// out (the first from the front, InjectGenome main/cPopulation.cc:6964-6968),
+// the cell pushed at the front (ActivateOrganism :1358-1361)
+static void reaper_inject(World& w, int64_t c, bool was_alive) {
+  if (w.cfg.birth_method != 5 || !w.reaper_init) return;
+  if (was_alive) {
+    auto it = std::find(w.reaper.begin(), w.reaper.end(), c);
+    if (it != w.reaper.end()) w.reaper.erase(it);
+  }
+  w.reaper.push_front(c);
+}
 static int64_t serial_eldest(World& w, int64_t parent) {
   int64_t c = w.reaper.back();
   w.reaper.pop_back();
@@ -3166,7 +3195,7 @@ static int serial_place(World& w, SerialSched& sch, Birth& b) {
   w.orgs[t].spec_count = 0;                               // InsertOrganism (main/cPopulationCell.cc:270-271)
   w.orgs[t].spec_die = false;
   sch.set(t, w.orgs[t].merit);
-  if (parent_alive) {                                     // Rotate(parent_cell) :935-944
+  if (parent_alive && w.cfg.birth_method < 4) {          // Rotate(parent_cell) :935-944 (local methods, :938)
     int64_t base[8];
     const int nb = conn_base(w, t, base);
     for (int k = 0; k < nb; k++) if (base[k] == b.parent) { w.face[t] = (uint8_t)k; break; }
@@ -3279,4 +3308,68 @@ int orc_run_serial_updates(void* h, int n_updates, avgpu_update_stats* out) {
   return 0;
 }
 
+}  // extern "C"
+
+extern "C" {
+// the serial world's own state (avgpu_get_serial_state / avgpu_set_serial_state):
+// stream positions, speculative credit and death, faces, soup_perm (identity
+// before its first use), the reaper queue rear first (-1: not built yet)
+int orc_get_serial_state(void* h, avgpu_serial_state* st, int32_t* spec, uint8_t* face, int32_t* soup_perm,
+                         int32_t* reaper, int64_t cap) {
+  World& w = *(World*)h;
+  const bool started = (int64_t)w.face.size() == w.ncells;
+  const int64_t n = w.reaper_init ? (int64_t)w.reaper.size() : -1;
+  if (st) {
+    memset(st, 0, sizeof(*st));
+    st->sched_pos = w.global_rng.ctr;
+    st->ctx_pos = w.ctx_rng.ctr;
+    st->reaper_len = n;
+    st->started = started ? 1 : 0;
+  }
+  for (int64_t c = 0; c < w.ncells; c++) {
+    if (spec) spec[c] = (w.orgs[c].spec_count & 0xFFFF) | (w.orgs[c].spec_die ? 1 << 16 : 0);
+    if (face) face[c] = started ? w.face[c] : 0;
+    if (soup_perm) soup_perm[c] = (int32_t)((int64_t)w.soup_cells.size() == w.ncells ? w.soup_cells[c] : c);
+  }
+  if (reaper && n > 0) {
+    if (cap < n) return fail(AVGPU_EINVAL, "reaper buffer too small");
+    int64_t k = 0;
+    for (auto it = w.reaper.rbegin(); it != w.reaper.rend(); ++it) reaper[k++] = (int32_t)*it;
+  }
+  return 0;
+}
+
+int orc_set_serial_state(void* h, const avgpu_serial_state* st, const int32_t* spec, const uint8_t* face,
+                         const int32_t* soup_perm, const int32_t* reaper) {
+  World& w = *(World*)h;
+  if (!st) return fail(AVGPU_EINVAL, "serial state");
+  if (!st->started) return 0;
+  if (soup_perm) {
+    std::vector<char> seen((size_t)w.ncells, 0);
+    for (int64_t c = 0; c < w.ncells; c++) {
+      if (soup_perm[c] < 0 || soup_perm[c] >= w.ncells || seen[(size_t)soup_perm[c]])
+        return fail(AVGPU_EINVAL, "soup_perm is not a permutation of the cells");
+      seen[(size_t)soup_perm[c]] = 1;
+    }
+  }
+  const int64_t len = st->reaper_len;
+  if (len > 2 * w.ncells + 64) return fail(AVGPU_EINVAL, "reaper queue longer than 2n + 64");
+  if (len > 0 && !reaper) return fail(AVGPU_EINVAL, "reaper queue");
+  for (int64_t k = 0; k < len; k++)
+    if (reaper[k] < 0 || reaper[k] >= w.ncells) return fail(AVGPU_EINVAL, "reaper queue cell out of range");
+  w.global_rng.ctr = (uint32_t)st->sched_pos;
+  w.ctx_rng.ctr = (uint32_t)st->ctx_pos;
+  if ((int64_t)w.face.size() != w.ncells) w.face.assign(w.ncells, 0);
+  for (int64_t c = 0; c < w.ncells; c++) {
+    if (spec) { w.orgs[c].spec_count = spec[c] & 0xFFFF; w.orgs[c].spec_die = (spec[c] >> 16) & 1; }
+    if (face) w.face[c] = face[c];
+  }
+  if (soup_perm) w.soup_cells.assign(soup_perm, soup_perm + w.ncells);
+  if (w.cfg.birth_method == 5) {
+    w.reaper.clear();
+    w.reaper_init = len >= 0;
+    for (int64_t k = 0; k < len; k++) w.reaper.push_front(reaper[k]);
+  }
+  return 0;
+}
 }  // extern "C"

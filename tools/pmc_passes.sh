@@ -22,3 +22,5 @@ python tools/pmc_summary.py "gpurun_out/pmc_${TAG}_*/**/*counter_collection.csv"
   --json gpurun_out/pmc_k_interpret320.json --world 1024x1024 \
   --source "profiles/${TAG}_pmc_k_interpret320.txt (rocprofv3 --pmc, 5 passes over bench.py --steps 5 --warmup 2 --no-cpu after 150 burn-in updates; average over the class-0 dispatches)" \
   > gpurun_out/${TAG}_pmc_k_interpret320.txt
+python tools/pmc_summary.py "gpurun_out/pmc_${TAG}_*/**/*counter_collection.csv" 'k_interpret<(316|320),[^(]*true>\(' \
+  > gpurun_out/${TAG}_pmc_k_interpret320_newborn.txt

@@ -14,7 +14,13 @@ import re
 from collections import defaultdict
 
 
-def summarize(pattern, regex=r"k_interpret<(316|320)[,>]|k_interpretILi(316|320)"):
+# the class-0 main pass (its last template flag, NB, false; the newborn pass
+# is the same kernel with NB = true: tools/pmc_summary.py PATTERN NB_REGEX)
+MAIN = r"k_interpret<(316|320),[^(]*false>\("
+NB_REGEX = r"k_interpret<(316|320),[^(]*true>\("
+
+
+def summarize(pattern, regex=MAIN):
     vals = defaultdict(list)
     for f in sorted(glob.glob(pattern, recursive=True)):
         with open(f) as fh:
@@ -28,7 +34,7 @@ def summarize(pattern, regex=r"k_interpret<(316|320)[,>]|k_interpretILi(316|320)
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("pattern")
-    ap.add_argument("regex", nargs="?", default=r"k_interpret<(316|320)[,>]|k_interpretILi(316|320)")
+    ap.add_argument("regex", nargs="?", default=MAIN)
     ap.add_argument("--json")
     ap.add_argument("--world", default="1024x1024")
     ap.add_argument("--source", default="")

@@ -8,7 +8,12 @@ from collections import defaultdict
 def main():
     rows = list(csv.DictReader(open(sys.argv[1])))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-    idx = [i for i, r in enumerate(rows) if ("k_interpret<316" in r["Kernel_Name"] or "k_interpret<320" in r["Kernel_Name"])]
+    # anchors: the class-0 main pass (the newborn pass, template flag NB = true,
+    # is a tail item of its own)
+    def main_pass(r):
+        n = r["Kernel_Name"]
+        return ("k_interpret<316" in n or "k_interpret<320" in n) and not n.split("(DevWorld")[0].endswith("true>")
+    idx = [i for i, r in enumerate(rows) if main_pass(r)]
     acc = defaultdict(float)
     gaps = aux_over = 0.0
     steps = 0
@@ -23,8 +28,10 @@ def main():
                 continue
             gaps += max(0, s - t) / 1e3
             name = r["Kernel_Name"].replace("void ", "").replace("(anonymous namespace)::", "").split("(")[0]
-            if name.startswith("k_interpret"):
-                name = "spill " + name
+            if name.startswith("k_interpret<316") or name.startswith("k_interpret<320"):
+                name = "newborn pass " + name
+            elif name.startswith("k_interpret"):
+                name = ("newborn " if name.endswith("true>") else "") + "spill " + name
             if name == "k_place_pick_mut":   # the split diagnostic build launches its parts apart
                 name += " [%d blocks]" % (int(r["Grid_Size_X"]) // int(r["Workgroup_Size_X"]))
             acc[name] += (e - s) / 1e3
@@ -35,7 +42,7 @@ def main():
     for k, v in sorted(acc.items(), key=lambda kv: -kv[1]):
         print("%-40s %7.1f us/update" % (k, v / steps))
     print("%-40s %7.1f us/update" % ("gaps (incl. waits for aux streams)", gaps / steps))
-    print("%-40s %7.1f us/update" % ("total outside class 0", tot / steps))
+    print("%-40s %7.1f us/update" % ("total outside the class-0 main pass", tot / steps))
 
 
 if __name__ == "__main__":

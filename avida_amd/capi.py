@@ -79,6 +79,7 @@ class AvgpuCfg(C.Structure):
         ("require_exact_copy", C.c_int32), ("fitness_method", C.c_int32),
         ("juv_period", C.c_int32), ("no_mut_insts_len", C.c_int32),
         ("test_fitness_measures", C.c_int32), ("pad_cfg2", C.c_int32),
+        ("no_mut_insts", C.c_char * 64),
     ]
 
 
@@ -312,7 +313,9 @@ def cfg_from_avida(cfg, seed=None) -> AvgpuCfg:
     for key, field, default, kind in REFUSED_KNOBS:
         setattr(c, field, _num(g(key, default), kind, default))
     nmi = g("NO_MUT_INSTS", "")
-    c.no_mut_insts_len = len(str(nmi).strip()) if nmi not in (None, 0) else 0
+    nmi = str(nmi).strip() if nmi not in (None, 0) else ""
+    c.no_mut_insts_len = len(nmi)
+    c.no_mut_insts = nmi.encode()[:63]
     c.test_fitness_measures = int(any(_num(g(k, 0), float, 1.0) != 0.0 for k in TEST_FITNESS_KNOBS))
     return c
 

@@ -343,14 +343,17 @@ std::string unsupported_cfg(const avgpu_cfg& c) {
   if (c.reset_inputs_on_divide != 0) return "RESET_INPUTS_ON_DIVIDE";
   if (c.epigenetic_method != 0) return "EPIGENETIC_METHOD";
   if (c.min_cycles != 0) return "MIN_CYCLES";
-  if (c.required_task >= 0 || c.immunity_task >= 0 || c.required_reaction >= 0 || c.immunity_reaction >= 0 ||
-      c.require_single_reaction != 0 || c.max_unique_task_count >= 0)
-    return "REQUIRED_TASK / IMMUNITY_TASK / REQUIRED_REACTION / IMMUNITY_REACTION / REQUIRE_SINGLE_REACTION / "
-           "MAX_UNIQUE_TASK_COUNT";
+  if (c.required_task < -1 || c.immunity_task < -1 || c.required_reaction < -1 || c.immunity_reaction < -1 ||
+      c.required_task >= AVGPU_MAX_REACTIONS || c.immunity_task >= AVGPU_MAX_REACTIONS ||
+      c.required_reaction >= 12 || c.immunity_reaction >= 12)
+    return "REQUIRED_TASK / IMMUNITY_TASK outside the task library, REQUIRED_REACTION / IMMUNITY_REACTION "
+           "beyond reaction 11";
   if (c.require_exact_copy != 0) return "REQUIRE_EXACT_COPY";
   if (c.fitness_method != 0) return "FITNESS_METHOD other than 0";
   if (c.juv_period != 0) return "JUV_PERIOD";
-  if (c.no_mut_insts_len != 0) return "NO_MUT_INSTS";
+  if (c.no_mut_insts_len < 0 || c.no_mut_insts_len > 63 ||
+      (size_t)c.no_mut_insts_len != strnlen(c.no_mut_insts, sizeof(c.no_mut_insts)))
+    return "NO_MUT_INSTS longer than 63 symbols, or no_mut_insts_len not its length";
   if (c.test_fitness_measures != 0) return "REVERT_* / STERILIZE_* (Divide_TestFitnessMeasures1)";
   return std::string();
 }
@@ -413,6 +416,9 @@ int copy_tables(avgpu_world* dst, const avgpu_world* src) {
   D.n_ops = S.n_ops; D.rand_total = S.rand_total; D.fill_code = S.fill_code;
   D.n_react = S.n_react;
   D.env_simple = S.env_simple; D.env_react_mask = S.env_react_mask; D.env_once_mask = S.env_once_mask;
+  D.no_mut_mask = S.no_mut_mask;                       // (load_instset / load_env derive these)
+  D.req_task = S.req_task; D.imm_task = S.imm_task; D.req_react = S.req_react; D.imm_react = S.imm_react;
+  D.single_react = S.single_react; D.max_task_cnt = S.max_task_cnt; D.div_req = S.div_req;
   // the source's tables as its stream leaves them, into the destination on its own
   HIPCHK(hipStreamSynchronize(src->stream));
   HIPCHK(hipMemcpyAsync(D.task_tab, S.task_tab, 32 * sizeof(double), hipMemcpyDeviceToDevice, dst->stream));
@@ -715,6 +721,17 @@ int avgpu_load_instset(avgpu_world* w, int n, const uint8_t* handler_id, const i
     w->code2op[h] = (int16_t)i;
   }
   if (total <= 0) return fail(AVGPU_EINVAL, "zero total redundancy");
+  // NO_MUT_INSTS over the handler codes the tapes hold (op i's symbol:
+  // Instruction::GetSymbol, core/InstructionSequence.cc:69-106, its first
+  // character -- '+', '-', '~', '?' past op 61)
+  uint64_t nomut = 0;
+  for (int i = 0; i < n; i++) {
+    const int k = i % 62;
+    const char sym = i >= 62 ? "+-~?"[std::min(i / 62, 4) - 1]
+                             : (char)(k < 26 ? 'a' + k : (k < 52 ? 'A' + k - 26 : '0' + k - 52));
+    if (memchr(w->cfg.no_mut_insts, sym, (size_t)w->cfg.no_mut_insts_len)) nomut |= 1ull << code[i];
+  }
+  w->W.no_mut_mask = nomut;
   w->n_ops = n;
   w->W.n_ops = n;
   w->W.rand_total = total;
@@ -755,6 +772,34 @@ int avgpu_load_env(avgpu_world* w, int nreact, const avgpu_reaction* r) {
     memcpy(t + RT_ADD, &bonus, 8);
   }
   W.n_react = nreact;
+  // cOrganism::Divide_CheckViable's requirements (main/cOrganism.cc:788-919):
+  // REQUIRED_TASK / IMMUNITY_TASK index the task library -- the distinct
+  // tasks in the order of their first REACTION line (cTaskLib::AddTask) --,
+  // the reaction knobs the reactions in environment order
+  {
+    int lib[AVGPU_MAX_REACTIONS], nlib = 0;
+    for (int i = 0; i < nreact; i++) {
+      bool seen = false;
+      for (int k = 0; k < nlib; k++) seen = seen || lib[k] == r[i].task;
+      if (!seen) lib[nlib++] = r[i].task;
+    }
+    const avgpu_cfg& c = w->cfg;
+    auto task_of = [&](int t) { return t >= 0 && t < nlib ? lib[t] : -2; };
+    W.req_task = c.required_task >= 0 ? task_of(c.required_task) : -1;
+    W.imm_task = c.immunity_task >= 0 ? task_of(c.immunity_task) : -1;
+    if (W.req_task == -2 || W.imm_task == -2)
+      return fail(AVGPU_EUNSUPPORTED, "REQUIRED_TASK / IMMUNITY_TASK past the environment's task library");
+    if (c.required_reaction >= nreact || c.immunity_reaction >= nreact)
+      return fail(AVGPU_EUNSUPPORTED, "REQUIRED_REACTION / IMMUNITY_REACTION past the environment's reactions");
+    if (c.require_single_reaction && nreact > 12)
+      return fail(AVGPU_EUNSUPPORTED, "REQUIRE_SINGLE_REACTION with more than 12 reactions");
+    W.req_react = c.required_reaction;
+    W.imm_react = c.immunity_reaction;
+    W.single_react = c.require_single_reaction ? 1 : 0;
+    W.max_task_cnt = c.max_unique_task_count;
+    W.div_req = (W.req_task >= 0 || (!W.single_react && W.req_react >= 0) || W.single_react ||
+                 W.max_task_cnt > 0) ? 1 : 0;
+  }
   // simple-environment fast path of the IO task check (interp.hip)
   double ttab[32];
   for (int t = 0; t < 16; t++) { ttab[t] = 1.0; ttab[16 + t] = 0.0; }

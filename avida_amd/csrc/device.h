@@ -255,6 +255,11 @@ struct DevWorld {
   uint64_t th_copy_ins, th_copy_del, th_copy_uni, th_copy_slip;
   double p_copy_ins, p_copy_del, p_copy_uni, p_copy_slip;
   int32_t copy_ext;
+  uint64_t no_mut_mask;   // NO_MUT_INSTS: handler codes copy mutations leave alone (bit per code)
+  // Divide_CheckViable's task / reaction requirements (avgpu_load_env): the
+  // required / immunity task (avgpu_task, -1 none), reaction (index, -1
+  // none), REQUIRE_SINGLE_REACTION, MAX_UNIQUE_TASK_COUNT; div_req: any set
+  int32_t req_task, imm_task, req_react, imm_react, single_react, max_task_cnt, div_req;
   uint64_t th_div_site;   // DIV_MUT_PROB (per-site substitutions on divide)
   double p_div_site;
   uint64_t th_par_site;   // PARENT_MUT_PROB (per-site substitutions in the parent)

@@ -566,6 +566,7 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
   const int k_require_allocate = DEF ? 1 : W.require_allocate, k_alloc_method = DEF ? 0 : W.alloc_method;
   const uint64_t k_th_copy_mut = W.th_copy_mut;
   const int k_copy_ext = DEF ? 0 : W.copy_ext;
+  const uint64_t k_no_mut = DEF ? 0ull : W.no_mut_mask;   // NO_MUT_INSTS (checkNoMutList)
   const uint64_t k_th_copy_ins = DEF ? 0ull : W.th_copy_ins, k_th_copy_del = DEF ? 0ull : W.th_copy_del;
   const uint64_t k_th_copy_uni = DEF ? 0ull : W.th_copy_uni, k_th_copy_slip = DEF ? 0ull : W.th_copy_slip;
   const int k_slip_whole = DEF ? 0 : W.slip_copy_mode;
@@ -725,7 +726,8 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
       // common path falls through instead of branching around it)
       const bool cmut = mode != AVGPU_MODE_TEST && k_th_copy_mut && draw_p(k_th_copy_mut, W.p_copy_mut);
       if (__builtin_expect(__ballot(cmut) != 0ull, 0)) {
-        if (cmut) v = rand_code();
+        // a listed read instruction keeps itself (no GetRandomInst draw, :7144)
+        if (cmut && !((k_no_mut >> v) & 1ull)) v = rand_code();
       }
       // the write head's executed flag: as read, or just set if it is the IP
       const int wex = (wh == ip) ? TF_EXEC : (dst_byte & TF_EXEC);
@@ -747,6 +749,19 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
         if (k_th_copy_del) e_del = draw_p(k_th_copy_del, W.p_copy_del);
         if (k_th_copy_uni && draw_p(k_th_copy_uni, W.p_copy_uni)) e_uni = (int)draw_below((uint32_t)(2 * k_n_ops + 1));
         const bool e_slp = k_th_copy_slip && draw_p(k_th_copy_slip, W.p_copy_slip);
+        // NO_MUT_INSTS: the uniform mutation leaves a listed write-head
+        // instruction (doUniformCopyMutation, cpu/cHardwareBase.cc:597-612),
+        // the one at the write head after the insertion / deletion above (a
+        // head past the end reads none)
+        if (e_uni >= 0 && k_no_mut) {
+          const bool ins = e_ins >= 0 && M < AVGPU_MAX_GENOME;
+          const bool del = e_del && M + (ins ? 1 : 0) > 1;
+          int at;
+          if (ins) at = del ? v : e_ins;                        // the inserted site, or (removed again) the written one
+          else if (del) at = wh + 1 < M ? (T[wh + 1] & CODE_MASK) : -1;
+          else at = v;
+          if (at >= 0 && ((k_no_mut >> at) & 1ull)) e_uni = -1;
+        }
         const bool ev = e_ins >= 0 || e_del || e_uni >= 0 || e_slp;
         if (__builtin_expect(__ballot(ev) != 0ull, 0)) {
           if (ev) {
@@ -1251,6 +1266,29 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
           double bon = bonus;
           if (ok) {  // cOrganism::Divide_CheckViable (main/cOrganism.cc:788-919)
             if (bon < p_req) ok = false;
+            if (!DEF && W.div_req) {
+              // the required task unless the immunity task was done, the
+              // required reaction likewise (no stolen reactions on this
+              // path), at most MAX_UNIQUE_TASK_COUNT distinct tasks, with
+              // REQUIRE_SINGLE_REACTION some reaction (:826-880)
+              int nt = 0, ct_req = 0, ct_imm = 0, cr_req = 0, cr_imm = 0, any = 0;
+#pragma unroll
+              for (int q = 0; q < AVGPU_NUM_LOGIC_TASKS; q++) {
+                nt += tc[q] > 0 ? 1 : 0;
+                ct_req = q == W.req_task ? tc[q] : ct_req;
+                ct_imm = q == W.imm_task ? tc[q] : ct_imm;
+              }
+#pragma unroll
+              for (int q = 0; q < 12; q++) {
+                cr_req = q == W.req_react ? rc[q] : cr_req;
+                cr_imm = q == W.imm_react ? rc[q] : cr_imm;
+                any |= rc[q];
+              }
+              if (W.req_task >= 0 && ct_req == 0 && (W.imm_task < 0 || ct_imm == 0)) ok = false;
+              if (!W.single_react && W.req_react >= 0 && cr_req == 0 && (W.imm_react < 0 || cr_imm == 0)) ok = false;
+              if (W.max_task_cnt > 0 && nt > W.max_task_cnt) ok = false;
+              if (W.single_react && any == 0) ok = false;
+            }
             const double base0 = (double)size_merit(p_bmm, p_bcm, blen, dcop, dexe);
             double b0 = bon;
             if (p_mdb != 0.0) b0 = p_mdb;
@@ -2446,7 +2484,7 @@ static bool def_knobs(const DevWorld& W) {
          W.base_merit_method == 4 && W.th_div_uni == 0 && !W.seg_any && W.th_par_site == 0 && W.th_par_ins == 0 &&
          W.th_par_del == 0 && W.size_range == 2.0 && W.min_exe_lines == 0.5 &&
          W.min_copied_lines == 0.5 && W.required_bonus == 0.0 && W.default_bonus == 1.0 && W.rand_total <= 256 &&
-         !W.copy_ext && !W.track_age;
+         !W.copy_ext && !W.track_age && W.no_mut_mask == 0 && !W.div_req;
 }
 
 // NB: the newborn pass of a world update (launch_newborns): the same launches

@@ -211,11 +211,19 @@ typedef struct avgpu_cfg {
   int32_t require_exact_copy;      /* REQUIRE_EXACT_COPY (0) */
   int32_t fitness_method;          /* FITNESS_METHOD (0) */
   int32_t juv_period;              /* JUV_PERIOD (0) */
-  int32_t no_mut_insts_len;        /* strlen(NO_MUT_INSTS) (0) */
+  int32_t no_mut_insts_len;        /* strlen(no_mut_insts) (0) */
   /* non-zero when any REVERT_* / STERILIZE_* probability or STERILIZE_UNSTABLE
    * is set (Divide_TestFitnessMeasures1, cpu/cHardwareBase.cc:978-1085) */
   int32_t test_fitness_measures;
   int32_t pad_cfg2;
+  /* NO_MUT_INSTS (""): symbols of the instructions that copy mutations leave
+   * alone (cHardwareCPU::checkNoMutList, cpu/cHardwareCPU.cc:797-810): an
+   * h-copy whose read instruction's symbol (Instruction::GetSymbol's first
+   * character, core/InstructionSequence.cc:69-106) is listed draws its copy
+   * mutation but keeps the instruction (:7144), and a uniform copy mutation
+   * leaves a listed write-head instruction (cpu/cHardwareBase.cc:597-612).
+   * NUL-terminated, at most 63 symbols; no_mut_insts_len its length. */
+  char no_mut_insts[64];
 } avgpu_cfg;
 
 /* One REACTION line of environment.cfg (main/cEnvironment.cc:1185-1211,

@@ -137,6 +137,8 @@ struct InstSet {
   int64_t cum[256];  // cOrderedWeightedIndex cumulative weights (tools/cOrderedWeightedIndex.cc:43-50)
   int64_t total = 0;
   bool is_nop(int op) const { return op >= 0 && op < n && nopmod[op] >= 0; }
+  uint64_t nomut = 0;   // NO_MUT_INSTS: the ops (bit per op) copy mutations leave alone
+  bool no_mut(int op) const { return op >= 0 && op < 64 && ((nomut >> op) & 1ull); }
   // cInstSet::GetRandomInst (cpu/cInstSet.cc:83-88) on the project RNG
   int random_inst(Stream& s) const {
     uint32_t r = s.uint_below((uint32_t)total);
@@ -333,6 +335,7 @@ struct World {
   int step_sub = 0, step_k = 1;
   int64_t step_uds = 0;
   int64_t upd_ud = 0;      // the update's picks UD, fixed at its first batch step
+  int req_task = -1, imm_task = -1;   // REQUIRED_TASK / IMMUNITY_TASK as avgpu_task ids (orc_load_env)
   double step_total = 0.0;
   int64_t acc_placed = 0, acc_dropped = 0, acc_insts = 0, acc_deaths = 0, acc_divides = 0, acc_slices = 0;
   int64_t acc_overwritten = 0, acc_cancelled = 0;
@@ -767,8 +770,27 @@ struct Exec {
     for (int i = parent_size; i < parent_size + child_size; i++) if (o.flg[i] & F_COPIED) copied++;
     const int min_copied = (int)(child_size * w.cfg.min_copied_lines);
     if (copied < min_copied) { return false; }
-    // cOrganism::Divide_CheckViable
+    // cOrganism::Divide_CheckViable (main/cOrganism.cc:788-919)
     if (o.cur_bonus < w.cfg.required_bonus) return false;
+    // the required task unless the immunity task was done (:826-832)
+    if (w.req_task >= 0 && o.cur_task[w.req_task] == 0 && (w.imm_task < 0 || o.cur_task[w.imm_task] == 0))
+      return false;
+    // the required reaction likewise (:839-847; nothing is stolen on this path)
+    const int rr = w.cfg.required_reaction, ir = w.cfg.immunity_reaction;
+    if (w.cfg.require_single_reaction == 0 && rr >= 0 && o.cur_react[rr] == 0 && (ir < 0 || o.cur_react[ir] == 0))
+      return false;
+    // at most MAX_UNIQUE_TASK_COUNT distinct tasks (:849-862)
+    if (w.cfg.max_unique_task_count > 0) {
+      int nt = 0;
+      for (int t = 0; t < AVGPU_NUM_LOGIC_TASKS; t++) nt += o.cur_task[t] > 0;
+      if (nt > w.cfg.max_unique_task_count) return false;
+    }
+    // REQUIRE_SINGLE_REACTION: some reaction (:864-880)
+    if (w.cfg.require_single_reaction != 0) {
+      bool any = false;
+      for (int i = 0; i < (int)w.react.size(); i++) any = any || o.cur_react[i] > 0;
+      if (!any) return false;
+    }
     double base = (double)calc_size_merit();
     double bonus = o.cur_bonus;
     if (w.cfg.merit_default_bonus != 0.0) bonus = w.cfg.merit_default_bonus;
@@ -986,7 +1008,9 @@ struct Exec {
     const bool muts = mode != AVGPU_MODE_TEST;
     // TestCopy*: no draw when the rate is 0 (main/cMutationRates.h:111-120)
     Stream& r = rng();
-    if (muts && w.p_copy_mut.th && r.p(w.p_copy_mut)) {
+    // checkNoMutList (cpu/cHardwareCPU.cc:797-810, :7144): the draw always,
+    // the mutation (and its GetRandomInst draw) only for an unlisted instruction
+    if (muts && w.p_copy_mut.th && r.p(w.p_copy_mut) && !w.is.no_mut(read_inst)) {
       read_inst = w.is.random_inst(r);
       o.flg[wh] |= F_MUTATED | F_COPYMUT;
     }
@@ -1018,13 +1042,15 @@ struct Exec {
     if (muts && w.p_copy_ins.th && r.p(w.p_copy_ins)) insert_at(wh, w.is.random_inst(r));
     if (muts && w.p_copy_del.th && r.p(w.p_copy_del)) remove_at(wh);
     if (muts && w.p_copy_uni.th && r.p(w.p_copy_uni)) {
-      // doUniformCopyMutation (cpu/cHardwareBase.cc:597-612; NO_MUT_INSTS empty):
-      // op codes, not weighted
+      // doUniformCopyMutation (cpu/cHardwareBase.cc:597-612): op codes, not
+      // weighted; nothing for a write-head instruction NO_MUT_INSTS lists
       const int n_ops = w.is.n;
       const int mut = (int)r.uint_below((uint32_t)(2 * n_ops + 1));
-      if (mut < n_ops) { if (wh < size()) o.mem[wh] = (uint8_t)mut; }   // SetInst: flags kept
-      else if (mut == n_ops) remove_at(wh);
-      else insert_at(wh, mut - n_ops - 1);
+      if (!(wh < size() && w.is.no_mut(o.mem[wh]))) {
+        if (mut < n_ops) { if (wh < size()) o.mem[wh] = (uint8_t)mut; }   // SetInst: flags kept
+        else if (mut == n_ops) remove_at(wh);
+        else insert_at(wh, mut - n_ops - 1);
+      }
     }
     // SLIP_COPY_MODE 0 (m_slip_read_head, cpu/cHardwareCPU.cc:785): the read
     // head jumps to GetInt(memory size) (:7157-7158); SLIP_COPY_MODE 1: a slip
@@ -1519,6 +1545,15 @@ int orc_load_instset(void* h, int n, const uint8_t* handler_id, const int32_t* r
     w.is.cum[i] = cum;
   }
   w.is.total = cum;
+  // NO_MUT_INSTS: op i's symbol (Instruction::GetSymbol, core/InstructionSequence.cc:
+  // 69-106), its first character
+  w.is.nomut = 0;
+  for (int i = 0; i < n; i++) {
+    const int k = i % 62;
+    const char sym = i >= 62 ? "+-~?"[std::min(i / 62, 4) - 1]
+                             : (char)(k < 26 ? 'a' + k : (k < 52 ? 'A' + k - 26 : '0' + k - 52));
+    if (memchr(w.cfg.no_mut_insts, sym, (size_t)w.cfg.no_mut_insts_len)) w.is.nomut |= 1ull << i;
+  }
   return 0;
 }
 
@@ -1619,6 +1654,14 @@ int orc_load_env(void* h, int n, const avgpu_reaction* r) {
     x.add = bonus;
     w.react.push_back(x);
   }
+  // REQUIRED_TASK / IMMUNITY_TASK index the task library: the distinct tasks
+  // in the order of their first REACTION line (cTaskLib::AddTask)
+  std::vector<int> lib;
+  for (int i = 0; i < n; i++)
+    if (std::find(lib.begin(), lib.end(), r[i].task) == lib.end()) lib.push_back(r[i].task);
+  auto task_of = [&](int t) { return t >= 0 && t < (int)lib.size() ? lib[t] : -1; };
+  w.req_task = task_of(w.cfg.required_task);
+  w.imm_task = task_of(w.cfg.immunity_task);
   return 0;
 }
 

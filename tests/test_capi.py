@@ -78,8 +78,8 @@ REFUSED_C = [
     ("death_prob", "0.1"), ("age_deviation", "3"), ("divide_failure_resets", "1"),
     ("special_mut_line", "5"), ("population_cap", "100"), ("generation_inc_method", "0"),
     ("reset_inputs_on_divide", "1"), ("epigenetic_method", "1"), ("min_cycles", "10"),
-    ("required_task", "2"), ("immunity_task", "2"), ("required_reaction", "2"),
-    ("immunity_reaction", "2"), ("require_single_reaction", "1"), ("max_unique_task_count", "3"),
+    ("required_task", "16"), ("immunity_task", "16"), ("required_reaction", "12"),
+    ("immunity_reaction", "12"),
     ("require_exact_copy", "1"), ("fitness_method", "1"), ("juv_period", "5"),
     ("no_mut_insts_len", "1"), ("test_fitness_measures", "1"),
     ("divide_method", "0"), ("world_geometry", "3"), ("slicing_method", "3"),
@@ -127,8 +127,11 @@ def test_python_config_reaches_the_refusal(golden, tmp_path):
         assert key.split("_")[0] in lib.avgpu_last_error().decode().upper()
     c = capi.cfg_from_avida(files.read_avida_cfg(None, {"STERILIZE_UNSTABLE": 1}))
     assert c.test_fitness_measures == 1 and lib.avgpu_check_cfg(C.byref(c)) == -5
+    # NO_MUT_INSTS runs (tests/test_no_mut.py); a length that is not its string's is refused
     c = capi.cfg_from_avida(files.read_avida_cfg(None, {"NO_MUT_INSTS": "abc"}))
-    assert c.no_mut_insts_len == 3 and lib.avgpu_check_cfg(C.byref(c)) == -5
+    assert c.no_mut_insts_len == 3 and c.no_mut_insts == b"abc" and lib.avgpu_check_cfg(C.byref(c)) == 0
+    c.no_mut_insts_len = 4
+    assert lib.avgpu_check_cfg(C.byref(c)) == -5
     # SLIP_COPY_MODE 1 (memory slips) runs with fill modes 0 / 2 / 4; 3 and 1 are refused
     for fill, rc in ((0, 0), (2, 0), (4, 0), (3, -5), (1, -5)):
         c = capi.cfg_from_avida(files.read_avida_cfg(None, {"COPY_SLIP_PROB": 0.01, "SLIP_COPY_MODE": 1,

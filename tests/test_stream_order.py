@@ -3,15 +3,18 @@ API call makes runs on the world's own (non-blocking) stream and is complete
 on return (capi.hip COPY_SYNC / SET_SYNC), so calls issued right behind
 updates that are still queued -- avgpu_run_update(w, NULL) returns before its
 kernels finish -- see the world those updates leave, and the next update sees
-what the call wrote.  The same sequence on the oracle (synchronous by
+what the call wrote: avgpu_kill, avgpu_get_resources / avgpu_set_resources,
+avgpu_test_genomes, avgpu_set_rng_mode (recorded, then counter streams) and
+avgpu_set_serial_streams, each right behind queued updates.  The same sequence on the oracle (synchronous by
 construction) is the expected result, bit for bit: organisms, resources and
 the test CPU's results."""
 import ctypes as C
 import os
 
+import numpy as np
 import pytest
 
-from avida_amd import files
+from avida_amd import capi, files
 import test_checkpoint as tc
 
 
@@ -40,6 +43,20 @@ def _sequence(b, golden):
     _queue(b, 2)
     anc = files.read_org(os.path.join(golden, "default-heads.org"), b.instset)
     tests = b.test_genomes([anc, anc[:40] + anc[41:]])   # the test CPU's own world, its tables copied
+    _queue(b, 2)
+    # per-organism recorded streams set right behind queued updates, then back
+    # to the counter streams
+    rnd = np.random.default_rng(5).random(40000)
+    b.set_rng_mode(capi.RNG_RECORDED, rnd, np.arange(b.ncells, dtype=np.int64) * 37)
+    _queue(b, 2)
+    b.set_rng_mode(capi.RNG_COUNTER)
+    _queue(b, 1)
+    # the serial world's two recorded streams, set behind a queued update
+    b._sched = np.ascontiguousarray(np.random.default_rng(6).random(60000))
+    b._ctx = np.ascontiguousarray(np.random.default_rng(7).random(60000))
+    b._call("set_serial_streams", b.h, b._sched.ctypes.data_as(C.c_void_p), len(b._sched),
+            b._ctx.ctypes.data_as(C.c_void_p), len(b._ctx))
+    b.run_serial_update()
     _queue(b, 2)
     st = b.run_update()
     return tests, st

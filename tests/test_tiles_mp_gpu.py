@@ -24,10 +24,10 @@ import tile_util as tu
 
 pytestmark = pytest.mark.gpu
 CAP = 512
-X, Y, U = 64, 64, 30
+X, U = 64, 30
 
 
-def _env(golden, env_kind):
+def _env(golden, env_kind, Y):
     if env_kind == "bench":              # configs[4]'s environment (bench.py --env resources)
         import bench
         from avida_amd import files
@@ -51,13 +51,13 @@ class _Counting:
         return fn
 
 
-def _rank_main(rank, world_size, golden, port, out_dir, env_kind):
+def _rank_main(rank, world_size, golden, port, out_dir, env_kind, Y):
     import torch.distributed as dist
     from avida_amd import tiles
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", rank=rank, world_size=world_size)
-    b, t = tu.make_tile("gpu", golden, X, Y, world_size, rank, device="cuda", env=_env(golden, env_kind))
+    b, t = tu.make_tile("gpu", golden, X, Y, world_size, rank, device="cuda", env=_env(golden, env_kind, Y))
     tr = _Counting(tiles.StagedTransport(dist))
     sw = tiles.StripWorld([t], tr)
     sent = births = steps = 0
@@ -79,16 +79,16 @@ def _rank_main(rank, world_size, golden, port, out_dir, env_kind):
 
 
 @pytest.mark.timeout(600)
-@pytest.mark.parametrize("env_kind,T", [(None, 2), ("bench", 2), (None, 4)])
-def test_gpu_strips_processes_equal_untiled_oracle(golden, tmp_path, env_kind, T):
+@pytest.mark.parametrize("env_kind,T,Y", [(None, 2, 64), ("bench", 2, 64), (None, 4, 128), ("bench", 4, 128)])
+def test_gpu_strips_processes_equal_untiled_oracle(golden, tmp_path, env_kind, T, Y):
     import torch.multiprocessing as mp
     from avida_amd import capi
     import parity_util as pu
     with socket.socket() as sk:
         sk.bind(("127.0.0.1", 0))
         port = sk.getsockname()[1]
-    mp.spawn(_rank_main, args=(T, golden, port, str(tmp_path), env_kind), nprocs=T, join=True)
-    ref, _ = tu.single("oracle", golden, X, Y, U, env=_env(golden, env_kind))
+    mp.spawn(_rank_main, args=(T, golden, port, str(tmp_path), env_kind, Y), nprocs=T, join=True)
+    ref, _ = tu.single("oracle", golden, X, Y, U, env=_env(golden, env_kind, Y))
     a, oa, fa = ref.states(0, X * Y, CAP)
     per = X * Y // T
     if env_kind:

@@ -18,9 +18,9 @@ for C in "FETCH_SIZE" "WRITE_SIZE GRBM_COUNT GRBM_GUI_ACTIVE" \
     python bench.py --steps 5 --warmup 2 --no-cpu --long-updates 0 > gpurun_out/pmc_${TAG}_$P.log 2>&1 || { echo "pass $P failed"; exit 1; }
   P=$((P + 1))
 done
-python tools/pmc_summary.py "gpurun_out/pmc_${TAG}_*/**/*counter_collection.csv" \
+python tools/pmc_summary.py "gpurun_out/pmc_${TAG}_*/**/*counter_collection.csv" --last 7 \
   --json gpurun_out/pmc_k_interpret320.json --world 1024x1024 \
-  --source "profiles/${TAG}_pmc_k_interpret320.txt (rocprofv3 --pmc, 5 passes over bench.py --steps 5 --warmup 2 --no-cpu after 150 burn-in updates; average over the class-0 dispatches)" \
+  --source "profiles/${TAG}_pmc_k_interpret320.txt (rocprofv3 --pmc, 5 passes over bench.py --steps 5 --warmup 2 --no-cpu after 150 burn-in updates; average over each pass's last 7 class-0 main-pass dispatches: the warmup and timed updates)" \
   > gpurun_out/${TAG}_pmc_k_interpret320.txt
-python tools/pmc_summary.py "gpurun_out/pmc_${TAG}_*/**/*counter_collection.csv" 'k_interpret<(316|320),[^(]*true>\(' \
+python tools/pmc_summary.py "gpurun_out/pmc_${TAG}_*/**/*counter_collection.csv" 'k_interpret<(316|320),[^(]*true>\(' --last 7 \
   > gpurun_out/${TAG}_pmc_k_interpret320_newborn.txt

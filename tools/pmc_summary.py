@@ -20,14 +20,22 @@ MAIN = r"k_interpret<(316|320),[^(]*false>\("
 NB_REGEX = r"k_interpret<(316|320),[^(]*true>\("
 
 
-def summarize(pattern, regex=MAIN):
+def summarize(pattern, regex=MAIN, last=0):
+    """per counter, the average over the matching dispatches (last > 0: each
+    file's last `last` of them by dispatch id -- the bench's warmup and timed
+    updates, not the burn-in, whose lock-step first updates take more batch
+    steps of fewer instructions each)"""
     vals = defaultdict(list)
     for f in sorted(glob.glob(pattern, recursive=True)):
+        per = defaultdict(list)
         with open(f) as fh:
             for row in csv.DictReader(fh):
                 if not re.search(regex, row.get("Kernel_Name", "")):
                     continue
-                vals[row["Counter_Name"]].append(float(row["Counter_Value"]))
+                per[row["Counter_Name"]].append((int(row["Dispatch_Id"]), float(row["Counter_Value"])))
+        for k, v in per.items():
+            v.sort()
+            vals[k].extend(x for _, x in (v[-last:] if last > 0 else v))
     return {k: sum(v) / len(v) for k, v in vals.items()}, {k: len(v) for k, v in vals.items()}
 
 
@@ -38,8 +46,9 @@ if __name__ == "__main__":
     ap.add_argument("--json")
     ap.add_argument("--world", default="1024x1024")
     ap.add_argument("--source", default="")
+    ap.add_argument("--last", type=int, default=0, help="each file's last N matching dispatches only")
     a = ap.parse_args()
-    avg, n = summarize(a.pattern, a.regex)
+    avg, n = summarize(a.pattern, a.regex, a.last)
     for k in sorted(avg):
         print("%-28s %18.1f  (n=%d)" % (k, avg[k], n[k]))
     if a.json:

@@ -8,7 +8,11 @@ One GPU runs the T strips one after another on one stream, so
   strip overhead          t_T - t_1 / T  (the strip's extra launches + copies)
 
 and an update on T GPUs (one strip each) is predicted as t_T + the RCCL
-exchange latencies the loopback copies stand for.
+exchange latencies the loopback copies stand for: an explicit term of
+(dependent collective rounds per update, counted here) x (latency of one
+small RCCL round over xGMI, AVGPU_RCCL_ROUND_US, default 20 us -- an assumed
+figure: RCCL refuses two ranks on this pool's one GPU, so it is not measured
+here) + the halo bytes at one xGMI link's ~50 GB/s.
 usage (GPU box): python tools/strip_timing.py X Y T [burn_in] [K]   -> one JSON line"""
 import ctypes as C
 import json
@@ -62,15 +66,41 @@ def main():
         sl = slice(k * rows * X, (k + 1) * rows * X)
         _seed(b, 0, idx[sl], gen, glen, gmer)
         strips.append((b, t))
-    world = tiles.StripWorld([t for _, t in strips], tiles.LoopbackTransport())
+    class Counting(tiles.LoopbackTransport):
+        """the loopback transport, counting the collective rounds"""
+        rounds = 0
+
+        def all_gather(self, tiles_):
+            Counting.rounds += 1
+            return super().all_gather(tiles_)
+
+        def exchange(self, tiles_, kind):
+            Counting.rounds += 1
+            return super().exchange(tiles_, kind)
+
+        def exchange_start(self, tiles_, kind):
+            Counting.rounds += 1
+            return super().exchange_start(tiles_, kind)
+
+        def all_reduce_sum(self, tiles_):
+            Counting.rounds += 1
+            return super().all_reduce_sum(tiles_)
+
+    world = tiles.StripWorld([t for _, t in strips], Counting())
     for _ in range(B):
         world.update()
     torch.cuda.synchronize()
+    Counting.rounds = 0
     t0 = time.perf_counter()
     for _ in range(K):
         world.update()
     torch.cuda.synchronize()
     tT = (time.perf_counter() - t0) / K
+    rounds = Counting.rounds / K
+    rccl_us = float(os.environ.get("AVGPU_RCCL_ROUND_US", "20"))
+    t0_ = strips[0][1]
+    halo_bytes = 2 * (t0_.halo_send[0].numel() + t0_.rec_send[0].numel())
+    comm_ms = rounds * rccl_us * 1e-3 + halo_bytes / 50e9 * 1e3
     import numpy as np
     d_strips = np.concatenate([b.digests() for b, _ in strips])
     out.update({
@@ -79,7 +109,10 @@ def main():
         "per_strip_ms": round(tT * 1e3 / T, 4),
         "ideal_per_strip_ms": round(t1 * 1e3 / T, 4),
         "strip_overhead_ms": round((tT - t1) * 1e3 / T, 4),
-        "halo_exchanges_per_update": 5, "all_gathers_per_update": 1, "record_exchanges_per_update": 1,
+        "collective_rounds_per_update": rounds,
+        "assumed_rccl_round_us": rccl_us,
+        "predicted_ms_per_update_on_T_gpus": round(tT * 1e3 / T + comm_ms, 4),
+        "predicted_weak_scaling_efficiency": round((t1 * 1e3 / T) / (tT * 1e3 / T + comm_ms), 3),
         "strips_equal_untiled": bool((d_full == d_strips).all()),
     })
     print(json.dumps(out))

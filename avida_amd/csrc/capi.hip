@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -95,12 +96,12 @@ struct avgpu_world {
   int ntiles_last = 0;
   bool tile_buffers = false;
   // batch steps: the last update's predictor and organisms
-  // (mapped host memory the update's last step writes, ev_pred after it), the
+  // (coherent mapped host memory the update's last step writes, then pred_seq), the
   // host's copy, the steps the last update ran; strips: the current step
   long long* h_pred = nullptr;
   long long* d_pred = nullptr;   // its device address
-  hipEvent_t ev_pred = nullptr;
   bool pred_pending = false;
+  long long pred_seq = 0;       // the sequence number k_place_claim0 publishes with the predictor
   bool reaper_rebuild = false;  // the serial reaper queue is built again at the next serial update
   long long pred_acc = 0, pred_n = 0, pred_cnt = 0;
   int last_k = 1;
@@ -276,6 +277,11 @@ int setup_world(avgpu_world* w, int64_t n, bool test_buffers) {
   // interpreter slow-op batching (interp.hip); AVGPU_SLOW_BATCH overrides (tuning)
   W.slow_batch = 12;
   if (const char* e = getenv("AVGPU_SLOW_BATCH")) W.slow_batch = std::max(1, std::min(64, atoi(e)));
+  // the newborn pass's own: 1 -- its duration is its longest newborn's, and a
+  // parked lane waiting for a batch lengthens exactly that path (1.344 ->
+  // 1.323 ms per update, profiles/r06g_ab_nbsb.txt)
+  W.nb_slow_batch = 1;
+  if (const char* e = getenv("AVGPU_NB_SLOW_BATCH")) W.nb_slow_batch = std::max(1, std::min(64, atoi(e)));
   W.row0 = 0;
   W.global_rows = c.world_y;
   W.rows = c.world_y;
@@ -387,12 +393,12 @@ avgpu_world* create_world(const avgpu_cfg* cfg, int device, int64_t n, bool test
       hipEventCreateWithFlags(&w->ev_join[1], hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&w->ev_join[2], hipEventDisableTiming) != hipSuccess ||
       hipEventCreate(&w->ev0) != hipSuccess || hipEventCreate(&w->ev1) != hipSuccess ||
-      hipEventCreateWithFlags(&w->ev_pred, hipEventDisableTiming) != hipSuccess ||
-      hipHostMalloc((void**)&w->h_pred, 3 * sizeof(long long), hipHostMallocMapped) != hipSuccess ||
+      hipHostMalloc((void**)&w->h_pred, 4 * sizeof(long long), hipHostMallocMapped | hipHostMallocCoherent) !=
+          hipSuccess ||
       hipHostGetDevicePointer((void**)&w->d_pred, w->h_pred, 0) != hipSuccess) {
     delete w; fail(AVGPU_EHIP, "stream/event creation failed"); return nullptr;
   }
-  w->h_pred[0] = w->h_pred[1] = w->h_pred[2] = 0;
+  w->h_pred[0] = w->h_pred[1] = w->h_pred[2] = w->h_pred[3] = 0;
   w->stream = w->own_stream;
   for (int i = 0; i < avgpu_world::RING; i++) {
     for (int k = 0; k <= NUM_CLASSES; k++)
@@ -680,7 +686,6 @@ int avgpu_destroy(avgpu_world* w) {
     if (w->ev_join[k]) hipEventDestroy(w->ev_join[k]);
   }
   if (w->ev_fork) hipEventDestroy(w->ev_fork);
-  if (w->ev_pred) hipEventDestroy(w->ev_pred);
   if (w->h_pred) hipHostFree(w->h_pred);
   delete w;
   return 0;
@@ -975,10 +980,21 @@ int avgpu_run_update(avgpu_world* w, avgpu_update_stats* out) {
   // the host waits for it (here, at the next update) while the GPU runs the
   // rest of that update.
   if (w->pred_pending) {
-    HIPCHK(hipEventSynchronize(w->ev_pred));
-    w->pred_acc = w->h_pred[0];
-    w->pred_n = w->h_pred[1];
-    w->pred_cnt = w->h_pred[2];
+    // the last step's placement launch published the predictor into
+    // coherent mapped memory, then its sequence number (k_place_claim0): the
+    // host polls that instead of an event on the stream (an event record
+    // there left ~6 us of dead time per update before the next launch)
+    const auto t0 = std::chrono::steady_clock::now();
+    while (__atomic_load_n(w->h_pred + 3, __ATOMIC_ACQUIRE) != w->pred_seq) {
+      if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) {
+        HIPCHK(hipStreamSynchronize(w->stream));   // a fault surfaces here
+        if (__atomic_load_n(w->h_pred + 3, __ATOMIC_ACQUIRE) != w->pred_seq)
+          return fail(AVGPU_EHIP, "the batch-step predictor was never published");
+      }
+    }
+    w->pred_acc = __atomic_load_n(w->h_pred + 0, __ATOMIC_ACQUIRE);
+    w->pred_n = __atomic_load_n(w->h_pred + 1, __ATOMIC_ACQUIRE);
+    w->pred_cnt = __atomic_load_n(w->h_pred + 2, __ATOMIC_ACQUIRE);
     w->pred_pending = false;
   }
   const int K = choose_k(w->cfg, w->pred_acc, w->pred_n, false, w->pred_cnt);
@@ -990,7 +1006,8 @@ int avgpu_run_update(avgpu_world* w, avgpu_update_stats* out) {
     rc = interpret(w, AVGPU_MODE_WORLD, 0, w->W.n, true);
     if (rc < 0) return rc;
     const bool last = sub == K - 1;
-    launch_world_post(w->W, w->stream, key, sub, K, last ? w->d_pred : nullptr, last ? w->ev_pred : nullptr);
+    if (last) w->pred_seq++;
+    launch_world_post(w->W, w->stream, key, sub, K, last ? w->d_pred : nullptr, w->pred_seq);
     launch_newborns(w->W, w->d_W, w->stream);
     // statistics only when asked for: a run without them (out == NULL) leaves
     // the reduction to avgpu_get_stats / avgpu_stats_vector, or skips it

@@ -206,6 +206,7 @@ struct DevWorld {
   int32_t rand_total;
   uint8_t* rand_lut;  // [256] draw -> canonical code when rand_total <= 256
   int32_t slow_batch;   // parked lanes that trigger the interpreter's slow phase (1..64)
+  int32_t nb_slow_batch;  // the same in the newborn pass
   int n_react;
   // reactions, RT_STRIDE words each: task, process type, requisite min / max
   // count, has-requisite, in-use, bonus multiplier (f64), bonus addend (f64)
@@ -784,10 +785,10 @@ bool res_stepped(const DevWorld& W);   // launch_resources_begin wrote res_amoun
 void launch_resources_settle(const DevWorld& W, hipStream_t s, const unsigned long long* sum);
 // placement and activation of batch step `sub` of `nsub` (key: its scheduler
 // key), the newborns listed for the newborn pass; then launch_world_end
-// pred_out (mapped host memory, the update's last step): the predictor and
-// its organisms, ev_pred recorded after them
+// pred_out (coherent mapped host memory, the update's last step): the
+// predictor, its organisms and divide count, then pred_seq at system scope
 void launch_world_post(const DevWorld& W, hipStream_t s, uint32_t key, int sub, int nsub,
-                       long long* pred_out = nullptr, hipEvent_t ev_pred = nullptr);
+                       long long* pred_out = nullptr, long long pred_seq = 0);
 void launch_world_end(const DevWorld& W, hipStream_t s, double* d_stats, bool eager);
 // the newborn pass of a batch step (interp.hip): the organisms k_activate listed
 void launch_newborns(const DevWorld& W, const DevWorld* dW, hipStream_t s);

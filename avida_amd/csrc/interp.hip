@@ -646,7 +646,7 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
     ttab = reinterpret_cast<const uint32_t*>(W.task_tab)[lane];
   }
   const uint32_t* T32 = reinterpret_cast<const uint32_t*>(T);
-  const int slow_batch = W.slow_batch;
+  const int slow_batch = NB ? W.nb_slow_batch : W.slow_batch;
   uint32_t rpq = 0u;        // configs[4]'s queued reward events (res_flush)
 
   while (true) {

@@ -1265,7 +1265,7 @@ __global__ void k_place_round(DevWorld W, int m) {
 // its own birth time (a round-0 pick of an earlier birth landed there:
 // killt[parent] > 2^16 - t) is cancelled -- the reference would have killed
 // its parent before this divide; the others claim their round-0 targets.
-__global__ void k_place_claim0(DevWorld W, long long* pred_out) {
+__global__ void k_place_claim0(DevWorld W, long long* pred_out, long long pred_seq) {
   // the list rows are free after the main pass: the newborn pass's (k_activate)
   if (blockIdx.x == 0 && threadIdx.x < NUM_LISTS) W.class_count[threadIdx.x] = 0;
   // the update's last step: its predictor and organisms to the host (mapped
@@ -1274,6 +1274,9 @@ __global__ void k_place_claim0(DevWorld W, long long* pred_out) {
     pred_out[0] = W.sched[0];
     pred_out[1] = (long long)W.totals[1];
     pred_out[2] = W.sched[3];
+    // then its sequence number, after them at system scope: the host polls it
+    __threadfence_system();
+    __hip_atomic_store(pred_out + 3, pred_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
   QUEUE_LOOP(q) {
     const int64_t r = rec_of(W, q);
@@ -1498,11 +1501,13 @@ __device__ __forceinline__ void newborn_credit(const DevWorld& W, int64_t c, uin
   }
 }
 // one newborn in cell c: credit, budget, carry; returns its list row (-1: no slice)
+// (ran: W.ran[c], loaded by the caller ahead of the offspring's stores -- a
+// load behind them would wait for all of them)
 __device__ __forceinline__ int newborn_setup(const DevWorld& W, int64_t c, uint32_t t, double merit, int len,
                                              uint32_t key, long long uds, double total, long long& carry,
-                                             unsigned long long& wasted) {
+                                             unsigned long long& wasted, int ran) {
   if (W.env_resources) newborn_credit(W, c, t);
-  const long long left = (long long)__dmul_rn((double)W.ran[c], nb_frac(t));
+  const long long left = (long long)__dmul_rn((double)ran, nb_frac(t));
   const long long bud = newborn_budget(W, c, t, merit, key, uds, total);
   carry += bud - left;
   wasted += (unsigned long long)left;
@@ -1588,8 +1593,9 @@ __global__ __launch_bounds__(64) void k_activate(DevWorld W, int fused, uint32_t
       if (tgt >= W.n) break;                   // sent to the neighbouring tile
       born++;
       b.hs = 0;                                // it runs its share of this step instead (newborn pass)
+      const int ran = W.ran[tgt];
       setup_child_lane<8>(W, tgt, b, W.b_genome + i * TAPE_SLOT, pre);
-      nrow = newborn_setup(W, tgt, t, b.merit, b.len, key, uds, total, carry, wasted);
+      nrow = newborn_setup(W, tgt, t, b.merit, b.len, key, uds, total, carry, wasted, ran);
       ncell_nb = tgt;
     } while (0);
     nbs += nrow >= 0 ? 1ull : 0ull;
@@ -1721,9 +1727,10 @@ __global__ __launch_bounds__(64) void k_activate_remote(DevWorld W, uint32_t key
     b.hs = 0;                                  // it runs its share of this step (newborn pass)
     b.merit = r.merit; b.fitness = r.fitness; b.lo = r.rng_lo; b.hi = r.rng_hi; b.ctr = r.rng_ctr;
     b.ltask = recs[q].last_task; b.lstride = 1;
+    const int ran = W.ran[c];
     setup_child<64>(W, c, b, reinterpret_cast<const uint32_t*>(arena + r.off), lane);
     if (lane == 0) {
-      const int row = newborn_setup(W, c, r.t, r.merit, r.len, key, uds, total, carry, wasted);
+      const int row = newborn_setup(W, c, r.t, r.merit, r.len, key, uds, total, carry, wasted, ran);
       if (row >= 0) {
         nbs++;
         const int slot = atomicAdd(&W.class_count[row], 1);
@@ -2065,7 +2072,7 @@ void launch_reset_counts(const DevWorld& W, hipStream_t s) {
 // claims into array k & 1 after zeroing its records' round k-1 claims; the
 // last round's are zeroed by k_activate): no clearing launch per round.
 void launch_world_post(const DevWorld& W, hipStream_t s, uint32_t key, int sub, int nsub, long long* pred_out,
-                       hipEvent_t ev_pred) {
+                       long long pred_seq) {
   // the occupancy was initialised by k_allot_total; the divide mutations
   // ride in round 0's pick launch
   // round 0's pick (with the divide mutations beside it), then three launches
@@ -2090,8 +2097,7 @@ void launch_world_post(const DevWorld& W, hipStream_t s, uint32_t key, int sub, 
 #else
   hipLaunchKernelGGL(k_place_pick_mut, dim3(nbk), dim3(256), 0, s, W, (int)bb, pf, 0, nbk);
 #endif
-  hipLaunchKernelGGL(k_place_claim0, dim3(bb), dim3(256), 0, s, W, pred_out);
-  if (pred_out && ev_pred) hipEventRecord(ev_pred, s);
+  hipLaunchKernelGGL(k_place_claim0, dim3(bb), dim3(256), 0, s, W, pred_out, pred_seq);
   for (int m = 1; m < 4; m++) {
     if (soup) soup_cells(m);
     hipLaunchKernelGGL(k_place_round, dim3(bb), dim3(256), 0, s, W, m);

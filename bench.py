@@ -255,8 +255,9 @@ def main():
                     help="untimed updates that age the seeded population before the warmup "
                          "(its organisms start in lock step; ~10 gestations spread them out)")
     ap.add_argument("--seed", type=int, default=101)
-    ap.add_argument("--time-every", type=int, default=1,
-                    help="bracket every k-th update's class-0 launch with HIP events (roofline timing)")
+    ap.add_argument("--time-every", type=int, default=4,
+                    help="bracket every k-th update's class-0 launch with HIP events (roofline timing; "
+                         "each event record leaves a few us of dead time on the stream)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--env", choices=["logic9", "resources"], default="logic9",

@@ -164,6 +164,7 @@ class AvgpuUpdateStats(C.Structure):
         ("lane_steps", C.c_int64), ("births_overwritten", C.c_int64), ("births_cancelled", C.c_int64),
         ("seed", C.c_uint64), ("sched_pred", C.c_int64), ("sched_pred_n", C.c_int64), ("sub_steps", C.c_int64),
         ("sched_carry", C.c_int64), ("insts_wasted", C.c_int64), ("sched_pred_cnt", C.c_int64),
+        ("sched_pred_bins", C.c_int64 * 4),
     ]
 
 

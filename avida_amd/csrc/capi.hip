@@ -187,7 +187,7 @@ int setup_world(avgpu_world* w, int64_t n, bool test_buffers) {
   // occupancy, owners and the four placement rounds' claims, each with the two
   // ghost rows a strip tile keeps after its n cells
   const int64_t ng = n + 2 * (int64_t)c.world_x;
-  A(occ, ng); A(claim, ng); A(claim2, ng); A(owner, ng); A(killt, n); A(sdone, n); A(ran, n); A(sched, 8);
+  A(occ, ng); A(claim, ng); A(claim2, ng); A(owner, ng); A(killt, n); A(sdone, n); A(ran, n); A(sched, 12); A(pacc, NSHARD * PACC_STRIDE);
   W.claim_r[0] = W.claim; W.claim_r[1] = W.claim2;
   A(claim_r[2], ng); A(claim_r[3], ng); A(b_tgt, 4 * R);
   if (c.birth_method == 4) {
@@ -219,7 +219,7 @@ int setup_world(avgpu_world* w, int64_t n, bool test_buffers) {
   while (W.tree_cap < nb) W.tree_cap <<= 1;
   if ((rc = w->alloc(&W.tree_scr, (size_t)(2 * W.tree_cap)))) return rc;
   if ((rc = w->alloc(&W.tree_cnt, (size_t)(2 * W.tree_cap)))) return rc;
-  if ((rc = w->alloc(&w->d_stats, (size_t)(41 + 24 * nb)))) return rc;
+  if ((rc = w->alloc(&w->d_stats, (size_t)(45 + 24 * nb)))) return rc;
 #undef A
   w->has_test_buffers = test_buffers;
   // config scalars
@@ -617,8 +617,9 @@ int update_run(avgpu_world* w, const double* dev_totals, avgpu_update_stats* out
 // when set; else the more of two rules over the last step's predictor: with E
 // its weight term in mean weights per organism (the total weight's expected
 // move within the update), ceil(E / 0.05) steps above E = 0.1; with D the
-// fraction of organisms it expects to divide within the update (a cohort in
-// lock step), ceil(D / 0.15) steps above D = 0.3; one step otherwise, at most
+// fraction of organisms it expects to divide within the densest quarter of
+// the update (a cohort in lock step; a steady state spreads its divides over
+// the four), ceil(D / 0.15) steps above D = 0.3; one step otherwise, at most
 // ADAPT_KMAX.
 constexpr int ADAPT_KMAX = 16;
 int choose_k(const avgpu_cfg& c, long long pred, long long n, bool handed_in, long long cnt) {
@@ -1216,7 +1217,7 @@ int avgpu_run_updates(avgpu_world* w, int n, avgpu_update_stats* last) {
 
 int avgpu_get_stats(avgpu_world* w, avgpu_update_stats* out) {
   if (!w || !out) return fail(AVGPU_EINVAL, "args");
-  double v[41];
+  double v[45];
   if (w->stats_stale) {
     launch_stats(w->W, w->stream, w->d_stats);
     HIPCHK(hipGetLastError());
@@ -1252,6 +1253,7 @@ int avgpu_get_stats(avgpu_world* w, avgpu_update_stats* out) {
   memcpy(&out->sched_carry, v + 38, 8);
   out->sched_pred_n = (int64_t)v[39];
   memcpy(&out->sched_pred_cnt, v + 40, 8);
+  for (int q = 0; q < 4; q++) memcpy(&out->sched_pred_bins[q], v + 41 + q, 8);
   out->sub_steps = w->last_k;
   return 0;
 }
@@ -1433,10 +1435,17 @@ int avgpu_set_clock(avgpu_world* w, const avgpu_update_stats* last) {
   // the batch-step predictor and the pick carry
   w->pred_acc = last->sched_pred;
   w->pred_n = last->sched_pred_n;
-  w->pred_cnt = last->sched_pred_cnt;
+  w->pred_cnt = std::max(std::max(last->sched_pred_bins[0], last->sched_pred_bins[1]),
+                          std::max(last->sched_pred_bins[2], last->sched_pred_bins[3]));
   w->pred_pending = false;
-  const long long sv[4] = {last->sched_pred, 0, last->sched_carry, last->sched_pred_cnt};
+  const long long sv[5] = {0, 0, last->sched_carry, 0, 0};
   HIPCHK(hipMemcpyAsync(w->W.sched, sv, sizeof(sv), hipMemcpyHostToDevice, w->stream));
+  // the predictor into shard 0 (device.h pacc_sum), the other shards zero
+  std::vector<long long> pa(NSHARD * PACC_STRIDE, 0);
+  pa[0] = last->sched_pred;
+  pa[1] = (long long)((uint64_t)last->sched_pred_bins[0] | ((uint64_t)last->sched_pred_bins[1] << 32));
+  pa[2] = (long long)((uint64_t)last->sched_pred_bins[2] | ((uint64_t)last->sched_pred_bins[3] << 32));
+  HIPCHK(hipMemcpyAsync(w->W.pacc, pa.data(), pa.size() * sizeof(long long), hipMemcpyHostToDevice, w->stream));
   const double nv = (double)last->sched_pred_n;
   HIPCHK(hipMemcpyAsync(w->d_totals + 1, &nv, sizeof(nv), hipMemcpyHostToDevice, w->stream));
   HIPCHK(hipStreamSynchronize(w->stream));
@@ -1815,22 +1824,26 @@ int avgpu_tile_steps(avgpu_world* w, const double* dev_gathered, int ntiles, int
   if (rc < 0) return rc;
   if (!dev_gathered || ntiles < 1 || !k_out) return fail(AVGPU_EINVAL, "gathered partials / k_out");
   const int64_t nb = (w->W.n + 255) / 256, stride = tile_part_stride(nb);
-  std::vector<double> tail((size_t)(3 * ntiles));
+  std::vector<double> tail((size_t)(6 * ntiles));
   for (int k = 0; k < ntiles; k++)
-    HIPCHK(hipMemcpyAsync(tail.data() + 3 * k, dev_gathered + k * stride + 2 * nb, 3 * sizeof(double),
+    HIPCHK(hipMemcpyAsync(tail.data() + 6 * k, dev_gathered + k * stride + 2 * nb, 6 * sizeof(double),
                           hipMemcpyDeviceToHost, w->stream));
   double n = 0.0;
   HIPCHK(hipMemcpyAsync(&n, w->d_totals + 1, sizeof(double), hipMemcpyDeviceToHost, w->stream));
   HIPCHK(hipStreamSynchronize(w->stream));
-  long long sum = 0, cnt = 0;
+  long long sum = 0, bins[4] = {0, 0, 0, 0};
   for (int k = 0; k < ntiles; k++) {
-    long long v, c;
-    memcpy(&v, tail.data() + 3 * k, 8);
-    memcpy(&c, tail.data() + 3 * k + 2, 8);
+    long long v;
+    memcpy(&v, tail.data() + 6 * k, 8);
     sum += v;
-    cnt += c;
+    for (int q = 0; q < 4; q++) {
+      long long c;
+      memcpy(&c, tail.data() + 6 * k + 2 + q, 8);
+      bins[q] += c;
+    }
   }
-  *k_out = choose_k(w->cfg, sum, (long long)n, false, cnt);
+  const long long dens = std::max(std::max(bins[0], bins[1]), std::max(bins[2], bins[3]));
+  *k_out = choose_k(w->cfg, sum, (long long)n, false, dens);
   return 0;
 }
 

@@ -332,20 +332,23 @@ struct DevWorld {
   // the batch step's newborns and sub-steps:
   int32_t* ran;       // [n] instructions each cell's organism ran in this step's main pass (k_allot zeroes)
   double* cons;       // [n_res][n] its depletable consumption in that pass (k_allot zeroes; env_resources)
-  // [0] the sub-step predictor of this step's main pass (2^-20 mean weights,
-  // k_block_counts zeroes it), [1] this step's pick carry (newborn picks beyond
+  // [1] this step's pick carry (newborn picks beyond
   // their victims' leftovers, k_activate), [2] the carry not yet taken (taken
-  // at an update's first step), [3] the organisms of this step's main pass
-  // expected to divide within the next update (zeroed with [0]), [4] the
-  // update's UD (AVE_TIME_SLICE x the organisms at its first step)
+  // at an update's first step), [4] the update's UD (AVE_TIME_SLICE x the
+  // organisms at its first step)
   long long* sched;
+  // the sub-step predictor of this step's main pass, sharded by block like
+  // the counters (k_block_counts zeroes it): shard s at pacc[s * PACC_STRIDE]
+  // holds [0] its weight term (2^-20 mean weights), [1] its divide counts of
+  // quarters 0 | 1 << 32, [2] of quarters 2 | 3 << 32 (pacc_sum)
+  long long* pacc;
   const double* totals;   // the step's totals (k_block_counts): [1] organisms, [2] weight total, [3] UD
 };
 
 // a strip's partials vector (avgpu_tile_partials): nb block partials, nb alive
 // counts, its sub-step predictor, its pick carry and its predictor's divide
-// count (int64 bits)
-__host__ __device__ inline int64_t tile_part_stride(int64_t nb) { return 2 * nb + 3; }
+// counts by quarter (int64 bits)
+__host__ __device__ inline int64_t tile_part_stride(int64_t nb) { return 2 * nb + 6; }
 // owner of a cell won by a neighbouring strip's offspring in round k at birth time t
 #define REMOTE_OWNER(k, t) (-2 - ((k) + 4 * (int)(t)))
 // halo buffer: per round parity X u64 claims on the receiver's edge row and X
@@ -423,6 +426,21 @@ enum { SEG_OSLIP = 0, SEG_PSLIP, SEG_SSLIP, SEG_TTRANS, SEG_PTRANS, SEG_STRANS, 
 #define CNT_STRIDE 64
 #define CNT_CUM_BASE (NSHARD * CNT_STRIDE)
 #define CNT_WORDS (NSHARD * CNT_STRIDE + CNT_STRIDE)
+#define PACC_STRIDE 8
+// the predictor's word k summed over the shards (a packed pair of 32-bit
+// counts sums without carries for worlds below 2^32 organisms)
+__device__ __forceinline__ long long pacc_sum(const DevWorld& W, int k) {
+  long long s = 0;
+  for (int sh = 0; sh < NSHARD; sh++) s += W.pacc[sh * PACC_STRIDE + k];
+  return s;
+}
+// quarter k's divide count
+__device__ __forceinline__ long long quarter_count(const DevWorld& W, int k) {
+  return (long long)(((unsigned long long)pacc_sum(W, 1 + (k >> 1)) >> (32 * (k & 1))) & 0xFFFFFFFFull);
+}
+__device__ __forceinline__ long long densest_quarter(const DevWorld& W) {
+  return max(max(quarter_count(W, 0), quarter_count(W, 1)), max(quarter_count(W, 2), quarter_count(W, 3)));
+}
 #define CNT_CUM_INSTS (CNT_CUM_BASE + CNT_INSTS)
 #define CNT_CUM_BIRTHS (CNT_CUM_BASE + CNT_BIRTHS)
 // 1 once this update's counts are in the running sums (k_stats_final); 0 after

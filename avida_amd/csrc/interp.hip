@@ -224,11 +224,12 @@ __host__ __device__ constexpr int tape_stride(int S) { return S == CLASS0_SIZE ?
 // The adaptive sub-step predictor's term of one organism at the end of its
 // slice (oracle pred_term, the same IEEE operations): an
 // organism expected to divide within the next update's share of picks is
-// counted (imm) and moves the total weight by twice its merit's change at the
-// divide (its own and its offspring's, which replaces a relative of about its
-// old merit) from that point on, in mean weights, 2^-20 fixed point.
+// counted in the quarter of the update its divide is expected in (q, -1
+// none) and moves the total weight by twice its merit's change at the divide
+// (its own and its offspring's, which replaces a relative of about its old
+// merit) from that point on, in mean weights, 2^-20 fixed point.
 __device__ __forceinline__ long long pred_term(const DevWorld& W, int cell, int tu, int gs, int blen, int dcop,
-                                               int dexe, double bonus, bool& imm) {
+                                               int dexe, double bonus, int& q) {
   const double total = W.totals[2], n = W.totals[1];
   if (!(total > 0.0) || !(n > 0.0)) return 0;
   const double wbar = __ddiv_rn(total, n);
@@ -239,8 +240,8 @@ __device__ __forceinline__ long long pred_term(const DevWorld& W, int cell, int 
   const int G = gt > 0 ? gt : blen;
   const double r = (double)(G - (tu - gs));
   if (!(r <= __dmul_rn(e, 1.25))) return 0;
-  imm = true;
   const double t = r <= 0.0 ? 0.0 : fmin(__ddiv_rn(r, e), 1.0);
+  q = min(3, (int)__dmul_rn(t, 4.0));
   int sz = blen;
   if (sz > dcop) sz = dcop;
   if (sz > dexe) sz = dexe;
@@ -282,8 +283,8 @@ __device__ __forceinline__ int edit_word(int kind, int a, int b) { return kind |
 // class 0 takes its organisms from list row 0 (k_activate), and a viable
 // h-divide is not run -- its cycle is taken back and the slice ends before it.
 // pred: a world update's main pass, whose slices add their sub-step
-// predictor terms (pred_term) to W.sched[0] and count the organisms expected
-// to divide within the next update into W.sched[3].
+// predictor terms (pred_term) to W.pacc (its block's shard) and count the
+// organisms expected to divide within the next update by quarter there.
 template <int S, bool REC, bool C0W = false, bool SIMPLE = false, bool DEF = false, bool RES = false,
           bool MIX = false, bool NB = false>
 __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, int cls_arg, int mode_arg,
@@ -1977,13 +1978,19 @@ __device__ __forceinline__ int interpret_chunk(const DevWorld* __restrict__ Wp, 
   // step's main pass to its slice's end, alive, without a divide in it
   if (pred) {
     long long pt = 0;
-    bool imm = false;
+    int q = -1;
     if (active && !(fl & (F_DEAD | F_SPILL)) && alive0 && gs <= tu - executed - sdone)
-      pt = pred_term(W, cell, tu, gs, blen, dcop, dexe, bonus, imm);
+      pt = pred_term(W, cell, tu, gs, blen, dcop, dexe, bonus, q);
     for (int off = 32; off > 0; off >>= 1) pt += __shfl_xor(pt, off);
-    const unsigned long long ni = __popcll(__ballot(imm));
-    if (lane == 0 && pt) atomicAdd(reinterpret_cast<unsigned long long*>(W.sched), (unsigned long long)pt);
-    if (lane == 0 && ni) atomicAdd(reinterpret_cast<unsigned long long*>(W.sched + 3), ni);
+    unsigned long long* pa = reinterpret_cast<unsigned long long*>(W.pacc) + (blockIdx.x & (NSHARD - 1)) * PACC_STRIDE;
+    if (lane == 0 && pt) atomicAdd(pa, (unsigned long long)pt);
+    // the quarter counts, two per 64-bit word: two atomics per wave
+    const unsigned long long q01 = (unsigned long long)__popcll(__ballot(q == 0)) |
+                                   ((unsigned long long)__popcll(__ballot(q == 1)) << 32);
+    const unsigned long long q23 = (unsigned long long)__popcll(__ballot(q == 2)) |
+                                   ((unsigned long long)__popcll(__ballot(q == 3)) << 32);
+    if (lane == 0 && q01) atomicAdd(pa + 1, q01);
+    if (lane == 0 && q23) atomicAdd(pa + 2, q23);
   }
   // counters: one atomic per wave
   unsigned long long e = (unsigned long long)executed;

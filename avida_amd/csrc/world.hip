@@ -412,11 +412,13 @@ __global__ __launch_bounds__(256) void k_merit_partial(DevWorld W, double* parti
   if (reset == 1 && blockIdx.x == 0) reset_counts_block(W);
   if (reset == 2 && blockIdx.x == 0) reset_queues_block(W);
   // a strip's partials end with its last step's predictor, pick carry and
-  // divide count (the oracle's orc_tile_partials; summed on every strip after
-  // the gather)
-  if (alive_d && blockIdx.x == 0 && threadIdx.x < 3) {
+  // divide counts by quarter (the oracle's orc_tile_partials; summed on every
+  // strip after the gather)
+  if (alive_d && blockIdx.x == 0 && threadIdx.x < 6) {
     const int64_t nbl = (W.n + 255) / 256;
-    partial[2 * nbl + threadIdx.x] = __longlong_as_double(W.sched[threadIdx.x == 2 ? 3 : threadIdx.x]);
+    const long long v = threadIdx.x == 0 ? pacc_sum(W, 0)
+                        : (threadIdx.x == 1 ? W.sched[1] : quarter_count(W, (int)threadIdx.x - 2));
+    partial[2 * nbl + threadIdx.x] = __longlong_as_double(v);
   }
   const int lane = threadIdx.x & 63;
   const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -557,14 +559,13 @@ __global__ __launch_bounds__(1024) void k_block_counts(DevWorld W, const double*
       }
       W.sched[1] = 0;
       W.sched[2] = rem;
-      W.sched[0] = 0;                         // this step's predictor (interp.hip pred_term)
-      W.sched[3] = 0;
       count_add(W, CNT_STEPS, 1ull);
     }
     cnt[1] = nroot;
   }
   __syncthreads();
   if (mode == 3) return;
+  for (int i = tid; i < NSHARD * PACC_STRIDE; i += 1024) W.pacc[i] = 0;   // this step's predictor (interp.hip pred_term)
   // top down, only the nodes over this world's blocks [b0, b0 + nloc) (a
   // node's count depends on its ancestors' alone): a strip of T splits its
   // own subtree and the path to it, not the whole gathered world's tree
@@ -1271,9 +1272,9 @@ __global__ void k_place_claim0(DevWorld W, long long* pred_out, long long pred_s
   // the update's last step: its predictor and organisms to the host (mapped
   // memory), which chooses the next update's steps from them
   if (pred_out && blockIdx.x == 0 && threadIdx.x == 0) {
-    pred_out[0] = W.sched[0];
+    pred_out[0] = pacc_sum(W, 0);
     pred_out[1] = (long long)W.totals[1];
-    pred_out[2] = W.sched[3];
+    pred_out[2] = densest_quarter(W);
     // then its sequence number, after them at system scope: the host polls it
     __threadfence_system();
     __hip_atomic_store(pred_out + 3, pred_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -1752,7 +1753,7 @@ __global__ __launch_bounds__(64) void k_activate_remote(DevWorld W, uint32_t key
 // 6 generation 7 memory size 8..16 task organisms
 #define NPART 24
 #define NUSED (8 + AVGPU_NUM_LOGIC_TASKS)
-#define NSTAT 41
+#define NSTAT 45
 __device__ __forceinline__ double wave_sum(double v) {
   for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
   return v;
@@ -1880,10 +1881,11 @@ __global__ __launch_bounds__(256) void k_stats_final(DevWorld W, const double* p
     out[34] = (double)cs[0][CNT_OVERWRITTEN];
     out[35] = (double)cs[0][CNT_CANCELLED];
     out[36] = (double)cs[0][CNT_WASTED];
-    out[37] = __longlong_as_double(W.sched[0]);             // the predictor (bits)
+    out[37] = __longlong_as_double(pacc_sum(W, 0));         // the predictor (bits)
     out[38] = __longlong_as_double(W.sched[1] + W.sched[2]); // the pick carry (bits)
     out[39] = W.totals[1];                                  // the organisms it is relative to
-    out[40] = __longlong_as_double(W.sched[3]);             // the predictor's divide count (bits)
+    out[40] = __longlong_as_double(densest_quarter(W));
+    for (int q = 0; q < 4; q++) out[41 + q] = __longlong_as_double(quarter_count(W, q));   // (bits)
   }
 }
 

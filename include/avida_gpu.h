@@ -370,8 +370,9 @@ typedef struct avgpu_update_stats {
                                   avgpu_set_clock restores it */
   int64_t insts_wasted;        /* instructions the replaced organisms ran after their newborns' birth
                                   times (counted in insts_executed) */
-  int64_t sched_pred_cnt;      /* organisms the predictor expects to divide within the next update
-                                  (avgpu_set_clock restores it) */
+  int64_t sched_pred_cnt;      /* organisms the predictor expects to divide within the densest
+                                  quarter of the next update */
+  int64_t sched_pred_bins[4];  /* ... in each quarter (avgpu_set_clock restores them) */
 } avgpu_update_stats;
 
 typedef struct avgpu_world avgpu_world;   /* opaque handle */

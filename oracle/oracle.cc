@@ -322,7 +322,8 @@ struct World {
   // the adaptive sub-step predictor: the last batch step's sum
   // (2^-20 units) and the living organisms it was relative to; the batch
   // steps the last update ran
-  int64_t pred_acc = 0, pred_n = 0, pred_cnt = 0;
+  int64_t pred_acc = 0, pred_n = 0;
+  int64_t pred_bin[4] = {0, 0, 0, 0};   // the divide count by quarter of the update (pred_term)
   int64_t last_k = 1;
   // the picks the last batch step's newborns took beyond what the organisms
   // they replaced left (newborn_pass), taken from the next step's allotment;
@@ -1884,7 +1885,7 @@ int orc_set_clock(void* h, const avgpu_update_stats* last) {
   w.pred_n = last->sched_pred_n;
   w.carry_rem = last->sched_carry;
   w.carry_new = 0;
-  w.pred_cnt = last->sched_pred_cnt;
+  for (int k = 0; k < 4; k++) w.pred_bin[k] = last->sched_pred_bins[k];
   return 0;
 }
 
@@ -2097,11 +2098,20 @@ static inline uint32_t birth_time(int k, int budget) {
   return (uint32_t)(((double)k * 65536.0) / (double)((int64_t)budget + 1));
 }
 
+// the densest quarter's divide count (choose_k)
+static int64_t densest(const int64_t* bins) {
+  int64_t m = 0;
+  for (int k = 0; k < 4; k++) m = std::max(m, bins[k]);
+  return m;
+}
+
 // The adaptive sub-step predictor, one organism's term at the
 // end of its slice: an organism expected to reach its divide within the next
 // update's share of picks (its gestation time, or for one that never divided
 // its genome length, against the cycles of its current gestation) is counted
-// (the divide density), and it changes the scheduler's total weight by its
+// in the quarter of the update its divide is expected in (the divide
+// density: a cohort in lock step fills one quarter, a steady state spreads
+// over all four), and it changes the scheduler's total weight by its
 // merit's change at the divide (its size times its bonus so far, for one
 // that never divided; else its merit stays) and by as much again through its
 // offspring, which takes the merit to a neighbour's cell (a relative's, of
@@ -2111,7 +2121,7 @@ static inline uint32_t birth_time(int k, int budget) {
 // the mean weight, 2^-20 fixed point (an order-free sum).  Organisms that
 // divided in this slice are left out (their next divide is a gestation away).
 // The device's pred_term (interp.hip) is the same arithmetic.
-static int64_t pred_term(const World& w, const Org& o, double total, int64_t nalive, int64_t& cnt) {
+static int64_t pred_term(const World& w, const Org& o, double total, int64_t nalive, int64_t* bins) {
   const double wbar = total / (double)nalive;
   const double wi = o.merit;
   if (!(wi > 0.0) || !(wi <= 1.7976931348623157e308) || !(wbar > 0.0)) return 0;
@@ -2119,8 +2129,8 @@ static int64_t pred_term(const World& w, const Org& o, double total, int64_t nal
   const int G = o.gestation_time > 0 ? o.gestation_time : o.genome_length;
   const double r = (double)(G - (o.time_used - o.gestation_start));
   if (!(r <= e * 1.25)) return 0;
-  cnt++;
   const double t = r <= 0.0 ? 0.0 : std::fmin(r / e, 1.0);
+  bins[std::min(3, (int)(t * 4.0))]++;
   int sz = o.genome_length;
   if (sz > o.copied_size) sz = o.copied_size;
   if (sz > o.executed_size) sz = o.executed_size;
@@ -2162,7 +2172,7 @@ static void allot_interpret(World& w, const std::vector<int64_t>& blk, double to
   w.births.clear();
   for (auto& v : w.cons_cell) std::fill(v.begin(), v.end(), 0.0);
   w.pred_acc = 0;
-  w.pred_cnt = 0;
+  for (int k = 0; k < 4; k++) w.pred_bin[k] = 0;
   w.pred_n = nalive;
   w.ran.assign(w.ncells, 0);
   int64_t insts = 0, deaths = 0, divides = 0;
@@ -2181,7 +2191,7 @@ static void allot_interpret(World& w, const std::vector<int64_t>& blk, double to
     divides += o.num_divides - d0;
     if (!o.alive) deaths++;
     else if (budget[c] > 0 && o.gestation_start <= tu0 && total > 0.0 && nalive > 0)
-      w.pred_acc += pred_term(w, o, total, nalive, w.pred_cnt);
+      w.pred_acc += pred_term(w, o, total, nalive, w.pred_bin);
   }
   w.t_insts = insts; w.t_deaths = deaths; w.t_divides = divides;
 }
@@ -2280,7 +2290,8 @@ static void finish_stats(World& w, int64_t placed, int64_t dropped) {
   st.sched_pred_n = w.pred_n;
   st.sub_steps = w.last_k;
   st.sched_carry = w.carry_rem + w.carry_new;
-  st.sched_pred_cnt = w.pred_cnt;
+  st.sched_pred_cnt = densest(w.pred_bin);
+  for (int k = 0; k < 4; k++) st.sched_pred_bins[k] = w.pred_bin[k];
   st.insts_wasted = w.t_wasted;
   w.t_wasted = 0;
   w.t_overwritten = 0;
@@ -2527,8 +2538,9 @@ static int64_t take_carry(World& w, int64_t fresh, int64_t n_root, bool first) {
 // when set; else the more of two rules, each one step up to its threshold:
 // with E = |predictor| in mean weights per organism (the total weight's
 // expected move within the update), ceil(E / 0.05) steps above E = 0.1; with
-// D the fraction of organisms expected to divide within it (a cohort in lock
-// step), ceil(D / 0.15) steps above D = 0.3; at most ADAPT_KMAX
+// D the fraction of organisms expected to divide within its densest quarter
+// (a cohort in lock step), ceil(D / 0.15) steps above D = 0.3; at most
+// ADAPT_KMAX
 static constexpr int ADAPT_KMAX = 16;
 static int choose_k(const avgpu_cfg& c, int64_t pred, int64_t n, bool handed_in, int64_t cnt) {
   if (c.sub_updates > 0) return c.sub_updates;
@@ -2546,7 +2558,7 @@ static int choose_k(const avgpu_cfg& c, int64_t pred, int64_t n, bool handed_in,
 static int run_update_impl(World& w) {
   if (w.cfg.birth_method == 5)
     return fail(AVGPU_EUNSUPPORTED, "BIRTH_METHOD 5 (the reaper queue) runs on the serial world only");
-  const int K = choose_k(w.cfg, w.pred_acc, w.pred_n, w.have_global, w.pred_cnt);
+  const int K = choose_k(w.cfg, w.pred_acc, w.pred_n, w.have_global, densest(w.pred_bin));
   if (K > 1 && w.have_global)
     return fail(AVGPU_EUNSUPPORTED, "sub_updates > 1 needs the world's own totals (no handed-in totals)");
   int64_t placed = 0, dropped = 0, insts = 0, deaths = 0, divides = 0, slices = 0;
@@ -2736,7 +2748,7 @@ int orc_tile_res_settle(void* h, const uint64_t* sum) {
 int orc_tile_buffer_bytes(void* h, int64_t* part, int64_t* halo, int64_t* rec) {
   World& w = *(World*)h;
   const int X = w.cfg.world_x;
-  if (part) *part = (2 * ((w.ncells + 255) / 256) + 3) * 8;
+  if (part) *part = (2 * ((w.ncells + 255) / 256) + 6) * 8;
   if (halo) *halo = halo_bytes_of(X);
   if (rec) *rec = (int64_t)sizeof(HaloHdr) + (int64_t)X * (int64_t)sizeof(HaloRec) + w.r_arena;
   return 0;
@@ -2768,7 +2780,7 @@ int orc_tile_partials(void* h, double* out) {
   // avgpu_tile_steps on every strip
   memcpy(out + 2 * nb, &w.pred_acc, 8);
   memcpy(out + 2 * nb + 1, &w.carry_new, 8);
-  memcpy(out + 2 * nb + 2, &w.pred_cnt, 8);
+  for (int k = 0; k < 4; k++) memcpy(out + 2 * nb + 2 + k, &w.pred_bin[k], 8);
   // edge rows of the spatial amounts for the neighbours' flow step
   const int X = w.cfg.world_x;
   if (w.tiled && w.rs_send[0])
@@ -2787,16 +2799,19 @@ int orc_tile_partials(void* h, double* out) {
 // partials (the single world's choose_k over the same integer sum)
 int orc_tile_steps(void* h, const double* gathered, int ntiles, int* k_out) {
   World& w = *(World*)h;
-  const int64_t nb = (w.ncells + 255) / 256, stride = 2 * nb + 3;
-  int64_t sum = 0, cnt = 0;
+  const int64_t nb = (w.ncells + 255) / 256, stride = 2 * nb + 6;
+  int64_t sum = 0, bins[4] = {0, 0, 0, 0};
   for (int k = 0; k < ntiles; k++) {
-    int64_t v, c;
+    int64_t v;
     memcpy(&v, gathered + k * stride + 2 * nb, 8);
-    memcpy(&c, gathered + k * stride + 2 * nb + 2, 8);
     sum += v;
-    cnt += c;
+    for (int q = 0; q < 4; q++) {
+      int64_t c;
+      memcpy(&c, gathered + k * stride + 2 * nb + 2 + q, 8);
+      bins[q] += c;
+    }
   }
-  if (k_out) *k_out = choose_k(w.cfg, sum, w.pred_n, false, cnt);
+  if (k_out) *k_out = choose_k(w.cfg, sum, w.pred_n, false, densest(bins));
   return 0;
 }
 
@@ -2811,7 +2826,7 @@ int orc_tile_begin_step(void* h, const double* gathered, int ntiles, int sub, in
     w.acc_overwritten = w.acc_cancelled = 0;
   }
   // the top tree over every strip's block partials (tile order = block order)
-  const int64_t nb = (w.ncells + 255) / 256, stride = 2 * nb + 3;
+  const int64_t nb = (w.ncells + 255) / 256, stride = 2 * nb + 6;
   std::vector<double> leaf((size_t)(nb * ntiles));
   int64_t cnt = 0, fresh = 0;
   for (int k = 0; k < ntiles; k++) {

@@ -134,9 +134,9 @@ def test_product_world_vs_serial_world_midrun():
     the nine task-organism counts and average merit, gestation time and
     fitness at every printed update 5..30, Bonferroni at a family-wise 0.01.
     The loaded population divides in lock-step waves (updates 5-6, 11-12,
-    17-18, ...): measured at 256 seeds the smallest p is 0.0092 (task8 at
-    update 20, threshold 7e-5), and the world takes 1.27 batch steps per
-    update on average over updates 40-150 (1 outside the lock-step waves)."""
+    17-18, ...): measured at 256 seeds the smallest p is 0.0020 (merit at
+    update 30, threshold 7e-5); the world takes up to 3 batch steps per
+    update in its first lock-step waves and 1 from update ~10 on."""
     import midrun_stats as ms
     b = ms.runs("batch0", 192)
     s = ms.runs("serial", 192)

@@ -17,7 +17,7 @@ step's remaining picks after placement (a replaced organism's consumption
 after the birth given back, the picks beyond what it had left carried into
 the next update), and an update takes more batch steps the more its sub-step
 predictor expects the total weight to move or the more organisms it expects
-to divide in it (the lock-step start of the 100 ancestors) -- the bench's own
+to divide in one quarter of it (the lock-step start of the 100 ancestors) -- the bench's own
 world runs the same code and takes one step per update (bench.py
 batch_steps_per_update).  No effect-size carve-out, no update excluded:
 
@@ -34,9 +34,9 @@ batch_steps_per_update).  No effect-size carve-out, no update excluded:
   run): an early, strong Or sweep, around the 97th percentile.
 
 Measured (1024 seeds, this build; tools/piece_stats.py): smallest
-trajectory / discovery p 0.011 (OrNot at update 30; threshold 0.01 / 65 =
-1.5e-4), largest |Cohen's d| 0.12; the reference run's mid-ranks 0.018 ..
-0.995.  The GPU batch world is the oracle's bit for bit (checked
+trajectory / discovery p 0.0126 (ResA at update 10; threshold 0.01 / 65 =
+1.5e-4), largest |Cohen's d| 0.12; the reference run's mid-ranks 0.012 ..
+0.996.  The GPU batch world is the oracle's bit for bit (checked
 per seed below), so its statistics are these.
 """
 import numpy as np

@@ -1626,6 +1626,7 @@ int avgpu_load_resources(avgpu_world* w, int nres, const avgpu_resource* res, in
     w->res_geom[r] = q.geometry;
     W.res_spatial_host[r] = q.geometry != AVGPU_RES_GLOBAL;
     W.res_flows_host[r] = (int8_t)p.flows;
+    W.res_grav_host[r] = (int8_t)(q.xgravity != 0.0 || q.ygravity != 0.0);
     W.res_cells_host[r] = 0;
   }
   for (int i = 0; i < ncell; i++) {
@@ -1641,7 +1642,7 @@ int avgpu_load_resources(avgpu_world* w, int nres, const avgpu_resource* res, in
     w->allocs.push_back(W.res_amount);
     HIPCHK(hipMalloc(&W.res_amount_alt, (size_t)AVGPU_MAX_RESOURCES * n * sizeof(double)));
     w->allocs.push_back(W.res_amount_alt);
-    HIPCHK(hipMalloc(&W.res_delta, (size_t)n * sizeof(double)));
+    HIPCHK(hipMalloc(&W.res_delta, (size_t)(n + 64) * sizeof(double)));   // + k_res_step's junk lanes
     w->allocs.push_back(W.res_delta);
   }
   if (nres && !W.cons) {   // each cell's consumption in a step (newborn credit)

@@ -222,7 +222,7 @@ struct DevWorld {
   int32_t n_res, n_cellres, env_resources;   // env_resources: some reaction consumes a resource
   struct ResParam* res_param;   // [AVGPU_MAX_RESOURCES]
   double* res_amount;           // [n_spatial][n] spatial amounts (row = ResParam::slot)
-  double* res_delta;            // [n] rate scratch of the spatial step
+  double* res_delta;            // [n] rate scratch of the spatial step (+ 64: k_res_step's junk stores)
   double* res_global;           // [AVGPU_MAX_RESOURCES] global levels, fixed during an update
   unsigned long long* res_cons; // [AVGPU_MAX_RESOURCES] global consumption of the update, 2^-32 units
   avgpu_cell_resource* res_cells; // [n_cellres] CELL entries (cell ids are global)
@@ -230,6 +230,7 @@ struct DevWorld {
   int8_t res_spatial_host[AVGPU_MAX_RESOURCES];   // host-side launch flags
   int8_t res_flows_host[AVGPU_MAX_RESOURCES];
   int8_t res_cells_host[AVGPU_MAX_RESOURCES];     // resource has CELL entries
+  int8_t res_grav_host[AVGPU_MAX_RESOURCES];      // resource has gravity on an axis
   double* res_amount_alt;       // [n_spatial][n] the other buffer of the spatial step
   int8_t res_first;             // host: the next update is the first since the load
   int32_t n_spatial;            // spatial resources (rows of res_amount)

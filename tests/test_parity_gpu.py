@@ -258,6 +258,33 @@ def test_world_updates_resources_bit_exact(golden, variant):
     assert so.num_organisms > 200
 
 
+@pytest.mark.parametrize("shape", [(130, 37), (5, 7), (63, 18), (2, 33), (124, 16)])
+def test_resource_step_world_shapes(golden, shape):
+    """k_res_step's windows (62 written columns x 16 rows a wave, the rim lanes
+    wrapping mod WORLD_X): worlds narrower than a window, a last window that
+    wraps, row counts off the band size, a torus and a grid resource with
+    diffusion and gravity -- every level and per-cell amount == the oracle's
+    after every update."""
+    env, anc = _resource_env(golden, "flow")
+    iset = files.read_instset(os.path.join(golden, "resources_9r", "instset-heads.cfg"))
+    X, Y = shape
+    cfg = capi.cfg_from_avida(files.read_avida_cfg(None, {"WORLD_X": X, "WORLD_Y": Y}), seed=29)
+    n = X * Y
+    orc = ol.Backend("oracle", cfg, iset, env, ncells=n)
+    gpu = ol.Backend("gpu", cfg, iset, env, ncells=n)
+    k = min(60, n // 2)
+    for b in (orc, gpu):
+        b.set_orgs(0, [anc] * k, [100.0] * k, deterministic=False)
+    for upd in range(25):
+        so, sg = orc.run_update(), gpu.run_update()
+        assert (so.num_organisms, so.insts_executed, so.births) == (sg.num_organisms, sg.insts_executed, sg.births)
+        lo, go = orc.resources(spatial=True)
+        lg, gg = gpu.resources(spatial=True)
+        assert lo == lg, (upd, lo, lg)
+        assert go == gg, upd
+    assert (orc.digests() == gpu.digests()).all()
+
+
 @pytest.mark.parametrize("variant", ["logic9", "9r"])
 def test_world_subupdates_bit_exact(golden, variant):
     """sub_updates = 3 (DESIGN.md 5 "Sub-updates": an update's picks in three

@@ -698,11 +698,13 @@ __global__ __launch_bounds__(1024) void k_allot(DevWorld W, const double* totals
   uint32_t ctl[4];
   double wt[4];
   bool alive[4];
+  int msz[4];                                  // loaded ahead of the tree (the class needs it)
 #pragma unroll
   for (int j = 0; j < 4; j++) {
     const int64_t c = b * 256 + lane + 64 * j;
     ctl[j] = (b < nb && c < W.n) ? W.ctl[c] : 0u;
     alive[j] = (ctl[j] & CTL_ALIVE) != 0;
+    msz[j] = alive[j] ? W.mem_size[c] : 0;
     const double m = alive[j] ? W.merit[c] : 0.0;
     if (alive[j] && !merit_ok(m)) count_add(W, CNT_BAD_RECORD, 1ull);   // counted; sched_weight gives it 0
     wt[j] = alive[j] ? sched_weight(m, ctl[j]) : 0.0;
@@ -746,7 +748,7 @@ __global__ __launch_bounds__(1024) void k_allot(DevWorld W, const double* totals
     cnt[0] = x0; cnt[2] = c7a - x0; cnt[1] = x1; cnt[3] = c7b - x1;
   }
   bool want[4] = {false, false, false, false};
-  int cls[4] = {0, 0, 0, 0};
+  int cls[4] = {0, 0, 0, 0}, buds[4] = {0, 0, 0, 0};
 #pragma unroll
   for (int j = 0; j < 4; j++) {
     const int64_t c = b * 256 + lane + 64 * j;
@@ -768,8 +770,9 @@ __global__ __launch_bounds__(1024) void k_allot(DevWorld W, const double* totals
       if (ctl[j] & CTL_HS_MASK) W.ctl[c] = ctl[j] & ~CTL_HS_MASK;   // the head start is used up
       if (tick && W.track_age) W.age[c] += 1;   // cPhenotype::IncAge at the previous update's end (oracle age_tick)
       want[j] = bud > 0;
-      if (want[j]) cls[j] = class_of(need_of_cell(W, (int)c));
+      if (want[j]) cls[j] = class_of(need_of(msz[j], ctl[j], W.size_range));   // need_of_cell
     }
+    buds[j] = bud;
     W.budget[c] = bud;
     W.aclass[c] = want[j] ? (uint8_t)cls[j] : (uint8_t)ACLASS_NONE;
     W.ran[c] = 0;
@@ -795,7 +798,7 @@ __global__ __launch_bounds__(1024) void k_allot(DevWorld W, const double* totals
 #pragma unroll
   for (int j = 0; j < 4; j++) {
     const int64_t c = b * 256 + lane + 64 * j;
-    if (b < nb && c < W.n) atomicAdd(&sh[window_bucket(want[j] && cls[j] == 0, W.budget[c])], 1);
+    if (b < nb && c < W.n) atomicAdd(&sh[window_bucket(want[j] && cls[j] == 0, buds[j])], 1);
   }
   __syncthreads();
   for (int i = threadIdx.x; i < SORT_BUCKETS; i += 1024) W.sub_hist[(int64_t)blockIdx.x * SORT_BUCKETS + i] = sh[i];
@@ -1544,6 +1547,9 @@ __device__ __forceinline__ void newborn_enqueue(const DevWorld& W, int cell, int
 // are cleared by k_allot).  A record that does not own its cell was placed
 // and overwritten (CNT_OVERWRITTEN), unless it was cancelled
 // (CNT_CANCELLED: its parent died first) or found no cell (CNT_DROPPED).
+#ifndef ACT_PRE
+#define ACT_PRE 8    // 16-B quads of the offspring's genome k_activate loads ahead
+#endif
 __global__ __launch_bounds__(64) void k_activate(DevWorld W, int fused, uint32_t key, int sub, int nsub) {
   const int nb = queue_len(W);
   const int64_t ncell = W.n + (W.tiled ? 2 * (int64_t)W.world_x : 0);
@@ -1559,14 +1565,17 @@ __global__ __launch_bounds__(64) void k_activate(DevWorld W, int fused, uint32_t
       if (q >= nb) break;
       const int64_t i = rec_of(W, q);
       // the genome's first 128 B, loaded before the claims decide whether the
-      // record won (a dependent round trip less for the ~95 % that do)
+      // record won (a dependent round trip less for the ~95 % that do; the
+      // whole class-0 genome, 20 quads, measured no faster)
       const uint4* g4 = reinterpret_cast<const uint4*>(W.b_genome + i * TAPE_SLOT);
-      uint4 pre[8];
+      uint4 pre[ACT_PRE];
 #pragma unroll
-      for (int u = 0; u < 8; u++) pre[u] = g4[u];
+      for (int u = 0; u < ACT_PRE; u++) pre[u] = g4[u];
       const int tgt = W.b_target[i];
       const int8_t st = W.b_state[i];
       Child b = child_of_record(W, i);
+      // the replaced organism's instructions, loaded with the claim words
+      const int ran = (tgt >= 0 && (int64_t)tgt < W.n) ? W.ran[tgt] : 0;
       const int lastr = last_claim_round(st);
       // the record's claims, round k's at b_tgt[k] (the last one its target);
       // a target out of range is a corrupt record: counted, never written
@@ -1594,8 +1603,7 @@ __global__ __launch_bounds__(64) void k_activate(DevWorld W, int fused, uint32_t
       if (tgt >= W.n) break;                   // sent to the neighbouring tile
       born++;
       b.hs = 0;                                // it runs its share of this step instead (newborn pass)
-      const int ran = W.ran[tgt];
-      setup_child_lane<8>(W, tgt, b, W.b_genome + i * TAPE_SLOT, pre);
+      setup_child_lane<ACT_PRE>(W, tgt, b, W.b_genome + i * TAPE_SLOT, pre);
       nrow = newborn_setup(W, tgt, t, b.merit, b.len, key, uds, total, carry, wasted, ran);
       ncell_nb = tgt;
     } while (0);

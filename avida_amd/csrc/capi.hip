@@ -68,9 +68,16 @@ struct avgpu_world {
   double acc_class_ms[NUM_CLASSES] = {};
   int64_t acc_phases = 0;
   DevWorld W;
-  DevWorld* d_W = nullptr;      // device copy of W read by k_interpret
-  DevWorld pushed;              // what d_W holds
-  bool pushed_valid = false;
+  DevWorld* d_W = nullptr;      // device copy of W read by k_interpret: one of d_Wv
+  // two device copies (a world whose resources swap their buffers every
+  // update alternates between two descriptors: after two updates neither
+  // is uploaded again), uploaded in stream order from pinned staging
+  DevWorld* d_Wv[2] = {};
+  DevWorld pushedv[2];          // what d_Wv[k] holds
+  bool validv[2] = {false, false};
+  int cur_w = 0;
+  DevWorld* h_stage = nullptr;  // [2] pinned
+  hipEvent_t ev_stage[2] = {};  // the last upload from h_stage[k]
   std::vector<void*> allocs;
   // instruction set translation
   int n_ops = 0;
@@ -208,7 +215,9 @@ int setup_world(avgpu_world* w, int64_t n, bool test_buffers) {
   A(react_tab, AVGPU_MAX_REACTIONS * RT_STRIDE); A(task_tab, 32);
   A(react_res, AVGPU_MAX_REACTIONS * RR_STRIDE); A(res_param, AVGPU_MAX_RESOURCES);
   A(res_global, AVGPU_MAX_RESOURCES); A(res_cons, AVGPU_MAX_RESOURCES);
-  if ((rc = w->alloc(&w->d_W, 1))) return rc;
+  if ((rc = w->alloc(&w->d_Wv[0], 1)) || (rc = w->alloc(&w->d_Wv[1], 1))) return rc;
+  w->d_W = w->d_Wv[0];
+  w->validv[0] = w->validv[1] = false;
   const int64_t nb = (n + 255) / 256;
   if ((rc = w->alloc(&w->d_totals, (size_t)(8 + 2 * nb)))) return rc;
   W.totals = w->d_totals;
@@ -395,6 +404,9 @@ avgpu_world* create_world(const avgpu_cfg* cfg, int device, int64_t n, bool test
       hipEventCreate(&w->ev0) != hipSuccess || hipEventCreate(&w->ev1) != hipSuccess ||
       hipHostMalloc((void**)&w->h_pred, 4 * sizeof(long long), hipHostMallocMapped | hipHostMallocCoherent) !=
           hipSuccess ||
+      hipHostMalloc((void**)&w->h_stage, 2 * sizeof(DevWorld), hipHostMallocDefault) != hipSuccess ||
+      hipEventCreateWithFlags(&w->ev_stage[0], hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&w->ev_stage[1], hipEventDisableTiming) != hipSuccess ||
       hipHostGetDevicePointer((void**)&w->d_pred, w->h_pred, 0) != hipSuccess) {
     delete w; fail(AVGPU_EHIP, "stream/event creation failed"); return nullptr;
   }
@@ -578,13 +590,30 @@ int drain_ring(avgpu_world* w, int keep) {
   return 0;
 }
 
-// refresh the device copy of the world descriptor when the host copy changed
+// point d_W at a device copy of the world descriptor equal to the host copy,
+// uploading it into the other slot when neither holds it.  The upload is
+// stream-ordered after every launch queued before it (the only readers of
+// that slot: the aux streams of AVGPU_NO_MIX join the stream within their
+// update, avgpu_set_stream synchronises), from pinned staging whose last
+// upload is waited for -- no stream synchronisation on the update path
+// (it cost ~30 us of idle GPU per configs[4] update, whose resource buffers
+// swap every update).
 int push_world(avgpu_world* w) {
-  if (w->pushed_valid && memcmp(&w->pushed, &w->W, sizeof(DevWorld)) == 0) return 0;
-  HIPCHK(hipMemcpyAsync(w->d_W, &w->W, sizeof(DevWorld), hipMemcpyHostToDevice, w->stream));
-  HIPCHK(hipStreamSynchronize(w->stream));
-  memcpy(&w->pushed, &w->W, sizeof(DevWorld));
-  w->pushed_valid = true;
+  for (int k = 0; k < 2; k++)
+    if (w->validv[k] && memcmp(&w->pushedv[k], &w->W, sizeof(DevWorld)) == 0) {
+      w->cur_w = k;
+      w->d_W = w->d_Wv[k];
+      return 0;
+    }
+  const int k = 1 - w->cur_w;
+  HIPCHK(hipEventSynchronize(w->ev_stage[k]));
+  memcpy(&w->h_stage[k], &w->W, sizeof(DevWorld));
+  HIPCHK(hipMemcpyAsync(w->d_Wv[k], &w->h_stage[k], sizeof(DevWorld), hipMemcpyHostToDevice, w->stream));
+  HIPCHK(hipEventRecord(w->ev_stage[k], w->stream));
+  memcpy(&w->pushedv[k], &w->W, sizeof(DevWorld));
+  w->validv[k] = true;
+  w->cur_w = k;
+  w->d_W = w->d_Wv[k];
   return 0;
 }
 
@@ -688,6 +717,9 @@ int avgpu_destroy(avgpu_world* w) {
   }
   if (w->ev_fork) hipEventDestroy(w->ev_fork);
   if (w->h_pred) hipHostFree(w->h_pred);
+  if (w->h_stage) hipHostFree(w->h_stage);
+  for (int k = 0; k < 2; k++)
+    if (w->ev_stage[k]) hipEventDestroy(w->ev_stage[k]);
   delete w;
   return 0;
 }
